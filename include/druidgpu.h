@@ -1,0 +1,227 @@
+/*
+ * druidgpu.h — C-ABI of the MI355X segment scan-and-aggregate engine.
+ *
+ * This is the drop-in boundary a JNI shim binds. Every entry point replaces
+ * one reference interface on the historical's per-segment query path (paths relative to the
+ * reference root; processing/... = processing/src/main/java/org/apache/druid/...):
+ *
+ *   dg_segment_attach        <- IndexIO.loadIndex / V9IndexLoader.load (processing/.../segment/IndexIO.java:569-663)
+ *                               + Segment.asQueryableIndex/asStorageAdapter (processing/.../segment/Segment.java:30-35)
+ *   dg_segment_release       <- QueryableIndex.close / ReferenceCountingSegment (SmooshedFileMapper.close)
+ *   dg_segment_time_bounds   <- StorageAdapter.getMinTime / getMaxTime (processing/.../segment/StorageAdapter.java:33-80)
+ *   dg_segment_dim_*         <- StorageAdapter.getDimensionCardinality, DimensionSelector.lookupName,
+ *                               GenericIndexed.get (processing/.../segment/data/GenericIndexed.java:479-492)
+ *   dg_filter_bitmap         <- Filter.getBitmapResult over BitmapIndexSelector
+ *                               (processing/.../query/filter/Filter.java:28-110; segment/filter/{Selector,In,Bound,
+ *                               And,Or,Not}Filter.java) as used by QueryableIndexStorageAdapter.makeCursors (:244-299)
+ *   dg_timeseries_run        <- TimeseriesQueryRunnerFactory.createRunner(segment).run
+ *                               (processing/.../query/timeseries/TimeseriesQueryRunnerFactory.java:93-105,
+ *                               TimeseriesQueryEngine.java:40-111)
+ *   dg_topn_run              <- TopNQueryRunnerFactory.createRunner(segment).run (query/topn/TopNQueryRunnerFactory.java:61-90,
+ *                               TopNQueryEngine.java:60-160 -> PooledTopNAlgorithm + TopNNumericResultBuilder)
+ *   dg_groupby_run           <- GroupByStrategyV2.process -> GroupByQueryEngineV2.process
+ *                               (query/groupby/strategy/GroupByStrategyV2.java:472-477, epinephelinae/GroupByQueryEngineV2.java:91-187)
+ *
+ * Segment arrays: every *_run takes n_segs segments that are attached to the SAME context (device)
+ * and runs them as one batched launch sequence; results stay per segment, exactly as the
+ * reference's per-segment runners return them (cross-segment merging is QueryRunnerFactory.mergeRunners,
+ * done by the host layer / RCCL, see incubator-druid_amd/runners.py and distributed.py).
+ *
+ * Conventions: 0 = DG_OK, otherwise a DG_ERR_* code and dg_last_error() (thread-local) describes it.
+ * All output buffers are caller-allocated host memory. No callbacks into the caller. Every entry
+ * point is safe to call concurrently for different segments; calls on one context serialize on
+ * that context's HIP stream. Only the reference's default null mode is implemented
+ * (druid.generic.useDefaultValueForNull=true, common/config/NullHandling.java:34,54): anything else
+ * is the caller's problem (the Java shim keeps its CPU path, DG_ERR_UNSUPPORTED).
+ */
+#ifndef DRUIDGPU_H
+#define DRUIDGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DG_ABI_VERSION 1
+
+/* status codes (the JNI shim maps them to the reference's exceptions) */
+#define DG_OK 0
+#define DG_ERR_FORMAT 1      /* IAE / ISE on malformed segment bytes (GenericIndexed.java:131-149) */
+#define DG_ERR_UNSUPPORTED 2 /* shape not implemented on GPU: caller keeps its CPU engine */
+#define DG_ERR_OOM 3         /* device allocation failed */
+#define DG_ERR_INTERRUPTED 4 /* QueryInterruptedException (BaseQuery.checkInterrupted, BaseQuery.java:46-51) */
+#define DG_ERR_TABLE_FULL 5  /* Groupers.HASH_TABLE_FULL (Groupers.java:36-40) */
+#define DG_ERR_ARG 6         /* IllegalArgumentException */
+#define DG_ERR_DEVICE 7      /* HIP runtime failure */
+#define DG_ERR_NOT_FOUND 8   /* SegmentMissingException (TimeseriesQueryEngine.java:42-46) */
+
+/* column types (ValueType, processing/.../segment/column/ValueType.java) */
+#define DG_COL_MISSING 0
+#define DG_COL_LONG 1
+#define DG_COL_FLOAT 2
+#define DG_COL_DOUBLE 3
+#define DG_COL_STRING 4
+#define DG_COL_UNSUPPORTED 5 /* complex / multi-value / unsupported codec */
+
+/* aggregator kinds (query/aggregation/...AggregatorFactory.java) */
+#define DG_AGG_COUNT 0
+#define DG_AGG_LONG_SUM 1
+#define DG_AGG_DOUBLE_SUM 2
+#define DG_AGG_FLOAT_SUM 3
+#define DG_AGG_LONG_MIN 4
+#define DG_AGG_LONG_MAX 5
+#define DG_AGG_DOUBLE_MIN 6
+#define DG_AGG_DOUBLE_MAX 7
+#define DG_AGG_FLOAT_MIN 8
+#define DG_AGG_FLOAT_MAX 9
+
+/* filter node kinds (query/filter/...DimFilter.java -> segment/filter/...Filter.java) */
+#define DG_F_AND 1
+#define DG_F_OR 2
+#define DG_F_NOT 3
+#define DG_F_SELECTOR 4
+#define DG_F_IN 5
+#define DG_F_BOUND 6
+
+/* bound orderings (query/ordering/StringComparators.java) */
+#define DG_ORDER_LEXICOGRAPHIC 0
+#define DG_ORDER_NUMERIC 1
+
+typedef struct dg_context dg_context;
+typedef struct dg_segment dg_segment;
+typedef struct dg_result dg_result;
+
+/*
+ * One filter node. A filter is an array of nodes in prefix order: an AND/OR node is followed by
+ * its n_children subtrees, a NOT node by exactly one subtree. Strings are NUL-terminated UTF-8;
+ * a NULL value pointer means the null value ("" in default null mode).
+ */
+typedef struct {
+  int32_t kind;
+  int32_t n_children;
+  const char* dimension;
+  const char* const* values; /* SELECTOR: values[0]; IN: values[0..n_values) */
+  int32_t n_values;
+  const char* lower;         /* BOUND: NULL = no bound */
+  const char* upper;
+  int32_t lower_strict;
+  int32_t upper_strict;
+  int32_t ordering;          /* DG_ORDER_* */
+} dg_filter;
+
+/* AggregatorFactory (name is the caller's business; field is the input column, NULL for count) */
+typedef struct {
+  int32_t kind;
+  const char* field;
+} dg_agg;
+
+/*
+ * The scan common to all three query types (what makeCursors receives:
+ * CursorFactory.makeCursors(filter, interval, virtualColumns, gran, descending, metrics),
+ * processing/.../segment/CursorFactory.java:32-42).
+ * Granularity: period_ms == 0 is ALL; otherwise a fixed-length UTC period with bucket starts at
+ * origin_ms + k * period_ms (PeriodGranularity.truncateMillisPeriod, PeriodGranularity.java:411-428).
+ */
+typedef struct {
+  int64_t interval_start; /* [start, end) epoch millis */
+  int64_t interval_end;
+  int64_t period_ms;
+  int64_t origin_ms;
+  const dg_filter* filter; /* NULL / n_filter == 0: no filter */
+  int32_t n_filter;
+  const dg_agg* aggs;
+  int32_t n_aggs;
+  const volatile int32_t* cancel; /* optional; non-zero => DG_ERR_INTERRUPTED between kernels */
+} dg_scan;
+
+/* QueryMetrics counters (query/QueryMetrics.java:295-306) + device timings */
+typedef struct {
+  int64_t segment_rows;      /* reportSegmentRows */
+  int64_t pre_filtered_rows; /* reportPreFilteredRows: rows passing the bitmap filter */
+  int64_t selected_rows;     /* rows aggregated (filter AND interval) */
+  int64_t bytes_read;        /* algorithmic HBM bytes of the column blocks / bitmaps scanned */
+  double bitmap_ms;          /* reportBitmapConstructionTime (device time) */
+  double decode_ms;          /* column decode kernels */
+  double aggregate_ms;       /* aggregation kernels */
+  double total_ms;           /* whole call, host wall */
+} dg_metrics;
+
+/* Aggregate values are returned in 8-byte slots: int64 for count/long*, double for double*,
+ * and for float* a float32 in the first 4 bytes of the slot (rest zero). */
+
+/* ---- library / context ---- */
+const char* dg_last_error(void);
+int dg_abi_version(void);
+int dg_device_count(int* out);
+int dg_context_create(int device, dg_context** out);
+void dg_context_release(dg_context* ctx);
+/* Bind the context's work to an existing HIP stream (e.g. torch's current stream); NULL resets. */
+int dg_context_set_stream(dg_context* ctx, void* hip_stream);
+
+/* ---- segments ---- */
+int dg_segment_attach(dg_context* ctx, const char* segment_dir, dg_segment** out);
+void dg_segment_release(dg_segment* seg);
+int64_t dg_segment_num_rows(const dg_segment* seg);
+int dg_segment_interval(const dg_segment* seg, int64_t* start, int64_t* end);
+int dg_segment_time_bounds(const dg_segment* seg, int64_t* min_time, int64_t* max_time);
+int dg_segment_num_columns(const dg_segment* seg);
+const char* dg_segment_column_name(const dg_segment* seg, int index);
+int dg_segment_column_type(const dg_segment* seg, const char* column);
+int64_t dg_segment_device_bytes(const dg_segment* seg);
+int32_t dg_segment_dim_cardinality(const dg_segment* seg, const char* dim);
+/* lookupName: *len = -1 for null (empty) values */
+int dg_segment_dim_value(const dg_segment* seg, const char* dim, int32_t id, const char** out, int32_t* len);
+/* Bulk dictionary export: offsets[card + 1] (byte offsets into bytes), bytes (size offsets[card]).
+ * Call with bytes == NULL to get *total_bytes first. */
+int dg_segment_dim_dictionary(const dg_segment* seg, const char* dim, int64_t* offsets, char* bytes,
+                              int64_t* total_bytes);
+
+/* ---- scan pieces ---- */
+/* Filter.getBitmapResult: row bitset (uint32 words, bit r = row r) of the filter, into out_words
+ * (ceil(num_rows / 32) words); *out_count = cardinality of the result. */
+int dg_filter_bitmap(dg_segment* seg, const dg_filter* filter, int32_t n_filter, uint32_t* out_words,
+                     int64_t* out_count);
+
+/* ---- timeseries ---- */
+/* Per segment i: out_n_buckets[i] cursors (one per granularity bucket of the segment's actual
+ * interval, TimeseriesQueryEngine emits each even when empty); bucket k of segment i is at
+ * index i * bucket_cap + k of out_bucket_time / out_bucket_rows, and its aggregate slots at
+ * (i * bucket_cap + k) * n_aggs. out_bucket_rows = rows aggregated (skipEmptyBuckets decision). */
+int dg_timeseries_run(dg_segment* const* segs, int32_t n_segs, const dg_scan* scan, int32_t bucket_cap,
+                      int32_t* out_n_buckets, int64_t* out_bucket_time, int64_t* out_bucket_rows,
+                      uint64_t* out_values, dg_metrics* metrics);
+
+/* ---- topN ---- */
+typedef struct {
+  const char* dimension;
+  int32_t metric_agg; /* index into scan->aggs of the NumericTopNMetricSpec metric */
+  int32_t inverted;   /* InvertedTopNMetricSpec */
+  int32_t threshold;  /* per-segment threshold, i.e. max(query threshold, minTopNThreshold) */
+} dg_topn;
+
+/* ALL granularity only. Per segment i: out_n[i] entries, ordered as TopNNumericResultBuilder.build()
+ * returns them; entry j at index i * threshold + j: dictionary id (segment-local) and n_aggs slots. */
+int dg_topn_run(dg_segment* const* segs, int32_t n_segs, const dg_scan* scan, const dg_topn* topn,
+                int32_t* out_n, int32_t* out_ids, uint64_t* out_values, dg_metrics* metrics);
+
+/* ---- groupBy (v2) ---- */
+typedef struct {
+  const char* const* dimensions;
+  int32_t n_dims;
+} dg_groupby;
+
+/* Runs the grouping; results are kept in a dg_result until fetched. */
+int dg_groupby_run(dg_segment* const* segs, int32_t n_segs, const dg_scan* scan, const dg_groupby* g,
+                   dg_result** out, dg_metrics* metrics);
+/* number of groups of segment i */
+int64_t dg_result_groups(const dg_result* res, int32_t seg_index);
+/* bucket_time[n], ids[n * n_dims] (segment-local dictionary ids), values[n * n_aggs] slots */
+int dg_result_fetch_groups(dg_result* res, int32_t seg_index, int64_t* bucket_time, int32_t* ids,
+                           uint64_t* values);
+void dg_result_release(dg_result* res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRUIDGPU_H */

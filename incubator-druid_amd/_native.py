@@ -1,0 +1,235 @@
+"""ctypes binding of the C-ABI (include/druidgpu.h) — the same entry points a JNI shim binds.
+
+The library is built in-tree (``lib/libdruidgpu.so``). There is no fallback: if the HIP library
+cannot be loaded the product path raises, it never silently runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdruidgpu.so")
+
+DG_OK = 0
+ERRORS = {1: "DG_ERR_FORMAT", 2: "DG_ERR_UNSUPPORTED", 3: "DG_ERR_OOM", 4: "DG_ERR_INTERRUPTED",
+          5: "DG_ERR_TABLE_FULL", 6: "DG_ERR_ARG", 7: "DG_ERR_DEVICE", 8: "DG_ERR_NOT_FOUND"}
+COL_MISSING, COL_LONG, COL_FLOAT, COL_DOUBLE, COL_STRING, COL_UNSUPPORTED = range(6)
+F_AND, F_OR, F_NOT, F_SELECTOR, F_IN, F_BOUND = 1, 2, 3, 4, 5, 6
+ORDER = {"lexicographic": 0, "numeric": 1}
+
+
+class DruidGpuError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class UnsupportedQuery(DruidGpuError):
+    """DG_ERR_UNSUPPORTED: the reference keeps its CPU engine for this shape."""
+
+
+class QueryInterrupted(DruidGpuError):
+    pass
+
+
+class ResourceLimitExceeded(DruidGpuError):
+    pass
+
+
+class dg_filter(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("n_children", ctypes.c_int32), ("dimension", ctypes.c_char_p),
+                ("values", ctypes.POINTER(ctypes.c_char_p)), ("n_values", ctypes.c_int32),
+                ("lower", ctypes.c_char_p), ("upper", ctypes.c_char_p), ("lower_strict", ctypes.c_int32),
+                ("upper_strict", ctypes.c_int32), ("ordering", ctypes.c_int32)]
+
+
+class dg_agg(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("field", ctypes.c_char_p)]
+
+
+class dg_scan(ctypes.Structure):
+    _fields_ = [("interval_start", ctypes.c_int64), ("interval_end", ctypes.c_int64),
+                ("period_ms", ctypes.c_int64), ("origin_ms", ctypes.c_int64),
+                ("filter", ctypes.POINTER(dg_filter)), ("n_filter", ctypes.c_int32),
+                ("aggs", ctypes.POINTER(dg_agg)), ("n_aggs", ctypes.c_int32),
+                ("cancel", ctypes.POINTER(ctypes.c_int32))]
+
+
+class dg_metrics(ctypes.Structure):
+    _fields_ = [("segment_rows", ctypes.c_int64), ("pre_filtered_rows", ctypes.c_int64),
+                ("selected_rows", ctypes.c_int64), ("bytes_read", ctypes.c_int64),
+                ("bitmap_ms", ctypes.c_double), ("decode_ms", ctypes.c_double),
+                ("aggregate_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class dg_topn(ctypes.Structure):
+    _fields_ = [("dimension", ctypes.c_char_p), ("metric_agg", ctypes.c_int32), ("inverted", ctypes.c_int32),
+                ("threshold", ctypes.c_int32)]
+
+
+class dg_groupby(ctypes.Structure):
+    _fields_ = [("dimensions", ctypes.POINTER(ctypes.c_char_p)), ("n_dims", ctypes.c_int32)]
+
+
+# every symbol the header declares (checked by the CPU test suite)
+EXPORTS = [
+    "dg_last_error", "dg_abi_version", "dg_device_count", "dg_context_create", "dg_context_release",
+    "dg_context_set_stream", "dg_segment_attach", "dg_segment_release", "dg_segment_num_rows",
+    "dg_segment_interval", "dg_segment_time_bounds", "dg_segment_num_columns", "dg_segment_column_name",
+    "dg_segment_column_type", "dg_segment_device_bytes", "dg_segment_dim_cardinality", "dg_segment_dim_value",
+    "dg_segment_dim_dictionary", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_groupby_run",
+    "dg_result_groups", "dg_result_fetch_groups", "dg_result_release",
+]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                           "(make -C incubator-druid_amd/csrc); there is no CPU fallback")
+    l = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, cp = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_char_p
+    P = ctypes.POINTER
+    sig = {
+        "dg_last_error": (cp, []),
+        "dg_abi_version": (ctypes.c_int, []),
+        "dg_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
+        "dg_context_create": (ctypes.c_int, [ctypes.c_int, P(vp)]),
+        "dg_context_release": (None, [vp]),
+        "dg_context_set_stream": (ctypes.c_int, [vp, vp]),
+        "dg_segment_attach": (ctypes.c_int, [vp, cp, P(vp)]),
+        "dg_segment_release": (None, [vp]),
+        "dg_segment_num_rows": (i64, [vp]),
+        "dg_segment_interval": (ctypes.c_int, [vp, P(i64), P(i64)]),
+        "dg_segment_time_bounds": (ctypes.c_int, [vp, P(i64), P(i64)]),
+        "dg_segment_num_columns": (ctypes.c_int, [vp]),
+        "dg_segment_column_name": (cp, [vp, ctypes.c_int]),
+        "dg_segment_column_type": (ctypes.c_int, [vp, cp]),
+        "dg_segment_device_bytes": (i64, [vp]),
+        "dg_segment_dim_cardinality": (i32, [vp, cp]),
+        "dg_segment_dim_value": (ctypes.c_int, [vp, cp, i32, P(ctypes.c_void_p), P(i32)]),
+        "dg_segment_dim_dictionary": (ctypes.c_int, [vp, cp, vp, vp, P(i64)]),
+        "dg_filter_bitmap": (ctypes.c_int, [vp, P(dg_filter), i32, vp, P(i64)]),
+        "dg_timeseries_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), i32, vp, vp, vp, vp, P(dg_metrics)]),
+        "dg_topn_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), P(dg_topn), vp, vp, vp, P(dg_metrics)]),
+        "dg_groupby_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), P(dg_groupby), P(vp), P(dg_metrics)]),
+        "dg_result_groups": (i64, [vp, i32]),
+        "dg_result_fetch_groups": (ctypes.c_int, [vp, i32, vp, vp, vp]),
+        "dg_result_release": (None, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(l, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = l
+    return l
+
+
+def check(rc: int):
+    if rc == DG_OK:
+        return
+    msg = lib().dg_last_error().decode("utf-8", "replace")
+    if rc == 2:
+        raise UnsupportedQuery(rc, msg)
+    if rc == 4:
+        raise QueryInterrupted(rc, msg)
+    if rc == 5:
+        raise ResourceLimitExceeded(rc, msg)
+    raise DruidGpuError(rc, msg)
+
+
+def _b(s: Optional[str]) -> Optional[bytes]:
+    return None if s is None else str(s).encode("utf-8")
+
+
+class FilterProgram:
+    """DimFilter tree -> prefix-ordered dg_filter array (keeps the backing strings alive)."""
+
+    def __init__(self, flt, query_module):
+        self._keep: List = []
+        self.nodes: List[dg_filter] = []
+        self.Q = query_module
+        if flt is not None:
+            self._emit(flt)
+        self.array = (dg_filter * max(len(self.nodes), 1))(*self.nodes) if self.nodes else None
+
+    def _strs(self, vals: Sequence[Optional[str]]):
+        arr = (ctypes.c_char_p * max(len(vals), 1))(*[_b(v) for v in vals])
+        self._keep.append(arr)
+        return arr
+
+    def _emit(self, f):
+        Q = self.Q
+        node = dg_filter()
+        if isinstance(f, Q.AndDimFilter) or isinstance(f, Q.OrDimFilter):
+            node.kind = F_AND if isinstance(f, Q.AndDimFilter) else F_OR
+            node.n_children = len(f.fields)
+            self.nodes.append(node)
+            for c in f.fields:
+                self._emit(c)
+            return
+        if isinstance(f, Q.NotDimFilter):
+            node.kind = F_NOT
+            node.n_children = 1
+            self.nodes.append(node)
+            self._emit(f.field)
+            return
+        dim = _b(f.dimension)
+        self._keep.append(dim)
+        node.dimension = dim
+        if isinstance(f, Q.SelectorDimFilter):
+            node.kind = F_SELECTOR
+            node.values = self._strs([f.value])
+            node.n_values = 1
+        elif isinstance(f, Q.InDimFilter):
+            node.kind = F_IN
+            node.values = self._strs(list(f.values))
+            node.n_values = len(f.values)
+        elif isinstance(f, Q.BoundDimFilter):
+            node.kind = F_BOUND
+            lo, hi = _b(f.lower), _b(f.upper)
+            self._keep += [lo, hi]
+            node.lower, node.upper = lo, hi
+            node.lower_strict, node.upper_strict = int(f.lowerStrict), int(f.upperStrict)
+            if f.ordering not in ORDER:
+                raise UnsupportedQuery(2, f"bound ordering {f.ordering}")
+            node.ordering = ORDER[f.ordering]
+        else:
+            raise UnsupportedQuery(2, f"filter {type(f).__name__}")
+        self.nodes.append(node)
+
+
+def make_scan(query, query_module, cancel: Optional[ctypes.c_int32] = None):
+    """Build a dg_scan (+ keep-alive list) from a query's interval, granularity, filter and aggs."""
+    keep = []
+    fp = FilterProgram(query.effective_filter(), query_module)
+    keep.append(fp)
+    aggs = (dg_agg * max(len(query.aggregations), 1))()
+    for i, a in enumerate(query.aggregations):
+        aggs[i].kind = a.kind
+        fld = _b(a.fieldName) if a.kind != 0 else None
+        keep.append(fld)
+        aggs[i].field = fld
+    keep.append(aggs)
+    s = dg_scan()
+    s.interval_start, s.interval_end = query.interval
+    s.period_ms = query.granularity.period_ms
+    s.origin_ms = query.granularity.origin_ms
+    if fp.array is not None:
+        s.filter = ctypes.cast(fp.array, ctypes.POINTER(dg_filter))
+        s.n_filter = len(fp.nodes)
+    s.aggs = ctypes.cast(aggs, ctypes.POINTER(dg_agg))
+    s.n_aggs = len(query.aggregations)
+    if cancel is not None:
+        s.cancel = ctypes.pointer(cancel)
+        keep.append(cancel)
+    return s, keep

@@ -1,0 +1,1482 @@
+// dg_engine.cpp — C-ABI entry points and query execution on one device.
+//
+// Host side of the per-segment runners (reference: TimeseriesQueryEngine.process, TopNQueryEngine.query +
+// PooledTopNAlgorithm, GroupByQueryEngineV2.process). The host resolves filters against the segment
+// dictionaries (BitmapIndexSelector semantics), computes granularity buckets from the segment time
+// bounds (QueryableIndexStorageAdapter.makeCursors:190-316 + CursorSequenceBuilder.build:367-456),
+// builds the kernel job tables and launches; every row-level operation runs on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cerrno>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <queue>
+#include <string>
+#include <vector>
+
+#include "dg_internal.h"
+
+namespace dg {
+
+// ------------------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------------------
+static thread_local char g_err[1024] = "";
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+void DevBuf::reset() {
+  if (p) hipFree(p);
+  p = nullptr;
+  n = 0;
+}
+
+bool DevBuf::alloc(size_t bytes) {
+  reset();
+  if (bytes == 0) bytes = 16;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
+    p = nullptr;
+    return false;
+  }
+  n = bytes;
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-call device/pinned scratch
+// ------------------------------------------------------------------------------------------------
+struct Pool {
+  struct Chunk {
+    void* p;
+    size_t n;
+  };
+  std::vector<Chunk> chunks;
+  size_t cur = 0, off = 0;
+  bool pinned = false;
+  ~Pool() {
+    for (auto& c : chunks) {
+      if (pinned) hipHostFree(c.p);
+      else hipFree(c.p);
+    }
+  }
+  void reset() {
+    cur = 0;
+    off = 0;
+  }
+  void* take(size_t n) {
+    n = (n + 255) & ~(size_t)255;
+    while (cur < chunks.size()) {
+      if (off + n <= chunks[cur].n) {
+        void* r = (char*)chunks[cur].p + off;
+        off += n;
+        return r;
+      }
+      cur++;
+      off = 0;
+    }
+    size_t sz = std::max(n, (size_t)64 << 20);
+    void* p = nullptr;
+    hipError_t e = pinned ? hipHostMalloc(&p, sz, hipHostMallocDefault) : hipMalloc(&p, sz);
+    if (e != hipSuccess) return nullptr;
+    chunks.push_back({p, sz});
+    cur = chunks.size() - 1;
+    off = n;
+    return p;
+  }
+};
+
+struct CallScratch {
+  Pool dev;
+  Pool host;
+  CallScratch() { host.pinned = true; }
+};
+
+static CallScratch* scratch_of(Context* ctx) {
+  static std::mutex m;
+  static std::map<Context*, CallScratch*> s;
+  std::lock_guard<std::mutex> g(m);
+  auto it = s.find(ctx);
+  if (it != s.end()) return it->second;
+  CallScratch* c = new CallScratch();
+  s[ctx] = c;
+  return c;
+}
+
+template <class T>
+static T* dev_take(CallScratch* cs, size_t count) {
+  return static_cast<T*>(cs->dev.take(count * sizeof(T)));
+}
+template <class T>
+static T* host_take(CallScratch* cs, size_t count) {
+  return static_cast<T*>(cs->host.take(count * sizeof(T)));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Java string ordering (String.compareTo = UTF-16 code units; GenericIndexed.STRING_STRATEGY is
+// naturalNullsFirst) and dictionary search (GenericIndexed.indexOf, GenericIndexed.java:308-333)
+// ------------------------------------------------------------------------------------------------
+static void to_utf16(const std::string& s, std::vector<uint16_t>* out) {
+  out->clear();
+  for (size_t i = 0; i < s.size();) {
+    uint32_t c = (uint8_t)s[i];
+    int n = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+    if (n == 2) c &= 0x1F;
+    else if (n == 3) c &= 0x0F;
+    else if (n == 4) c &= 0x07;
+    for (int k = 1; k < n && i + k < s.size(); ++k) c = (c << 6) | ((uint8_t)s[i + k] & 0x3F);
+    i += n;
+    if (c >= 0x10000) {
+      c -= 0x10000;
+      out->push_back((uint16_t)(0xD800 + (c >> 10)));
+      out->push_back((uint16_t)(0xDC00 + (c & 0x3FF)));
+    } else {
+      out->push_back((uint16_t)c);
+    }
+  }
+}
+
+static int java_compare(const std::string& a, const std::string& b) {
+  bool ascii = true;
+  for (unsigned char ch : a) ascii &= ch < 0x80;
+  for (unsigned char ch : b) ascii &= ch < 0x80;
+  if (ascii) {
+    int c = a.compare(b);
+    return (c > 0) - (c < 0);
+  }
+  std::vector<uint16_t> ua, ub;
+  to_utf16(a, &ua);
+  to_utf16(b, &ub);
+  size_t n = std::min(ua.size(), ub.size());
+  for (size_t i = 0; i < n; ++i)
+    if (ua[i] != ub[i]) return ua[i] < ub[i] ? -1 : 1;
+  return ua.size() == ub.size() ? 0 : (ua.size() < ub.size() ? -1 : 1);
+}
+
+// null-aware compare: null < anything
+static int cmp_nullable(bool an, const std::string& a, bool bn, const std::string& b) {
+  if (an || bn) return an == bn ? 0 : (an ? -1 : 1);
+  return java_compare(a, b);
+}
+
+static int index_of(const Column* c, const char* value) {
+  const bool vnull = value == nullptr || value[0] == 0;  // NullHandling.emptyToNullIfNeeded
+  const std::string v = vnull ? std::string() : std::string(value);
+  int lo = 0, hi = (int)c->dict.size() - 1;
+  while (lo <= hi) {
+    int mid = (lo + hi) >> 1;
+    int r = cmp_nullable(c->dict_null[mid], c->dict[mid], vnull, v);
+    if (r == 0) return mid;
+    if (r < 0) lo = mid + 1;
+    else hi = mid - 1;
+  }
+  return -(lo + 1);
+}
+
+// StringComparators.NumericComparator (query/ordering/StringComparators.java:346-392)
+static bool try_long(const char* s, long long* out) {
+  if (!s || !*s) return false;
+  const char* p = s;
+  if (*p == '-') p++;
+  if (!*p) return false;
+  for (const char* q = p; *q; ++q)
+    if (*q < '0' || *q > '9') return false;
+  errno = 0;
+  char* end;
+  long long v = strtoll(s, &end, 10);
+  if (errno || *end) return false;
+  *out = v;
+  return true;
+}
+
+static bool try_decimal(const char* s, long double* out) {
+  if (!s || !*s) return false;
+  // BigDecimal grammar: [+-]digits[.digits][(e|E)[+-]digits] or [+-].digits...
+  const char* p = s;
+  if (*p == '+' || *p == '-') p++;
+  bool digits = false;
+  while (*p >= '0' && *p <= '9') p++, digits = true;
+  if (*p == '.') {
+    p++;
+    while (*p >= '0' && *p <= '9') p++, digits = true;
+  }
+  if (!digits) return false;
+  if (*p == 'e' || *p == 'E') {
+    p++;
+    if (*p == '+' || *p == '-') p++;
+    if (!(*p >= '0' && *p <= '9')) return false;
+    while (*p >= '0' && *p <= '9') p++;
+  }
+  if (*p) return false;
+  *out = strtold(s, nullptr);
+  return true;
+}
+
+static int numeric_compare(const char* a, const char* b) {
+  if (a == b) return 0;
+  if (!a) return -1;
+  if (!b) return 1;
+  long long la, lb;
+  bool ha = try_long(a, &la), hb = try_long(b, &lb);
+  if (ha && hb) return (la > lb) - (la < lb);
+  long double da = ha ? (long double)la : 0, db = hb ? (long double)lb : 0;
+  bool pa = ha || try_decimal(a, &da), pb = hb || try_decimal(b, &db);
+  if (pa && pb) return (da > db) - (da < db);
+  if (!pa && !pb) return java_compare(a, b);
+  return pa ? 1 : -1;
+}
+
+// BoundFilter.doesMatch (BoundFilter.java:249-275), default null mode
+static bool bound_matches(const dg_filter& f, const char* value /* NULL = null */) {
+  const bool has_lower = f.lower != nullptr, has_upper = f.upper != nullptr;
+  if (!value) {
+    const bool lower_null = !has_lower || f.lower[0] == 0;
+    const bool upper_null = !has_upper || f.upper[0] == 0;
+    return (!has_lower || (lower_null && !f.lower_strict)) && (!has_upper || !upper_null || !f.upper_strict);
+  }
+  auto cmp = [&](const char* x, const char* y) {
+    if (f.ordering == DG_ORDER_NUMERIC) return numeric_compare(x, y);
+    return cmp_nullable(x == nullptr, x ? x : "", y == nullptr, y ? y : "");
+  };
+  const int lc = has_lower ? cmp(value, f.lower) : 1;
+  const int uc = has_upper ? cmp(f.upper, value) : 1;
+  if (f.lower_strict && f.upper_strict) return lc > 0 && uc > 0;
+  if (f.lower_strict) return lc > 0 && uc >= 0;
+  if (f.upper_strict) return lc >= 0 && uc > 0;
+  return lc >= 0 && uc >= 0;
+}
+
+static bool leaf_matches_null(const dg_filter& f) {
+  if (f.kind == DG_F_SELECTOR) return f.n_values < 1 || !f.values || !f.values[0] || !f.values[0][0];
+  if (f.kind == DG_F_IN) {
+    for (int i = 0; i < f.n_values; ++i)
+      if (!f.values[i] || !f.values[i][0]) return true;
+    return false;
+  }
+  return bound_matches(f, nullptr);
+}
+
+// ------------------------------------------------------------------------------------------------
+// filter planning: prefix nodes -> postfix program over leaf bitsets
+// ------------------------------------------------------------------------------------------------
+struct FilterPlan {
+  std::vector<int32_t> prog;
+  std::vector<std::vector<int32_t>> leaf_ids;  // dictionary ids whose bitmaps are OR-ed
+  std::vector<const Column*> leaf_col;
+};
+
+static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos, FilterPlan* fp) {
+  if (*pos >= n) return set_error(DG_ERR_ARG, "truncated filter");
+  const dg_filter& f = nodes[(*pos)++];
+  switch (f.kind) {
+    case DG_F_AND:
+    case DG_F_OR: {
+      if (f.n_children < 1) return set_error(DG_ERR_ARG, "empty and/or filter");
+      for (int c = 0; c < f.n_children; ++c) {
+        int rc = plan_node(seg, nodes, n, pos, fp);
+        if (rc) return rc;
+        if (c > 0) fp->prog.push_back(f.kind == DG_F_AND ? -3 : -4);
+      }
+      return DG_OK;
+    }
+    case DG_F_NOT: {
+      int rc = plan_node(seg, nodes, n, pos, fp);
+      if (rc) return rc;
+      fp->prog.push_back(-5);
+      return DG_OK;
+    }
+    case DG_F_SELECTOR:
+    case DG_F_IN:
+    case DG_F_BOUND: {
+      if (!f.dimension) return set_error(DG_ERR_ARG, "filter without dimension");
+      const Column* c = seg->find(f.dimension);
+      if (!c || c->type == DG_COL_LONG || c->type == DG_COL_FLOAT || c->type == DG_COL_DOUBLE) {
+        if (c) return set_error(DG_ERR_UNSUPPORTED, "filter on numeric column %s", f.dimension);
+        // missing column: allTrue iff the filter matches null (ColumnSelectorBitmapIndexSelector.java:212-218)
+        fp->prog.push_back(leaf_matches_null(f) ? -1 : -2);
+        return DG_OK;
+      }
+      if (c->type != DG_COL_STRING || !c->has_bitmaps)
+        return set_error(DG_ERR_UNSUPPORTED, "filter on %s needs a bitmap index", f.dimension);
+      std::vector<int32_t> ids;
+      if (f.kind == DG_F_SELECTOR) {
+        int i = index_of(c, f.n_values > 0 && f.values ? f.values[0] : nullptr);
+        if (i >= 0) ids.push_back(i);
+      } else if (f.kind == DG_F_IN) {
+        for (int k = 0; k < f.n_values; ++k) {
+          int i = index_of(c, f.values[k]);
+          if (i >= 0) ids.push_back(i);
+        }
+        std::sort(ids.begin(), ids.end());
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      } else if (f.ordering == DG_ORDER_LEXICOGRAPHIC) {
+        // BoundFilter.getStartEndIndexes (BoundFilter.java:141-174)
+        const int card = (int)c->dict.size();
+        int start, end;
+        if (!f.lower) start = 0;
+        else {
+          int found = index_of(c, f.lower);
+          start = found >= 0 ? (f.lower_strict ? found + 1 : found) : -(found + 1);
+        }
+        if (!f.upper) end = card;
+        else {
+          int found = index_of(c, f.upper);
+          end = found >= 0 ? (f.upper_strict ? found : found + 1) : -(found + 1);
+        }
+        if (end < start) end = start;
+        for (int i = start; i < end; ++i) ids.push_back(i);
+      } else if (f.ordering == DG_ORDER_NUMERIC) {
+        // predicate over every dictionary value (Filters.matchPredicate, Filters.java:239-290)
+        for (int i = 0; i < (int)c->dict.size(); ++i)
+          if (bound_matches(f, c->dict_null[i] ? nullptr : c->dict[i].c_str())) ids.push_back(i);
+      } else {
+        return set_error(DG_ERR_UNSUPPORTED, "bound ordering %d", f.ordering);
+      }
+      if (ids.empty()) {
+        fp->prog.push_back(-2);
+        return DG_OK;
+      }
+      fp->prog.push_back((int32_t)fp->leaf_ids.size());
+      fp->leaf_ids.push_back(std::move(ids));
+      fp->leaf_col.push_back(c);
+      return DG_OK;
+    }
+    default:
+      return set_error(DG_ERR_ARG, "unknown filter kind %d", f.kind);
+  }
+}
+
+// Build the row bitset of `filter` for segment `seg` on the device. *out = nullptr means "all rows".
+static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, int n_filter, uint32_t** out,
+                        int64_t* count, hipStream_t st) {
+  *out = nullptr;
+  *count = seg->nrows;
+  if (!filter || n_filter <= 0) return DG_OK;
+  FilterPlan fp;
+  int pos = 0;
+  int rc = plan_node(seg, filter, n_filter, &pos, &fp);
+  if (rc) return rc;
+  if (pos != n_filter) return set_error(DG_ERR_ARG, "filter has %d trailing nodes", n_filter - pos);
+  if (fp.prog.size() > 64) return set_error(DG_ERR_UNSUPPORTED, "filter program too long");
+  // stack depth check (kernel stack of 16)
+  int depth = 0, maxd = 0;
+  for (int op : fp.prog) {
+    if (op >= -2) depth++;
+    else if (op != -5) depth--;
+    maxd = std::max(maxd, depth);
+  }
+  if (maxd > 16) return set_error(DG_ERR_UNSUPPORTED, "filter nesting too deep");
+  const int64_t nwords = (seg->nrows + 31) / 32;
+  const int nleaves = (int)fp.leaf_ids.size();
+  uint32_t** h_sets = host_take<uint32_t*>(cs, std::max(nleaves, 1));
+  for (int l = 0; l < nleaves; ++l) {
+    h_sets[l] = dev_take<uint32_t>(cs, (size_t)nwords + 2);
+    if (!h_sets[l]) return set_error(DG_ERR_OOM, "bitset scratch");
+    DG_HIP(hipMemsetAsync(h_sets[l], 0, (size_t)(nwords + 2) * 4, st));
+  }
+  uint32_t** d_sets = dev_take<uint32_t*>(cs, std::max(nleaves, 1));
+  DG_HIP(hipMemcpyAsync(d_sets, h_sets, sizeof(void*) * std::max(nleaves, 1), hipMemcpyHostToDevice, st));
+  // one launch per (column, codec): group leaves by column
+  for (int l = 0; l < nleaves; ++l) {
+    const Column* c = fp.leaf_col[l];
+    // gather all leaves on the same column into this launch
+    bool first = true;
+    for (int k = 0; k < l; ++k)
+      if (fp.leaf_col[k] == c) first = false;
+    if (!first) continue;
+    std::vector<int64_t> offs;
+    std::vector<int32_t> lens, tgts;
+    for (int k = l; k < nleaves; ++k) {
+      if (fp.leaf_col[k] != c) continue;
+      for (int32_t id : fp.leaf_ids[k]) {
+        if (c->bm_len[id] == 0) continue;
+        offs.push_back(c->bm_off[id]);
+        lens.push_back(c->bm_len[id]);
+        tgts.push_back(k);
+      }
+    }
+    if (offs.empty()) continue;
+    const int nb = (int)offs.size();
+    int64_t* h_off = host_take<int64_t>(cs, nb);
+    int32_t* h_len = host_take<int32_t>(cs, nb);
+    int32_t* h_tgt = host_take<int32_t>(cs, nb);
+    memcpy(h_off, offs.data(), nb * 8);
+    memcpy(h_len, lens.data(), nb * 4);
+    memcpy(h_tgt, tgts.data(), nb * 4);
+    int64_t* d_off = dev_take<int64_t>(cs, nb);
+    int32_t* d_len = dev_take<int32_t>(cs, nb);
+    int32_t* d_tgt = dev_take<int32_t>(cs, nb);
+    DG_HIP(hipMemcpyAsync(d_off, h_off, nb * 8, hipMemcpyHostToDevice, st));
+    DG_HIP(hipMemcpyAsync(d_len, h_len, nb * 4, hipMemcpyHostToDevice, st));
+    DG_HIP(hipMemcpyAsync(d_tgt, h_tgt, nb * 4, hipMemcpyHostToDevice, st));
+    if (c->bitmap_roaring) {
+      int32_t* d_err = dev_take<int32_t>(cs, 1);
+      DG_HIP(hipMemsetAsync(d_err, 0, 4, st));
+      launch_roaring_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, d_err, (nwords + 2) * 32, st);
+    } else {
+      launch_concise_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, (nwords + 2) * 32, st);
+    }
+  }
+  const int plen = (int)fp.prog.size();
+  int32_t* h_prog = host_take<int32_t>(cs, plen);
+  memcpy(h_prog, fp.prog.data(), plen * 4);
+  int32_t* d_prog = dev_take<int32_t>(cs, plen);
+  DG_HIP(hipMemcpyAsync(d_prog, h_prog, plen * 4, hipMemcpyHostToDevice, st));
+  uint32_t* result = dev_take<uint32_t>(cs, (size_t)nwords + 2);
+  unsigned long long* d_count = dev_take<unsigned long long>(cs, 1);
+  DG_HIP(hipMemsetAsync(d_count, 0, 8, st));
+  launch_filter_eval(d_prog, plen, d_sets, result, seg->nrows, d_count, st);
+  unsigned long long* h_count = host_take<unsigned long long>(cs, 1);
+  DG_HIP(hipMemcpyAsync(h_count, d_count, 8, hipMemcpyDeviceToHost, st));
+  DG_HIP(hipStreamSynchronize(st));
+  *count = (int64_t)*h_count;
+  *out = result;
+  return DG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// column decode: returns a ColView, scheduling LZ4 block decodes into scratch when needed
+// ------------------------------------------------------------------------------------------------
+struct DecodeBatch {
+  std::vector<Lz4Job> jobs;
+  int64_t bytes = 0;  // algorithmic bytes read
+};
+
+static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
+  const BlockColumn& b = c->data;
+  v->log2_per = b.log2_per;
+  v->width = b.width;
+  v->pad = 0;
+  if (c->type == DG_COL_LONG) v->kind = VIEW_LONG;
+  else if (c->type == DG_COL_DOUBLE) v->kind = VIEW_DOUBLE;
+  else if (c->type == DG_COL_FLOAT) v->kind = VIEW_FLOAT;
+  else v->kind = VIEW_IDS;
+  db->bytes += b.stored_bytes;
+  if (b.codec == CODEC_LZ4) {
+    uint8_t* slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
+    const uint8_t** h_ptrs = host_take<const uint8_t*>(cs, std::max(b.nblocks, 1));
+    const uint8_t** d_ptrs = dev_take<const uint8_t*>(cs, std::max(b.nblocks, 1));
+    if (!slots || !h_ptrs || !d_ptrs) return set_error(DG_ERR_OOM, "decode scratch");
+    for (int32_t k = 0; k < b.nblocks; ++k) {
+      uint8_t* dst = slots + (size_t)k * kBlockBytes;
+      h_ptrs[k] = dst;
+      int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
+      if (rows <= 0) continue;
+      Lz4Job j;
+      j.src = b.comp.as<uint8_t>() + b.comp_off[k];
+      j.dst = dst;
+      j.src_len = b.comp_len[k];
+      j.expect_len = (int32_t)(rows * b.width);
+      db->jobs.push_back(j);
+    }
+    DG_HIP(hipMemcpyAsync(d_ptrs, h_ptrs, sizeof(void*) * std::max(b.nblocks, 1), hipMemcpyHostToDevice, st));
+    v->blocks = d_ptrs;
+    return DG_OK;
+  }
+  if (b.codec == CODEC_UNCOMPRESSED || b.codec == CODEC_NONE) {
+    v->blocks = b.block_ptrs.as<const uint8_t*>();
+    return DG_OK;
+  }
+  return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, c->name.c_str());
+}
+
+static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
+  if (db->jobs.empty()) return DG_OK;
+  const int n = (int)db->jobs.size();
+  Lz4Job* h = host_take<Lz4Job>(cs, n);
+  memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
+  Lz4Job* d = dev_take<Lz4Job>(cs, n);
+  int32_t* d_err = dev_take<int32_t>(cs, 1);
+  if (!h || !d || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
+  DG_HIP(hipMemcpyAsync(d, h, sizeof(Lz4Job) * n, hipMemcpyHostToDevice, st));
+  DG_HIP(hipMemsetAsync(d_err, 0, 4, st));
+  launch_lz4_decode(d, n, d_err, st);
+  int32_t* h_err = host_take<int32_t>(cs, 1);
+  DG_HIP(hipMemcpyAsync(h_err, d_err, 4, hipMemcpyDeviceToHost, st));
+  DG_HIP(hipStreamSynchronize(st));
+  if (*h_err) return set_error(DG_ERR_FORMAT, "corrupt LZ4 block");
+  return DG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// aggregator plan
+// ------------------------------------------------------------------------------------------------
+static int slot_op(int kind) {
+  switch (kind) {
+    case DG_AGG_COUNT:
+    case DG_AGG_LONG_SUM: return OP_ADD_I64;
+    case DG_AGG_DOUBLE_SUM:
+    case DG_AGG_FLOAT_SUM: return OP_ADD_F64;
+    case DG_AGG_LONG_MIN:
+    case DG_AGG_DOUBLE_MIN:
+    case DG_AGG_FLOAT_MIN: return OP_MIN_U64;
+    default: return OP_MAX_U64;
+  }
+}
+
+static uint64_t identity_host(int kind) {
+  switch (kind) {
+    case DG_AGG_LONG_MIN: return (uint64_t)INT64_MAX ^ 0x8000000000000000ull;
+    case DG_AGG_LONG_MAX: return (uint64_t)INT64_MIN ^ 0x8000000000000000ull;
+    case DG_AGG_DOUBLE_MIN:
+    case DG_AGG_FLOAT_MIN: return 0xFFF0000000000000ull;
+    case DG_AGG_DOUBLE_MAX:
+    case DG_AGG_FLOAT_MAX: return 0x000FFFFFFFFFFFFFull;
+    default: return 0;
+  }
+}
+
+static double unord_host(uint64_t k) {
+  uint64_t u = (k & 0x8000000000000000ull) ? (k & ~0x8000000000000000ull) : ~k;
+  double d;
+  memcpy(&d, &u, 8);
+  return d;
+}
+
+// device slot -> ABI slot (int64 / double / float-in-low-bytes)
+static uint64_t finalize_slot(int kind, uint64_t s) {
+  uint64_t out = 0;
+  switch (kind) {
+    case DG_AGG_COUNT:
+    case DG_AGG_LONG_SUM:
+    case DG_AGG_DOUBLE_SUM: return s;
+    case DG_AGG_FLOAT_SUM: {
+      double d;
+      memcpy(&d, &s, 8);
+      float f = (float)d;
+      memcpy(&out, &f, 4);
+      return out;
+    }
+    case DG_AGG_LONG_MIN:
+    case DG_AGG_LONG_MAX: return s ^ 0x8000000000000000ull;
+    case DG_AGG_DOUBLE_MIN:
+    case DG_AGG_DOUBLE_MAX: {
+      bool nan = kind == DG_AGG_DOUBLE_MIN ? s == 0 : s == ~0ull;
+      double d = nan ? NAN : unord_host(s);
+      memcpy(&out, &d, 8);
+      return out;
+    }
+    default: {
+      bool nan = kind == DG_AGG_FLOAT_MIN ? s == 0 : s == ~0ull;
+      float f = nan ? NAN : (float)unord_host(s);
+      memcpy(&out, &f, 4);
+      return out;
+    }
+  }
+}
+
+static int make_plan(const dg_scan* q, AggPlan* plan) {
+  if (q->n_aggs < 0 || q->n_aggs > kMaxAggs) return set_error(DG_ERR_UNSUPPORTED, "%d aggregators (max %d)", q->n_aggs, kMaxAggs);
+  memset(plan, 0, sizeof *plan);
+  plan->n = q->n_aggs;
+  for (int a = 0; a < q->n_aggs; ++a) {
+    int k = q->aggs[a].kind;
+    if (k < DG_AGG_COUNT || k > DG_AGG_FLOAT_MAX) return set_error(DG_ERR_ARG, "aggregator kind %d", k);
+    plan->kind[a] = k;
+    plan->op[a] = slot_op(k);
+  }
+  return DG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// cursors: granularity buckets of one segment (makeCursors / CursorSequenceBuilder.build)
+// ------------------------------------------------------------------------------------------------
+static const int64_t kMinInstant = -(1ll << 62);
+static const int64_t kMaxInstant = (1ll << 62) - 1;
+
+static int64_t floor_mod(int64_t a, int64_t b) {
+  int64_t m = a % b;
+  return m < 0 ? m + b : m;
+}
+
+struct Cursors {
+  bool any = false;       // interval overlaps the data interval
+  int64_t t_lo = 0, t_hi = 0;  // actual interval
+  int64_t bucket0 = 0;    // first bucket start (period) / bucket time (ALL)
+  int64_t nbuckets = 0;
+  bool need_time = false;
+};
+
+static Cursors plan_cursors(const Segment* seg, const dg_scan* q) {
+  Cursors c;
+  if (seg->nrows == 0) return c;
+  const int64_t P = q->period_ms;
+  auto bucket_start = [&](int64_t t) { return P ? t - floor_mod(t - q->origin_ms, P) : kMinInstant; };
+  const int64_t data_s = seg->min_time;
+  const int64_t data_e = P ? bucket_start(seg->max_time) + P : kMaxInstant;
+  if (!(q->interval_start < data_e && data_s < q->interval_end)) return c;
+  c.any = true;
+  c.t_lo = std::max(q->interval_start, data_s);
+  c.t_hi = std::min(q->interval_end, data_e);
+  if (P == 0) {
+    c.bucket0 = c.t_lo;
+    c.nbuckets = 1;
+    c.need_time = !(c.t_lo <= seg->min_time && seg->max_time < c.t_hi);
+  } else {
+    c.bucket0 = bucket_start(c.t_lo);
+    c.nbuckets = (c.t_hi - c.bucket0 + P - 1) / P;
+    c.need_time = true;
+  }
+  return c;
+}
+
+// ------------------------------------------------------------------------------------------------
+// ABI: library & context
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* dg_last_error(void) { return g_err; }
+int dg_abi_version(void) { return DG_ABI_VERSION; }
+
+int dg_device_count(int* out) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *out = n;
+  return DG_OK;
+}
+
+int dg_context_create(int device, dg_context** out) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return set_error(DG_ERR_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return set_error(DG_ERR_ARG, "device %d of %d", device, n);
+  DG_HIP(hipSetDevice(device));
+  Context* ctx = new Context();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return set_error(DG_ERR_DEVICE, "stream create failed");
+  }
+  ctx->own_stream = true;
+  for (auto& e : ctx->ev) hipEventCreate(&e);
+  *out = reinterpret_cast<dg_context*>(ctx);
+  return DG_OK;
+}
+
+void dg_context_release(dg_context* c) {
+  Context* ctx = reinterpret_cast<Context*>(c);
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  for (auto& e : ctx->ev) hipEventDestroy(e);
+  if (ctx->own_stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int dg_context_set_stream(dg_context* c, void* stream) {
+  Context* ctx = reinterpret_cast<Context*>(c);
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (ctx->own_stream) hipStreamDestroy(ctx->stream);
+  if (stream) {
+    ctx->stream = (hipStream_t)stream;
+    ctx->own_stream = false;
+  } else {
+    hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    ctx->own_stream = true;
+  }
+  return DG_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// time bounds (getMinTime / getMaxTime read the first / last __time row)
+// ------------------------------------------------------------------------------------------------
+int read_time_bounds(Segment* seg) {
+  if (seg->nrows == 0) return DG_OK;
+  Context* ctx = seg->ctx;
+  Column* t = seg->find("__time");
+  CallScratch* cs = scratch_of(ctx);
+  cs->dev.reset();
+  cs->host.reset();
+  DecodeBatch db;
+  ColView v;
+  hipStream_t st = ctx->stream;
+  const BlockColumn& b = t->data;
+  int64_t* h = host_take<int64_t>(cs, 2);
+  if (b.codec == CODEC_LZ4) {
+    // decode only the first and last block
+    uint8_t* slots = dev_take<uint8_t>(cs, 2 * (size_t)kBlockBytes + 64);
+    int32_t last = (int32_t)((seg->nrows - 1) >> b.log2_per);
+    for (int k = 0; k < 2; ++k) {
+      int32_t blk = k == 0 ? 0 : last;
+      int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)blk * b.size_per);
+      Lz4Job j;
+      j.src = b.comp.as<uint8_t>() + b.comp_off[blk];
+      j.dst = slots + (size_t)k * kBlockBytes;
+      j.src_len = b.comp_len[blk];
+      j.expect_len = (int32_t)(rows * 8);
+      db.jobs.push_back(j);
+    }
+    int rc = run_decodes(cs, &db, st);
+    if (rc) return rc;
+    int64_t idx_last = (seg->nrows - 1) & ((1ll << b.log2_per) - 1);
+    DG_HIP(hipMemcpyAsync(h, slots, 8, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h + 1, slots + kBlockBytes + idx_last * 8, 8, hipMemcpyDeviceToHost, st));
+  } else {
+    std::vector<const uint8_t*> ptrs(b.nblocks);
+    DG_HIP(hipMemcpy(ptrs.data(), b.block_ptrs.p, sizeof(void*) * b.nblocks, hipMemcpyDeviceToHost));
+    int64_t last = seg->nrows - 1;
+    DG_HIP(hipMemcpyAsync(h, ptrs[0], 8, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h + 1, ptrs[last >> b.log2_per] + (last & ((1ll << b.log2_per) - 1)) * 8, 8,
+                          hipMemcpyDeviceToHost, st));
+  }
+  (void)v;
+  DG_HIP(hipStreamSynchronize(st));
+  seg->min_time = h[0];
+  seg->max_time = h[1];
+  return DG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// common per-call setup
+// ------------------------------------------------------------------------------------------------
+struct CallGuard {
+  Context* ctx;
+  std::unique_lock<std::mutex> lock;
+  CallScratch* cs;
+  explicit CallGuard(Context* c) : ctx(c), lock(c->mu), cs(scratch_of(c)) {
+    hipSetDevice(c->device);
+    cs->dev.reset();
+    cs->host.reset();
+  }
+};
+
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+static int check_segments(dg_segment* const* segs, int32_t n, Context** ctx) {
+  if (n <= 0 || !segs) return set_error(DG_ERR_ARG, "no segments");
+  Context* c = nullptr;
+  for (int i = 0; i < n; ++i) {
+    Segment* s = reinterpret_cast<Segment*>(segs[i]);
+    if (!s) return set_error(DG_ERR_NOT_FOUND, "null segment");
+    if (c && s->ctx != c) return set_error(DG_ERR_ARG, "segments of one call must share a context");
+    c = s->ctx;
+  }
+  *ctx = c;
+  return DG_OK;
+}
+
+static bool cancelled(const dg_scan* q) { return q->cancel && *q->cancel; }
+
+// resolve an aggregator's input column into a view (absent column reads 0)
+static int agg_view(Segment* seg, const dg_agg& a, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
+  memset(v, 0, sizeof *v);
+  v->kind = VIEW_ABSENT;
+  if (a.kind == DG_AGG_COUNT || !a.field) return DG_OK;
+  Column* c = seg->find(a.field);
+  if (!c) return DG_OK;
+  if (c->type == DG_COL_STRING || c->type == DG_COL_UNSUPPORTED)
+    return set_error(DG_ERR_UNSUPPORTED, "aggregating non-numeric column %s", a.field);
+  return column_view(c, cs, db, v, st);
+}
+
+// per-segment tile assignment
+static int32_t* tile_table(CallScratch* cs, const std::vector<int64_t>& nrows, std::vector<int32_t>* begin, int* ntiles,
+                           hipStream_t st) {
+  int total = 0;
+  begin->resize(nrows.size());
+  for (size_t i = 0; i < nrows.size(); ++i) {
+    (*begin)[i] = total;
+    total += (int)((nrows[i] + kTileRows - 1) / kTileRows);
+  }
+  *ntiles = total;
+  int32_t* h = host_take<int32_t>(cs, std::max(total, 1));
+  for (size_t i = 0; i < nrows.size(); ++i) {
+    int nt = (int)((nrows[i] + kTileRows - 1) / kTileRows);
+    for (int k = 0; k < nt; ++k) h[(*begin)[i] + k] = (int32_t)i;
+  }
+  int32_t* d = dev_take<int32_t>(cs, std::max(total, 1));
+  if (hipMemcpyAsync(d, h, sizeof(int32_t) * std::max(total, 1), hipMemcpyHostToDevice, st) != hipSuccess) return nullptr;
+  return d;
+}
+
+}  // namespace dg
+
+using namespace dg;
+
+extern "C" {
+
+// ------------------------------------------------------------------------------------------------
+// segments
+// ------------------------------------------------------------------------------------------------
+int dg_segment_attach(dg_context* c, const char* dir, dg_segment** out) {
+  Context* ctx = reinterpret_cast<Context*>(c);
+  if (!ctx || !dir || !out) return set_error(DG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  hipSetDevice(ctx->device);
+  Segment* seg = nullptr;
+  int rc = load_segment(ctx, dir, &seg);
+  if (rc) return rc;
+  *out = reinterpret_cast<dg_segment*>(seg);
+  return DG_OK;
+}
+
+void dg_segment_release(dg_segment* s) {
+  Segment* seg = reinterpret_cast<Segment*>(s);
+  if (!seg) return;
+  std::lock_guard<std::mutex> g(seg->ctx->mu);
+  hipSetDevice(seg->ctx->device);
+  delete seg;
+}
+
+int64_t dg_segment_num_rows(const dg_segment* s) { return reinterpret_cast<const Segment*>(s)->nrows; }
+
+int dg_segment_interval(const dg_segment* s, int64_t* st, int64_t* en) {
+  const Segment* seg = reinterpret_cast<const Segment*>(s);
+  *st = seg->istart;
+  *en = seg->iend;
+  return DG_OK;
+}
+
+int dg_segment_time_bounds(const dg_segment* s, int64_t* mn, int64_t* mx) {
+  const Segment* seg = reinterpret_cast<const Segment*>(s);
+  *mn = seg->min_time;
+  *mx = seg->max_time;
+  return DG_OK;
+}
+
+int dg_segment_num_columns(const dg_segment* s) { return (int)reinterpret_cast<const Segment*>(s)->columns.size(); }
+
+const char* dg_segment_column_name(const dg_segment* s, int i) {
+  const Segment* seg = reinterpret_cast<const Segment*>(s);
+  if (i < 0 || i >= (int)seg->columns.size()) return nullptr;
+  return seg->columns[i]->name.c_str();
+}
+
+int dg_segment_column_type(const dg_segment* s, const char* col) {
+  const Column* c = reinterpret_cast<const Segment*>(s)->find(col ? col : "");
+  return c ? c->type : DG_COL_MISSING;
+}
+
+int64_t dg_segment_device_bytes(const dg_segment* s) { return reinterpret_cast<const Segment*>(s)->device_bytes; }
+
+int32_t dg_segment_dim_cardinality(const dg_segment* s, const char* dim) {
+  const Column* c = reinterpret_cast<const Segment*>(s)->find(dim ? dim : "");
+  if (!c || c->type != DG_COL_STRING) return -1;
+  return (int32_t)c->dict.size();
+}
+
+int dg_segment_dim_value(const dg_segment* s, const char* dim, int32_t id, const char** out, int32_t* len) {
+  const Column* c = reinterpret_cast<const Segment*>(s)->find(dim ? dim : "");
+  if (!c || c->type != DG_COL_STRING) return set_error(DG_ERR_NOT_FOUND, "no string column %s", dim ? dim : "");
+  if (id < 0 || id >= (int32_t)c->dict.size()) return set_error(DG_ERR_ARG, "id %d out of range", id);
+  *out = c->dict[id].c_str();
+  *len = c->dict_null[id] ? -1 : (int32_t)c->dict[id].size();
+  return DG_OK;
+}
+
+int dg_segment_dim_dictionary(const dg_segment* s, const char* dim, int64_t* offsets, char* bytes, int64_t* total) {
+  const Column* c = reinterpret_cast<const Segment*>(s)->find(dim ? dim : "");
+  if (!c || c->type != DG_COL_STRING) return set_error(DG_ERR_NOT_FOUND, "no string column %s", dim ? dim : "");
+  int64_t t = 0;
+  for (size_t i = 0; i < c->dict.size(); ++i) {
+    if (offsets) offsets[i] = t;
+    if (bytes) memcpy(bytes + t, c->dict[i].data(), c->dict[i].size());
+    t += (int64_t)c->dict[i].size();
+  }
+  if (offsets) offsets[c->dict.size()] = t;
+  if (total) *total = t;
+  return DG_OK;
+}
+
+int dg_filter_bitmap(dg_segment* s, const dg_filter* filter, int32_t n_filter, uint32_t* out_words, int64_t* out_count) {
+  Segment* seg = reinterpret_cast<Segment*>(s);
+  if (!seg || !out_words) return set_error(DG_ERR_ARG, "null argument");
+  CallGuard g(seg->ctx);
+  hipStream_t st = seg->ctx->stream;
+  uint32_t* bits = nullptr;
+  int64_t count = 0;
+  int rc = build_bitset(seg, g.cs, filter, n_filter, &bits, &count, st);
+  if (rc) return rc;
+  const int64_t nwords = (seg->nrows + 31) / 32;
+  if (!bits) {
+    for (int64_t w = 0; w < nwords; ++w) out_words[w] = 0xFFFFFFFFu;
+    if (seg->nrows & 31) out_words[nwords - 1] = (1u << (seg->nrows & 31)) - 1u;
+  } else {
+    DG_HIP(hipMemcpyAsync(out_words, bits, nwords * 4, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipStreamSynchronize(st));
+  }
+  if (out_count) *out_count = count;
+  return DG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// timeseries
+// ------------------------------------------------------------------------------------------------
+int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int32_t bucket_cap, int32_t* out_nb,
+                      int64_t* out_time, int64_t* out_rows, uint64_t* out_values, dg_metrics* metrics) {
+  auto t0 = std::chrono::steady_clock::now();
+  Context* ctx;
+  int rc = check_segments(segs, n, &ctx);
+  if (rc) return rc;
+  if (!q) return set_error(DG_ERR_ARG, "null scan");
+  AggPlan plan;
+  rc = make_plan(q, &plan);
+  if (rc) return rc;
+  CallGuard g(ctx);
+  CallScratch* cs = g.cs;
+  hipStream_t st = ctx->stream;
+  dg_metrics m;
+  memset(&m, 0, sizeof m);
+  const int na = plan.n, rec = na + 1;
+  std::vector<Cursors> cur(n);
+  std::vector<ScanJob> jobs(n);
+  std::vector<int64_t> tiles_rows(n, 0);
+  DecodeBatch db;
+  hipEventRecord(ctx->ev[0], st);
+  for (int i = 0; i < n; ++i) {
+    Segment* seg = reinterpret_cast<Segment*>(segs[i]);
+    cur[i] = plan_cursors(seg, q);
+    out_nb[i] = (int32_t)(cur[i].any ? cur[i].nbuckets : 0);
+    m.segment_rows += seg->nrows;
+    if (!cur[i].any) continue;
+    if (cur[i].nbuckets > bucket_cap) return set_error(DG_ERR_ARG, "%lld buckets > cap %d", (long long)cur[i].nbuckets, bucket_cap);
+    uint32_t* bits = nullptr;
+    int64_t cnt = 0;
+    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &cnt, st);
+    if (rc) return rc;
+    m.pre_filtered_rows += cnt;
+    ScanJob& j = jobs[i];
+    memset(&j, 0, sizeof j);
+    j.nrows = (int32_t)seg->nrows;
+    j.bitset = bits;
+    j.t_lo = cur[i].t_lo;
+    j.t_hi = cur[i].t_hi;
+    j.bucket0 = cur[i].bucket0;
+    j.period = q->period_ms;
+    j.nbuckets = (int32_t)cur[i].nbuckets;
+    j.time.kind = VIEW_ABSENT;
+    if (cur[i].need_time) {
+      rc = column_view(seg->find("__time"), cs, &db, &j.time, st);
+      if (rc) return rc;
+    }
+    for (int a = 0; a < na; ++a) {
+      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], st);
+      if (rc) return rc;
+    }
+    j.out = dev_take<uint64_t>(cs, (size_t)cur[i].nbuckets * rec);
+    if (!j.out) return set_error(DG_ERR_OOM, "accumulators");
+    tiles_rows[i] = seg->nrows;
+    for (int k = 0; k < n; ++k) (void)k;
+  }
+  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  hipEventRecord(ctx->ev[1], st);
+  rc = run_decodes(cs, &db, st);
+  if (rc) return rc;
+  hipEventRecord(ctx->ev[2], st);
+  m.bytes_read = db.bytes;
+  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  // init accumulators
+  uint64_t* h_init = host_take<uint64_t>(cs, rec);
+  h_init[0] = 0;
+  for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
+  uint64_t* d_init = dev_take<uint64_t>(cs, rec);
+  DG_HIP(hipMemcpyAsync(d_init, h_init, rec * 8, hipMemcpyHostToDevice, st));
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, d_init, st);
+  std::vector<int32_t> begin;
+  int ntiles = 0;
+  for (int i = 0; i < n; ++i)
+    if (!cur[i].any) tiles_rows[i] = 0;
+  int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
+  if (!d_tile) return set_error(DG_ERR_DEVICE, "tile table");
+  for (int i = 0; i < n; ++i) jobs[i].tile_begin = begin[i];
+  ScanJob* h_jobs = host_take<ScanJob>(cs, n);
+  memcpy(h_jobs, jobs.data(), sizeof(ScanJob) * n);
+  ScanJob* d_jobs = dev_take<ScanJob>(cs, n);
+  DG_HIP(hipMemcpyAsync(d_jobs, h_jobs, sizeof(ScanJob) * n, hipMemcpyHostToDevice, st));
+  hipEventRecord(ctx->ev[3], st);
+  launch_scan_agg(d_jobs, d_tile, ntiles, plan, 0, st);
+  hipEventRecord(ctx->ev[4], st);
+  // results
+  std::vector<uint64_t*> h_out(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    h_out[i] = host_take<uint64_t>(cs, (size_t)cur[i].nbuckets * rec);
+    DG_HIP(hipMemcpyAsync(h_out[i], jobs[i].out, (size_t)cur[i].nbuckets * rec * 8, hipMemcpyDeviceToHost, st));
+  }
+  DG_HIP(hipStreamSynchronize(st));
+  DG_HIP(hipGetLastError());
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    for (int64_t b = 0; b < cur[i].nbuckets; ++b) {
+      const int64_t o = (int64_t)i * bucket_cap + b;
+      out_time[o] = q->period_ms ? cur[i].bucket0 + b * q->period_ms : cur[i].t_lo;
+      out_rows[o] = (int64_t)h_out[i][b * rec];
+      m.selected_rows += out_rows[o];
+      for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_out[i][b * rec + 1 + a]);
+    }
+  }
+  float f1 = 0, f2 = 0, f3 = 0;
+  hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
+  hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
+  hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
+  m.bitmap_ms = f1;
+  m.decode_ms = f2;
+  m.aggregate_ms = f3;
+  m.total_ms = ms_since(t0);
+  if (metrics) *metrics = m;
+  return DG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// topN
+// ------------------------------------------------------------------------------------------------
+static uint64_t metric_key_host(uint64_t slot, int kind, int inverted) {
+  uint64_t k;
+  auto ord = [](double d) {
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+  };
+  int op = slot_op(kind);
+  if (op == OP_ADD_I64) {
+    k = slot ^ 0x8000000000000000ull;
+  } else if (op == OP_ADD_F64) {
+    double d;
+    memcpy(&d, &slot, 8);
+    if (kind == DG_AGG_FLOAT_SUM) d = (double)(float)d;
+    k = std::isnan(d) ? ~0ull : ord(d);
+  } else if (kind == DG_AGG_LONG_MIN || kind == DG_AGG_LONG_MAX) {
+    k = slot;
+  } else {
+    bool nan = op == OP_MIN_U64 ? slot == 0 : slot == ~0ull;
+    if (nan) k = ~0ull;
+    else {
+      double d = unord_host(slot);
+      if (kind == DG_AGG_FLOAT_MIN || kind == DG_AGG_FLOAT_MAX) d = (double)(float)d;
+      k = ord(d);
+    }
+  }
+  return inverted ? ~k : k;
+}
+
+int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_topn* t, int32_t* out_n, int32_t* out_ids,
+                uint64_t* out_values, dg_metrics* metrics) {
+  auto t0 = std::chrono::steady_clock::now();
+  Context* ctx;
+  int rc = check_segments(segs, n, &ctx);
+  if (rc) return rc;
+  if (!q || !t || !t->dimension) return set_error(DG_ERR_ARG, "null argument");
+  if (q->period_ms != 0) return set_error(DG_ERR_UNSUPPORTED, "topN with non-ALL granularity");
+  if (t->metric_agg < 0 || t->metric_agg >= q->n_aggs) return set_error(DG_ERR_ARG, "metric index");
+  if (t->threshold <= 0) return set_error(DG_ERR_ARG, "threshold");
+  AggPlan plan;
+  rc = make_plan(q, &plan);
+  if (rc) return rc;
+  CallGuard g(ctx);
+  CallScratch* cs = g.cs;
+  hipStream_t st = ctx->stream;
+  dg_metrics m;
+  memset(&m, 0, sizeof m);
+  const int na = plan.n, rec = na + 1;
+  std::vector<Cursors> cur(n);
+  std::vector<ScanJob> jobs(n);
+  std::vector<int64_t> card(n, 1), tiles_rows(n, 0);
+  DecodeBatch db;
+  hipEventRecord(ctx->ev[0], st);
+  for (int i = 0; i < n; ++i) {
+    Segment* seg = reinterpret_cast<Segment*>(segs[i]);
+    cur[i] = plan_cursors(seg, q);
+    m.segment_rows += seg->nrows;
+    out_n[i] = -1;
+    if (!cur[i].any) continue;
+    ScanJob& j = jobs[i];
+    memset(&j, 0, sizeof j);
+    Column* dc = seg->find(t->dimension);
+    if (dc && dc->type != DG_COL_STRING) return set_error(DG_ERR_UNSUPPORTED, "topN on non-string dimension %s", t->dimension);
+    uint32_t* bits = nullptr;
+    int64_t cnt = 0;
+    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &cnt, st);
+    if (rc) return rc;
+    m.pre_filtered_rows += cnt;
+    j.nrows = (int32_t)seg->nrows;
+    j.bitset = bits;
+    j.t_lo = cur[i].t_lo;
+    j.t_hi = cur[i].t_hi;
+    j.time.kind = VIEW_ABSENT;
+    if (cur[i].need_time) {
+      rc = column_view(seg->find("__time"), cs, &db, &j.time, st);
+      if (rc) return rc;
+    }
+    if (dc) {
+      rc = column_view(dc, cs, &db, &j.key, st);
+      if (rc) return rc;
+      card[i] = std::max<int64_t>((int64_t)dc->dict.size(), 1);
+    } else {
+      // missing dimension: every row has the null value -> one group (id 0)
+      static_assert(sizeof(ColView) == 24, "ColView layout");
+      memset(&j.key, 0, sizeof j.key);
+      j.key.kind = VIEW_ABSENT;
+      card[i] = 1;
+    }
+    for (int a = 0; a < na; ++a) {
+      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], st);
+      if (rc) return rc;
+    }
+    j.out = dev_take<uint64_t>(cs, (size_t)card[i] * rec);
+    if (!j.out) return set_error(DG_ERR_OOM, "topN table");
+    tiles_rows[i] = seg->nrows;
+  }
+  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  hipEventRecord(ctx->ev[1], st);
+  rc = run_decodes(cs, &db, st);
+  if (rc) return rc;
+  hipEventRecord(ctx->ev[2], st);
+  m.bytes_read = db.bytes;
+  uint64_t* h_init = host_take<uint64_t>(cs, rec);
+  h_init[0] = 0;
+  for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
+  uint64_t* d_init = dev_take<uint64_t>(cs, rec);
+  DG_HIP(hipMemcpyAsync(d_init, h_init, rec * 8, hipMemcpyHostToDevice, st));
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) launch_fill_u64(jobs[i].out, card[i], rec, d_init, st);
+  std::vector<int32_t> begin;
+  int ntiles = 0;
+  int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
+  if (!d_tile) return set_error(DG_ERR_DEVICE, "tile table");
+  for (int i = 0; i < n; ++i) jobs[i].tile_begin = begin[i];
+  ScanJob* h_jobs = host_take<ScanJob>(cs, n);
+  memcpy(h_jobs, jobs.data(), sizeof(ScanJob) * n);
+  ScanJob* d_jobs = dev_take<ScanJob>(cs, n);
+  DG_HIP(hipMemcpyAsync(d_jobs, h_jobs, sizeof(ScanJob) * n, hipMemcpyHostToDevice, st));
+  hipEventRecord(ctx->ev[3], st);
+  // missing-dimension segments: the key view is absent; load_id would fault, so route them
+  // through a 1-entry table with a zero id view
+  for (int i = 0; i < n; ++i) {
+    if (cur[i].any && jobs[i].key.kind == VIEW_ABSENT) {
+      // a constant-zero id column: block pointer table pointing at a zeroed 64 KiB slot
+      uint8_t* zero = dev_take<uint8_t>(cs, kBlockBytes);
+      DG_HIP(hipMemsetAsync(zero, 0, kBlockBytes, st));
+      const int nb = (int)((jobs[i].nrows + 65535) / 65536) + 1;
+      const uint8_t** hp = host_take<const uint8_t*>(cs, nb);
+      for (int k = 0; k < nb; ++k) hp[k] = zero;
+      const uint8_t** dp = dev_take<const uint8_t*>(cs, nb);
+      DG_HIP(hipMemcpyAsync(dp, hp, sizeof(void*) * nb, hipMemcpyHostToDevice, st));
+      ScanJob fixed = jobs[i];
+      fixed.key.blocks = dp;
+      fixed.key.log2_per = 16;
+      fixed.key.width = 1;
+      fixed.key.kind = VIEW_IDS;
+      h_jobs[i] = fixed;
+      DG_HIP(hipMemcpyAsync(d_jobs + i, h_jobs + i, sizeof(ScanJob), hipMemcpyHostToDevice, st));
+    }
+  }
+  launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
+  // selection
+  const int mk = plan.kind[t->metric_agg];
+  const int metric_op = (slot_op(mk) << 8) | mk;
+  std::vector<int32_t*> d_cand(n, nullptr);
+  int32_t* d_ncand = dev_take<int32_t>(cs, n);
+  uint64_t* d_state = dev_take<uint64_t>(cs, n);
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    d_cand[i] = dev_take<int32_t>(cs, (size_t)card[i]);
+    launch_topn_select(jobs[i].out, card[i], na, t->metric_agg, metric_op, t->inverted, t->threshold, d_state + i,
+                       d_cand[i], d_ncand + i, (int)card[i], st);
+  }
+  hipEventRecord(ctx->ev[4], st);
+  int32_t* h_ncand = host_take<int32_t>(cs, n);
+  DG_HIP(hipMemcpyAsync(h_ncand, d_ncand, 4 * n, hipMemcpyDeviceToHost, st));
+  DG_HIP(hipStreamSynchronize(st));
+  DG_HIP(hipGetLastError());
+  // fetch candidate ids and their records (small: threshold + ties)
+  std::vector<int32_t*> h_cand(n, nullptr);
+  std::vector<uint64_t*> h_tab(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    const int nc = h_ncand[i];
+    h_cand[i] = host_take<int32_t>(cs, std::max(nc, 1));
+    DG_HIP(hipMemcpyAsync(h_cand[i], d_cand[i], 4 * (size_t)std::max(nc, 0), hipMemcpyDeviceToHost, st));
+  }
+  DG_HIP(hipStreamSynchronize(st));
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    const int nc = h_ncand[i];
+    h_tab[i] = host_take<uint64_t>(cs, (size_t)std::max(nc, 1) * rec);
+    // candidates are ascending ids: copy contiguous runs of records
+    for (int k = 0; k < nc;) {
+      int e = k + 1;
+      while (e < nc && h_cand[i][e] == h_cand[i][e - 1] + 1) e++;
+      DG_HIP(hipMemcpyAsync(h_tab[i] + (size_t)k * rec, jobs[i].out + (size_t)h_cand[i][k] * rec,
+                            (size_t)(e - k) * rec * 8, hipMemcpyDeviceToHost, st));
+      k = e;
+    }
+  }
+  DG_HIP(hipStreamSynchronize(st));
+  // replay TopNNumericResultBuilder over the candidates in id (= dimension value) order
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    const int nc = h_ncand[i];
+    struct E {
+      uint64_t key;
+      int32_t id;
+      int32_t idx;
+    };
+    auto less = [](const E& a, const E& b) { return a.key != b.key ? a.key < b.key : a.id < b.id; };
+    auto gt = [&](const E& a, const E& b) { return less(b, a); };
+    std::priority_queue<E, std::vector<E>, decltype(gt)> pq(gt);  // min-heap on (key, id)
+    for (int k = 0; k < nc; ++k) {
+      E e{metric_key_host(h_tab[i][(size_t)k * rec + 1 + t->metric_agg], mk, t->inverted), h_cand[i][k], k};
+      m.selected_rows += 0;
+      if ((int)pq.size() < t->threshold || pq.top().key < e.key) pq.push(e);
+      if ((int)pq.size() > t->threshold) pq.pop();
+    }
+    std::vector<E> v;
+    while (!pq.empty()) {
+      v.push_back(pq.top());
+      pq.pop();
+    }
+    std::sort(v.begin(), v.end(), [](const E& a, const E& b) { return a.key != b.key ? a.key > b.key : a.id < b.id; });
+    out_n[i] = (int32_t)v.size();
+    for (size_t k = 0; k < v.size(); ++k) {
+      const int64_t o = (int64_t)i * t->threshold + (int64_t)k;
+      out_ids[o] = v[k].id;
+      for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[i][(size_t)v[k].idx * rec + 1 + a]);
+    }
+  }
+  float f1 = 0, f2 = 0, f3 = 0;
+  hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
+  hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
+  hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
+  m.bitmap_ms = f1;
+  m.decode_ms = f2;
+  m.aggregate_ms = f3;
+  m.total_ms = ms_since(t0);
+  if (metrics) *metrics = m;
+  return DG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// groupBy
+// ------------------------------------------------------------------------------------------------
+}  // extern "C"
+
+struct dg_result {
+  int n = 0;
+  int ndims = 0, naggs = 0;
+  std::vector<std::vector<int64_t>> time;
+  std::vector<std::vector<int32_t>> ids;
+  std::vector<std::vector<uint64_t>> vals;
+};
+
+static int bits_for(int64_t card) {
+  int b = 0;
+  while ((1ll << b) < card) b++;
+  return b;
+}
+
+extern "C" {
+
+int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_groupby* gb, dg_result** out,
+                   dg_metrics* metrics) {
+  auto t0 = std::chrono::steady_clock::now();
+  Context* ctx;
+  int rc = check_segments(segs, n, &ctx);
+  if (rc) return rc;
+  if (!q || !gb || !out) return set_error(DG_ERR_ARG, "null argument");
+  if (gb->n_dims < 0 || gb->n_dims > 4) return set_error(DG_ERR_UNSUPPORTED, "%d groupBy dimensions (max 4)", gb->n_dims);
+  AggPlan plan;
+  rc = make_plan(q, &plan);
+  if (rc) return rc;
+  CallGuard g(ctx);
+  CallScratch* cs = g.cs;
+  hipStream_t st = ctx->stream;
+  dg_metrics m;
+  memset(&m, 0, sizeof m);
+  const int na = plan.n, rec = na + 1;
+  std::vector<Cursors> cur(n);
+  std::vector<GroupJob> jobs(n);
+  std::vector<int64_t> tiles_rows(n, 0);
+  std::vector<uint64_t> cap(n, 0);
+  DecodeBatch db;
+  int32_t* d_over = dev_take<int32_t>(cs, 1);
+  DG_HIP(hipMemsetAsync(d_over, 0, 4, st));
+  hipEventRecord(ctx->ev[0], st);
+  for (int i = 0; i < n; ++i) {
+    Segment* seg = reinterpret_cast<Segment*>(segs[i]);
+    cur[i] = plan_cursors(seg, q);
+    m.segment_rows += seg->nrows;
+    if (!cur[i].any) continue;
+    GroupJob& j = jobs[i];
+    memset(&j, 0, sizeof j);
+    uint32_t* bits = nullptr;
+    int64_t cnt = 0;
+    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &cnt, st);
+    if (rc) return rc;
+    m.pre_filtered_rows += cnt;
+    j.nrows = (int32_t)seg->nrows;
+    j.bitset = bits;
+    j.t_lo = cur[i].t_lo;
+    j.t_hi = cur[i].t_hi;
+    j.bucket0 = cur[i].bucket0;
+    j.period = q->period_ms;
+    j.nbuckets = (int32_t)cur[i].nbuckets;
+    j.time.kind = VIEW_ABSENT;
+    if (cur[i].need_time) {
+      rc = column_view(seg->find("__time"), cs, &db, &j.time, st);
+      if (rc) return rc;
+    }
+    j.ndims = gb->n_dims;
+    int shift = 0;
+    double space = 1.0;
+    for (int d = gb->n_dims - 1; d >= 0; --d) {
+      Column* c = seg->find(gb->dimensions[d]);
+      int64_t card = 1;
+      if (c) {
+        if (c->type != DG_COL_STRING) return set_error(DG_ERR_UNSUPPORTED, "groupBy on non-string column %s", gb->dimensions[d]);
+        rc = column_view(c, cs, &db, &j.dims[d], st);
+        if (rc) return rc;
+        card = std::max<int64_t>((int64_t)c->dict.size(), 1);
+      } else {
+        j.dims[d].kind = VIEW_ABSENT;
+      }
+      j.dim_shift[d] = shift;
+      shift += bits_for(card);
+      space *= (double)card;
+    }
+    j.bucket_shift = shift;
+    shift += bits_for(cur[i].nbuckets);
+    space *= (double)cur[i].nbuckets;
+    if (shift > 63) return set_error(DG_ERR_UNSUPPORTED, "groupBy key of %d bits", shift);
+    for (int a = 0; a < na; ++a) {
+      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], st);
+      if (rc) return rc;
+    }
+    double groups = std::min(space, (double)std::max<int64_t>(cnt, 1));
+    uint64_t c2 = 1024;
+    while ((double)c2 < 2.0 * groups) c2 <<= 1;
+    cap[i] = c2;
+    j.keys = dev_take<uint64_t>(cs, c2);
+    j.slots = dev_take<uint64_t>(cs, c2 * rec);
+    if (!j.keys || !j.slots) return set_error(DG_ERR_OOM, "groupBy table of %llu", (unsigned long long)c2);
+    j.mask = c2 - 1;
+    j.overflow = d_over;
+    DG_HIP(hipMemsetAsync(j.keys, 0xFF, c2 * 8, st));
+    tiles_rows[i] = seg->nrows;
+  }
+  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  hipEventRecord(ctx->ev[1], st);
+  rc = run_decodes(cs, &db, st);
+  if (rc) return rc;
+  hipEventRecord(ctx->ev[2], st);
+  m.bytes_read = db.bytes;
+  uint64_t* h_init = host_take<uint64_t>(cs, rec);
+  h_init[0] = 0;
+  for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
+  uint64_t* d_init = dev_take<uint64_t>(cs, rec);
+  DG_HIP(hipMemcpyAsync(d_init, h_init, rec * 8, hipMemcpyHostToDevice, st));
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) launch_fill_u64(jobs[i].slots, (int64_t)cap[i], rec, d_init, st);
+  std::vector<int32_t> begin;
+  int ntiles = 0;
+  int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
+  if (!d_tile) return set_error(DG_ERR_DEVICE, "tile table");
+  for (int i = 0; i < n; ++i) jobs[i].tile_begin = begin[i];
+  GroupJob* h_jobs = host_take<GroupJob>(cs, n);
+  memcpy(h_jobs, jobs.data(), sizeof(GroupJob) * n);
+  GroupJob* d_jobs = dev_take<GroupJob>(cs, n);
+  DG_HIP(hipMemcpyAsync(d_jobs, h_jobs, sizeof(GroupJob) * n, hipMemcpyHostToDevice, st));
+  hipEventRecord(ctx->ev[3], st);
+  launch_groupby(d_jobs, d_tile, ntiles, plan, st);
+  // compaction
+  unsigned long long* d_cnt = dev_take<unsigned long long>(cs, n);
+  DG_HIP(hipMemsetAsync(d_cnt, 0, 8 * n, st));
+  std::vector<uint64_t*> ok(n, nullptr), os(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    uint64_t bound = std::min<uint64_t>(cap[i], (uint64_t)std::max<int64_t>(jobs[i].nrows, 1));
+    ok[i] = dev_take<uint64_t>(cs, bound);
+    os[i] = dev_take<uint64_t>(cs, bound * rec);
+    if (!ok[i] || !os[i]) return set_error(DG_ERR_OOM, "groupBy output");
+    launch_groupby_compact(jobs[i].keys, jobs[i].slots, cap[i], rec, ok[i], os[i], d_cnt + i, st);
+  }
+  hipEventRecord(ctx->ev[4], st);
+  unsigned long long* h_cnt = host_take<unsigned long long>(cs, n);
+  int32_t* h_over = host_take<int32_t>(cs, 1);
+  DG_HIP(hipMemcpyAsync(h_cnt, d_cnt, 8 * n, hipMemcpyDeviceToHost, st));
+  DG_HIP(hipMemcpyAsync(h_over, d_over, 4, hipMemcpyDeviceToHost, st));
+  DG_HIP(hipStreamSynchronize(st));
+  DG_HIP(hipGetLastError());
+  if (*h_over) return set_error(DG_ERR_TABLE_FULL, "groupBy hash table full");
+  std::unique_ptr<dg_result> res(new dg_result());
+  res->n = n;
+  res->ndims = gb->n_dims;
+  res->naggs = na;
+  res->time.resize(n);
+  res->ids.resize(n);
+  res->vals.resize(n);
+  std::vector<std::vector<uint64_t>> hk(n), hs(n);
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    hk[i].resize(h_cnt[i]);
+    hs[i].resize(h_cnt[i] * rec);
+    if (h_cnt[i]) {
+      DG_HIP(hipMemcpyAsync(hk[i].data(), ok[i], h_cnt[i] * 8, hipMemcpyDeviceToHost, st));
+      DG_HIP(hipMemcpyAsync(hs[i].data(), os[i], h_cnt[i] * rec * 8, hipMemcpyDeviceToHost, st));
+    }
+  }
+  DG_HIP(hipStreamSynchronize(st));
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    const GroupJob& j = jobs[i];
+    const size_t ng = hk[i].size();
+    res->time[i].resize(ng);
+    res->ids[i].resize(ng * gb->n_dims);
+    res->vals[i].resize(ng * na);
+    for (size_t k = 0; k < ng; ++k) {
+      const uint64_t key = hk[i][k];
+      const int64_t b = (int64_t)(key >> j.bucket_shift);
+      res->time[i][k] = q->period_ms ? cur[i].bucket0 + b * q->period_ms : cur[i].t_lo;
+      for (int d = 0; d < gb->n_dims; ++d) {
+        const int next = d == 0 ? j.bucket_shift : j.dim_shift[d - 1];
+        const int width = next - j.dim_shift[d];
+        res->ids[i][k * gb->n_dims + d] = (int32_t)((key >> j.dim_shift[d]) & (width ? ((1ull << width) - 1) : 0));
+      }
+      m.selected_rows += (int64_t)hs[i][k * rec];
+      for (int a = 0; a < na; ++a) res->vals[i][k * na + a] = finalize_slot(plan.kind[a], hs[i][k * rec + 1 + a]);
+    }
+  }
+  float f1 = 0, f2 = 0, f3 = 0;
+  hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
+  hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
+  hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
+  m.bitmap_ms = f1;
+  m.decode_ms = f2;
+  m.aggregate_ms = f3;
+  m.total_ms = ms_since(t0);
+  if (metrics) *metrics = m;
+  *out = res.release();
+  return DG_OK;
+}
+
+int64_t dg_result_groups(const dg_result* r, int32_t i) {
+  if (!r || i < 0 || i >= r->n) return -1;
+  return (int64_t)r->time[i].size();
+}
+
+int dg_result_fetch_groups(dg_result* r, int32_t i, int64_t* t, int32_t* ids, uint64_t* vals) {
+  if (!r || i < 0 || i >= r->n) return set_error(DG_ERR_ARG, "bad result index");
+  const size_t ng = r->time[i].size();
+  if (t) memcpy(t, r->time[i].data(), ng * 8);
+  if (ids) memcpy(ids, r->ids[i].data(), ng * r->ndims * 4);
+  if (vals) memcpy(vals, r->vals[i].data(), ng * r->naggs * 8);
+  return DG_OK;
+}
+
+void dg_result_release(dg_result* r) { delete r; }
+
+}  // extern "C"

@@ -1,0 +1,194 @@
+// dg_internal.h — structures shared by the host engine (dg_segment.cpp, dg_engine.cpp) and the
+// HIP kernels (dg_kernels.hip). Device-side descriptors are plain PODs copied into HBM per call.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/druidgpu.h"
+
+namespace dg {
+
+constexpr int kMaxAggs = 8;
+constexpr int kBlockBytes = 65536;  // CompressedPools.BUFFER_SIZE (segment/CompressedPools.java:39)
+
+// stored codecs (CompressionStrategy ids, data/CompressionStrategy.java:48-107)
+enum Codec : int32_t { CODEC_LZ4 = 0x01, CODEC_UNCOMPRESSED = 0xFF, CODEC_NONE = 0xFE };
+
+// value kinds a kernel can read from a column view
+enum ViewKind : int32_t { VIEW_ABSENT = 0, VIEW_LONG = 1, VIEW_FLOAT = 2, VIEW_DOUBLE = 3, VIEW_IDS = 4 };
+
+// accumulator slot ops (all slots are 8 bytes)
+enum SlotOp : int32_t { OP_ADD_I64 = 0, OP_ADD_F64 = 1, OP_MIN_U64 = 2, OP_MAX_U64 = 3 };
+
+// A column as the kernels see it: value(row) lives at blocks[row >> log2_per] + (row & mask) * width.
+struct ColView {
+  const uint8_t* const* blocks;
+  int32_t log2_per;
+  int32_t width;
+  int32_t kind;
+  int32_t pad;
+};
+
+// One LZ4 block to decode (compressed bytes are 16-byte aligned in the device image).
+struct Lz4Job {
+  const uint8_t* src;
+  uint8_t* dst;
+  int32_t src_len;
+  int32_t expect_len;  // bytes that must come out (>= rows * width of the block)
+};
+
+struct AggPlan {
+  int32_t n;
+  int32_t kind[kMaxAggs];   // DG_AGG_*
+  int32_t op[kMaxAggs];     // SlotOp
+};
+
+// One segment's share of a scan kernel.
+struct ScanJob {
+  int32_t nrows;
+  int32_t tile_begin;       // first global tile index of this segment
+  const uint32_t* bitset;   // null: every row passes the filter
+  ColView time;             // VIEW_ABSENT when the time column is not needed
+  int64_t t_lo, t_hi;       // rows with t in [t_lo, t_hi)
+  int64_t bucket0;          // start of the first bucket
+  int64_t period;           // 0 = ALL (single bucket)
+  int32_t nbuckets;
+  int32_t pad;
+  ColView vals[kMaxAggs];   // input column per aggregator
+  ColView key;              // topN: dimension ids
+  uint64_t* out;            // accumulator table of this segment
+};
+
+// groupBy: per-segment open-addressing table
+struct GroupJob {
+  int32_t nrows;
+  int32_t tile_begin;
+  const uint32_t* bitset;
+  ColView time;
+  int64_t t_lo, t_hi;
+  int64_t bucket0;
+  int64_t period;
+  int32_t nbuckets;
+  int32_t ndims;
+  ColView dims[4];
+  int32_t dim_shift[4];     // key = (bucket << bucket_shift) | sum(id_d << dim_shift[d])
+  int32_t bucket_shift;
+  int32_t pad2;
+  ColView vals[kMaxAggs];
+  uint64_t* keys;           // [cap]
+  uint64_t* slots;          // [cap * (naggs + 1)], slot 0 = rows
+  uint64_t mask;            // cap - 1
+  int32_t* overflow;        // set when the table is full
+};
+
+// ---------------------------------------------------------------------------------------------
+// Host-side objects
+// ---------------------------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { reset(); }
+  void reset();
+  bool alloc(size_t bytes);
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// A block-layout column (numeric values or dictionary ids) resident in HBM.
+struct BlockColumn {
+  int32_t total = 0;      // rows
+  int32_t size_per = 0;   // rows per block (power of two)
+  int32_t log2_per = 0;
+  int32_t width = 0;      // bytes per value
+  int32_t codec = 0;
+  int32_t nblocks = 0;
+  int64_t stored_bytes = 0;            // on-HBM bytes of all blocks (algorithmic bytes of a full scan)
+  std::vector<int64_t> comp_off;       // host copy: offset of block b inside comp
+  std::vector<int32_t> comp_len;
+  DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)
+  DevBuf raw;                          // UNCOMPRESSED: 64 KiB slot per block; NONE: flat values
+  DevBuf block_ptrs;                   // const uint8_t*[nblocks]: raw slots (UNCOMPRESSED/NONE)
+};
+
+struct Column {
+  std::string name;
+  int type = DG_COL_MISSING;
+  BlockColumn data;
+  // dictionary-encoded string column
+  std::vector<std::string> dict;
+  std::vector<uint8_t> dict_null;      // 1 = null / empty value
+  int bitmap_roaring = 0;
+  bool has_bitmaps = false;
+  std::vector<int64_t> bm_off;         // byte offset of each bitmap inside bm_bytes (4-byte aligned)
+  std::vector<int32_t> bm_len;
+  DevBuf bm_bytes;
+};
+
+struct Context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::mutex mu;
+  // grow-only scratch arenas reused across calls
+  DevBuf scratch[6];
+  DevBuf pinned_dummy;
+  hipEvent_t ev[8] = {};
+};
+
+struct Segment {
+  Context* ctx = nullptr;
+  std::string dir;
+  int64_t nrows = 0;
+  int64_t istart = 0, iend = 0;
+  int64_t min_time = 0, max_time = 0;
+  int bitmap_roaring = 0;
+  std::vector<std::unique_ptr<Column>> columns;
+  std::map<std::string, Column*> by_name;
+  int64_t device_bytes = 0;
+  Column* find(const std::string& n) const {
+    auto it = by_name.find(n);
+    return it == by_name.end() ? nullptr : it->second;
+  }
+};
+
+// error reporting
+int set_error(int code, const char* fmt, ...);
+#define DG_HIP(call)                                                                       \
+  do {                                                                                     \
+    hipError_t _e = (call);                                                                \
+    if (_e != hipSuccess) return ::dg::set_error(DG_ERR_DEVICE, "%s: %s", #call, hipGetErrorString(_e)); \
+  } while (0)
+
+// segment loading (dg_segment.cpp)
+int load_segment(Context* ctx, const char* dir, Segment** out);
+
+// kernel launchers (dg_kernels.hip)
+void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
+void launch_concise_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
+                       int nbitmaps, uint32_t* const* d_sets, int64_t limit_bits, hipStream_t s);
+void launch_roaring_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
+                       int nbitmaps, uint32_t* const* d_sets, int32_t* d_err, int64_t limit_bits, hipStream_t s);
+void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_sets, uint32_t* out, int64_t nrows,
+                        unsigned long long* d_count, hipStream_t s);
+void launch_fill_u64(uint64_t* p, int64_t n_rows_of_slots, int slots_per_row, const uint64_t* d_init, hipStream_t s);
+void launch_scan_agg(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, int topn, hipStream_t s);
+void launch_topn_select(const uint64_t* table, int64_t card, int naggs, int metric, int metric_op, int inverted,
+                        int threshold, uint64_t* d_state, int32_t* d_cand, int32_t* d_ncand, int cand_cap,
+                        hipStream_t s);
+void launch_groupby(const GroupJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, hipStream_t s);
+void launch_groupby_compact(const uint64_t* keys, const uint64_t* slots, uint64_t cap, int nslots, uint64_t* out_keys,
+                            uint64_t* out_slots, unsigned long long* d_count, hipStream_t s);
+
+constexpr int kTileRows = 2048;
+
+}  // namespace dg

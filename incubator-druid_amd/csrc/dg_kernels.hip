@@ -1,0 +1,832 @@
+// dg_kernels.hip — HIP kernels (gfx950 / CDNA4) of the segment scan-and-aggregate path.
+//
+// Every kernel here replaces a Java hot loop of the reference:
+//   k_lz4_decode      LZ4 block decompression          CompressionStrategy.LZ4Decompressor (data/CompressionStrategy.java:284-305)
+//                                                      -> lz4-java LZ4SafeDecompressor (LZ4 block format)
+//   k_concise_or      Concise word expansion + union   ImmutableConciseSet.union / BitIterator (extendedset/.../BitIterator.java:145-281)
+//   k_roaring_or      Roaring container expansion      ImmutableRoaringBitmap.or (RoaringBitmapFactory.java:145-179)
+//   k_filter_eval     AND/OR/NOT over row bitsets       AndFilter/OrFilter/NotFilter.getBitmapResult (segment/filter/*.java)
+//   k_scan_agg        masked per-bucket aggregation     TimeseriesQueryEngine.java:86-92 (Aggregator.aggregate per cursor row),
+//                     / per-dictionary-id aggregation   PooledTopNAlgorithm.aggregateDimValue (query/topn/PooledTopNAlgorithm.java:661-719)
+//   k_topn_select     K-th largest metric + candidates  TopNNumericResultBuilder priority queue (TopNNumericResultBuilder.java:94-191)
+//   k_groupby         open-addressing hash grouping    BufferHashGrouper/ByteBufferHashTable (epinephelinae/ByteBufferHashTable.java:286-327)
+//
+// Nothing here is a dense contraction, so there is no MFMA: every kernel is HBM/L2-bound integer and
+// byte work, written for 64-wide wavefronts (ballot masks are 64-bit) with coalesced row tiles.
+#include <hip/hip_runtime.h>
+
+#include "dg_internal.h"
+
+namespace dg {
+
+constexpr uint64_t kSign = 0x8000000000000000ull;
+
+// ------------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ord_key(double d) {
+  uint64_t u = __double_as_longlong(d);
+  return (u & kSign) ? ~u : (u | kSign);
+}
+__device__ __forceinline__ double unord_key(uint64_t k) {
+  uint64_t u = (k & kSign) ? (k & ~kSign) : ~k;
+  return __longlong_as_double((long long)u);
+}
+// java (long) double: NaN -> 0, saturating
+__device__ __forceinline__ int64_t java_d2l(double d) {
+  if (d != d) return 0;
+  if (d >= 9223372036854775807.0) return INT64_MAX;
+  if (d <= -9223372036854775808.0) return INT64_MIN;
+  return (int64_t)d;
+}
+
+__device__ __forceinline__ const uint8_t* cv_ptr(const ColView& v, int64_t r) {
+  const uint8_t* base = v.blocks[r >> v.log2_per];
+  return base + (size_t)(r & ((1ll << v.log2_per) - 1)) * (size_t)v.width;
+}
+
+__device__ __forceinline__ uint32_t load_id(const ColView& v, int64_t r) {
+  const uint8_t* p = cv_ptr(v, r);
+  switch (v.width) {
+    case 1: return p[0];
+    case 2: return *reinterpret_cast<const uint16_t*>(p);
+    case 3: return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+    default: return *reinterpret_cast<const uint32_t*>(p);
+  }
+}
+
+// Input of one aggregator for row r, encoded for its slot op.
+// Selector coercions follow LongColumnSelector / DoubleColumnSelector / FloatColumnSelector
+// (segment/DoubleColumnSelector.java:40-55): getLong of a double = (long) d, getFloat = (float) x, ...
+__device__ __forceinline__ uint64_t agg_input(int kind, const ColView& v, int64_t r) {
+  int64_t l = 0;
+  double d = 0.0;
+  float f = 0.0f;
+  if (kind != DG_AGG_COUNT && v.kind != VIEW_ABSENT) {
+    const uint8_t* p = cv_ptr(v, r);
+    if (v.kind == VIEW_LONG) {
+      l = *reinterpret_cast<const int64_t*>(p);
+      d = (double)l;
+      f = (float)l;
+    } else if (v.kind == VIEW_DOUBLE) {
+      d = *reinterpret_cast<const double*>(p);
+      l = java_d2l(d);
+      f = (float)d;
+    } else {
+      f = *reinterpret_cast<const float*>(p);
+      d = (double)f;
+      l = java_d2l(d);
+    }
+  }
+  switch (kind) {
+    case DG_AGG_COUNT: return 1;
+    case DG_AGG_LONG_SUM: return (uint64_t)l;
+    case DG_AGG_DOUBLE_SUM: return (uint64_t)__double_as_longlong(d);
+    case DG_AGG_FLOAT_SUM: return (uint64_t)__double_as_longlong((double)f);
+    case DG_AGG_LONG_MIN:
+    case DG_AGG_LONG_MAX: return (uint64_t)l ^ kSign;
+    case DG_AGG_DOUBLE_MIN: return d != d ? 0ull : ord_key(d);
+    case DG_AGG_DOUBLE_MAX: return d != d ? ~0ull : ord_key(d);
+    case DG_AGG_FLOAT_MIN: return f != f ? 0ull : ord_key((double)f);
+    default: return f != f ? ~0ull : ord_key((double)f);  // FLOAT_MAX
+  }
+}
+
+__device__ __forceinline__ uint64_t combine_op(int op, uint64_t a, uint64_t b) {
+  switch (op) {
+    case OP_ADD_I64: return a + b;
+    case OP_ADD_F64: return (uint64_t)__double_as_longlong(__longlong_as_double((long long)a) + __longlong_as_double((long long)b));
+    case OP_MIN_U64: return a < b ? a : b;
+    default: return a > b ? a : b;
+  }
+}
+
+__device__ __forceinline__ void atomic_op(int op, uint64_t* p, uint64_t v) {
+  switch (op) {
+    case OP_ADD_I64: atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v); break;
+    case OP_ADD_F64: atomicAdd(reinterpret_cast<double*>(p), __longlong_as_double((long long)v)); break;
+    case OP_MIN_U64: atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v); break;
+    default: atomicMax(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v); break;
+  }
+}
+
+__device__ __forceinline__ uint64_t identity_of(int op, int kind) {
+  switch (op) {
+    case OP_ADD_I64: return 0;
+    case OP_ADD_F64: return 0;  // +0.0
+    case OP_MIN_U64:
+      if (kind == DG_AGG_LONG_MIN) return (uint64_t)INT64_MAX ^ kSign;
+      return 0xFFF0000000000000ull;  // ord_key(+inf)
+    default:
+      if (kind == DG_AGG_LONG_MAX) return (uint64_t)INT64_MIN ^ kSign;
+      return 0x000FFFFFFFFFFFFFull;  // ord_key(-inf)
+  }
+}
+
+// block-wide (256 threads = 4 waves) exclusive scan of int64; returns total via *total
+__device__ int64_t block_exclusive_scan(int64_t v, int64_t* total, int64_t* s_tmp) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[wave] = x;
+  __syncthreads();
+  int64_t wave_off = 0, tot = 0;
+  const int nw = blockDim.x >> 6;
+  for (int w = 0; w < nw; ++w) {
+    if (w < wave) wave_off += s_tmp[w];
+    tot += s_tmp[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return wave_off + x - v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// LZ4 block decode: one wave per block, compressed input and decoded output staged in LDS.
+// Tokens are parsed in order (the format is sequential); literal and match copies are spread over
+// the 64 lanes. Overlapping matches (offset < length) use the periodic form
+// out[op + k] = out[op - off + k % off], which only reads bytes before op, so the lanes never race.
+// ------------------------------------------------------------------------------------------------
+constexpr int kLz4InCap = kBlockBytes + 2048;
+
+__global__ __launch_bounds__(64) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap];
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[kBlockBytes + 64];
+  const Lz4Job job = jobs[blockIdx.x];
+  const int lane = threadIdx.x;
+  const int iend = job.src_len;
+  if (iend <= 0 || iend > kLz4InCap) {
+    if (lane == 0) atomicOr(err, 1);
+    return;
+  }
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(job.src);
+    uint4* dst = reinterpret_cast<uint4*>(s_in);
+    const int n16 = (iend + 15) >> 4;
+    for (int i = lane; i < n16; i += 64) dst[i] = src[i];
+  }
+  __syncthreads();
+  int ip = 0, op = 0;
+  bool bad = false;
+  for (;;) {
+    if (ip >= iend) {
+      bad = true;
+      break;
+    }
+    const int tok = __builtin_amdgcn_readfirstlane(s_in[ip]);
+    ip++;
+    int lit = tok >> 4;
+    if (lit == 15) {
+      int b;
+      do {
+        if (ip >= iend) {
+          bad = true;
+          break;
+        }
+        b = __builtin_amdgcn_readfirstlane(s_in[ip]);
+        ip++;
+        lit += b;
+      } while (b == 255);
+      if (bad) break;
+    }
+    if (lit > iend - ip || lit > kBlockBytes - op) {
+      bad = true;
+      break;
+    }
+    for (int k = lane; k < lit; k += 64) s_out[op + k] = s_in[ip + k];
+    ip += lit;
+    op += lit;
+    if (ip == iend) break;  // last sequence: literals only
+    if (iend - ip < 2) {
+      bad = true;
+      break;
+    }
+    const int off = __builtin_amdgcn_readfirstlane((int)s_in[ip] | ((int)s_in[ip + 1] << 8));
+    ip += 2;
+    int ml = tok & 15;
+    if (ml == 15) {
+      int b;
+      do {
+        if (ip >= iend) {
+          bad = true;
+          break;
+        }
+        b = __builtin_amdgcn_readfirstlane(s_in[ip]);
+        ip++;
+        ml += b;
+      } while (b == 255);
+      if (bad) break;
+    }
+    ml += 4;
+    if (off == 0 || off > op || ml > kBlockBytes - op) {
+      bad = true;
+      break;
+    }
+    __syncthreads();
+    if (off >= ml) {
+      for (int k = lane; k < ml; k += 64) s_out[op + k] = s_out[op - off + k];
+    } else {
+      for (int k = lane; k < ml; k += 64) s_out[op + k] = s_out[op - off + (k % off)];
+    }
+    op += ml;
+    __syncthreads();
+  }
+  __syncthreads();
+  if (bad || op < job.expect_len) {
+    if (lane == 0) atomicOr(err, 1);
+    return;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(job.dst);
+  const uint4* src = reinterpret_cast<const uint4*>(s_out);
+  const int n16 = (op + 15) >> 4;
+  for (int i = lane; i < n16; i += 64) dst[i] = src[i];
+}
+
+void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(k_lz4_decode, dim3(njobs), dim3(64), 0, s, d_jobs, d_err);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Concise -> dense row bitset (OR). One workgroup per bitmap; 256 words per step: each thread
+// decodes one big-endian word, a block scan turns word spans (31 or 31*(n+1) rows) into row
+// offsets, then the word's bits are OR-ed into the dense uint32 bitset.
+// Word format: ConciseSetUtils.java:45-75,149-281 (literal = MSB 1 + 31 bits; fill = bit30 fill
+// value, bits25-29 flipped bit+1, bits0-24 blocks-1; flipped bit is in the first block).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void or_bits(uint32_t* set, int64_t bit, uint32_t bits31, int64_t limit) {
+  if (!bits31 || bit < 0 || bit >= limit) return;
+  const int64_t w = bit >> 5;
+  const int sh = (int)(bit & 31);
+  const uint32_t lo = bits31 << sh;
+  if (lo) atomicOr(set + w, lo);
+  if (sh > 1 && ((w + 1) << 5) < limit) {
+    const uint32_t hi = bits31 >> (32 - sh);
+    if (hi) atomicOr(set + w + 1, hi);
+  }
+}
+
+__device__ void or_range(uint32_t* set, int64_t lo, int64_t hi, int64_t skip, int64_t limit) {
+  // set bits [lo, hi) except `skip`; bits at or beyond `limit` (the bitset capacity) are dropped
+  if (hi > limit) hi = limit;
+  if (lo < 0) lo = 0;
+  if (hi <= lo) return;
+  for (int64_t w = lo >> 5; w <= ((hi - 1) >> 5); ++w) {
+    int64_t b0 = w << 5;
+    uint32_t m = 0xFFFFFFFFu;
+    if (lo > b0) m &= 0xFFFFFFFFu << (lo - b0);
+    if (hi < b0 + 32) m &= 0xFFFFFFFFu >> (b0 + 32 - hi);
+    if (skip >= b0 && skip < b0 + 32) m &= ~(1u << (skip - b0));
+    if (m == 0xFFFFFFFFu) set[w] = m;  // idempotent with concurrent ORs
+    else if (m) atomicOr(set + w, m);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_concise_or(const uint8_t* __restrict__ base, const int64_t* __restrict__ off,
+                                                    const int32_t* __restrict__ len, const int32_t* __restrict__ target,
+                                                    uint32_t* const* __restrict__ sets, int64_t limit) {
+  __shared__ int64_t s_tmp[8];
+  const int b = blockIdx.x;
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(base + off[b]);
+  const int nw = len[b] >> 2;
+  uint32_t* set = sets[target[b]];
+  int64_t carry = 0;
+  for (int basew = 0; basew < nw; basew += 256) {
+    const int i = basew + threadIdx.x;
+    uint32_t w = 0;
+    int64_t span = 0;
+    if (i < nw) {
+      w = __builtin_bswap32(words[i]);
+      span = (w & 0x80000000u) ? 31 : 31ll * ((int64_t)(w & 0x01FFFFFFu) + 1);
+    }
+    int64_t total;
+    const int64_t o = carry + block_exclusive_scan(span, &total, s_tmp);
+    if (i < nw) {
+      if (w & 0x80000000u) {
+        or_bits(set, o, w & 0x7FFFFFFFu, limit);
+      } else {
+        const int flip = (int)((w >> 25) & 0x1Fu) - 1;
+        if ((w & 0x40000000u) == 0) {
+          if (flip >= 0) or_bits(set, o + flip, 1u, limit);
+        } else {
+          or_range(set, o, o + span, flip >= 0 ? o + flip : -1, limit);
+        }
+      }
+    }
+    carry += total;
+  }
+}
+
+void launch_concise_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
+                       int nbitmaps, uint32_t* const* d_sets, int64_t limit, hipStream_t s) {
+  if (nbitmaps <= 0) return;
+  hipLaunchKernelGGL(k_concise_or, dim3(nbitmaps), dim3(256), 0, s, bm_base, d_off, d_len, d_target, d_sets, limit);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Roaring (portable format, RoaringFormatSpec) -> dense row bitset (OR). One workgroup per bitmap;
+// thread 0 walks the headers into LDS, then waves take containers round-robin.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMaxContainers = 4096;
+
+__device__ __forceinline__ uint32_t rd16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+__device__ __forceinline__ uint32_t rd32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__global__ __launch_bounds__(256) void k_roaring_or(const uint8_t* __restrict__ base, const int64_t* __restrict__ off,
+                                                    const int32_t* __restrict__ len, const int32_t* __restrict__ target,
+                                                    uint32_t* const* __restrict__ sets, int32_t* __restrict__ err,
+                                                    int64_t limit) {
+  __shared__ int32_t s_key[kMaxContainers];
+  __shared__ int32_t s_card[kMaxContainers];
+  __shared__ int32_t s_off[kMaxContainers];
+  __shared__ uint8_t s_run[kMaxContainers];
+  __shared__ int32_t s_n;
+  const int b = blockIdx.x;
+  const uint8_t* p = base + off[b];
+  const int nbytes = len[b];
+  uint32_t* set = sets[target[b]];
+  if (threadIdx.x == 0) {
+    int n = 0;
+    if (nbytes >= 4) {
+      const uint32_t cookie = rd32(p);
+      int pos = 4;
+      const uint8_t* runbits = nullptr;
+      bool has_off = true;
+      bool ok = true;
+      if ((cookie & 0xFFFFu) == 12347u) {
+        n = (int)(cookie >> 16) + 1;
+        runbits = p + pos;
+        pos += (n + 7) / 8;
+        has_off = n >= 4;
+      } else if (cookie == 12346u) {
+        n = (int)rd32(p + 4);
+        pos = 8;
+      } else {
+        ok = false;
+      }
+      if (!ok || n > kMaxContainers || n < 0) {
+        atomicOr(err, 2);
+        n = 0;
+      } else {
+        const uint8_t* desc = p + pos;
+        pos += 4 * n;
+        const uint8_t* offs = has_off ? p + pos : nullptr;
+        if (has_off) pos += 4 * n;
+        int cur = pos;
+        for (int c = 0; c < n; ++c) {
+          s_key[c] = (int)rd16(desc + 4 * c);
+          s_card[c] = (int)rd16(desc + 4 * c + 2) + 1;
+          s_run[c] = runbits ? ((runbits[c >> 3] >> (c & 7)) & 1) : 0;
+          const int start = offs ? (int)rd32(offs + 4 * c) : cur;
+          s_off[c] = start;
+          int sz;
+          if (s_run[c]) sz = 2 + 4 * (int)rd16(p + start);
+          else if (s_card[c] <= 4096) sz = 2 * s_card[c];
+          else sz = 8192;
+          cur = start + sz;
+        }
+      }
+    }
+    s_n = n;
+  }
+  __syncthreads();
+  const int n = s_n;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = wave; c < n; c += 4) {
+    const int64_t row0 = (int64_t)s_key[c] << 16;
+    const uint8_t* d = p + s_off[c];
+    if (s_run[c]) {
+      const int nruns = (int)rd16(d);
+      for (int r = lane; r < nruns; r += 64) {
+        const int64_t st = row0 + rd16(d + 2 + 4 * r);
+        const int64_t ln = (int64_t)rd16(d + 4 + 4 * r) + 1;
+        or_range(set, st, st + ln, -1, limit);
+      }
+    } else if (s_card[c] <= 4096) {
+      for (int k = lane; k < s_card[c]; k += 64) {
+        const int64_t row = row0 + rd16(d + 2 * k);
+        if (row < limit) atomicOr(set + (row >> 5), 1u << (row & 31));
+      }
+    } else {
+      uint32_t* dst = set + (row0 >> 5);
+      for (int k = lane; k < 2048; k += 64) {
+        const uint32_t w = rd32(d + 4 * k);
+        if (w && row0 + 32ll * k < limit) atomicOr(dst + k, w);
+      }
+    }
+  }
+}
+
+void launch_roaring_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
+                       int nbitmaps, uint32_t* const* d_sets, int32_t* d_err, int64_t limit, hipStream_t s) {
+  if (nbitmaps <= 0) return;
+  hipLaunchKernelGGL(k_roaring_or, dim3(nbitmaps), dim3(256), 0, s, bm_base, d_off, d_len, d_target, d_sets, d_err,
+                     limit);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Filter program over dense bitsets (postfix): >= 0 push set i; -1 all; -2 none; -3 AND; -4 OR; -5 NOT.
+// Rows >= nrows are kept clear (complement is within numRows, NotFilter.java:44-50).
+// ------------------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_filter_eval(const int32_t* __restrict__ prog, int prog_len,
+                                                     uint32_t* const* __restrict__ sets, uint32_t* __restrict__ out,
+                                                     int64_t nrows, unsigned long long* __restrict__ count) {
+  const int64_t nwords = (nrows + 31) >> 5;
+  unsigned long long local = 0;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t st[16];
+    int sp = 0;
+    const uint32_t valid = (w == nwords - 1 && (nrows & 31)) ? ((1u << (nrows & 31)) - 1u) : 0xFFFFFFFFu;
+    for (int i = 0; i < prog_len; ++i) {
+      const int c = prog[i];
+      if (c >= 0) st[sp++] = sets[c][w];
+      else if (c == -1) st[sp++] = valid;
+      else if (c == -2) st[sp++] = 0u;
+      else if (c == -3) { sp--; st[sp - 1] &= st[sp]; }
+      else if (c == -4) { sp--; st[sp - 1] |= st[sp]; }
+      else st[sp - 1] = ~st[sp - 1] & valid;
+    }
+    const uint32_t r = st[0] & valid;
+    out[w] = r;
+    local += __popc(r);
+  }
+  // wave reduce then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, 64);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
+}
+
+void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_sets, uint32_t* out, int64_t nrows,
+                        unsigned long long* d_count, hipStream_t s) {
+  const int64_t nwords = (nrows + 31) >> 5;
+  int grid = (int)((nwords + 255) / 256);
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_filter_eval, dim3(grid), dim3(256), 0, s, d_prog, prog_len, d_sets, out, nrows, d_count);
+}
+
+// ------------------------------------------------------------------------------------------------
+// accumulator init
+// ------------------------------------------------------------------------------------------------
+__global__ void k_fill_u64(uint64_t* __restrict__ p, int64_t rows, int slots, const uint64_t* __restrict__ init) {
+  const int64_t n = rows * slots;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = init[i % slots];
+}
+
+void launch_fill_u64(uint64_t* p, int64_t rows, int slots, const uint64_t* d_init, hipStream_t s) {
+  const int64_t n = rows * slots;
+  if (n <= 0) return;
+  int grid = (int)((n + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(k_fill_u64, dim3(grid), dim3(256), 0, s, p, rows, slots, d_init);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Scan + aggregate. One workgroup per tile of kTileRows rows of one segment; row r of the tile is
+// handled by thread (r % 256) so every column read is coalesced.
+//   TOPN == false: timeseries. Rows are time-sorted, so a tile touches few granularity buckets:
+//     each thread keeps register partials for its current bucket and flushes them into LDS bins
+//     (one bin per bucket touched by the tile), then the bins go to HBM with one atomic per
+//     (bucket, aggregator) per tile.
+//   TOPN == true: aggregate by dictionary id into the segment's dense [card][1 + naggs] table.
+// Slot 0 of every record counts aggregated rows (skipEmptyBuckets / topN "touched" position).
+// ------------------------------------------------------------------------------------------------
+constexpr int kBins = 32;
+
+__device__ __forceinline__ bool row_selected(const ScanJob& j, int64_t r, int64_t* bucket) {
+  if (j.bitset && !((j.bitset[r >> 5] >> (r & 31)) & 1u)) return false;
+  if (j.time.kind != VIEW_ABSENT) {
+    const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, r));
+    if (t < j.t_lo || t >= j.t_hi) return false;
+    *bucket = j.period ? (t - j.bucket0) / j.period : 0;
+  } else {
+    *bucket = 0;
+  }
+  return true;
+}
+
+template <bool TOPN>
+__global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
+                                                  AggPlan plan) {
+  __shared__ uint64_t s_bins[kBins][kMaxAggs + 1];
+  __shared__ int64_t s_b0;
+  const int tile = blockIdx.x;
+  const ScanJob& j = jobs[tile_job[tile]];
+  const int64_t row0 = (int64_t)(tile - j.tile_begin) * kTileRows;
+  const int64_t row_end = min((int64_t)j.nrows, row0 + kTileRows);
+  const int na = plan.n;
+
+  if (TOPN) {
+    for (int64_t r = row0 + threadIdx.x; r < row_end; r += 256) {
+      int64_t b;
+      if (!row_selected(j, r, &b)) continue;
+      const uint32_t id = load_id(j.key, r);
+      uint64_t* rec = j.out + (size_t)id * (na + 1);
+      atomicAdd(reinterpret_cast<unsigned long long*>(rec), 1ull);
+#pragma unroll
+      for (int a = 0; a < kMaxAggs; ++a) {
+        if (a < na) atomic_op(plan.op[a], rec + 1 + a, agg_input(plan.kind[a], j.vals[a], r));
+      }
+    }
+    return;
+  }
+
+  // timeseries
+  if (threadIdx.x == 0) {
+    int64_t b0 = 0;
+    if (j.period && j.time.kind != VIEW_ABSENT) {
+      const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, row0));
+      b0 = t >= j.bucket0 ? (t - j.bucket0) / j.period : 0;
+    }
+    s_b0 = b0;
+  }
+  for (int i = threadIdx.x; i < kBins * (kMaxAggs + 1); i += 256) {
+    const int bin = i / (kMaxAggs + 1), s = i % (kMaxAggs + 1);
+    (void)bin;
+    s_bins[i / (kMaxAggs + 1)][s] = s == 0 ? 0ull : (s - 1 < na ? identity_of(plan.op[s - 1], plan.kind[s - 1]) : 0ull);
+  }
+  __syncthreads();
+  const int64_t b0 = s_b0;
+
+  uint64_t acc[kMaxAggs];
+  uint64_t cnt = 0;
+  int64_t cur = -1;
+  auto flush = [&](int64_t bucket) {
+    if (bucket < 0 || cnt == 0) return;
+    const int64_t lb = bucket - b0;
+    if (lb >= 0 && lb < kBins) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&s_bins[lb][0]), (unsigned long long)cnt);
+#pragma unroll
+      for (int a = 0; a < kMaxAggs; ++a) {
+        if (a < na) atomic_op(plan.op[a], &s_bins[lb][1 + a], acc[a]);
+      }
+    } else {
+      uint64_t* rec = j.out + (size_t)bucket * (na + 1);
+      atomicAdd(reinterpret_cast<unsigned long long*>(rec), (unsigned long long)cnt);
+#pragma unroll
+      for (int a = 0; a < kMaxAggs; ++a) {
+        if (a < na) atomic_op(plan.op[a], rec + 1 + a, acc[a]);
+      }
+    }
+  };
+  for (int64_t r = row0 + threadIdx.x; r < row_end; r += 256) {
+    int64_t b;
+    if (!row_selected(j, r, &b)) continue;
+    if (b != cur) {
+      flush(cur);
+      cur = b;
+      cnt = 0;
+#pragma unroll
+      for (int a = 0; a < kMaxAggs; ++a) acc[a] = a < na ? identity_of(plan.op[a], plan.kind[a]) : 0ull;
+    }
+    cnt++;
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; ++a) {
+      if (a < na) acc[a] = combine_op(plan.op[a], acc[a], agg_input(plan.kind[a], j.vals[a], r));
+    }
+  }
+  flush(cur);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins * (na + 1); i += 256) {
+    const int bin = i / (na + 1), s = i % (na + 1);
+    const int64_t bucket = b0 + bin;
+    if (bucket >= j.nbuckets || s_bins[bin][0] == 0) continue;
+    uint64_t* rec = j.out + (size_t)bucket * (na + 1);
+    if (s == 0) atomicAdd(reinterpret_cast<unsigned long long*>(rec), (unsigned long long)s_bins[bin][0]);
+    else atomic_op(plan.op[s - 1], rec + s, s_bins[bin][s]);
+  }
+}
+
+void launch_scan_agg(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, int topn, hipStream_t s) {
+  if (ntiles <= 0) return;
+  if (topn) hipLaunchKernelGGL(k_scan_agg<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, plan);
+  else hipLaunchKernelGGL(k_scan_agg<false>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, plan);
+}
+
+// ------------------------------------------------------------------------------------------------
+// topN selection for one segment: the K-th largest metric key among touched ids (8-bit radix
+// select over the ordered key), then the ids whose key >= that K-th key, compacted in id order.
+// The host replays TopNNumericResultBuilder's priority queue over those candidates only (ids with a
+// smaller key can never survive it, whatever the insertion order).
+// Metric keys realise the factory comparators: Long.compare, Double.compare / Float.compare
+// (NaN greatest, -0.0 < 0.0); inverted flips them.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t metric_key(uint64_t slot, int op, int kind, int inverted) {
+  uint64_t k;
+  if (op == OP_ADD_I64) {
+    k = slot ^ kSign;
+  } else if (op == OP_ADD_F64) {
+    double d = __longlong_as_double((long long)slot);
+    if (kind == DG_AGG_FLOAT_SUM) d = (double)(float)d;
+    k = d != d ? ~0ull : ord_key(d);
+  } else if (kind == DG_AGG_LONG_MIN || kind == DG_AGG_LONG_MAX) {
+    k = slot;  // biased signed already ordered
+  } else {
+    // min/max key: decode (NaN encodings 0 / ~0) and re-key with NaN greatest
+    bool nan = (op == OP_MIN_U64) ? slot == 0 : slot == ~0ull;
+    if (nan) k = ~0ull;
+    else {
+      double d = unord_key(slot);
+      if (kind == DG_AGG_FLOAT_MIN || kind == DG_AGG_FLOAT_MAX) d = (double)(float)d;
+      k = ord_key(d);
+    }
+  }
+  return inverted ? ~k : k;
+}
+
+__global__ __launch_bounds__(1024) void k_topn_select(const uint64_t* __restrict__ table, int64_t card, int naggs,
+                                                      int metric, int op, int kind, int inverted, int threshold,
+                                                      uint64_t* __restrict__ state, int32_t* __restrict__ cand,
+                                                      int32_t* __restrict__ ncand, int cand_cap) {
+  __shared__ unsigned int s_hist[256];
+  __shared__ uint64_t s_prefix, s_mask;
+  __shared__ int64_t s_krem, s_touched;
+  __shared__ int64_t s_tmp[16];
+  const int rec = naggs + 1;
+  if (threadIdx.x == 0) {
+    s_prefix = 0;
+    s_mask = 0;
+    s_krem = threshold;
+    s_touched = 0;
+  }
+  __syncthreads();
+  // count touched
+  {
+    unsigned long long c = 0;
+    for (int64_t i = threadIdx.x; i < card; i += blockDim.x) c += table[i * rec] != 0;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&s_touched), c);
+  }
+  __syncthreads();
+  uint64_t kth = 0;  // keep everything when touched <= threshold
+  if (s_touched > threshold) {
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      for (int i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0;
+      __syncthreads();
+      const uint64_t prefix = s_prefix, mask = s_mask;
+      for (int64_t i = threadIdx.x; i < card; i += blockDim.x) {
+        if (table[i * rec] == 0) continue;
+        const uint64_t k = metric_key(table[i * rec + 1 + metric], op, kind, inverted);
+        if ((k & mask) == prefix) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int64_t cum = 0, krem = s_krem;
+        for (int dgt = 255; dgt >= 0; --dgt) {
+          const int64_t h = s_hist[dgt];
+          if (cum + h >= krem) {
+            s_prefix = prefix | ((uint64_t)dgt << shift);
+            s_mask = mask | (255ull << shift);
+            s_krem = krem - cum;
+            break;
+          }
+          cum += h;
+        }
+      }
+      __syncthreads();
+    }
+    kth = s_prefix;
+  }
+  // ordered compaction of touched ids with key >= kth
+  int64_t base = 0;
+  for (int64_t start = 0; start < card; start += blockDim.x) {
+    const int64_t i = start + threadIdx.x;
+    int f = 0;
+    if (i < card && table[i * rec] != 0) f = metric_key(table[i * rec + 1 + metric], op, kind, inverted) >= kth;
+    // block scan over 1024 threads (16 waves)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(f);
+    const int below = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_tmp[wave] = __popcll(m);
+    __syncthreads();
+    int64_t woff = 0, tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+      if (w < wave) woff += s_tmp[w];
+      tot += s_tmp[w];
+    }
+    if (f) {
+      const int64_t pos = base + woff + below;
+      if (pos < cand_cap) cand[pos] = (int32_t)i;
+    }
+    base += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *ncand = (int32_t)(base < 0x7fffffff ? base : 0x7fffffff);
+    state[0] = kth;
+  }
+}
+
+void launch_topn_select(const uint64_t* table, int64_t card, int naggs, int metric, int metric_op, int inverted,
+                        int threshold, uint64_t* d_state, int32_t* d_cand, int32_t* d_ncand, int cand_cap,
+                        hipStream_t s) {
+  (void)metric_op;
+  // metric_op encodes (op << 8) | kind
+  hipLaunchKernelGGL(k_topn_select, dim3(1), dim3(1024), 0, s, table, card, naggs, metric, metric_op >> 8,
+                     metric_op & 255, inverted, threshold, d_state, d_cand, d_ncand, cand_cap);
+}
+
+// ------------------------------------------------------------------------------------------------
+// groupBy: open addressing (linear probing) on a 64-bit packed key (bucket, dictionary ids),
+// CAS-claimed slots, per-aggregator atomics on the slot (ByteBufferHashTable.findBucket semantics
+// without the byte-wise key compare: the key is one word).
+// ------------------------------------------------------------------------------------------------
+constexpr uint64_t kEmpty = ~0ull;
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+__global__ __launch_bounds__(256) void k_groupby(const GroupJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
+                                                 AggPlan plan) {
+  const int tile = blockIdx.x;
+  const GroupJob& j = jobs[tile_job[tile]];
+  const int64_t row0 = (int64_t)(tile - j.tile_begin) * kTileRows;
+  const int64_t row_end = min((int64_t)j.nrows, row0 + kTileRows);
+  const int na = plan.n;
+  for (int64_t r = row0 + threadIdx.x; r < row_end; r += 256) {
+    if (j.bitset && !((j.bitset[r >> 5] >> (r & 31)) & 1u)) continue;
+    int64_t bucket = 0;
+    if (j.time.kind != VIEW_ABSENT) {
+      const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, r));
+      if (t < j.t_lo || t >= j.t_hi) continue;
+      bucket = j.period ? (t - j.bucket0) / j.period : 0;
+    }
+    uint64_t key = (uint64_t)bucket << j.bucket_shift;
+    for (int d = 0; d < j.ndims; ++d) {
+      const uint64_t id = j.dims[d].kind == VIEW_IDS ? load_id(j.dims[d], r) : 0u;
+      key |= id << j.dim_shift[d];
+    }
+    uint64_t h = fmix64(key) & j.mask;
+    bool placed = false;
+    for (uint64_t probe = 0; probe <= j.mask; ++probe) {
+      const unsigned long long prev =
+          atomicCAS(reinterpret_cast<unsigned long long*>(j.keys + h), (unsigned long long)kEmpty, (unsigned long long)key);
+      if (prev == kEmpty || prev == key) {
+        placed = true;
+        break;
+      }
+      h = (h + 1) & j.mask;
+    }
+    if (!placed) {
+      atomicOr(j.overflow, 1);
+      continue;
+    }
+    uint64_t* rec = j.slots + h * (uint64_t)(na + 1);
+    atomicAdd(reinterpret_cast<unsigned long long*>(rec), 1ull);
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; ++a) {
+      if (a < na) atomic_op(plan.op[a], rec + 1 + a, agg_input(plan.kind[a], j.vals[a], r));
+    }
+  }
+}
+
+void launch_groupby(const GroupJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, hipStream_t s) {
+  if (ntiles <= 0) return;
+  hipLaunchKernelGGL(k_groupby, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, plan);
+}
+
+__global__ __launch_bounds__(256) void k_groupby_compact(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ slots,
+                                                         uint64_t cap, int nslots, uint64_t* __restrict__ out_keys,
+                                                         uint64_t* __restrict__ out_slots,
+                                                         unsigned long long* __restrict__ count) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    const bool f = k != kEmpty;
+    const unsigned long long m = __ballot(f);
+    if (!m) continue;
+    const int lane = threadIdx.x & 63;
+    unsigned long long base = 0;
+    const int leader = __ffsll((long long)m) - 1;
+    if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (f) {
+      const unsigned long long pos = base + __popcll(m & ((1ull << lane) - 1ull));
+      out_keys[pos] = k;
+      for (int s = 0; s < nslots; ++s) out_slots[pos * nslots + s] = slots[i * nslots + s];
+    }
+  }
+}
+
+void launch_groupby_compact(const uint64_t* keys, const uint64_t* slots, uint64_t cap, int nslots, uint64_t* out_keys,
+                            uint64_t* out_slots, unsigned long long* d_count, hipStream_t s) {
+  uint64_t g = (cap + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(k_groupby_compact, dim3((unsigned)g), dim3(256), 0, s, keys, slots, cap, nslots, out_keys, out_slots,
+                     d_count);
+}
+
+}  // namespace dg

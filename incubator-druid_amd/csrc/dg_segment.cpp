@@ -1,0 +1,417 @@
+// dg_segment.cpp — v9 segment loader: parses the on-disk format on the host and builds the
+// device-resident columnar image in HBM.
+//
+// Format followed (reference paths, processing/... = processing/src/main/java/org/apache/druid/...):
+//   version.bin / meta.smoosh / NNNNN.smoosh   IndexIO.V9IndexLoader.load (segment/IndexIO.java:569-663),
+//                                              SmooshedFileMapper (java-util/.../io/smoosh/SmooshedFileMapper.java)
+//   index.drd                                  cols, dims (GenericIndexed<String>), interval, bitmap serde JSON
+//   column = int32 BE json length + ColumnDescriptor JSON + part (IndexIO.java:665-672)
+//   GenericIndexed v1                          data/GenericIndexed.java:52-77, 479-492
+//   long/float/double part                     data/CompressedColumnar{Longs,Floats}Supplier.fromByteBuffer,
+//                                              CompressedColumnarDoublesSuppliers (+ CompressionFactory flag logic
+//                                              data/CompressionFactory.java:64-116); V2 serdes skip their int offset +
+//                                              null bitmap (serde/DoubleGenericColumnPartSerdeV2.java:140-162)
+//   stringDictionary part                      serde/DictionaryEncodedColumnPartSerde.java:283-345,
+//                                              data/CompressedVSizeColumnarIntsSupplier.java:143-168
+//
+// Device image (all HBM, built once at attach; queries never touch the files again):
+//   LZ4 blocks        packed, each block 16-byte aligned, + host offset/length tables
+//   UNCOMPRESSED      one 64 KiB-aligned slot per block (so every value is naturally aligned)
+//   NONE              the flat value array
+//   bitmaps           every dictionary value's serialized Concise/Roaring bytes, 4-byte aligned
+//   dictionaries      host-side (filters resolve on the host like BitmapIndexSelector does)
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "dg_internal.h"
+
+namespace dg {
+
+namespace {
+
+int32_t be32(const uint8_t* p) {
+  return (int32_t)(((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]);
+}
+int64_t be64(const uint8_t* p) { return ((int64_t)(uint32_t)be32(p) << 32) | (uint32_t)be32(p + 4); }
+
+struct MappedFile {
+  void* base = nullptr;
+  size_t size = 0;
+  ~MappedFile() {
+    if (base && base != MAP_FAILED) munmap(base, size);
+  }
+  bool open(const std::string& path) {
+    int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+      ::close(fd);
+      return false;
+    }
+    size = (size_t)st.st_size;
+    if (size == 0) {
+      ::close(fd);
+      base = nullptr;
+      return true;
+    }
+    base = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    return base != MAP_FAILED;
+  }
+  const uint8_t* data() const { return static_cast<const uint8_t*>(base); }
+};
+
+struct Slice {
+  const uint8_t* p = nullptr;
+  const uint8_t* end = nullptr;
+  int64_t left() const { return end - p; }
+};
+
+// GenericIndexed v1 view
+struct GI {
+  int32_t n = 0;
+  const uint8_t* header = nullptr;
+  const uint8_t* values = nullptr;
+  int32_t get(int32_t i, const uint8_t** ptr) const {
+    int32_t start = i == 0 ? 4 : be32(header + 4 * (i - 1)) + 4;
+    int32_t end = be32(header + 4 * i);
+    *ptr = values + start;
+    return end - start;
+  }
+};
+
+bool gi_read(Slice& s, GI* g) {
+  if (s.left() < 6) return false;
+  if (s.p[0] != 0x01) return false;  // version 2 (multi-file, > 2 GiB columns) not supported
+  int32_t used = be32(s.p + 2);
+  const uint8_t* body = s.p + 6;
+  if (used < 4 || s.end - body < used) return false;
+  g->n = be32(body);
+  if (g->n < 0 || 4 + 4 * (int64_t)g->n > used) return false;
+  g->header = body + 4;
+  g->values = body + 4 + 4 * (int64_t)g->n;
+  s.p = body + used;
+  return true;
+}
+
+// tiny JSON probe: value of "key" at/after `from`
+std::string json_get(const std::string& js, const char* key, size_t from = 0) {
+  std::string pat = std::string("\"") + key + "\":";
+  size_t k = js.find(pat, from);
+  if (k == std::string::npos) return "";
+  k += pat.size();
+  while (k < js.size() && js[k] == ' ') k++;
+  if (k < js.size() && js[k] == '"') {
+    size_t e = js.find('"', k + 1);
+    return js.substr(k + 1, e - k - 1);
+  }
+  size_t e = k;
+  while (e < js.size() && js[e] != ',' && js[e] != '}') e++;
+  return js.substr(k, e - k);
+}
+
+int log2i(int32_t v) {
+  int l = 0;
+  while ((1 << l) < v) l++;
+  return (1 << l) == v ? l : -1;
+}
+
+// Upload the blocks of a GenericIndexed of (compressed or raw) blocks.
+int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
+  col->nblocks = blocks.n;
+  if (col->codec == CODEC_LZ4) {
+    col->comp_off.resize(blocks.n);
+    col->comp_len.resize(blocks.n);
+    int64_t total = 0;
+    for (int32_t b = 0; b < blocks.n; ++b) {
+      const uint8_t* p;
+      int32_t len = blocks.get(b, &p);
+      if (len <= 0) return set_error(DG_ERR_FORMAT, "empty LZ4 block %d", b);
+      col->comp_off[b] = total;
+      col->comp_len[b] = len;
+      total += (len + 15) & ~15;
+    }
+    std::vector<uint8_t> host((size_t)total + 16, 0);
+    for (int32_t b = 0; b < blocks.n; ++b) {
+      const uint8_t* p;
+      int32_t len = blocks.get(b, &p);
+      memcpy(host.data() + col->comp_off[b], p, (size_t)len);
+      col->stored_bytes += len;
+    }
+    if (!col->comp.alloc(host.size())) return set_error(DG_ERR_OOM, "hipMalloc %zu", host.size());
+    DG_HIP(hipMemcpy(col->comp.p, host.data(), host.size(), hipMemcpyHostToDevice));
+    return DG_OK;
+  }
+  if (col->codec == CODEC_UNCOMPRESSED) {
+    size_t bytes = (size_t)blocks.n * kBlockBytes;
+    std::vector<uint8_t> host(bytes > 0 ? bytes : 16, 0);
+    for (int32_t b = 0; b < blocks.n; ++b) {
+      const uint8_t* p;
+      int32_t len = blocks.get(b, &p);
+      if (len > kBlockBytes) return set_error(DG_ERR_FORMAT, "uncompressed block of %d bytes", len);
+      memcpy(host.data() + (size_t)b * kBlockBytes, p, (size_t)len);
+      col->stored_bytes += len;
+    }
+    if (!col->raw.alloc(host.size())) return set_error(DG_ERR_OOM, "hipMalloc %zu", host.size());
+    DG_HIP(hipMemcpy(col->raw.p, host.data(), host.size(), hipMemcpyHostToDevice));
+    std::vector<const uint8_t*> ptrs(blocks.n > 0 ? blocks.n : 1);
+    for (int32_t b = 0; b < blocks.n; ++b) ptrs[b] = col->raw.as<uint8_t>() + (size_t)b * kBlockBytes;
+    if (!col->block_ptrs.alloc(ptrs.size() * sizeof(void*))) return set_error(DG_ERR_OOM, "hipMalloc ptrs");
+    DG_HIP(hipMemcpy(col->block_ptrs.p, ptrs.data(), ptrs.size() * sizeof(void*), hipMemcpyHostToDevice));
+    return DG_OK;
+  }
+  return set_error(DG_ERR_UNSUPPORTED, "compression id 0x%02x", col->codec);
+}
+
+// NONE layout: flat values directly after the header (EntireLayoutColumnar*Supplier)
+int upload_flat(BlockColumn* col, const uint8_t* p, const uint8_t* end) {
+  size_t bytes = (size_t)col->total * col->width;
+  if ((int64_t)bytes > end - p) return set_error(DG_ERR_FORMAT, "truncated NONE column");
+  if (!col->raw.alloc(bytes + 16)) return set_error(DG_ERR_OOM, "hipMalloc %zu", bytes);
+  DG_HIP(hipMemcpy(col->raw.p, p, bytes, hipMemcpyHostToDevice));
+  col->stored_bytes = (int64_t)bytes;
+  // virtual 64 KiB blocks so kernels address every layout the same way
+  col->size_per = kBlockBytes / col->width;
+  col->log2_per = log2i(col->size_per);
+  col->nblocks = (int32_t)((col->total + col->size_per - 1) / col->size_per);
+  std::vector<const uint8_t*> ptrs(col->nblocks > 0 ? col->nblocks : 1);
+  for (int32_t b = 0; b < col->nblocks; ++b) ptrs[b] = col->raw.as<uint8_t>() + (size_t)b * kBlockBytes;
+  if (!col->block_ptrs.alloc(ptrs.size() * sizeof(void*))) return set_error(DG_ERR_OOM, "hipMalloc ptrs");
+  DG_HIP(hipMemcpy(col->block_ptrs.p, ptrs.data(), ptrs.size() * sizeof(void*), hipMemcpyHostToDevice));
+  return DG_OK;
+}
+
+int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
+  // [u8 version][i32 total][i32 sizePer][u8 compression (maybe flagged)][encoding?][blocks | values]
+  if (s.left() < 10) return set_error(DG_ERR_FORMAT, "%s: truncated numeric column", c->name.c_str());
+  uint8_t version = s.p[0];
+  if (version != 0x02) return set_error(DG_ERR_UNSUPPORTED, "%s: numeric column version %d (LZF)", c->name.c_str(), version);
+  BlockColumn& col = c->data;
+  col.total = be32(s.p + 1);
+  col.size_per = be32(s.p + 5);
+  int8_t cid = (int8_t)s.p[9];
+  s.p += 10;
+  if (cid < (int8_t)0xFE) {  // CompressionFactory.hasEncodingFlag
+    uint8_t enc = *s.p++;
+    cid = (int8_t)(cid + 126);
+    if (enc != 0xFF)
+      return set_error(DG_ERR_UNSUPPORTED, "%s: long encoding %d (DELTA/TABLE) not implemented", c->name.c_str(), enc);
+  }
+  col.codec = (uint8_t)cid;
+  col.width = width;
+  if (col.codec == CODEC_NONE) return upload_flat(&col, s.p, s.end);
+  col.log2_per = log2i(col.size_per);
+  if (col.log2_per < 0 || (int64_t)col.size_per * width > kBlockBytes)
+    return set_error(DG_ERR_FORMAT, "%s: bad block size %d", c->name.c_str(), col.size_per);
+  GI blocks;
+  if (!gi_read(s, &blocks)) return set_error(DG_ERR_FORMAT, "%s: bad block index", c->name.c_str());
+  if ((int64_t)blocks.n * col.size_per < col.total) return set_error(DG_ERR_FORMAT, "%s: too few blocks", c->name.c_str());
+  return upload_blocks(ctx, &col, blocks);
+}
+
+int parse_string(Context* ctx, Column* c, Slice s) {
+  if (s.left() < 1) return set_error(DG_ERR_FORMAT, "%s: empty", c->name.c_str());
+  int version = s.p[0];
+  s.p++;
+  int flags = 0;
+  if (version >= 2) {
+    flags = be32(s.p);
+    s.p += 4;
+  } else if (version == 1) {
+    flags = 1;
+  }
+  if (flags & 3) return set_error(DG_ERR_UNSUPPORTED, "%s: multi-value dimension", c->name.c_str());
+  GI dict;
+  if (!gi_read(s, &dict)) return set_error(DG_ERR_FORMAT, "%s: bad dictionary", c->name.c_str());
+  c->dict.resize(dict.n);
+  c->dict_null.resize(dict.n);
+  for (int32_t i = 0; i < dict.n; ++i) {
+    const uint8_t* p;
+    int32_t len = dict.get(i, &p);
+    c->dict[i].assign((const char*)p, len > 0 ? len : 0);
+    c->dict_null[i] = len <= 0;  // size 0 => null (replaceWithDefault), GenericIndexed.java:369-372
+  }
+  if (version != 2) return set_error(DG_ERR_UNSUPPORTED, "%s: uncompressed VSize ids", c->name.c_str());
+  if (s.left() < 11 || s.p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: bad id stream", c->name.c_str());
+  BlockColumn& col = c->data;
+  col.width = s.p[1];
+  col.total = be32(s.p + 2);
+  col.size_per = be32(s.p + 6);
+  col.codec = s.p[10];
+  s.p += 11;
+  col.log2_per = log2i(col.size_per);
+  if (col.width < 1 || col.width > 4 || col.log2_per < 0)
+    return set_error(DG_ERR_FORMAT, "%s: bad id stream header", c->name.c_str());
+  GI blocks;
+  if (!gi_read(s, &blocks)) return set_error(DG_ERR_FORMAT, "%s: bad id blocks", c->name.c_str());
+  int rc = upload_blocks(ctx, &col, blocks);
+  if (rc) return rc;
+  if (!(flags & 4)) {
+    GI bms;
+    if (!gi_read(s, &bms)) return set_error(DG_ERR_FORMAT, "%s: bad bitmap index", c->name.c_str());
+    if (bms.n != dict.n) return set_error(DG_ERR_FORMAT, "%s: %d bitmaps for %d values", c->name.c_str(), bms.n, dict.n);
+    c->has_bitmaps = true;
+    c->bm_off.resize(bms.n);
+    c->bm_len.resize(bms.n);
+    int64_t total = 0;
+    for (int32_t i = 0; i < bms.n; ++i) {
+      const uint8_t* p;
+      int32_t len = bms.get(i, &p);
+      c->bm_off[i] = total;
+      c->bm_len[i] = len > 0 ? len : 0;
+      total += (c->bm_len[i] + 3) & ~3;
+    }
+    std::vector<uint8_t> host((size_t)total + 16, 0);
+    for (int32_t i = 0; i < bms.n; ++i) {
+      const uint8_t* p;
+      bms.get(i, &p);
+      if (c->bm_len[i]) memcpy(host.data() + c->bm_off[i], p, (size_t)c->bm_len[i]);
+    }
+    if (!c->bm_bytes.alloc(host.size())) return set_error(DG_ERR_OOM, "hipMalloc bitmaps");
+    DG_HIP(hipMemcpy(c->bm_bytes.p, host.data(), host.size(), hipMemcpyHostToDevice));
+  }
+  return DG_OK;
+}
+
+int64_t column_device_bytes(const Column& c) {
+  return (int64_t)(c.data.comp.n + c.data.raw.n + c.data.block_ptrs.n + c.bm_bytes.n);
+}
+
+}  // namespace
+
+int read_time_bounds(Segment* seg);  // dg_engine.cpp
+
+int load_segment(Context* ctx, const char* dir, Segment** out) {
+  std::unique_ptr<Segment> seg(new Segment());
+  seg->ctx = ctx;
+  seg->dir = dir;
+  std::string d(dir);
+  {
+    MappedFile vf;
+    if (!vf.open(d + "/version.bin") || vf.size != 4) return set_error(DG_ERR_FORMAT, "%s: missing version.bin", dir);
+    if (be32(vf.data()) != 9) return set_error(DG_ERR_FORMAT, "Expected version[9], got[%d]", be32(vf.data()));
+  }
+  MappedFile meta;
+  if (!meta.open(d + "/meta.smoosh")) return set_error(DG_ERR_FORMAT, "%s: missing meta.smoosh", dir);
+  std::string text((const char*)meta.data(), meta.size);
+  size_t pos = text.find('\n');
+  int nchunks = 0;
+  if (sscanf(text.c_str(), "v1,%*d,%d", &nchunks) != 1 || nchunks < 0) return set_error(DG_ERR_FORMAT, "bad meta.smoosh");
+  std::vector<std::unique_ptr<MappedFile>> chunks(nchunks);
+  for (int i = 0; i < nchunks; ++i) {
+    char name[32];
+    snprintf(name, sizeof name, "/%05d.smoosh", i);
+    chunks[i].reset(new MappedFile());
+    if (!chunks[i]->open(d + name)) return set_error(DG_ERR_FORMAT, "%s: missing chunk %s", dir, name);
+  }
+  struct Entry {
+    std::string name;
+    Slice s;
+  };
+  std::vector<Entry> entries;
+  Slice index_drd;
+  while (pos != std::string::npos && pos + 1 < text.size()) {
+    size_t nl = text.find('\n', pos + 1);
+    std::string line = text.substr(pos + 1, nl == std::string::npos ? std::string::npos : nl - pos - 1);
+    pos = nl;
+    if (line.empty()) continue;
+    size_t c3 = line.rfind(','), c2 = c3 == std::string::npos ? c3 : line.rfind(',', c3 - 1),
+           c1 = c2 == std::string::npos ? c2 : line.rfind(',', c2 - 1);
+    if (c1 == std::string::npos) continue;
+    std::string nm = line.substr(0, c1);
+    int chunk = atoi(line.c_str() + c1 + 1);
+    long st = atol(line.c_str() + c2 + 1), en = atol(line.c_str() + c3 + 1);
+    if (chunk < 0 || chunk >= nchunks || en < st || (size_t)en > chunks[chunk]->size)
+      return set_error(DG_ERR_FORMAT, "bad smoosh entry %s", nm.c_str());
+    Slice s{chunks[chunk]->data() + st, chunks[chunk]->data() + en};
+    if (nm == "index.drd") index_drd = s;
+    else if (nm != "metadata.drd") entries.push_back({nm, s});
+  }
+  if (!index_drd.p) return set_error(DG_ERR_FORMAT, "%s: missing index.drd", dir);
+  {
+    Slice s = index_drd;
+    GI cols, dims;
+    if (!gi_read(s, &cols) || !gi_read(s, &dims) || s.left() < 16) return set_error(DG_ERR_FORMAT, "bad index.drd");
+    seg->istart = be64(s.p);
+    seg->iend = be64(s.p + 8);
+    s.p += 16;
+    if (s.left() >= 4) {
+      int32_t l = be32(s.p);
+      if (l > 0 && l <= s.left() - 4) {
+        std::string js((const char*)s.p + 4, l);
+        seg->bitmap_roaring = js.find("roaring") != std::string::npos;
+      }
+    }
+  }
+  for (auto& e : entries) {
+    std::unique_ptr<Column> c(new Column());
+    c->name = e.name;
+    if (e.s.left() < 4) return set_error(DG_ERR_FORMAT, "%s: truncated", e.name.c_str());
+    int32_t jlen = be32(e.s.p);
+    if (jlen < 0 || jlen > e.s.left() - 4) return set_error(DG_ERR_FORMAT, "%s: bad descriptor", e.name.c_str());
+    std::string js((const char*)e.s.p + 4, jlen);
+    Slice part{e.s.p + 4 + jlen, e.s.end};
+    size_t parts = js.find("\"parts\"");
+    std::string ptype = json_get(js, "type", parts == std::string::npos ? 0 : parts);
+    std::string order = json_get(js, "byteOrder");
+    int rc = DG_OK;
+    bool v2 = ptype.size() > 2 && ptype.compare(ptype.size() - 2, 2, "V2") == 0;
+    if (v2) {
+      if (part.left() < 4) return set_error(DG_ERR_FORMAT, "%s: truncated V2", e.name.c_str());
+      part.p += 4;  // int offset to the null bitmap (nulls read as 0 in default null mode)
+      ptype = ptype.substr(0, ptype.size() - 2);
+    }
+    if (order == "BIG_ENDIAN") {
+      c->type = DG_COL_UNSUPPORTED;
+    } else if (ptype == "long") {
+      c->type = DG_COL_LONG;
+      rc = parse_numeric(ctx, c.get(), part, 8);
+    } else if (ptype == "double") {
+      c->type = DG_COL_DOUBLE;
+      rc = parse_numeric(ctx, c.get(), part, 8);
+    } else if (ptype == "float") {
+      c->type = DG_COL_FLOAT;
+      rc = parse_numeric(ctx, c.get(), part, 4);
+    } else if (ptype == "stringDictionary") {
+      c->type = DG_COL_STRING;
+      size_t bsf = js.find("\"bitmapSerdeFactory\"");
+      c->bitmap_roaring = bsf != std::string::npos && json_get(js, "type", bsf) == "roaring";
+      rc = parse_string(ctx, c.get(), part);
+    } else {
+      c->type = DG_COL_UNSUPPORTED;
+    }
+    if (rc == DG_ERR_UNSUPPORTED) {
+      c->type = DG_COL_UNSUPPORTED;  // a query touching it gets DG_ERR_UNSUPPORTED
+      c->data.comp.reset();
+      c->data.raw.reset();
+      c->data.block_ptrs.reset();
+      c->bm_bytes.reset();
+    } else if (rc) {
+      return rc;
+    }
+    seg->device_bytes += column_device_bytes(*c);
+    seg->by_name[c->name] = c.get();
+    seg->columns.push_back(std::move(c));
+  }
+  Column* t = seg->find("__time");
+  if (!t || t->type != DG_COL_LONG) return set_error(DG_ERR_FORMAT, "%s: missing __time", dir);
+  seg->nrows = t->data.total;
+  for (auto& c : seg->columns) {
+    if ((c->type == DG_COL_LONG || c->type == DG_COL_FLOAT || c->type == DG_COL_DOUBLE || c->type == DG_COL_STRING) &&
+        c->data.total != seg->nrows)
+      return set_error(DG_ERR_FORMAT, "%s: %d rows, segment has %lld", c->name.c_str(), c->data.total,
+                       (long long)seg->nrows);
+  }
+  int rc = read_time_bounds(seg.get());
+  if (rc) return rc;
+  *out = seg.release();
+  return DG_OK;
+}
+
+}  // namespace dg

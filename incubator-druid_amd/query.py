@@ -1,0 +1,619 @@
+"""Native query model: the JSON query specs of Druid's timeseries / topN / groupBy (v2) path.
+
+Mirrors the reference's query objects closely enough that a Druid native query JSON can be
+fed in unchanged (``Query.from_json``):
+
+* granularities: java-util/.../granularity/{Granularity,AllGranularity,PeriodGranularity}.java
+  (bucketStart / increment / getIterable, PeriodGranularity.java:222-230,411-428)
+* filters: query/filter/{SelectorDimFilter,InDimFilter,BoundDimFilter,AndDimFilter,OrDimFilter,
+  NotDimFilter}.java (``toFilter`` / ``optimize``, e.g. InDimFilter.java:132-139)
+* aggregators: query/aggregation/{Count,LongSum,DoubleSum,FloatSum,LongMin,LongMax,DoubleMin,
+  DoubleMax,FloatMin,FloatMax}AggregatorFactory.java (combine / comparator / initial values)
+* queries: query/timeseries/TimeseriesQuery.java, query/topn/TopNQuery.java,
+  query/groupby/GroupByQuery.java; topN metric specs NumericTopNMetricSpec / InvertedTopNMetricSpec
+  / DimensionTopNMetricSpec.
+
+Only the null-handling mode the reference defaults to is modelled
+(``druid.generic.useDefaultValueForNull=true``, common/config/NullHandling.java:34,54):
+null string == "" and numeric nulls read as 0.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import math
+import re
+import struct
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+# ----------------------------------------------------------------------------------------------
+# time helpers
+# ----------------------------------------------------------------------------------------------
+MIN_INSTANT = -(2 ** 62)   # JodaUtils.MIN_INSTANT (Long.MIN_VALUE / 2)
+MAX_INSTANT = 2 ** 62 - 1  # JodaUtils.MAX_INSTANT
+_EPOCH = _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc)
+
+
+def parse_time(s) -> int:
+    """ISO-8601 instant (or epoch millis) -> epoch millis (UTC)."""
+    if isinstance(s, (int,)):
+        return int(s)
+    s = str(s).strip()
+    if re.fullmatch(r"-?\d+", s) and len(s) > 8:
+        return int(s)
+    m = re.fullmatch(r"(\d{4})(?:-(\d{2})(?:-(\d{2}))?)?(?:T(\d{2})(?::(\d{2})(?::(\d{2})(?:\.(\d{1,3}))?)?)?)?(Z|[+-]\d{2}:?\d{2})?", s)
+    if not m:
+        raise ValueError(f"unparseable time {s!r}")
+    y, mo, d, h, mi, se, ms, tz = m.groups()
+    t = _dt.datetime(int(y), int(mo or 1), int(d or 1), int(h or 0), int(mi or 0), int(se or 0),
+                     tzinfo=_dt.timezone.utc)
+    millis = int((t - _EPOCH) // _dt.timedelta(milliseconds=1)) + int((ms or "0").ljust(3, "0"))
+    if tz and tz != "Z":
+        sign = 1 if tz[0] == "+" else -1
+        hh, mm = int(tz[1:3]), int(tz[-2:])
+        millis -= sign * (hh * 3600 + mm * 60) * 1000
+    return millis
+
+
+def format_time(ms: int) -> str:
+    t = _EPOCH + _dt.timedelta(milliseconds=int(ms))
+    return t.strftime("%Y-%m-%dT%H:%M:%S.") + f"{int(ms) % 1000:03d}Z"
+
+
+def parse_interval(s) -> Tuple[int, int]:
+    if isinstance(s, (tuple, list)):
+        return int(s[0]), int(s[1])
+    a, b = str(s).split("/")
+    return parse_time(a), parse_time(b)
+
+
+# ----------------------------------------------------------------------------------------------
+# granularity
+# ----------------------------------------------------------------------------------------------
+_PERIOD_MS = {
+    "none": 1, "second": 1000, "minute": 60_000, "five_minute": 300_000, "ten_minute": 600_000,
+    "fifteen_minute": 900_000, "thirty_minute": 1_800_000, "hour": 3_600_000, "six_hour": 21_600_000,
+    "day": 86_400_000, "week": 604_800_000,
+}
+_ISO_PERIOD = re.compile(r"P(?:(\d+)W)?(?:(\d+)D)?(?:T(?:(\d+)H)?(?:(\d+)M)?(?:(\d+)S)?)?")
+
+
+@dataclass(frozen=True)
+class Granularity:
+    """ALL (period_ms == 0) or a fixed-length UTC period with an origin.
+
+    bucketStart(t) = t - floorMod(t - origin, period) (PeriodGranularity.truncateMillisPeriod,
+    PeriodGranularity.java:411-428, UTC so fixed-length days/hours/weeks); Joda weeks start on
+    Monday, so WEEK carries origin 1969-12-29 (Monday) = -3 days.
+    """
+    period_ms: int = 0
+    origin_ms: int = 0
+    name: str = "all"
+
+    @property
+    def is_all(self) -> bool:
+        return self.period_ms == 0
+
+    def bucket_start(self, t: int) -> int:
+        if self.is_all:
+            return MIN_INSTANT
+        return t - ((t - self.origin_ms) % self.period_ms)
+
+    def increment(self, t: int) -> int:
+        if self.is_all:
+            return MAX_INSTANT
+        return t + self.period_ms
+
+    def bucket_end(self, t: int) -> int:
+        return self.increment(self.bucket_start(t))
+
+    def iterable(self, interval: Tuple[int, int]) -> List[Tuple[int, int]]:
+        """Granularity.getIterable (Granularity.java:176-240); AllGranularity yields the input."""
+        s, e = interval
+        if self.is_all:
+            return [(s, e)]
+        out = []
+        cur = self.bucket_start(s)
+        while cur < e:
+            out.append((cur, cur + self.period_ms))
+            cur += self.period_ms
+        return out
+
+    def to_json(self):
+        if self.is_all:
+            return "all"
+        if self.name in _PERIOD_MS:
+            return self.name
+        return {"type": "duration", "duration": self.period_ms, "origin": self.origin_ms}
+
+    @staticmethod
+    def of(spec) -> "Granularity":
+        if isinstance(spec, Granularity):
+            return spec
+        if spec is None:
+            return ALL
+        if isinstance(spec, str):
+            k = spec.lower()
+            if k == "all":
+                return ALL
+            if k in _PERIOD_MS:
+                return Granularity(_PERIOD_MS[k], -3 * 86_400_000 if k == "week" else 0, k)
+            raise ValueError(f"unsupported granularity {spec!r}")
+        t = spec.get("type")
+        if t == "all":
+            return ALL
+        if t == "duration":
+            origin = parse_time(spec["origin"]) if spec.get("origin") is not None else 0
+            return Granularity(int(spec["duration"]), origin, "duration")
+        if t == "period":
+            if spec.get("timeZone") not in (None, "UTC", "Etc/UTC"):
+                raise ValueError("only UTC period granularities are supported")
+            m = _ISO_PERIOD.fullmatch(spec["period"])
+            if not m or not any(m.groups()):
+                raise ValueError(f"unsupported period {spec['period']!r} (months/years are not fixed-length)")
+            w, d, h, mi, s = (int(x or 0) for x in m.groups())
+            ms = ((((w * 7 + d) * 24 + h) * 60 + mi) * 60 + s) * 1000
+            default_origin = -3 * 86_400_000 if (w and not (d or h or mi or s)) else 0
+            origin = parse_time(spec["origin"]) if spec.get("origin") is not None else default_origin
+            return Granularity(ms, origin, "period")
+        raise ValueError(f"unsupported granularity {spec!r}")
+
+
+ALL = Granularity(0, 0, "all")
+HOUR = Granularity.of("hour")
+DAY = Granularity.of("day")
+
+
+# ----------------------------------------------------------------------------------------------
+# filters
+# ----------------------------------------------------------------------------------------------
+class DimFilter:
+    def to_json(self) -> Dict[str, Any]:
+        raise NotImplementedError
+
+    def optimize(self) -> "DimFilter":
+        return self
+
+    @staticmethod
+    def from_json(js) -> Optional["DimFilter"]:
+        if js is None:
+            return None
+        if isinstance(js, DimFilter):
+            return js
+        t = js["type"]
+        if t == "selector":
+            return SelectorDimFilter(js["dimension"], js.get("value"))
+        if t == "in":
+            return InDimFilter(js["dimension"], list(js["values"]))
+        if t == "bound":
+            return BoundDimFilter(js["dimension"], js.get("lower"), js.get("upper"),
+                                  bool(js.get("lowerStrict", False)), bool(js.get("upperStrict", False)),
+                                  _ordering_name(js.get("ordering"), js.get("alphaNumeric", False)))
+        if t == "and":
+            return AndDimFilter([DimFilter.from_json(f) for f in js["fields"]])
+        if t == "or":
+            return OrDimFilter([DimFilter.from_json(f) for f in js["fields"]])
+        if t == "not":
+            return NotDimFilter(DimFilter.from_json(js["field"]))
+        raise ValueError(f"unsupported filter type {t!r}")
+
+
+def _ordering_name(o, alpha_numeric=False) -> str:
+    if o is None:
+        return "alphanumeric" if alpha_numeric else "lexicographic"
+    if isinstance(o, dict):
+        o = o.get("type")
+    return str(o).lower()
+
+
+def _empty_to_null(v):
+    return None if v is None or v == "" else str(v)
+
+
+@dataclass
+class SelectorDimFilter(DimFilter):
+    dimension: str
+    value: Optional[str]
+
+    def to_json(self):
+        return {"type": "selector", "dimension": self.dimension, "value": self.value}
+
+
+@dataclass
+class InDimFilter(DimFilter):
+    dimension: str
+    values: List[Optional[str]]
+
+    def optimize(self):
+        # InDimFilter.optimize (InDimFilter.java:132-139): single value -> selector
+        vals = sorted({_empty_to_null(v) or "" for v in self.values})
+        if len(vals) == 1:
+            return SelectorDimFilter(self.dimension, _empty_to_null(vals[0]))
+        return InDimFilter(self.dimension, [_empty_to_null(v) for v in vals])
+
+    def to_json(self):
+        return {"type": "in", "dimension": self.dimension, "values": list(self.values)}
+
+
+@dataclass
+class BoundDimFilter(DimFilter):
+    dimension: str
+    lower: Optional[str] = None
+    upper: Optional[str] = None
+    lowerStrict: bool = False
+    upperStrict: bool = False
+    ordering: str = "lexicographic"
+
+    def to_json(self):
+        return {"type": "bound", "dimension": self.dimension, "lower": self.lower, "upper": self.upper,
+                "lowerStrict": self.lowerStrict, "upperStrict": self.upperStrict, "ordering": self.ordering}
+
+
+@dataclass
+class AndDimFilter(DimFilter):
+    fields: List[DimFilter]
+
+    def optimize(self):
+        fs = [f.optimize() for f in self.fields]
+        return fs[0] if len(fs) == 1 else AndDimFilter(fs)
+
+    def to_json(self):
+        return {"type": "and", "fields": [f.to_json() for f in self.fields]}
+
+
+@dataclass
+class OrDimFilter(DimFilter):
+    fields: List[DimFilter]
+
+    def optimize(self):
+        fs = [f.optimize() for f in self.fields]
+        return fs[0] if len(fs) == 1 else OrDimFilter(fs)
+
+    def to_json(self):
+        return {"type": "or", "fields": [f.to_json() for f in self.fields]}
+
+
+@dataclass
+class NotDimFilter(DimFilter):
+    field: DimFilter
+
+    def optimize(self):
+        return NotDimFilter(self.field.optimize())
+
+    def to_json(self):
+        return {"type": "not", "field": self.field.to_json()}
+
+
+# ----------------------------------------------------------------------------------------------
+# aggregators
+# ----------------------------------------------------------------------------------------------
+AGG_KINDS = {
+    "count": 0, "longSum": 1, "doubleSum": 2, "floatSum": 3, "longMin": 4, "longMax": 5,
+    "doubleMin": 6, "doubleMax": 7, "floatMin": 8, "floatMax": 9,
+}
+AGG_OUTPUT = {0: "long", 1: "long", 4: "long", 5: "long", 2: "double", 6: "double", 7: "double",
+              3: "float", 8: "float", 9: "float"}
+
+
+def _f32(x: float) -> float:
+    return struct.unpack("<f", struct.pack("<f", x))[0]
+
+
+def java_min(a, b):
+    """java.lang.Math.min for doubles/floats (NaN-propagating, -0.0 < +0.0)."""
+    if a != a:
+        return a
+    if a == 0.0 and b == 0.0 and math.copysign(1.0, b) < 0:
+        return b
+    return a if a <= b else b
+
+
+def java_max(a, b):
+    if a != a:
+        return a
+    if a == 0.0 and b == 0.0 and math.copysign(1.0, a) < 0:
+        return b
+    return a if a >= b else b
+
+
+def _wrap64(v: int) -> int:
+    v &= (1 << 64) - 1
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+@dataclass
+class AggregatorFactory:
+    type: str
+    name: str
+    fieldName: Optional[str] = None
+
+    def __post_init__(self):
+        if self.type not in AGG_KINDS:
+            raise ValueError(f"unsupported aggregator type {self.type!r}")
+
+    @property
+    def kind(self) -> int:
+        return AGG_KINDS[self.type]
+
+    @property
+    def output_type(self) -> str:
+        return AGG_OUTPUT[self.kind]
+
+    def initial(self):
+        """Aggregator reset / BufferAggregator.init values."""
+        k = self.kind
+        if k in (0, 1):
+            return 0
+        if k == 4:
+            return (1 << 63) - 1
+        if k == 5:
+            return -(1 << 63)
+        if k in (2, 3):
+            return 0.0
+        if k in (6, 8):
+            return math.inf
+        return -math.inf
+
+    def combine(self, a, b):
+        """AggregatorFactory.combine (e.g. LongSumAggregator.combineValues, FloatSumAggregator.java:40-43)."""
+        k = self.kind
+        if k in (0, 1):
+            return _wrap64(int(a) + int(b))
+        if k == 4:
+            return min(int(a), int(b))
+        if k == 5:
+            return max(int(a), int(b))
+        if k == 2:
+            return float(a) + float(b)
+        if k == 3:
+            return _f32(_f32(a) + _f32(b))
+        if k in (6, 8):
+            r = java_min(float(a), float(b))
+            return _f32(r) if k == 8 else r
+        r = java_max(float(a), float(b))
+        return _f32(r) if k == 9 else r
+
+    def compare_key(self, v):
+        """Sort key realising the factory comparator (Long.compare / Doubles.compare)."""
+        if self.output_type == "long":
+            return (0, int(v))
+        v = float(v)
+        if v != v:
+            return (1, 0.0)  # Double.compare: NaN is greatest
+        if v == 0.0:
+            return (0, -0.0 if math.copysign(1.0, v) < 0 else 0.0, 1 if math.copysign(1.0, v) > 0 else 0)
+        return (0, v, 0)
+
+    def to_json(self):
+        js = {"type": self.type, "name": self.name}
+        if self.fieldName is not None:
+            js["fieldName"] = self.fieldName
+        return js
+
+    @staticmethod
+    def from_json(js) -> "AggregatorFactory":
+        if isinstance(js, AggregatorFactory):
+            return js
+        return AggregatorFactory(js["type"], js["name"], js.get("fieldName"))
+
+
+def count(name="count"):
+    return AggregatorFactory("count", name)
+
+
+def long_sum(name, field_name=None):
+    return AggregatorFactory("longSum", name, field_name or name)
+
+
+def double_sum(name, field_name=None):
+    return AggregatorFactory("doubleSum", name, field_name or name)
+
+
+def float_sum(name, field_name=None):
+    return AggregatorFactory("floatSum", name, field_name or name)
+
+
+def long_min(name, field_name=None):
+    return AggregatorFactory("longMin", name, field_name or name)
+
+
+def long_max(name, field_name=None):
+    return AggregatorFactory("longMax", name, field_name or name)
+
+
+def double_min(name, field_name=None):
+    return AggregatorFactory("doubleMin", name, field_name or name)
+
+
+def double_max(name, field_name=None):
+    return AggregatorFactory("doubleMax", name, field_name or name)
+
+
+def float_min(name, field_name=None):
+    return AggregatorFactory("floatMin", name, field_name or name)
+
+
+def float_max(name, field_name=None):
+    return AggregatorFactory("floatMax", name, field_name or name)
+
+
+# ----------------------------------------------------------------------------------------------
+# topN metric specs
+# ----------------------------------------------------------------------------------------------
+@dataclass
+class TopNMetricSpec:
+    """numeric (metric name), inverted(numeric), or dimension ordering."""
+    type: str = "numeric"
+    metric: Optional[str] = None
+    ordering: str = "lexicographic"
+    previous_stop: Optional[str] = None
+
+    @staticmethod
+    def of(spec) -> "TopNMetricSpec":
+        if isinstance(spec, TopNMetricSpec):
+            return spec
+        if isinstance(spec, str):
+            return TopNMetricSpec("numeric", spec)
+        t = spec.get("type")
+        if t == "numeric":
+            return TopNMetricSpec("numeric", spec["metric"])
+        if t == "inverted":
+            inner = TopNMetricSpec.of(spec["metric"])
+            if inner.type != "numeric":
+                raise ValueError("only inverted numeric metric specs are supported")
+            return TopNMetricSpec("inverted", inner.metric)
+        if t in ("dimension", "lexicographic", "alphaNumeric"):
+            ordering = _ordering_name(spec.get("ordering"), t == "alphaNumeric")
+            return TopNMetricSpec("dimension", None, ordering, spec.get("previousStop"))
+        raise ValueError(f"unsupported topN metric spec {spec!r}")
+
+    def to_json(self):
+        if self.type == "numeric":
+            return {"type": "numeric", "metric": self.metric}
+        if self.type == "inverted":
+            return {"type": "inverted", "metric": {"type": "numeric", "metric": self.metric}}
+        return {"type": "dimension", "ordering": self.ordering, "previousStop": self.previous_stop}
+
+
+# ----------------------------------------------------------------------------------------------
+# queries
+# ----------------------------------------------------------------------------------------------
+@dataclass
+class BaseQuery:
+    dataSource: str = "ds"
+    intervals: List[Tuple[int, int]] = field(default_factory=lambda: [(MIN_INSTANT, MAX_INSTANT)])
+    granularity: Granularity = ALL
+    filter: Optional[DimFilter] = None
+    aggregations: List[AggregatorFactory] = field(default_factory=list)
+    context: Dict[str, Any] = field(default_factory=dict)
+
+    def __post_init__(self):
+        self.intervals = [parse_interval(i) for i in self.intervals]
+        if len(self.intervals) != 1:
+            raise ValueError("exactly one query interval is supported (TopNQueryEngine.java:75-77)")
+        self.granularity = Granularity.of(self.granularity)
+        self.filter = DimFilter.from_json(self.filter)
+        self.aggregations = [AggregatorFactory.from_json(a) for a in self.aggregations]
+        names = [a.name for a in self.aggregations]
+        if len(set(names)) != len(names):
+            raise ValueError("duplicate aggregator names")
+
+    @property
+    def interval(self) -> Tuple[int, int]:
+        return self.intervals[0]
+
+    def effective_filter(self) -> Optional[DimFilter]:
+        return self.filter.optimize() if self.filter is not None else None
+
+    def _base_json(self, qtype):
+        js = {"queryType": qtype, "dataSource": self.dataSource,
+              "intervals": [f"{format_time(s)}/{format_time(e)}" for s, e in self.intervals],
+              "granularity": self.granularity.to_json(),
+              "aggregations": [a.to_json() for a in self.aggregations]}
+        if self.filter is not None:
+            js["filter"] = self.filter.to_json()
+        if self.context:
+            js["context"] = dict(self.context)
+        return js
+
+
+@dataclass
+class TimeseriesQuery(BaseQuery):
+    descending: bool = False
+
+    @property
+    def skip_empty_buckets(self) -> bool:
+        return bool(self.context.get("skipEmptyBuckets", False))
+
+    def to_json(self):
+        js = self._base_json("timeseries")
+        js["descending"] = self.descending
+        return js
+
+
+@dataclass
+class TopNQuery(BaseQuery):
+    dimension: str = ""
+    metric: Any = None
+    threshold: int = 10
+
+    def __post_init__(self):
+        super().__post_init__()
+        if isinstance(self.dimension, dict):
+            if self.dimension.get("extractionFn") is not None:
+                raise ValueError("extraction functions are out of scope")
+            self.dimension = self.dimension["dimension"]
+        self.metric = TopNMetricSpec.of(self.metric)
+        if self.metric.type in ("numeric", "inverted") and self.metric.metric not in {a.name for a in self.aggregations}:
+            raise ValueError("topN metric must name an aggregator")
+
+    @property
+    def min_topn_threshold(self) -> int:
+        # TopNQueryConfig.minTopNThreshold = 1000 (TopNQueryConfig.java:32), context override
+        return int(self.context.get("minTopNThreshold", 1000))
+
+    @property
+    def segment_threshold(self) -> int:
+        """Per-segment threshold after TopNQueryQueryToolChest.preMergeQueryDecoration (:553-561)."""
+        return max(self.threshold, self.min_topn_threshold)
+
+    def to_json(self):
+        js = self._base_json("topN")
+        js.update({"dimension": self.dimension, "metric": self.metric.to_json(), "threshold": self.threshold})
+        return js
+
+
+@dataclass
+class GroupByQuery(BaseQuery):
+    dimensions: List[str] = field(default_factory=list)
+
+    def __post_init__(self):
+        super().__post_init__()
+        dims = []
+        for d in self.dimensions:
+            if isinstance(d, dict):
+                if d.get("extractionFn") is not None:
+                    raise ValueError("extraction functions are out of scope")
+                dims.append(d["dimension"])
+            else:
+                dims.append(d)
+        self.dimensions = dims
+
+    def to_json(self):
+        js = self._base_json("groupBy")
+        js["dimensions"] = list(self.dimensions)
+        return js
+
+
+def query_from_json(js: Dict[str, Any]):
+    qt = js["queryType"]
+    common = dict(dataSource=js.get("dataSource", "ds"), intervals=js["intervals"],
+                  granularity=js.get("granularity", "all"), filter=js.get("filter"),
+                  aggregations=js.get("aggregations", []), context=js.get("context", {}) or {})
+    if qt == "timeseries":
+        return TimeseriesQuery(descending=bool(js.get("descending", False)), **common)
+    if qt == "topN":
+        return TopNQuery(dimension=js["dimension"], metric=js["metric"], threshold=int(js["threshold"]), **common)
+    if qt == "groupBy":
+        return GroupByQuery(dimensions=js.get("dimensions", []), **common)
+    raise ValueError(f"unsupported queryType {qt!r}")
+
+
+@dataclass
+class Result:
+    """Result<T> (query/Result.java): timestamp + value (dict for timeseries, list for topN)."""
+    timestamp: int
+    value: Any
+
+    def to_json(self):
+        return {"timestamp": format_time(self.timestamp), "result": self.value}
+
+
+@dataclass
+class Row:
+    """groupBy MapBasedRow: timestamp + event."""
+    timestamp: int
+    event: Dict[str, Any]
+
+    def to_json(self):
+        return {"version": "v1", "timestamp": format_time(self.timestamp), "event": self.event}

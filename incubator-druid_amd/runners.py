@@ -1,0 +1,478 @@
+"""Query runners: the QueryRunnerFactory / QueryToolChest surface over the GPU engine.
+
+Mirrors the reference's per-segment runner + merge structure:
+
+* ``TimeseriesQueryRunnerFactory`` (query/timeseries/TimeseriesQueryRunnerFactory.java:66-105):
+  ``createRunner(segment)`` -> per-segment results (one Result per granularity bucket,
+  TimeseriesQueryEngine.java:57-111); ``mergeRunners`` -> results combined per bucket with
+  ``AggregatorFactory.combine`` (TimeseriesBinaryFn.java:55-81).
+* ``TopNQueryRunnerFactory`` (query/topn/TopNQueryRunnerFactory.java:61-90): per-segment top
+  ``max(threshold, minTopNThreshold)`` (TopNQueryQueryToolChest.java:553-561) from the GPU, merged
+  pairwise by TopNBinaryFn (TopNBinaryFn.java:75-135) with the query threshold, then truncated.
+* ``GroupByQueryRunnerFactory`` (GroupByStrategyV2.process/mergeRunners, GroupByStrategyV2.java:453-477):
+  per-segment grouping on the GPU, merged by dimension values (GroupByMergingQueryRunnerV2.java:170-290)
+  and ordered by timestamp then dimension values.
+
+Segments that share a device are executed as ONE batched native call (all their rows in one
+launch sequence); results are still kept per segment and merged exactly like the reference merges
+per-segment runners. Cross-device / cross-rank merging is in distributed.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import heapq
+import math
+from collections import OrderedDict, defaultdict
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+from . import query as Q
+from .segment import GpuSegment
+
+
+# ----------------------------------------------------------------------------------------------
+# slot decoding
+# ----------------------------------------------------------------------------------------------
+def _decode_slots(aggs: Sequence[Q.AggregatorFactory], slots: np.ndarray) -> List[np.ndarray]:
+    """[n, naggs] uint64 ABI slots -> one typed column per aggregator."""
+    out = []
+    for a, col in zip(aggs, slots.T):
+        col = np.ascontiguousarray(col)
+        if a.output_type == "long":
+            out.append(col.view(np.int64))
+        elif a.output_type == "double":
+            out.append(col.view(np.float64))
+        else:
+            out.append(col.astype(np.uint64).view(np.uint32)[0::2].view(np.float32))
+    return out
+
+
+def _py(v, out_type):
+    return int(v) if out_type == "long" else float(v)
+
+
+def _group_by_device(segments: Sequence[GpuSegment]) -> "OrderedDict[int, List[int]]":
+    g: "OrderedDict[int, List[int]]" = OrderedDict()
+    for i, s in enumerate(segments):
+        g.setdefault(id(s.context), []).append(i)
+    return g
+
+
+def _handles(segs: Sequence[GpuSegment]):
+    arr = (ctypes.c_void_p * len(segs))(*[s.handle.value for s in segs])
+    return arr
+
+
+class RunStats:
+    """Per-call QueryMetrics counters accumulated over native calls."""
+
+    def __init__(self):
+        self.calls: List[Dict] = []
+
+    def add(self, m: N.dg_metrics):
+        self.calls.append(m.as_dict())
+
+    def total(self, key):
+        return sum(c[key] for c in self.calls)
+
+
+# ----------------------------------------------------------------------------------------------
+# timeseries
+# ----------------------------------------------------------------------------------------------
+def timeseries_per_segment(segments: Sequence[GpuSegment], query: Q.TimeseriesQuery,
+                           stats: Optional[RunStats] = None) -> List[List[Q.Result]]:
+    out: List[List[Q.Result]] = [[] for _ in segments]
+    na = len(query.aggregations)
+    for _, idx in _group_by_device(segments).items():
+        segs = [segments[i] for i in idx]
+        cap = _bucket_cap(segs, query)
+        scan, keep = N.make_scan(query, Q)
+        n = len(segs)
+        nb = np.zeros(n, dtype=np.int32)
+        times = np.zeros(n * cap, dtype=np.int64)
+        rows = np.zeros(n * cap, dtype=np.int64)
+        vals = np.zeros(n * cap * max(na, 1), dtype=np.uint64)
+        m = N.dg_metrics()
+        N.check(N.lib().dg_timeseries_run(_handles(segs), n, ctypes.byref(scan), cap, nb.ctypes.data,
+                                          times.ctypes.data, rows.ctypes.data, vals.ctypes.data, ctypes.byref(m)))
+        if stats is not None:
+            stats.add(m)
+        for k, i in enumerate(idx):
+            res = []
+            cols = _decode_slots(query.aggregations, vals.reshape(-1, max(na, 1))[k * cap:k * cap + nb[k], :na])
+            for b in range(nb[k]):
+                if query.skip_empty_buckets and rows[k * cap + b] == 0:
+                    continue
+                res.append(Q.Result(int(times[k * cap + b]),
+                                    {a.name: _py(c[b], a.output_type) for a, c in zip(query.aggregations, cols)}))
+            out[i] = res
+    return out
+
+
+def _bucket_cap(segs, query) -> int:
+    g = query.granularity
+    if g.is_all:
+        return 1
+    cap = 1
+    qs, qe = query.interval
+    for s in segs:
+        lo = max(qs, s.min_time)
+        hi = min(qe, g.bucket_end(s.max_time))
+        if hi > lo:
+            cap = max(cap, (hi - g.bucket_start(lo) + g.period_ms - 1) // g.period_ms)
+    return int(cap)
+
+
+def merge_timeseries(query: Q.TimeseriesQuery, per_segment: List[List[Q.Result]]) -> List[Q.Result]:
+    """ResultMergeQueryRunner + TimeseriesBinaryFn: combine results of the same bucket."""
+    gran = query.granularity
+    merged: Dict[int, Q.Result] = {}
+    flat = sorted(((r.timestamp, si, k, r) for si, rs in enumerate(per_segment) for k, r in enumerate(rs)),
+                  key=lambda x: (x[0], x[1], x[2]))
+    for ts, _, _, r in flat:
+        key = 0 if gran.is_all else gran.bucket_start(ts)
+        if key not in merged:
+            merged[key] = Q.Result(r.timestamp if gran.is_all else key, dict(r.value))
+        else:
+            acc = merged[key].value
+            for a in query.aggregations:
+                acc[a.name] = a.combine(acc[a.name], r.value[a.name])
+    out = [merged[k] for k in sorted(merged)]
+    if query.descending:
+        out.reverse()
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# topN
+# ----------------------------------------------------------------------------------------------
+def _java_key(s: Optional[str]):
+    return (0, b"") if s is None else (1, s.encode("utf-16-be", "surrogatepass"))
+
+
+class _HeapItem:
+    __slots__ = ("mk", "dk", "entry")
+
+    def __init__(self, mk, dk, entry):
+        self.mk, self.dk, self.entry = mk, dk, entry
+
+    def __lt__(self, o):
+        return (self.mk, self.dk) < (o.mk, o.dk)
+
+
+class TopNResultBuilder:
+    """TopNNumericResultBuilder (TopNNumericResultBuilder.java:94-235): bounded priority queue,
+    add only when below threshold or strictly better than the current minimum metric."""
+
+    def __init__(self, query: Q.TopNQuery, threshold: int):
+        spec = query.metric
+        agg = next(a for a in query.aggregations if a.name == spec.metric)
+        self.metric = spec.metric
+        self.dim = query.dimension
+        self.inverted = spec.type == "inverted"
+        self.agg = agg
+        self.threshold = threshold
+        self.heap: List[_HeapItem] = []
+
+    def _mk(self, v):
+        k = self.agg.compare_key(v)
+        return _Rev(k) if self.inverted else k
+
+    def add(self, entry: Dict):
+        mk = self._mk(entry[self.metric])
+        if len(self.heap) < self.threshold or self.heap[0].mk < mk:
+            heapq.heappush(self.heap, _HeapItem(mk, _java_key(entry[self.dim]), entry))
+        if len(self.heap) > self.threshold:
+            heapq.heappop(self.heap)
+
+    def build(self) -> List[Dict]:
+        items = sorted(self.heap, key=lambda h: (_Rev(h.mk), h.dk))
+        return [h.entry for h in items]
+
+
+class _Rev:
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+    def __lt__(self, o):
+        return o.v < self.v
+
+    def __eq__(self, o):
+        return self.v == o.v
+
+
+def topn_per_segment(segments: Sequence[GpuSegment], query: Q.TopNQuery,
+                     stats: Optional[RunStats] = None) -> List[List[Q.Result]]:
+    if query.metric.type not in ("numeric", "inverted"):
+        raise N.UnsupportedQuery(2, "dimension-ordered topN")
+    if not query.granularity.is_all:
+        raise N.UnsupportedQuery(2, "topN with non-ALL granularity")
+    out: List[List[Q.Result]] = [[] for _ in segments]
+    na = len(query.aggregations)
+    K = query.segment_threshold
+    metric_idx = [a.name for a in query.aggregations].index(query.metric.metric)
+    for _, idx in _group_by_device(segments).items():
+        segs = [segments[i] for i in idx]
+        scan, keep = N.make_scan(query, Q)
+        t = N.dg_topn()
+        dim = query.dimension.encode()
+        t.dimension = dim
+        t.metric_agg = metric_idx
+        t.inverted = int(query.metric.type == "inverted")
+        t.threshold = K
+        n = len(segs)
+        cnt = np.zeros(n, dtype=np.int32)
+        ids = np.zeros(n * K, dtype=np.int32)
+        vals = np.zeros(n * K * max(na, 1), dtype=np.uint64)
+        m = N.dg_metrics()
+        N.check(N.lib().dg_topn_run(_handles(segs), n, ctypes.byref(scan), ctypes.byref(t), cnt.ctypes.data,
+                                    ids.ctypes.data, vals.ctypes.data, ctypes.byref(m)))
+        if stats is not None:
+            stats.add(m)
+        for k, i in enumerate(idx):
+            if cnt[k] < 0:  # no cursor: the segment does not overlap the interval
+                out[i] = []
+                continue
+            seg = segs[k]
+            dictionary = seg.dictionary(query.dimension)
+            c = int(cnt[k])
+            cols = _decode_slots(query.aggregations, vals.reshape(-1, max(na, 1))[k * K:k * K + c, :na])
+            entries = []
+            for j in range(c):
+                e = {query.dimension: dictionary[ids[k * K + j]] if dictionary else None}
+                for a, col in zip(query.aggregations, cols):
+                    e[a.name] = _py(col[j], a.output_type)
+                entries.append(e)
+            ts = max(query.interval[0], seg.min_time)
+            out[i] = [Q.Result(ts, entries)]
+    return out
+
+
+def topn_binary_fn(query: Q.TopNQuery, r1: Optional[Q.Result], r2: Optional[Q.Result]) -> Optional[Q.Result]:
+    """TopNBinaryFn.apply (TopNBinaryFn.java:75-135)."""
+    if r1 is None:
+        return r2
+    if r2 is None:
+        return r1
+    dim = query.dimension
+    ret: Dict = {}
+    for v in r1.value:
+        ret[v[dim]] = v
+    for v in r2.value:
+        k = v[dim]
+        if k in ret:
+            a = ret[k]
+            c = {dim: k}
+            for agg in query.aggregations:
+                c[agg.name] = agg.combine(a[agg.name], v[agg.name])
+            ret[k] = c
+        else:
+            ret[k] = v
+    bob = TopNResultBuilder(query, query.threshold)
+    for v in ret.values():
+        bob.add(v)
+    ts = r1.timestamp if query.granularity.is_all else query.granularity.bucket_start(r1.timestamp)
+    return Q.Result(ts, bob.build())
+
+
+def merge_topn(query: Q.TopNQuery, per_segment: List[List[Q.Result]]) -> List[Q.Result]:
+    gran = query.granularity
+    flat = sorted(((r.timestamp, si, r) for si, rs in enumerate(per_segment) for r in rs), key=lambda x: (x[0], x[1]))
+    merged: Dict[int, Q.Result] = {}
+    for ts, _, r in flat:
+        key = 0 if gran.is_all else gran.bucket_start(ts)
+        merged[key] = topn_binary_fn(query, merged.get(key), r)
+    return [Q.Result(merged[k].timestamp, merged[k].value[:query.threshold]) for k in sorted(merged)]
+
+
+# ----------------------------------------------------------------------------------------------
+# groupBy
+# ----------------------------------------------------------------------------------------------
+class GroupByPartial:
+    """Columnar per-segment groupBy output: bucket times, dimension values, aggregate columns."""
+
+    def __init__(self, times: np.ndarray, dims: List[np.ndarray], aggs: List[np.ndarray]):
+        self.times, self.dims, self.aggs = times, dims, aggs
+
+    def __len__(self):
+        return len(self.times)
+
+
+def groupby_per_segment(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
+                        stats: Optional[RunStats] = None) -> List[GroupByPartial]:
+    out: List[Optional[GroupByPartial]] = [None] * len(segments)
+    na = len(query.aggregations)
+    nd = len(query.dimensions)
+    for _, idx in _group_by_device(segments).items():
+        segs = [segments[i] for i in idx]
+        scan, keep = N.make_scan(query, Q)
+        dims = (ctypes.c_char_p * max(nd, 1))(*[d.encode() for d in query.dimensions])
+        g = N.dg_groupby()
+        g.dimensions = ctypes.cast(dims, ctypes.POINTER(ctypes.c_char_p))
+        g.n_dims = nd
+        res = ctypes.c_void_p()
+        m = N.dg_metrics()
+        N.check(N.lib().dg_groupby_run(_handles(segs), len(segs), ctypes.byref(scan), ctypes.byref(g),
+                                       ctypes.byref(res), ctypes.byref(m)))
+        if stats is not None:
+            stats.add(m)
+        try:
+            for k, i in enumerate(idx):
+                ng = max(int(N.lib().dg_result_groups(res, k)), 0)
+                t = np.zeros(max(ng, 1), dtype=np.int64)
+                ids = np.zeros(max(ng * nd, 1), dtype=np.int32)
+                vals = np.zeros(max(ng * na, 1), dtype=np.uint64)
+                N.check(N.lib().dg_result_fetch_groups(res, k, t.ctypes.data, ids.ctypes.data, vals.ctypes.data))
+                ids = ids[:ng * nd].reshape(ng, nd) if nd else np.zeros((ng, 0), np.int32)
+                dim_cols = []
+                for d, dname in enumerate(query.dimensions):
+                    dictionary = np.array(segs[k].dictionary(dname), dtype=object)
+                    dim_cols.append(dictionary[ids[:, d]] if ng else np.zeros(0, dtype=object))
+                agg_cols = _decode_slots(query.aggregations, vals[:ng * na].reshape(ng, na)) if na else []
+                out[i] = GroupByPartial(t[:ng], dim_cols, agg_cols)
+        finally:
+            N.lib().dg_result_release(res)
+    return out  # type: ignore
+
+
+def merge_groupby_columnar(query: Q.GroupByQuery, partials: Sequence[GroupByPartial]):
+    """Merge per-segment partials by (bucket, dimension values); returns sorted columnar arrays."""
+    gran = query.granularity
+    parts = [p for p in partials if p is not None and len(p)]
+    nd = len(query.dimensions)
+    if not parts:
+        return np.zeros(0, np.int64), [np.zeros(0, object) for _ in range(nd)], [np.zeros(0) for _ in query.aggregations]
+    times = np.concatenate([p.times for p in parts])
+    keys_t = times if not gran.is_all else np.zeros(len(times), np.int64)
+    dim_codes = []
+    dim_values = []
+    for d in range(nd):
+        col = np.concatenate([p.dims[d] for p in parts])
+        uniq = sorted(set(col.tolist()), key=_java_key)  # global dictionary in Java order, null first
+        index = {v: i for i, v in enumerate(uniq)}
+        dim_codes.append(np.fromiter((index[v] for v in col), dtype=np.int64, count=len(col)))
+        dim_values.append(np.array(uniq, dtype=object))
+    order_keys = [keys_t] + dim_codes
+    order = np.lexsort(tuple(reversed(order_keys)))
+    sk = [k[order] for k in order_keys]
+    change = np.ones(len(order), dtype=bool)
+    if len(order) > 1:
+        diff = np.zeros(len(order) - 1, dtype=bool)
+        for k in sk:
+            diff |= k[1:] != k[:-1]
+        change[1:] = diff
+    starts = np.nonzero(change)[0]
+    out_aggs = []
+    for a_i, a in enumerate(query.aggregations):
+        col = np.concatenate([p.aggs[a_i] for p in parts])[order]
+        out_aggs.append(_reduce(a, col, starts))
+    out_times = (np.minimum.reduceat(times[order], starts) if gran.is_all else sk[0][starts])
+    out_dims = [dim_values[d][sk[1 + d][starts]] for d in range(nd)]
+    return out_times, out_dims, out_aggs
+
+
+def _reduce(a: Q.AggregatorFactory, col: np.ndarray, starts: np.ndarray) -> np.ndarray:
+    k = a.kind
+    if k in (0, 1):
+        return np.add.reduceat(col.astype(np.int64), starts)
+    if k == 4:
+        return np.minimum.reduceat(col, starts)
+    if k == 5:
+        return np.maximum.reduceat(col, starts)
+    if k in (2, 3):
+        return np.add.reduceat(col, starts)
+    # Math.min / Math.max: NaN propagates (np.minimum propagates NaN too)
+    if k in (6, 8):
+        return np.minimum.reduceat(col, starts)
+    return np.maximum.reduceat(col, starts)
+
+
+def merge_groupby(query: Q.GroupByQuery, partials: Sequence[GroupByPartial]) -> List[Q.Row]:
+    t, dims, aggs = merge_groupby_columnar(query, partials)
+    rows = []
+    for r in range(len(t)):
+        ev = {d: dims[i][r] for i, d in enumerate(query.dimensions)}
+        for a, col in zip(query.aggregations, aggs):
+            ev[a.name] = _py(col[r], a.output_type)
+        rows.append(Q.Row(int(t[r]), ev))
+    return rows
+
+
+# ----------------------------------------------------------------------------------------------
+# factories (QueryRunnerFactory surface)
+# ----------------------------------------------------------------------------------------------
+class SegmentQueryRunner:
+    """QueryRunner for one segment (QueryRunnerFactory.createRunner)."""
+
+    def __init__(self, factory, segment: GpuSegment):
+        self.factory, self.segment = factory, segment
+
+    def run(self, query):
+        return self.factory.toolchest.merge(query, self.factory.per_segment([self.segment], query))
+
+
+class MergedQueryRunner:
+    """QueryRunnerFactory.mergeRunners: all segments of one device run as one batched native call."""
+
+    def __init__(self, factory, runners: Iterable[SegmentQueryRunner]):
+        self.factory = factory
+        self.segments = [r.segment for r in runners]
+        self.stats = RunStats()
+
+    def run(self, query):
+        per = self.factory.per_segment(self.segments, query, self.stats)
+        return self.factory.toolchest.merge(query, per)
+
+
+class _ToolChest:
+    def __init__(self, merge_fn):
+        self.merge = merge_fn
+
+
+class TimeseriesQueryRunnerFactory:
+    toolchest = _ToolChest(merge_timeseries)
+
+    @staticmethod
+    def per_segment(segments, query, stats=None):
+        return timeseries_per_segment(segments, query, stats)
+
+    def createRunner(self, segment):
+        return SegmentQueryRunner(self, segment)
+
+    def mergeRunners(self, runners):
+        return MergedQueryRunner(self, runners)
+
+
+class TopNQueryRunnerFactory(TimeseriesQueryRunnerFactory):
+    toolchest = _ToolChest(merge_topn)
+
+    @staticmethod
+    def per_segment(segments, query, stats=None):
+        return topn_per_segment(segments, query, stats)
+
+
+class GroupByQueryRunnerFactory(TimeseriesQueryRunnerFactory):
+    toolchest = _ToolChest(merge_groupby)
+
+    @staticmethod
+    def per_segment(segments, query, stats=None):
+        return groupby_per_segment(segments, query, stats)
+
+
+FACTORIES = {Q.TimeseriesQuery: TimeseriesQueryRunnerFactory(), Q.TopNQuery: TopNQueryRunnerFactory(),
+             Q.GroupByQuery: GroupByQueryRunnerFactory()}
+
+
+def run_query(query, segments: Sequence[GpuSegment], stats: Optional[RunStats] = None):
+    """QueryRunnerFactoryConglomerate lookup + mergeRunners over the given segments."""
+    if isinstance(query, dict):
+        query = Q.query_from_json(query)
+    f = FACTORIES[type(query)]
+    runner = f.mergeRunners([f.createRunner(s) for s in segments])
+    if stats is not None:
+        runner.stats = stats
+    return runner.run(query)

@@ -1,0 +1,384 @@
+"""Druid v9 segment writer (the build's IndexMergerV9 for synthetic and fixture data).
+
+Writes a segment directory that the reference's ``IndexIO.V9IndexLoader.load``
+(processing/.../segment/IndexIO.java:569-663) would map, byte layout per column:
+
+* smoosh container: ``version.bin`` (int 9, big-endian), ``meta.smoosh`` and
+  ``00000.smoosh`` (java-util/.../io/smoosh/FileSmoosher.java, SmooshedFileMapper.java).
+* ``index.drd``: GenericIndexed<String> columns, GenericIndexed<String> dimensions,
+  interval (2 x int64 BE), bitmap serde JSON (IndexIO.java:584-610).
+* every column: int32 BE length + ColumnDescriptor JSON, then its part
+  (IndexIO.java:665-672).
+* GenericIndexed v1 (processing/.../segment/data/GenericIndexed.java:52-77,479-492):
+  ``[0x01][sorted][int32 numBytesUsed][int32 n][n x int32 end offsets][(int32 marker)(bytes)...]``.
+* string columns: DictionaryEncodedColumnPartSerde COMPRESSED (version 2) + flags
+  (serde/DictionaryEncodedColumnPartSerde.java:283-345), ids via
+  CompressedVSizeColumnarIntsSerializer (data/CompressedVSizeColumnarIntsSerializer.java:47-62,
+  chunk sizing data/CompressedVSizeColumnarIntsSupplier.java:82-101), one Concise or Roaring bitmap
+  per dictionary value.
+* long/float/double columns: BlockLayoutColumnar{Longs,Floats,Doubles}Serializer with LONGS
+  encoding (data/BlockLayoutColumnarLongsSerializer.java:60-66, 8192 longs or 16384 floats per
+  64 KiB block), LZ4 (id 0x01), UNCOMPRESSED blocks (0xFF) or NONE (0xFE, EntireLayout).
+
+LZ4 blocks are produced with the system ``liblz4.so.1`` (HC level 9 by default, like
+lz4-java's ``highCompressor``; "fast" for large synthetic data). Byte order inside blocks is
+little-endian (IndexIO.BYTE_ORDER = nativeOrder, IndexIO.java:90).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _tools
+
+BUFFER_SIZE = 65536  # CompressedPools.BUFFER_SIZE (segment/CompressedPools.java:39)
+
+COMPRESSION_IDS = {"lzf": 0x00, "lz4": 0x01, "uncompressed": 0xFF, "none": 0xFE}
+
+MIN_INSTANT = -(2 ** 62)  # JodaUtils.MIN_INSTANT = Long.MIN_VALUE / 2
+
+
+# --------------------------------------------------------------------------------------------
+# LZ4 (system liblz4; the decoder used by queries is the build's own HIP kernel)
+# --------------------------------------------------------------------------------------------
+_lz4 = None
+
+
+def _lz4lib():
+    global _lz4
+    if _lz4 is None:
+        lib = ctypes.CDLL("liblz4.so.1")
+        lib.LZ4_compressBound.restype = ctypes.c_int
+        lib.LZ4_compressBound.argtypes = [ctypes.c_int]
+        lib.LZ4_compress_HC.restype = ctypes.c_int
+        lib.LZ4_compress_HC.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        lib.LZ4_compress_default.restype = ctypes.c_int
+        lib.LZ4_compress_default.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        _lz4 = lib
+    return _lz4
+
+
+def lz4_compress(data: bytes, mode: str = "hc") -> bytes:
+    lib = _lz4lib()
+    bound = lib.LZ4_compressBound(len(data))
+    out = ctypes.create_string_buffer(bound)
+    if mode == "hc":
+        n = lib.LZ4_compress_HC(data, out, len(data), bound, 9)
+    else:
+        n = lib.LZ4_compress_default(data, out, len(data), bound)
+    if n <= 0:
+        raise RuntimeError("LZ4 compression failed")
+    return out.raw[:n]
+
+
+# --------------------------------------------------------------------------------------------
+# GenericIndexed v1
+# --------------------------------------------------------------------------------------------
+def generic_indexed(values: Sequence[Optional[bytes]], sorted_flag: bool) -> bytes:
+    """Serialize a GenericIndexed v1 (GenericIndexed.java:52-77; writer GenericIndexedWriter)."""
+    n = len(values)
+    ends = np.empty(n, dtype=">i4")
+    parts = []
+    pos = 0
+    for i, v in enumerate(values):
+        if v is None:
+            parts.append(struct.pack(">i", -1))
+            pos += 4
+        else:
+            parts.append(struct.pack(">i", len(v)))
+            parts.append(v)
+            pos += 4 + len(v)
+        ends[i] = pos
+    body = struct.pack(">i", n) + ends.tobytes() + b"".join(parts)
+    return bytes([0x01, 0x01 if sorted_flag else 0x00]) + struct.pack(">i", len(body)) + body
+
+
+def _blocks_generic_indexed(blocks: List[bytes]) -> bytes:
+    return generic_indexed(blocks, sorted_flag=False)
+
+
+# --------------------------------------------------------------------------------------------
+# Dictionary ordering (GenericIndexed.STRING_STRATEGY: Comparators.naturalNullsFirst over
+# java.lang.String.compareTo, i.e. UTF-16 code-unit order)
+# --------------------------------------------------------------------------------------------
+def java_string_key(s: str) -> bytes:
+    return s.encode("utf-16-be", "surrogatepass")
+
+
+def num_bytes_for_max(max_value: int) -> int:
+    """VSizeColumnarInts.getNumBytesForMax (data/VSizeColumnarInts.java:84-99)."""
+    if max_value <= 0xFF:
+        return 1
+    if max_value <= 0xFFFF:
+        return 2
+    if max_value <= 0xFFFFFF:
+        return 3
+    return 4
+
+
+def max_ints_in_buffer_for_bytes(num_bytes: int) -> int:
+    """CompressedVSizeColumnarIntsSupplier.maxIntsInBufferForBytes (:82-101)."""
+    padding = 0 if num_bytes in (1, 2) else 4 - num_bytes
+    max_size_per = (BUFFER_SIZE - padding) // num_bytes
+    return 1 << (max_size_per.bit_length() - 1)
+
+
+# --------------------------------------------------------------------------------------------
+# Column part serializers
+# --------------------------------------------------------------------------------------------
+def _compress_blocks(raw: bytes, block_bytes: int, compression: str, lz4_mode: str) -> List[bytes]:
+    blocks = []
+    for off in range(0, len(raw), block_bytes):
+        chunk = raw[off:off + block_bytes]
+        if compression == "lz4":
+            blocks.append(lz4_compress(chunk, lz4_mode))
+        elif compression == "uncompressed":
+            blocks.append(chunk)
+        else:
+            raise ValueError(f"unsupported block compression {compression}")
+    return blocks
+
+
+def numeric_column_part(values: np.ndarray, kind: str, compression: str, lz4_mode: str) -> bytes:
+    """CompressedColumnar{Longs,Floats,Doubles}Supplier layout, LONGS encoding (legacy, no flag)."""
+    dtype = {"long": "<i8", "double": "<f8", "float": "<f4"}[kind]
+    arr = np.ascontiguousarray(values, dtype=dtype)
+    width = arr.dtype.itemsize
+    size_per = BUFFER_SIZE // width  # 8192 longs/doubles, 16384 floats
+    cid = COMPRESSION_IDS[compression]
+    header = struct.pack(">Bii", 0x02, len(arr), size_per) + bytes([cid])
+    raw = arr.tobytes()
+    if compression == "none":
+        # EntireLayoutColumnar{Longs,...}: values follow directly (CompressionFactory.getLongSupplier)
+        return header + raw
+    return header + _blocks_generic_indexed(_compress_blocks(raw, size_per * width, compression, lz4_mode))
+
+
+def ids_part(ids: np.ndarray, cardinality: int, compression: str, lz4_mode: str) -> bytes:
+    """CompressedVSizeColumnarIntsSerializer (little-endian values, numBytes from cardinality)."""
+    nb = num_bytes_for_max(cardinality)
+    size_per = max_ints_in_buffer_for_bytes(nb)
+    ids32 = np.ascontiguousarray(ids, dtype="<u4")
+    if nb == 4:
+        raw = ids32.tobytes()
+    else:
+        raw = ids32.view(np.uint8).reshape(-1, 4)[:, :nb].tobytes()
+    cid = COMPRESSION_IDS["uncompressed" if compression == "none" else compression]
+    header = struct.pack(">BBii", 0x02, nb, len(ids32), size_per) + bytes([cid])
+    comp = "uncompressed" if compression == "none" else compression
+    return header + _blocks_generic_indexed(_compress_blocks(raw, size_per * nb, comp, lz4_mode))
+
+
+def concise_bitmaps(ids: np.ndarray, cardinality: int) -> List[bytes]:
+    words, counts = _tools.concise_encode_column(ids, cardinality)
+    out = []
+    pos = 0
+    be = words.astype(">i4")
+    for c in counts:
+        out.append(be[pos:pos + c].tobytes())
+        pos += c
+    return out
+
+
+def roaring_serialize(rows: np.ndarray, run_optimize: bool = True) -> bytes:
+    """Portable Roaring format (RoaringFormatSpec; RoaringBitmap 0.5.18 ``serialize``)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    if len(rows) == 0:
+        return struct.pack("<II", 12346, 0)
+    keys = (rows >> 16).astype(np.int64)
+    uk, starts = np.unique(keys, return_index=True)
+    ends = np.append(starts[1:], len(rows))
+    containers = []  # (key, card, kind, payload)
+    for k, s, e in zip(uk, starts, ends):
+        lows = (rows[s:e] & 0xFFFF).astype(np.uint16)
+        card = e - s
+        # run detection
+        brk = np.nonzero(np.diff(lows.astype(np.int32)) != 1)[0]
+        n_runs = len(brk) + 1
+        run_bytes = 2 + 4 * n_runs
+        arr_bytes = 2 * card if card <= 4096 else 1 << 30
+        bmp_bytes = 8192
+        if run_optimize and run_bytes < min(arr_bytes, bmp_bytes):
+            rs = np.concatenate([[0], brk + 1])
+            re_ = np.concatenate([brk, [card - 1]])
+            starts_v = lows[rs].astype(np.uint16)
+            lens_v = (lows[re_].astype(np.int32) - lows[rs].astype(np.int32)).astype(np.uint16)
+            payload = struct.pack("<H", n_runs) + np.stack([starts_v, lens_v], axis=1).astype("<u2").tobytes()
+            containers.append((int(k), card, "run", payload))
+        elif card <= 4096:
+            containers.append((int(k), card, "array", lows.astype("<u2").tobytes()))
+        else:
+            bits = np.zeros(65536, dtype=np.uint8)
+            bits[lows] = 1
+            containers.append((int(k), card, "bitmap", np.packbits(bits, bitorder="little").tobytes()))
+    size = len(containers)
+    has_run = any(c[2] == "run" for c in containers)
+    out = bytearray()
+    if has_run:
+        out += struct.pack("<I", 12347 | ((size - 1) << 16))
+        runbits = np.zeros(((size + 7) // 8) * 8, dtype=np.uint8)
+        for i, c in enumerate(containers):
+            if c[2] == "run":
+                runbits[i] = 1
+        out += np.packbits(runbits, bitorder="little").tobytes()
+    else:
+        out += struct.pack("<II", 12346, size)
+    for k, card, _, _ in containers:
+        out += struct.pack("<HH", k, card - 1)
+    if (not has_run) or size >= 4:
+        offset = len(out) + 4 * size
+        for c in containers:
+            out += struct.pack("<I", offset)
+            offset += len(c[3])
+    for c in containers:
+        out += c[3]
+    return bytes(out)
+
+
+def roaring_bitmaps(ids: np.ndarray, cardinality: int) -> List[bytes]:
+    order = np.argsort(ids, kind="stable")
+    sorted_ids = ids[order]
+    bounds = np.searchsorted(sorted_ids, np.arange(cardinality + 1))
+    return [roaring_serialize(np.sort(order[bounds[v]:bounds[v + 1]])) for v in range(cardinality)]
+
+
+def string_column_part(dictionary: List[Optional[str]], ids: np.ndarray, bitmap: str,
+                       compression: str, lz4_mode: str) -> bytes:
+    card = len(dictionary)
+    dict_vals = [None if (v is None or v == "") else v.encode("utf-8") for v in dictionary]
+    # null / "" are both stored as a zero-length value (NullHandling.replaceWithDefault)
+    dict_vals = [b"" if v is None else v for v in dict_vals]
+    out = bytes([0x02]) + struct.pack(">i", 0)  # COMPRESSED, flags = 0 (single-value, bitmaps)
+    out += generic_indexed(dict_vals, sorted_flag=True)
+    out += ids_part(ids, card, compression, lz4_mode)
+    if bitmap == "concise":
+        bms = concise_bitmaps(ids, card)
+    else:
+        bms = roaring_bitmaps(ids, card)
+    out += generic_indexed(bms, sorted_flag=False)
+    return out
+
+
+def _bitmap_json(bitmap: str) -> dict:
+    if bitmap == "concise":
+        return {"type": "concise"}
+    return {"type": "roaring", "compressRunOnSerialization": True}
+
+
+def _descriptor(value_type: str, part: dict) -> bytes:
+    js = json.dumps({"valueType": value_type, "hasMultipleValues": False, "parts": [part]},
+                    separators=(",", ":")).encode()
+    return struct.pack(">i", len(js)) + js
+
+
+# --------------------------------------------------------------------------------------------
+# Dimension encoding helpers
+# --------------------------------------------------------------------------------------------
+def encode_strings(values: Sequence[Optional[str]]) -> Tuple[List[str], np.ndarray]:
+    """Build a sorted dictionary (nulls first) and per-row ids from python strings."""
+    norm = ["" if v is None else str(v) for v in values]
+    uniq = sorted(set(norm), key=java_string_key)
+    index = {v: i for i, v in enumerate(uniq)}
+    ids = np.fromiter((index[v] for v in norm), dtype=np.int32, count=len(norm))
+    return uniq, ids
+
+
+def encode_int_strings(values: np.ndarray, null_mask: Optional[np.ndarray] = None) -> Tuple[List[str], np.ndarray]:
+    """Fast path for integer-valued string dims: dictionary = sorted(str(v)), ids by table lookup."""
+    values = np.asarray(values, dtype=np.int64)
+    present = np.unique(values if null_mask is None else values[~null_mask])
+    strs = [str(int(v)) for v in present]
+    has_null = null_mask is not None and bool(null_mask.any())
+    order = sorted(range(len(strs)), key=lambda i: java_string_key(strs[i]))
+    dictionary = ([""] if has_null else []) + [strs[i] for i in order]
+    rank = np.empty(len(strs), dtype=np.int32)
+    rank[np.asarray(order, dtype=np.int64)] = np.arange(len(strs), dtype=np.int32) + (1 if has_null else 0)
+    pos = np.searchsorted(present, values)
+    pos = np.clip(pos, 0, max(len(present) - 1, 0))
+    ids = rank[pos] if len(present) else np.zeros(len(values), dtype=np.int32)
+    if has_null:
+        ids = np.where(null_mask, 0, ids).astype(np.int32)
+    return dictionary, ids.astype(np.int32)
+
+
+@dataclass
+class SegmentSpec:
+    timestamps: np.ndarray
+    dims: Dict[str, Tuple[List[str], np.ndarray]] = field(default_factory=dict)
+    metrics: Dict[str, Tuple[str, np.ndarray]] = field(default_factory=dict)
+    interval: Optional[Tuple[int, int]] = None
+
+
+def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", compression: str = "lz4",
+                  dim_compression: Optional[str] = None, lz4_mode: str = "hc") -> str:
+    """Write a v9 segment directory. Rows must already be in segment order (time-sorted)."""
+    os.makedirs(out_dir, exist_ok=True)
+    n = len(spec.timestamps)
+    ts = np.asarray(spec.timestamps, dtype=np.int64)
+    if n and np.any(np.diff(ts) < 0):
+        raise ValueError("segment rows must be sorted by __time")
+    dim_comp = dim_compression or ("uncompressed" if compression == "none" else compression)
+    files: Dict[str, bytes] = {}
+    files["__time"] = _descriptor("LONG", {"type": "long", "byteOrder": "LITTLE_ENDIAN"}) + \
+        numeric_column_part(ts, "long", compression, lz4_mode)
+    for name, (dictionary, ids) in spec.dims.items():
+        ids = np.asarray(ids, dtype=np.int32)
+        if len(ids) != n:
+            raise ValueError(f"dimension {name} has {len(ids)} rows, expected {n}")
+        part = {"type": "stringDictionary", "bitmapSerdeFactory": _bitmap_json(bitmap), "byteOrder": "LITTLE_ENDIAN"}
+        files[name] = _descriptor("STRING", part) + string_column_part(dictionary, ids, bitmap, dim_comp, lz4_mode)
+    for name, (kind, vals) in spec.metrics.items():
+        vals = np.asarray(vals)
+        if len(vals) != n:
+            raise ValueError(f"metric {name} has {len(vals)} rows, expected {n}")
+        vt = {"long": "LONG", "double": "DOUBLE", "float": "FLOAT"}[kind]
+        files[name] = _descriptor(vt, {"type": kind, "byteOrder": "LITTLE_ENDIAN"}) + \
+            numeric_column_part(vals, kind, compression, lz4_mode)
+    dims = list(spec.dims.keys())
+    cols = dims + list(spec.metrics.keys())
+    if spec.interval is not None:
+        istart, iend = spec.interval
+    else:
+        istart = int(ts[0]) if n else 0
+        iend = int(ts[-1]) + 1 if n else 1
+    bm_json = json.dumps(_bitmap_json(bitmap), separators=(",", ":")).encode()
+    files["index.drd"] = (generic_indexed([c.encode() for c in cols], sorted_flag=False)
+                          + generic_indexed([d.encode() for d in dims], sorted_flag=False)
+                          + struct.pack(">qq", istart, iend)
+                          + struct.pack(">i", len(bm_json)) + bm_json)
+    files["metadata.drd"] = json.dumps({"container": {}, "aggregators": None, "timestampSpec": None,
+                                        "queryGranularity": {"type": "none"}, "rollup": False}).encode()
+    _write_smoosh(out_dir, files)
+    with open(os.path.join(out_dir, "version.bin"), "wb") as f:
+        f.write(struct.pack(">i", 9))
+    return out_dir
+
+
+def _write_smoosh(out_dir: str, files: Dict[str, bytes], max_chunk: int = 2 ** 31 - 1) -> None:
+    """FileSmoosher layout: numbered chunk files + meta.smoosh 'name,chunk,start,end' lines."""
+    names = sorted(files.keys())
+    chunks: List[List[Tuple[str, bytes]]] = [[]]
+    size = 0
+    for nm in names:
+        b = files[nm]
+        if size + len(b) > max_chunk and chunks[-1]:
+            chunks.append([])
+            size = 0
+        chunks[-1].append((nm, b))
+        size += len(b)
+    lines = [f"v1,{max_chunk},{len(chunks)}"]
+    for ci, chunk in enumerate(chunks):
+        pos = 0
+        with open(os.path.join(out_dir, f"{ci:05d}.smoosh"), "wb") as f:
+            for nm, b in chunk:
+                f.write(b)
+                lines.append(f"{nm},{ci},{pos},{pos + len(b)}")
+                pos += len(b)
+    with open(os.path.join(out_dir, "meta.smoosh"), "w") as f:
+        f.write("\n".join(lines) + "\n")

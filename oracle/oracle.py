@@ -1,0 +1,644 @@
+"""CPU oracle for the segment scan-and-aggregate path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's ``cpu_baseline`` leg may import this module;
+it is the parity checker, never part of the product path.
+
+It restates the reference engines on top of ``libdruid_oracle.so`` (druid_oracle.c: segment
+decoding, Concise/Roaring iteration, Java-semantics aggregation loops in cursor order):
+
+* cursors & buckets: QueryableIndexStorageAdapter.makeCursors / CursorSequenceBuilder.build
+  (processing/.../segment/QueryableIndexStorageAdapter.java:190-316, 367-456)
+* bitmap filters: SelectorFilter.java:47-50, InFilter.java:72-137, BoundFilter.java:67-89,141-195,
+  249-275, AndFilter.java:64-88, OrFilter.java:56-68, NotFilter.java:44-50, missing-column
+  semantics ColumnSelectorBitmapIndexSelector.java:205-226
+* timeseries: TimeseriesQueryEngine.java:57-111 + TimeseriesBinaryFn.java:55-81
+* topN: PooledTopNAlgorithm (aggregate per dictionary id, emit touched ids in id order,
+  PooledTopNAlgorithm.java:661-754) -> TopNNumericResultBuilder (TopNNumericResultBuilder.java:94-235)
+  with the per-segment threshold max(threshold, minTopNThreshold)
+  (TopNQueryQueryToolChest.java:553-561), merged by TopNBinaryFn (TopNBinaryFn.java:75-135)
+* groupBy v2: per-segment grouping on dictionary ids (GroupByQueryEngineV2.java:413-475),
+  merged by value (GroupByMergingQueryRunnerV2.java:170-290), rows ordered by timestamp then
+  dimension values (lexicographic, nulls first).
+
+Parity pinning: tests/test_oracle.py checks this oracle against the reference's own committed
+segment (processing/src/test/resources/v8SegmentPersistDir, copied to tests/golden/) and
+the known-answer tests transcribed from the reference's unit tests (tests/golden/*.json).
+"""
+from __future__ import annotations
+
+import ctypes
+import heapq
+import importlib
+import math
+import os
+import sys
+from decimal import Decimal, InvalidOperation
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_REPO = os.path.dirname(_HERE)
+if _REPO not in sys.path:
+    sys.path.insert(0, _REPO)
+Q = importlib.import_module("incubator-druid_amd.query")
+
+OR_MISSING, OR_LONG, OR_FLOAT, OR_DOUBLE, OR_STRING, OR_UNSUPPORTED = range(6)
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "libdruid_oracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/libdruid_oracle.so missing: run `make -C oracle`")
+        l = ctypes.CDLL(path)
+        vp, i64, i32, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_char_p
+        l.or_open.restype = vp
+        l.or_open.argtypes = [cp, ctypes.c_char_p, ctypes.c_int]
+        l.or_close.argtypes = [vp]
+        l.or_num_rows.restype = i64
+        l.or_num_rows.argtypes = [vp]
+        l.or_interval.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        l.or_bitmap_roaring.argtypes = [vp]
+        l.or_num_columns.argtypes = [vp]
+        l.or_column_name.restype = cp
+        l.or_column_name.argtypes = [vp, ctypes.c_int]
+        l.or_column_kind.argtypes = [vp, cp]
+        l.or_read_column.argtypes = [vp, cp, ctypes.c_int, vp]
+        l.or_dim_cardinality.restype = i32
+        l.or_dim_cardinality.argtypes = [vp, cp]
+        l.or_dim_value.restype = i32
+        l.or_dim_value.argtypes = [vp, cp, i32, ctypes.POINTER(ctypes.c_void_p)]
+        l.or_dim_ids.argtypes = [vp, cp, vp]
+        l.or_dim_bitmap.restype = i64
+        l.or_dim_bitmap.argtypes = [vp, cp, i32, vp, i64]
+        l.or_agg_init.argtypes = [ctypes.c_int, i32, vp]
+        l.or_agg_apply.argtypes = [ctypes.c_int, i64, vp, vp, vp, vp]
+        l.or_agg_combine.argtypes = [ctypes.c_int, i32, vp, vp]
+        l.or_lz4_decompress.restype = i64
+        l.or_lz4_decompress.argtypes = [vp, i64, vp, i64]
+        l.or_concise_decode.restype = i64
+        l.or_concise_decode.argtypes = [vp, i64, vp, i64]
+        l.or_roaring_decode.restype = i64
+        l.or_roaring_decode.argtypes = [vp, i64, vp, i64]
+        _lib = l
+    return _lib
+
+
+def lz4_decompress(data: bytes, cap: int = 65536 + 16) -> bytes:
+    src = np.frombuffer(data, dtype=np.uint8)
+    dst = np.zeros(cap, dtype=np.uint8)
+    n = lib().or_lz4_decompress(src.ctypes.data, len(src), dst.ctypes.data, cap)
+    if n < 0:
+        raise ValueError("corrupt LZ4 block")
+    return dst[:n].tobytes()
+
+
+def concise_rows(be_bytes: bytes) -> np.ndarray:
+    src = np.frombuffer(be_bytes, dtype=np.uint8)
+    n = lib().or_concise_decode(src.ctypes.data, len(src), None, 0)
+    out = np.empty(max(n, 1), dtype=np.int32)
+    lib().or_concise_decode(src.ctypes.data, len(src), out.ctypes.data, n)
+    return out[:n]
+
+
+def roaring_rows(data: bytes) -> np.ndarray:
+    src = np.frombuffer(data, dtype=np.uint8)
+    n = lib().or_roaring_decode(src.ctypes.data, len(src), None, 0)
+    if n < 0:
+        raise ValueError("corrupt roaring bitmap")
+    out = np.empty(max(n, 1), dtype=np.int32)
+    lib().or_roaring_decode(src.ctypes.data, len(src), out.ctypes.data, n)
+    return out[:n]
+
+
+_NP_STATE = {"long": np.int64, "double": np.float64, "float": np.float32}
+_READ_KIND = {"long": OR_LONG, "double": OR_DOUBLE, "float": OR_FLOAT}
+
+
+class OracleSegment:
+    """A v9 segment decoded on the CPU (QueryableIndex restated)."""
+
+    def __init__(self, path: str):
+        err = ctypes.create_string_buffer(512)
+        h = lib().or_open(path.encode(), err, 512)
+        if not h:
+            raise IOError(err.value.decode())
+        self._h = h
+        self.path = path
+        self.num_rows = int(lib().or_num_rows(h))
+        s, e = ctypes.c_int64(), ctypes.c_int64()
+        lib().or_interval(h, ctypes.byref(s), ctypes.byref(e))
+        self.interval = (s.value, e.value)
+        self._cache: Dict = {}
+
+    def close(self):
+        if self._h:
+            lib().or_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def column_kind(self, name: str) -> int:
+        return lib().or_column_kind(self._h, name.encode())
+
+    def columns(self) -> List[str]:
+        return [lib().or_column_name(self._h, i).decode() for i in range(lib().or_num_columns(self._h))]
+
+    def numeric(self, name: str, as_type: str) -> np.ndarray:
+        key = ("num", name, as_type)
+        if key not in self._cache:
+            out = np.zeros(self.num_rows, dtype=_NP_STATE[as_type])
+            rc = lib().or_read_column(self._h, name.encode(), _READ_KIND[as_type], out.ctypes.data)
+            if rc < 0:
+                raise ValueError(f"cannot decode column {name}")
+            self._cache[key] = out
+        return self._cache[key]
+
+    def time(self) -> np.ndarray:
+        return self.numeric("__time", "long")
+
+    def cardinality(self, dim: str) -> int:
+        return int(lib().or_dim_cardinality(self._h, dim.encode()))
+
+    def dictionary(self, dim: str) -> List[Optional[str]]:
+        key = ("dict", dim)
+        if key not in self._cache:
+            card = self.cardinality(dim)
+            vals = []
+            p = ctypes.c_void_p()
+            for i in range(card):
+                n = lib().or_dim_value(self._h, dim.encode(), i, ctypes.byref(p))
+                vals.append(None if n <= 0 else ctypes.string_at(p.value, n).decode("utf-8"))
+            self._cache[key] = vals
+        return self._cache[key]
+
+    def ids(self, dim: str) -> np.ndarray:
+        key = ("ids", dim)
+        if key not in self._cache:
+            out = np.empty(self.num_rows, dtype=np.int32)
+            if lib().or_dim_ids(self._h, dim.encode(), out.ctypes.data) != 0:
+                raise ValueError(f"cannot decode ids of {dim}")
+            self._cache[key] = out
+        return self._cache[key]
+
+    def bitmap_rows(self, dim: str, idx: int) -> np.ndarray:
+        n = lib().or_dim_bitmap(self._h, dim.encode(), idx, None, 0)
+        if n < 0:
+            raise ValueError("bad bitmap")
+        out = np.empty(max(n, 1), dtype=np.int32)
+        lib().or_dim_bitmap(self._h, dim.encode(), idx, out.ctypes.data, n)
+        return out[:n]
+
+    def is_dim(self, dim: str) -> bool:
+        return self.column_kind(dim) == OR_STRING
+
+
+# ----------------------------------------------------------------------------------------------
+# dictionary search & filters
+# ----------------------------------------------------------------------------------------------
+def _jkey(s: Optional[str]):
+    return (0, b"") if s is None else (1, s.encode("utf-16-be", "surrogatepass"))
+
+
+def index_of(dictionary: Sequence[Optional[str]], value: Optional[str]) -> int:
+    """GenericIndexed.indexOf (GenericIndexed.java:308-333): binary search, naturalNullsFirst."""
+    lo, hi = 0, len(dictionary) - 1
+    k = _jkey(value)
+    while lo <= hi:
+        mid = (lo + hi) >> 1
+        c = _jkey(dictionary[mid])
+        if c == k:
+            return mid
+        if c < k:
+            lo = mid + 1
+        else:
+            hi = mid - 1
+    return -(lo + 1)
+
+
+def _try_long(s: str):
+    try:
+        if s.strip() != s or s == "":
+            return None
+        v = int(s, 10)
+        return v if -(1 << 63) <= v < (1 << 63) else None
+    except ValueError:
+        return None
+
+
+def numeric_compare(a: Optional[str], b: Optional[str]) -> int:
+    """StringComparators.NumericComparator (query/ordering/StringComparators.java:346-392)."""
+    if a == b:
+        return 0
+    if a is None:
+        return -1
+    if b is None:
+        return 1
+    la, lb = _try_long(a), _try_long(b)
+    if la is not None and lb is not None:
+        return (la > lb) - (la < lb)
+
+    def dec(s, l):
+        if l is not None:
+            return Decimal(l)
+        try:
+            return Decimal(s)
+        except InvalidOperation:
+            return None
+
+    da, db = dec(a, la), dec(b, lb)
+    if da is not None and db is not None:
+        return (da > db) - (da < db)
+    if da is None and db is None:
+        ka, kb = _jkey(a), _jkey(b)
+        return (ka > kb) - (ka < kb)
+    return -1 if da is None else 1
+
+
+def _lex_compare(a, b):
+    ka, kb = _jkey(a), _jkey(b)
+    return (ka > kb) - (ka < kb)
+
+
+def _bound_matches(f, value: Optional[str]) -> bool:
+    """BoundFilter.doesMatch (BoundFilter.java:249-275) in default null mode."""
+    lower = Q._empty_to_null(f.lower)
+    upper = Q._empty_to_null(f.upper)
+    has_lower, has_upper = f.lower is not None, f.upper is not None
+    if value is None:
+        return ((not has_lower) or (lower is None and not f.lowerStrict)) and \
+               ((not has_upper) or upper is not None or not f.upperStrict)
+    cmp = numeric_compare if f.ordering == "numeric" else _lex_compare
+    lc = cmp(value, f.lower) if has_lower else 1
+    uc = cmp(f.upper, value) if has_upper else 1
+    if f.lowerStrict and f.upperStrict:
+        return lc > 0 and uc > 0
+    if f.lowerStrict:
+        return lc > 0 and uc >= 0
+    if f.upperStrict:
+        return lc >= 0 and uc > 0
+    return lc >= 0 and uc >= 0
+
+
+def filter_id_set(seg: OracleSegment, f) -> Optional[List[int]]:
+    """Dictionary ids selected by a leaf filter; None means 'dimension missing' handled by caller."""
+    dictionary = seg.dictionary(f.dimension)
+    if isinstance(f, Q.SelectorDimFilter):
+        i = index_of(dictionary, Q._empty_to_null(f.value))
+        return [i] if i >= 0 else []
+    if isinstance(f, Q.InDimFilter):
+        ids = set()
+        for v in f.values:
+            i = index_of(dictionary, Q._empty_to_null(v))
+            if i >= 0:
+                ids.add(i)
+        return sorted(ids)
+    if isinstance(f, Q.BoundDimFilter):
+        if f.ordering == "lexicographic":
+            card = len(dictionary)
+            if f.lower is None:
+                start = 0
+            else:
+                found = index_of(dictionary, Q._empty_to_null(f.lower))
+                start = (found + 1 if f.lowerStrict else found) if found >= 0 else -(found + 1)
+            if f.upper is None:
+                end = card
+            else:
+                found = index_of(dictionary, Q._empty_to_null(f.upper))
+                end = (found if f.upperStrict else found + 1) if found >= 0 else -(found + 1)
+            end = max(start, end)
+            return list(range(start, end))
+        if f.ordering != "numeric":
+            raise NotImplementedError(f"bound ordering {f.ordering}")
+        return [i for i, v in enumerate(dictionary) if _bound_matches(f, v)]
+    raise TypeError(f)
+
+
+def _leaf_matches_null(f) -> bool:
+    if isinstance(f, Q.SelectorDimFilter):
+        return Q._empty_to_null(f.value) is None
+    if isinstance(f, Q.InDimFilter):
+        return any(Q._empty_to_null(v) is None for v in f.values)
+    if isinstance(f, Q.BoundDimFilter):
+        return _bound_matches(f, None)
+    raise TypeError(f)
+
+
+def filter_mask(seg: OracleSegment, f) -> np.ndarray:
+    n = seg.num_rows
+    if f is None:
+        return np.ones(n, dtype=bool)
+    if isinstance(f, Q.AndDimFilter):
+        m = np.ones(n, dtype=bool)
+        for c in f.fields:
+            m &= filter_mask(seg, c)
+        return m
+    if isinstance(f, Q.OrDimFilter):
+        m = np.zeros(n, dtype=bool)
+        for c in f.fields:
+            m |= filter_mask(seg, c)
+        return m
+    if isinstance(f, Q.NotDimFilter):
+        return ~filter_mask(seg, f.field)
+    if not seg.is_dim(f.dimension):
+        # missing column: allTrue iff the filter matches null (ColumnSelectorBitmapIndexSelector:212-218)
+        return np.full(n, _leaf_matches_null(f), dtype=bool)
+    m = np.zeros(n, dtype=bool)
+    for i in filter_id_set(seg, f):
+        m[seg.bitmap_rows(f.dimension, i)] = True
+    return m
+
+
+# ----------------------------------------------------------------------------------------------
+# cursors / buckets
+# ----------------------------------------------------------------------------------------------
+def cursor_buckets(seg: OracleSegment, query) -> List[Tuple[int, int, int]]:
+    """(bucket_time, row_start, row_end) per cursor, makeCursors + CursorSequenceBuilder.build."""
+    if seg.num_rows == 0:
+        return []
+    t = seg.time()
+    gran = query.granularity
+    min_t, max_t = int(t[0]), int(t[-1])
+    data = (min_t, gran.bucket_end(max_t))
+    qs, qe = query.interval
+    if not (qs < data[1] and data[0] < qe):
+        return []
+    actual = (max(qs, data[0]), min(qe, data[1]))
+    out = []
+    for bs, be in gran.iterable(actual):
+        ts = max(actual[0], bs)
+        te = min(actual[1], gran.increment(bs))
+        r0 = int(np.searchsorted(t, ts, side="left"))
+        r1 = int(np.searchsorted(t, te, side="left"))
+        out.append((bs if not gran.is_all else actual[0], r0, max(r0, r1)))
+    return out
+
+
+def _agg_input(seg: OracleSegment, agg) -> Optional[np.ndarray]:
+    if agg.kind == 0:
+        return None
+    return seg.numeric(agg.fieldName, agg.output_type)
+
+
+def aggregate_groups(seg: OracleSegment, aggs, rows: np.ndarray, groups: np.ndarray, ngroups: int) -> List[np.ndarray]:
+    """Sequential per-group aggregation in row order (Aggregator.aggregate per cursor row)."""
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    groups = np.ascontiguousarray(groups, dtype=np.int32)
+    states = []
+    for a in aggs:
+        st = np.zeros(max(ngroups, 1), dtype=_NP_STATE[a.output_type])
+        lib().or_agg_init(a.kind, ngroups, st.ctypes.data)
+        vals = _agg_input(seg, a)
+        lib().or_agg_apply(a.kind, len(rows), rows.ctypes.data, groups.ctypes.data,
+                           None if vals is None else vals.ctypes.data, st.ctypes.data)
+        states.append(st[:ngroups])
+    return states
+
+
+def _py(v, out_type):
+    if out_type == "long":
+        return int(v)
+    return float(v)
+
+
+# ----------------------------------------------------------------------------------------------
+# timeseries
+# ----------------------------------------------------------------------------------------------
+def timeseries_segment(seg: OracleSegment, query) -> List:
+    mask = filter_mask(seg, query.effective_filter())
+    results = []
+    for bt, r0, r1 in cursor_buckets(seg, query):
+        rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
+        if query.skip_empty_buckets and len(rows) == 0:
+            continue
+        states = aggregate_groups(seg, query.aggregations, rows, np.zeros(len(rows), np.int32), 1)
+        results.append(Q.Result(bt, {a.name: _py(s[0], a.output_type) for a, s in zip(query.aggregations, states)}))
+    return results
+
+
+def merge_timeseries(query, per_segment: List[List]) -> List:
+    gran = query.granularity
+    merged: Dict[int, Q.Result] = {}
+    order = []
+    flat = sorted(((r.timestamp, si, k, r) for si, rs in enumerate(per_segment) for k, r in enumerate(rs)),
+                  key=lambda x: (x[0], x[1], x[2]))
+    for ts, _, _, r in flat:
+        key = 0 if gran.is_all else gran.bucket_start(ts)
+        if key not in merged:
+            merged[key] = Q.Result(r.timestamp if gran.is_all else key, dict(r.value))
+            order.append(key)
+        else:
+            acc = merged[key].value
+            for a in query.aggregations:
+                acc[a.name] = a.combine(acc[a.name], r.value[a.name])
+    out = [merged[k] for k in sorted(order)]
+    if getattr(query, "descending", False):
+        out.reverse()
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# topN
+# ----------------------------------------------------------------------------------------------
+class _Key:
+    """(metric, dimValue) ordering of TopNNumericResultBuilder's dimValHolderComparator."""
+    __slots__ = ("m", "d")
+
+    def __init__(self, m, d):
+        self.m, self.d = m, d
+
+    def __lt__(self, o):
+        if self.m != o.m:
+            return self.m < o.m
+        return _jkey(self.d) < _jkey(o.d)
+
+
+class NumericResultBuilder:
+    """TopNNumericResultBuilder: PriorityQueue(threshold+1), shouldAdd / poll semantics."""
+
+    def __init__(self, metric_key, threshold: int):
+        self.metric_key = metric_key
+        self.threshold = threshold
+        self.heap: List = []
+        self.seq = 0
+
+    def add(self, dim_value, metric_value, values: Dict):
+        mk = self.metric_key(metric_value)
+        below = len(self.heap) < self.threshold or (self.heap and self.heap[0][0].m < mk)
+        if below:
+            heapq.heappush(self.heap, (_Key(mk, dim_value), self.seq, dim_value, values))
+            self.seq += 1
+        if len(self.heap) > self.threshold:
+            heapq.heappop(self.heap)
+
+    def build(self) -> List[Dict]:
+        items = sorted(self.heap, key=lambda x: x[0])
+        # metric descending, ties by dim value ascending
+        items.sort(key=lambda x: (_Neg(x[0].m), _jkey(x[2])))
+        return [x[3] for x in items]
+
+
+class _Neg:
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+    def __lt__(self, o):
+        return o.v < self.v
+
+    def __eq__(self, o):
+        return self.v == o.v
+
+
+def _metric_key_fn(query):
+    spec = query.metric
+    agg = next(a for a in query.aggregations if a.name == spec.metric)
+    if spec.type == "inverted":
+        return lambda v: _Neg(agg.compare_key(v))
+    return agg.compare_key
+
+
+def topn_segment(seg: OracleSegment, query) -> List:
+    if query.metric.type == "dimension":
+        raise NotImplementedError("dimension-ordered topN")
+    mask = filter_mask(seg, query.effective_filter())
+    out = []
+    dim_present = seg.is_dim(query.dimension)
+    dictionary = seg.dictionary(query.dimension) if dim_present else [None]
+    ids_all = seg.ids(query.dimension) if dim_present else np.zeros(seg.num_rows, np.int32)
+    for bt, r0, r1 in cursor_buckets(seg, query):
+        rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
+        card = len(dictionary)
+        gids = ids_all[rows]
+        states = aggregate_groups(seg, query.aggregations, rows, gids, card)
+        touched = np.zeros(card, dtype=bool)
+        touched[gids] = True
+        bob = NumericResultBuilder(_metric_key_fn(query), query.segment_threshold)
+        for i in np.nonzero(touched)[0]:
+            vals = {query.dimension: dictionary[i]}
+            for a, s in zip(query.aggregations, states):
+                vals[a.name] = _py(s[i], a.output_type)
+            bob.add(dictionary[i], vals[query.metric.metric], vals)
+        out.append(Q.Result(bt, bob.build()))
+    return out
+
+
+def topn_binary_fn(query, r1, r2):
+    """TopNBinaryFn.apply (TopNBinaryFn.java:75-135) with the query's own threshold."""
+    if r1 is None:
+        return r2
+    if r2 is None:
+        return r1
+    dim = query.dimension
+    ret: Dict = {}
+    for v in r1.value:
+        ret[v[dim]] = v
+    for v in r2.value:
+        k = v[dim]
+        if k in ret:
+            a = ret[k]
+            c = {dim: k}
+            for agg in query.aggregations:
+                c[agg.name] = agg.combine(a[agg.name], v[agg.name])
+            ret[k] = c
+        else:
+            ret[k] = v
+    bob = NumericResultBuilder(_metric_key_fn(query), query.threshold)
+    for v in ret.values():
+        bob.add(v[dim], v[query.metric.metric], v)
+    ts = r1.timestamp if query.granularity.is_all else query.granularity.bucket_start(r1.timestamp)
+    return Q.Result(ts, bob.build())
+
+
+def merge_topn(query, per_segment: List[List]) -> List:
+    gran = query.granularity
+    flat = sorted(((r.timestamp, si, r) for si, rs in enumerate(per_segment) for r in rs), key=lambda x: (x[0], x[1]))
+    merged: Dict[int, Q.Result] = {}
+    for ts, _, r in flat:
+        key = 0 if gran.is_all else gran.bucket_start(ts)
+        merged[key] = topn_binary_fn(query, merged.get(key), r)
+    out = []
+    for k in sorted(merged):
+        r = merged[k]
+        # final truncation to the query threshold (Iterables.limit in the toolchest)
+        out.append(Q.Result(r.timestamp, r.value[:query.threshold]))
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# groupBy (v2)
+# ----------------------------------------------------------------------------------------------
+def groupby_segment(seg: OracleSegment, query) -> List[Tuple[int, Tuple, Dict]]:
+    mask = filter_mask(seg, query.effective_filter())
+    dims = query.dimensions
+    dicts, idcols = [], []
+    for d in dims:
+        if seg.is_dim(d):
+            dicts.append(seg.dictionary(d))
+            idcols.append(seg.ids(d).astype(np.int64))
+        else:
+            dicts.append([None])
+            idcols.append(np.zeros(seg.num_rows, np.int64))
+    out = []
+    for bt, r0, r1 in cursor_buckets(seg, query):
+        rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
+        if len(rows) == 0:
+            continue
+        key = np.zeros(len(rows), dtype=np.int64)
+        for d, col in zip(dicts, idcols):
+            key = key * len(d) + col[rows]
+        uniq, inv = np.unique(key, return_inverse=True)
+        states = aggregate_groups(seg, query.aggregations, rows, inv.astype(np.int32), len(uniq))
+        for g, k in enumerate(uniq):
+            vals = []
+            kk = int(k)
+            for d in reversed(dicts):
+                vals.append(d[kk % len(d)])
+                kk //= len(d)
+            vals.reverse()
+            aggs = {a.name: _py(s[g], a.output_type) for a, s in zip(query.aggregations, states)}
+            out.append((bt, tuple(vals), aggs))
+    return out
+
+
+def merge_groupby(query, per_segment: List[List]) -> List:
+    gran = query.granularity
+    merged: Dict = {}
+    for rows in per_segment:
+        for bt, vals, aggs in rows:
+            key = (0 if gran.is_all else gran.bucket_start(bt), vals)
+            if key not in merged:
+                merged[key] = (bt, dict(aggs))
+            else:
+                t0, acc = merged[key]
+                for a in query.aggregations:
+                    acc[a.name] = a.combine(acc[a.name], aggs[a.name])
+                merged[key] = (min(t0, bt), acc)
+    out = []
+    for (k, vals), (bt, aggs) in merged.items():
+        ev = {d: v for d, v in zip(query.dimensions, vals)}
+        ev.update(aggs)
+        out.append(Q.Row(bt if gran.is_all else k, ev))
+    out.sort(key=lambda r: (r.timestamp, tuple(_jkey(r.event[d]) for d in query.dimensions)))
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# entry point
+# ----------------------------------------------------------------------------------------------
+def run(query, segments: Sequence[OracleSegment]):
+    if isinstance(query, Q.TimeseriesQuery):
+        return merge_timeseries(query, [timeseries_segment(s, query) for s in segments])
+    if isinstance(query, Q.TopNQuery):
+        return merge_topn(query, [topn_segment(s, query) for s in segments])
+    if isinstance(query, Q.GroupByQuery):
+        return merge_groupby(query, [groupby_segment(s, query) for s in segments])
+    raise TypeError(query)
