@@ -1181,18 +1181,22 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   const int metric_op = (slot_op(mk) << 8) | mk;
   std::vector<int32_t*> d_cand(n, nullptr);
   int32_t* d_ncand = dev_take<int32_t>(cs, n);
-  uint64_t* d_state = dev_take<uint64_t>(cs, n);
+  uint64_t* d_state = dev_take<uint64_t>(cs, 2 * (size_t)n);
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
     d_cand[i] = dev_take<int32_t>(cs, (size_t)card[i]);
-    launch_topn_select(jobs[i].out, card[i], na, t->metric_agg, metric_op, t->inverted, t->threshold, d_state + i,
+    launch_topn_select(jobs[i].out, card[i], na, t->metric_agg, metric_op, t->inverted, t->threshold, d_state + 2 * i,
                        d_cand[i], d_ncand + i, (int)card[i], st);
   }
   hipEventRecord(ctx->ev[4], st);
   int32_t* h_ncand = host_take<int32_t>(cs, n);
+  uint64_t* h_state = host_take<uint64_t>(cs, 2 * (size_t)n);
   DG_HIP(hipMemcpyAsync(h_ncand, d_ncand, 4 * n, hipMemcpyDeviceToHost, st));
+  DG_HIP(hipMemcpyAsync(h_state, d_state, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
   DG_HIP(hipStreamSynchronize(st));
   DG_HIP(hipGetLastError());
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) m.selected_rows += (int64_t)h_state[2 * i + 1];
   // fetch candidate ids and their records (small: threshold + ties)
   std::vector<int32_t*> h_cand(n, nullptr);
   std::vector<uint64_t*> h_tab(n, nullptr);
@@ -1231,7 +1235,6 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     std::priority_queue<E, std::vector<E>, decltype(gt)> pq(gt);  // min-heap on (key, id)
     for (int k = 0; k < nc; ++k) {
       E e{metric_key_host(h_tab[i][(size_t)k * rec + 1 + t->metric_agg], mk, t->inverted), h_cand[i][k], k};
-      m.selected_rows += 0;
       if ((int)pq.size() < t->threshold || pq.top().key < e.key) pq.push(e);
       if ((int)pq.size() > t->threshold) pq.pop();
     }

@@ -16,7 +16,7 @@
 
 namespace dg {
 
-constexpr int kMaxAggs = 8;
+constexpr int kMaxAggs = 16;
 constexpr int kBlockBytes = 65536;  // CompressedPools.BUFFER_SIZE (segment/CompressedPools.java:39)
 
 // stored codecs (CompressionStrategy ids, data/CompressionStrategy.java:48-107)

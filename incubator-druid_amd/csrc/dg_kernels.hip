@@ -657,12 +657,25 @@ __global__ __launch_bounds__(1024) void k_topn_select(const uint64_t* __restrict
     s_touched = 0;
   }
   __syncthreads();
-  // count touched
+  // count touched ids and aggregated rows
+  __shared__ unsigned long long s_rows;
+  if (threadIdx.x == 0) s_rows = 0;
+  __syncthreads();
   {
-    unsigned long long c = 0;
-    for (int64_t i = threadIdx.x; i < card; i += blockDim.x) c += table[i * rec] != 0;
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&s_touched), c);
+    unsigned long long c = 0, rows = 0;
+    for (int64_t i = threadIdx.x; i < card; i += blockDim.x) {
+      const uint64_t n = table[i * rec];
+      c += n != 0;
+      rows += n;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      c += __shfl_down(c, o, 64);
+      rows += __shfl_down(rows, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&s_touched), c);
+      atomicAdd(&s_rows, rows);
+    }
   }
   __syncthreads();
   uint64_t kth = 0;  // keep everything when touched <= threshold
@@ -721,6 +734,7 @@ __global__ __launch_bounds__(1024) void k_topn_select(const uint64_t* __restrict
   if (threadIdx.x == 0) {
     *ncand = (int32_t)(base < 0x7fffffff ? base : 0x7fffffff);
     state[0] = kth;
+    state[1] = s_rows;
   }
 }
 
