@@ -145,111 +145,6 @@ __device__ int64_t block_exclusive_scan(int64_t v, int64_t* total, int64_t* s_tm
   return wave_off + x - v;
 }
 
-// ------------------------------------------------------------------------------------------------
-// LZ4 block decode: one wave per block, compressed input and decoded output staged in LDS.
-// Tokens are parsed in order (the format is sequential); literal and match copies are spread over
-// the 64 lanes. Overlapping matches (offset < length) use the periodic form
-// out[op + k] = out[op - off + k % off], which only reads bytes before op, so the lanes never race.
-// ------------------------------------------------------------------------------------------------
-constexpr int kLz4InCap = kBlockBytes + 2048;
-
-__global__ __launch_bounds__(64) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap];
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[kBlockBytes + 64];
-  const Lz4Job job = jobs[blockIdx.x];
-  const int lane = threadIdx.x;
-  const int iend = job.src_len;
-  if (iend <= 0 || iend > kLz4InCap) {
-    if (lane == 0) atomicOr(err, 1);
-    return;
-  }
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(job.src);
-    uint4* dst = reinterpret_cast<uint4*>(s_in);
-    const int n16 = (iend + 15) >> 4;
-    for (int i = lane; i < n16; i += 64) dst[i] = src[i];
-  }
-  __syncthreads();
-  int ip = 0, op = 0;
-  bool bad = false;
-  for (;;) {
-    if (ip >= iend) {
-      bad = true;
-      break;
-    }
-    const int tok = __builtin_amdgcn_readfirstlane(s_in[ip]);
-    ip++;
-    int lit = tok >> 4;
-    if (lit == 15) {
-      int b;
-      do {
-        if (ip >= iend) {
-          bad = true;
-          break;
-        }
-        b = __builtin_amdgcn_readfirstlane(s_in[ip]);
-        ip++;
-        lit += b;
-      } while (b == 255);
-      if (bad) break;
-    }
-    if (lit > iend - ip || lit > kBlockBytes - op) {
-      bad = true;
-      break;
-    }
-    for (int k = lane; k < lit; k += 64) s_out[op + k] = s_in[ip + k];
-    ip += lit;
-    op += lit;
-    if (ip == iend) break;  // last sequence: literals only
-    if (iend - ip < 2) {
-      bad = true;
-      break;
-    }
-    const int off = __builtin_amdgcn_readfirstlane((int)s_in[ip] | ((int)s_in[ip + 1] << 8));
-    ip += 2;
-    int ml = tok & 15;
-    if (ml == 15) {
-      int b;
-      do {
-        if (ip >= iend) {
-          bad = true;
-          break;
-        }
-        b = __builtin_amdgcn_readfirstlane(s_in[ip]);
-        ip++;
-        ml += b;
-      } while (b == 255);
-      if (bad) break;
-    }
-    ml += 4;
-    if (off == 0 || off > op || ml > kBlockBytes - op) {
-      bad = true;
-      break;
-    }
-    __syncthreads();
-    if (off >= ml) {
-      for (int k = lane; k < ml; k += 64) s_out[op + k] = s_out[op - off + k];
-    } else {
-      for (int k = lane; k < ml; k += 64) s_out[op + k] = s_out[op - off + (k % off)];
-    }
-    op += ml;
-    __syncthreads();
-  }
-  __syncthreads();
-  if (bad || op < job.expect_len) {
-    if (lane == 0) atomicOr(err, 1);
-    return;
-  }
-  uint4* dst = reinterpret_cast<uint4*>(job.dst);
-  const uint4* src = reinterpret_cast<const uint4*>(s_out);
-  const int n16 = (op + 15) >> 4;
-  for (int i = lane; i < n16; i += 64) dst[i] = src[i];
-}
-
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s) {
-  if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_lz4_decode, dim3(njobs), dim3(64), 0, s, d_jobs, d_err);
-}
 
 // ------------------------------------------------------------------------------------------------
 // Concise -> dense row bitset (OR). One workgroup per bitmap; 256 words per step: each thread

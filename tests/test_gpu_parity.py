@@ -187,3 +187,45 @@ def test_per_segment_runner_and_merge(R, Q, O, gpu_basic, oracle_basic):
     per = [f.createRunner(s).run(q) for s in gpu_basic[("concise", "lz4")]]
     merged = R.merge_timeseries(q, per)
     assert_results(q, merged, O.run(q, oracle_basic[("concise", "lz4")]))
+
+
+def _pattern_columns(n, rng):
+    """Long/double columns that stress every LZ4 token shape (long literal runs, offset-1 runs,
+    short periodic matches, token-dense sequences, incompressible data, mixtures)."""
+    seq = np.arange(n, dtype=np.int64)
+    spikes = np.zeros(n, dtype=np.int64)
+    spikes[rng.integers(0, n, n // 500)] = rng.integers(1, 1 << 40, n // 500)
+    mixed = np.where((seq // 3000) % 2 == 0, rng.integers(-(1 << 62), 1 << 62, n), seq % 7)
+    return {
+        "zeros": ("long", np.zeros(n, dtype=np.int64)),
+        "const": ("long", np.full(n, 0x0102030405060708, dtype=np.int64)),
+        "seq": ("long", seq % 10000),
+        "period3": ("long", seq % 3),
+        "random": ("long", rng.integers(-(1 << 62), 1 << 62, n)),
+        "spikes": ("long", spikes),
+        "mixed": ("long", mixed),
+        "dbl": ("double", rng.normal(5000.0, 1.0, n)),
+        "dblround": ("double", np.round(rng.normal(100.0, 10.0, n), 1)),
+    }
+
+
+@pytest.mark.parametrize("mode", ["hc", "fast"])
+def test_lz4_every_value_round_trips(R, Q, O, S, W, tmp_path, mode):
+    """Per-row buckets (1 ms granularity) make every decoded value visible: bit-exact vs the oracle."""
+    rng = np.random.default_rng(7)
+    n = 70_000  # > 8 blocks of longs, partial last block
+    metrics = _pattern_columns(n, rng)
+    spec = W.SegmentSpec(timestamps=np.arange(n, dtype=np.int64),
+                         dims={"d": W.encode_int_strings(rng.integers(0, 300, n))}, metrics=metrics)
+    p = W.write_segment(str(tmp_path / f"pat_{mode}"), spec, compression="lz4", lz4_mode=mode)
+    g, o = S.GpuSegment(p), O.OracleSegment(p)
+    aggs = [Q.long_sum(k, k) for k, (t, _) in metrics.items() if t == "long"] + \
+           [Q.double_max(k, k) for k, (t, _) in metrics.items() if t == "double"]
+    for chunk in range(0, len(aggs), 8):
+        q = Q.TimeseriesQuery(intervals=[(0, n)], granularity={"type": "duration", "duration": 1},
+                              aggregations=aggs[chunk:chunk + 8])
+        got, exp = R.run_query(q, [g]), O.run(q, [o])
+        assert len(got) == n
+        assert_results(q, got, exp)
+    q = Q.GroupByQuery(intervals=[(0, n)], dimensions=["d"], aggregations=[Q.count("rows"), Q.long_sum("seq")])
+    assert_results(q, R.run_query(q, [g]), O.run(q, [o]))
