@@ -497,10 +497,11 @@ static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   Lz4Job* d = dev_take<Lz4Job>(cs, n);
   int32_t* d_err = dev_take<int32_t>(cs, 1);
-  if (!h || !d || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
+  uint64_t* d_mtab = dev_take<uint64_t>(cs, (size_t)n * kLz4MatchTable);
+  if (!h || !d || !d_err || !d_mtab) return set_error(DG_ERR_OOM, "lz4 jobs");
   DG_HIP(hipMemcpyAsync(d, h, sizeof(Lz4Job) * n, hipMemcpyHostToDevice, st));
   DG_HIP(hipMemsetAsync(d_err, 0, 4, st));
-  launch_lz4_decode(d, n, d_err, st);
+  launch_lz4_decode(d, n, d_err, d_mtab, st);
   int32_t* h_err = host_take<int32_t>(cs, 1);
   DG_HIP(hipMemcpyAsync(h_err, d_err, 4, hipMemcpyDeviceToHost, st));
   DG_HIP(hipStreamSynchronize(st));
@@ -1483,3 +1484,39 @@ int dg_result_fetch_groups(dg_result* r, int32_t i, int64_t* t, int32_t* ids, ui
 void dg_result_release(dg_result* r) { delete r; }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// diagnostics (not part of the ABI header): per-block LZ4 phase timestamps of one column
+// ------------------------------------------------------------------------------------------------
+extern "C" int dg_debug_lz4_profile(dg_segment* s, const char* column, uint64_t* out, int32_t cap, int32_t* nblocks,
+                                    double* ms) {
+  Segment* seg = reinterpret_cast<Segment*>(s);
+  Column* c = seg ? seg->find(column ? column : "") : nullptr;
+  if (!c || c->data.codec != CODEC_LZ4) return set_error(DG_ERR_ARG, "not an LZ4 column");
+  CallGuard g(seg->ctx);
+  hipStream_t st = seg->ctx->stream;
+  DecodeBatch db;
+  ColView v;
+  int rc = column_view(c, g.cs, &db, &v, st);
+  if (rc) return rc;
+  const int n = (int)db.jobs.size();
+  *nblocks = n;
+  Lz4Job* h = host_take<Lz4Job>(g.cs, n);
+  memcpy(h, db.jobs.data(), sizeof(Lz4Job) * n);
+  Lz4Job* d = dev_take<Lz4Job>(g.cs, n);
+  int32_t* d_err = dev_take<int32_t>(g.cs, 1);
+  uint64_t* d_prof = dev_take<uint64_t>(g.cs, (size_t)n * 10);
+  uint64_t* d_mtab = dev_take<uint64_t>(g.cs, (size_t)n * kLz4MatchTable);
+  DG_HIP(hipMemcpyAsync(d, h, sizeof(Lz4Job) * n, hipMemcpyHostToDevice, st));
+  DG_HIP(hipMemsetAsync(d_err, 0, 4, st));
+  DG_HIP(hipMemsetAsync(d_prof, 0, (size_t)n * 80, st));
+  hipEventRecord(seg->ctx->ev[0], st);
+  launch_lz4_decode(d, n, d_err, d_mtab, st, d_prof);
+  hipEventRecord(seg->ctx->ev[1], st);
+  DG_HIP(hipStreamSynchronize(st));
+  float f = 0;
+  hipEventElapsedTime(&f, seg->ctx->ev[0], seg->ctx->ev[1]);
+  *ms = f;
+  DG_HIP(hipMemcpy(out, d_prof, (size_t)std::min(cap, n) * 80, hipMemcpyDeviceToHost));
+  return DG_OK;
+}

@@ -173,7 +173,10 @@ int set_error(int code, const char* fmt, ...);
 int load_segment(Context* ctx, const char* dir, Segment** out);
 
 // kernel launchers (dg_kernels.hip)
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
+// d_mtab: njobs * kLz4MatchTable scratch words (per-block match table of the parallel decoder)
+constexpr size_t kLz4MatchTable = kBlockBytes / 4;
+void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, uint64_t* d_mtab, hipStream_t s,
+                       uint64_t* d_prof = nullptr);
 void launch_concise_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
                        int nbitmaps, uint32_t* const* d_sets, int64_t limit_bits, hipStream_t s);
 void launch_roaring_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,

@@ -2,22 +2,27 @@
 //
 // Replaces CompressionStrategy.LZ4Decompressor.decompress (processing/.../segment/data/
 // CompressionStrategy.java:284-305 -> lz4-java 1.4.0 LZ4SafeDecompressor): one 64 KiB Druid block
-// (CompressedPools.BUFFER_SIZE) per workgroup, compressed input and decoded output both in LDS.
+// (CompressedPools.BUFFER_SIZE) per 256-thread workgroup, compressed input and decoded output in LDS.
 //
-// LZ4's token stream is sequential (a token's position depends on every earlier token) and Druid's
-// numeric blocks are token-dense (~8k tokens / block for sequential longs), so one lane walking the
-// stream is latency-bound (measured: ~2 ms per block). This kernel parses speculatively in parallel:
-//   1. the compressed block is cut into 256 chunks; thread i walks the token chain from the start of
-//      chunk i as if a token started there, marking the positions it visits (LDS bitmap);
-//   2. the true chain enters chunk i at the exit of chunk i-1; walking from there, it meets the
-//      speculative chain within a few tokens (chains are functions of position, so they merge) —
-//      checked in parallel, with a wave-level fix-up where an entry guess was wrong (long tokens);
-//   3. each thread re-walks its chunk's true tokens: output sizes -> block scan -> output offsets;
-//   4. literals are copied (long runs cooperatively);
-//   5. matches are resolved in rounds: a match runs once every byte it copies from is final
-//      (per-chunk "done" frontiers); matches longer than kLongMatch are copied by the whole block.
-// The sequential one-wave decoder is kept (k_lz4_decode_seq) as a differential reference and
-// selected with DG_LZ4_SEQ=1.
+// LZ4's token stream is sequential and Druid's numeric blocks are token-dense: a block of sequential
+// longs is ~8k tokens of [1 literal byte, 7-byte match at offset 8], i.e. ONE dependency chain
+// through the whole block (every match copies bytes the previous match produced). Neither a lane
+// walking the stream (~2 ms/block measured) nor match-by-match rounds (one round per chunk) scale.
+// This kernel decodes in five data-parallel phases:
+//   1. parse, speculatively: the compressed block is cut into 256 chunks; thread i walks the token
+//      chain from the start of its chunk as if a token started there, marking visited positions;
+//   2. the true chain enters chunk i at the exit of chunk i-1 and meets the speculative chain within
+//      a few tokens (chains are functions of position, so they merge): exits are computed in
+//      parallel for the assumed entry and for the likely correction, wave 0 stitches them together;
+//   3. each chunk's true tokens give output sizes and match counts -> block scans -> offsets;
+//   4. literals are copied into the output (long runs cooperatively) and every match is recorded
+//      as (output offset, distance, length) in a per-block table in global memory;
+//   5. matches are resolved by pointer jumping instead of by copying in order: for each output
+//      byte, P[x] = x for a literal byte and P[x] = src + (x - start) mod distance for a match byte
+//      (LZ4 overlap semantics); repeated P[x] <- P[P[x]] converges in log2(chain depth) rounds, then
+//      out[x] = out[P[x]]. P is 16 bits per byte and lives in the (dead) input buffer, one 32 KiB
+//      half of the output at a time (the second half's pointers into the first half are final).
+// The sequential one-wave decoder (k_lz4_decode_seq) stays as a differential reference, DG_LZ4_SEQ=1.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -27,22 +32,23 @@
 namespace dg {
 
 constexpr int kLzThreads = 256;
-constexpr int kLz4InCap = kBlockBytes + 2048;  // LZ4_compressBound(65536) = 65809
-constexpr int kLongLit = 48;                   // literal runs above this are copied cooperatively
-constexpr int kLongMatch = 48;                 // matches above this are copied cooperatively
-constexpr int kMaxLitJobs = 512;
-constexpr int kMaxRounds = 1 << 16;
+constexpr int kLz4InCap = kBlockBytes + 2048;  // >= LZ4_compressBound(65536) = 65809
+constexpr int kLongLit = 32;                   // literal runs above this are copied cooperatively
+constexpr int kLongFill = 64;                  // match spans above this fill P cooperatively
+constexpr int kMaxJobs = 512;
+constexpr int kHalf = kBlockBytes / 2;
+constexpr int kMaxJumpRounds = 40;
 
 struct Tok {
   int lit;   // literal start (input offset)
   int L;     // literal length
-  int off;   // match offset (0 for the last sequence)
+  int off;   // match distance (0 for the last sequence)
   int M;     // match length (0 for the last sequence)
   int next;  // next token start
 };
 
-// Parse the token starting at p. false = not a valid token here (speculative walks just stop).
-__device__ __forceinline__ bool parse_tok(const uint8_t* __restrict__ in, int n, int p, Tok& t) {
+// Byte-wise parse (long lengths / windows that do not hold the offset).
+__device__ __forceinline__ bool parse_tok_slow(const uint8_t* __restrict__ in, int n, int p, Tok& t) {
   if (p >= n) return false;
   const int tk = in[p];
   int q = p + 1;
@@ -82,18 +88,61 @@ __device__ __forceinline__ bool parse_tok(const uint8_t* __restrict__ in, int n,
   return t.off != 0;
 }
 
-// block-wide (256 threads) exclusive scan of int; total via *total
-__device__ int64_t block_exclusive_scan_lz(int v, int64_t* total, int64_t* s_tmp) {
+// Parse the token at p from one 8-byte window (three aligned dword reads, one LDS round trip) when
+// the token, its literals and its distance fit in it; false = not a valid token here.
+__device__ __forceinline__ bool parse_tok(const uint8_t* __restrict__ in, int n, int p, Tok& t) {
+  if (p >= n) return false;
+  const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
+  const int a = p >> 2, sh = (p & 3) << 3;
+  const uint64_t w01 = (uint64_t)in32[a] | ((uint64_t)in32[a + 1] << 32);
+  const uint32_t w2 = in32[a + 2];
+  const uint64_t win = sh ? ((w01 >> sh) | ((uint64_t)w2 << (64 - sh))) : w01;
+  const int tk = (int)(win & 0xFF);
+  const int L = tk >> 4, M = tk & 15;
+  if (L > 5 || M == 15) return parse_tok_slow(in, n, p, t);
+  const int q = p + 1 + L;
+  t.lit = p + 1;
+  t.L = L;
+  if (q > n) return false;
+  if (q == n) {
+    t.off = 0;
+    t.M = 0;
+    t.next = n;
+    return true;
+  }
+  if (q + 2 > n) return false;
+  t.off = (int)((win >> (8 * (1 + L))) & 0xFFFF);
+  t.M = M + 4;
+  t.next = q + 2;
+  return t.off != 0;
+}
+
+// walk from `pos` inside [.., ce): stop on a position the speculative chain of this chunk visited
+// (then the exit is that chain's exit `spec_exit`) or at the first token start >= ce
+__device__ __forceinline__ int walk_to_exit(const uint8_t* __restrict__ in, int n, int pos, int ce,
+                                            const uint32_t* __restrict__ vb, int spec_exit) {
+  while (pos < ce) {
+    if ((vb[pos >> 5] >> (pos & 31)) & 1u) return spec_exit;
+    Tok t;
+    if (!parse_tok(in, n, pos, t)) return n;
+    pos = t.next;
+  }
+  return pos;
+}
+
+// block-wide (256 threads) exclusive scan; total via *total
+__device__ int block_scan_lz(int v, int* total, int* s_tmp) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int64_t x = v;
+  int x = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    int64_t y = __shfl_up(x, o, 64);
+    int y = __shfl_up(x, o, 64);
     if (lane >= o) x += y;
   }
   if (lane == 63) s_tmp[wave] = x;
   __syncthreads();
-  int64_t wave_off = 0, tot = 0;
+  int wave_off = 0, tot = 0;
+#pragma unroll
   for (int w = 0; w < (kLzThreads >> 6); ++w) {
     if (w < wave) wave_off += s_tmp[w];
     tot += s_tmp[w];
@@ -103,43 +152,50 @@ __device__ int64_t block_exclusive_scan_lz(int v, int64_t* total, int64_t* s_tmp
   return wave_off + x - v;
 }
 
-__global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap];
+#define LZ_STAMP(k)                                                                      \
+  do {                                                                                   \
+    if (prof && tid == 0) prof[(size_t)blockIdx.x * 10 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+__global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+                                                           uint64_t* __restrict__ mtab_all, uint64_t* __restrict__ prof) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kBlockBytes + 64];
-  __shared__ int s_x[kLzThreads];       // speculative exit of each chunk
-  __shared__ int s_pexit[kLzThreads];   // true exit assuming entry = s_x[i-1]
-  __shared__ int s_t[kLzThreads];       // true entry
-  __shared__ int s_ostart[kLzThreads + 1];
-  __shared__ int s_done[kLzThreads];    // output bytes of chunk i below this are final
-  __shared__ uint16_t s_chunk_at[kBlockBytes / 64 + 1];
-  __shared__ int s_lit_job[kMaxLitJobs][3];
-  __shared__ int s_m_job[kLzThreads][3];
-  __shared__ int s_nlit, s_nm, s_bad;
-  __shared__ int64_t s_scan_tmp[8];
+  __shared__ int s_x[kLzThreads];      // speculative exit of each chunk
+  __shared__ int s_pexit[kLzThreads];  // exit assuming entry = s_x[i-1]
+  __shared__ int s_e2[kLzThreads];     // corrected entry guess (= s_pexit[i-1]) or -1
+  __shared__ int s_pexit2[kLzThreads]; // exit assuming entry = s_e2[i]
+  __shared__ int s_t[kLzThreads];      // true entry
+  __shared__ int s_job[kMaxJobs][3];
+  __shared__ int s_njob, s_bad;
+  __shared__ int s_tmp[8];
 
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  LZ_STAMP(0);
   const int n = job.src_len;
   if (n <= 0 || n > kLz4InCap) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
-  // ---- stage input, clear the visited bitmap (aliases the output buffer) ----
+  uint64_t* mtab = mtab_all + (size_t)blockIdx.x * (kBlockBytes / 4);
+  // ---- stage input; clear the visited bitmap (aliases the output buffer) ----
   {
     const uint4* src = reinterpret_cast<const uint4*>(job.src);
     uint4* dst = reinterpret_cast<uint4*>(s_in);
     const int n16 = (n + 15) >> 4;
     for (int i = tid; i < n16; i += kLzThreads) dst[i] = src[i];
+    if (tid == 0) *reinterpret_cast<uint4*>(s_in + (n16 << 4)) = make_uint4(0, 0, 0, 0);
     uint32_t* vb = reinterpret_cast<uint32_t*>(s_out);
     const int nw = (n + 32) >> 5;
     for (int i = tid; i < nw; i += kLzThreads) vb[i] = 0;
     if (tid == 0) {
-      s_nlit = 0;
-      s_nm = 0;
+      s_njob = 0;
       s_bad = 0;
     }
   }
   __syncthreads();
+  LZ_STAMP(1);
   uint32_t* vb = reinterpret_cast<uint32_t*>(s_out);
   const int CH = (n + kLzThreads - 1) / kLzThreads;
   const int cs = min(tid * CH, n), ce = min(cs + CH, n);
@@ -159,39 +215,37 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     s_x[tid] = pos;
   }
   __syncthreads();
-  // ---- 2a. walk from the assumed entry until the speculative chain is met ----
+  LZ_STAMP(2);
+  // ---- 2. exits for the assumed entry, then for the corrected entry where the predecessor missed ----
+  const int x_me = s_x[tid];
   {
     const int a = tid == 0 ? 0 : s_x[tid - 1];
-    int pos = a;
-    if (pos < ce) {
-      while (pos < ce) {
-        if ((vb[pos >> 5] >> (pos & 31)) & 1u) {
-          pos = s_x[tid];
-          break;
-        }
-        Tok t;
-        if (!parse_tok(s_in, n, pos, t)) {
-          pos = n;
-          break;
-        }
-        pos = t.next;
-      }
-    }
-    s_pexit[tid] = pos;
+    s_pexit[tid] = a >= ce ? a : walk_to_exit(s_in, n, a, ce, vb, x_me);
   }
   __syncthreads();
-  // ---- 2b. resolve true entries (wave 0; a run of consistent chunks is one ballot) ----
+  {
+    int e2 = -1, p2 = 0;
+    if (tid > 0 && s_pexit[tid - 1] != s_x[tid - 1]) {
+      e2 = s_pexit[tid - 1];
+      p2 = e2 >= ce ? e2 : walk_to_exit(s_in, n, e2, ce, vb, x_me);
+    }
+    s_e2[tid] = e2;
+    s_pexit2[tid] = p2;
+  }
+  __syncthreads();
+  LZ_STAMP(3);
   if (wave == 0) {
     int cur = 0, i = 0;
     while (i < kLzThreads) {
       const int assumed = i == 0 ? 0 : s_x[i - 1];
       if (cur == assumed) {
+        // a run of chunks whose speculative chain absorbed the assumed entry: one ballot
         const int idx = i + lane;
         const bool valid = idx < kLzThreads;
         const bool ok = valid && s_pexit[idx] == s_x[idx];
         const unsigned long long badm = __ballot(valid && !ok);
         const int first_bad = badm ? (__ffsll((long long)badm) - 1) : 64;
-        const int upto = min(first_bad + 1, kLzThreads - i);  // chunks i .. i+upto-1 get t = assumed
+        const int upto = min(first_bad + 1, kLzThreads - i);
         if (lane < upto) s_t[idx] = idx == 0 ? 0 : s_x[idx - 1];
         if (first_bad < 64 && i + first_bad < kLzThreads) {
           cur = s_pexit[i + first_bad];
@@ -200,33 +254,24 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
           i = min(i + 64, kLzThreads);
           cur = s_x[i - 1];
         }
+      } else if (cur == s_e2[i]) {
+        if (lane == 0) s_t[i] = cur;
+        cur = s_pexit2[i];
+        i++;
       } else {
         int next_i = i + 1, next_cur = cur;
         if (lane == 0) {
           const int ci_s = min(i * CH, n), ci_e = min(ci_s + CH, n);
           if (cur >= ci_e) {
-            // a token spans the whole chunk: every chunk ending at or before cur has no token start
-            int j = CH > 0 ? cur / CH : kLzThreads;
+            // a long token covers whole chunks: they contain no token start
+            int j = cur / CH;
             if (j > kLzThreads) j = kLzThreads;
             if (j <= i) j = i + 1;
             for (int k = i; k < j; ++k) s_t[k] = cur;
             next_i = j;
           } else {
             s_t[i] = cur;
-            int pos = cur;
-            while (pos < ci_e) {
-              if ((vb[pos >> 5] >> (pos & 31)) & 1u) {
-                pos = s_x[i];
-                break;
-              }
-              Tok t;
-              if (!parse_tok(s_in, n, pos, t)) {
-                pos = n;
-                break;
-              }
-              pos = t.next;
-            }
-            next_cur = pos;
+            next_cur = walk_to_exit(s_in, n, cur, ci_e, vb, s_x[i]);
           }
         }
         i = __shfl(next_i, 0, 64);
@@ -235,9 +280,10 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
   }
   __syncthreads();
-  // ---- 3. output size of my chunk's true tokens -> block scan ----
+  LZ_STAMP(4);
+  // ---- 3. sizes of my chunk's true tokens -> output offsets, match-table offsets ----
   const int my_t = s_t[tid];
-  int my_out = 0;
+  int my_out = 0, my_nm = 0;
   {
     int pos = my_t;
     while (pos < ce) {
@@ -247,155 +293,131 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         break;
       }
       my_out += t.L + t.M;
+      my_nm += t.M > 0;
       pos = t.next;
     }
   }
-  int64_t total64;
-  const int my_ostart = (int)block_exclusive_scan_lz(my_out, &total64, s_scan_tmp);
-  const int total = (int)total64;
-  s_ostart[tid] = my_ostart;
-  if (tid == 0) s_ostart[kLzThreads] = total;
-  if (total > kBlockBytes || total < job.expect_len) s_bad = 1;
+  int total, nmatch;
+  const int my_ostart = block_scan_lz(my_out, &total, s_tmp);
+  const int my_mstart = block_scan_lz(my_nm, &nmatch, s_tmp);
+  if (tid == 0 && (total > kBlockBytes || total < job.expect_len)) s_bad = 1;
   __syncthreads();
+  LZ_STAMP(5);
   if (s_bad) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
-  // chunk lookup table over 64-byte output granules (output ranges partition [0, total))
-  for (int g = (my_ostart + 63) >> 6; (g << 6) < my_ostart + my_out; ++g) s_chunk_at[g] = (uint16_t)tid;
-  // ---- 4. literals (the visited bitmap in s_out is dead from here) ----
-  int first_match_out = my_ostart + my_out;
+  // ---- 4. literals -> output; matches -> table (the visited bitmap in s_out is dead) ----
   {
-    int pos = my_t, o = my_ostart;
-    bool seen_match = false;
+    int pos = my_t, o = my_ostart, m = my_mstart;
     while (pos < ce) {
       Tok t;
       parse_tok(s_in, n, pos, t);
       if (t.L <= kLongLit) {
         for (int k = 0; k < t.L; ++k) s_out[o + k] = s_in[t.lit + k];
       } else {
-        const int j = atomicAdd(&s_nlit, 1);
-        if (j < kMaxLitJobs) {
-          s_lit_job[j][0] = t.lit;
-          s_lit_job[j][1] = o;
-          s_lit_job[j][2] = t.L;
+        const int j = atomicAdd(&s_njob, 1);
+        if (j < kMaxJobs) {
+          s_job[j][0] = t.lit;
+          s_job[j][1] = o;
+          s_job[j][2] = t.L;
         } else {
           for (int k = 0; k < t.L; ++k) s_out[o + k] = s_in[t.lit + k];
         }
       }
-      if (!seen_match && t.M > 0) {
-        first_match_out = o + t.L;
-        seen_match = true;
+      o += t.L;
+      if (t.M > 0) {
+        if (t.off > o) s_bad = 1;  // distance before the block start
+        mtab[m++] = (uint64_t)o | ((uint64_t)t.off << 16) | ((uint64_t)t.M << 32);
       }
-      o += t.L + t.M;
+      o += t.M;
       pos = t.next;
     }
   }
   __syncthreads();
   {
-    const int nj = min(s_nlit, kMaxLitJobs);
+    const int nj = min(s_njob, kMaxJobs);
     for (int j = 0; j < nj; ++j) {
-      const int li = s_lit_job[j][0], lo = s_lit_job[j][1], ll = s_lit_job[j][2];
+      const int li = s_job[j][0], lo = s_job[j][1], ll = s_job[j][2];
       for (int k = tid; k < ll; k += kLzThreads) s_out[lo + k] = s_in[li + k];
     }
   }
-  s_done[tid] = first_match_out;
   __syncthreads();
-  // ---- 5. matches in rounds ----
-  volatile int* vdone = s_done;
-  int pos = my_t, o = my_ostart;
-  bool have = false, waiting = false, finished = pos >= ce;
-  Tok t;
-  int rounds = 0;
-  for (;;) {
-    while (!finished && !waiting) {
-      if (!have) {
-        parse_tok(s_in, n, pos, t);
-        have = true;
-      }
-      if (t.M == 0) {  // last sequence
-        o += t.L;
-        pos = t.next;
-        have = false;
-        if (pos >= ce) finished = true;
-        continue;
-      }
-      const int om = o + t.L;
-      const int src = om - t.off;
-      if (src < 0) {
-        s_bad = 1;
-        finished = true;
-        break;
-      }
-      // bytes [src, src + min(off, M)) must be final; those of my own chunk are (in-order processing)
-      const int need_end = min(src + min(t.off, t.M), my_ostart);
-      bool ready = true;
-      int xq = src;
-      while (xq < need_end) {
-        int c = s_chunk_at[xq >> 6];
-        while (s_ostart[c + 1] <= xq) c++;
-        const int cend = s_ostart[c + 1];
-        const int want = min(need_end, cend);
-        if (vdone[c] < want) {
-          ready = false;
-          break;
-        }
-        xq = cend;
-      }
-      if (!ready) break;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (t.M > kLongMatch) {
-        const int j = atomicAdd(&s_nm, 1);
-        s_m_job[j][0] = om;
-        s_m_job[j][1] = t.off;
-        s_m_job[j][2] = t.M;
-        waiting = true;
-        break;
-      }
-      if (t.off >= t.M) {
-        for (int k = 0; k < t.M; ++k) s_out[om + k] = s_out[src + k];
-      } else {
-        for (int k = 0; k < t.M; ++k) s_out[om + k] = s_out[src + (k % t.off)];
-      }
-      o = om + t.M;
-      pos = t.next;
-      have = false;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      vdone[tid] = o;
-      if (pos >= ce) finished = true;
-    }
-    __syncthreads();
-    const int nm = s_nm;
-    for (int j = 0; j < nm; ++j) {
-      const int mo = s_m_job[j][0], moff = s_m_job[j][1], mlen = s_m_job[j][2];
-      const int msrc = mo - moff;
-      if (moff >= mlen) {
-        for (int k = tid; k < mlen; k += kLzThreads) s_out[mo + k] = s_out[msrc + k];
-      } else {
-        for (int k = tid; k < mlen; k += kLzThreads) s_out[mo + k] = s_out[msrc + (k % moff)];
-      }
-    }
-    __syncthreads();
-    if (waiting) {
-      o = o + t.L + t.M;
-      pos = t.next;
-      have = false;
-      waiting = false;
-      vdone[tid] = o;
-      if (pos >= ce) finished = true;
-    }
-    if (tid == 0) s_nm = 0;
-    if (finished) vdone[tid] = my_ostart + my_out;
-    const int pending = __syncthreads_count(!finished);
-    if (pending == 0) break;
-    if (++rounds > kMaxRounds) {
-      if (tid == 0) atomicOr(err, 1);
-      return;
-    }
-  }
+  LZ_STAMP(6);
   if (s_bad) {
     if (tid == 0) atomicOr(err, 1);
     return;
+  }
+  // ---- 5. matches by pointer jumping, one 32 KiB half of the output at a time ----
+  uint16_t* P = reinterpret_cast<uint16_t*>(s_in);  // input is dead; 32 Ki x u16 = 64 KiB
+  int jump_rounds = 0;
+  for (int lo = 0; lo < total; lo += kHalf) {
+    const int hi = min(lo + kHalf, total);
+    for (int x = lo + tid; x < hi; x += kLzThreads) P[x - lo] = (uint16_t)x;
+    if (tid == 0) s_njob = 0;
+    __syncthreads();
+    for (int m = my_mstart; m < my_mstart + my_nm; ++m) {
+      const uint64_t e = mtab[m];
+      const int om = (int)(e & 0xFFFF), off = (int)((e >> 16) & 0xFFFF), M = (int)(e >> 32);
+      const int a = max(om, lo), b = min(om + M, hi);
+      if (a >= b) continue;
+      if (b - a > kLongFill) {
+        const int j = atomicAdd(&s_njob, 1);
+        if (j < kMaxJobs) {
+          s_job[j][0] = om;
+          s_job[j][1] = off;
+          s_job[j][2] = M;
+          continue;
+        }
+      }
+      const int src = om - off;
+      if (off >= M) {
+        for (int x = a; x < b; ++x) P[x - lo] = (uint16_t)(src + (x - om));
+      } else {
+        for (int x = a; x < b; ++x) P[x - lo] = (uint16_t)(src + (x - om) % off);
+      }
+    }
+    __syncthreads();
+    {
+      const int nj = min(s_njob, kMaxJobs);
+      for (int j = 0; j < nj; ++j) {
+        const int om = s_job[j][0], off = s_job[j][1], M = s_job[j][2];
+        const int a = max(om, lo), b = min(om + M, hi), src = om - off;
+        for (int x = a + tid; x < b; x += kLzThreads) P[x - lo] = (uint16_t)(src + (x - om) % off);
+      }
+    }
+    __syncthreads();
+    // P[x] <- P[P[x]] until every pointer is a root (a literal byte of this half, or a byte of an
+    // earlier half, which is final); asynchronous updates only make pointers jump further
+    for (int r = 0;; ++r) {
+      int changed = 0;
+      for (int x = lo + tid; x < hi; x += kLzThreads) {
+        const int p = P[x - lo];
+        if (p >= lo && p != x) {
+          const int pp = P[p - lo];
+          if (pp != p) {
+            P[x - lo] = (uint16_t)pp;
+            changed = 1;
+          }
+        }
+      }
+      jump_rounds++;
+      if (!__syncthreads_or(changed)) break;
+      if (r >= kMaxJumpRounds) {
+        if (tid == 0) atomicOr(err, 1);
+        return;
+      }
+    }
+    for (int x = lo + tid; x < hi; x += kLzThreads) {
+      const int p = P[x - lo];
+      if (p != x) s_out[x] = s_out[p];
+    }
+    __syncthreads();
+  }
+  LZ_STAMP(7);
+  if (prof && tid == 0) {
+    prof[(size_t)blockIdx.x * 10 + 8] = (uint64_t)jump_rounds;
+    prof[(size_t)blockIdx.x * 10 + 9] = (uint64_t)n;
   }
   // ---- 6. write the decoded block ----
   uint4* dst = reinterpret_cast<uint4*>(job.dst);
@@ -412,7 +434,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 // ------------------------------------------------------------------------------------------------
 
 __global__ __launch_bounds__(64) void k_lz4_decode_seq(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap];
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kBlockBytes + 64];
   const Lz4Job job = jobs[blockIdx.x];
   const int lane = threadIdx.x;
@@ -505,11 +527,12 @@ __global__ __launch_bounds__(64) void k_lz4_decode_seq(const Lz4Job* __restrict_
 }
 
 
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s) {
+void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, uint64_t* d_mtab, hipStream_t s,
+                       uint64_t* d_prof) {
   if (njobs <= 0) return;
   static const bool seq = getenv("DG_LZ4_SEQ") && getenv("DG_LZ4_SEQ")[0] == '1';
   if (seq) hipLaunchKernelGGL(k_lz4_decode_seq, dim3(njobs), dim3(64), 0, s, d_jobs, d_err);
-  else hipLaunchKernelGGL(k_lz4_decode, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err);
+  else hipLaunchKernelGGL(k_lz4_decode, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_mtab, d_prof);
 }
 
 }  // namespace dg

@@ -78,16 +78,23 @@ class GlobalDictionary:
 # ----------------------------------------------------------------------------------------------
 # timeseries
 # ----------------------------------------------------------------------------------------------
-def allreduce_timeseries(dist, query: Q.TimeseriesQuery, local: List[Q.Result], buckets: Sequence[int]):
-    """Reduce this rank's merged timeseries results over all ranks.
+def allreduce_timeseries(dist, query: Q.TimeseriesQuery, local: List[Q.Result],
+                         buckets: Optional[Sequence[int]] = None):
+    """Reduce this rank's merged timeseries results over all ranks (every rank gets the result).
 
-    `buckets` is the (cluster-wide, identical on every rank) list of bucket keys; ranks without data
-    for a bucket contribute identities."""
+    `buckets` is the cluster-wide, identical-on-every-rank list of bucket keys (bucket starts; [0] for
+    ALL granularity); None derives it with one all_gather_object of the local keys. Ranks without
+    data for a bucket contribute identities."""
     torch, _ = _torch()
     dev = _device(dist)
+    gran = query.granularity
+    if buckets is None:
+        mine = sorted({0 if gran.is_all else gran.bucket_start(r.timestamp) for r in local})
+        gathered: List = [None] * dist.get_world_size()
+        dist.all_gather_object(gathered, mine)
+        buckets = sorted({b for g in gathered for b in g})
     nb, aggs = len(buckets), query.aggregations
     pos = {b: i for i, b in enumerate(buckets)}
-    gran = query.granularity
     present = np.zeros(nb, dtype=np.int64)
     ts = np.full(nb, Q.MAX_INSTANT, dtype=np.int64)
     cols = {a.name: np.full(nb, a.initial(), dtype=_np_type(a)) for a in aggs}

@@ -413,13 +413,25 @@ def _py(v, out_type):
 # ----------------------------------------------------------------------------------------------
 def timeseries_segment(seg: OracleSegment, query) -> List:
     mask = filter_mask(seg, query.effective_filter())
-    results = []
-    for bt, r0, r1 in cursor_buckets(seg, query):
+    buckets = cursor_buckets(seg, query)
+    # one cursor per bucket; rows of every cursor are aggregated in row order (one C pass per aggregator,
+    # group = cursor index, identical to running each cursor's Aggregator loop on its own)
+    rows_l, grp_l, counts = [], [], []
+    for g, (bt, r0, r1) in enumerate(buckets):
         rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
-        if query.skip_empty_buckets and len(rows) == 0:
+        rows_l.append(rows)
+        grp_l.append(np.full(len(rows), g, np.int32))
+        counts.append(len(rows))
+    if not buckets:
+        return []
+    rows = np.concatenate(rows_l)
+    groups = np.concatenate(grp_l)
+    states = aggregate_groups(seg, query.aggregations, rows, groups, len(buckets))
+    results = []
+    for g, (bt, r0, r1) in enumerate(buckets):
+        if query.skip_empty_buckets and counts[g] == 0:
             continue
-        states = aggregate_groups(seg, query.aggregations, rows, np.zeros(len(rows), np.int32), 1)
-        results.append(Q.Result(bt, {a.name: _py(s[0], a.output_type) for a, s in zip(query.aggregations, states)}))
+        results.append(Q.Result(bt, {a.name: _py(s[g], a.output_type) for a, s in zip(query.aggregations, states)}))
     return results
 
 
