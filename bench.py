@@ -129,16 +129,16 @@ def main():
     gdict = None
     if dist is not None and args.config == "topn":
         gdict = D.GlobalDictionary.build(dist, [s.dictionary(query.dimension) for s in segs])
+        translations = [gdict.translate(s.dictionary(query.dimension)) for s in segs]
     gdicts = None
     if dist is not None and args.config == "groupby":
         gdicts = {d: D.GlobalDictionary.build(dist, [s.dictionary(d) for s in segs]) for d in query.dimensions}
 
     def step(stats):
         if isinstance(query, Q.TopNQuery):
-            per = R.topn_per_segment(segs, query, stats)
             if dist is None:
-                return R.merge_topn(query, per)
-            return D.gather_topn(dist, query, per, gdict, nseg)
+                return R.run_topn(segs, query, stats)
+            return D.gather_topn(dist, query, R.topn_raw(segs, query, stats), gdict, translations)
         if isinstance(query, Q.TimeseriesQuery):
             per = R.timeseries_per_segment(segs, query, stats)
             res = R.merge_timeseries(query, per)

@@ -19,6 +19,7 @@
  *                               TimeseriesQueryEngine.java:40-111)
  *   dg_topn_run              <- TopNQueryRunnerFactory.createRunner(segment).run (query/topn/TopNQueryRunnerFactory.java:61-90,
  *                               TopNQueryEngine.java:60-160 -> PooledTopNAlgorithm + TopNNumericResultBuilder)
+ *   dg_topn_merge            <- TopNBinaryFn.apply fold of QueryRunnerFactory.mergeRunners (query/topn/TopNBinaryFn.java:75-135)
  *   dg_groupby_run           <- GroupByStrategyV2.process -> GroupByQueryEngineV2.process
  *                               (query/groupby/strategy/GroupByStrategyV2.java:472-477, epinephelinae/GroupByQueryEngineV2.java:91-187)
  *
@@ -204,6 +205,27 @@ typedef struct {
  * returns them; entry j at index i * threshold + j: dictionary id (segment-local) and n_aggs slots. */
 int dg_topn_run(dg_segment* const* segs, int32_t n_segs, const dg_scan* scan, const dg_topn* topn,
                 int32_t* out_n, int32_t* out_ids, uint64_t* out_values, dg_metrics* metrics);
+
+/* TopNBinaryFn fold (query/topn/TopNBinaryFn.java:75-135) of per-segment topN lists, as
+ * TopNQueryQueryToolChest.mergeResults applies it over the per-segment runners' results
+ * (QueryRunnerFactory.mergeRunners): lists in merge order (result timestamp, then segment index),
+ * pairwise: union by dimension value with AggregatorFactory.combine, then TopNNumericResultBuilder with
+ * the query threshold; the final list is truncated to the query threshold. ALL granularity.
+ *   keys: segment mode (segs != NULL, one per list): segment-local dictionary ids, values compared by
+ *         string through segs[i]'s dictionary; global mode (segs == NULL): ids of one cluster-wide
+ *         dictionary whose order is Java String order, nulls first.
+ * Output: out_n entries (<= topn->threshold), entry j taken from list out_list[j] with key out_keys[j]
+ * and n_aggs slots in dg_topn_run's encoding. topn->threshold here is the QUERY threshold. */
+typedef struct {
+  int32_t n_lists;
+  const int32_t* list_n;   /* entries of list i; <= 0: empty (no cursor) */
+  int32_t stride;          /* entry j of list i is at index i * stride + j */
+  const int64_t* keys;
+  const uint64_t* values;  /* n_aggs slots per entry */
+} dg_topn_lists;
+
+int dg_topn_merge(dg_segment* const* segs, const dg_scan* scan, const dg_topn* topn, const dg_topn_lists* in,
+                  int32_t* out_n, int32_t* out_list, int64_t* out_keys, uint64_t* out_values);
 
 /* ---- groupBy (v2) ---- */
 typedef struct {

@@ -72,6 +72,11 @@ class dg_topn(ctypes.Structure):
                 ("threshold", ctypes.c_int32)]
 
 
+class dg_topn_lists(ctypes.Structure):
+    _fields_ = [("n_lists", ctypes.c_int32), ("list_n", ctypes.c_void_p), ("stride", ctypes.c_int32),
+                ("keys", ctypes.c_void_p), ("values", ctypes.c_void_p)]
+
+
 class dg_groupby(ctypes.Structure):
     _fields_ = [("dimensions", ctypes.POINTER(ctypes.c_char_p)), ("n_dims", ctypes.c_int32)]
 
@@ -82,7 +87,7 @@ EXPORTS = [
     "dg_context_set_stream", "dg_segment_attach", "dg_segment_release", "dg_segment_num_rows",
     "dg_segment_interval", "dg_segment_time_bounds", "dg_segment_num_columns", "dg_segment_column_name",
     "dg_segment_column_type", "dg_segment_device_bytes", "dg_segment_dim_cardinality", "dg_segment_dim_value",
-    "dg_segment_dim_dictionary", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_groupby_run",
+    "dg_segment_dim_dictionary", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_topn_merge", "dg_groupby_run",
     "dg_result_groups", "dg_result_fetch_groups", "dg_result_release",
 ]
 
@@ -121,6 +126,7 @@ def lib():
         "dg_filter_bitmap": (ctypes.c_int, [vp, P(dg_filter), i32, vp, P(i64)]),
         "dg_timeseries_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), i32, vp, vp, vp, vp, P(dg_metrics)]),
         "dg_topn_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), P(dg_topn), vp, vp, vp, P(dg_metrics)]),
+        "dg_topn_merge": (ctypes.c_int, [vp, P(dg_scan), P(dg_topn), P(dg_topn_lists), P(i32), vp, vp, vp]),
         "dg_groupby_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), P(dg_groupby), P(vp), P(dg_metrics)]),
         "dg_result_groups": (i64, [vp, i32]),
         "dg_result_fetch_groups": (ctypes.c_int, [vp, i32, vp, vp, vp]),

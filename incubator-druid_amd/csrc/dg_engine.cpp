@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <queue>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -99,7 +100,17 @@ struct Pool {
 struct CallScratch {
   Pool dev;
   Pool host;
+  // per-call device error word (bit 0: corrupt LZ4 block, bit 1: corrupt Roaring bitmap), read once
+  // at the call's final synchronisation instead of after every kernel
+  int32_t* d_err = nullptr;
+  int32_t* h_err = nullptr;
   CallScratch() { host.pinned = true; }
+  void reset() {
+    dev.reset();
+    host.reset();
+    d_err = nullptr;
+    h_err = nullptr;
+  }
 };
 
 static CallScratch* scratch_of(Context* ctx) {
@@ -120,6 +131,27 @@ static T* dev_take(CallScratch* cs, size_t count) {
 template <class T>
 static T* host_take(CallScratch* cs, size_t count) {
   return static_cast<T*>(cs->host.take(count * sizeof(T)));
+}
+
+static int32_t* call_err(CallScratch* cs, hipStream_t st) {
+  if (!cs->d_err) {
+    cs->d_err = dev_take<int32_t>(cs, 1);
+    cs->h_err = host_take<int32_t>(cs, 1);
+    if (!cs->d_err || !cs->h_err) return nullptr;
+    *cs->h_err = 0;
+    if (hipMemsetAsync(cs->d_err, 0, 4, st) != hipSuccess) return nullptr;
+  }
+  return cs->d_err;
+}
+
+// Enqueue the error-word read-back, wait for the stream, and turn device-side errors into codes.
+static int finish_call(CallScratch* cs, hipStream_t st) {
+  if (cs->d_err) DG_HIP(hipMemcpyAsync(cs->h_err, cs->d_err, 4, hipMemcpyDeviceToHost, st));
+  DG_HIP(hipStreamSynchronize(st));
+  DG_HIP(hipGetLastError());
+  if (cs->d_err && *cs->h_err)
+    return set_error(DG_ERR_FORMAT, (*cs->h_err & 1) ? "corrupt LZ4 block" : "corrupt Roaring bitmap");
+  return DG_OK;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -357,10 +389,12 @@ static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos
 }
 
 // Build the row bitset of `filter` for segment `seg` on the device. *out = nullptr means "all rows".
+// The bitset's cardinality lands in the pinned word *count once the stream reaches this point
+// (nullptr when there is no filter: every row). Nothing here synchronises.
 static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, int n_filter, uint32_t** out,
-                        int64_t* count, hipStream_t st) {
+                        const unsigned long long** count, hipStream_t st) {
   *out = nullptr;
-  *count = seg->nrows;
+  *count = nullptr;
   if (!filter || n_filter <= 0) return DG_OK;
   FilterPlan fp;
   int pos = 0;
@@ -420,8 +454,8 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
     DG_HIP(hipMemcpyAsync(d_len, h_len, nb * 4, hipMemcpyHostToDevice, st));
     DG_HIP(hipMemcpyAsync(d_tgt, h_tgt, nb * 4, hipMemcpyHostToDevice, st));
     if (c->bitmap_roaring) {
-      int32_t* d_err = dev_take<int32_t>(cs, 1);
-      DG_HIP(hipMemsetAsync(d_err, 0, 4, st));
+      int32_t* d_err = call_err(cs, st);
+      if (!d_err) return set_error(DG_ERR_OOM, "error word");
       launch_roaring_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, d_err, (nwords + 2) * 32, st);
     } else {
       launch_concise_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, (nwords + 2) * 32, st);
@@ -438,8 +472,7 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
   launch_filter_eval(d_prog, plen, d_sets, result, seg->nrows, d_count, st);
   unsigned long long* h_count = host_take<unsigned long long>(cs, 1);
   DG_HIP(hipMemcpyAsync(h_count, d_count, 8, hipMemcpyDeviceToHost, st));
-  DG_HIP(hipStreamSynchronize(st));
-  *count = (int64_t)*h_count;
+  *count = h_count;
   *out = result;
   return DG_OK;
 }
@@ -496,17 +529,12 @@ static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
   Lz4Job* h = host_take<Lz4Job>(cs, n);
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   Lz4Job* d = dev_take<Lz4Job>(cs, n);
-  int32_t* d_err = dev_take<int32_t>(cs, 1);
+  int32_t* d_err = call_err(cs, st);
   uint64_t* d_mtab = dev_take<uint64_t>(cs, (size_t)n * kLz4MatchTable);
   if (!h || !d || !d_err || !d_mtab) return set_error(DG_ERR_OOM, "lz4 jobs");
   DG_HIP(hipMemcpyAsync(d, h, sizeof(Lz4Job) * n, hipMemcpyHostToDevice, st));
-  DG_HIP(hipMemsetAsync(d_err, 0, 4, st));
   launch_lz4_decode(d, n, d_err, d_mtab, st);
-  int32_t* h_err = host_take<int32_t>(cs, 1);
-  DG_HIP(hipMemcpyAsync(h_err, d_err, 4, hipMemcpyDeviceToHost, st));
-  DG_HIP(hipStreamSynchronize(st));
-  if (*h_err) return set_error(DG_ERR_FORMAT, "corrupt LZ4 block");
-  return DG_OK;
+  return DG_OK;  // errors surface at finish_call
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -698,8 +726,7 @@ int read_time_bounds(Segment* seg) {
   Context* ctx = seg->ctx;
   Column* t = seg->find("__time");
   CallScratch* cs = scratch_of(ctx);
-  cs->dev.reset();
-  cs->host.reset();
+  cs->reset();
   DecodeBatch db;
   ColView v;
   hipStream_t st = ctx->stream;
@@ -719,8 +746,8 @@ int read_time_bounds(Segment* seg) {
       j.expect_len = (int32_t)(rows * 8);
       db.jobs.push_back(j);
     }
-    int rc = run_decodes(cs, &db, st);
-    if (rc) return rc;
+    int rc0 = run_decodes(cs, &db, st);
+    if (rc0) return rc0;
     int64_t idx_last = (seg->nrows - 1) & ((1ll << b.log2_per) - 1);
     DG_HIP(hipMemcpyAsync(h, slots, 8, hipMemcpyDeviceToHost, st));
     DG_HIP(hipMemcpyAsync(h + 1, slots + kBlockBytes + idx_last * 8, 8, hipMemcpyDeviceToHost, st));
@@ -733,7 +760,8 @@ int read_time_bounds(Segment* seg) {
                           hipMemcpyDeviceToHost, st));
   }
   (void)v;
-  DG_HIP(hipStreamSynchronize(st));
+  int rc = finish_call(cs, st);
+  if (rc) return rc;
   seg->min_time = h[0];
   seg->max_time = h[1];
   return DG_OK;
@@ -748,8 +776,7 @@ struct CallGuard {
   CallScratch* cs;
   explicit CallGuard(Context* c) : ctx(c), lock(c->mu), cs(scratch_of(c)) {
     hipSetDevice(c->device);
-    cs->dev.reset();
-    cs->host.reset();
+    cs->reset();
   }
 };
 
@@ -899,7 +926,7 @@ int dg_filter_bitmap(dg_segment* s, const dg_filter* filter, int32_t n_filter, u
   CallGuard g(seg->ctx);
   hipStream_t st = seg->ctx->stream;
   uint32_t* bits = nullptr;
-  int64_t count = 0;
+  const unsigned long long* count = nullptr;
   int rc = build_bitset(seg, g.cs, filter, n_filter, &bits, &count, st);
   if (rc) return rc;
   const int64_t nwords = (seg->nrows + 31) / 32;
@@ -908,9 +935,10 @@ int dg_filter_bitmap(dg_segment* s, const dg_filter* filter, int32_t n_filter, u
     if (seg->nrows & 31) out_words[nwords - 1] = (1u << (seg->nrows & 31)) - 1u;
   } else {
     DG_HIP(hipMemcpyAsync(out_words, bits, nwords * 4, hipMemcpyDeviceToHost, st));
-    DG_HIP(hipStreamSynchronize(st));
   }
-  if (out_count) *out_count = count;
+  rc = finish_call(g.cs, st);
+  if (rc) return rc;
+  if (out_count) *out_count = count ? (int64_t)*count : seg->nrows;
   return DG_OK;
 }
 
@@ -936,6 +964,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   std::vector<Cursors> cur(n);
   std::vector<ScanJob> jobs(n);
   std::vector<int64_t> tiles_rows(n, 0);
+  std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db;
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
@@ -946,10 +975,8 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     if (!cur[i].any) continue;
     if (cur[i].nbuckets > bucket_cap) return set_error(DG_ERR_ARG, "%lld buckets > cap %d", (long long)cur[i].nbuckets, bucket_cap);
     uint32_t* bits = nullptr;
-    int64_t cnt = 0;
-    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &cnt, st);
+    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &counts[i], st);
     if (rc) return rc;
-    m.pre_filtered_rows += cnt;
     ScanJob& j = jobs[i];
     memset(&j, 0, sizeof j);
     j.nrows = (int32_t)seg->nrows;
@@ -1009,10 +1036,11 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     h_out[i] = host_take<uint64_t>(cs, (size_t)cur[i].nbuckets * rec);
     DG_HIP(hipMemcpyAsync(h_out[i], jobs[i].out, (size_t)cur[i].nbuckets * rec * 8, hipMemcpyDeviceToHost, st));
   }
-  DG_HIP(hipStreamSynchronize(st));
-  DG_HIP(hipGetLastError());
+  rc = finish_call(cs, st);
+  if (rc) return rc;
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
+    m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : reinterpret_cast<Segment*>(segs[i])->nrows;
     for (int64_t b = 0; b < cur[i].nbuckets; ++b) {
       const int64_t o = (int64_t)i * bucket_cap + b;
       out_time[o] = q->period_ms ? cur[i].bucket0 + b * q->period_ms : cur[i].t_lo;
@@ -1087,6 +1115,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   std::vector<Cursors> cur(n);
   std::vector<ScanJob> jobs(n);
   std::vector<int64_t> card(n, 1), tiles_rows(n, 0);
+  std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db;
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
@@ -1100,10 +1129,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     Column* dc = seg->find(t->dimension);
     if (dc && dc->type != DG_COL_STRING) return set_error(DG_ERR_UNSUPPORTED, "topN on non-string dimension %s", t->dimension);
     uint32_t* bits = nullptr;
-    int64_t cnt = 0;
-    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &cnt, st);
+    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &counts[i], st);
     if (rc) return rc;
-    m.pre_filtered_rows += cnt;
     j.nrows = (int32_t)seg->nrows;
     j.bitset = bits;
     j.t_lo = cur[i].t_lo;
@@ -1128,8 +1155,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], st);
       if (rc) return rc;
     }
-    j.out = dev_take<uint64_t>(cs, (size_t)card[i] * rec);
-    if (!j.out) return set_error(DG_ERR_OOM, "topN table");
+    j.out = nullptr;  // allocated below, once the aggregation layout (split partial tables) is known
     tiles_rows[i] = seg->nrows;
   }
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
@@ -1143,8 +1169,19 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
   uint64_t* d_init = dev_take<uint64_t>(cs, rec);
   DG_HIP(hipMemcpyAsync(d_init, h_init, rec * 8, hipMemcpyHostToDevice, st));
+  // LDS-privatised id ranges when the per-segment table needs few of them, else HBM atomics
+  int64_t max_card_all = 0;
   for (int i = 0; i < n; ++i)
-    if (cur[i].any) launch_fill_u64(jobs[i].out, card[i], rec, d_init, st);
+    if (cur[i].any) max_card_all = std::max(max_card_all, card[i]);
+  const bool part = (max_card_all + topn_part_range(na) - 1) / topn_part_range(na) <= kMaxIdRanges;
+  const int splits = part ? topn_part_splits(max_card_all, na, n) : 1;
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    jobs[i].nbuckets = (int32_t)card[i];
+    jobs[i].out = dev_take<uint64_t>(cs, (size_t)card[i] * rec * splits);
+    if (!jobs[i].out) return set_error(DG_ERR_OOM, "topN table");
+    if (!part) launch_fill_u64(jobs[i].out, card[i], rec, d_init, st);
+  }
   std::vector<int32_t> begin;
   int ntiles = 0;
   int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
@@ -1176,56 +1213,107 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       DG_HIP(hipMemcpyAsync(d_jobs + i, h_jobs + i, sizeof(ScanJob), hipMemcpyHostToDevice, st));
     }
   }
-  launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
-  // selection
+  if (part) launch_topn_part(d_jobs, n, max_card_all, plan, splits, st);
+  else launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
+  // selection + gather of the candidates' records, all segments in one launch
   const int mk = plan.kind[t->metric_agg];
   const int metric_op = (slot_op(mk) << 8) | mk;
-  std::vector<int32_t*> d_cand(n, nullptr);
-  int32_t* d_ncand = dev_take<int32_t>(cs, n);
-  uint64_t* d_state = dev_take<uint64_t>(cs, 2 * (size_t)n);
+  std::vector<TopnSelJob> sel;
+  std::vector<int> sel_seg;
+  std::vector<int64_t> gcap(n, 0);
+  int64_t max_card = 0;
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
-    d_cand[i] = dev_take<int32_t>(cs, (size_t)card[i]);
-    launch_topn_select(jobs[i].out, card[i], na, t->metric_agg, metric_op, t->inverted, t->threshold, d_state + 2 * i,
-                       d_cand[i], d_ncand + i, (int)card[i], st);
+    TopnSelJob sj;
+    memset(&sj, 0, sizeof sj);
+    sj.table = jobs[i].out;
+    sj.card = card[i];
+    sj.cand = dev_take<int32_t>(cs, (size_t)card[i]);
+    sj.keys = dev_take<uint64_t>(cs, (size_t)card[i]);
+    sj.blkcnt = dev_take<int32_t>(cs, (size_t)((card[i] + kSelBlock - 1) / kSelBlock));
+    // candidates = ids whose key >= the K-th key: the threshold plus ties, rarely more
+    gcap[i] = std::min<int64_t>(card[i], 2 * (int64_t)t->threshold + 64);
+    sj.gather_cap = (int32_t)gcap[i];
+    sj.gathered = dev_take<uint64_t>(cs, (size_t)gcap[i] * rec);
+    if (!sj.cand || !sj.gathered || !sj.keys || !sj.blkcnt) return set_error(DG_ERR_OOM, "topN candidates");
+    max_card = std::max(max_card, card[i]);
+    sel.push_back(sj);
+    sel_seg.push_back(i);
+  }
+  const int ns = (int)sel.size();
+  int32_t* d_ncand = dev_take<int32_t>(cs, std::max(ns, 1));
+  // per selection: state[4] + hist[8][256], zeroed with one memset
+  const size_t sel_words = 4 + 8 * 256 / 2;
+  uint64_t* d_selmem = dev_take<uint64_t>(cs, sel_words * std::max(ns, 1));
+  uint64_t* d_state = d_selmem;
+  for (int k = 0; k < ns; ++k) {
+    sel[k].ncand = d_ncand + k;
+    sel[k].state = d_selmem + sel_words * k;
+    sel[k].hist = reinterpret_cast<uint32_t*>(d_selmem + sel_words * k + 4);
+  }
+  TopnSelJob* h_sel = host_take<TopnSelJob>(cs, std::max(ns, 1));
+  TopnSelJob* d_sel = dev_take<TopnSelJob>(cs, std::max(ns, 1));
+  if (!h_sel || !d_sel || !d_ncand || !d_selmem) return set_error(DG_ERR_OOM, "topN selection");
+  if (ns) {
+    memcpy(h_sel, sel.data(), sizeof(TopnSelJob) * ns);
+    DG_HIP(hipMemcpyAsync(d_sel, h_sel, sizeof(TopnSelJob) * ns, hipMemcpyHostToDevice, st));
+    DG_HIP(hipMemsetAsync(d_selmem, 0, 8 * sel_words * ns, st));
+    launch_topn_select(d_sel, ns, max_card, na, t->metric_agg, metric_op, t->inverted, t->threshold, st);
   }
   hipEventRecord(ctx->ev[4], st);
-  int32_t* h_ncand = host_take<int32_t>(cs, n);
-  uint64_t* h_state = host_take<uint64_t>(cs, 2 * (size_t)n);
-  DG_HIP(hipMemcpyAsync(h_ncand, d_ncand, 4 * n, hipMemcpyDeviceToHost, st));
-  DG_HIP(hipMemcpyAsync(h_state, d_state, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
-  DG_HIP(hipStreamSynchronize(st));
-  DG_HIP(hipGetLastError());
-  for (int i = 0; i < n; ++i)
-    if (cur[i].any) m.selected_rows += (int64_t)h_state[2 * i + 1];
-  // fetch candidate ids and their records (small: threshold + ties)
-  std::vector<int32_t*> h_cand(n, nullptr);
-  std::vector<uint64_t*> h_tab(n, nullptr);
-  for (int i = 0; i < n; ++i) {
-    if (!cur[i].any) continue;
-    const int nc = h_ncand[i];
-    h_cand[i] = host_take<int32_t>(cs, std::max(nc, 1));
-    DG_HIP(hipMemcpyAsync(h_cand[i], d_cand[i], 4 * (size_t)std::max(nc, 0), hipMemcpyDeviceToHost, st));
+  int32_t* h_ncand = host_take<int32_t>(cs, std::max(ns, 1));
+  uint64_t* h_state = host_take<uint64_t>(cs, sel_words * (size_t)std::max(ns, 1));
+  std::vector<int32_t*> h_cand(ns, nullptr);
+  std::vector<uint64_t*> h_tab(ns, nullptr);
+  if (ns) {
+    DG_HIP(hipMemcpyAsync(h_ncand, d_ncand, 4 * ns, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h_state, d_state, 8 * sel_words * (size_t)ns, hipMemcpyDeviceToHost, st));
   }
-  DG_HIP(hipStreamSynchronize(st));
-  for (int i = 0; i < n; ++i) {
-    if (!cur[i].any) continue;
-    const int nc = h_ncand[i];
-    h_tab[i] = host_take<uint64_t>(cs, (size_t)std::max(nc, 1) * rec);
-    // candidates are ascending ids: copy contiguous runs of records
-    for (int k = 0; k < nc;) {
-      int e = k + 1;
-      while (e < nc && h_cand[i][e] == h_cand[i][e - 1] + 1) e++;
-      DG_HIP(hipMemcpyAsync(h_tab[i] + (size_t)k * rec, jobs[i].out + (size_t)h_cand[i][k] * rec,
-                            (size_t)(e - k) * rec * 8, hipMemcpyDeviceToHost, st));
-      k = e;
+  for (int k = 0; k < ns; ++k) {
+    const int i = sel_seg[k];
+    h_cand[k] = host_take<int32_t>(cs, (size_t)std::max<int64_t>(gcap[i], 1));
+    h_tab[k] = host_take<uint64_t>(cs, (size_t)std::max<int64_t>(gcap[i], 1) * rec);
+    if (!h_cand[k] || !h_tab[k]) return set_error(DG_ERR_OOM, "topN read-back");
+    DG_HIP(hipMemcpyAsync(h_cand[k], sel[k].cand, 4 * (size_t)gcap[i], hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h_tab[k], sel[k].gathered, 8 * (size_t)gcap[i] * rec, hipMemcpyDeviceToHost, st));
+  }
+  rc = finish_call(cs, st);
+  if (rc) return rc;
+  // rare: more candidates than the speculative read-back held (many ties at the K-th key)
+  bool again = false;
+  for (int k = 0; k < ns; ++k) {
+    const int i = sel_seg[k];
+    const int nc = h_ncand[k];
+    if (nc <= gcap[i]) continue;
+    again = true;
+    h_cand[k] = host_take<int32_t>(cs, (size_t)nc);
+    h_tab[k] = host_take<uint64_t>(cs, (size_t)nc * rec);
+    if (!h_cand[k] || !h_tab[k]) return set_error(DG_ERR_OOM, "topN read-back");
+    DG_HIP(hipMemcpyAsync(h_cand[k], sel[k].cand, 4 * (size_t)nc, hipMemcpyDeviceToHost, st));
+  }
+  if (again) {
+    DG_HIP(hipStreamSynchronize(st));
+    for (int k = 0; k < ns; ++k) {
+      const int i = sel_seg[k];
+      const int nc = h_ncand[k];
+      if (nc <= gcap[i]) continue;
+      for (int c = 0; c < nc;) {  // candidates ascend: copy contiguous id runs
+        int e = c + 1;
+        while (e < nc && h_cand[k][e] == h_cand[k][e - 1] + 1) e++;
+        DG_HIP(hipMemcpyAsync(h_tab[k] + (size_t)c * rec, jobs[i].out + (size_t)h_cand[k][c] * rec,
+                              (size_t)(e - c) * rec * 8, hipMemcpyDeviceToHost, st));
+        c = e;
+      }
     }
+    DG_HIP(hipStreamSynchronize(st));
   }
-  DG_HIP(hipStreamSynchronize(st));
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : reinterpret_cast<Segment*>(segs[i])->nrows;
   // replay TopNNumericResultBuilder over the candidates in id (= dimension value) order
-  for (int i = 0; i < n; ++i) {
-    if (!cur[i].any) continue;
-    const int nc = h_ncand[i];
+  for (int k = 0; k < ns; ++k) {
+    const int i = sel_seg[k];
+    m.selected_rows += (int64_t)h_state[sel_words * k + 1];
+    const int nc = h_ncand[k];
     struct E {
       uint64_t key;
       int32_t id;
@@ -1234,8 +1322,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     auto less = [](const E& a, const E& b) { return a.key != b.key ? a.key < b.key : a.id < b.id; };
     auto gt = [&](const E& a, const E& b) { return less(b, a); };
     std::priority_queue<E, std::vector<E>, decltype(gt)> pq(gt);  // min-heap on (key, id)
-    for (int k = 0; k < nc; ++k) {
-      E e{metric_key_host(h_tab[i][(size_t)k * rec + 1 + t->metric_agg], mk, t->inverted), h_cand[i][k], k};
+    for (int c = 0; c < nc; ++c) {
+      E e{metric_key_host(h_tab[k][(size_t)c * rec + 1 + t->metric_agg], mk, t->inverted), h_cand[k][c], c};
       if ((int)pq.size() < t->threshold || pq.top().key < e.key) pq.push(e);
       if ((int)pq.size() > t->threshold) pq.pop();
     }
@@ -1246,10 +1334,10 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     }
     std::sort(v.begin(), v.end(), [](const E& a, const E& b) { return a.key != b.key ? a.key > b.key : a.id < b.id; });
     out_n[i] = (int32_t)v.size();
-    for (size_t k = 0; k < v.size(); ++k) {
-      const int64_t o = (int64_t)i * t->threshold + (int64_t)k;
-      out_ids[o] = v[k].id;
-      for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[i][(size_t)v[k].idx * rec + 1 + a]);
+    for (size_t e = 0; e < v.size(); ++e) {
+      const int64_t o = (int64_t)i * t->threshold + (int64_t)e;
+      out_ids[o] = v[e].id;
+      for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[k][(size_t)v[e].idx * rec + 1 + a]);
     }
   }
   float f1 = 0, f2 = 0, f3 = 0;
@@ -1261,6 +1349,195 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   m.aggregate_ms = f3;
   m.total_ms = ms_since(t0);
   if (metrics) *metrics = m;
+  return DG_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// topN merge (TopNBinaryFn fold)
+// ------------------------------------------------------------------------------------------------
+}  // extern "C"
+
+namespace dg {
+
+// AggregatorFactory.combine on ABI-encoded values (Java semantics: long wrap, float adds in float,
+// Math.min / Math.max with NaN propagation and -0.0 < 0.0)
+template <class F>
+static F java_min(F a, F b) {
+  if (a != a) return a;
+  if (a == 0 && b == 0 && std::signbit(b)) return b;
+  return a <= b ? a : b;
+}
+template <class F>
+static F java_max(F a, F b) {
+  if (a != a) return a;
+  if (a == 0 && b == 0 && std::signbit(a)) return b;
+  return a >= b ? a : b;
+}
+static uint64_t combine_abi(int kind, uint64_t a, uint64_t b) {
+  uint64_t out = 0;
+  switch (kind) {
+    case DG_AGG_COUNT:
+    case DG_AGG_LONG_SUM: return (uint64_t)((int64_t)a + (int64_t)b);
+    case DG_AGG_LONG_MIN: return (uint64_t)std::min((int64_t)a, (int64_t)b);
+    case DG_AGG_LONG_MAX: return (uint64_t)std::max((int64_t)a, (int64_t)b);
+    case DG_AGG_DOUBLE_SUM:
+    case DG_AGG_DOUBLE_MIN:
+    case DG_AGG_DOUBLE_MAX: {
+      double x, y, r;
+      memcpy(&x, &a, 8);
+      memcpy(&y, &b, 8);
+      r = kind == DG_AGG_DOUBLE_SUM ? x + y : kind == DG_AGG_DOUBLE_MIN ? java_min(x, y) : java_max(x, y);
+      memcpy(&out, &r, 8);
+      return out;
+    }
+    default: {
+      float x, y, r;
+      memcpy(&x, &a, 4);
+      memcpy(&y, &b, 4);
+      r = kind == DG_AGG_FLOAT_SUM ? x + y : kind == DG_AGG_FLOAT_MIN ? java_min(x, y) : java_max(x, y);
+      memcpy(&out, &r, 4);
+      return out;
+    }
+  }
+}
+
+// comparator key of an ABI-encoded metric value (Long.compare / Double.compare / Float.compare)
+static uint64_t abi_metric_key(int kind, uint64_t v, int inverted) {
+  uint64_t k;
+  if (kind == DG_AGG_COUNT || kind == DG_AGG_LONG_SUM || kind == DG_AGG_LONG_MIN || kind == DG_AGG_LONG_MAX) {
+    k = v ^ 0x8000000000000000ull;
+  } else {
+    double d;
+    if (kind == DG_AGG_DOUBLE_SUM || kind == DG_AGG_DOUBLE_MIN || kind == DG_AGG_DOUBLE_MAX) {
+      memcpy(&d, &v, 8);
+    } else {
+      float f;
+      memcpy(&f, &v, 4);
+      d = f;
+    }
+    if (d != d) {
+      k = ~0ull;
+    } else {
+      uint64_t u;
+      memcpy(&u, &d, 8);
+      k = (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+    }
+  }
+  return inverted ? ~k : k;
+}
+
+}  // namespace dg
+
+extern "C" {
+
+int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, const dg_topn_lists* in, int32_t* out_n,
+                  int32_t* out_list, int64_t* out_keys, uint64_t* out_values) {
+  if (!q || !t || !in || !out_n || (in->n_lists > 0 && (!in->list_n || !in->keys || !in->values)))
+    return set_error(DG_ERR_ARG, "null argument");
+  AggPlan plan;
+  int rc = make_plan(q, &plan);
+  if (rc) return rc;
+  if (t->metric_agg < 0 || t->metric_agg >= plan.n) return set_error(DG_ERR_ARG, "metric index");
+  if (t->threshold <= 0) return set_error(DG_ERR_ARG, "threshold");
+  const int na = plan.n, mk = plan.kind[t->metric_agg];
+  struct Ent {
+    int32_t list;
+    int64_t key;
+    std::vector<uint64_t> v;
+  };
+  // dimension value of an entry (segment mode) and its ordering
+  auto value_of = [&](const Ent& e, bool* isnull) -> const std::string* {
+    const Segment* seg = reinterpret_cast<const Segment*>(segs[e.list]);
+    const Column* c = seg->find(t->dimension ? t->dimension : "");
+    if (!c || c->type != DG_COL_STRING || e.key < 0 || e.key >= (int64_t)c->dict.size()) {
+      *isnull = true;
+      return nullptr;
+    }
+    *isnull = c->dict_null[e.key] != 0;
+    return &c->dict[e.key];
+  };
+  static const std::string kEmptyStr;
+  auto dim_cmp = [&](const Ent& a, const Ent& b) -> int {
+    if (!segs) return a.key < b.key ? -1 : (a.key > b.key ? 1 : 0);
+    bool an, bn;
+    const std::string* sa = value_of(a, &an);
+    const std::string* sb = value_of(b, &bn);
+    return cmp_nullable(an, an ? kEmptyStr : *sa, bn, bn ? kEmptyStr : *sb);
+  };
+  auto identity = [&](const Ent& e) -> std::string {
+    if (!segs) return std::string(reinterpret_cast<const char*>(&e.key), 8);
+    bool isnull;
+    const std::string* sv = value_of(e, &isnull);
+    return isnull ? std::string(1, '\0') : std::string(1, '\1') + *sv;
+  };
+  // TopNNumericResultBuilder over `ents` (insertion order matters for ties at the minimum)
+  auto build = [&](std::vector<Ent>& ents, int threshold) {
+    std::vector<uint64_t> mkey(ents.size());
+    for (size_t e = 0; e < ents.size(); ++e) mkey[e] = abi_metric_key(mk, ents[e].v[t->metric_agg], t->inverted);
+    auto less = [&](size_t a, size_t b) {
+      if (mkey[a] != mkey[b]) return mkey[a] < mkey[b];
+      return dim_cmp(ents[a], ents[b]) < 0;
+    };
+    auto gt = [&](size_t a, size_t b) { return less(b, a); };
+    std::priority_queue<size_t, std::vector<size_t>, decltype(gt)> pq(gt);
+    for (size_t e = 0; e < ents.size(); ++e) {
+      if ((int)pq.size() < threshold || mkey[pq.top()] < mkey[e]) pq.push(e);
+      if ((int)pq.size() > threshold) pq.pop();
+    }
+    std::vector<size_t> keep;
+    while (!pq.empty()) {
+      keep.push_back(pq.top());
+      pq.pop();
+    }
+    std::sort(keep.begin(), keep.end(), [&](size_t a, size_t b) {
+      if (mkey[a] != mkey[b]) return mkey[a] > mkey[b];
+      return dim_cmp(ents[a], ents[b]) < 0;
+    });
+    std::vector<Ent> out;
+    out.reserve(keep.size());
+    for (size_t k : keep) out.push_back(std::move(ents[k]));
+    ents.swap(out);
+  };
+  std::vector<Ent> acc;
+  bool have = false;
+  for (int l = 0; l < in->n_lists; ++l) {
+    const int cnt = in->list_n[l];
+    if (cnt < 0) continue;  // no cursor: no result from this segment
+    std::vector<Ent> cur(cnt);
+    for (int e = 0; e < cnt; ++e) {
+      const int64_t o = (int64_t)l * in->stride + e;
+      cur[e].list = l;
+      cur[e].key = in->keys[o];
+      cur[e].v.assign(in->values + o * na, in->values + o * na + na);
+    }
+    if (!have) {
+      acc.swap(cur);
+      have = true;
+      continue;
+    }
+    // retVals (LinkedHashMap): r1's entries, then r2's new values; shared values combined in place
+    std::unordered_map<std::string, size_t> pos;
+    pos.reserve(acc.size() * 2 + 16);
+    for (size_t e = 0; e < acc.size(); ++e) pos.emplace(identity(acc[e]), e);
+    for (auto& e : cur) {
+      auto it = pos.find(identity(e));
+      if (it != pos.end()) {
+        Ent& a = acc[it->second];
+        for (int k = 0; k < na; ++k) a.v[k] = combine_abi(plan.kind[k], a.v[k], e.v[k]);
+      } else {
+        pos.emplace(identity(e), acc.size());
+        acc.push_back(std::move(e));
+      }
+    }
+    build(acc, t->threshold);
+  }
+  const int nout = std::min<int>((int)acc.size(), t->threshold);
+  *out_n = have ? nout : -1;
+  for (int e = 0; e < nout; ++e) {
+    if (out_list) out_list[e] = acc[e].list;
+    if (out_keys) out_keys[e] = acc[e].key;
+    if (out_values) memcpy(out_values + (size_t)e * na, acc[e].v.data(), 8 * (size_t)na);
+  }
   return DG_OK;
 }
 
@@ -1318,9 +1595,11 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     GroupJob& j = jobs[i];
     memset(&j, 0, sizeof j);
     uint32_t* bits = nullptr;
-    int64_t cnt = 0;
-    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &cnt, st);
+    const unsigned long long* pcnt = nullptr;
+    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &pcnt, st);
     if (rc) return rc;
+    if (pcnt) DG_HIP(hipStreamSynchronize(st));  // the hash table is sized by the selected rows
+    const int64_t cnt = pcnt ? (int64_t)*pcnt : seg->nrows;
     m.pre_filtered_rows += cnt;
     j.nrows = (int32_t)seg->nrows;
     j.bitset = bits;
@@ -1413,8 +1692,8 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   int32_t* h_over = host_take<int32_t>(cs, 1);
   DG_HIP(hipMemcpyAsync(h_cnt, d_cnt, 8 * n, hipMemcpyDeviceToHost, st));
   DG_HIP(hipMemcpyAsync(h_over, d_over, 4, hipMemcpyDeviceToHost, st));
-  DG_HIP(hipStreamSynchronize(st));
-  DG_HIP(hipGetLastError());
+  rc = finish_call(cs, st);
+  if (rc) return rc;
   if (*h_over) return set_error(DG_ERR_TABLE_FULL, "groupBy hash table full");
   std::unique_ptr<dg_result> res(new dg_result());
   res->n = n;
@@ -1505,11 +1784,11 @@ extern "C" int dg_debug_lz4_profile(dg_segment* s, const char* column, uint64_t*
   memcpy(h, db.jobs.data(), sizeof(Lz4Job) * n);
   Lz4Job* d = dev_take<Lz4Job>(g.cs, n);
   int32_t* d_err = dev_take<int32_t>(g.cs, 1);
-  uint64_t* d_prof = dev_take<uint64_t>(g.cs, (size_t)n * 10);
+  uint64_t* d_prof = dev_take<uint64_t>(g.cs, (size_t)n * kLz4ProfWords);
   uint64_t* d_mtab = dev_take<uint64_t>(g.cs, (size_t)n * kLz4MatchTable);
   DG_HIP(hipMemcpyAsync(d, h, sizeof(Lz4Job) * n, hipMemcpyHostToDevice, st));
   DG_HIP(hipMemsetAsync(d_err, 0, 4, st));
-  DG_HIP(hipMemsetAsync(d_prof, 0, (size_t)n * 80, st));
+  DG_HIP(hipMemsetAsync(d_prof, 0, (size_t)n * kLz4ProfWords * 8, st));
   hipEventRecord(seg->ctx->ev[0], st);
   launch_lz4_decode(d, n, d_err, d_mtab, st, d_prof);
   hipEventRecord(seg->ctx->ev[1], st);
@@ -1517,6 +1796,6 @@ extern "C" int dg_debug_lz4_profile(dg_segment* s, const char* column, uint64_t*
   float f = 0;
   hipEventElapsedTime(&f, seg->ctx->ev[0], seg->ctx->ev[1]);
   *ms = f;
-  DG_HIP(hipMemcpy(out, d_prof, (size_t)std::min(cap, n) * 80, hipMemcpyDeviceToHost));
+  DG_HIP(hipMemcpy(out, d_prof, (size_t)std::min(cap, n) * kLz4ProfWords * 8, hipMemcpyDeviceToHost));
   return DG_OK;
 }

@@ -175,6 +175,7 @@ int load_segment(Context* ctx, const char* dir, Segment** out);
 // kernel launchers (dg_kernels.hip)
 // d_mtab: njobs * kLz4MatchTable scratch words (per-block match table of the parallel decoder)
 constexpr size_t kLz4MatchTable = kBlockBytes / 4;
+constexpr int kLz4ProfWords = 12;  // per-block words of the decoder's phase profile (diagnostic)
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, uint64_t* d_mtab, hipStream_t s,
                        uint64_t* d_prof = nullptr);
 void launch_concise_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
@@ -185,9 +186,36 @@ void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_
                         unsigned long long* d_count, hipStream_t s);
 void launch_fill_u64(uint64_t* p, int64_t n_rows_of_slots, int slots_per_row, const uint64_t* d_init, hipStream_t s);
 void launch_scan_agg(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, int topn, hipStream_t s);
-void launch_topn_select(const uint64_t* table, int64_t card, int naggs, int metric, int metric_op, int inverted,
-                        int threshold, uint64_t* d_state, int32_t* d_cand, int32_t* d_ncand, int cand_cap,
-                        hipStream_t s);
+// topN aggregation with LDS-private dictionary-id ranges: workgroup (p, s) owns ids
+// [p * range, (p + 1) * range) of segment s, scans every row of the segment and writes its range of
+// the record table with plain stores (no HBM atomics). Applicable when the table needs at most
+// kMaxIdRanges ranges; the caller skips the table fill.
+constexpr int kPartLdsBytes = 144 * 1024;
+constexpr int kMaxIdRanges = 64;
+constexpr int kPartTargetGroups = 256;  // one workgroup per CU (the LDS table fills the CU)
+inline int64_t topn_part_range(int naggs) { return kPartLdsBytes / (8 * (naggs + 1)); }
+// row splits per (segment, id range); each split writes its own [card][1 + naggs] partial table
+int topn_part_splits(int64_t max_card, int naggs, int njobs);
+void launch_topn_part(const ScanJob* d_jobs, int njobs, int64_t max_card, AggPlan plan, int splits, hipStream_t s);
+// topN selection of one segment: K-th largest metric key (8-bit radix select over all touched ids,
+// many workgroups per segment), candidate ids (key >= K-th) in id order, and the candidates'
+// records gathered into a compact buffer for one read-back.
+struct TopnSelJob {
+  const uint64_t* table;  // [card][1 + naggs] accumulator records
+  int64_t card;
+  uint64_t* state;        // [0] = K-th key, [1] = aggregated rows, [2] = touched ids (zeroed by the host)
+  int32_t* cand;          // candidate ids (capacity card)
+  int32_t* ncand;
+  uint64_t* gathered;     // [gather_cap][1 + naggs] records of cand[0 .. gather_cap)
+  uint64_t* keys;         // [card] metric keys (0 = untouched)
+  uint32_t* hist;         // [8][256] radix histograms (zeroed by the host)
+  int32_t* blkcnt;        // [ceil(card / 1024)] candidates per workgroup
+  int32_t gather_cap;
+  int32_t pad;
+};
+constexpr int kSelBlock = 1024;
+void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, int naggs, int metric, int metric_op,
+                        int inverted, int threshold, hipStream_t s);
 void launch_groupby(const GroupJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, hipStream_t s);
 void launch_groupby_compact(const uint64_t* keys, const uint64_t* slots, uint64_t cap, int nslots, uint64_t* out_keys,
                             uint64_t* out_slots, unsigned long long* d_count, hipStream_t s);

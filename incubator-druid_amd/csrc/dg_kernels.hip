@@ -15,6 +15,8 @@
 // byte work, written for 64-wide wavefronts (ballot masks are 64-bit) with coalesced row tiles.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dg_internal.h"
 
 namespace dg {
@@ -74,6 +76,97 @@ __device__ __forceinline__ uint64_t agg_input(int kind, const ColView& v, int64_
       f = (float)d;
     } else {
       f = *reinterpret_cast<const float*>(p);
+      d = (double)f;
+      l = java_d2l(d);
+    }
+  }
+  switch (kind) {
+    case DG_AGG_COUNT: return 1;
+    case DG_AGG_LONG_SUM: return (uint64_t)l;
+    case DG_AGG_DOUBLE_SUM: return (uint64_t)__double_as_longlong(d);
+    case DG_AGG_FLOAT_SUM: return (uint64_t)__double_as_longlong((double)f);
+    case DG_AGG_LONG_MIN:
+    case DG_AGG_LONG_MAX: return (uint64_t)l ^ kSign;
+    case DG_AGG_DOUBLE_MIN: return d != d ? 0ull : ord_key(d);
+    case DG_AGG_DOUBLE_MAX: return d != d ? ~0ull : ord_key(d);
+    case DG_AGG_FLOAT_MIN: return f != f ? 0ull : ord_key((double)f);
+    default: return f != f ? ~0ull : ord_key((double)f);  // FLOAT_MAX
+  }
+}
+
+// ---- four consecutive rows r .. r + 3 (r % 4 == 0, all inside the view's block): one or a few
+// wide loads per column instead of four scalar ones; consecutive threads read consecutive quads, so
+// every load instruction of a wave is one contiguous span ----
+__device__ __forceinline__ void load_ids4(const ColView& v, int64_t r, uint32_t id[4]) {
+  const uint8_t* p = cv_ptr(v, r);
+  switch (v.width) {
+    case 1: {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) id[k] = (w >> (8 * k)) & 0xFF;
+      break;
+    }
+    case 2: {
+      const uint2 w = *reinterpret_cast<const uint2*>(p);
+      id[0] = w.x & 0xFFFF;
+      id[1] = w.x >> 16;
+      id[2] = w.y & 0xFFFF;
+      id[3] = w.y >> 16;
+      break;
+    }
+    case 3: {
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+      const uint32_t a = q[0], b = q[1], c = q[2];
+      id[0] = a & 0xFFFFFF;
+      id[1] = (a >> 24) | ((b & 0xFFFF) << 8);
+      id[2] = (b >> 16) | ((c & 0xFF) << 16);
+      id[3] = c >> 8;
+      break;
+    }
+    default: {
+      const uint4 w = *reinterpret_cast<const uint4*>(p);
+      id[0] = w.x;
+      id[1] = w.y;
+      id[2] = w.z;
+      id[3] = w.w;
+    }
+  }
+}
+
+// raw 8-byte lanes of a numeric view for rows r .. r + 3 (float views: 4-byte values in the low half)
+__device__ __forceinline__ void load_raw4(const ColView& v, int64_t r, uint64_t x[4]) {
+  const uint8_t* p = cv_ptr(v, r);
+  if (v.kind == VIEW_FLOAT) {
+    const uint4 w = *reinterpret_cast<const uint4*>(p);
+    x[0] = w.x;
+    x[1] = w.y;
+    x[2] = w.z;
+    x[3] = w.w;
+  } else {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+    x[0] = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    x[1] = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    x[2] = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    x[3] = (uint64_t)b.z | ((uint64_t)b.w << 32);
+  }
+}
+
+// agg_input on an already loaded raw lane (same coercions)
+__device__ __forceinline__ uint64_t agg_input_raw(int kind, int view_kind, uint64_t raw) {
+  int64_t l = 0;
+  double d = 0.0;
+  float f = 0.0f;
+  if (kind != DG_AGG_COUNT && view_kind != VIEW_ABSENT) {
+    if (view_kind == VIEW_LONG) {
+      l = (int64_t)raw;
+      d = (double)l;
+      f = (float)l;
+    } else if (view_kind == VIEW_DOUBLE) {
+      d = __longlong_as_double((long long)raw);
+      l = java_d2l(d);
+      f = (float)d;
+    } else {
+      f = __uint_as_float((uint32_t)raw);
       d = (double)f;
       l = java_d2l(d);
     }
@@ -506,6 +599,151 @@ void launch_scan_agg(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntile
 }
 
 // ------------------------------------------------------------------------------------------------
+// topN aggregation, LDS-privatised by dictionary-id range (PooledTopNAlgorithm's per-id records,
+// PooledTopNAlgorithm.java:661-719, held in LDS instead of a 1 GiB ByteBuffer). ScanJob.nbuckets
+// carries the segment's cardinality.
+// ------------------------------------------------------------------------------------------------
+constexpr int kPartThreads = 1024;
+constexpr int kPartUnroll = 4;
+
+// rows of the quad that pass the bitset and the interval (bit k = row r + k)
+__device__ __forceinline__ unsigned quad_selected(const ScanJob& j, int64_t r) {
+  unsigned m = 0xF;
+  if (j.bitset) m = (j.bitset[r >> 5] >> (r & 31)) & 0xF;
+  if (m && j.time.kind != VIEW_ABSENT) {
+    uint64_t t[4];
+    load_raw4(j.time, r, t);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((int64_t)t[k] < j.t_lo || (int64_t)t[k] >= j.t_hi) m &= ~(1u << k);
+  }
+  return m;
+}
+
+// workgroup (x = range * splits + split, y = segment): ids [range_lo, range_hi) of the segment,
+// rows of one split; the range goes to partial table `split` with plain stores
+__global__ __launch_bounds__(kPartThreads) void k_topn_part(const ScanJob* __restrict__ jobs, AggPlan plan, int64_t range,
+                                                            int splits) {
+  extern __shared__ uint64_t s_tab[];
+  const ScanJob& j = jobs[blockIdx.y];
+  const int64_t card = j.nbuckets;
+  const int split = (int)(blockIdx.x % splits);
+  const int64_t lo = (int64_t)(blockIdx.x / splits) * range;
+  if (lo >= card) return;
+  const int64_t hi = min(card, lo + range);
+  const int na = plan.n, rec = na + 1;
+  const int64_t nslots = (hi - lo) * rec;
+  for (int64_t x = threadIdx.x; x < nslots; x += kPartThreads) {
+    const int s = (int)(x % rec);
+    s_tab[x] = s == 0 ? 0ull : identity_of(plan.op[s - 1], plan.kind[s - 1]);
+  }
+  __syncthreads();
+  // rows of this split, in whole quads; kPartUnroll quads per thread are in flight at once
+  const int64_t nrows = j.nrows;
+  const int64_t nfull = nrows >> 2;  // quads without a ragged tail
+  const int64_t nquads = (nrows + 3) >> 2;
+  const int64_t qper = (nquads + splits - 1) / splits;
+  const int64_t q0 = split * qper, q1 = min(nquads, q0 + qper), q1f = min(q1, nfull);
+  for (int64_t qb = q0 + threadIdx.x; qb < q1f; qb += kPartThreads * kPartUnroll) {
+    uint32_t id[kPartUnroll][4];
+    unsigned m[kPartUnroll];
+#pragma unroll
+    for (int u = 0; u < kPartUnroll; ++u) {
+      const int64_t q = qb + (int64_t)u * kPartThreads;
+      m[u] = 0;
+      if (q < q1f) {
+        m[u] = quad_selected(j, q << 2);
+        load_ids4(j.key, q << 2, id[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPartUnroll; ++u) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((int64_t)id[u][k] < lo || (int64_t)id[u][k] >= hi) m[u] &= ~(1u << k);
+    }
+#pragma unroll
+    for (int u = 0; u < kPartUnroll; ++u) {
+      if (!m[u]) continue;
+      const int64_t r = (qb + (int64_t)u * kPartThreads) << 2;
+      uint64_t* e[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        e[k] = s_tab + ((int64_t)id[u][k] - lo) * rec;
+        if ((m[u] >> k) & 1) atomicAdd(reinterpret_cast<unsigned long long*>(e[k]), 1ull);
+      }
+      for (int a = 0; a < na; ++a) {  // one column at a time keeps four lanes of it in registers
+        uint64_t raw[4] = {0, 0, 0, 0};
+        const int vk = j.vals[a].kind;
+        if (plan.kind[a] != DG_AGG_COUNT && vk != VIEW_ABSENT) load_raw4(j.vals[a], r, raw);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((m[u] >> k) & 1) atomic_op(plan.op[a], e[k] + 1 + a, agg_input_raw(plan.kind[a], vk, raw[k]));
+      }
+    }
+  }
+  if (q1 > nfull && threadIdx.x == 0) {  // the segment's ragged last quad
+    for (int64_t rr = nfull << 2; rr < nrows; ++rr) {
+      int64_t b;
+      if (!row_selected(j, rr, &b)) continue;
+      const int64_t id = (int64_t)load_id(j.key, rr);
+      if (id < lo || id >= hi) continue;
+      uint64_t* e = s_tab + (id - lo) * rec;
+      atomicAdd(reinterpret_cast<unsigned long long*>(e), 1ull);
+      for (int a = 0; a < na; ++a) atomic_op(plan.op[a], e + 1 + a, agg_input(plan.kind[a], j.vals[a], rr));
+    }
+  }
+  __syncthreads();
+  uint64_t* out = j.out + (size_t)split * (size_t)card * rec + lo * rec;
+  for (int64_t x = threadIdx.x; x < nslots; x += kPartThreads) out[x] = s_tab[x];
+}
+
+// fold the split partial tables into table 0
+__global__ __launch_bounds__(256) void k_topn_combine(const ScanJob* __restrict__ jobs, AggPlan plan, int splits) {
+  const ScanJob& j = jobs[blockIdx.y];
+  const int64_t card = j.nbuckets;
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (id >= card) return;
+  const int rec = plan.n + 1;
+  uint64_t* e = j.out + id * rec;
+  uint64_t acc[kMaxAggs + 1];
+#pragma unroll
+  for (int a = 0; a <= kMaxAggs; ++a)
+    if (a < rec) acc[a] = e[a];
+  for (int s = 1; s < splits; ++s) {
+    const uint64_t* f = j.out + ((size_t)s * card + id) * rec;
+    acc[0] += f[0];
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; ++a)
+      if (a < plan.n) acc[1 + a] = combine_op(plan.op[a], acc[1 + a], f[1 + a]);
+  }
+#pragma unroll
+  for (int a = 0; a <= kMaxAggs; ++a)
+    if (a < rec) e[a] = acc[a];
+}
+
+int topn_part_splits(int64_t max_card, int naggs, int njobs) {
+  const int64_t ranges = (max_card + topn_part_range(naggs) - 1) / topn_part_range(naggs);
+  const int64_t groups = std::max<int64_t>(1, ranges * njobs);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(16, kPartTargetGroups / groups));
+}
+
+void launch_topn_part(const ScanJob* d_jobs, int njobs, int64_t max_card, AggPlan plan, int splits, hipStream_t s) {
+  if (njobs <= 0 || max_card <= 0) return;
+  const int64_t range = topn_part_range(plan.n);
+  const int64_t ranges = (max_card + range - 1) / range;
+  const dim3 grid((unsigned)(ranges * splits), (unsigned)njobs);
+  const size_t lds = (size_t)std::min<int64_t>(range, max_card) * (plan.n + 1) * 8;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_topn_part),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kPartLdsBytes);
+  (void)attr;
+  hipLaunchKernelGGL(k_topn_part, grid, dim3(kPartThreads), lds, s, d_jobs, plan, range, splits);
+  if (splits > 1)
+    hipLaunchKernelGGL(k_topn_combine, dim3((unsigned)((max_card + 255) / 256), (unsigned)njobs), dim3(256), 0, s,
+                       d_jobs, plan, splits);
+}
+
+// ------------------------------------------------------------------------------------------------
 // topN selection for one segment: the K-th largest metric key among touched ids (8-bit radix
 // select over the ordered key), then the ids whose key >= that K-th key, compacted in id order.
 // The host replays TopNNumericResultBuilder's priority queue over those candidates only (ids with a
@@ -536,110 +774,220 @@ __device__ __forceinline__ uint64_t metric_key(uint64_t slot, int op, int kind, 
   return inverted ? ~k : k;
 }
 
-__global__ __launch_bounds__(1024) void k_topn_select(const uint64_t* __restrict__ table, int64_t card, int naggs,
-                                                      int metric, int op, int kind, int inverted, int threshold,
-                                                      uint64_t* __restrict__ state, int32_t* __restrict__ cand,
-                                                      int32_t* __restrict__ ncand, int cand_cap) {
-  __shared__ unsigned int s_hist[256];
-  __shared__ uint64_t s_prefix, s_mask;
-  __shared__ int64_t s_krem, s_touched;
-  __shared__ int64_t s_tmp[16];
-  const int rec = naggs + 1;
-  if (threadIdx.x == 0) {
-    s_prefix = 0;
-    s_mask = 0;
-    s_krem = threshold;
-    s_touched = 0;
-  }
-  __syncthreads();
-  // count touched ids and aggregated rows
-  __shared__ unsigned long long s_rows;
-  if (threadIdx.x == 0) s_rows = 0;
-  __syncthreads();
-  {
-    unsigned long long c = 0, rows = 0;
-    for (int64_t i = threadIdx.x; i < card; i += blockDim.x) {
-      const uint64_t n = table[i * rec];
-      c += n != 0;
-      rows += n;
+// Replay the radix digit choices of levels [0, levels) from the histograms: wave-parallel (64 lanes x
+// 4 bins, descending digit order), result in (*prefix, *mask). Called by one full wave.
+__device__ void replay_digits(const uint32_t* __restrict__ hist, int levels, int64_t threshold, uint64_t* prefix_out,
+                              uint64_t* mask_out) {
+  const int lane = threadIdx.x & 63;
+  uint64_t prefix = 0, mask = 0;
+  int64_t krem = threshold;
+  for (int q = 0; q < levels; ++q) {
+    const int shift = 56 - 8 * q;
+    int64_t h[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      h[j] = hist[q * 256 + 255 - (lane * 4 + j)];
+      sum += h[j];
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      c += __shfl_down(c, o, 64);
-      rows += __shfl_down(rows, o, 64);
+    int64_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
     }
-    if ((threadIdx.x & 63) == 0) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(&s_touched), c);
-      atomicAdd(&s_rows, rows);
-    }
-  }
-  __syncthreads();
-  uint64_t kth = 0;  // keep everything when touched <= threshold
-  if (s_touched > threshold) {
-    for (int shift = 56; shift >= 0; shift -= 8) {
-      for (int i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0;
-      __syncthreads();
-      const uint64_t prefix = s_prefix, mask = s_mask;
-      for (int64_t i = threadIdx.x; i < card; i += blockDim.x) {
-        if (table[i * rec] == 0) continue;
-        const uint64_t k = metric_key(table[i * rec + 1 + metric], op, kind, inverted);
-        if ((k & mask) == prefix) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        int64_t cum = 0, krem = s_krem;
-        for (int dgt = 255; dgt >= 0; --dgt) {
-          const int64_t h = s_hist[dgt];
-          if (cum + h >= krem) {
-            s_prefix = prefix | ((uint64_t)dgt << shift);
-            s_mask = mask | (255ull << shift);
-            s_krem = krem - cum;
-            break;
-          }
-          cum += h;
+    const int64_t excl = incl - sum;
+    const bool hit = excl < krem && incl >= krem;
+    const unsigned long long bm = __ballot(hit);
+    int digit = 0;
+    int64_t nk = krem;
+    if (hit) {
+      int64_t cum = excl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (cum + h[j] >= krem) {
+          digit = 255 - (lane * 4 + j);
+          nk = krem - cum;
+          break;
         }
+        cum += h[j];
       }
-      __syncthreads();
     }
-    kth = s_prefix;
+    if (bm) {
+      const int src = __ffsll((long long)bm) - 1;
+      digit = __shfl(digit, src, 64);
+      nk = __shfl(nk, src, 64);
+    }
+    prefix |= (uint64_t)digit << shift;
+    mask |= 255ull << shift;
+    krem = nk;
   }
-  // ordered compaction of touched ids with key >= kth
-  int64_t base = 0;
-  for (int64_t start = 0; start < card; start += blockDim.x) {
-    const int64_t i = start + threadIdx.x;
-    int f = 0;
-    if (i < card && table[i * rec] != 0) f = metric_key(table[i * rec + 1 + metric], op, kind, inverted) >= kth;
-    // block scan over 1024 threads (16 waves)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long m = __ballot(f);
-    const int below = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) s_tmp[wave] = __popcll(m);
-    __syncthreads();
-    int64_t woff = 0, tot = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-      if (w < wave) woff += s_tmp[w];
-      tot += s_tmp[w];
-    }
-    if (f) {
-      const int64_t pos = base + woff + below;
-      if (pos < cand_cap) cand[pos] = (int32_t)i;
-    }
-    base += tot;
-    __syncthreads();
-  }
+  *prefix_out = prefix;
+  *mask_out = mask;
+}
+
+// pass 0: metric keys, touched / row counts, histogram of the top byte
+__global__ __launch_bounds__(kSelBlock) void k_topn_keys(const TopnSelJob* __restrict__ jobs, int naggs, int metric,
+                                                         int op, int kind, int inverted) {
+  __shared__ unsigned int s_hist[256];
+  __shared__ unsigned long long s_c, s_rows;
+  const TopnSelJob& jb = jobs[blockIdx.y];
+  const int64_t i = (int64_t)blockIdx.x * kSelBlock + threadIdx.x;
+  if ((int64_t)blockIdx.x * kSelBlock >= jb.card) return;
+  if (threadIdx.x < 256) s_hist[threadIdx.x] = 0;
   if (threadIdx.x == 0) {
-    *ncand = (int32_t)(base < 0x7fffffff ? base : 0x7fffffff);
-    state[0] = kth;
-    state[1] = s_rows;
+    s_c = 0;
+    s_rows = 0;
+  }
+  __syncthreads();
+  const int rec = naggs + 1;
+  unsigned long long c = 0, rows = 0;
+  if (i < jb.card) {
+    const uint64_t n = jb.table[i * rec];
+    uint64_t k = 0;
+    if (n) {
+      k = metric_key(jb.table[i * rec + 1 + metric], op, kind, inverted);
+      k = k ? k : 1;  // 0 marks untouched ids; a touched key of 0 becomes 1 (only widens the candidates)
+      atomicAdd(&s_hist[k >> 56], 1u);
+    }
+    jb.keys[i] = k;
+    c = n != 0;
+    rows = n;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_down(c, o, 64);
+    rows += __shfl_down(rows, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&s_c, c);
+    atomicAdd(&s_rows, rows);
+  }
+  __syncthreads();
+  if (threadIdx.x < 256 && s_hist[threadIdx.x]) atomicAdd(&jb.hist[threadIdx.x], s_hist[threadIdx.x]);
+  if (threadIdx.x == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&jb.state[2]), s_c);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&jb.state[1]), s_rows);
   }
 }
 
-void launch_topn_select(const uint64_t* table, int64_t card, int naggs, int metric, int metric_op, int inverted,
-                        int threshold, uint64_t* d_state, int32_t* d_cand, int32_t* d_ncand, int cand_cap,
-                        hipStream_t s) {
-  (void)metric_op;
+// pass `level` (1..7): histogram of byte (56 - 8 level) among keys matching the chosen prefix
+__global__ __launch_bounds__(kSelBlock) void k_topn_radix(const TopnSelJob* __restrict__ jobs, int level, int threshold) {
+  __shared__ unsigned int s_hist[256];
+  __shared__ uint64_t s_prefix, s_mask;
+  const TopnSelJob& jb = jobs[blockIdx.y];
+  if ((int64_t)blockIdx.x * kSelBlock >= jb.card) return;
+  if ((int64_t)jb.state[2] <= threshold) return;  // everything touched is a candidate
+  if (threadIdx.x < 64) {
+    uint64_t p, m;
+    replay_digits(jb.hist, level, threshold, &p, &m);
+    if (threadIdx.x == 0) {
+      s_prefix = p;
+      s_mask = m;
+    }
+  }
+  if (threadIdx.x < 256) s_hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kSelBlock + threadIdx.x;
+  const int shift = 56 - 8 * level;
+  if (i < jb.card) {
+    const uint64_t k = jb.keys[i];
+    if (k && (k & s_mask) == s_prefix) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 256 && s_hist[threadIdx.x]) atomicAdd(&jb.hist[level * 256 + threadIdx.x], s_hist[threadIdx.x]);
+}
+
+__device__ __forceinline__ uint64_t sel_kth(const TopnSelJob& jb, int threshold, uint64_t* s_kth) {
+  if (threadIdx.x < 64) {
+    uint64_t p = 0, m = 0;
+    if ((int64_t)jb.state[2] > threshold) replay_digits(jb.hist, 8, threshold, &p, &m);
+    if (threadIdx.x == 0) *s_kth = p;
+  }
+  __syncthreads();
+  return *s_kth;
+}
+
+// candidates per workgroup
+__global__ __launch_bounds__(kSelBlock) void k_topn_count(const TopnSelJob* __restrict__ jobs, int threshold) {
+  __shared__ uint64_t s_kth;
+  __shared__ int s_n;
+  const TopnSelJob& jb = jobs[blockIdx.y];
+  if ((int64_t)blockIdx.x * kSelBlock >= jb.card) return;
+  const uint64_t kth = sel_kth(jb, threshold, &s_kth);
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kSelBlock + threadIdx.x;
+  int f = 0;
+  if (i < jb.card) {
+    const uint64_t k = jb.keys[i];
+    f = k != 0 && k >= kth;
+  }
+  const unsigned long long m = __ballot(f);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_n, __popcll(m));
+  __syncthreads();
+  if (threadIdx.x == 0) jb.blkcnt[blockIdx.x] = s_n;
+}
+
+// ordered compaction of the candidates + gather of their records
+__global__ __launch_bounds__(kSelBlock) void k_topn_compact(const TopnSelJob* __restrict__ jobs, int naggs, int threshold) {
+  __shared__ uint64_t s_kth;
+  __shared__ int s_wave[kSelBlock / 64];
+  __shared__ long long s_base, s_total;
+  const TopnSelJob& jb = jobs[blockIdx.y];
+  if ((int64_t)blockIdx.x * kSelBlock >= jb.card) return;
+  const uint64_t kth = sel_kth(jb, threshold, &s_kth);
+  const int nblk = (int)((jb.card + kSelBlock - 1) / kSelBlock);
+  if (threadIdx.x < 64) {
+    long long before = 0, total = 0;
+    for (int b = threadIdx.x; b < nblk; b += 64) {
+      const int c = jb.blkcnt[b];
+      total += c;
+      before += b < (int)blockIdx.x ? c : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      before += __shfl_down(before, o, 64);
+      total += __shfl_down(total, o, 64);
+    }
+    if (threadIdx.x == 0) {
+      s_base = before;
+      s_total = total;
+    }
+  }
+  const int64_t i = (int64_t)blockIdx.x * kSelBlock + threadIdx.x;
+  int f = 0;
+  if (i < jb.card) {
+    const uint64_t k = jb.keys[i];
+    f = k != 0 && k >= kth;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long m = __ballot(f);
+  if (lane == 0) s_wave[wave] = __popcll(m);
+  __syncthreads();
+  if (f) {
+    long long pos = s_base + __popcll(m & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wave; ++w) pos += s_wave[w];
+    jb.cand[pos] = (int32_t)i;
+    if (pos < jb.gather_cap) {
+      const int rec = naggs + 1;
+      for (int c = 0; c < rec; ++c) jb.gathered[pos * rec + c] = jb.table[i * rec + c];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *jb.ncand = (int32_t)(s_total < 0x7fffffff ? s_total : 0x7fffffff);
+    jb.state[0] = kth;
+  }
+}
+
+void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, int naggs, int metric, int metric_op,
+                        int inverted, int threshold, hipStream_t s) {
+  if (njobs <= 0 || max_card <= 0) return;
+  const dim3 grid((unsigned)((max_card + kSelBlock - 1) / kSelBlock), (unsigned)njobs);
   // metric_op encodes (op << 8) | kind
-  hipLaunchKernelGGL(k_topn_select, dim3(1), dim3(1024), 0, s, table, card, naggs, metric, metric_op >> 8,
-                     metric_op & 255, inverted, threshold, d_state, d_cand, d_ncand, cand_cap);
+  hipLaunchKernelGGL(k_topn_keys, grid, dim3(kSelBlock), 0, s, d_jobs, naggs, metric, metric_op >> 8, metric_op & 255,
+                     inverted);
+  for (int level = 1; level < 8; ++level)
+    hipLaunchKernelGGL(k_topn_radix, grid, dim3(kSelBlock), 0, s, d_jobs, level, threshold);
+  hipLaunchKernelGGL(k_topn_count, grid, dim3(kSelBlock), 0, s, d_jobs, threshold);
+  hipLaunchKernelGGL(k_topn_compact, grid, dim3(kSelBlock), 0, s, d_jobs, naggs, threshold);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -31,13 +31,23 @@
 
 namespace dg {
 
-constexpr int kLzThreads = 256;
+constexpr int kLzThreads = 1024;               // 16 waves: 4 per SIMD hide LDS latency
+constexpr int kLzWaves = kLzThreads / 64;
+constexpr int kMinChunk = 32;                  // bytes of compressed input per speculative chunk (min)
 constexpr int kLz4InCap = kBlockBytes + 2048;  // >= LZ4_compressBound(65536) = 65809
 constexpr int kLongLit = 32;                   // literal runs above this are copied cooperatively
 constexpr int kLongFill = 64;                  // match spans above this fill P cooperatively
 constexpr int kMaxJobs = 512;
 constexpr int kHalf = kBlockBytes / 2;
 constexpr int kMaxJumpRounds = 40;
+constexpr int kFixRounds = 8;                  // parallel entry fix-point rounds before the serial stitch
+constexpr int kSeqFraction = 4;                // > 1/4 of chunks inconsistent after one round and a
+                                               // compression ratio < 1.05: walk the tokens serially
+constexpr int kJumpBatch = 8;                  // independent pointer chases in flight per thread
+// per-chunk arrays live in the output buffer while it is free (phases 1-3), after the visited bitmap
+constexpr int kChunkArrOff = 16384;
+static_assert(kChunkArrOff >= (kLz4InCap + 64) / 8, "visited bitmap overlaps the chunk arrays");
+static_assert(kChunkArrOff + 4 * kLzThreads * 4 <= kBlockBytes, "chunk arrays exceed the output buffer");
 
 struct Tok {
   int lit;   // literal start (input offset)
@@ -47,20 +57,32 @@ struct Tok {
   int next;  // next token start
 };
 
+// LZ4 extended length: sum of bytes up to and including the first byte != 255. Runs of 255 (long
+// zero runs in dictionary-id blocks: a 64 KiB match is 256 of them) are skipped 16 bytes at a time.
+__device__ __forceinline__ bool ext_len(const uint8_t* __restrict__ in, int n, int& q, int& len) {
+  for (;;) {
+    if ((q & 15) == 0 && q + 16 <= n) {
+      const uint4 w = *reinterpret_cast<const uint4*>(in + q);
+      if ((w.x & w.y & w.z & w.w) == 0xFFFFFFFFu) {
+        len += 16 * 255;
+        q += 16;
+        continue;
+      }
+    }
+    if (q >= n) return false;
+    const int b = in[q++];
+    len += b;
+    if (b != 255) return true;
+  }
+}
+
 // Byte-wise parse (long lengths / windows that do not hold the offset).
 __device__ __forceinline__ bool parse_tok_slow(const uint8_t* __restrict__ in, int n, int p, Tok& t) {
   if (p >= n) return false;
   const int tk = in[p];
   int q = p + 1;
   int L = tk >> 4;
-  if (L == 15) {
-    int b;
-    do {
-      if (q >= n) return false;
-      b = in[q++];
-      L += b;
-    } while (b == 255);
-  }
+  if (L == 15 && !ext_len(in, n, q, L)) return false;
   t.lit = q;
   t.L = L;
   q += L;
@@ -75,14 +97,7 @@ __device__ __forceinline__ bool parse_tok_slow(const uint8_t* __restrict__ in, i
   t.off = (int)in[q] | ((int)in[q + 1] << 8);
   q += 2;
   int M = tk & 15;
-  if (M == 15) {
-    int b;
-    do {
-      if (q >= n) return false;
-      b = in[q++];
-      M += b;
-    } while (b == 255);
-  }
+  if (M == 15 && !ext_len(in, n, q, M)) return false;
   t.M = M + 4;
   t.next = q;
   return t.off != 0;
@@ -130,7 +145,7 @@ __device__ __forceinline__ int walk_to_exit(const uint8_t* __restrict__ in, int 
   return pos;
 }
 
-// block-wide (256 threads) exclusive scan; total via *total
+// block-wide exclusive scan; total via *total
 __device__ int block_scan_lz(int v, int* total, int* s_tmp) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int x = v;
@@ -143,32 +158,28 @@ __device__ int block_scan_lz(int v, int* total, int* s_tmp) {
   __syncthreads();
   int wave_off = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < (kLzThreads >> 6); ++w) {
-    if (w < wave) wave_off += s_tmp[w];
-    tot += s_tmp[w];
+  for (int w = 0; w < kLzWaves; ++w) {
+    const int y = s_tmp[w];
+    wave_off += w < wave ? y : 0;
+    tot += y;
   }
   __syncthreads();
   *total = tot;
   return wave_off + x - v;
 }
 
-#define LZ_STAMP(k)                                                                      \
-  do {                                                                                   \
-    if (prof && tid == 0) prof[(size_t)blockIdx.x * 10 + (k)] = __builtin_amdgcn_s_memtime(); \
+#define LZ_STAMP(k)                                                                                   \
+  do {                                                                                                \
+    if (prof && tid == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
 __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
                                                            uint64_t* __restrict__ mtab_all, uint64_t* __restrict__ prof) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kBlockBytes + 64];
-  __shared__ int s_x[kLzThreads];      // speculative exit of each chunk
-  __shared__ int s_pexit[kLzThreads];  // exit assuming entry = s_x[i-1]
-  __shared__ int s_e2[kLzThreads];     // corrected entry guess (= s_pexit[i-1]) or -1
-  __shared__ int s_pexit2[kLzThreads]; // exit assuming entry = s_e2[i]
-  __shared__ int s_t[kLzThreads];      // true entry
   __shared__ int s_job[kMaxJobs][3];
-  __shared__ int s_njob, s_bad;
-  __shared__ int s_tmp[8];
+  __shared__ int s_njob, s_bad, s_slow, s_e2hit;
+  __shared__ int s_tmp[kLzWaves];
 
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -178,30 +189,38 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     if (tid == 0) atomicOr(err, 1);
     return;
   }
-  uint64_t* mtab = mtab_all + (size_t)blockIdx.x * (kBlockBytes / 4);
-  // ---- stage input; clear the visited bitmap (aliases the output buffer) ----
+  uint64_t* mtab = mtab_all + (size_t)blockIdx.x * kLz4MatchTable;
+  uint32_t* vb = reinterpret_cast<uint32_t*>(s_out);  // visited bitmap (phases 1-2)
+  int* s_x = reinterpret_cast<int*>(s_out + kChunkArrOff);  // speculative exit of each chunk
+  int* s_E = s_x + kLzThreads;                              // entry guess of each chunk
+  int* s_P = s_E + kLzThreads;                              // exit of each chunk from its entry guess
+  int* s_t = s_P + kLzThreads;                              // true entry
+  // ---- stage input; clear the visited bitmap ----
   {
     const uint4* src = reinterpret_cast<const uint4*>(job.src);
     uint4* dst = reinterpret_cast<uint4*>(s_in);
     const int n16 = (n + 15) >> 4;
     for (int i = tid; i < n16; i += kLzThreads) dst[i] = src[i];
     if (tid == 0) *reinterpret_cast<uint4*>(s_in + (n16 << 4)) = make_uint4(0, 0, 0, 0);
-    uint32_t* vb = reinterpret_cast<uint32_t*>(s_out);
     const int nw = (n + 32) >> 5;
     for (int i = tid; i < nw; i += kLzThreads) vb[i] = 0;
     if (tid == 0) {
       s_njob = 0;
       s_bad = 0;
+      s_slow = 0;
+      s_e2hit = 0;
     }
   }
   __syncthreads();
   LZ_STAMP(1);
-  uint32_t* vb = reinterpret_cast<uint32_t*>(s_out);
-  const int CH = (n + kLzThreads - 1) / kLzThreads;
-  const int cs = min(tid * CH, n), ce = min(cs + CH, n);
+  // chunking: NC chunks of CH bytes (threads >= NC only help in the cooperative phases)
+  const int NC = max(1, min(kLzThreads, n / kMinChunk));
+  const int CH = (n + NC - 1) / NC;
+  const bool has_chunk = tid < NC;
+  const int cs = has_chunk ? min(tid * CH, n) : n, ce = has_chunk ? min(cs + CH, n) : n;
 
   // ---- 1. speculative walk of my chunk ----
-  {
+  if (has_chunk) {
     int pos = cs;
     while (pos < ce) {
       atomicOr(&vb[pos >> 5], 1u << (pos & 31));
@@ -216,48 +235,78 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   }
   __syncthreads();
   LZ_STAMP(2);
-  // ---- 2. exits for the assumed entry, then for the corrected entry where the predecessor missed ----
-  const int x_me = s_x[tid];
-  {
-    const int a = tid == 0 ? 0 : s_x[tid - 1];
-    s_pexit[tid] = a >= ce ? a : walk_to_exit(s_in, n, a, ce, vb, x_me);
+  // ---- 2. entry fix-point: chunk i's entry guess E_i starts as the speculative exit of chunk i-1,
+  // P_i = exit of chunk i from E_i; then rounds of E_i <- P_{i-1} (in parallel, re-walking only chunks
+  // whose guess changed) until nothing changes or kFixRounds. Chains are functions of position and
+  // merge quickly, so a few rounds make nearly every chunk consistent (P_i == E_{i+1}); wave 0 then
+  // stitches the true chain from chunk 0, 64 consistent chunks per ballot. ----
+  const int x_me = has_chunk ? s_x[tid] : n;
+  int myE = n, myP = n;
+  if (has_chunk) {
+    myE = tid == 0 ? 0 : s_x[tid - 1];
+    myP = myE >= ce ? myE : walk_to_exit(s_in, n, myE, ce, vb, x_me);
+    s_E[tid] = myE;
+    s_P[tid] = myP;
   }
-  __syncthreads();
-  {
-    int e2 = -1, p2 = 0;
-    if (tid > 0 && s_pexit[tid - 1] != s_x[tid - 1]) {
-      e2 = s_pexit[tid - 1];
-      p2 = e2 >= ce ? e2 : walk_to_exit(s_in, n, e2, ce, vb, x_me);
+  // Literal-heavy blocks (near-incompressible data: few, long tokens) give speculative chains that
+  // rarely merge (a wrong parse lands on a true token start about once per token length); there one
+  // lane simply walks the true tokens and records every chunk's entry. Dense blocks with the same
+  // first-round inconsistency converge in a few fix-point rounds instead.
+  const int inconsistent = __syncthreads_count(has_chunk && tid + 1 < NC && myP != s_E[tid + 1]);
+  const bool sequential = inconsistent * kSeqFraction > NC && n * 20 > job.expect_len * 19;
+  int fix_rounds = 0;
+  if (sequential) {
+    if (tid == 0) {
+      int pos = 0, k = 0, bad = 0;
+      while (pos < n) {
+        while (k < NC && k * CH <= pos) s_t[k++] = pos;
+        Tok t;
+        if (!parse_tok(s_in, n, pos, t)) {
+          bad = 1;
+          break;
+        }
+        pos = t.next;
+      }
+      while (k < NC) s_t[k++] = n;
+      s_bad = bad;
+      s_slow = 0;
+      s_e2hit = -1;
     }
-    s_e2[tid] = e2;
-    s_pexit2[tid] = p2;
+    __syncthreads();
   }
-  __syncthreads();
+  for (int r = 0; r < kFixRounds && !sequential; ++r) {
+    const int newE = (has_chunk && tid > 0) ? s_P[tid - 1] : myE;
+    const bool changed = newE != myE;
+    __syncthreads();  // every read of s_P precedes this round's writes
+    if (changed) {
+      myE = newE;
+      myP = myE >= ce ? myE : walk_to_exit(s_in, n, myE, ce, vb, x_me);
+      s_E[tid] = myE;
+      s_P[tid] = myP;
+    }
+    fix_rounds++;
+    if (!__syncthreads_or(changed)) break;
+  }
   LZ_STAMP(3);
-  if (wave == 0) {
-    int cur = 0, i = 0;
-    while (i < kLzThreads) {
-      const int assumed = i == 0 ? 0 : s_x[i - 1];
-      if (cur == assumed) {
-        // a run of chunks whose speculative chain absorbed the assumed entry: one ballot
+  if (wave == 0 && !sequential) {
+    int cur = 0, i = 0, slow = 0;
+    while (i < NC) {
+      if (cur == s_E[i]) {
+        // a run of consistent chunks: one ballot
         const int idx = i + lane;
-        const bool valid = idx < kLzThreads;
-        const bool ok = valid && s_pexit[idx] == s_x[idx];
+        const bool valid = idx < NC;
+        const bool ok = valid && (idx == NC - 1 || s_P[idx] == s_E[idx + 1]);
         const unsigned long long badm = __ballot(valid && !ok);
         const int first_bad = badm ? (__ffsll((long long)badm) - 1) : 64;
-        const int upto = min(first_bad + 1, kLzThreads - i);
-        if (lane < upto) s_t[idx] = idx == 0 ? 0 : s_x[idx - 1];
-        if (first_bad < 64 && i + first_bad < kLzThreads) {
-          cur = s_pexit[i + first_bad];
+        const int upto = min(first_bad + 1, NC - i);
+        if (lane < upto) s_t[idx] = s_E[idx];
+        if (first_bad < 64 && i + first_bad < NC) {
+          cur = s_P[i + first_bad];
           i = i + first_bad + 1;
         } else {
-          i = min(i + 64, kLzThreads);
-          cur = s_x[i - 1];
+          i = min(i + 64, NC);
+          cur = s_P[i - 1];
         }
-      } else if (cur == s_e2[i]) {
-        if (lane == 0) s_t[i] = cur;
-        cur = s_pexit2[i];
-        i++;
       } else {
         int next_i = i + 1, next_cur = cur;
         if (lane == 0) {
@@ -265,7 +314,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
           if (cur >= ci_e) {
             // a long token covers whole chunks: they contain no token start
             int j = cur / CH;
-            if (j > kLzThreads) j = kLzThreads;
+            if (j > NC) j = NC;
             if (j <= i) j = i + 1;
             for (int k = i; k < j; ++k) s_t[k] = cur;
             next_i = j;
@@ -276,13 +325,18 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         }
         i = __shfl(next_i, 0, 64);
         cur = __shfl(next_cur, 0, 64);
+        slow++;
       }
+    }
+    if (tid == 0) {
+      s_slow = slow;
+      s_e2hit = fix_rounds;
     }
   }
   __syncthreads();
   LZ_STAMP(4);
   // ---- 3. sizes of my chunk's true tokens -> output offsets, match-table offsets ----
-  const int my_t = s_t[tid];
+  const int my_t = has_chunk ? s_t[tid] : n;
   int my_out = 0, my_nm = 0;
   {
     int pos = my_t;
@@ -300,14 +354,14 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   int total, nmatch;
   const int my_ostart = block_scan_lz(my_out, &total, s_tmp);
   const int my_mstart = block_scan_lz(my_nm, &nmatch, s_tmp);
-  if (tid == 0 && (total > kBlockBytes || total < job.expect_len)) s_bad = 1;
+  if (tid == 0 && (total > kBlockBytes || total < job.expect_len || nmatch > (int)kLz4MatchTable)) s_bad = 1;
   __syncthreads();
   LZ_STAMP(5);
   if (s_bad) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
-  // ---- 4. literals -> output; matches -> table (the visited bitmap in s_out is dead) ----
+  // ---- 4. literals -> output; matches -> table (the chunk arrays in s_out are dead) ----
   {
     int pos = my_t, o = my_ostart, m = my_mstart;
     while (pos < ce) {
@@ -374,7 +428,11 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       if (off >= M) {
         for (int x = a; x < b; ++x) P[x - lo] = (uint16_t)(src + (x - om));
       } else {
-        for (int x = a; x < b; ++x) P[x - lo] = (uint16_t)(src + (x - om) % off);
+        int r = (a - om) % off;
+        for (int x = a; x < b; ++x) {
+          P[x - lo] = (uint16_t)(src + r);
+          if (++r == off) r = 0;
+        }
       }
     }
     __syncthreads();
@@ -383,20 +441,42 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       for (int j = 0; j < nj; ++j) {
         const int om = s_job[j][0], off = s_job[j][1], M = s_job[j][2];
         const int a = max(om, lo), b = min(om + M, hi), src = om - off;
-        for (int x = a + tid; x < b; x += kLzThreads) P[x - lo] = (uint16_t)(src + (x - om) % off);
+        if (off >= M) {
+          for (int x = a + tid; x < b; x += kLzThreads) P[x - lo] = (uint16_t)(src + (x - om));
+        } else {
+          const int step = kLzThreads % off;
+          int r = (a + tid - om) % off;
+          for (int x = a + tid; x < b; x += kLzThreads) {
+            P[x - lo] = (uint16_t)(src + r);
+            r += step;
+            if (r >= off) r -= off;
+          }
+        }
       }
     }
     __syncthreads();
     // P[x] <- P[P[x]] until every pointer is a root (a literal byte of this half, or a byte of an
-    // earlier half, which is final); asynchronous updates only make pointers jump further
+    // earlier half, which is final); asynchronous updates only make pointers jump further.
+    // kJumpBatch chases per thread are issued together so their LDS latencies overlap.
     for (int r = 0;; ++r) {
       int changed = 0;
-      for (int x = lo + tid; x < hi; x += kLzThreads) {
-        const int p = P[x - lo];
-        if (p >= lo && p != x) {
-          const int pp = P[p - lo];
-          if (pp != p) {
-            P[x - lo] = (uint16_t)pp;
+      for (int x0 = lo + tid; x0 < hi; x0 += kLzThreads * kJumpBatch) {
+        int p[kJumpBatch], pp[kJumpBatch];
+#pragma unroll
+        for (int k = 0; k < kJumpBatch; ++k) {
+          const int x = x0 + k * kLzThreads;
+          p[k] = x < hi ? (int)P[x - lo] : x;
+        }
+#pragma unroll
+        for (int k = 0; k < kJumpBatch; ++k) {
+          const int x = x0 + k * kLzThreads;
+          pp[k] = (p[k] >= lo && p[k] != x) ? (int)P[p[k] - lo] : p[k];
+        }
+#pragma unroll
+        for (int k = 0; k < kJumpBatch; ++k) {
+          const int x = x0 + k * kLzThreads;
+          if (pp[k] != p[k]) {
+            P[x - lo] = (uint16_t)pp[k];
             changed = 1;
           }
         }
@@ -416,8 +496,11 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   }
   LZ_STAMP(7);
   if (prof && tid == 0) {
-    prof[(size_t)blockIdx.x * 10 + 8] = (uint64_t)jump_rounds;
-    prof[(size_t)blockIdx.x * 10 + 9] = (uint64_t)n;
+    uint64_t* pr = prof + (size_t)blockIdx.x * kLz4ProfWords;
+    pr[8] = (uint64_t)jump_rounds;
+    pr[9] = (uint64_t)n;
+    pr[10] = (uint64_t)s_slow;
+    pr[11] = (uint64_t)s_e2hit;
   }
   // ---- 6. write the decoded block ----
   uint4* dst = reinterpret_cast<uint4*>(job.dst);
@@ -426,7 +509,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   for (int i = tid; i < n16; i += kLzThreads) dst[i] = srco[i];
 }
 
-// ------------------------------------------------------------------------------------------------
 // Sequential reference decoder (DG_LZ4_SEQ=1): one wave per block, compressed input and decoded output staged in LDS.
 // Tokens are parsed in order (the format is sequential); literal and match copies are spread over
 // the 64 lanes. Overlapping matches (offset < length) use the periodic form

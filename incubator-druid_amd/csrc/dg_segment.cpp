@@ -176,12 +176,15 @@ int upload_flat(BlockColumn* col, const uint8_t* p, const uint8_t* end) {
   if (!col->raw.alloc(bytes + 16)) return set_error(DG_ERR_OOM, "hipMalloc %zu", bytes);
   DG_HIP(hipMemcpy(col->raw.p, p, bytes, hipMemcpyHostToDevice));
   col->stored_bytes = (int64_t)bytes;
-  // virtual 64 KiB blocks so kernels address every layout the same way
-  col->size_per = kBlockBytes / col->width;
-  col->log2_per = log2i(col->size_per);
+  // virtual blocks of a power-of-two row count so kernels address every layout the same way
+  int l2 = 0;
+  while ((2 << l2) <= kBlockBytes / col->width) l2++;
+  col->log2_per = l2;
+  col->size_per = 1 << l2;
   col->nblocks = (int32_t)((col->total + col->size_per - 1) / col->size_per);
   std::vector<const uint8_t*> ptrs(col->nblocks > 0 ? col->nblocks : 1);
-  for (int32_t b = 0; b < col->nblocks; ++b) ptrs[b] = col->raw.as<uint8_t>() + (size_t)b * kBlockBytes;
+  for (int32_t b = 0; b < col->nblocks; ++b)
+    ptrs[b] = col->raw.as<uint8_t>() + (size_t)b * (size_t)col->size_per * (size_t)col->width;
   if (!col->block_ptrs.alloc(ptrs.size() * sizeof(void*))) return set_error(DG_ERR_OOM, "hipMalloc ptrs");
   DG_HIP(hipMemcpy(col->block_ptrs.p, ptrs.data(), ptrs.size() * sizeof(void*), hipMemcpyHostToDevice));
   return DG_OK;

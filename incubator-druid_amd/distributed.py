@@ -9,8 +9,8 @@ merged with one collective per query — backend "nccl" (= RCCL over xGMI) on MI
   FloatSumAggregator.combine), then TimeseriesBinaryFn semantics per bucket.
 * topN: per-segment top-K lists (dictionary values mapped to a cluster-wide id space) ->
   all_gather of fixed-size [segments, K, 1 + aggs] tensors; rank 0 folds them with TopNBinaryFn in
-  global segment order — the reference's approximation (per-segment top max(K, 1000), pairwise merge
-  to the query threshold) is kept exactly.
+  global segment order inside the engine (dg_topn_merge) — the reference's approximation
+  (per-segment top max(K, 1000), pairwise merge to the query threshold) is kept exactly.
 * groupBy: per-rank merged groups -> all_gather of row counts + padded (time, ids, aggs) tensors;
   rank 0 merges by key (GroupByMergingQueryRunnerV2.java:170-290).
 """
@@ -61,6 +61,10 @@ class GlobalDictionary:
     def __init__(self, values: Sequence[Optional[str]]):
         self.values = list(values)
         self.index = {v: i for i, v in enumerate(self.values)}
+
+    def translate(self, local_values: Sequence[Optional[str]]) -> np.ndarray:
+        """segment-local dictionary id -> cluster-wide id (computed once per segment at load time)"""
+        return np.fromiter((self.index[v] for v in local_values), dtype=np.int64, count=len(local_values))
 
     @staticmethod
     def build(dist, local_dicts: Sequence[Sequence[Optional[str]]]) -> "GlobalDictionary":
@@ -134,55 +138,43 @@ def _np_type(a):
 # ----------------------------------------------------------------------------------------------
 # topN
 # ----------------------------------------------------------------------------------------------
-def gather_topn(dist, query: Q.TopNQuery, per_segment: List[List[Q.Result]], gdict: GlobalDictionary,
-                segments_per_rank: int) -> Optional[List[Q.Result]]:
-    """all_gather per-segment top-K lists; rank 0 returns the merged result (others None)."""
+def gather_topn(dist, query: Q.TopNQuery, raw: "R.TopNRaw", gdict: GlobalDictionary,
+                translations: Sequence[np.ndarray]) -> Optional[List[Q.Result]]:
+    """all_gather every rank's per-segment top-K lists (ids mapped to the cluster-wide dictionary);
+    rank 0 folds them with TopNBinaryFn in global segment order (rank-major) inside the engine
+    (dg_topn_merge, global-id mode) and returns the result; other ranks return None.
+
+    The reference's approximation is kept exactly: each segment contributes its own top
+    max(threshold, 1000) list and the fold truncates to the query threshold after every step."""
     torch, _ = _torch()
     dev = _device(dist)
-    K = query.segment_threshold
+    K = raw.K
     na = len(query.aggregations)
-    S = segments_per_rank
-    # [S, K, 3 + na] float64 payload: valid flag, global id, timestamp, aggs (longs are exact in f64
-    # only up to 2^53, so longs travel as int64 bit patterns in a second tensor)
-    ids = np.full((S, K), -1, dtype=np.int64)
-    tss = np.full(S, Q.MAX_INSTANT, dtype=np.int64)
-    has = np.zeros(S, dtype=np.int64)
-    vals = np.zeros((S, K, max(na, 1)), dtype=np.int64)
-    for s, res in enumerate(per_segment[:S]):
-        if not res:
-            continue
-        has[s] = 1
-        tss[s] = res[0].timestamp
-        for j, e in enumerate(res[0].value[:K]):
-            ids[s, j] = gdict.index[e[query.dimension]]
-            for a_i, a in enumerate(query.aggregations):
-                vals[s, j, a_i] = _to_bits(a, e[a.name])
+    S = len(raw.cnt)
+    cnt = raw.cnt.astype(np.int64)
+    gids = np.full((S, K), -1, dtype=np.int64)
+    for s in range(S):
+        c = int(cnt[s])
+        if c > 0:
+            gids[s, :c] = translations[s][raw.ids[s * K:s * K + c]]
+    vals = raw.vals.reshape(S, K, max(na, 1)).view(np.int64)
+    payload = torch.from_numpy(np.concatenate([raw.ts.astype(np.int64), cnt, gids.ravel(), vals.ravel()])).to(dev)
     world = dist.get_world_size()
-    payload = torch.from_numpy(np.concatenate([has, tss, ids.ravel(), vals.ravel()])).to(dev)
     bufs = [torch.empty_like(payload) for _ in range(world)]
     dist.all_gather(bufs, payload)
     if dist.get_rank() != 0:
         return None
-    per_all: List[List[Q.Result]] = []
-    for b in bufs:
-        arr = b.cpu().numpy()
-        h, t = arr[:S], arr[S:2 * S]
-        gi = arr[2 * S:2 * S + S * K].reshape(S, K)
-        gv = arr[2 * S + S * K:].reshape(S, K, max(na, 1))
-        for s in range(S):
-            if not h[s]:
-                per_all.append([])
-                continue
-            entries = []
-            for j in range(K):
-                if gi[s, j] < 0:
-                    break
-                e = {query.dimension: gdict.values[gi[s, j]]}
-                for a_i, a in enumerate(query.aggregations):
-                    e[a.name] = _from_bits(a, gv[s, j, a_i])
-                entries.append(e)
-            per_all.append([Q.Result(int(t[s]), entries)])
-    return R.merge_topn(query, per_all)
+    arrs = [b.cpu().numpy() for b in bufs]
+    ts = np.concatenate([a[:S] for a in arrs])
+    cn = np.concatenate([a[S:2 * S] for a in arrs]).astype(np.int32)
+    keys = np.concatenate([a[2 * S:2 * S + S * K] for a in arrs])
+    vv = np.concatenate([a[2 * S + S * K:] for a in arrs]).view(np.uint64)
+    res = R.topn_merge_raw(query, cn, keys, vv, K, ts, handles=None)
+    if res is None:
+        return []
+    t0, _lists, out_keys, slots = res
+    values = [gdict.values[int(k)] for k in out_keys]
+    return [Q.Result(t0, R._topn_entries(query, values, slots))]
 
 
 def _to_bits(a, v) -> int:

@@ -205,50 +205,139 @@ class _Rev:
         return self.v == o.v
 
 
-def topn_per_segment(segments: Sequence[GpuSegment], query: Q.TopNQuery,
-                     stats: Optional[RunStats] = None) -> List[List[Q.Result]]:
+class TopNRaw:
+    """dg_topn_run output for segments of one device: per segment `cnt[i]` entries (-1 = no cursor),
+    entry j at i * K + j of `ids` (segment-local dictionary ids) and `vals` (n_aggs slots)."""
+
+    def __init__(self, segments, cnt, ids, vals, K, ts):
+        self.segments, self.cnt, self.ids, self.vals, self.K, self.ts = segments, cnt, ids, vals, K, ts
+
+
+def _topn_struct(query: Q.TopNQuery, threshold: int):
+    t = N.dg_topn()
+    dim = query.dimension.encode()
+    t.dimension = dim
+    t.metric_agg = [a.name for a in query.aggregations].index(query.metric.metric)
+    t.inverted = int(query.metric.type == "inverted")
+    t.threshold = threshold
+    return t, dim
+
+
+def _check_topn(query: Q.TopNQuery):
     if query.metric.type not in ("numeric", "inverted"):
         raise N.UnsupportedQuery(2, "dimension-ordered topN")
     if not query.granularity.is_all:
         raise N.UnsupportedQuery(2, "topN with non-ALL granularity")
-    out: List[List[Q.Result]] = [[] for _ in segments]
+
+
+def topn_raw(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional[RunStats] = None) -> TopNRaw:
+    """One batched dg_topn_run over segments that share a device (PooledTopNAlgorithm +
+    TopNNumericResultBuilder per segment, threshold max(threshold, minTopNThreshold))."""
+    _check_topn(query)
+    if len(_group_by_device(segments)) != 1:
+        raise ValueError("topn_raw: segments must share one device")
     na = len(query.aggregations)
     K = query.segment_threshold
-    metric_idx = [a.name for a in query.aggregations].index(query.metric.metric)
+    scan, keep = N.make_scan(query, Q)
+    t, dim = _topn_struct(query, K)
+    n = len(segments)
+    cnt = np.zeros(n, dtype=np.int32)
+    ids = np.zeros(n * K, dtype=np.int32)
+    vals = np.zeros(n * K * max(na, 1), dtype=np.uint64)
+    m = N.dg_metrics()
+    N.check(N.lib().dg_topn_run(_handles(segments), n, ctypes.byref(scan), ctypes.byref(t), cnt.ctypes.data,
+                                ids.ctypes.data, vals.ctypes.data, ctypes.byref(m)))
+    if stats is not None:
+        stats.add(m)
+    ts = np.array([max(query.interval[0], s.min_time) for s in segments], dtype=np.int64)
+    return TopNRaw(list(segments), cnt, ids, vals, K, ts)
+
+
+def topn_merge_raw(query: Q.TopNQuery, cnt: np.ndarray, keys: np.ndarray, vals: np.ndarray, K: int,
+                   ts: np.ndarray, handles=None):
+    """dg_topn_merge over lists ordered by (timestamp, index) (TopNQueryQueryToolChest merge order).
+    Returns (timestamp, list index, keys, value slots) of the merged entries, or None when no list
+    has a cursor. handles: per-list segment handles (segment mode) or None (global ids)."""
+    na = len(query.aggregations)
+    live = [i for i in range(len(cnt)) if cnt[i] >= 0]
+    if not live:
+        return None
+    order = np.array(sorted(live, key=lambda i: (int(ts[i]), i)), dtype=np.int64)
+    n = len(order)
+    o_cnt = np.ascontiguousarray(cnt[order].astype(np.int32))
+    o_keys = np.ascontiguousarray(keys.reshape(-1, K)[order].astype(np.int64))
+    o_vals = np.ascontiguousarray(vals.reshape(-1, K, max(na, 1))[order])
+    lists = N.dg_topn_lists()
+    lists.n_lists = n
+    lists.list_n = o_cnt.ctypes.data
+    lists.stride = K
+    lists.keys = o_keys.ctypes.data
+    lists.values = o_vals.ctypes.data
+    scan, keep = N.make_scan(query, Q)
+    t, dim = _topn_struct(query, query.threshold)
+    out_n = ctypes.c_int32()
+    T = query.threshold
+    out_list = np.zeros(T, dtype=np.int32)
+    out_keys = np.zeros(T, dtype=np.int64)
+    out_vals = np.zeros(T * max(na, 1), dtype=np.uint64)
+    hs = None
+    if handles is not None:
+        hs = (ctypes.c_void_p * n)(*[handles[i] for i in order])
+    N.check(N.lib().dg_topn_merge(hs, ctypes.byref(scan), ctypes.byref(t), ctypes.byref(lists), ctypes.byref(out_n),
+                                  out_list.ctypes.data, out_keys.ctypes.data, out_vals.ctypes.data))
+    k = out_n.value
+    if k < 0:
+        return None
+    return int(ts[order[0]]), order[out_list[:k]], out_keys[:k], out_vals[:k * na].reshape(k, na) if na else None
+
+
+def _topn_entries(query: Q.TopNQuery, values: List[Optional[str]], slots) -> List[Dict]:
+    cols = _decode_slots(query.aggregations, slots) if len(values) and query.aggregations else []
+    out = []
+    for j, v in enumerate(values):
+        e = {query.dimension: v}
+        for a, col in zip(query.aggregations, cols):
+            e[a.name] = _py(col[j], a.output_type)
+        out.append(e)
+    return out
+
+
+def run_topn(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional[RunStats] = None) -> List[Q.Result]:
+    """Per-segment topN on the GPU + TopNBinaryFn merge in the engine (one device); falls back to the
+    Python merge when the segments span devices."""
+    _check_topn(query)
+    if len(_group_by_device(segments)) != 1:
+        return merge_topn(query, topn_per_segment(segments, query, stats))
+    raw = topn_raw(segments, query, stats)
+    handles = [s.handle for s in segments]
+    res = topn_merge_raw(query, raw.cnt, raw.ids, raw.vals, raw.K, raw.ts, handles)
+    if res is None:
+        return []
+    ts, lists, keys, slots = res
+    values = [segments[int(l)].dim_value(query.dimension, int(k)) for l, k in zip(lists, keys)]
+    return [Q.Result(ts, _topn_entries(query, values, slots))]
+
+
+def topn_per_segment(segments: Sequence[GpuSegment], query: Q.TopNQuery,
+                     stats: Optional[RunStats] = None) -> List[List[Q.Result]]:
+    """Per-segment results (what each segment's QueryRunner returns), as Result lists."""
+    _check_topn(query)
+    out: List[List[Q.Result]] = [[] for _ in segments]
+    na = len(query.aggregations)
     for _, idx in _group_by_device(segments).items():
         segs = [segments[i] for i in idx]
-        scan, keep = N.make_scan(query, Q)
-        t = N.dg_topn()
-        dim = query.dimension.encode()
-        t.dimension = dim
-        t.metric_agg = metric_idx
-        t.inverted = int(query.metric.type == "inverted")
-        t.threshold = K
-        n = len(segs)
-        cnt = np.zeros(n, dtype=np.int32)
-        ids = np.zeros(n * K, dtype=np.int32)
-        vals = np.zeros(n * K * max(na, 1), dtype=np.uint64)
-        m = N.dg_metrics()
-        N.check(N.lib().dg_topn_run(_handles(segs), n, ctypes.byref(scan), ctypes.byref(t), cnt.ctypes.data,
-                                    ids.ctypes.data, vals.ctypes.data, ctypes.byref(m)))
-        if stats is not None:
-            stats.add(m)
+        raw = topn_raw(segs, query, stats)
+        K = raw.K
         for k, i in enumerate(idx):
-            if cnt[k] < 0:  # no cursor: the segment does not overlap the interval
-                out[i] = []
+            if raw.cnt[k] < 0:  # no cursor: the segment does not overlap the interval
                 continue
             seg = segs[k]
             dictionary = seg.dictionary(query.dimension)
-            c = int(cnt[k])
-            cols = _decode_slots(query.aggregations, vals.reshape(-1, max(na, 1))[k * K:k * K + c, :na])
-            entries = []
-            for j in range(c):
-                e = {query.dimension: dictionary[ids[k * K + j]] if dictionary else None}
-                for a, col in zip(query.aggregations, cols):
-                    e[a.name] = _py(col[j], a.output_type)
-                entries.append(e)
-            ts = max(query.interval[0], seg.min_time)
-            out[i] = [Q.Result(ts, entries)]
+            c = int(raw.cnt[k])
+            ids = raw.ids[k * K:k * K + c]
+            values = [dictionary[x] if dictionary else None for x in ids]
+            slots = raw.vals.reshape(-1, max(na, 1))[k * K:k * K + c, :na]
+            out[i] = [Q.Result(int(raw.ts[k]), _topn_entries(query, values, slots))]
     return out
 
 
@@ -424,8 +513,7 @@ class MergedQueryRunner:
         self.stats = RunStats()
 
     def run(self, query):
-        per = self.factory.per_segment(self.segments, query, self.stats)
-        return self.factory.toolchest.merge(query, per)
+        return self.factory.run_merged(self.segments, query, self.stats)
 
 
 class _ToolChest:
@@ -440,6 +528,9 @@ class TimeseriesQueryRunnerFactory:
     def per_segment(segments, query, stats=None):
         return timeseries_per_segment(segments, query, stats)
 
+    def run_merged(self, segments, query, stats=None):
+        return self.toolchest.merge(query, self.per_segment(segments, query, stats))
+
     def createRunner(self, segment):
         return SegmentQueryRunner(self, segment)
 
@@ -453,6 +544,10 @@ class TopNQueryRunnerFactory(TimeseriesQueryRunnerFactory):
     @staticmethod
     def per_segment(segments, query, stats=None):
         return topn_per_segment(segments, query, stats)
+
+    def run_merged(self, segments, query, stats=None):
+        # TopNBinaryFn fold inside the engine (dg_topn_merge)
+        return run_topn(segments, query, stats)
 
 
 class GroupByQueryRunnerFactory(TimeseriesQueryRunnerFactory):

@@ -102,6 +102,19 @@ class GpuSegment:
                 self._dicts[dim] = vals
         return self._dicts[dim]
 
+    def dim_value(self, dim: str, idx: int) -> Optional[str]:
+        """DimensionSelector.lookupName for one id (no full dictionary export)."""
+        d = self._dicts.get(dim)
+        if d is not None:
+            return d[idx]
+        if self.column_type(dim) != N.COL_STRING:
+            return None
+        p, n = ctypes.c_void_p(), ctypes.c_int32()
+        N.check(N.lib().dg_segment_dim_value(self.handle, dim.encode(), int(idx), ctypes.byref(p), ctypes.byref(n)))
+        if n.value <= 0:
+            return None
+        return ctypes.string_at(p.value, n.value).decode("utf-8")
+
     def filter_bitmap(self, flt, query_module) -> Tuple[np.ndarray, int]:
         """Filter.getBitmapResult as a dense row bitset (uint32 words) + cardinality."""
         fp = N.FilterProgram(flt, query_module)

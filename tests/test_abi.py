@@ -33,13 +33,14 @@ def test_abi_version_and_structs():
     assert ctypes.sizeof(N.dg_agg) == 16
     assert ctypes.sizeof(N.dg_scan) == 72
     assert ctypes.sizeof(N.dg_metrics) == 64
+    assert ctypes.sizeof(N.dg_topn_lists) == 40
 
 
 def test_gpu_kernels_are_gfx950_code_objects():
     N = importlib.import_module("incubator-druid_amd._native")
     data = open(N.LIB_PATH, "rb").read()
     assert b"gfx950" in data
-    for k in (b"k_lz4_decode", b"k_concise_or", b"k_roaring_or", b"k_scan_agg", b"k_topn_select", b"k_groupby"):
+    for k in (b"k_lz4_decode", b"k_concise_or", b"k_roaring_or", b"k_scan_agg", b"k_topn_radix", b"k_topn_compact", b"k_groupby"):
         assert k in data, k
 
 

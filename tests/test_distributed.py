@@ -54,6 +54,35 @@ def _partial_from_oracle(R, np, query, rows):
     return R.GroupByPartial(t, dims, aggs)
 
 
+def _raw_from_oracle(R, np, O, query, segs):
+    """per-segment oracle topN lists in dg_topn_run's output layout (local ids, ABI value slots)"""
+    K = query.segment_threshold
+    na = len(query.aggregations)
+    cnt = np.full(len(segs), -1, dtype=np.int32)
+    ids = np.zeros(len(segs) * K, dtype=np.int32)
+    vals = np.zeros(len(segs) * K * na, dtype=np.uint64)
+    ts = np.zeros(len(segs), dtype=np.int64)
+    for i, s in enumerate(segs):
+        res = O.topn_segment(s, query)
+        if not res:
+            continue
+        ts[i] = res[0].timestamp
+        cnt[i] = len(res[0].value)
+        index = {v: k for k, v in enumerate(s.dictionary(query.dimension))}
+        for j, e in enumerate(res[0].value):
+            ids[i * K + j] = index[e[query.dimension]]
+            for a_i, a in enumerate(query.aggregations):
+                v = e[a.name]
+                if a.output_type == "long":
+                    bits = np.int64(v).view(np.uint64)
+                elif a.output_type == "double":
+                    bits = np.float64(v).view(np.uint64)
+                else:
+                    bits = np.uint64(np.float32(v).view(np.uint32))
+                vals[(i * K + j) * na + a_i] = bits
+    return R.TopNRaw(None, cnt, ids, vals, K, ts)
+
+
 def _worker(rank, port, paths, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank))
@@ -77,7 +106,9 @@ def _worker(rank, port, paths, out_dir):
         elif isinstance(q, Q.TopNQuery):
             d = q.dimension
             gdict = D.GlobalDictionary.build(dist, [s.dictionary(d) for s in segs])
-            got = D.gather_topn(dist, q, [O.topn_segment(s, q) for s in segs], gdict, SEGS_PER_RANK)
+            trans = [gdict.translate(s.dictionary(d)) for s in segs]
+            raw = _raw_from_oracle(R, np, O, q, segs)
+            got = D.gather_topn(dist, q, raw, gdict, trans)
         else:
             gd = {d: D.GlobalDictionary.build(dist, [s.dictionary(d) for s in segs]) for d in q.dimensions}
             parts = [_partial_from_oracle(R, np, q, O.groupby_segment(s, q)) for s in segs]
