@@ -243,6 +243,15 @@ int dg_result_fetch_groups(dg_result* res, int32_t seg_index, int64_t* bucket_ti
                            uint64_t* values);
 void dg_result_release(dg_result* res);
 
+/* ---- diagnostics (test harness; no reference counterpart) ----
+ * Decode n raw LZ4 blocks (host buffers, <= 64 KiB decoded each) through the same attach-time
+ * checkpoint index and HIP decoder the segment path uses. out: n * 65536 bytes, block i at
+ * i * 65536; out_lens[i] = decoded length, or -1 when the block fails validation (not decoded).
+ * *ms = device time of the decode kernel; prof (optional, NULL = off): 12 words per decoded block,
+ * s_memtime stamps of the decoder's phases + counters (tools/lz4_profile.py prints them). */
+int dg_debug_lz4_decode(dg_context* ctx, const uint8_t* const* blocks, const int32_t* lens, int32_t n, uint8_t* out,
+                        int32_t* out_lens, double* ms, uint64_t* prof);
+
 #ifdef __cplusplus
 }
 #endif

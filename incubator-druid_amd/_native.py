@@ -10,7 +10,8 @@ import os
 from typing import List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdruidgpu.so")
+# DRUID_AMD_LIB: an alternative in-tree build of the same library (A/B variants of a kernel)
+LIB_PATH = os.environ.get("DRUID_AMD_LIB") or os.path.join(_HERE, "lib", "libdruidgpu.so")
 
 DG_OK = 0
 ERRORS = {1: "DG_ERR_FORMAT", 2: "DG_ERR_UNSUPPORTED", 3: "DG_ERR_OOM", 4: "DG_ERR_INTERRUPTED",
@@ -88,7 +89,7 @@ EXPORTS = [
     "dg_segment_interval", "dg_segment_time_bounds", "dg_segment_num_columns", "dg_segment_column_name",
     "dg_segment_column_type", "dg_segment_device_bytes", "dg_segment_dim_cardinality", "dg_segment_dim_value",
     "dg_segment_dim_dictionary", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_topn_merge", "dg_groupby_run",
-    "dg_result_groups", "dg_result_fetch_groups", "dg_result_release",
+    "dg_result_groups", "dg_result_fetch_groups", "dg_result_release", "dg_debug_lz4_decode",
 ]
 
 _lib = None
@@ -131,6 +132,7 @@ def lib():
         "dg_result_groups": (i64, [vp, i32]),
         "dg_result_fetch_groups": (ctypes.c_int, [vp, i32, vp, vp, vp]),
         "dg_result_release": (None, [vp]),
+        "dg_debug_lz4_decode": (ctypes.c_int, [vp, P(vp), P(i32), i32, vp, P(i32), P(ctypes.c_double), vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(l, name)

@@ -485,6 +485,18 @@ struct DecodeBatch {
   int64_t bytes = 0;  // algorithmic bytes read
 };
 
+static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect) {
+  Lz4Job j;
+  j.src = b.comp.as<uint8_t>() + b.comp_off[k];
+  j.dst = dst;
+  j.cp = b.cps.as<uint32_t>() + b.cp_off[k];
+  j.src_len = b.comp_len[k];
+  j.expect_len = expect;
+  j.ncp = b.cp_n[k];
+  j.dec_len = b.dec_len[k];
+  return j;
+}
+
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
   const BlockColumn& b = c->data;
   v->log2_per = b.log2_per;
@@ -494,7 +506,7 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
   else if (c->type == DG_COL_DOUBLE) v->kind = VIEW_DOUBLE;
   else if (c->type == DG_COL_FLOAT) v->kind = VIEW_FLOAT;
   else v->kind = VIEW_IDS;
-  db->bytes += b.stored_bytes;
+  db->bytes += b.stored_bytes + b.index_bytes;
   if (b.codec == CODEC_LZ4) {
     uint8_t* slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
     const uint8_t** h_ptrs = host_take<const uint8_t*>(cs, std::max(b.nblocks, 1));
@@ -505,12 +517,7 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
       h_ptrs[k] = dst;
       int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
       if (rows <= 0) continue;
-      Lz4Job j;
-      j.src = b.comp.as<uint8_t>() + b.comp_off[k];
-      j.dst = dst;
-      j.src_len = b.comp_len[k];
-      j.expect_len = (int32_t)(rows * b.width);
-      db->jobs.push_back(j);
+      db->jobs.push_back(lz4_job(b, k, dst, (int32_t)(rows * b.width)));
     }
     DG_HIP(hipMemcpyAsync(d_ptrs, h_ptrs, sizeof(void*) * std::max(b.nblocks, 1), hipMemcpyHostToDevice, st));
     v->blocks = d_ptrs;
@@ -523,17 +530,16 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
   return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, c->name.c_str());
 }
 
-static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
+static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr) {
   if (db->jobs.empty()) return DG_OK;
   const int n = (int)db->jobs.size();
   Lz4Job* h = host_take<Lz4Job>(cs, n);
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   Lz4Job* d = dev_take<Lz4Job>(cs, n);
   int32_t* d_err = call_err(cs, st);
-  uint64_t* d_mtab = dev_take<uint64_t>(cs, (size_t)n * kLz4MatchTable);
-  if (!h || !d || !d_err || !d_mtab) return set_error(DG_ERR_OOM, "lz4 jobs");
+  if (!h || !d || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
   DG_HIP(hipMemcpyAsync(d, h, sizeof(Lz4Job) * n, hipMemcpyHostToDevice, st));
-  launch_lz4_decode(d, n, d_err, d_mtab, st);
+  launch_lz4_decode(d, n, d_err, st, d_prof);
   return DG_OK;  // errors surface at finish_call
 }
 
@@ -739,12 +745,7 @@ int read_time_bounds(Segment* seg) {
     for (int k = 0; k < 2; ++k) {
       int32_t blk = k == 0 ? 0 : last;
       int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)blk * b.size_per);
-      Lz4Job j;
-      j.src = b.comp.as<uint8_t>() + b.comp_off[blk];
-      j.dst = slots + (size_t)k * kBlockBytes;
-      j.src_len = b.comp_len[blk];
-      j.expect_len = (int32_t)(rows * 8);
-      db.jobs.push_back(j);
+      db.jobs.push_back(lz4_job(b, blk, slots + (size_t)k * kBlockBytes, (int32_t)(rows * 8)));
     }
     int rc0 = run_decodes(cs, &db, st);
     if (rc0) return rc0;
@@ -1765,37 +1766,66 @@ void dg_result_release(dg_result* r) { delete r; }
 }  // extern "C"
 
 // ------------------------------------------------------------------------------------------------
-// diagnostics (not part of the ABI header): per-block LZ4 phase timestamps of one column
+// diagnostics: decode arbitrary LZ4 blocks through the engine's attach-time index + HIP decoder
 // ------------------------------------------------------------------------------------------------
-extern "C" int dg_debug_lz4_profile(dg_segment* s, const char* column, uint64_t* out, int32_t cap, int32_t* nblocks,
-                                    double* ms) {
-  Segment* seg = reinterpret_cast<Segment*>(s);
-  Column* c = seg ? seg->find(column ? column : "") : nullptr;
-  if (!c || c->data.codec != CODEC_LZ4) return set_error(DG_ERR_ARG, "not an LZ4 column");
-  CallGuard g(seg->ctx);
-  hipStream_t st = seg->ctx->stream;
+extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, const int32_t* lens, int32_t n,
+                                   uint8_t* out, int32_t* out_lens, double* ms, uint64_t* prof) {
+  Context* ctx = reinterpret_cast<Context*>(c);
+  if (!ctx || n <= 0 || !blocks || !lens || !out || !out_lens) return set_error(DG_ERR_ARG, "bad arguments");
+  BlockColumn b;
+  b.codec = CODEC_LZ4;
+  b.nblocks = n;
+  b.comp_off.resize(n);
+  b.comp_len.resize(n);
+  b.cp_off.resize(n);
+  b.cp_n.resize(n);
+  b.dec_len.resize(n);
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    if (lens[i] <= 0 || lens[i] > kBlockBytes + 2048) return set_error(DG_ERR_ARG, "block %d length %d", i, lens[i]);
+    b.comp_off[i] = total;
+    b.comp_len[i] = lens[i];
+    total += (lens[i] + 15) & ~15;
+  }
+  std::vector<uint8_t> host((size_t)total + 16, 0);
+  std::vector<uint32_t> cps;
+  for (int i = 0; i < n; ++i) {
+    memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
+    std::vector<uint32_t> one;
+    const int d = lz4_index_block(blocks[i], lens[i], &one);
+    b.cp_off[i] = (int64_t)cps.size();
+    b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size();
+    b.dec_len[i] = d < 0 ? 0 : d;
+    out_lens[i] = d;
+    if (d >= 0) cps.insert(cps.end(), one.begin(), one.end());
+  }
+  if (cps.empty()) cps.push_back(0);
+  CallGuard g(ctx);
+  hipStream_t st = ctx->stream;
+  if (!b.comp.alloc(host.size()) || !b.cps.alloc(cps.size() * 4)) return set_error(DG_ERR_OOM, "debug decode");
+  DG_HIP(hipMemcpy(b.comp.p, host.data(), host.size(), hipMemcpyHostToDevice));
+  DG_HIP(hipMemcpy(b.cps.p, cps.data(), cps.size() * 4, hipMemcpyHostToDevice));
   DecodeBatch db;
-  ColView v;
-  int rc = column_view(c, g.cs, &db, &v, st);
+  uint8_t* slots = dev_take<uint8_t>(g.cs, (size_t)n * kBlockBytes + 64);
+  if (!slots) return set_error(DG_ERR_OOM, "debug decode slots");
+  for (int i = 0; i < n; ++i)
+    if (out_lens[i] >= 0) db.jobs.push_back(lz4_job(b, i, slots + (size_t)i * kBlockBytes, out_lens[i]));
+  uint64_t* d_prof = nullptr;
+  if (prof) {
+    d_prof = dev_take<uint64_t>(g.cs, (size_t)n * kLz4ProfWords);
+    if (!d_prof) return set_error(DG_ERR_OOM, "debug decode profile");
+    DG_HIP(hipMemsetAsync(d_prof, 0, (size_t)n * kLz4ProfWords * 8, st));
+  }
+  hipEventRecord(ctx->ev[0], st);
+  int rc = run_decodes(g.cs, &db, st, d_prof);
   if (rc) return rc;
-  const int n = (int)db.jobs.size();
-  *nblocks = n;
-  Lz4Job* h = host_take<Lz4Job>(g.cs, n);
-  memcpy(h, db.jobs.data(), sizeof(Lz4Job) * n);
-  Lz4Job* d = dev_take<Lz4Job>(g.cs, n);
-  int32_t* d_err = dev_take<int32_t>(g.cs, 1);
-  uint64_t* d_prof = dev_take<uint64_t>(g.cs, (size_t)n * kLz4ProfWords);
-  uint64_t* d_mtab = dev_take<uint64_t>(g.cs, (size_t)n * kLz4MatchTable);
-  DG_HIP(hipMemcpyAsync(d, h, sizeof(Lz4Job) * n, hipMemcpyHostToDevice, st));
-  DG_HIP(hipMemsetAsync(d_err, 0, 4, st));
-  DG_HIP(hipMemsetAsync(d_prof, 0, (size_t)n * kLz4ProfWords * 8, st));
-  hipEventRecord(seg->ctx->ev[0], st);
-  launch_lz4_decode(d, n, d_err, d_mtab, st, d_prof);
-  hipEventRecord(seg->ctx->ev[1], st);
-  DG_HIP(hipStreamSynchronize(st));
+  hipEventRecord(ctx->ev[1], st);
+  rc = finish_call(g.cs, st);
+  if (rc) return rc;
   float f = 0;
-  hipEventElapsedTime(&f, seg->ctx->ev[0], seg->ctx->ev[1]);
-  *ms = f;
-  DG_HIP(hipMemcpy(out, d_prof, (size_t)std::min(cap, n) * kLz4ProfWords * 8, hipMemcpyDeviceToHost));
+  hipEventElapsedTime(&f, ctx->ev[0], ctx->ev[1]);
+  if (ms) *ms = f;
+  DG_HIP(hipMemcpy(out, slots, (size_t)n * kBlockBytes, hipMemcpyDeviceToHost));
+  if (prof) DG_HIP(hipMemcpy(prof, d_prof, (size_t)db.jobs.size() * kLz4ProfWords * 8, hipMemcpyDeviceToHost));
   return DG_OK;
 }

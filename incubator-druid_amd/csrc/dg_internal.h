@@ -37,13 +37,25 @@ struct ColView {
   int32_t pad;
 };
 
+// LZ4 sequence checkpoints: built once per block at attach (lz4_index_block), one entry per
+// kLzSeqPerCp sequences = the compressed offset where that sequence's token starts. They let the
+// decoder parse every interval of a block in parallel; the bytes themselves stay LZ4.
+constexpr int kLzSeqPerCp = 16;
+
 // One LZ4 block to decode (compressed bytes are 16-byte aligned in the device image).
 struct Lz4Job {
   const uint8_t* src;
   uint8_t* dst;
+  const uint32_t* cp;  // checkpoints of this block
   int32_t src_len;
   int32_t expect_len;  // bytes that must come out (>= rows * width of the block)
+  int32_t ncp;         // number of checkpoints; < 0: the block failed validation at attach
+  int32_t dec_len;     // decoded length found at attach
 };
+
+// Host-side validating parse of one LZ4 block (lz4-java safe-decompressor semantics): appends the
+// block's checkpoints to *cps and returns the decoded length, or -1 for a malformed block.
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps);
 
 struct AggPlan {
   int32_t n;
@@ -115,7 +127,12 @@ struct BlockColumn {
   int64_t stored_bytes = 0;            // on-HBM bytes of all blocks (algorithmic bytes of a full scan)
   std::vector<int64_t> comp_off;       // host copy: offset of block b inside comp
   std::vector<int32_t> comp_len;
+  std::vector<int64_t> cp_off;         // LZ4: first checkpoint of block b inside cps
+  std::vector<int32_t> cp_n;           // LZ4: checkpoints of block b (-1: malformed block)
+  std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
+  int64_t index_bytes = 0;             // LZ4: bytes of the checkpoint index (read per query)
   DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)
+  DevBuf cps;                          // LZ4: uint32 checkpoints of every block
   DevBuf raw;                          // UNCOMPRESSED: 64 KiB slot per block; NONE: flat values
   DevBuf block_ptrs;                   // const uint8_t*[nblocks]: raw slots (UNCOMPRESSED/NONE)
 };
@@ -173,11 +190,8 @@ int set_error(int code, const char* fmt, ...);
 int load_segment(Context* ctx, const char* dir, Segment** out);
 
 // kernel launchers (dg_kernels.hip)
-// d_mtab: njobs * kLz4MatchTable scratch words (per-block match table of the parallel decoder)
-constexpr size_t kLz4MatchTable = kBlockBytes / 4;
-constexpr int kLz4ProfWords = 12;  // per-block words of the decoder's phase profile (diagnostic)
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, uint64_t* d_mtab, hipStream_t s,
-                       uint64_t* d_prof = nullptr);
+constexpr int kLz4ProfWords = 12;  // per-block phase stamps of the decoder (diagnostic builds of the call)
+void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_concise_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
                        int nbitmaps, uint32_t* const* d_sets, int64_t limit_bits, hipStream_t s);
 void launch_roaring_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,

@@ -2,26 +2,25 @@
 //
 // Replaces CompressionStrategy.LZ4Decompressor.decompress (processing/.../segment/data/
 // CompressionStrategy.java:284-305 -> lz4-java 1.4.0 LZ4SafeDecompressor): one 64 KiB Druid block
-// (CompressedPools.BUFFER_SIZE) per 256-thread workgroup, compressed input and decoded output in LDS.
+// (CompressedPools.BUFFER_SIZE, segment/CompressedPools.java:39) per 1024-thread workgroup.
 //
-// LZ4's token stream is sequential and Druid's numeric blocks are token-dense: a block of sequential
-// longs is ~8k tokens of [1 literal byte, 7-byte match at offset 8], i.e. ONE dependency chain
-// through the whole block (every match copies bytes the previous match produced). Neither a lane
-// walking the stream (~2 ms/block measured) nor match-by-match rounds (one round per chunk) scale.
-// This kernel decodes in five data-parallel phases:
-//   1. parse, speculatively: the compressed block is cut into 256 chunks; thread i walks the token
-//      chain from the start of its chunk as if a token started there, marking visited positions;
-//   2. the true chain enters chunk i at the exit of chunk i-1 and meets the speculative chain within
-//      a few tokens (chains are functions of position, so they merge): exits are computed in
-//      parallel for the assumed entry and for the likely correction, wave 0 stitches them together;
-//   3. each chunk's true tokens give output sizes and match counts -> block scans -> offsets;
-//   4. literals are copied into the output (long runs cooperatively) and every match is recorded
-//      as (output offset, distance, length) in a per-block table in global memory;
-//   5. matches are resolved by pointer jumping instead of by copying in order: for each output
-//      byte, P[x] = x for a literal byte and P[x] = src + (x - start) mod distance for a match byte
-//      (LZ4 overlap semantics); repeated P[x] <- P[P[x]] converges in log2(chain depth) rounds, then
-//      out[x] = out[P[x]]. P is 16 bits per byte and lives in the (dead) input buffer, one 32 KiB
-//      half of the output at a time (the second half's pointers into the first half are final).
+// Druid's numeric blocks are token-dense: a block of sequential longs is ~8,160 sequences of
+// [1 literal byte, 7-byte match] whose matches copy bytes earlier matches produced (copy chains up
+// to ~300 deep), so neither a lane walking the token stream nor match-by-match copying is fast. The
+// block is decoded in four data-parallel phases, all in LDS:
+//   1. parse: the attach-time checkpoint index (lz4_index_block: the token offset of every 16th
+//      sequence) gives every thread its own 16 sequences; it parses them from the staged input into
+//      registers (literal start, literal length, distance, match length);
+//   2. a block scan of the threads' output lengths places every sequence; each output byte x gets a
+//      16-bit entry E[x] in LDS: a literal is 0xFF00 | byte, a match byte the distance to the byte
+//      it copies (LZ4 overlap semantics: src = start - dist + (k mod dist));
+//   3. pointer jumping: E[x] += E[x - E[x]] until x - E[x] is a literal (log2(chain depth) rounds;
+//      updates are asynchronous, any value read is a valid ancestor distance);
+//   4. out[x] = low byte of the literal at x - E[x], written as 16-byte stores.
+// The staged input and E share one 128 KiB LDS array (the parse finishes before E is written;
+// literals are re-read from the compressed block in HBM/L2). Entries >= 0xFF00 are literals, so a
+// distance must stay below 0xFF00: the last 256 output positions, whose distances can exceed it,
+// keep absolute source positions in a small tail table and are resolved by a short chase.
 // The sequential one-wave decoder (k_lz4_decode_seq) stays as a differential reference, DG_LZ4_SEQ=1.
 #include <hip/hip_runtime.h>
 
@@ -33,25 +32,22 @@ namespace dg {
 
 constexpr int kLzThreads = 1024;               // 16 waves: 4 per SIMD hide LDS latency
 constexpr int kLzWaves = kLzThreads / 64;
-constexpr int kMinChunk = 32;                  // bytes of compressed input per speculative chunk (min)
 constexpr int kLz4InCap = kBlockBytes + 2048;  // >= LZ4_compressBound(65536) = 65809
+constexpr int kTail = 0xFF00;                  // E codes >= kTail are literals; positions >= kTail use the tail table
+constexpr int kTailN = kBlockBytes - kTail;    // 256
 constexpr int kLongLit = 32;                   // literal runs above this are copied cooperatively
-constexpr int kLongFill = 64;                  // match spans above this fill P cooperatively
-constexpr int kMaxJobs = 512;
-constexpr int kHalf = kBlockBytes / 2;
-constexpr int kMaxJumpRounds = 40;
-constexpr int kFixRounds = 8;                  // parallel entry fix-point rounds before the serial stitch
-constexpr int kSeqFraction = 4;                // > 1/4 of chunks inconsistent after one round and a
-                                               // compression ratio < 1.05: walk the tokens serially
-constexpr int kJumpBatch = 8;                  // independent pointer chases in flight per thread
-// per-chunk arrays live in the output buffer while it is free (phases 1-3), after the visited bitmap
-constexpr int kChunkArrOff = 16384;
-static_assert(kChunkArrOff >= (kLz4InCap + 64) / 8, "visited bitmap overlaps the chunk arrays");
-static_assert(kChunkArrOff + 4 * kLzThreads * 4 <= kBlockBytes, "chunk arrays exceed the output buffer");
+constexpr int kLongFill = 48;                  // matches above this are filled cooperatively
+constexpr int kMaxJobs = 2048;
+constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
+constexpr int kJumpBatch = 8;                 // steps of a jump sweep whose reads are issued together
+constexpr int kMaxRounds = 20;                 // > log2(65536) + 1: pointer jumping always converges before
+static_assert(kLz4InCap + 32 <= kBlockBytes * 2, "staged input must fit in the E array");
+static_assert(kLzThreads * kLzSeqPerCp >= kBlockBytes / 4, "a block can hold 16384 sequences");
 
 struct Tok {
   int lit;   // literal start (input offset)
   int L;     // literal length
+  uint32_t lv;  // the first min(L, 4) literal bytes, little-endian
   int off;   // match distance (0 for the last sequence)
   int M;     // match length (0 for the last sequence)
   int next;  // next token start
@@ -85,6 +81,9 @@ __device__ __forceinline__ bool parse_tok_slow(const uint8_t* __restrict__ in, i
   if (L == 15 && !ext_len(in, n, q, L)) return false;
   t.lit = q;
   t.L = L;
+  t.lv = 0;
+  if (L <= 4 && q + L <= n)
+    for (int k = 0; k < L; ++k) t.lv |= (uint32_t)in[q + k] << (8 * k);
   q += L;
   if (q > n) return false;
   if (q == n) {  // last sequence: literals only
@@ -118,6 +117,7 @@ __device__ __forceinline__ bool parse_tok(const uint8_t* __restrict__ in, int n,
   const int q = p + 1 + L;
   t.lit = p + 1;
   t.L = L;
+  t.lv = (uint32_t)(win >> 8);
   if (q > n) return false;
   if (q == n) {
     t.off = 0;
@@ -132,20 +132,7 @@ __device__ __forceinline__ bool parse_tok(const uint8_t* __restrict__ in, int n,
   return t.off != 0;
 }
 
-// walk from `pos` inside [.., ce): stop on a position the speculative chain of this chunk visited
-// (then the exit is that chain's exit `spec_exit`) or at the first token start >= ce
-__device__ __forceinline__ int walk_to_exit(const uint8_t* __restrict__ in, int n, int pos, int ce,
-                                            const uint32_t* __restrict__ vb, int spec_exit) {
-  while (pos < ce) {
-    if ((vb[pos >> 5] >> (pos & 31)) & 1u) return spec_exit;
-    Tok t;
-    if (!parse_tok(in, n, pos, t)) return n;
-    pos = t.next;
-  }
-  return pos;
-}
-
-// block-wide exclusive scan; total via *total
+// block-wide (1024 threads) exclusive scan; total via *total
 __device__ int block_scan_lz(int v, int* total, int* s_tmp) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int x = v;
@@ -168,345 +155,364 @@ __device__ int block_scan_lz(int v, int* total, int* s_tmp) {
   return wave_off + x - v;
 }
 
-#define LZ_STAMP(k)                                                                                   \
-  do {                                                                                                \
-    if (prof && tid == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + (k)] = __builtin_amdgcn_s_memtime(); \
+// E is skewed by one dword every 128 entries so that the threads of a wave, whose intervals start
+// ~128 output bytes apart in token-dense blocks, write different LDS banks.
+#ifndef DG_LZ_NOSKEW
+constexpr int kESkewShift = 7;
+constexpr int kEWords = kBlockBytes + (kBlockBytes >> kESkewShift) * 2;  // u16 entries incl. skew
+__device__ __forceinline__ int eph(int x) { return x + ((x >> kESkewShift) << 1); }
+#else
+constexpr int kESkewShift = 16;
+constexpr int kEWords = kBlockBytes;
+__device__ __forceinline__ int eph(int x) { return x; }
+#endif
+
+struct LzState {
+  uint16_t* e;
+  uint16_t* tsrc;
+  uint32_t* tlit;
+};
+
+__device__ __forceinline__ void put_lit(const LzState& S, int x, int v) {
+  if (x < kTail) {
+    S.e[eph(x)] = (uint16_t)(0xFF00 | v);
+  } else {
+    S.tsrc[x - kTail] = (uint16_t)v;
+    atomicOr(&S.tlit[(x - kTail) >> 5], 1u << ((x - kTail) & 31));
+  }
+}
+
+__device__ __forceinline__ void put_ptr(const LzState& S, int x, int src) {
+  if (x < kTail) S.e[eph(x)] = (uint16_t)(x - src);
+  else S.tsrc[x - kTail] = (uint16_t)src;
+}
+
+// value of output byte x once E and the tail table have converged (both hold literal codes)
+__device__ __forceinline__ uint32_t lz_value(const LzState& S, int x) {
+  if (x < kTail) return S.e[eph(x)] & 0xFF;
+  return S.tsrc[x - kTail] & 0xFF;
+}
+
+#define LZ_STAMP(k)                                                                           \
+  do {                                                                                        \
+    if (PROF && tid == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
+// cooperative-copy job: x = output start | (len - 1) << 16, y = literal input offset (kind 0) or
+// match distance | 1 << 31 (kind 1)
+__device__ __forceinline__ int job_len(uint2 j) { return (int)(j.x >> 16) + 1; }
+
+template <bool PROF>
 __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
-                                                           uint64_t* __restrict__ mtab_all, uint64_t* __restrict__ prof) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[kBlockBytes + 64];
-  __shared__ int s_job[kMaxJobs][3];
-  __shared__ int s_njob, s_bad, s_slow, s_e2hit;
+                                                           uint64_t* __restrict__ prof) {
+  __shared__ __attribute__((aligned(16))) uint16_t s_e[kEWords];  // 130 KiB: staged input, then E
+  __shared__ uint16_t s_tsrc[kTailN];
+  __shared__ uint32_t s_tlit[kTailN / 32];
+  __shared__ uint2 s_job[kMaxJobs];
+  __shared__ int s_jpre[kMaxJobs];
+  __shared__ int s_njob, s_bad;
   __shared__ int s_tmp[kLzWaves];
 
   const Lz4Job job = jobs[blockIdx.x];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  LZ_STAMP(0);
-  const int n = job.src_len;
-  if (n <= 0 || n > kLz4InCap) {
+  const int tid = threadIdx.x;
+  const int n = job.src_len, ncp = job.ncp;
+  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzThreads || job.dec_len > kBlockBytes ||
+      job.dec_len < job.expect_len) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
-  uint64_t* mtab = mtab_all + (size_t)blockIdx.x * kLz4MatchTable;
-  uint32_t* vb = reinterpret_cast<uint32_t*>(s_out);  // visited bitmap (phases 1-2)
-  int* s_x = reinterpret_cast<int*>(s_out + kChunkArrOff);  // speculative exit of each chunk
-  int* s_E = s_x + kLzThreads;                              // entry guess of each chunk
-  int* s_P = s_E + kLzThreads;                              // exit of each chunk from its entry guess
-  int* s_t = s_P + kLzThreads;                              // true entry
-  // ---- stage input; clear the visited bitmap ----
+  LZ_STAMP(0);
+  uint8_t* s_in = reinterpret_cast<uint8_t*>(s_e);
+  const LzState S{s_e, s_tsrc, s_tlit};
+  // ---- stage the compressed block (16-byte aligned and padded in the device image) ----
   {
     const uint4* src = reinterpret_cast<const uint4*>(job.src);
     uint4* dst = reinterpret_cast<uint4*>(s_in);
     const int n16 = (n + 15) >> 4;
     for (int i = tid; i < n16; i += kLzThreads) dst[i] = src[i];
-    if (tid == 0) *reinterpret_cast<uint4*>(s_in + (n16 << 4)) = make_uint4(0, 0, 0, 0);
-    const int nw = (n + 32) >> 5;
-    for (int i = tid; i < nw; i += kLzThreads) vb[i] = 0;
     if (tid == 0) {
+      dst[n16] = make_uint4(0, 0, 0, 0);
       s_njob = 0;
       s_bad = 0;
-      s_slow = 0;
-      s_e2hit = 0;
     }
+    if (tid < kTailN / 32) s_tlit[tid] = 0;
   }
   __syncthreads();
   LZ_STAMP(1);
-  // chunking: NC chunks of CH bytes (threads >= NC only help in the cooperative phases)
-  const int NC = max(1, min(kLzThreads, n / kMinChunk));
-  const int CH = (n + NC - 1) / NC;
-  const bool has_chunk = tid < NC;
-  const int cs = has_chunk ? min(tid * CH, n) : n, ce = has_chunk ? min(cs + CH, n) : n;
-
-  // ---- 1. speculative walk of my chunk ----
-  if (has_chunk) {
-    int pos = cs;
-    while (pos < ce) {
-      atomicOr(&vb[pos >> 5], 1u << (pos & 31));
-      Tok t;
-      if (!parse_tok(s_in, n, pos, t)) {
-        pos = n;
-        break;
-      }
-      pos = t.next;
-    }
-    s_x[tid] = pos;
-  }
-  __syncthreads();
-  LZ_STAMP(2);
-  // ---- 2. entry fix-point: chunk i's entry guess E_i starts as the speculative exit of chunk i-1,
-  // P_i = exit of chunk i from E_i; then rounds of E_i <- P_{i-1} (in parallel, re-walking only chunks
-  // whose guess changed) until nothing changes or kFixRounds. Chains are functions of position and
-  // merge quickly, so a few rounds make nearly every chunk consistent (P_i == E_{i+1}); wave 0 then
-  // stitches the true chain from chunk 0, 64 consistent chunks per ballot. ----
-  const int x_me = has_chunk ? s_x[tid] : n;
-  int myE = n, myP = n;
-  if (has_chunk) {
-    myE = tid == 0 ? 0 : s_x[tid - 1];
-    myP = myE >= ce ? myE : walk_to_exit(s_in, n, myE, ce, vb, x_me);
-    s_E[tid] = myE;
-    s_P[tid] = myP;
-  }
-  // Literal-heavy blocks (near-incompressible data: few, long tokens) give speculative chains that
-  // rarely merge (a wrong parse lands on a true token start about once per token length); there one
-  // lane simply walks the true tokens and records every chunk's entry. Dense blocks with the same
-  // first-round inconsistency converge in a few fix-point rounds instead.
-  const int inconsistent = __syncthreads_count(has_chunk && tid + 1 < NC && myP != s_E[tid + 1]);
-  const bool sequential = inconsistent * kSeqFraction > NC && n * 20 > job.expect_len * 19;
-  int fix_rounds = 0;
-  if (sequential) {
-    if (tid == 0) {
-      int pos = 0, k = 0, bad = 0;
-      while (pos < n) {
-        while (k < NC && k * CH <= pos) s_t[k++] = pos;
+  // ---- 1. parse my interval of kLzSeqPerCp sequences into registers ----
+  uint32_t r_L[kLzSeqPerCp], r_DM[kLzSeqPerCp], r_lv[kLzSeqPerCp];  // r_lv: literal bytes (L <= 4) or offset
+  int cnt = 0, out_rel = 0;
+  if (tid < ncp) {
+    int pos = (int)job.cp[tid];
+    const int end = tid + 1 < ncp ? (int)job.cp[tid + 1] : n;
+#pragma unroll
+    for (int s = 0; s < kLzSeqPerCp; ++s) {
+      if (pos < end) {
         Tok t;
-        if (!parse_tok(s_in, n, pos, t)) {
-          bad = 1;
-          break;
-        }
-        pos = t.next;
-      }
-      while (k < NC) s_t[k++] = n;
-      s_bad = bad;
-      s_slow = 0;
-      s_e2hit = -1;
-    }
-    __syncthreads();
-  }
-  for (int r = 0; r < kFixRounds && !sequential; ++r) {
-    const int newE = (has_chunk && tid > 0) ? s_P[tid - 1] : myE;
-    const bool changed = newE != myE;
-    __syncthreads();  // every read of s_P precedes this round's writes
-    if (changed) {
-      myE = newE;
-      myP = myE >= ce ? myE : walk_to_exit(s_in, n, myE, ce, vb, x_me);
-      s_E[tid] = myE;
-      s_P[tid] = myP;
-    }
-    fix_rounds++;
-    if (!__syncthreads_or(changed)) break;
-  }
-  LZ_STAMP(3);
-  if (wave == 0 && !sequential) {
-    int cur = 0, i = 0, slow = 0;
-    while (i < NC) {
-      if (cur == s_E[i]) {
-        // a run of consistent chunks: one ballot
-        const int idx = i + lane;
-        const bool valid = idx < NC;
-        const bool ok = valid && (idx == NC - 1 || s_P[idx] == s_E[idx + 1]);
-        const unsigned long long badm = __ballot(valid && !ok);
-        const int first_bad = badm ? (__ffsll((long long)badm) - 1) : 64;
-        const int upto = min(first_bad + 1, NC - i);
-        if (lane < upto) s_t[idx] = s_E[idx];
-        if (first_bad < 64 && i + first_bad < NC) {
-          cur = s_P[i + first_bad];
-          i = i + first_bad + 1;
+        if (parse_tok(s_in, n, pos, t)) {
+          r_L[s] = (uint32_t)t.L;
+          r_DM[s] = (uint32_t)t.off | ((uint32_t)t.M << 16);
+          r_lv[s] = t.L <= 4 ? t.lv : (uint32_t)t.lit;
+          out_rel += t.L + t.M;
+          pos = t.next;
+          cnt = s + 1;
         } else {
-          i = min(i + 64, NC);
-          cur = s_P[i - 1];
+          pos = -1;
         }
-      } else {
-        int next_i = i + 1, next_cur = cur;
-        if (lane == 0) {
-          const int ci_s = min(i * CH, n), ci_e = min(ci_s + CH, n);
-          if (cur >= ci_e) {
-            // a long token covers whole chunks: they contain no token start
-            int j = cur / CH;
-            if (j > NC) j = NC;
-            if (j <= i) j = i + 1;
-            for (int k = i; k < j; ++k) s_t[k] = cur;
-            next_i = j;
+      }
+    }
+    if (pos != end) s_bad = 1;
+  }
+  int total;
+  const int base = block_scan_lz(out_rel, &total, s_tmp);  // its barriers end every read of s_in
+  LZ_STAMP(2);
+  if (s_bad || total != job.dec_len) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  // ---- 2. E entries: short literals from registers, short matches as distances; longer runs
+  // become jobs for the cooperative pass (their literals come from the compressed block in HBM) ----
+  const uint8_t* __restrict__ gin = job.src;
+  if (tid < ncp) {
+    int o = base;
+#pragma unroll
+    for (int s = 0; s < kLzSeqPerCp; ++s) {
+      if (s < cnt) {
+        const int L = (int)r_L[s];
+        const int d = (int)(r_DM[s] & 0xFFFF), M = (int)(r_DM[s] >> 16);
+        if (L <= 4) {
+          const uint32_t lv = r_lv[s];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k < L) put_lit(S, o + k, (lv >> (8 * k)) & 0xFF);
+        } else {
+          const int j = atomicAdd(&s_njob, 1);
+          if (j < kMaxJobs) {
+            s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(L - 1) << 16), r_lv[s]);
           } else {
-            s_t[i] = cur;
-            next_cur = walk_to_exit(s_in, n, cur, ci_e, vb, s_x[i]);
+            for (int k = 0; k < L; ++k) put_lit(S, o + k, gin[r_lv[s] + k]);
           }
         }
-        i = __shfl(next_i, 0, 64);
-        cur = __shfl(next_cur, 0, 64);
-        slow++;
+        o += L;
+        if (M > 0) {
+          if (d > o) s_bad = 1;
+          int j = kMaxJobs;
+          if (M > kLongFill) {
+            j = atomicAdd(&s_njob, 1);
+            if (j < kMaxJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(M - 1) << 16), (uint32_t)d | 0x80000000u);
+          }
+          if (j >= kMaxJobs) {
+            if (d >= M) {
+              for (int k = 0; k < M; ++k) put_ptr(S, o + k, o + k - d);
+            } else {
+              int r = 0;
+              for (int k = 0; k < M; ++k) {
+                put_ptr(S, o + k, o - d + r);
+                if (++r == d) r = 0;
+              }
+            }
+          }
+          o += M;
+        }
       }
-    }
-    if (tid == 0) {
-      s_slow = slow;
-      s_e2hit = fix_rounds;
     }
   }
   __syncthreads();
+  LZ_STAMP(3);
+  // ---- cooperative pass: the jobs' bytes as one flat range, split evenly over the threads ----
+  const int nj = min(s_njob, kMaxJobs);
+  if (nj > 0) {
+    int l0 = 0, l1 = 0;
+    if (2 * tid < nj) l0 = job_len(s_job[2 * tid]);
+    if (2 * tid + 1 < nj) l1 = job_len(s_job[2 * tid + 1]);
+    int tot;
+    const int pre = block_scan_lz(l0 + l1, &tot, s_tmp);
+    if (2 * tid < nj) s_jpre[2 * tid] = pre;
+    if (2 * tid + 1 < nj) s_jpre[2 * tid + 1] = pre + l0;
+    __syncthreads();
+    const int f0 = (int)(((int64_t)tot * tid) / kLzThreads), f1 = (int)(((int64_t)tot * (tid + 1)) / kLzThreads);
+    if (f0 < f1) {
+      int lo = 0, hi = nj - 1;  // last job with s_jpre <= f0
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_jpre[mid] <= f0) lo = mid;
+        else hi = mid - 1;
+      }
+      int j = lo;
+      uint2 jb = s_job[j];
+      int jstart = s_jpre[j], jend = jstart + job_len(jb);
+      for (int f = f0; f < f1; f += 8) {
+        int xs[8], srcs[8];
+        uint32_t vals[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          xs[u] = -1;
+          const int g = f + u;
+          if (g < f1) {
+            while (g >= jend) {
+              ++j;
+              jb = s_job[j];
+              jstart = s_jpre[j];
+              jend = jstart + job_len(jb);
+            }
+            const int k = g - jstart, o = (int)(jb.x & 0xFFFF);
+            xs[u] = o + k;
+            if (jb.y & 0x80000000u) {
+              const int d = (int)(jb.y & 0xFFFF);
+              srcs[u] = d >= job_len(jb) ? o + k - d : o - d + k % d;
+            } else {
+              srcs[u] = -1 - ((int)jb.y + k);  // literal: input offset, encoded negative
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (xs[u] >= 0 && srcs[u] < 0) vals[u] = gin[-1 - srcs[u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (xs[u] < 0) continue;
+          if (srcs[u] < 0) put_lit(S, xs[u], vals[u]);
+          else put_ptr(S, xs[u], srcs[u]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (s_bad) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
   LZ_STAMP(4);
-  // ---- 3. sizes of my chunk's true tokens -> output offsets, match-table offsets ----
-  const int my_t = has_chunk ? s_t[tid] : n;
-  int my_out = 0, my_nm = 0;
-  {
-    int pos = my_t;
-    while (pos < ce) {
-      Tok t;
-      if (!parse_tok(s_in, n, pos, t)) {
-        s_bad = 1;
-        break;
-      }
-      my_out += t.L + t.M;
-      my_nm += t.M > 0;
-      pos = t.next;
-    }
+  // ---- 3. pointer jumping with value propagation over positions [0, min(total, kTail)):
+  // E[x] += E[x - E[x]] while that target holds a distance; once it holds a literal code, x takes
+  // the code itself, so later readers of x resolve in one step. My pairs stay in registers. ----
+  const int lim = min(total, kTail);
+  uint32_t* s_e32 = reinterpret_cast<uint32_t*>(s_e);
+  // positions in [lim, 2 * kPairs * kLzThreads) act as resolved literals
+  if (lim < kTail) {
+    for (int x = lim + tid; x < kTail; x += kLzThreads) s_e[eph(x)] = 0xFF00;
   }
-  int total, nmatch;
-  const int my_ostart = block_scan_lz(my_out, &total, s_tmp);
-  const int my_mstart = block_scan_lz(my_nm, &nmatch, s_tmp);
-  if (tid == 0 && (total > kBlockBytes || total < job.expect_len || nmatch > (int)kLz4MatchTable)) s_bad = 1;
-  __syncthreads();
-  LZ_STAMP(5);
-  if (s_bad) {
-    if (tid == 0) atomicOr(err, 1);
-    return;
-  }
-  // ---- 4. literals -> output; matches -> table (the chunk arrays in s_out are dead) ----
-  {
-    int pos = my_t, o = my_ostart, m = my_mstart;
-    while (pos < ce) {
-      Tok t;
-      parse_tok(s_in, n, pos, t);
-      if (t.L <= kLongLit) {
-        for (int k = 0; k < t.L; ++k) s_out[o + k] = s_in[t.lit + k];
-      } else {
-        const int j = atomicAdd(&s_njob, 1);
-        if (j < kMaxJobs) {
-          s_job[j][0] = t.lit;
-          s_job[j][1] = o;
-          s_job[j][2] = t.L;
-        } else {
-          for (int k = 0; k < t.L; ++k) s_out[o + k] = s_in[t.lit + k];
-        }
-      }
-      o += t.L;
-      if (t.M > 0) {
-        if (t.off > o) s_bad = 1;  // distance before the block start
-        mtab[m++] = (uint64_t)o | ((uint64_t)t.off << 16) | ((uint64_t)t.M << 32);
-      }
-      o += t.M;
-      pos = t.next;
-    }
-  }
-  __syncthreads();
-  {
-    const int nj = min(s_njob, kMaxJobs);
-    for (int j = 0; j < nj; ++j) {
-      const int li = s_job[j][0], lo = s_job[j][1], ll = s_job[j][2];
-      for (int k = tid; k < ll; k += kLzThreads) s_out[lo + k] = s_in[li + k];
-    }
-  }
-  __syncthreads();
-  LZ_STAMP(6);
-  if (s_bad) {
-    if (tid == 0) atomicOr(err, 1);
-    return;
-  }
-  // ---- 5. matches by pointer jumping, one 32 KiB half of the output at a time ----
-  uint16_t* P = reinterpret_cast<uint16_t*>(s_in);  // input is dead; 32 Ki x u16 = 64 KiB
+  bool any = true;
   int jump_rounds = 0;
-  for (int lo = 0; lo < total; lo += kHalf) {
-    const int hi = min(lo + kHalf, total);
-    for (int x = lo + tid; x < hi; x += kLzThreads) P[x - lo] = (uint16_t)x;
-    if (tid == 0) s_njob = 0;
-    __syncthreads();
-    for (int m = my_mstart; m < my_mstart + my_nm; ++m) {
-      const uint64_t e = mtab[m];
-      const int om = (int)(e & 0xFFFF), off = (int)((e >> 16) & 0xFFFF), M = (int)(e >> 32);
-      const int a = max(om, lo), b = min(om + M, hi);
-      if (a >= b) continue;
-      if (b - a > kLongFill) {
-        const int j = atomicAdd(&s_njob, 1);
-        if (j < kMaxJobs) {
-          s_job[j][0] = om;
-          s_job[j][1] = off;
-          s_job[j][2] = M;
-          continue;
-        }
-      }
-      const int src = om - off;
-      if (off >= M) {
-        for (int x = a; x < b; ++x) P[x - lo] = (uint16_t)(src + (x - om));
-      } else {
-        int r = (a - om) % off;
-        for (int x = a; x < b; ++x) {
-          P[x - lo] = (uint16_t)(src + r);
-          if (++r == off) r = 0;
-        }
-      }
+  // Rounds of jumping. Wave w sweeps its own 4 KiB of positions in increasing order, 64 pairs per
+  // step, so within a round a position already sees the updates of the earlier steps of its wave
+  // (LDS ops of one wave complete in order): chains collapse to the region start in one round, and
+  // the rounds only have to jump across the 16 regions. A batch of kJumpBatch steps issues its
+  // reads back to back; a resolved position reads itself; only changed pairs are written.
+  const int wv = tid >> 6, ln = tid & 63;
+  uint32_t done = 0;  // wave-uniform: batch b of my wave's region is fully resolved
+  for (int round = 0; __syncthreads_or(any); ++round) {
+    if (round > kMaxRounds) {  // unreachable for a valid block
+      if (tid == 0) atomicOr(err, 1);
+      return;
     }
-    __syncthreads();
-    {
-      const int nj = min(s_njob, kMaxJobs);
-      for (int j = 0; j < nj; ++j) {
-        const int om = s_job[j][0], off = s_job[j][1], M = s_job[j][2];
-        const int a = max(om, lo), b = min(om + M, hi), src = om - off;
-        if (off >= M) {
-          for (int x = a + tid; x < b; x += kLzThreads) P[x - lo] = (uint16_t)(src + (x - om));
+    jump_rounds++;
+    any = false;
+#pragma unroll 1
+    for (int b = 0; b < kPairs / kJumpBatch; ++b) {
+      if ((done >> b) & 1u) continue;
+      const int j0 = b * kJumpBatch;
+      uint32_t dv[kJumpBatch], ta[kJumpBatch], tb[kJumpBatch];
+#pragma unroll
+      for (int k = 0; k < kJumpBatch; ++k) {
+        const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
+        dv[k] = x < kTail ? s_e32[eph(x) >> 1] : 0xFF00FF00u;
+      }
+#pragma unroll
+      for (int k = 0; k < kJumpBatch; ++k) {
+        const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
+        const uint32_t v = dv[k], d0 = v & 0xFFFF, d1 = v >> 16;
+        const int a0 = x - (d0 < (uint32_t)kTail ? (int)d0 : 0);
+        const int a1 = x + 1 - (d1 < (uint32_t)kTail ? (int)d1 : 0);
+        ta[k] = x < kTail ? s_e[eph(a0)] : 0xFF00u;
+        tb[k] = x < kTail ? s_e[eph(a1)] : 0xFF00u;
+      }
+      bool open = false;
+#pragma unroll
+      for (int k = 0; k < kJumpBatch; ++k) {
+        const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
+        const uint32_t v = dv[k], d0 = v & 0xFFFF, d1 = v >> 16;
+        const uint32_t e0 = ta[k], e1 = tb[k];
+        const uint32_t n0 = d0 >= (uint32_t)kTail ? d0 : (e0 >= (uint32_t)kTail ? e0 : d0 + e0);
+        const uint32_t n1 = d1 >= (uint32_t)kTail ? d1 : (e1 >= (uint32_t)kTail ? e1 : d1 + e1);
+        const uint32_t nv = n0 | (n1 << 16);
+        if (nv != v) s_e32[eph(x) >> 1] = nv;
+        open |= n0 < (uint32_t)kTail || n1 < (uint32_t)kTail;
+      }
+      if (__ballot(open) == 0) done |= 1u << b;
+      any |= open;
+    }
+  }
+  LZ_STAMP(5);
+  if (PROF && tid == 0) {
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 8] = (uint64_t)jump_rounds;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 9] = (uint64_t)n;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 10] = (uint64_t)nj;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
+  }
+  // ---- tail: positions [kTail, total) hold absolute sources; rounds of jumping over the table ----
+  if (total > kTail) {
+    const int nt = total - kTail;
+    bool tact = tid < nt && !((s_tlit[tid >> 5] >> (tid & 31)) & 1u);
+    for (int round = 0;; ++round) {
+      uint32_t nsrc = 0;
+      bool res = false;
+      if (tact) {
+        const int src = s_tsrc[tid];
+        if (src < kTail) {
+          nsrc = s_e[eph(src)];  // a literal code: E has converged
+          res = true;
         } else {
-          const int step = kLzThreads % off;
-          int r = (a + tid - om) % off;
-          for (int x = a + tid; x < b; x += kLzThreads) {
-            P[x - lo] = (uint16_t)(src + r);
-            r += step;
-            if (r >= off) r -= off;
-          }
+          const int i2 = src - kTail;
+          nsrc = s_tsrc[i2];
+          res = (s_tlit[i2 >> 5] >> (i2 & 31)) & 1u;
         }
       }
-    }
-    __syncthreads();
-    // P[x] <- P[P[x]] until every pointer is a root (a literal byte of this half, or a byte of an
-    // earlier half, which is final); asynchronous updates only make pointers jump further.
-    // kJumpBatch chases per thread are issued together so their LDS latencies overlap.
-    for (int r = 0;; ++r) {
-      int changed = 0;
-      for (int x0 = lo + tid; x0 < hi; x0 += kLzThreads * kJumpBatch) {
-        int p[kJumpBatch], pp[kJumpBatch];
-#pragma unroll
-        for (int k = 0; k < kJumpBatch; ++k) {
-          const int x = x0 + k * kLzThreads;
-          p[k] = x < hi ? (int)P[x - lo] : x;
-        }
-#pragma unroll
-        for (int k = 0; k < kJumpBatch; ++k) {
-          const int x = x0 + k * kLzThreads;
-          pp[k] = (p[k] >= lo && p[k] != x) ? (int)P[p[k] - lo] : p[k];
-        }
-#pragma unroll
-        for (int k = 0; k < kJumpBatch; ++k) {
-          const int x = x0 + k * kLzThreads;
-          if (pp[k] != p[k]) {
-            P[x - lo] = (uint16_t)pp[k];
-            changed = 1;
-          }
+      __syncthreads();
+      if (tact) {
+        s_tsrc[tid] = (uint16_t)nsrc;
+        if (res) {
+          atomicOr(&s_tlit[tid >> 5], 1u << (tid & 31));
+          tact = false;
         }
       }
-      jump_rounds++;
-      if (!__syncthreads_or(changed)) break;
-      if (r >= kMaxJumpRounds) {
+      if (!__syncthreads_or(tact)) break;
+      if (round > 10) {  // 256 positions: 9 rounds suffice
         if (tid == 0) atomicOr(err, 1);
         return;
       }
     }
-    for (int x = lo + tid; x < hi; x += kLzThreads) {
-      const int p = P[x - lo];
-      if (p != x) s_out[x] = s_out[p];
-    }
-    __syncthreads();
   }
-  LZ_STAMP(7);
-  if (prof && tid == 0) {
-    uint64_t* pr = prof + (size_t)blockIdx.x * kLz4ProfWords;
-    pr[8] = (uint64_t)jump_rounds;
-    pr[9] = (uint64_t)n;
-    pr[10] = (uint64_t)s_slow;
-    pr[11] = (uint64_t)s_e2hit;
-  }
-  // ---- 6. write the decoded block ----
+  // ---- 4. output: every entry is now a literal code; 16 bytes per 16-byte store ----
   uint4* dst = reinterpret_cast<uint4*>(job.dst);
-  const uint4* srco = reinterpret_cast<const uint4*>(s_out);
-  const int n16 = (total + 15) >> 4;
-  for (int i = tid; i < n16; i += kLzThreads) dst[i] = srco[i];
+  const int nchunks = (total + 15) >> 4;
+  for (int c = tid; c < nchunks; c += kLzThreads) {
+    const int x0 = c << 4;
+    uint32_t w[4];
+    if (x0 + 16 <= lim) {
+      const uint32_t* ep = s_e32 + (eph(x0) >> 1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t e0 = ep[2 * q], e1 = ep[2 * q + 1];
+        w[q] = (e0 & 0xFF) | ((e0 >> 8) & 0xFF00) | ((e1 & 0xFF) << 16) | ((e1 & 0xFF0000) << 8);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t acc = 0;
+        for (int i = 0; i < 4; ++i) {
+          const int x = x0 + 4 * q + i;
+          if (x < total) acc |= lz_value(S, x) << (8 * i);
+        }
+        w[q] = acc;
+      }
+    }
+    dst[c] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  if (PROF) {
+    __syncthreads();
+    LZ_STAMP(6);
+  }
 }
 
 // Sequential reference decoder (DG_LZ4_SEQ=1): one wave per block, compressed input and decoded output staged in LDS.
@@ -609,12 +615,12 @@ __global__ __launch_bounds__(64) void k_lz4_decode_seq(const Lz4Job* __restrict_
 }
 
 
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, uint64_t* d_mtab, hipStream_t s,
-                       uint64_t* d_prof) {
+void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
   static const bool seq = getenv("DG_LZ4_SEQ") && getenv("DG_LZ4_SEQ")[0] == '1';
   if (seq) hipLaunchKernelGGL(k_lz4_decode_seq, dim3(njobs), dim3(64), 0, s, d_jobs, d_err);
-  else hipLaunchKernelGGL(k_lz4_decode, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_mtab, d_prof);
+  else if (d_prof) hipLaunchKernelGGL(k_lz4_decode<true>, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
+  else hipLaunchKernelGGL(k_lz4_decode<false>, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
 }
 
 }  // namespace dg

@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 
 #include "dg_internal.h"
 
@@ -122,6 +123,47 @@ int log2i(int32_t v) {
   return (1 << l) == v ? l : -1;
 }
 
+}  // namespace
+
+// Validating parse of one LZ4 block (the checks of lz4-java's LZ4SafeDecompressor / liblz4's
+// LZ4_decompress_safe: lengths inside the input, match distance inside the output produced so far,
+// output within one 64 KiB Druid block, CompressedPools.java:39). Records the token offset of every
+// kLzSeqPerCp-th sequence.
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps) {
+  int pos = 0, out = 0;
+  int64_t seq = 0;
+  auto ext = [&](int* len) {
+    for (;;) {
+      if (pos >= n) return false;
+      const int b = in[pos++];
+      *len += b;
+      if (b != 255) return true;
+    }
+  };
+  for (;;) {
+    if (seq % kLzSeqPerCp == 0) cps->push_back((uint32_t)pos);
+    seq++;
+    if (pos >= n) return -1;
+    const int tok = in[pos++];
+    int L = tok >> 4;
+    if (L == 15 && !ext(&L)) return -1;
+    if (L > n - pos || L > kBlockBytes - out) return -1;
+    pos += L;
+    out += L;
+    if (pos == n) return out;  // last sequence: literals only
+    if (n - pos < 2) return -1;
+    const int off = in[pos] | (in[pos + 1] << 8);
+    pos += 2;
+    int M = tok & 15;
+    if (M == 15 && !ext(&M)) return -1;
+    M += 4;
+    if (off == 0 || off > out || M > kBlockBytes - out) return -1;
+    out += M;
+  }
+}
+
+namespace {
+
 // Upload the blocks of a GenericIndexed of (compressed or raw) blocks.
 int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
   col->nblocks = blocks.n;
@@ -146,6 +188,32 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     }
     if (!col->comp.alloc(host.size())) return set_error(DG_ERR_OOM, "hipMalloc %zu", host.size());
     DG_HIP(hipMemcpy(col->comp.p, host.data(), host.size(), hipMemcpyHostToDevice));
+    // sequence checkpoints of every block (host threads over blocks; validated parse)
+    col->cp_off.assign(blocks.n, 0);
+    col->cp_n.assign(blocks.n, -1);
+    col->dec_len.assign(blocks.n, 0);
+    std::vector<std::vector<uint32_t>> per(blocks.n);
+    const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int nt = blocks.n >= 64 ? nth : 1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t] {
+        for (int32_t b = t; b < blocks.n; b += nt) {
+          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b]);
+          col->dec_len[b] = d;
+          col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size();
+        }
+      });
+    for (auto& x : th) x.join();
+    std::vector<uint32_t> all;
+    for (int32_t b = 0; b < blocks.n; ++b) {
+      col->cp_off[b] = (int64_t)all.size();
+      if (col->cp_n[b] > 0) all.insert(all.end(), per[b].begin(), per[b].end());
+    }
+    if (all.empty()) all.push_back(0);
+    col->index_bytes = (int64_t)all.size() * 4;
+    if (!col->cps.alloc(all.size() * 4)) return set_error(DG_ERR_OOM, "hipMalloc lz4 index");
+    DG_HIP(hipMemcpy(col->cps.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
     return DG_OK;
   }
   if (col->codec == CODEC_UNCOMPRESSED) {

@@ -12,7 +12,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def header_symbols():
     text = open(os.path.join(REPO, "include", "druidgpu.h")).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(dg_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(dg_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_header_symbols():

@@ -1,0 +1,186 @@
+"""LZ4 block decoder (k_lz4_decode via dg_debug_lz4_decode) vs the oracle's decoder, bit-exact.
+
+Blocks come from the system liblz4 (the lz4-java block format Druid writes, HC and fast) over the
+value patterns of Druid's columns, plus hand-built sequence streams for the decoder's edge cases:
+matches with distance 1 / overlapping periods, literal runs and matches crossing the last 256 output
+positions (the decoder's tail table), far distances into that tail, a single literal-only block and
+malformed blocks (rejected at attach-time validation, like LZ4SafeDecompressor would at query time).
+"""
+import ctypes
+import importlib
+
+import numpy as np
+import pytest
+
+BLOCK = 65536
+
+
+def lz4_sequences(seqs, last_literals: bytes) -> bytes:
+    """Encode an LZ4 block from explicit sequences [(literals, distance, match_len)] + final literals."""
+    out = bytearray()
+
+    def ext(n):
+        while n >= 255:
+            out.append(255)
+            n -= 255
+        out.append(n)
+
+    for lit, dist, mlen in seqs:
+        L, M = len(lit), mlen - 4
+        assert M >= 0 and 1 <= dist <= 65535
+        out.append((min(L, 15) << 4) | min(M, 15))
+        if L >= 15:
+            ext(L - 15)
+        out += lit
+        out += bytes([dist & 0xFF, dist >> 8])
+        if M >= 15:
+            ext(M - 15)
+    L = len(last_literals)
+    out.append(min(L, 15) << 4)
+    if L >= 15:
+        ext(L - 15)
+    out += last_literals
+    return bytes(out)
+
+
+def gpu_decode(blocks):
+    N = importlib.import_module("incubator-druid_amd._native")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    ctx = S.GpuContext.get(0)
+    n = len(blocks)
+    bufs = [np.frombuffer(b, dtype=np.uint8).copy() for b in blocks]
+    ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    lens = (ctypes.c_int32 * n)(*[len(b) for b in blocks])
+    out = np.zeros(n * BLOCK, dtype=np.uint8)
+    out_lens = (ctypes.c_int32 * n)()
+    ms = ctypes.c_double()
+    N.check(N.lib().dg_debug_lz4_decode(ctx.handle, ptrs, lens, n, out.ctypes.data, out_lens, ctypes.byref(ms), None))
+    res = []
+    for i in range(n):
+        k = out_lens[i]
+        res.append(None if k < 0 else out[i * BLOCK:i * BLOCK + k].tobytes())
+    return res
+
+
+def _column_payloads(rng):
+    n8 = BLOCK // 8
+    seq = np.arange(n8, dtype=np.int64)
+    return {
+        "seqlong": (seq % 10000).astype("<i8").tobytes(),
+        "time": np.round(seq * 1.3333).astype("<i8").tobytes(),
+        "ones": np.ones(n8, dtype="<i8").tobytes(),
+        "zeros": bytes(BLOCK),
+        "normal": rng.normal(5000, 1, n8).astype("<f8").tobytes(),
+        "zipf": rng.zipf(1.3, n8).astype("<f8").tobytes(),
+        "uniform3": b"".join(int(x).to_bytes(4, "little")[:3] for x in rng.integers(1, 100001, BLOCK // 3 + 1))[:BLOCK],
+        "ids1": rng.integers(0, 101, BLOCK).astype(np.uint8).tobytes(),
+        "ids2": (seq.repeat(4)[:BLOCK // 2] % 1000).astype("<u2").tobytes(),
+        "random": rng.integers(0, 256, BLOCK).astype(np.uint8).tobytes(),
+        "period3": (seq % 3).astype("<i8").tobytes(),
+        "short": (seq[:13] * 7).astype("<i8").tobytes(),
+        "tail6": (seq[:6] + 1388534400000).astype("<i8").tobytes(),
+    }
+
+
+def _crafted(rng):
+    r = lambda k: rng.integers(0, 256, k).astype(np.uint8).tobytes()  # noqa: E731
+    cases = {}
+    # one distance-1 match over the whole block (RLE), ending exactly at 65536
+    cases["rle_full"] = lz4_sequences([(b"\x07", 1, BLOCK - 1 - 5)], r(5))
+    # overlapping periods 2..9 chained through the block
+    seqs, o = [], 0
+    while o < BLOCK - 400:
+        p = int(rng.integers(2, 10))
+        lit = r(p)
+        m = int(rng.integers(4, 200))
+        seqs.append((lit, p, m))
+        o += p + m
+    cases["periods"] = lz4_sequences(seqs, r(BLOCK - o) if BLOCK - o <= 300 else r(5))
+    # far distances into the tail: literals up to 65000, then matches from the start into the last 256 bytes
+    body = r(65000)
+    seqs = [(body, 65000, 200), (r(3), 65203, 64), (b"", 60, 100 - 5 - 9)]
+    used = 65000 + 200 + 3 + 64 + (100 - 5 - 9)
+    cases["far_tail"] = lz4_sequences(seqs, r(BLOCK - used))
+    # a tail made of short chained matches (distance 1..3) crossing 0xFF00
+    seqs, o = [(r(65270), 17, 4)], 65274
+    while o < BLOCK - 20:
+        seqs.append((r(1), int(rng.integers(1, 4)), 4))
+        o += 5
+    cases["tail_chain"] = lz4_sequences(seqs, r(BLOCK - o))
+    # a literal run crossing the tail boundary, then a match copying it
+    cases["lit_cross"] = lz4_sequences([(r(65400), 300, 100)], r(36))
+    # literal-only block (incompressible, one sequence)
+    cases["literal_only"] = lz4_sequences([], r(BLOCK))
+    # many long literal runs and long matches (cooperative paths), random distances
+    seqs, o = [], 0
+    while o < BLOCK - 3000:
+        L = int(rng.integers(0, 600))
+        m = int(rng.integers(4, 900))
+        d = int(rng.integers(1, o + L + 1)) if o + L > 0 else 1
+        if o + L == 0:
+            L = 1
+            d = 1
+        seqs.append((r(L), min(d, o + L), m))
+        o += L + m
+    cases["long_runs"] = lz4_sequences(seqs, r(BLOCK - o) if BLOCK - o < 3000 else r(10))
+    return cases
+
+
+@pytest.mark.gpu
+def test_lz4_column_patterns_bit_exact(O, W):
+    rng = np.random.default_rng(11)
+    blocks, names = [], []
+    for name, raw in _column_payloads(rng).items():
+        for mode in ("hc", "fast"):
+            blocks.append(W.lz4_compress(raw, mode))
+            names.append((name, mode))
+    got = gpu_decode(blocks)
+    for (name, mode), b, g in zip(names, blocks, got):
+        assert g == O.lz4_decompress(b), (name, mode)
+
+
+@pytest.mark.gpu
+def test_lz4_crafted_streams_bit_exact(O):
+    rng = np.random.default_rng(5)
+    cases = _crafted(rng)
+    blocks = list(cases.values())
+    got = gpu_decode(blocks)
+    for name, b, g in zip(cases, blocks, got):
+        exp = O.lz4_decompress(b)
+        assert len(exp) <= BLOCK, name
+        assert g == exp, name
+
+
+@pytest.mark.gpu
+def test_lz4_malformed_blocks_rejected(O):
+    good = lz4_sequences([(b"abcd", 4, 20)], b"xyzw!")
+    bad_dist = lz4_sequences([(b"abcd", 9, 20)], b"xyzw!")       # distance beyond the output
+    truncated = good[:-3]                                         # last literals cut short
+    no_last = lz4_sequences([(b"abcd", 4, 20)], b"")[:-1]        # ends right after a match
+    got = gpu_decode([good, bad_dist, truncated, no_last])
+    assert got[0] == O.lz4_decompress(good)
+    for b, g in zip([bad_dist, truncated, no_last], got[1:]):
+        assert g is None
+        with pytest.raises(ValueError):
+            O.lz4_decompress(b)
+
+
+@pytest.mark.gpu
+def test_lz4_many_blocks_one_launch(O, W):
+    """A batch larger than the CU count, mixed block kinds, decoded in one launch."""
+    rng = np.random.default_rng(3)
+    pays = list(_column_payloads(rng).values())
+    blocks = [W.lz4_compress(pays[i % len(pays)], "hc" if i % 3 else "fast") for i in range(600)]
+    got = gpu_decode(blocks)
+    for b, g in zip(blocks, got):
+        assert g == O.lz4_decompress(b)
+
+
+def test_crafted_streams_pinned_by_system_liblz4(O):
+    """CPU: the crafted streams decode identically with the oracle and the system liblz4 1.9.3."""
+    lib = ctypes.CDLL("liblz4.so.1")
+    rng = np.random.default_rng(5)
+    for name, b in _crafted(rng).items():
+        dst = ctypes.create_string_buffer(BLOCK + 16)
+        n = lib.LZ4_decompress_safe(b, dst, len(b), BLOCK)
+        assert n > 0 and dst.raw[:n] == O.lz4_decompress(b), name

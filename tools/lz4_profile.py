@@ -1,25 +1,81 @@
-"""Per-phase cycle breakdown of the LZ4 decoder on the bench segments (diagnostic)."""
-import ctypes, importlib, os, sys
+"""Per-phase cycle breakdown of the LZ4 decoder (diagnostic; runs on a GPU box).
+
+Blocks are the bench segments' column kinds (basic schema, LZ4-HC): sequential longs, __time,
+normal doubles, 3-byte dimUniform ids. Prints, per kind and for the bench's mix, the kernel time
+and the mean s_memtime cycles of each phase (stage, parse, fill, coop, jump, output).
+"""
+import ctypes
+import importlib
+import os
+import sys
+
 import numpy as np
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 N = importlib.import_module("incubator-druid_amd._native")
 S = importlib.import_module("incubator-druid_amd.segment")
-DG = importlib.import_module("incubator-druid_amd.datagen")
-path = sys.argv[1] if len(sys.argv) > 1 else "/tmp/druid_amd_bench/lz4prof/seg"
-if not os.path.exists(os.path.join(path, "version.bin")):
-    DG.write_basic_segment(path, 750_000, seed=9999)
-seg = S.GpuSegment(path)
-L = N.lib()
-L.dg_debug_lz4_profile.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int32,
-                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
-names = ["stage", "spec_walk", "fixpoint", "resolve", "count+scan", "literals+table", "pointer_jump"]
-for col in ["sumLongSequential", "sumFloatNormal", "dimUniform", "__time", "dimSequential"]:
-    for rep in range(2):
-        buf = np.zeros(200 * 12, dtype=np.uint64)
-        nb, ms = ctypes.c_int32(), ctypes.c_double()
-        N.check(L.dg_debug_lz4_profile(seg.handle, col.encode(), buf.ctypes.data, 200, ctypes.byref(nb), ctypes.byref(ms)))
-    p = buf.reshape(-1, 12)[:min(nb.value, 200)].astype(np.int64)
-    d = np.diff(p[:, :8], axis=1)
-    print(f"{col:20s} blocks={nb.value:4d} kernel={ms.value:8.3f} ms  n(avg)={p[:,9].mean():7.0f} jump_rounds(avg/max)={p[:,8].mean():6.1f}/{p[:,8].max():4d} slow={p[:,10].mean():6.1f} fix_rounds={p[:,11].mean():4.1f}")
-    print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(names, d.mean(axis=0))))
+W = importlib.import_module("incubator-druid_amd.writer")
+BLOCK = 65536
+PHASES = ["stage", "parse+scan", "fill", "coop", "jump", "output"]
+
+
+def payloads(rng, k):
+    n8 = BLOCK // 8
+    out = {"seqlong": [], "time": [], "normal": [], "uniform3": []}
+    for i in range(k):
+        seq = np.arange(i * n8, (i + 1) * n8, dtype=np.int64)
+        out["seqlong"].append((seq % 10000).astype("<i8").tobytes())
+        out["time"].append(np.round(seq * 1.3333).astype("<i8").tobytes())
+        out["normal"].append(rng.normal(5000, 1, n8).astype("<f8").tobytes())
+        ids = rng.integers(1, 100001, BLOCK // 3 + 1).astype("<u4").view(np.uint8).reshape(-1, 4)[:, :3]
+        out["uniform3"].append(ids.tobytes()[:3 * 16384])
+    return out
+
+
+def run(ctx, blocks):
+    n = len(blocks)
+    bufs = [np.frombuffer(b, dtype=np.uint8).copy() for b in blocks]
+    ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    lens = (ctypes.c_int32 * n)(*[len(b) for b in blocks])
+    out = np.zeros(n * BLOCK, dtype=np.uint8)
+    out_lens = (ctypes.c_int32 * n)()
+    ms = ctypes.c_double()
+    prof = np.zeros(n * 12, dtype=np.uint64)
+    for _ in range(2):
+        N.check(N.lib().dg_debug_lz4_decode(ctx.handle, ptrs, lens, n, out.ctypes.data, out_lens, ctypes.byref(ms),
+                                            prof.ctypes.data))
+    p = prof.reshape(n, 12).astype(np.int64)
+    return ms.value, p
+
+
+def report(name, ms, p):
+    d = np.diff(p[:, :7], axis=1)
+    print(f"{name:10s} blocks={len(p):4d} kernel={ms:7.3f} ms  in_bytes(avg)={p[:, 9].mean():7.0f} "
+          f"jump_rounds(avg/max)={p[:, 8].mean():5.1f}/{p[:, 8].max():3d} coop_jobs={p[:, 10].mean():6.1f} "
+          f"cps={p[:, 11].mean():6.1f}")
+    print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(PHASES, d.mean(axis=0))))
+
+
+def main():
+    ctx = S.GpuContext.get(0)
+    rng = np.random.default_rng(1)
+    pays = payloads(rng, 92)
+    comp = {k: [W.lz4_compress(x, "hc") for x in v] for k, v in pays.items()}
+    kinds = sys.argv[1:] or list(comp)
+    for k, blocks in comp.items():
+        if k not in kinds:
+            continue
+        ms, p = run(ctx, blocks)
+        report(k, ms, p)
+    if sys.argv[1:] and "mix" not in kinds:
+        return
+    mix = []
+    for s in range(4):
+        mix += comp["uniform3"][:46] + comp["seqlong"] + comp["normal"]
+    ms, p = run(ctx, mix)
+    report("bench-mix", ms, p)
+
+
+if __name__ == "__main__":
+    main()
