@@ -18,6 +18,7 @@
 #include <queue>
 #include <unordered_map>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "dg_internal.h"
@@ -1156,7 +1157,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], st);
       if (rc) return rc;
     }
-    j.out = nullptr;  // allocated below, once the aggregation layout (split partial tables) is known
+    j.out = nullptr;  // allocated below with the bins
     tiles_rows[i] = seg->nrows;
   }
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
@@ -1165,24 +1166,33 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
   m.bytes_read = db.bytes;
-  uint64_t* h_init = host_take<uint64_t>(cs, rec);
-  h_init[0] = 0;
-  for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
-  uint64_t* d_init = dev_take<uint64_t>(cs, rec);
-  DG_HIP(hipMemcpyAsync(d_init, h_init, rec * 8, hipMemcpyHostToDevice, st));
-  // LDS-privatised id ranges when the per-segment table needs few of them, else HBM atomics
-  int64_t max_card_all = 0;
-  for (int i = 0; i < n; ++i)
-    if (cur[i].any) max_card_all = std::max(max_card_all, card[i]);
-  const bool part = (max_card_all + topn_part_range(na) - 1) / topn_part_range(na) <= kMaxIdRanges;
-  const int splits = part ? topn_part_splits(max_card_all, na, n) : 1;
+  // dictionary-id bins: every segment's table [card][rec] is written whole by the bin reduce
+  const int shift = topn_bin_shift(na);
+  std::vector<int32_t> bin_first(n, 0), bin_seg;
+  int64_t cap = 0;
   for (int i = 0; i < n; ++i) {
+    bin_first[i] = (int32_t)bin_seg.size();
     if (!cur[i].any) continue;
     jobs[i].nbuckets = (int32_t)card[i];
-    jobs[i].out = dev_take<uint64_t>(cs, (size_t)card[i] * rec * splits);
+    jobs[i].out = dev_take<uint64_t>(cs, (size_t)card[i] * rec);
     if (!jobs[i].out) return set_error(DG_ERR_OOM, "topN table");
-    if (!part) launch_fill_u64(jobs[i].out, card[i], rec, d_init, st);
+    const int64_t nb = (card[i] + (1ll << shift) - 1) >> shift;
+    for (int64_t k = 0; k < nb; ++k) bin_seg.push_back(i);
+    cap += tiles_rows[i];
   }
+  const int nbins = (int)bin_seg.size();
+  int32_t* d_bin_first = dev_take<int32_t>(cs, std::max(n, 1));
+  int32_t* d_bin_seg = dev_take<int32_t>(cs, std::max(nbins, 1));
+  uint32_t* d_bins = dev_take<uint32_t>(cs, 3 * (size_t)std::max(nbins, 1));  // hist | base | cursor
+  uint16_t* d_lid = dev_take<uint16_t>(cs, (size_t)std::max<int64_t>(cap, 1) + 8);
+  uint64_t* d_bvals = dev_take<uint64_t>(cs, (size_t)std::max<int64_t>(cap, 1) * std::max(na, 1));
+  int32_t* h_bins = host_take<int32_t>(cs, (size_t)n + std::max(nbins, 1));
+  if (!d_bin_first || !d_bin_seg || !d_bins || !d_lid || !d_bvals || !h_bins) return set_error(DG_ERR_OOM, "topN bins");
+  memcpy(h_bins, bin_first.data(), sizeof(int32_t) * n);
+  if (nbins) memcpy(h_bins + n, bin_seg.data(), sizeof(int32_t) * nbins);
+  DG_HIP(hipMemcpyAsync(d_bin_first, h_bins, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+  if (nbins) DG_HIP(hipMemcpyAsync(d_bin_seg, h_bins + n, sizeof(int32_t) * nbins, hipMemcpyHostToDevice, st));
+  DG_HIP(hipMemsetAsync(d_bins, 0, sizeof(uint32_t) * std::max(nbins, 1), st));
   std::vector<int32_t> begin;
   int ntiles = 0;
   int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
@@ -1214,8 +1224,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       DG_HIP(hipMemcpyAsync(d_jobs + i, h_jobs + i, sizeof(ScanJob), hipMemcpyHostToDevice, st));
     }
   }
-  if (part) launch_topn_part(d_jobs, n, max_card_all, plan, splits, st);
-  else launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
+  launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
+                   d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
   // selection + gather of the candidates' records, all segments in one launch
   const int mk = plan.kind[t->metric_agg];
   const int metric_op = (slot_op(mk) << 8) | mk;
@@ -1440,76 +1450,97 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
   if (rc) return rc;
   if (t->metric_agg < 0 || t->metric_agg >= plan.n) return set_error(DG_ERR_ARG, "metric index");
   if (t->threshold <= 0) return set_error(DG_ERR_ARG, "threshold");
-  const int na = plan.n, mk = plan.kind[t->metric_agg];
+  const int na = plan.n, mk = plan.kind[t->metric_agg], nl = in->n_lists;
+  // the dimension column of every list's segment, resolved once (segment mode)
+  std::vector<const Column*> lcol(nl > 0 ? nl : 1, nullptr);
+  if (segs) {
+    const std::string dim = t->dimension ? t->dimension : "";
+    for (int l = 0; l < nl; ++l) {
+      const Column* c = reinterpret_cast<const Segment*>(segs[l])->find(dim);
+      lcol[l] = (c && c->type == DG_COL_STRING) ? c : nullptr;
+    }
+  }
   struct Ent {
     int32_t list;
     int64_t key;
-    std::vector<uint64_t> v;
+    uint64_t mkey;  // comparator key of the metric (Long/Double/Float.compare, inverted)
+    size_t vo;      // first value slot in `vals`
   };
-  // dimension value of an entry (segment mode) and its ordering
-  auto value_of = [&](const Ent& e, bool* isnull) -> const std::string* {
-    const Segment* seg = reinterpret_cast<const Segment*>(segs[e.list]);
-    const Column* c = seg->find(t->dimension ? t->dimension : "");
-    if (!c || c->type != DG_COL_STRING || e.key < 0 || e.key >= (int64_t)c->dict.size()) {
-      *isnull = true;
-      return nullptr;
-    }
-    *isnull = c->dict_null[e.key] != 0;
-    return &c->dict[e.key];
+  int64_t total = 0;
+  for (int l = 0; l < nl; ++l) total += std::max(in->list_n[l], 0);
+  std::vector<uint64_t> vals((size_t)std::max<int64_t>(total, 1) * std::max(na, 1));
+  // dimension value of an entry: (is null, bytes)
+  auto value_of = [&](const Ent& e, std::string_view* sv) -> bool {
+    const Column* c = lcol[e.list];
+    if (!c || e.key < 0 || e.key >= (int64_t)c->dict.size() || c->dict_null[e.key]) return true;
+    *sv = c->dict[e.key];
+    return false;
   };
-  static const std::string kEmptyStr;
   auto dim_cmp = [&](const Ent& a, const Ent& b) -> int {
     if (!segs) return a.key < b.key ? -1 : (a.key > b.key ? 1 : 0);
-    bool an, bn;
-    const std::string* sa = value_of(a, &an);
-    const std::string* sb = value_of(b, &bn);
-    return cmp_nullable(an, an ? kEmptyStr : *sa, bn, bn ? kEmptyStr : *sb);
-  };
-  auto identity = [&](const Ent& e) -> std::string {
-    if (!segs) return std::string(reinterpret_cast<const char*>(&e.key), 8);
-    bool isnull;
-    const std::string* sv = value_of(e, &isnull);
-    return isnull ? std::string(1, '\0') : std::string(1, '\1') + *sv;
+    std::string_view sa, sb;
+    const bool an = value_of(a, &sa), bn = value_of(b, &sb);
+    if (an || bn) return an == bn ? 0 : (an ? -1 : 1);
+    return java_compare(std::string(sa), std::string(sb));
   };
   // TopNNumericResultBuilder over `ents` (insertion order matters for ties at the minimum)
+  std::vector<size_t> keep;
   auto build = [&](std::vector<Ent>& ents, int threshold) {
-    std::vector<uint64_t> mkey(ents.size());
-    for (size_t e = 0; e < ents.size(); ++e) mkey[e] = abi_metric_key(mk, ents[e].v[t->metric_agg], t->inverted);
     auto less = [&](size_t a, size_t b) {
-      if (mkey[a] != mkey[b]) return mkey[a] < mkey[b];
+      if (ents[a].mkey != ents[b].mkey) return ents[a].mkey < ents[b].mkey;
       return dim_cmp(ents[a], ents[b]) < 0;
     };
     auto gt = [&](size_t a, size_t b) { return less(b, a); };
-    std::priority_queue<size_t, std::vector<size_t>, decltype(gt)> pq(gt);
+    std::vector<size_t> heap;
+    heap.reserve(threshold + 1);
     for (size_t e = 0; e < ents.size(); ++e) {
-      if ((int)pq.size() < threshold || mkey[pq.top()] < mkey[e]) pq.push(e);
-      if ((int)pq.size() > threshold) pq.pop();
+      if ((int)heap.size() < threshold || ents[heap.front()].mkey < ents[e].mkey) {
+        heap.push_back(e);
+        std::push_heap(heap.begin(), heap.end(), gt);
+      }
+      if ((int)heap.size() > threshold) {
+        std::pop_heap(heap.begin(), heap.end(), gt);
+        heap.pop_back();
+      }
     }
-    std::vector<size_t> keep;
-    while (!pq.empty()) {
-      keep.push_back(pq.top());
-      pq.pop();
-    }
+    keep.assign(heap.begin(), heap.end());
     std::sort(keep.begin(), keep.end(), [&](size_t a, size_t b) {
-      if (mkey[a] != mkey[b]) return mkey[a] > mkey[b];
+      if (ents[a].mkey != ents[b].mkey) return ents[a].mkey > ents[b].mkey;
       return dim_cmp(ents[a], ents[b]) < 0;
     });
     std::vector<Ent> out;
     out.reserve(keep.size());
-    for (size_t k : keep) out.push_back(std::move(ents[k]));
+    for (size_t k : keep) out.push_back(ents[k]);
     ents.swap(out);
   };
-  std::vector<Ent> acc;
+  // identity of a dimension value across segments (TopNBinaryFn keys results by value)
+  struct IdHash {
+    size_t operator()(const std::pair<bool, std::string_view>& k) const {
+      return std::hash<std::string_view>()(k.second) ^ (k.first ? 0x9e3779b97f4a7c15ull : 0);
+    }
+  };
+  std::unordered_map<std::pair<bool, std::string_view>, size_t, IdHash> pos;
+  std::unordered_map<int64_t, size_t> kpos;
+  auto ident = [&](const Ent& e) {
+    std::string_view sv;
+    const bool isnull = value_of(e, &sv);
+    return std::make_pair(isnull, isnull ? std::string_view() : sv);
+  };
+  std::vector<Ent> acc, cur;
   bool have = false;
-  for (int l = 0; l < in->n_lists; ++l) {
+  size_t vo = 0;
+  for (int l = 0; l < nl; ++l) {
     const int cnt = in->list_n[l];
     if (cnt < 0) continue;  // no cursor: no result from this segment
-    std::vector<Ent> cur(cnt);
+    cur.resize(cnt);
     for (int e = 0; e < cnt; ++e) {
       const int64_t o = (int64_t)l * in->stride + e;
       cur[e].list = l;
       cur[e].key = in->keys[o];
-      cur[e].v.assign(in->values + o * na, in->values + o * na + na);
+      cur[e].vo = vo;
+      memcpy(vals.data() + vo, in->values + o * na, 8 * (size_t)na);
+      cur[e].mkey = abi_metric_key(mk, vals[vo + t->metric_agg], t->inverted);
+      vo += na;
     }
     if (!have) {
       acc.swap(cur);
@@ -1517,17 +1548,32 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
       continue;
     }
     // retVals (LinkedHashMap): r1's entries, then r2's new values; shared values combined in place
-    std::unordered_map<std::string, size_t> pos;
-    pos.reserve(acc.size() * 2 + 16);
-    for (size_t e = 0; e < acc.size(); ++e) pos.emplace(identity(acc[e]), e);
+    if (segs) {
+      pos.clear();
+      pos.reserve(2 * (acc.size() + cur.size()) + 16);
+      for (size_t e = 0; e < acc.size(); ++e) pos.emplace(ident(acc[e]), e);
+    } else {
+      kpos.clear();
+      kpos.reserve(2 * (acc.size() + cur.size()) + 16);
+      for (size_t e = 0; e < acc.size(); ++e) kpos.emplace(acc[e].key, e);
+    }
     for (auto& e : cur) {
-      auto it = pos.find(identity(e));
-      if (it != pos.end()) {
-        Ent& a = acc[it->second];
-        for (int k = 0; k < na; ++k) a.v[k] = combine_abi(plan.kind[k], a.v[k], e.v[k]);
+      size_t hit = SIZE_MAX;
+      if (segs) {
+        auto it = pos.find(ident(e));
+        if (it != pos.end()) hit = it->second;
       } else {
-        pos.emplace(identity(e), acc.size());
-        acc.push_back(std::move(e));
+        auto it = kpos.find(e.key);
+        if (it != kpos.end()) hit = it->second;
+      }
+      if (hit != SIZE_MAX) {
+        Ent& a = acc[hit];
+        for (int k = 0; k < na; ++k) vals[a.vo + k] = combine_abi(plan.kind[k], vals[a.vo + k], vals[e.vo + k]);
+        a.mkey = abi_metric_key(mk, vals[a.vo + t->metric_agg], t->inverted);
+      } else {
+        if (segs) pos.emplace(ident(e), acc.size());
+        else kpos.emplace(e.key, acc.size());
+        acc.push_back(e);
       }
     }
     build(acc, t->threshold);
@@ -1537,7 +1583,7 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
   for (int e = 0; e < nout; ++e) {
     if (out_list) out_list[e] = acc[e].list;
     if (out_keys) out_keys[e] = acc[e].key;
-    if (out_values) memcpy(out_values + (size_t)e * na, acc[e].v.data(), 8 * (size_t)na);
+    if (out_values) memcpy(out_values + (size_t)e * na, vals.data() + acc[e].vo, 8 * (size_t)na);
   }
   return DG_OK;
 }

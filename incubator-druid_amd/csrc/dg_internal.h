@@ -211,6 +211,14 @@ inline int64_t topn_part_range(int naggs) { return kPartLdsBytes / (8 * (naggs +
 // row splits per (segment, id range); each split writes its own [card][1 + naggs] partial table
 int topn_part_splits(int64_t max_card, int naggs, int njobs);
 void launch_topn_part(const ScanJob* d_jobs, int njobs, int64_t max_card, AggPlan plan, int splits, hipStream_t s);
+// topN aggregation by dictionary-id bins of 2^shift ids (radix partition of the rows, then one
+// LDS table per bin); see dg_kernels.hip. bin_first[seg] = first global bin of segment seg,
+// bin_seg[b] = segment of global bin b; hist/base/cursor: nbins words (hist zeroed by the caller);
+// lid/vals: cap selected-row slots (vals is naggs x cap).
+int topn_bin_shift(int naggs);
+void launch_topn_bins(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, const int32_t* d_bin_first,
+                      const int32_t* d_bin_seg, int nbins, int shift, uint32_t* d_hist, uint32_t* d_base,
+                      uint32_t* d_cursor, AggPlan plan, uint16_t* d_lid, uint64_t* d_vals, int64_t cap, hipStream_t s);
 // topN selection of one segment: K-th largest metric key (8-bit radix select over all touched ids,
 // many workgroups per segment), candidate ids (key >= K-th) in id order, and the candidates'
 // records gathered into a compact buffer for one read-back.

@@ -744,6 +744,213 @@ void launch_topn_part(const ScanJob* d_jobs, int njobs, int64_t max_card, AggPla
 }
 
 // ------------------------------------------------------------------------------------------------
+// topN aggregation by dictionary-id bins (PooledTopNAlgorithm.scanAndAggregate,
+// PooledTopNAlgorithm.java:438-719: one record per dictionary id). With ~7 rows per id (dimUniform)
+// a workgroup's rows hit almost only distinct ids, so privatising per row tile buys nothing and
+// per-row HBM atomics are slow. The rows are radix-partitioned once by id >> shift instead:
+//   k_topn_bin_count    per tile: LDS histogram of selected rows per bin -> global bin counts
+//   k_topn_bin_scan     exclusive scan of all bins (every segment's bins are consecutive)
+//   k_topn_bin_scatter  per tile: recount, reserve one chunk per (tile, bin), write (id, inputs)
+//   k_topn_bin_reduce   per bin: LDS table of its 2^shift records, streamed rows, plain stores
+// Traffic per selected row: id read twice + inputs read once + (2 + 8 * naggs) B written and read.
+// ScanJob.nbuckets carries the segment's cardinality.
+// ------------------------------------------------------------------------------------------------
+constexpr int kBinThreads = 256;
+constexpr int kMaxTileBins = 4096;  // bins of one segment counted in LDS; above that, global atomics
+
+__device__ __forceinline__ bool tile_rows(const ScanJob& j, int t, int64_t* r0, int64_t* r1) {
+  *r0 = (int64_t)(t - j.tile_begin) * kTileRows;
+  *r1 = min((int64_t)j.nrows, *r0 + kTileRows);
+  return *r0 < *r1;
+}
+
+__global__ __launch_bounds__(kBinThreads) void k_topn_bin_count(const ScanJob* __restrict__ jobs,
+                                                                const int32_t* __restrict__ tile_job,
+                                                                const int32_t* __restrict__ bin_first, int shift,
+                                                                uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s_cnt[kMaxTileBins];
+  const int seg = tile_job[blockIdx.x];
+  const ScanJob& j = jobs[seg];
+  const int nb = (int)((j.nbuckets + (1ll << shift) - 1) >> shift);
+  const bool lds = nb <= kMaxTileBins;
+  if (lds)
+    for (int b = threadIdx.x; b < nb; b += kBinThreads) s_cnt[b] = 0;
+  __syncthreads();
+  uint32_t* h = hist + bin_first[seg];
+  int64_t r0, r1;
+  tile_rows(j, blockIdx.x, &r0, &r1);
+  const int64_t full = r0 + ((r1 - r0) & ~3ll);
+  for (int64_t r = r0 + 4 * threadIdx.x; r < full; r += 4 * kBinThreads) {
+    const unsigned m = quad_selected(j, r);
+    if (!m) continue;
+    uint32_t id[4];
+    load_ids4(j.key, r, id);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((m >> k) & 1) atomicAdd(lds ? &s_cnt[id[k] >> shift] : &h[id[k] >> shift], 1u);
+  }
+  if (threadIdx.x == 0)
+    for (int64_t r = full; r < r1; ++r) {
+      int64_t b;
+      if (row_selected(j, r, &b)) atomicAdd(lds ? &s_cnt[load_id(j.key, r) >> shift] : &h[load_id(j.key, r) >> shift], 1u);
+    }
+  __syncthreads();
+  if (lds)
+    for (int b = threadIdx.x; b < nb; b += kBinThreads)
+      if (s_cnt[b]) atomicAdd(&h[b], s_cnt[b]);
+}
+
+// one workgroup: base[b] = exclusive prefix of hist over all bins, cursor[b] = base[b]
+__global__ __launch_bounds__(1024) void k_topn_bin_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ base,
+                                                        uint32_t* __restrict__ cursor, int nbins) {
+  __shared__ int64_t s_tmp[16];
+  __shared__ uint32_t s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (int c = 0; c < nbins; c += 1024) {
+    const int b = c + threadIdx.x;
+    const uint32_t v = b < nbins ? hist[b] : 0;
+    int64_t tot;
+    const uint32_t pre = (uint32_t)block_exclusive_scan(v, &tot, s_tmp) + s_carry;
+    if (b < nbins) {
+      base[b] = pre;
+      cursor[b] = pre;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += (uint32_t)tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBinThreads) void k_topn_bin_scatter(const ScanJob* __restrict__ jobs,
+                                                                  const int32_t* __restrict__ tile_job,
+                                                                  const int32_t* __restrict__ bin_first, int shift,
+                                                                  uint32_t* __restrict__ cursor, AggPlan plan,
+                                                                  uint16_t* __restrict__ lid, uint64_t* __restrict__ vals,
+                                                                  int64_t cap) {
+  __shared__ uint32_t s_cnt[kMaxTileBins];
+  const int seg = tile_job[blockIdx.x];
+  const ScanJob& j = jobs[seg];
+  const int nb = (int)((j.nbuckets + (1ll << shift) - 1) >> shift);
+  const bool lds = nb <= kMaxTileBins;
+  const uint32_t lmask = (1u << shift) - 1;
+  uint32_t* cur = cursor + bin_first[seg];
+  const int na = plan.n;
+  if (lds)
+    for (int b = threadIdx.x; b < nb; b += kBinThreads) s_cnt[b] = 0;
+  __syncthreads();
+  int64_t r0, r1;
+  tile_rows(j, blockIdx.x, &r0, &r1);
+  const int64_t full = r0 + ((r1 - r0) & ~3ll);
+  if (lds) {  // this tile's rows per bin -> one reserved chunk per bin
+    for (int64_t r = r0 + 4 * threadIdx.x; r < full; r += 4 * kBinThreads) {
+      const unsigned m = quad_selected(j, r);
+      if (!m) continue;
+      uint32_t id[4];
+      load_ids4(j.key, r, id);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((m >> k) & 1) atomicAdd(&s_cnt[id[k] >> shift], 1u);
+    }
+    if (threadIdx.x == 0)
+      for (int64_t r = full; r < r1; ++r) {
+        int64_t b;
+        if (row_selected(j, r, &b)) atomicAdd(&s_cnt[load_id(j.key, r) >> shift], 1u);
+      }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += kBinThreads)
+      if (s_cnt[b]) s_cnt[b] = atomicAdd(&cur[b], s_cnt[b]);
+    __syncthreads();
+  }
+  auto put = [&](uint32_t id, uint64_t pos, const uint64_t* in) {
+    lid[pos] = (uint16_t)(id & lmask);
+    for (int a = 0; a < na; ++a) vals[(size_t)a * cap + pos] = in[a];
+  };
+  for (int64_t r = r0 + 4 * threadIdx.x; r < full; r += 4 * kBinThreads) {
+    const unsigned m = quad_selected(j, r);
+    if (!m) continue;
+    uint32_t id[4];
+    load_ids4(j.key, r, id);
+    uint64_t in[4][kMaxAggs];
+    for (int a = 0; a < na; ++a) {
+      uint64_t raw[4] = {0, 0, 0, 0};
+      const int vk = j.vals[a].kind;
+      if (plan.kind[a] != DG_AGG_COUNT && vk != VIEW_ABSENT) load_raw4(j.vals[a], r, raw);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) in[k][a] = agg_input_raw(plan.kind[a], vk, raw[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!((m >> k) & 1)) continue;
+      const uint32_t b = id[k] >> shift;
+      const uint64_t pos = lds ? atomicAdd(&s_cnt[b], 1u) : atomicAdd(&cur[b], 1u);
+      put(id[k], pos, in[k]);
+    }
+  }
+  if (threadIdx.x == 0)
+    for (int64_t r = full; r < r1; ++r) {
+      int64_t bb;
+      if (!row_selected(j, r, &bb)) continue;
+      const uint32_t id = load_id(j.key, r), b = id >> shift;
+      uint64_t in[kMaxAggs];
+      for (int a = 0; a < na; ++a) in[a] = agg_input(plan.kind[a], j.vals[a], r);
+      const uint64_t pos = lds ? atomicAdd(&s_cnt[b], 1u) : atomicAdd(&cur[b], 1u);
+      put(id, pos, in);
+    }
+}
+
+__global__ __launch_bounds__(kBinThreads) void k_topn_bin_reduce(const ScanJob* __restrict__ jobs,
+                                                                 const int32_t* __restrict__ bin_seg,
+                                                                 const int32_t* __restrict__ bin_first, int shift,
+                                                                 const uint32_t* __restrict__ base,
+                                                                 const uint32_t* __restrict__ hist, AggPlan plan,
+                                                                 const uint16_t* __restrict__ lid,
+                                                                 const uint64_t* __restrict__ vals, int64_t cap) {
+  extern __shared__ uint64_t s_tab[];
+  const int gb = blockIdx.x, seg = bin_seg[gb];
+  const ScanJob& j = jobs[seg];
+  const int na = plan.n, rec = na + 1;
+  const int64_t id0 = (int64_t)(gb - bin_first[seg]) << shift;
+  const int64_t nid = min((int64_t)j.nbuckets - id0, 1ll << shift);
+  const int nslots = (int)nid * rec;
+  for (int x = threadIdx.x; x < nslots; x += kBinThreads) {
+    const int sl = x % rec;
+    s_tab[x] = sl == 0 ? 0ull : identity_of(plan.op[sl - 1], plan.kind[sl - 1]);
+  }
+  __syncthreads();
+  const int64_t p0 = base[gb], p1 = p0 + hist[gb];
+  for (int64_t p = p0 + threadIdx.x; p < p1; p += kBinThreads) {
+    uint64_t* e = s_tab + (int)lid[p] * rec;
+    atomicAdd(reinterpret_cast<unsigned long long*>(e), 1ull);
+    for (int a = 0; a < na; ++a) atomic_op(plan.op[a], e + 1 + a, vals[(size_t)a * cap + p]);
+  }
+  __syncthreads();
+  uint64_t* out = j.out + id0 * rec;
+  for (int x = threadIdx.x; x < nslots; x += kBinThreads) out[x] = s_tab[x];
+}
+
+int topn_bin_shift(int naggs) {
+  const int rec = naggs + 1;
+  int shift = 10;
+  while (shift > 6 && ((size_t)rec << shift) * 8 > 48 * 1024) shift--;
+  return shift;
+}
+
+void launch_topn_bins(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, const int32_t* d_bin_first,
+                      const int32_t* d_bin_seg, int nbins, int shift, uint32_t* d_hist, uint32_t* d_base,
+                      uint32_t* d_cursor, AggPlan plan, uint16_t* d_lid, uint64_t* d_vals, int64_t cap, hipStream_t s) {
+  if (ntiles <= 0 || nbins <= 0) return;
+  hipLaunchKernelGGL(k_topn_bin_count, dim3(ntiles), dim3(kBinThreads), 0, s, d_jobs, d_tile_job, d_bin_first, shift,
+                     d_hist);
+  hipLaunchKernelGGL(k_topn_bin_scan, dim3(1), dim3(1024), 0, s, d_hist, d_base, d_cursor, nbins);
+  hipLaunchKernelGGL(k_topn_bin_scatter, dim3(ntiles), dim3(kBinThreads), 0, s, d_jobs, d_tile_job, d_bin_first, shift,
+                     d_cursor, plan, d_lid, d_vals, cap);
+  const size_t lds = ((size_t)(plan.n + 1) << shift) * 8;
+  hipLaunchKernelGGL(k_topn_bin_reduce, dim3(nbins), dim3(kBinThreads), lds, s, d_jobs, d_bin_seg, d_bin_first, shift,
+                     d_base, d_hist, plan, d_lid, d_vals, cap);
+}
+
+// ------------------------------------------------------------------------------------------------
 // topN selection for one segment: the K-th largest metric key among touched ids (8-bit radix
 // select over the ordered key), then the ids whose key >= that K-th key, compacted in id order.
 // The host replays TopNNumericResultBuilder's priority queue over those candidates only (ids with a

@@ -35,7 +35,8 @@ constexpr int kLzWaves = kLzThreads / 64;
 constexpr int kLz4InCap = kBlockBytes + 2048;  // >= LZ4_compressBound(65536) = 65809
 constexpr int kTail = 0xFF00;                  // E codes >= kTail are literals; positions >= kTail use the tail table
 constexpr int kTailN = kBlockBytes - kTail;    // 256
-constexpr int kLongLit = 32;                   // literal runs above this are copied cooperatively
+constexpr int kShortLit = 4;                   // literal runs up to this ride in the parse registers
+static_assert(kShortLit <= 4, "Tok::lv holds four literal bytes");
 constexpr int kLongFill = 48;                  // matches above this are filled cooperatively
 constexpr int kMaxJobs = 2048;
 constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         if (parse_tok(s_in, n, pos, t)) {
           r_L[s] = (uint32_t)t.L;
           r_DM[s] = (uint32_t)t.off | ((uint32_t)t.M << 16);
-          r_lv[s] = t.L <= 4 ? t.lv : (uint32_t)t.lit;
+          r_lv[s] = t.L <= kShortLit ? t.lv : (uint32_t)t.lit;
           out_rel += t.L + t.M;
           pos = t.next;
           cnt = s + 1;
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       if (s < cnt) {
         const int L = (int)r_L[s];
         const int d = (int)(r_DM[s] & 0xFFFF), M = (int)(r_DM[s] >> 16);
-        if (L <= 4) {
+        if (L <= kShortLit) {
           const uint32_t lv = r_lv[s];
 #pragma unroll
           for (int k = 0; k < 4; ++k)
