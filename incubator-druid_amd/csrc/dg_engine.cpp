@@ -98,9 +98,68 @@ struct Pool {
   }
 };
 
+// Host->device staging: tables built on the host go into a pinned chunk mirrored by a device chunk
+// and leave in ONE copy per launch group (up_flush), instead of one hipMemcpyAsync per table.
+struct UpPool {
+  struct Chunk {
+    void* h;
+    void* d;
+    size_t n;
+  };
+  std::vector<Chunk> chunks;
+  size_t cur = 0, off = 0, flushed = 0;
+  ~UpPool() {
+    for (auto& c : chunks) {
+      hipHostFree(c.h);
+      hipFree(c.d);
+    }
+  }
+  void reset() {
+    cur = 0;
+    off = 0;
+    flushed = 0;
+  }
+  bool flush(hipStream_t st) {
+    if (cur < chunks.size() && off > flushed) {
+      const Chunk& c = chunks[cur];
+      if (hipMemcpyAsync((char*)c.d + flushed, (char*)c.h + flushed, off - flushed, hipMemcpyHostToDevice, st) !=
+          hipSuccess)
+        return false;
+    }
+    flushed = off;
+    return true;
+  }
+  void* take(size_t n, void** dev, hipStream_t st) {
+    n = (n + 255) & ~(size_t)255;
+    if (cur >= chunks.size() || off + n > chunks[cur].n) {
+      if (!flush(st)) return nullptr;
+      size_t next = cur < chunks.size() ? cur + 1 : 0;
+      while (next < chunks.size() && chunks[next].n < n) next++;
+      if (next >= chunks.size()) {
+        Chunk c{nullptr, nullptr, std::max(n, (size_t)8 << 20)};
+        if (hipHostMalloc(&c.h, c.n, hipHostMallocDefault) != hipSuccess) return nullptr;
+        if (hipMalloc(&c.d, c.n) != hipSuccess) {
+          hipHostFree(c.h);
+          return nullptr;
+        }
+        chunks.push_back(c);
+        next = chunks.size() - 1;
+      }
+      cur = next;
+      off = 0;
+      flushed = 0;
+    }
+    void* h = (char*)chunks[cur].h + off;
+    *dev = (char*)chunks[cur].d + off;
+    off += n;
+    return h;
+  }
+};
+
 struct CallScratch {
   Pool dev;
   Pool host;
+  UpPool up;
   // per-call device error word (bit 0: corrupt LZ4 block, bit 1: corrupt Roaring bitmap), read once
   // at the call's final synchronisation instead of after every kernel
   int32_t* d_err = nullptr;
@@ -109,6 +168,7 @@ struct CallScratch {
   void reset() {
     dev.reset();
     host.reset();
+    up.reset();
     d_err = nullptr;
     h_err = nullptr;
   }
@@ -133,20 +193,34 @@ template <class T>
 static T* host_take(CallScratch* cs, size_t count) {
   return static_cast<T*>(cs->host.take(count * sizeof(T)));
 }
+// staged upload of `count` T: returns the host view to fill, *dev = its device address (valid for
+// kernels after the next up_flush)
+template <class T>
+static T* up_take(CallScratch* cs, size_t count, T** dev, hipStream_t st) {
+  void* d = nullptr;
+  T* h = static_cast<T*>(cs->up.take(std::max<size_t>(count, 1) * sizeof(T), &d, st));
+  *dev = static_cast<T*>(d);
+  return h;
+}
+#define DG_FLUSH(cs, st)                                                                   \
+  do {                                                                                     \
+    if (!(cs)->up.flush(st)) return ::dg::set_error(DG_ERR_DEVICE, "staged upload failed"); \
+  } while (0)
 
 static int32_t* call_err(CallScratch* cs, hipStream_t st) {
   if (!cs->d_err) {
-    cs->d_err = dev_take<int32_t>(cs, 1);
+    int32_t* z = up_take<int32_t>(cs, 1, &cs->d_err, st);  // zeroed by the next flush
     cs->h_err = host_take<int32_t>(cs, 1);
-    if (!cs->d_err || !cs->h_err) return nullptr;
+    if (!z || !cs->h_err) return nullptr;
+    *z = 0;
     *cs->h_err = 0;
-    if (hipMemsetAsync(cs->d_err, 0, 4, st) != hipSuccess) return nullptr;
   }
   return cs->d_err;
 }
 
 // Enqueue the error-word read-back, wait for the stream, and turn device-side errors into codes.
 static int finish_call(CallScratch* cs, hipStream_t st) {
+  DG_FLUSH(cs, st);
   if (cs->d_err) DG_HIP(hipMemcpyAsync(cs->h_err, cs->d_err, 4, hipMemcpyDeviceToHost, st));
   DG_HIP(hipStreamSynchronize(st));
   DG_HIP(hipGetLastError());
@@ -413,14 +487,12 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
   if (maxd > 16) return set_error(DG_ERR_UNSUPPORTED, "filter nesting too deep");
   const int64_t nwords = (seg->nrows + 31) / 32;
   const int nleaves = (int)fp.leaf_ids.size();
-  uint32_t** h_sets = host_take<uint32_t*>(cs, std::max(nleaves, 1));
-  for (int l = 0; l < nleaves; ++l) {
-    h_sets[l] = dev_take<uint32_t>(cs, (size_t)nwords + 2);
-    if (!h_sets[l]) return set_error(DG_ERR_OOM, "bitset scratch");
-    DG_HIP(hipMemsetAsync(h_sets[l], 0, (size_t)(nwords + 2) * 4, st));
-  }
-  uint32_t** d_sets = dev_take<uint32_t*>(cs, std::max(nleaves, 1));
-  DG_HIP(hipMemcpyAsync(d_sets, h_sets, sizeof(void*) * std::max(nleaves, 1), hipMemcpyHostToDevice, st));
+  uint32_t** d_sets;
+  uint32_t** h_sets = up_take<uint32_t*>(cs, std::max(nleaves, 1), &d_sets, st);
+  uint32_t* leaf_mem = dev_take<uint32_t>(cs, (size_t)std::max(nleaves, 1) * (nwords + 2));
+  if (!h_sets || !leaf_mem) return set_error(DG_ERR_OOM, "bitset scratch");
+  for (int l = 0; l < nleaves; ++l) h_sets[l] = leaf_mem + (size_t)l * (nwords + 2);
+  DG_HIP(hipMemsetAsync(leaf_mem, 0, (size_t)std::max(nleaves, 1) * (nwords + 2) * 4, st));
   // one launch per (column, codec): group leaves by column
   for (int l = 0; l < nleaves; ++l) {
     const Column* c = fp.leaf_col[l];
@@ -442,34 +514,34 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
     }
     if (offs.empty()) continue;
     const int nb = (int)offs.size();
-    int64_t* h_off = host_take<int64_t>(cs, nb);
-    int32_t* h_len = host_take<int32_t>(cs, nb);
-    int32_t* h_tgt = host_take<int32_t>(cs, nb);
+    int64_t* d_off;
+    int32_t *d_len, *d_tgt;
+    int64_t* h_off = up_take<int64_t>(cs, nb, &d_off, st);
+    int32_t* h_len = up_take<int32_t>(cs, nb, &d_len, st);
+    int32_t* h_tgt = up_take<int32_t>(cs, nb, &d_tgt, st);
+    if (!h_off || !h_len || !h_tgt) return set_error(DG_ERR_OOM, "bitmap tables");
     memcpy(h_off, offs.data(), nb * 8);
     memcpy(h_len, lens.data(), nb * 4);
     memcpy(h_tgt, tgts.data(), nb * 4);
-    int64_t* d_off = dev_take<int64_t>(cs, nb);
-    int32_t* d_len = dev_take<int32_t>(cs, nb);
-    int32_t* d_tgt = dev_take<int32_t>(cs, nb);
-    DG_HIP(hipMemcpyAsync(d_off, h_off, nb * 8, hipMemcpyHostToDevice, st));
-    DG_HIP(hipMemcpyAsync(d_len, h_len, nb * 4, hipMemcpyHostToDevice, st));
-    DG_HIP(hipMemcpyAsync(d_tgt, h_tgt, nb * 4, hipMemcpyHostToDevice, st));
     if (c->bitmap_roaring) {
       int32_t* d_err = call_err(cs, st);
       if (!d_err) return set_error(DG_ERR_OOM, "error word");
+      DG_FLUSH(cs, st);
       launch_roaring_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, d_err, (nwords + 2) * 32, st);
     } else {
+      DG_FLUSH(cs, st);
       launch_concise_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, (nwords + 2) * 32, st);
     }
   }
   const int plen = (int)fp.prog.size();
-  int32_t* h_prog = host_take<int32_t>(cs, plen);
+  int32_t* d_prog;
+  int32_t* h_prog = up_take<int32_t>(cs, plen + 2, &d_prog, st);  // + the zeroed 8-byte count
+  if (!h_prog) return set_error(DG_ERR_OOM, "filter program");
   memcpy(h_prog, fp.prog.data(), plen * 4);
-  int32_t* d_prog = dev_take<int32_t>(cs, plen);
-  DG_HIP(hipMemcpyAsync(d_prog, h_prog, plen * 4, hipMemcpyHostToDevice, st));
+  unsigned long long* d_count = reinterpret_cast<unsigned long long*>(d_prog + ((plen + 1) & ~1));
+  memset(h_prog + ((plen + 1) & ~1), 0, 8);
   uint32_t* result = dev_take<uint32_t>(cs, (size_t)nwords + 2);
-  unsigned long long* d_count = dev_take<unsigned long long>(cs, 1);
-  DG_HIP(hipMemsetAsync(d_count, 0, 8, st));
+  DG_FLUSH(cs, st);
   launch_filter_eval(d_prog, plen, d_sets, result, seg->nrows, d_count, st);
   unsigned long long* h_count = host_take<unsigned long long>(cs, 1);
   DG_HIP(hipMemcpyAsync(h_count, d_count, 8, hipMemcpyDeviceToHost, st));
@@ -510,8 +582,8 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
   db->bytes += b.stored_bytes + b.index_bytes;
   if (b.codec == CODEC_LZ4) {
     uint8_t* slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
-    const uint8_t** h_ptrs = host_take<const uint8_t*>(cs, std::max(b.nblocks, 1));
-    const uint8_t** d_ptrs = dev_take<const uint8_t*>(cs, std::max(b.nblocks, 1));
+    const uint8_t** d_ptrs;
+    const uint8_t** h_ptrs = up_take<const uint8_t*>(cs, std::max(b.nblocks, 1), &d_ptrs, st);
     if (!slots || !h_ptrs || !d_ptrs) return set_error(DG_ERR_OOM, "decode scratch");
     for (int32_t k = 0; k < b.nblocks; ++k) {
       uint8_t* dst = slots + (size_t)k * kBlockBytes;
@@ -520,7 +592,6 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
       if (rows <= 0) continue;
       db->jobs.push_back(lz4_job(b, k, dst, (int32_t)(rows * b.width)));
     }
-    DG_HIP(hipMemcpyAsync(d_ptrs, h_ptrs, sizeof(void*) * std::max(b.nblocks, 1), hipMemcpyHostToDevice, st));
     v->blocks = d_ptrs;
     return DG_OK;
   }
@@ -534,12 +605,12 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
 static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr) {
   if (db->jobs.empty()) return DG_OK;
   const int n = (int)db->jobs.size();
-  Lz4Job* h = host_take<Lz4Job>(cs, n);
-  memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
-  Lz4Job* d = dev_take<Lz4Job>(cs, n);
+  Lz4Job* d;
+  Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
   int32_t* d_err = call_err(cs, st);
-  if (!h || !d || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
-  DG_HIP(hipMemcpyAsync(d, h, sizeof(Lz4Job) * n, hipMemcpyHostToDevice, st));
+  if (!h || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
+  memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
+  DG_FLUSH(cs, st);
   launch_lz4_decode(d, n, d_err, st, d_prof);
   return DG_OK;  // errors surface at finish_call
 }
@@ -782,6 +853,24 @@ struct CallGuard {
   }
 };
 
+// DG_HOST_TRACE=1: per-call host wall stamps (diagnostic) printed to stderr
+struct HostTrace {
+  bool on;
+  std::chrono::steady_clock::time_point t0;
+  std::vector<std::pair<const char*, double>> pts;
+  HostTrace() : on(getenv("DG_HOST_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (on)
+      pts.emplace_back(what, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+  ~HostTrace() {
+    if (!on || pts.empty()) return;
+    fprintf(stderr, "[dg host]");
+    for (auto& p : pts) fprintf(stderr, " %s=%.3f", p.first, p.second);
+    fprintf(stderr, "\n");
+  }
+};
+
 static double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -823,13 +912,13 @@ static int32_t* tile_table(CallScratch* cs, const std::vector<int64_t>& nrows, s
     total += (int)((nrows[i] + kTileRows - 1) / kTileRows);
   }
   *ntiles = total;
-  int32_t* h = host_take<int32_t>(cs, std::max(total, 1));
+  int32_t* d;
+  int32_t* h = up_take<int32_t>(cs, std::max(total, 1), &d, st);
+  if (!h) return nullptr;
   for (size_t i = 0; i < nrows.size(); ++i) {
     int nt = (int)((nrows[i] + kTileRows - 1) / kTileRows);
     for (int k = 0; k < nt; ++k) h[(*begin)[i] + k] = (int32_t)i;
   }
-  int32_t* d = dev_take<int32_t>(cs, std::max(total, 1));
-  if (hipMemcpyAsync(d, h, sizeof(int32_t) * std::max(total, 1), hipMemcpyHostToDevice, st) != hipSuccess) return nullptr;
   return d;
 }
 
@@ -1010,13 +1099,11 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   m.bytes_read = db.bytes;
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
   // init accumulators
-  uint64_t* h_init = host_take<uint64_t>(cs, rec);
+  uint64_t* d_init;
+  uint64_t* h_init = up_take<uint64_t>(cs, rec, &d_init, st);
+  if (!h_init) return set_error(DG_ERR_OOM, "accumulator init");
   h_init[0] = 0;
   for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
-  uint64_t* d_init = dev_take<uint64_t>(cs, rec);
-  DG_HIP(hipMemcpyAsync(d_init, h_init, rec * 8, hipMemcpyHostToDevice, st));
-  for (int i = 0; i < n; ++i)
-    if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, d_init, st);
   std::vector<int32_t> begin;
   int ntiles = 0;
   for (int i = 0; i < n; ++i)
@@ -1024,10 +1111,13 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
   if (!d_tile) return set_error(DG_ERR_DEVICE, "tile table");
   for (int i = 0; i < n; ++i) jobs[i].tile_begin = begin[i];
-  ScanJob* h_jobs = host_take<ScanJob>(cs, n);
+  ScanJob* d_jobs;
+  ScanJob* h_jobs = up_take<ScanJob>(cs, n, &d_jobs, st);
+  if (!h_jobs) return set_error(DG_ERR_OOM, "scan jobs");
   memcpy(h_jobs, jobs.data(), sizeof(ScanJob) * n);
-  ScanJob* d_jobs = dev_take<ScanJob>(cs, n);
-  DG_HIP(hipMemcpyAsync(d_jobs, h_jobs, sizeof(ScanJob) * n, hipMemcpyHostToDevice, st));
+  DG_FLUSH(cs, st);
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, d_init, st);
   hipEventRecord(ctx->ev[3], st);
   launch_scan_agg(d_jobs, d_tile, ntiles, plan, 0, st);
   hipEventRecord(ctx->ev[4], st);
@@ -1098,6 +1188,7 @@ static uint64_t metric_key_host(uint64_t slot, int kind, int inverted) {
 int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_topn* t, int32_t* out_n, int32_t* out_ids,
                 uint64_t* out_values, dg_metrics* metrics) {
   auto t0 = std::chrono::steady_clock::now();
+  HostTrace ht;
   Context* ctx;
   int rc = check_segments(segs, n, &ctx);
   if (rc) return rc;
@@ -1162,7 +1253,9 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   }
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
   hipEventRecord(ctx->ev[1], st);
+  ht.mark("planned");
   rc = run_decodes(cs, &db, st);
+  ht.mark("decode_launched");
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
   m.bytes_read = db.bytes;
@@ -1181,27 +1274,27 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     cap += tiles_rows[i];
   }
   const int nbins = (int)bin_seg.size();
-  int32_t* d_bin_first = dev_take<int32_t>(cs, std::max(n, 1));
-  int32_t* d_bin_seg = dev_take<int32_t>(cs, std::max(nbins, 1));
-  uint32_t* d_bins = dev_take<uint32_t>(cs, 3 * (size_t)std::max(nbins, 1));  // hist | base | cursor
+  // staged: bin_first[n] | bin_seg[nbins] | hist[nbins] (zero) | base | cursor
+  const size_t nbw = (size_t)std::max(nbins, 1);
+  int32_t* d_bin_first;
+  int32_t* h_bins = up_take<int32_t>(cs, (size_t)n + 4 * nbw, &d_bin_first, st);
   uint16_t* d_lid = dev_take<uint16_t>(cs, (size_t)std::max<int64_t>(cap, 1) + 8);
   uint64_t* d_bvals = dev_take<uint64_t>(cs, (size_t)std::max<int64_t>(cap, 1) * std::max(na, 1));
-  int32_t* h_bins = host_take<int32_t>(cs, (size_t)n + std::max(nbins, 1));
-  if (!d_bin_first || !d_bin_seg || !d_bins || !d_lid || !d_bvals || !h_bins) return set_error(DG_ERR_OOM, "topN bins");
+  if (!h_bins || !d_lid || !d_bvals) return set_error(DG_ERR_OOM, "topN bins");
   memcpy(h_bins, bin_first.data(), sizeof(int32_t) * n);
   if (nbins) memcpy(h_bins + n, bin_seg.data(), sizeof(int32_t) * nbins);
-  DG_HIP(hipMemcpyAsync(d_bin_first, h_bins, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
-  if (nbins) DG_HIP(hipMemcpyAsync(d_bin_seg, h_bins + n, sizeof(int32_t) * nbins, hipMemcpyHostToDevice, st));
-  DG_HIP(hipMemsetAsync(d_bins, 0, sizeof(uint32_t) * std::max(nbins, 1), st));
+  memset(h_bins + n + nbw, 0, 4 * nbw);
+  int32_t* d_bin_seg = d_bin_first + n;
+  uint32_t* d_bins = reinterpret_cast<uint32_t*>(d_bin_first + n + nbw);  // hist | base | cursor
   std::vector<int32_t> begin;
   int ntiles = 0;
   int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
   if (!d_tile) return set_error(DG_ERR_DEVICE, "tile table");
   for (int i = 0; i < n; ++i) jobs[i].tile_begin = begin[i];
-  ScanJob* h_jobs = host_take<ScanJob>(cs, n);
+  ScanJob* d_jobs;
+  ScanJob* h_jobs = up_take<ScanJob>(cs, n, &d_jobs, st);
+  if (!h_jobs) return set_error(DG_ERR_OOM, "scan jobs");
   memcpy(h_jobs, jobs.data(), sizeof(ScanJob) * n);
-  ScanJob* d_jobs = dev_take<ScanJob>(cs, n);
-  DG_HIP(hipMemcpyAsync(d_jobs, h_jobs, sizeof(ScanJob) * n, hipMemcpyHostToDevice, st));
   hipEventRecord(ctx->ev[3], st);
   // missing-dimension segments: the key view is absent; load_id would fault, so route them
   // through a 1-entry table with a zero id view
@@ -1211,28 +1304,39 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       uint8_t* zero = dev_take<uint8_t>(cs, kBlockBytes);
       DG_HIP(hipMemsetAsync(zero, 0, kBlockBytes, st));
       const int nb = (int)((jobs[i].nrows + 65535) / 65536) + 1;
-      const uint8_t** hp = host_take<const uint8_t*>(cs, nb);
+      const uint8_t** dp;
+      const uint8_t** hp = up_take<const uint8_t*>(cs, nb, &dp, st);
+      if (!hp) return set_error(DG_ERR_OOM, "zero id view");
       for (int k = 0; k < nb; ++k) hp[k] = zero;
-      const uint8_t** dp = dev_take<const uint8_t*>(cs, nb);
-      DG_HIP(hipMemcpyAsync(dp, hp, sizeof(void*) * nb, hipMemcpyHostToDevice, st));
       ScanJob fixed = jobs[i];
       fixed.key.blocks = dp;
       fixed.key.log2_per = 16;
       fixed.key.width = 1;
       fixed.key.kind = VIEW_IDS;
       h_jobs[i] = fixed;
-      DG_HIP(hipMemcpyAsync(d_jobs + i, h_jobs + i, sizeof(ScanJob), hipMemcpyHostToDevice, st));
     }
   }
+  DG_FLUSH(cs, st);
   launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
                    d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
+  ht.mark("bins_launched");
   // selection + gather of the candidates' records, all segments in one launch
   const int mk = plan.kind[t->metric_agg];
   const int metric_op = (slot_op(mk) << 8) | mk;
   std::vector<TopnSelJob> sel;
   std::vector<int> sel_seg;
-  std::vector<int64_t> gcap(n, 0);
-  int64_t max_card = 0;
+  std::vector<int64_t> gcap(n, 0), goff(n, 0);
+  int64_t max_card = 0, gtotal = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    // candidates = ids whose key >= the K-th key: the threshold plus ties, rarely more
+    gcap[i] = std::min<int64_t>(card[i], 2 * (int64_t)t->threshold + 64);
+    goff[i] = gtotal;
+    gtotal += gcap[i] * (rec + 1);
+  }
+  // read-back block (one D2H copy): gathered records of every segment
+  uint64_t* d_gath = dev_take<uint64_t>(cs, (size_t)std::max<int64_t>(gtotal, 1));
+  if (!d_gath) return set_error(DG_ERR_OOM, "topN gather");
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
     TopnSelJob sj;
@@ -1242,54 +1346,62 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     sj.cand = dev_take<int32_t>(cs, (size_t)card[i]);
     sj.keys = dev_take<uint64_t>(cs, (size_t)card[i]);
     sj.blkcnt = dev_take<int32_t>(cs, (size_t)((card[i] + kSelBlock - 1) / kSelBlock));
-    // candidates = ids whose key >= the K-th key: the threshold plus ties, rarely more
-    gcap[i] = std::min<int64_t>(card[i], 2 * (int64_t)t->threshold + 64);
     sj.gather_cap = (int32_t)gcap[i];
-    sj.gathered = dev_take<uint64_t>(cs, (size_t)gcap[i] * rec);
-    if (!sj.cand || !sj.gathered || !sj.keys || !sj.blkcnt) return set_error(DG_ERR_OOM, "topN candidates");
+    sj.gathered = d_gath + goff[i];
+    if (!sj.cand || !sj.keys || !sj.blkcnt) return set_error(DG_ERR_OOM, "topN candidates");
     max_card = std::max(max_card, card[i]);
     sel.push_back(sj);
     sel_seg.push_back(i);
   }
   const int ns = (int)sel.size();
-  int32_t* d_ncand = dev_take<int32_t>(cs, std::max(ns, 1));
-  // per selection: state[4] + hist[8][256], zeroed with one memset
-  const size_t sel_words = 4 + 8 * 256 / 2;
-  uint64_t* d_selmem = dev_take<uint64_t>(cs, sel_words * std::max(ns, 1));
-  uint64_t* d_state = d_selmem;
+  // staged zero block: per selection state[4] | ncand (+pad) | hist[8][256] words
+  const size_t sel_words = 4 + 1 + 8 * 256 / 2;
+  uint64_t* d_selmem;
+  uint64_t* h_selz = up_take<uint64_t>(cs, sel_words * std::max(ns, 1), &d_selmem, st);
+  TopnSelJob* d_sel;
+  TopnSelJob* h_sel = up_take<TopnSelJob>(cs, std::max(ns, 1), &d_sel, st);
+  if (!h_selz || !h_sel) return set_error(DG_ERR_OOM, "topN selection");
+  memset(h_selz, 0, 8 * sel_words * std::max(ns, 1));
   for (int k = 0; k < ns; ++k) {
-    sel[k].ncand = d_ncand + k;
     sel[k].state = d_selmem + sel_words * k;
-    sel[k].hist = reinterpret_cast<uint32_t*>(d_selmem + sel_words * k + 4);
+    sel[k].ncand = reinterpret_cast<int32_t*>(d_selmem + sel_words * k + 4);
+    sel[k].hist = reinterpret_cast<uint32_t*>(d_selmem + sel_words * k + 5);
   }
-  TopnSelJob* h_sel = host_take<TopnSelJob>(cs, std::max(ns, 1));
-  TopnSelJob* d_sel = dev_take<TopnSelJob>(cs, std::max(ns, 1));
-  if (!h_sel || !d_sel || !d_ncand || !d_selmem) return set_error(DG_ERR_OOM, "topN selection");
   if (ns) {
     memcpy(h_sel, sel.data(), sizeof(TopnSelJob) * ns);
-    DG_HIP(hipMemcpyAsync(d_sel, h_sel, sizeof(TopnSelJob) * ns, hipMemcpyHostToDevice, st));
-    DG_HIP(hipMemsetAsync(d_selmem, 0, 8 * sel_words * ns, st));
+    DG_FLUSH(cs, st);
     launch_topn_select(d_sel, ns, max_card, na, t->metric_agg, metric_op, t->inverted, t->threshold, st);
+    ht.mark("select_launched");
   }
   hipEventRecord(ctx->ev[4], st);
-  int32_t* h_ncand = host_take<int32_t>(cs, std::max(ns, 1));
-  uint64_t* h_state = host_take<uint64_t>(cs, sel_words * (size_t)std::max(ns, 1));
+  uint64_t* h_selmem = host_take<uint64_t>(cs, sel_words * (size_t)std::max(ns, 1));
+  uint64_t* h_gath = host_take<uint64_t>(cs, (size_t)std::max<int64_t>(gtotal, 1));
+  if (!h_selmem || !h_gath) return set_error(DG_ERR_OOM, "topN read-back");
+  if (ns) {
+    DG_HIP(hipMemcpyAsync(h_selmem, d_selmem, 8 * sel_words * (size_t)ns, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h_gath, d_gath, 8 * (size_t)gtotal, hipMemcpyDeviceToHost, st));
+  }
+  std::vector<int32_t> h_ncand_v(std::max(ns, 1));
+  int32_t* h_ncand = h_ncand_v.data();
+  uint64_t* h_state = h_selmem;
   std::vector<int32_t*> h_cand(ns, nullptr);
   std::vector<uint64_t*> h_tab(ns, nullptr);
-  if (ns) {
-    DG_HIP(hipMemcpyAsync(h_ncand, d_ncand, 4 * ns, hipMemcpyDeviceToHost, st));
-    DG_HIP(hipMemcpyAsync(h_state, d_state, 8 * sel_words * (size_t)ns, hipMemcpyDeviceToHost, st));
-  }
-  for (int k = 0; k < ns; ++k) {
+  rc = finish_call(cs, st);
+  ht.mark("synced");
+  if (rc) return rc;
+  for (int k = 0; k < ns; ++k) {  // unpack [id, rec slots] records into ids + rec-strided slots
     const int i = sel_seg[k];
+    h_ncand[k] = *reinterpret_cast<const int32_t*>(h_selmem + sel_words * k + 4);
+    const int64_t g = std::min<int64_t>(gcap[i], h_ncand[k]);
     h_cand[k] = host_take<int32_t>(cs, (size_t)std::max<int64_t>(gcap[i], 1));
     h_tab[k] = host_take<uint64_t>(cs, (size_t)std::max<int64_t>(gcap[i], 1) * rec);
     if (!h_cand[k] || !h_tab[k]) return set_error(DG_ERR_OOM, "topN read-back");
-    DG_HIP(hipMemcpyAsync(h_cand[k], sel[k].cand, 4 * (size_t)gcap[i], hipMemcpyDeviceToHost, st));
-    DG_HIP(hipMemcpyAsync(h_tab[k], sel[k].gathered, 8 * (size_t)gcap[i] * rec, hipMemcpyDeviceToHost, st));
+    const uint64_t* src = h_gath + goff[i];
+    for (int64_t c = 0; c < g; ++c) {
+      h_cand[k][c] = (int32_t)src[c * (rec + 1)];
+      memcpy(h_tab[k] + c * rec, src + c * (rec + 1) + 1, 8 * (size_t)rec);
+    }
   }
-  rc = finish_call(cs, st);
-  if (rc) return rc;
   // rare: more candidates than the speculative read-back held (many ties at the K-th key)
   bool again = false;
   for (int k = 0; k < ns; ++k) {
@@ -1330,18 +1442,52 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       int32_t id;
       int32_t idx;
     };
-    auto less = [](const E& a, const E& b) { return a.key != b.key ? a.key < b.key : a.id < b.id; };
-    auto gt = [&](const E& a, const E& b) { return less(b, a); };
-    std::priority_queue<E, std::vector<E>, decltype(gt)> pq(gt);  // min-heap on (key, id)
-    for (int c = 0; c < nc; ++c) {
-      E e{metric_key_host(h_tab[k][(size_t)c * rec + 1 + t->metric_agg], mk, t->inverted), h_cand[k][c], c};
-      if ((int)pq.size() < t->threshold || pq.top().key < e.key) pq.push(e);
-      if ((int)pq.size() > t->threshold) pq.pop();
-    }
+    const int K = t->threshold;
+    std::vector<E> all(nc);
+    for (int c = 0; c < nc; ++c)
+      all[c] = E{metric_key_host(h_tab[k][(size_t)c * rec + 1 + t->metric_agg], mk, t->inverted), h_cand[k][c], c};
     std::vector<E> v;
-    while (!pq.empty()) {
-      v.push_back(pq.top());
-      pq.pop();
+    // The candidates are the ids whose key >= the K-th largest key (kth), in id order. The builder's
+    // priority queue (min-heap on (key, id), push when not full or top.key < key, pop the minimum
+    // when over K) then keeps every key > kth and, of the kth ties, those pushed while it was not
+    // full minus one per later push into a full queue, oldest (= smallest id) first: linear time.
+    uint64_t kth = 0;
+    if (nc > 0) {
+      std::vector<uint64_t> keys(nc);
+      for (int c = 0; c < nc; ++c) keys[c] = all[c].key;
+      const int r = std::min(nc, K) - 1;
+      std::nth_element(keys.begin(), keys.begin() + r, keys.end(), std::greater<uint64_t>());
+      kth = keys[r];
+    }
+    bool fifo = true;
+    for (int c = 0; c < nc && fifo; ++c) fifo = all[c].key >= kth;
+    if (fifo) {
+      std::vector<int> ties;
+      int count = 0;
+      size_t popped = 0;
+      for (int c = 0; c < nc; ++c) {
+        if (all[c].key > kth) {
+          v.push_back(all[c]);
+          if (count < K) count++;
+          else popped++;
+        } else if (count < K) {
+          ties.push_back(c);
+          count++;
+        }
+      }
+      for (size_t q = popped; q < ties.size(); ++q) v.push_back(all[ties[q]]);
+    } else {  // not reached for an exact K-th key; the builder's queue, literally
+      auto less = [](const E& a, const E& b) { return a.key != b.key ? a.key < b.key : a.id < b.id; };
+      auto gt = [&](const E& a, const E& b) { return less(b, a); };
+      std::priority_queue<E, std::vector<E>, decltype(gt)> pq(gt);  // min-heap on (key, id)
+      for (int c = 0; c < nc; ++c) {
+        if ((int)pq.size() < K || pq.top().key < all[c].key) pq.push(all[c]);
+        if ((int)pq.size() > K) pq.pop();
+      }
+      while (!pq.empty()) {
+        v.push_back(pq.top());
+        pq.pop();
+      }
     }
     std::sort(v.begin(), v.end(), [](const E& a, const E& b) { return a.key != b.key ? a.key > b.key : a.id < b.id; });
     out_n[i] = (int32_t)v.size();
@@ -1359,6 +1505,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   m.decode_ms = f2;
   m.aggregate_ms = f3;
   m.total_ms = ms_since(t0);
+  ht.mark("done");
   if (metrics) *metrics = m;
   return DG_OK;
 }
@@ -1513,18 +1660,30 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
     for (size_t k : keep) out.push_back(ents[k]);
     ents.swap(out);
   };
-  // identity of a dimension value across segments (TopNBinaryFn keys results by value)
-  struct IdHash {
-    size_t operator()(const std::pair<bool, std::string_view>& k) const {
-      return std::hash<std::string_view>()(k.second) ^ (k.first ? 0x9e3779b97f4a7c15ull : 0);
-    }
+  // identity of a dimension value across segments (TopNBinaryFn keys results by value): the
+  // attach-time value hash (segment mode) or the global id, in a flat open-addressing table; a hash
+  // hit is confirmed on the bytes
+  auto ident = [&](const Ent& e) -> uint64_t {
+    if (!segs) return (uint64_t)e.key * 0x9e3779b97f4a7c15ull;
+    const Column* c = lcol[e.list];
+    if (!c || e.key < 0 || e.key >= (int64_t)c->dict.size()) return kNullValueHash;
+    return c->dict_hash[e.key];
   };
-  std::unordered_map<std::pair<bool, std::string_view>, size_t, IdHash> pos;
-  std::unordered_map<int64_t, size_t> kpos;
-  auto ident = [&](const Ent& e) {
-    std::string_view sv;
-    const bool isnull = value_of(e, &sv);
-    return std::make_pair(isnull, isnull ? std::string_view() : sv);
+  auto same = [&](const Ent& a, const Ent& b) -> bool {
+    if (!segs) return a.key == b.key;
+    std::string_view sa, sb;
+    const bool an = value_of(a, &sa), bn = value_of(b, &sb);
+    return an == bn && (an || sa == sb);
+  };
+  std::vector<int32_t> slot_of;
+  std::vector<uint64_t> slot_hash;
+  size_t tmask = 0;
+  auto table_reset = [&](size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 16) cap <<= 1;
+    slot_of.assign(cap, -1);
+    slot_hash.resize(cap);
+    tmask = cap - 1;
   };
   std::vector<Ent> acc, cur;
   bool have = false;
@@ -1548,31 +1707,26 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
       continue;
     }
     // retVals (LinkedHashMap): r1's entries, then r2's new values; shared values combined in place
-    if (segs) {
-      pos.clear();
-      pos.reserve(2 * (acc.size() + cur.size()) + 16);
-      for (size_t e = 0; e < acc.size(); ++e) pos.emplace(ident(acc[e]), e);
-    } else {
-      kpos.clear();
-      kpos.reserve(2 * (acc.size() + cur.size()) + 16);
-      for (size_t e = 0; e < acc.size(); ++e) kpos.emplace(acc[e].key, e);
-    }
-    for (auto& e : cur) {
-      size_t hit = SIZE_MAX;
-      if (segs) {
-        auto it = pos.find(ident(e));
-        if (it != pos.end()) hit = it->second;
-      } else {
-        auto it = kpos.find(e.key);
-        if (it != kpos.end()) hit = it->second;
+    table_reset(acc.size() + cur.size());
+    auto find_or_insert = [&](const Ent& e, int32_t idx) -> int32_t {
+      const uint64_t h = ident(e);
+      for (size_t q = h & tmask;; q = (q + 1) & tmask) {
+        if (slot_of[q] < 0) {
+          slot_of[q] = idx;
+          slot_hash[q] = h;
+          return -1;
+        }
+        if (slot_hash[q] == h && same(acc[slot_of[q]], e)) return slot_of[q];
       }
-      if (hit != SIZE_MAX) {
+    };
+    for (size_t e = 0; e < acc.size(); ++e) find_or_insert(acc[e], (int32_t)e);
+    for (auto& e : cur) {
+      const int32_t hit = find_or_insert(e, (int32_t)acc.size());
+      if (hit >= 0) {
         Ent& a = acc[hit];
         for (int k = 0; k < na; ++k) vals[a.vo + k] = combine_abi(plan.kind[k], vals[a.vo + k], vals[e.vo + k]);
         a.mkey = abi_metric_key(mk, vals[a.vo + t->metric_agg], t->inverted);
       } else {
-        if (segs) pos.emplace(ident(e), acc.size());
-        else kpos.emplace(e.key, acc.size());
         acc.push_back(e);
       }
     }
@@ -1631,8 +1785,12 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   std::vector<int64_t> tiles_rows(n, 0);
   std::vector<uint64_t> cap(n, 0);
   DecodeBatch db;
-  int32_t* d_over = dev_take<int32_t>(cs, 1);
-  DG_HIP(hipMemsetAsync(d_over, 0, 4, st));
+  // staged zeros: overflow flag + per-segment compaction counts (one read-back)
+  int32_t* d_over;
+  int32_t* h_z = up_take<int32_t>(cs, 2 + 2 * (size_t)std::max(n, 1), &d_over, st);
+  if (!h_z) return set_error(DG_ERR_OOM, "groupBy counters");
+  memset(h_z, 0, 4 * (2 + 2 * (size_t)std::max(n, 1)));
+  unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(d_over + 2);
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
@@ -1704,27 +1862,26 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
   m.bytes_read = db.bytes;
-  uint64_t* h_init = host_take<uint64_t>(cs, rec);
+  uint64_t* d_init;
+  uint64_t* h_init = up_take<uint64_t>(cs, rec, &d_init, st);
+  if (!h_init) return set_error(DG_ERR_OOM, "accumulator init");
   h_init[0] = 0;
   for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
-  uint64_t* d_init = dev_take<uint64_t>(cs, rec);
-  DG_HIP(hipMemcpyAsync(d_init, h_init, rec * 8, hipMemcpyHostToDevice, st));
-  for (int i = 0; i < n; ++i)
-    if (cur[i].any) launch_fill_u64(jobs[i].slots, (int64_t)cap[i], rec, d_init, st);
   std::vector<int32_t> begin;
   int ntiles = 0;
   int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
   if (!d_tile) return set_error(DG_ERR_DEVICE, "tile table");
   for (int i = 0; i < n; ++i) jobs[i].tile_begin = begin[i];
-  GroupJob* h_jobs = host_take<GroupJob>(cs, n);
+  GroupJob* d_jobs;
+  GroupJob* h_jobs = up_take<GroupJob>(cs, n, &d_jobs, st);
+  if (!h_jobs) return set_error(DG_ERR_OOM, "groupBy jobs");
   memcpy(h_jobs, jobs.data(), sizeof(GroupJob) * n);
-  GroupJob* d_jobs = dev_take<GroupJob>(cs, n);
-  DG_HIP(hipMemcpyAsync(d_jobs, h_jobs, sizeof(GroupJob) * n, hipMemcpyHostToDevice, st));
+  DG_FLUSH(cs, st);
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) launch_fill_u64(jobs[i].slots, (int64_t)cap[i], rec, d_init, st);
   hipEventRecord(ctx->ev[3], st);
   launch_groupby(d_jobs, d_tile, ntiles, plan, st);
   // compaction
-  unsigned long long* d_cnt = dev_take<unsigned long long>(cs, n);
-  DG_HIP(hipMemsetAsync(d_cnt, 0, 8 * n, st));
   std::vector<uint64_t*> ok(n, nullptr), os(n, nullptr);
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
@@ -1735,10 +1892,10 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     launch_groupby_compact(jobs[i].keys, jobs[i].slots, cap[i], rec, ok[i], os[i], d_cnt + i, st);
   }
   hipEventRecord(ctx->ev[4], st);
-  unsigned long long* h_cnt = host_take<unsigned long long>(cs, n);
-  int32_t* h_over = host_take<int32_t>(cs, 1);
-  DG_HIP(hipMemcpyAsync(h_cnt, d_cnt, 8 * n, hipMemcpyDeviceToHost, st));
-  DG_HIP(hipMemcpyAsync(h_over, d_over, 4, hipMemcpyDeviceToHost, st));
+  int32_t* h_over = host_take<int32_t>(cs, 2 + 2 * (size_t)std::max(n, 1));
+  if (!h_over) return set_error(DG_ERR_OOM, "groupBy read-back");
+  unsigned long long* h_cnt = reinterpret_cast<unsigned long long*>(h_over + 2);
+  DG_HIP(hipMemcpyAsync(h_over, d_over, 4 * (2 + 2 * (size_t)n), hipMemcpyDeviceToHost, st));
   rc = finish_call(cs, st);
   if (rc) return rc;
   if (*h_over) return set_error(DG_ERR_TABLE_FULL, "groupBy hash table full");

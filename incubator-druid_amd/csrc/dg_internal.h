@@ -144,6 +144,7 @@ struct Column {
   // dictionary-encoded string column
   std::vector<std::string> dict;
   std::vector<uint8_t> dict_null;      // 1 = null / empty value
+  std::vector<uint64_t> dict_hash;     // value_hash of every dictionary value (cross-segment merges)
   int bitmap_roaring = 0;
   bool has_bitmaps = false;
   std::vector<int64_t> bm_off;         // byte offset of each bitmap inside bm_bytes (4-byte aligned)
@@ -177,6 +178,17 @@ struct Segment {
     return it == by_name.end() ? nullptr : it->second;
   }
 };
+
+// 64-bit hash of a dimension value (FNV-1a + avalanche); identity across segments' dictionaries
+constexpr uint64_t kNullValueHash = 0x6e756c6c2d76616cull;
+inline uint64_t value_hash(const std::string& v) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (unsigned char ch : v) h = (h ^ ch) * 0x100000001b3ull;
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  return h == kNullValueHash ? h + 1 : h;
+}
 
 // error reporting
 int set_error(int code, const char* fmt, ...);
@@ -228,7 +240,7 @@ struct TopnSelJob {
   uint64_t* state;        // [0] = K-th key, [1] = aggregated rows, [2] = touched ids (zeroed by the host)
   int32_t* cand;          // candidate ids (capacity card)
   int32_t* ncand;
-  uint64_t* gathered;     // [gather_cap][1 + naggs] records of cand[0 .. gather_cap)
+  uint64_t* gathered;     // [gather_cap][2 + naggs]: id, then the record of cand[0 .. gather_cap)
   uint64_t* keys;         // [card] metric keys (0 = untouched)
   uint32_t* hist;         // [8][256] radix histograms (zeroed by the host)
   int32_t* blkcnt;        // [ceil(card / 1024)] candidates per workgroup

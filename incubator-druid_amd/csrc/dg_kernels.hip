@@ -1173,9 +1173,10 @@ __global__ __launch_bounds__(kSelBlock) void k_topn_compact(const TopnSelJob* __
     long long pos = s_base + __popcll(m & ((1ull << lane) - 1ull));
     for (int w = 0; w < wave; ++w) pos += s_wave[w];
     jb.cand[pos] = (int32_t)i;
-    if (pos < jb.gather_cap) {
+    if (pos < jb.gather_cap) {  // read-back record: [id, rec slots]
       const int rec = naggs + 1;
-      for (int c = 0; c < rec; ++c) jb.gathered[pos * rec + c] = jb.table[i * rec + c];
+      jb.gathered[pos * (rec + 1)] = (uint64_t)i;
+      for (int c = 0; c < rec; ++c) jb.gathered[pos * (rec + 1) + 1 + c] = jb.table[i * rec + c];
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {

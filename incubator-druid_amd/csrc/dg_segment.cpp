@@ -308,6 +308,8 @@ int parse_string(Context* ctx, Column* c, Slice s) {
     c->dict[i].assign((const char*)p, len > 0 ? len : 0);
     c->dict_null[i] = len <= 0;  // size 0 => null (replaceWithDefault), GenericIndexed.java:369-372
   }
+  c->dict_hash.resize(dict.n);
+  for (int32_t i = 0; i < dict.n; ++i) c->dict_hash[i] = c->dict_null[i] ? kNullValueHash : value_hash(c->dict[i]);
   if (version != 2) return set_error(DG_ERR_UNSUPPORTED, "%s: uncompressed VSize ids", c->name.c_str());
   if (s.left() < 11 || s.p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: bad id stream", c->name.c_str());
   BlockColumn& col = c->data;
