@@ -1332,7 +1332,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     // candidates = ids whose key >= the K-th key: the threshold plus ties, rarely more
     gcap[i] = std::min<int64_t>(card[i], 2 * (int64_t)t->threshold + 64);
     goff[i] = gtotal;
-    gtotal += gcap[i] * (rec + 1);
+    gtotal += gcap[i] * (rec + 1) + (gcap[i] + 3) / 4;  // records + u16 builder order
   }
   // read-back block (one D2H copy): gathered records of every segment
   uint64_t* d_gath = dev_take<uint64_t>(cs, (size_t)std::max<int64_t>(gtotal, 1));
@@ -1348,6 +1348,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     sj.blkcnt = dev_take<int32_t>(cs, (size_t)((card[i] + kSelBlock - 1) / kSelBlock));
     sj.gather_cap = (int32_t)gcap[i];
     sj.gathered = d_gath + goff[i];
+    sj.order = reinterpret_cast<uint16_t*>(d_gath + goff[i] + gcap[i] * (rec + 1));
     if (!sj.cand || !sj.keys || !sj.blkcnt) return set_error(DG_ERR_OOM, "topN candidates");
     max_card = std::max(max_card, card[i]);
     sel.push_back(sj);
@@ -1402,6 +1403,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       memcpy(h_tab[k] + c * rec, src + c * (rec + 1) + 1, 8 * (size_t)rec);
     }
   }
+  ht.mark("unpacked");
   // rare: more candidates than the speculative read-back held (many ties at the K-th key)
   bool again = false;
   for (int k = 0; k < ns; ++k) {
@@ -1432,6 +1434,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   }
   for (int i = 0; i < n; ++i)
     if (cur[i].any) m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : reinterpret_cast<Segment*>(segs[i])->nrows;
+  ht.mark("overflow_checked");
   // replay TopNNumericResultBuilder over the candidates in id (= dimension value) order
   for (int k = 0; k < ns; ++k) {
     const int i = sel_seg[k];
@@ -1443,10 +1446,42 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       int32_t idx;
     };
     const int K = t->threshold;
+    std::vector<E> v;
+    if (nc > 0 && nc <= gcap[i] && nc <= kTopnOrderCap) {
+      // k_topn_order sorted the candidates by (key desc, id asc); keep every key > kth and, of the
+      // kth ties, those the builder's queue keeps (see below), already in output order
+      const uint16_t* ord = reinterpret_cast<const uint16_t*>(h_gath + goff[i] + gcap[i] * (rec + 1));
+      auto key_at = [&](int c) { return metric_key_host(h_tab[k][(size_t)c * rec + 1 + t->metric_agg], mk, t->inverted); };
+      const int r = std::min(nc, K) - 1;
+      const uint64_t kth = key_at(ord[r]);
+      bool exact = key_at(ord[nc - 1]) >= kth;  // nothing below the K-th key
+      int g = 0, gF = 0;
+      while (g < nc && key_at(ord[g]) > kth) gF += ord[g++] < K;
+      if (exact) {
+        for (int e = 0; e < g; ++e) v.push_back(E{0, h_cand[k][ord[e]], (int32_t)ord[e]});
+        int skip = g - gF;  // ties popped by later pushes into the full queue, oldest first
+        for (int e = g; e < nc && (int)v.size() < K; ++e) {
+          if (ord[e] >= K) continue;  // a tie after the queue filled is never pushed
+          if (skip > 0) {
+            skip--;
+            continue;
+          }
+          v.push_back(E{0, h_cand[k][ord[e]], (int32_t)ord[e]});
+        }
+        out_n[i] = (int32_t)v.size();
+        for (size_t e = 0; e < v.size(); ++e) {
+          const int64_t o = (int64_t)i * t->threshold + (int64_t)e;
+          out_ids[o] = v[e].id;
+          for (int a = 0; a < na; ++a)
+            out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[k][(size_t)v[e].idx * rec + 1 + a]);
+        }
+        continue;
+      }
+      v.clear();
+    }
     std::vector<E> all(nc);
     for (int c = 0; c < nc; ++c)
       all[c] = E{metric_key_host(h_tab[k][(size_t)c * rec + 1 + t->metric_agg], mk, t->inverted), h_cand[k][c], c};
-    std::vector<E> v;
     // The candidates are the ids whose key >= the K-th largest key (kth), in id order. The builder's
     // priority queue (min-heap on (key, id), push when not full or top.key < key, pop the minimum
     // when over K) then keeps every key > kth and, of the kth ties, those pushed while it was not
@@ -1497,6 +1532,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[k][(size_t)v[e].idx * rec + 1 + a]);
     }
   }
+  ht.mark("replayed");
   float f1 = 0, f2 = 0, f3 = 0;
   hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
   hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);

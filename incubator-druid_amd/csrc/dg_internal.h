@@ -244,10 +244,12 @@ struct TopnSelJob {
   uint64_t* keys;         // [card] metric keys (0 = untouched)
   uint32_t* hist;         // [8][256] radix histograms (zeroed by the host)
   int32_t* blkcnt;        // [ceil(card / 1024)] candidates per workgroup
+  uint16_t* order;        // [gather_cap] gather positions in builder order (filled when ncand <= 4096)
   int32_t gather_cap;
   int32_t pad;
 };
 constexpr int kSelBlock = 1024;
+constexpr int kTopnOrderCap = 4096;  // k_topn_order sorts at most this many candidates
 void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, int naggs, int metric, int metric_op,
                         int inverted, int threshold, hipStream_t s);
 void launch_groupby(const GroupJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, hipStream_t s);

@@ -822,81 +822,137 @@ __global__ __launch_bounds__(1024) void k_topn_bin_scan(const uint32_t* __restri
   }
 }
 
+// Rows of one tile are counting-sorted by bin in LDS first, so that every bin's chunk of this tile
+// goes out as consecutive lanes writing consecutive slots (coalesced), not as scattered 2- and
+// 8-byte stores. Segments with more than kMaxSortBins bins take per-row global reservations.
+constexpr int kMaxSortBins = 2048;
+constexpr int kRowsPerThread = kTileRows / kBinThreads;  // 8 = two quads
+static_assert(kRowsPerThread == 8, "tile = two quads per thread");
+
 __global__ __launch_bounds__(kBinThreads) void k_topn_bin_scatter(const ScanJob* __restrict__ jobs,
                                                                   const int32_t* __restrict__ tile_job,
                                                                   const int32_t* __restrict__ bin_first, int shift,
                                                                   uint32_t* __restrict__ cursor, AggPlan plan,
                                                                   uint16_t* __restrict__ lid, uint64_t* __restrict__ vals,
                                                                   int64_t cap) {
-  __shared__ uint32_t s_cnt[kMaxTileBins];
+  __shared__ uint32_t s_cnt[kMaxSortBins];   // counts, then tile-local starts
+  __shared__ uint32_t s_goff[kMaxSortBins];  // reserved global offsets
+  __shared__ uint32_t s_gpos[kTileRows];     // global slot of the k-th sorted row
+  __shared__ uint64_t s_val[kTileRows];
+  __shared__ uint16_t s_lid[kTileRows];
+  __shared__ int64_t s_tmp[kBinThreads / 64];
   const int seg = tile_job[blockIdx.x];
   const ScanJob& j = jobs[seg];
   const int nb = (int)((j.nbuckets + (1ll << shift) - 1) >> shift);
-  const bool lds = nb <= kMaxTileBins;
   const uint32_t lmask = (1u << shift) - 1;
   uint32_t* cur = cursor + bin_first[seg];
   const int na = plan.n;
-  if (lds)
-    for (int b = threadIdx.x; b < nb; b += kBinThreads) s_cnt[b] = 0;
-  __syncthreads();
   int64_t r0, r1;
   tile_rows(j, blockIdx.x, &r0, &r1);
   const int64_t full = r0 + ((r1 - r0) & ~3ll);
-  if (lds) {  // this tile's rows per bin -> one reserved chunk per bin
-    for (int64_t r = r0 + 4 * threadIdx.x; r < full; r += 4 * kBinThreads) {
-      const unsigned m = quad_selected(j, r);
-      if (!m) continue;
-      uint32_t id[4];
-      load_ids4(j.key, r, id);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if ((m >> k) & 1) atomicAdd(&s_cnt[id[k] >> shift], 1u);
-    }
-    if (threadIdx.x == 0)
-      for (int64_t r = full; r < r1; ++r) {
-        int64_t b;
-        if (row_selected(j, r, &b)) atomicAdd(&s_cnt[load_id(j.key, r) >> shift], 1u);
-      }
-    __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += kBinThreads)
-      if (s_cnt[b]) s_cnt[b] = atomicAdd(&cur[b], s_cnt[b]);
-    __syncthreads();
-  }
-  auto put = [&](uint32_t id, uint64_t pos, const uint64_t* in) {
-    lid[pos] = (uint16_t)(id & lmask);
-    for (int a = 0; a < na; ++a) vals[(size_t)a * cap + pos] = in[a];
-  };
-  for (int64_t r = r0 + 4 * threadIdx.x; r < full; r += 4 * kBinThreads) {
-    const unsigned m = quad_selected(j, r);
-    if (!m) continue;
-    uint32_t id[4];
-    load_ids4(j.key, r, id);
-    uint64_t in[4][kMaxAggs];
-    for (int a = 0; a < na; ++a) {
-      uint64_t raw[4] = {0, 0, 0, 0};
-      const int vk = j.vals[a].kind;
-      if (plan.kind[a] != DG_AGG_COUNT && vk != VIEW_ABSENT) load_raw4(j.vals[a], r, raw);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) in[k][a] = agg_input_raw(plan.kind[a], vk, raw[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (!((m >> k) & 1)) continue;
-      const uint32_t b = id[k] >> shift;
-      const uint64_t pos = lds ? atomicAdd(&s_cnt[b], 1u) : atomicAdd(&cur[b], 1u);
-      put(id[k], pos, in[k]);
-    }
-  }
-  if (threadIdx.x == 0)
-    for (int64_t r = full; r < r1; ++r) {
+  if (nb > kMaxSortBins) {  // huge dictionaries: per-row reservation
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kBinThreads) {
       int64_t bb;
       if (!row_selected(j, r, &bb)) continue;
-      const uint32_t id = load_id(j.key, r), b = id >> shift;
-      uint64_t in[kMaxAggs];
-      for (int a = 0; a < na; ++a) in[a] = agg_input(plan.kind[a], j.vals[a], r);
-      const uint64_t pos = lds ? atomicAdd(&s_cnt[b], 1u) : atomicAdd(&cur[b], 1u);
-      put(id, pos, in);
+      const uint32_t id = load_id(j.key, r);
+      const uint32_t pos = atomicAdd(&cur[id >> shift], 1u);
+      lid[pos] = (uint16_t)(id & lmask);
+      for (int a = 0; a < na; ++a) vals[(size_t)a * cap + pos] = agg_input(plan.kind[a], j.vals[a], r);
     }
+    return;
+  }
+  for (int b = threadIdx.x; b < nb; b += kBinThreads) s_cnt[b] = 0;
+  __syncthreads();
+  // pass 1: my two quads (rows r0 + 4 * (tid + 256 * u) ..): bin and rank within the tile's bin
+  uint32_t id[2][4], rk[2][4];
+  unsigned m[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t r = r0 + 4 * (threadIdx.x + (int64_t)u * kBinThreads);
+    m[u] = 0;
+    if (r < full) {
+      m[u] = quad_selected(j, r);
+      if (m[u]) load_ids4(j.key, r, id[u]);
+    } else if (r < r1) {  // the segment's ragged last quad
+      for (int k = 0; k < 4 && r + k < r1; ++k) {
+        int64_t bb;
+        if (row_selected(j, r + k, &bb)) {
+          m[u] |= 1u << k;
+          id[u][k] = load_id(j.key, r + k);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((m[u] >> k) & 1) rk[u][k] = atomicAdd(&s_cnt[id[u][k] >> shift], 1u);
+  }
+  __syncthreads();
+  // tile-local starts (exclusive scan of the counts) + one global reservation per non-empty bin
+  {
+    const int per = (nb + kBinThreads - 1) / kBinThreads;
+    const int b0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (int q = 0; q < per; ++q)
+      if (b0 + q < nb) sum += s_cnt[b0 + q];
+    int64_t tot;
+    uint32_t run = (uint32_t)block_exclusive_scan(sum, &tot, s_tmp);
+    for (int q = 0; q < per; ++q) {
+      const int b = b0 + q;
+      if (b >= nb) break;
+      const uint32_t c = s_cnt[b];
+      s_goff[b] = c ? atomicAdd(&cur[b], c) : 0u;
+      s_cnt[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  // pass 2: global slots and local ids into sorted order
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((m[u] >> k) & 1) {
+        const uint32_t b = id[u][k] >> shift;
+        const uint32_t p = s_cnt[b] + rk[u][k];
+        s_gpos[p] = s_goff[b] + rk[u][k];
+        s_lid[p] = (uint16_t)(id[u][k] & lmask);
+      }
+  __syncthreads();
+  int ntile = 0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) ntile += __popc(m[u]);
+  int64_t tot_sel;
+  {
+    int64_t t;
+    block_exclusive_scan(ntile, &t, s_tmp);
+    tot_sel = t;
+  }
+  for (int p = threadIdx.x; p < tot_sel; p += kBinThreads) lid[s_gpos[p]] = s_lid[p];
+  // pass 3, per aggregator: inputs into sorted order, then coalesced stores
+  for (int a = 0; a < na; ++a) {
+    const int vk = j.vals[a].kind;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!m[u]) continue;
+      const int64_t r = r0 + 4 * (threadIdx.x + (int64_t)u * kBinThreads);
+      uint64_t in[4];
+      if (r + 4 <= full) {
+        uint64_t raw[4] = {0, 0, 0, 0};
+        if (plan.kind[a] != DG_AGG_COUNT && vk != VIEW_ABSENT) load_raw4(j.vals[a], r, raw);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) in[k] = agg_input_raw(plan.kind[a], vk, raw[k]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) in[k] = ((m[u] >> k) & 1) ? agg_input(plan.kind[a], j.vals[a], r + k) : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((m[u] >> k) & 1) s_val[s_cnt[id[u][k] >> shift] + rk[u][k]] = in[k];
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < tot_sel; p += kBinThreads) vals[(size_t)a * cap + s_gpos[p]] = s_val[p];
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(kBinThreads) void k_topn_bin_reduce(const ScanJob* __restrict__ jobs,
@@ -1185,6 +1241,51 @@ __global__ __launch_bounds__(kSelBlock) void k_topn_compact(const TopnSelJob* __
   }
 }
 
+// Final ordering of one segment's gathered candidates (TopNNumericResultBuilder.build order:
+// metric descending, then dimension value = dictionary id ascending), one workgroup per segment:
+// order[k] = gather position of the k-th entry. Bitonic sort in LDS; skipped (order untouched)
+// when the candidates exceed kOrderCap (the host sorts then).
+constexpr int kOrderCap = 4096;
+__global__ __launch_bounds__(1024) void k_topn_order(const TopnSelJob* __restrict__ jobs, int naggs, int metric, int op,
+                                                     int kind, int inverted) {
+  __shared__ uint64_t s_key[kOrderCap];
+  __shared__ uint16_t s_pos[kOrderCap];
+  const TopnSelJob& jb = jobs[blockIdx.x];
+  const int n = min(*jb.ncand, jb.gather_cap);
+  if (n > kOrderCap || n <= 0) return;
+  int P = 1;
+  while (P < n) P <<= 1;
+  const int rec = naggs + 1;
+  for (int c = threadIdx.x; c < P; c += 1024) {
+    s_key[c] = c < n ? metric_key(jb.gathered[(size_t)c * (rec + 1) + 1 + 1 + metric], op, kind, inverted) : 0ull;
+    s_pos[c] = (uint16_t)c;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int c = threadIdx.x; c < P; c += 1024) {
+        const int o = c ^ stride;
+        if (o > c) {
+          const uint64_t ka = s_key[c], kb = s_key[o];
+          const uint16_t pa = s_pos[c], pb = s_pos[o];
+          // a precedes b: larger key, or equal key and smaller position (a padding slot has key 0
+          // and position >= n, so it sorts last)
+          const bool a_first = ka != kb ? ka > kb : pa < pb;
+          const bool up = (c & size) == 0;
+          if (a_first != up) {
+            s_key[c] = kb;
+            s_key[o] = ka;
+            s_pos[c] = pb;
+            s_pos[o] = pa;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int c = threadIdx.x; c < n; c += 1024) jb.order[c] = s_pos[c];
+}
+
 void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, int naggs, int metric, int metric_op,
                         int inverted, int threshold, hipStream_t s) {
   if (njobs <= 0 || max_card <= 0) return;
@@ -1196,6 +1297,8 @@ void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, i
     hipLaunchKernelGGL(k_topn_radix, grid, dim3(kSelBlock), 0, s, d_jobs, level, threshold);
   hipLaunchKernelGGL(k_topn_count, grid, dim3(kSelBlock), 0, s, d_jobs, threshold);
   hipLaunchKernelGGL(k_topn_compact, grid, dim3(kSelBlock), 0, s, d_jobs, naggs, threshold);
+  hipLaunchKernelGGL(k_topn_order, dim3((unsigned)njobs), dim3(1024), 0, s, d_jobs, naggs, metric, metric_op >> 8,
+                     metric_op & 255, inverted);
 }
 
 // ------------------------------------------------------------------------------------------------

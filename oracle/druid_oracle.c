@@ -294,6 +294,7 @@ typedef struct {
   /* string */
   gindexed dict, bitmaps;
   int num_bytes;
+  const uint8_t* vsize; /* uncompressed VSizeColumnarInts values (big-endian), or NULL */
 } ocol;
 
 typedef struct {
@@ -359,8 +360,19 @@ static int parse_string(ocol* c, const uint8_t* p) {
     c->compression = q[10];
     q += 11;
     if (gi_read(&q, c->end, &c->blocks)) return -1;
+  } else if (version == 0 || version == 3) {
+    /* VSizeColumnarInts.readFromByteBuffer (data/VSizeColumnarInts.java:177-195):
+     * [u8 ver 0][u8 numBytes][i32 size BE][size bytes: big-endian values + (4 - numBytes) pad] */
+    if (q[0] != 0x00) return -1;
+    c->num_bytes = q[1];
+    int32_t nbytes = be32(q + 2);
+    if (c->num_bytes < 1 || c->num_bytes > 4 || nbytes < 4 - c->num_bytes) return -1;
+    c->total = (nbytes - (4 - c->num_bytes)) / c->num_bytes;
+    c->vsize = q + 6;
+    c->compression = -1;
+    q += 6 + nbytes;
   } else {
-    return -2; /* VSizeColumnarInts (uncompressed dims) not restated yet */
+    return -1;
   }
   if (!(flags & 4)) {
     if (gi_read(&q, c->end, &c->bitmaps)) return -1;
@@ -632,6 +644,14 @@ int or_dim_ids(void* h, const char* name, int32_t* out) {
   oseg* s = (oseg*)h;
   ocol* c = find_col(s, name);
   if (!c || c->kind != OR_STRING) return -1;
+  if (c->vsize) { /* VSizeColumnarInts.get (:124-127): getInt(pos) >>> (32 - 8 * numBytes), big-endian */
+    for (int64_t k = 0; k < c->total; ++k) {
+      const uint8_t* p = c->vsize + k * c->num_bytes;
+      uint32_t v = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+      out[k] = (int32_t)(v >> (32 - 8 * c->num_bytes));
+    }
+    return 0;
+  }
   uint8_t* buf = (uint8_t*)malloc(65536 + 16);
   int64_t done = 0;
   for (int32_t b = 0; b < c->blocks.n && done < c->total; ++b) {
