@@ -574,7 +574,7 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
   const BlockColumn& b = c->data;
   v->log2_per = b.log2_per;
   v->width = b.width;
-  v->pad = 0;
+  v->pad = b.big_endian ? kViewBigEndian : 0;
   if (c->type == DG_COL_LONG) v->kind = VIEW_LONG;
   else if (c->type == DG_COL_DOUBLE) v->kind = VIEW_DOUBLE;
   else if (c->type == DG_COL_FLOAT) v->kind = VIEW_FLOAT;
@@ -1312,6 +1312,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       fixed.key.blocks = dp;
       fixed.key.log2_per = 16;
       fixed.key.width = 1;
+      fixed.key.pad = 0;
       fixed.key.kind = VIEW_IDS;
       h_jobs[i] = fixed;
     }

@@ -29,13 +29,15 @@ enum ViewKind : int32_t { VIEW_ABSENT = 0, VIEW_LONG = 1, VIEW_FLOAT = 2, VIEW_D
 enum SlotOp : int32_t { OP_ADD_I64 = 0, OP_ADD_F64 = 1, OP_MIN_U64 = 2, OP_MAX_U64 = 3 };
 
 // A column as the kernels see it: value(row) lives at blocks[row >> log2_per] + (row & mask) * width.
+// flags: kViewBigEndian = dictionary ids stored big-endian (uncompressed VSizeColumnarInts).
 struct ColView {
   const uint8_t* const* blocks;
   int32_t log2_per;
   int32_t width;
   int32_t kind;
-  int32_t pad;
+  int32_t pad;  // flags
 };
+constexpr int32_t kViewBigEndian = 1;
 
 // LZ4 sequence checkpoints: built once per block at attach (lz4_index_block), one entry per
 // kLzSeqPerCp sequences = the compressed offset where that sequence's token starts. They let the
@@ -124,6 +126,7 @@ struct BlockColumn {
   int32_t width = 0;      // bytes per value
   int32_t codec = 0;
   int32_t nblocks = 0;
+  int32_t big_endian = 0;  // VSizeColumnarInts ids (uncompressed dimension)
   int64_t stored_bytes = 0;            // on-HBM bytes of all blocks (algorithmic bytes of a full scan)
   std::vector<int64_t> comp_off;       // host copy: offset of block b inside comp
   std::vector<int32_t> comp_len;

@@ -47,8 +47,19 @@ __device__ __forceinline__ const uint8_t* cv_ptr(const ColView& v, int64_t r) {
   return base + (size_t)(r & ((1ll << v.log2_per) - 1)) * (size_t)v.width;
 }
 
+// a width-byte big-endian id read as little-endian -> its value (VSizeColumnarInts.get, :124-127)
+__device__ __forceinline__ uint32_t id_bswap(uint32_t x, int width) {
+  const uint32_t b = __builtin_bswap32(x);
+  return width >= 4 ? b : b >> (32 - 8 * width);
+}
+
 __device__ __forceinline__ uint32_t load_id(const ColView& v, int64_t r) {
   const uint8_t* p = cv_ptr(v, r);
+  if (v.pad & kViewBigEndian) {  // uncompressed VSizeColumnarInts: big-endian, byte aligned
+    uint32_t x = 0;
+    for (int k = 0; k < v.width; ++k) x = (x << 8) | p[k];
+    return x;
+  }
   switch (v.width) {
     case 1: return p[0];
     case 2: return *reinterpret_cast<const uint16_t*>(p);
@@ -97,7 +108,7 @@ __device__ __forceinline__ uint64_t agg_input(int kind, const ColView& v, int64_
 // ---- four consecutive rows r .. r + 3 (r % 4 == 0, all inside the view's block): one or a few
 // wide loads per column instead of four scalar ones; consecutive threads read consecutive quads, so
 // every load instruction of a wave is one contiguous span ----
-__device__ __forceinline__ void load_ids4(const ColView& v, int64_t r, uint32_t id[4]) {
+__device__ __forceinline__ void load_ids4_le(const ColView& v, int64_t r, uint32_t id[4]) {
   const uint8_t* p = cv_ptr(v, r);
   switch (v.width) {
     case 1: {
@@ -130,6 +141,14 @@ __device__ __forceinline__ void load_ids4(const ColView& v, int64_t r, uint32_t 
       id[2] = w.z;
       id[3] = w.w;
     }
+  }
+}
+
+__device__ __forceinline__ void load_ids4(const ColView& v, int64_t r, uint32_t id[4]) {
+  load_ids4_le(v, r, id);
+  if (v.pad & kViewBigEndian) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) id[k] = id_bswap(id[k], v.width);
   }
 }
 

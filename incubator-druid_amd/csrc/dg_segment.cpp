@@ -310,21 +310,40 @@ int parse_string(Context* ctx, Column* c, Slice s) {
   }
   c->dict_hash.resize(dict.n);
   for (int32_t i = 0; i < dict.n; ++i) c->dict_hash[i] = c->dict_null[i] ? kNullValueHash : value_hash(c->dict[i]);
-  if (version != 2) return set_error(DG_ERR_UNSUPPORTED, "%s: uncompressed VSize ids", c->name.c_str());
-  if (s.left() < 11 || s.p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: bad id stream", c->name.c_str());
   BlockColumn& col = c->data;
-  col.width = s.p[1];
-  col.total = be32(s.p + 2);
-  col.size_per = be32(s.p + 6);
-  col.codec = s.p[10];
-  s.p += 11;
-  col.log2_per = log2i(col.size_per);
-  if (col.width < 1 || col.width > 4 || col.log2_per < 0)
-    return set_error(DG_ERR_FORMAT, "%s: bad id stream header", c->name.c_str());
-  GI blocks;
-  if (!gi_read(s, &blocks)) return set_error(DG_ERR_FORMAT, "%s: bad id blocks", c->name.c_str());
-  int rc = upload_blocks(ctx, &col, blocks);
-  if (rc) return rc;
+  if (version == 0 || version == 3) {
+    // UNCOMPRESSED_SINGLE_VALUE / UNCOMPRESSED_WITH_FLAGS: VSizeColumnarInts.readFromByteBuffer
+    // (data/VSizeColumnarInts.java:177-195): [0x00][numBytes][i32 size][big-endian values + pad].
+    // Read in place: kernels load numBytes big-endian bytes per row (getInt >>> bitsToShift, :124-127).
+    if (s.left() < 6 || s.p[0] != 0x00) return set_error(DG_ERR_FORMAT, "%s: bad VSize id stream", c->name.c_str());
+    col.width = s.p[1];
+    const int32_t nbytes = be32(s.p + 2);
+    if (col.width < 1 || col.width > 4 || nbytes < 4 - col.width || s.left() < 6 + (int64_t)nbytes)
+      return set_error(DG_ERR_FORMAT, "%s: bad VSize id stream header", c->name.c_str());
+    col.total = (nbytes - (4 - col.width)) / col.width;
+    col.codec = CODEC_NONE;
+    col.big_endian = 1;
+    s.p += 6;
+    int rc = upload_flat(&col, s.p, s.end);
+    if (rc) return rc;
+    s.p += nbytes;
+  } else if (version == 2) {
+    if (s.left() < 11 || s.p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: bad id stream", c->name.c_str());
+    col.width = s.p[1];
+    col.total = be32(s.p + 2);
+    col.size_per = be32(s.p + 6);
+    col.codec = s.p[10];
+    s.p += 11;
+    col.log2_per = log2i(col.size_per);
+    if (col.width < 1 || col.width > 4 || col.log2_per < 0)
+      return set_error(DG_ERR_FORMAT, "%s: bad id stream header", c->name.c_str());
+    GI blocks;
+    if (!gi_read(s, &blocks)) return set_error(DG_ERR_FORMAT, "%s: bad id blocks", c->name.c_str());
+    int rc = upload_blocks(ctx, &col, blocks);
+    if (rc) return rc;
+  } else {
+    return set_error(DG_ERR_FORMAT, "%s: dictionary-encoded part version %d", c->name.c_str(), version);
+  }
   if (!(flags & 4)) {
     GI bms;
     if (!gi_read(s, &bms)) return set_error(DG_ERR_FORMAT, "%s: bad bitmap index", c->name.c_str());

@@ -175,6 +175,16 @@ def ids_part(ids: np.ndarray, cardinality: int, compression: str, lz4_mode: str)
     return header + _blocks_generic_indexed(_compress_blocks(raw, size_per * nb, comp, lz4_mode))
 
 
+def vsize_ids_part(ids: np.ndarray, cardinality: int) -> bytes:
+    """VSizeColumnarIntsSerializer (data/VSizeColumnarIntsSerializer.java:40-96): header
+    [0x00][numBytes][i32 size], then each id as its low numBytes bytes big-endian, then
+    4 - numBytes zero bytes so the reader's getInt never runs off the end."""
+    nb = num_bytes_for_max(cardinality)
+    be = np.ascontiguousarray(ids, dtype=">u4").view(np.uint8).reshape(-1, 4)[:, 4 - nb:].tobytes()
+    payload = be + bytes(4 - nb)
+    return struct.pack(">BBi", 0x00, nb, len(payload)) + payload
+
+
 def concise_bitmaps(ids: np.ndarray, cardinality: int) -> List[bytes]:
     words, counts = _tools.concise_encode_column(ids, cardinality)
     out = []
@@ -254,9 +264,17 @@ def string_column_part(dictionary: List[Optional[str]], ids: np.ndarray, bitmap:
     dict_vals = [None if (v is None or v == "") else v.encode("utf-8") for v in dictionary]
     # null / "" are both stored as a zero-length value (NullHandling.replaceWithDefault)
     dict_vals = [b"" if v is None else v for v in dict_vals]
-    out = bytes([0x02]) + struct.pack(">i", 0)  # COMPRESSED, flags = 0 (single-value, bitmaps)
-    out += generic_indexed(dict_vals, sorted_flag=True)
-    out += ids_part(ids, card, compression, lz4_mode)
+    if compression == "uncompressed":
+        # IndexSpec dimensionCompression UNCOMPRESSED: VSizeColumnarIntsSerializer, part version
+        # UNCOMPRESSED_SINGLE_VALUE without flags (StringDimensionMergerV9.java:217-225,
+        # DictionaryEncodedColumnPartSerde.java:191-217)
+        out = bytes([0x00])
+        out += generic_indexed(dict_vals, sorted_flag=True)
+        out += vsize_ids_part(ids, card)
+    else:
+        out = bytes([0x02]) + struct.pack(">i", 0)  # COMPRESSED, flags = 0 (single-value, bitmaps)
+        out += generic_indexed(dict_vals, sorted_flag=True)
+        out += ids_part(ids, card, compression, lz4_mode)
     if bitmap == "concise":
         bms = concise_bitmaps(ids, card)
     else:
