@@ -19,6 +19,8 @@
  *                               TimeseriesQueryEngine.java:40-111)
  *   dg_topn_run              <- TopNQueryRunnerFactory.createRunner(segment).run (query/topn/TopNQueryRunnerFactory.java:61-90,
  *                               TopNQueryEngine.java:60-160 -> PooledTopNAlgorithm + TopNNumericResultBuilder)
+ *   dg_segment_set_dim_order <- StringComparator.compare over one dictionary (query/ordering/StringComparators.java),
+ *                               the order DimensionTopNMetricSpec / TopNLexicographicResultBuilder ranks values by
  *   dg_topn_merge            <- TopNBinaryFn.apply fold of QueryRunnerFactory.mergeRunners (query/topn/TopNBinaryFn.java:75-135)
  *   dg_groupby_run           <- GroupByStrategyV2.process -> GroupByQueryEngineV2.process
  *                               (query/groupby/strategy/GroupByStrategyV2.java:472-477, epinephelinae/GroupByQueryEngineV2.java:91-187)
@@ -44,7 +46,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 1
+#define DG_ABI_VERSION 2
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -85,9 +87,12 @@ extern "C" {
 #define DG_F_IN 5
 #define DG_F_BOUND 6
 
-/* bound orderings (query/ordering/StringComparators.java) */
+/* string orderings (query/ordering/StringComparators.java): bound filters use LEXICOGRAPHIC / NUMERIC,
+ * dimension-ordered topN all four */
 #define DG_ORDER_LEXICOGRAPHIC 0
 #define DG_ORDER_NUMERIC 1
+#define DG_ORDER_ALPHANUMERIC 2
+#define DG_ORDER_STRLEN 3
 
 typedef struct dg_context dg_context;
 typedef struct dg_segment dg_segment;
@@ -177,6 +182,13 @@ int dg_segment_dim_value(const dg_segment* seg, const char* dim, int32_t id, con
  * Call with bytes == NULL to get *total_bytes first. */
 int dg_segment_dim_dictionary(const dg_segment* seg, const char* dim, int64_t* offsets, char* bytes,
                               int64_t* total_bytes);
+/* Hand the engine one dictionary order (kept in HBM with the segment, set once per segment):
+ * slot = 2 * DG_ORDER_* + inverted (InvertedTopNMetricSpec over DimensionTopNMetricSpec);
+ * rank[id] for every dictionary id (card of them): position of the value under the comparator,
+ * comparator-equal values share a rank (has_ties != 0 then). The ordering is the caller's
+ * StringComparator (the JNI shim sorts the dictionary with the Java comparator itself). */
+int dg_segment_set_dim_order(dg_segment* seg, const char* dim, int32_t slot, const int32_t* rank, int32_t card,
+                             int32_t has_ties);
 
 /* ---- scan pieces ---- */
 /* Filter.getBitmapResult: row bitset (uint32 words, bit r = row r) of the filter, into out_words
@@ -199,10 +211,18 @@ typedef struct {
   int32_t metric_agg; /* index into scan->aggs of the NumericTopNMetricSpec metric */
   int32_t inverted;   /* InvertedTopNMetricSpec */
   int32_t threshold;  /* per-segment threshold, i.e. max(query threshold, minTopNThreshold) */
+  /* DimensionTopNMetricSpec / LexicographicTopNMetricSpec / AlphaNumericTopNMetricSpec
+   * (query/topn/DimensionTopNMetricSpec.java): dim_order = order slot set with
+   * dg_segment_set_dim_order (metric_agg / inverted ignored), -1 = metric ordering. */
+  int32_t dim_order;
+  const char* previous_stop;  /* NULL = none; LEXICOGRAPHIC skips to it (computeStartEnd) */
+  const int32_t* min_rank;    /* per segment: values need rank >= min_rank[i], i.e. after previousStop
+                                 under the comparator (NULL = no previousStop) */
 } dg_topn;
 
 /* ALL granularity only. Per segment i: out_n[i] entries, ordered as TopNNumericResultBuilder.build()
- * returns them; entry j at index i * threshold + j: dictionary id (segment-local) and n_aggs slots. */
+ * (or, for a dimension order, TopNLexicographicResultBuilder.build()) returns them; entry j at index
+ * i * threshold + j: dictionary id (segment-local) and n_aggs slots. */
 int dg_topn_run(dg_segment* const* segs, int32_t n_segs, const dg_scan* scan, const dg_topn* topn,
                 int32_t* out_n, int32_t* out_ids, uint64_t* out_values, dg_metrics* metrics);
 

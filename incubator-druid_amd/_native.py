@@ -70,7 +70,8 @@ class dg_metrics(ctypes.Structure):
 
 class dg_topn(ctypes.Structure):
     _fields_ = [("dimension", ctypes.c_char_p), ("metric_agg", ctypes.c_int32), ("inverted", ctypes.c_int32),
-                ("threshold", ctypes.c_int32)]
+                ("threshold", ctypes.c_int32), ("dim_order", ctypes.c_int32), ("previous_stop", ctypes.c_char_p),
+                ("min_rank", ctypes.c_void_p)]
 
 
 class dg_topn_lists(ctypes.Structure):
@@ -88,7 +89,7 @@ EXPORTS = [
     "dg_context_set_stream", "dg_segment_attach", "dg_segment_release", "dg_segment_num_rows",
     "dg_segment_interval", "dg_segment_time_bounds", "dg_segment_num_columns", "dg_segment_column_name",
     "dg_segment_column_type", "dg_segment_device_bytes", "dg_segment_dim_cardinality", "dg_segment_dim_value",
-    "dg_segment_dim_dictionary", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_topn_merge", "dg_groupby_run",
+    "dg_segment_dim_dictionary", "dg_segment_set_dim_order", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_topn_merge", "dg_groupby_run",
     "dg_result_groups", "dg_result_fetch_groups", "dg_result_release", "dg_debug_lz4_decode",
 ]
 
@@ -124,6 +125,7 @@ def lib():
         "dg_segment_dim_cardinality": (i32, [vp, cp]),
         "dg_segment_dim_value": (ctypes.c_int, [vp, cp, i32, P(ctypes.c_void_p), P(i32)]),
         "dg_segment_dim_dictionary": (ctypes.c_int, [vp, cp, vp, vp, P(i64)]),
+        "dg_segment_set_dim_order": (ctypes.c_int, [vp, cp, i32, vp, i32, i32]),
         "dg_filter_bitmap": (ctypes.c_int, [vp, P(dg_filter), i32, vp, P(i64)]),
         "dg_timeseries_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), i32, vp, vp, vp, vp, P(dg_metrics)]),
         "dg_topn_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), P(dg_topn), vp, vp, vp, P(dg_metrics)]),

@@ -1011,6 +1011,27 @@ int dg_segment_dim_dictionary(const dg_segment* s, const char* dim, int64_t* off
   return DG_OK;
 }
 
+int dg_segment_set_dim_order(dg_segment* s, const char* dim, int32_t slot, const int32_t* rank, int32_t card,
+                             int32_t has_ties) {
+  Segment* seg = reinterpret_cast<Segment*>(s);
+  if (!seg || !dim || !rank) return set_error(DG_ERR_ARG, "null argument");
+  if (slot < 0 || slot >= kOrderSlots) return set_error(DG_ERR_ARG, "order slot %d", slot);
+  Column* c = seg->find(dim);
+  if (!c || c->type != DG_COL_STRING) return set_error(DG_ERR_NOT_FOUND, "no string column %s", dim);
+  if (card != (int32_t)c->dict.size()) return set_error(DG_ERR_ARG, "rank of %d ids for cardinality %zu", card, c->dict.size());
+  for (int32_t i = 0; i < card; ++i)
+    if (rank[i] < 0 || rank[i] >= card) return set_error(DG_ERR_ARG, "rank[%d] = %d out of range", i, rank[i]);
+  std::lock_guard<std::mutex> g(seg->ctx->mu);
+  hipSetDevice(seg->ctx->device);
+  DevBuf& b = c->order_rank[slot];
+  if (!b.alloc(sizeof(int32_t) * (size_t)std::max(card, 1))) return set_error(DG_ERR_OOM, "hipMalloc order");
+  if (card) DG_HIP(hipMemcpy(b.p, rank, sizeof(int32_t) * (size_t)card, hipMemcpyHostToDevice));
+  c->order_host[slot].assign(rank, rank + card);
+  c->order_ties[slot] = has_ties != 0;
+  c->order_set[slot] = true;
+  return DG_OK;
+}
+
 int dg_filter_bitmap(dg_segment* s, const dg_filter* filter, int32_t n_filter, uint32_t* out_words, int64_t* out_count) {
   Segment* seg = reinterpret_cast<Segment*>(s);
   if (!seg || !out_words) return set_error(DG_ERR_ARG, "null argument");
@@ -1194,7 +1215,9 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   if (rc) return rc;
   if (!q || !t || !t->dimension) return set_error(DG_ERR_ARG, "null argument");
   if (q->period_ms != 0) return set_error(DG_ERR_UNSUPPORTED, "topN with non-ALL granularity");
-  if (t->metric_agg < 0 || t->metric_agg >= q->n_aggs) return set_error(DG_ERR_ARG, "metric index");
+  const bool dim = t->dim_order >= 0;
+  if (dim && t->dim_order >= kOrderSlots) return set_error(DG_ERR_ARG, "order slot %d", t->dim_order);
+  if (!dim && (t->metric_agg < 0 || t->metric_agg >= q->n_aggs)) return set_error(DG_ERR_ARG, "metric index");
   if (t->threshold <= 0) return set_error(DG_ERR_ARG, "threshold");
   AggPlan plan;
   rc = make_plan(q, &plan);
@@ -1234,6 +1257,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       if (rc) return rc;
     }
     if (dc) {
+      if (dim && !dc->order_set[t->dim_order])
+        return set_error(DG_ERR_ARG, "order slot %d of %s not set (dg_segment_set_dim_order)", t->dim_order, t->dimension);
       rc = column_view(dc, cs, &db, &j.key, st);
       if (rc) return rc;
       card[i] = std::max<int64_t>((int64_t)dc->dict.size(), 1);
@@ -1322,16 +1347,57 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
                    d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
   ht.mark("bins_launched");
   // selection + gather of the candidates' records, all segments in one launch
-  const int mk = plan.kind[t->metric_agg];
+  const int mk = dim ? DG_AGG_COUNT : plan.kind[t->metric_agg];
+  const int metric_agg = dim ? 0 : t->metric_agg;
   const int metric_op = (slot_op(mk) << 8) | mk;
   std::vector<TopnSelJob> sel;
   std::vector<int> sel_seg;
   std::vector<int64_t> gcap(n, 0), goff(n, 0);
   int64_t max_card = 0, gtotal = 0;
+  // DimensionTopNMetricSpec: per segment the dictionary order, the computeStartEnd id range
+  // (BaseTopNAlgorithm.java:296-326; only LEXICOGRAPHIC is optimized, DimensionTopNMetricSpec.java:117-124)
+  // and whether the order has comparator-equal values (then the builder's queue is replayed literally)
+  std::vector<const int32_t*> dim_rank(n, nullptr), dim_rank_host(n, nullptr);
+  std::vector<int32_t> dim_lo(n, 0), dim_hi(n, 0);
+  std::vector<char> dim_ties(n, 0);
+  bool any_ties = false;
+  if (dim) {
+    for (int i = 0; i < n; ++i) {
+      if (!cur[i].any) continue;
+      Segment* seg = reinterpret_cast<Segment*>(segs[i]);
+      const Column* dc = seg->find(t->dimension);
+      const int32_t cd = (int32_t)card[i];
+      if (dc) {
+        dim_rank[i] = dc->order_rank[t->dim_order].as<int32_t>();
+        dim_rank_host[i] = dc->order_host[t->dim_order].data();
+        dim_ties[i] = (char)dc->order_ties[t->dim_order];
+        any_ties |= dim_ties[i] != 0;
+      }
+      int32_t lo = 0, hi = cd;
+      if (t->dim_order == 2 * DG_ORDER_LEXICOGRAPHIC) {
+        if (t->previous_stop) {
+          // lookupId(previousStop) + 1, negated when missing; a missing dimension's selector
+          // resolves only null / "" (to id 0)
+          int64_t look;
+          if (dc) look = (int64_t)index_of(dc, t->previous_stop) + 1;
+          else look = t->previous_stop[0] == 0 ? 1 : 0;
+          if (look < 0) look = -look;
+          lo = look > cd ? cd : (int32_t)look;
+        }
+        const bool covers = q->interval_start <= seg->istart && seg->iend <= q->interval_end && seg->istart < q->interval_end;
+        if (q->n_filter == 0 && covers) hi = (int32_t)std::min<int64_t>(hi, (int64_t)lo + t->threshold);
+      }
+      dim_lo[i] = lo;
+      dim_hi[i] = hi;
+    }
+  }
+  // with comparator-equal values every eligible id is a candidate (the queue is replayed in id order)
+  const int sel_threshold = any_ties ? 0x3fffffff : t->threshold;
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
     // candidates = ids whose key >= the K-th key: the threshold plus ties, rarely more
     gcap[i] = std::min<int64_t>(card[i], 2 * (int64_t)t->threshold + 64);
+    if (any_ties) gcap[i] = card[i];
     goff[i] = gtotal;
     gtotal += gcap[i] * (rec + 1) + (gcap[i] + 3) / 4;  // records + u16 builder order
   }
@@ -1348,6 +1414,13 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     sj.keys = dev_take<uint64_t>(cs, (size_t)card[i]);
     sj.blkcnt = dev_take<int32_t>(cs, (size_t)((card[i] + kSelBlock - 1) / kSelBlock));
     sj.gather_cap = (int32_t)gcap[i];
+    if (dim) {
+      sj.dim_mode = 1;
+      sj.rank = dim_rank[i];
+      sj.lo = dim_lo[i];
+      sj.hi = dim_hi[i];
+      sj.min_rank = t->min_rank ? t->min_rank[i] : 0;
+    }
     sj.gathered = d_gath + goff[i];
     sj.order = reinterpret_cast<uint16_t*>(d_gath + goff[i] + gcap[i] * (rec + 1));
     if (!sj.cand || !sj.keys || !sj.blkcnt) return set_error(DG_ERR_OOM, "topN candidates");
@@ -1372,7 +1445,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   if (ns) {
     memcpy(h_sel, sel.data(), sizeof(TopnSelJob) * ns);
     DG_FLUSH(cs, st);
-    launch_topn_select(d_sel, ns, max_card, na, t->metric_agg, metric_op, t->inverted, t->threshold, st);
+    launch_topn_select(d_sel, ns, max_card, na, metric_agg, metric_op, t->inverted, sel_threshold, st);
     ht.mark("select_launched");
   }
   hipEventRecord(ctx->ev[4], st);
@@ -1447,6 +1520,70 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       int32_t idx;
     };
     const int K = t->threshold;
+    if (dim) {
+      // TopNLexicographicResultBuilder (TopNLexicographicResultBuilder.java:40-176) over the eligible
+      // ids in id order: every non-null value is offered (shouldAdd compares the head's unset metric
+      // value, null, with it), the queue's head is the largest value under the comparator and is
+      // polled past the threshold; build() sorts the queue's array by the comparator (stable).
+      const int32_t* hr = dim_rank_host[i];
+      auto rank_of = [&](int c) { return hr ? hr[h_cand[k][c]] : 0; };
+      std::vector<int> res;
+      if (!dim_ties[i]) {  // distinct ranks: the K smallest, ascending
+        if (nc > 0 && nc <= gcap[i] && nc <= kTopnOrderCap) {
+          const uint16_t* ord = reinterpret_cast<const uint16_t*>(h_gath + goff[i] + gcap[i] * (rec + 1));
+          for (int e = 0; e < std::min(nc, K); ++e) res.push_back(ord[e]);
+        } else {
+          res.resize(nc);
+          for (int c = 0; c < nc; ++c) res[c] = c;
+          std::sort(res.begin(), res.end(), [&](int a, int b) { return rank_of(a) < rank_of(b); });
+          if ((int)res.size() > K) res.resize(K);
+        }
+      } else {  // java.util.PriorityQueue, literally (OpenJDK 8 siftUp / siftDown)
+        const Column* dc = reinterpret_cast<Segment*>(segs[i])->find(t->dimension);
+        auto is_null = [&](int c) { return !dc || dc->dict_null[h_cand[k][c]]; };
+        auto pq_cmp = [&](int a, int b) { return (rank_of(b) > rank_of(a)) - (rank_of(b) < rank_of(a)); };
+        std::vector<int> q;
+        for (int c = 0; c < nc; ++c) {
+          if ((int)q.size() >= K && is_null(c)) continue;
+          int x = c, at = (int)q.size();
+          q.push_back(c);
+          while (at > 0) {
+            const int parent = (at - 1) >> 1;
+            if (pq_cmp(x, q[parent]) >= 0) break;
+            q[at] = q[parent];
+            at = parent;
+          }
+          q[at] = x;
+          if ((int)q.size() > K) {  // poll
+            const int last = q.back();
+            q.pop_back();
+            const int size = (int)q.size();
+            if (size) {
+              int a = 0;
+              const int half = size >> 1;
+              while (a < half) {
+                int child = 2 * a + 1;
+                const int right = child + 1;
+                if (right < size && pq_cmp(q[child], q[right]) > 0) child = right;
+                if (pq_cmp(last, q[child]) <= 0) break;
+                q[a] = q[child];
+                a = child;
+              }
+              q[a] = last;
+            }
+          }
+        }
+        res = q;
+        std::stable_sort(res.begin(), res.end(), [&](int a, int b) { return rank_of(a) < rank_of(b); });
+      }
+      out_n[i] = (int32_t)res.size();
+      for (size_t e = 0; e < res.size(); ++e) {
+        const int64_t o = (int64_t)i * t->threshold + (int64_t)e;
+        out_ids[o] = h_cand[k][res[e]];
+        for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[k][(size_t)res[e] * rec + 1 + a]);
+      }
+      continue;
+    }
     std::vector<E> v;
     if (nc > 0 && nc <= gcap[i] && nc <= kTopnOrderCap) {
       // k_topn_order sorted the candidates by (key desc, id asc); keep every key > kth and, of the

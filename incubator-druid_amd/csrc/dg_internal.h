@@ -140,6 +140,8 @@ struct BlockColumn {
   DevBuf block_ptrs;                   // const uint8_t*[nblocks]: raw slots (UNCOMPRESSED/NONE)
 };
 
+constexpr int kOrderSlots = 8;
+
 struct Column {
   std::string name;
   int type = DG_COL_MISSING;
@@ -153,6 +155,12 @@ struct Column {
   std::vector<int64_t> bm_off;         // byte offset of each bitmap inside bm_bytes (4-byte aligned)
   std::vector<int32_t> bm_len;
   DevBuf bm_bytes;
+  // dictionary orders handed in by dg_segment_set_dim_order (slot = 2 * DG_ORDER_* + inverted):
+  // rank of every dictionary id under the StringComparator, comparator-equal values share a rank
+  DevBuf order_rank[kOrderSlots];
+  std::vector<int32_t> order_host[kOrderSlots];
+  int32_t order_ties[kOrderSlots] = {};
+  bool order_set[kOrderSlots] = {};
 };
 
 struct Context {
@@ -249,6 +257,12 @@ struct TopnSelJob {
   int32_t* blkcnt;        // [ceil(card / 1024)] candidates per workgroup
   uint16_t* order;        // [gather_cap] gather positions in builder order (filled when ncand <= 4096)
   int32_t gather_cap;
+  // DimensionTopNMetricSpec: key of a touched id = its dictionary rank (smaller first), eligible when
+  // lo <= id < hi and rank >= min_rank; rank == nullptr: every id has rank 0 (missing dimension)
+  int32_t dim_mode;
+  const int32_t* rank;
+  int32_t lo, hi;
+  int32_t min_rank;
   int32_t pad;
 };
 constexpr int kSelBlock = 1024;

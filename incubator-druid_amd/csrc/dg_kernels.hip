@@ -1107,6 +1107,15 @@ __device__ void replay_digits(const uint32_t* __restrict__ hist, int levels, int
   *mask_out = mask;
 }
 
+// DimensionTopNMetricSpec key of a touched id: smaller dictionary rank = larger key; 0 = not eligible
+// (outside the computeStartEnd id range, BaseTopNAlgorithm.java:296-326, or not after previousStop,
+// TopNLexicographicResultBuilder.shouldAdd :166-174)
+__device__ __forceinline__ uint64_t dim_key(const TopnSelJob& jb, int64_t id) {
+  const int32_t r = jb.rank ? jb.rank[id] : 0;
+  if (id < jb.lo || id >= jb.hi || r < jb.min_rank) return 0;
+  return (uint64_t)(0xFFFFFFFFu - (uint32_t)r) + 1ull;
+}
+
 // pass 0: metric keys, touched / row counts, histogram of the top byte
 __global__ __launch_bounds__(kSelBlock) void k_topn_keys(const TopnSelJob* __restrict__ jobs, int naggs, int metric,
                                                          int op, int kind, int inverted) {
@@ -1127,12 +1136,16 @@ __global__ __launch_bounds__(kSelBlock) void k_topn_keys(const TopnSelJob* __res
     const uint64_t n = jb.table[i * rec];
     uint64_t k = 0;
     if (n) {
-      k = metric_key(jb.table[i * rec + 1 + metric], op, kind, inverted);
-      k = k ? k : 1;  // 0 marks untouched ids; a touched key of 0 becomes 1 (only widens the candidates)
-      atomicAdd(&s_hist[k >> 56], 1u);
+      if (jb.dim_mode) {
+        k = dim_key(jb, i);
+      } else {
+        k = metric_key(jb.table[i * rec + 1 + metric], op, kind, inverted);
+        k = k ? k : 1;  // 0 marks untouched ids; a touched key of 0 becomes 1 (only widens the candidates)
+      }
+      if (k) atomicAdd(&s_hist[k >> 56], 1u);
     }
     jb.keys[i] = k;
-    c = n != 0;
+    c = k != 0;
     rows = n;
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -1276,7 +1289,8 @@ __global__ __launch_bounds__(1024) void k_topn_order(const TopnSelJob* __restric
   while (P < n) P <<= 1;
   const int rec = naggs + 1;
   for (int c = threadIdx.x; c < P; c += 1024) {
-    s_key[c] = c < n ? metric_key(jb.gathered[(size_t)c * (rec + 1) + 1 + 1 + metric], op, kind, inverted) : 0ull;
+    const uint64_t* g = jb.gathered + (size_t)c * (rec + 1);
+    s_key[c] = c >= n ? 0ull : jb.dim_mode ? dim_key(jb, (int64_t)g[0]) : metric_key(g[1 + 1 + metric], op, kind, inverted);
     s_pos[c] = (uint16_t)c;
   }
   __syncthreads();

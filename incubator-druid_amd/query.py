@@ -442,11 +442,14 @@ def float_max(name, field_name=None):
 # ----------------------------------------------------------------------------------------------
 @dataclass
 class TopNMetricSpec:
-    """numeric (metric name), inverted(numeric), or dimension ordering."""
+    """numeric (metric name), inverted(numeric), or dimension ordering (DimensionTopNMetricSpec,
+    LexicographicTopNMetricSpec, AlphaNumericTopNMetricSpec; `inverted` = InvertedTopNMetricSpec
+    around it)."""
     type: str = "numeric"
     metric: Optional[str] = None
     ordering: str = "lexicographic"
     previous_stop: Optional[str] = None
+    inverted: bool = False
 
     @staticmethod
     def of(spec) -> "TopNMetricSpec":
@@ -459,8 +462,10 @@ class TopNMetricSpec:
             return TopNMetricSpec("numeric", spec["metric"])
         if t == "inverted":
             inner = TopNMetricSpec.of(spec["metric"])
+            if inner.type == "dimension":
+                return TopNMetricSpec("dimension", None, inner.ordering, inner.previous_stop, not inner.inverted)
             if inner.type != "numeric":
-                raise ValueError("only inverted numeric metric specs are supported")
+                raise ValueError("only inverted numeric or dimension metric specs are supported")
             return TopNMetricSpec("inverted", inner.metric)
         if t in ("dimension", "lexicographic", "alphaNumeric"):
             ordering = _ordering_name(spec.get("ordering"), t == "alphaNumeric")
@@ -472,7 +477,8 @@ class TopNMetricSpec:
             return {"type": "numeric", "metric": self.metric}
         if self.type == "inverted":
             return {"type": "inverted", "metric": {"type": "numeric", "metric": self.metric}}
-        return {"type": "dimension", "ordering": self.ordering, "previousStop": self.previous_stop}
+        js = {"type": "dimension", "ordering": self.ordering, "previousStop": self.previous_stop}
+        return {"type": "inverted", "metric": js} if self.inverted else js
 
 
 # ----------------------------------------------------------------------------------------------

@@ -28,6 +28,7 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native as N
+from . import ordering as O
 from . import query as Q
 from .segment import GpuSegment
 
@@ -192,6 +193,92 @@ class TopNResultBuilder:
         return [h.entry for h in items]
 
 
+class JavaPriorityQueue:
+    """java.util.PriorityQueue with a comparator (offer = siftUp, poll = siftDown, toArray = the
+    heap array): which of several comparator-equal entries a poll removes, and the order a stable
+    sort leaves them in, follow from this exact layout."""
+
+    def __init__(self, cmp):
+        self.cmp = cmp
+        self.q: List = []
+
+    def __len__(self):
+        return len(self.q)
+
+    def offer(self, x):
+        q, cmp = self.q, self.cmp
+        k = len(q)
+        q.append(x)
+        while k > 0:
+            parent = (k - 1) >> 1
+            if cmp(x, q[parent]) >= 0:
+                break
+            q[k] = q[parent]
+            k = parent
+        q[k] = x
+
+    def poll(self):
+        q, cmp = self.q, self.cmp
+        top = q[0]
+        x = q.pop()
+        n = len(q)
+        if n:
+            k = 0
+            while k < (n >> 1):
+                child = 2 * k + 1
+                if child + 1 < n and cmp(q[child], q[child + 1]) > 0:
+                    child += 1
+                if cmp(x, q[child]) <= 0:
+                    break
+                q[k] = q[child]
+                k = child
+            q[k] = x
+        return top
+
+
+def _key_cmp(key):
+    def cmp(a, b):
+        ka, kb = key(a), key(b)
+        return (ka > kb) - (ka < kb)
+    return cmp
+
+
+class LexicographicResultBuilder:
+    """TopNLexicographicResultBuilder (query/topn/TopNLexicographicResultBuilder.java:40-176) with
+    the topN comparator given as a sort key (ordering.sort_key): shouldAdd takes every non-null
+    value once the queue is full (the head's topN metric value it compares against is never set),
+    values must come after previousStop; the queue's head is the largest value, polled past the
+    threshold; build() sorts the queue's array by the comparator, stably."""
+
+    def __init__(self, query: Q.TopNQuery, threshold: int):
+        spec = query.metric
+        self.dim = query.dimension
+        self.key = O.sort_key(spec.ordering, spec.inverted)
+        self.cmp = _key_cmp(self.key)
+        self.threshold = threshold
+        self.stop = spec.previous_stop
+        self.pq = JavaPriorityQueue(lambda a, b: self.cmp(b[self.dim], a[self.dim]))
+
+    def add(self, entry: Dict):
+        v = entry[self.dim]
+        if len(self.pq) >= self.threshold and v is None:
+            return
+        if self.stop is not None and self.cmp(v, self.stop) <= 0:
+            return
+        self.pq.offer(entry)
+        if len(self.pq) > self.threshold:
+            self.pq.poll()
+
+    def build(self) -> List[Dict]:
+        return sorted(self.pq.q, key=lambda e: self.key(e[self.dim]))
+
+
+def _result_builder(query: Q.TopNQuery, threshold: int):
+    if query.metric.type == "dimension":
+        return LexicographicResultBuilder(query, threshold)
+    return TopNResultBuilder(query, threshold)
+
+
 class _Rev:
     __slots__ = ("v",)
 
@@ -213,19 +300,41 @@ class TopNRaw:
         self.segments, self.cnt, self.ids, self.vals, self.K, self.ts = segments, cnt, ids, vals, K, ts
 
 
-def _topn_struct(query: Q.TopNQuery, threshold: int):
+def _topn_struct(query: Q.TopNQuery, threshold: int, segments: Optional[Sequence[GpuSegment]] = None):
+    """dg_topn for a numeric / inverted metric, or a dimension ordering (then the segments'
+    dictionary orders are registered and their previousStop cuts computed). Returns the struct and
+    the buffers it points into."""
     t = N.dg_topn()
     dim = query.dimension.encode()
     t.dimension = dim
-    t.metric_agg = [a.name for a in query.aggregations].index(query.metric.metric)
-    t.inverted = int(query.metric.type == "inverted")
     t.threshold = threshold
-    return t, dim
+    spec = query.metric
+    keep = [dim]
+    if spec.type == "dimension":
+        t.metric_agg, t.inverted = 0, 0
+        t.dim_order = O.order_slot(spec.ordering, spec.inverted)
+        if spec.previous_stop is not None:
+            stop = spec.previous_stop.encode()
+            t.previous_stop = stop
+            keep.append(stop)
+        if segments is not None:
+            mins = np.zeros(len(segments), dtype=np.int32)
+            for i, seg in enumerate(segments):
+                order = seg.dim_order(query.dimension, spec.ordering, spec.inverted)
+                if order is not None:
+                    mins[i] = order.min_rank(spec.previous_stop)
+                else:  # missing dimension: its one value is null, never after a previousStop
+                    mins[i] = 0 if spec.previous_stop is None else 1
+            t.min_rank = mins.ctypes.data
+            keep.append(mins)
+    else:
+        t.metric_agg = [a.name for a in query.aggregations].index(spec.metric)
+        t.inverted = int(spec.type == "inverted")
+        t.dim_order = -1
+    return t, keep
 
 
 def _check_topn(query: Q.TopNQuery):
-    if query.metric.type not in ("numeric", "inverted"):
-        raise N.UnsupportedQuery(2, "dimension-ordered topN")
     if not query.granularity.is_all:
         raise N.UnsupportedQuery(2, "topN with non-ALL granularity")
 
@@ -239,7 +348,7 @@ def topn_raw(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional
     na = len(query.aggregations)
     K = query.segment_threshold
     scan, keep = N.make_scan(query, Q)
-    t, dim = _topn_struct(query, K)
+    t, keep_t = _topn_struct(query, K, segments)
     n = len(segments)
     cnt = np.zeros(n, dtype=np.int32)
     ids = np.zeros(n * K, dtype=np.int32)
@@ -302,12 +411,71 @@ def _topn_entries(query: Q.TopNQuery, values: List[Optional[str]], slots) -> Lis
     return out
 
 
+def _merge_topn_dimension(query: Q.TopNQuery, segments: Sequence[GpuSegment], raw: TopNRaw) -> List[Q.Result]:
+    """TopNBinaryFn fold of dimension-ordered per-segment lists. Each list is its segment's values
+    in comparator order; when no two values compare equal (no segment order has ties and the
+    merged head values have distinct keys), the fold keeps the `threshold` smallest values of the
+    union, which all sit in the first `threshold` entries of every list that holds them: only those
+    are looked at. Otherwise the literal pairwise fold (merge_topn) runs."""
+    spec = query.metric
+    live = sorted((i for i in range(len(segments)) if raw.cnt[i] >= 0), key=lambda i: (int(raw.ts[i]), i))
+    if not live:
+        return []
+    orders = [segments[i].dim_order(query.dimension, spec.ordering, spec.inverted) for i in live]
+    if any(o is not None and o.has_ties for o in orders):
+        return merge_topn(query, _raw_results(query, segments, raw))
+    T, K, na = query.threshold, raw.K, len(query.aggregations)
+    key = O.sort_key(spec.ordering, spec.inverted)
+    slots = raw.vals.reshape(-1, max(na, 1))
+    merged: "OrderedDict[Optional[str], List]" = OrderedDict()
+    for i in live:
+        c = min(int(raw.cnt[i]), T)
+        for j in range(c):
+            v = segments[i].dim_value(query.dimension, int(raw.ids[i * K + j]))
+            row = slots[i * K + j, :na]
+            if v in merged:
+                merged[v].append(row)
+            else:
+                merged[v] = [row]
+    keys = {v: key(v) for v in merged}
+    ranked = sorted(merged, key=keys.__getitem__)
+    if any(keys[a] == keys[b] for a, b in zip(ranked, ranked[1:])):
+        return merge_topn(query, _raw_results(query, segments, raw))
+    out = []
+    for v in ranked[:T]:
+        e = {query.dimension: v}
+        if na:
+            cols = _decode_slots(query.aggregations, np.asarray(merged[v]))
+            for agg, col in zip(query.aggregations, cols):
+                acc = _py(col[0], agg.output_type)
+                for x in col[1:]:  # TopNBinaryFn: combine(accumulated, next list's value)
+                    acc = agg.combine(acc, _py(x, agg.output_type))
+                e[agg.name] = acc
+        out.append(e)
+    return [Q.Result(int(raw.ts[live[0]]), out)]
+
+
+def _raw_results(query: Q.TopNQuery, segments: Sequence[GpuSegment], raw: TopNRaw) -> List[List[Q.Result]]:
+    out: List[List[Q.Result]] = [[] for _ in segments]
+    na, K = len(query.aggregations), raw.K
+    for k, seg in enumerate(segments):
+        if raw.cnt[k] < 0:
+            continue
+        c = int(raw.cnt[k])
+        values = [seg.dim_value(query.dimension, int(x)) for x in raw.ids[k * K:k * K + c]]
+        slots = raw.vals.reshape(-1, max(na, 1))[k * K:k * K + c, :na]
+        out[k] = [Q.Result(int(raw.ts[k]), _topn_entries(query, values, slots))]
+    return out
+
+
 def run_topn(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional[RunStats] = None) -> List[Q.Result]:
     """Per-segment topN on the GPU + TopNBinaryFn merge in the engine (one device); falls back to the
     Python merge when the segments span devices."""
     _check_topn(query)
     if len(_group_by_device(segments)) != 1:
         return merge_topn(query, topn_per_segment(segments, query, stats))
+    if query.metric.type == "dimension":
+        return _merge_topn_dimension(query, segments, topn_raw(segments, query, stats))
     raw = topn_raw(segments, query, stats)
     handles = [s.handle for s in segments]
     res = topn_merge_raw(query, raw.cnt, raw.ids, raw.vals, raw.K, raw.ts, handles)
@@ -361,7 +529,7 @@ def topn_binary_fn(query: Q.TopNQuery, r1: Optional[Q.Result], r2: Optional[Q.Re
             ret[k] = c
         else:
             ret[k] = v
-    bob = TopNResultBuilder(query, query.threshold)
+    bob = _result_builder(query, query.threshold)
     for v in ret.values():
         bob.add(v)
     ts = r1.timestamp if query.granularity.is_all else query.granularity.bucket_start(r1.timestamp)

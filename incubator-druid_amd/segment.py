@@ -14,6 +14,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
+from . import ordering as O
 
 
 class GpuContext:
@@ -66,6 +67,7 @@ class GpuSegment:
         L.dg_segment_time_bounds(h, ctypes.byref(s), ctypes.byref(e))
         self.min_time, self.max_time = s.value, e.value
         self._dicts: Dict[str, List[Optional[str]]] = {}
+        self._orders: Dict[Tuple[str, int], O.DictionaryOrder] = {}
 
     # -- StorageAdapter-ish facts ------------------------------------------------------------
     def columns(self) -> List[str]:
@@ -101,6 +103,21 @@ class GpuSegment:
                     vals.append(raw[a:b].decode("utf-8") if b > a else None)
                 self._dicts[dim] = vals
         return self._dicts[dim]
+
+    def dim_order(self, dim: str, ordering: str, inverted: bool = False) -> Optional[O.DictionaryOrder]:
+        """The dictionary's order under a topN comparator, handed to the engine once
+        (dg_segment_set_dim_order); None for a missing dimension (its only value is null)."""
+        if self.column_type(dim) != N.COL_STRING:
+            return None
+        slot = O.order_slot(ordering, inverted)
+        key = (dim, slot)
+        if key not in self._orders:
+            order = O.DictionaryOrder(self.dictionary(dim), ordering, inverted)
+            rank = np.ascontiguousarray(order.rank, dtype=np.int32)
+            N.check(N.lib().dg_segment_set_dim_order(self.handle, dim.encode(), slot, rank.ctypes.data, len(rank),
+                                                     int(order.has_ties)))
+            self._orders[key] = order
+        return self._orders[key]
 
     def dim_value(self, dim: str, idx: int) -> Optional[str]:
         """DimensionSelector.lookupName for one id (no full dictionary export)."""

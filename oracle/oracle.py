@@ -224,13 +224,63 @@ def index_of(dictionary: Sequence[Optional[str]], value: Optional[str]) -> int:
 
 
 def _try_long(s: str):
-    try:
-        if s.strip() != s or s == "":
-            return None
-        v = int(s, 10)
-        return v if -(1 << 63) <= v < (1 << 63) else None
-    except ValueError:
+    """GuavaUtils.tryParseLong (common/.../guava/GuavaUtils.java:37-42): strip one leading '+', then
+    Guava Longs.tryParse (radix 10, ASCII digits, optional leading '-', null on overflow)."""
+    if not s:
         return None
+    t = s[1:] if s[0] == "+" else s
+    neg = t.startswith("-")
+    digits = t[1:] if neg else t
+    if not digits or any(not ("0" <= ch <= "9") for ch in digits):
+        return None
+    v = -int(digits) if neg else int(digits)
+    return v if -(1 << 63) <= v < (1 << 63) else None
+
+
+def _java_big_decimal(s: str):
+    """new BigDecimal(String) (java.math.BigDecimal(char[], int, int)): [sign] significand with
+    Character.isDigit digits and at most one '.', optional exponent [eE][sign]digits that fits an
+    int; anything else is a NumberFormatException (-> None, convertStringToBigDecimal :334-345)."""
+    i, n = 0, len(s)
+    if i < n and s[i] in "+-":
+        i += 1
+    mant, seen_dot, nd = [], False, 0
+    while i < n:
+        ch = s[i]
+        if ch == ".":
+            if seen_dot:
+                return None
+            seen_dot = True
+            mant.append(".")
+        elif ch.isdecimal():
+            mant.append(str(int(ch)))
+            nd += 1
+        else:
+            break
+        i += 1
+    if nd == 0:
+        return None
+    exp = 0
+    if i < n:
+        if s[i] not in "eE":
+            return None
+        i += 1
+        eneg = False
+        if i < n and s[i] in "+-":
+            eneg = s[i] == "-"
+            i += 1
+        if i >= n:
+            return None
+        e = 0
+        while i < n:
+            if not s[i].isdecimal():
+                return None
+            e = e * 10 + int(s[i])
+            i += 1
+        exp = -e if eneg else e
+        if not -(1 << 31) <= exp < (1 << 31):
+            return None
+    return Decimal(("-" if s[0] == "-" else "") + "".join(mant) + f"E{exp}")
 
 
 def numeric_compare(a: Optional[str], b: Optional[str]) -> int:
@@ -244,22 +294,188 @@ def numeric_compare(a: Optional[str], b: Optional[str]) -> int:
     la, lb = _try_long(a), _try_long(b)
     if la is not None and lb is not None:
         return (la > lb) - (la < lb)
-
-    def dec(s, l):
-        if l is not None:
-            return Decimal(l)
-        try:
-            return Decimal(s)
-        except InvalidOperation:
-            return None
-
-    da, db = dec(a, la), dec(b, lb)
+    da = Decimal(la) if la is not None else _java_big_decimal(a)
+    db = Decimal(lb) if lb is not None else _java_big_decimal(b)
     if da is not None and db is not None:
         return (da > db) - (da < db)
     if da is None and db is None:
-        ka, kb = _jkey(a), _jkey(b)
-        return (ka > kb) - (ka < kb)
+        return lexicographic_compare(a, b)
     return -1 if da is None else 1
+
+
+def lexicographic_compare(a: Optional[str], b: Optional[str]) -> int:
+    """StringComparators.LexicographicComparator (:48-70): UnsignedBytes over UTF-8, nulls first."""
+    if a == b:
+        return 0
+    if a is None:
+        return -1
+    if b is None:
+        return 1
+    ba, bb = a.encode("utf-8", "replace"), b.encode("utf-8", "replace")
+    return (ba > bb) - (ba < bb)
+
+
+def _utf16(s: str) -> List[int]:
+    b = s.encode("utf-16-le", "surrogatepass")
+    return [b[i] | (b[i + 1] << 8) for i in range(0, len(b), 2)]
+
+
+def _code_point_at(u: List[int], i: int) -> int:
+    c = u[i]
+    if 0xD800 <= c <= 0xDBFF and i + 1 < len(u) and 0xDC00 <= u[i + 1] <= 0xDFFF:
+        return 0x10000 + ((c - 0xD800) << 10) + (u[i + 1] - 0xDC00)
+    return c
+
+
+def _char_count(cp: int) -> int:
+    return 2 if cp >= 0x10000 else 1
+
+
+def _an_is_digit(ch: int) -> bool:
+    return (0x30 <= ch <= 0x39 or 0x660 <= ch <= 0x669 or 0x6F0 <= ch <= 0x6F9 or 0x966 <= ch <= 0x96F
+            or 0xFF10 <= ch <= 0xFF19)
+
+
+def _an_is_zero(ch: int) -> bool:
+    return ch in (0x30, 0x660, 0x6F0, 0x966, 0xFF10)
+
+
+def _an_value_of(d: int) -> int:
+    for zero, nine in ((0x30, 0x39), (0x660, 0x669), (0x6F0, 0x6F9), (0x966, 0x96F), (0xFF10, 0xFF19)):
+        if d <= nine:
+            return d - zero
+    return d
+
+
+def _java_upper(c: int) -> int:
+    u = chr(c).upper()
+    return ord(u) if len(u) == 1 else c
+
+
+def _java_lower(c: int) -> int:
+    u = chr(c).lower()
+    return ord(u) if len(u) == 1 else c
+
+
+def _case_insensitive(a: List[int], b: List[int]) -> int:
+    """String.CASE_INSENSITIVE_ORDER on UTF-16 units (java.lang.String.CaseInsensitiveComparator)."""
+    for c1, c2 in zip(a, b):
+        if c1 != c2:
+            c1, c2 = _java_upper(c1), _java_upper(c2)
+            if c1 != c2:
+                c1, c2 = _java_lower(c1), _java_lower(c2)
+                if c1 != c2:
+                    return c1 - c2
+    return len(a) - len(b)
+
+
+def _an_compare_numbers(s0: List[int], s1: List[int], pos: List[int]) -> int:
+    """AlphanumericComparator.compareNumbers (StringComparators.java:140-200), literally."""
+    delta = 0
+    zeroes0 = zeroes1 = 0
+    ch0 = ch1 = -1
+    while pos[0] < len(s0):
+        ch0 = _code_point_at(s0, pos[0])
+        if not _an_is_zero(ch0):
+            break
+        zeroes0 += 1
+        pos[0] += _char_count(ch0)
+    while pos[1] < len(s1):
+        ch1 = _code_point_at(s1, pos[1])
+        if not _an_is_zero(ch1):
+            break
+        zeroes1 += 1
+        pos[1] += _char_count(ch1)
+    while True:
+        no0 = ch0 < 0 or not _an_is_digit(ch0)
+        no1 = ch1 < 0 or not _an_is_digit(ch1)
+        if no0 and no1:
+            return delta if delta != 0 else zeroes0 - zeroes1
+        if no0:
+            return -1
+        if no1:
+            return 1
+        if delta == 0 and ch0 != ch1:
+            delta = _an_value_of(ch0) - _an_value_of(ch1)
+        if pos[0] < len(s0):
+            ch0 = _code_point_at(s0, pos[0])
+            if _an_is_digit(ch0):
+                pos[0] += _char_count(ch0)
+            else:
+                ch0 = -1
+        else:
+            ch0 = -1
+        if pos[1] < len(s1):
+            ch1 = _code_point_at(s1, pos[1])
+            if _an_is_digit(ch1):
+                pos[1] += _char_count(ch1)
+            else:
+                ch1 = -1
+        else:
+            ch1 = -1
+
+
+def _an_compare_non_numeric(s0: List[int], s1: List[int], pos: List[int]) -> int:
+    """AlphanumericComparator.compareNonNumeric (StringComparators.java:241-258)."""
+    start0 = pos[0]
+    ch0 = _code_point_at(s0, pos[0])
+    pos[0] += _char_count(ch0)
+    while pos[0] < len(s0):
+        ch0 = _code_point_at(s0, pos[0])
+        if _an_is_digit(ch0):
+            break
+        pos[0] += _char_count(ch0)
+    start1 = pos[1]
+    ch1 = _code_point_at(s1, pos[1])
+    pos[1] += _char_count(ch1)
+    while pos[1] < len(s1):
+        ch1 = _code_point_at(s1, pos[1])
+        if _an_is_digit(ch1):
+            break
+        pos[1] += _char_count(ch1)
+    return _case_insensitive(s0[start0:pos[0]], s1[start1:pos[1]])
+
+
+def alphanumeric_compare(a: Optional[str], b: Optional[str]) -> int:
+    """StringComparators.AlphanumericComparator.compare (StringComparators.java:99-134)."""
+    if a is None:
+        return 0 if b is None else -1
+    if b is None:
+        return 1
+    s0, s1 = _utf16(a), _utf16(b)
+    if not s0:
+        return 0 if not s1 else -1
+    if not s1:
+        return 1
+    pos = [0, 0]
+    while pos[0] < len(s0) and pos[1] < len(s1):
+        ch0 = _code_point_at(s0, pos[0])
+        ch1 = _code_point_at(s1, pos[1])
+        if _an_is_digit(ch0):
+            r = _an_compare_numbers(s0, s1, pos) if _an_is_digit(ch1) else -1
+        else:
+            r = 1 if _an_is_digit(ch1) else _an_compare_non_numeric(s0, s1, pos)
+        if r != 0:
+            return r
+    return len(s0) - len(s1)
+
+
+def strlen_compare(a: Optional[str], b: Optional[str]) -> int:
+    """StringComparators.StrlenComparator (:281-300): nullsFirst(UTF-16 length), then String order."""
+    if a == b:
+        return 0
+    if a is None:
+        return -1
+    if b is None:
+        return 1
+    ua, ub = _utf16(a), _utf16(b)
+    if len(ua) != len(ub):
+        return -1 if len(ua) < len(ub) else 1
+    return (ua > ub) - (ua < ub)
+
+
+STRING_COMPARATORS = {"lexicographic": lexicographic_compare, "numeric": numeric_compare,
+                      "alphanumeric": alphanumeric_compare, "strlen": strlen_compare}
 
 
 def _lex_compare(a, b):
@@ -510,6 +726,143 @@ class _Neg:
         return self.v == o.v
 
 
+class JavaPriorityQueue:
+    """java.util.PriorityQueue with a comparator (OpenJDK 8 offer/siftUp/poll/siftDown/toArray):
+    the exact array layout matters for which of several comparator-equal entries is polled and for
+    the order Arrays.sort (stable) leaves ties in."""
+
+    def __init__(self, cmp):
+        self.cmp = cmp
+        self.q: List = []
+
+    def __len__(self):
+        return len(self.q)
+
+    def peek(self):
+        return self.q[0] if self.q else None
+
+    def offer(self, x):
+        q = self.q
+        q.append(x)
+        k = len(q) - 1
+        while k > 0:
+            parent = (k - 1) >> 1
+            e = q[parent]
+            if self.cmp(x, e) >= 0:
+                break
+            q[k] = e
+            k = parent
+        q[k] = x
+
+    def poll(self):
+        q = self.q
+        result = q[0]
+        x = q.pop()
+        size = len(q)
+        if size:
+            k, half = 0, size >> 1
+            while k < half:
+                child = 2 * k + 1
+                c = q[child]
+                right = child + 1
+                if right < size and self.cmp(c, q[right]) > 0:
+                    child = right
+                    c = q[child]
+                if self.cmp(x, c) <= 0:
+                    break
+                q[k] = c
+                k = child
+            q[k] = x
+        return result
+
+    def to_array(self) -> List:
+        return list(self.q)
+
+
+class LexicographicResultBuilder:
+    """TopNLexicographicResultBuilder (query/topn/TopNLexicographicResultBuilder.java:40-176): queue
+    ordered by the reversed dimension comparator (head = largest value); shouldAdd compares the
+    head's (never set, null) topN metric value with the entry's dimension value, so a full queue
+    takes every non-null value; entries must be after previousStop; build() sorts by the comparator
+    (stable over the queue's array order)."""
+
+    def __init__(self, comparator, threshold: int, previous_stop: Optional[str]):
+        self.cmp = comparator
+        self.threshold = threshold
+        self.previous_stop = previous_stop
+        self.pq = JavaPriorityQueue(lambda o1, o2: comparator(o2[0], o1[0]))
+
+    def _should_add(self, dim_value) -> bool:
+        below = len(self.pq) < self.threshold or self.cmp(None, dim_value) < 0
+        return below and (self.previous_stop is None or self.cmp(dim_value, self.previous_stop) > 0)
+
+    def add(self, dim_value, values: Dict):
+        if self._should_add(dim_value):
+            self.pq.offer((dim_value, values))
+            if len(self.pq) > self.threshold:
+                self.pq.poll()
+
+    def build(self) -> List[Dict]:
+        import functools
+        arr = self.pq.to_array()
+        arr.sort(key=functools.cmp_to_key(lambda a, b: self.cmp(a[0], b[0])))
+        return [v for _, v in arr]
+
+
+def topn_comparator(spec):
+    """TopNMetricSpec.getComparator of a dimension ordering: the StringComparator, or
+    InvertedTopNMetricSpec's inverse(nulls-last delegate) (InvertedTopNMetricSpec.java:62-84)."""
+    base = STRING_COMPARATORS[spec.ordering]
+    if not spec.inverted:
+        return base
+
+    def nulls_last(o1, o2):
+        if o1 is None:
+            return 1
+        if o2 is None:
+            return -1
+        return base(o1, o2)
+
+    return lambda a, b: nulls_last(b, a)
+
+
+def _make_builder(query, threshold: int):
+    spec = query.metric
+    if spec.type == "dimension":
+        return LexicographicResultBuilder(topn_comparator(spec), threshold, spec.previous_stop)
+    return NumericResultBuilder(_metric_key_fn(query), threshold)
+
+
+def _builder_add(bob, query, dim_value, vals: Dict):
+    if isinstance(bob, LexicographicResultBuilder):
+        bob.add(dim_value, vals)
+    else:
+        bob.add(dim_value, vals[query.metric.metric], vals)
+
+
+def _dimension_id_range(seg: OracleSegment, query, dictionary, threshold: int) -> Tuple[int, int]:
+    """BaseTopNAlgorithm.BaseArrayProvider.computeStartEnd (BaseTopNAlgorithm.java:296-326) after
+    DimensionTopNMetricSpec.configureOptimizer (DimensionTopNMetricSpec.java:117-124): only the
+    LEXICOGRAPHIC ordering skips to previousStop and, unfiltered over a fully covered segment, stops
+    after `threshold` dictionary ids. One pass (numValuesPerPass >= cardinality)."""
+    card = len(dictionary)
+    spec = query.metric
+    if spec.type != "dimension" or spec.ordering != "lexicographic" or spec.inverted:
+        return 0, card  # InvertedTopNMetricSpec.configureOptimizer: canBeOptimizedUnordered() is false
+    start = 0
+    if spec.previous_stop is not None:
+        lookup = index_of(dictionary, spec.previous_stop) + 1
+        if lookup < 0:
+            lookup = -lookup
+        start = card if lookup > card else max(lookup, 0)
+    end = card
+    qs, qe = query.interval
+    ss, se = seg.interval
+    if query.filter is None and qs <= ss and se <= qe:
+        end = min(end, start + threshold)
+    return start, end
+
+
 def _metric_key_fn(query):
     spec = query.metric
     agg = next(a for a in query.aggregations if a.name == spec.metric)
@@ -519,13 +872,13 @@ def _metric_key_fn(query):
 
 
 def topn_segment(seg: OracleSegment, query) -> List:
-    if query.metric.type == "dimension":
-        raise NotImplementedError("dimension-ordered topN")
     mask = filter_mask(seg, query.effective_filter())
     out = []
     dim_present = seg.is_dim(query.dimension)
     dictionary = seg.dictionary(query.dimension) if dim_present else [None]
     ids_all = seg.ids(query.dimension) if dim_present else np.zeros(seg.num_rows, np.int32)
+    T = query.segment_threshold
+    lo, hi = _dimension_id_range(seg, query, dictionary, T)
     for bt, r0, r1 in cursor_buckets(seg, query):
         rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
         card = len(dictionary)
@@ -533,12 +886,14 @@ def topn_segment(seg: OracleSegment, query) -> List:
         states = aggregate_groups(seg, query.aggregations, rows, gids, card)
         touched = np.zeros(card, dtype=bool)
         touched[gids] = True
-        bob = NumericResultBuilder(_metric_key_fn(query), query.segment_threshold)
+        touched[:lo] = False
+        touched[hi:] = False
+        bob = _make_builder(query, T)
         for i in np.nonzero(touched)[0]:
             vals = {query.dimension: dictionary[i]}
             for a, s in zip(query.aggregations, states):
                 vals[a.name] = _py(s[i], a.output_type)
-            bob.add(dictionary[i], vals[query.metric.metric], vals)
+            _builder_add(bob, query, dictionary[i], vals)
         out.append(Q.Result(bt, bob.build()))
     return out
 
@@ -563,9 +918,9 @@ def topn_binary_fn(query, r1, r2):
             ret[k] = c
         else:
             ret[k] = v
-    bob = NumericResultBuilder(_metric_key_fn(query), query.threshold)
+    bob = _make_builder(query, query.threshold)
     for v in ret.values():
-        bob.add(v[dim], v[query.metric.metric], v)
+        _builder_add(bob, query, v[dim], v)
     ts = r1.timestamp if query.granularity.is_all else query.granularity.bucket_start(r1.timestamp)
     return Q.Result(ts, bob.build())
 

@@ -1,0 +1,115 @@
+"""StringComparators: the oracle's literal comparators and the product's sort keys
+(incubator-druid_amd/ordering.py), both pinned by the reference's StringComparatorsTest assertions
+(tests/golden/kats.json "string_comparators") and checked against each other on random strings.
+CPU only."""
+import functools
+import importlib
+import random
+
+import pytest
+
+ORDERINGS = ("lexicographic", "numeric", "alphanumeric", "strlen")
+
+
+@pytest.fixture(scope="module")
+def ORD():
+    return importlib.import_module("incubator-druid_amd.ordering")
+
+
+def _sign(x):
+    return (x > 0) - (x < 0)
+
+
+def _pairs(kats, name):
+    sc = kats["string_comparators"]
+    return [tuple(p) for p in sc["common"]] + [tuple(p) for p in sc[name]["pairs"]]
+
+
+@pytest.mark.parametrize("name", ORDERINGS)
+def test_oracle_comparators_match_reference_kats(O, kats, name):
+    cmp = O.STRING_COMPARATORS[name]
+    for a, b, want in _pairs(kats, name):
+        assert _sign(cmp(a, b)) == want, (name, a, b)
+    for unsorted, want in kats["string_comparators"][name].get("sorted", []):
+        assert sorted(unsorted, key=functools.cmp_to_key(cmp)) == want
+
+
+@pytest.mark.parametrize("name", ORDERINGS)
+def test_product_sort_keys_match_reference_kats(ORD, kats, name):
+    key = ORD.KEY_FUNCTIONS[name]
+    for a, b, want in _pairs(kats, name):
+        ka, kb = key(a), key(b)
+        assert _sign((ka > kb) - (ka < kb)) == want, (name, a, b)
+    for unsorted, want in kats["string_comparators"][name].get("sorted", []):
+        assert sorted(unsorted, key=key) == want
+
+
+_ALPHABET = (list("0000123456789") + ["٠", "١", "۵", "१", "０", "３"] + list("aAbBzZ")
+             + list(".-+eE _") + ["ß", "é", "É", "İ", "\U0001f600", "K"])
+
+
+def _random_strings(rng, n):
+    out = [None, ""]
+    for _ in range(n):
+        k = rng.randint(1, 7)
+        out.append("".join(rng.choice(_ALPHABET) for _ in range(k)))
+    # numeric-looking values and decimal ties ("1" / "1.0" / "01" / "+1" / "1e0")
+    out += ["1", "1.0", "01", "+1", "1e0", "10E-1", "-0", "0", "0.00", "-1.10", "-1.1", "9223372036854775807",
+            "9223372036854775808", "-9223372036854775809", "1e2147483648", "+-5", "++5", "١٢", "1_0",
+            " 1", "Infinity", "NaN", "0x10", "1.", ".5", "."]
+    return out
+
+
+@pytest.mark.parametrize("name", ORDERINGS)
+@pytest.mark.parametrize("inverted", [False, True])
+def test_sort_keys_agree_with_literal_comparators(O, ORD, name, inverted):
+    """Every pair: sign(key order) == sign(Java comparator), including comparator-equal values."""
+    rng = random.Random(7 + 13 * ORDERINGS.index(name) + inverted)
+    vals = _random_strings(rng, 160)
+    spec = type("S", (), {"ordering": name, "inverted": inverted})()
+    cmp = O.topn_comparator(spec)
+    key = ORD.sort_key(name, inverted)
+    keys = [key(v) for v in vals]
+    for i, a in enumerate(vals):
+        for j, b in enumerate(vals):
+            if a is None and b is None:
+                continue  # inverse(nulls-last) says 1 for (null, null); no list holds null twice
+            got = (keys[i] > keys[j]) - (keys[i] < keys[j])
+            assert got == _sign(cmp(a, b)), (name, inverted, a, b)
+
+
+def test_dictionary_order_ranks_and_previous_stop(ORD, O):
+    dictionary = [None, "1", "1.0", "10", "2", "a", "b"]
+    o = ORD.DictionaryOrder(dictionary, "numeric")
+    # NUMERIC: null, then unparseable ("a" < "b"), then by value with "1" == "1.0"
+    assert o.rank.tolist() == [0, 3, 3, 5, 4, 1, 2]
+    assert o.has_ties
+    assert o.min_rank(None) == 0
+    for stop in ("1", "1.5", "a", "", "0"):
+        eligible = [v for v in dictionary if O.numeric_compare(v, stop) > 0]
+        got = [v for v, r in zip(dictionary, o.rank) if r >= o.min_rank(stop)]
+        assert got == eligible, stop
+    inv = ORD.DictionaryOrder(dictionary, "numeric", inverted=True)
+    spec = type("S", (), {"ordering": "numeric", "inverted": True})()
+    cmp = O.topn_comparator(spec)
+    for stop in ("1", "2", "b"):
+        eligible = [v for v in dictionary if cmp(v, stop) > 0]
+        got = [v for v, r in zip(dictionary, inv.rank) if r >= inv.min_rank(stop)]
+        assert got == eligible, stop
+
+
+def test_java_priority_queue_layout_matches_oracle(O):
+    """The product's and the oracle's java.util.PriorityQueue restatements agree on array layouts
+    (offer/poll sequences with many comparator-equal entries)."""
+    R = importlib.import_module("incubator-druid_amd.runners")
+    rng = random.Random(5)
+    for _ in range(200):
+        cmp = lambda a, b: (a[0] > b[0]) - (a[0] < b[0])  # noqa: E731
+        p, o = R.JavaPriorityQueue(cmp), O.JavaPriorityQueue(cmp)
+        for i in range(rng.randint(1, 60)):
+            x = (rng.randint(0, 5), i)
+            p.offer(x)
+            o.offer(x)
+            if len(p) > 7:
+                assert p.poll() == o.poll()
+            assert p.q == o.q

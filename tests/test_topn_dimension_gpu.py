@@ -1,0 +1,122 @@
+"""Dimension-ordered topN on the GPU (DimensionTopNMetricSpec / LexicographicTopNMetricSpec /
+AlphaNumericTopNMetricSpec, optionally inverted) against the oracle's literal restatement
+(computeStartEnd, TopNLexicographicResultBuilder's java.util.PriorityQueue, TopNBinaryFn fold).
+Integer aggregates bit-exact, doubleSum 1e-9, floatSum 1e-5 (tests/compare.py)."""
+import importlib
+
+import numpy as np
+import pytest
+
+from compare import assert_results
+
+pytestmark = pytest.mark.gpu
+
+ALL = ["1970-01-01/2020-01-01"]
+
+
+@pytest.fixture(scope="module")
+def R():
+    return importlib.import_module("incubator-druid_amd.runners")
+
+
+@pytest.fixture(scope="module")
+def S():
+    return importlib.import_module("incubator-druid_amd.segment")
+
+
+def _spec(ordering, stop, inverted):
+    m = {"type": "dimension", "ordering": ordering, "previousStop": stop}
+    return {"type": "inverted", "metric": m} if inverted else m
+
+
+def _aggs(Q):
+    return [Q.count("rows"), Q.long_sum("ls", "sumLongSequential"), Q.double_sum("ds", "sumFloatNormal"),
+            Q.float_sum("fs", "sumFloatNormal")]
+
+
+@pytest.fixture(scope="module")
+def basic(S, O, basic_dirs):
+    out = {}
+    for layout in (("concise", "lz4"), ("roaring", "none")):
+        out[layout] = ([S.GpuSegment(p) for p in basic_dirs[layout]], [O.OracleSegment(p) for p in basic_dirs[layout]])
+    return out
+
+
+@pytest.mark.parametrize("layout", [("concise", "lz4"), ("roaring", "none")])
+@pytest.mark.parametrize("dim", ["dimZipf", "dimSequential", "dimSequentialHalfNull", "missingDim"])
+@pytest.mark.parametrize("ordering", ["lexicographic", "numeric", "alphanumeric", "strlen"])
+def test_dimension_topn_matches_oracle(R, Q, O, basic, layout, dim, ordering):
+    g, o = basic[layout]
+    for stop, inverted, threshold, flt in ((None, False, 10, None), ("5", False, 7, None), ("", True, 4, None),
+                                          ("50", True, 1001, None),
+                                          (None, False, 3, Q.BoundDimFilter("dimSequential", "100", "200"))):
+        q = Q.TopNQuery(intervals=ALL, dimension=dim, metric=_spec(ordering, stop, inverted), threshold=threshold,
+                        aggregations=_aggs(Q), filter=flt)
+        assert_results(q, R.run_query(q, g), O.run(q, o))
+
+
+@pytest.mark.parametrize("ordering", ["lexicographic", "numeric", "alphanumeric"])
+def test_dimension_topn_high_cardinality(R, Q, O, basic, ordering):
+    """dimUniform (~33k ids per segment): the LEXICOGRAPHIC id-range optimization (no filter, the
+    interval covers the segment) and, for the other orders, a filtered scan."""
+    g, o = basic[("concise", "lz4")]
+    flt = None if ordering == "lexicographic" else Q.SelectorDimFilter("dimZipf", "1")
+    for stop in ((None, "5", "99999") if ordering != "alphanumeric" else (None, "99999")):
+        q = Q.TopNQuery(intervals=ALL, dimension="dimUniform", metric=_spec(ordering, stop, False), threshold=10,
+                        aggregations=_aggs(Q), filter=flt)
+        assert_results(q, R.run_query(q, g), O.run(q, o))
+    # interval not covering the segments: no id-range cut, every touched id is ranked
+    q = Q.TopNQuery(intervals=["1970-01-01T00:00:00Z/1970-01-01T00:05:00Z"], dimension="dimUniform",
+                    metric=_spec(ordering, None, False), threshold=10, aggregations=_aggs(Q), filter=flt)
+    assert_results(q, R.run_query(q, g), O.run(q, o))
+
+
+TIE_VALUES = ["1", "1.0", "01", "+1", "1e0", "10", "2", "a", "A", "b", "B", "ab", "AB", "Ab", "x1", "X01", "x001",
+              "ß", "SS", "é", "É", "zz", "Zz", "-1", "-1.0", "", "0", "0.0", "١", "٢"]
+
+
+@pytest.fixture(scope="module")
+def tie_segments(S, O, W, tmp_path_factory):
+    """Dictionaries with comparator-equal values (NUMERIC: 1 = 1.0 = 01 = +1 = 1e0; ALPHANUMERIC: a = A,
+    x1 / X01 / x001 differ only in zeros...) so the queue's literal tie behaviour decides."""
+    base = tmp_path_factory.mktemp("ties")
+    rng = np.random.default_rng(11)
+    gs, os_ = [], []
+    for k in range(3):
+        n = 3000 + 500 * k
+        vals = [TIE_VALUES[i] for i in rng.integers(0, len(TIE_VALUES) - 3 * k, n)]
+        dictionary, ids = W.encode_strings(vals)
+        spec = W.SegmentSpec(timestamps=np.sort(rng.integers(0, 86_400_000, n)),
+                             dims={"v": (dictionary, ids)},
+                             metrics={"m": ("long", rng.integers(0, 1000, n)), "d": ("double", rng.random(n))})
+        p = W.write_segment(str(base / f"t{k}"), spec, compression="lz4" if k != 1 else "none")
+        gs.append(S.GpuSegment(p))
+        os_.append(O.OracleSegment(p))
+    return gs, os_
+
+
+@pytest.mark.parametrize("ordering", ["lexicographic", "numeric", "alphanumeric", "strlen"])
+@pytest.mark.parametrize("inverted", [False, True])
+def test_dimension_topn_comparator_ties(R, Q, O, tie_segments, ordering, inverted):
+    g, o = tie_segments
+    for stop, threshold, min_t in ((None, 3, 2), ("1", 4, 3), ("A", 2, 5), (None, 40, 1000), ("", 6, 6)):
+        q = Q.TopNQuery(intervals=ALL, dimension="v", metric=_spec(ordering, stop, inverted), threshold=threshold,
+                        aggregations=[Q.count("rows"), Q.long_sum("m"), Q.double_sum("d")],
+                        context={"minTopNThreshold": min_t})
+        assert_results(q, R.run_query(q, g), O.run(q, o))
+        # per-segment lists (createRunner) follow the builder's queue as well
+        per = R.TopNQueryRunnerFactory().per_segment(g, q)
+        for seg_res, os in zip(per, o):
+            assert_results(q, seg_res, O.topn_segment(os, q))
+
+
+def test_numeric_sort_bench_shape(R, Q, basic):
+    """TopNBenchmark numericSort / alphanumericSort shape (dimUniform, longSum, NUMERIC/ALPHANUMERIC):
+    the dictionary holds "1".."100000", so both orders give the numerically smallest values."""
+    g, _ = basic[("concise", "lz4")]
+    for ordering in ("numeric", "alphanumeric"):
+        q = Q.TopNQuery(intervals=ALL, dimension="dimUniform", metric=_spec(ordering, None, False), threshold=10,
+                        aggregations=[Q.long_sum("sumLongSequential")])
+        got = R.run_query(q, g)[0].value
+        present = sorted({int(v) for s in g for v in s.dictionary("dimUniform") if v is not None})
+        assert [int(e["dimUniform"]) for e in got] == present[:10]
