@@ -139,7 +139,7 @@ def _np_type(a):
 # topN
 # ----------------------------------------------------------------------------------------------
 def gather_topn(dist, query: Q.TopNQuery, raw: "R.TopNRaw", gdict: GlobalDictionary,
-                translations: Sequence[np.ndarray]) -> Optional[List[Q.Result]]:
+                translations: Sequence[np.ndarray], segments: Optional[Sequence] = None) -> Optional[List[Q.Result]]:
     """all_gather every rank's per-segment top-K lists (ids mapped to the cluster-wide dictionary);
     rank 0 folds them with TopNBinaryFn in global segment order (rank-major) inside the engine
     (dg_topn_merge, global-id mode) and returns the result; other ranks return None.
@@ -158,7 +158,14 @@ def gather_topn(dist, query: Q.TopNQuery, raw: "R.TopNRaw", gdict: GlobalDiction
         if c > 0:
             gids[s, :c] = translations[s][raw.ids[s * K:s * K + c]]
     vals = raw.vals.reshape(S, K, max(na, 1)).view(np.int64)
-    payload = torch.from_numpy(np.concatenate([raw.ts.astype(np.int64), cnt, gids.ravel(), vals.ravel()])).to(dev)
+    dim_spec = query.metric if query.metric.type == "dimension" else None
+    ties = np.zeros(S, dtype=np.int64)  # dimension orders: does the segment's order have ties
+    if dim_spec is not None:
+        for s in range(S):
+            o = segments[s].dim_order(query.dimension, dim_spec.ordering, dim_spec.inverted) if segments else None
+            ties[s] = int(o is not None and o.has_ties)
+    payload = torch.from_numpy(np.concatenate([raw.ts.astype(np.int64), cnt, gids.ravel(), vals.ravel(),
+                                               ties])).to(dev)
     world = dist.get_world_size()
     bufs = [torch.empty_like(payload) for _ in range(world)]
     dist.all_gather(bufs, payload)
@@ -168,7 +175,14 @@ def gather_topn(dist, query: Q.TopNQuery, raw: "R.TopNRaw", gdict: GlobalDiction
     ts = np.concatenate([a[:S] for a in arrs])
     cn = np.concatenate([a[S:2 * S] for a in arrs]).astype(np.int32)
     keys = np.concatenate([a[2 * S:2 * S + S * K] for a in arrs])
-    vv = np.concatenate([a[2 * S + S * K:] for a in arrs]).view(np.uint64)
+    vv = np.concatenate([a[2 * S + S * K:len(a) - S] for a in arrs]).view(np.uint64)
+    if dim_spec is not None:  # TopNLexicographicResultBuilder fold over the gathered lists
+        tie_free = not any(int(a[len(a) - S + s]) for a in arrs for s in range(S))
+        slots = vv.reshape(-1, max(na, 1))
+        order = sorted((i for i in range(len(cn)) if cn[i] >= 0), key=lambda i: (int(ts[i]), i))
+        lists = [(int(ts[i]), int(cn[i]), (lambda j, i=i: gdict.values[int(keys[i * K + j])]),
+                  slots[i * K:i * K + int(cn[i])]) for i in order]
+        return R.merge_dimension_lists(query, lists, tie_free)
     res = R.topn_merge_raw(query, cn, keys, vv, K, ts, handles=None)
     if res is None:
         return []

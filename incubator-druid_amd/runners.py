@@ -411,36 +411,35 @@ def _topn_entries(query: Q.TopNQuery, values: List[Optional[str]], slots) -> Lis
     return out
 
 
-def _merge_topn_dimension(query: Q.TopNQuery, segments: Sequence[GpuSegment], raw: TopNRaw) -> List[Q.Result]:
-    """TopNBinaryFn fold of dimension-ordered per-segment lists. Each list is its segment's values
-    in comparator order; when no two values compare equal (no segment order has ties and the
-    merged head values have distinct keys), the fold keeps the `threshold` smallest values of the
-    union, which all sit in the first `threshold` entries of every list that holds them: only those
-    are looked at. Otherwise the literal pairwise fold (merge_topn) runs."""
-    spec = query.metric
-    live = sorted((i for i in range(len(segments)) if raw.cnt[i] >= 0), key=lambda i: (int(raw.ts[i]), i))
-    if not live:
+def merge_dimension_lists(query: Q.TopNQuery, lists: Sequence[Tuple[int, int, "callable", np.ndarray]],
+                          tie_free: bool) -> List[Q.Result]:
+    """TopNBinaryFn fold of dimension-ordered per-segment lists, given in merge order as
+    (timestamp, length, value_of(j), [length, n_aggs] slots). Each list is its segment's values in
+    comparator order; when no two values compare equal (`tie_free`: no segment order has ties, and
+    the head values checked here have distinct keys) the fold keeps the `threshold` smallest values
+    of the union, which all sit in the first `threshold` entries of every list holding them: only
+    those are looked at. Otherwise the literal pairwise fold with the builder's queue runs."""
+    if not lists:
         return []
-    orders = [segments[i].dim_order(query.dimension, spec.ordering, spec.inverted) for i in live]
-    if any(o is not None and o.has_ties for o in orders):
-        return merge_topn(query, _raw_results(query, segments, raw))
-    T, K, na = query.threshold, raw.K, len(query.aggregations)
+    spec = query.metric
+    T, na = query.threshold, len(query.aggregations)
     key = O.sort_key(spec.ordering, spec.inverted)
-    slots = raw.vals.reshape(-1, max(na, 1))
+
+    def literal():
+        per = [[Q.Result(ts, _topn_entries(query, [value_of(j) for j in range(c)], slots[:c]))]
+               for ts, c, value_of, slots in lists]
+        return merge_topn(query, per)
+
+    if not tie_free:
+        return literal()
     merged: "OrderedDict[Optional[str], List]" = OrderedDict()
-    for i in live:
-        c = min(int(raw.cnt[i]), T)
-        for j in range(c):
-            v = segments[i].dim_value(query.dimension, int(raw.ids[i * K + j]))
-            row = slots[i * K + j, :na]
-            if v in merged:
-                merged[v].append(row)
-            else:
-                merged[v] = [row]
+    for ts, c, value_of, slots in lists:
+        for j in range(min(c, T)):
+            merged.setdefault(value_of(j), []).append(slots[j, :na])
     keys = {v: key(v) for v in merged}
     ranked = sorted(merged, key=keys.__getitem__)
     if any(keys[a] == keys[b] for a, b in zip(ranked, ranked[1:])):
-        return merge_topn(query, _raw_results(query, segments, raw))
+        return literal()
     out = []
     for v in ranked[:T]:
         e = {query.dimension: v}
@@ -452,20 +451,23 @@ def _merge_topn_dimension(query: Q.TopNQuery, segments: Sequence[GpuSegment], ra
                     acc = agg.combine(acc, _py(x, agg.output_type))
                 e[agg.name] = acc
         out.append(e)
-    return [Q.Result(int(raw.ts[live[0]]), out)]
+    return [Q.Result(int(lists[0][0]), out)]
 
 
-def _raw_results(query: Q.TopNQuery, segments: Sequence[GpuSegment], raw: TopNRaw) -> List[List[Q.Result]]:
-    out: List[List[Q.Result]] = [[] for _ in segments]
-    na, K = len(query.aggregations), raw.K
-    for k, seg in enumerate(segments):
-        if raw.cnt[k] < 0:
-            continue
-        c = int(raw.cnt[k])
-        values = [seg.dim_value(query.dimension, int(x)) for x in raw.ids[k * K:k * K + c]]
-        slots = raw.vals.reshape(-1, max(na, 1))[k * K:k * K + c, :na]
-        out[k] = [Q.Result(int(raw.ts[k]), _topn_entries(query, values, slots))]
-    return out
+def _merge_topn_dimension(query: Q.TopNQuery, segments: Sequence[GpuSegment], raw: TopNRaw) -> List[Q.Result]:
+    spec = query.metric
+    K, na = raw.K, len(query.aggregations)
+    live = sorted((i for i in range(len(segments)) if raw.cnt[i] >= 0), key=lambda i: (int(raw.ts[i]), i))
+    orders = [segments[i].dim_order(query.dimension, spec.ordering, spec.inverted) for i in live]
+    tie_free = not any(o is not None and o.has_ties for o in orders)
+    slots = raw.vals.reshape(-1, max(na, 1))
+    lists = []
+    for i in live:
+        seg, base = segments[i], i * K
+        lists.append((int(raw.ts[i]), int(raw.cnt[i]),
+                      (lambda j, seg=seg, base=base: seg.dim_value(query.dimension, int(raw.ids[base + j]))),
+                      slots[base:base + int(raw.cnt[i])]))
+    return merge_dimension_lists(query, lists, tie_free)
 
 
 def run_topn(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional[RunStats] = None) -> List[Q.Result]:

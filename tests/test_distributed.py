@@ -38,6 +38,10 @@ def _queries(Q):
                             aggregations=aggs[1:3]),
         "topn_uniform": Q.TopNQuery(intervals=iv, dimension="dimUniform", metric="sumLongSequential", threshold=7,
                                     aggregations=aggs[1:3]),
+        "topn_numeric_order": Q.TopNQuery(intervals=iv, dimension="dimUniform", threshold=6, aggregations=aggs[1:3],
+                                          metric={"type": "dimension", "ordering": "numeric", "previousStop": "50"}),
+        "topn_inverted_alnum": Q.TopNQuery(intervals=iv, dimension="dimSequential", threshold=4, aggregations=aggs[:2],
+                                           metric={"type": "inverted", "metric": {"type": "alphaNumeric"}}),
         "groupby": Q.GroupByQuery(intervals=iv, dimensions=["dimZipf", "dimSequential"], aggregations=aggs[:4],
                                   filter=Q.InDimFilter("dimZipf", ["1", "2", "3"])),
     }
