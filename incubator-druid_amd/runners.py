@@ -414,44 +414,35 @@ def _topn_entries(query: Q.TopNQuery, values: List[Optional[str]], slots) -> Lis
 def merge_dimension_lists(query: Q.TopNQuery, lists: Sequence[Tuple[int, int, "callable", np.ndarray]],
                           tie_free: bool) -> List[Q.Result]:
     """TopNBinaryFn fold of dimension-ordered per-segment lists, given in merge order as
-    (timestamp, length, value_of(j), [length, n_aggs] slots). Each list is its segment's values in
-    comparator order; when no two values compare equal (`tie_free`: no segment order has ties, and
-    the head values checked here have distinct keys) the fold keeps the `threshold` smallest values
-    of the union, which all sit in the first `threshold` entries of every list holding them: only
-    those are looked at. Otherwise the literal pairwise fold with the builder's queue runs."""
+    (timestamp, length, value_of(j), [length, n_aggs] slots), with the builder's literal queue
+    (LexicographicResultBuilder). Each list is its segment's values in comparator order. When no
+    two values compare equal (`tie_free`: no segment order has ties, and the head entries checked
+    here have distinct keys), every value the fold keeps or ranks sits in the first `threshold`
+    non-null entries of each list holding it, and the queue sizes the fold sees (which decide
+    whether a late null is taken) are the same over those heads: the fold runs over the heads only."""
     if not lists:
         return []
     spec = query.metric
-    T, na = query.threshold, len(query.aggregations)
-    key = O.sort_key(spec.ordering, spec.inverted)
+    T = query.threshold
 
-    def literal():
-        per = [[Q.Result(ts, _topn_entries(query, [value_of(j) for j in range(c)], slots[:c]))]
-               for ts, c, value_of, slots in lists]
+    def head(c, value_of):  # the first T non-null entries (a list's null comes first)
+        return min(c, T + (1 if c and value_of(0) is None else 0))
+
+    def fold(limit):
+        per = []
+        for ts, c, value_of, slots in lists:
+            k = c if limit is None else head(c, value_of)
+            per.append([Q.Result(ts, _topn_entries(query, [value_of(j) for j in range(k)], slots[:k]))])
         return merge_topn(query, per)
 
     if not tie_free:
-        return literal()
-    merged: "OrderedDict[Optional[str], List]" = OrderedDict()
-    for ts, c, value_of, slots in lists:
-        for j in range(min(c, T)):
-            merged.setdefault(value_of(j), []).append(slots[j, :na])
-    keys = {v: key(v) for v in merged}
-    ranked = sorted(merged, key=keys.__getitem__)
-    if any(keys[a] == keys[b] for a, b in zip(ranked, ranked[1:])):
-        return literal()
-    out = []
-    for v in ranked[:T]:
-        e = {query.dimension: v}
-        if na:
-            cols = _decode_slots(query.aggregations, np.asarray(merged[v]))
-            for agg, col in zip(query.aggregations, cols):
-                acc = _py(col[0], agg.output_type)
-                for x in col[1:]:  # TopNBinaryFn: combine(accumulated, next list's value)
-                    acc = agg.combine(acc, _py(x, agg.output_type))
-                e[agg.name] = acc
-        out.append(e)
-    return [Q.Result(int(lists[0][0]), out)]
+        return fold(None)
+    key = O.sort_key(spec.ordering, spec.inverted)
+    heads = {value_of(j) for _, c, value_of, _ in lists for j in range(head(c, value_of))}
+    keys = sorted(key(v) for v in heads)
+    if any(a == b for a, b in zip(keys, keys[1:])):
+        return fold(None)
+    return fold(T)
 
 
 def _merge_topn_dimension(query: Q.TopNQuery, segments: Sequence[GpuSegment], raw: TopNRaw) -> List[Q.Result]:

@@ -97,3 +97,45 @@ def test_topn_merge_no_cursor_anywhere(Q):
     cnt = np.full(3, -1, dtype=np.int32)
     assert R.topn_merge_raw(q, cnt, np.zeros(3 * 4, np.int64), np.zeros(3 * 4, np.uint64), 4,
                             np.zeros(3, np.int64)) is None
+
+
+@pytest.mark.parametrize("ordering", ["lexicographic", "numeric", "alphanumeric", "strlen"])
+@pytest.mark.parametrize("inverted", [False, True])
+def test_dimension_order_merge_matches_oracle(O, Q, ordering, inverted):
+    """runners.merge_dimension_lists (head-only fold when tie-free, literal fold otherwise) against
+    the oracle's TopNBinaryFn fold with TopNLexicographicResultBuilder and the literal comparators;
+    lists hold nulls (dropped when they reach a full queue) and comparator-equal values."""
+    import random
+    R = importlib.import_module("incubator-druid_amd.runners")
+    rng = random.Random(hash((ordering, inverted)) & 0xffff)
+    tie_pool = ["1", "1.0", "01", "a", "A", "x1", "X01", "ab", "AB"]
+    plain_pool = [str(i) for i in range(15)] + list("bcdefg")
+    for trial in range(150):
+        ties = trial % 3 == 0
+        pool = [None] + plain_pool + (tie_pool if ties else [])
+        T, min_t = rng.randint(1, 5), rng.randint(1, 9)
+        stop = rng.choice([None, "3", "c", ""])
+        m = {"type": "dimension", "ordering": ordering, "previousStop": stop}
+        q = Q.TopNQuery(intervals=["1970-01-01/2020-01-01"], dimension="v", threshold=T,
+                        aggregations=[Q.count("rows"), Q.double_sum("d", "d")],
+                        metric={"type": "inverted", "metric": m} if inverted else m,
+                        context={"minTopNThreshold": min_t})
+        cmp = O.topn_comparator(q.metric)
+        per, lists = [], []
+        for seg in range(rng.randint(1, 5)):
+            vals = [v for v in rng.sample(pool, rng.randint(0, len(pool))) if stop is None or cmp(v, stop) > 0]
+            b = O.LexicographicResultBuilder(cmp, q.segment_threshold, stop)
+            for v in sorted(vals, key=lambda x: (x is not None, x or "")):  # any deterministic order
+                b.add(v, {"v": v, "rows": rng.randint(1, 9), "d": rng.random()})
+            entries = b.build()
+            ts = rng.choice([0, 0, 5])
+            per.append([Q.Result(ts, entries)] if entries or rng.random() < 0.8 else [])
+            if per[-1]:
+                slots = np.array([[_encode(q.aggregations[0], e["rows"]), _encode(q.aggregations[1], e["d"])]
+                                  for e in entries], dtype=np.uint64).reshape(-1, 2)
+                lists.append((ts, len(entries), (lambda j, en=entries: en[j]["v"]), slots))
+        order = sorted(range(len(lists)), key=lambda i: (lists[i][0], i))
+        tie_free = not ties
+        got = R.merge_dimension_lists(q, [lists[i] for i in order], tie_free)
+        exp = O.merge_topn(q, [p for p in per if p])
+        assert_results(q, got, exp)
