@@ -29,7 +29,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 CONFIGS = {
     # name: (rows per segment, segments per GPU, description)
     "topn": (750_000, 4, "TopNBenchmark basic: topN dimUniform threshold=10, metric sumFloatNormal, 4 x 750k rows/GPU"),
+    "topn_numeric": (750_000, 4, "TopNBenchmark basic.numericSort: topN dimUniform threshold=10, "
+                                 "DimensionTopNMetricSpec(NUMERIC), longSum, 4 x 750k rows/GPU"),
+    "topn_alphanumeric": (750_000, 4, "TopNBenchmark basic.alphanumericSort: topN dimUniform threshold=10, "
+                                      "DimensionTopNMetricSpec(ALPHANUMERIC), longSum, 4 x 750k rows/GPU"),
     "timeseries": (750_000, 1, "TimeseriesBenchmark basic: timeseries ALL count+longSum+doubleSum, selector dimSequential=399"),
+    # 1e9 rows in 64 time-partitioned segments over 30 days, 8 segments per GPU
+    "ts_hourly": (15_625_000, 8, "1B-row dataset (64 x 15.625M rows, 30 days), 8 segments/GPU: timeseries HOUR "
+                                 "count+longSum+doubleSum+longMax+doubleMin"),
+    "groupby_hourly": (15_625_000, 8, "1B-row dataset (64 x 15.625M rows, 30 days), 8 segments/GPU: groupBy HOUR "
+                                      "(dimZipf, dimSequential) longSum+doubleSum"),
     "groupby": (12_500_000, 1, "GroupByV2 dimUniform x dimHyperUnique + longSum/doubleSum"),
     "filtered": (12_500_000, 1, "compound AND/OR bound+selector+in filter, timeseries count"),
 }
@@ -40,10 +49,23 @@ def make_query(Q, name):
     if name == "topn":
         return Q.TopNQuery(intervals=iv, dimension="dimUniform", metric="sumFloatNormal", threshold=10,
                            aggregations=[Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal")])
+    if name in ("topn_numeric", "topn_alphanumeric"):
+        ordering = name.split("_")[1]
+        return Q.TopNQuery(intervals=iv, dimension="dimUniform", threshold=10,
+                           metric={"type": "dimension", "ordering": ordering, "previousStop": None},
+                           aggregations=[Q.long_sum("sumLongSequential")])
     if name == "timeseries":
         return Q.TimeseriesQuery(intervals=iv, aggregations=[Q.count("rows"), Q.long_sum("sumLongSequential"),
                                                              Q.double_sum("sumFloatNormal")],
                                  filter=Q.SelectorDimFilter("dimSequential", "399"))
+    if name == "ts_hourly":
+        return Q.TimeseriesQuery(intervals=iv, granularity="hour",
+                                 aggregations=[Q.count("rows"), Q.long_sum("sumLongSequential"),
+                                               Q.double_sum("sumFloatNormal"), Q.long_max("maxLongUniform"),
+                                               Q.double_min("minFloatZipf")])
+    if name == "groupby_hourly":
+        return Q.GroupByQuery(intervals=iv, granularity="hour", dimensions=["dimZipf", "dimSequential"],
+                              aggregations=[Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal")])
     if name == "groupby":
         return Q.GroupByQuery(intervals=iv, dimensions=["dimUniform", "dimHyperUnique"],
                               aggregations=[Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal")])
@@ -56,17 +78,52 @@ def make_query(Q, name):
     raise ValueError(name)
 
 
-def ensure_segments(DG, root, rank, nseg, rows, compression, bitmap, lz4_mode):
-    d = os.path.join(root, f"r{rows}_s{nseg}_{compression}_{bitmap}_{lz4_mode}", f"rank{rank}")
+DATASET_1B = {"segments": 64, "interval": (0, 30 * 86_400_000),
+              "dims": ["dimZipf", "dimSequential"],
+              "metrics": ["sumLongSequential", "sumFloatNormal", "maxLongUniform", "minFloatZipf"]}
+
+
+def _write_one(job):
+    DG = importlib.import_module("incubator-druid_amd.datagen")
+    p, rows, seed, bitmap, compression, lz4_mode, part = job
+    if part is None:
+        DG.write_basic_segment(p, rows, seed=seed, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode)
+    else:  # time chunk `part` of the 1B-row dataset; the segment's interval is its chunk
+        W = importlib.import_module("incubator-druid_amd.writer")
+        n_all = DATASET_1B["segments"]
+        start, end = DATASET_1B["interval"]
+        spec = DG.basic_columns(rows, seed, interval=DATASET_1B["interval"], row_offset=part * rows,
+                                total_rows=n_all * rows, dims=DATASET_1B["dims"], metrics=DATASET_1B["metrics"])
+        span = (end - start) // n_all
+        spec.interval = (start + part * span, end if part == n_all - 1 else start + (part + 1) * span)
+        idx = np.arange(part * rows, (part + 1) * rows, dtype=np.int64)
+        spec.timestamps = ts = start + idx * (end - start) // (n_all * rows)  # row r at floor(r * 30d / 1e9)
+        assert spec.interval[0] <= int(ts[0]) and int(ts[-1]) < spec.interval[1], (part, spec.interval, ts[0], ts[-1])
+        W.write_segment(p, spec, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode)
+    return p
+
+
+def ensure_segments(DG, root, rank, nseg, rows, compression, bitmap, lz4_mode, partitioned=False, workers=8):
+    """This rank's segments (seed 9999 + global segment index). partitioned: consecutive time chunks
+    of the 1B-row dataset (rank r holds global chunks r*nseg ..); otherwise every segment spans the
+    basic interval like the JMH benchmarks' segments. Written once, in parallel, and reused."""
+    tag = "p1b_" if partitioned else ""
+    d = os.path.join(root, f"{tag}r{rows}_s{nseg}_{compression}_{bitmap}_{lz4_mode}", f"rank{rank}")
     marker = os.path.join(d, "DONE")
     paths = [os.path.join(d, f"seg{i:04d}") for i in range(nseg)]
     if not os.path.exists(marker):
         shutil.rmtree(d, ignore_errors=True)
         os.makedirs(d, exist_ok=True)
-        for i, p in enumerate(paths):
-            DG.write_basic_segment(p, rows, seed=9999 + rank * nseg + i, bitmap=bitmap, compression=compression,
-                                   lz4_mode=lz4_mode)
-            print(f"[rank {rank}] wrote {p}", file=sys.stderr, flush=True)
+        jobs = [(p, rows, 9999 + rank * nseg + i, bitmap, compression, lz4_mode,
+                 (rank * nseg + i) if partitioned else None) for i, p in enumerate(paths)]
+        if len(jobs) > 1 and workers > 1:
+            import multiprocessing as mp
+            with mp.get_context("spawn").Pool(min(workers, len(jobs))) as pool:
+                for p in pool.imap_unordered(_write_one, jobs):
+                    print(f"[rank {rank}] wrote {p}", file=sys.stderr, flush=True)
+        else:
+            for j in jobs:
+                print(f"[rank {rank}] wrote {_write_one(j)}", file=sys.stderr, flush=True)
         open(marker, "w").close()
     return paths
 
@@ -104,6 +161,7 @@ def main():
     ap.add_argument("--data-dir", default=os.environ.get("DRUID_AMD_BENCH_DATA", "/tmp/druid_amd_bench"))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--write-workers", type=int, default=8, help="processes writing the synthetic segments")
     args = ap.parse_args()
 
     Q = importlib.import_module("incubator-druid_amd.query")
@@ -122,29 +180,38 @@ def main():
     rows_per, nseg, desc = CONFIGS[args.config]
     rows_per = args.rows or rows_per
     nseg = args.segments or nseg
-    paths = ensure_segments(DG, args.data_dir, rank, nseg, rows_per, args.compression, args.bitmap, args.lz4_mode)
+    paths = ensure_segments(DG, args.data_dir, rank, nseg, rows_per, args.compression, args.bitmap, args.lz4_mode,
+                            partitioned=args.config in ("ts_hourly", "groupby_hourly"), workers=args.write_workers)
     segs = [S.GpuSegment(p, device=local_rank) for p in paths]
     query = make_query(Q, args.config)
 
     gdict = None
-    if dist is not None and args.config == "topn":
+    if dist is not None and args.config.startswith("topn"):
         gdict = D.GlobalDictionary.build(dist, [s.dictionary(query.dimension) for s in segs])
         translations = [gdict.translate(s.dictionary(query.dimension)) for s in segs]
     gdicts = None
-    if dist is not None and args.config == "groupby":
+    if dist is not None and args.config.startswith("groupby"):
         gdicts = {d: D.GlobalDictionary.build(dist, [s.dictionary(d) for s in segs]) for d in query.dimensions}
+
+    ts_buckets = None  # cluster-wide bucket keys of a timeseries query (identical on every rank), once
+    if dist is not None and isinstance(query, Q.TimeseriesQuery):
+        local = R.merge_timeseries(query, R.timeseries_per_segment(segs, query, R.RunStats()))
+        mine = sorted({0 if query.granularity.is_all else query.granularity.bucket_start(r.timestamp) for r in local})
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        ts_buckets = sorted({b for g in gathered for b in g})
 
     def step(stats):
         if isinstance(query, Q.TopNQuery):
             if dist is None:
                 return R.run_topn(segs, query, stats)
-            return D.gather_topn(dist, query, R.topn_raw(segs, query, stats), gdict, translations)
+            return D.gather_topn(dist, query, R.topn_raw(segs, query, stats), gdict, translations, segs)
         if isinstance(query, Q.TimeseriesQuery):
             per = R.timeseries_per_segment(segs, query, stats)
             res = R.merge_timeseries(query, per)
             if dist is None:
                 return res
-            return D.allreduce_timeseries(dist, query, res, [0])
+            return D.allreduce_timeseries(dist, query, res, ts_buckets)
         per = R.groupby_per_segment(segs, query, stats)
         if dist is None:
             return R.merge_groupby_columnar(query, per)
@@ -185,6 +252,8 @@ def main():
     uncompressed_equiv = None
     if args.config == "topn":
         uncompressed_equiv = scanned_local * (3 + 8 + 8)
+    elif args.config.startswith("topn_"):
+        uncompressed_equiv = scanned_local * (3 + 8)
     if decode_ms >= agg_ms and decode_ms > 0:
         kernel, k_ms, k_bytes = "k_lz4_decode", decode_ms, bytes_read
     else:
