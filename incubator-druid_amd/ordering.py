@@ -24,6 +24,7 @@ inverse(nulls-last delegate): nulls first, then the delegate order reversed.
 from __future__ import annotations
 
 import bisect
+import functools
 from decimal import Decimal
 from typing import List, Optional, Sequence, Tuple
 
@@ -208,12 +209,18 @@ class _Desc:
         return hash(self.k)
 
 
+_SORT_KEYS: dict = {}
+
+
 def sort_key(ordering: str, inverted: bool = False):
-    """Key function of the topN comparator: StringComparator, or InvertedTopNMetricSpec over it."""
-    base = KEY_FUNCTIONS[ordering]
-    if not inverted:
-        return base
-    return lambda s: (0,) if s is None else (1, _Desc(base(s)))
+    """Key function of the topN comparator: StringComparator, or InvertedTopNMetricSpec over it
+    (memoized: merges rank the same head values query after query)."""
+    fn = _SORT_KEYS.get((ordering, inverted))
+    if fn is None:
+        base = KEY_FUNCTIONS[ordering]
+        raw = base if not inverted else (lambda s: (0,) if s is None else (1, _Desc(base(s))))
+        fn = _SORT_KEYS[(ordering, inverted)] = functools.lru_cache(maxsize=1 << 16)(raw)
+    return fn
 
 
 class DictionaryOrder:
