@@ -116,10 +116,15 @@ typedef struct {
   int32_t ordering;          /* DG_ORDER_* */
 } dg_filter;
 
-/* AggregatorFactory (name is the caller's business; field is the input column, NULL for count) */
+/* AggregatorFactory (name is the caller's business; field is the input column, NULL for count).
+ * filter / n_filter: FilteredAggregatorFactory (query/aggregation/FilteredAggregatorFactory.java:56-73,
+ * FilteredBufferAggregator.java:45-50): the aggregator takes a cursor row only when the filter
+ * (same node encoding as dg_scan.filter) matches it; NULL / 0 = unfiltered. */
 typedef struct {
   int32_t kind;
   const char* field;
+  const dg_filter* filter;
+  int32_t n_filter;
 } dg_agg;
 
 /*

@@ -6,6 +6,7 @@ cannot be loaded the product path raises, it never silently runs on the CPU.
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 from typing import List, Optional, Sequence
 
@@ -47,7 +48,8 @@ class dg_filter(ctypes.Structure):
 
 
 class dg_agg(ctypes.Structure):
-    _fields_ = [("kind", ctypes.c_int32), ("field", ctypes.c_char_p)]
+    _fields_ = [("kind", ctypes.c_int32), ("field", ctypes.c_char_p), ("filter", ctypes.c_void_p),
+                ("n_filter", ctypes.c_int32)]
 
 
 class dg_scan(ctypes.Structure):
@@ -164,10 +166,11 @@ def _b(s: Optional[str]) -> Optional[bytes]:
 class FilterProgram:
     """DimFilter tree -> prefix-ordered dg_filter array (keeps the backing strings alive)."""
 
-    def __init__(self, flt, query_module):
+    def __init__(self, flt, query_module, segments=None):
         self._keep: List = []
         self.nodes: List[dg_filter] = []
         self.Q = query_module
+        self.segments = segments
         if flt is not None:
             self._emit(flt)
         self.array = (dg_filter * max(len(self.nodes), 1))(*self.nodes) if self.nodes else None
@@ -204,6 +207,15 @@ class FilterProgram:
             node.kind = F_IN
             node.values = self._strs(list(f.values))
             node.n_values = len(f.values)
+        elif isinstance(f, Q.PREDICATE_FILTERS) or (isinstance(f, Q.BoundDimFilter) and f.ordering not in ORDER):
+            # predicate over dictionary values (Filters.matchPredicate): the host evaluates it on the
+            # dictionaries of the segments of this call, the engine unions the matching values' bitmaps
+            if self.segments is None:
+                raise UnsupportedQuery(2, f"filter {type(f).__name__} needs the segments' dictionaries")
+            vals = predicate_values(f, self.segments, Q)
+            node.kind = F_IN
+            node.values = self._strs(vals)
+            node.n_values = len(vals)
         elif isinstance(f, Q.BoundDimFilter):
             node.kind = F_BOUND
             lo, hi = _b(f.lower), _b(f.upper)
@@ -218,10 +230,50 @@ class FilterProgram:
         self.nodes.append(node)
 
 
-def make_scan(query, query_module, cancel: Optional[ctypes.c_int32] = None):
-    """Build a dg_scan (+ keep-alive list) from a query's interval, granularity, filter and aggs."""
+def predicate_values(f, segments, Q) -> List[Optional[str]]:
+    """Dictionary values (over the given segments) a predicate filter accepts, null included when the
+    predicate accepts it (missing columns then read as all-true, Filters.matchPredicate). Cached per
+    segment and filter."""
+    key = (f.dimension, json.dumps(f.to_json(), sort_keys=True))
+    pred = f.predicate if not isinstance(f, Q.BoundDimFilter) else _bound_predicate(f)
+    out = set()
+    for seg in segments:
+        cache = seg.__dict__.setdefault("_pred_cache", {})
+        if key not in cache:
+            vals = seg.dictionary(f.dimension)
+            cache[key] = frozenset(v for v in vals if pred(v))
+        out |= cache[key]
+    if pred(None):
+        out.add(None)
+    return sorted(out, key=lambda v: (v is not None, v or ""))
+
+
+def _bound_predicate(f):
+    """BoundFilter.doesMatch (segment/filter/BoundFilter.java:249-275) for orderings the engine does not
+    evaluate itself (alphanumeric, strlen), through the comparator's sort key."""
+    from . import ordering as O
+    from .query import _empty_to_null
+    key = O.sort_key(f.ordering)
+    lower, upper = _empty_to_null(f.lower), _empty_to_null(f.upper)
+    has_lower, has_upper = f.lower is not None, f.upper is not None
+
+    def pred(v):
+        if v is None:
+            return ((not has_lower) or (lower is None and not f.lowerStrict)) and \
+                   ((not has_upper) or upper is not None or not f.upperStrict)
+        kv = key(v)
+        lc = 1 if not has_lower else (kv > key(f.lower)) - (kv < key(f.lower))
+        uc = 1 if not has_upper else (key(f.upper) > kv) - (key(f.upper) < kv)
+        return (lc > 0 if f.lowerStrict else lc >= 0) and (uc > 0 if f.upperStrict else uc >= 0)
+    return pred
+
+
+def make_scan(query, query_module, cancel: Optional[ctypes.c_int32] = None, segments=None, filters: bool = True):
+    """Build a dg_scan (+ keep-alive list) from a query's interval, granularity, filter and aggs.
+    segments: the segments of the call (predicate filters are resolved over their dictionaries);
+    filters=False leaves the query and aggregator filters out (merges only need the aggregators)."""
     keep = []
-    fp = FilterProgram(query.effective_filter(), query_module)
+    fp = FilterProgram(query.effective_filter() if filters else None, query_module, segments)
     keep.append(fp)
     aggs = (dg_agg * max(len(query.aggregations), 1))()
     for i, a in enumerate(query.aggregations):
@@ -229,6 +281,12 @@ def make_scan(query, query_module, cancel: Optional[ctypes.c_int32] = None):
         fld = _b(a.fieldName) if a.kind != 0 else None
         keep.append(fld)
         aggs[i].field = fld
+        if a.filter is not None and filters:  # FilteredAggregatorFactory: the delegate's row matcher
+            afp = FilterProgram(a.filter.optimize(), query_module, segments)
+            keep.append(afp)
+            if afp.array is not None:
+                aggs[i].filter = ctypes.cast(afp.array, ctypes.c_void_p)
+                aggs[i].n_filter = len(afp.nodes)
     keep.append(aggs)
     s = dg_scan()
     s.interval_start, s.interval_end = query.interval

@@ -890,10 +890,22 @@ static int check_segments(dg_segment* const* segs, int32_t n, Context** ctx) {
 
 static bool cancelled(const dg_scan* q) { return q->cancel && *q->cancel; }
 
-// resolve an aggregator's input column into a view (absent column reads 0)
-static int agg_view(Segment* seg, const dg_agg& a, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
+// resolve an aggregator's input column into a view (absent column reads 0) and, for a
+// FilteredAggregatorFactory, its filter into a row bitset (the ValueMatcher of
+// FilteredBufferAggregator.aggregate, FilteredBufferAggregator.java:45-50: for the supported filters
+// the row matcher and the bitmap index select the same rows)
+static int agg_view(Segment* seg, const dg_agg& a, CallScratch* cs, DecodeBatch* db, ColView* v, const uint32_t** bits,
+                    hipStream_t st) {
   memset(v, 0, sizeof *v);
   v->kind = VIEW_ABSENT;
+  *bits = nullptr;
+  if (a.filter && a.n_filter > 0) {
+    uint32_t* b = nullptr;
+    const unsigned long long* cnt = nullptr;
+    int rc = build_bitset(seg, cs, a.filter, a.n_filter, &b, &cnt, st);
+    if (rc) return rc;
+    *bits = b;
+  }
   if (a.kind == DG_AGG_COUNT || !a.field) return DG_OK;
   Column* c = seg->find(a.field);
   if (!c) return DG_OK;
@@ -1104,7 +1116,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
       if (rc) return rc;
     }
     for (int a = 0; a < na; ++a) {
-      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], st);
+      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
       if (rc) return rc;
     }
     j.out = dev_take<uint64_t>(cs, (size_t)cur[i].nbuckets * rec);
@@ -1270,7 +1282,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       card[i] = 1;
     }
     for (int a = 0; a < na; ++a) {
-      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], st);
+      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
       if (rc) return rc;
     }
     j.out = nullptr;  // allocated below with the bins
@@ -2015,7 +2027,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     space *= (double)cur[i].nbuckets;
     if (shift > 63) return set_error(DG_ERR_UNSUPPORTED, "groupBy key of %d bits", shift);
     for (int a = 0; a < na; ++a) {
-      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], st);
+      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
       if (rc) return rc;
     }
     double groups = std::min(space, (double)std::max<int64_t>(cnt, 1));

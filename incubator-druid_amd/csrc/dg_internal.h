@@ -77,6 +77,7 @@ struct ScanJob {
   int32_t nbuckets;
   int32_t pad;
   ColView vals[kMaxAggs];   // input column per aggregator
+  const uint32_t* agg_bits[kMaxAggs];  // FilteredAggregatorFactory row matcher per aggregator (null: all rows)
   ColView key;              // topN: dimension ids
   uint64_t* out;            // accumulator table of this segment
 };
@@ -97,6 +98,7 @@ struct GroupJob {
   int32_t bucket_shift;
   int32_t pad2;
   ColView vals[kMaxAggs];
+  const uint32_t* agg_bits[kMaxAggs];  // FilteredAggregatorFactory row matcher per aggregator (null: all rows)
   uint64_t* keys;           // [cap]
   uint64_t* slots;          // [cap * (naggs + 1)], slot 0 = rows
   uint64_t mask;            // cap - 1

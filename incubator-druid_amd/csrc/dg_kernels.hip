@@ -519,6 +519,19 @@ __device__ __forceinline__ bool row_selected(const ScanJob& j, int64_t r, int64_
   return true;
 }
 
+// FilteredAggregatorFactory: a row the aggregator's matcher rejects contributes the slot identity
+// (FilteredBufferAggregator.aggregate skips the delegate; the record keeps its init value)
+__device__ __forceinline__ bool agg_row(const uint32_t* bits, int64_t r) {
+  return !bits || ((bits[r >> 5] >> (r & 31)) & 1u);
+}
+__device__ __forceinline__ unsigned agg_quad(const uint32_t* bits, int64_t r) {  // r % 4 == 0
+  return bits ? (bits[r >> 5] >> (r & 31)) & 0xFu : 0xFu;
+}
+template <class Job>
+__device__ __forceinline__ uint64_t agg_in(const Job& j, const AggPlan& plan, int a, int64_t r) {
+  return agg_row(j.agg_bits[a], r) ? agg_input(plan.kind[a], j.vals[a], r) : identity_of(plan.op[a], plan.kind[a]);
+}
+
 template <bool TOPN>
 __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                   AggPlan plan) {
@@ -539,7 +552,7 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
       atomicAdd(reinterpret_cast<unsigned long long*>(rec), 1ull);
 #pragma unroll
       for (int a = 0; a < kMaxAggs; ++a) {
-        if (a < na) atomic_op(plan.op[a], rec + 1 + a, agg_input(plan.kind[a], j.vals[a], r));
+        if (a < na) atomic_op(plan.op[a], rec + 1 + a, agg_in(j, plan, a, r));
       }
     }
     return;
@@ -596,7 +609,7 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
     cnt++;
 #pragma unroll
     for (int a = 0; a < kMaxAggs; ++a) {
-      if (a < na) acc[a] = combine_op(plan.op[a], acc[a], agg_input(plan.kind[a], j.vals[a], r));
+      if (a < na) acc[a] = combine_op(plan.op[a], acc[a], agg_in(j, plan, a, r));
     }
   }
   flush(cur);
@@ -695,9 +708,12 @@ __global__ __launch_bounds__(kPartThreads) void k_topn_part(const ScanJob* __res
         uint64_t raw[4] = {0, 0, 0, 0};
         const int vk = j.vals[a].kind;
         if (plan.kind[a] != DG_AGG_COUNT && vk != VIEW_ABSENT) load_raw4(j.vals[a], r, raw);
+        const unsigned fm = agg_quad(j.agg_bits[a], r);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          if ((m[u] >> k) & 1) atomic_op(plan.op[a], e[k] + 1 + a, agg_input_raw(plan.kind[a], vk, raw[k]));
+          if ((m[u] >> k) & 1)
+            atomic_op(plan.op[a], e[k] + 1 + a,
+                      (fm >> k) & 1 ? agg_input_raw(plan.kind[a], vk, raw[k]) : identity_of(plan.op[a], plan.kind[a]));
       }
     }
   }
@@ -709,7 +725,7 @@ __global__ __launch_bounds__(kPartThreads) void k_topn_part(const ScanJob* __res
       if (id < lo || id >= hi) continue;
       uint64_t* e = s_tab + (id - lo) * rec;
       atomicAdd(reinterpret_cast<unsigned long long*>(e), 1ull);
-      for (int a = 0; a < na; ++a) atomic_op(plan.op[a], e + 1 + a, agg_input(plan.kind[a], j.vals[a], rr));
+      for (int a = 0; a < na; ++a) atomic_op(plan.op[a], e + 1 + a, agg_in(j, plan, a, rr));
     }
   }
   __syncthreads();
@@ -876,7 +892,7 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_bin_scatter(const ScanJob*
       const uint32_t id = load_id(j.key, r);
       const uint32_t pos = atomicAdd(&cur[id >> shift], 1u);
       lid[pos] = (uint16_t)(id & lmask);
-      for (int a = 0; a < na; ++a) vals[(size_t)a * cap + pos] = agg_input(plan.kind[a], j.vals[a], r);
+      for (int a = 0; a < na; ++a) vals[(size_t)a * cap + pos] = agg_in(j, plan, a, r);
     }
     return;
   }
@@ -958,11 +974,13 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_bin_scatter(const ScanJob*
       if (r + 4 <= full) {
         uint64_t raw[4] = {0, 0, 0, 0};
         if (plan.kind[a] != DG_AGG_COUNT && vk != VIEW_ABSENT) load_raw4(j.vals[a], r, raw);
+        const unsigned fm = agg_quad(j.agg_bits[a], r);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) in[k] = agg_input_raw(plan.kind[a], vk, raw[k]);
+        for (int k = 0; k < 4; ++k)
+          in[k] = (fm >> k) & 1 ? agg_input_raw(plan.kind[a], vk, raw[k]) : identity_of(plan.op[a], plan.kind[a]);
       } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) in[k] = ((m[u] >> k) & 1) ? agg_input(plan.kind[a], j.vals[a], r + k) : 0;
+        for (int k = 0; k < 4; ++k) in[k] = ((m[u] >> k) & 1) ? agg_in(j, plan, a, r + k) : 0;
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k)
@@ -1389,7 +1407,7 @@ __global__ __launch_bounds__(256) void k_groupby(const GroupJob* __restrict__ jo
     atomicAdd(reinterpret_cast<unsigned long long*>(rec), 1ull);
 #pragma unroll
     for (int a = 0; a < kMaxAggs; ++a) {
-      if (a < na) atomic_op(plan.op[a], rec + 1 + a, agg_input(plan.kind[a], j.vals[a], r));
+      if (a < na) atomic_op(plan.op[a], rec + 1 + a, agg_in(j, plan, a, r));
     }
   }
 }

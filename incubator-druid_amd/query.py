@@ -195,6 +195,12 @@ class DimFilter:
             return OrDimFilter([DimFilter.from_json(f) for f in js["fields"]])
         if t == "not":
             return NotDimFilter(DimFilter.from_json(js["field"]))
+        if t == "regex":
+            return RegexDimFilter(js["dimension"], js["pattern"])
+        if t == "search":
+            return SearchQueryDimFilter(js["dimension"], dict(js["query"]))
+        if t == "like":
+            return LikeDimFilter(js["dimension"], js["pattern"], js.get("escape"))
         raise ValueError(f"unsupported filter type {t!r}")
 
 
@@ -284,6 +290,130 @@ class NotDimFilter(DimFilter):
         return {"type": "not", "field": self.field.to_json()}
 
 
+# ---- predicate filters: evaluated over dictionary values (DimensionPredicateFilter ->
+# Filters.matchPredicate, segment/filter/Filters.java:239-290), i.e. the union of the bitmaps of every
+# value the predicate accepts; a missing column is all-true iff the predicate accepts null ----
+def _java_regex(pattern: str) -> "re.Pattern":
+    """java.util.regex.Pattern.compile for the common syntax (Python re; \\p{..} classes and
+    possessive quantifiers are not translated)."""
+    return re.compile(pattern)
+
+
+def _region_matches_ignore_case(s: str, i: int, sub: str) -> bool:
+    """String.regionMatches(true, i, sub, 0, len): per UTF-16 char, equal after toUpperCase or
+    toLowerCase (BMP characters; Python's case tables)."""
+    def up(c):
+        u = c.upper()
+        return u if len(u) == 1 else c
+
+    def low(c):
+        u = c.lower()
+        return u if len(u) == 1 else c
+
+    for a, b in zip(s[i:i + len(sub)], sub):
+        if a == b:
+            continue
+        ua, ub = up(a), up(b)
+        if ua == ub or low(ua) == low(ub):
+            continue
+        return False
+    return True
+
+
+def contains_ignore_case(s: Optional[str], sub: Optional[str]) -> bool:
+    """commons-lang StringUtils.containsIgnoreCase."""
+    if s is None or sub is None:
+        return False
+    return any(_region_matches_ignore_case(s, i, sub) for i in range(len(s) - len(sub) + 1))
+
+
+@dataclass
+class RegexDimFilter(DimFilter):
+    """RegexDimFilter -> RegexFilter (segment/filter/RegexFilter.java:44-48): non-null and find()."""
+    dimension: str
+    pattern: str
+
+    def predicate(self, v: Optional[str]) -> bool:
+        return v is not None and _java_regex(self.pattern).search(v) is not None
+
+    def to_json(self):
+        return {"type": "regex", "dimension": self.dimension, "pattern": self.pattern}
+
+
+@dataclass
+class SearchQueryDimFilter(DimFilter):
+    """SearchQueryDimFilter with a SearchQuerySpec (query/search/*SearchQuerySpec.java accept()):
+    contains / insensitive_contains (StringUtils.containsIgnoreCase), fragment (every value
+    contained), regex (find), all."""
+    dimension: str
+    query: Dict[str, Any]
+
+    def predicate(self, v: Optional[str]) -> bool:
+        q, t = self.query, self.query.get("type")
+        if t == "all":
+            return True
+        if v is None:
+            return False
+        if t in ("contains", "insensitive_contains"):
+            val = q.get("value")
+            if val is None:
+                return False
+            if t == "contains" and q.get("caseSensitive", False):
+                return val in v
+            return contains_ignore_case(v, val)
+        if t == "fragment":
+            vals = q.get("values")
+            if vals is None:
+                return False
+            if q.get("caseSensitive", False):
+                return all(x in v for x in set(vals))
+            return all(contains_ignore_case(v, x) for x in set(vals))
+        if t == "regex":
+            return _java_regex(q["pattern"]).search(v) is not None
+        raise ValueError(f"unsupported search query spec {t!r}")
+
+    def to_json(self):
+        return {"type": "search", "dimension": self.dimension, "query": dict(self.query)}
+
+
+@dataclass
+class LikeDimFilter(DimFilter):
+    """LikeDimFilter.LikeMatcher (query/filter/LikeDimFilter.java:75-158): % -> .*, _ -> ., the escape
+    character quotes the next one, other characters outside [\\w\\d\\s-] as \\uXXXX; matches()
+    over nullToEmpty(value) in default null mode."""
+    dimension: str
+    pattern: str
+    escape: Optional[str] = None
+
+    def _regex(self) -> "re.Pattern":
+        esc = self.escape[0] if self.escape else None
+        out, escaping = [], False
+        for c in self.pattern:
+            if esc is not None and c == esc and not escaping:
+                escaping = True
+            elif c == "%" and not escaping:
+                out.append(".*")
+            elif c == "_" and not escaping:
+                out.append(".")
+            else:
+                out.append(c if re.fullmatch(r"[A-Za-z0-9_\s-]", c) else "\\u%04x" % ord(c) if ord(c) < 0x10000
+                           else re.escape(c))
+                escaping = False
+        return re.compile("".join(out))
+
+    def predicate(self, v: Optional[str]) -> bool:
+        return self._regex().fullmatch("" if v is None else v) is not None
+
+    def to_json(self):
+        js = {"type": "like", "dimension": self.dimension, "pattern": self.pattern}
+        if self.escape is not None:
+            js["escape"] = self.escape
+        return js
+
+
+PREDICATE_FILTERS = (RegexDimFilter, SearchQueryDimFilter, LikeDimFilter)
+
+
 # ----------------------------------------------------------------------------------------------
 # aggregators
 # ----------------------------------------------------------------------------------------------
@@ -323,9 +453,13 @@ def _wrap64(v: int) -> int:
 
 @dataclass
 class AggregatorFactory:
+    """An aggregator factory; `filter` set = FilteredAggregatorFactory around it
+    (query/aggregation/FilteredAggregatorFactory.java:40-73: the delegate aggregates a row only when
+    the filter's ValueMatcher matches it; name, combine and comparator are the delegate's)."""
     type: str
     name: str
     fieldName: Optional[str] = None
+    filter: Optional["DimFilter"] = None
 
     def __post_init__(self):
         if self.type not in AGG_KINDS:
@@ -388,13 +522,28 @@ class AggregatorFactory:
         js = {"type": self.type, "name": self.name}
         if self.fieldName is not None:
             js["fieldName"] = self.fieldName
+        if self.filter is not None:
+            return {"type": "filtered", "filter": self.filter.to_json(), "aggregator": js}
         return js
 
     @staticmethod
     def from_json(js) -> "AggregatorFactory":
         if isinstance(js, AggregatorFactory):
             return js
+        if js["type"] == "filtered":
+            inner = AggregatorFactory.from_json(js["aggregator"])
+            f = DimFilter.from_json(js["filter"])
+            if f is None:
+                raise ValueError("filtered aggregator without a filter")
+            # FilteredAggregatorFactory(FilteredAggregatorFactory(x, f1), f2) matches f2 and then f1
+            both = f if inner.filter is None else AndDimFilter([f, inner.filter])
+            return AggregatorFactory(inner.type, inner.name, inner.fieldName, both)
         return AggregatorFactory(js["type"], js["name"], js.get("fieldName"))
+
+
+def filtered(agg: AggregatorFactory, flt) -> AggregatorFactory:
+    """FilteredAggregatorFactory(agg, filter)."""
+    return AggregatorFactory.from_json({"type": "filtered", "filter": flt, "aggregator": agg})
 
 
 def count(name="count"):

@@ -89,7 +89,7 @@ def timeseries_per_segment(segments: Sequence[GpuSegment], query: Q.TimeseriesQu
     for _, idx in _group_by_device(segments).items():
         segs = [segments[i] for i in idx]
         cap = _bucket_cap(segs, query)
-        scan, keep = N.make_scan(query, Q)
+        scan, keep = N.make_scan(query, Q, segments=segs)
         n = len(segs)
         nb = np.zeros(n, dtype=np.int32)
         times = np.zeros(n * cap, dtype=np.int64)
@@ -347,7 +347,7 @@ def topn_raw(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional
         raise ValueError("topn_raw: segments must share one device")
     na = len(query.aggregations)
     K = query.segment_threshold
-    scan, keep = N.make_scan(query, Q)
+    scan, keep = N.make_scan(query, Q, segments=segments)
     t, keep_t = _topn_struct(query, K, segments)
     n = len(segments)
     cnt = np.zeros(n, dtype=np.int32)
@@ -382,7 +382,7 @@ def topn_merge_raw(query: Q.TopNQuery, cnt: np.ndarray, keys: np.ndarray, vals: 
     lists.stride = K
     lists.keys = o_keys.ctypes.data
     lists.values = o_vals.ctypes.data
-    scan, keep = N.make_scan(query, Q)
+    scan, keep = N.make_scan(query, Q, filters=False)  # the fold needs the aggregators only
     t, dim = _topn_struct(query, query.threshold)
     out_n = ctypes.c_int32()
     T = query.threshold
@@ -559,7 +559,7 @@ def groupby_per_segment(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
     nd = len(query.dimensions)
     for _, idx in _group_by_device(segments).items():
         segs = [segments[i] for i in idx]
-        scan, keep = N.make_scan(query, Q)
+        scan, keep = N.make_scan(query, Q, segments=segs)
         dims = (ctypes.c_char_p * max(nd, 1))(*[d.encode() for d in query.dimensions])
         g = N.dg_groupby()
         g.dimensions = ctypes.cast(dims, ctypes.POINTER(ctypes.c_char_p))

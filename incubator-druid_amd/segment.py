@@ -134,7 +134,7 @@ class GpuSegment:
 
     def filter_bitmap(self, flt, query_module) -> Tuple[np.ndarray, int]:
         """Filter.getBitmapResult as a dense row bitset (uint32 words) + cardinality."""
-        fp = N.FilterProgram(flt, query_module)
+        fp = N.FilterProgram(flt, query_module, [self])
         words = np.zeros((self.num_rows + 31) // 32, dtype=np.uint32)
         cnt = ctypes.c_int64()
         arr = ctypes.cast(fp.array, ctypes.POINTER(N.dg_filter)) if fp.array is not None else None

@@ -491,7 +491,8 @@ def _bound_matches(f, value: Optional[str]) -> bool:
     if value is None:
         return ((not has_lower) or (lower is None and not f.lowerStrict)) and \
                ((not has_upper) or upper is not None or not f.upperStrict)
-    cmp = numeric_compare if f.ordering == "numeric" else _lex_compare
+    cmp = {"numeric": numeric_compare, "alphanumeric": alphanumeric_compare,
+           "strlen": strlen_compare}.get(f.ordering, _lex_compare)
     lc = cmp(value, f.lower) if has_lower else 1
     uc = cmp(f.upper, value) if has_upper else 1
     if f.lowerStrict and f.upperStrict:
@@ -501,6 +502,88 @@ def _bound_matches(f, value: Optional[str]) -> bool:
     if f.upperStrict:
         return lc >= 0 and uc > 0
     return lc >= 0 and uc >= 0
+
+
+def _oracle_region_matches_ci(s: str, off: int, sub: str) -> bool:
+    """String.regionMatches(true, off, sub, 0, sub.length()) (java.lang.String, JDK 8)."""
+    for k in range(len(sub)):
+        c1, c2 = ord(s[off + k]), ord(sub[k])
+        if c1 == c2:
+            continue
+        u1, u2 = _java_upper(c1), _java_upper(c2)
+        if u1 == u2:
+            continue
+        if _java_lower(u1) == _java_lower(u2):
+            continue
+        return False
+    return True
+
+
+def _oracle_contains_ci(s, sub) -> bool:
+    """commons-lang 2.6 StringUtils.containsIgnoreCase."""
+    if s is None or sub is None:
+        return False
+    for i in range(len(s) - len(sub) + 1):
+        if _oracle_region_matches_ci(s, i, sub):
+            return True
+    return False
+
+
+def _oracle_like_regex(pattern: str, escape: Optional[str]):
+    """LikeDimFilter.LikeMatcher.from (query/filter/LikeDimFilter.java:107-152)."""
+    import re
+    esc = escape[0] if escape else None
+    regex, escaping = [], False
+    for c in pattern:
+        if esc is not None and c == esc and not escaping:
+            escaping = True
+        elif c == "%" and not escaping:
+            regex.append(".*")
+        elif c == "_" and not escaping:
+            regex.append(".")
+        else:
+            fine = c.isascii() and (c.isalnum() or c == "_" or c == "-" or c in " \t\n\x0b\f\r")
+            regex.append(c if fine else re.escape(c) if ord(c) >= 0x10000 else "\\u%04X" % ord(c))
+            escaping = False
+    return re.compile("".join(regex))
+
+
+def predicate_matches(f, value: Optional[str]) -> bool:
+    """DruidPredicateFactory.makeStringPredicate of the predicate filters: RegexFilter
+    (segment/filter/RegexFilter.java:44-48), SearchQueryFilter + SearchQuerySpec.accept
+    (query/search/ContainsSearchQuerySpec.java:63-72, FragmentSearchQuerySpec.java:79-103,
+    AllSearchQuerySpec), LikeMatcher.matches (LikeDimFilter.java:154-158), BoundFilter.doesMatch."""
+    import re
+    if isinstance(f, Q.RegexDimFilter):
+        return value is not None and re.search(f.pattern, value) is not None
+    if isinstance(f, Q.SearchQueryDimFilter):
+        q = f.query
+        t = q.get("type")
+        if t == "all":
+            return True
+        if value is None:
+            return False
+        if t == "contains" or t == "insensitive_contains":
+            if q.get("value") is None:
+                return False
+            if t == "contains" and q.get("caseSensitive", False):
+                return q["value"] in value
+            return _oracle_contains_ci(value, q["value"])
+        if t == "fragment":
+            if q.get("values") is None:
+                return False
+            target = sorted(set(q["values"]))
+            if q.get("caseSensitive", False):
+                return all(x in value for x in target)
+            return all(_oracle_contains_ci(value, x) for x in target)
+        if t == "regex":
+            return re.search(q["pattern"], value) is not None
+        raise NotImplementedError(t)
+    if isinstance(f, Q.LikeDimFilter):
+        return _oracle_like_regex(f.pattern, f.escape).fullmatch("" if value is None else value) is not None
+    if isinstance(f, Q.BoundDimFilter):
+        return _bound_matches(f, value)
+    raise TypeError(f)
 
 
 def filter_id_set(seg: OracleSegment, f) -> Optional[List[int]]:
@@ -531,9 +614,9 @@ def filter_id_set(seg: OracleSegment, f) -> Optional[List[int]]:
                 end = (found if f.upperStrict else found + 1) if found >= 0 else -(found + 1)
             end = max(start, end)
             return list(range(start, end))
-        if f.ordering != "numeric":
-            raise NotImplementedError(f"bound ordering {f.ordering}")
         return [i for i, v in enumerate(dictionary) if _bound_matches(f, v)]
+    if isinstance(f, Q.PREDICATE_FILTERS):  # Filters.matchPredicate: every dictionary value it accepts
+        return [i for i, v in enumerate(dictionary) if predicate_matches(f, v)]
     raise TypeError(f)
 
 
@@ -544,6 +627,8 @@ def _leaf_matches_null(f) -> bool:
         return any(Q._empty_to_null(v) is None for v in f.values)
     if isinstance(f, Q.BoundDimFilter):
         return _bound_matches(f, None)
+    if isinstance(f, Q.PREDICATE_FILTERS):
+        return predicate_matches(f, None)
     raise TypeError(f)
 
 
@@ -612,7 +697,13 @@ def aggregate_groups(seg: OracleSegment, aggs, rows: np.ndarray, groups: np.ndar
         st = np.zeros(max(ngroups, 1), dtype=_NP_STATE[a.output_type])
         lib().or_agg_init(a.kind, ngroups, st.ctypes.data)
         vals = _agg_input(seg, a)
-        lib().or_agg_apply(a.kind, len(rows), rows.ctypes.data, groups.ctypes.data,
+        r, g = rows, groups
+        if a.filter is not None:
+            # FilteredBufferAggregator.aggregate (FilteredBufferAggregator.java:45-50): the delegate
+            # sees a cursor row only when the filter's ValueMatcher matches it
+            keep = filter_mask(seg, a.filter)[rows]
+            r, g = np.ascontiguousarray(rows[keep]), np.ascontiguousarray(groups[keep])
+        lib().or_agg_apply(a.kind, len(r), r.ctypes.data, g.ctypes.data,
                            None if vals is None else vals.ctypes.data, st.ctypes.data)
         states.append(st[:ngroups])
     return states

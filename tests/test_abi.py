@@ -30,7 +30,7 @@ def test_abi_version_and_structs():
     assert N.lib().dg_abi_version() == 2
     # struct layouts the header fixes (LP64)
     assert ctypes.sizeof(N.dg_filter) == 64
-    assert ctypes.sizeof(N.dg_agg) == 16
+    assert ctypes.sizeof(N.dg_agg) == 32
     assert ctypes.sizeof(N.dg_scan) == 72
     assert ctypes.sizeof(N.dg_metrics) == 64
     assert ctypes.sizeof(N.dg_topn_lists) == 40

@@ -113,3 +113,31 @@ def test_java_priority_queue_layout_matches_oracle(O):
             if len(p) > 7:
                 assert p.poll() == o.poll()
             assert p.q == o.q
+
+
+def test_predicate_filters_product_vs_oracle(O, Q):
+    """regex / search (contains, insensitive_contains, fragment, regex, all) / like predicates and
+    alphanumeric / strlen bounds: the product's host predicates (incubator-druid_amd/query.py,
+    _native._bound_predicate) against the oracle's restatements, on tricky strings."""
+    N = importlib.import_module("incubator-druid_amd._native")
+    rng = random.Random(3)
+    vals = _random_strings(rng, 120) + ["abc", "ABC", "xAbCx", "a%b", "a_b", "10%", "ß", "SS", "ﬀ", "İi"]
+    filters = [
+        Q.RegexDimFilter("d", "^a"), Q.RegexDimFilter("d", "[0-9]{2}"), Q.RegexDimFilter("d", ""),
+        Q.SearchQueryDimFilter("d", {"type": "contains", "value": "ab", "caseSensitive": True}),
+        Q.SearchQueryDimFilter("d", {"type": "contains", "value": "ab"}),
+        Q.SearchQueryDimFilter("d", {"type": "insensitive_contains", "value": "ss"}),
+        Q.SearchQueryDimFilter("d", {"type": "fragment", "values": ["a", "B"], "caseSensitive": False}),
+        Q.SearchQueryDimFilter("d", {"type": "fragment", "values": ["1", "0"], "caseSensitive": True}),
+        Q.SearchQueryDimFilter("d", {"type": "regex", "pattern": "e$"}),
+        Q.SearchQueryDimFilter("d", {"type": "all"}),
+        Q.LikeDimFilter("d", "a%"), Q.LikeDimFilter("d", "%b_"), Q.LikeDimFilter("d", ""),
+        Q.LikeDimFilter("d", "1\\%", "\\"), Q.LikeDimFilter("d", "a.b"), Q.LikeDimFilter("d", "%ß%"),
+        Q.BoundDimFilter("d", "2", "11", False, True, "alphanumeric"),
+        Q.BoundDimFilter("d", None, "abc", False, False, "strlen"),
+        Q.BoundDimFilter("d", "", None, True, False, "alphanumeric"),
+    ]
+    for f in filters:
+        prod = f.predicate if not isinstance(f, Q.BoundDimFilter) else N._bound_predicate(f)
+        for v in vals:
+            assert bool(prod(v)) == bool(O.predicate_matches(f, v)), (f, v)
