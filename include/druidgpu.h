@@ -223,11 +223,15 @@ typedef struct {
   const char* previous_stop;  /* NULL = none; LEXICOGRAPHIC skips to it (computeStartEnd) */
   const int32_t* min_rank;    /* per segment: values need rank >= min_rank[i], i.e. after previousStop
                                  under the comparator (NULL = no previousStop) */
+  /* non-ALL granularity (scan->period_ms != 0): one result list per cursor (granularity bucket) */
+  int32_t bucket_cap;         /* list slots per segment (>= its bucket count) */
+  int64_t* out_bucket_time;   /* [n_segs * bucket_cap] bucket start of every list */
 } dg_topn;
 
-/* ALL granularity only. Per segment i: out_n[i] entries, ordered as TopNNumericResultBuilder.build()
- * (or, for a dimension order, TopNLexicographicResultBuilder.build()) returns them; entry j at index
- * i * threshold + j: dictionary id (segment-local) and n_aggs slots. */
+/* Per segment i and cursor b (b = 0 for ALL granularity, where bucket_cap counts as 1): list
+ * L = i * bucket_cap + b holds out_n[L] entries (-1: no cursor), ordered as
+ * TopNNumericResultBuilder.build() (or, for a dimension order, TopNLexicographicResultBuilder.build())
+ * returns them; entry j at index L * threshold + j: dictionary id (segment-local) and n_aggs slots. */
 int dg_topn_run(dg_segment* const* segs, int32_t n_segs, const dg_scan* scan, const dg_topn* topn,
                 int32_t* out_n, int32_t* out_ids, uint64_t* out_values, dg_metrics* metrics);
 

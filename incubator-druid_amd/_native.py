@@ -73,7 +73,7 @@ class dg_metrics(ctypes.Structure):
 class dg_topn(ctypes.Structure):
     _fields_ = [("dimension", ctypes.c_char_p), ("metric_agg", ctypes.c_int32), ("inverted", ctypes.c_int32),
                 ("threshold", ctypes.c_int32), ("dim_order", ctypes.c_int32), ("previous_stop", ctypes.c_char_p),
-                ("min_rank", ctypes.c_void_p)]
+                ("min_rank", ctypes.c_void_p), ("bucket_cap", ctypes.c_int32), ("out_bucket_time", ctypes.c_void_p)]
 
 
 class dg_topn_lists(ctypes.Structure):

@@ -1226,7 +1226,10 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   int rc = check_segments(segs, n, &ctx);
   if (rc) return rc;
   if (!q || !t || !t->dimension) return set_error(DG_ERR_ARG, "null argument");
-  if (q->period_ms != 0) return set_error(DG_ERR_UNSUPPORTED, "topN with non-ALL granularity");
+  // non-ALL granularity: one cursor (and result list) per bucket, TopNQueryEngine.java:80-104
+  const int bcap = q->period_ms ? t->bucket_cap : 1;
+  if (bcap <= 0) return set_error(DG_ERR_ARG, "bucket_cap");
+  if (q->period_ms && !t->out_bucket_time) return set_error(DG_ERR_ARG, "out_bucket_time");
   const bool dim = t->dim_order >= 0;
   if (dim && t->dim_order >= kOrderSlots) return set_error(DG_ERR_ARG, "order slot %d", t->dim_order);
   if (!dim && (t->metric_agg < 0 || t->metric_agg >= q->n_aggs)) return set_error(DG_ERR_ARG, "metric index");
@@ -1250,8 +1253,10 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
     cur[i] = plan_cursors(seg, q);
     m.segment_rows += seg->nrows;
-    out_n[i] = -1;
+    for (int b = 0; b < bcap; ++b) out_n[(int64_t)i * bcap + b] = -1;
     if (!cur[i].any) continue;
+    if (cur[i].nbuckets > bcap) return set_error(DG_ERR_ARG, "segment %d has %lld buckets > bucket_cap %d", i,
+                                                 (long long)cur[i].nbuckets, bcap);
     ScanJob& j = jobs[i];
     memset(&j, 0, sizeof j);
     Column* dc = seg->find(t->dimension);
@@ -1303,10 +1308,17 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   for (int i = 0; i < n; ++i) {
     bin_first[i] = (int32_t)bin_seg.size();
     if (!cur[i].any) continue;
-    jobs[i].nbuckets = (int32_t)card[i];
-    jobs[i].out = dev_take<uint64_t>(cs, (size_t)card[i] * rec);
+    // table keys: dictionary ids, or bucket * cardinality + id over granularity buckets
+    const int64_t nkeys = card[i] * (q->period_ms ? cur[i].nbuckets : 1);
+    if (nkeys > (1ll << 31) - 1 || (double)nkeys * rec * 8 > 16e9)
+      return set_error(DG_ERR_UNSUPPORTED, "topN table of %lld keys", (long long)nkeys);
+    jobs[i].nbuckets = (int32_t)nkeys;
+    jobs[i].key_card = q->period_ms ? (int32_t)card[i] : 0;
+    jobs[i].bucket0 = cur[i].bucket0;
+    jobs[i].period = q->period_ms;
+    jobs[i].out = dev_take<uint64_t>(cs, (size_t)nkeys * rec);
     if (!jobs[i].out) return set_error(DG_ERR_OOM, "topN table");
-    const int64_t nb = (card[i] + (1ll << shift) - 1) >> shift;
+    const int64_t nb = (nkeys + (1ll << shift) - 1) >> shift;
     for (int64_t k = 0; k < nb; ++k) bin_seg.push_back(i);
     cap += tiles_rows[i];
   }
@@ -1363,8 +1375,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   const int metric_agg = dim ? 0 : t->metric_agg;
   const int metric_op = (slot_op(mk) << 8) | mk;
   std::vector<TopnSelJob> sel;
-  std::vector<int> sel_seg;
-  std::vector<int64_t> gcap(n, 0), goff(n, 0);
+  std::vector<int> sel_seg, sel_bucket;  // one selection per (segment, bucket)
+  std::vector<int64_t> jgcap, jgoff, out_base;
   int64_t max_card = 0, gtotal = 0;
   // DimensionTopNMetricSpec: per segment the dictionary order, the computeStartEnd id range
   // (BaseTopNAlgorithm.java:296-326; only LEXICOGRAPHIC is optimized, DimensionTopNMetricSpec.java:117-124)
@@ -1407,25 +1419,32 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   const int sel_threshold = any_ties ? 0x3fffffff : t->threshold;
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
-    // candidates = ids whose key >= the K-th key: the threshold plus ties, rarely more
-    gcap[i] = std::min<int64_t>(card[i], 2 * (int64_t)t->threshold + 64);
-    if (any_ties) gcap[i] = card[i];
-    goff[i] = gtotal;
-    gtotal += gcap[i] * (rec + 1) + (gcap[i] + 3) / 4;  // records + u16 builder order
+    for (int64_t b = 0; b < (q->period_ms ? cur[i].nbuckets : 1); ++b) {
+      // candidates = ids whose key >= the K-th key: the threshold plus ties, rarely more
+      int64_t gc = std::min<int64_t>(card[i], 2 * (int64_t)t->threshold + 64);
+      if (any_ties) gc = card[i];
+      sel_seg.push_back(i);
+      sel_bucket.push_back((int)b);
+      out_base.push_back((int64_t)i * bcap + b);
+      if (q->period_ms) t->out_bucket_time[(int64_t)i * bcap + b] = cur[i].bucket0 + b * q->period_ms;
+      jgcap.push_back(gc);
+      jgoff.push_back(gtotal);
+      gtotal += gc * (rec + 1) + (gc + 3) / 4;  // records + u16 builder order
+    }
   }
-  // read-back block (one D2H copy): gathered records of every segment
+  // read-back block (one D2H copy): gathered records of every (segment, bucket)
   uint64_t* d_gath = dev_take<uint64_t>(cs, (size_t)std::max<int64_t>(gtotal, 1));
   if (!d_gath) return set_error(DG_ERR_OOM, "topN gather");
-  for (int i = 0; i < n; ++i) {
-    if (!cur[i].any) continue;
+  for (size_t k = 0; k < sel_seg.size(); ++k) {
+    const int i = sel_seg[k];
     TopnSelJob sj;
     memset(&sj, 0, sizeof sj);
-    sj.table = jobs[i].out;
+    sj.table = jobs[i].out + (size_t)sel_bucket[k] * (size_t)card[i] * rec;
     sj.card = card[i];
     sj.cand = dev_take<int32_t>(cs, (size_t)card[i]);
     sj.keys = dev_take<uint64_t>(cs, (size_t)card[i]);
     sj.blkcnt = dev_take<int32_t>(cs, (size_t)((card[i] + kSelBlock - 1) / kSelBlock));
-    sj.gather_cap = (int32_t)gcap[i];
+    sj.gather_cap = (int32_t)jgcap[k];
     if (dim) {
       sj.dim_mode = 1;
       sj.rank = dim_rank[i];
@@ -1433,12 +1452,11 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       sj.hi = dim_hi[i];
       sj.min_rank = t->min_rank ? t->min_rank[i] : 0;
     }
-    sj.gathered = d_gath + goff[i];
-    sj.order = reinterpret_cast<uint16_t*>(d_gath + goff[i] + gcap[i] * (rec + 1));
+    sj.gathered = d_gath + jgoff[k];
+    sj.order = reinterpret_cast<uint16_t*>(d_gath + jgoff[k] + jgcap[k] * (rec + 1));
     if (!sj.cand || !sj.keys || !sj.blkcnt) return set_error(DG_ERR_OOM, "topN candidates");
     max_card = std::max(max_card, card[i]);
     sel.push_back(sj);
-    sel_seg.push_back(i);
   }
   const int ns = (int)sel.size();
   // staged zero block: per selection state[4] | ncand (+pad) | hist[8][256] words
@@ -1477,13 +1495,12 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   ht.mark("synced");
   if (rc) return rc;
   for (int k = 0; k < ns; ++k) {  // unpack [id, rec slots] records into ids + rec-strided slots
-    const int i = sel_seg[k];
     h_ncand[k] = *reinterpret_cast<const int32_t*>(h_selmem + sel_words * k + 4);
-    const int64_t g = std::min<int64_t>(gcap[i], h_ncand[k]);
-    h_cand[k] = host_take<int32_t>(cs, (size_t)std::max<int64_t>(gcap[i], 1));
-    h_tab[k] = host_take<uint64_t>(cs, (size_t)std::max<int64_t>(gcap[i], 1) * rec);
+    const int64_t g = std::min<int64_t>(jgcap[k], h_ncand[k]);
+    h_cand[k] = host_take<int32_t>(cs, (size_t)std::max<int64_t>(jgcap[k], 1));
+    h_tab[k] = host_take<uint64_t>(cs, (size_t)std::max<int64_t>(jgcap[k], 1) * rec);
     if (!h_cand[k] || !h_tab[k]) return set_error(DG_ERR_OOM, "topN read-back");
-    const uint64_t* src = h_gath + goff[i];
+    const uint64_t* src = h_gath + jgoff[k];
     for (int64_t c = 0; c < g; ++c) {
       h_cand[k][c] = (int32_t)src[c * (rec + 1)];
       memcpy(h_tab[k] + c * rec, src + c * (rec + 1) + 1, 8 * (size_t)rec);
@@ -1493,9 +1510,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   // rare: more candidates than the speculative read-back held (many ties at the K-th key)
   bool again = false;
   for (int k = 0; k < ns; ++k) {
-    const int i = sel_seg[k];
     const int nc = h_ncand[k];
-    if (nc <= gcap[i]) continue;
+    if (nc <= jgcap[k]) continue;
     again = true;
     h_cand[k] = host_take<int32_t>(cs, (size_t)nc);
     h_tab[k] = host_take<uint64_t>(cs, (size_t)nc * rec);
@@ -1505,13 +1521,12 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   if (again) {
     DG_HIP(hipStreamSynchronize(st));
     for (int k = 0; k < ns; ++k) {
-      const int i = sel_seg[k];
       const int nc = h_ncand[k];
-      if (nc <= gcap[i]) continue;
+      if (nc <= jgcap[k]) continue;
       for (int c = 0; c < nc;) {  // candidates ascend: copy contiguous id runs
         int e = c + 1;
         while (e < nc && h_cand[k][e] == h_cand[k][e - 1] + 1) e++;
-        DG_HIP(hipMemcpyAsync(h_tab[k] + (size_t)c * rec, jobs[i].out + (size_t)h_cand[k][c] * rec,
+        DG_HIP(hipMemcpyAsync(h_tab[k] + (size_t)c * rec, sel[k].table + (size_t)h_cand[k][c] * rec,
                               (size_t)(e - c) * rec * 8, hipMemcpyDeviceToHost, st));
         c = e;
       }
@@ -1541,8 +1556,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       auto rank_of = [&](int c) { return hr ? hr[h_cand[k][c]] : 0; };
       std::vector<int> res;
       if (!dim_ties[i]) {  // distinct ranks: the K smallest, ascending
-        if (nc > 0 && nc <= gcap[i] && nc <= kTopnOrderCap) {
-          const uint16_t* ord = reinterpret_cast<const uint16_t*>(h_gath + goff[i] + gcap[i] * (rec + 1));
+        if (nc > 0 && nc <= jgcap[k] && nc <= kTopnOrderCap) {
+          const uint16_t* ord = reinterpret_cast<const uint16_t*>(h_gath + jgoff[k] + jgcap[k] * (rec + 1));
           for (int e = 0; e < std::min(nc, K); ++e) res.push_back(ord[e]);
         } else {
           res.resize(nc);
@@ -1588,19 +1603,19 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
         res = q;
         std::stable_sort(res.begin(), res.end(), [&](int a, int b) { return rank_of(a) < rank_of(b); });
       }
-      out_n[i] = (int32_t)res.size();
+      out_n[out_base[k]] = (int32_t)res.size();
       for (size_t e = 0; e < res.size(); ++e) {
-        const int64_t o = (int64_t)i * t->threshold + (int64_t)e;
+        const int64_t o = out_base[k] * t->threshold + (int64_t)e;
         out_ids[o] = h_cand[k][res[e]];
         for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[k][(size_t)res[e] * rec + 1 + a]);
       }
       continue;
     }
     std::vector<E> v;
-    if (nc > 0 && nc <= gcap[i] && nc <= kTopnOrderCap) {
+    if (nc > 0 && nc <= jgcap[k] && nc <= kTopnOrderCap) {
       // k_topn_order sorted the candidates by (key desc, id asc); keep every key > kth and, of the
       // kth ties, those the builder's queue keeps (see below), already in output order
-      const uint16_t* ord = reinterpret_cast<const uint16_t*>(h_gath + goff[i] + gcap[i] * (rec + 1));
+      const uint16_t* ord = reinterpret_cast<const uint16_t*>(h_gath + jgoff[k] + jgcap[k] * (rec + 1));
       auto key_at = [&](int c) { return metric_key_host(h_tab[k][(size_t)c * rec + 1 + t->metric_agg], mk, t->inverted); };
       const int r = std::min(nc, K) - 1;
       const uint64_t kth = key_at(ord[r]);
@@ -1618,9 +1633,9 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
           }
           v.push_back(E{0, h_cand[k][ord[e]], (int32_t)ord[e]});
         }
-        out_n[i] = (int32_t)v.size();
+        out_n[out_base[k]] = (int32_t)v.size();
         for (size_t e = 0; e < v.size(); ++e) {
-          const int64_t o = (int64_t)i * t->threshold + (int64_t)e;
+          const int64_t o = out_base[k] * t->threshold + (int64_t)e;
           out_ids[o] = v[e].id;
           for (int a = 0; a < na; ++a)
             out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[k][(size_t)v[e].idx * rec + 1 + a]);
@@ -1675,9 +1690,9 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       }
     }
     std::sort(v.begin(), v.end(), [](const E& a, const E& b) { return a.key != b.key ? a.key > b.key : a.id < b.id; });
-    out_n[i] = (int32_t)v.size();
+    out_n[out_base[k]] = (int32_t)v.size();
     for (size_t e = 0; e < v.size(); ++e) {
-      const int64_t o = (int64_t)i * t->threshold + (int64_t)e;
+      const int64_t o = out_base[k] * t->threshold + (int64_t)e;
       out_ids[o] = v[e].id;
       for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[k][(size_t)v[e].idx * rec + 1 + a]);
     }

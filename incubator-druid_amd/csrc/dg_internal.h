@@ -74,8 +74,8 @@ struct ScanJob {
   int64_t t_lo, t_hi;       // rows with t in [t_lo, t_hi)
   int64_t bucket0;          // start of the first bucket
   int64_t period;           // 0 = ALL (single bucket)
-  int32_t nbuckets;
-  int32_t pad;
+  int32_t nbuckets;         // timeseries: buckets; topN: table keys (cardinality, x buckets when key_card)
+  int32_t key_card;         // topN over granularity buckets: key = bucket * key_card + id (0: key = id)
   ColView vals[kMaxAggs];   // input column per aggregator
   const uint32_t* agg_bits[kMaxAggs];  // FilteredAggregatorFactory row matcher per aggregator (null: all rows)
   ColView key;              // topN: dimension ids

@@ -793,6 +793,23 @@ void launch_topn_part(const ScanJob* d_jobs, int njobs, int64_t max_card, AggPla
 constexpr int kBinThreads = 256;
 constexpr int kMaxTileBins = 4096;  // bins of one segment counted in LDS; above that, global atomics
 
+// topN over granularity buckets (one cursor per bucket, TopNQueryEngine.java:80-104): the table key of
+// a row is bucket * cardinality + dictionary id, so every bucket has its own per-id records
+__device__ __forceinline__ uint32_t row_key(const ScanJob& j, int64_t r, int64_t b) {
+  const uint32_t id = load_id(j.key, r);
+  return j.key_card ? (uint32_t)b * (uint32_t)j.key_card + id : id;
+}
+// keys of rows r .. r + 3 (r % 4 == 0); rows outside the interval get garbage keys and stay masked
+__device__ __forceinline__ void quad_keys(const ScanJob& j, int64_t r, uint32_t id[4]) {
+  load_ids4(j.key, r, id);
+  if (j.key_card) {
+    uint64_t t[4];
+    load_raw4(j.time, r, t);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) id[k] += (uint32_t)(((int64_t)t[k] - j.bucket0) / j.period) * (uint32_t)j.key_card;
+  }
+}
+
 __device__ __forceinline__ bool tile_rows(const ScanJob& j, int t, int64_t* r0, int64_t* r1) {
   *r0 = (int64_t)(t - j.tile_begin) * kTileRows;
   *r1 = min((int64_t)j.nrows, *r0 + kTileRows);
@@ -819,7 +836,7 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_bin_count(const ScanJob* _
     const unsigned m = quad_selected(j, r);
     if (!m) continue;
     uint32_t id[4];
-    load_ids4(j.key, r, id);
+    quad_keys(j, r, id);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if ((m >> k) & 1) atomicAdd(lds ? &s_cnt[id[k] >> shift] : &h[id[k] >> shift], 1u);
@@ -827,7 +844,10 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_bin_count(const ScanJob* _
   if (threadIdx.x == 0)
     for (int64_t r = full; r < r1; ++r) {
       int64_t b;
-      if (row_selected(j, r, &b)) atomicAdd(lds ? &s_cnt[load_id(j.key, r) >> shift] : &h[load_id(j.key, r) >> shift], 1u);
+      if (row_selected(j, r, &b)) {
+        const uint32_t key = row_key(j, r, b);
+        atomicAdd(lds ? &s_cnt[key >> shift] : &h[key >> shift], 1u);
+      }
     }
   __syncthreads();
   if (lds)
@@ -889,7 +909,7 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_bin_scatter(const ScanJob*
     for (int64_t r = r0 + threadIdx.x; r < r1; r += kBinThreads) {
       int64_t bb;
       if (!row_selected(j, r, &bb)) continue;
-      const uint32_t id = load_id(j.key, r);
+      const uint32_t id = row_key(j, r, bb);
       const uint32_t pos = atomicAdd(&cur[id >> shift], 1u);
       lid[pos] = (uint16_t)(id & lmask);
       for (int a = 0; a < na; ++a) vals[(size_t)a * cap + pos] = agg_in(j, plan, a, r);
@@ -907,13 +927,13 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_bin_scatter(const ScanJob*
     m[u] = 0;
     if (r < full) {
       m[u] = quad_selected(j, r);
-      if (m[u]) load_ids4(j.key, r, id[u]);
+      if (m[u]) quad_keys(j, r, id[u]);
     } else if (r < r1) {  // the segment's ragged last quad
       for (int k = 0; k < 4 && r + k < r1; ++k) {
         int64_t bb;
         if (row_selected(j, r + k, &bb)) {
           m[u] |= 1u << k;
-          id[u][k] = load_id(j.key, r + k);
+          id[u][k] = row_key(j, r + k, bb);
         }
       }
     }

@@ -150,6 +150,26 @@ def gather_topn(dist, query: Q.TopNQuery, raw: "R.TopNRaw", gdict: GlobalDiction
     dev = _device(dist)
     K = raw.K
     na = len(query.aggregations)
+    if not query.granularity.is_all:
+        # one list per (segment, cursor): ranks hold different cursor counts, so the lists travel as
+        # objects; rank 0 folds them per bucket (merge_topn) in global segment order
+        local = []
+        for s in range(len(raw.cnt) // raw.bcap):
+            res = []
+            for b in range(raw.bcap):
+                L = s * raw.bcap + b
+                c = int(raw.cnt[L])
+                if c < 0:
+                    continue
+                values = [gdict.values[int(g)] for g in translations[s][raw.ids[L * K:L * K + c]]]
+                slots = raw.vals.reshape(-1, max(na, 1))[L * K:L * K + c, :na]
+                res.append(Q.Result(int(raw.ts[L]), R._topn_entries(query, values, slots)))
+            local.append(res)
+        gathered: List = [None] * dist.get_world_size()
+        dist.all_gather_object(gathered, local)
+        if dist.get_rank() != 0:
+            return None
+        return R.merge_topn(query, [lst for g in gathered for lst in g])
     S = len(raw.cnt)
     cnt = raw.cnt.astype(np.int64)
     gids = np.full((S, K), -1, dtype=np.int64)

@@ -293,11 +293,13 @@ class _Rev:
 
 
 class TopNRaw:
-    """dg_topn_run output for segments of one device: per segment `cnt[i]` entries (-1 = no cursor),
-    entry j at i * K + j of `ids` (segment-local dictionary ids) and `vals` (n_aggs slots)."""
+    """dg_topn_run output for segments of one device: list L = i * bcap + b (segment i, cursor b; bcap = 1
+    for ALL granularity) has `cnt[L]` entries (-1 = no cursor), entry j at L * K + j of `ids`
+    (segment-local dictionary ids) and `vals` (n_aggs slots); `ts[L]` is the list's result timestamp."""
 
-    def __init__(self, segments, cnt, ids, vals, K, ts):
+    def __init__(self, segments, cnt, ids, vals, K, ts, bcap=1):
         self.segments, self.cnt, self.ids, self.vals, self.K, self.ts = segments, cnt, ids, vals, K, ts
+        self.bcap = bcap
 
 
 def _topn_struct(query: Q.TopNQuery, threshold: int, segments: Optional[Sequence[GpuSegment]] = None):
@@ -335,8 +337,7 @@ def _topn_struct(query: Q.TopNQuery, threshold: int, segments: Optional[Sequence
 
 
 def _check_topn(query: Q.TopNQuery):
-    if not query.granularity.is_all:
-        raise N.UnsupportedQuery(2, "topN with non-ALL granularity")
+    pass
 
 
 def topn_raw(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional[RunStats] = None) -> TopNRaw:
@@ -350,16 +351,23 @@ def topn_raw(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional
     scan, keep = N.make_scan(query, Q, segments=segments)
     t, keep_t = _topn_struct(query, K, segments)
     n = len(segments)
-    cnt = np.zeros(n, dtype=np.int32)
-    ids = np.zeros(n * K, dtype=np.int32)
-    vals = np.zeros(n * K * max(na, 1), dtype=np.uint64)
+    bcap = _bucket_cap(segments, query)
+    cnt = np.zeros(n * bcap, dtype=np.int32)
+    ids = np.zeros(n * bcap * K, dtype=np.int32)
+    vals = np.zeros(n * bcap * K * max(na, 1), dtype=np.uint64)
+    bt = np.zeros(n * bcap, dtype=np.int64)
+    t.bucket_cap = bcap
+    t.out_bucket_time = bt.ctypes.data
     m = N.dg_metrics()
     N.check(N.lib().dg_topn_run(_handles(segments), n, ctypes.byref(scan), ctypes.byref(t), cnt.ctypes.data,
                                 ids.ctypes.data, vals.ctypes.data, ctypes.byref(m)))
     if stats is not None:
         stats.add(m)
-    ts = np.array([max(query.interval[0], s.min_time) for s in segments], dtype=np.int64)
-    return TopNRaw(list(segments), cnt, ids, vals, K, ts)
+    if query.granularity.is_all:  # the cursor's time: start of the segment's part of the interval
+        ts = np.array([max(query.interval[0], s.min_time) for s in segments], dtype=np.int64)
+    else:
+        ts = bt
+    return TopNRaw(list(segments), cnt, ids, vals, K, ts, bcap)
 
 
 def topn_merge_raw(query: Q.TopNQuery, cnt: np.ndarray, keys: np.ndarray, vals: np.ndarray, K: int,
@@ -465,7 +473,7 @@ def run_topn(segments: Sequence[GpuSegment], query: Q.TopNQuery, stats: Optional
     """Per-segment topN on the GPU + TopNBinaryFn merge in the engine (one device); falls back to the
     Python merge when the segments span devices."""
     _check_topn(query)
-    if len(_group_by_device(segments)) != 1:
+    if len(_group_by_device(segments)) != 1 or not query.granularity.is_all:
         return merge_topn(query, topn_per_segment(segments, query, stats))
     if query.metric.type == "dimension":
         return _merge_topn_dimension(query, segments, topn_raw(segments, query, stats))
@@ -488,17 +496,19 @@ def topn_per_segment(segments: Sequence[GpuSegment], query: Q.TopNQuery,
     for _, idx in _group_by_device(segments).items():
         segs = [segments[i] for i in idx]
         raw = topn_raw(segs, query, stats)
-        K = raw.K
+        K, bcap = raw.K, raw.bcap
         for k, i in enumerate(idx):
-            if raw.cnt[k] < 0:  # no cursor: the segment does not overlap the interval
-                continue
             seg = segs[k]
-            dictionary = seg.dictionary(query.dimension)
-            c = int(raw.cnt[k])
-            ids = raw.ids[k * K:k * K + c]
-            values = [dictionary[x] if dictionary else None for x in ids]
-            slots = raw.vals.reshape(-1, max(na, 1))[k * K:k * K + c, :na]
-            out[i] = [Q.Result(int(raw.ts[k]), _topn_entries(query, values, slots))]
+            res = []
+            for b in range(bcap):
+                L = k * bcap + b
+                if raw.cnt[L] < 0:  # no cursor: the segment does not overlap the interval / bucket
+                    continue
+                c = int(raw.cnt[L])
+                values = [seg.dim_value(query.dimension, int(x)) for x in raw.ids[L * K:L * K + c]]
+                slots = raw.vals.reshape(-1, max(na, 1))[L * K:L * K + c, :na]
+                res.append(Q.Result(int(raw.ts[L]), _topn_entries(query, values, slots)))
+            out[i] = res
     return out
 
 

@@ -34,7 +34,7 @@ def test_abi_version_and_structs():
     assert ctypes.sizeof(N.dg_scan) == 72
     assert ctypes.sizeof(N.dg_metrics) == 64
     assert ctypes.sizeof(N.dg_topn_lists) == 40
-    assert ctypes.sizeof(N.dg_topn) == 40
+    assert ctypes.sizeof(N.dg_topn) == 56
 
 
 def test_gpu_kernels_are_gfx950_code_objects():

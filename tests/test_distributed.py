@@ -42,6 +42,8 @@ def _queries(Q):
                                           metric={"type": "dimension", "ordering": "numeric", "previousStop": "50"}),
         "topn_inverted_alnum": Q.TopNQuery(intervals=iv, dimension="dimSequential", threshold=4, aggregations=aggs[:2],
                                            metric={"type": "inverted", "metric": {"type": "alphaNumeric"}}),
+        "topn_minute": Q.TopNQuery(intervals=iv, granularity="minute", dimension="dimZipf", metric="sumLongSequential",
+                                   threshold=3, aggregations=aggs[1:3]),
         "groupby": Q.GroupByQuery(intervals=iv, dimensions=["dimZipf", "dimSequential"], aggregations=aggs[:4],
                                   filter=Q.InDimFilter("dimZipf", ["1", "2", "3"])),
     }
@@ -59,32 +61,34 @@ def _partial_from_oracle(R, np, query, rows):
 
 
 def _raw_from_oracle(R, np, O, query, segs):
-    """per-segment oracle topN lists in dg_topn_run's output layout (local ids, ABI value slots)"""
+    """per-segment oracle topN lists in dg_topn_run's output layout (list L = segment * bcap + cursor,
+    local ids, ABI value slots)"""
     K = query.segment_threshold
     na = len(query.aggregations)
-    cnt = np.full(len(segs), -1, dtype=np.int32)
-    ids = np.zeros(len(segs) * K, dtype=np.int32)
-    vals = np.zeros(len(segs) * K * na, dtype=np.uint64)
-    ts = np.zeros(len(segs), dtype=np.int64)
+    per = [O.topn_segment(s, query) for s in segs]
+    bcap = max([len(r) for r in per] + [1])
+    cnt = np.full(len(segs) * bcap, -1, dtype=np.int32)
+    ids = np.zeros(len(segs) * bcap * K, dtype=np.int32)
+    vals = np.zeros(len(segs) * bcap * K * na, dtype=np.uint64)
+    ts = np.zeros(len(segs) * bcap, dtype=np.int64)
     for i, s in enumerate(segs):
-        res = O.topn_segment(s, query)
-        if not res:
-            continue
-        ts[i] = res[0].timestamp
-        cnt[i] = len(res[0].value)
         index = {v: k for k, v in enumerate(s.dictionary(query.dimension))}
-        for j, e in enumerate(res[0].value):
-            ids[i * K + j] = index[e[query.dimension]]
-            for a_i, a in enumerate(query.aggregations):
-                v = e[a.name]
-                if a.output_type == "long":
-                    bits = np.int64(v).view(np.uint64)
-                elif a.output_type == "double":
-                    bits = np.float64(v).view(np.uint64)
-                else:
-                    bits = np.uint64(np.float32(v).view(np.uint32))
-                vals[(i * K + j) * na + a_i] = bits
-    return R.TopNRaw(None, cnt, ids, vals, K, ts)
+        for b, res in enumerate(per[i]):
+            L = i * bcap + b
+            ts[L] = res.timestamp
+            cnt[L] = len(res.value)
+            for j, e in enumerate(res.value):
+                ids[L * K + j] = index[e[query.dimension]]
+                for a_i, a in enumerate(query.aggregations):
+                    v = e[a.name]
+                    if a.output_type == "long":
+                        bits = np.int64(v).view(np.uint64)
+                    elif a.output_type == "double":
+                        bits = np.float64(v).view(np.uint64)
+                    else:
+                        bits = np.uint64(np.float32(v).view(np.uint32))
+                    vals[(L * K + j) * na + a_i] = bits
+    return R.TopNRaw(None, cnt, ids, vals, K, ts, bcap)
 
 
 def _worker(rank, port, paths, out_dir):

@@ -120,3 +120,23 @@ def test_numeric_sort_bench_shape(R, Q, basic):
         got = R.run_query(q, g)[0].value
         present = sorted({int(v) for s in g for v in s.dictionary("dimUniform") if v is not None})
         assert [int(e["dimUniform"]) for e in got] == present[:10]
+
+
+@pytest.mark.parametrize("gran", ["minute", {"type": "duration", "duration": 100_000}, "second"])
+def test_topn_granularity_buckets(R, Q, O, basic, gran):
+    """One cursor per granularity bucket (TopNQueryEngine.java:80-104): per-(segment, bucket) lists,
+    empty buckets included, merged per bucket; metric and dimension orders, filters, partial
+    intervals."""
+    g, o = basic[("concise", "lz4")]
+    specs = ["ds", {"type": "inverted", "metric": {"type": "numeric", "metric": "ls"}}, _spec("numeric", "5", False),
+             _spec("lexicographic", None, True)]
+    for spec, dim, iv, flt in ((specs[0], "dimZipf", ALL, None),
+                               (specs[1], "dimSequential", ["1970-01-01T00:01:30Z/1970-01-01T00:09:10Z"], None),
+                               (specs[2], "dimUniform", ALL, Q.InDimFilter("dimZipf", ["1", "2"])),
+                               (specs[3], "dimSequentialHalfNull", ALL, None),
+                               (specs[0], "missingDim", ALL, None)):
+        if gran == "second" and dim != "dimZipf":
+            continue  # 1000 one-second buckets per segment: one case is enough
+        q = Q.TopNQuery(intervals=iv, granularity=gran, dimension=dim, metric=spec, threshold=4,
+                        aggregations=_aggs(Q), filter=flt, context={"minTopNThreshold": 20})
+        assert_results(q, R.run_query(q, g), O.run(q, o))
