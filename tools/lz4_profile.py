@@ -22,12 +22,16 @@ PHASES = ["stage", "parse+scan", "fill", "coop", "jump", "output"]
 
 def payloads(rng, k):
     n8 = BLOCK // 8
-    out = {"seqlong": [], "time": [], "normal": [], "uniform3": []}
+    out = {"seqlong": [], "time": [], "normal": [], "uniform3": [], "ulong500": [], "zipfdbl": []}
     for i in range(k):
         seq = np.arange(i * n8, (i + 1) * n8, dtype=np.int64)
         out["seqlong"].append((seq % 10000).astype("<i8").tobytes())
         out["time"].append(np.round(seq * 1.3333).astype("<i8").tobytes())
         out["normal"].append(rng.normal(5000, 1, n8).astype("<f8").tobytes())
+        out["ulong500"].append(rng.integers(0, 501, n8).astype("<i8").tobytes())
+        zk = np.arange(1, 1001, dtype=np.float64)
+        zp = 1.0 / zk
+        out["zipfdbl"].append(rng.choice(zk - 1, size=n8, p=zp / zp.sum()).astype("<f8").tobytes())
         ids = rng.integers(1, 100001, BLOCK // 3 + 1).astype("<u4").view(np.uint8).reshape(-1, 4)[:, :3]
         out["uniform3"].append(ids.tobytes()[:3 * 16384])
     return out
