@@ -188,20 +188,6 @@ __device__ __forceinline__ void put_ptr(const LzState& S, int x, int src) {
   else S.tsrc[x - kTail] = (uint16_t)src;
 }
 
-// E entries of [x, end) for positions below kTail, two per dword store where aligned (x even ->
-// eph(x) even: a pair never straddles a skew gap). val(k) = entry of position x0 + k.
-template <class F>
-__device__ __forceinline__ void put_run(const LzState& S, int x0, int end, F val) {
-  int x = x0;
-  if (x < end && (x & 1)) {
-    S.e[eph(x)] = (uint16_t)val(0);
-    x++;
-  }
-  uint32_t* e32 = reinterpret_cast<uint32_t*>(S.e);
-  for (; x + 1 < end; x += 2) e32[eph(x) >> 1] = val(x - x0) | (val(x + 1 - x0) << 16);
-  if (x < end) S.e[eph(x)] = (uint16_t)val(x - x0);
-}
-
 // value of output byte x once E and the tail table have converged (both hold literal codes)
 __device__ __forceinline__ uint32_t lz_value(const LzState& S, int x) {
   if (x < kTail) return S.e[eph(x)] & 0xFF;
@@ -297,16 +283,9 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         const int d = (int)(r_DM[s] & 0xFFFF), M = (int)(r_DM[s] >> 16);
         if (L <= kShortLit) {
           const uint32_t lv = r_lv[s];
-#ifndef DG_LZ_BYTEFILL
-          if (o + L <= kTail) {
-            put_run(S, o, o + L, [&](int k) { return 0xFF00u | ((lv >> (8 * k)) & 0xFF); });
-          } else
-#endif
-          {
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-              if (k < L) put_lit(S, o + k, (lv >> (8 * k)) & 0xFF);
-          }
+          for (int k = 0; k < 4; ++k)
+            if (k < L) put_lit(S, o + k, (lv >> (8 * k)) & 0xFF);
         } else {
           const int j = atomicAdd(&s_njob, 1);
           if (j < kMaxJobs) {
@@ -324,11 +303,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
             if (j < kMaxJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(M - 1) << 16), (uint32_t)d | 0x80000000u);
           }
           if (j >= kMaxJobs) {
-#ifndef DG_LZ_BYTEFILL
-            if (d >= M && o + M <= kTail) {
-              put_run(S, o, o + M, [&](int) { return (uint32_t)d; });
-            } else
-#endif
             if (d >= M) {
               for (int k = 0; k < M; ++k) put_ptr(S, o + k, o + k - d);
             } else {
