@@ -605,6 +605,13 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
 static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr) {
   if (db->jobs.empty()) return DG_OK;
   const int n = (int)db->jobs.size();
+  // longest blocks first (token-dense blocks cost the most; workgroups dispatch in order, so this
+  // is greedy LPT scheduling of the blocks over the CUs and shortens the ragged last wave). Only for
+  // a few waves of blocks: with hundreds of waves the tail is noise and the host sort is not.
+#ifndef DG_NO_LPT
+  if (n <= 16 * 256)
+    std::stable_sort(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; });
+#endif
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
   int32_t* d_err = call_err(cs, st);
