@@ -42,6 +42,7 @@ constexpr int kMaxJobs = 2048;
 constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
 constexpr int kJumpBatch = 8;                 // steps of a jump sweep whose reads are issued together
 constexpr int kMaxRounds = 20;                 // > log2(65536) + 1: pointer jumping always converges before
+constexpr int kClass = 8;                      // the value width whose distance-8 copy chains are scanned
 static_assert(kLz4InCap + 32 <= kBlockBytes * 2, "staged input must fit in the E array");
 static_assert(kLzThreads * kLzSeqPerCp >= kBlockBytes / 4, "a block can hold 16384 sequences");
 
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   __shared__ uint32_t s_tlit[kTailN / 32];
   __shared__ uint2 s_job[kMaxJobs];
   __shared__ int s_jpre[kMaxJobs];
-  __shared__ int s_njob, s_bad;
+  __shared__ int s_njob, s_bad, s_c8;
   __shared__ int s_tmp[kLzWaves];
 
   const Lz4Job job = jobs[blockIdx.x];
@@ -235,6 +236,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       dst[n16] = make_uint4(0, 0, 0, 0);
       s_njob = 0;
       s_bad = 0;
+      s_c8 = 0;
     }
     if (tid < kTailN / 32) s_tlit[tid] = 0;
   }
@@ -274,6 +276,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   // ---- 2. E entries: short literals from registers, short matches as distances; longer runs
   // become jobs for the cooperative pass (their literals come from the compressed block in HBM) ----
   const uint8_t* __restrict__ gin = job.src;
+  int c8 = 0;  // my match bytes at distance 8 (class chains of 8-byte values, resolved by a scan below)
   if (tid < ncp) {
     int o = base;
 #pragma unroll
@@ -297,13 +300,14 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         o += L;
         if (M > 0) {
           if (d > o) s_bad = 1;
+          c8 += d == 8 ? M : 0;
           int j = kMaxJobs;
           if (M > kLongFill) {
             j = atomicAdd(&s_njob, 1);
             if (j < kMaxJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(M - 1) << 16), (uint32_t)d | 0x80000000u);
           }
           if (j >= kMaxJobs) {
-            if (d >= M) {
+            if (d >= M || d == kClass) {  // distance 8: plain x - 8 (same value, same class chain)
               for (int k = 0; k < M; ++k) put_ptr(S, o + k, o + k - d);
             } else {
               int r = 0;
@@ -318,6 +322,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       }
     }
   }
+  if (c8) atomicAdd(&s_c8, c8);
   __syncthreads();
   LZ_STAMP(3);
   // ---- cooperative pass: the jobs' bytes as one flat range, split evenly over the threads ----
@@ -360,7 +365,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
             xs[u] = o + k;
             if (jb.y & 0x80000000u) {
               const int d = (int)(jb.y & 0xFFFF);
-              srcs[u] = d >= job_len(jb) ? o + k - d : o - d + k % d;
+              srcs[u] = (d >= job_len(jb) || d == kClass) ? o + k - d : o - d + k % d;
             } else {
               srcs[u] = -1 - ((int)jb.y + k);  // literal: input offset, encoded negative
             }
@@ -393,6 +398,68 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   if (lim < kTail) {
     for (int x = lim + tid; x < kTail; x += kLzThreads) s_e[eph(x)] = 0xFF00;
   }
+#ifndef DG_LZ_NOSCAN8
+  // ---- 2b. class chains: a byte copied from 8 back holds the value of the last "terminal" (a
+  // literal, or a byte of a match at another distance) of its residue class mod 8 before it. A
+  // carry scan over the block turns every distance-8 entry into the distance to that terminal, so
+  // the jumping below only has to chase the few other matches (8-byte value columns: sequential
+  // longs and timestamps are ~99.5 % distance-8 matches chaining through the whole block). ----
+  if (s_c8 * 4 > total) {
+    __syncthreads();
+    const int x0 = tid * 64;
+    // my 64 entries as pairs (read twice: keeping them in registers spills); positions >= lim read
+    // as literals
+    auto pair_at = [&](int q) { return x0 + 2 * q < lim ? s_e32[eph(x0 + 2 * q) >> 1] : 0xFF00FF00u; };
+    int last[kClass];
+#pragma unroll
+    for (int c = 0; c < kClass; ++c) last[c] = -1;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int c = (2 * q) & 7;
+      const uint32_t v = pair_at(q);
+      if ((v & 0xFFFF) != (uint32_t)kClass) last[c] = x0 + 2 * q;
+      if ((v >> 16) != (uint32_t)kClass) last[c + 1] = x0 + 2 * q + 1;
+    }
+    // exclusive max-scan of the per-class last terminal over the threads (positions grow with tid)
+    const int lane = tid & 63, wave = tid >> 6;
+    int carry[kClass];
+    int* s_scan = s_jpre;  // free after the cooperative pass: [kLzWaves][kClass]
+#pragma unroll
+    for (int c = 0; c < kClass; ++c) {
+      int v = last[c];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o, 64);
+        if (lane >= o) v = max(v, y);
+      }
+      const int ex = __shfl_up(v, 1, 64);
+      carry[c] = lane ? ex : -1;
+      if (lane == 63) s_scan[wave * kClass + c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < kClass; ++c)
+      for (int w = 0; w < wave; ++w) carry[c] = max(carry[c], s_scan[w * kClass + c]);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int c = (2 * q) & 7, x = x0 + 2 * q;
+      const uint32_t v = pair_at(q);
+      uint32_t lo = v & 0xFFFF, hi = v >> 16;
+      if (lo == (uint32_t)kClass) {
+        if (carry[c] >= 0) lo = (uint32_t)(x - carry[c]);
+      } else {
+        carry[c] = x;
+      }
+      if (hi == (uint32_t)kClass) {
+        if (carry[c + 1] >= 0) hi = (uint32_t)(x + 1 - carry[c + 1]);
+      } else {
+        carry[c + 1] = x + 1;
+      }
+      const uint32_t nv = lo | (hi << 16);
+      if (nv != v && x < lim) s_e32[eph(x) >> 1] = nv;
+    }
+  }
+#endif
   bool any = true;
   int jump_rounds = 0;
   // Rounds of jumping. Wave w sweeps its own 4 KiB of positions in increasing order, 64 pairs per
