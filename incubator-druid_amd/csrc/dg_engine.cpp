@@ -555,6 +555,9 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
 // ------------------------------------------------------------------------------------------------
 struct DecodeBatch {
   std::vector<Lz4Job> jobs;
+  std::vector<VsJob> expands;  // DELTA / TABLE blocks, expanded after the LZ4 decodes
+  int32_t expand_rows = 0;     // largest block of `expands` (grid width)
+  int64_t* last_expanded = nullptr;
   int64_t bytes = 0;  // algorithmic bytes read
 };
 
@@ -580,30 +583,72 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
   else if (c->type == DG_COL_FLOAT) v->kind = VIEW_FLOAT;
   else v->kind = VIEW_IDS;
   db->bytes += b.stored_bytes + b.index_bytes;
+  if (b.codec != CODEC_LZ4 && b.codec != CODEC_UNCOMPRESSED && b.codec != CODEC_NONE)
+    return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, c->name.c_str());
+  uint8_t* slots = nullptr;
   if (b.codec == CODEC_LZ4) {
-    uint8_t* slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
-    const uint8_t** d_ptrs;
-    const uint8_t** h_ptrs = up_take<const uint8_t*>(cs, std::max(b.nblocks, 1), &d_ptrs, st);
-    if (!slots || !h_ptrs || !d_ptrs) return set_error(DG_ERR_OOM, "decode scratch");
-    for (int32_t k = 0; k < b.nblocks; ++k) {
-      uint8_t* dst = slots + (size_t)k * kBlockBytes;
-      h_ptrs[k] = dst;
-      int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
-      if (rows <= 0) continue;
-      db->jobs.push_back(lz4_job(b, k, dst, (int32_t)(rows * b.width)));
-    }
-    v->blocks = d_ptrs;
-    return DG_OK;
+    slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
+    if (!slots) return set_error(DG_ERR_OOM, "decode scratch");
   }
-  if (b.codec == CODEC_UNCOMPRESSED || b.codec == CODEC_NONE) {
+  int64_t* expanded = nullptr;
+  if (b.vbits) {
+    expanded = dev_take<int64_t>(cs, (size_t)b.nblocks * b.size_per + 8);
+    if (!expanded) return set_error(DG_ERR_OOM, "expand scratch");
+    db->last_expanded = expanded;
+  }
+  if (!slots && !expanded) {
     v->blocks = b.block_ptrs.as<const uint8_t*>();
     return DG_OK;
   }
-  return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, c->name.c_str());
+  const uint8_t** d_ptrs;
+  const uint8_t** h_ptrs = up_take<const uint8_t*>(cs, std::max(b.nblocks, 1), &d_ptrs, st);
+  if (!h_ptrs || !d_ptrs) return set_error(DG_ERR_OOM, "decode scratch");
+  for (int32_t k = 0; k < b.nblocks; ++k) {
+    const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
+    // the packed (or plain) bytes of block k: an LZ4 slot, an uncompressed slot or a NONE range
+    const uint8_t* src;
+    if (slots) src = slots + (size_t)k * kBlockBytes;
+    else if (b.codec == CODEC_UNCOMPRESSED) src = b.raw.as<uint8_t>() + (size_t)k * kBlockBytes;
+    else src = b.raw.as<uint8_t>() + (size_t)k * (size_t)b.size_per * b.vbits / 8;
+    h_ptrs[k] = expanded ? reinterpret_cast<const uint8_t*>(expanded + (size_t)k * b.size_per) : src;
+    if (rows <= 0) continue;
+    if (slots) {
+      const int64_t expect = b.vbits ? (b.vbits * rows + 7) / 8 : rows * b.width;
+      db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect));
+    }
+    if (expanded) {
+      VsJob e;
+      e.src = src;
+      e.dst = expanded + (size_t)k * b.size_per;
+      e.table = b.table.p ? b.table.as<int64_t>() : nullptr;
+      e.base = b.delta_base;
+      e.rows = (int32_t)rows;
+      e.bits = b.vbits;
+      e.table_n = b.table_n;
+      e.pad = 0;
+      db->expands.push_back(e);
+      db->expand_rows = std::max(db->expand_rows, (int32_t)rows);
+    }
+  }
+  v->blocks = d_ptrs;
+  return DG_OK;
+}
+
+static int run_expands(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
+  if (db->expands.empty()) return DG_OK;
+  const int n = (int)db->expands.size();
+  VsJob* d;
+  VsJob* h = up_take<VsJob>(cs, n, &d, st);
+  int32_t* d_err = call_err(cs, st);
+  if (!h || !d_err) return set_error(DG_ERR_OOM, "expand jobs");
+  memcpy(h, db->expands.data(), sizeof(VsJob) * n);
+  DG_FLUSH(cs, st);
+  launch_vsize_expand(d, n, db->expand_rows, d_err, st);
+  return DG_OK;
 }
 
 static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr) {
-  if (db->jobs.empty()) return DG_OK;
+  if (db->jobs.empty()) return run_expands(cs, db, st);
   const int n = (int)db->jobs.size();
   // longest blocks first (token-dense blocks cost the most; workgroups dispatch in order, so this
   // is greedy LPT scheduling of the blocks over the CUs and shortens the ragged last wave). Only for
@@ -619,7 +664,7 @@ static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
   launch_lz4_decode(d, n, d_err, st, d_prof);
-  return DG_OK;  // errors surface at finish_call
+  return run_expands(cs, db, st);  // errors surface at finish_call
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -817,7 +862,14 @@ int read_time_bounds(Segment* seg) {
   hipStream_t st = ctx->stream;
   const BlockColumn& b = t->data;
   int64_t* h = host_take<int64_t>(cs, 2);
-  if (b.codec == CODEC_LZ4) {
+  if (b.vbits) {
+    // DELTA / TABLE __time: expand the column once and read its first and last row
+    int rc0 = column_view(t, cs, &db, &v, st);
+    if (!rc0) rc0 = run_decodes(cs, &db, st);
+    if (rc0) return rc0;
+    DG_HIP(hipMemcpyAsync(h, db.last_expanded, 8, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h + 1, db.last_expanded + (seg->nrows - 1), 8, hipMemcpyDeviceToHost, st));
+  } else if (b.codec == CODEC_LZ4) {
     // decode only the first and last block
     uint8_t* slots = dev_take<uint8_t>(cs, 2 * (size_t)kBlockBytes + 64);
     int32_t last = (int32_t)((seg->nrows - 1) >> b.log2_per);

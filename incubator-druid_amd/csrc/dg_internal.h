@@ -55,6 +55,20 @@ struct Lz4Job {
   int32_t dec_len;     // decoded length found at attach
 };
 
+// Expansion of one block of a DELTA / TABLE long column (CompressionFactory.LongEncodingFormat,
+// CompressionFactory.java:153-188): `rows` values of `bits` bits packed MSB-first
+// (VSizeLongSerde deserializers, VSizeLongSerde.java:416-657) -> little-endian int64 at dst.
+struct VsJob {
+  const uint8_t* src;   // packed block (decoded LZ4 slot, uncompressed block or NONE range)
+  int64_t* dst;         // size_per int64 slots
+  const int64_t* table; // TABLE: table values; DELTA: nullptr
+  int64_t base;         // DELTA: base (DeltaLongEncodingReader.read, :63-66)
+  int32_t rows;
+  int32_t bits;
+  int32_t table_n;
+  int32_t pad;
+};
+
 // Host-side validating parse of one LZ4 block (lz4-java safe-decompressor semantics): appends the
 // block's checkpoints to *cps and returns the decoded length, or -1 for a malformed block.
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps);
@@ -129,6 +143,12 @@ struct BlockColumn {
   int32_t codec = 0;
   int32_t nblocks = 0;
   int32_t big_endian = 0;  // VSizeColumnarInts ids (uncompressed dimension)
+  // DELTA / TABLE long encodings: blocks hold `vbits`-bit packed values (0 = plain LONGS);
+  // `width` stays 8, the width of the expanded view the kernels read
+  int32_t vbits = 0;
+  int32_t table_n = 0;
+  int64_t delta_base = 0;
+  DevBuf table;                        // TABLE: int64[table_n]
   int64_t stored_bytes = 0;            // on-HBM bytes of all blocks (algorithmic bytes of a full scan)
   std::vector<int64_t> comp_off;       // host copy: offset of block b inside comp
   std::vector<int32_t> comp_len;
@@ -217,6 +237,9 @@ int load_segment(Context* ctx, const char* dir, Segment** out);
 // kernel launchers (dg_kernels.hip)
 constexpr int kLz4ProfWords = 12;  // per-block phase stamps of the decoder (diagnostic builds of the call)
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
+// VSizeLongSerde.getSerializedSize (VSizeLongSerde.java:61-65)
+inline int64_t vsize_serialized(int bits, int64_t n) { return (bits * n + 7) / 8 + 4; }
 void launch_concise_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
                        int nbitmaps, uint32_t* const* d_sets, int64_t limit_bits, hipStream_t s);
 void launch_roaring_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,

@@ -1468,4 +1468,68 @@ void launch_groupby_compact(const uint64_t* keys, const uint64_t* slots, uint64_
                      d_count);
 }
 
+// ------------------------------------------------------------------------------------------------
+// DELTA / TABLE long blocks -> int64 (CompressionFactory.LongEncodingFormat, CompressionFactory.java:153-188)
+// Values are packed MSB-first at `bits` bits (VSizeLongSerde.java:416-657: Size1Des..Size64Des all read
+// the same big-endian bit stream). One 256-thread workgroup expands a chunk of 2048 rows: the chunk's
+// 256 * bits packed bytes are staged into LDS with coalesced dword loads, every thread then cuts its
+// values out of a 96-bit big-endian window and stores int64 rows with consecutive lanes on
+// consecutive rows. DELTA adds the base (DeltaLongEncodingReader.read, :63-66); TABLE looks the id up
+// in the LDS copy of the table (TableLongEncodingReader.read, :69-72; an id past the table is a
+// malformed segment -> error word).
+// ------------------------------------------------------------------------------------------------
+constexpr int kVsRows = 2048;
+
+__global__ __launch_bounds__(256) void k_vsize_expand(const VsJob* __restrict__ jobs, int32_t* __restrict__ err) {
+  __shared__ uint32_t lds[kVsRows * 64 / 32 + 4];
+  __shared__ int64_t tab[256];
+  const VsJob j = jobs[blockIdx.y];
+  const int64_t r0 = (int64_t)blockIdx.x * kVsRows;
+  if (r0 >= j.rows) return;
+  const int n = (int)min<int64_t>(kVsRows, j.rows - r0);
+  const int bits = j.bits;
+  const int tid = threadIdx.x;
+  // chunk start is r0 * bits / 8 = blockIdx.x * 256 * bits bytes: dword aligned
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(j.src + (size_t)blockIdx.x * 256 * bits);
+  const int nbytes = (n * bits + 7) >> 3;  // packed bytes of this chunk (the 4 closing bytes follow)
+  const int ndw = (nbytes + 3) >> 2;
+  for (int q = tid; q < ndw; q += 256) lds[q] = src[q];
+  if (tid < 4) lds[ndw + tid] = 0;
+  const bool is_table = j.table != nullptr;
+  if (is_table)
+    for (int t = tid; t < j.table_n; t += 256) tab[t] = j.table[t];
+  __syncthreads();
+  int64_t* dst = j.dst + r0;
+  bool bad = false;
+  for (int i = tid; i < n; i += 256) {
+    const int64_t o = (int64_t)i * bits;
+    const int byte = (int)(o >> 3);
+    const int q = byte >> 2;
+    const int start = ((byte & 3) << 3) + (int)(o & 7);  // <= 31
+    const uint64_t hi = ((uint64_t)__builtin_bswap32(lds[q]) << 32) | __builtin_bswap32(lds[q + 1]);
+    const uint32_t lo = __builtin_bswap32(lds[q + 2]);
+    const unsigned __int128 w = (((unsigned __int128)hi << 32) | lo) << (32 + start);
+    const uint64_t v = (uint64_t)(w >> (128 - bits));
+    int64_t out;
+    if (is_table) {
+      if (v >= (uint64_t)j.table_n) {
+        bad = true;
+        out = 0;
+      } else {
+        out = tab[v];
+      }
+    } else {
+      out = (int64_t)((uint64_t)j.base + v);
+    }
+    dst[i] = out;
+  }
+  if (bad) atomicOr(err, 1);
+}
+
+void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s) {
+  if (njobs <= 0 || max_rows <= 0) return;
+  const unsigned gx = (unsigned)((max_rows + kVsRows - 1) / kVsRows);
+  hipLaunchKernelGGL(k_vsize_expand, dim3(gx, (unsigned)njobs), dim3(256), 0, s, d_jobs, d_err);
+}
+
 }  // namespace dg

@@ -258,6 +258,82 @@ int upload_flat(BlockColumn* col, const uint8_t* p, const uint8_t* end) {
   return DG_OK;
 }
 
+// DELTA / TABLE encoding metadata (CompressionFactory.LongEncodingFormat.getReader, :153-188):
+// DELTA = [u8 version 1][i64 base][i32 bitsPerValue] (DeltaLongEncodingReader.java:34-46);
+// TABLE = [u8 version 1][i32 size <= 256][size x i64] with bits = getBitsForMax(size)
+// (TableLongEncodingReader.java:33-52). All big-endian.
+static int bits_for_max(int64_t value) {  // VSizeLongSerde.getBitsForMax (:41-59)
+  static const int sizes[] = {1, 2, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64};
+  int nbits = 0;
+  int64_t max_value = 1;
+  for (int sz : sizes) {
+    while (nbits < sz && max_value < INT64_MAX / 2) {
+      nbits++;
+      max_value *= 2;
+    }
+    if (value <= max_value || max_value >= INT64_MAX / 2) return sz;
+  }
+  return 64;
+}
+
+static bool supported_bits(int b) {
+  switch (b) {
+    case 1: case 2: case 4: case 8: case 12: case 16: case 20: case 24: case 32: case 40: case 48: case 56: case 64:
+      return true;
+    default:
+      return false;
+  }
+}
+
+int parse_long_encoding(Column* c, uint8_t enc, Slice* s) {
+  BlockColumn& col = c->data;
+  if (enc == 0x00) {  // DELTA
+    if (s->left() < 13) return set_error(DG_ERR_FORMAT, "%s: truncated DELTA header", c->name.c_str());
+    if (s->p[0] != 0x01) return set_error(DG_ERR_FORMAT, "%s: DELTA version %d", c->name.c_str(), s->p[0]);
+    col.delta_base = (int64_t)be64(s->p + 1);
+    col.vbits = be32(s->p + 9);
+    s->p += 13;
+    if (!supported_bits(col.vbits)) return set_error(DG_ERR_FORMAT, "%s: unsupported size %d", c->name.c_str(), col.vbits);
+    return DG_OK;
+  }
+  if (enc == 0x01) {  // TABLE
+    if (s->left() < 5) return set_error(DG_ERR_FORMAT, "%s: truncated TABLE header", c->name.c_str());
+    if (s->p[0] != 0x01) return set_error(DG_ERR_FORMAT, "%s: TABLE version %d", c->name.c_str(), s->p[0]);
+    const int32_t n = be32(s->p + 1);
+    if (n < 0 || n > 256) return set_error(DG_ERR_FORMAT, "%s: Invalid table size[%d]", c->name.c_str(), n);
+    s->p += 5;
+    if (s->left() < (int64_t)n * 8) return set_error(DG_ERR_FORMAT, "%s: truncated table", c->name.c_str());
+    std::vector<int64_t> t(n > 0 ? n : 1, 0);
+    for (int32_t i = 0; i < n; ++i) t[i] = (int64_t)be64(s->p + 8 * i);
+    s->p += (size_t)n * 8;
+    col.table_n = n;
+    col.vbits = bits_for_max(n);
+    if (!col.table.alloc(t.size() * 8)) return set_error(DG_ERR_OOM, "hipMalloc table");
+    DG_HIP(hipMemcpy(col.table.p, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+    return DG_OK;
+  }
+  return set_error(DG_ERR_FORMAT, "%s: unknown long encoding %d", c->name.c_str(), enc);
+}
+
+// NONE layout of a packed column (EntireLayoutColumnarLongsSupplier over a Delta/Table reader): one
+// packed stream of `total` values; addressed as virtual blocks of 8192 rows (8192 * bits / 8 bytes)
+int upload_flat_packed(BlockColumn* col, const uint8_t* p, const uint8_t* end) {
+  const int64_t bytes = vsize_serialized(col->vbits, col->total);
+  if (bytes > end - p) return set_error(DG_ERR_FORMAT, "truncated NONE column");
+  if (!col->raw.alloc((size_t)bytes + 16)) return set_error(DG_ERR_OOM, "hipMalloc %lld", (long long)bytes);
+  DG_HIP(hipMemcpy(col->raw.p, p, (size_t)bytes, hipMemcpyHostToDevice));
+  col->stored_bytes = bytes;
+  col->log2_per = 13;
+  col->size_per = 1 << 13;
+  col->nblocks = (int32_t)((col->total + col->size_per - 1) / col->size_per);
+  std::vector<const uint8_t*> ptrs(col->nblocks > 0 ? col->nblocks : 1);
+  for (int32_t b = 0; b < col->nblocks; ++b)
+    ptrs[b] = col->raw.as<uint8_t>() + (size_t)b * (size_t)col->size_per * col->vbits / 8;
+  if (!col->block_ptrs.alloc(ptrs.size() * sizeof(void*))) return set_error(DG_ERR_OOM, "hipMalloc ptrs");
+  DG_HIP(hipMemcpy(col->block_ptrs.p, ptrs.data(), ptrs.size() * sizeof(void*), hipMemcpyHostToDevice));
+  return DG_OK;
+}
+
 int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
   // [u8 version][i32 total][i32 sizePer][u8 compression (maybe flagged)][encoding?][blocks | values]
   if (s.left() < 10) return set_error(DG_ERR_FORMAT, "%s: truncated numeric column", c->name.c_str());
@@ -271,19 +347,35 @@ int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
   if (cid < (int8_t)0xFE) {  // CompressionFactory.hasEncodingFlag
     uint8_t enc = *s.p++;
     cid = (int8_t)(cid + 126);
-    if (enc != 0xFF)
-      return set_error(DG_ERR_UNSUPPORTED, "%s: long encoding %d (DELTA/TABLE) not implemented", c->name.c_str(), enc);
+    if (enc != 0xFF) {
+      int rc = parse_long_encoding(c, enc, &s);
+      if (rc) return rc;
+    }
   }
   col.codec = (uint8_t)cid;
   col.width = width;
-  if (col.codec == CODEC_NONE) return upload_flat(&col, s.p, s.end);
+  if (col.codec == CODEC_NONE) return col.vbits ? upload_flat_packed(&col, s.p, s.end) : upload_flat(&col, s.p, s.end);
   col.log2_per = log2i(col.size_per);
-  if (col.log2_per < 0 || (int64_t)col.size_per * width > kBlockBytes)
+  const int64_t block_bytes = col.vbits ? vsize_serialized(col.vbits, col.size_per) : (int64_t)col.size_per * width;
+  if (col.log2_per < 0 || block_bytes > kBlockBytes)
     return set_error(DG_ERR_FORMAT, "%s: bad block size %d", c->name.c_str(), col.size_per);
   GI blocks;
   if (!gi_read(s, &blocks)) return set_error(DG_ERR_FORMAT, "%s: bad block index", c->name.c_str());
   if ((int64_t)blocks.n * col.size_per < col.total) return set_error(DG_ERR_FORMAT, "%s: too few blocks", c->name.c_str());
-  return upload_blocks(ctx, &col, blocks);
+  int rc = upload_blocks(ctx, &col, blocks);
+  if (rc || !col.vbits) return rc;
+  // every block must hold the packed bytes of its rows (the expansion reads exactly those)
+  for (int32_t k = 0; k < col.nblocks; ++k) {
+    const int64_t rows = std::min<int64_t>(col.size_per, (int64_t)col.total - (int64_t)k * col.size_per);
+    if (rows <= 0) continue;
+    const int64_t need = (col.vbits * rows + 7) / 8;
+    const uint8_t* bp;
+    const int64_t have = col.codec == CODEC_LZ4 ? col.dec_len[k] : blocks.get(k, &bp);
+    if (have >= 0 && have < need)
+      return set_error(DG_ERR_FORMAT, "%s: packed block %d holds %lld of %lld bytes", c->name.c_str(), k,
+                       (long long)have, (long long)need);
+  }
+  return DG_OK;
 }
 
 int parse_string(Context* ctx, Column* c, Slice s) {

@@ -145,8 +145,112 @@ def _compress_blocks(raw: bytes, block_bytes: int, compression: str, lz4_mode: s
     return blocks
 
 
-def numeric_column_part(values: np.ndarray, kind: str, compression: str, lz4_mode: str) -> bytes:
-    """CompressedColumnar{Longs,Floats,Doubles}Supplier layout, LONGS encoding (legacy, no flag)."""
+VSIZE_SUPPORTED = (1, 2, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64)
+MAX_TABLE_SIZE = 256  # CompressionFactory.MAX_TABLE_SIZE (data/CompressionFactory.java:85)
+_I64_MAX = 2 ** 63 - 1
+
+
+def bits_for_max(value: int) -> int:
+    """VSizeLongSerde.getBitsForMax (data/VSizeLongSerde.java:41-59)."""
+    if value < 0:
+        raise ValueError(f"maxValue[{value}] must be positive")
+    nbits, max_value = 0, 1
+    for size in VSIZE_SUPPORTED:
+        while nbits < size and max_value < _I64_MAX // 2:
+            nbits += 1
+            max_value *= 2
+        if value <= max_value or max_value >= _I64_MAX // 2:
+            return size
+    return 64
+
+
+def vsize_serialized_size(bits: int, n: int) -> int:
+    """VSizeLongSerde.getSerializedSize (:61-65): packed bytes rounded up + 4 closing bytes."""
+    return (bits * n + 7) // 8 + 4
+
+
+def vsize_values_per_block(bits: int, block_bytes: int = BUFFER_SIZE) -> int:
+    """VSizeLongSerde.getNumValuesPerBlock (:70-77)."""
+    ret = 1
+    while vsize_serialized_size(bits, ret) <= block_bytes:
+        ret *= 2
+    return ret // 2
+
+
+def vsize_pack(values: np.ndarray, bits: int) -> bytes:
+    """VSizeLongSerde serializers (Size1Ser, Size2Ser, Mult4Ser, Mult8Ser, :190-414): values written
+    MSB-first as one big-endian bit stream, the last partial byte zero-filled, then 4 zero bytes."""
+    v = np.ascontiguousarray(values, dtype=np.uint64)
+    if bits % 8 == 0:
+        nb = bits // 8
+        body = v.astype(">u8").view(np.uint8).reshape(-1, 8)[:, 8 - nb:].tobytes()
+    else:
+        shifts = np.arange(bits - 1, -1, -1, dtype=np.uint64)
+        bitmat = ((v[:, None] >> shifts[None, :]) & np.uint64(1)).astype(np.uint8)
+        body = np.packbits(bitmat.reshape(-1)).tobytes()
+    return body + bytes(4)
+
+
+def choose_long_encoding(values: np.ndarray):
+    """IntermediateColumnarLongsSerializer.makeDelegate (:103-124) for longEncoding=auto: TABLE when at
+    most 256 distinct values (table in first-appearance order), DELTA when max - min does not overflow
+    and is not Long.MAX_VALUE, LONGS otherwise. Returns (format, meta) with meta the ids/offsets."""
+    v = np.asarray(values, dtype=np.int64)
+    uniq, first = np.unique(v, return_index=True)
+    if len(uniq) <= MAX_TABLE_SIZE:
+        order = np.argsort(first, kind="stable")
+        table = uniq[order]
+        rank = np.empty(len(uniq), dtype=np.int64)
+        rank[order] = np.arange(len(uniq))
+        ids = rank[np.searchsorted(uniq, v)] if len(v) else np.zeros(0, dtype=np.int64)
+        return "table", (table, ids.astype(np.uint64), bits_for_max(len(table)))
+    lo, hi = int(v.min()), int(v.max())
+    delta = hi - lo
+    if delta <= _I64_MAX and delta != _I64_MAX:
+        offsets = (v.astype(np.uint64) - np.uint64(lo & 0xFFFFFFFFFFFFFFFF))
+        return "delta", (lo, offsets, bits_for_max(delta + 1))
+    return "longs", None
+
+
+def packed_long_column_part(values: np.ndarray, compression: str, lz4_mode: str, fmt: str, meta) -> bytes:
+    """BlockLayout / EntireLayout long column with a DELTA or TABLE LongEncodingWriter:
+    [0x02][i32 total][i32 sizePer][cid - 126 (encoding flag)][format id][encoding meta][blocks]
+    (BlockLayoutColumnarLongsSerializer.java:37-41,60-66; DeltaLongEncodingWriter.putMeta :59-66;
+    TableLongEncodingWriter.putMeta :77-86). Every block restarts the packed stream."""
+    n = len(values)
+    if fmt == "delta":
+        base, packed, bits = meta
+        enc = bytes([0x00, 0x01]) + struct.pack(">qi", base, bits)
+    else:
+        table, packed, bits = meta
+        enc = bytes([0x01, 0x01]) + struct.pack(">i", len(table)) + np.asarray(table, dtype=">i8").tobytes()
+    cid = COMPRESSION_IDS[compression]
+    flagged = ((cid - 256 if cid > 127 else cid) - 126) & 0xFF  # CompressionFactory.setEncodingFlag
+    if compression == "none":  # EntireLayoutColumnarLongsSerializer writes sizePer 0 (:35-39)
+        return struct.pack(">Bii", 0x02, n, 0) + bytes([flagged]) + enc + vsize_pack(packed, bits)
+    size_per = vsize_values_per_block(bits)
+    blocks = []
+    for off in range(0, n, size_per):
+        chunk = vsize_pack(packed[off:off + size_per], bits)
+        if compression == "lz4":
+            blocks.append(lz4_compress(chunk, lz4_mode))
+        elif compression == "uncompressed":
+            blocks.append(chunk)
+        else:
+            raise ValueError(f"unsupported block compression {compression}")
+    return struct.pack(">Bii", 0x02, n, size_per) + bytes([flagged]) + enc + _blocks_generic_indexed(blocks)
+
+
+def numeric_column_part(values: np.ndarray, kind: str, compression: str, lz4_mode: str,
+                        long_encoding: str = "longs") -> bytes:
+    """CompressedColumnar{Longs,Floats,Doubles}Supplier layout, LONGS encoding (legacy, no flag), or
+    for longs with long_encoding="auto" the format IntermediateColumnarLongsSerializer picks."""
+    if kind == "long" and long_encoding == "auto" and len(values):
+        fmt, meta = choose_long_encoding(values)
+        if fmt != "longs":
+            return packed_long_column_part(np.asarray(values, dtype=np.int64), compression, lz4_mode, fmt, meta)
+    elif long_encoding not in ("longs", "auto"):
+        raise ValueError(f"unknown long encoding {long_encoding}")
     dtype = {"long": "<i8", "double": "<f8", "float": "<f4"}[kind]
     arr = np.ascontiguousarray(values, dtype=dtype)
     width = arr.dtype.itemsize
@@ -334,8 +438,10 @@ class SegmentSpec:
 
 
 def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", compression: str = "lz4",
-                  dim_compression: Optional[str] = None, lz4_mode: str = "hc") -> str:
-    """Write a v9 segment directory. Rows must already be in segment order (time-sorted)."""
+                  dim_compression: Optional[str] = None, lz4_mode: str = "hc", long_encoding: str = "longs") -> str:
+    """Write a v9 segment directory. Rows must already be in segment order (time-sorted).
+    long_encoding: IndexSpec.longEncoding, "longs" (default) or "auto" (DELTA / TABLE / LONGS per column,
+    __time included: IndexMergerV9 serializes it with the same long encoding)."""
     os.makedirs(out_dir, exist_ok=True)
     n = len(spec.timestamps)
     ts = np.asarray(spec.timestamps, dtype=np.int64)
@@ -344,7 +450,7 @@ def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", comp
     dim_comp = dim_compression or ("uncompressed" if compression == "none" else compression)
     files: Dict[str, bytes] = {}
     files["__time"] = _descriptor("LONG", {"type": "long", "byteOrder": "LITTLE_ENDIAN"}) + \
-        numeric_column_part(ts, "long", compression, lz4_mode)
+        numeric_column_part(ts, "long", compression, lz4_mode, long_encoding)
     for name, (dictionary, ids) in spec.dims.items():
         ids = np.asarray(ids, dtype=np.int32)
         if len(ids) != n:
@@ -357,7 +463,7 @@ def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", comp
             raise ValueError(f"metric {name} has {len(vals)} rows, expected {n}")
         vt = {"long": "LONG", "double": "DOUBLE", "float": "FLOAT"}[kind]
         files[name] = _descriptor(vt, {"type": kind, "byteOrder": "LITTLE_ENDIAN"}) + \
-            numeric_column_part(vals, kind, compression, lz4_mode)
+            numeric_column_part(vals, kind, compression, lz4_mode, long_encoding)
     dims = list(spec.dims.keys())
     cols = dims + list(spec.metrics.keys())
     if spec.interval is not None:

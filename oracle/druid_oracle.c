@@ -289,6 +289,11 @@ typedef struct {
   /* numeric */
   int32_t total, size_per;
   int compression;
+  int long_enc;          /* 0xFF LONGS, 0x00 DELTA, 0x01 TABLE (CompressionFactory.LongEncodingFormat) */
+  int vbits;             /* DELTA / TABLE: bits per packed value */
+  int64_t delta_base;
+  int32_t table_n;
+  const uint8_t* table;  /* TABLE: table_n big-endian longs */
   const uint8_t* raw;    /* NONE layout */
   gindexed blocks;
   /* string */
@@ -314,6 +319,59 @@ static ocol* find_col(oseg* s, const char* name) {
   return NULL;
 }
 
+/* ---- VSizeLongSerde (VSizeLongSerde.java) restated: getBitsForMax (:41-59) and the per-size
+ * deserializers Size1Des..Size64Des (:416-657), each reading the big-endian buffer exactly as the
+ * Java get(index) does (getShort / getInt / getLong are big-endian, >> on them is arithmetic) ---- */
+int or_bits_for_max(int64_t value) {
+  static const int sizes[] = {1, 2, 4, 8, 12, 16, 20, 24, 32, 40, 48, 56, 64};
+  if (value < 0) return -1;
+  int nbits = 0;
+  int64_t max_value = 1;
+  for (int i = 0; i < 13; ++i) {
+    while (nbits < sizes[i] && max_value < INT64_MAX / 2) {
+      nbits++;
+      max_value *= 2;
+    }
+    if (value <= max_value || max_value >= INT64_MAX / 2) return sizes[i];
+  }
+  return 64;
+}
+
+static int16_t j_short(const uint8_t* p) { return (int16_t)(((uint16_t)p[0] << 8) | p[1]); }
+static int32_t j_int(const uint8_t* p) { return be32(p); }
+static int64_t j_long(const uint8_t* p) { return be64(p); }
+
+int64_t or_vsize_get(int bits, const uint8_t* b, int64_t index) {
+  switch (bits) {
+    case 1: return ((int8_t)b[index >> 3] >> (7 - (index & 7))) & 1;
+    case 2: return ((int8_t)b[index >> 2] >> (6 - ((index & 3) << 1))) & 3;
+    case 4: return ((int8_t)b[index >> 1] >> (((index + 1) & 1) << 2)) & 0xF;
+    case 8: return b[index] & 0xFF;
+    case 12: return (j_short(b + ((index * 3) >> 1)) >> (((index + 1) & 1) << 2)) & 0xFFF;
+    case 16: return j_short(b + (index << 1)) & 0xFFFF;
+    case 20: return (j_int(b + ((index * 5) >> 1)) >> ((((index + 1) & 1) << 2) + 8)) & 0xFFFFF;
+    case 24: return (int64_t)((uint32_t)j_int(b + index * 3) >> 8);
+    case 32: return (int64_t)(uint32_t)j_int(b + (index << 2));
+    case 40: return (int64_t)((uint64_t)j_long(b + index * 5) >> 24);
+    case 48: return (int64_t)((uint64_t)j_long(b + index * 6) >> 16);
+    case 56: return (int64_t)((uint64_t)j_long(b + index * 7) >> 8);
+    case 64: return j_long(b + (index << 3));
+    default: return 0;
+  }
+}
+
+/* one packed value -> the long the reader returns (Delta: base + v, :63-66; Table: table[v], :69-72) */
+static int packed_value(const ocol* c, const uint8_t* buf, int64_t idx, int64_t* out) {
+  int64_t v = or_vsize_get(c->vbits, buf, idx);
+  if (c->long_enc == 0x00) {
+    *out = (int64_t)((uint64_t)c->delta_base + (uint64_t)v);
+    return 0;
+  }
+  if (v < 0 || v >= c->table_n) return -1; /* ArrayIndexOutOfBounds in the reference */
+  *out = be64(c->table + 8 * v);
+  return 0;
+}
+
 static int parse_numeric(ocol* c, const uint8_t* p) {
   /* CompressedColumnar{Longs,Floats,Doubles}Supplier.fromByteBuffer */
   if (p[0] != 0x02 && p[0] != 0x01) return -1;
@@ -328,7 +386,24 @@ static int parse_numeric(ocol* c, const uint8_t* p) {
   if (cid < (int8_t)0xFE) { /* CompressionFactory.hasEncodingFlag */
     uint8_t enc = *q++;
     cid = (int8_t)(cid + 126);
-    if (enc != 0xFF) return -2; /* DELTA / TABLE encodings not restated yet */
+    c->long_enc = enc;
+    if (enc == 0x00) { /* DeltaLongEncodingReader(ByteBuffer) :34-46 */
+      if (q[0] != 0x01) return -1;
+      c->delta_base = be64(q + 1);
+      c->vbits = be32(q + 9);
+      q += 13;
+    } else if (enc == 0x01) { /* TableLongEncodingReader(ByteBuffer) :33-52 */
+      if (q[0] != 0x01) return -1;
+      c->table_n = be32(q + 1);
+      if (c->table_n < 0 || c->table_n > 256) return -1; /* CompressionFactory.MAX_TABLE_SIZE */
+      c->table = q + 5;
+      c->vbits = or_bits_for_max(c->table_n);
+      q += 5 + 8 * (size_t)c->table_n;
+    } else if (enc != 0xFF) {
+      return -1;
+    }
+  } else {
+    c->long_enc = 0xFF;
   }
   c->compression = (uint8_t)cid;
   if (c->compression == 0xFE) {
@@ -550,6 +625,35 @@ static int64_t decode_block(ocol* c, int32_t i, uint8_t* dst, int64_t cap) {
 
 /* Materialize a numeric column as raw little-endian values of its stored width. */
 static int read_numeric_raw(ocol* c, uint8_t* out, int width) {
+  if (c->long_enc == 0x00 || c->long_enc == 0x01) {
+    /* EntireLayout (NONE): one packed stream; BlockLayout: every block restarts at index 0 */
+    int64_t* o = (int64_t*)out;
+    if (c->compression == 0xFE) {
+      for (int64_t r = 0; r < c->total; ++r)
+        if (packed_value(c, c->raw, r, &o[r])) return -1;
+      return 0;
+    }
+    uint8_t* buf = (uint8_t*)calloc(65536 + 16, 1);
+    int64_t done = 0;
+    for (int32_t b = 0; b < c->blocks.n && done < c->total; ++b) {
+      int64_t got = decode_block(c, b, buf, 65536 + 16);
+      int64_t vals = c->size_per;
+      if (vals > c->total - done) vals = c->total - done;
+      if (got < 0 || got < (c->vbits * vals + 7) / 8) {
+        free(buf);
+        return -1;
+      }
+      if (got < 65536 + 16) memset(buf + got, 0, (size_t)(65536 + 16 - got));
+      for (int64_t r = 0; r < vals; ++r)
+        if (packed_value(c, buf, r, &o[done + r])) {
+          free(buf);
+          return -1;
+        }
+      done += vals;
+    }
+    free(buf);
+    return done == c->total ? 0 : -1;
+  }
   if (c->compression == 0xFE) {
     memcpy(out, c->raw, (size_t)c->total * (size_t)width);
     return 0;

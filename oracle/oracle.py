@@ -83,8 +83,23 @@ def lib():
         l.or_concise_decode.argtypes = [vp, i64, vp, i64]
         l.or_roaring_decode.restype = i64
         l.or_roaring_decode.argtypes = [vp, i64, vp, i64]
+        l.or_bits_for_max.restype = ctypes.c_int
+        l.or_bits_for_max.argtypes = [i64]
+        l.or_vsize_get.restype = i64
+        l.or_vsize_get.argtypes = [ctypes.c_int, vp, i64]
         _lib = l
     return _lib
+
+
+def bits_for_max(value: int) -> int:
+    """VSizeLongSerde.getBitsForMax (VSizeLongSerde.java:41-59), restated in druid_oracle.c."""
+    return int(lib().or_bits_for_max(value))
+
+
+def vsize_unpack(buf: bytes, bits: int, n: int) -> np.ndarray:
+    """VSizeLongSerde.getDeserializer(bits).get(i) for i < n (VSizeLongSerde.java:416-657)."""
+    b = ctypes.create_string_buffer(bytes(buf) + bytes(8))
+    return np.array([lib().or_vsize_get(bits, b, i) for i in range(n)], dtype=np.int64)
 
 
 def lz4_decompress(data: bytes, cap: int = 65536 + 16) -> bytes:
