@@ -719,11 +719,117 @@ class TopNQuery(BaseQuery):
 
 
 @dataclass
+class OrderByColumnSpec:
+    """groupby/orderby/OrderByColumnSpec.java: column, direction, dimensionOrder (StringComparator)."""
+    dimension: str
+    direction: str = "ascending"
+    dimensionOrder: str = "lexicographic"
+
+    @staticmethod
+    def from_json(js) -> "OrderByColumnSpec":
+        if isinstance(js, str):
+            return OrderByColumnSpec(js)
+        d = str(js.get("direction", "ascending")).lower()
+        if d in ("asc", "ascending"):
+            d = "ascending"
+        elif d in ("desc", "descending"):
+            d = "descending"
+        else:
+            raise ValueError(f"Unknown direction[{d}]")
+        order = js.get("dimensionOrder", "lexicographic") or "lexicographic"
+        if isinstance(order, dict):
+            order = order.get("type", "lexicographic")
+        order = str(order).lower()
+        if order not in ("lexicographic", "alphanumeric", "numeric", "strlen"):
+            raise ValueError(f"unsupported dimensionOrder {order!r}")
+        return OrderByColumnSpec(js["dimension"], d, order)
+
+    def to_json(self):
+        return {"dimension": self.dimension, "direction": self.direction, "dimensionOrder": self.dimensionOrder}
+
+
+@dataclass
+class DefaultLimitSpec:
+    """groupby/orderby/DefaultLimitSpec.java: ORDER BY columns + LIMIT (None = Integer.MAX_VALUE)."""
+    columns: List[OrderByColumnSpec] = field(default_factory=list)
+    limit: Optional[int] = None
+
+    @staticmethod
+    def from_json(js) -> Optional["DefaultLimitSpec"]:
+        if js is None:
+            return None
+        t = js.get("type", "default")
+        if t == "noop":
+            return None
+        if t != "default":
+            raise ValueError(f"unsupported limitSpec {t!r}")
+        limit = js.get("limit")
+        if limit is not None and int(limit) <= 0:
+            raise ValueError(f"limit[{limit}] must be >0")
+        return DefaultLimitSpec([OrderByColumnSpec.from_json(c) for c in js.get("columns") or []],
+                                None if limit is None else int(limit))
+
+    def to_json(self):
+        js = {"type": "default", "columns": [c.to_json() for c in self.columns]}
+        if self.limit is not None:
+            js["limit"] = self.limit
+        return js
+
+
+@dataclass
+class HavingSpec:
+    """groupby/having/*HavingSpec.java as a tree: type in greaterThan / lessThan / equalTo
+    (aggregation, value), dimSelector (dimension, value), and / or (specs), not (specs[0]), always,
+    never."""
+    type: str
+    aggregation: Optional[str] = None
+    value: Any = None
+    dimension: Optional[str] = None
+    specs: List["HavingSpec"] = field(default_factory=list)
+
+    @staticmethod
+    def from_json(js) -> Optional["HavingSpec"]:
+        if js is None:
+            return None
+        t = js["type"]
+        if t in ("greaterThan", "lessThan", "equalTo"):
+            return HavingSpec(t, aggregation=js["aggregation"], value=js["value"])
+        if t == "dimSelector":
+            if js.get("extractionFn") is not None:
+                raise ValueError("extraction functions are out of scope")
+            return HavingSpec(t, dimension=js["dimension"], value=js.get("value"))
+        if t in ("and", "or"):
+            return HavingSpec(t, specs=[HavingSpec.from_json(x) for x in js["havingSpecs"]])
+        if t == "not":
+            return HavingSpec(t, specs=[HavingSpec.from_json(js["havingSpec"])])
+        if t in ("always", "never"):
+            return HavingSpec(t)
+        raise ValueError(f"unsupported having {t!r}")
+
+    def to_json(self):
+        if self.type in ("greaterThan", "lessThan", "equalTo"):
+            return {"type": self.type, "aggregation": self.aggregation, "value": self.value}
+        if self.type == "dimSelector":
+            return {"type": self.type, "dimension": self.dimension, "value": self.value}
+        if self.type in ("and", "or"):
+            return {"type": self.type, "havingSpecs": [x.to_json() for x in self.specs]}
+        if self.type == "not":
+            return {"type": "not", "havingSpec": self.specs[0].to_json()}
+        return {"type": self.type}
+
+
+@dataclass
 class GroupByQuery(BaseQuery):
     dimensions: List[str] = field(default_factory=list)
+    limitSpec: Optional[DefaultLimitSpec] = None
+    having: Optional[HavingSpec] = None
 
     def __post_init__(self):
         super().__post_init__()
+        if isinstance(self.limitSpec, dict):
+            self.limitSpec = DefaultLimitSpec.from_json(self.limitSpec)
+        if isinstance(self.having, dict):
+            self.having = HavingSpec.from_json(self.having)
         dims = []
         for d in self.dimensions:
             if isinstance(d, dict):
@@ -737,6 +843,10 @@ class GroupByQuery(BaseQuery):
     def to_json(self):
         js = self._base_json("groupBy")
         js["dimensions"] = list(self.dimensions)
+        if self.limitSpec is not None:
+            js["limitSpec"] = self.limitSpec.to_json()
+        if self.having is not None:
+            js["having"] = self.having.to_json()
         return js
 
 
@@ -750,7 +860,8 @@ def query_from_json(js: Dict[str, Any]):
     if qt == "topN":
         return TopNQuery(dimension=js["dimension"], metric=js["metric"], threshold=int(js["threshold"]), **common)
     if qt == "groupBy":
-        return GroupByQuery(dimensions=js.get("dimensions", []), **common)
+        return GroupByQuery(dimensions=js.get("dimensions", []), limitSpec=js.get("limitSpec"),
+                            having=js.get("having"), **common)
     raise ValueError(f"unsupported queryType {qt!r}")
 
 

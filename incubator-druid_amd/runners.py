@@ -23,6 +23,8 @@ import ctypes
 import heapq
 import math
 from collections import OrderedDict, defaultdict
+from decimal import Decimal
+from fractions import Fraction
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -659,7 +661,92 @@ def merge_groupby(query: Q.GroupByQuery, partials: Sequence[GroupByPartial]) -> 
         for a, col in zip(query.aggregations, aggs):
             ev[a.name] = _py(col[r], a.output_type)
         rows.append(Q.Row(int(t[r]), ev))
-    return rows
+    return postprocess_groupby(query, rows)
+
+
+# ----------------------------------------------------------------------------------------------
+# groupBy post-processing (GroupByQuery.postProcess: having, then the limitSpec;
+# GroupByStrategyV2.applyPostProcessing). Host-side over the merged rows, which arrive in the
+# natural (time, dimensions) order.
+# ----------------------------------------------------------------------------------------------
+def _double_key(v: float):
+    if v != v:
+        return (1, 0.0, 0)  # Doubles.compare: NaN greatest, -0.0 < 0.0
+    return (0, v, 1 if (v == 0.0 and math.copysign(1.0, v) > 0) else 0)
+
+
+def _having_compare(metric, value) -> int:
+    """HavingSpecMetricComparator.compare (having/HavingSpecMetricComparator.java:36-80)."""
+    if metric is None:
+        a, b = _double_key(0.0), _double_key(float(value))
+        return (a > b) - (a < b)
+    if isinstance(metric, int):
+        if isinstance(value, int):
+            return (metric > value) - (metric < value)
+        x, y = Fraction(metric), Fraction(Decimal(repr(float(value))))  # BigDecimal.valueOf
+        return (x > y) - (x < y)
+    m = float(metric)
+    if isinstance(value, int):
+        x, y = Fraction(Decimal(repr(m))), Fraction(value)
+        return (x > y) - (x < y)
+    a, b = _double_key(m), _double_key(float(value))
+    return (a > b) - (a < b)
+
+
+def _having_eval(h: Q.HavingSpec, row: Q.Row) -> bool:
+    t = h.type
+    if t == "always":
+        return True
+    if t == "never":
+        return False
+    if t == "and":
+        return all(_having_eval(x, row) for x in h.specs)
+    if t == "or":
+        return any(_having_eval(x, row) for x in h.specs)
+    if t == "not":
+        return not _having_eval(h.specs[0], row)
+    if t == "dimSelector":  # DimensionSelectorHavingSpec.eval: emptyToNull on both sides
+        return (row.event.get(h.dimension) or None) == (h.value or None)
+    metric = row.event.get(h.aggregation)
+    if t == "equalTo" and metric is None and h.value is None:
+        return True
+    if h.value is None:
+        return False
+    c = _having_compare(metric, h.value)
+    return c > 0 if t == "greaterThan" else (c < 0 if t == "lessThan" else c == 0)
+
+
+def postprocess_groupby(query: Q.GroupByQuery, rows: List[Q.Row]) -> List[Q.Row]:
+    if query.having is not None:
+        rows = [r for r in rows if _having_eval(query.having, r)]
+    ls = query.limitSpec
+    if ls is None:
+        return rows
+    if ls.columns:
+        aggs = {a.name: a for a in query.aggregations}
+        dims = set(query.dimensions)
+        parts = []
+        for c in ls.columns:
+            if c.dimension in aggs:
+                fn = aggs[c.dimension].compare_key
+                kf = (lambda f, n: lambda r: f(r.event[n]))(fn, c.dimension)
+            elif c.dimension in dims:
+                sk = O.sort_key(c.dimensionOrder)
+                kf = (lambda f, n: lambda r: f(r.event.get(n)))(sk, c.dimension)
+            else:
+                raise ValueError(f"Unknown column in order clause[{c.dimension}]")
+            parts.append((kf, c.direction == "descending"))
+        by_dims_first = bool(query.context.get("sortByDimsFirst", False))
+        gran_all = query.granularity.is_all
+
+        def key(r):
+            ks = tuple(O._Desc(f(r)) if desc else f(r) for f, desc in parts)
+            if gran_all:
+                return ks
+            return ks + (r.timestamp,) if by_dims_first else (r.timestamp,) + ks
+
+        rows = sorted(rows, key=key)  # stable: ties keep the natural order
+    return rows if ls.limit is None else rows[:ls.limit]
 
 
 # ----------------------------------------------------------------------------------------------

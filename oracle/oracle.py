@@ -27,10 +27,12 @@ the known-answer tests transcribed from the reference's unit tests (tests/golden
 from __future__ import annotations
 
 import ctypes
+import functools
 import heapq
 import importlib
 import math
 import os
+import struct
 import sys
 from decimal import Decimal, InvalidOperation
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -1101,7 +1103,130 @@ def merge_groupby(query, per_segment: List[List]) -> List:
         ev.update(aggs)
         out.append(Q.Row(bt if gran.is_all else k, ev))
     out.sort(key=lambda r: (r.timestamp, tuple(_jkey(r.event[d]) for d in query.dimensions)))
-    return out
+    return groupby_post_process(query, out)
+
+
+# ---- GroupByQuery.postProcess: having (having/*HavingSpec.java) then DefaultLimitSpec
+# (orderby/DefaultLimitSpec.java:150-268), restated as comparator functions ----
+def _doubles_compare(a: float, b: float) -> int:
+    """Guava Doubles.compare = Double.compare: NaN greatest, -0.0 < 0.0."""
+    if a < b:
+        return -1
+    if a > b:
+        return 1
+    ab = 0x7FF8000000000000 if a != a else struct.unpack("<q", struct.pack("<d", a))[0]
+    bb = 0x7FF8000000000000 if b != b else struct.unpack("<q", struct.pack("<d", b))[0]
+    return (ab > bb) - (ab < bb)
+
+
+def _big_decimal_compare(a, b) -> int:
+    """BigDecimal.valueOf(x).compareTo(BigDecimal.valueOf(y)); valueOf(double) goes via Double.toString."""
+    from decimal import Decimal
+    da = Decimal(a) if isinstance(a, int) else Decimal(repr(float(a)))
+    db = Decimal(b) if isinstance(b, int) else Decimal(repr(float(b)))
+    return (da > db) - (da < db)
+
+
+def having_metric_compare(value, metric) -> int:
+    """HavingSpecMetricComparator.compare(aggregationName, value, aggregators, metricValueObj) :36-80."""
+    if metric is None:
+        return _doubles_compare(0.0, float(value))
+    if isinstance(metric, int):
+        if isinstance(value, int):
+            return (metric > value) - (metric < value)
+        return -_big_decimal_compare(float(value), metric)
+    if isinstance(value, int):
+        return _big_decimal_compare(float(metric), value)
+    return _doubles_compare(float(metric), float(value))
+
+
+def having_eval(h, row) -> bool:
+    t = h.type
+    if t == "always":
+        return True  # AlwaysHavingSpec
+    if t == "never":
+        return False  # NeverHavingSpec
+    if t == "and":  # AndHavingSpec.eval: every spec
+        for x in h.specs:
+            if not having_eval(x, row):
+                return False
+        return True
+    if t == "or":  # OrHavingSpec.eval: any spec
+        for x in h.specs:
+            if having_eval(x, row):
+                return True
+        return False
+    if t == "not":
+        return not having_eval(h.specs[0], row)
+    if t == "dimSelector":  # DimensionSelectorHavingSpec.eval
+        v = row.event.get(h.dimension)
+        v = None if v == "" else v
+        w = None if h.value == "" else h.value
+        return v == w
+    metric = row.event.get(h.aggregation)
+    if t == "equalTo":  # EqualToHavingSpec.eval :69-76
+        if h.value is None:
+            return metric is None
+        return having_metric_compare(h.value, metric) == 0
+    if h.value is None:
+        return False
+    c = having_metric_compare(h.value, metric)
+    return c > 0 if t == "greaterThan" else c < 0
+
+
+_STRING_COMPARATORS = {"lexicographic": lambda a, b: lexicographic_compare(a, b),
+                       "alphanumeric": lambda a, b: alphanumeric_compare(a, b),
+                       "numeric": lambda a, b: numeric_compare(a, b),
+                       "strlen": lambda a, b: strlen_compare(a, b)}
+
+
+def _metric_compare(agg, a, b) -> int:
+    """AggregatorFactory.getComparator: LongSumAggregator.COMPARATOR (Long.compare) or
+    DoubleSumAggregator.COMPARATOR (Doubles.compare) and the float/min/max equivalents."""
+    if a is None or b is None:  # Ordering.natural().nullsFirst()
+        return (a is not None) - (b is not None)
+    if agg.output_type == "long":
+        return (a > b) - (a < b)
+    return _doubles_compare(float(a), float(b))
+
+
+def groupby_post_process(query, rows: List) -> List:
+    if getattr(query, "having", None) is not None:
+        rows = [r for r in rows if having_eval(query.having, r)]
+    ls = getattr(query, "limitSpec", None)
+    if ls is None:
+        return rows
+    if not ls.columns:
+        return rows if ls.limit is None else rows[:ls.limit]  # LimitingFn
+    aggs = {a.name: a for a in query.aggregations}
+    comparators = []
+    for c in ls.columns:  # makeComparator: post-aggs, then aggregators, then dimensions
+        if c.dimension in aggs:
+            cmp = (lambda a, n: lambda x, y: _metric_compare(a, x.event[n], y.event[n]))(aggs[c.dimension], c.dimension)
+        elif c.dimension in query.dimensions:
+            sc = _STRING_COMPARATORS[c.dimensionOrder]
+            cmp = (lambda f, n: lambda x, y: f(x.event.get(n), y.event.get(n)))(sc, c.dimension)
+        else:
+            raise ValueError(f"Unknown column in order clause[{c.dimension}]")
+        if c.direction == "descending":
+            cmp = (lambda f: lambda x, y: f(y, x))(cmp)
+        comparators.append(cmp)
+
+    def time_cmp(x, y):
+        return (x.timestamp > y.timestamp) - (x.timestamp < y.timestamp)
+
+    by_dims_first = bool(query.context.get("sortByDimsFirst", False))
+    chain = comparators + [time_cmp] if by_dims_first else [time_cmp] + comparators
+
+    def ordering(x, y):
+        for f in chain:
+            c = f(x, y)
+            if c:
+                return c
+        return 0
+
+    out = sorted(rows, key=functools.cmp_to_key(ordering))
+    return out if ls.limit is None else out[:ls.limit]
 
 
 # ----------------------------------------------------------------------------------------------

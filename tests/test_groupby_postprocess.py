@@ -1,0 +1,120 @@
+"""groupBy post-processing: HavingSpec filtering and DefaultLimitSpec ordering + limit
+(GroupByQuery.postProcess; having/*HavingSpec.java, orderby/DefaultLimitSpec.java:150-268).
+
+CPU: the host implementation (runners.postprocess_groupby, sort keys) against the oracle's
+comparator-chain restatement on seeded random rows, and known answers for the having comparator
+(HavingSpecMetricComparator: long/double mixing via BigDecimal, Doubles.compare).
+GPU: full groupBy queries with limitSpec / having through the engine vs the oracle."""
+import importlib
+
+import numpy as np
+import pytest
+
+from compare import assert_results
+
+
+def _rows(Q, rng, n, gran_all=True):
+    out = []
+    for i in range(n):
+        ev = {
+            "a": rng.choice([None, "1", "10", "2", "b", "a10", "a9", "-3", "0.5", "zz"]),
+            "b": str(int(rng.integers(0, 30))),
+            "ls": int(rng.integers(-50, 50)),
+            "ds": float(rng.choice([-0.0, 0.0, 1.5, -2.25, 3.0, 1e300, float(rng.normal())])),
+            "rows": int(rng.integers(1, 5)),
+        }
+        out.append(Q.Row(0 if gran_all else int(rng.integers(0, 4)) * 3_600_000, ev))
+    out.sort(key=lambda r: r.timestamp)
+    return out
+
+
+def _query(Q, limit_spec, having=None, gran="all", by_dims_first=False):
+    return Q.GroupByQuery(intervals=[(0, 1 << 40)], granularity=gran, dimensions=["a", "b"],
+                          aggregations=[Q.long_sum("ls", "ls"), Q.AggregatorFactory("doubleSum", "ds", "ds"),
+                                        Q.count("rows")],
+                          limitSpec=limit_spec, having=having,
+                          context={"sortByDimsFirst": True} if by_dims_first else {})
+
+
+LIMIT_SPECS = [
+    {"type": "default", "limit": 7},
+    {"type": "default", "columns": ["a"], "limit": 5},
+    {"type": "default", "columns": [{"dimension": "ls", "direction": "descending"}], "limit": 10},
+    {"type": "default", "columns": [{"dimension": "ds", "direction": "ascending"}, "a"]},
+    {"type": "default", "columns": [{"dimension": "a", "direction": "descending", "dimensionOrder": "alphanumeric"},
+                                    {"dimension": "b", "dimensionOrder": "numeric"}], "limit": 12},
+    {"type": "default", "columns": [{"dimension": "a", "dimensionOrder": "numeric"},
+                                    {"dimension": "b", "dimensionOrder": "strlen", "direction": "desc"}]},
+    {"type": "default", "columns": [{"dimension": "rows", "direction": "descending"},
+                                    {"dimension": "ls", "direction": "ascending"}, "a", "b"], "limit": 3},
+]
+HAVINGS = [
+    None,
+    {"type": "greaterThan", "aggregation": "ls", "value": 0},
+    {"type": "lessThan", "aggregation": "ds", "value": 1},
+    {"type": "equalTo", "aggregation": "rows", "value": 2},
+    {"type": "greaterThan", "aggregation": "ls", "value": 2.5},
+    {"type": "and", "havingSpecs": [{"type": "greaterThan", "aggregation": "rows", "value": 1},
+                                    {"type": "not", "havingSpec": {"type": "dimSelector", "dimension": "a",
+                                                                    "value": "b"}}]},
+    {"type": "or", "havingSpecs": [{"type": "dimSelector", "dimension": "a", "value": None},
+                                   {"type": "equalTo", "aggregation": "ds", "value": 0}]},
+]
+
+
+@pytest.mark.parametrize("gran,by_dims_first", [("all", False), ("hour", False), ("hour", True)])
+def test_postprocess_matches_oracle(Q, O, gran, by_dims_first):
+    R = importlib.import_module("incubator-druid_amd.runners")
+    rng = np.random.default_rng(21)
+    for trial in range(4):
+        rows = _rows(Q, rng, 120, gran_all=gran == "all")
+        for ls in LIMIT_SPECS:
+            for hv in HAVINGS:
+                q = _query(Q, ls, hv, gran, by_dims_first)
+                got = R.postprocess_groupby(q, list(rows))
+                exp = O.groupby_post_process(q, list(rows))
+                assert [(r.timestamp, r.event) for r in got] == [(r.timestamp, r.event) for r in exp], (ls, hv)
+
+
+def test_having_comparator_kats(O):
+    R = importlib.import_module("incubator-druid_amd.runners")
+    # (metric, value, expected sign) per HavingSpecMetricComparator.compare
+    cases = [(5, 4, 1), (4, 4, 0), (4, 4.0, 0), (4, 4.5, -1), (4.5, 4, 1), (-0.0, 0.0, -1), (0.0, 0, 0),
+             (float("nan"), 1.0, 1), (None, 0.5, -1), (None, -1, 1), (2 ** 62 + 1, float(2 ** 62), -1),  # BigDecimal.valueOf(4.611686018427388E18) > 2^62 + 1
+             (0.1, 0, 1)]
+    for metric, value, sign in cases:
+        assert O.having_metric_compare(value, metric) == sign, (metric, value)
+        assert R._having_compare(metric, value) == sign, (metric, value)
+
+
+def test_limit_spec_json_round_trip(Q):
+    js = {"queryType": "groupBy", "intervals": ["2000-01-01/2001-01-01"], "dimensions": ["a"],
+          "aggregations": [{"type": "count", "name": "rows"}],
+          "limitSpec": {"type": "default", "limit": 3, "columns": [{"dimension": "rows", "direction": "DESCENDING"}]},
+          "having": {"type": "not", "havingSpec": {"type": "always"}}}
+    q = Q.query_from_json(js)
+    assert q.limitSpec.limit == 3 and q.limitSpec.columns[0].direction == "descending"
+    q2 = Q.query_from_json(q.to_json())
+    assert q2.limitSpec == q.limitSpec and q2.having == q.having
+    with pytest.raises(ValueError):
+        Q.query_from_json(dict(js, limitSpec={"type": "default", "limit": 0}))
+
+
+@pytest.mark.gpu
+def test_gpu_groupby_with_limit_and_having(Q, O, basic_dirs):
+    R = importlib.import_module("incubator-druid_amd.runners")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    paths = basic_dirs[("concise", "lz4")]
+    g = [S.GpuSegment(p) for p in paths]
+    o = [O.OracleSegment(p) for p in paths]
+    aggs = [Q.count("rows"), Q.long_sum("ls", "sumLongSequential"),
+            Q.AggregatorFactory("doubleSum", "ds", "sumFloatNormal")]
+    for ls, hv in [({"type": "default", "columns": [{"dimension": "ls", "direction": "descending"}], "limit": 10}, None),
+                   ({"type": "default", "columns": [{"dimension": "dimZipf", "dimensionOrder": "numeric"}]},
+                    {"type": "greaterThan", "aggregation": "rows", "value": 100}),
+                   ({"type": "default", "limit": 5}, {"type": "lessThan", "aggregation": "ds", "value": 1e6})]:
+        q = Q.GroupByQuery(intervals=[(0, 1 << 42)], dimensions=["dimZipf"], aggregations=aggs,
+                           limitSpec=ls, having=hv)
+        got, exp = R.run_query(q, g), O.run(q, o)
+        assert [r.event["dimZipf"] for r in got] == [r.event["dimZipf"] for r in exp]
+        assert_results(q, got, exp)
