@@ -574,6 +574,8 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
 }
 
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
+  if (c->multi_value)
+    return set_error(DG_ERR_UNSUPPORTED, "%s: grouping on a multi-value dimension", c->name.c_str());
   const BlockColumn& b = c->data;
   v->log2_per = b.log2_per;
   v->width = b.width;

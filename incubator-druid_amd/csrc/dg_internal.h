@@ -174,6 +174,7 @@ struct Column {
   std::vector<uint64_t> dict_hash;     // value_hash of every dictionary value (cross-segment merges)
   int bitmap_roaring = 0;
   bool has_bitmaps = false;
+  bool multi_value = false;            // row value lists not on the device: bitmap filters only
   std::vector<int64_t> bm_off;         // byte offset of each bitmap inside bm_bytes (4-byte aligned)
   std::vector<int32_t> bm_len;
   DevBuf bm_bytes;

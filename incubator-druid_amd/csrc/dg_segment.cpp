@@ -378,6 +378,34 @@ int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
   return DG_OK;
 }
 
+// Multi-value id parts (DictionaryEncodedColumnPartSerde.readMultiValuedColumn):
+// UNCOMPRESSED_MULTI_VALUE = VSizeColumnarMultiInts [0x01][numBytes][i32 size][size bytes]
+// (VSizeColumnarMultiInts.readFromByteBuffer); COMPRESSED + MULTI_VALUE_V3 =
+// [0x03][CompressedColumnarIntsSupplier offsets: 0x02, i32 total, i32 sizePer, u8 codec, GI]
+// [CompressedVSizeColumnarIntsSupplier values: 0x02, u8 numBytes, i32, i32, u8 codec, GI]
+// (V3CompressedVSizeColumnarMultiIntsSupplier.fromByteBuffer, CompressedColumnarIntsSupplier.fromByteBuffer).
+static int skip_multi_value_ids(Column* c, Slice* s, int version) {
+  if (version == 1) {
+    if (s->left() < 6 || s->p[0] != 0x01) return set_error(DG_ERR_FORMAT, "%s: bad VSize multi-ints", c->name.c_str());
+    const int32_t size = be32(s->p + 2);
+    if (size < 4 || s->left() < 6 + (int64_t)size) return set_error(DG_ERR_FORMAT, "%s: truncated multi-ints", c->name.c_str());
+    c->data.total = be32(s->p + 6);  // [i32 count] opens the payload
+    s->p += 6 + size;
+    return DG_OK;
+  }
+  if (s->left() < 1 + 10 || s->p[0] != 0x03 || s->p[1] != 0x02)
+    return set_error(DG_ERR_FORMAT, "%s: bad V3 multi-value ids", c->name.c_str());
+  c->data.total = be32(s->p + 2) - 1;  // rows + 1 offsets
+  s->p += 1 + 10;
+  GI offsets;
+  if (!gi_read(*s, &offsets)) return set_error(DG_ERR_FORMAT, "%s: bad multi-value offsets", c->name.c_str());
+  if (s->left() < 11 || s->p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: bad multi-value values", c->name.c_str());
+  s->p += 11;
+  GI values;
+  if (!gi_read(*s, &values)) return set_error(DG_ERR_FORMAT, "%s: bad multi-value value blocks", c->name.c_str());
+  return DG_OK;
+}
+
 int parse_string(Context* ctx, Column* c, Slice s) {
   if (s.left() < 1) return set_error(DG_ERR_FORMAT, "%s: empty", c->name.c_str());
   int version = s.p[0];
@@ -389,7 +417,9 @@ int parse_string(Context* ctx, Column* c, Slice s) {
   } else if (version == 1) {
     flags = 1;
   }
-  if (flags & 3) return set_error(DG_ERR_UNSUPPORTED, "%s: multi-value dimension", c->name.c_str());
+  c->multi_value = (flags & 3) != 0;
+  if (c->multi_value && version == 2 && !(flags & 2))
+    return set_error(DG_ERR_UNSUPPORTED, "%s: legacy compressed multi-value ids", c->name.c_str());
   GI dict;
   if (!gi_read(s, &dict)) return set_error(DG_ERR_FORMAT, "%s: bad dictionary", c->name.c_str());
   c->dict.resize(dict.n);
@@ -403,7 +433,12 @@ int parse_string(Context* ctx, Column* c, Slice s) {
   c->dict_hash.resize(dict.n);
   for (int32_t i = 0; i < dict.n; ++i) c->dict_hash[i] = c->dict_null[i] ? kNullValueHash : value_hash(c->dict[i]);
   BlockColumn& col = c->data;
-  if (version == 0 || version == 3) {
+  if (c->multi_value) {
+    // Row value lists are not uploaded: filters on the column run on its bitmap index, grouping on
+    // it is DG_ERR_UNSUPPORTED (column_view). Skip the id part to reach the bitmaps.
+    int rc = skip_multi_value_ids(c, &s, version);
+    if (rc) return rc;
+  } else if (version == 0 || version == 3) {
     // UNCOMPRESSED_SINGLE_VALUE / UNCOMPRESSED_WITH_FLAGS: VSizeColumnarInts.readFromByteBuffer
     // (data/VSizeColumnarInts.java:177-195): [0x00][numBytes][i32 size][big-endian values + pad].
     // Read in place: kernels load numBytes big-endian bytes per row (getInt >>> bitsToShift, :124-127).

@@ -387,14 +387,66 @@ def string_column_part(dictionary: List[Optional[str]], ids: np.ndarray, bitmap:
     return out
 
 
+def encode_multi_strings(rows: Sequence[Sequence[Optional[str]]]) -> Tuple[List[str], List[np.ndarray]]:
+    """Multi-value rows -> (sorted dictionary, per-row sorted id arrays). MultiValueHandling
+    SORTED_ARRAY (the default: values sorted, duplicates kept); an empty row is stored as [null]
+    (StringDimensionIndexer / DictionaryEncodedColumnMerger), "" and null are the same value."""
+    norm = [sorted(("" if v is None else str(v)) for v in r) or [""] for r in rows]
+    uniq = sorted({v for r in norm for v in r}, key=java_string_key)
+    index = {v: i for i, v in enumerate(uniq)}
+    return uniq, [np.array(sorted(index[v] for v in r), dtype=np.int32) for r in norm]
+
+
+def multi_string_column_part(dictionary: List[Optional[str]], rows: Sequence[np.ndarray], bitmap: str,
+                             compression: str, lz4_mode: str) -> bytes:
+    """Multi-value dictionary-encoded column (DictionaryEncodedColumnPartSerde.java:183-217):
+    compressed = version COMPRESSED + MULTI_VALUE_V3 flag, ids as V3CompressedVSizeColumnarMultiInts
+    ([0x03][CompressedColumnarInts row start offsets + end][CompressedVSizeColumnarInts values],
+    V3CompressedVSizeColumnarMultiIntsSerializer.java:87-120); uncompressed = version
+    UNCOMPRESSED_MULTI_VALUE with VSizeColumnarMultiInts ([0x01][numBytes][i32 size][i32 count]
+    [count end byte offsets][big-endian values][4 - numBytes pad], VSizeColumnarMultiInts.fromIterable).
+    Value v's bitmap holds every row whose list contains v."""
+    card = len(dictionary)
+    dict_vals = [b"" if (v is None or v == "") else v.encode("utf-8") for v in dictionary]
+    nb = num_bytes_for_max(card)
+    lens = np.array([len(r) for r in rows], dtype=np.int64)
+    flat = np.concatenate([np.asarray(r, dtype=np.int32) for r in rows]) if len(rows) else np.zeros(0, np.int32)
+    if compression in ("uncompressed", "none"):
+        out = bytes([0x01]) + generic_indexed(dict_vals, sorted_flag=True)
+        ends = np.cumsum(lens * nb).astype(">i4")
+        values = np.ascontiguousarray(flat, dtype=">u4").view(np.uint8).reshape(-1, 4)[:, 4 - nb:].tobytes()
+        payload = struct.pack(">i", len(rows)) + ends.tobytes() + values + bytes(4 - nb)
+        out += struct.pack(">BBi", 0x01, nb, len(payload)) + payload
+    else:
+        out = bytes([0x02]) + struct.pack(">i", 0x2) + generic_indexed(dict_vals, sorted_flag=True)
+        offsets = np.concatenate([[0], np.cumsum(lens)]).astype("<i4")
+        size_per = BUFFER_SIZE // 4  # CompressedColumnarIntsSupplier.MAX_INTS_IN_BUFFER
+        cid = COMPRESSION_IDS[compression]
+        out += bytes([0x03]) + struct.pack(">Bii", 0x02, len(offsets), size_per) + bytes([cid])
+        out += _blocks_generic_indexed(_compress_blocks(offsets.tobytes(), size_per * 4, compression, lz4_mode))
+        out += ids_part(flat, card, compression, lz4_mode)
+    row_of = np.repeat(np.arange(len(rows), dtype=np.int64), lens)
+    order = np.lexsort((row_of, flat))
+    sf, sr = flat[order], row_of[order]
+    bounds = np.searchsorted(sf, np.arange(card + 1))
+    bms = []
+    for v in range(card):
+        rws = np.unique(sr[bounds[v]:bounds[v + 1]])
+        if bitmap == "concise":
+            bms.append(_tools.concise_encode(rws).astype(">i4").tobytes())
+        else:
+            bms.append(roaring_serialize(rws))
+    return out + generic_indexed(bms, sorted_flag=False)
+
+
 def _bitmap_json(bitmap: str) -> dict:
     if bitmap == "concise":
         return {"type": "concise"}
     return {"type": "roaring", "compressRunOnSerialization": True}
 
 
-def _descriptor(value_type: str, part: dict) -> bytes:
-    js = json.dumps({"valueType": value_type, "hasMultipleValues": False, "parts": [part]},
+def _descriptor(value_type: str, part: dict, multi: bool = False) -> bytes:
+    js = json.dumps({"valueType": value_type, "hasMultipleValues": multi, "parts": [part]},
                     separators=(",", ":")).encode()
     return struct.pack(">i", len(js)) + js
 
@@ -452,6 +504,14 @@ def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", comp
     files["__time"] = _descriptor("LONG", {"type": "long", "byteOrder": "LITTLE_ENDIAN"}) + \
         numeric_column_part(ts, "long", compression, lz4_mode, long_encoding)
     for name, (dictionary, ids) in spec.dims.items():
+        if isinstance(ids, list) and ids and isinstance(ids[0], (list, tuple, np.ndarray)):
+            if len(ids) != n:
+                raise ValueError(f"dimension {name} has {len(ids)} rows, expected {n}")
+            part = {"type": "stringDictionary", "bitmapSerdeFactory": _bitmap_json(bitmap),
+                    "byteOrder": "LITTLE_ENDIAN"}
+            files[name] = _descriptor("STRING", part, multi=True) + multi_string_column_part(
+                dictionary, [np.asarray(r, dtype=np.int32) for r in ids], bitmap, dim_comp, lz4_mode)
+            continue
         ids = np.asarray(ids, dtype=np.int32)
         if len(ids) != n:
             raise ValueError(f"dimension {name} has {len(ids)} rows, expected {n}")

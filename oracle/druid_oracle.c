@@ -426,8 +426,23 @@ static int parse_string(ocol* c, const uint8_t* p) {
   }
   c->multi_value = (flags & 3) != 0;
   if (gi_read(&q, c->end, &c->dict)) return -1;
-  if (c->multi_value) return -2;
-  if (version == 2) { /* CompressedVSizeColumnarIntsSupplier */
+  if (c->multi_value) {
+    /* readMultiValuedColumn: only the bitmap index is restated (filters); skip the id part */
+    gindexed skip;
+    if (version == 1) { /* VSizeColumnarMultiInts [0x01][numBytes][i32 size][size bytes] */
+      if (q[0] != 0x01) return -1;
+      q += 6 + be32(q + 2);
+    } else if (version == 2 && (flags & 2)) { /* V3: [0x03][offsets CompressedColumnarInts][values CompressedVSize] */
+      if (q[0] != 0x03 || q[1] != 0x02) return -1;
+      q += 11;
+      if (gi_read(&q, c->end, &skip)) return -1;
+      if (q[0] != 0x02) return -1;
+      q += 11;
+      if (gi_read(&q, c->end, &skip)) return -1;
+    } else {
+      return -2;
+    }
+  } else if (version == 2) { /* CompressedVSizeColumnarIntsSupplier */
     if (q[0] != 0x02) return -1;
     c->num_bytes = q[1];
     c->total = be32(q + 2);
@@ -748,6 +763,7 @@ int or_dim_ids(void* h, const char* name, int32_t* out) {
   oseg* s = (oseg*)h;
   ocol* c = find_col(s, name);
   if (!c || c->kind != OR_STRING) return -1;
+  if (c->multi_value) return -2; /* row value lists not restated (grouping on them unsupported) */
   if (c->vsize) { /* VSizeColumnarInts.get (:124-127): getInt(pos) >>> (32 - 8 * numBytes), big-endian */
     for (int64_t k = 0; k < c->total; ++k) {
       const uint8_t* p = c->vsize + k * c->num_bytes;

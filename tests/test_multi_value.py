@@ -1,0 +1,106 @@
+"""Multi-value string dimensions: the V3 compressed and
+UNCOMPRESSED_MULTI_VALUE id layouts are parsed at attach; filters on the column run on its bitmap
+index (a row matches when any of its values matches, an empty row is [null]); grouping on it is
+DG_ERR_UNSUPPORTED (the Java factory keeps its CPU engine for those queries).
+
+CPU: the writer's bitmaps through the oracle's filter evaluation against the row-list semantics
+computed directly from the written rows. GPU: filter bitsets and filtered timeseries / topN /
+groupBy (grouping on other dimensions) through the engine vs the oracle."""
+import importlib
+
+import numpy as np
+import pytest
+
+from compare import assert_results
+
+VALUES = ["a", "b", "c", "d", "e", "ff", "g10", "g9", "10", "9"]
+LAYOUTS = [("concise", "lz4"), ("roaring", "lz4"), ("concise", "uncompressed"), ("roaring", "none")]
+
+
+def _rows(n, seed=2):
+    rng = np.random.default_rng(seed)
+    return [list(rng.choice(VALUES, int(rng.integers(0, 4)))) for _ in range(n)]
+
+
+def _filters(Q):
+    return [
+        Q.SelectorDimFilter("tags", "a"),
+        Q.SelectorDimFilter("tags", None),
+        Q.SelectorDimFilter("tags", "zz"),
+        Q.InDimFilter("tags", ["b", "ff", "nope"]),
+        Q.BoundDimFilter("tags", "c", "f", False, True),
+        Q.BoundDimFilter("tags", "9", "10", False, False, ordering="numeric"),
+        Q.NotDimFilter(Q.SelectorDimFilter("tags", "a")),
+        Q.AndDimFilter([Q.SelectorDimFilter("tags", "a"), Q.SelectorDimFilter("tags", "b")]),
+        Q.OrDimFilter([Q.SelectorDimFilter("tags", "g9"), Q.SelectorDimFilter("s", "3")]),
+    ]
+
+
+def _expected_mask(O, Q, f, rows, s_vals):
+    """Row-list semantics: a leaf matches a row when any of its values (an empty row = [null]) does."""
+    if isinstance(f, Q.AndDimFilter):
+        return np.logical_and.reduce([_expected_mask(O, Q, x, rows, s_vals) for x in f.fields])
+    if isinstance(f, Q.OrDimFilter):
+        return np.logical_or.reduce([_expected_mask(O, Q, x, rows, s_vals) for x in f.fields])
+    if isinstance(f, Q.NotDimFilter):
+        return ~_expected_mask(O, Q, f.field, rows, s_vals)
+    vals = rows if f.dimension == "tags" else [[v] for v in s_vals]
+
+    def leaf(v):
+        if isinstance(f, Q.SelectorDimFilter):
+            return v == f.value
+        if isinstance(f, Q.InDimFilter):
+            return v in f.values
+        return O._bound_matches(f, v)
+
+    return np.array([any(leaf(v) for v in (r or [None])) for r in vals])
+
+
+def _segment(W, path, rows, bitmap, comp, seed=3):
+    rng = np.random.default_rng(seed)
+    n = len(rows)
+    dic, ids = W.encode_multi_strings(rows)
+    s_vals = [str(x) for x in rng.integers(0, 10, n)]
+    spec = W.SegmentSpec(timestamps=np.sort(rng.integers(0, 86_400_000, n)).astype(np.int64),
+                         dims={"tags": (dic, ids), "s": W.encode_strings(s_vals)},
+                         metrics={"m": ("long", rng.integers(0, 1000, n)), "x": ("double", rng.normal(10, 2, n))})
+    return W.write_segment(path, spec, bitmap=bitmap, compression=comp, lz4_mode="fast"), s_vals
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_oracle_filters_follow_row_lists(Q, O, W, tmp_path, layout):
+    rows = _rows(20_000)
+    p, s_vals = _segment(W, str(tmp_path / "mv"), rows, *layout)
+    o = O.OracleSegment(p)
+    assert o.dictionary("tags")[0] is None  # empty rows are [null]
+    for f in _filters(Q):
+        assert np.array_equal(O.filter_mask(o, f.optimize()), _expected_mask(O, Q, f, rows, s_vals)), f
+    with pytest.raises(ValueError):
+        o.ids("tags")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_gpu_multi_value_filters(Q, O, W, tmp_path, layout):
+    R = importlib.import_module("incubator-druid_amd.runners")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    rows = _rows(60_000, seed=5)
+    p, s_vals = _segment(W, str(tmp_path / "mv"), rows, *layout)
+    g, o = S.GpuSegment(p), O.OracleSegment(p)
+    aggs = [Q.count("rows"), Q.long_sum("m", "m"), Q.AggregatorFactory("doubleSum", "x", "x"),
+            Q.AggregatorFactory("longMax", "mx", "m")]
+    for f in _filters(Q):
+        words, cnt = g.filter_bitmap(f.optimize(), Q)
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:g.num_rows].astype(bool)
+        exp = _expected_mask(O, Q, f, rows, s_vals)
+        assert cnt == int(exp.sum()) and np.array_equal(bits, exp), f
+        q = Q.TimeseriesQuery(intervals=[(0, 1 << 40)], granularity="hour", aggregations=aggs, filter=f)
+        assert_results(q, R.run_query(q, [g]), O.run(q, [o]))
+        q = Q.TopNQuery(intervals=[(0, 1 << 40)], dimension="s", metric="m", threshold=5, aggregations=aggs, filter=f)
+        assert_results(q, R.run_query(q, [g]), O.run(q, [o]))
+    q = Q.GroupByQuery(intervals=[(0, 1 << 40)], dimensions=["s"], aggregations=aggs,
+                       filter=Q.InDimFilter("tags", ["a", "e"]))
+    assert_results(q, R.run_query(q, [g]), O.run(q, [o]))
+    with pytest.raises(Exception):
+        R.run_query(Q.TopNQuery(intervals=[(0, 1 << 40)], dimension="tags", metric="m", threshold=5,
+                                aggregations=aggs), [g])
