@@ -85,9 +85,10 @@ DATASET_1B = {"segments": 64, "interval": (0, 30 * 86_400_000),
 
 def _write_one(job):
     DG = importlib.import_module("incubator-druid_amd.datagen")
-    p, rows, seed, bitmap, compression, lz4_mode, part = job
+    p, rows, seed, bitmap, compression, lz4_mode, part, long_encoding = job
     if part is None:
-        DG.write_basic_segment(p, rows, seed=seed, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode)
+        DG.write_basic_segment(p, rows, seed=seed, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode,
+                               long_encoding=long_encoding)
     else:  # time chunk `part` of the 1B-row dataset; the segment's interval is its chunk
         W = importlib.import_module("incubator-druid_amd.writer")
         n_all = DATASET_1B["segments"]
@@ -99,15 +100,17 @@ def _write_one(job):
         idx = np.arange(part * rows, (part + 1) * rows, dtype=np.int64)
         spec.timestamps = ts = start + idx * (end - start) // (n_all * rows)  # row r at floor(r * 30d / 1e9)
         assert spec.interval[0] <= int(ts[0]) and int(ts[-1]) < spec.interval[1], (part, spec.interval, ts[0], ts[-1])
-        W.write_segment(p, spec, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode)
+        W.write_segment(p, spec, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode,
+                        long_encoding=long_encoding)
     return p
 
 
-def ensure_segments(DG, root, rank, nseg, rows, compression, bitmap, lz4_mode, partitioned=False, workers=8):
+def ensure_segments(DG, root, rank, nseg, rows, compression, bitmap, lz4_mode, partitioned=False, workers=8,
+                    long_encoding="longs"):
     """This rank's segments (seed 9999 + global segment index). partitioned: consecutive time chunks
     of the 1B-row dataset (rank r holds global chunks r*nseg ..); otherwise every segment spans the
     basic interval like the JMH benchmarks' segments. Written once, in parallel, and reused."""
-    tag = "p1b_" if partitioned else ""
+    tag = ("p1b_" if partitioned else "") + ("auto_" if long_encoding == "auto" else "")
     d = os.path.join(root, f"{tag}r{rows}_s{nseg}_{compression}_{bitmap}_{lz4_mode}", f"rank{rank}")
     marker = os.path.join(d, "DONE")
     paths = [os.path.join(d, f"seg{i:04d}") for i in range(nseg)]
@@ -115,7 +118,7 @@ def ensure_segments(DG, root, rank, nseg, rows, compression, bitmap, lz4_mode, p
         shutil.rmtree(d, ignore_errors=True)
         os.makedirs(d, exist_ok=True)
         jobs = [(p, rows, 9999 + rank * nseg + i, bitmap, compression, lz4_mode,
-                 (rank * nseg + i) if partitioned else None) for i, p in enumerate(paths)]
+                 (rank * nseg + i) if partitioned else None, long_encoding) for i, p in enumerate(paths)]
         if len(jobs) > 1 and workers > 1:
             import multiprocessing as mp
             with mp.get_context("spawn").Pool(min(workers, len(jobs))) as pool:
@@ -158,6 +161,8 @@ def main():
     ap.add_argument("--compression", default="lz4", choices=["lz4", "uncompressed", "none"])
     ap.add_argument("--bitmap", default="concise", choices=["concise", "roaring"])
     ap.add_argument("--lz4-mode", default="hc", choices=["hc", "fast"])
+    ap.add_argument("--long-encoding", default="longs", choices=["longs", "auto"],
+                    help="IndexSpec longEncoding of the written segments (auto: DELTA / TABLE / LONGS per column)")
     ap.add_argument("--data-dir", default=os.environ.get("DRUID_AMD_BENCH_DATA", "/tmp/druid_amd_bench"))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -181,7 +186,8 @@ def main():
     rows_per = args.rows or rows_per
     nseg = args.segments or nseg
     paths = ensure_segments(DG, args.data_dir, rank, nseg, rows_per, args.compression, args.bitmap, args.lz4_mode,
-                            partitioned=args.config in ("ts_hourly", "groupby_hourly"), workers=args.write_workers)
+                            partitioned=args.config in ("ts_hourly", "groupby_hourly"), workers=args.write_workers,
+                            long_encoding=args.long_encoding)
     segs = [S.GpuSegment(p, device=local_rank) for p in paths]
     query = make_query(Q, args.config)
 
@@ -256,6 +262,8 @@ def main():
         uncompressed_equiv = scanned_local * (3 + 8)
     if decode_ms >= agg_ms and decode_ms > 0:
         kernel, k_ms, k_bytes = "k_lz4_decode", decode_ms, bytes_read
+        if args.long_encoding == "auto":
+            kernel = "k_lz4_decode+k_vsize_expand"  # the decode phase holds both launches
     else:
         # the aggregation kernel reads the decoded column bytes (ids + values) of every row
         kernel, k_ms = ("k_scan_agg" if args.config != "groupby" else "k_groupby"), agg_ms
@@ -275,7 +283,8 @@ def main():
         "dtype": "int64/f64",
         "data": "synthetic (basic schema, seeded numpy generator, written as Druid v9 segments)",
         "config": {"workload": desc, "config": args.config, "rows_per_segment": rows_per, "segments_per_gpu": nseg,
-                   "compression": args.compression, "bitmap": args.bitmap, "parallelism": f"segments sharded over {world} GPU(s)"},
+                   "compression": args.compression, "bitmap": args.bitmap, "long_encoding": args.long_encoding,
+                   "parallelism": f"segments sharded over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_launch": k_bytes, "avg_launch_ms": k_ms},

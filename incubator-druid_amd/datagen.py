@@ -76,9 +76,10 @@ def basic_columns(num_rows: int, seed: int, interval=BASIC_INTERVAL, row_offset:
 
 
 def write_basic_segment(out_dir: str, num_rows: int, seed: int = 9999, bitmap: str = "concise",
-                        compression: str = "lz4", lz4_mode: str = "hc", **kw) -> str:
+                        compression: str = "lz4", lz4_mode: str = "hc", long_encoding: str = "longs", **kw) -> str:
     spec = basic_columns(num_rows, seed, **kw)
-    return write_segment(out_dir, spec, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode)
+    return write_segment(out_dir, spec, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode,
+                         long_encoding=long_encoding)
 
 
 def write_basic_dataset(root: str, num_segments: int, rows_per_segment: int, base_seed: int = 9999,
