@@ -22,6 +22,8 @@ def lib():
         l.dgt_concise_encode_column.restype = ctypes.c_int64
         l.dgt_concise_encode_column.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                                 ctypes.c_void_p, ctypes.c_void_p]
+        l.dgt_lzf_compress.restype = ctypes.c_int64
+        l.dgt_lzf_compress.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
         _lib = l
     return _lib
 
@@ -42,3 +44,13 @@ def concise_encode_column(ids, cardinality: int):
     if n < 0:
         raise ValueError("dictionary id out of range")
     return words[:n], counts[:cardinality]
+
+
+def lzf_compress(data: bytes) -> bytes:
+    """compress-lzf chunked LZF (LZFEncoder.appendEncoded layout) of one block."""
+    cap = len(data) + len(data) // 16 + 64
+    out = ctypes.create_string_buffer(cap)
+    n = lib().dgt_lzf_compress(data, len(data), out, cap)
+    if n < 0:
+        raise RuntimeError("LZF compression failed")
+    return out.raw[:n]

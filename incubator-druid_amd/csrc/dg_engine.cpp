@@ -555,9 +555,11 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
 // ------------------------------------------------------------------------------------------------
 struct DecodeBatch {
   std::vector<Lz4Job> jobs;
+  std::vector<LzfJob> lzf_jobs;  // LZF blocks, decoded one wave per block
   std::vector<VsJob> expands;  // DELTA / TABLE blocks, expanded after the LZ4 decodes
   int32_t expand_rows = 0;     // largest block of `expands` (grid width)
   int64_t* last_expanded = nullptr;
+  uint8_t* last_slots = nullptr;  // decode slots of the last viewed LZ4 / LZF column
   int64_t bytes = 0;  // algorithmic bytes read
 };
 
@@ -585,12 +587,13 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
   else if (c->type == DG_COL_FLOAT) v->kind = VIEW_FLOAT;
   else v->kind = VIEW_IDS;
   db->bytes += b.stored_bytes + b.index_bytes;
-  if (b.codec != CODEC_LZ4 && b.codec != CODEC_UNCOMPRESSED && b.codec != CODEC_NONE)
+  if (b.codec != CODEC_LZ4 && b.codec != CODEC_LZF && b.codec != CODEC_UNCOMPRESSED && b.codec != CODEC_NONE)
     return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, c->name.c_str());
   uint8_t* slots = nullptr;
-  if (b.codec == CODEC_LZ4) {
+  if (b.codec == CODEC_LZ4 || b.codec == CODEC_LZF) {
     slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
     if (!slots) return set_error(DG_ERR_OOM, "decode scratch");
+    db->last_slots = slots;
   }
   int64_t* expanded = nullptr;
   if (b.vbits) {
@@ -616,7 +619,16 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
     if (rows <= 0) continue;
     if (slots) {
       const int64_t expect = b.vbits ? (b.vbits * rows + 7) / 8 : rows * b.width;
-      db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect));
+      if (b.codec == CODEC_LZ4) {
+        db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect));
+      } else {
+        LzfJob lj;
+        lj.src = b.comp.as<uint8_t>() + b.comp_off[k];
+        lj.dst = const_cast<uint8_t*>(src);
+        lj.src_len = b.comp_len[k];
+        lj.expect_len = (int32_t)expect;
+        db->lzf_jobs.push_back(lj);
+      }
     }
     if (expanded) {
       VsJob e;
@@ -649,7 +661,22 @@ static int run_expands(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
   return DG_OK;
 }
 
+static int run_lzf(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
+  if (db->lzf_jobs.empty()) return DG_OK;
+  const int n = (int)db->lzf_jobs.size();
+  LzfJob* d;
+  LzfJob* h = up_take<LzfJob>(cs, n, &d, st);
+  int32_t* d_err = call_err(cs, st);
+  if (!h || !d_err) return set_error(DG_ERR_OOM, "lzf jobs");
+  memcpy(h, db->lzf_jobs.data(), sizeof(LzfJob) * n);
+  DG_FLUSH(cs, st);
+  launch_lzf_decode(d, n, d_err, st);
+  return DG_OK;
+}
+
 static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr) {
+  int rcl = run_lzf(cs, db, st);
+  if (rcl) return rcl;
   if (db->jobs.empty()) return run_expands(cs, db, st);
   const int n = (int)db->jobs.size();
   // longest blocks first (token-dense blocks cost the most; workgroups dispatch in order, so this
@@ -864,13 +891,18 @@ int read_time_bounds(Segment* seg) {
   hipStream_t st = ctx->stream;
   const BlockColumn& b = t->data;
   int64_t* h = host_take<int64_t>(cs, 2);
-  if (b.vbits) {
-    // DELTA / TABLE __time: expand the column once and read its first and last row
+  if (b.vbits || b.codec == CODEC_LZF) {
+    // DELTA / TABLE or LZF __time: decode the column once and read its first and last row
     int rc0 = column_view(t, cs, &db, &v, st);
     if (!rc0) rc0 = run_decodes(cs, &db, st);
     if (rc0) return rc0;
-    DG_HIP(hipMemcpyAsync(h, db.last_expanded, 8, hipMemcpyDeviceToHost, st));
-    DG_HIP(hipMemcpyAsync(h + 1, db.last_expanded + (seg->nrows - 1), 8, hipMemcpyDeviceToHost, st));
+    const int64_t last = seg->nrows - 1;
+    const uint8_t* first_p = b.vbits ? reinterpret_cast<const uint8_t*>(db.last_expanded) : db.last_slots;
+    const uint8_t* last_p = b.vbits ? reinterpret_cast<const uint8_t*>(db.last_expanded + last)
+                                    : db.last_slots + (size_t)(last >> b.log2_per) * kBlockBytes +
+                                          (size_t)(last & ((1ll << b.log2_per) - 1)) * 8;
+    DG_HIP(hipMemcpyAsync(h, first_p, 8, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h + 1, last_p, 8, hipMemcpyDeviceToHost, st));
   } else if (b.codec == CODEC_LZ4) {
     // decode only the first and last block
     uint8_t* slots = dev_take<uint8_t>(cs, 2 * (size_t)kBlockBytes + 64);

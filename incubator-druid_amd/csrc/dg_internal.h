@@ -20,7 +20,7 @@ constexpr int kMaxAggs = 16;
 constexpr int kBlockBytes = 65536;  // CompressedPools.BUFFER_SIZE (segment/CompressedPools.java:39)
 
 // stored codecs (CompressionStrategy ids, data/CompressionStrategy.java:48-107)
-enum Codec : int32_t { CODEC_LZ4 = 0x01, CODEC_UNCOMPRESSED = 0xFF, CODEC_NONE = 0xFE };
+enum Codec : int32_t { CODEC_LZF = 0x00, CODEC_LZ4 = 0x01, CODEC_UNCOMPRESSED = 0xFF, CODEC_NONE = 0xFE };
 
 // value kinds a kernel can read from a column view
 enum ViewKind : int32_t { VIEW_ABSENT = 0, VIEW_LONG = 1, VIEW_FLOAT = 2, VIEW_DOUBLE = 3, VIEW_IDS = 4 };
@@ -53,6 +53,14 @@ struct Lz4Job {
   int32_t expect_len;  // bytes that must come out (>= rows * width of the block)
   int32_t ncp;         // number of checkpoints; < 0: the block failed validation at attach
   int32_t dec_len;     // decoded length found at attach
+};
+
+// One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
+struct LzfJob {
+  const uint8_t* src;
+  uint8_t* dst;
+  int32_t src_len;
+  int32_t expect_len;  // bytes that must come out
 };
 
 // Expansion of one block of a DELTA / TABLE long column (CompressionFactory.LongEncodingFormat,
@@ -238,6 +246,7 @@ int load_segment(Context* ctx, const char* dir, Segment** out);
 // kernel launchers (dg_kernels.hip)
 constexpr int kLz4ProfWords = 12;  // per-block phase stamps of the decoder (diagnostic builds of the call)
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // VSizeLongSerde.getSerializedSize (VSizeLongSerde.java:61-65)
 inline int64_t vsize_serialized(int bits, int64_t n) { return (bits * n + 7) / 8 + 4; }

@@ -1532,4 +1532,120 @@ void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32
   hipLaunchKernelGGL(k_vsize_expand, dim3(gx, (unsigned)njobs), dim3(256), 0, s, d_jobs, d_err);
 }
 
+// ------------------------------------------------------------------------------------------------
+// LZF blocks (CompressionStrategy.LZF, id 0x00 / LZF_VERSION columns): compress-lzf 1.0.4's chunk
+// stream ("ZV" + type 0 raw | type 1 liblzf, ChunkDecoder.decodeChunk). One wave per block: the
+// compressed block is staged into LDS with coalesced dword loads, the wave walks the tokens in
+// lockstep (every lane reads the same LDS token bytes, so control flow stays uniform) and copies
+// literal runs and back-references lane-parallel into an LDS output image (overlapping references
+// copy in rounds of their distance, so each round reads only finished bytes), which is then
+// written out with 16-byte stores. A malformed stream sets the error word.
+// ------------------------------------------------------------------------------------------------
+constexpr int kLzfInCap = 65536 + 64;
+
+__global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jobs, int32_t* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) uint8_t outb[kBlockBytes + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t inb[kLzfInCap + 16];
+  const LzfJob j = jobs[blockIdx.x];
+  const int lane = threadIdx.x;
+  const int n = j.src_len;
+  if (n > kLzfInCap || n < 0) {
+    if (lane == 0) atomicOr(err, 1);
+    return;
+  }
+  // stage: src is 16-byte aligned (packed at attach); tail bytes one by one
+  const int n16 = n >> 4;
+  for (int q = lane; q < n16; q += 64)
+    reinterpret_cast<uint4*>(inb)[q] = reinterpret_cast<const uint4*>(j.src)[q];
+  for (int b = (n16 << 4) + lane; b < n; b += 64) inb[b] = j.src[b];
+  __syncthreads();
+  int ip = 0, op = 0;
+  bool bad = false;
+  while (ip < n && !bad) {
+    if (ip + 5 > n || inb[ip] != 'Z' || inb[ip + 1] != 'V') {
+      bad = true;
+      break;
+    }
+    const int type = inb[ip + 2];
+    const int len = ((int)inb[ip + 3] << 8) | inb[ip + 4];
+    if (type == 0) {
+      ip += 5;
+      if (ip + len > n || op + len > kBlockBytes) {
+        bad = true;
+        break;
+      }
+      for (int k = lane; k < len; k += 64) outb[op + k] = inb[ip + k];
+      ip += len;
+      op += len;
+      __syncthreads();
+      continue;
+    }
+    if (type != 1 || ip + 7 > n) {
+      bad = true;
+      break;
+    }
+    const int ulen = ((int)inb[ip + 5] << 8) | inb[ip + 6];
+    ip += 7;
+    const int end = ip + len, oend = op + ulen;
+    if (end > n || oend > kBlockBytes) {
+      bad = true;
+      break;
+    }
+    while (ip < end) {
+      const int ctrl = inb[ip++];
+      if (ctrl < 32) {
+        const int run = ctrl + 1;
+        if (ip + run > end || op + run > oend) {
+          bad = true;
+          break;
+        }
+        if (lane < run) outb[op + lane] = inb[ip + lane];
+        ip += run;
+        op += run;
+      } else {
+        int l = ctrl >> 5;
+        if (l == 7) {
+          if (ip >= end) {
+            bad = true;
+            break;
+          }
+          l += inb[ip++];
+        }
+        if (ip >= end) {
+          bad = true;
+          break;
+        }
+        const int dist = ((ctrl & 31) << 8) + 1 + inb[ip++];
+        l += 2;
+        if (dist > op || op + l > oend) {
+          bad = true;
+          break;
+        }
+        const int step = dist < 64 ? dist : 64;
+        for (int s0 = 0; s0 < l; s0 += step) {
+          __syncthreads();  // the previous round's bytes are in place (one-wave workgroup)
+          if (lane < step && s0 + lane < l) outb[op + s0 + lane] = outb[op - dist + s0 + lane];
+        }
+        op += l;
+      }
+      __syncthreads();
+    }
+    if (!bad && op != oend) bad = true;
+  }
+  __syncthreads();
+  if (bad || op < j.expect_len) {
+    if (lane == 0) atomicOr(err, 1);
+    return;
+  }
+  const int o16 = op >> 4;
+  for (int q = lane; q < o16; q += 64)
+    reinterpret_cast<uint4*>(j.dst)[q] = reinterpret_cast<const uint4*>(outb)[q];
+  for (int b = (o16 << 4) + lane; b < op; b += 64) j.dst[b] = outb[b];
+}
+
+void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(k_lzf_decode, dim3((unsigned)njobs), dim3(64), 0, s, d_jobs, d_err);
+}
+
 }  // namespace dg

@@ -167,14 +167,14 @@ namespace {
 // Upload the blocks of a GenericIndexed of (compressed or raw) blocks.
 int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
   col->nblocks = blocks.n;
-  if (col->codec == CODEC_LZ4) {
+  if (col->codec == CODEC_LZ4 || col->codec == CODEC_LZF) {
     col->comp_off.resize(blocks.n);
     col->comp_len.resize(blocks.n);
     int64_t total = 0;
     for (int32_t b = 0; b < blocks.n; ++b) {
       const uint8_t* p;
       int32_t len = blocks.get(b, &p);
-      if (len <= 0) return set_error(DG_ERR_FORMAT, "empty LZ4 block %d", b);
+      if (len <= 0) return set_error(DG_ERR_FORMAT, "empty compressed block %d", b);
       col->comp_off[b] = total;
       col->comp_len[b] = len;
       total += (len + 15) & ~15;
@@ -188,6 +188,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     }
     if (!col->comp.alloc(host.size())) return set_error(DG_ERR_OOM, "hipMalloc %zu", host.size());
     DG_HIP(hipMemcpy(col->comp.p, host.data(), host.size(), hipMemcpyHostToDevice));
+    if (col->codec == CODEC_LZF) return DG_OK;  // decoded sequentially per block: no index
     // sequence checkpoints of every block (host threads over blocks; validated parse)
     col->cp_off.assign(blocks.n, 0);
     col->cp_n.assign(blocks.n, -1);
@@ -338,13 +339,20 @@ int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
   // [u8 version][i32 total][i32 sizePer][u8 compression (maybe flagged)][encoding?][blocks | values]
   if (s.left() < 10) return set_error(DG_ERR_FORMAT, "%s: truncated numeric column", c->name.c_str());
   uint8_t version = s.p[0];
-  if (version != 0x02) return set_error(DG_ERR_UNSUPPORTED, "%s: numeric column version %d (LZF)", c->name.c_str(), version);
+  if (version != 0x02 && version != 0x01)
+    return set_error(DG_ERR_FORMAT, "%s: Unknown version[%d]", c->name.c_str(), version);
   BlockColumn& col = c->data;
   col.total = be32(s.p + 1);
   col.size_per = be32(s.p + 5);
-  int8_t cid = (int8_t)s.p[9];
-  s.p += 10;
-  if (cid < (int8_t)0xFE) {  // CompressionFactory.hasEncodingFlag
+  int8_t cid;
+  if (version == 0x01) {  // LZF_VERSION: no compression byte, LZF blocks (CompressedColumnarLongsSupplier:104-116)
+    cid = (int8_t)CODEC_LZF;
+    s.p += 9;
+  } else {
+    cid = (int8_t)s.p[9];
+    s.p += 10;
+  }
+  if (version == 0x02 && cid < (int8_t)0xFE) {  // CompressionFactory.hasEncodingFlag
     uint8_t enc = *s.p++;
     cid = (int8_t)(cid + 126);
     if (enc != 0xFF) {
@@ -370,7 +378,8 @@ int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
     if (rows <= 0) continue;
     const int64_t need = (col.vbits * rows + 7) / 8;
     const uint8_t* bp;
-    const int64_t have = col.codec == CODEC_LZ4 ? col.dec_len[k] : blocks.get(k, &bp);
+    // LZF blocks carry no decoded length until decoded: k_lzf_decode checks it against the expectation
+    const int64_t have = col.codec == CODEC_LZ4 ? col.dec_len[k] : (col.codec == CODEC_LZF ? -1 : blocks.get(k, &bp));
     if (have >= 0 && have < need)
       return set_error(DG_ERR_FORMAT, "%s: packed block %d holds %lld of %lld bytes", c->name.c_str(), k,
                        (long long)have, (long long)need);

@@ -163,3 +163,86 @@ int64_t dgt_concise_encode_column(const int32_t* ids, int64_t n_rows, int32_t ca
   free(rows);
   return total;
 }
+
+/* ---- LZF encoder for the segment writer (compress-lzf 1.0.4 chunk format, what
+ * CompressionStrategy.LZFCompressor writes through LZFEncoder.appendEncoded): the input is cut
+ * into chunks of at most 65535 bytes; each chunk is "ZV" + type 1 + u16 BE compressed length +
+ * u16 BE uncompressed length + liblzf data, or "ZV" + type 0 + u16 BE length + raw bytes when
+ * compression does not pay. liblzf data: ctrl < 32 -> ctrl + 1 literals; otherwise a back-reference
+ * of length (ctrl >> 5) + 2 (7 -> + next byte) at distance ((ctrl & 31) << 8 | next) + 1. ---- */
+static int64_t lzf_chunk(const uint8_t* in, int n, uint8_t* out) {
+  enum { HBITS = 14, MAX_OFF = 8192, MAX_REF = 264, MAX_LIT = 32 };
+  static int32_t table[1 << HBITS];
+  for (int i = 0; i < (1 << HBITS); ++i) table[i] = -1;
+  int64_t op = 0;
+  int lit_start = 0, ip = 0;
+#define FLUSH_LITS(upto)                                 \
+  while (lit_start < (upto)) {                           \
+    int run = (upto) - lit_start;                        \
+    if (run > MAX_LIT) run = MAX_LIT;                    \
+    out[op++] = (uint8_t)(run - 1);                      \
+    memcpy(out + op, in + lit_start, (size_t)run);       \
+    op += run;                                           \
+    lit_start += run;                                    \
+  }
+  while (ip + 2 < n) {
+    uint32_t h = ((uint32_t)in[ip] << 16 | (uint32_t)in[ip + 1] << 8 | in[ip + 2]) * 2654435761u >> (32 - HBITS);
+    int32_t ref = table[h];
+    table[h] = ip;
+    if (ref >= 0 && ip - ref <= MAX_OFF && in[ref] == in[ip] && in[ref + 1] == in[ip + 1] && in[ref + 2] == in[ip + 2]) {
+      int len = 3;
+      while (len < MAX_REF && ip + len < n && in[ref + len] == in[ip + len]) len++;
+      FLUSH_LITS(ip);
+      int off = ip - ref - 1, l = len - 2;
+      if (l < 7) {
+        out[op++] = (uint8_t)((l << 5) | (off >> 8));
+      } else {
+        out[op++] = (uint8_t)((7 << 5) | (off >> 8));
+        out[op++] = (uint8_t)(l - 7);
+      }
+      out[op++] = (uint8_t)(off & 0xFF);
+      ip += len;
+      lit_start = ip;
+    } else {
+      ip++;
+    }
+  }
+  FLUSH_LITS(n);
+#undef FLUSH_LITS
+  return op;
+}
+
+int64_t dgt_lzf_compress(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap) {
+  int64_t op = 0;
+  uint8_t* tmp = (uint8_t*)malloc(65535 * 2 + 64);
+  for (int64_t pos = 0; pos < n || (n == 0 && pos == 0); ) {
+    int len = (int)(n - pos > 65535 ? 65535 : n - pos);
+    int64_t c = lzf_chunk(in + pos, len, tmp);
+    int64_t need = c < len ? 7 + c : 5 + len;
+    if (op + need > cap) {
+      free(tmp);
+      return -1;
+    }
+    out[op++] = 'Z';
+    out[op++] = 'V';
+    if (c < len) {
+      out[op++] = 1;
+      out[op++] = (uint8_t)(c >> 8);
+      out[op++] = (uint8_t)c;
+      out[op++] = (uint8_t)(len >> 8);
+      out[op++] = (uint8_t)len;
+      memcpy(out + op, tmp, (size_t)c);
+      op += c;
+    } else {
+      out[op++] = 0;
+      out[op++] = (uint8_t)(len >> 8);
+      out[op++] = (uint8_t)len;
+      memcpy(out + op, in + pos, (size_t)len);
+      op += len;
+    }
+    pos += len;
+    if (n == 0) break;
+  }
+  free(tmp);
+  return op;
+}

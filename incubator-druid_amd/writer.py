@@ -138,6 +138,8 @@ def _compress_blocks(raw: bytes, block_bytes: int, compression: str, lz4_mode: s
         chunk = raw[off:off + block_bytes]
         if compression == "lz4":
             blocks.append(lz4_compress(chunk, lz4_mode))
+        elif compression == "lzf":
+            blocks.append(_tools.lzf_compress(chunk))
         elif compression == "uncompressed":
             blocks.append(chunk)
         else:
@@ -234,6 +236,8 @@ def packed_long_column_part(values: np.ndarray, compression: str, lz4_mode: str,
         chunk = vsize_pack(packed[off:off + size_per], bits)
         if compression == "lz4":
             blocks.append(lz4_compress(chunk, lz4_mode))
+        elif compression == "lzf":
+            blocks.append(_tools.lzf_compress(chunk))
         elif compression == "uncompressed":
             blocks.append(chunk)
         else:
@@ -255,6 +259,11 @@ def numeric_column_part(values: np.ndarray, kind: str, compression: str, lz4_mod
     arr = np.ascontiguousarray(values, dtype=dtype)
     width = arr.dtype.itemsize
     size_per = BUFFER_SIZE // width  # 8192 longs/doubles, 16384 floats
+    if compression == "lzf_v1":
+        # LZF_VERSION (0x01) columns of older segments: no compression byte, LZF blocks
+        # (CompressedColumnarLongsSupplier.fromByteBuffer, :102-116)
+        return struct.pack(">Bii", 0x01, len(arr), size_per) + \
+            _blocks_generic_indexed(_compress_blocks(arr.tobytes(), size_per * width, "lzf", lz4_mode))
     cid = COMPRESSION_IDS[compression]
     header = struct.pack(">Bii", 0x02, len(arr), size_per) + bytes([cid])
     raw = arr.tobytes()
@@ -499,7 +508,8 @@ def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", comp
     ts = np.asarray(spec.timestamps, dtype=np.int64)
     if n and np.any(np.diff(ts) < 0):
         raise ValueError("segment rows must be sorted by __time")
-    dim_comp = dim_compression or ("uncompressed" if compression == "none" else compression)
+    dim_comp = dim_compression or ("uncompressed" if compression == "none" else
+                                   "lzf" if compression == "lzf_v1" else compression)
     files: Dict[str, bytes] = {}
     files["__time"] = _descriptor("LONG", {"type": "long", "byteOrder": "LITTLE_ENDIAN"}) + \
         numeric_column_part(ts, "long", compression, lz4_mode, long_encoding)

@@ -379,9 +379,11 @@ static int parse_numeric(ocol* c, const uint8_t* p) {
   c->size_per = be32(p + 5);
   int8_t cid = (int8_t)p[9];
   const uint8_t* q = p + 10;
-  if (p[0] == 0x01) {
-    c->compression = 0x00; /* LZF legacy: unsupported */
-    return -1;
+  if (p[0] == 0x01) { /* LZF_VERSION: no compression byte, LZF blocks, legacy LONGS encoding */
+    c->compression = 0x00;
+    c->long_enc = 0xFF;
+    q = p + 9;
+    return gi_read(&q, c->end, &c->blocks);
   }
   if (cid < (int8_t)0xFE) { /* CompressionFactory.hasEncodingFlag */
     uint8_t enc = *q++;
@@ -625,11 +627,65 @@ int or_column_kind(void* h, const char* name) {
   return c ? c->kind : OR_MISSING;
 }
 
+/* compress-lzf 1.0.4 LZFDecoder.decode restated (the library is a pom dependency, not vendored):
+ * a sequence of chunks "ZV" + type; type 0 = u16 BE length + raw bytes, type 1 = u16 BE compressed
+ * length + u16 BE uncompressed length + liblzf data (ChunkDecoder.decodeChunk: ctrl < 32 -> ctrl + 1
+ * literals, else length (ctrl >> 5) + 2 with 7 extended by the next byte, back-reference distance
+ * ((ctrl & 31) << 8 | next) + 1, copied byte by byte so overlaps repeat). Returns decoded bytes or -1. */
+int64_t or_lzf_decompress(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap) {
+  int64_t ip = 0, op = 0;
+  while (ip < n) {
+    if (ip + 5 > n || in[ip] != 'Z' || in[ip + 1] != 'V') return -1;
+    const int type = in[ip + 2];
+    const int64_t len = ((int64_t)in[ip + 3] << 8) | in[ip + 4];
+    if (type == 0) {
+      ip += 5;
+      if (ip + len > n || op + len > cap) return -1;
+      memcpy(out + op, in + ip, (size_t)len);
+      ip += len;
+      op += len;
+    } else if (type == 1) {
+      if (ip + 7 > n) return -1;
+      const int64_t ulen = ((int64_t)in[ip + 5] << 8) | in[ip + 6];
+      ip += 7;
+      const int64_t end = ip + len, oend = op + ulen;
+      if (end > n || oend > cap) return -1;
+      while (ip < end) {
+        int ctrl = in[ip++];
+        if (ctrl < 32) {
+          int64_t run = ctrl + 1;
+          if (ip + run > end || op + run > oend) return -1;
+          memcpy(out + op, in + ip, (size_t)run);
+          ip += run;
+          op += run;
+        } else {
+          int64_t l = ctrl >> 5;
+          if (l == 7) {
+            if (ip >= end) return -1;
+            l += in[ip++];
+          }
+          if (ip >= end) return -1;
+          int64_t ref = op - ((int64_t)(ctrl & 31) << 8) - 1 - in[ip++];
+          l += 2;
+          if (ref < 0 || op + l > oend) return -1;
+          for (int64_t k = 0; k < l; ++k) out[op + k] = out[ref + k];
+          op += l;
+        }
+      }
+      if (op != oend) return -1;
+    } else {
+      return -1;
+    }
+  }
+  return op;
+}
+
 /* decode block i of a block-layout column into dst (cap bytes); returns decoded bytes */
 static int64_t decode_block(ocol* c, int32_t i, uint8_t* dst, int64_t cap) {
   const uint8_t* p;
   int32_t len = gi_get(&c->blocks, i, &p);
   if (c->compression == 0x01) return or_lz4_decompress(p, len, dst, cap);
+  if (c->compression == 0x00) return or_lzf_decompress(p, len, dst, cap);
   if (c->compression == 0xFF) {
     if (len > cap) return -1;
     memcpy(dst, p, (size_t)len);

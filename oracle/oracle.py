@@ -81,6 +81,8 @@ def lib():
         l.or_agg_combine.argtypes = [ctypes.c_int, i32, vp, vp]
         l.or_lz4_decompress.restype = i64
         l.or_lz4_decompress.argtypes = [vp, i64, vp, i64]
+        l.or_lzf_decompress.restype = i64
+        l.or_lzf_decompress.argtypes = [vp, i64, vp, i64]
         l.or_concise_decode.restype = i64
         l.or_concise_decode.argtypes = [vp, i64, vp, i64]
         l.or_roaring_decode.restype = i64
@@ -91,6 +93,16 @@ def lib():
         l.or_vsize_get.argtypes = [ctypes.c_int, vp, i64]
         _lib = l
     return _lib
+
+
+def lzf_decompress(data: bytes, cap: int = 65536 + 16) -> bytes:
+    """LZFDecoder.decode (compress-lzf 1.0.4), restated in druid_oracle.c."""
+    out = ctypes.create_string_buffer(cap)
+    src = ctypes.create_string_buffer(bytes(data), len(data))
+    n = lib().or_lzf_decompress(src, len(data), out, cap)
+    if n < 0:
+        raise ValueError("malformed LZF stream")
+    return out.raw[:n]
 
 
 def bits_for_max(value: int) -> int:
