@@ -158,7 +158,7 @@ def main():
     ap.add_argument("--config", default="topn", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--segments", type=int, default=None)
-    ap.add_argument("--compression", default="lz4", choices=["lz4", "uncompressed", "none"])
+    ap.add_argument("--compression", default="lz4", choices=["lz4", "lzf", "uncompressed", "none"])
     ap.add_argument("--bitmap", default="concise", choices=["concise", "roaring"])
     ap.add_argument("--lz4-mode", default="hc", choices=["hc", "fast"])
     ap.add_argument("--long-encoding", default="longs", choices=["longs", "auto"],
@@ -261,7 +261,7 @@ def main():
     elif args.config.startswith("topn_"):
         uncompressed_equiv = scanned_local * (3 + 8)
     if decode_ms >= agg_ms and decode_ms > 0:
-        kernel, k_ms, k_bytes = "k_lz4_decode", decode_ms, bytes_read
+        kernel, k_ms, k_bytes = ("k_lzf_decode" if args.compression == "lzf" else "k_lz4_decode"), decode_ms, bytes_read
         if args.long_encoding == "auto":
             kernel = "k_lz4_decode+k_vsize_expand"  # the decode phase holds both launches
     else:
