@@ -1537,8 +1537,8 @@ void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32
 // stream ("ZV" + type 0 raw | type 1 liblzf, ChunkDecoder.decodeChunk). One wave per block: the
 // compressed block is staged into LDS with coalesced dword loads, the wave walks the tokens in
 // lockstep (every lane reads the same LDS token bytes, so control flow stays uniform) and copies
-// literal runs and back-references lane-parallel into an LDS output image (overlapping references
-// copy in rounds of their distance, so each round reads only finished bytes), which is then
+// literal runs and back-references lane-parallel into an LDS output image (an overlapping reference
+// is the periodic extension of its last `dist` bytes, copied in one pass), which is then
 // written out with 16-byte stores. A malformed stream sets the error word.
 // ------------------------------------------------------------------------------------------------
 constexpr int kLzfInCap = 65536 + 64;
@@ -1566,8 +1566,8 @@ __global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jo
       bad = true;
       break;
     }
-    const int type = inb[ip + 2];
-    const int len = ((int)inb[ip + 3] << 8) | inb[ip + 4];
+    const int type = __builtin_amdgcn_readfirstlane(inb[ip + 2]);
+    const int len = __builtin_amdgcn_readfirstlane(((int)inb[ip + 3] << 8) | inb[ip + 4]);
     if (type == 0) {
       ip += 5;
       if (ip + len > n || op + len > kBlockBytes) {
@@ -1584,7 +1584,7 @@ __global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jo
       bad = true;
       break;
     }
-    const int ulen = ((int)inb[ip + 5] << 8) | inb[ip + 6];
+    const int ulen = __builtin_amdgcn_readfirstlane(((int)inb[ip + 5] << 8) | inb[ip + 6]);
     ip += 7;
     const int end = ip + len, oend = op + ulen;
     if (end > n || oend > kBlockBytes) {
@@ -1592,7 +1592,13 @@ __global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jo
       break;
     }
     while (ip < end) {
-      const int ctrl = inb[ip++];
+      // one 4-byte peek (two aligned LDS dwords) yields ctrl and both back-reference bytes
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(inb);
+      const uint64_t pw = (uint64_t)w[ip >> 2] | ((uint64_t)w[(ip >> 2) + 1] << 32);
+      // every lane holds the same token: make it wave-uniform so the token branches are scalar
+      const uint32_t tok = __builtin_amdgcn_readfirstlane((uint32_t)(pw >> ((ip & 3) * 8)));
+      const int ctrl = tok & 0xFF;
+      ip++;
       if (ctrl < 32) {
         const int run = ctrl + 1;
         if (ip + run > end || op + run > oend) {
@@ -1604,27 +1610,32 @@ __global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jo
         op += run;
       } else {
         int l = ctrl >> 5;
+        int offb;
         if (l == 7) {
-          if (ip >= end) {
-            bad = true;
-            break;
-          }
-          l += inb[ip++];
+          l += (tok >> 8) & 0xFF;
+          offb = (tok >> 16) & 0xFF;
+          ip += 2;
+        } else {
+          offb = (tok >> 8) & 0xFF;
+          ip += 1;
         }
-        if (ip >= end) {
+        if (ip > end) {
           bad = true;
           break;
         }
-        const int dist = ((ctrl & 31) << 8) + 1 + inb[ip++];
+        const int dist = ((ctrl & 31) << 8) + 1 + offb;
         l += 2;
         if (dist > op || op + l > oend) {
           bad = true;
           break;
         }
-        const int step = dist < 64 ? dist : 64;
-        for (int s0 = 0; s0 < l; s0 += step) {
-          __syncthreads();  // the previous round's bytes are in place (one-wave workgroup)
-          if (lane < step && s0 + lane < l) outb[op + s0 + lane] = outb[op - dist + s0 + lane];
+        // an overlapping reference repeats its last `dist` bytes: byte k of the copy is
+        // out[op - dist + k % dist], all of which precede op, so one lane-parallel pass suffices
+        __syncthreads();
+        if (dist >= l) {
+          for (int k = lane; k < l; k += 64) outb[op + k] = outb[op - dist + k];
+        } else {
+          for (int k = lane; k < l; k += 64) outb[op + k] = outb[op - dist + k % dist];
         }
         op += l;
       }
