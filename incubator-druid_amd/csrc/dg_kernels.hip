@@ -1536,45 +1536,62 @@ void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32
 // LZF blocks (CompressionStrategy.LZF, id 0x00 / LZF_VERSION columns): compress-lzf 1.0.4's chunk
 // stream ("ZV" + type 0 raw | type 1 liblzf, ChunkDecoder.decodeChunk). One wave per block: the
 // compressed block is staged into LDS with coalesced dword loads, the wave walks the tokens in
-// lockstep (every lane reads the same LDS token bytes, so control flow stays uniform) and copies
+// lockstep (every lane reads the same LDS token bytes, so control flow stays uniform; the input is
+// staged through an 8 KiB LDS window so two workgroups fit a CU) and copies
 // literal runs and back-references lane-parallel into an LDS output image (an overlapping reference
 // is the periodic extension of its last `dist` bytes, copied in one pass), which is then
 // written out with 16-byte stores. A malformed stream sets the error word.
 // ------------------------------------------------------------------------------------------------
-constexpr int kLzfInCap = 65536 + 64;
+constexpr int kLzfWin = 8192;  // staged input window: 64 KiB output + 8 KiB input -> two workgroups per CU
 
 __global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jobs, int32_t* __restrict__ err) {
   __shared__ __attribute__((aligned(16))) uint8_t outb[kBlockBytes + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t inb[kLzfInCap + 16];
+  __shared__ __attribute__((aligned(16))) uint32_t win[kLzfWin / 4 + 4];
   const LzfJob j = jobs[blockIdx.x];
   const int lane = threadIdx.x;
   const int n = j.src_len;
-  if (n > kLzfInCap || n < 0) {
-    if (lane == 0) atomicOr(err, 1);
-    return;
-  }
-  // stage: src is 16-byte aligned (packed at attach); tail bytes one by one
-  const int n16 = n >> 4;
-  for (int q = lane; q < n16; q += 64)
-    reinterpret_cast<uint4*>(inb)[q] = reinterpret_cast<const uint4*>(j.src)[q];
-  for (int b = (n16 << 4) + lane; b < n; b += 64) inb[b] = j.src[b];
-  __syncthreads();
+  const uint8_t* winb = reinterpret_cast<const uint8_t*>(win);
+  int wb = 0, we = 0;  // window = input bytes [wb, we), wb 4-byte aligned (src is 16-byte aligned)
+  // (re)stage the window at ip when fewer than 48 bytes (chunk header, longest token + literals) remain
+  auto refill = [&](int ip) {
+    if (ip + 48 <= we || we >= n) return;
+    __syncthreads();
+    wb = ip & ~3;
+    we = min(n, wb + kLzfWin);
+    const int ndw = (we - wb + 3) >> 2;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(j.src + wb);
+    const int full = (n - wb) >> 2;  // whole dwords inside the block
+    for (int q = lane; q < ndw; q += 64) {
+      uint32_t v;
+      if (q < full) {
+        v = src[q];
+      } else {
+        v = 0;
+        for (int b = 0; b < 4 && wb + 4 * q + b < n; ++b) v |= (uint32_t)j.src[wb + 4 * q + b] << (8 * b);
+      }
+      win[q] = v;
+    }
+    if (lane < 4) win[ndw + lane] = 0;
+    __syncthreads();
+  };
+  auto in8 = [&](int x) -> int { return winb[x - wb]; };
   int ip = 0, op = 0;
   bool bad = false;
   while (ip < n && !bad) {
-    if (ip + 5 > n || inb[ip] != 'Z' || inb[ip + 1] != 'V') {
+    refill(ip);
+    if (ip + 5 > n || in8(ip) != 'Z' || in8(ip + 1) != 'V') {
       bad = true;
       break;
     }
-    const int type = __builtin_amdgcn_readfirstlane(inb[ip + 2]);
-    const int len = __builtin_amdgcn_readfirstlane(((int)inb[ip + 3] << 8) | inb[ip + 4]);
-    if (type == 0) {
+    const int type = __builtin_amdgcn_readfirstlane(in8(ip + 2));
+    const int len = __builtin_amdgcn_readfirstlane((in8(ip + 3) << 8) | in8(ip + 4));
+    if (type == 0) {  // raw chunk: straight from global memory
       ip += 5;
       if (ip + len > n || op + len > kBlockBytes) {
         bad = true;
         break;
       }
-      for (int k = lane; k < len; k += 64) outb[op + k] = inb[ip + k];
+      for (int k = lane; k < len; k += 64) outb[op + k] = j.src[ip + k];
       ip += len;
       op += len;
       __syncthreads();
@@ -1584,7 +1601,7 @@ __global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jo
       bad = true;
       break;
     }
-    const int ulen = __builtin_amdgcn_readfirstlane(((int)inb[ip + 5] << 8) | inb[ip + 6]);
+    const int ulen = __builtin_amdgcn_readfirstlane((in8(ip + 5) << 8) | in8(ip + 6));
     ip += 7;
     const int end = ip + len, oend = op + ulen;
     if (end > n || oend > kBlockBytes) {
@@ -1592,11 +1609,12 @@ __global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jo
       break;
     }
     while (ip < end) {
+      refill(ip);
       // one 4-byte peek (two aligned LDS dwords) yields ctrl and both back-reference bytes
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(inb);
-      const uint64_t pw = (uint64_t)w[ip >> 2] | ((uint64_t)w[(ip >> 2) + 1] << 32);
+      const int x = ip - wb;
+      const uint64_t pw = (uint64_t)win[x >> 2] | ((uint64_t)win[(x >> 2) + 1] << 32);
       // every lane holds the same token: make it wave-uniform so the token branches are scalar
-      const uint32_t tok = __builtin_amdgcn_readfirstlane((uint32_t)(pw >> ((ip & 3) * 8)));
+      const uint32_t tok = __builtin_amdgcn_readfirstlane((uint32_t)(pw >> ((x & 3) * 8)));
       const int ctrl = tok & 0xFF;
       ip++;
       if (ctrl < 32) {
@@ -1605,7 +1623,7 @@ __global__ __launch_bounds__(64) void k_lzf_decode(const LzfJob* __restrict__ jo
           bad = true;
           break;
         }
-        if (lane < run) outb[op + lane] = inb[ip + lane];
+        if (lane < run) outb[op + lane] = winb[ip - wb + lane];
         ip += run;
         op += run;
       } else {
