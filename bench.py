@@ -131,7 +131,7 @@ def ensure_segments(DG, root, rank, nseg, rows, compression, bitmap, lz4_mode, p
     return paths
 
 
-def cpu_baseline(Q, query, path, rows, seconds):
+def cpu_baseline(Q, query, path, rows, seconds, codec="lz4"):
     """The oracle (scalar CPU restatement of the reference loops) on one segment, fresh decode each run."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
@@ -147,7 +147,7 @@ def cpu_baseline(Q, query, path, rows, seconds):
             break
     return {"value": rows * runs / el, "unit": "rows/s", "cores": 1, "kind": "port",
             "sample": f"{runs} run(s) of the query over 1 segment x {rows} rows (oracle/ C+numpy restatement, "
-                      f"single thread, LZ4 decode included), {el:.1f} s"}
+                      f"single thread, {codec.upper()} decode included), {el:.1f} s"}
 
 
 def main():
@@ -294,7 +294,7 @@ def main():
         "rows_scanned_per_step": scanned_local * world,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(Q, query, paths[0], rows_per, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(Q, query, paths[0], rows_per, args.cpu_seconds, args.compression)
         line["cpu_baseline"]["cpu_model"] = _cpu_model()
     if rank == 0:
         print(json.dumps(line), flush=True)
