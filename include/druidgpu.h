@@ -64,8 +64,9 @@ extern "C" {
 #define DG_COL_LONG 1
 #define DG_COL_FLOAT 2
 #define DG_COL_DOUBLE 3
-#define DG_COL_STRING 4
-#define DG_COL_UNSUPPORTED 5 /* complex / multi-value / unsupported codec */
+#define DG_COL_STRING 4      /* single- or multi-value (V3 / UNCOMPRESSED_MULTI_VALUE: bitmap filters only,
+                                grouping on it -> DG_ERR_UNSUPPORTED) */
+#define DG_COL_UNSUPPORTED 5 /* complex / legacy non-V3 compressed multi-value / unsupported codec */
 
 /* aggregator kinds (query/aggregation/...AggregatorFactory.java) */
 #define DG_AGG_COUNT 0
