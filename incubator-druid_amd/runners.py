@@ -555,10 +555,21 @@ def merge_topn(query: Q.TopNQuery, per_segment: List[List[Q.Result]]) -> List[Q.
 # groupBy
 # ----------------------------------------------------------------------------------------------
 class GroupByPartial:
-    """Columnar per-segment groupBy output: bucket times, dimension values, aggregate columns."""
+    """Columnar per-segment groupBy output: bucket times, dimension values, aggregate columns.
+    Engine partials also carry `codes` (segment-local dictionary ids per dimension) and `dicts` (the
+    segments' sorted dictionaries): the merge then works on integer codes, and the value columns are
+    only materialised when asked for."""
 
-    def __init__(self, times: np.ndarray, dims: List[np.ndarray], aggs: List[np.ndarray]):
-        self.times, self.dims, self.aggs = times, dims, aggs
+    def __init__(self, times: np.ndarray, dims: Optional[List[np.ndarray]], aggs: List[np.ndarray],
+                 codes: Optional[List[np.ndarray]] = None, dicts: Optional[List[List[Optional[str]]]] = None):
+        self.times, self._dims, self.aggs = times, dims, aggs
+        self.codes, self.dicts = codes, dicts
+
+    @property
+    def dims(self) -> List[np.ndarray]:
+        if self._dims is None:
+            self._dims = [np.array(dd, dtype=object)[c] for c, dd in zip(self.codes, self.dicts)]
+        return self._dims
 
     def __len__(self):
         return len(self.times)
@@ -590,12 +601,10 @@ def groupby_per_segment(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
                 vals = np.zeros(max(ng * na, 1), dtype=np.uint64)
                 N.check(N.lib().dg_result_fetch_groups(res, k, t.ctypes.data, ids.ctypes.data, vals.ctypes.data))
                 ids = ids[:ng * nd].reshape(ng, nd) if nd else np.zeros((ng, 0), np.int32)
-                dim_cols = []
-                for d, dname in enumerate(query.dimensions):
-                    dictionary = np.array(segs[k].dictionary(dname), dtype=object)
-                    dim_cols.append(dictionary[ids[:, d]] if ng else np.zeros(0, dtype=object))
+                codes = [np.ascontiguousarray(ids[:, d]) for d in range(nd)]
+                dicts = [segs[k].dictionary(dname) for dname in query.dimensions]
                 agg_cols = _decode_slots(query.aggregations, vals[:ng * na].reshape(ng, na)) if na else []
-                out[i] = GroupByPartial(t[:ng], dim_cols, agg_cols)
+                out[i] = GroupByPartial(t[:ng], None, agg_cols, codes, dicts)
         finally:
             N.lib().dg_result_release(res)
     return out  # type: ignore
@@ -612,21 +621,55 @@ def merge_groupby_columnar(query: Q.GroupByQuery, partials: Sequence[GroupByPart
     keys_t = times if not gran.is_all else np.zeros(len(times), np.int64)
     dim_codes = []
     dim_values = []
+    coded = all(p.codes is not None for p in parts)
     for d in range(nd):
+        if coded:
+            # segment dictionaries are sorted (GenericIndexed STRING_STRATEGY): merge them into one
+            # global dictionary and remap each segment's ids with one vectorised lookup
+            dicts = [p.dicts[d] for p in parts]
+            if all(dd is dicts[0] or dd == dicts[0] for dd in dicts[1:]):
+                uniq, maps = list(dicts[0]), [None] * len(parts)
+            else:
+                uniq = sorted(set().union(*map(set, dicts)), key=_java_key)
+                index = {v: i for i, v in enumerate(uniq)}
+                maps = [np.array([index[v] for v in dd], dtype=np.int64) for dd in dicts]
+            dim_codes.append(np.concatenate([p.codes[d].astype(np.int64) if m is None else m[p.codes[d]]
+                                             for p, m in zip(parts, maps)]))
+            dim_values.append(np.array(uniq, dtype=object))
+            continue
         col = np.concatenate([p.dims[d] for p in parts])
         uniq = sorted(set(col.tolist()), key=_java_key)  # global dictionary in Java order, null first
         index = {v: i for i, v in enumerate(uniq)}
         dim_codes.append(np.fromiter((index[v] for v in col), dtype=np.int64, count=len(col)))
         dim_values.append(np.array(uniq, dtype=object))
     order_keys = [keys_t] + dim_codes
-    order = np.lexsort(tuple(reversed(order_keys)))
-    sk = [k[order] for k in order_keys]
-    change = np.ones(len(order), dtype=bool)
-    if len(order) > 1:
-        diff = np.zeros(len(order) - 1, dtype=bool)
-        for k in sk:
-            diff |= k[1:] != k[:-1]
-        change[1:] = diff
+    # one composite int64 key (time rank, then each dimension's code) when the ranges fit: a single
+    # argsort instead of a multi-key lexsort
+    if len(keys_t) and keys_t.min() == keys_t.max():
+        t_rank, n_t = np.zeros(len(keys_t), np.int64), 1
+    else:
+        t_vals, t_rank = np.unique(keys_t, return_inverse=True)
+        n_t = len(t_vals)
+    radices = [n_t] + [len(v) for v in dim_values]
+    if float(np.prod([float(r) for r in radices])) < 2.0 ** 62:
+        comp = t_rank.astype(np.int64)
+        for c, r in zip(dim_codes, radices[1:]):
+            comp = comp * r + c
+        order = np.argsort(comp)  # equal keys are folded below; introsort is deterministic
+        sc = comp[order]
+        change = np.ones(len(order), dtype=bool)
+        if len(order) > 1:
+            change[1:] = sc[1:] != sc[:-1]
+        sk = [k[order] for k in order_keys]
+    else:
+        order = np.lexsort(tuple(reversed(order_keys)))
+        sk = [k[order] for k in order_keys]
+        change = np.ones(len(order), dtype=bool)
+        if len(order) > 1:
+            diff = np.zeros(len(order) - 1, dtype=bool)
+            for k in sk:
+                diff |= k[1:] != k[:-1]
+            change[1:] = diff
     starts = np.nonzero(change)[0]
     out_aggs = []
     for a_i, a in enumerate(query.aggregations):
