@@ -22,8 +22,10 @@
  *   dg_segment_set_dim_order <- StringComparator.compare over one dictionary (query/ordering/StringComparators.java),
  *                               the order DimensionTopNMetricSpec / TopNLexicographicResultBuilder ranks values by
  *   dg_topn_merge            <- TopNBinaryFn.apply fold of QueryRunnerFactory.mergeRunners (query/topn/TopNBinaryFn.java:75-135)
- *   dg_groupby_run           <- GroupByStrategyV2.process -> GroupByQueryEngineV2.process
+ *   dg_groupby_run           <- GroupByStrategyV2.process -> GroupByQueryEngineV2.process per segment
  *                               (query/groupby/strategy/GroupByStrategyV2.java:472-477, epinephelinae/GroupByQueryEngineV2.java:91-187)
+ *                               + GroupByStrategyV2.mergeRunners -> GroupByMergingQueryRunnerV2.run (:170-290)
+ *   dg_result_*              <- the merged grouper's sorted iterator (ConcurrentGrouper.iterator(true))
  *
  * Segment arrays: every *_run takes n_segs segments that are attached to the SAME context (device)
  * and runs them as one batched launch sequence; results stay per segment, exactly as the
@@ -46,7 +48,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 2
+#define DG_ABI_VERSION 3
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -258,19 +260,34 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* scan, const dg_topn* t
                   int32_t* out_n, int32_t* out_list, int64_t* out_keys, uint64_t* out_values);
 
 /* ---- groupBy (v2) ---- */
+/* GroupByStrategyV2.mergeRunners over the call's segments: every segment's rows grouped
+ * (GroupByQueryEngineV2.process, epinephelinae/GroupByQueryEngineV2.java:91-187) and merged by
+ * (bucket, dimension values) like GroupByMergingQueryRunnerV2 (:170-290), in that order. A call
+ * with one segment is that segment's runner (createRunner(segment).run). The groups stay in HBM in
+ * the dg_result until fetched (page by page for large results). */
 typedef struct {
   const char* const* dimensions;
   int32_t n_dims;
 } dg_groupby;
 
-/* Runs the grouping; results are kept in a dg_result until fetched. */
 int dg_groupby_run(dg_segment* const* segs, int32_t n_segs, const dg_scan* scan, const dg_groupby* g,
                    dg_result** out, dg_metrics* metrics);
-/* number of groups of segment i */
-int64_t dg_result_groups(const dg_result* res, int32_t seg_index);
-/* bucket_time[n], ids[n * n_dims] (segment-local dictionary ids), values[n * n_aggs] slots */
-int dg_result_fetch_groups(dg_result* res, int32_t seg_index, int64_t* bucket_time, int32_t* ids,
+/* number of merged groups */
+int64_t dg_result_groups(const dg_result* res);
+/* groups [start, start + count), in result order (bucket time, then dimension values in Java
+ * String order, nulls first): bucket_time[count] (ALL granularity: the universal timestamp = the
+ * query interval's start, GroupByStrategyV2.getUniversalTimestamp :125-138), ids[count * n_dims]
+ * = indices into the result's merged dictionary of each dimension, values[count * n_aggs] in the
+ * slot encoding of dg_timeseries_run. Any output pointer may be NULL. */
+int dg_result_fetch_groups(dg_result* res, int64_t start, int64_t count, int64_t* bucket_time, int32_t* ids,
                            uint64_t* values);
+/* rows aggregated into each group of [start, start + count) */
+int dg_result_fetch_rows(dg_result* res, int64_t start, int64_t count, int64_t* rows);
+/* merged dictionary of dimension `dim` (the union of the segments' dictionaries, Java String
+ * order, null first when present): cardinality, and a bulk export like dg_segment_dim_dictionary
+ * (a null value has length 0) */
+int32_t dg_result_dim_cardinality(const dg_result* res, int32_t dim);
+int dg_result_dim_dictionary(const dg_result* res, int32_t dim, int64_t* offsets, char* bytes, int64_t* total_bytes);
 void dg_result_release(dg_result* res);
 
 /* ---- diagnostics (test harness; no reference counterpart) ----

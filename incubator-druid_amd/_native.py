@@ -92,7 +92,8 @@ EXPORTS = [
     "dg_segment_interval", "dg_segment_time_bounds", "dg_segment_num_columns", "dg_segment_column_name",
     "dg_segment_column_type", "dg_segment_device_bytes", "dg_segment_dim_cardinality", "dg_segment_dim_value",
     "dg_segment_dim_dictionary", "dg_segment_set_dim_order", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_topn_merge", "dg_groupby_run",
-    "dg_result_groups", "dg_result_fetch_groups", "dg_result_release", "dg_debug_lz4_decode",
+    "dg_result_groups", "dg_result_fetch_groups", "dg_result_fetch_rows", "dg_result_dim_cardinality",
+    "dg_result_dim_dictionary", "dg_result_release", "dg_debug_lz4_decode",
 ]
 
 _lib = None
@@ -133,8 +134,11 @@ def lib():
         "dg_topn_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), P(dg_topn), vp, vp, vp, P(dg_metrics)]),
         "dg_topn_merge": (ctypes.c_int, [vp, P(dg_scan), P(dg_topn), P(dg_topn_lists), P(i32), vp, vp, vp]),
         "dg_groupby_run": (ctypes.c_int, [P(vp), i32, P(dg_scan), P(dg_groupby), P(vp), P(dg_metrics)]),
-        "dg_result_groups": (i64, [vp, i32]),
-        "dg_result_fetch_groups": (ctypes.c_int, [vp, i32, vp, vp, vp]),
+        "dg_result_groups": (i64, [vp]),
+        "dg_result_fetch_groups": (ctypes.c_int, [vp, i64, i64, vp, vp, vp]),
+        "dg_result_fetch_rows": (ctypes.c_int, [vp, i64, i64, vp]),
+        "dg_result_dim_cardinality": (i32, [vp, i32]),
+        "dg_result_dim_dictionary": (ctypes.c_int, [vp, i32, vp, vp, P(i64)]),
         "dg_result_release": (None, [vp]),
         "dg_debug_lz4_decode": (ctypes.c_int, [vp, P(vp), P(i32), i32, vp, P(i32), P(ctypes.c_double), vp]),
     }

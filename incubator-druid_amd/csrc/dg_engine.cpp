@@ -857,6 +857,7 @@ void dg_context_release(dg_context* c) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   for (auto& e : ctx->ev) hipEventDestroy(e);
+  for (auto& b : ctx->free_blocks) hipFree(b.first);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1025,6 +1026,93 @@ static int32_t* tile_table(CallScratch* cs, const std::vector<int64_t>& nrows, s
     for (int k = 0; k < nt; ++k) h[(*begin)[i] + k] = (int32_t)i;
   }
   return d;
+}
+
+static int bits_for(int64_t card) {
+  int b = 0;
+  while ((1ll << b) < card) b++;
+  return b;
+}
+
+static bool has_float_sum(const AggPlan& plan) {
+  for (int a = 0; a < plan.n; ++a)
+    if (plan.kind[a] == DG_AGG_FLOAT_SUM) return true;
+  return false;
+}
+
+// device buffers of a sort-based grouping of at most `cap` rows (call scratch)
+static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, SortBufs* sb) {
+  memset(sb, 0, sizeof *sb);
+  sb->cap = cap;
+  sb->ntiles_sort = sort_tiles(cap);
+  const size_t c = (size_t)std::max<int64_t>(cap, 1) + 16;
+  for (int k = 0; k < 2; ++k) {
+    sb->keys[k] = dev_take<uint64_t>(cs, c);
+    sb->refs[k] = dev_take<uint32_t>(cs, c);
+    if (!sb->keys[k] || !sb->refs[k]) return set_error(DG_ERR_OOM, "sort buffers of %lld rows", (long long)cap);
+  }
+  sb->tile_cnt = dev_take<uint32_t>(cs, (size_t)std::max(ntiles_keygen, 1));
+  sb->n = dev_take<uint32_t>(cs, 4);
+  sb->hist = dev_take<uint32_t>(cs, (size_t)256 * sb->ntiles_sort);
+  sb->bin_total = dev_take<uint32_t>(cs, 256);
+  sb->run_cnt = dev_take<uint32_t>(cs, (size_t)sb->ntiles_sort);
+  if (!sb->tile_cnt || !sb->n || !sb->hist || !sb->bin_total || !sb->run_cnt) return set_error(DG_ERR_OOM, "sort tables");
+  return DG_OK;
+}
+
+// keygen tiles + row refs of the call's jobs, and the job table in HBM
+static int upload_gb_jobs(CallScratch* cs, std::vector<GbJob>& gj, const std::vector<int64_t>& rows, GbJob** d_jobs,
+                          int32_t** d_tile, int* ntiles, int64_t* total, hipStream_t st) {
+  if (gj.size() > (size_t)kMaxCallSegs) return set_error(DG_ERR_UNSUPPORTED, "%zu segments in one call (max %d)", gj.size(), kMaxCallSegs);
+  std::vector<int32_t> begin;
+  *d_tile = tile_table(cs, rows, &begin, ntiles, st);
+  if (!*d_tile) return set_error(DG_ERR_OOM, "tile table");
+  int64_t t = 0;
+  for (size_t i = 0; i < gj.size(); ++i) {
+    gj[i].tile_begin = begin[i];
+    gj[i].row_base = (uint32_t)t;
+    gj[i].nrows = (int32_t)rows[i];
+    t += rows[i];
+  }
+  if (t >= (1ll << 32)) return set_error(DG_ERR_UNSUPPORTED, "%lld rows in one call (row refs are 32-bit)", (long long)t);
+  *total = t;
+  GbJob* h = up_take<GbJob>(cs, gj.size(), d_jobs, st);
+  if (!h) return set_error(DG_ERR_OOM, "job table");
+  memcpy(h, gj.data(), sizeof(GbJob) * gj.size());
+  return DG_OK;
+}
+
+// floatSum of the per-segment engines (timeseries, topN), as the reference computes it: every
+// (segment, bucket[, id]) cell's float32 sum in row order, written over the cell's slot in the
+// accumulator tables (the scan kernels accumulate floatSum in fp64 first; this pass replaces it).
+// Keys are already in (segment, bucket) order unless `sort`.
+static int fsum_pass(CallScratch* cs, std::vector<GbJob>& gj, const std::vector<int64_t>& rows, int key_bits, bool sort,
+                     const AggPlan& plan, hipStream_t st) {
+  if (key_bits > 64) return set_error(DG_ERR_UNSUPPORTED, "floatSum cell key of %d bits", key_bits);
+  GbJob* d_jobs;
+  int32_t* d_tile;
+  int ntiles = 0;
+  int64_t total = 0;
+  int rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
+  if (rc) return rc;
+  SortBufs sb;
+  rc = sort_bufs(cs, total, ntiles, &sb);
+  if (rc) return rc;
+  uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)total + 16);
+  if (!head_pos) return set_error(DG_ERR_OOM, "floatSum runs");
+  DG_FLUSH(cs, st);
+  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, st);
+  if (sort) launch_radix_sort(&sb, key_bits, st);
+  launch_run_heads(&sb, st);
+  launch_run_mark(&sb, head_pos, st);
+  for (int a = 0; a < plan.n; ++a)
+    if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, (int)gj.size(), &sb, plan, a, head_pos, nullptr, st);
+  return DG_OK;
+}
+
+static void gb_copy_aggs(GbJob* g, const ScanJob& j) {
+  memcpy(g->vals, j.vals, sizeof g->vals);
+  memcpy(g->agg_bits, j.agg_bits, sizeof g->agg_bits);
 }
 
 }  // namespace dg
@@ -1246,6 +1334,35 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, d_init, st);
   hipEventRecord(ctx->ev[3], st);
   launch_scan_agg(d_jobs, d_tile, ntiles, plan, 0, st);
+  if (has_float_sum(plan)) {
+    // floatSum as the reference adds it: float32, one row at a time per cursor (bucket)
+    std::vector<GbJob> gj(n);
+    std::vector<int64_t> frows(n, 0);
+    int64_t maxb = 1;
+    for (int i = 0; i < n; ++i)
+      if (cur[i].any) maxb = std::max<int64_t>(maxb, cur[i].nbuckets);
+    const int bb = bits_for(maxb);
+    for (int i = 0; i < n; ++i) {
+      GbJob& f = gj[i];
+      memset(&f, 0, sizeof f);
+      if (!cur[i].any) continue;
+      f.bitset = jobs[i].bitset;
+      f.time = jobs[i].time;
+      f.t_lo = jobs[i].t_lo;
+      f.t_hi = jobs[i].t_hi;
+      f.bucket0 = cur[i].bucket0;
+      f.period = q->period_ms;
+      f.seg_slot = i;
+      f.seg_shift = bb;
+      f.bucket_bits = bb;
+      gb_copy_aggs(&f, jobs[i]);
+      f.fs_out = jobs[i].out;
+      f.fs_mul = 1;
+      frows[i] = jobs[i].nrows;
+    }
+    rc = fsum_pass(cs, gj, frows, bb + bits_for(n), false, plan, st);
+    if (rc) return rc;
+  }
   hipEventRecord(ctx->ev[4], st);
   // results
   std::vector<uint64_t*> h_out(n, nullptr);
@@ -1463,6 +1580,43 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
                    d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
   ht.mark("bins_launched");
+  if (has_float_sum(plan)) {
+    // floatSum as the reference adds it: float32, one row at a time per (cursor, dictionary id)
+    // position of the pooled buffer (PooledTopNAlgorithm.aggregateDimValue -> FloatSumBufferAggregator)
+    std::vector<GbJob> gj(n);
+    std::vector<int64_t> frows(n, 0);
+    int64_t maxb = 1, maxc = 1;
+    for (int i = 0; i < n; ++i)
+      if (cur[i].any) {
+        maxb = std::max<int64_t>(maxb, q->period_ms ? cur[i].nbuckets : 1);
+        maxc = std::max<int64_t>(maxc, card[i]);
+      }
+    const int bb = q->period_ms ? bits_for(maxb) : 0, ib = bits_for(maxc);
+    for (int i = 0; i < n; ++i) {
+      GbJob& f = gj[i];
+      memset(&f, 0, sizeof f);
+      if (!cur[i].any) continue;
+      f.bitset = jobs[i].bitset;
+      f.time = jobs[i].time;
+      f.t_lo = jobs[i].t_lo;
+      f.t_hi = jobs[i].t_hi;
+      f.bucket0 = cur[i].bucket0;
+      f.period = q->period_ms;
+      f.ndims = 1;
+      f.dims[0] = jobs[i].key;  // VIEW_ABSENT for a missing dimension: id 0 (its null value)
+      f.dim_bits[0] = ib;
+      f.bucket_shift = ib;
+      f.bucket_bits = bb;
+      f.seg_slot = i;
+      f.seg_shift = ib + bb;
+      gb_copy_aggs(&f, jobs[i]);
+      f.fs_out = jobs[i].out;
+      f.fs_mul = jobs[i].key_card;
+      frows[i] = jobs[i].nrows;
+    }
+    rc = fsum_pass(cs, gj, frows, bits_for(n) + bb + ib, true, plan, st);
+    if (rc) return rc;
+  }
   // selection + gather of the candidates' records, all segments in one launch
   const int mk = dim ? DG_AGG_COUNT : plan.kind[t->metric_agg];
   const int metric_agg = dim ? 0 : t->metric_agg;
@@ -2037,23 +2191,147 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
 }
 
 // ------------------------------------------------------------------------------------------------
-// groupBy
+// groupBy (v2): per-segment grouping + GroupByMergingQueryRunnerV2 merge, as one device-wide sort
 // ------------------------------------------------------------------------------------------------
 }  // extern "C"
 
-struct dg_result {
-  int n = 0;
-  int ndims = 0, naggs = 0;
-  std::vector<std::vector<int64_t>> time;
-  std::vector<std::vector<int32_t>> ids;
-  std::vector<std::vector<uint64_t>> vals;
-};
+namespace dg {
 
-static int bits_for(int64_t card) {
-  int b = 0;
-  while ((1ll << b) < card) b++;
-  return b;
+// Merged dictionary of `dim` over the call's segments: k-way merge of their sorted dictionaries
+// (GenericIndexed STRING_STRATEGY = Java String.compareTo with nulls first), plus each segment's
+// local id -> merged id table in HBM. A segment without the column contributes the null value.
+static int merged_dict(Context* ctx, Segment* const* segs, int n, const std::string& dim, std::shared_ptr<MergedDict>* out) {
+  std::vector<uint64_t> uids(n);
+  for (int i = 0; i < n; ++i) uids[i] = segs[i]->uid;
+  for (auto it = ctx->dict_cache.rbegin(); it != ctx->dict_cache.rend(); ++it)
+    if ((*it)->dim == dim && (*it)->uids == uids) {
+      *out = *it;
+      return DG_OK;
+    }
+  auto md = std::make_shared<MergedDict>();
+  md->uids = uids;
+  md->dim = dim;
+  md->remap.resize(n);
+  std::vector<const Column*> cols(n, nullptr);
+  bool need_null = false;
+  for (int i = 0; i < n; ++i) {
+    const Column* c = segs[i]->find(dim);
+    if (c && c->type != DG_COL_STRING) return set_error(DG_ERR_UNSUPPORTED, "groupBy on non-string column %s", dim.c_str());
+    cols[i] = c;
+    need_null |= c == nullptr;
+  }
+  bool same = cols[0] != nullptr;
+  for (int i = 1; i < n && same; ++i)
+    same = cols[i] && (cols[i] == cols[0] || (cols[i]->dict == cols[0]->dict && cols[i]->dict_null == cols[0]->dict_null));
+  if (same) {  // identical dictionaries (one segment, or segments of one generator): identity maps
+    md->values = cols[0]->dict;
+    md->is_null = cols[0]->dict_null;
+  } else {
+    if (need_null) {
+      md->values.emplace_back();
+      md->is_null.push_back(1);
+    }
+    struct Cur {
+      int seg, pos;
+    };
+    auto entry_cmp = [&](const Cur& a, const Cur& b) {
+      return cmp_nullable(cols[a.seg]->dict_null[a.pos], cols[a.seg]->dict[a.pos], cols[b.seg]->dict_null[b.pos],
+                          cols[b.seg]->dict[b.pos]);
+    };
+    auto later = [&](const Cur& a, const Cur& b) {  // min-heap on (value, segment)
+      const int c = entry_cmp(a, b);
+      return c != 0 ? c > 0 : a.seg > b.seg;
+    };
+    std::priority_queue<Cur, std::vector<Cur>, decltype(later)> pq(later);
+    std::vector<std::vector<int32_t>> host(n);
+    for (int i = 0; i < n; ++i) {
+      if (!cols[i] || cols[i]->dict.empty()) continue;
+      host[i].resize(cols[i]->dict.size());
+      pq.push(Cur{i, 0});
+    }
+    while (!pq.empty()) {
+      Cur c = pq.top();
+      pq.pop();
+      const Column* col = cols[c.seg];
+      const bool nul = col->dict_null[c.pos] != 0;
+      const std::string& v = col->dict[c.pos];
+      if (md->values.empty() || cmp_nullable(md->is_null.back() != 0, md->values.back(), nul, v) != 0) {
+        md->values.push_back(nul ? std::string() : v);
+        md->is_null.push_back(nul ? 1 : 0);
+      }
+      host[c.seg][c.pos] = (int32_t)md->values.size() - 1;
+      if (++c.pos < (int)col->dict.size()) pq.push(c);
+    }
+    for (int i = 0; i < n; ++i) {
+      if (host[i].empty()) continue;
+      md->remap[i].reset(new DevBuf());
+      if (!md->remap[i]->alloc(host[i].size() * 4)) return set_error(DG_ERR_OOM, "hipMalloc dictionary map");
+      DG_HIP(hipMemcpy(md->remap[i]->p, host[i].data(), host[i].size() * 4, hipMemcpyHostToDevice));
+    }
+  }
+  md->null_gid = (!md->values.empty() && md->is_null[0]) ? 0 : -1;
+  if (need_null && md->null_gid != 0) return set_error(DG_ERR_ARG, "merged dictionary of %s lacks null", dim.c_str());
+  ctx->dict_cache.push_back(md);
+  if (ctx->dict_cache.size() > 32) ctx->dict_cache.erase(ctx->dict_cache.begin());
+  *out = md;
+  return DG_OK;
 }
+
+// Result buffers outlive the call. They come from a per-context cache of device blocks: a released
+// result's blocks are kept for the next result (every call ends with a stream synchronisation, so a
+// cached block is idle) instead of a hipMalloc / hipFree (device-synchronising) per query.
+static void* result_alloc(Context* ctx, size_t bytes) {
+  bytes = (std::max<size_t>(bytes, 256) + 255) & ~(size_t)255;
+  size_t best = (size_t)-1;
+  for (size_t i = 0; i < ctx->free_blocks.size(); ++i) {
+    const size_t sz = ctx->free_blocks[i].second;
+    if (sz >= bytes && sz <= 2 * bytes + (64 << 20) && (best == (size_t)-1 || sz < ctx->free_blocks[best].second)) best = i;
+  }
+  if (best != (size_t)-1) {
+    void* p = ctx->free_blocks[best].first;
+    ctx->block_size[p] = ctx->free_blocks[best].second;
+    ctx->free_blocks.erase(ctx->free_blocks.begin() + best);
+    return p;
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
+    // give the cached blocks back and retry once
+    for (auto& b : ctx->free_blocks) hipFree(b.first);
+    ctx->free_blocks.clear();
+    (void)hipGetLastError();
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  }
+  ctx->block_size[p] = bytes;
+  return p;
+}
+
+static void result_free(Context* ctx, void* p) {
+  if (!p) return;
+  auto it = ctx->block_size.find(p);
+  if (it == ctx->block_size.end()) return;
+  ctx->free_blocks.emplace_back(p, it->second);
+  ctx->block_size.erase(it);
+}
+
+}  // namespace dg
+
+struct dg_result {
+  dg::Context* ctx = nullptr;
+  int ndims = 0, naggs = 0;
+  int64_t ngroups = 0;
+  uint64_t* keys = nullptr;   // [ngroups] packed keys, ascending
+  uint64_t* slots = nullptr;  // [ngroups][1 + naggs]: rows, then the ABI-encoded aggregate values
+  dg::KeyLayout lay{};
+  int64_t bucket0 = 0, period = 0, universal = 0;
+  std::vector<std::shared_ptr<dg::MergedDict>> dicts;
+  ~dg_result() {
+    if (!ctx) return;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    hipSetDevice(ctx->device);
+    dg::result_free(ctx, keys);
+    dg::result_free(ctx, slots);
+  }
+};
 
 extern "C" {
 
@@ -2064,7 +2342,9 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   int rc = check_segments(segs, n, &ctx);
   if (rc) return rc;
   if (!q || !gb || !out) return set_error(DG_ERR_ARG, "null argument");
-  if (gb->n_dims < 0 || gb->n_dims > 4) return set_error(DG_ERR_UNSUPPORTED, "%d groupBy dimensions (max 4)", gb->n_dims);
+  const int nd = gb->n_dims;
+  if (nd < 0 || nd > kMaxGroupDims) return set_error(DG_ERR_UNSUPPORTED, "%d groupBy dimensions (max %d)", nd, kMaxGroupDims);
+  if (n > kMaxCallSegs) return set_error(DG_ERR_UNSUPPORTED, "%d segments in one call (max %d)", n, kMaxCallSegs);
   AggPlan plan;
   rc = make_plan(q, &plan);
   if (rc) return rc;
@@ -2074,81 +2354,87 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   dg_metrics m;
   memset(&m, 0, sizeof m);
   const int na = plan.n, rec = na + 1;
+  std::vector<Segment*> sv(n);
+  for (int i = 0; i < n; ++i) sv[i] = reinterpret_cast<Segment*>(segs[i]);
   std::vector<Cursors> cur(n);
-  std::vector<GroupJob> jobs(n);
-  std::vector<int64_t> tiles_rows(n, 0);
-  std::vector<uint64_t> cap(n, 0);
-  DecodeBatch db;
-  // staged zeros: overflow flag + per-segment compaction counts (one read-back)
-  int32_t* d_over;
-  int32_t* h_z = up_take<int32_t>(cs, 2 + 2 * (size_t)std::max(n, 1), &d_over, st);
-  if (!h_z) return set_error(DG_ERR_OOM, "groupBy counters");
-  memset(h_z, 0, 4 * (2 + 2 * (size_t)std::max(n, 1)));
-  unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(d_over + 2);
-  hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
-    Segment* seg = reinterpret_cast<Segment*>(segs[i]);
-    cur[i] = plan_cursors(seg, q);
-    m.segment_rows += seg->nrows;
-    if (!cur[i].any) continue;
-    GroupJob& j = jobs[i];
-    memset(&j, 0, sizeof j);
-    uint32_t* bits = nullptr;
-    const unsigned long long* pcnt = nullptr;
-    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &pcnt, st);
+    cur[i] = plan_cursors(sv[i], q);
+    m.segment_rows += sv[i]->nrows;
+  }
+  // merged dictionaries (GroupByMergingQueryRunnerV2 merges by value; merged ids order like values)
+  std::vector<std::shared_ptr<MergedDict>> md(nd);
+  for (int d = 0; d < nd; ++d) {
+    if (!gb->dimensions || !gb->dimensions[d]) return set_error(DG_ERR_ARG, "null dimension %d", d);
+    rc = merged_dict(ctx, sv.data(), n, gb->dimensions[d], &md[d]);
     if (rc) return rc;
-    if (pcnt) DG_HIP(hipStreamSynchronize(st));  // the hash table is sized by the selected rows
-    const int64_t cnt = pcnt ? (int64_t)*pcnt : seg->nrows;
-    m.pre_filtered_rows += cnt;
-    j.nrows = (int32_t)seg->nrows;
+  }
+  // buckets shared by the segments: one index origin (bucket starts are on one period grid)
+  int64_t gb0 = 0, gend = 0;
+  bool anyc = false;
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any || !q->period_ms) continue;
+    const int64_t b0 = cur[i].bucket0, e = b0 + cur[i].nbuckets * q->period_ms;
+    gb0 = anyc ? std::min(gb0, b0) : b0;
+    gend = anyc ? std::max(gend, e) : e;
+    anyc = true;
+  }
+  // key = [bucket | d0 | d1 | ... ], the last dimension least significant
+  KeyLayout lay{};
+  lay.ndims = nd;
+  int shift = 0;
+  for (int d = nd - 1; d >= 0; --d) {
+    lay.dim_shift[d] = shift;
+    lay.dim_bits[d] = bits_for(std::max<int64_t>((int64_t)md[d]->values.size(), 1));
+    shift += lay.dim_bits[d];
+  }
+  lay.bucket_shift = shift;
+  lay.bucket_bits = (q->period_ms && anyc) ? bits_for((gend - gb0) / q->period_ms) : 0;
+  const int key_bits = shift + lay.bucket_bits;
+  if (key_bits > 64) return set_error(DG_ERR_UNSUPPORTED, "groupBy key of %d bits", key_bits);
+  hipEventRecord(ctx->ev[0], st);
+  std::vector<GbJob> gj(n);
+  std::vector<int64_t> rows(n, 0);
+  std::vector<const unsigned long long*> counts(n, nullptr);
+  DecodeBatch db;
+  for (int i = 0; i < n; ++i) {
+    GbJob& j = gj[i];
+    memset(&j, 0, sizeof j);
+    if (!cur[i].any) continue;
+    Segment* seg = sv[i];
+    uint32_t* bits = nullptr;
+    rc = build_bitset(seg, cs, q->filter, q->n_filter, &bits, &counts[i], st);
+    if (rc) return rc;
     j.bitset = bits;
-    j.t_lo = cur[i].t_lo;
-    j.t_hi = cur[i].t_hi;
-    j.bucket0 = cur[i].bucket0;
-    j.period = q->period_ms;
-    j.nbuckets = (int32_t)cur[i].nbuckets;
     j.time.kind = VIEW_ABSENT;
     if (cur[i].need_time) {
       rc = column_view(seg->find("__time"), cs, &db, &j.time, st);
       if (rc) return rc;
     }
-    j.ndims = gb->n_dims;
-    int shift = 0;
-    double space = 1.0;
-    for (int d = gb->n_dims - 1; d >= 0; --d) {
+    j.t_lo = cur[i].t_lo;
+    j.t_hi = cur[i].t_hi;
+    j.bucket0 = gb0;
+    j.period = q->period_ms;
+    j.bucket_shift = lay.bucket_shift;
+    j.bucket_bits = lay.bucket_bits;
+    j.ndims = nd;
+    for (int d = 0; d < nd; ++d) {
       Column* c = seg->find(gb->dimensions[d]);
-      int64_t card = 1;
       if (c) {
-        if (c->type != DG_COL_STRING) return set_error(DG_ERR_UNSUPPORTED, "groupBy on non-string column %s", gb->dimensions[d]);
         rc = column_view(c, cs, &db, &j.dims[d], st);
         if (rc) return rc;
-        card = std::max<int64_t>((int64_t)c->dict.size(), 1);
+        j.remap[d] = md[d]->remap[i] ? md[d]->remap[i]->as<int32_t>() : nullptr;
       } else {
         j.dims[d].kind = VIEW_ABSENT;
       }
-      j.dim_shift[d] = shift;
-      shift += bits_for(card);
-      space *= (double)card;
+      j.null_gid[d] = std::max(md[d]->null_gid, 0);
+      j.dim_shift[d] = lay.dim_shift[d];
+      j.dim_bits[d] = lay.dim_bits[d];
     }
-    j.bucket_shift = shift;
-    shift += bits_for(cur[i].nbuckets);
-    space *= (double)cur[i].nbuckets;
-    if (shift > 63) return set_error(DG_ERR_UNSUPPORTED, "groupBy key of %d bits", shift);
     for (int a = 0; a < na; ++a) {
       rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
       if (rc) return rc;
     }
-    double groups = std::min(space, (double)std::max<int64_t>(cnt, 1));
-    uint64_t c2 = 1024;
-    while ((double)c2 < 2.0 * groups) c2 <<= 1;
-    cap[i] = c2;
-    j.keys = dev_take<uint64_t>(cs, c2);
-    j.slots = dev_take<uint64_t>(cs, c2 * rec);
-    if (!j.keys || !j.slots) return set_error(DG_ERR_OOM, "groupBy table of %llu", (unsigned long long)c2);
-    j.mask = c2 - 1;
-    j.overflow = d_over;
-    DG_HIP(hipMemsetAsync(j.keys, 0xFF, c2 * 8, st));
-    tiles_rows[i] = seg->nrows;
+    rows[i] = seg->nrows;
   }
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
   hipEventRecord(ctx->ev[1], st);
@@ -2156,81 +2442,69 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
   m.bytes_read = db.bytes;
-  uint64_t* d_init;
-  uint64_t* h_init = up_take<uint64_t>(cs, rec, &d_init, st);
-  if (!h_init) return set_error(DG_ERR_OOM, "accumulator init");
-  h_init[0] = 0;
-  for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
-  std::vector<int32_t> begin;
+  GbJob* d_jobs;
+  int32_t* d_tile;
   int ntiles = 0;
-  int32_t* d_tile = tile_table(cs, tiles_rows, &begin, &ntiles, st);
-  if (!d_tile) return set_error(DG_ERR_DEVICE, "tile table");
-  for (int i = 0; i < n; ++i) jobs[i].tile_begin = begin[i];
-  GroupJob* d_jobs;
-  GroupJob* h_jobs = up_take<GroupJob>(cs, n, &d_jobs, st);
-  if (!h_jobs) return set_error(DG_ERR_OOM, "groupBy jobs");
-  memcpy(h_jobs, jobs.data(), sizeof(GroupJob) * n);
+  int64_t total = 0;
+  rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
+  if (rc) return rc;
+  SortBufs sb;
+  rc = sort_bufs(cs, total, ntiles, &sb);
+  if (rc) return rc;
+  uint32_t* h_n = host_take<uint32_t>(cs, 4);
+  if (!h_n) return set_error(DG_ERR_OOM, "groupBy counters");
   DG_FLUSH(cs, st);
-  for (int i = 0; i < n; ++i)
-    if (cur[i].any) launch_fill_u64(jobs[i].slots, (int64_t)cap[i], rec, d_init, st);
   hipEventRecord(ctx->ev[3], st);
-  launch_groupby(d_jobs, d_tile, ntiles, plan, st);
-  // compaction
-  std::vector<uint64_t*> ok(n, nullptr), os(n, nullptr);
-  for (int i = 0; i < n; ++i) {
-    if (!cur[i].any) continue;
-    uint64_t bound = std::min<uint64_t>(cap[i], (uint64_t)std::max<int64_t>(jobs[i].nrows, 1));
-    ok[i] = dev_take<uint64_t>(cs, bound);
-    os[i] = dev_take<uint64_t>(cs, bound * rec);
-    if (!ok[i] || !os[i]) return set_error(DG_ERR_OOM, "groupBy output");
-    launch_groupby_compact(jobs[i].keys, jobs[i].slots, cap[i], rec, ok[i], os[i], d_cnt + i, st);
+  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, st);
+  launch_radix_sort(&sb, key_bits, st);
+  launch_run_heads(&sb, st);
+  DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));
+  rc = finish_call(cs, st);  // the result is sized by the group count
+  if (rc) return rc;
+  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  const int64_t nsel = h_n[0], ng = h_n[1];
+  std::unique_ptr<dg_result> res(new dg_result());
+  res->ctx = ctx;
+  res->ndims = nd;
+  res->naggs = na;
+  res->ngroups = ng;
+  res->lay = lay;
+  res->bucket0 = gb0;
+  res->period = q->period_ms;
+  res->universal = q->interval_start;  // GroupByStrategyV2.getUniversalTimestamp (ALL granularity)
+  res->dicts = md;
+  res->keys = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * 8));
+  res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * rec * 8));
+  if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "groupBy result of %lld groups", (long long)ng);
+  if (ng > 0) {
+    uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)ng + 16);
+    const size_t nthr = (size_t)sb.ntiles_sort * 256;
+    int64_t* carry_g = dev_take<int64_t>(cs, nthr);
+    uint64_t* carry_slots = dev_take<uint64_t>(cs, nthr * rec);
+    if (!head_pos || !carry_g || !carry_slots) return set_error(DG_ERR_OOM, "groupBy reduce scratch");
+    launch_gb_reduce(d_jobs, n, &sb, plan, res->keys, res->slots, head_pos, carry_g, carry_slots, st);
+    for (int a = 0; a < na; ++a)
+      if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, &sb, plan, a, head_pos, res->slots, st);
+    launch_slots_finalize(res->slots, sb.n + 1, ng, plan, st);
   }
   hipEventRecord(ctx->ev[4], st);
-  int32_t* h_over = host_take<int32_t>(cs, 2 + 2 * (size_t)std::max(n, 1));
-  if (!h_over) return set_error(DG_ERR_OOM, "groupBy read-back");
-  unsigned long long* h_cnt = reinterpret_cast<unsigned long long*>(h_over + 2);
-  DG_HIP(hipMemcpyAsync(h_over, d_over, 4 * (2 + 2 * (size_t)n), hipMemcpyDeviceToHost, st));
   rc = finish_call(cs, st);
   if (rc) return rc;
-  if (*h_over) return set_error(DG_ERR_TABLE_FULL, "groupBy hash table full");
-  std::unique_ptr<dg_result> res(new dg_result());
-  res->n = n;
-  res->ndims = gb->n_dims;
-  res->naggs = na;
-  res->time.resize(n);
-  res->ids.resize(n);
-  res->vals.resize(n);
-  std::vector<std::vector<uint64_t>> hk(n), hs(n);
-  for (int i = 0; i < n; ++i) {
-    if (!cur[i].any) continue;
-    hk[i].resize(h_cnt[i]);
-    hs[i].resize(h_cnt[i] * rec);
-    if (h_cnt[i]) {
-      DG_HIP(hipMemcpyAsync(hk[i].data(), ok[i], h_cnt[i] * 8, hipMemcpyDeviceToHost, st));
-      DG_HIP(hipMemcpyAsync(hs[i].data(), os[i], h_cnt[i] * rec * 8, hipMemcpyDeviceToHost, st));
+  if (getenv("DG_DEBUG_GB")) {
+    uint32_t dn[2] = {0, 0};
+    uint64_t s0[4] = {0, 0, 0, 0}, k0 = 0;
+    hipMemcpy(dn, sb.n, 8, hipMemcpyDeviceToHost);
+    if (ng) {
+      hipMemcpy(s0, res->slots, 8 * std::min(rec, 4), hipMemcpyDeviceToHost);
+      hipMemcpy(&k0, res->keys, 8, hipMemcpyDeviceToHost);
     }
+    fprintf(stderr, "[dg gb] n=%d segs nsel=%lld ng=%lld dev n=%u,%u keys=%p slots=%p k0=%llx s0=%llx,%llx,%llx cap=%lld tiles=%d\n",
+            n, (long long)nsel, (long long)ng, dn[0], dn[1], (void*)res->keys, (void*)res->slots, (unsigned long long)k0, (unsigned long long)s0[0], (unsigned long long)s0[1],
+            (unsigned long long)s0[2], (long long)sb.cap, sb.ntiles_sort);
   }
-  DG_HIP(hipStreamSynchronize(st));
-  for (int i = 0; i < n; ++i) {
-    if (!cur[i].any) continue;
-    const GroupJob& j = jobs[i];
-    const size_t ng = hk[i].size();
-    res->time[i].resize(ng);
-    res->ids[i].resize(ng * gb->n_dims);
-    res->vals[i].resize(ng * na);
-    for (size_t k = 0; k < ng; ++k) {
-      const uint64_t key = hk[i][k];
-      const int64_t b = (int64_t)(key >> j.bucket_shift);
-      res->time[i][k] = q->period_ms ? cur[i].bucket0 + b * q->period_ms : cur[i].t_lo;
-      for (int d = 0; d < gb->n_dims; ++d) {
-        const int next = d == 0 ? j.bucket_shift : j.dim_shift[d - 1];
-        const int width = next - j.dim_shift[d];
-        res->ids[i][k * gb->n_dims + d] = (int32_t)((key >> j.dim_shift[d]) & (width ? ((1ull << width) - 1) : 0));
-      }
-      m.selected_rows += (int64_t)hs[i][k * rec];
-      for (int a = 0; a < na; ++a) res->vals[i][k * na + a] = finalize_slot(plan.kind[a], hs[i][k * rec + 1 + a]);
-    }
-  }
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : sv[i]->nrows;
+  m.selected_rows = nsel;
   float f1 = 0, f2 = 0, f3 = 0;
   hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
   hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
@@ -2244,18 +2518,66 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   return DG_OK;
 }
 
-int64_t dg_result_groups(const dg_result* r, int32_t i) {
-  if (!r || i < 0 || i >= r->n) return -1;
-  return (int64_t)r->time[i].size();
+int64_t dg_result_groups(const dg_result* r) { return r ? r->ngroups : -1; }
+
+int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* bucket_time, int32_t* ids,
+                           uint64_t* values) {
+  if (!r || start < 0 || count < 0 || start + count > r->ngroups) return set_error(DG_ERR_ARG, "bad result range");
+  if (count == 0) return DG_OK;
+  CallGuard g(r->ctx);
+  CallScratch* cs = g.cs;
+  hipStream_t st = r->ctx->stream;
+  const int nd = r->ndims, rec = r->naggs + 1;
+  if (bucket_time || ids) {
+    int64_t* d_b = dev_take<int64_t>(cs, (size_t)count);
+    int32_t* d_ids = dev_take<int32_t>(cs, (size_t)count * std::max(nd, 1));
+    if (!d_b || !d_ids) return set_error(DG_ERR_OOM, "fetch staging");
+    launch_gb_unpack(r->keys, start, count, r->lay, d_b, d_ids, st);
+    if (bucket_time) DG_HIP(hipMemcpyAsync(bucket_time, d_b, (size_t)count * 8, hipMemcpyDeviceToHost, st));
+    if (ids && nd) DG_HIP(hipMemcpyAsync(ids, d_ids, (size_t)count * nd * 4, hipMemcpyDeviceToHost, st));
+  }
+  std::vector<uint64_t> tmp;
+  if (values && r->naggs) {
+    tmp.resize((size_t)count * rec);
+    DG_HIP(hipMemcpyAsync(tmp.data(), r->slots + (size_t)start * rec, tmp.size() * 8, hipMemcpyDeviceToHost, st));
+  }
+  int rc = finish_call(cs, st);
+  if (rc) return rc;
+  if (bucket_time)
+    for (int64_t i = 0; i < count; ++i)
+      bucket_time[i] = r->period ? r->bucket0 + bucket_time[i] * r->period : r->universal;
+  if (values && r->naggs)
+    for (int64_t i = 0; i < count; ++i) memcpy(values + i * r->naggs, tmp.data() + i * rec + 1, 8 * (size_t)r->naggs);
+  return DG_OK;
 }
 
-int dg_result_fetch_groups(dg_result* r, int32_t i, int64_t* t, int32_t* ids, uint64_t* vals) {
-  if (!r || i < 0 || i >= r->n) return set_error(DG_ERR_ARG, "bad result index");
-  const size_t ng = r->time[i].size();
-  if (t) memcpy(t, r->time[i].data(), ng * 8);
-  if (ids) memcpy(ids, r->ids[i].data(), ng * r->ndims * 4);
-  if (vals) memcpy(vals, r->vals[i].data(), ng * r->naggs * 8);
+int dg_result_fetch_rows(dg_result* r, int64_t start, int64_t count, int64_t* rows) {
+  if (!r || !rows || start < 0 || count < 0 || start + count > r->ngroups) return set_error(DG_ERR_ARG, "bad result range");
+  if (count == 0) return DG_OK;
+  CallGuard g(r->ctx);
+  const int rec = r->naggs + 1;
+  DG_HIP(hipMemcpy2DAsync(rows, 8, r->slots + (size_t)start * rec, 8 * (size_t)rec, 8, (size_t)count,
+                          hipMemcpyDeviceToHost, r->ctx->stream));
+  return finish_call(g.cs, r->ctx->stream);
+}
+
+int dg_result_dim_dictionary(const dg_result* r, int32_t dim, int64_t* offsets, char* bytes, int64_t* total) {
+  if (!r || dim < 0 || dim >= r->ndims) return set_error(DG_ERR_ARG, "dimension index %d", dim);
+  const MergedDict& d = *r->dicts[dim];
+  int64_t t = 0;
+  for (size_t i = 0; i < d.values.size(); ++i) {
+    if (offsets) offsets[i] = t;
+    if (bytes && !d.is_null[i]) memcpy(bytes + t, d.values[i].data(), d.values[i].size());
+    t += d.is_null[i] ? 0 : (int64_t)d.values[i].size();
+  }
+  if (offsets) offsets[d.values.size()] = t;
+  if (total) *total = t;
   return DG_OK;
+}
+
+int32_t dg_result_dim_cardinality(const dg_result* r, int32_t dim) {
+  if (!r || dim < 0 || dim >= r->ndims) return -1;
+  return (int32_t)r->dicts[dim]->values.size();
 }
 
 void dg_result_release(dg_result* r) { delete r; }

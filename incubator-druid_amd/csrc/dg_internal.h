@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <memory>
@@ -104,27 +105,51 @@ struct ScanJob {
   uint64_t* out;            // accumulator table of this segment
 };
 
-// groupBy: per-segment open-addressing table
-struct GroupJob {
+// groupBy by sort (dg_sort.hip) and the floatSum row-order pass. One job per segment of the call.
+// A selected row becomes (key, row ref): key = [seg slot | bucket | merged id of every dimension],
+// most significant field first, so ascending keys are the reference's merged row order
+// (timestamp, then dimension values in Java String order, nulls first); the row ref is the row's
+// index over the call's segments (row_base + row), so a stable sort keeps equal keys in
+// (segment, row) order.
+constexpr int kMaxGroupDims = 8;
+
+struct GbJob {
   int32_t nrows;
-  int32_t tile_begin;
-  const uint32_t* bitset;
-  ColView time;
-  int64_t t_lo, t_hi;
-  int64_t bucket0;
-  int64_t period;
-  int32_t nbuckets;
+  int32_t tile_begin;           // first keygen tile (kTileRows rows) of this segment
+  uint32_t row_base;            // row ref of row 0
   int32_t ndims;
-  ColView dims[4];
-  int32_t dim_shift[4];     // key = (bucket << bucket_shift) | sum(id_d << dim_shift[d])
-  int32_t bucket_shift;
-  int32_t pad2;
+  const uint32_t* bitset;       // null: every row passes the filter
+  ColView time;                 // VIEW_ABSENT when the time column is not needed
+  int64_t t_lo, t_hi;           // rows with t in [t_lo, t_hi)
+  int64_t bucket0;              // origin of the bucket index (shared by the call's segments in a merge)
+  int64_t period;               // 0 = ALL
+  int32_t seg_slot, seg_shift;  // key field of the segment (0 / 0 when the groups are merged)
+  int32_t bucket_shift, bucket_bits;
+  ColView dims[kMaxGroupDims];
+  const int32_t* remap[kMaxGroupDims];  // local dictionary id -> merged id (null: identity)
+  int32_t null_gid[kMaxGroupDims];      // merged id of the null value (a missing dimension's rows)
+  int32_t dim_shift[kMaxGroupDims];
+  int32_t dim_bits[kMaxGroupDims];
   ColView vals[kMaxAggs];
-  const uint32_t* agg_bits[kMaxAggs];  // FilteredAggregatorFactory row matcher per aggregator (null: all rows)
-  uint64_t* keys;           // [cap]
-  uint64_t* slots;          // [cap * (naggs + 1)], slot 0 = rows
-  uint64_t mask;            // cap - 1
-  int32_t* overflow;        // set when the table is full
+  const uint32_t* agg_bits[kMaxAggs];  // FilteredAggregatorFactory row matcher per aggregator
+  // floatSum sink of the per-segment engines (timeseries / topN): slot (bucket * fs_mul + id) of this
+  // segment's [keys][1 + naggs] accumulator table
+  uint64_t* fs_out;
+  int64_t fs_mul;
+};
+
+// Device buffers of one sort-based grouping; *_n are device words (counts known only on the device).
+struct SortBufs {
+  uint64_t* keys[2];
+  uint32_t* refs[2];
+  int cur;                // which of the ping-pong buffers holds the result
+  uint32_t* tile_cnt;     // keygen tiles: selected rows, then their offsets
+  uint32_t* n;            // [0] selected rows, [1] groups
+  uint32_t* hist;         // radix histograms [bins][tiles]
+  uint32_t* bin_total;    // [256]
+  uint32_t* run_cnt;      // per sort tile: run heads, then their offsets
+  int64_t cap;            // element capacity (rows of the call)
+  int ntiles_sort;        // sort tiles of `cap`
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -194,6 +219,20 @@ struct Column {
   bool order_set[kOrderSlots] = {};
 };
 
+// Merged dictionary of one dimension over a set of segments (the union of their sorted
+// dictionaries in Java String order, nulls first) + each segment's local id -> merged id table in
+// HBM. GroupByMergingQueryRunnerV2 merges rows by dimension VALUE (:188-246); the engine merges by
+// merged id instead, which orders exactly like the values. Built on the host once per
+// (segment set, dimension) and cached in the context, like a datasource-level dictionary.
+struct MergedDict {
+  std::vector<uint64_t> uids;  // attach serials of the segments, in call order
+  std::string dim;
+  std::vector<std::string> values;
+  std::vector<uint8_t> is_null;
+  int32_t null_gid = -1;                        // merged id of null (-1: no null value)
+  std::vector<std::unique_ptr<DevBuf>> remap;   // per segment: int32[card] (empty = identity)
+};
+
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -203,10 +242,15 @@ struct Context {
   DevBuf scratch[6];
   DevBuf pinned_dummy;
   hipEvent_t ev[8] = {};
+  std::vector<std::shared_ptr<MergedDict>> dict_cache;  // most recent last
+  // device blocks of groupBy results: live (size by pointer) and released for reuse
+  std::map<void*, size_t> block_size;
+  std::vector<std::pair<void*, size_t>> free_blocks;
 };
 
 struct Segment {
   Context* ctx = nullptr;
+  uint64_t uid = 0;  // attach serial (never reused: a cache key that outlives the segment)
   std::string dir;
   int64_t nrows = 0;
   int64_t istart = 0, iend = 0;
@@ -304,10 +348,42 @@ constexpr int kSelBlock = 1024;
 constexpr int kTopnOrderCap = 4096;  // k_topn_order sorts at most this many candidates
 void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, int naggs, int metric, int metric_op,
                         int inverted, int threshold, hipStream_t s);
-void launch_groupby(const GroupJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, hipStream_t s);
-void launch_groupby_compact(const uint64_t* keys, const uint64_t* slots, uint64_t cap, int nslots, uint64_t* out_keys,
-                            uint64_t* out_slots, unsigned long long* d_count, hipStream_t s);
 
 constexpr int kTileRows = 2048;
+
+// dg_sort.hip
+constexpr int kSortTile = 4096;  // elements per radix / run tile (256 threads x 16)
+constexpr int kMaxCallSegs = 1024;  // segments of one sort-based call (row-ref bases live in LDS)
+inline int sort_tiles(int64_t n) { return (int)std::max<int64_t>(1, (n + kSortTile - 1) / kSortTile); }
+// selected rows -> (key, ref) in (segment, row) order; sb->n[0] = selected rows
+void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, hipStream_t s);
+// stable LSD radix sort of sb->keys/refs[cur] on key bits [0, key_bits)
+void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s);
+// run heads of the sorted keys: sb->run_cnt = per-tile offsets, sb->n[1] = runs
+void launch_run_heads(SortBufs* sb, hipStream_t s);
+// head_pos[g] = first sorted element of run g (after launch_run_heads)
+void launch_run_mark(SortBufs* sb, uint32_t* head_pos, hipStream_t s);
+// groupBy merge of the sorted rows: one record per run (out_keys[g], out_slots[g][1 + naggs] in the
+// device slot encoding), head_pos[g] = first sorted element of run g; floatSum slots are left to
+// launch_fsum_runs. carry: scratch of sort_tiles(cap) * 256 entries (g) and * (1 + naggs) slots.
+void launch_gb_reduce(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, uint64_t* out_keys,
+                      uint64_t* out_slots, uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, hipStream_t s);
+// floatSum aggregator `agg` as the reference computes it: a float32 sum in row order per run and
+// segment (FloatSumBufferAggregator.aggregate), segments combined in order with float adds
+// (FloatSumAggregator.combine). groupBy: into out_slots[g][1 + agg]; per-segment engines
+// (out_slots == null): into the job's fs_out table. head_pos null: runs found by a linear scan.
+void launch_fsum_runs(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, int agg, const uint32_t* head_pos,
+                      uint64_t* out_slots, hipStream_t s);
+// device slot encoding -> ABI encoding (finalize) for n records
+void launch_slots_finalize(uint64_t* slots, const uint32_t* n_ptr, int64_t cap, AggPlan plan, hipStream_t s);
+// groups [start, start + count): key fields -> bucket index and merged ids (int32 per dimension)
+struct KeyLayout {
+  int32_t ndims;
+  int32_t bucket_shift, bucket_bits;
+  int32_t dim_shift[kMaxGroupDims];
+  int32_t dim_bits[kMaxGroupDims];
+};
+void launch_gb_unpack(const uint64_t* keys, int64_t start, int64_t count, KeyLayout lay, int64_t* bucket, int32_t* ids,
+                      hipStream_t s);
 
 }  // namespace dg

@@ -75,15 +75,25 @@ struct Slice {
 };
 
 // GenericIndexed v1 view
+// Element i occupies [end[i-1] + 4, end[i]) of the values region (the 4 bytes skipped are the
+// element's length prefix, GenericIndexed.java:479-492); offsets read from the file are checked
+// against the region the header declares (numBytesUsed), so a truncated or corrupt segment is a
+// format error (the reference's IAE/ISE), never an out-of-bounds read.
 struct GI {
   int32_t n = 0;
+  int64_t size = 0;  // bytes of the values region
   const uint8_t* header = nullptr;
   const uint8_t* values = nullptr;
+  // length of element i (0 = null / empty), or -1 when its offsets are outside the region
   int32_t get(int32_t i, const uint8_t** ptr) const {
-    int32_t start = i == 0 ? 4 : be32(header + 4 * (i - 1)) + 4;
-    int32_t end = be32(header + 4 * i);
+    *ptr = values;
+    if (i < 0 || i >= n) return -1;
+    const int64_t start = i == 0 ? 4 : (int64_t)be32(header + 4 * (i - 1)) + 4;
+    const int64_t end = be32(header + 4 * i);
+    if (start < 4 || start > size || end < start - 4 || end > size) return -1;
+    if (end < start) return 0;  // an empty element directly after a length prefix of 0
     *ptr = values + start;
-    return end - start;
+    return (int32_t)(end - start);
   }
 };
 
@@ -97,6 +107,7 @@ bool gi_read(Slice& s, GI* g) {
   if (g->n < 0 || 4 + 4 * (int64_t)g->n > used) return false;
   g->header = body + 4;
   g->values = body + 4 + 4 * (int64_t)g->n;
+  g->size = (int64_t)used - 4 - 4 * (int64_t)g->n;
   s.p = body + used;
   return true;
 }
@@ -174,7 +185,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int32_t b = 0; b < blocks.n; ++b) {
       const uint8_t* p;
       int32_t len = blocks.get(b, &p);
-      if (len <= 0) return set_error(DG_ERR_FORMAT, "empty compressed block %d", b);
+      if (len <= 0) return set_error(DG_ERR_FORMAT, "empty or out-of-range compressed block %d", b);
       col->comp_off[b] = total;
       col->comp_len[b] = len;
       total += (len + 15) & ~15;
@@ -223,7 +234,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int32_t b = 0; b < blocks.n; ++b) {
       const uint8_t* p;
       int32_t len = blocks.get(b, &p);
-      if (len > kBlockBytes) return set_error(DG_ERR_FORMAT, "uncompressed block of %d bytes", len);
+      if (len < 0 || len > kBlockBytes) return set_error(DG_ERR_FORMAT, "uncompressed block %d of %d bytes", b, len);
       memcpy(host.data() + (size_t)b * kBlockBytes, p, (size_t)len);
       col->stored_bytes += len;
     }
@@ -436,6 +447,7 @@ int parse_string(Context* ctx, Column* c, Slice s) {
   for (int32_t i = 0; i < dict.n; ++i) {
     const uint8_t* p;
     int32_t len = dict.get(i, &p);
+    if (len < 0) return set_error(DG_ERR_FORMAT, "%s: dictionary entry %d outside its GenericIndexed", c->name.c_str(), i);
     c->dict[i].assign((const char*)p, len > 0 ? len : 0);
     c->dict_null[i] = len <= 0;  // size 0 => null (replaceWithDefault), GenericIndexed.java:369-372
   }
@@ -491,6 +503,7 @@ int parse_string(Context* ctx, Column* c, Slice s) {
     for (int32_t i = 0; i < bms.n; ++i) {
       const uint8_t* p;
       int32_t len = bms.get(i, &p);
+      if (len < 0) return set_error(DG_ERR_FORMAT, "%s: bitmap %d outside its GenericIndexed", c->name.c_str(), i);
       c->bm_off[i] = total;
       c->bm_len[i] = len > 0 ? len : 0;
       total += (c->bm_len[i] + 3) & ~3;
@@ -516,8 +529,10 @@ int64_t column_device_bytes(const Column& c) {
 int read_time_bounds(Segment* seg);  // dg_engine.cpp
 
 int load_segment(Context* ctx, const char* dir, Segment** out) {
+  static std::atomic<uint64_t> serial{0};
   std::unique_ptr<Segment> seg(new Segment());
   seg->ctx = ctx;
+  seg->uid = ++serial;
   seg->dir = dir;
   std::string d(dir);
   {

@@ -1,0 +1,595 @@
+// dg_sort.hip — groupBy v2 as a device-wide sort, and the floatSum row-order pass (gfx950).
+//
+// Replaces, for the merged result of the segments of one call:
+//   GroupByQueryEngineV2.HashAggregateIterator.aggregateSingleValueDims + BufferHashGrouper per
+//     segment (query/groupby/epinephelinae/GroupByQueryEngineV2.java:413-475,
+//     ByteBufferHashTable.java:286-327, AbstractBufferHashGrouper.java:119-171), and
+//   GroupByMergingQueryRunnerV2.run (epinephelinae/GroupByMergingQueryRunnerV2.java:170-290): the
+//     ConcurrentGrouper merge of the segments' rows keyed by dimension values and its sorted iterator.
+// A hash grouper pays one random CAS + one random atomic per aggregator per row (memory-side
+// atomics on gfx950, ~17x slower than coalesced ones when every lane hits another row) and still
+// has to sort its groups for the merged, ordered result. At Druid's high-cardinality shapes
+// (config 3: ~1 group per row) sorting the rows is the whole job, so it is done directly:
+//   keygen   selected rows -> (key, row ref): key = [segment slot | bucket | merged dictionary id of
+//            each dimension] (ids of the call's merged dictionaries, Java String order, nulls first),
+//            written in (segment, row) order with a deterministic per-tile compaction;
+//   sort     stable LSD radix sort over the key's used bits (<= 8-bit digits: per-tile histograms,
+//            per-digit scans, a ballot match-any ranking per wave, one scatter per pass);
+//   runs     run heads of the sorted keys = the groups, in output order;
+//   reduce   one record per group: 16 consecutive sorted rows per thread, inputs gathered by row
+//            ref, the record written by the thread that owns the group's head with plain stores;
+//            the partial of a group that started in an earlier thread goes to a carry slot that a
+//            second kernel folds in with one atomic per (wave, group);
+//   floatSum the reference adds float32 values one row at a time in row order per segment
+//            (FloatSumBufferAggregator.java:38-46) and combines segments with float adds
+//            (FloatSumAggregator.java:40-43); fp32 addition is not associative, so a floatSum slot
+//            is computed by one thread per group walking its rows in (segment, row) order — exact
+//            parity with the reference's recurrence instead of a tree sum.
+// Integer results are exact; doubleSum partials combine in a different order than the reference's
+// row loop (within the 1e-9 relative tolerance north_star states).
+#include <hip/hip_runtime.h>
+
+#include "dg_device.h"
+
+namespace dg {
+
+constexpr int kST = 256;                 // threads of the sort / run kernels
+constexpr int kSPT = kSortTile / kST;    // 16 elements per thread
+
+// exclusive scan of one u32 per thread over an NT-thread workgroup; *total = workgroup sum
+template <int NT>
+__device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* total, uint32_t* s_tmp) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[wave] = x;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const uint32_t y = s_tmp[w];
+    off += w < wave ? y : 0u;
+    tot += y;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + x - v;
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* s_tmp) {
+  uint32_t t;
+  block_scan_u32<NT>(v, &t, s_tmp);
+  return t;
+}
+
+// one workgroup: exclusive scan of a[0..n) in place, *total = sum
+__global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ a, int n, uint32_t* __restrict__ total) {
+  __shared__ uint32_t s_tmp[16];
+  uint32_t carry = 0;
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + threadIdx.x;
+    const uint32_t v = i < n ? a[i] : 0u;
+    uint32_t t;
+    const uint32_t ex = block_scan_u32<1024>(v, &t, s_tmp);
+    if (i < n) a[i] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// segment of a row ref: last job whose row_base <= ref (bases ascend)
+__device__ __forceinline__ int locate_seg(const uint32_t* s_base, int njobs, uint32_t ref) {
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_base[mid] <= ref) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// ------------------------------------------------------------------------------------------------
+// keygen: the cursor's rows (bitmap offset + interval, QueryableIndexStorageAdapter.makeCursors
+// :190-316, CursorSequenceBuilder.build :367-456) -> grouping keys
+// (GroupByQueryEngineV2.aggregateSingleValueDims :457-475 writes the row's dictionary ids as the key)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool gb_select(const GbJob& j, int64_t r, int64_t* bucket) {
+  if (j.bitset && !((j.bitset[r >> 5] >> (r & 31)) & 1u)) return false;
+  *bucket = 0;
+  if (j.time.kind != VIEW_ABSENT) {
+    const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, r));
+    if (t < j.t_lo || t >= j.t_hi) return false;
+    if (j.period) *bucket = (t - j.bucket0) / j.period;
+  }
+  return true;
+}
+
+__device__ __forceinline__ uint64_t gb_key(const GbJob& j, int64_t r, int64_t bucket) {
+  uint64_t k = ((uint64_t)j.seg_slot << j.seg_shift) | ((uint64_t)bucket << j.bucket_shift);
+  for (int d = 0; d < j.ndims; ++d) {
+    uint32_t g;
+    if (j.dims[d].kind == VIEW_IDS) {
+      const uint32_t id = load_id(j.dims[d], r);
+      g = j.remap[d] ? (uint32_t)j.remap[d][id] : id;
+    } else {
+      g = (uint32_t)j.null_gid[d];  // missing dimension: every row has the null value
+    }
+    k |= (uint64_t)g << j.dim_shift[d];
+  }
+  return k;
+}
+
+__global__ __launch_bounds__(256) void k_gb_count(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
+                                                  uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_tmp[4];
+  const GbJob& j = jobs[tile_job[blockIdx.x]];
+  const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
+  const int64_t r1 = min((int64_t)j.nrows, r0 + kTileRows);
+  uint32_t c = 0;
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+    int64_t b;
+    c += gb_select(j, r, &b) ? 1u : 0u;
+  }
+  const uint32_t t = block_sum_u32<256>(c, s_tmp);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
+                                                   const uint32_t* __restrict__ offs, uint64_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ refs) {
+  __shared__ uint32_t s_tmp[4];
+  const GbJob& j = jobs[tile_job[blockIdx.x]];
+  const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
+  const int64_t r1 = min((int64_t)j.nrows, r0 + kTileRows);
+  uint32_t base = offs[blockIdx.x];
+  for (int64_t rb = r0; rb < r1; rb += 256) {
+    const int64_t r = rb + threadIdx.x;
+    int64_t b = 0;
+    const bool sel = r < r1 && gb_select(j, r, &b);
+    uint32_t tot;
+    const uint32_t ex = block_scan_u32<256>(sel ? 1u : 0u, &tot, s_tmp);
+    if (sel) {
+      keys[base + ex] = gb_key(j, r, b);
+      refs[base + ex] = j.row_base + (uint32_t)r;
+    }
+    base += tot;
+  }
+}
+
+void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, hipStream_t s) {
+  if (ntiles <= 0) {
+    hipMemsetAsync(sb->n, 0, 4, s);
+    return;
+  }
+  hipLaunchKernelGGL(k_gb_count, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt);
+  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, sb->tile_cnt, ntiles, sb->n);
+  hipLaunchKernelGGL(k_gb_keygen, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
+                     sb->keys[sb->cur], sb->refs[sb->cur]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// stable LSD radix sort (keys + u32 refs), tiles of kSortTile consecutive elements
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kST) void k_rs_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
+                                                 int shift, int bits, uint32_t* __restrict__ hist, int ntiles) {
+  __shared__ uint32_t s_h[4 * 256];  // one histogram per wave (fewer same-address LDS atomics)
+  const uint32_t n = *n_ptr;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int nb = 1 << bits;
+  for (int i = threadIdx.x; i < 4 * 256; i += kST) s_h[i] = 0;
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  if (base < n) {
+#pragma unroll 4
+    for (int c = 0; c < kSPT; ++c) {
+      const int64_t i = base + c * kST + threadIdx.x;
+      if (i < n) atomicAdd(&s_h[wave * 256 + (int)((keys[i] >> shift) & (uint64_t)(nb - 1))], 1u);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nb; d += kST)
+    hist[(size_t)d * ntiles + blockIdx.x] = s_h[d] + s_h[256 + d] + s_h[512 + d] + s_h[768 + d];
+}
+
+// one workgroup per digit: exclusive scan of that digit's tile counts in place + the digit's total
+__global__ __launch_bounds__(1024) void k_rs_binscan(uint32_t* __restrict__ hist, int ntiles, uint32_t* __restrict__ bin_total) {
+  __shared__ uint32_t s_tmp[16];
+  uint32_t* h = hist + (size_t)blockIdx.x * ntiles;
+  uint32_t carry = 0;
+  for (int base = 0; base < ntiles; base += 1024) {
+    const int i = base + threadIdx.x;
+    const uint32_t v = i < ntiles ? h[i] : 0u;
+    uint32_t t;
+    const uint32_t ex = block_scan_u32<1024>(v, &t, s_tmp);
+    if (i < ntiles) h[i] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) bin_total[blockIdx.x] = carry;
+}
+
+// lanes of the wave whose digit equals mine (ballot per digit bit), restricted to valid lanes
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, int bits, bool valid) {
+  uint64_t m = __ballot(valid);
+  for (int b = 0; b < bits; ++b) {
+    const bool x = (d >> b) & 1u;
+    const uint64_t bb = __ballot(x);
+    m &= x ? bb : ~bb;
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Wave w of a tile owns its elements [w * 1024, (w + 1) * 1024) in 16 chunks of 64. Pass A ranks
+// each element among the earlier elements of its wave with the same digit (chunk order, then lane
+// order = element order); the per-digit wave counts become per-wave bases; pass B scatters.
+__global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                    const uint32_t* __restrict__ n_ptr, int shift, int bits,
+                                                    const uint32_t* __restrict__ hist,
+                                                    const uint32_t* __restrict__ bin_total, int ntiles) {
+  __shared__ uint32_t s_cnt[4 * 256];
+  __shared__ uint32_t s_base[256];
+  __shared__ uint32_t s_tmp[4];
+  const uint32_t n = *n_ptr;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  if (base >= n) return;
+  const int nb = 1 << bits;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  {
+    const uint32_t v = tid < nb ? bin_total[tid] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_scan_u32<kST>(v, &tot, s_tmp);
+    if (tid < nb) s_base[tid] = ex + hist[(size_t)tid * ntiles + blockIdx.x];
+  }
+  for (int i = tid; i < 4 * 256; i += kST) s_cnt[i] = 0;
+  __syncthreads();
+  uint64_t k[kSPT];
+  uint32_t v[kSPT], rank[kSPT];
+  const int64_t wbase = base + (int64_t)wave * (kSortTile / 4);
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) {
+    const int64_t i = wbase + c * 64 + lane;
+    const bool ok = i < n;
+    k[c] = ok ? kin[i] : 0ull;
+    v[c] = ok ? vin[i] : 0u;
+  }
+  uint32_t* cnt = s_cnt + wave * 256;
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) {
+    const bool ok = wbase + c * 64 + lane < n;
+    const uint32_t d = (uint32_t)(k[c] >> shift) & (uint32_t)(nb - 1);
+    const uint64_t peers = match_digit(d, bits, ok);
+    uint32_t prior = 0;
+    if (ok) prior = cnt[d];
+    rank[c] = prior + lanes_below(peers);
+    // the highest lane of each digit group advances the wave's count (a wave's LDS operations
+    // complete in issue order, so every lane above read the count before this write)
+    if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  if (tid < nb) {
+    uint32_t run = s_base[tid];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t x = s_cnt[w * 256 + tid];
+      s_cnt[w * 256 + tid] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) {
+    if (wbase + c * 64 + lane >= n) continue;
+    const uint32_t d = (uint32_t)(k[c] >> shift) & (uint32_t)(nb - 1);
+    const uint32_t pos = cnt[d] + rank[c];
+    kout[pos] = k[c];
+    vout[pos] = v[c];
+  }
+}
+
+void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
+  if (key_bits <= 0) return;
+  const int npass = (key_bits + 7) / 8;
+  const int w = (key_bits + npass - 1) / npass;
+  const int nt = sb->ntiles_sort;
+  for (int p = 0, shift = 0; p < npass; ++p, shift += w) {
+    const int bits = std::min(w, key_bits - shift);
+    const int in = sb->cur, out = sb->cur ^ 1;
+    hipLaunchKernelGGL(k_rs_hist, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->n, shift, bits, sb->hist, nt);
+    hipLaunchKernelGGL(k_rs_binscan, dim3(1 << bits), dim3(1024), 0, s, sb->hist, nt, sb->bin_total);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
+                       sb->refs[out], sb->n, shift, bits, sb->hist, sb->bin_total, nt);
+    sb->cur = out;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// runs of equal keys (= groups, in output order)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kST) void k_run_count(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
+                                                   uint32_t* __restrict__ run_cnt) {
+  __shared__ uint32_t s_tmp[4];
+  const uint32_t n = *n_ptr;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  uint32_t c = 0;
+  if (base < n) {
+#pragma unroll 4
+    for (int q = 0; q < kSPT; ++q) {
+      const int64_t i = base + q * kST + threadIdx.x;
+      if (i < n) c += (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+    }
+  }
+  const uint32_t t = block_sum_u32<kST>(c, s_tmp);
+  if (threadIdx.x == 0) run_cnt[blockIdx.x] = t;
+}
+
+void launch_run_heads(SortBufs* sb, hipStream_t s) {
+  hipLaunchKernelGGL(k_run_count, dim3(sb->ntiles_sort), dim3(kST), 0, s, sb->keys[sb->cur], sb->n, sb->run_cnt);
+  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, sb->run_cnt, sb->ntiles_sort, sb->n + 1);
+}
+
+// head_pos[g] = first element of run g (per-segment engines; the groupBy reduce writes its own)
+__global__ __launch_bounds__(kST) void k_run_mark(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
+                                                  const uint32_t* __restrict__ run_off, uint32_t* __restrict__ head_pos) {
+  __shared__ uint32_t s_tmp[4];
+  const uint32_t n = *n_ptr;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  if (base >= n) return;
+  const int64_t x0 = base + (int64_t)threadIdx.x * kSPT;
+  uint32_t h = 0;
+  for (int q = 0; q < kSPT; ++q) {
+    const int64_t i = x0 + q;
+    if (i < n && (i == 0 || keys[i] != keys[i - 1])) h |= 1u << q;
+  }
+  uint32_t tot;
+  uint32_t g = run_off[blockIdx.x] + block_scan_u32<kST>((uint32_t)__popc(h), &tot, s_tmp);
+  for (int q = 0; q < kSPT; ++q)
+    if ((h >> q) & 1u) head_pos[g++] = (uint32_t)(x0 + q);
+}
+
+void launch_run_mark(SortBufs* sb, uint32_t* head_pos, hipStream_t s) {
+  hipLaunchKernelGGL(k_run_mark, dim3(sb->ntiles_sort), dim3(kST), 0, s, sb->keys[sb->cur], sb->n, sb->run_cnt, head_pos);
+}
+
+// ------------------------------------------------------------------------------------------------
+// groupBy reduce: the merged grouper's records (AggregatorFactory.combine semantics across segments
+// = the per-row aggregate ops, both exact for counts / long sums / min / max)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ jobs, int njobs,
+                                                   const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
+                                                   const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ run_off,
+                                                   AggPlan plan, uint64_t* __restrict__ out_keys,
+                                                   uint64_t* __restrict__ out_slots, uint32_t* __restrict__ head_pos,
+                                                   int64_t* __restrict__ carry_g, uint64_t* __restrict__ carry_slots) {
+  __shared__ uint64_t s_key[kSortTile + 1];
+  __shared__ uint32_t s_ref[kSortTile];
+  __shared__ uint32_t s_base[kMaxCallSegs];
+  __shared__ uint32_t s_tmp[4];
+  const uint32_t n = *n_ptr;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int64_t gt = (int64_t)blockIdx.x * kST + threadIdx.x;
+  carry_g[gt] = -1;
+  if (base >= n) return;
+  const int tid = threadIdx.x;
+  for (int x = tid; x < kSortTile; x += kST) {
+    const int64_t i = base + x;
+    s_key[1 + x] = i < n ? keys[i] : 0ull;
+    s_ref[x] = i < n ? refs[i] : 0u;
+  }
+  if (tid == 0) s_key[0] = base > 0 ? keys[base - 1] : ~keys[0];
+  for (int x = tid; x < njobs; x += kST) s_base[x] = jobs[x].row_base;
+  __syncthreads();
+  const int na = plan.n, rec = na + 1;
+  const int x0 = tid * kSPT;
+  const int m = (int)max<int64_t>(0, min<int64_t>(kSPT, (int64_t)n - base - x0));
+  uint32_t h = 0;
+  for (int q = 0; q < m; ++q)
+    if (s_key[1 + x0 + q] != s_key[x0 + q]) h |= 1u << q;
+  uint32_t tot;
+  const uint32_t ex = block_scan_u32<kST>((uint32_t)__popc(h), &tot, s_tmp);
+  if (m == 0) return;
+  // group of the thread's first element: the next head's index, or the open group before it
+  int64_t g = (int64_t)run_off[blockIdx.x] + ex - ((h & 1u) ? 0 : 1);
+  bool owner = h & 1u;
+  uint64_t acc[kMaxAggs + 1];
+  auto reset = [&]() {
+    acc[0] = 0;
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; ++a) acc[1 + a] = a < na ? identity_of(plan.op[a], plan.kind[a]) : 0ull;
+  };
+  auto flush = [&]() {
+    if (owner) {
+      for (int s = 0; s < rec; ++s) out_slots[g * rec + s] = acc[s];
+    } else {  // the group's head (and record) belongs to an earlier thread: carry the partial
+      carry_g[gt] = g;
+      for (int s = 0; s < rec; ++s) carry_slots[gt * rec + s] = acc[s];
+    }
+  };
+  reset();
+  for (int q = 0; q < m; ++q) {
+    const uint64_t key = s_key[1 + x0 + q];
+    if ((h >> q) & 1u) {
+      if (q > 0) {
+        flush();
+        g++;
+        owner = true;
+        reset();
+      }
+      head_pos[g] = (uint32_t)(base + x0 + q);
+      out_keys[g] = key;
+    }
+    const uint32_t ref = s_ref[x0 + q];
+    const int seg = locate_seg(s_base, njobs, ref);
+    const GbJob& j = jobs[seg];
+    const int64_t row = (int64_t)(ref - s_base[seg]);
+    acc[0] += 1;
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; ++a)
+      if (a < na && plan.kind[a] != DG_AGG_FLOAT_SUM) acc[1 + a] = combine_op(plan.op[a], acc[1 + a], agg_in(j, plan, a, row));
+  }
+  flush();
+}
+
+// carried partials -> their group's record: equal groups are consecutive, so one segmented combine
+// per wave and one atomic per (wave, group, slot)
+__global__ __launch_bounds__(256) void k_gb_carry(const int64_t* __restrict__ carry_g, const uint64_t* __restrict__ carry_slots,
+                                                  int64_t nthreads, AggPlan plan, uint64_t* __restrict__ out_slots) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t g = t < nthreads ? carry_g[t] : -1;
+  if (__ballot(g >= 0) == 0) return;
+  const int64_t gprev = __shfl_up(g, 1, 64);
+  const int64_t gnext = __shfl_down(g, 1, 64);
+  const bool tail = lane == 63 || gnext != g;
+  const int rec = plan.n + 1;
+  for (int s = 0; s < rec; ++s) {
+    const int op = s == 0 ? (int)OP_ADD_I64 : plan.op[s - 1];
+    if (s > 0 && plan.kind[s - 1] == DG_AGG_FLOAT_SUM) continue;
+    uint64_t v = g >= 0 ? carry_slots[t * rec + s] : 0ull;
+    // inclusive scan restricted to the run of equal g ending at this lane (runs are contiguous)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(v, o, 64);
+      const int64_t gy = __shfl_up(g, o, 64);
+      if (lane >= o && gy == g) v = combine_op(op, y, v);
+    }
+    if (g >= 0 && tail) atomic_op(op, out_slots + g * rec + s, v);
+  }
+  (void)gprev;
+}
+
+void launch_gb_reduce(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, uint64_t* out_keys,
+                      uint64_t* out_slots, uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, hipStream_t s) {
+  const int nt = sb->ntiles_sort;
+  hipLaunchKernelGGL(k_gb_reduce, dim3(nt), dim3(kST), 0, s, d_jobs, njobs, sb->keys[sb->cur], sb->refs[sb->cur], sb->n,
+                     sb->run_cnt, plan, out_keys, out_slots, head_pos, carry_g, carry_slots);
+  hipLaunchKernelGGL(k_gb_carry, dim3(nt), dim3(256), 0, s, carry_g, carry_slots, (int64_t)nt * kST, plan, out_slots);
+}
+
+// ------------------------------------------------------------------------------------------------
+// floatSum in row order (FloatSumBufferAggregator.aggregate: buf.putFloat(pos, buf.getFloat(pos) +
+// selector.getFloat()), FloatSumAggregator.combine across segments)
+// ------------------------------------------------------------------------------------------------
+// FloatColumnSelector.getFloat of the aggregator's input (segment/*ColumnSelector coercions)
+__device__ __forceinline__ float agg_float(const ColView& v, int64_t r) {
+  if (v.kind == VIEW_ABSENT) return 0.0f;
+  const uint8_t* p = cv_ptr(v, r);
+  if (v.kind == VIEW_FLOAT) return *reinterpret_cast<const float*>(p);
+  if (v.kind == VIEW_LONG) return (float)*reinterpret_cast<const int64_t*>(p);
+  return (float)*reinterpret_cast<const double*>(p);
+}
+
+__global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ jobs, int njobs,
+                                                   const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
+                                                   const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ head_pos,
+                                                   int rec, int agg, uint64_t* __restrict__ out_slots) {
+  __shared__ uint32_t s_base[kMaxCallSegs];
+  for (int x = threadIdx.x; x < njobs; x += 256) s_base[x] = jobs[x].row_base;
+  __syncthreads();
+  const uint32_t n = n_ptr[0], ng = n_ptr[1];
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (int64_t)gridDim.x * 256) {
+    const uint32_t i0 = head_pos[g], i1 = g + 1 < ng ? head_pos[g + 1] : n;
+    float total = 0.0f, sum = 0.0f;
+    int cur = -1;
+    bool first = true;
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint32_t ref = refs[i];
+      const int seg = locate_seg(s_base, njobs, ref);
+      if (seg != cur) {
+        if (cur >= 0) {
+          total = first ? sum : total + sum;
+          first = false;
+        }
+        sum = 0.0f;
+        cur = seg;
+      }
+      const GbJob& j = jobs[seg];
+      const int64_t row = (int64_t)(ref - s_base[seg]);
+      if (agg_row(j.agg_bits[agg], row)) sum = sum + agg_float(j.vals[agg], row);
+    }
+    if (cur >= 0) total = first ? sum : total + sum;
+    const uint64_t bits = (uint64_t)__double_as_longlong((double)total);
+    if (out_slots) {
+      out_slots[g * rec + 1 + agg] = bits;
+    } else if (cur >= 0) {  // per-segment engines: the run is one (segment, bucket, id) cell
+      const GbJob& j = jobs[cur];
+      const uint64_t key = keys[i0];
+      const int64_t bucket = j.bucket_bits ? (int64_t)((key >> j.bucket_shift) & ((1ull << j.bucket_bits) - 1)) : 0;
+      const int64_t id = j.ndims ? (int64_t)((key >> j.dim_shift[0]) & ((1ull << j.dim_bits[0]) - 1)) : 0;
+      j.fs_out[(bucket * j.fs_mul + id) * rec + 1 + agg] = bits;
+    }
+  }
+}
+
+void launch_fsum_runs(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, int agg, const uint32_t* head_pos,
+                      uint64_t* out_slots, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (sb->cap + 255) / 256));
+  hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->keys[sb->cur],
+                     sb->refs[sb->cur], sb->n, head_pos, plan.n + 1, agg, out_slots);
+}
+
+// ------------------------------------------------------------------------------------------------
+// finalize (device slot encoding -> the ABI's: int64 / double / float32 in the low 4 bytes) and unpack
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t finalize_dev(int kind, uint64_t s) {
+  switch (kind) {
+    case DG_AGG_COUNT:
+    case DG_AGG_LONG_SUM:
+    case DG_AGG_DOUBLE_SUM: return s;
+    case DG_AGG_FLOAT_SUM: return (uint64_t)__float_as_uint((float)__longlong_as_double((long long)s));
+    case DG_AGG_LONG_MIN:
+    case DG_AGG_LONG_MAX: return s ^ kSign;
+    case DG_AGG_DOUBLE_MIN:
+    case DG_AGG_DOUBLE_MAX: {
+      const bool nan = kind == DG_AGG_DOUBLE_MIN ? s == 0 : s == ~0ull;
+      const double d = nan ? __longlong_as_double(0x7ff8000000000000ll) : unord_key(s);
+      return (uint64_t)__double_as_longlong(d);
+    }
+    default: {
+      const bool nan = kind == DG_AGG_FLOAT_MIN ? s == 0 : s == ~0ull;
+      const float f = nan ? __uint_as_float(0x7fc00000u) : (float)unord_key(s);
+      return (uint64_t)__float_as_uint(f);
+    }
+  }
+}
+
+__global__ void k_slots_finalize(uint64_t* __restrict__ slots, const uint32_t* __restrict__ n_ptr, AggPlan plan) {
+  const int64_t ng = n_ptr[0];
+  const int rec = plan.n + 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ng * rec; i += (int64_t)gridDim.x * blockDim.x) {
+    const int s = (int)(i % rec);
+    if (s > 0) slots[i] = finalize_dev(plan.kind[s - 1], slots[i]);
+  }
+}
+
+void launch_slots_finalize(uint64_t* slots, const uint32_t* n_ptr, int64_t cap, AggPlan plan, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(16384, std::max<int64_t>(1, (cap * (plan.n + 1) + 255) / 256));
+  hipLaunchKernelGGL(k_slots_finalize, dim3((unsigned)blocks), dim3(256), 0, s, slots, n_ptr, plan);
+}
+
+__global__ void k_gb_unpack(const uint64_t* __restrict__ keys, int64_t start, int64_t count, KeyLayout lay,
+                            int64_t* __restrict__ bucket, int32_t* __restrict__ ids) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[start + i];
+    bucket[i] = lay.bucket_bits ? (int64_t)((k >> lay.bucket_shift) & ((1ull << lay.bucket_bits) - 1)) : 0;
+    for (int d = 0; d < lay.ndims; ++d)
+      ids[i * lay.ndims + d] = lay.dim_bits[d] ? (int32_t)((k >> lay.dim_shift[d]) & ((1ull << lay.dim_bits[d]) - 1)) : 0;
+  }
+}
+
+void launch_gb_unpack(const uint64_t* keys, int64_t start, int64_t count, KeyLayout lay, int64_t* bucket, int32_t* ids,
+                      hipStream_t s) {
+  if (count <= 0) return;
+  const int64_t blocks = std::min<int64_t>(16384, (count + 255) / 256);
+  hipLaunchKernelGGL(k_gb_unpack, dim3((unsigned)blocks), dim3(256), 0, s, keys, start, count, lay, bucket, ids);
+}
+
+}  // namespace dg

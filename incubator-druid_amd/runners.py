@@ -561,9 +561,11 @@ class GroupByPartial:
     only materialised when asked for."""
 
     def __init__(self, times: np.ndarray, dims: Optional[List[np.ndarray]], aggs: List[np.ndarray],
-                 codes: Optional[List[np.ndarray]] = None, dicts: Optional[List[List[Optional[str]]]] = None):
+                 codes: Optional[List[np.ndarray]] = None, dicts: Optional[List[List[Optional[str]]]] = None,
+                 merged: bool = False):
         self.times, self._dims, self.aggs = times, dims, aggs
         self.codes, self.dicts = codes, dicts
+        self.merged = merged  # already one merged, ordered result (a whole device's engine call)
 
     @property
     def dims(self) -> List[np.ndarray]:
@@ -575,39 +577,90 @@ class GroupByPartial:
         return len(self.times)
 
 
+class GroupByResult:
+    """A dg_result: the merged groups of one dg_groupby_run, resident in HBM until fetched."""
+
+    def __init__(self, handle: ctypes.c_void_p, query: Q.GroupByQuery):
+        self.handle, self.query = handle, query
+        self.groups = int(N.lib().dg_result_groups(handle))
+
+    def dictionary(self, d: int) -> List[Optional[str]]:
+        L = N.lib()
+        card = int(L.dg_result_dim_cardinality(self.handle, d))
+        offs = np.zeros(card + 1, dtype=np.int64)
+        total = ctypes.c_int64()
+        N.check(L.dg_result_dim_dictionary(self.handle, d, None, None, ctypes.byref(total)))
+        buf = ctypes.create_string_buffer(max(total.value, 1))
+        N.check(L.dg_result_dim_dictionary(self.handle, d, offs.ctypes.data, buf, ctypes.byref(total)))
+        raw = buf.raw
+        return [raw[int(offs[i]):int(offs[i + 1])].decode("utf-8") if offs[i + 1] > offs[i] else None
+                for i in range(card)]
+
+    def fetch(self, start: int = 0, count: Optional[int] = None) -> "GroupByPartial":
+        q = self.query
+        nd, na = len(q.dimensions), len(q.aggregations)
+        count = self.groups - start if count is None else count
+        t = np.zeros(max(count, 1), dtype=np.int64)
+        ids = np.zeros(max(count * nd, 1), dtype=np.int32)
+        vals = np.zeros(max(count * na, 1), dtype=np.uint64)
+        if count:
+            N.check(N.lib().dg_result_fetch_groups(self.handle, start, count, t.ctypes.data, ids.ctypes.data,
+                                                   vals.ctypes.data))
+        ids = ids[:count * nd].reshape(count, nd) if nd else np.zeros((count, 0), np.int32)
+        codes = [np.ascontiguousarray(ids[:, d]) for d in range(nd)]
+        aggs = _decode_slots(q.aggregations, vals[:count * na].reshape(count, na)) if na else []
+        return GroupByPartial(t[:count], None, aggs, codes, [self.dictionary(d) for d in range(nd)], merged=True)
+
+    def release(self):
+        if self.handle:
+            N.lib().dg_result_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+def groupby_run(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
+                stats: Optional[RunStats] = None) -> GroupByResult:
+    """One dg_groupby_run over segments of ONE device: GroupByStrategyV2.mergeRunners over their
+    per-segment runners (GroupByMergingQueryRunnerV2.java:170-290), the groups left in HBM."""
+    if len(_group_by_device(segments)) != 1:
+        raise ValueError("groupby_run: segments must share one device")
+    nd = len(query.dimensions)
+    scan, keep = N.make_scan(query, Q, segments=segments)
+    dims = (ctypes.c_char_p * max(nd, 1))(*[d.encode() for d in query.dimensions])
+    g = N.dg_groupby()
+    g.dimensions = ctypes.cast(dims, ctypes.POINTER(ctypes.c_char_p))
+    g.n_dims = nd
+    res = ctypes.c_void_p()
+    m = N.dg_metrics()
+    N.check(N.lib().dg_groupby_run(_handles(segments), len(segments), ctypes.byref(scan), ctypes.byref(g),
+                                   ctypes.byref(res), ctypes.byref(m)))
+    if stats is not None:
+        stats.add(m)
+    return GroupByResult(res, query)
+
+
+def groupby_per_device(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
+                       stats: Optional[RunStats] = None) -> List[GroupByPartial]:
+    """The merged, ordered groups of every device's segments (one engine call per device)."""
+    out = []
+    for _, idx in _group_by_device(segments).items():
+        r = groupby_run([segments[i] for i in idx], query, stats)
+        try:
+            out.append(r.fetch())
+        finally:
+            r.release()
+    return out
+
+
 def groupby_per_segment(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
                         stats: Optional[RunStats] = None) -> List[GroupByPartial]:
-    out: List[Optional[GroupByPartial]] = [None] * len(segments)
-    na = len(query.aggregations)
-    nd = len(query.dimensions)
-    for _, idx in _group_by_device(segments).items():
-        segs = [segments[i] for i in idx]
-        scan, keep = N.make_scan(query, Q, segments=segs)
-        dims = (ctypes.c_char_p * max(nd, 1))(*[d.encode() for d in query.dimensions])
-        g = N.dg_groupby()
-        g.dimensions = ctypes.cast(dims, ctypes.POINTER(ctypes.c_char_p))
-        g.n_dims = nd
-        res = ctypes.c_void_p()
-        m = N.dg_metrics()
-        N.check(N.lib().dg_groupby_run(_handles(segs), len(segs), ctypes.byref(scan), ctypes.byref(g),
-                                       ctypes.byref(res), ctypes.byref(m)))
-        if stats is not None:
-            stats.add(m)
-        try:
-            for k, i in enumerate(idx):
-                ng = max(int(N.lib().dg_result_groups(res, k)), 0)
-                t = np.zeros(max(ng, 1), dtype=np.int64)
-                ids = np.zeros(max(ng * nd, 1), dtype=np.int32)
-                vals = np.zeros(max(ng * na, 1), dtype=np.uint64)
-                N.check(N.lib().dg_result_fetch_groups(res, k, t.ctypes.data, ids.ctypes.data, vals.ctypes.data))
-                ids = ids[:ng * nd].reshape(ng, nd) if nd else np.zeros((ng, 0), np.int32)
-                codes = [np.ascontiguousarray(ids[:, d]) for d in range(nd)]
-                dicts = [segs[k].dictionary(dname) for dname in query.dimensions]
-                agg_cols = _decode_slots(query.aggregations, vals[:ng * na].reshape(ng, na)) if na else []
-                out[i] = GroupByPartial(t[:ng], None, agg_cols, codes, dicts)
-        finally:
-            N.lib().dg_result_release(res)
-    return out  # type: ignore
+    """What each segment's QueryRunner returns (createRunner(segment).run), one engine call each."""
+    return [groupby_per_device([s], query, stats)[0] for s in segments]
 
 
 def merge_groupby_columnar(query: Q.GroupByQuery, partials: Sequence[GroupByPartial]):
@@ -617,6 +670,8 @@ def merge_groupby_columnar(query: Q.GroupByQuery, partials: Sequence[GroupByPart
     nd = len(query.dimensions)
     if not parts:
         return np.zeros(0, np.int64), [np.zeros(0, object) for _ in range(nd)], [np.zeros(0) for _ in query.aggregations]
+    if len(parts) == 1 and parts[0].merged:  # the engine merged and ordered the call's segments already
+        return parts[0].times, parts[0].dims, parts[0].aggs
     times = np.concatenate([p.times for p in parts])
     keys_t = times if not gran.is_all else np.zeros(len(times), np.int64)
     dim_codes = []
@@ -655,7 +710,7 @@ def merge_groupby_columnar(query: Q.GroupByQuery, partials: Sequence[GroupByPart
         comp = t_rank.astype(np.int64)
         for c, r in zip(dim_codes, radices[1:]):
             comp = comp * r + c
-        order = np.argsort(comp)  # equal keys are folded below; introsort is deterministic
+        order = np.argsort(comp, kind="stable")  # equal keys fold in partial (segment) order
         sc = comp[order]
         change = np.ones(len(order), dtype=bool)
         if len(order) > 1:
@@ -675,9 +730,31 @@ def merge_groupby_columnar(query: Q.GroupByQuery, partials: Sequence[GroupByPart
     for a_i, a in enumerate(query.aggregations):
         col = np.concatenate([p.aggs[a_i] for p in parts])[order]
         out_aggs.append(_reduce(a, col, starts))
-    out_times = (np.minimum.reduceat(times[order], starts) if gran.is_all else sk[0][starts])
+    # ALL granularity: every merged row carries the universal timestamp, the query interval's start
+    # (GroupByStrategyV2.getUniversalTimestamp, strategy/GroupByStrategyV2.java:125-138)
+    out_times = np.full(len(starts), query.interval[0], np.int64) if gran.is_all else sk[0][starts]
     out_dims = [dim_values[d][sk[1 + d][starts]] for d in range(nd)]
     return out_times, out_dims, out_aggs
+
+
+def _java_minmax_reduce(col: np.ndarray, starts: np.ndarray, is_min: bool) -> np.ndarray:
+    """Math.min / Math.max folded over runs (DoubleMinAggregator.combine, java/lang/Math.java): NaN
+    wins, and -0.0 < 0.0 — reduced on order-preserving integer keys (the engine's ord_key)."""
+    if col.dtype == np.float32:
+        bits, sign, udt = col.view(np.uint32).astype(np.uint64), np.uint64(1 << 31), np.uint32
+    else:
+        bits, sign, udt = col.view(np.uint64), np.uint64(1 << 63), np.uint64
+    neg = (bits & sign) != 0
+    key = np.where(neg, ~bits & (sign | (sign - np.uint64(1))), bits | sign)
+    nan = np.isnan(col)
+    red = (np.minimum if is_min else np.maximum).reduceat(key, starts)
+    any_nan = np.logical_or.reduceat(nan, starts) if len(col) else np.zeros(0, bool)
+    neg_key = (red & sign) == 0
+    mask = sign | (sign - np.uint64(1))
+    raw = np.where(neg_key, ~red & mask, red & ~sign).astype(udt)
+    out = raw.view(col.dtype).copy()
+    out[any_nan] = np.nan
+    return out
 
 
 def _reduce(a: Q.AggregatorFactory, col: np.ndarray, starts: np.ndarray) -> np.ndarray:
@@ -690,10 +767,7 @@ def _reduce(a: Q.AggregatorFactory, col: np.ndarray, starts: np.ndarray) -> np.n
         return np.maximum.reduceat(col, starts)
     if k in (2, 3):
         return np.add.reduceat(col, starts)
-    # Math.min / Math.max: NaN propagates (np.minimum propagates NaN too)
-    if k in (6, 8):
-        return np.minimum.reduceat(col, starts)
-    return np.maximum.reduceat(col, starts)
+    return _java_minmax_reduce(col, starts, k in (6, 8))
 
 
 def merge_groupby(query: Q.GroupByQuery, partials: Sequence[GroupByPartial]) -> List[Q.Row]:
@@ -857,6 +931,10 @@ class GroupByQueryRunnerFactory(TimeseriesQueryRunnerFactory):
     @staticmethod
     def per_segment(segments, query, stats=None):
         return groupby_per_segment(segments, query, stats)
+
+    def run_merged(self, segments, query, stats=None):
+        # the engine merges each device's segments (GroupByMergingQueryRunnerV2); devices by value
+        return self.toolchest.merge(query, groupby_per_device(segments, query, stats))
 
 
 FACTORIES = {Q.TimeseriesQuery: TimeseriesQueryRunnerFactory(), Q.TopNQuery: TopNQueryRunnerFactory(),

@@ -1096,6 +1096,13 @@ def groupby_segment(seg: OracleSegment, query) -> List[Tuple[int, Tuple, Dict]]:
     return out
 
 
+def _universal_timestamp(query) -> int:
+    """GroupByStrategyV2.getUniversalTimestamp (query/groupby/strategy/GroupByStrategyV2.java:125-138):
+    with ALL granularity every merged row carries the start of the query's first interval
+    (AllGranularity.getIterable returns the interval itself, AllGranularity.java:70-73)."""
+    return query.intervals[0][0]
+
+
 def merge_groupby(query, per_segment: List[List]) -> List:
     gran = query.granularity
     merged: Dict = {}
@@ -1113,7 +1120,7 @@ def merge_groupby(query, per_segment: List[List]) -> List:
     for (k, vals), (bt, aggs) in merged.items():
         ev = {d: v for d, v in zip(query.dimensions, vals)}
         ev.update(aggs)
-        out.append(Q.Row(bt if gran.is_all else k, ev))
+        out.append(Q.Row(_universal_timestamp(query) if gran.is_all else k, ev))
     out.sort(key=lambda r: (r.timestamp, tuple(_jkey(r.event[d]) for d in query.dimensions)))
     return groupby_post_process(query, out)
 

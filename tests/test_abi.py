@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_structs():
     N = importlib.import_module("incubator-druid_amd._native")
-    assert N.lib().dg_abi_version() == 2
+    assert N.lib().dg_abi_version() == 3
     # struct layouts the header fixes (LP64)
     assert ctypes.sizeof(N.dg_filter) == 64
     assert ctypes.sizeof(N.dg_agg) == 32
@@ -41,7 +41,8 @@ def test_gpu_kernels_are_gfx950_code_objects():
     N = importlib.import_module("incubator-druid_amd._native")
     data = open(N.LIB_PATH, "rb").read()
     assert b"gfx950" in data
-    for k in (b"k_lz4_decode", b"k_concise_or", b"k_roaring_or", b"k_scan_agg", b"k_topn_radix", b"k_topn_compact", b"k_groupby"):
+    for k in (b"k_lz4_decode", b"k_concise_or", b"k_roaring_or", b"k_scan_agg", b"k_topn_radix", b"k_topn_compact", b"k_gb_keygen",
+              b"k_rs_scatter", b"k_gb_reduce", b"k_fsum_runs"):
         assert k in data, k
 
 
