@@ -1,16 +1,26 @@
 """Benchmark: filtered rows aggregated per second (+ HBM GB/s vs the MI355X roofline).
 
-Default workload = BASELINE.json configs[1]: TopNBenchmark 'basic' schema, topN over dimUniform
-(threshold 10, metric sumFloatNormal, aggregators longSum(sumLongSequential) +
-doubleSum(sumFloatNormal)), 4 segments x 750,000 rows per GPU, written with the reference's default
-IndexSpec (Concise bitmaps, LZ4 blocks, LONGS encoding). A step = one topN query over all of this
-rank's segments (one batched GPU call) + the cross-segment merge (TopNBinaryFn) + for N > 1 the
-cross-rank all_gather / merge. Segments are resident in HBM before timing (attached once); every
-step decodes the LZ4 blocks again, exactly as the reference decompresses blocks per query.
+Default workload = BASELINE.json configs[2], the largest single-GPU configuration: GroupByV2 over
+two high-cardinality string dimensions (dimUniform ~100k values x dimHyperUnique 100k values, both
+3-byte dictionary ids, ~1 group per row) with longSum(sumLongSequential) + doubleSum(sumFloatNormal),
+100M rows = 8 segments x 12.5M rows per GPU, 'basic' schema columns written as Druid v9 segments
+with the reference's default IndexSpec (Concise bitmaps, LZ4-HC blocks, LONGS encoding).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config topn|timeseries|groupby|filtered]
+A step = one groupBy query over the rank's 8 segments: per-segment grouping + the
+GroupByMergingQueryRunnerV2 merge by value, i.e. the merged, ordered groups, produced in HBM
+(dg_groupby_run; LZ4 blocks decoded again every step, as the reference decompresses per query).
+The groups are not copied to the host inside the timed region (the boundary hands them over as a
+dg_result; the PCIe-inclusive rate is measured after the loop and reported as `pcie_fetch`).
+For N > 1 (weak scaling, one process per GPU) the ranks' groups are exchanged by key range over RCCL
+and merged on the receiving GPU (dg_merge), so every rank ends with its range of the final result.
+
+The other configs (--config) are secondary lines / parity shapes: topn (configs[1]), timeseries
+(configs[0]), filtered (configs[3], one GPU's share), ts_hourly / groupby_hourly (configs[4]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config groupby|topn|...]
 """
 import argparse
+import ctypes
 import json
 import os
 import shutil
@@ -26,21 +36,26 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
+BASIC = {"dims": None, "metrics": None}
+GB_COLS = {"dims": ["dimUniform", "dimHyperUnique"], "metrics": ["rows", "sumLongSequential", "sumFloatNormal"]}
 CONFIGS = {
-    # name: (rows per segment, segments per GPU, description)
-    "topn": (750_000, 4, "TopNBenchmark basic: topN dimUniform threshold=10, metric sumFloatNormal, 4 x 750k rows/GPU"),
-    "topn_numeric": (750_000, 4, "TopNBenchmark basic.numericSort: topN dimUniform threshold=10, "
-                                 "DimensionTopNMetricSpec(NUMERIC), longSum, 4 x 750k rows/GPU"),
-    "topn_alphanumeric": (750_000, 4, "TopNBenchmark basic.alphanumericSort: topN dimUniform threshold=10, "
-                                      "DimensionTopNMetricSpec(ALPHANUMERIC), longSum, 4 x 750k rows/GPU"),
-    "timeseries": (750_000, 1, "TimeseriesBenchmark basic: timeseries ALL count+longSum+doubleSum, selector dimSequential=399"),
-    # 1e9 rows in 64 time-partitioned segments over 30 days, 8 segments per GPU
-    "ts_hourly": (15_625_000, 8, "1B-row dataset (64 x 15.625M rows, 30 days), 8 segments/GPU: timeseries HOUR "
-                                 "count+longSum+doubleSum+longMax+doubleMin"),
-    "groupby_hourly": (15_625_000, 8, "1B-row dataset (64 x 15.625M rows, 30 days), 8 segments/GPU: groupBy HOUR "
-                                      "(dimZipf, dimSequential) longSum+doubleSum"),
-    "groupby": (12_500_000, 1, "GroupByV2 dimUniform x dimHyperUnique + longSum/doubleSum"),
-    "filtered": (12_500_000, 1, "compound AND/OR bound+selector+in filter, timeseries count"),
+    # name: (rows per segment, segments per GPU, description, columns written)
+    "groupby": (12_500_000, 8, "BASELINE configs[2]: GroupByV2 dimUniform x dimHyperUnique (3-byte ids, ~1 group/row) "
+                               "+ longSum/doubleSum, 100M rows = 8 x 12.5M-row segments per MI355X", GB_COLS),
+    "topn": (750_000, 4, "BASELINE configs[1]: TopNBenchmark basic, topN dimUniform threshold=10 by doubleSum, "
+                         "4 x 750k rows/GPU", BASIC),
+    "topn_numeric": (750_000, 4, "TopNBenchmark basic.numericSort: DimensionTopNMetricSpec(NUMERIC), longSum, "
+                                 "4 x 750k rows/GPU", BASIC),
+    "topn_alphanumeric": (750_000, 4, "TopNBenchmark basic.alphanumericSort: DimensionTopNMetricSpec(ALPHANUMERIC), "
+                                      "longSum, 4 x 750k rows/GPU", BASIC),
+    "timeseries": (750_000, 1, "BASELINE configs[0]: TimeseriesBenchmark basic, ALL count+longSum+doubleSum, "
+                               "selector dimSequential=399", BASIC),
+    "ts_hourly": (15_625_000, 8, "BASELINE configs[4]a: 1B-row dataset (64 x 15.625M rows, 30 days), 8 segments/GPU: "
+                                 "timeseries HOUR count+longSum+doubleSum+longMax+doubleMin", BASIC),
+    "groupby_hourly": (15_625_000, 8, "BASELINE configs[4]b: same 1B-row dataset, 8 segments/GPU: groupBy HOUR "
+                                      "(dimZipf, dimSequential) longSum+doubleSum", BASIC),
+    "filtered": (12_500_000, 1, "BASELINE configs[3] (one GPU's 12.5M-row share): compound AND/OR bound+selector+in "
+                                "filter, timeseries count", BASIC),
 }
 
 
@@ -85,10 +100,10 @@ DATASET_1B = {"segments": 64, "interval": (0, 30 * 86_400_000),
 
 def _write_one(job):
     DG = importlib.import_module("incubator-druid_amd.datagen")
-    p, rows, seed, bitmap, compression, lz4_mode, part, long_encoding = job
+    p, rows, seed, bitmap, compression, lz4_mode, part, long_encoding, cols = job
     if part is None:
         DG.write_basic_segment(p, rows, seed=seed, bitmap=bitmap, compression=compression, lz4_mode=lz4_mode,
-                               long_encoding=long_encoding)
+                               long_encoding=long_encoding, dims=cols["dims"], metrics=cols["metrics"])
     else:  # time chunk `part` of the 1B-row dataset; the segment's interval is its chunk
         W = importlib.import_module("incubator-druid_amd.writer")
         n_all = DATASET_1B["segments"]
@@ -105,12 +120,14 @@ def _write_one(job):
     return p
 
 
-def ensure_segments(DG, root, rank, nseg, rows, compression, bitmap, lz4_mode, partitioned=False, workers=8,
+def ensure_segments(root, rank, nseg, rows, compression, bitmap, lz4_mode, cols, partitioned=False, workers=8,
                     long_encoding="longs"):
     """This rank's segments (seed 9999 + global segment index). partitioned: consecutive time chunks
     of the 1B-row dataset (rank r holds global chunks r*nseg ..); otherwise every segment spans the
     basic interval like the JMH benchmarks' segments. Written once, in parallel, and reused."""
     tag = ("p1b_" if partitioned else "") + ("auto_" if long_encoding == "auto" else "")
+    if cols["dims"] is not None:
+        tag += "c" + "-".join(cols["dims"] + cols["metrics"]) + "_"
     d = os.path.join(root, f"{tag}r{rows}_s{nseg}_{compression}_{bitmap}_{lz4_mode}", f"rank{rank}")
     marker = os.path.join(d, "DONE")
     paths = [os.path.join(d, f"seg{i:04d}") for i in range(nseg)]
@@ -118,23 +135,87 @@ def ensure_segments(DG, root, rank, nseg, rows, compression, bitmap, lz4_mode, p
         shutil.rmtree(d, ignore_errors=True)
         os.makedirs(d, exist_ok=True)
         jobs = [(p, rows, 9999 + rank * nseg + i, bitmap, compression, lz4_mode,
-                 (rank * nseg + i) if partitioned else None, long_encoding) for i, p in enumerate(paths)]
+                 (rank * nseg + i) if partitioned else None, long_encoding, cols) for i, p in enumerate(paths)]
+        t0 = time.time()
         if len(jobs) > 1 and workers > 1:
             import multiprocessing as mp
             with mp.get_context("spawn").Pool(min(workers, len(jobs))) as pool:
                 for p in pool.imap_unordered(_write_one, jobs):
-                    print(f"[rank {rank}] wrote {p}", file=sys.stderr, flush=True)
+                    print(f"[rank {rank}] wrote {p} ({time.time() - t0:.0f} s)", file=sys.stderr, flush=True)
         else:
             for j in jobs:
-                print(f"[rank {rank}] wrote {_write_one(j)}", file=sys.stderr, flush=True)
+                print(f"[rank {rank}] wrote {_write_one(j)} ({time.time() - t0:.0f} s)", file=sys.stderr, flush=True)
         open(marker, "w").close()
     return paths
 
 
-def cpu_baseline(Q, query, path, rows, seconds, codec="lz4", selected_fraction=1.0):
-    """The oracle (scalar CPU restatement of the reference loops) on one segment, fresh decode each run.
-    Reported in the metric's unit: selected (filtered) rows per second, i.e. the segment's rows times
-    the query's selectivity measured on the GPU side."""
+def _cpu_model():
+    try:
+        for l in open("/proc/cpuinfo"):
+            if l.startswith("model name"):
+                return l.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_threads():
+    try:
+        return max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    except (AttributeError, ValueError):
+        return max(1, min(os.cpu_count() or 1, 16))
+
+
+def cpu_baseline_groupby(paths, query, threads):
+    """oracle/libdruid_cpu.so: the reference's per-segment GroupByV2 loop (LZ4 decode, hash grouping,
+    merge by value, ordered result) in C -O3 -march=native, one segment per thread, on the whole
+    workload. Merged-dictionary maps are built before timing (the GPU engine caches them too)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    lib = ctypes.CDLL(os.path.join(REPO, "oracle", "libdruid_cpu.so"))
+    lib.cpu_groupby2.restype = ctypes.c_int64
+    lib.cpu_groupby2.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                 ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                 ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    segs = [O.OracleSegment(p) for p in paths]
+    d1, d2 = query.dimensions
+    maps = []
+    for dim in (d1, d2):
+        dicts = [s.dictionary(dim) for s in segs]
+        merged = sorted(set().union(*map(set, dicts)), key=lambda v: (v is not None, (v or "").encode("utf-16-be")))
+        index = {v: i for i, v in enumerate(merged)}
+        maps.append(([np.array([index[v] for v in dd], dtype=np.int32) for dd in dicts], len(merged)))
+    (m1, card1), (m2, _) = maps
+    ptr1 = (ctypes.c_void_p * len(segs))(*[a.ctypes.data for a in m1])
+    ptr2 = (ctypes.c_void_p * len(segs))(*[a.ctypes.data for a in m2])
+    lib.or_open.restype = ctypes.c_void_p
+    lib.or_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+    lib.or_close.argtypes = [ctypes.c_void_p]
+    err = ctypes.create_string_buffer(512)
+    hs = [lib.or_open(p.encode(), err, 512) for p in paths]  # the engine library's own segment readers
+    if not all(hs):
+        raise IOError(err.value.decode())
+    handles = (ctypes.c_void_p * len(segs))(*hs)
+    sums = (ctypes.c_double * 3)()
+    ls, ds = query.aggregations[0].fieldName, query.aggregations[1].fieldName
+    t0 = time.perf_counter()
+    ng = lib.cpu_groupby2(handles, len(segs), d1.encode(), d2.encode(), ls.encode(), ds.encode(), ptr1, ptr2, card1,
+                          threads, sums)
+    el = time.perf_counter() - t0
+    rows = sum(s.num_rows for s in segs)
+    for s, h in zip(segs, hs):
+        s.close()
+        lib.or_close(h)
+    return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"the whole step workload: {len(paths)} segments x {rows // len(paths)} rows, GroupByV2 "
+                      f"{d1} x {d2} longSum+doubleSum -> {ng} merged groups in {el:.2f} s "
+                      f"(oracle/cpu_engine.c + druid_oracle.c, C -O3 -march=native, {threads} threads, "
+                      f"LZ4 decoded per block inside the timing)",
+            "cpu_model": _cpu_model(), "groups": int(ng), "checks": [sums[0], sums[1], sums[2]]}
+
+
+def cpu_baseline_oracle(query, path, rows, seconds, selected_fraction):
+    """Secondary configs: the oracle (scalar C + numpy restatement, one thread) on one segment."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     t0 = time.perf_counter()
@@ -148,18 +229,17 @@ def cpu_baseline(Q, query, path, rows, seconds, codec="lz4", selected_fraction=1
         if el >= seconds or runs >= 50:
             break
     return {"value": rows * selected_fraction * runs / el, "unit": "rows/s", "cores": 1, "kind": "port",
-            "scanned_rows_per_s": rows * runs / el,
             "sample": f"{runs} run(s) of the query over 1 segment x {rows} rows (oracle/ C+numpy restatement, "
-                      f"single thread, {codec.upper()} decode included), {el:.1f} s; value = scanned rows/s x "
-                      f"selectivity {selected_fraction:.4g}"}
+                      f"single thread, decode included), {el:.1f} s; value = scanned rows/s x selectivity "
+                      f"{selected_fraction:.4g}", "cpu_model": _cpu_model()}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="topn", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="groupby", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--segments", type=int, default=None)
     ap.add_argument("--compression", default="lz4", choices=["lz4", "lzf", "uncompressed", "none"])
@@ -174,7 +254,6 @@ def main():
     args = ap.parse_args()
 
     Q = importlib.import_module("incubator-druid_amd.query")
-    DG = importlib.import_module("incubator-druid_amd.datagen")
     R = importlib.import_module("incubator-druid_amd.runners")
     S = importlib.import_module("incubator-druid_amd.segment")
 
@@ -186,10 +265,10 @@ def main():
         D = importlib.import_module("incubator-druid_amd.distributed")
         dist = D.init_from_env()
 
-    rows_per, nseg, desc = CONFIGS[args.config]
+    rows_per, nseg, desc, cols = CONFIGS[args.config]
     rows_per = args.rows or rows_per
     nseg = args.segments or nseg
-    paths = ensure_segments(DG, args.data_dir, rank, nseg, rows_per, args.compression, args.bitmap, args.lz4_mode,
+    paths = ensure_segments(args.data_dir, rank, nseg, rows_per, args.compression, args.bitmap, args.lz4_mode, cols,
                             partitioned=args.config in ("ts_hourly", "groupby_hourly"), workers=args.write_workers,
                             long_encoding=args.long_encoding)
     segs = [S.GpuSegment(p, device=local_rank) for p in paths]
@@ -199,9 +278,9 @@ def main():
     if dist is not None and args.config.startswith("topn"):
         gdict = D.GlobalDictionary.build(dist, [s.dictionary(query.dimension) for s in segs])
         translations = [gdict.translate(s.dictionary(query.dimension)) for s in segs]
-    gdicts = None
-    if dist is not None and args.config.startswith("groupby"):
-        gdicts = {d: D.GlobalDictionary.build(dist, [s.dictionary(d) for s in segs]) for d in query.dimensions}
+    gmerge = None
+    if dist is not None and isinstance(query, Q.GroupByQuery):
+        gmerge = D.GroupByExchange(dist, query, segs)  # cluster-wide dictionaries + maps, built once
 
     ts_buckets = None  # cluster-wide bucket keys of a timeseries query (identical on every rank), once
     if dist is not None and isinstance(query, Q.TimeseriesQuery):
@@ -222,12 +301,14 @@ def main():
             if dist is None:
                 return res
             return D.allreduce_timeseries(dist, query, res, ts_buckets)
-        per = R.groupby_per_segment(segs, query, stats)
-        if dist is None:
-            return R.merge_groupby_columnar(query, per)
-        merged = R.merge_groupby_columnar(query, per)
-        part = R.GroupByPartial(merged[0], merged[1], merged[2])
-        return D.gather_groupby(dist, query, part, gdicts)
+        res = R.groupby_run(segs, query, stats)  # merged, ordered groups in HBM
+        if dist is not None:
+            merged = gmerge.exchange(res)  # this rank's key range of the cluster-wide result, in HBM
+            res.release()
+            res = merged
+        n = res.groups
+        res.release()
+        return n
 
     import torch
     sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
@@ -250,29 +331,43 @@ def main():
         elapsed = float(t.item())
 
     steps = args.steps
-    selected_local = stats.total("selected_rows") / steps
+    calls = [c for c in stats.calls if c["segment_rows"] > 0]
+    per_step = lambda k: sum(c[k] for c in calls) / steps  # noqa: E731
+    selected_local = per_step("selected_rows")
     scanned_local = sum(s.num_rows for s in segs)
-    selected_all = selected_local * world  # every rank holds the same shape of data (weak scaling)
-    value = selected_all * steps / elapsed
-    # dominant kernel from the library's HIP-event timings (recorded on the context stream)
-    decode_ms = stats.total("decode_ms") / steps
-    agg_ms = stats.total("aggregate_ms") / steps
-    bitmap_ms = stats.total("bitmap_ms") / steps
-    bytes_read = stats.total("bytes_read") / steps
-    uncompressed_equiv = None
-    if args.config == "topn":
-        uncompressed_equiv = scanned_local * (3 + 8 + 8)
-    elif args.config.startswith("topn_"):
-        uncompressed_equiv = scanned_local * (3 + 8)
-    if decode_ms >= agg_ms and decode_ms > 0:
-        kernel, k_ms, k_bytes = ("k_lzf_decode" if args.compression == "lzf" else "k_lz4_decode"), decode_ms, bytes_read
-        if args.long_encoding == "auto":
-            kernel = "k_lz4_decode+k_vsize_expand"  # the decode phase holds both launches
-    else:
-        # the aggregation kernel reads the decoded column bytes (ids + values) of every row
-        kernel, k_ms = ("k_scan_agg" if args.config != "groupby" else "k_groupby"), agg_ms
-        k_bytes = uncompressed_equiv if uncompressed_equiv else bytes_read
-    achieved = (k_bytes / (k_ms / 1e3)) / 1e9 if k_ms > 0 else 0.0
+    value = selected_local * world * steps / elapsed  # every rank holds the same shape of data (weak scaling)
+    phases = {"bitmap": per_step("bitmap_ms"), "decode": per_step("decode_ms"), "aggregate": per_step("aggregate_ms"),
+              "query_wall": per_step("total_ms")}
+    bytes_read = per_step("bytes_read")
+    kernels = {}  # phase -> (kernel, algorithmic bytes per launch, launches per step, ms per step)
+    if phases["decode"] > 0:
+        dk = "k_lzf_decode" if args.compression == "lzf" else "k_lz4_decode"
+        kernels["decode"] = (dk if args.long_encoding == "longs" else dk + "+k_vsize_expand", bytes_read, 1,
+                             phases["decode"])
+    if isinstance(query, Q.GroupByQuery):
+        phases.update({"keygen": per_step("keygen_ms"), "sort": per_step("sort_ms"), "reduce": per_step("reduce_ms")})
+        passes = max(1, int(round(per_step("sort_passes"))))
+        n_sel = selected_local
+        # one radix pass reads and writes every (key, row ref) once: 2 x 12 B per selected row
+        kernels["sort"] = ("k_rs_hist+k_rs_binscan+k_rs_scatter", 24.0 * n_sel, passes, phases["sort"])
+        kernels["keygen"] = ("k_gb_count+k_gb_keygen", n_sel * (3 + 3 + 12), 1, phases["keygen"])
+    elif phases["aggregate"] > 0:
+        per_row = {"topn": 3 + 8 + 8}.get(args.config, 8)
+        kernels["aggregate"] = ("k_topn_bin_*" if args.config.startswith("topn") else "k_scan_agg",
+                                scanned_local * per_row, 1, phases["aggregate"])
+    if phases["bitmap"] > 0:
+        kernels["bitmap"] = ("k_concise_or+k_filter_eval" if args.bitmap == "concise" else "k_roaring_or+k_filter_eval",
+                             None, 1, phases["bitmap"])
+    dom = max(kernels, key=lambda k: kernels[k][3]) if kernels else None
+    roofline = None
+    if dom is not None:
+        kname, kbytes, launches, kms = kernels[dom]
+        per_launch_ms = kms / launches
+        achieved = (kbytes / launches) / (per_launch_ms / 1e3) / 1e9 if kbytes else None
+        roofline = {"bound": "hbm", "kernel": kname, "phase": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
+                    "bytes_per_launch": kbytes / launches if kbytes else None, "avg_launch_ms": per_launch_ms,
+                    "launches_per_step": launches}
     line = {
         "metric": "filtered rows aggregated/sec",
         "value": value,
@@ -285,37 +380,49 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int64/f64",
-        "data": "synthetic (basic schema, seeded numpy generator, written as Druid v9 segments)",
+        "data": "synthetic (basic schema columns, seeded numpy generator, written as Druid v9 segments)",
         "config": {"workload": desc, "config": args.config, "rows_per_segment": rows_per, "segments_per_gpu": nseg,
                    "compression": args.compression, "bitmap": args.bitmap, "long_encoding": args.long_encoding,
                    "parallelism": f"segments sharded over {world} GPU(s)"},
-        "roofline": {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "bytes_per_launch": k_bytes, "avg_launch_ms": k_ms},
-        "phases_ms": {"bitmap": bitmap_ms, "decode": decode_ms, "aggregate": agg_ms,
-                      "query_wall": stats.total("total_ms") / steps},
+        "roofline": roofline,
+        "phases_ms": phases,
         "stored_bytes_per_step": bytes_read,
         "rows_scanned_per_step": scanned_local * world,
     }
+    if isinstance(query, Q.GroupByQuery):
+        line["groups_per_step"] = per_step("groups")
+    if isinstance(query, Q.GroupByQuery) and dist is None:
+        # the merged result, fetched to the host once (PCIe-inclusive; not part of `value`), and checked
+        t1 = time.perf_counter()
+        res = R.groupby_run(segs, query)
+        part = res.fetch()
+        fetch_s = time.perf_counter() - t1
+        res.release()
+        line["pcie_fetch"] = {"groups": len(part), "query_plus_fetch_ms": fetch_s * 1e3,
+                              "rows_per_s_incl_fetch": scanned_local / fetch_s}
+        checks = [float(len(part)), float(np.sum(part.aggs[0], dtype=np.float64)),
+                  float(np.sum(part.aggs[1], dtype=np.float64))]
+        line["result_checks"] = {"groups": checks[0], "long_sum": checks[1], "double_sum": checks[2],
+                                 "sorted": bool(np.all(np.diff(part.codes[0].astype(np.int64) * (1 << 32) +
+                                                               part.codes[1].astype(np.int64)) > 0))}
+        del part
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(Q, query, paths[0], rows_per, args.cpu_seconds, args.compression,
-                                            selected_local / scanned_local if scanned_local else 1.0)
-        line["cpu_baseline"]["cpu_model"] = _cpu_model()
+        if args.config == "groupby":
+            cb = cpu_baseline_groupby(paths, query, _cpu_threads())
+            if "result_checks" in line:
+                rc = line["result_checks"]
+                rc["cpu_groups_equal"] = cb["groups"] == int(rc["groups"])
+                rc["cpu_long_sum_equal"] = abs(cb["checks"][1] - rc["long_sum"]) <= 1e-6 * max(1.0, abs(rc["long_sum"]))
+                rc["cpu_double_sum_rel"] = abs(cb["checks"][2] - rc["double_sum"]) / max(1.0, abs(rc["double_sum"]))
+            line["cpu_baseline"] = cb
+        else:
+            line["cpu_baseline"] = cpu_baseline_oracle(query, paths[0], rows_per, args.cpu_seconds,
+                                                       selected_local / scanned_local if scanned_local else 1.0)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-
-
-def _cpu_model():
-    try:
-        for l in open("/proc/cpuinfo"):
-            if l.startswith("model name"):
-                return l.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
 
 
 if __name__ == "__main__":

@@ -157,8 +157,15 @@ typedef struct {
   int64_t bytes_read;        /* algorithmic HBM bytes of the column blocks / bitmaps scanned */
   double bitmap_ms;          /* reportBitmapConstructionTime (device time) */
   double decode_ms;          /* column decode kernels */
-  double aggregate_ms;       /* aggregation kernels */
+  double aggregate_ms;       /* aggregation kernels (all of them, groupBy: keygen + sort + reduce) */
   double total_ms;           /* whole call, host wall */
+  /* groupBy phases (device time) and their element counts */
+  double keygen_ms;          /* selected rows -> (key, row ref) */
+  double sort_ms;            /* radix passes */
+  double reduce_ms;          /* run heads + segmented reduce + floatSum pass + finalize */
+  int32_t sort_passes;
+  int32_t key_bits;
+  int64_t groups;            /* merged groups */
 } dg_metrics;
 
 /* Aggregate values are returned in 8-byte slots: int64 for count/long*, double for double*,

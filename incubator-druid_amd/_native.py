@@ -64,7 +64,9 @@ class dg_metrics(ctypes.Structure):
     _fields_ = [("segment_rows", ctypes.c_int64), ("pre_filtered_rows", ctypes.c_int64),
                 ("selected_rows", ctypes.c_int64), ("bytes_read", ctypes.c_int64),
                 ("bitmap_ms", ctypes.c_double), ("decode_ms", ctypes.c_double),
-                ("aggregate_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+                ("aggregate_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("keygen_ms", ctypes.c_double), ("sort_ms", ctypes.c_double), ("reduce_ms", ctypes.c_double),
+                ("sort_passes", ctypes.c_int32), ("key_bits", ctypes.c_int32), ("groups", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -2456,7 +2456,9 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   DG_FLUSH(cs, st);
   hipEventRecord(ctx->ev[3], st);
   launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, st);
+  hipEventRecord(ctx->ev[5], st);
   launch_radix_sort(&sb, key_bits, st);
+  hipEventRecord(ctx->ev[6], st);
   launch_run_heads(&sb, st);
   DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));
   rc = finish_call(cs, st);  // the result is sized by the group count
@@ -2505,13 +2507,22 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   for (int i = 0; i < n; ++i)
     if (cur[i].any) m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : sv[i]->nrows;
   m.selected_rows = nsel;
-  float f1 = 0, f2 = 0, f3 = 0;
+  float f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, f6 = 0;
   hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
   hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
   hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
+  hipEventElapsedTime(&f4, ctx->ev[3], ctx->ev[5]);
+  hipEventElapsedTime(&f5, ctx->ev[5], ctx->ev[6]);
+  hipEventElapsedTime(&f6, ctx->ev[6], ctx->ev[4]);
   m.bitmap_ms = f1;
   m.decode_ms = f2;
   m.aggregate_ms = f3;
+  m.keygen_ms = f4;
+  m.sort_ms = f5;
+  m.reduce_ms = f6;  // includes the group-count read-back between the sort and the reduce
+  m.sort_passes = key_bits > 0 ? (key_bits + 7) / 8 : 0;
+  m.key_bits = key_bits;
+  m.groups = ng;
   m.total_ms = ms_since(t0);
   if (metrics) *metrics = m;
   *out = res.release();
