@@ -297,6 +297,45 @@ int32_t dg_result_dim_cardinality(const dg_result* res, int32_t dim);
 int dg_result_dim_dictionary(const dg_result* res, int32_t dim, int64_t* offsets, char* bytes, int64_t* total_bytes);
 void dg_result_release(dg_result* res);
 
+/* ---- cross-device groupBy merge (QueryRunnerFactory.mergeRunners over devices, processing/.../query/
+ * QueryRunnerFactory.java:62; GroupByMergingQueryRunnerV2.java:170-290 semantics) ----
+ * Every device runs dg_groupby_run over its segments; the devices' groups are then re-keyed into one
+ * cluster-wide key space (dg_result_export), cut into key ranges (dg_keys_partition), exchanged
+ * (RCCL all-to-all over xGMI — the transport is the caller's: torch.distributed in
+ * incubator-druid_amd/distributed.py, or the JNI shim's own communicator) and merged on the receiving
+ * device (dg_merge), which combines equal keys with the combining aggregators in partial order. */
+typedef struct {
+  int32_t n_dims;
+  const int32_t* card;      /* [n_dims] cardinality of the cluster-wide dictionary of each dimension
+                               (the union of every device's merged dictionary, Java String order,
+                               nulls first) */
+  int64_t period_ms;        /* 0 = ALL granularity */
+  int64_t bucket0;          /* non-ALL: epoch ms of bucket index 0 (on the query's period grid) */
+  int64_t n_buckets;        /* non-ALL: bucket indices [0, n_buckets) */
+  int64_t universal_time;   /* ALL: the result timestamp (GroupByStrategyV2.getUniversalTimestamp) */
+  int32_t n_aggs;
+  const int32_t* agg_kinds; /* [n_aggs] DG_AGG_* (combine semantics of each aggregator) */
+} dg_keyspace;
+
+/* total bits of a key of the key space; DG_ERR_UNSUPPORTED above 64 */
+int dg_keyspace_bits(const dg_keyspace* ks, int32_t* bits);
+/* Re-key res into the key space: maps[d][merged id of res] = cluster-wide id, strictly increasing
+ * (so the ascending order is kept). Writes dg_result_groups(res) records into caller-allocated
+ * DEVICE buffers of res's device: d_keys[n], d_slots[n * (1 + n_aggs)] (rows aggregated, then the
+ * values in the slot encoding of dg_timeseries_run). Completes before returning. */
+int dg_result_export(dg_result* res, const dg_keyspace* ks, const int32_t* const* maps, uint64_t* d_keys,
+                     uint64_t* d_slots);
+/* Key ranges of ascending device keys d_keys[n]: out_pos[i] = first index with key >= splits[i]
+ * (splits ascending, host array), i.e. range i = [out_pos[i - 1], out_pos[i]). */
+int dg_keys_partition(dg_context* ctx, const uint64_t* d_keys, int64_t n, const uint64_t* splits, int32_t n_splits,
+                      int64_t* out_pos);
+/* Merge n records (device buffers of ctx's device: keys, slots as written by dg_result_export),
+ * the concatenation of partials that are each ascending, into a dg_result in the key space. Equal
+ * keys combine in input order. The result's dimension ids are cluster-wide ids: its
+ * dg_result_dim_cardinality is ks->card[d], and the dictionary is the caller's. */
+int dg_merge(dg_context* ctx, const dg_keyspace* ks, const uint64_t* d_keys, const uint64_t* d_slots, int64_t n,
+             dg_result** out, dg_metrics* metrics);
+
 /* ---- diagnostics (test harness; no reference counterpart) ----
  * Decode n raw LZ4 blocks (host buffers, <= 64 KiB decoded each) through the same attach-time
  * checkpoint index and HIP decoder the segment path uses. out: n * 65536 bytes, block i at

@@ -1040,16 +1040,20 @@ static bool has_float_sum(const AggPlan& plan) {
   return false;
 }
 
-// device buffers of a sort-based grouping of at most `cap` rows (call scratch)
-static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, SortBufs* sb) {
+// device buffers of a sort-based grouping of at most `cap` rows with keys of key_bits bits (call
+// scratch): one 8-byte word per element [key | row ref] when both fit, else keys + a u32 ref array
+static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bits, SortBufs* sb) {
   memset(sb, 0, sizeof *sb);
   sb->cap = cap;
   sb->ntiles_sort = sort_tiles(cap);
+  const int rb = bits_for(std::max<int64_t>(cap, 1));
+  const bool packed = key_bits + rb <= 64;
+  sb->ref_bits = packed ? rb : 0;
   const size_t c = (size_t)std::max<int64_t>(cap, 1) + 16;
   for (int k = 0; k < 2; ++k) {
     sb->keys[k] = dev_take<uint64_t>(cs, c);
-    sb->refs[k] = dev_take<uint32_t>(cs, c);
-    if (!sb->keys[k] || !sb->refs[k]) return set_error(DG_ERR_OOM, "sort buffers of %lld rows", (long long)cap);
+    sb->refs[k] = packed ? nullptr : dev_take<uint32_t>(cs, c);
+    if (!sb->keys[k] || (!packed && !sb->refs[k])) return set_error(DG_ERR_OOM, "sort buffers of %lld rows", (long long)cap);
   }
   sb->tile_cnt = dev_take<uint32_t>(cs, (size_t)std::max(ntiles_keygen, 1));
   sb->n = dev_take<uint32_t>(cs, 4);
@@ -1096,7 +1100,7 @@ static int fsum_pass(CallScratch* cs, std::vector<GbJob>& gj, const std::vector<
   int rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
   if (rc) return rc;
   SortBufs sb;
-  rc = sort_bufs(cs, total, ntiles, &sb);
+  rc = sort_bufs(cs, total, ntiles, key_bits, &sb);
   if (rc) return rc;
   uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)total + 16);
   if (!head_pos) return set_error(DG_ERR_OOM, "floatSum runs");
@@ -2323,7 +2327,8 @@ struct dg_result {
   uint64_t* slots = nullptr;  // [ngroups][1 + naggs]: rows, then the ABI-encoded aggregate values
   dg::KeyLayout lay{};
   int64_t bucket0 = 0, period = 0, universal = 0;
-  std::vector<std::shared_ptr<dg::MergedDict>> dicts;
+  std::vector<std::shared_ptr<dg::MergedDict>> dicts;  // empty for a dg_merge result (cluster ids)
+  std::vector<int32_t> cards;                         // dg_merge result: cluster dictionary sizes
   ~dg_result() {
     if (!ctx) return;
     std::lock_guard<std::mutex> g(ctx->mu);
@@ -2449,7 +2454,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
   if (rc) return rc;
   SortBufs sb;
-  rc = sort_bufs(cs, total, ntiles, &sb);
+  rc = sort_bufs(cs, total, ntiles, key_bits, &sb);
   if (rc) return rc;
   uint32_t* h_n = host_take<uint32_t>(cs, 4);
   if (!h_n) return set_error(DG_ERR_OOM, "groupBy counters");
@@ -2482,28 +2487,16 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)ng + 16);
     const size_t nthr = (size_t)sb.ntiles_sort * 256;
     int64_t* carry_g = dev_take<int64_t>(cs, nthr);
+    int64_t* open_g = dev_take<int64_t>(cs, nthr);
     uint64_t* carry_slots = dev_take<uint64_t>(cs, nthr * rec);
-    if (!head_pos || !carry_g || !carry_slots) return set_error(DG_ERR_OOM, "groupBy reduce scratch");
-    launch_gb_reduce(d_jobs, n, &sb, plan, res->keys, res->slots, head_pos, carry_g, carry_slots, st);
+    if (!head_pos || !carry_g || !open_g || !carry_slots) return set_error(DG_ERR_OOM, "groupBy reduce scratch");
+    launch_gb_reduce(d_jobs, n, &sb, plan, res->keys, res->slots, head_pos, carry_g, carry_slots, open_g, st);
     for (int a = 0; a < na; ++a)
       if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, &sb, plan, a, head_pos, res->slots, st);
-    launch_slots_finalize(res->slots, sb.n + 1, ng, plan, st);
   }
   hipEventRecord(ctx->ev[4], st);
   rc = finish_call(cs, st);
   if (rc) return rc;
-  if (getenv("DG_DEBUG_GB")) {
-    uint32_t dn[2] = {0, 0};
-    uint64_t s0[4] = {0, 0, 0, 0}, k0 = 0;
-    hipMemcpy(dn, sb.n, 8, hipMemcpyDeviceToHost);
-    if (ng) {
-      hipMemcpy(s0, res->slots, 8 * std::min(rec, 4), hipMemcpyDeviceToHost);
-      hipMemcpy(&k0, res->keys, 8, hipMemcpyDeviceToHost);
-    }
-    fprintf(stderr, "[dg gb] n=%d segs nsel=%lld ng=%lld dev n=%u,%u keys=%p slots=%p k0=%llx s0=%llx,%llx,%llx cap=%lld tiles=%d\n",
-            n, (long long)nsel, (long long)ng, dn[0], dn[1], (void*)res->keys, (void*)res->slots, (unsigned long long)k0, (unsigned long long)s0[0], (unsigned long long)s0[1],
-            (unsigned long long)s0[2], (long long)sb.cap, sb.ntiles_sort);
-  }
   for (int i = 0; i < n; ++i)
     if (cur[i].any) m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : sv[i]->nrows;
   m.selected_rows = nsel;
@@ -2574,6 +2567,7 @@ int dg_result_fetch_rows(dg_result* r, int64_t start, int64_t count, int64_t* ro
 
 int dg_result_dim_dictionary(const dg_result* r, int32_t dim, int64_t* offsets, char* bytes, int64_t* total) {
   if (!r || dim < 0 || dim >= r->ndims) return set_error(DG_ERR_ARG, "dimension index %d", dim);
+  if (r->dicts.empty()) return set_error(DG_ERR_ARG, "a merged result's dictionary is the caller's cluster dictionary");
   const MergedDict& d = *r->dicts[dim];
   int64_t t = 0;
   for (size_t i = 0; i < d.values.size(); ++i) {
@@ -2588,10 +2582,199 @@ int dg_result_dim_dictionary(const dg_result* r, int32_t dim, int64_t* offsets, 
 
 int32_t dg_result_dim_cardinality(const dg_result* r, int32_t dim) {
   if (!r || dim < 0 || dim >= r->ndims) return -1;
+  if (r->dicts.empty()) return r->cards[dim];
   return (int32_t)r->dicts[dim]->values.size();
 }
 
 void dg_result_release(dg_result* r) { delete r; }
+
+// ---- cross-device merge ----
+static int keyspace_layout(const dg_keyspace* ks, KeyLayout* lay, AggPlan* plan) {
+  if (!ks || ks->n_dims < 0 || ks->n_dims > kMaxGroupDims || (ks->n_dims && !ks->card))
+    return set_error(DG_ERR_ARG, "bad key space");
+  if (ks->n_aggs < 0 || ks->n_aggs > kMaxAggs || (ks->n_aggs && !ks->agg_kinds)) return set_error(DG_ERR_ARG, "bad key space aggregators");
+  memset(lay, 0, sizeof *lay);
+  lay->ndims = ks->n_dims;
+  int shift = 0;
+  for (int d = ks->n_dims - 1; d >= 0; --d) {
+    if (ks->card[d] < 0) return set_error(DG_ERR_ARG, "cardinality of dimension %d", d);
+    lay->dim_shift[d] = shift;
+    lay->dim_bits[d] = bits_for(std::max<int64_t>(ks->card[d], 1));
+    shift += lay->dim_bits[d];
+  }
+  lay->bucket_shift = shift;
+  if (ks->period_ms < 0 || (ks->period_ms && ks->n_buckets <= 0)) return set_error(DG_ERR_ARG, "bad key space buckets");
+  lay->bucket_bits = ks->period_ms ? bits_for(ks->n_buckets) : 0;
+  if (shift + lay->bucket_bits > 64) return set_error(DG_ERR_UNSUPPORTED, "cluster groupBy key of %d bits", shift + lay->bucket_bits);
+  if (plan) {
+    memset(plan, 0, sizeof *plan);
+    plan->n = ks->n_aggs;
+    for (int a = 0; a < ks->n_aggs; ++a) {
+      const int k = ks->agg_kinds[a];
+      if (k < DG_AGG_COUNT || k > DG_AGG_FLOAT_MAX) return set_error(DG_ERR_ARG, "aggregator kind %d", k);
+      plan->kind[a] = k;
+      plan->op[a] = slot_op(k);
+    }
+  }
+  return DG_OK;
+}
+
+int dg_keyspace_bits(const dg_keyspace* ks, int32_t* bits) {
+  KeyLayout lay;
+  int rc = keyspace_layout(ks, &lay, nullptr);
+  if (rc) return rc;
+  if (bits) *bits = lay.bucket_shift + lay.bucket_bits;
+  return DG_OK;
+}
+
+int dg_result_export(dg_result* r, const dg_keyspace* ks, const int32_t* const* maps, uint64_t* d_keys, uint64_t* d_slots) {
+  if (!r) return set_error(DG_ERR_ARG, "null result");
+  KeyLayout lay;
+  AggPlan plan;
+  int rc = keyspace_layout(ks, &lay, &plan);
+  if (rc) return rc;
+  if (ks->n_dims != r->ndims || ks->n_aggs != r->naggs) return set_error(DG_ERR_ARG, "key space does not match the result");
+  if (r->ngroups > 0 && (!d_keys || !d_slots)) return set_error(DG_ERR_ARG, "null output buffer");
+  int64_t bucket_delta = 0;
+  if (ks->period_ms) {
+    if (r->period != ks->period_ms) return set_error(DG_ERR_ARG, "granularity differs from the key space");
+    const int64_t off = r->bucket0 - ks->bucket0;
+    if (off < 0 || off % ks->period_ms) return set_error(DG_ERR_ARG, "result buckets off the key space grid");
+    bucket_delta = off / ks->period_ms;  // the extent is checked on the last key below
+  } else if (r->period) {
+    return set_error(DG_ERR_ARG, "granularity differs from the key space");
+  }
+  for (int d = 0; d < r->ndims; ++d) {
+    const int32_t card = dg_result_dim_cardinality(r, d);
+    if (card > 0 && (!maps || !maps[d])) return set_error(DG_ERR_ARG, "null id map of dimension %d", d);
+    for (int32_t i = 0; i < card; ++i) {
+      const int32_t v = maps[d][i];
+      if (v < 0 || v >= ks->card[d] || (i > 0 && v <= maps[d][i - 1]))
+        return set_error(DG_ERR_ARG, "id map of dimension %d is not strictly increasing into [0, %d)", d, ks->card[d]);
+    }
+  }
+  if (r->ngroups == 0) return DG_OK;
+  CallGuard g(r->ctx);
+  CallScratch* cs = g.cs;
+  hipStream_t st = r->ctx->stream;
+  RekeyMaps rm;
+  memset(&rm, 0, sizeof rm);
+  for (int d = 0; d < r->ndims; ++d) {
+    const int32_t card = std::max(dg_result_dim_cardinality(r, d), 1);
+    int32_t* dev;
+    int32_t* h = up_take<int32_t>(cs, (size_t)card, &dev, st);
+    if (!h) return set_error(DG_ERR_OOM, "id maps");
+    if (dg_result_dim_cardinality(r, d) > 0) memcpy(h, maps[d], 4 * (size_t)card);
+    else h[0] = 0;
+    rm.m[d] = dev;
+  }
+  DG_FLUSH(cs, st);
+  launch_gb_rekey(r->keys, r->ngroups, r->lay, lay, bucket_delta, rm, d_keys, st);
+  DG_HIP(hipMemcpyAsync(d_slots, r->slots, (size_t)r->ngroups * (r->naggs + 1) * 8, hipMemcpyDeviceToDevice, st));
+  if (ks->period_ms) {  // the last group holds the largest bucket index
+    uint64_t last = 0;
+    DG_HIP(hipMemcpyAsync(&last, r->keys + r->ngroups - 1, 8, hipMemcpyDeviceToHost, st));
+    rc = finish_call(cs, st);
+    if (rc) return rc;
+    const int64_t b = r->lay.bucket_bits ? (int64_t)((last >> r->lay.bucket_shift) & ((1ull << r->lay.bucket_bits) - 1)) : 0;
+    if (b + bucket_delta >= ks->n_buckets) return set_error(DG_ERR_ARG, "result bucket beyond the key space");
+    return DG_OK;
+  }
+  return finish_call(cs, st);
+}
+
+int dg_keys_partition(dg_context* c, const uint64_t* d_keys, int64_t n, const uint64_t* splits, int32_t nsplit,
+                      int64_t* out_pos) {
+  Context* ctx = reinterpret_cast<Context*>(c);
+  if (!ctx || n < 0 || nsplit < 0 || (nsplit && (!splits || !out_pos)) || (n > 0 && !d_keys))
+    return set_error(DG_ERR_ARG, "bad arguments");
+  if (nsplit == 0) return DG_OK;
+  CallGuard g(ctx);
+  CallScratch* cs = g.cs;
+  hipStream_t st = ctx->stream;
+  uint64_t* d_split;
+  uint64_t* h = up_take<uint64_t>(cs, (size_t)nsplit, &d_split, st);
+  int64_t* d_pos = dev_take<int64_t>(cs, (size_t)nsplit);
+  int64_t* h_pos = host_take<int64_t>(cs, (size_t)nsplit);
+  if (!h || !d_pos || !h_pos) return set_error(DG_ERR_OOM, "partition tables");
+  memcpy(h, splits, 8 * (size_t)nsplit);
+  DG_FLUSH(cs, st);
+  launch_lower_bound(d_keys, n, d_split, nsplit, d_pos, st);
+  DG_HIP(hipMemcpyAsync(h_pos, d_pos, 8 * (size_t)nsplit, hipMemcpyDeviceToHost, st));
+  int rc = finish_call(cs, st);
+  if (rc) return rc;
+  memcpy(out_pos, h_pos, 8 * (size_t)nsplit);
+  return DG_OK;
+}
+
+int dg_merge(dg_context* c, const dg_keyspace* ks, const uint64_t* d_keys, const uint64_t* d_slots, int64_t n,
+             dg_result** out, dg_metrics* metrics) {
+  auto t0 = std::chrono::steady_clock::now();
+  Context* ctx = reinterpret_cast<Context*>(c);
+  if (!ctx || !out || n < 0 || (n > 0 && (!d_keys || !d_slots))) return set_error(DG_ERR_ARG, "bad arguments");
+  if (n >= (1ll << 32) - 16) return set_error(DG_ERR_UNSUPPORTED, "%lld records in one merge", (long long)n);
+  KeyLayout lay;
+  AggPlan plan;
+  int rc = keyspace_layout(ks, &lay, &plan);
+  if (rc) return rc;
+  const int key_bits = lay.bucket_shift + lay.bucket_bits;
+  const int rec = plan.n + 1;
+  CallGuard g(ctx);
+  CallScratch* cs = g.cs;
+  hipStream_t st = ctx->stream;
+  std::unique_ptr<dg_result> res(new dg_result());
+  res->ctx = ctx;
+  res->ndims = ks->n_dims;
+  res->naggs = plan.n;
+  res->lay = lay;
+  res->bucket0 = ks->bucket0;
+  res->period = ks->period_ms;
+  res->universal = ks->universal_time;
+  res->cards.assign(ks->card, ks->card + ks->n_dims);
+  dg_metrics m;
+  memset(&m, 0, sizeof m);
+  int64_t ng = 0;
+  if (n > 0) {
+    SortBufs sb;
+    rc = sort_bufs(cs, n, 1, key_bits, &sb);
+    if (rc) return rc;
+    uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)n + 16);
+    uint32_t* h_n = host_take<uint32_t>(cs, 4);
+    if (!head_pos || !h_n) return set_error(DG_ERR_OOM, "merge scratch of %lld records", (long long)n);
+    // groups <= records: the result is sized by the input (no second pass over the groups)
+    res->keys = static_cast<uint64_t*>(result_alloc(ctx, (size_t)n * 8));
+    res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)n * rec * 8));
+    if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "merged result of %lld records", (long long)n);
+    hipEventRecord(ctx->ev[3], st);
+    launch_merge_load(d_keys, n, &sb, st);
+    launch_radix_sort(&sb, key_bits, st);
+    hipEventRecord(ctx->ev[5], st);
+    launch_run_heads(&sb, st);
+    launch_run_mark(&sb, head_pos, st);
+    launch_merge_reduce(&sb, head_pos, d_slots, plan, n, res->keys, res->slots, st);
+    launch_slots_finalize(res->slots, sb.n + 1, n, plan, st);
+    DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));
+    hipEventRecord(ctx->ev[4], st);
+    rc = finish_call(cs, st);
+    if (rc) return rc;
+    ng = h_n[1];
+    float fs = 0, fr = 0;
+    hipEventElapsedTime(&fs, ctx->ev[3], ctx->ev[5]);
+    hipEventElapsedTime(&fr, ctx->ev[5], ctx->ev[4]);
+    m.sort_ms = fs;
+    m.reduce_ms = fr;
+    m.aggregate_ms = fs + fr;
+    m.sort_passes = key_bits > 0 ? (key_bits + 7) / 8 : 0;
+    m.key_bits = key_bits;
+  }
+  res->ngroups = ng;
+  m.selected_rows = n;
+  m.groups = ng;
+  m.total_ms = ms_since(t0);
+  if (metrics) *metrics = m;
+  *out = res.release();
+  return DG_OK;
+}
 
 }  // extern "C"
 

@@ -140,8 +140,9 @@ struct GbJob {
 
 // Device buffers of one sort-based grouping; *_n are device words (counts known only on the device).
 struct SortBufs {
-  uint64_t* keys[2];
-  uint32_t* refs[2];
+  uint64_t* keys[2];      // packed (refs null): [key | row ref in the low ref_bits bits]; else keys
+  uint32_t* refs[2];      // row refs when the key and the ref do not fit one word, else null
+  int ref_bits;           // packed: bits of the row ref (the sort key starts there); else 0
   int cur;                // which of the ping-pong buffers holds the result
   uint32_t* tile_cnt;     // keygen tiles: selected rows, then their offsets
   uint32_t* n;            // [0] selected rows, [1] groups
@@ -364,10 +365,12 @@ void launch_run_heads(SortBufs* sb, hipStream_t s);
 // head_pos[g] = first sorted element of run g (after launch_run_heads)
 void launch_run_mark(SortBufs* sb, uint32_t* head_pos, hipStream_t s);
 // groupBy merge of the sorted rows: one record per run (out_keys[g], out_slots[g][1 + naggs] in the
-// device slot encoding), head_pos[g] = first sorted element of run g; floatSum slots are left to
+// ABI slot encoding), head_pos[g] = first sorted element of run g; floatSum slots are left to
 // launch_fsum_runs. carry: scratch of sort_tiles(cap) * 256 entries (g) and * (1 + naggs) slots.
+// open_g: scratch like carry_g (groups written in the device encoding, finalized after the carries)
 void launch_gb_reduce(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, uint64_t* out_keys,
-                      uint64_t* out_slots, uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, hipStream_t s);
+                      uint64_t* out_slots, uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, int64_t* open_g,
+                      hipStream_t s);
 // floatSum aggregator `agg` as the reference computes it: a float32 sum in row order per run and
 // segment (FloatSumBufferAggregator.aggregate), segments combined in order with float adds
 // (FloatSumAggregator.combine). groupBy: into out_slots[g][1 + agg]; per-segment engines
@@ -385,5 +388,17 @@ struct KeyLayout {
 };
 void launch_gb_unpack(const uint64_t* keys, int64_t start, int64_t count, KeyLayout lay, int64_t* bucket, int32_t* ids,
                       hipStream_t s);
+// cross-device merge: keys of layout lin -> layout lout (bucket index + bucket_delta, ids through maps)
+struct RekeyMaps {
+  const int32_t* m[kMaxGroupDims];
+};
+void launch_gb_rekey(const uint64_t* in, int64_t n, KeyLayout lin, KeyLayout lout, int64_t bucket_delta,
+                     RekeyMaps maps, uint64_t* out, hipStream_t s);
+void launch_lower_bound(const uint64_t* keys, int64_t n, const uint64_t* split, int nsplit, int64_t* pos, hipStream_t s);
+// sort input of a merge (refs = record index, sb->n[0] = n)
+void launch_merge_load(const uint64_t* keys, int64_t n, SortBufs* sb, hipStream_t s);
+// one record per run of the sorted merge input, partial values combined in order (device encoding)
+void launch_merge_reduce(SortBufs* sb, const uint32_t* head_pos, const uint64_t* in_slots, AggPlan plan, int64_t cap,
+                         uint64_t* out_keys, uint64_t* out_slots, hipStream_t s);
 
 }  // namespace dg

@@ -139,9 +139,15 @@ __global__ __launch_bounds__(256) void k_gb_count(const GbJob* __restrict__ jobs
   if (threadIdx.x == 0) cnt[blockIdx.x] = t;
 }
 
+// element of the sort: packed = one word [key | row ref] (ref in the low sb->ref_bits bits, so equal
+// keys stay in row-ref order without a second array), otherwise key words + a u32 ref array
+__device__ __forceinline__ uint32_t elem_ref(uint64_t w, const uint32_t* refs, int64_t i, int kshift) {
+  return refs ? refs[i] : (uint32_t)(w & ((1ull << kshift) - 1ull));
+}
+
 __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                    const uint32_t* __restrict__ offs, uint64_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ refs) {
+                                                   uint32_t* __restrict__ refs, int kshift) {
   __shared__ uint32_t s_tmp[4];
   const GbJob& j = jobs[tile_job[blockIdx.x]];
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
@@ -154,8 +160,13 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
     uint32_t tot;
     const uint32_t ex = block_scan_u32<256>(sel ? 1u : 0u, &tot, s_tmp);
     if (sel) {
-      keys[base + ex] = gb_key(j, r, b);
-      refs[base + ex] = j.row_base + (uint32_t)r;
+      const uint32_t ref = j.row_base + (uint32_t)r;
+      if (refs) {
+        keys[base + ex] = gb_key(j, r, b);
+        refs[base + ex] = ref;
+      } else {
+        keys[base + ex] = (gb_key(j, r, b) << kshift) | ref;
+      }
     }
     base += tot;
   }
@@ -169,11 +180,11 @@ void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles
   hipLaunchKernelGGL(k_gb_count, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt);
   hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, sb->tile_cnt, ntiles, sb->n);
   hipLaunchKernelGGL(k_gb_keygen, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                     sb->keys[sb->cur], sb->refs[sb->cur]);
+                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits);
 }
 
 // ------------------------------------------------------------------------------------------------
-// stable LSD radix sort (keys + u32 refs), tiles of kSortTile consecutive elements
+// stable LSD radix sort (key words [+ u32 refs]), tiles of kSortTile consecutive elements
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kST) void k_rs_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
                                                  int shift, int bits, uint32_t* __restrict__ hist, int ntiles) {
@@ -227,45 +238,45 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Wave w of a tile owns its elements [w * 1024, (w + 1) * 1024) in 16 chunks of 64. Pass A ranks
-// each element among the earlier elements of its wave with the same digit (chunk order, then lane
-// order = element order); the per-digit wave counts become per-wave bases; pass B scatters.
+// Wave w of a tile owns its elements [w * 1024, (w + 1) * 1024) in 16 chunks of 64. Each element is
+// ranked among the earlier elements of its wave with the same digit (chunk order, then lane order =
+// element order); the tile is then reordered by digit in LDS, so the global stores of a wave run
+// along each digit's contiguous output range (coalesced) instead of scattering lane by lane.
+template <bool REFS>
 __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     const uint32_t* __restrict__ n_ptr, int shift, int bits,
                                                     const uint32_t* __restrict__ hist,
                                                     const uint32_t* __restrict__ bin_total, int ntiles) {
+  __shared__ uint64_t s_k[kSortTile];
+  __shared__ uint32_t s_v[REFS ? kSortTile : 1];
   __shared__ uint32_t s_cnt[4 * 256];
-  __shared__ uint32_t s_base[256];
+  __shared__ int64_t s_delta[256];  // global position of tile-sorted element i of digit d = s_delta[d] + i
   __shared__ uint32_t s_tmp[4];
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
   if (base >= n) return;
+  const int tile_n = (int)min<int64_t>(kSortTile, (int64_t)n - base);
   const int nb = 1 << bits;
+  const uint64_t dmask = (uint64_t)(nb - 1);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  {
-    const uint32_t v = tid < nb ? bin_total[tid] : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_scan_u32<kST>(v, &tot, s_tmp);
-    if (tid < nb) s_base[tid] = ex + hist[(size_t)tid * ntiles + blockIdx.x];
-  }
   for (int i = tid; i < 4 * 256; i += kST) s_cnt[i] = 0;
   __syncthreads();
   uint64_t k[kSPT];
   uint32_t v[kSPT], rank[kSPT];
-  const int64_t wbase = base + (int64_t)wave * (kSortTile / 4);
+  const int wbase = wave * (kSortTile / 4);
 #pragma unroll
   for (int c = 0; c < kSPT; ++c) {
-    const int64_t i = wbase + c * 64 + lane;
-    const bool ok = i < n;
-    k[c] = ok ? kin[i] : 0ull;
-    v[c] = ok ? vin[i] : 0u;
+    const int x = wbase + c * 64 + lane;
+    const bool ok = x < tile_n;
+    k[c] = ok ? kin[base + x] : 0ull;
+    if (REFS) v[c] = ok ? vin[base + x] : 0u;
   }
   uint32_t* cnt = s_cnt + wave * 256;
 #pragma unroll
   for (int c = 0; c < kSPT; ++c) {
-    const bool ok = wbase + c * 64 + lane < n;
-    const uint32_t d = (uint32_t)(k[c] >> shift) & (uint32_t)(nb - 1);
+    const bool ok = wbase + c * 64 + lane < tile_n;
+    const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
     const uint64_t peers = match_digit(d, bits, ok);
     uint32_t prior = 0;
     if (ok) prior = cnt[d];
@@ -275,23 +286,38 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
     if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
   }
   __syncthreads();
-  if (tid < nb) {
-    uint32_t run = s_base[tid];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const uint32_t x = s_cnt[w * 256 + tid];
-      s_cnt[w * 256 + tid] = run;
-      run += x;
+  // per digit: tile offset (scan over digits of the tile's counts), wave offsets inside it, and the
+  // digit's global base (earlier digits' totals + earlier tiles' counts of this digit)
+  {
+    const uint32_t c0 = tid < nb ? s_cnt[tid] : 0u, c1 = tid < nb ? s_cnt[256 + tid] : 0u;
+    const uint32_t c2 = tid < nb ? s_cnt[512 + tid] : 0u, c3 = tid < nb ? s_cnt[768 + tid] : 0u;
+    uint32_t tot;
+    const uint32_t toff = block_scan_u32<kST>(c0 + c1 + c2 + c3, &tot, s_tmp);
+    const uint32_t gtot = tid < nb ? bin_total[tid] : 0u;
+    const uint32_t gex = block_scan_u32<kST>(gtot, &tot, s_tmp);
+    if (tid < nb) {
+      s_cnt[tid] = toff;
+      s_cnt[256 + tid] = toff + c0;
+      s_cnt[512 + tid] = toff + c0 + c1;
+      s_cnt[768 + tid] = toff + c0 + c1 + c2;
+      s_delta[tid] = (int64_t)gex + (int64_t)hist[(size_t)tid * ntiles + blockIdx.x] - (int64_t)toff;
     }
   }
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < kSPT; ++c) {
-    if (wbase + c * 64 + lane >= n) continue;
-    const uint32_t d = (uint32_t)(k[c] >> shift) & (uint32_t)(nb - 1);
-    const uint32_t pos = cnt[d] + rank[c];
-    kout[pos] = k[c];
-    vout[pos] = v[c];
+    if (wbase + c * 64 + lane >= tile_n) continue;
+    const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
+    const uint32_t lp = cnt[d] + rank[c];
+    s_k[lp] = k[c];
+    if (REFS) s_v[lp] = v[c];
+  }
+  __syncthreads();
+  for (int i = tid; i < tile_n; i += kST) {
+    const uint64_t kk = s_k[i];
+    const int64_t pos = s_delta[(kk >> shift) & dmask] + i;
+    kout[pos] = kk;
+    if (REFS) vout[pos] = s_v[i];
   }
 }
 
@@ -300,13 +326,18 @@ void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
   const int npass = (key_bits + 7) / 8;
   const int w = (key_bits + npass - 1) / npass;
   const int nt = sb->ntiles_sort;
-  for (int p = 0, shift = 0; p < npass; ++p, shift += w) {
-    const int bits = std::min(w, key_bits - shift);
+  for (int p = 0, off = 0; p < npass; ++p, off += w) {
+    const int bits = std::min(w, key_bits - off);
+    const int shift = sb->ref_bits + off;
     const int in = sb->cur, out = sb->cur ^ 1;
     hipLaunchKernelGGL(k_rs_hist, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->n, shift, bits, sb->hist, nt);
     hipLaunchKernelGGL(k_rs_binscan, dim3(1 << bits), dim3(1024), 0, s, sb->hist, nt, sb->bin_total);
-    hipLaunchKernelGGL(k_rs_scatter, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
-                       sb->refs[out], sb->n, shift, bits, sb->hist, sb->bin_total, nt);
+    if (sb->refs[in])
+      hipLaunchKernelGGL(k_rs_scatter<true>, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
+                         sb->refs[out], sb->n, shift, bits, sb->hist, sb->bin_total, nt);
+    else
+      hipLaunchKernelGGL(k_rs_scatter<false>, dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out], nullptr,
+                         sb->n, shift, bits, sb->hist, sb->bin_total, nt);
     sb->cur = out;
   }
 }
@@ -315,7 +346,7 @@ void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
 // runs of equal keys (= groups, in output order)
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kST) void k_run_count(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
-                                                   uint32_t* __restrict__ run_cnt) {
+                                                   int kshift, uint32_t* __restrict__ run_cnt) {
   __shared__ uint32_t s_tmp[4];
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
@@ -324,7 +355,7 @@ __global__ __launch_bounds__(kST) void k_run_count(const uint64_t* __restrict__ 
 #pragma unroll 4
     for (int q = 0; q < kSPT; ++q) {
       const int64_t i = base + q * kST + threadIdx.x;
-      if (i < n) c += (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+      if (i < n) c += (i == 0 || (keys[i] >> kshift) != (keys[i - 1] >> kshift)) ? 1u : 0u;
     }
   }
   const uint32_t t = block_sum_u32<kST>(c, s_tmp);
@@ -332,13 +363,15 @@ __global__ __launch_bounds__(kST) void k_run_count(const uint64_t* __restrict__ 
 }
 
 void launch_run_heads(SortBufs* sb, hipStream_t s) {
-  hipLaunchKernelGGL(k_run_count, dim3(sb->ntiles_sort), dim3(kST), 0, s, sb->keys[sb->cur], sb->n, sb->run_cnt);
+  hipLaunchKernelGGL(k_run_count, dim3(sb->ntiles_sort), dim3(kST), 0, s, sb->keys[sb->cur], sb->n, sb->ref_bits,
+                     sb->run_cnt);
   hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, sb->run_cnt, sb->ntiles_sort, sb->n + 1);
 }
 
 // head_pos[g] = first element of run g (per-segment engines; the groupBy reduce writes its own)
 __global__ __launch_bounds__(kST) void k_run_mark(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
-                                                  const uint32_t* __restrict__ run_off, uint32_t* __restrict__ head_pos) {
+                                                  int kshift, const uint32_t* __restrict__ run_off,
+                                                  uint32_t* __restrict__ head_pos) {
   __shared__ uint32_t s_tmp[4];
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
@@ -347,7 +380,7 @@ __global__ __launch_bounds__(kST) void k_run_mark(const uint64_t* __restrict__ k
   uint32_t h = 0;
   for (int q = 0; q < kSPT; ++q) {
     const int64_t i = x0 + q;
-    if (i < n && (i == 0 || keys[i] != keys[i - 1])) h |= 1u << q;
+    if (i < n && (i == 0 || (keys[i] >> kshift) != (keys[i - 1] >> kshift))) h |= 1u << q;
   }
   uint32_t tot;
   uint32_t g = run_off[blockIdx.x] + block_scan_u32<kST>((uint32_t)__popc(h), &tot, s_tmp);
@@ -356,188 +389,12 @@ __global__ __launch_bounds__(kST) void k_run_mark(const uint64_t* __restrict__ k
 }
 
 void launch_run_mark(SortBufs* sb, uint32_t* head_pos, hipStream_t s) {
-  hipLaunchKernelGGL(k_run_mark, dim3(sb->ntiles_sort), dim3(kST), 0, s, sb->keys[sb->cur], sb->n, sb->run_cnt, head_pos);
+  hipLaunchKernelGGL(k_run_mark, dim3(sb->ntiles_sort), dim3(kST), 0, s, sb->keys[sb->cur], sb->n, sb->ref_bits,
+                     sb->run_cnt, head_pos);
 }
 
 // ------------------------------------------------------------------------------------------------
-// groupBy reduce: the merged grouper's records (AggregatorFactory.combine semantics across segments
-// = the per-row aggregate ops, both exact for counts / long sums / min / max)
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ jobs, int njobs,
-                                                   const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
-                                                   const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ run_off,
-                                                   AggPlan plan, uint64_t* __restrict__ out_keys,
-                                                   uint64_t* __restrict__ out_slots, uint32_t* __restrict__ head_pos,
-                                                   int64_t* __restrict__ carry_g, uint64_t* __restrict__ carry_slots) {
-  __shared__ uint64_t s_key[kSortTile + 1];
-  __shared__ uint32_t s_ref[kSortTile];
-  __shared__ uint32_t s_base[kMaxCallSegs];
-  __shared__ uint32_t s_tmp[4];
-  const uint32_t n = *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  const int64_t gt = (int64_t)blockIdx.x * kST + threadIdx.x;
-  carry_g[gt] = -1;
-  if (base >= n) return;
-  const int tid = threadIdx.x;
-  for (int x = tid; x < kSortTile; x += kST) {
-    const int64_t i = base + x;
-    s_key[1 + x] = i < n ? keys[i] : 0ull;
-    s_ref[x] = i < n ? refs[i] : 0u;
-  }
-  if (tid == 0) s_key[0] = base > 0 ? keys[base - 1] : ~keys[0];
-  for (int x = tid; x < njobs; x += kST) s_base[x] = jobs[x].row_base;
-  __syncthreads();
-  const int na = plan.n, rec = na + 1;
-  const int x0 = tid * kSPT;
-  const int m = (int)max<int64_t>(0, min<int64_t>(kSPT, (int64_t)n - base - x0));
-  uint32_t h = 0;
-  for (int q = 0; q < m; ++q)
-    if (s_key[1 + x0 + q] != s_key[x0 + q]) h |= 1u << q;
-  uint32_t tot;
-  const uint32_t ex = block_scan_u32<kST>((uint32_t)__popc(h), &tot, s_tmp);
-  if (m == 0) return;
-  // group of the thread's first element: the next head's index, or the open group before it
-  int64_t g = (int64_t)run_off[blockIdx.x] + ex - ((h & 1u) ? 0 : 1);
-  bool owner = h & 1u;
-  uint64_t acc[kMaxAggs + 1];
-  auto reset = [&]() {
-    acc[0] = 0;
-#pragma unroll
-    for (int a = 0; a < kMaxAggs; ++a) acc[1 + a] = a < na ? identity_of(plan.op[a], plan.kind[a]) : 0ull;
-  };
-  auto flush = [&]() {
-    if (owner) {
-      for (int s = 0; s < rec; ++s) out_slots[g * rec + s] = acc[s];
-    } else {  // the group's head (and record) belongs to an earlier thread: carry the partial
-      carry_g[gt] = g;
-      for (int s = 0; s < rec; ++s) carry_slots[gt * rec + s] = acc[s];
-    }
-  };
-  reset();
-  for (int q = 0; q < m; ++q) {
-    const uint64_t key = s_key[1 + x0 + q];
-    if ((h >> q) & 1u) {
-      if (q > 0) {
-        flush();
-        g++;
-        owner = true;
-        reset();
-      }
-      head_pos[g] = (uint32_t)(base + x0 + q);
-      out_keys[g] = key;
-    }
-    const uint32_t ref = s_ref[x0 + q];
-    const int seg = locate_seg(s_base, njobs, ref);
-    const GbJob& j = jobs[seg];
-    const int64_t row = (int64_t)(ref - s_base[seg]);
-    acc[0] += 1;
-#pragma unroll
-    for (int a = 0; a < kMaxAggs; ++a)
-      if (a < na && plan.kind[a] != DG_AGG_FLOAT_SUM) acc[1 + a] = combine_op(plan.op[a], acc[1 + a], agg_in(j, plan, a, row));
-  }
-  flush();
-}
-
-// carried partials -> their group's record: equal groups are consecutive, so one segmented combine
-// per wave and one atomic per (wave, group, slot)
-__global__ __launch_bounds__(256) void k_gb_carry(const int64_t* __restrict__ carry_g, const uint64_t* __restrict__ carry_slots,
-                                                  int64_t nthreads, AggPlan plan, uint64_t* __restrict__ out_slots) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const int64_t g = t < nthreads ? carry_g[t] : -1;
-  if (__ballot(g >= 0) == 0) return;
-  const int64_t gprev = __shfl_up(g, 1, 64);
-  const int64_t gnext = __shfl_down(g, 1, 64);
-  const bool tail = lane == 63 || gnext != g;
-  const int rec = plan.n + 1;
-  for (int s = 0; s < rec; ++s) {
-    const int op = s == 0 ? (int)OP_ADD_I64 : plan.op[s - 1];
-    if (s > 0 && plan.kind[s - 1] == DG_AGG_FLOAT_SUM) continue;
-    uint64_t v = g >= 0 ? carry_slots[t * rec + s] : 0ull;
-    // inclusive scan restricted to the run of equal g ending at this lane (runs are contiguous)
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t y = __shfl_up(v, o, 64);
-      const int64_t gy = __shfl_up(g, o, 64);
-      if (lane >= o && gy == g) v = combine_op(op, y, v);
-    }
-    if (g >= 0 && tail) atomic_op(op, out_slots + g * rec + s, v);
-  }
-  (void)gprev;
-}
-
-void launch_gb_reduce(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, uint64_t* out_keys,
-                      uint64_t* out_slots, uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, hipStream_t s) {
-  const int nt = sb->ntiles_sort;
-  hipLaunchKernelGGL(k_gb_reduce, dim3(nt), dim3(kST), 0, s, d_jobs, njobs, sb->keys[sb->cur], sb->refs[sb->cur], sb->n,
-                     sb->run_cnt, plan, out_keys, out_slots, head_pos, carry_g, carry_slots);
-  hipLaunchKernelGGL(k_gb_carry, dim3(nt), dim3(256), 0, s, carry_g, carry_slots, (int64_t)nt * kST, plan, out_slots);
-}
-
-// ------------------------------------------------------------------------------------------------
-// floatSum in row order (FloatSumBufferAggregator.aggregate: buf.putFloat(pos, buf.getFloat(pos) +
-// selector.getFloat()), FloatSumAggregator.combine across segments)
-// ------------------------------------------------------------------------------------------------
-// FloatColumnSelector.getFloat of the aggregator's input (segment/*ColumnSelector coercions)
-__device__ __forceinline__ float agg_float(const ColView& v, int64_t r) {
-  if (v.kind == VIEW_ABSENT) return 0.0f;
-  const uint8_t* p = cv_ptr(v, r);
-  if (v.kind == VIEW_FLOAT) return *reinterpret_cast<const float*>(p);
-  if (v.kind == VIEW_LONG) return (float)*reinterpret_cast<const int64_t*>(p);
-  return (float)*reinterpret_cast<const double*>(p);
-}
-
-__global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ jobs, int njobs,
-                                                   const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
-                                                   const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ head_pos,
-                                                   int rec, int agg, uint64_t* __restrict__ out_slots) {
-  __shared__ uint32_t s_base[kMaxCallSegs];
-  for (int x = threadIdx.x; x < njobs; x += 256) s_base[x] = jobs[x].row_base;
-  __syncthreads();
-  const uint32_t n = n_ptr[0], ng = n_ptr[1];
-  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (int64_t)gridDim.x * 256) {
-    const uint32_t i0 = head_pos[g], i1 = g + 1 < ng ? head_pos[g + 1] : n;
-    float total = 0.0f, sum = 0.0f;
-    int cur = -1;
-    bool first = true;
-    for (uint32_t i = i0; i < i1; ++i) {
-      const uint32_t ref = refs[i];
-      const int seg = locate_seg(s_base, njobs, ref);
-      if (seg != cur) {
-        if (cur >= 0) {
-          total = first ? sum : total + sum;
-          first = false;
-        }
-        sum = 0.0f;
-        cur = seg;
-      }
-      const GbJob& j = jobs[seg];
-      const int64_t row = (int64_t)(ref - s_base[seg]);
-      if (agg_row(j.agg_bits[agg], row)) sum = sum + agg_float(j.vals[agg], row);
-    }
-    if (cur >= 0) total = first ? sum : total + sum;
-    const uint64_t bits = (uint64_t)__double_as_longlong((double)total);
-    if (out_slots) {
-      out_slots[g * rec + 1 + agg] = bits;
-    } else if (cur >= 0) {  // per-segment engines: the run is one (segment, bucket, id) cell
-      const GbJob& j = jobs[cur];
-      const uint64_t key = keys[i0];
-      const int64_t bucket = j.bucket_bits ? (int64_t)((key >> j.bucket_shift) & ((1ull << j.bucket_bits) - 1)) : 0;
-      const int64_t id = j.ndims ? (int64_t)((key >> j.dim_shift[0]) & ((1ull << j.dim_bits[0]) - 1)) : 0;
-      j.fs_out[(bucket * j.fs_mul + id) * rec + 1 + agg] = bits;
-    }
-  }
-}
-
-void launch_fsum_runs(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, int agg, const uint32_t* head_pos,
-                      uint64_t* out_slots, hipStream_t s) {
-  const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (sb->cap + 255) / 256));
-  hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->keys[sb->cur],
-                     sb->refs[sb->cur], sb->n, head_pos, plan.n + 1, agg, out_slots);
-}
-
-// ------------------------------------------------------------------------------------------------
-// finalize (device slot encoding -> the ABI's: int64 / double / float32 in the low 4 bytes) and unpack
+// finalize: device slot encoding -> the ABI's (int64 / double / float32 in the low 4 bytes)
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t finalize_dev(int kind, uint64_t s) {
   switch (kind) {
@@ -561,6 +418,239 @@ __device__ __forceinline__ uint64_t finalize_dev(int kind, uint64_t s) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// groupBy reduce: the merged grouper's records (AggregatorFactory.combine semantics across segments
+// = the per-row aggregate ops, both exact for counts / long sums / min / max)
+// ------------------------------------------------------------------------------------------------
+// A thread owns kSPT consecutive sorted elements. A group whose head and end both lie in one thread
+// is written finalized (ABI encoding) by that thread. A group crossing a thread boundary is written
+// by its head's thread in the device encoding (open_g), later threads send their partials to carry
+// slots; k_gb_carry folds the carries in and k_gb_open_finalize finalizes the open groups.
+// floatSum slots are left to k_fsum_runs.
+template <bool REFS>
+__global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ jobs, int njobs,
+                                                   const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
+                                                   int kshift, const uint32_t* __restrict__ n_ptr,
+                                                   const uint32_t* __restrict__ run_off, AggPlan plan,
+                                                   uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_slots,
+                                                   uint32_t* __restrict__ head_pos, int64_t* __restrict__ carry_g,
+                                                   uint64_t* __restrict__ carry_slots, int64_t* __restrict__ open_g) {
+  // tile in LDS, one pad word per 16 elements (a thread reads its 16 consecutive elements; without
+  // the pad the 64 lanes' rows of 128 bytes would all start on one bank)
+  __shared__ uint64_t s_key[kSortTile + kSortTile / 16];
+  __shared__ uint32_t s_ref[kSortTile + kSortTile / 16];
+  __shared__ uint32_t s_base[kMaxCallSegs];
+  __shared__ uint32_t s_tmp[4];
+  __shared__ uint64_t s_edge[2];  // keys of the elements just before and just after the tile
+  const uint32_t n = *n_ptr;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int64_t gt = (int64_t)blockIdx.x * kST + threadIdx.x;
+  carry_g[gt] = -1;
+  open_g[gt] = -1;
+  if (base >= n) return;
+  const int tid = threadIdx.x;
+  const uint64_t kmask = kshift ? ((1ull << kshift) - 1ull) : 0ull;
+  for (int x = tid; x < kSortTile; x += kST) {
+    const int64_t i = base + x;
+    const uint64_t w = i < n ? keys[i] : 0ull;
+    const int px = x + (x >> 4);
+    s_key[px] = w >> kshift;
+    s_ref[px] = REFS ? (i < n ? refs[i] : 0u) : (uint32_t)(w & kmask);
+  }
+  if (tid == 0) {
+    s_edge[0] = base > 0 ? keys[base - 1] >> kshift : ~(keys[0] >> kshift);
+    s_edge[1] = base + kSortTile < n ? keys[base + kSortTile] >> kshift : 0ull;
+  }
+  for (int x = tid; x < njobs; x += kST) s_base[x] = jobs[x].row_base;
+  __syncthreads();
+  const int na = plan.n;
+  const int x0 = tid * kSPT;
+  const int m = (int)max<int64_t>(0, min<int64_t>(kSPT, (int64_t)n - base - x0));
+  uint64_t kr[kSPT];
+#pragma unroll
+  for (int q = 0; q < kSPT; ++q) kr[q] = s_key[tid * 17 + q];
+  const uint64_t prev = tid > 0 ? s_key[tid * 17 - 2] : s_edge[0];  // element x0 - 1 (last of thread tid - 1)
+  uint32_t h = 0;
+#pragma unroll
+  for (int q = 0; q < kSPT; ++q)
+    if (q < m && kr[q] != (q ? kr[q - 1] : prev)) h |= 1u << q;
+  // does the element after my range start a new group (or is there none)?
+  bool next_head = true;
+  if (m == kSPT && base + x0 + kSPT < n) {
+    const uint64_t nk = tid + 1 < kST ? s_key[(tid + 1) * 17] : s_edge[1];
+    next_head = nk != kr[kSPT - 1];
+  }
+  uint32_t tot;
+  const uint32_t ex = block_scan_u32<kST>((uint32_t)__popc(h), &tot, s_tmp);
+  if (m == 0) return;
+  // group of the thread's first element: the next head's index, or the open group before it
+  int64_t g = (int64_t)run_off[blockIdx.x] + ex - ((h & 1u) ? 0 : 1);
+  bool owner = h & 1u;
+  uint64_t acc[kMaxAggs];
+  uint64_t rows = 0;
+  auto reset = [&]() {
+    rows = 0;
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; ++a) acc[a] = a < na ? identity_of(plan.op[a], plan.kind[a]) : 0ull;
+  };
+  const int rec = na + 1;
+  auto flush = [&](bool complete) {
+    if (owner) {
+      uint64_t* o = out_slots + g * rec;
+      o[0] = rows;
+#pragma unroll
+      for (int a = 0; a < kMaxAggs; ++a)
+        if (a < na && plan.kind[a] != DG_AGG_FLOAT_SUM) o[1 + a] = complete ? finalize_dev(plan.kind[a], acc[a]) : acc[a];
+      if (!complete) open_g[gt] = g;
+    } else {  // the group's head (and record) belongs to an earlier thread: carry the partial
+      carry_g[gt] = g;
+      uint64_t* o = carry_slots + gt * rec;
+      o[0] = rows;
+#pragma unroll
+      for (int a = 0; a < kMaxAggs; ++a)
+        if (a < na) o[1 + a] = acc[a];
+    }
+  };
+  reset();
+  for (int q = 0; q < m; ++q) {
+    if ((h >> q) & 1u) {
+      if (q > 0) {
+        flush(true);
+        g++;
+        owner = true;
+        reset();
+      }
+      head_pos[g] = (uint32_t)(base + x0 + q);
+      out_keys[g] = s_key[tid * 17 + q];
+    }
+    const uint32_t ref = s_ref[tid * 17 + q];
+    const int seg = locate_seg(s_base, njobs, ref);
+    const GbJob& j = jobs[seg];
+    const int64_t row = (int64_t)(ref - s_base[seg]);
+    rows += 1;
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; ++a)
+      if (a < na && plan.kind[a] != DG_AGG_FLOAT_SUM) acc[a] = combine_op(plan.op[a], acc[a], agg_in(j, plan, a, row));
+  }
+  flush(next_head);
+}
+
+// carried partials -> their group's record: equal groups are consecutive, so one segmented combine
+// per wave and one atomic per (wave, group, slot)
+__global__ __launch_bounds__(256) void k_gb_carry(const int64_t* __restrict__ carry_g, const uint64_t* __restrict__ carry_slots,
+                                                  int64_t nthreads, AggPlan plan, uint64_t* __restrict__ out_slots) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t g = t < nthreads ? carry_g[t] : -1;
+  if (__ballot(g >= 0) == 0) return;
+  const int64_t gnext = __shfl_down(g, 1, 64);
+  const bool tail = lane == 63 || gnext != g;
+  const int rec = plan.n + 1;
+  for (int s = 0; s < rec; ++s) {
+    const int op = s == 0 ? (int)OP_ADD_I64 : plan.op[s - 1];
+    if (s > 0 && plan.kind[s - 1] == DG_AGG_FLOAT_SUM) continue;
+    uint64_t v = g >= 0 ? carry_slots[t * rec + s] : 0ull;
+    // inclusive scan restricted to the run of equal g ending at this lane (runs are contiguous)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(v, o, 64);
+      const int64_t gy = __shfl_up(g, o, 64);
+      if (lane >= o && gy == g) v = combine_op(op, y, v);
+    }
+    if (g >= 0 && tail) atomic_op(op, out_slots + g * rec + s, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gb_open_finalize(const int64_t* __restrict__ open_g, int64_t nthreads, AggPlan plan,
+                                                          uint64_t* __restrict__ out_slots) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t g = t < nthreads ? open_g[t] : -1;
+  if (g < 0) return;
+  const int rec = plan.n + 1;
+  for (int a = 0; a < plan.n; ++a)
+    if (plan.kind[a] != DG_AGG_FLOAT_SUM) out_slots[g * rec + 1 + a] = finalize_dev(plan.kind[a], out_slots[g * rec + 1 + a]);
+}
+
+void launch_gb_reduce(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, uint64_t* out_keys,
+                      uint64_t* out_slots, uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, int64_t* open_g,
+                      hipStream_t s) {
+  const int nt = sb->ntiles_sort;
+  const uint32_t* refs = sb->refs[sb->cur];
+  if (refs)
+    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kST), 0, s, d_jobs, njobs, sb->keys[sb->cur], refs, sb->ref_bits,
+                       sb->n, sb->run_cnt, plan, out_keys, out_slots, head_pos, carry_g, carry_slots, open_g);
+  else
+    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kST), 0, s, d_jobs, njobs, sb->keys[sb->cur], refs, sb->ref_bits,
+                       sb->n, sb->run_cnt, plan, out_keys, out_slots, head_pos, carry_g, carry_slots, open_g);
+  hipLaunchKernelGGL(k_gb_carry, dim3(nt), dim3(256), 0, s, carry_g, carry_slots, (int64_t)nt * kST, plan, out_slots);
+  hipLaunchKernelGGL(k_gb_open_finalize, dim3(nt), dim3(256), 0, s, open_g, (int64_t)nt * kST, plan, out_slots);
+}
+
+// ------------------------------------------------------------------------------------------------
+// floatSum in row order (FloatSumBufferAggregator.aggregate: buf.putFloat(pos, buf.getFloat(pos) +
+// selector.getFloat()), FloatSumAggregator.combine across segments)
+// ------------------------------------------------------------------------------------------------
+// FloatColumnSelector.getFloat of the aggregator's input (segment/*ColumnSelector coercions)
+__device__ __forceinline__ float agg_float(const ColView& v, int64_t r) {
+  if (v.kind == VIEW_ABSENT) return 0.0f;
+  const uint8_t* p = cv_ptr(v, r);
+  if (v.kind == VIEW_FLOAT) return *reinterpret_cast<const float*>(p);
+  if (v.kind == VIEW_LONG) return (float)*reinterpret_cast<const int64_t*>(p);
+  return (float)*reinterpret_cast<const double*>(p);
+}
+
+__global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ jobs, int njobs,
+                                                   const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
+                                                   int kshift, const uint32_t* __restrict__ n_ptr,
+                                                   const uint32_t* __restrict__ head_pos, int rec, int agg,
+                                                   uint64_t* __restrict__ out_slots) {
+  __shared__ uint32_t s_base[kMaxCallSegs];
+  for (int x = threadIdx.x; x < njobs; x += 256) s_base[x] = jobs[x].row_base;
+  __syncthreads();
+  const uint32_t n = n_ptr[0], ng = n_ptr[1];
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (int64_t)gridDim.x * 256) {
+    const uint32_t i0 = head_pos[g], i1 = g + 1 < ng ? head_pos[g + 1] : n;
+    float total = 0.0f, sum = 0.0f;
+    int cur = -1;
+    bool first = true;
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint32_t ref = elem_ref(keys[i], refs, i, kshift);
+      const int seg = locate_seg(s_base, njobs, ref);
+      if (seg != cur) {
+        if (cur >= 0) {
+          total = first ? sum : total + sum;
+          first = false;
+        }
+        sum = 0.0f;
+        cur = seg;
+      }
+      const GbJob& j = jobs[seg];
+      const int64_t row = (int64_t)(ref - s_base[seg]);
+      if (agg_row(j.agg_bits[agg], row)) sum = sum + agg_float(j.vals[agg], row);
+    }
+    if (cur >= 0) total = first ? sum : total + sum;
+    if (out_slots) {  // groupBy: the final ABI value
+      out_slots[g * rec + 1 + agg] = (uint64_t)__float_as_uint(total);
+    } else if (cur >= 0) {  // per-segment engines: the run is one (segment, bucket, id) cell (device encoding)
+      const GbJob& j = jobs[cur];
+      const uint64_t key = keys[i0] >> kshift;
+      const int64_t bucket = j.bucket_bits ? (int64_t)((key >> j.bucket_shift) & ((1ull << j.bucket_bits) - 1)) : 0;
+      const int64_t id = j.ndims ? (int64_t)((key >> j.dim_shift[0]) & ((1ull << j.dim_bits[0]) - 1)) : 0;
+      j.fs_out[(bucket * j.fs_mul + id) * rec + 1 + agg] = (uint64_t)__double_as_longlong((double)total);
+    }
+  }
+}
+
+void launch_fsum_runs(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, int agg, const uint32_t* head_pos,
+                      uint64_t* out_slots, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (sb->cap + 255) / 256));
+  hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->keys[sb->cur],
+                     sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, plan.n + 1, agg, out_slots);
+}
+
+// ------------------------------------------------------------------------------------------------
+// finalize (for slots written in the device encoding) and unpack
+// ------------------------------------------------------------------------------------------------
 __global__ void k_slots_finalize(uint64_t* __restrict__ slots, const uint32_t* __restrict__ n_ptr, AggPlan plan) {
   const int64_t ng = n_ptr[0];
   const int rec = plan.n + 1;
@@ -590,6 +680,136 @@ void launch_gb_unpack(const uint64_t* keys, int64_t start, int64_t count, KeyLay
   if (count <= 0) return;
   const int64_t blocks = std::min<int64_t>(16384, (count + 255) / 256);
   hipLaunchKernelGGL(k_gb_unpack, dim3((unsigned)blocks), dim3(256), 0, s, keys, start, count, lay, bucket, ids);
+}
+
+// ------------------------------------------------------------------------------------------------
+// cross-device merge (QueryRunnerFactory.mergeRunners over the devices' merged groups): re-key a
+// result into the cluster key space, split it by key range, merge the received partials
+// ------------------------------------------------------------------------------------------------
+__global__ void k_gb_rekey(const uint64_t* __restrict__ in, int64_t n, KeyLayout lin, KeyLayout lout,
+                           int64_t bucket_delta, RekeyMaps maps, uint64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = in[i];
+    uint64_t o = 0;
+    if (lout.bucket_bits) {
+      const int64_t b = lin.bucket_bits ? (int64_t)((k >> lin.bucket_shift) & ((1ull << lin.bucket_bits) - 1)) : 0;
+      o |= (uint64_t)(b + bucket_delta) << lout.bucket_shift;
+    }
+    for (int d = 0; d < lout.ndims; ++d) {
+      const uint32_t id = lin.dim_bits[d] ? (uint32_t)((k >> lin.dim_shift[d]) & ((1ull << lin.dim_bits[d]) - 1)) : 0u;
+      o |= (uint64_t)(uint32_t)maps.m[d][id] << lout.dim_shift[d];
+    }
+    out[i] = o;
+  }
+}
+
+void launch_gb_rekey(const uint64_t* in, int64_t n, KeyLayout lin, KeyLayout lout, int64_t bucket_delta,
+                     RekeyMaps maps, uint64_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>(16384, (n + 255) / 256);
+  hipLaunchKernelGGL(k_gb_rekey, dim3((unsigned)blocks), dim3(256), 0, s, in, n, lin, lout, bucket_delta, maps, out);
+}
+
+// pos[i] = first index of the ascending keys[0, n) whose key >= split[i]
+__global__ void k_lower_bound(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __restrict__ split, int nsplit,
+                              int64_t* __restrict__ pos) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsplit) return;
+  const uint64_t x = split[i];
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  pos[i] = lo;
+}
+
+void launch_lower_bound(const uint64_t* keys, int64_t n, const uint64_t* split, int nsplit, int64_t* pos, hipStream_t s) {
+  if (nsplit <= 0) return;
+  hipLaunchKernelGGL(k_lower_bound, dim3((nsplit + 255) / 256), dim3(256), 0, s, keys, n, split, nsplit, pos);
+}
+
+// sort input of a merge: the concatenated partials' keys, row refs = record index; n[0] = n
+__global__ void k_merge_load(const uint64_t* __restrict__ keys, int64_t n, uint64_t* __restrict__ kout,
+                             uint32_t* __restrict__ rout, int kshift, uint32_t* __restrict__ n_out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) n_out[0] = (uint32_t)n;
+  for (int64_t i = t; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (rout) {
+      kout[i] = keys[i];
+      rout[i] = (uint32_t)i;
+    } else {
+      kout[i] = (keys[i] << kshift) | (uint64_t)i;
+    }
+  }
+}
+
+void launch_merge_load(const uint64_t* keys, int64_t n, SortBufs* sb, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(16384, std::max<int64_t>(1, (n + 255) / 256));
+  hipLaunchKernelGGL(k_merge_load, dim3((unsigned)blocks), dim3(256), 0, s, keys, n, sb->keys[sb->cur], sb->refs[sb->cur],
+                     sb->ref_bits, sb->n);
+}
+
+// AggregatorFactory.getCombiningFactory semantics on ABI-encoded partial values: the combining
+// aggregator starts from its identity and folds the partials in order (sums: LongSumAggregator /
+// DoubleSumAggregator / FloatSumAggregator.combine with float adds; min / max: Math.min / Math.max,
+// NaN-propagating with -0.0 < 0.0, DoubleMinAggregator.combine etc.)
+__device__ __forceinline__ uint64_t abi_to_dev(int kind, uint64_t v) {
+  switch (kind) {
+    case DG_AGG_COUNT:
+    case DG_AGG_LONG_SUM:
+    case DG_AGG_DOUBLE_SUM: return v;
+    case DG_AGG_FLOAT_SUM: return (uint64_t)__double_as_longlong((double)__uint_as_float((uint32_t)v));
+    case DG_AGG_LONG_MIN:
+    case DG_AGG_LONG_MAX: return v ^ kSign;
+    case DG_AGG_DOUBLE_MIN:
+    case DG_AGG_DOUBLE_MAX: {
+      const double d = __longlong_as_double((long long)v);
+      return d != d ? (kind == DG_AGG_DOUBLE_MIN ? 0ull : ~0ull) : ord_key(d);
+    }
+    default: {
+      const float f = __uint_as_float((uint32_t)v);
+      return f != f ? (kind == DG_AGG_FLOAT_MIN ? 0ull : ~0ull) : ord_key((double)f);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_merge_reduce(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
+                                                      int kshift, const uint32_t* __restrict__ n_ptr,
+                                                      const uint32_t* __restrict__ head_pos,
+                                                      const uint64_t* __restrict__ in_slots, AggPlan plan,
+                                                      uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_slots) {
+  const uint32_t n = n_ptr[0], ng = n_ptr[1];
+  const int na = plan.n, rec = na + 1;
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (int64_t)gridDim.x * 256) {
+    const uint32_t i0 = head_pos[g], i1 = g + 1 < ng ? head_pos[g + 1] : n;
+    out_keys[g] = keys[i0] >> kshift;
+    uint64_t rows = 0;
+    for (uint32_t i = i0; i < i1; ++i) rows += in_slots[(size_t)elem_ref(keys[i], refs, i, kshift) * rec];
+    out_slots[(size_t)g * rec] = rows;
+    for (int a = 0; a < na; ++a) {
+      const int kind = plan.kind[a];
+      if (kind == DG_AGG_FLOAT_SUM) {  // float adds in partial order
+        float acc = 0.0f;
+        for (uint32_t i = i0; i < i1; ++i)
+          acc = acc + __uint_as_float((uint32_t)in_slots[(size_t)elem_ref(keys[i], refs, i, kshift) * rec + 1 + a]);
+        out_slots[(size_t)g * rec + 1 + a] = (uint64_t)__double_as_longlong((double)acc);  // finalized later
+        continue;
+      }
+      uint64_t acc = identity_of(plan.op[a], kind);
+      for (uint32_t i = i0; i < i1; ++i)
+        acc = combine_op(plan.op[a], acc, abi_to_dev(kind, in_slots[(size_t)elem_ref(keys[i], refs, i, kshift) * rec + 1 + a]));
+      out_slots[(size_t)g * rec + 1 + a] = acc;
+    }
+  }
+}
+
+void launch_merge_reduce(SortBufs* sb, const uint32_t* head_pos, const uint64_t* in_slots, AggPlan plan, int64_t cap,
+                         uint64_t* out_keys, uint64_t* out_slots, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (cap + 255) / 256));
+  hipLaunchKernelGGL(k_merge_reduce, dim3((unsigned)blocks), dim3(256), 0, s, sb->keys[sb->cur], sb->refs[sb->cur],
+                     sb->ref_bits, sb->n, head_pos, in_slots, plan, out_keys, out_slots);
 }
 
 }  // namespace dg

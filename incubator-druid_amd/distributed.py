@@ -11,11 +11,15 @@ merged with one collective per query — backend "nccl" (= RCCL over xGMI) on MI
   all_gather of fixed-size [segments, K, 1 + aggs] tensors; rank 0 folds them with TopNBinaryFn in
   global segment order inside the engine (dg_topn_merge) — the reference's approximation
   (per-segment top max(K, 1000), pairwise merge to the query threshold) is kept exactly.
-* groupBy: per-rank merged groups -> all_gather of row counts + padded (time, ids, aggs) tensors;
-  rank 0 merges by key (GroupByMergingQueryRunnerV2.java:170-290).
+* groupBy: every rank's merged groups (in HBM, dg_groupby_run) are re-keyed into one cluster-wide
+  key space (dg_result_export), cut into key ranges at sampled splitters (dg_keys_partition), sent
+  to the rank owning each range with one all_to_all (RCCL over xGMI) and merged there
+  (dg_merge, GroupByMergingQueryRunnerV2.java:170-290 semantics): every rank ends with its key range
+  of the final, ordered result, no rank holds the whole table (GroupByExchange).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Dict, List, Optional, Sequence
 
@@ -114,10 +118,15 @@ def allreduce_timeseries(dist, query: Q.TimeseriesQuery, local: List[Q.Result],
     dist.all_reduce(t_ts, op=dist.ReduceOp.MIN)
     out_cols = {}
     for a in aggs:
-        t = torch.from_numpy(cols[a.name].copy()).to(dev)
-        op = dist.ReduceOp.SUM if a.kind in (0, 1, 2, 3) else (dist.ReduceOp.MIN if a.kind in (4, 6, 8) else dist.ReduceOp.MAX)
+        is_min = a.kind in (4, 6, 8)
+        fp_minmax = a.kind in (6, 7, 8, 9)
+        col = cols[a.name]
+        # double/float min/max reduce on order-preserving int64 keys (Math.min/max: NaN wins, -0.0 < 0.0)
+        t = torch.from_numpy(_ord_keys(col, is_min) if fp_minmax else col.copy()).to(dev)
+        op = dist.ReduceOp.SUM if a.kind in (0, 1, 2, 3) else (dist.ReduceOp.MIN if is_min else dist.ReduceOp.MAX)
         dist.all_reduce(t, op=op)
-        out_cols[a.name] = t.cpu().numpy()
+        out = t.cpu().numpy()
+        out_cols[a.name] = _from_ord_keys(out, is_min, col.dtype) if fp_minmax else out
     present = t_present.cpu().numpy()
     ts = t_ts.cpu().numpy()
     out = []
@@ -129,6 +138,31 @@ def allreduce_timeseries(dist, query: Q.TimeseriesQuery, local: List[Q.Result],
     if query.descending:
         out.reverse()
     return out
+
+
+_SIGN = np.uint64(1 << 63)
+
+
+def _ord_keys(col: np.ndarray, is_min: bool) -> np.ndarray:
+    """float64/float32 values -> int64 keys whose signed order is Java's Math.min/Math.max order:
+    -0.0 < 0.0, and NaN is the extreme the operator picks (the smallest key for min, largest for max),
+    so an integer MIN/MAX all_reduce reproduces DoubleMinAggregator.combine / DoubleMaxAggregator.combine."""
+    d = col.astype(np.float64)
+    u = d.view(np.uint64)
+    k = np.where((u & _SIGN) != 0, ~u, u | _SIGN)
+    s = (k ^ _SIGN).view(np.int64)
+    nan = np.isnan(d)
+    s = np.where(nan, np.iinfo(np.int64).min if is_min else np.iinfo(np.int64).max, s)
+    return s.astype(np.int64)
+
+
+def _from_ord_keys(s: np.ndarray, is_min: bool, dtype) -> np.ndarray:
+    nan = s == (np.iinfo(np.int64).min if is_min else np.iinfo(np.int64).max)
+    k = s.astype(np.int64).view(np.uint64) ^ _SIGN
+    u = np.where((k & _SIGN) != 0, k & ~_SIGN, ~k)
+    d = u.view(np.float64)
+    d = np.where(nan, np.nan, d)
+    return d.astype(dtype)
 
 
 def _np_type(a):
@@ -209,6 +243,197 @@ def gather_topn(dist, query: Q.TopNQuery, raw: "R.TopNRaw", gdict: GlobalDiction
     t0, _lists, out_keys, slots = res
     values = [gdict.values[int(k)] for k in out_keys]
     return [Q.Result(t0, R._topn_entries(query, values, slots))]
+
+
+# ----------------------------------------------------------------------------------------------
+# groupBy: key-range exchange + device merge
+# ----------------------------------------------------------------------------------------------
+class NativeMerge:
+    """The device side of the exchange through the C-ABI (dg_result_export / dg_keys_partition /
+    dg_merge) on one context; records travel as torch tensors on that device."""
+
+    def __init__(self, context):
+        self.context = context
+
+    def export(self, res, ks, maps, rec):
+        torch, _ = _torch()
+        from . import _native as N
+        n = res.groups
+        dev = torch.device("cuda", self.context.device)
+        keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        slots = torch.empty(max(n, 1) * rec, dtype=torch.int64, device=dev)
+        arr = (ctypes.c_void_p * max(len(maps), 1))(*[m.ctypes.data for m in maps])
+        torch.cuda.current_stream(dev).synchronize()  # allocations are ordered on torch's stream
+        N.check(N.lib().dg_result_export(res.handle, ctypes.byref(ks.struct), arr, keys.data_ptr(), slots.data_ptr()))
+        return keys[:n], slots[:n * rec]
+
+    def partition(self, keys, splits):
+        from . import _native as N
+        pos = np.zeros(len(splits), dtype=np.int64)
+        if len(splits):
+            sp = np.ascontiguousarray(splits, dtype=np.uint64)
+            N.check(N.lib().dg_keys_partition(self.context.handle, keys.data_ptr() if keys.numel() else None,
+                                              keys.numel(), sp.ctypes.data, len(sp), pos.ctypes.data))
+        return pos
+
+    def sample(self, keys, idx):
+        torch, _ = _torch()
+        return keys[torch.from_numpy(idx).to(keys.device)].cpu().numpy()
+
+    def merge(self, ks, keys, slots, query, dictionaries):
+        torch, _ = _torch()
+        from . import _native as N
+        torch.cuda.current_stream(keys.device).synchronize()  # the received records have landed
+        out = ctypes.c_void_p()
+        m = N.dg_metrics()
+        n = keys.numel()
+        N.check(N.lib().dg_merge(self.context.handle, ctypes.byref(ks.struct), keys.data_ptr() if n else None,
+                                 slots.data_ptr() if n else None, n, ctypes.byref(out), ctypes.byref(m)))
+        return R.GroupByResult(out, query, dictionaries=dictionaries)
+
+
+class KeySpace:
+    """dg_keyspace of one groupBy query over the cluster (kept alive with its arrays)."""
+
+    def __init__(self, cards, period_ms, bucket0, n_buckets, universal, agg_kinds):
+        from . import _native as N
+        self.cards = np.ascontiguousarray(cards, dtype=np.int32)
+        self.kinds = np.ascontiguousarray(agg_kinds, dtype=np.int32)
+        self.period_ms, self.bucket0, self.n_buckets, self.universal = period_ms, bucket0, n_buckets, universal
+        st = N.dg_keyspace()
+        st.n_dims = len(self.cards)
+        st.card = self.cards.ctypes.data if len(self.cards) else None
+        st.period_ms, st.bucket0, st.n_buckets, st.universal_time = period_ms, bucket0, n_buckets, universal
+        st.n_aggs = len(self.kinds)
+        st.agg_kinds = self.kinds.ctypes.data if len(self.kinds) else None
+        self.struct = st
+        # key = [bucket | d0 | d1 | ...], the last dimension least significant (dg_groupby_run's layout)
+        self.dim_bits = [max(int(c) - 1, 0).bit_length() for c in self.cards]
+        self.bucket_bits = max(n_buckets - 1, 0).bit_length() if period_ms else 0
+        self.bits = sum(self.dim_bits) + self.bucket_bits
+
+
+class GroupByExchange:
+    """Cluster-wide merge of one groupBy query's per-rank results (built once per query shape:
+    cluster dictionaries, id maps, bucket grid; then one `exchange` per run).
+
+    Key-range partitioning: each rank samples its sorted keys, the samples (weighted by the rank's
+    group count) give world - 1 splitters identical on every rank, dg_keys_partition cuts the
+    rank's keys at them, one all_to_all moves every range to its owner, dg_merge combines equal
+    keys (sources in rank order). Rank r ends with range r of the ordered result."""
+
+    SAMPLES = 256
+
+    def __init__(self, dist, query: Q.GroupByQuery, segments, engine=None):
+        self.dist, self.query = dist, query
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.engine = engine if engine is not None else NativeMerge(segments[0].context)
+        nd = len(query.dimensions)
+        # this rank's merged dictionaries: the union of its segments' dictionaries (a segment without
+        # the column contributes null), exactly as dg_groupby_run builds them
+        local = []
+        for d in query.dimensions:
+            vals = set()
+            for s in segments:
+                vals.update(s.dictionary(d))
+            local.append(sorted(vals, key=R._java_key))
+        gran = query.granularity
+        span = None
+        if not gran.is_all:  # the grid of bucket indices every rank's result is re-keyed onto
+            q0, q1 = query.interval
+            for s in segments:
+                if s.num_rows == 0:
+                    continue
+                data_e = gran.bucket_start(s.max_time) + gran.period_ms
+                if not (q0 < data_e and s.min_time < q1):
+                    continue
+                lo = gran.bucket_start(max(q0, s.min_time))
+                hi = gran.bucket_start(min(q1, data_e) - 1)
+                span = (lo, hi) if span is None else (min(span[0], lo), max(span[1], hi))
+        gathered: List = [None] * self.world
+        dist.all_gather_object(gathered, {"dicts": local, "span": span})
+        self.dicts = []
+        for i in range(nd):
+            allv = set()
+            for g in gathered:
+                allv.update(g["dicts"][i])
+            self.dicts.append(sorted(allv, key=R._java_key))
+        index = [{v: k for k, v in enumerate(gd)} for gd in self.dicts]
+        self.local = local
+        self.maps = [np.array([index[i][v] for v in local[i]], dtype=np.int32) for i in range(nd)]
+        spans = [g["span"] for g in gathered if g["span"] is not None]
+        if gran.is_all or not spans:
+            bucket0, nb = 0, 1
+        else:
+            bucket0 = min(s[0] for s in spans)
+            nb = (max(s[1] for s in spans) - bucket0) // gran.period_ms + 1
+        self.ks = KeySpace([len(d) for d in self.dicts], gran.period_ms, bucket0, nb, query.interval[0],
+                           [a.kind for a in query.aggregations])
+        if self.ks.bits > 63:
+            raise R.N.UnsupportedQuery(2, f"cluster groupBy key of {self.ks.bits} bits")
+        self.rec = 1 + len(query.aggregations)
+        self._checked = False
+
+    def _splitters(self, keys) -> np.ndarray:
+        """world - 1 ascending splitters from every rank's evenly spaced key samples, each weighted by
+        the share of its rank's groups it stands for (identical on every rank)."""
+        torch, _ = _torch()
+        n = keys.numel()
+        S = self.SAMPLES
+        k = min(S, n)
+        idx = (np.arange(k, dtype=np.int64) * n) // max(k, 1)
+        samp = np.full(S, -1, dtype=np.int64)
+        if k:
+            samp[:k] = self.engine.sample(keys, idx)
+        payload = torch.from_numpy(np.concatenate([[n, k], samp]).astype(np.int64)).to(_device(self.dist))
+        bufs = [torch.empty_like(payload) for _ in range(self.world)]
+        self.dist.all_gather(bufs, payload)
+        pts, wts = [], []
+        for b in bufs:
+            a = b.cpu().numpy()
+            nn, kk = int(a[0]), int(a[1])
+            if kk:
+                pts.append(a[2:2 + kk])
+                wts.append(np.full(kk, nn / kk))
+        if not pts:
+            return np.zeros(self.world - 1, dtype=np.uint64)
+        pts = np.concatenate(pts)
+        wts = np.concatenate(wts)
+        order = np.argsort(pts, kind="stable")
+        pts, cum = pts[order], np.cumsum(wts[order])
+        total = cum[-1]
+        out = []
+        for r in range(1, self.world):
+            j = int(np.searchsorted(cum, total * r / self.world, side="left"))
+            out.append(int(pts[min(j, len(pts) - 1)]))
+        return np.maximum.accumulate(np.array(out, dtype=np.int64)).astype(np.uint64)
+
+    def exchange(self, res):
+        """This rank's key range of the cluster-wide merged result (a device-resident result whose
+        dimension ids index `self.dicts`)."""
+        torch, _ = _torch()
+        if not self._checked:  # the engine's merged dictionaries are the ones the maps were built for
+            for d in range(len(self.query.dimensions)):
+                if res.dictionary(d) != self.local[d]:
+                    raise RuntimeError(f"merged dictionary of {self.query.dimensions[d]} differs from the segments'")
+            self._checked = True
+        keys, slots = self.engine.export(res, self.ks, self.maps, self.rec)
+        n = keys.numel()
+        splits = self._splitters(keys)
+        pos = self.engine.partition(keys, splits)
+        bounds = np.concatenate([[0], pos, [n]]).astype(np.int64)
+        send = np.diff(bounds)
+        dev = keys.device
+        cnt_in = torch.from_numpy(send.astype(np.int64)).to(_device(self.dist))
+        cnt_out = torch.empty_like(cnt_in)
+        self.dist.all_to_all_single(cnt_out, cnt_in)
+        recv = cnt_out.cpu().numpy().astype(np.int64)
+        rkeys = torch.empty(int(recv.sum()), dtype=torch.int64, device=dev)
+        rslots = torch.empty(int(recv.sum()) * self.rec, dtype=torch.int64, device=dev)
+        self.dist.all_to_all_single(rkeys, keys.contiguous(), [int(x) for x in recv], [int(x) for x in send])
+        self.dist.all_to_all_single(rslots, slots.contiguous(), [int(x) * self.rec for x in recv],
+                                    [int(x) * self.rec for x in send])
+        return self.engine.merge(self.ks, rkeys, rslots, self.query, self.dicts)
 
 
 def _to_bits(a, v) -> int:

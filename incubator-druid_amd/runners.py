@@ -578,13 +578,18 @@ class GroupByPartial:
 
 
 class GroupByResult:
-    """A dg_result: the merged groups of one dg_groupby_run, resident in HBM until fetched."""
+    """A dg_result: the merged groups of one dg_groupby_run (or of a dg_merge across devices, whose
+    ids index the caller's cluster dictionaries), resident in HBM until fetched."""
 
-    def __init__(self, handle: ctypes.c_void_p, query: Q.GroupByQuery):
+    def __init__(self, handle: ctypes.c_void_p, query: Q.GroupByQuery,
+                 dictionaries: Optional[List[List[Optional[str]]]] = None):
         self.handle, self.query = handle, query
         self.groups = int(N.lib().dg_result_groups(handle))
+        self._dicts = dictionaries
 
     def dictionary(self, d: int) -> List[Optional[str]]:
+        if self._dicts is not None:
+            return self._dicts[d]
         L = N.lib()
         card = int(L.dg_result_dim_cardinality(self.handle, d))
         offs = np.zeros(card + 1, dtype=np.int64)

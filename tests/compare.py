@@ -8,7 +8,9 @@ TOL = {"long": 0.0, "double": 1e-9, "float": 1e-5}
 def _close(a, b, rel):
     if isinstance(a, float) and math.isnan(a):
         return isinstance(b, float) and math.isnan(b)
-    if rel == 0.0:
+    if rel == 0.0:  # exact: for floats also the sign of zero (Math.min/max order -0.0 < 0.0)
+        if isinstance(a, float) or isinstance(b, float):
+            return a == b and math.copysign(1.0, a) == math.copysign(1.0, b)
         return a == b
     if a == b:
         return True

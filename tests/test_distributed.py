@@ -24,6 +24,15 @@ def _free_port():
     return port
 
 
+def _special_aggs(Q):
+    """Math.min / Math.max edge cases across ranks: NaN wins, -0.0 < 0.0 (specialDouble / specialFloat
+    hold NaN, -0.0 and 0.0 rows, written by _write_dataset)"""
+    return [Q.AggregatorFactory("doubleMin", "sdmin", "specialDouble"),
+            Q.AggregatorFactory("doubleMax", "sdmax", "specialDouble"),
+            Q.AggregatorFactory("floatMin", "sfmin", "specialFloat"),
+            Q.AggregatorFactory("floatMax", "sfmax", "specialFloat")]
+
+
 def _queries(Q):
     iv = ["1970-01-01/2020-01-01"]
     aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal"),
@@ -33,6 +42,9 @@ def _queries(Q):
     return {
         "ts_all": Q.TimeseriesQuery(intervals=iv, aggregations=aggs,
                                     filter=Q.BoundDimFilter("dimSequential", "100", "300")),
+        "ts_special": Q.TimeseriesQuery(intervals=iv, aggregations=aggs[:1] + _special_aggs(Q)),
+        "ts_special_minute": Q.TimeseriesQuery(intervals=iv, granularity="minute", aggregations=_special_aggs(Q),
+                                               filter=Q.InDimFilter("dimZipf", ["1", "2"])),
         "ts_minute": Q.TimeseriesQuery(intervals=iv, granularity="minute", aggregations=aggs[:3]),
         "topn": Q.TopNQuery(intervals=iv, dimension="dimZipf", metric="sumFloatNormal", threshold=5,
                             aggregations=aggs[1:3]),
@@ -46,6 +58,13 @@ def _queries(Q):
                                    threshold=3, aggregations=aggs[1:3]),
         "groupby": Q.GroupByQuery(intervals=iv, dimensions=["dimZipf", "dimSequential"], aggregations=aggs[:4],
                                   filter=Q.InDimFilter("dimZipf", ["1", "2", "3"])),
+        "groupby_special": Q.GroupByQuery(intervals=iv, dimensions=["dimZipf"],
+                                          aggregations=aggs[:1] + [aggs[5]] + _special_aggs(Q)),
+        "groupby_uniform": Q.GroupByQuery(intervals=iv, dimensions=["dimUniform", "dimSequential"],
+                                          aggregations=aggs[:3] + [aggs[5]]),
+        "groupby_minute": Q.GroupByQuery(intervals=iv, granularity="minute", dimensions=["dimSequential"],
+                                         aggregations=aggs[:2] + _special_aggs(Q)[:2],
+                                         filter=Q.BoundDimFilter("dimSequential", "10", "20")),
     }
 
 
@@ -118,19 +137,19 @@ def _worker(rank, port, paths, out_dir):
             raw = _raw_from_oracle(R, np, O, q, segs)
             got = D.gather_topn(dist, q, raw, gdict, trans)
         else:
-            gd = {d: D.GlobalDictionary.build(dist, [s.dictionary(d) for s in segs]) for d in q.dimensions}
-            parts = [_partial_from_oracle(R, np, q, O.groupby_segment(s, q)) for s in segs]
-            t, dims, aggs = R.merge_groupby_columnar(q, parts)
-            res = D.gather_groupby(dist, q, R.GroupByPartial(t, dims, aggs), gd)
+            # key-range exchange (the device side stood in by host_merge; every rank ends with its range)
+            import host_merge as HM
+            facts = [HM.SegFacts(s) for s in segs]
+            ex = D.GroupByExchange(dist, q, facts, engine=HM.HostMerge())
+            local = O.merge_groupby(q, [O.groupby_segment(s, q) for s in segs])
+            res = HM.HostResult(q, [(r.timestamp, tuple(r.event[d] for d in q.dimensions), r.event) for r in local],
+                                segs)
+            mine = ex.exchange(res).rows()
+            parts: list = [None] * WORLD
+            dist.all_gather_object(parts, [[r.timestamp, r.event] for r in mine])
             got = None
-            if res is not None:
-                t, dims, aggs = res
-                got = []
-                for r in range(len(t)):
-                    ev = {dn: dims[i][r] for i, dn in enumerate(q.dimensions)}
-                    for a, col in zip(q.aggregations, aggs):
-                        ev[a.name] = R._py(col[r], a.output_type)
-                    got.append(Q.Row(int(t[r]), ev))
+            if rank == 0:
+                got = [Q.Row(t, ev) for part in parts for t, ev in part]  # ranges in rank order
         if got is not None:
             report[name] = [[r.timestamp, getattr(r, "value", None) if hasattr(r, "value") else r.event]
                             for r in got]
@@ -143,10 +162,30 @@ def _worker(rank, port, paths, out_dir):
     dist.destroy_process_group()
 
 
+def _write_dataset(DG, W, root, nseg, rows):
+    """basic-schema segments plus specialDouble / specialFloat columns of NaN, -0.0, 0.0 and small
+    values; even segments have no NaN, so some results are decided by -0.0 vs 0.0 alone."""
+    import numpy as np
+    paths = []
+    for i in range(nseg):
+        spec = DG.basic_columns(rows, 9999 + i)
+        rng = np.random.default_rng(77 + i)
+        pick = rng.integers(0, 1000, size=rows)
+        sd = np.where(pick < 20, np.nan, np.where(pick < 500, -0.0, np.where(pick < 999, 0.0, rng.normal(0, 1, rows))))
+        if i % 2 == 0:  # even segments: no NaN, so some buckets' min/max are decided by -0.0 vs 0.0
+            sd = np.where(np.isnan(sd), -0.0, sd)
+        spec.metrics["specialDouble"] = ("double", sd.astype(np.float64))
+        spec.metrics["specialFloat"] = ("float", sd.astype(np.float32))
+        p = os.path.join(root, f"seg{i:04d}")
+        W.write_segment(p, spec, lz4_mode="fast")
+        paths.append(p)
+    return paths
+
+
 @pytest.fixture(scope="module")
-def dist_dirs(tmp_path_factory, DG):
+def dist_dirs(tmp_path_factory, DG, W):
     base = tmp_path_factory.mktemp("dist")
-    return DG.write_basic_dataset(str(base), WORLD * SEGS_PER_RANK, 12_000, lz4_mode="fast")
+    return _write_dataset(DG, W, str(base), WORLD * SEGS_PER_RANK, 12_000)
 
 
 def test_gloo_world2_matches_single_process(dist_dirs, tmp_path, Q, O):
@@ -157,6 +196,7 @@ def test_gloo_world2_matches_single_process(dist_dirs, tmp_path, Q, O):
     with open(tmp_path / "rank0.json") as f:
         report = json.load(f)
     segs = [O.OracleSegment(p) for p in dist_dirs]
+    special = []
     try:
         for name, q in _queries(Q).items():
             exp = O.run(q, segs)
@@ -167,6 +207,14 @@ def test_gloo_world2_matches_single_process(dist_dirs, tmp_path, Q, O):
                 got = [Q.Result(t, v) for t, v in rows]
             assert_results(q, got, exp)
             assert len(exp) > 0, name
+            if "special" in name:
+                special += [v for r in exp for k, v in (r.event if hasattr(r, "event") else r.value).items()
+                            if k in ("sdmin", "sdmax", "sfmin", "sfmax")]
+        # the edge cases really occur in the expected results: NaN winning, and -0.0 deciding a min/max
+        import math
+        assert any(isinstance(v, float) and math.isnan(v) for v in special)
+        assert any(v == 0.0 and math.copysign(1.0, v) < 0 for v in special)
+        assert any(v == 0.0 and math.copysign(1.0, v) > 0 for v in special)
     finally:
         for s in segs:
             s.close()
