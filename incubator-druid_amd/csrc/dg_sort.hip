@@ -484,55 +484,63 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ job
   const uint32_t ex = block_scan_u32<kST>((uint32_t)__popc(h), &tot, s_tmp);
   if (m == 0) return;
   // group of the thread's first element: the next head's index, or the open group before it
-  int64_t g = (int64_t)run_off[blockIdx.x] + ex - ((h & 1u) ? 0 : 1);
-  bool owner = h & 1u;
-  uint64_t acc[kMaxAggs];
-  uint64_t rows = 0;
-  auto reset = [&]() {
-    rows = 0;
-#pragma unroll
-    for (int a = 0; a < kMaxAggs; ++a) acc[a] = a < na ? identity_of(plan.op[a], plan.kind[a]) : 0ull;
-  };
+  const int64_t g0 = (int64_t)run_off[blockIdx.x] + ex - ((h & 1u) ? 0 : 1);
+  const bool owner0 = h & 1u;
   const int rec = na + 1;
-  auto flush = [&](bool complete) {
-    if (owner) {
-      uint64_t* o = out_slots + g * rec;
-      o[0] = rows;
+  // the thread's elements: (segment, row) of each, keys and run heads
+  int seg_of[kSPT];
+  int32_t row_of[kSPT];
+  {
+    int64_t g = g0;
 #pragma unroll
-      for (int a = 0; a < kMaxAggs; ++a)
-        if (a < na && plan.kind[a] != DG_AGG_FLOAT_SUM) o[1 + a] = complete ? finalize_dev(plan.kind[a], acc[a]) : acc[a];
-      if (!complete) open_g[gt] = g;
-    } else {  // the group's head (and record) belongs to an earlier thread: carry the partial
-      carry_g[gt] = g;
-      uint64_t* o = carry_slots + gt * rec;
-      o[0] = rows;
-#pragma unroll
-      for (int a = 0; a < kMaxAggs; ++a)
-        if (a < na) o[1 + a] = acc[a];
-    }
-  };
-  reset();
-  for (int q = 0; q < m; ++q) {
-    if ((h >> q) & 1u) {
-      if (q > 0) {
-        flush(true);
-        g++;
-        owner = true;
-        reset();
+    for (int q = 0; q < kSPT; ++q) {
+      const uint32_t ref = s_ref[tid * 17 + q];
+      const int seg = locate_seg(s_base, njobs, ref);
+      seg_of[q] = seg;
+      row_of[q] = (int32_t)(ref - s_base[seg]);
+      if (q < m && ((h >> q) & 1u)) {
+        if (q > 0) g++;
+        head_pos[g] = (uint32_t)(base + x0 + q);
+        out_keys[g] = kr[q];
       }
-      head_pos[g] = (uint32_t)(base + x0 + q);
-      out_keys[g] = s_key[tid * 17 + q];
     }
-    const uint32_t ref = s_ref[tid * 17 + q];
-    const int seg = locate_seg(s_base, njobs, ref);
-    const GbJob& j = jobs[seg];
-    const int64_t row = (int64_t)(ref - s_base[seg]);
-    rows += 1;
-#pragma unroll
-    for (int a = 0; a < kMaxAggs; ++a)
-      if (a < na && plan.kind[a] != DG_AGG_FLOAT_SUM) acc[a] = combine_op(plan.op[a], acc[a], agg_in(j, plan, a, row));
   }
-  flush(next_head);
+  // one slot at a time: the thread's m inputs are loaded first (independent random loads in flight
+  // together), then folded along the runs. Slot -1 = rows aggregated (count of the run's elements).
+  if (!owner0) carry_g[gt] = g0;
+  for (int a = -1; a < na; ++a) {
+    const int kind = a < 0 ? DG_AGG_COUNT : plan.kind[a];
+    if (kind == DG_AGG_FLOAT_SUM) continue;  // k_fsum_runs: float32 in row order
+    const int op = a < 0 ? (int)OP_ADD_I64 : plan.op[a];
+    uint64_t x[kSPT];
+#pragma unroll
+    for (int q = 0; q < kSPT; ++q) x[q] = (a < 0 || q >= m) ? 1ull : agg_in(jobs[seg_of[q]], plan, a, row_of[q]);
+    const uint64_t ident = a < 0 ? 0ull : identity_of(op, kind);
+    uint64_t acc = ident;
+    int64_t g = g0;
+    bool own = owner0;
+#pragma unroll
+    for (int q = 0; q < kSPT; ++q) {
+      if (q >= m) continue;
+      if (q > 0 && ((h >> q) & 1u)) {  // the previous group ended inside my range: complete
+        if (own) out_slots[g * rec + 1 + a] = finalize_dev(kind, acc);
+        else carry_slots[gt * rec + 1 + a] = acc;
+        g++;
+        own = true;
+        acc = ident;
+      }
+      acc = combine_op(op, acc, x[q]);
+    }
+    if (own) out_slots[g * rec + 1 + a] = next_head ? finalize_dev(kind, acc) : acc;
+    else carry_slots[gt * rec + 1 + a] = acc;  // a range with no head: the whole range is one carry
+  }
+  if (!next_head) {
+    // my last group continues into the next thread: written (by me if I own it) in the device
+    // encoding, finalized after the carries
+    const int64_t glast = g0 + __popc(h & ~1u);
+    const bool own_last = owner0 || (h & ~1u);
+    if (own_last) open_g[gt] = glast;
+  }
 }
 
 // carried partials -> their group's record: equal groups are consecutive, so one segmented combine

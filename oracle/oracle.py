@@ -45,6 +45,133 @@ if _REPO not in sys.path:
     sys.path.insert(0, _REPO)
 Q = importlib.import_module("incubator-druid_amd.query")
 
+# The query objects of incubator-druid_amd/query.py are only the tests' input format (their fields:
+# dimensions, values, bounds, granularity period/origin, aggregator kinds). Every semantic rule the
+# checker applies to them is restated here from the reference, not taken from the product.
+_MIN_INSTANT = -(1 << 62)  # JodaUtils.MIN_INSTANT-like sentinels (bucket of ALL granularity)
+_MAX_INSTANT = (1 << 62) - 1
+
+
+def _jrem(a: int, b: int) -> int:
+    """Java's long % (truncated division: the remainder takes the dividend's sign)."""
+    r = abs(a) % abs(b)
+    return r if a >= 0 else -r
+
+
+def o_empty_to_null(v):
+    """NullHandling.emptyToNullIfNeeded in the default replaceWithDefault mode
+    (java-util/.../common/config/NullHandling.java:79-84): "" -> null."""
+    return None if v is None or v == "" else str(v)
+
+
+def o_bucket_start(gran, t: int) -> int:
+    """Granularity.bucketStart of a UTC granularity.
+    ALL: AllGranularity (every row in one bucket). duration: DurationGranularity.bucketStart
+    (java-util/.../granularity/DurationGranularity.java:80-89, origin normalised with `origin % duration`
+    at construction :48-53, Java remainders, a single +duration correction) restated literally.
+    Simple periods (minute / hour / day / week / single-field ISO periods): PeriodGranularity.truncate
+    (PeriodGranularity.java:222-330): roundFloor of the field, or with an origin / a multiple, the
+    difference in whole units from the origin rounded toward zero, stepped back one period for
+    timestamps before the aligned point — i.e. the floor relative to the origin; weeks start on
+    Monday (dayOfWeek().set(t, 1), :279-281) = origin 1969-12-29."""
+    P = gran.period_ms
+    if P == 0:
+        return _MIN_INSTANT
+    if gran.name == "duration":
+        origin = _jrem(gran.origin_ms, P)
+        offset = _jrem(t, P) - origin
+        if offset < 0:
+            offset += P
+        return t - offset
+    # difference in whole periods from the origin, truncated toward zero, then stepped back
+    diff = t - gran.origin_ms
+    units = abs(diff) // P * (1 if diff >= 0 else -1)
+    tt = gran.origin_ms + units * P
+    return tt - P if t < tt else tt
+
+
+def o_increment(gran, t: int) -> int:
+    return _MAX_INSTANT if gran.period_ms == 0 else t + gran.period_ms
+
+
+def o_iterable(gran, interval):
+    """Granularity.getIterable (java-util/.../granularity/Granularity.java:176-240): buckets from
+    bucketStart(start) while < end; AllGranularity yields the interval itself."""
+    s, e = interval
+    if gran.period_ms == 0:
+        return [(s, e)]
+    out, cur = [], o_bucket_start(gran, s)
+    while cur < e:
+        out.append((cur, o_increment(gran, cur)))
+        cur = o_increment(gran, cur)
+    return out
+
+
+def o_optimize(f):
+    """DimFilter.optimize: InDimFilter.optimize (query/filter/InDimFilter.java:132-139) turns a
+    one-value IN (values kept in a TreeSet after emptyToNullIfNeeded, :81-85) into a selector;
+    And/Or optimize their children and collapse to the only child (AndDimFilter.java:73-77,
+    OrDimFilter.java:83-87); Not optimizes its child (NotDimFilter.java:64-67)."""
+    if f is None:
+        return None
+    if isinstance(f, Q.InDimFilter):
+        vals = sorted({o_empty_to_null(v) for v in f.values}, key=lambda v: (v is not None, v or ""))
+        if len(vals) == 1:
+            return Q.SelectorDimFilter(f.dimension, vals[0])
+        return Q.InDimFilter(f.dimension, vals)
+    if isinstance(f, (Q.AndDimFilter, Q.OrDimFilter)):
+        fs = [o_optimize(c) for c in f.fields]
+        return fs[0] if len(fs) == 1 else type(f)(fs)
+    if isinstance(f, Q.NotDimFilter):
+        return Q.NotDimFilter(o_optimize(f.field))
+    return f
+
+
+def _o_f32(x: float) -> float:
+    return struct.unpack("<f", struct.pack("<f", x))[0]
+
+
+def o_java_min(a, b):
+    """java.lang.Math.min(double/float): NaN if either is NaN, -0.0 < 0.0."""
+    if a != a:
+        return a
+    if a == 0.0 and b == 0.0 and math.copysign(1.0, b) < 0:
+        return b
+    return a if a <= b else b
+
+
+def o_java_max(a, b):
+    """java.lang.Math.max(double/float): NaN if either is NaN, 0.0 > -0.0."""
+    if a != a:
+        return a
+    if a == 0.0 and b == 0.0 and math.copysign(1.0, a) < 0:
+        return b
+    return a if a >= b else b
+
+
+def o_combine(agg, a, b):
+    """AggregatorFactory.combine per kind: CountAggregator.combineValues / LongSumAggregator.combineValues
+    (long add, wraps), LongMin/Max (Math.min/max), DoubleSumAggregator.combineValues (double add),
+    FloatSumAggregator.combineValues (:40-43, float add), Double/FloatMin/Max (Math.min/max)."""
+    k = agg.kind
+    if k in (0, 1):
+        v = (int(a) + int(b)) & ((1 << 64) - 1)
+        return v - (1 << 64) if v >= (1 << 63) else v
+    if k == 4:
+        return min(int(a), int(b))
+    if k == 5:
+        return max(int(a), int(b))
+    if k == 2:
+        return float(a) + float(b)
+    if k == 3:
+        return _o_f32(_o_f32(a) + _o_f32(b))
+    if k in (6, 8):
+        r = o_java_min(float(a), float(b))
+        return _o_f32(r) if k == 8 else r
+    r = o_java_max(float(a), float(b))
+    return _o_f32(r) if k == 9 else r
+
+
 OR_MISSING, OR_LONG, OR_FLOAT, OR_DOUBLE, OR_STRING, OR_UNSUPPORTED = range(6)
 _lib = None
 
@@ -514,8 +641,8 @@ def _lex_compare(a, b):
 
 def _bound_matches(f, value: Optional[str]) -> bool:
     """BoundFilter.doesMatch (BoundFilter.java:249-275) in default null mode."""
-    lower = Q._empty_to_null(f.lower)
-    upper = Q._empty_to_null(f.upper)
+    lower = o_empty_to_null(f.lower)
+    upper = o_empty_to_null(f.upper)
     has_lower, has_upper = f.lower is not None, f.upper is not None
     if value is None:
         return ((not has_lower) or (lower is None and not f.lowerStrict)) and \
@@ -619,12 +746,12 @@ def filter_id_set(seg: OracleSegment, f) -> Optional[List[int]]:
     """Dictionary ids selected by a leaf filter; None means 'dimension missing' handled by caller."""
     dictionary = seg.dictionary(f.dimension)
     if isinstance(f, Q.SelectorDimFilter):
-        i = index_of(dictionary, Q._empty_to_null(f.value))
+        i = index_of(dictionary, o_empty_to_null(f.value))
         return [i] if i >= 0 else []
     if isinstance(f, Q.InDimFilter):
         ids = set()
         for v in f.values:
-            i = index_of(dictionary, Q._empty_to_null(v))
+            i = index_of(dictionary, o_empty_to_null(v))
             if i >= 0:
                 ids.add(i)
         return sorted(ids)
@@ -634,12 +761,12 @@ def filter_id_set(seg: OracleSegment, f) -> Optional[List[int]]:
             if f.lower is None:
                 start = 0
             else:
-                found = index_of(dictionary, Q._empty_to_null(f.lower))
+                found = index_of(dictionary, o_empty_to_null(f.lower))
                 start = (found + 1 if f.lowerStrict else found) if found >= 0 else -(found + 1)
             if f.upper is None:
                 end = card
             else:
-                found = index_of(dictionary, Q._empty_to_null(f.upper))
+                found = index_of(dictionary, o_empty_to_null(f.upper))
                 end = (found if f.upperStrict else found + 1) if found >= 0 else -(found + 1)
             end = max(start, end)
             return list(range(start, end))
@@ -651,9 +778,9 @@ def filter_id_set(seg: OracleSegment, f) -> Optional[List[int]]:
 
 def _leaf_matches_null(f) -> bool:
     if isinstance(f, Q.SelectorDimFilter):
-        return Q._empty_to_null(f.value) is None
+        return o_empty_to_null(f.value) is None
     if isinstance(f, Q.InDimFilter):
-        return any(Q._empty_to_null(v) is None for v in f.values)
+        return any(o_empty_to_null(v) is None for v in f.values)
     if isinstance(f, Q.BoundDimFilter):
         return _bound_matches(f, None)
     if isinstance(f, Q.PREDICATE_FILTERS):
@@ -696,15 +823,15 @@ def cursor_buckets(seg: OracleSegment, query) -> List[Tuple[int, int, int]]:
     t = seg.time()
     gran = query.granularity
     min_t, max_t = int(t[0]), int(t[-1])
-    data = (min_t, gran.bucket_end(max_t))
+    data = (min_t, o_increment(gran, o_bucket_start(gran, max_t)))
     qs, qe = query.interval
     if not (qs < data[1] and data[0] < qe):
         return []
     actual = (max(qs, data[0]), min(qe, data[1]))
     out = []
-    for bs, be in gran.iterable(actual):
+    for bs, be in o_iterable(gran, actual):
         ts = max(actual[0], bs)
-        te = min(actual[1], gran.increment(bs))
+        te = min(actual[1], o_increment(gran, bs))
         r0 = int(np.searchsorted(t, ts, side="left"))
         r1 = int(np.searchsorted(t, te, side="left"))
         out.append((bs if not gran.is_all else actual[0], r0, max(r0, r1)))
@@ -748,7 +875,7 @@ def _py(v, out_type):
 # timeseries
 # ----------------------------------------------------------------------------------------------
 def timeseries_segment(seg: OracleSegment, query) -> List:
-    mask = filter_mask(seg, query.effective_filter())
+    mask = filter_mask(seg, o_optimize(query.filter))
     buckets = cursor_buckets(seg, query)
     # one cursor per bucket; rows of every cursor are aggregated in row order (one C pass per aggregator,
     # group = cursor index, identical to running each cursor's Aggregator loop on its own)
@@ -778,14 +905,14 @@ def merge_timeseries(query, per_segment: List[List]) -> List:
     flat = sorted(((r.timestamp, si, k, r) for si, rs in enumerate(per_segment) for k, r in enumerate(rs)),
                   key=lambda x: (x[0], x[1], x[2]))
     for ts, _, _, r in flat:
-        key = 0 if gran.is_all else gran.bucket_start(ts)
+        key = 0 if gran.is_all else o_bucket_start(gran, ts)
         if key not in merged:
             merged[key] = Q.Result(r.timestamp if gran.is_all else key, dict(r.value))
             order.append(key)
         else:
             acc = merged[key].value
             for a in query.aggregations:
-                acc[a.name] = a.combine(acc[a.name], r.value[a.name])
+                acc[a.name] = o_combine(a, acc[a.name], r.value[a.name])
     out = [merged[k] for k in sorted(order)]
     if getattr(query, "descending", False):
         out.reverse()
@@ -992,12 +1119,15 @@ def _metric_key_fn(query):
 
 
 def topn_segment(seg: OracleSegment, query) -> List:
-    mask = filter_mask(seg, query.effective_filter())
+    mask = filter_mask(seg, o_optimize(query.filter))
     out = []
     dim_present = seg.is_dim(query.dimension)
     dictionary = seg.dictionary(query.dimension) if dim_present else [None]
     ids_all = seg.ids(query.dimension) if dim_present else np.zeros(seg.num_rows, np.int32)
-    T = query.segment_threshold
+    # TopNQueryQueryToolChest.preMergeQueryDecoration (:553-561): a threshold <= minTopNThreshold
+    # (context value, else TopNQueryConfig.minTopNThreshold = 1000) runs per segment with that minimum
+    min_t = int(query.context.get("minTopNThreshold", 1000))
+    T = query.threshold if query.threshold > min_t else min_t
     lo, hi = _dimension_id_range(seg, query, dictionary, T)
     for bt, r0, r1 in cursor_buckets(seg, query):
         rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
@@ -1034,14 +1164,14 @@ def topn_binary_fn(query, r1, r2):
             a = ret[k]
             c = {dim: k}
             for agg in query.aggregations:
-                c[agg.name] = agg.combine(a[agg.name], v[agg.name])
+                c[agg.name] = o_combine(agg, a[agg.name], v[agg.name])
             ret[k] = c
         else:
             ret[k] = v
     bob = _make_builder(query, query.threshold)
     for v in ret.values():
         _builder_add(bob, query, v[dim], v)
-    ts = r1.timestamp if query.granularity.is_all else query.granularity.bucket_start(r1.timestamp)
+    ts = r1.timestamp if query.granularity.is_all else o_bucket_start(query.granularity, r1.timestamp)
     return Q.Result(ts, bob.build())
 
 
@@ -1050,7 +1180,7 @@ def merge_topn(query, per_segment: List[List]) -> List:
     flat = sorted(((r.timestamp, si, r) for si, rs in enumerate(per_segment) for r in rs), key=lambda x: (x[0], x[1]))
     merged: Dict[int, Q.Result] = {}
     for ts, _, r in flat:
-        key = 0 if gran.is_all else gran.bucket_start(ts)
+        key = 0 if gran.is_all else o_bucket_start(gran, ts)
         merged[key] = topn_binary_fn(query, merged.get(key), r)
     out = []
     for k in sorted(merged):
@@ -1064,7 +1194,7 @@ def merge_topn(query, per_segment: List[List]) -> List:
 # groupBy (v2)
 # ----------------------------------------------------------------------------------------------
 def groupby_segment(seg: OracleSegment, query) -> List[Tuple[int, Tuple, Dict]]:
-    mask = filter_mask(seg, query.effective_filter())
+    mask = filter_mask(seg, o_optimize(query.filter))
     dims = query.dimensions
     dicts, idcols = [], []
     for d in dims:
@@ -1108,13 +1238,13 @@ def merge_groupby(query, per_segment: List[List]) -> List:
     merged: Dict = {}
     for rows in per_segment:
         for bt, vals, aggs in rows:
-            key = (0 if gran.is_all else gran.bucket_start(bt), vals)
+            key = (0 if gran.is_all else o_bucket_start(gran, bt), vals)
             if key not in merged:
                 merged[key] = (bt, dict(aggs))
             else:
                 t0, acc = merged[key]
                 for a in query.aggregations:
-                    acc[a.name] = a.combine(acc[a.name], aggs[a.name])
+                    acc[a.name] = o_combine(a, acc[a.name], aggs[a.name])
                 merged[key] = (min(t0, bt), acc)
     out = []
     for (k, vals), (bt, aggs) in merged.items():
