@@ -115,6 +115,14 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
                            "(make -C incubator-druid_amd/csrc); there is no CPU fallback")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7, the
+    # engine's NEEDED name). Loaded first, it is the one the engine binds to, so torch tensors,
+    # streams and RCCL (torch.distributed) share the engine's device runtime. Loaded after the
+    # engine's /opt/rocm copy, torch would map a second runtime that finds no devices.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     l = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, cp = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_char_p
     P = ctypes.POINTER

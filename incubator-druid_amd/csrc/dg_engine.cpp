@@ -373,13 +373,333 @@ static bool leaf_matches_null(const dg_filter& f) {
   return bound_matches(f, nullptr);
 }
 
+struct DecodeBatch {
+  std::vector<Lz4Job> jobs;
+  std::vector<LzfJob> lzf_jobs;  // LZF blocks, decoded one wave per block
+  std::vector<VsJob> expands;  // DELTA / TABLE blocks, expanded after the LZ4 decodes
+  int32_t expand_rows = 0;     // largest block of `expands` (grid width)
+  int64_t* last_expanded = nullptr;
+  uint8_t* last_slots = nullptr;  // decode slots of the last viewed LZ4 / LZF column
+  int64_t bytes = 0;  // algorithmic bytes read
+};
+static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
+static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr);
+
+// ------------------------------------------------------------------------------------------------
+// numeric post-filters: Java's parsing of the filter's strings (host side, once per call)
+// ------------------------------------------------------------------------------------------------
+// java.math.BigDecimal(String) (sign, digits with one optional '.', optional [eE][+-]digits; no
+// whitespace): value = (neg ? -1 : 1) * digits * 10^exp, digits without leading zeros
+struct Decimal {
+  bool neg = false;
+  std::string digits;  // "" = zero
+  long long exp = 0;
+};
+
+static bool parse_big_decimal(const char* s, Decimal* d) {
+  if (!s || !*s) return false;
+  const char* p = s;
+  d->neg = false;
+  if (*p == '+' || *p == '-') d->neg = *p++ == '-';
+  std::string all;
+  long long frac = 0;
+  bool dot = false, any = false;
+  for (; *p; ++p) {
+    if (*p >= '0' && *p <= '9') {
+      all.push_back(*p);
+      any = true;
+      if (dot) frac++;
+    } else if (*p == '.' && !dot) {
+      dot = true;
+    } else {
+      break;
+    }
+  }
+  if (!any) return false;
+  long long e = 0;
+  if (*p == 'e' || *p == 'E') {
+    p++;
+    bool eneg = false;
+    if (*p == '+' || *p == '-') eneg = *p++ == '-';
+    if (!(*p >= '0' && *p <= '9')) return false;
+    for (; *p >= '0' && *p <= '9'; ++p) {
+      e = e * 10 + (*p - '0');
+      if (e > 1000000000ll) return false;  // BigDecimal: the exponent must fit an int
+    }
+    if (eneg) e = -e;
+  }
+  if (*p) return false;
+  size_t z = 0;
+  while (z < all.size() && all[z] == '0') z++;
+  d->digits = all.substr(z);
+  d->exp = e - frac;
+  if (d->digits.empty()) d->neg = false;
+  return true;
+}
+
+// setScale(0, FLOOR / CEILING) (or exact: integral only) then longValueExact. Returns 1 = fits
+// *out, 0 = not integral (exact mode), +2 / -2 = beyond Long.MAX / Long.MIN
+static int decimal_to_long(const Decimal& d, int mode /* 0 exact, 1 floor, 2 ceiling */, long long* out) {
+  std::string ip;  // integer part digits
+  bool frac_nonzero = false;
+  if (d.exp >= 0) {
+    if (!d.digits.empty()) {
+      if (d.digits.size() + (size_t)d.exp > 40) return d.neg ? -2 : 2;
+      ip = d.digits + std::string((size_t)d.exp, '0');
+    }
+  } else {
+    const long long k = -d.exp;
+    if ((long long)d.digits.size() > k) ip = d.digits.substr(0, d.digits.size() - (size_t)k);
+    const std::string fr = (long long)d.digits.size() > k ? d.digits.substr(d.digits.size() - (size_t)k) : d.digits;
+    for (char c : fr) frac_nonzero |= c != '0';
+  }
+  if (mode == 0 && frac_nonzero) return 0;
+  if (ip.size() > 20) return d.neg ? -2 : 2;
+  unsigned __int128 m = 0;
+  for (char c : ip) m = m * 10 + (unsigned)(c - '0');
+  __int128 v = d.neg ? -(__int128)m : (__int128)m;
+  if (frac_nonzero) {
+    if (mode == 1 && d.neg) v -= 1;   // floor of a negative non-integer
+    if (mode == 2 && !d.neg) v += 1;  // ceiling of a positive non-integer
+  }
+  if (v > (__int128)INT64_MAX) return 2;
+  if (v < (__int128)INT64_MIN) return -2;
+  *out = (long long)v;
+  return 1;
+}
+
+// GuavaUtils.tryParseLong (a leading '+' stripped) -> Longs.tryParse: [-]digits within range
+static bool guava_try_parse_long(const char* s, long long* out) {
+  if (!s || !*s) return false;
+  if (*s == '+') s++;
+  return try_long(s, out);
+}
+
+// DimensionHandlerUtils.getExactLongFromDecimalString (DimensionHandlerUtils.java:404-426)
+static bool exact_long(const char* s, long long* out) {
+  if (guava_try_parse_long(s, out)) return true;
+  Decimal d;
+  if (!parse_big_decimal(s, &d)) return false;
+  return decimal_to_long(d, 0, out) == 1;
+}
+
+// Guava Floats/Doubles.tryParse: [+-]?(NaN|Infinity|decimal[eE..]?[fFdD]?|0[xX]hex[pP]exp[fFdD]?)
+// validated like FLOATING_POINT_PATTERN, then Float.parseFloat / Double.parseDouble (correctly rounded)
+static bool guava_float_syntax(const char* s, std::string* body) {
+  if (!s || !*s) return false;
+  const char* p = s;
+  std::string out;
+  if (*p == '+' || *p == '-') out.push_back(*p++);
+  if (!strcmp(p, "NaN") || !strcmp(p, "Infinity")) {
+    *body = out + p;
+    return true;
+  }
+  auto isx = [](char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); };
+  const char* q = p;
+  if (q[0] == '0' && (q[1] == 'x' || q[1] == 'X')) {
+    q += 2;
+    bool any = false;
+    while (isx(*q)) q++, any = true;
+    if (*q == '.') {
+      q++;
+      while (isx(*q)) q++, any = true;
+    }
+    if (!any || (*q != 'p' && *q != 'P')) return false;
+    q++;
+    if (*q == '+' || *q == '-') q++;
+    if (!(*q >= '0' && *q <= '9')) return false;
+    while (*q >= '0' && *q <= '9') q++;
+  } else {
+    bool any = false;
+    while (*q >= '0' && *q <= '9') q++, any = true;
+    if (*q == '.') {
+      q++;
+      while (*q >= '0' && *q <= '9') q++, any = true;
+    }
+    if (!any) return false;
+    if (*q == 'e' || *q == 'E') {
+      q++;
+      if (*q == '+' || *q == '-') q++;
+      if (!(*q >= '0' && *q <= '9')) return false;
+      while (*q >= '0' && *q <= '9') q++;
+    }
+  }
+  out.append(p, q);
+  if (*q == 'f' || *q == 'F' || *q == 'd' || *q == 'D') q++;
+  if (*q) return false;
+  *body = out;
+  return true;
+}
+
+static bool guava_try_parse_double(const char* s, double* out) {
+  std::string b;
+  if (!guava_float_syntax(s, &b)) return false;
+  *out = strtod(b.c_str(), nullptr);
+  return true;
+}
+
+static bool guava_try_parse_float(const char* s, float* out) {
+  std::string b;
+  if (!guava_float_syntax(s, &b)) return false;
+  *out = strtof(b.c_str(), nullptr);
+  return true;
+}
+
+static int64_t float_bits(float f) {  // Float.floatToIntBits
+  if (f != f) return 0x7fc00000ll;
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (int64_t)u;
+}
+
+static int64_t double_bits(double d) {  // Double.doubleToLongBits
+  if (d != d) return 0x7ff8000000000000ll;
+  int64_t u;
+  memcpy(&u, &d, 8);
+  return u;
+}
+
+static uint64_t dcmp_key_host(double d) {  // Double.compare order as unsigned keys
+  if (d != d) return ~0ull;
+  uint64_t u;
+  memcpy(&u, &d, 8);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+struct PredLeaf {
+  NumPred p;
+  std::vector<int64_t> set;
+  std::string lo, hi;
+  const Column* col;
+};
+
+// The row predicate of a selector / in / bound filter on a numeric column, as the reference builds
+// its ValueMatcher. Default null mode: a numeric row is never null, so null-matching predicates
+// (nullValueMatcher) select nothing.
+static int plan_numeric_leaf(const dg_filter& f, const Column* c, PredLeaf* L) {
+  memset(&L->p, 0, sizeof L->p);
+  L->col = c;
+  NumPred& p = L->p;
+  p.kind = PRED_FALSE;
+  const bool is_long = c->type == DG_COL_LONG, is_float = c->type == DG_COL_FLOAT;
+  auto add_value = [&](const char* v) {  // one selector / IN value
+    if (!v || !*v) return;  // emptyToNullIfNeeded -> null: no numeric row matches
+    if (is_long) {
+      long long x;
+      if (exact_long(v, &x)) L->set.push_back(x);
+    } else if (is_float) {
+      float x;
+      if (guava_try_parse_float(v, &x)) L->set.push_back(float_bits(x));
+    } else {
+      double x;
+      if (guava_try_parse_double(v, &x)) L->set.push_back(double_bits(x));
+    }
+  };
+  if (f.kind == DG_F_SELECTOR || f.kind == DG_F_IN) {
+    // SelectorFilter -> {Long,Float,Double}ValueMatcherColumnSelectorStrategy.makeValueMatcher(value)
+    // (convertObjectToLong = getExactLongFromDecimalString, Floats/Doubles.tryParse + *ToIntBits);
+    // InFilter -> InDimFilter.get{Long,Float,Double}PredicateSupplier (the same parsing, a set)
+    const int nv = f.kind == DG_F_SELECTOR ? std::min(f.n_values, 1) : f.n_values;
+    for (int k = 0; k < nv; ++k) add_value(f.values ? f.values[k] : nullptr);
+    std::sort(L->set.begin(), L->set.end());
+    L->set.erase(std::unique(L->set.begin(), L->set.end()), L->set.end());
+    if (!L->set.empty()) p.kind = is_long ? PRED_LONG_SET : PRED_BITS_SET;
+    return DG_OK;
+  }
+  // BoundFilter: NUMERIC ordering -> BoundDimFilter.{long,float,double}PredicateSupplier
+  // (BoundDimFilter.java:341-652); other orderings compare String.valueOf(value) (BoundFilter
+  // makeLongPredicate etc.: doesMatch) — for long columns under LEXICOGRAPHIC (UTF-8 bytes)
+  // the bounds are kept as given (BoundDimFilter.java:73-76; hasLowerBound = lower != null): "" is a
+  // bound, unparseable as a number
+  const char* lo = f.lower;
+  const char* hi = f.upper;
+  p.lo_strict = f.lower_strict;
+  p.hi_strict = f.upper_strict;
+  if (f.ordering != DG_ORDER_NUMERIC) {
+    if (!is_long || f.ordering != DG_ORDER_LEXICOGRAPHIC)
+      return set_error(DG_ERR_UNSUPPORTED, "bound ordering %d on numeric column %s (String.valueOf formatting)",
+                       f.ordering, c->name.c_str());
+    p.kind = PRED_LONG_LEX;
+    p.has_lo = lo != nullptr;
+    p.has_hi = hi != nullptr;
+    L->lo = lo ? lo : "";
+    L->hi = hi ? hi : "";
+    return DG_OK;
+  }
+  if (is_long) {
+    bool nothing = false;
+    long long lv = 0, hv = 0;
+    if (lo) {
+      if (guava_try_parse_long(lo, &lv)) {
+        p.has_lo = 1;
+      } else {
+        Decimal d;
+        if (!parse_big_decimal(lo, &d)) {
+          p.has_lo = 0;  // unparseable: below every number
+        } else {
+          const int r = decimal_to_long(d, f.lower_strict ? 1 : 2, &lv);
+          if (r == 1) p.has_lo = 1;
+          else if (r == 2) nothing = true;  // positive lower bound above every long
+        }
+      }
+    }
+    if (hi) {
+      if (guava_try_parse_long(hi, &hv)) {
+        p.has_hi = 1;
+      } else {
+        Decimal d;
+        if (!parse_big_decimal(hi, &d)) {
+          nothing = true;  // unparseable upper bound: below every number
+        } else {
+          const int r = decimal_to_long(d, f.upper_strict ? 2 : 1, &hv);
+          if (r == 1) p.has_hi = 1;
+          else if (r == -2) nothing = true;
+        }
+      }
+    }
+    p.kind = nothing ? PRED_FALSE : PRED_LONG_RANGE;
+    p.lo = lv;
+    p.hi = hv;
+    return DG_OK;
+  }
+  bool nothing = false;
+  double lv = 0, hv = 0;
+  if (lo) {
+    if (is_float) {
+      float x;
+      p.has_lo = guava_try_parse_float(lo, &x);
+      lv = x;
+    } else {
+      p.has_lo = guava_try_parse_double(lo, &lv);
+    }
+  }
+  if (hi) {
+    bool ok;
+    if (is_float) {
+      float x;
+      ok = guava_try_parse_float(hi, &x);
+      hv = x;
+    } else {
+      ok = guava_try_parse_double(hi, &hv);
+    }
+    p.has_hi = ok;
+    nothing = !ok;
+  }
+  p.kind = nothing ? PRED_FALSE : PRED_ORD_RANGE;
+  p.lo = (int64_t)dcmp_key_host(lv);
+  p.hi = (int64_t)dcmp_key_host(hv);
+  return DG_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // filter planning: prefix nodes -> postfix program over leaf bitsets
 // ------------------------------------------------------------------------------------------------
 struct FilterPlan {
   std::vector<int32_t> prog;
   std::vector<std::vector<int32_t>> leaf_ids;  // dictionary ids whose bitmaps are OR-ed
-  std::vector<const Column*> leaf_col;
+  std::vector<const Column*> leaf_col;         // null: a row-predicate leaf (leaf_pred)
+  std::vector<int32_t> leaf_pred;              // index into preds, -1 for bitmap leaves
+  std::vector<PredLeaf> preds;
 };
 
 static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos, FilterPlan* fp) {
@@ -407,10 +727,25 @@ static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos
     case DG_F_BOUND: {
       if (!f.dimension) return set_error(DG_ERR_ARG, "filter without dimension");
       const Column* c = seg->find(f.dimension);
-      if (!c || c->type == DG_COL_LONG || c->type == DG_COL_FLOAT || c->type == DG_COL_DOUBLE) {
-        if (c) return set_error(DG_ERR_UNSUPPORTED, "filter on numeric column %s", f.dimension);
+      if (!c) {
         // missing column: allTrue iff the filter matches null (ColumnSelectorBitmapIndexSelector.java:212-218)
         fp->prog.push_back(leaf_matches_null(f) ? -1 : -2);
+        return DG_OK;
+      }
+      if (c->type == DG_COL_LONG || c->type == DG_COL_FLOAT || c->type == DG_COL_DOUBLE) {
+        // no bitmap index: a row post-filter (QueryableIndexStorageAdapter.java:244-260, FilteredOffset)
+        PredLeaf L;
+        int rc = plan_numeric_leaf(f, c, &L);
+        if (rc) return rc;
+        if (L.p.kind == PRED_FALSE) {
+          fp->prog.push_back(-2);
+          return DG_OK;
+        }
+        fp->prog.push_back((int32_t)fp->leaf_ids.size());
+        fp->leaf_ids.emplace_back();
+        fp->leaf_col.push_back(nullptr);
+        fp->leaf_pred.push_back((int32_t)fp->preds.size());
+        fp->preds.push_back(std::move(L));
         return DG_OK;
       }
       if (c->type != DG_COL_STRING || !c->has_bitmaps)
@@ -456,6 +791,7 @@ static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos
       fp->prog.push_back((int32_t)fp->leaf_ids.size());
       fp->leaf_ids.push_back(std::move(ids));
       fp->leaf_col.push_back(c);
+      fp->leaf_pred.push_back(-1);
       return DG_OK;
     }
     default:
@@ -496,6 +832,7 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
   // one launch per (column, codec): group leaves by column
   for (int l = 0; l < nleaves; ++l) {
     const Column* c = fp.leaf_col[l];
+    if (!c) continue;  // row-predicate leaf, below
     // gather all leaves on the same column into this launch
     bool first = true;
     for (int k = 0; k < l; ++k)
@@ -533,6 +870,41 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
       launch_concise_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, (nwords + 2) * 32, st);
     }
   }
+  // row-predicate leaves: decode the column (its blocks, as the reference's post-filter reads them
+  // through the column selector) and evaluate the predicate per row into the leaf's bitset
+  for (int l = 0; l < nleaves; ++l) {
+    if (fp.leaf_pred[l] < 0) continue;
+    PredLeaf& L = fp.preds[fp.leaf_pred[l]];
+    DecodeBatch db;
+    ColView v;
+    memset(&v, 0, sizeof v);
+    int rc2 = column_view(L.col, cs, &db, &v, st);
+    if (rc2) return rc2;
+    if (!L.set.empty()) {
+      int64_t* d_set;
+      int64_t* h_set = up_take<int64_t>(cs, L.set.size(), &d_set, st);
+      if (!h_set) return set_error(DG_ERR_OOM, "predicate set");
+      memcpy(h_set, L.set.data(), 8 * L.set.size());
+      L.p.set = d_set;
+      L.p.nset = (int32_t)L.set.size();
+    }
+    if (L.p.kind == PRED_LONG_LEX) {
+      uint8_t *d_lo, *d_hi;
+      uint8_t* h_lo = up_take<uint8_t>(cs, L.lo.size() + 1, &d_lo, st);
+      uint8_t* h_hi = up_take<uint8_t>(cs, L.hi.size() + 1, &d_hi, st);
+      if (!h_lo || !h_hi) return set_error(DG_ERR_OOM, "predicate bounds");
+      memcpy(h_lo, L.lo.data(), L.lo.size());
+      memcpy(h_hi, L.hi.data(), L.hi.size());
+      L.p.lo_str = d_lo;
+      L.p.hi_str = d_hi;
+      L.p.lo_len = (int32_t)L.lo.size();
+      L.p.hi_len = (int32_t)L.hi.size();
+    }
+    rc2 = run_decodes(cs, &db, st);
+    if (rc2) return rc2;
+    DG_FLUSH(cs, st);
+    launch_num_pred(v, seg->nrows, L.p, h_sets[l], st);
+  }
   const int plen = (int)fp.prog.size();
   int32_t* d_prog;
   int32_t* h_prog = up_take<int32_t>(cs, plen + 2, &d_prog, st);  // + the zeroed 8-byte count
@@ -553,15 +925,6 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
 // ------------------------------------------------------------------------------------------------
 // column decode: returns a ColView, scheduling LZ4 block decodes into scratch when needed
 // ------------------------------------------------------------------------------------------------
-struct DecodeBatch {
-  std::vector<Lz4Job> jobs;
-  std::vector<LzfJob> lzf_jobs;  // LZF blocks, decoded one wave per block
-  std::vector<VsJob> expands;  // DELTA / TABLE blocks, expanded after the LZ4 decodes
-  int32_t expand_rows = 0;     // largest block of `expands` (grid width)
-  int64_t* last_expanded = nullptr;
-  uint8_t* last_slots = nullptr;  // decode slots of the last viewed LZ4 / LZF column
-  int64_t bytes = 0;  // algorithmic bytes read
-};
 
 static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect) {
   Lz4Job j;
@@ -674,7 +1037,7 @@ static int run_lzf(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
   return DG_OK;
 }
 
-static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr) {
+static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof) {
   int rcl = run_lzf(cs, db, st);
   if (rcl) return rcl;
   if (db->jobs.empty()) return run_expands(cs, db, st);

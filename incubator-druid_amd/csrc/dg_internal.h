@@ -301,6 +301,30 @@ void launch_roaring_or(const uint8_t* bm_base, const int64_t* d_off, const int32
                        int nbitmaps, uint32_t* const* d_sets, int32_t* d_err, int64_t limit_bits, hipStream_t s);
 void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_sets, uint32_t* out, int64_t nrows,
                         unsigned long long* d_count, hipStream_t s);
+// Row predicate of a filter on a numeric column: the reference evaluates it per row as a post-filter
+// (QueryableIndexStorageAdapter.makeCursors :244-260 -> FilteredOffset.java:40-105) through the
+// column's ValueMatcher ({Long,Float,Double}ValueMatcherColumnSelectorStrategy, the filters'
+// DruidLong/Float/DoublePredicate); here it becomes one more row bitset of the filter program.
+enum PredKind : int32_t {
+  PRED_FALSE = 0,       // matches no row (unparseable selector value, empty IN, ALWAYS_FALSE bounds)
+  PRED_LONG_RANGE = 1,  // long column: [lo, hi] with strictness (makeLongPredicateFromBounds)
+  PRED_LONG_SET = 2,    // long column: value in the sorted set (IN / selector)
+  PRED_ORD_RANGE = 3,   // float/double column: Double.compare range on (double) value, as ordered keys
+  PRED_BITS_SET = 4,    // float/double column: floatToIntBits / doubleToLongBits in the sorted set
+  PRED_LONG_LEX = 5,    // long column: String.valueOf(value) vs UTF-8 bound strings (LEXICOGRAPHIC)
+};
+struct NumPred {
+  int32_t kind;
+  int32_t has_lo, has_hi, lo_strict, hi_strict;
+  int32_t nset;
+  int64_t lo, hi;         // LONG_RANGE: bounds; ORD_RANGE: ordered keys (uint64 bit patterns)
+  const int64_t* set;     // LONG_SET / BITS_SET: sorted values / canonical bit patterns
+  const uint8_t* lo_str;  // LONG_LEX: bound bytes
+  const uint8_t* hi_str;
+  int32_t lo_len, hi_len;
+};
+// out: bitset words of rows [0, nrows) (bit r of word r >> 5); v: the decoded numeric column
+void launch_num_pred(ColView v, int64_t nrows, NumPred p, uint32_t* out, hipStream_t s);
 void launch_fill_u64(uint64_t* p, int64_t n_rows_of_slots, int slots_per_row, const uint64_t* d_init, hipStream_t s);
 void launch_scan_agg(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, int topn, hipStream_t s);
 // topN aggregation with LDS-private dictionary-id ranges: workgroup (p, s) owns ids

@@ -255,6 +255,93 @@ __global__ __launch_bounds__(256) void k_filter_eval(const int32_t* __restrict__
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
 }
 
+// ------------------------------------------------------------------------------------------------
+// numeric post-filters: per-row predicate -> bitset words (FilteredOffset + ValueMatcher, see NumPred)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool in_sorted(const int64_t* set, int n, int64_t x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (set[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < n && set[lo] == x;
+}
+
+// Double.compare order as unsigned keys: -0.0 < 0.0, every NaN equal and greatest
+__device__ __forceinline__ uint64_t dcmp_key(double d) { return d != d ? ~0ull : ord_key(d); }
+
+// UnsignedBytes.lexicographicalComparator of String.valueOf(x) (ASCII) against a UTF-8 string
+__device__ __forceinline__ int lex_cmp_long(int64_t x, const uint8_t* b, int blen) {
+  char buf[20];
+  int n = 0;
+  uint64_t u = x < 0 ? (uint64_t)0 - (uint64_t)x : (uint64_t)x;
+  do {
+    buf[n++] = (char)('0' + (int)(u % 10));
+    u /= 10;
+  } while (u);
+  const int len = n + (x < 0 ? 1 : 0);
+  for (int i = 0; i < len && i < blen; ++i) {
+    const int c = x < 0 ? (i == 0 ? '-' : buf[n - i]) : buf[n - 1 - i];
+    if (c != b[i]) return c < (int)b[i] ? -1 : 1;
+  }
+  return (len > blen) - (len < blen);
+}
+
+__device__ __forceinline__ bool range_ok(int lc, int uc, const NumPred& p) {
+  // lc = compare(value, lower), uc = compare(upper, value)
+  const bool lok = !p.has_lo || (p.lo_strict ? lc > 0 : lc >= 0);
+  const bool uok = !p.has_hi || (p.hi_strict ? uc > 0 : uc >= 0);
+  return lok && uok;
+}
+
+__global__ __launch_bounds__(256) void k_num_pred(ColView v, int64_t nrows, NumPred p, uint32_t* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool m = false;
+  if (r < nrows && p.kind != PRED_FALSE) {
+    const uint8_t* ptr = cv_ptr(v, r);
+    if (v.kind == VIEW_LONG) {
+      const int64_t x = *reinterpret_cast<const int64_t*>(ptr);
+      if (p.kind == PRED_LONG_RANGE) m = range_ok((x > p.lo) - (x < p.lo), (p.hi > x) - (p.hi < x), p);
+      else if (p.kind == PRED_LONG_SET) m = in_sorted(p.set, p.nset, x);
+      else if (p.kind == PRED_LONG_LEX) {
+        const int lc = p.has_lo ? lex_cmp_long(x, p.lo_str, p.lo_len) : 1;
+        const int uc = p.has_hi ? -lex_cmp_long(x, p.hi_str, p.hi_len) : 1;
+        m = range_ok(lc, uc, p);
+      }
+    } else {
+      int64_t bits;
+      double d;
+      if (v.kind == VIEW_FLOAT) {
+        const float f = *reinterpret_cast<const float*>(ptr);
+        bits = f != f ? 0x7fc00000ll : (int64_t)__float_as_uint(f);  // Float.floatToIntBits
+        d = (double)f;
+      } else {
+        d = *reinterpret_cast<const double*>(ptr);
+        bits = d != d ? 0x7ff8000000000000ll : (int64_t)__double_as_longlong(d);  // Double.doubleToLongBits
+      }
+      if (p.kind == PRED_BITS_SET) {
+        m = in_sorted(p.set, p.nset, bits);
+      } else if (p.kind == PRED_ORD_RANGE) {
+        const uint64_t k = dcmp_key(d), klo = (uint64_t)p.lo, khi = (uint64_t)p.hi;
+        m = range_ok((k > klo) - (k < klo), (khi > k) - (khi < k), p);
+      }
+    }
+  }
+  const uint64_t b = __ballot(m);
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (r - lane) >> 5;  // first word of this wave's 64 rows
+  if (r - lane < nrows) {
+    if (lane == 0) out[w] = (uint32_t)b;
+    if (lane == 32 && r < nrows) out[w + 1] = (uint32_t)(b >> 32);
+  }
+}
+
+void launch_num_pred(ColView v, int64_t nrows, NumPred p, uint32_t* out, hipStream_t s) {
+  if (nrows <= 0) return;
+  hipLaunchKernelGGL(k_num_pred, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, v, nrows, p, out);
+}
+
 void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_sets, uint32_t* out, int64_t nrows,
                         unsigned long long* d_count, hipStream_t s) {
   const int64_t nwords = (nrows + 31) >> 5;

@@ -32,6 +32,7 @@ import heapq
 import importlib
 import math
 import os
+import re
 import struct
 import sys
 from decimal import Decimal, InvalidOperation
@@ -788,6 +789,185 @@ def _leaf_matches_null(f) -> bool:
     raise TypeError(f)
 
 
+# ---- numeric columns: row post-filters (no bitmap index; QueryableIndexStorageAdapter.java:244-260,
+# FilteredOffset.java:40-105) through the column's ValueMatcher (query/filter/{Long,Float,Double}
+# ValueMatcherColumnSelectorStrategy.java) and the filters' numeric predicates ----
+_LONG_RE = re.compile(r"-?[0-9]+\Z")
+_BIGDEC_RE = re.compile(r"[+-]?(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?\Z")
+_GUAVA_FP_RE = re.compile(r"[+-]?(?:NaN|Infinity|(?:(?:[0-9]+(?:\.[0-9]*)?|\.[0-9]+)(?:[eE][+-]?[0-9]+)?"
+                          r"|0[xX](?:[0-9a-fA-F]+(?:\.[0-9a-fA-F]*)?|\.[0-9a-fA-F]+)[pP][+-]?[0-9]+)[fFdD]?)\Z")
+_I64 = (-(1 << 63), (1 << 63) - 1)
+
+
+def o_try_parse_long(v):
+    """GuavaUtils.tryParseLong (java-util GuavaUtils.java:37-42): '+' stripped, Longs.tryParse."""
+    if v is None or v == "":
+        return None
+    if v[0] == "+":
+        v = v[1:]
+    if not _LONG_RE.match(v):
+        return None
+    x = int(v)
+    return x if _I64[0] <= x <= _I64[1] else None
+
+
+def o_big_decimal(v):
+    """new BigDecimal(String): None when it throws NumberFormatException."""
+    if v is None or not _BIGDEC_RE.match(v):
+        return None
+    return Decimal(v)
+
+
+def o_exact_long(v):
+    """DimensionHandlerUtils.getExactLongFromDecimalString (:404-426)."""
+    x = o_try_parse_long(v)
+    if x is not None:
+        return x
+    d = o_big_decimal(v)
+    if d is None or d != d.to_integral_value():
+        return None
+    x = int(d)
+    return x if _I64[0] <= x <= _I64[1] else None
+
+
+def _o_float32_exact(v: str) -> float:
+    """Float.parseFloat: the float nearest the decimal value (ties to even), not via a double."""
+    from fractions import Fraction
+    x = Fraction(Decimal(v))
+    f0 = np.float32(float(x))
+    if not np.isfinite(f0):
+        return float(f0)
+    best = None
+    for c in (np.nextafter(f0, np.float32(-np.inf)), f0, np.nextafter(f0, np.float32(np.inf))):
+        if not np.isfinite(c):
+            continue
+        dist = abs(Fraction(float(c)) - x)
+        key = (dist, int(np.float32(c).view(np.uint32)) & 1)
+        if best is None or key < best[0]:
+            best = (key, c)
+    return float(best[1])
+
+
+def o_try_parse_fp(v, single: bool):
+    """Guava Floats.tryParse / Doubles.tryParse: FLOATING_POINT_PATTERN, then Float.parseFloat /
+    Double.parseDouble; None when it does not match."""
+    if v is None or not _GUAVA_FP_RE.match(v):
+        return None
+    body = v[:-1] if v[-1] in "fFdD" and not v.endswith("Infinity") else v
+    if body.lstrip("+-") in ("NaN", "Infinity"):
+        x = float(body.replace("Infinity", "inf"))
+        return float(np.float32(x)) if single else x
+    if "x" in body or "X" in body:
+        x = float.fromhex(body)
+        return float(np.float32(x)) if single else x
+    return _o_float32_exact(body) if single else float(body)
+
+
+def _o_bits(x, single: bool) -> int:
+    """Float.floatToIntBits / Double.doubleToLongBits (canonical NaN)."""
+    if x != x:
+        return 0x7fc00000 if single else 0x7ff8000000000000
+    return int(np.float32(x).view(np.uint32)) if single else int(np.float64(x).view(np.int64))
+
+
+def _o_dcmp(a: float, b: float) -> int:
+    """Double.compare: -0.0 < 0.0, NaN equal to itself and above everything."""
+    if a != a or b != b:
+        return (a != a) - (b != b)
+    if a < b:
+        return -1
+    if a > b:
+        return 1
+    sa, sb = math.copysign(1.0, a) < 0, math.copysign(1.0, b) < 0
+    return (sb > sa) - (sa > sb) if a == 0.0 else 0
+
+
+def _o_bound_ok(lc, uc, f, has_lo, has_hi):
+    lok = (not has_lo) or (lc > 0 if f.lowerStrict else lc >= 0)
+    uok = (not has_hi) or (uc > 0 if f.upperStrict else uc >= 0)
+    return lok and uok
+
+
+def numeric_leaf_mask(seg: OracleSegment, f) -> np.ndarray:
+    """Row mask of a selector / in / bound filter on a long, float or double column."""
+    kind = seg.column_kind(f.dimension)
+    n = seg.num_rows
+    single = kind == OR_FLOAT
+    vals = seg.numeric(f.dimension, {OR_LONG: "long", OR_FLOAT: "float", OR_DOUBLE: "double"}[kind])
+    if isinstance(f, (Q.SelectorDimFilter, Q.InDimFilter)):
+        raw = [f.value] if isinstance(f, Q.SelectorDimFilter) else list(f.values)
+        raw = [o_empty_to_null(v) for v in raw]  # null: nullValueMatcher, no numeric row is null
+        if kind == OR_LONG:
+            want = {x for x in (o_exact_long(v) for v in raw if v is not None) if x is not None}
+            return np.isin(vals, np.array(sorted(want), dtype=np.int64)) if want else np.zeros(n, bool)
+        want = {_o_bits(x, single) for x in (o_try_parse_fp(v, single) for v in raw if v is not None) if x is not None}
+        if not want:
+            return np.zeros(n, bool)
+        bits = np.array([_o_bits(float(x), single) for x in vals], dtype=np.int64)
+        return np.isin(bits, np.array(sorted(want), dtype=np.int64))
+    if not isinstance(f, Q.BoundDimFilter):
+        raise Unsupported(f"{type(f).__name__} on numeric column {f.dimension}")
+    has_lo, has_hi = f.lower is not None, f.upper is not None
+    if f.ordering != "numeric":
+        if kind != OR_LONG or f.ordering != "lexicographic":
+            raise Unsupported(f"bound ordering {f.ordering} on a {kind} column")
+        # BoundFilter makeLongPredicate: doesMatch(String.valueOf(x)) under the UTF-8 byte comparator
+        lo, hi = (f.lower or "").encode(), (f.upper or "").encode()
+        out = np.zeros(n, bool)
+        for i, x in enumerate(vals):
+            sv = str(int(x)).encode()
+            lc = (sv > lo) - (sv < lo) if has_lo else 1
+            uc = (hi > sv) - (hi < sv) if has_hi else 1
+            out[i] = _o_bound_ok(lc, uc, f, has_lo, has_hi)
+        return out
+    if kind == OR_LONG:  # BoundDimFilter.makeLongPredicateSupplier (:341-452)
+        nothing = False
+        lo = hi = 0
+        lo_ok = hi_ok = False
+        if has_lo:
+            x = o_try_parse_long(f.lower)
+            if x is not None:
+                lo, lo_ok = x, True
+            else:
+                d = o_big_decimal(f.lower)
+                if d is not None:
+                    r = int(d.to_integral_value(rounding="ROUND_FLOOR" if f.lowerStrict else "ROUND_CEILING"))
+                    if _I64[0] <= r <= _I64[1]:
+                        lo, lo_ok = r, True
+                    elif r > 0:
+                        nothing = True
+        if has_hi:
+            x = o_try_parse_long(f.upper)
+            if x is not None:
+                hi, hi_ok = x, True
+            else:
+                d = o_big_decimal(f.upper)
+                if d is None:
+                    nothing = True
+                else:
+                    r = int(d.to_integral_value(rounding="ROUND_CEILING" if f.upperStrict else "ROUND_FLOOR"))
+                    if _I64[0] <= r <= _I64[1]:
+                        hi, hi_ok = r, True
+                    elif r < 0:
+                        nothing = True
+        if nothing:
+            return np.zeros(n, bool)
+        v = vals.astype(object)
+        return np.array([_o_bound_ok((x > lo) - (x < lo), (hi > x) - (hi < x), f, lo_ok, hi_ok) for x in v], dtype=bool)
+    # float / double: Floats/Doubles.tryParse bounds, Double.compare on the (double) value (:489-588)
+    lo = o_try_parse_fp(f.lower, single) if has_lo else None
+    hi = o_try_parse_fp(f.upper, single) if has_hi else None
+    if has_hi and hi is None:
+        return np.zeros(n, bool)
+    return np.array([_o_bound_ok(_o_dcmp(float(x), lo) if lo is not None else 1,
+                                 _o_dcmp(hi, float(x)) if hi is not None else 1, f, lo is not None, hi is not None)
+                     for x in vals], dtype=bool)
+
+
+class Unsupported(Exception):
+    """A shape the engine answers with DG_ERR_UNSUPPORTED (the Java factory keeps its CPU path)."""
+
+
 def filter_mask(seg: OracleSegment, f) -> np.ndarray:
     n = seg.num_rows
     if f is None:
@@ -804,6 +984,8 @@ def filter_mask(seg: OracleSegment, f) -> np.ndarray:
         return m
     if isinstance(f, Q.NotDimFilter):
         return ~filter_mask(seg, f.field)
+    if seg.column_kind(f.dimension) in (OR_LONG, OR_FLOAT, OR_DOUBLE):
+        return numeric_leaf_mask(seg, f)
     if not seg.is_dim(f.dimension):
         # missing column: allTrue iff the filter matches null (ColumnSelectorBitmapIndexSelector:212-218)
         return np.full(n, _leaf_matches_null(f), dtype=bool)

@@ -145,13 +145,101 @@ SUITES = {
 }
 
 
+# numeric columns (no bitmap index: row post-filters). rows: [dim0, value of each numeric column]
+LONG_ROWS = [["1", 1], ["2", 2], ["3", 3], ["4", 4], ["5", 5], ["6", 6], ["7", 100000000], ["8", 100000001],
+             ["9", -25], ["10", -100000001]]
+FD_ROWS = [[str(i), float(i), float(i)] for i in range(1, 7)]
+ALL10 = [str(i) for i in range(1, 11)]
+
+
+def _fd_cases(col):
+    return [
+        [sel(col, "3"), ["3"]], [sel(col, "3.0"), ["3"]],
+        [bound(col, "2", "5", ordering="numeric"), ["2", "3", "4", "5"]],
+        [bound(col, "2.0", "5.0", ordering="numeric"), ["2", "3", "4", "5"]],
+        [bound(col, "1", "4", True, True, "numeric"), ["2", "3"]],
+        [bound(col, "1.0", "4.0", True, True, "numeric"), ["2", "3"]],
+        [inf(col, "2", "4", "8"), ["2", "4"]], [inf(col, "2.0", "4.0", "8.0"), ["2", "4"]],
+        [inf(col, *[str(2 * i) for i in range(32)]), ["2", "4", "6"]],
+        [sel(col, ""), []], [sel(col, None), []], [sel(col, "abc"), []],
+        [bound(col, "a", "b", ordering="numeric"), []],
+        [bound(col, " ", "4", ordering="numeric"), ["1", "2", "3", "4"]],
+        [bound(col, " ", "A", ordering="numeric"), []],
+    ]
+
+
+def _fd_unsupported(col):
+    # String.valueOf(float / double) under LEXICOGRAPHIC, regex / search over it: the engine returns
+    # DG_ERR_UNSUPPORTED (the Java factory keeps its CPU engine); expected results kept for reference
+    return [
+        [bound(col, " ", "4", ordering="lexicographic"), ["1", "2", "3"]],
+        [bound(col, " ", "4.0", ordering="lexicographic"), ["1", "2", "3", "4"]],
+        [bound(col, " ", "A", ordering="lexicographic"), ["1", "2", "3", "4", "5", "6"]],
+        [{"type": "regex", "dimension": col, "pattern": "4"}, ["4"]],
+        [{"type": "regex", "dimension": col, "pattern": "4.0"}, ["4"]],
+        [{"type": "search", "dimension": col, "query": {"type": "contains", "value": "2", "caseSensitive": True}},
+         ["2"]],
+    ]
+
+
+NUMERIC_SUITES = {
+    "LongFilteringTest": {
+        "_source": "LongFilteringTest.java:88-99 (rows), :129-316 (testLongColumnFiltering, "
+                   "testLongColumnFilteringWithNonNumbers)",
+        "columns": {"lng": "long"},
+        "rows": LONG_ROWS,
+        "cases": [
+            [sel("lng", "0"), []], [sel("lng", "3"), ["3"]], [sel("lng", "3.0"), ["3"]],
+            [sel("lng", "3.00000000000000000000001"), []], [sel("lng", "100000001.0"), ["8"]],
+            [sel("lng", "-100000001.0"), ["10"]], [sel("lng", "111119223372036854775807.674398674398"), []],
+            [bound("lng", "2", "5", ordering="numeric"), ["2", "3", "4", "5"]],
+            [bound("lng", "1", "4", True, True, "numeric"), ["2", "3"]],
+            [bound("lng", "2.0", "5.0", ordering="numeric"), ["2", "3", "4", "5"]],
+            [bound("lng", "2.0", "5.0", True, True, "numeric"), ["3", "4"]],
+            [bound("lng", "1.9", "5.9", True, True, "numeric"), ["2", "3", "4", "5"]],
+            [bound("lng", "2.1", "5.9", ordering="numeric"), ["3", "4", "5"]],
+            [bound("lng", "111119223372036854775807.67", "5.9", ordering="numeric"), []],
+            [bound("lng", "-111119223372036854775807.67", "5.9", ordering="numeric"), ["1", "2", "3", "4", "5", "9", "10"]],
+            [bound("lng", "2.1", "111119223372036854775807.67", ordering="numeric"), ["3", "4", "5", "6", "7", "8"]],
+            [bound("lng", "2.1", "-111119223372036854775807.67", ordering="numeric"), []],
+            [bound("lng", "100000000.0", "100000001.0", True, True, "numeric"), []],
+            [bound("lng", "100000000.0", "100000001.0", ordering="numeric"), ["7", "8"]],
+            [inf("lng", "2", "4", "8"), ["2", "4"]],
+            [inf("lng", "1.999999999999999999", "4.00000000000000000000001"), []],
+            [inf("lng", "100000001.0", "99999999.999999999"), ["8"]],
+            [inf("lng", "-25.0", "-99999999.999999999"), ["9"]],
+            [inf("lng", *[str(2 * i) for i in range(32)]), ["2", "4", "6"]],
+            [sel("lng", ""), []], [sel("lng", None), []], [sel("lng", "abc"), []],
+            [bound("lng", "a", "b", ordering="numeric"), []],
+            [bound("lng", " ", "4", ordering="numeric"), ["1", "2", "3", "4", "9", "10"]],
+            [bound("lng", " ", "4", ordering="lexicographic"), ["1", "2", "3", "4", "7", "8", "9", "10"]],
+            [bound("lng", " ", "A", ordering="numeric"), []],
+            [bound("lng", " ", "A", ordering="lexicographic"), ALL10],
+        ],
+        "unsupported": [
+            [{"type": "regex", "dimension": "lng", "pattern": "4"}, ["4"]],
+            [{"type": "search", "dimension": "lng", "query": {"type": "contains", "value": "2", "caseSensitive": True}},
+             ["2", "9"]],
+        ],
+    },
+    "FloatAndDoubleFilteringTest": {
+        "_source": "FloatAndDoubleFilteringTest.java:84-91 (rows), :160-290 (doTestFloatColumnFiltering, "
+                   "doTestFloatColumnFilteringWithNonNumbers; float and double columns)",
+        "columns": {"flt": "float", "dbl": "double"},
+        "rows": FD_ROWS,
+        "cases": _fd_cases("flt") + _fd_cases("dbl"),
+        "unsupported": _fd_unsupported("flt") + _fd_unsupported("dbl"),
+    },
+}
+
+
 def main():
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kats.json")
     with open(path) as f:
         kats = json.load(f)
     kats["filter_kats"] = {"_source": "processing/src/test/java/org/apache/druid/segment/filter/ "
                                       "(replaceWithDefault branch; expected = dim0 values of the matching rows)",
-                           "suites": SUITES}
+                           "suites": SUITES, "numeric_suites": NUMERIC_SUITES}
     with open(path, "w") as f:
         json.dump(kats, f, indent=1)
         f.write("\n")

@@ -31,10 +31,47 @@ def _suites(kats):
     return sorted(kats["filter_kats"]["suites"].items())
 
 
+def _numeric_suites(kats):
+    return sorted(kats["filter_kats"]["numeric_suites"].items())
+
+
+def _write_numeric(W, path, suite, comp, enc):
+    rows = suite["rows"]
+    n = len(rows)
+    dt = {"long": np.int64, "float": np.float32, "double": np.float64}
+    metrics = {c: (t, np.array([r[1 + i] for r in rows], dtype=dt[t])) for i, (c, t) in enumerate(suite["columns"].items())}
+    spec = W.SegmentSpec(timestamps=np.arange(1, n + 1, dtype=np.int64), dims={"dim0": W.encode_strings([r[0] for r in rows])},
+                         metrics=metrics)
+    return W.write_segment(path, spec, compression=comp, long_encoding=enc, lz4_mode="fast")
+
+
+NUM_LAYOUTS = [("lz4", "longs"), ("lz4", "auto"), ("uncompressed", "longs"), ("none", "auto")]
+
+
 def test_filter_kats_transcribed(kats):
     suites = dict(_suites(kats))
     assert set(suites) == {"SelectorFilterTest", "BoundFilterTest", "InFilterTest", "AndFilterTest", "NotFilterTest"}
     assert sum(len(s["cases"]) for s in suites.values()) >= 120
+    nums = dict(_numeric_suites(kats))
+    assert set(nums) == {"LongFilteringTest", "FloatAndDoubleFilteringTest"}
+    assert sum(len(s["cases"]) for s in nums.values()) >= 60
+
+
+@pytest.mark.parametrize("layout", NUM_LAYOUTS)
+def test_oracle_numeric_filter_kats(Q, O, W, kats, tmp_path, layout):
+    """Row post-filters on long / float / double columns (LongFilteringTest, FloatAndDoubleFilteringTest)."""
+    for name, suite in _numeric_suites(kats):
+        o = O.OracleSegment(_write_numeric(W, str(tmp_path / name), suite, *layout))
+        dim0 = [r[0] for r in suite["rows"]]
+        for fjs, expected in suite["cases"]:
+            mask = O.filter_mask(o, O.o_optimize(Q.DimFilter.from_json(fjs)))
+            got = sorted(dim0[i] for i in np.flatnonzero(mask))
+            assert got == sorted(expected), (name, fjs, got, expected)
+            # inside a compound filter with a bitmap leaf: AND(post-filter, dim0 bitmap) / OR / NOT
+            f = Q.DimFilter.from_json(fjs)
+            both = O.filter_mask(o, O.o_optimize(Q.AndDimFilter([f, Q.NotDimFilter(Q.SelectorDimFilter("dim0", "3"))])))
+            assert sorted(dim0[i] for i in np.flatnonzero(both)) == sorted(x for x in expected if x != "3")
+        o.close()
 
 
 @pytest.mark.parametrize("layout", LAYOUTS)
@@ -68,3 +105,64 @@ def test_gpu_filter_kats(Q, W, kats, tmp_path, layout):
             res = R.run_query(q, [g])
             assert (res[0].value["rows"] if res else 0) == len(expected), (name, fjs)
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", NUM_LAYOUTS)
+def test_gpu_numeric_filter_kats(Q, W, kats, tmp_path, layout):
+    R = importlib.import_module("incubator-druid_amd.runners")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    N = importlib.import_module("incubator-druid_amd._native")
+    for name, suite in _numeric_suites(kats):
+        g = S.GpuSegment(_write_numeric(W, str(tmp_path / name), suite, *layout))
+        dim0 = [r[0] for r in suite["rows"]]
+        for fjs, expected in suite["cases"]:
+            f = Q.DimFilter.from_json(fjs)
+            for flt, exp in ((f, expected),
+                             (Q.AndDimFilter([f, Q.NotDimFilter(Q.SelectorDimFilter("dim0", "3"))]),
+                              [x for x in expected if x != "3"]),
+                             (Q.OrDimFilter([f, Q.SelectorDimFilter("dim0", "1")]), sorted(set(expected) | {"1"}))):
+                words, cnt = g.filter_bitmap(flt.optimize(), Q)
+                bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:g.num_rows].astype(bool)
+                got = sorted(dim0[i] for i in np.flatnonzero(bits))
+                assert got == sorted(exp) and cnt == len(exp), (name, flt, got, exp)
+            q = Q.TimeseriesQuery(intervals=[(0, 1000)], aggregations=[Q.count("rows")], filter=f)
+            res = R.run_query(q, [g])
+            assert (res[0].value["rows"] if res else 0) == len(expected), (name, fjs)
+        for fjs, _ in suite["unsupported"]:
+            with pytest.raises(N.UnsupportedQuery):
+                g.filter_bitmap(Q.DimFilter.from_json(fjs).optimize(), Q)
+        g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", [("concise", "lz4"), ("roaring", "none")])
+def test_gpu_numeric_post_filters_match_oracle(Q, O, basic_dirs, layout):
+    """Numeric post-filters at scale (3 x 40k-row segments, multi-block columns): long / double
+    selector, in, numeric and lexicographic bounds, combined with bitmap filters, through every
+    engine (timeseries, topN, groupBy) vs the oracle."""
+    from compare import assert_results
+    R = importlib.import_module("incubator-druid_amd.runners")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    paths = basic_dirs[layout]
+    g, o = [S.GpuSegment(p) for p in paths], [O.OracleSegment(p) for p in paths]
+    filters = [
+        Q.BoundDimFilter("sumLongSequential", "100", "2500.5", False, True, ordering="numeric"),
+        Q.SelectorDimFilter("maxLongUniform", "250"),
+        Q.InDimFilter("maxLongUniform", ["1", "2.0", "3.5", "x", "499"]),
+        Q.BoundDimFilter("sumFloatNormal", "4999.5", "5000.25", True, False, ordering="numeric"),
+        Q.InDimFilter("minFloatZipf", ["0", "1.0", "7"]),
+        Q.BoundDimFilter("sumLongSequential", "12", "3", ordering="lexicographic"),
+        Q.AndDimFilter([Q.BoundDimFilter("maxLongUniform", None, "100", ordering="numeric"),
+                        Q.InDimFilter("dimZipf", ["1", "2", "3"])]),
+        Q.OrDimFilter([Q.SelectorDimFilter("minFloatZipf", "0.0"), Q.SelectorDimFilter("dimSequential", "7")]),
+        Q.NotDimFilter(Q.BoundDimFilter("__time", "100000", "900000", ordering="numeric")),
+    ]
+    aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal")]
+    iv = ["1970-01-01/2020-01-01"]
+    for f in filters:
+        for q in (Q.TimeseriesQuery(intervals=iv, aggregations=aggs, filter=f),
+                  Q.TopNQuery(intervals=iv, dimension="dimZipf", metric="sumLongSequential", threshold=5,
+                              aggregations=aggs, filter=f),
+                  Q.GroupByQuery(intervals=iv, dimensions=["dimZipf"], aggregations=aggs, filter=f)):
+            assert_results(q, R.run_query(q, g), O.run(q, o))
