@@ -237,6 +237,9 @@ class FilterProgram:
             # dictionaries of the segments of this call, the engine unions the matching values' bitmaps
             if self.segments is None:
                 raise UnsupportedQuery(2, f"filter {type(f).__name__} needs the segments' dictionaries")
+            if any(s.column_type(f.dimension) in (COL_LONG, COL_FLOAT, COL_DOUBLE) for s in self.segments):
+                # over String.valueOf(number) of every row: no dictionary to evaluate it on
+                raise UnsupportedQuery(2, f"filter {type(f).__name__} on numeric column {f.dimension}")
             vals = predicate_values(f, self.segments, Q)
             node.kind = F_IN
             node.values = self._strs(vals)

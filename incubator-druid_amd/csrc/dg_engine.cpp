@@ -2847,12 +2847,14 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * rec * 8));
   if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "groupBy result of %lld groups", (long long)ng);
   if (ng > 0) {
-    uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)ng + 16);
-    const size_t nthr = (size_t)sb.ntiles_sort * 256;
-    int64_t* carry_g = dev_take<int64_t>(cs, nthr);
-    int64_t* open_g = dev_take<int64_t>(cs, nthr);
-    uint64_t* carry_slots = dev_take<uint64_t>(cs, nthr * rec);
-    if (!head_pos || !carry_g || !open_g || !carry_slots) return set_error(DG_ERR_OOM, "groupBy reduce scratch");
+    // run heads are only needed by the floatSum row-order pass
+    uint32_t* head_pos = has_float_sum(plan) ? dev_take<uint32_t>(cs, (size_t)ng + 16) : nullptr;
+    const size_t nt = (size_t)sb.ntiles_sort;  // one carry / open group per tile
+    int64_t* carry_g = dev_take<int64_t>(cs, nt);
+    int64_t* open_g = dev_take<int64_t>(cs, nt);
+    uint64_t* carry_slots = dev_take<uint64_t>(cs, nt * rec);
+    if ((has_float_sum(plan) && !head_pos) || !carry_g || !open_g || !carry_slots)
+      return set_error(DG_ERR_OOM, "groupBy reduce scratch");
     launch_gb_reduce(d_jobs, n, &sb, plan, res->keys, res->slots, head_pos, carry_g, carry_slots, open_g, st);
     for (int a = 0; a < na; ++a)
       if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, &sb, plan, a, head_pos, res->slots, st);

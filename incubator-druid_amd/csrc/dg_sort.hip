@@ -422,11 +422,30 @@ __device__ __forceinline__ uint64_t finalize_dev(int kind, uint64_t s) {
 // groupBy reduce: the merged grouper's records (AggregatorFactory.combine semantics across segments
 // = the per-row aggregate ops, both exact for counts / long sums / min / max)
 // ------------------------------------------------------------------------------------------------
-// A thread owns kSPT consecutive sorted elements. A group whose head and end both lie in one thread
-// is written finalized (ABI encoding) by that thread. A group crossing a thread boundary is written
-// by its head's thread in the device encoding (open_g), later threads send their partials to carry
-// slots; k_gb_carry folds the carries in and k_gb_open_finalize finalizes the open groups.
-// floatSum slots are left to k_fsum_runs.
+// Reduce-by-key over a tile of kSortTile sorted elements, processed as 16 chunks of 256 consecutive
+// elements (lane = element): a segmented scan per chunk (wave shuffles, then the 4 waves' carries
+// through LDS, then the chunk's open run carried into the next chunk). The element that ends a run
+// writes its group's slot, so a wave's stores go to consecutive groups. A group that starts in the
+// tile and ends there is written finalized (ABI encoding); the tile's last group, if it continues,
+// is written in the device encoding and listed in open_g; the tile's leading part of a group that
+// started in an earlier tile goes to the tile's carry slot. k_gb_carry folds the carries in,
+// k_gb_open_finalize finalizes the open groups. floatSum slots are left to k_fsum_runs.
+__device__ __forceinline__ uint64_t seg_scan_wave(int op, uint64_t v, bool head, bool* any_head) {
+  const int lane = threadIdx.x & 63;
+  bool f = head;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(v, o, 64);
+    const int fy = __shfl_up((int)f, o, 64);
+    if (lane >= o) {
+      if (!f) v = combine_op(op, y, v);
+      f = f || fy;
+    }
+  }
+  *any_head = f;
+  return v;
+}
+
 template <bool REFS>
 __global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ jobs, int njobs,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
@@ -435,121 +454,135 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ job
                                                    uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_slots,
                                                    uint32_t* __restrict__ head_pos, int64_t* __restrict__ carry_g,
                                                    uint64_t* __restrict__ carry_slots, int64_t* __restrict__ open_g) {
-  // tile in LDS, one pad word per 16 elements (a thread reads its 16 consecutive elements; without
-  // the pad the 64 lanes' rows of 128 bytes would all start on one bank)
-  __shared__ uint64_t s_key[kSortTile + kSortTile / 16];
-  __shared__ uint32_t s_ref[kSortTile + kSortTile / 16];
+  __shared__ uint64_t s_key[kSortTile + 2];  // [0] = element before the tile, [1 + x] = element x
+  __shared__ uint32_t s_ref[kSortTile];
   __shared__ uint32_t s_base[kMaxCallSegs];
   __shared__ uint32_t s_tmp[4];
-  __shared__ uint64_t s_edge[2];  // keys of the elements just before and just after the tile
+  __shared__ uint64_t s_wv[4];
+  __shared__ int s_wf[4];
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  const int64_t gt = (int64_t)blockIdx.x * kST + threadIdx.x;
-  carry_g[gt] = -1;
-  open_g[gt] = -1;
-  if (base >= n) return;
-  const int tid = threadIdx.x;
-  const uint64_t kmask = kshift ? ((1ull << kshift) - 1ull) : 0ull;
-  for (int x = tid; x < kSortTile; x += kST) {
-    const int64_t i = base + x;
-    const uint64_t w = i < n ? keys[i] : 0ull;
-    const int px = x + (x >> 4);
-    s_key[px] = w >> kshift;
-    s_ref[px] = REFS ? (i < n ? refs[i] : 0u) : (uint32_t)(w & kmask);
-  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) {
-    s_edge[0] = base > 0 ? keys[base - 1] >> kshift : ~(keys[0] >> kshift);
-    s_edge[1] = base + kSortTile < n ? keys[base + kSortTile] >> kshift : 0ull;
+    carry_g[blockIdx.x] = -1;
+    open_g[blockIdx.x] = -1;
+  }
+  if (base >= n) return;
+  const int tile_n = (int)min<int64_t>(kSortTile, (int64_t)n - base);
+  const uint64_t kmask = kshift ? ((1ull << kshift) - 1ull) : 0ull;
+  for (int x = tid; x < tile_n; x += kST) {
+    const uint64_t w = keys[base + x];
+    s_key[1 + x] = w >> kshift;
+    s_ref[x] = REFS ? refs[base + x] : (uint32_t)(w & kmask);
+  }
+  const bool has_next = base + kSortTile < n;
+  if (tid == 0) {
+    s_key[0] = base > 0 ? keys[base - 1] >> kshift : ~(keys[0] >> kshift);
+    if (has_next) s_key[1 + kSortTile] = keys[base + kSortTile] >> kshift;
   }
   for (int x = tid; x < njobs; x += kST) s_base[x] = jobs[x].row_base;
   __syncthreads();
-  const int na = plan.n;
-  const int x0 = tid * kSPT;
-  const int m = (int)max<int64_t>(0, min<int64_t>(kSPT, (int64_t)n - base - x0));
-  uint64_t kr[kSPT];
-#pragma unroll
-  for (int q = 0; q < kSPT; ++q) kr[q] = s_key[tid * 17 + q];
-  const uint64_t prev = tid > 0 ? s_key[tid * 17 - 2] : s_edge[0];  // element x0 - 1 (last of thread tid - 1)
-  uint32_t h = 0;
-#pragma unroll
-  for (int q = 0; q < kSPT; ++q)
-    if (q < m && kr[q] != (q ? kr[q - 1] : prev)) h |= 1u << q;
-  // does the element after my range start a new group (or is there none)?
-  bool next_head = true;
-  if (m == kSPT && base + x0 + kSPT < n) {
-    const uint64_t nk = tid + 1 < kST ? s_key[(tid + 1) * 17] : s_edge[1];
-    next_head = nk != kr[kSPT - 1];
-  }
-  uint32_t tot;
-  const uint32_t ex = block_scan_u32<kST>((uint32_t)__popc(h), &tot, s_tmp);
-  if (m == 0) return;
-  // group of the thread's first element: the next head's index, or the open group before it
-  const int64_t g0 = (int64_t)run_off[blockIdx.x] + ex - ((h & 1u) ? 0 : 1);
-  const bool owner0 = h & 1u;
-  const int rec = na + 1;
-  // the thread's elements: (segment, row) of each, keys and run heads
+  const int na = plan.n, rec = na + 1;
+  const int64_t G0 = run_off[blockIdx.x];  // groups whose head lies in an earlier tile
+  // per element (chunk c, lane): run head / run end flags, group index (relative: -1 = the group
+  // carried in from an earlier tile), (segment, row) of its row ref
+  uint32_t hm = 0, tm = 0;
+  int32_t grel[kSPT];
   int seg_of[kSPT];
   int32_t row_of[kSPT];
-  {
-    int64_t g = g0;
+  int heads = 0;  // heads of the tile in the chunks before
 #pragma unroll
-    for (int q = 0; q < kSPT; ++q) {
-      const uint32_t ref = s_ref[tid * 17 + q];
-      const int seg = locate_seg(s_base, njobs, ref);
-      seg_of[q] = seg;
-      row_of[q] = (int32_t)(ref - s_base[seg]);
-      if (q < m && ((h >> q) & 1u)) {
-        if (q > 0) g++;
-        head_pos[g] = (uint32_t)(base + x0 + q);
-        out_keys[g] = kr[q];
-      }
+  for (int c = 0; c < kSPT; ++c) {
+    const int x = c * kST + tid;
+    const bool valid = x < tile_n;
+    const uint64_t k = s_key[1 + x];
+    const bool h = valid && k != s_key[x];
+    bool t = false;
+    if (valid) t = x + 1 < tile_n ? s_key[2 + x] != k : (!has_next || s_key[1 + kSortTile] != k);
+    hm |= (uint32_t)h << c;
+    tm |= (uint32_t)t << c;
+    uint32_t tot;
+    const uint32_t ex = block_scan_u32<kST>(h ? 1u : 0u, &tot, s_tmp);
+    grel[c] = heads + (int)ex + (h ? 1 : 0) - 1;
+    heads += (int)tot;
+    const uint32_t ref = s_ref[valid ? x : 0];
+    const int seg = locate_seg(s_base, njobs, ref);
+    seg_of[c] = seg;
+    row_of[c] = (int32_t)(ref - s_base[seg]);
+    if (h) {
+      out_keys[G0 + grel[c]] = k;
+      if (head_pos) head_pos[G0 + grel[c]] = (uint32_t)(base + x);
     }
   }
-  // one slot at a time: the thread's m inputs are loaded first (independent random loads in flight
-  // together), then folded along the runs. Slot -1 = rows aggregated (count of the run's elements).
-  if (!owner0) carry_g[gt] = g0;
+  __syncthreads();  // the keys and refs are consumed: their LDS now holds inputs / group indices
+  uint64_t* s_x = s_key;            // [x] = the current slot's input of element x
+  int32_t* s_g = reinterpret_cast<int32_t*>(s_ref);  // [x] = relative group index of element x
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) s_g[c * kST + tid] = grel[c];
+  // one slot at a time (-1 = rows aggregated): the 16 inputs are gathered first (independent random
+  // loads in flight together), then scanned chunk by chunk
   for (int a = -1; a < na; ++a) {
     const int kind = a < 0 ? DG_AGG_COUNT : plan.kind[a];
     if (kind == DG_AGG_FLOAT_SUM) continue;  // k_fsum_runs: float32 in row order
     const int op = a < 0 ? (int)OP_ADD_I64 : plan.op[a];
-    uint64_t x[kSPT];
-#pragma unroll
-    for (int q = 0; q < kSPT; ++q) x[q] = (a < 0 || q >= m) ? 1ull : agg_in(jobs[seg_of[q]], plan, a, row_of[q]);
     const uint64_t ident = a < 0 ? 0ull : identity_of(op, kind);
-    uint64_t acc = ident;
-    int64_t g = g0;
-    bool own = owner0;
+    {
+      uint64_t xv[kSPT];
 #pragma unroll
-    for (int q = 0; q < kSPT; ++q) {
-      if (q >= m) continue;
-      if (q > 0 && ((h >> q) & 1u)) {  // the previous group ended inside my range: complete
-        if (own) out_slots[g * rec + 1 + a] = finalize_dev(kind, acc);
-        else carry_slots[gt * rec + 1 + a] = acc;
-        g++;
-        own = true;
-        acc = ident;
+      for (int c = 0; c < kSPT; ++c) {
+        const bool valid = c * kST + tid < tile_n;
+        xv[c] = !valid ? ident : (a < 0 ? 1ull : agg_in(jobs[seg_of[c]], plan, a, row_of[c]));
       }
-      acc = combine_op(op, acc, x[q]);
+#pragma unroll
+      for (int c = 0; c < kSPT; ++c) s_x[c * kST + tid] = xv[c];
     }
-    if (own) out_slots[g * rec + 1 + a] = next_head ? finalize_dev(kind, acc) : acc;
-    else carry_slots[gt * rec + 1 + a] = acc;  // a range with no head: the whole range is one carry
-  }
-  if (!next_head) {
-    // my last group continues into the next thread: written (by me if I own it) in the device
-    // encoding, finalized after the carries
-    const int64_t glast = g0 + __popc(h & ~1u);
-    const bool own_last = owner0 || (h & ~1u);
-    if (own_last) open_g[gt] = glast;
+    uint64_t run = ident;  // value of the run open at the end of the previous chunk
+#pragma unroll 1
+    for (int c = 0; c < kSPT; ++c) {
+      const int x = c * kST + tid;
+      bool f;
+      uint64_t v = seg_scan_wave(op, s_x[x], (hm >> c) & 1u, &f);
+      if (lane == 63) {
+        s_wv[wave] = v;
+        s_wf[wave] = f;
+      }
+      __syncthreads();
+      uint64_t pre = run;  // what precedes my wave in the open run
+      uint64_t all = run;  // the open run at the end of the chunk
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint64_t wv = s_wv[w];
+        const uint64_t nx = s_wf[w] ? wv : combine_op(op, all, wv);
+        if (w < wave) pre = nx;
+        all = nx;
+      }
+      __syncthreads();
+      if (!f) v = combine_op(op, pre, v);
+      run = all;
+      if (x < tile_n) {
+        const bool t = (tm >> c) & 1u;
+        const int32_t gr = s_g[x];
+        if (t || x == tile_n - 1) {
+          if (gr >= 0) {  // a group of this tile: complete, or open at the tile's end
+            out_slots[(G0 + gr) * rec + 1 + a] = t ? finalize_dev(kind, v) : v;
+            if (!t) open_g[blockIdx.x] = G0 + gr;
+          } else {  // the tile's share of a group that began earlier
+            carry_slots[(int64_t)blockIdx.x * rec + 1 + a] = v;
+            carry_g[blockIdx.x] = G0 - 1;
+          }
+        }
+      }
+    }
   }
 }
 
-// carried partials -> their group's record: equal groups are consecutive, so one segmented combine
-// per wave and one atomic per (wave, group, slot)
+// carried partials (one per tile) -> their group's record: equal groups are consecutive, so one
+// segmented combine per wave and one atomic per (wave, group, slot)
 __global__ __launch_bounds__(256) void k_gb_carry(const int64_t* __restrict__ carry_g, const uint64_t* __restrict__ carry_slots,
-                                                  int64_t nthreads, AggPlan plan, uint64_t* __restrict__ out_slots) {
+                                                  int64_t ncarry, AggPlan plan, uint64_t* __restrict__ out_slots) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  const int64_t g = t < nthreads ? carry_g[t] : -1;
+  const int64_t g = t < ncarry ? carry_g[t] : -1;
   if (__ballot(g >= 0) == 0) return;
   const int64_t gnext = __shfl_down(g, 1, 64);
   const bool tail = lane == 63 || gnext != g;
@@ -569,10 +602,10 @@ __global__ __launch_bounds__(256) void k_gb_carry(const int64_t* __restrict__ ca
   }
 }
 
-__global__ __launch_bounds__(256) void k_gb_open_finalize(const int64_t* __restrict__ open_g, int64_t nthreads, AggPlan plan,
+__global__ __launch_bounds__(256) void k_gb_open_finalize(const int64_t* __restrict__ open_g, int64_t nopen, AggPlan plan,
                                                           uint64_t* __restrict__ out_slots) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t g = t < nthreads ? open_g[t] : -1;
+  const int64_t g = t < nopen ? open_g[t] : -1;
   if (g < 0) return;
   const int rec = plan.n + 1;
   for (int a = 0; a < plan.n; ++a)
@@ -590,8 +623,9 @@ void launch_gb_reduce(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan
   else
     hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kST), 0, s, d_jobs, njobs, sb->keys[sb->cur], refs, sb->ref_bits,
                        sb->n, sb->run_cnt, plan, out_keys, out_slots, head_pos, carry_g, carry_slots, open_g);
-  hipLaunchKernelGGL(k_gb_carry, dim3(nt), dim3(256), 0, s, carry_g, carry_slots, (int64_t)nt * kST, plan, out_slots);
-  hipLaunchKernelGGL(k_gb_open_finalize, dim3(nt), dim3(256), 0, s, open_g, (int64_t)nt * kST, plan, out_slots);
+  const unsigned g = (unsigned)((nt + 255) / 256);
+  hipLaunchKernelGGL(k_gb_carry, dim3(g), dim3(256), 0, s, carry_g, carry_slots, (int64_t)nt, plan, out_slots);
+  hipLaunchKernelGGL(k_gb_open_finalize, dim3(g), dim3(256), 0, s, open_g, (int64_t)nt, plan, out_slots);
 }
 
 // ------------------------------------------------------------------------------------------------
