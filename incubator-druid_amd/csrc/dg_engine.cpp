@@ -1405,7 +1405,7 @@ static bool has_float_sum(const AggPlan& plan) {
 
 // device buffers of a sort-based grouping of at most `cap` rows with keys of key_bits bits (call
 // scratch): one 8-byte word per element [key | row ref] when both fit, else keys + a u32 ref array
-static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bits, SortBufs* sb) {
+static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bits, int pw, SortBufs* sb) {
   memset(sb, 0, sizeof *sb);
   sb->cap = cap;
   sb->ntiles_sort = sort_tiles(cap);
@@ -1417,6 +1417,11 @@ static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bi
     sb->keys[k] = dev_take<uint64_t>(cs, c);
     sb->refs[k] = packed ? nullptr : dev_take<uint32_t>(cs, c);
     if (!sb->keys[k] || (!packed && !sb->refs[k])) return set_error(DG_ERR_OOM, "sort buffers of %lld rows", (long long)cap);
+  }
+  sb->pw = pw;
+  if (pw > 0) {
+    sb->payload = dev_take<uint64_t>(cs, c * (size_t)pw);
+    if (!sb->payload) return set_error(DG_ERR_OOM, "payload of %lld rows", (long long)cap);
   }
   sb->tile_cnt = dev_take<uint32_t>(cs, (size_t)std::max(ntiles_keygen, 1));
   sb->n = dev_take<uint32_t>(cs, 4);
@@ -1463,17 +1468,18 @@ static int fsum_pass(CallScratch* cs, std::vector<GbJob>& gj, const std::vector<
   int rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
   if (rc) return rc;
   SortBufs sb;
-  rc = sort_bufs(cs, total, ntiles, key_bits, &sb);
+  rc = sort_bufs(cs, total, ntiles, key_bits, plan.n, &sb);
   if (rc) return rc;
   uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)total + 16);
   if (!head_pos) return set_error(DG_ERR_OOM, "floatSum runs");
   DG_FLUSH(cs, st);
-  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, st);
+  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st);
   if (sort) launch_radix_sort(&sb, key_bits, st);
   launch_run_heads(&sb, st);
   launch_run_mark(&sb, head_pos, st);
   for (int a = 0; a < plan.n; ++a)
-    if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, (int)gj.size(), &sb, plan, a, head_pos, nullptr, st);
+    if (plan.kind[a] == DG_AGG_FLOAT_SUM)
+      launch_fsum_runs(d_jobs, (int)gj.size(), ntiles, &sb, plan, a, head_pos, nullptr, 0, st);
   return DG_OK;
 }
 
@@ -2687,7 +2693,8 @@ struct dg_result {
   int ndims = 0, naggs = 0;
   int64_t ngroups = 0;
   uint64_t* keys = nullptr;   // [ngroups] packed keys, ascending
-  uint64_t* slots = nullptr;  // [ngroups][1 + naggs]: rows, then the ABI-encoded aggregate values
+  uint64_t* slots = nullptr;  // [1 + naggs][cap] (slot-major): rows, then the ABI-encoded aggregate values
+  int64_t cap = 0;
   dg::KeyLayout lay{};
   int64_t bucket0 = 0, period = 0, universal = 0;
   std::vector<std::shared_ptr<dg::MergedDict>> dicts;  // empty for a dg_merge result (cluster ids)
@@ -2817,13 +2824,13 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
   if (rc) return rc;
   SortBufs sb;
-  rc = sort_bufs(cs, total, ntiles, key_bits, &sb);
+  rc = sort_bufs(cs, total, ntiles, key_bits, na, &sb);
   if (rc) return rc;
   uint32_t* h_n = host_take<uint32_t>(cs, 4);
   if (!h_n) return set_error(DG_ERR_OOM, "groupBy counters");
   DG_FLUSH(cs, st);
   hipEventRecord(ctx->ev[3], st);
-  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, st);
+  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st);
   hipEventRecord(ctx->ev[5], st);
   launch_radix_sort(&sb, key_bits, st);
   hipEventRecord(ctx->ev[6], st);
@@ -2845,6 +2852,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   res->dicts = md;
   res->keys = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * 8));
   res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * rec * 8));
+  res->cap = ng;
   if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "groupBy result of %lld groups", (long long)ng);
   if (ng > 0) {
     // run heads are only needed by the floatSum row-order pass
@@ -2855,9 +2863,9 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     uint64_t* carry_slots = dev_take<uint64_t>(cs, nt * rec);
     if ((has_float_sum(plan) && !head_pos) || !carry_g || !open_g || !carry_slots)
       return set_error(DG_ERR_OOM, "groupBy reduce scratch");
-    launch_gb_reduce(d_jobs, n, &sb, plan, res->keys, res->slots, head_pos, carry_g, carry_slots, open_g, st);
+    launch_gb_reduce(&sb, plan, res->keys, res->slots, ng, head_pos, carry_g, carry_slots, open_g, st);
     for (int a = 0; a < na; ++a)
-      if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, &sb, plan, a, head_pos, res->slots, st);
+      if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, ntiles, &sb, plan, a, head_pos, res->slots, ng, st);
   }
   hipEventRecord(ctx->ev[4], st);
   rc = finish_call(cs, st);
@@ -2896,7 +2904,7 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
   CallGuard g(r->ctx);
   CallScratch* cs = g.cs;
   hipStream_t st = r->ctx->stream;
-  const int nd = r->ndims, rec = r->naggs + 1;
+  const int nd = r->ndims;
   if (bucket_time || ids) {
     int64_t* d_b = dev_take<int64_t>(cs, (size_t)count);
     int32_t* d_ids = dev_take<int32_t>(cs, (size_t)count * std::max(nd, 1));
@@ -2907,8 +2915,10 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
   }
   std::vector<uint64_t> tmp;
   if (values && r->naggs) {
-    tmp.resize((size_t)count * rec);
-    DG_HIP(hipMemcpyAsync(tmp.data(), r->slots + (size_t)start * rec, tmp.size() * 8, hipMemcpyDeviceToHost, st));
+    tmp.resize((size_t)count * r->naggs);
+    for (int a = 0; a < r->naggs; ++a)
+      DG_HIP(hipMemcpyAsync(tmp.data() + (size_t)a * count, r->slots + (size_t)(1 + a) * r->cap + start, (size_t)count * 8,
+                            hipMemcpyDeviceToHost, st));
   }
   int rc = finish_call(cs, st);
   if (rc) return rc;
@@ -2916,7 +2926,8 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
     for (int64_t i = 0; i < count; ++i)
       bucket_time[i] = r->period ? r->bucket0 + bucket_time[i] * r->period : r->universal;
   if (values && r->naggs)
-    for (int64_t i = 0; i < count; ++i) memcpy(values + i * r->naggs, tmp.data() + i * rec + 1, 8 * (size_t)r->naggs);
+    for (int64_t i = 0; i < count; ++i)
+      for (int a = 0; a < r->naggs; ++a) values[i * r->naggs + a] = tmp[(size_t)a * count + i];
   return DG_OK;
 }
 
@@ -2924,9 +2935,7 @@ int dg_result_fetch_rows(dg_result* r, int64_t start, int64_t count, int64_t* ro
   if (!r || !rows || start < 0 || count < 0 || start + count > r->ngroups) return set_error(DG_ERR_ARG, "bad result range");
   if (count == 0) return DG_OK;
   CallGuard g(r->ctx);
-  const int rec = r->naggs + 1;
-  DG_HIP(hipMemcpy2DAsync(rows, 8, r->slots + (size_t)start * rec, 8 * (size_t)rec, 8, (size_t)count,
-                          hipMemcpyDeviceToHost, r->ctx->stream));
+  DG_HIP(hipMemcpyAsync(rows, r->slots + start, (size_t)count * 8, hipMemcpyDeviceToHost, r->ctx->stream));
   return finish_call(g.cs, r->ctx->stream);
 }
 
@@ -3035,7 +3044,7 @@ int dg_result_export(dg_result* r, const dg_keyspace* ks, const int32_t* const* 
   }
   DG_FLUSH(cs, st);
   launch_gb_rekey(r->keys, r->ngroups, r->lay, lay, bucket_delta, rm, d_keys, st);
-  DG_HIP(hipMemcpyAsync(d_slots, r->slots, (size_t)r->ngroups * (r->naggs + 1) * 8, hipMemcpyDeviceToDevice, st));
+  launch_soa_to_aos(r->slots, r->cap, r->ngroups, r->naggs + 1, d_slots, st);
   if (ks->period_ms) {  // the last group holds the largest bucket index
     uint64_t last = 0;
     DG_HIP(hipMemcpyAsync(&last, r->keys + r->ngroups - 1, 8, hipMemcpyDeviceToHost, st));
@@ -3101,7 +3110,7 @@ int dg_merge(dg_context* c, const dg_keyspace* ks, const uint64_t* d_keys, const
   int64_t ng = 0;
   if (n > 0) {
     SortBufs sb;
-    rc = sort_bufs(cs, n, 1, key_bits, &sb);
+    rc = sort_bufs(cs, n, 1, key_bits, 0, &sb);
     if (rc) return rc;
     uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)n + 16);
     uint32_t* h_n = host_take<uint32_t>(cs, 4);
@@ -3109,6 +3118,7 @@ int dg_merge(dg_context* c, const dg_keyspace* ks, const uint64_t* d_keys, const
     // groups <= records: the result is sized by the input (no second pass over the groups)
     res->keys = static_cast<uint64_t*>(result_alloc(ctx, (size_t)n * 8));
     res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)n * rec * 8));
+    res->cap = n;
     if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "merged result of %lld records", (long long)n);
     hipEventRecord(ctx->ev[3], st);
     launch_merge_load(d_keys, n, &sb, st);

@@ -142,7 +142,9 @@ struct GbJob {
 struct SortBufs {
   uint64_t* keys[2];      // packed (refs null): [key | row ref in the low ref_bits bits]; else keys
   uint32_t* refs[2];      // row refs when the key and the ref do not fit one word, else null
-  int ref_bits;           // packed: bits of the row ref (the sort key starts there); else 0
+  int ref_bits;           // packed: bits of the element index (the sort key starts there); else 0
+  uint64_t* payload;      // [cap][pw]: the aggregators' inputs of each element (device slot encoding)
+  int pw;
   int cur;                // which of the ping-pong buffers holds the result
   uint32_t* tile_cnt;     // keygen tiles: selected rows, then their offsets
   uint32_t* n;            // [0] selected rows, [1] groups
@@ -380,29 +382,32 @@ constexpr int kTileRows = 2048;
 constexpr int kSortTile = 4096;  // elements per radix / run tile (256 threads x 16)
 constexpr int kMaxCallSegs = 1024;  // segments of one sort-based call (row-ref bases live in LDS)
 inline int sort_tiles(int64_t n) { return (int)std::max<int64_t>(1, (n + kSortTile - 1) / kSortTile); }
-// selected rows -> (key, ref) in (segment, row) order; sb->n[0] = selected rows
-void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, hipStream_t s);
+// selected rows -> (key, element index) in (segment, row) order + their aggregator inputs in
+// sb->payload; sb->n[0] = selected rows
+void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
+                      hipStream_t s);
 // stable LSD radix sort of sb->keys/refs[cur] on key bits [0, key_bits)
 void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s);
 // run heads of the sorted keys: sb->run_cnt = per-tile offsets, sb->n[1] = runs
 void launch_run_heads(SortBufs* sb, hipStream_t s);
 // head_pos[g] = first sorted element of run g (after launch_run_heads)
 void launch_run_mark(SortBufs* sb, uint32_t* head_pos, hipStream_t s);
-// groupBy merge of the sorted rows: one record per run (out_keys[g], out_slots[g][1 + naggs] in the
-// ABI slot encoding), head_pos[g] = first sorted element of run g; floatSum slots are left to
-// launch_fsum_runs. carry: scratch of sort_tiles(cap) * 256 entries (g) and * (1 + naggs) slots.
-// open_g: scratch like carry_g (groups written in the device encoding, finalized after the carries)
-void launch_gb_reduce(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, uint64_t* out_keys,
-                      uint64_t* out_slots, uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, int64_t* open_g,
-                      hipStream_t s);
+// groupBy merge of the sorted rows: one record per run, out_keys[g] and slot s of group g at
+// out_slots[s * cap + g] (SoA) in the ABI slot encoding; head_pos (null unless a floatSum needs it)
+// = first sorted element of run g; floatSum slots are left to launch_fsum_runs. carry_g / open_g:
+// sort_tiles(cap) entries, carry_slots: sort_tiles(cap) * (1 + naggs).
+void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* out_slots, int64_t cap,
+                      uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, int64_t* open_g, hipStream_t s);
 // floatSum aggregator `agg` as the reference computes it: a float32 sum in row order per run and
 // segment (FloatSumBufferAggregator.aggregate), segments combined in order with float adds
-// (FloatSumAggregator.combine). groupBy: into out_slots[g][1 + agg]; per-segment engines
-// (out_slots == null): into the job's fs_out table. head_pos null: runs found by a linear scan.
-void launch_fsum_runs(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, int agg, const uint32_t* head_pos,
-                      uint64_t* out_slots, hipStream_t s);
-// device slot encoding -> ABI encoding (finalize) for n records
+// (FloatSumAggregator.combine). groupBy: into out_slots[(1 + agg) * cap + g]; per-segment engines
+// (out_slots == null): into the job's fs_out table.
+void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, AggPlan plan, int agg,
+                      const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s);
+// device slot encoding -> ABI encoding (finalize) of the aggregator slots [1 + a][cap] of n_ptr[0] groups
 void launch_slots_finalize(uint64_t* slots, const uint32_t* n_ptr, int64_t cap, AggPlan plan, hipStream_t s);
+// SoA slots [rec][cap] -> AoS records [n][rec]
+void launch_soa_to_aos(const uint64_t* soa, int64_t cap, int64_t n, int rec, uint64_t* aos, hipStream_t s);
 // groups [start, start + count): key fields -> bucket index and merged ids (int32 per dimension)
 struct KeyLayout {
   int32_t ndims;
@@ -421,7 +426,8 @@ void launch_gb_rekey(const uint64_t* in, int64_t n, KeyLayout lin, KeyLayout lou
 void launch_lower_bound(const uint64_t* keys, int64_t n, const uint64_t* split, int nsplit, int64_t* pos, hipStream_t s);
 // sort input of a merge (refs = record index, sb->n[0] = n)
 void launch_merge_load(const uint64_t* keys, int64_t n, SortBufs* sb, hipStream_t s);
-// one record per run of the sorted merge input, partial values combined in order (device encoding)
+// one record per run of the sorted merge input, partial values combined in order (device encoding,
+// SoA slots [rec][cap])
 void launch_merge_reduce(SortBufs* sb, const uint32_t* head_pos, const uint64_t* in_slots, AggPlan plan, int64_t cap,
                          uint64_t* out_keys, uint64_t* out_slots, hipStream_t s);
 

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ a, int
   if (threadIdx.x == 0) *total = carry;
 }
 
-// segment of a row ref: last job whose row_base <= ref (bases ascend)
+// segment of an element index (or row ref): the last job whose base <= it (bases ascend)
 __device__ __forceinline__ int locate_seg(const uint32_t* s_base, int njobs, uint32_t ref) {
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
@@ -145,9 +145,15 @@ __device__ __forceinline__ uint32_t elem_ref(uint64_t w, const uint32_t* refs, i
   return refs ? refs[i] : (uint32_t)(w & ((1ull << kshift) - 1ull));
 }
 
+// Selected rows in (segment, row) order get consecutive element indices; the element's sort word
+// carries its index (packed) or the ref array does. The aggregators' inputs of the element are
+// written at payload[index * pw] in the device slot encoding, in row order (coalesced column reads),
+// so the reduce after the sort gathers one payload record per element instead of one random read
+// per column.
 __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                    const uint32_t* __restrict__ offs, uint64_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ refs, int kshift) {
+                                                   uint32_t* __restrict__ refs, int kshift, AggPlan plan,
+                                                   uint64_t* __restrict__ payload, int pw) {
   __shared__ uint32_t s_tmp[4];
   const GbJob& j = jobs[tile_job[blockIdx.x]];
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
@@ -160,27 +166,29 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
     uint32_t tot;
     const uint32_t ex = block_scan_u32<256>(sel ? 1u : 0u, &tot, s_tmp);
     if (sel) {
-      const uint32_t ref = j.row_base + (uint32_t)r;
+      const uint32_t idx = base + ex;
       if (refs) {
-        keys[base + ex] = gb_key(j, r, b);
-        refs[base + ex] = ref;
+        keys[idx] = gb_key(j, r, b);
+        refs[idx] = idx;
       } else {
-        keys[base + ex] = (gb_key(j, r, b) << kshift) | ref;
+        keys[idx] = (gb_key(j, r, b) << kshift) | idx;
       }
+      for (int a = 0; a < pw; ++a) payload[(size_t)idx * pw + a] = agg_in(j, plan, a, r);
     }
     base += tot;
   }
 }
 
-void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, hipStream_t s) {
+void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
+                      hipStream_t s) {
   if (ntiles <= 0) {
-    hipMemsetAsync(sb->n, 0, 4, s);
+    (void)hipMemsetAsync(sb->n, 0, 4, s);
     return;
   }
   hipLaunchKernelGGL(k_gb_count, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt);
   hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, sb->tile_cnt, ntiles, sb->n);
   hipLaunchKernelGGL(k_gb_keygen, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits);
+                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -447,16 +455,16 @@ __device__ __forceinline__ uint64_t seg_scan_wave(int op, uint64_t v, bool head,
 }
 
 template <bool REFS>
-__global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ jobs, int njobs,
+__global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ run_off, AggPlan plan,
                                                    uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_slots,
-                                                   uint32_t* __restrict__ head_pos, int64_t* __restrict__ carry_g,
-                                                   uint64_t* __restrict__ carry_slots, int64_t* __restrict__ open_g) {
+                                                   int64_t cap, uint32_t* __restrict__ head_pos,
+                                                   int64_t* __restrict__ carry_g, uint64_t* __restrict__ carry_slots,
+                                                   int64_t* __restrict__ open_g) {
   __shared__ uint64_t s_key[kSortTile + 2];  // [0] = element before the tile, [1 + x] = element x
   __shared__ uint32_t s_ref[kSortTile];
-  __shared__ uint32_t s_base[kMaxCallSegs];
   __shared__ uint32_t s_tmp[4];
   __shared__ uint64_t s_wv[4];
   __shared__ int s_wf[4];
@@ -480,16 +488,14 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ job
     s_key[0] = base > 0 ? keys[base - 1] >> kshift : ~(keys[0] >> kshift);
     if (has_next) s_key[1 + kSortTile] = keys[base + kSortTile] >> kshift;
   }
-  for (int x = tid; x < njobs; x += kST) s_base[x] = jobs[x].row_base;
   __syncthreads();
   const int na = plan.n, rec = na + 1;
   const int64_t G0 = run_off[blockIdx.x];  // groups whose head lies in an earlier tile
   // per element (chunk c, lane): run head / run end flags, group index (relative: -1 = the group
-  // carried in from an earlier tile), (segment, row) of its row ref
+  // carried in from an earlier tile), payload index
   uint32_t hm = 0, tm = 0;
   int32_t grel[kSPT];
-  int seg_of[kSPT];
-  int32_t row_of[kSPT];
+  uint32_t idx_of[kSPT];
   int heads = 0;  // heads of the tile in the chunks before
 #pragma unroll
   for (int c = 0; c < kSPT; ++c) {
@@ -505,10 +511,7 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ job
     const uint32_t ex = block_scan_u32<kST>(h ? 1u : 0u, &tot, s_tmp);
     grel[c] = heads + (int)ex + (h ? 1 : 0) - 1;
     heads += (int)tot;
-    const uint32_t ref = s_ref[valid ? x : 0];
-    const int seg = locate_seg(s_base, njobs, ref);
-    seg_of[c] = seg;
-    row_of[c] = (int32_t)(ref - s_base[seg]);
+    idx_of[c] = s_ref[valid ? x : 0];
     if (h) {
       out_keys[G0 + grel[c]] = k;
       if (head_pos) head_pos[G0 + grel[c]] = (uint32_t)(base + x);
@@ -531,7 +534,7 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ job
 #pragma unroll
       for (int c = 0; c < kSPT; ++c) {
         const bool valid = c * kST + tid < tile_n;
-        xv[c] = !valid ? ident : (a < 0 ? 1ull : agg_in(jobs[seg_of[c]], plan, a, row_of[c]));
+        xv[c] = !valid ? ident : (a < 0 ? 1ull : payload[(size_t)idx_of[c] * pw + a]);
       }
 #pragma unroll
       for (int c = 0; c < kSPT; ++c) s_x[c * kST + tid] = xv[c];
@@ -564,7 +567,7 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ job
         const int32_t gr = s_g[x];
         if (t || x == tile_n - 1) {
           if (gr >= 0) {  // a group of this tile: complete, or open at the tile's end
-            out_slots[(G0 + gr) * rec + 1 + a] = t ? finalize_dev(kind, v) : v;
+            out_slots[(1 + a) * cap + G0 + gr] = t ? finalize_dev(kind, v) : v;
             if (!t) open_g[blockIdx.x] = G0 + gr;
           } else {  // the tile's share of a group that began earlier
             carry_slots[(int64_t)blockIdx.x * rec + 1 + a] = v;
@@ -579,7 +582,8 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const GbJob* __restrict__ job
 // carried partials (one per tile) -> their group's record: equal groups are consecutive, so one
 // segmented combine per wave and one atomic per (wave, group, slot)
 __global__ __launch_bounds__(256) void k_gb_carry(const int64_t* __restrict__ carry_g, const uint64_t* __restrict__ carry_slots,
-                                                  int64_t ncarry, AggPlan plan, uint64_t* __restrict__ out_slots) {
+                                                  int64_t ncarry, AggPlan plan, uint64_t* __restrict__ out_slots,
+                                                  int64_t cap) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t g = t < ncarry ? carry_g[t] : -1;
@@ -598,34 +602,34 @@ __global__ __launch_bounds__(256) void k_gb_carry(const int64_t* __restrict__ ca
       const int64_t gy = __shfl_up(g, o, 64);
       if (lane >= o && gy == g) v = combine_op(op, y, v);
     }
-    if (g >= 0 && tail) atomic_op(op, out_slots + g * rec + s, v);
+    if (g >= 0 && tail) atomic_op(op, out_slots + s * cap + g, v);
   }
 }
 
 __global__ __launch_bounds__(256) void k_gb_open_finalize(const int64_t* __restrict__ open_g, int64_t nopen, AggPlan plan,
-                                                          uint64_t* __restrict__ out_slots) {
+                                                          uint64_t* __restrict__ out_slots, int64_t cap) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t g = t < nopen ? open_g[t] : -1;
   if (g < 0) return;
-  const int rec = plan.n + 1;
   for (int a = 0; a < plan.n; ++a)
-    if (plan.kind[a] != DG_AGG_FLOAT_SUM) out_slots[g * rec + 1 + a] = finalize_dev(plan.kind[a], out_slots[g * rec + 1 + a]);
+    if (plan.kind[a] != DG_AGG_FLOAT_SUM) out_slots[(1 + a) * cap + g] = finalize_dev(plan.kind[a], out_slots[(1 + a) * cap + g]);
 }
 
-void launch_gb_reduce(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, uint64_t* out_keys,
-                      uint64_t* out_slots, uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, int64_t* open_g,
-                      hipStream_t s) {
+void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* out_slots, int64_t cap,
+                      uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, int64_t* open_g, hipStream_t s) {
   const int nt = sb->ntiles_sort;
   const uint32_t* refs = sb->refs[sb->cur];
   if (refs)
-    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kST), 0, s, d_jobs, njobs, sb->keys[sb->cur], refs, sb->ref_bits,
-                       sb->n, sb->run_cnt, plan, out_keys, out_slots, head_pos, carry_g, carry_slots, open_g);
+    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
+                       sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
+                       open_g);
   else
-    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kST), 0, s, d_jobs, njobs, sb->keys[sb->cur], refs, sb->ref_bits,
-                       sb->n, sb->run_cnt, plan, out_keys, out_slots, head_pos, carry_g, carry_slots, open_g);
+    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
+                       sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
+                       open_g);
   const unsigned g = (unsigned)((nt + 255) / 256);
-  hipLaunchKernelGGL(k_gb_carry, dim3(g), dim3(256), 0, s, carry_g, carry_slots, (int64_t)nt, plan, out_slots);
-  hipLaunchKernelGGL(k_gb_open_finalize, dim3(g), dim3(256), 0, s, open_g, (int64_t)nt, plan, out_slots);
+  hipLaunchKernelGGL(k_gb_carry, dim3(g), dim3(256), 0, s, carry_g, carry_slots, (int64_t)nt, plan, out_slots, cap);
+  hipLaunchKernelGGL(k_gb_open_finalize, dim3(g), dim3(256), 0, s, open_g, (int64_t)nt, plan, out_slots, cap);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -641,23 +645,28 @@ __device__ __forceinline__ float agg_float(const ColView& v, int64_t r) {
   return (float)*reinterpret_cast<const double*>(p);
 }
 
+// Element index -> segment: the last job whose first element index (its first keygen tile's offset)
+// is <= the index. Rows in an element's payload keep (segment, row) order, so the run's elements of
+// one segment are consecutive in it.
 __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ jobs, int njobs,
+                                                   const uint32_t* __restrict__ tile_off, int ntiles,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
-                                                   const uint32_t* __restrict__ head_pos, int rec, int agg,
-                                                   uint64_t* __restrict__ out_slots) {
+                                                   const uint32_t* __restrict__ head_pos, const uint64_t* __restrict__ payload,
+                                                   int pw, int agg, uint64_t* __restrict__ out_slots, int64_t cap,
+                                                   int rec) {
   __shared__ uint32_t s_base[kMaxCallSegs];
-  for (int x = threadIdx.x; x < njobs; x += 256) s_base[x] = jobs[x].row_base;
-  __syncthreads();
   const uint32_t n = n_ptr[0], ng = n_ptr[1];
+  for (int x = threadIdx.x; x < njobs; x += 256) s_base[x] = jobs[x].tile_begin < ntiles ? tile_off[jobs[x].tile_begin] : n;
+  __syncthreads();
   for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (int64_t)gridDim.x * 256) {
     const uint32_t i0 = head_pos[g], i1 = g + 1 < ng ? head_pos[g + 1] : n;
     float total = 0.0f, sum = 0.0f;
     int cur = -1;
     bool first = true;
     for (uint32_t i = i0; i < i1; ++i) {
-      const uint32_t ref = elem_ref(keys[i], refs, i, kshift);
-      const int seg = locate_seg(s_base, njobs, ref);
+      const uint32_t idx = elem_ref(keys[i], refs, i, kshift);
+      const int seg = locate_seg(s_base, njobs, idx);
       if (seg != cur) {
         if (cur >= 0) {
           total = first ? sum : total + sum;
@@ -666,13 +675,13 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
         sum = 0.0f;
         cur = seg;
       }
-      const GbJob& j = jobs[seg];
-      const int64_t row = (int64_t)(ref - s_base[seg]);
-      if (agg_row(j.agg_bits[agg], row)) sum = sum + agg_float(j.vals[agg], row);
+      // the row's float input (identity 0.0f for a row its FilteredAggregator rejects: x + 0.0f == x
+      // for every partial sum, which starts at +0.0f)
+      sum = sum + (float)__longlong_as_double((long long)payload[(size_t)idx * pw + agg]);
     }
     if (cur >= 0) total = first ? sum : total + sum;
     if (out_slots) {  // groupBy: the final ABI value
-      out_slots[g * rec + 1 + agg] = (uint64_t)__float_as_uint(total);
+      out_slots[(1 + agg) * cap + g] = (uint64_t)__float_as_uint(total);
     } else if (cur >= 0) {  // per-segment engines: the run is one (segment, bucket, id) cell (device encoding)
       const GbJob& j = jobs[cur];
       const uint64_t key = keys[i0] >> kshift;
@@ -683,28 +692,42 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
   }
 }
 
-void launch_fsum_runs(const GbJob* d_jobs, int njobs, SortBufs* sb, AggPlan plan, int agg, const uint32_t* head_pos,
-                      uint64_t* out_slots, hipStream_t s) {
+void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, AggPlan plan, int agg,
+                      const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s) {
   const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (sb->cap + 255) / 256));
-  hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->keys[sb->cur],
-                     sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, plan.n + 1, agg, out_slots);
+  hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->tile_cnt, ntiles,
+                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, sb->payload, sb->pw, agg,
+                     out_slots, cap, plan.n + 1);
 }
 
 // ------------------------------------------------------------------------------------------------
 // finalize (for slots written in the device encoding) and unpack
 // ------------------------------------------------------------------------------------------------
-__global__ void k_slots_finalize(uint64_t* __restrict__ slots, const uint32_t* __restrict__ n_ptr, AggPlan plan) {
+// slots [rec][cap] (SoA), groups n_ptr[0]
+__global__ void k_slots_finalize(uint64_t* __restrict__ slots, const uint32_t* __restrict__ n_ptr, AggPlan plan, int64_t cap) {
   const int64_t ng = n_ptr[0];
-  const int rec = plan.n + 1;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ng * rec; i += (int64_t)gridDim.x * blockDim.x) {
-    const int s = (int)(i % rec);
-    if (s > 0) slots[i] = finalize_dev(plan.kind[s - 1], slots[i]);
+  for (int a = 0; a < plan.n; ++a) {
+    uint64_t* col = slots + (1 + a) * cap;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ng; i += (int64_t)gridDim.x * blockDim.x)
+      col[i] = finalize_dev(plan.kind[a], col[i]);
   }
 }
 
 void launch_slots_finalize(uint64_t* slots, const uint32_t* n_ptr, int64_t cap, AggPlan plan, hipStream_t s) {
-  const int64_t blocks = std::min<int64_t>(16384, std::max<int64_t>(1, (cap * (plan.n + 1) + 255) / 256));
-  hipLaunchKernelGGL(k_slots_finalize, dim3((unsigned)blocks), dim3(256), 0, s, slots, n_ptr, plan);
+  const int64_t blocks = std::min<int64_t>(16384, std::max<int64_t>(1, (cap + 255) / 256));
+  hipLaunchKernelGGL(k_slots_finalize, dim3((unsigned)blocks), dim3(256), 0, s, slots, n_ptr, plan, cap);
+}
+
+// SoA result slots [rec][cap] -> AoS records [n][rec] (the exchange format of dg_result_export)
+__global__ void k_soa_to_aos(const uint64_t* __restrict__ soa, int64_t cap, int64_t n, int rec, uint64_t* __restrict__ aos) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * rec; i += (int64_t)gridDim.x * blockDim.x)
+    aos[i] = soa[(i % rec) * cap + i / rec];
+}
+
+void launch_soa_to_aos(const uint64_t* soa, int64_t cap, int64_t n, int rec, uint64_t* aos, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>(16384, (n * rec + 255) / 256);
+  hipLaunchKernelGGL(k_soa_to_aos, dim3((unsigned)blocks), dim3(256), 0, s, soa, cap, n, rec, aos);
 }
 
 __global__ void k_gb_unpack(const uint64_t* __restrict__ keys, int64_t start, int64_t count, KeyLayout lay,
@@ -821,7 +844,8 @@ __global__ __launch_bounds__(256) void k_merge_reduce(const uint64_t* __restrict
                                                       int kshift, const uint32_t* __restrict__ n_ptr,
                                                       const uint32_t* __restrict__ head_pos,
                                                       const uint64_t* __restrict__ in_slots, AggPlan plan,
-                                                      uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_slots) {
+                                                      uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_slots,
+                                                      int64_t cap) {
   const uint32_t n = n_ptr[0], ng = n_ptr[1];
   const int na = plan.n, rec = na + 1;
   for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (int64_t)gridDim.x * 256) {
@@ -829,20 +853,20 @@ __global__ __launch_bounds__(256) void k_merge_reduce(const uint64_t* __restrict
     out_keys[g] = keys[i0] >> kshift;
     uint64_t rows = 0;
     for (uint32_t i = i0; i < i1; ++i) rows += in_slots[(size_t)elem_ref(keys[i], refs, i, kshift) * rec];
-    out_slots[(size_t)g * rec] = rows;
+    out_slots[g] = rows;
     for (int a = 0; a < na; ++a) {
       const int kind = plan.kind[a];
       if (kind == DG_AGG_FLOAT_SUM) {  // float adds in partial order
         float acc = 0.0f;
         for (uint32_t i = i0; i < i1; ++i)
           acc = acc + __uint_as_float((uint32_t)in_slots[(size_t)elem_ref(keys[i], refs, i, kshift) * rec + 1 + a]);
-        out_slots[(size_t)g * rec + 1 + a] = (uint64_t)__double_as_longlong((double)acc);  // finalized later
+        out_slots[(1 + a) * cap + g] = (uint64_t)__double_as_longlong((double)acc);  // finalized later
         continue;
       }
       uint64_t acc = identity_of(plan.op[a], kind);
       for (uint32_t i = i0; i < i1; ++i)
         acc = combine_op(plan.op[a], acc, abi_to_dev(kind, in_slots[(size_t)elem_ref(keys[i], refs, i, kshift) * rec + 1 + a]));
-      out_slots[(size_t)g * rec + 1 + a] = acc;
+      out_slots[(1 + a) * cap + g] = acc;
     }
   }
 }
@@ -851,7 +875,7 @@ void launch_merge_reduce(SortBufs* sb, const uint32_t* head_pos, const uint64_t*
                          uint64_t* out_keys, uint64_t* out_slots, hipStream_t s) {
   const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (cap + 255) / 256));
   hipLaunchKernelGGL(k_merge_reduce, dim3((unsigned)blocks), dim3(256), 0, s, sb->keys[sb->cur], sb->refs[sb->cur],
-                     sb->ref_bits, sb->n, head_pos, in_slots, plan, out_keys, out_slots);
+                     sb->ref_bits, sb->n, head_pos, in_slots, plan, out_keys, out_slots, cap);
 }
 
 }  // namespace dg
