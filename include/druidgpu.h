@@ -26,6 +26,10 @@
  *                               (query/groupby/strategy/GroupByStrategyV2.java:472-477, epinephelinae/GroupByQueryEngineV2.java:91-187)
  *                               + GroupByStrategyV2.mergeRunners -> GroupByMergingQueryRunnerV2.run (:170-290)
  *   dg_result_*              <- the merged grouper's sorted iterator (ConcurrentGrouper.iterator(true))
+ *   dg_result_export / dg_keys_partition / dg_merge
+ *                            <- QueryRunnerFactory.mergeRunners across devices (query/QueryRunnerFactory.java:62):
+ *                               GroupByMergingQueryRunnerV2 semantics over the devices' merged groups
+ *   dg_records_pack          <- BufferAggregator.get* record layout (query/aggregation/BufferAggregator.java:35-199)
  *
  * Segment arrays: every *_run takes n_segs segments that are attached to the SAME context (device)
  * and runs them as one batched launch sequence; results stay per segment, exactly as the
@@ -48,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 3
+#define DG_ABI_VERSION 4
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -104,7 +108,13 @@ typedef struct dg_result dg_result;
 /*
  * One filter node. A filter is an array of nodes in prefix order: an AND/OR node is followed by
  * its n_children subtrees, a NOT node by exactly one subtree. Strings are NUL-terminated UTF-8;
- * a NULL value pointer means the null value ("" in default null mode).
+ * a NULL value pointer means the null value ("" in default null mode). A leaf on a string column
+ * runs on its bitmap index; a leaf on a long / float / double column (no bitmap index) is the
+ * reference's row post-filter (QueryableIndexStorageAdapter.java:244-260, FilteredOffset.java:40-105)
+ * with its ValueMatcher semantics: selector / in values parsed as getExactLongFromDecimalString or
+ * Floats/Doubles.tryParse, NUMERIC bounds as BoundDimFilter's long / float / double predicates,
+ * LEXICOGRAPHIC bounds on long columns over String.valueOf(value); other orderings on numeric
+ * columns -> DG_ERR_UNSUPPORTED.
  */
 typedef struct {
   int32_t kind;
@@ -335,6 +345,24 @@ int dg_keys_partition(dg_context* ctx, const uint64_t* d_keys, int64_t n, const 
  * dg_result_dim_cardinality is ks->card[d], and the dictionary is the caller's. */
 int dg_merge(dg_context* ctx, const dg_keyspace* ks, const uint64_t* d_keys, const uint64_t* d_slots, int64_t n,
              dg_result** out, dg_metrics* metrics);
+
+/* ---- BufferAggregator record layout (query/aggregation/BufferAggregator.java:35-199) ----
+ * Writes n records of aggregate slots (n_aggs per record, the dg_*_run slot encoding) into Druid's
+ * buffer layout so a JNI shim can fill a processing-pool direct ByteBuffer in place
+ * (GetDirectBufferAddress): aggregator a at byte offsets[a] of each record_size-byte record, the
+ * value as its BufferAggregator stores it — count / long* as an 8-byte long (LongSumBufferAggregator
+ * buf.putLong), double* as an 8-byte double, float* as a 4-byte float (FloatSumBufferAggregator
+ * buf.putFloat) — big-endian (java.nio.ByteBuffer's default order, big_endian != 0) or little-endian.
+ * Host memory only; no device work. */
+typedef struct {
+  int32_t n_aggs;
+  const int32_t* kinds;   /* DG_AGG_* */
+  const int32_t* offsets; /* byte offset of each aggregator inside a record */
+  int32_t record_size;
+  int32_t big_endian;
+} dg_record_layout;
+
+int dg_records_pack(const uint64_t* slots, int64_t n, const dg_record_layout* layout, void* out);
 
 /* ---- diagnostics (test harness; no reference counterpart) ----
  * Decode n raw LZ4 blocks (host buffers, <= 64 KiB decoded each) through the same attach-time

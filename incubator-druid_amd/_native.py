@@ -87,6 +87,11 @@ class dg_groupby(ctypes.Structure):
     _fields_ = [("dimensions", ctypes.POINTER(ctypes.c_char_p)), ("n_dims", ctypes.c_int32)]
 
 
+class dg_record_layout(ctypes.Structure):
+    _fields_ = [("n_aggs", ctypes.c_int32), ("kinds", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("record_size", ctypes.c_int32), ("big_endian", ctypes.c_int32)]
+
+
 class dg_keyspace(ctypes.Structure):
     _fields_ = [("n_dims", ctypes.c_int32), ("card", ctypes.c_void_p), ("period_ms", ctypes.c_int64),
                 ("bucket0", ctypes.c_int64), ("n_buckets", ctypes.c_int64), ("universal_time", ctypes.c_int64),
@@ -102,7 +107,7 @@ EXPORTS = [
     "dg_segment_dim_dictionary", "dg_segment_set_dim_order", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_topn_merge", "dg_groupby_run",
     "dg_result_groups", "dg_result_fetch_groups", "dg_result_fetch_rows", "dg_result_dim_cardinality",
     "dg_result_dim_dictionary", "dg_result_release", "dg_keyspace_bits", "dg_result_export", "dg_keys_partition",
-    "dg_merge", "dg_debug_lz4_decode",
+    "dg_merge", "dg_records_pack", "dg_debug_lz4_decode",
 ]
 
 _lib = None
@@ -161,6 +166,7 @@ def lib():
         "dg_result_export": (ctypes.c_int, [vp, P(dg_keyspace), P(vp), vp, vp]),
         "dg_keys_partition": (ctypes.c_int, [vp, vp, i64, vp, i32, vp]),
         "dg_merge": (ctypes.c_int, [vp, P(dg_keyspace), vp, vp, i64, P(vp), P(dg_metrics)]),
+        "dg_records_pack": (ctypes.c_int, [vp, i64, P(dg_record_layout), vp]),
         "dg_debug_lz4_decode": (ctypes.c_int, [vp, P(vp), P(i32), i32, vp, P(i32), P(ctypes.c_double), vp]),
     }
     for name, (res, args) in sig.items():

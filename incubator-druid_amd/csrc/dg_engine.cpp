@@ -2962,6 +2962,36 @@ int32_t dg_result_dim_cardinality(const dg_result* r, int32_t dim) {
 
 void dg_result_release(dg_result* r) { delete r; }
 
+// ---- BufferAggregator records ----
+int dg_records_pack(const uint64_t* slots, int64_t n, const dg_record_layout* lay, void* out) {
+  if (n < 0 || !lay || (n > 0 && (!slots || !out)) || lay->n_aggs < 0 || (lay->n_aggs && (!lay->kinds || !lay->offsets)))
+    return set_error(DG_ERR_ARG, "bad record layout");
+  const int na = lay->n_aggs;
+  for (int a = 0; a < na; ++a) {
+    const int k = lay->kinds[a];
+    if (k < DG_AGG_COUNT || k > DG_AGG_FLOAT_MAX) return set_error(DG_ERR_ARG, "aggregator kind %d", k);
+    const int w = (k == DG_AGG_FLOAT_SUM || k == DG_AGG_FLOAT_MIN || k == DG_AGG_FLOAT_MAX) ? 4 : 8;
+    if (lay->offsets[a] < 0 || lay->offsets[a] + w > lay->record_size)
+      return set_error(DG_ERR_ARG, "aggregator %d at offset %d does not fit a %d-byte record", a, lay->offsets[a], lay->record_size);
+  }
+  uint8_t* o = static_cast<uint8_t*>(out);
+  for (int64_t i = 0; i < n; ++i) {
+    uint8_t* rec = o + i * (int64_t)lay->record_size;
+    for (int a = 0; a < na; ++a) {
+      const int k = lay->kinds[a];
+      const uint64_t v = slots[i * na + a];
+      uint8_t* p = rec + lay->offsets[a];
+      if (k == DG_AGG_FLOAT_SUM || k == DG_AGG_FLOAT_MIN || k == DG_AGG_FLOAT_MAX) {
+        const uint32_t f = (uint32_t)v;  // the float's bits ride in the slot's low 4 bytes
+        for (int b = 0; b < 4; ++b) p[b] = (uint8_t)(f >> (8 * (lay->big_endian ? 3 - b : b)));
+      } else {
+        for (int b = 0; b < 8; ++b) p[b] = (uint8_t)(v >> (8 * (lay->big_endian ? 7 - b : b)));
+      }
+    }
+  }
+  return DG_OK;
+}
+
 // ---- cross-device merge ----
 static int keyspace_layout(const dg_keyspace* ks, KeyLayout* lay, AggPlan* plan) {
   if (!ks || ks->n_dims < 0 || ks->n_dims > kMaxGroupDims || (ks->n_dims && !ks->card))

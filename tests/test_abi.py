@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_structs():
     N = importlib.import_module("incubator-druid_amd._native")
-    assert N.lib().dg_abi_version() == 3
+    assert N.lib().dg_abi_version() == 4
     # struct layouts the header fixes (LP64)
     assert ctypes.sizeof(N.dg_filter) == 64
     assert ctypes.sizeof(N.dg_agg) == 32
@@ -53,3 +53,32 @@ def test_no_device_in_container_is_reported_not_faked():
     if n.value == 0:
         h = ctypes.c_void_p()
         assert N.lib().dg_context_create(0, ctypes.byref(h)) == 7  # DG_ERR_DEVICE, no CPU fallback
+
+
+def test_records_pack_druid_buffer_layout():
+    """dg_records_pack writes BufferAggregator records (host-only marshaling, no device): 8-byte
+    long / double, 4-byte float, at the layout's offsets, big-endian like java.nio.ByteBuffer."""
+    import struct
+    import numpy as np
+    N = importlib.import_module("incubator-druid_amd._native")
+    kinds = np.array([0, 2, 3, 5, 9], dtype=np.int32)       # count, doubleSum, floatSum, longMax, floatMax
+    offs = np.array([0, 8, 16, 20, 28], dtype=np.int32)
+    vals = [(7, -2.5, 1.25, -9, float("inf")), (1 << 40, 1e300, -0.0, 3, -3.5)]
+    slots = np.zeros((2, 5), dtype=np.uint64)
+    for i, (c, d, f, l, fm) in enumerate(vals):
+        slots[i] = [c, np.float64(d).view(np.uint64), np.float32(f).view(np.uint32), np.int64(l).view(np.uint64),
+                    np.float32(fm).view(np.uint32)]
+    for be in (1, 0):
+        lay = N.dg_record_layout(5, kinds.ctypes.data, offs.ctypes.data, 40, be)
+        out = np.zeros(80, dtype=np.uint8)
+        assert N.lib().dg_records_pack(slots.ctypes.data, 2, ctypes.byref(lay), out.ctypes.data) == 0
+        e = ">" if be else "<"
+        for i, (c, d, f, l, fm) in enumerate(vals):
+            rec = bytes(out[40 * i:40 * (i + 1)])
+            assert struct.unpack(e + "q", rec[0:8])[0] == c
+            assert struct.unpack(e + "d", rec[8:16])[0] == d
+            assert struct.unpack(e + "f", rec[16:20])[0] == f and str(struct.unpack(e + "f", rec[16:20])[0]) == str(f)
+            assert struct.unpack(e + "q", rec[20:28])[0] == l
+            assert struct.unpack(e + "f", rec[28:32])[0] == fm
+    bad = N.dg_record_layout(5, kinds.ctypes.data, offs.ctypes.data, 30, 1)  # floatMax at 28 does not fit 30
+    assert N.lib().dg_records_pack(slots.ctypes.data, 2, ctypes.byref(bad), None) == 6
