@@ -522,8 +522,27 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ 
   int32_t* s_g = reinterpret_cast<int32_t*>(s_ref);  // [x] = relative group index of element x
 #pragma unroll
   for (int c = 0; c < kSPT; ++c) s_g[c * kST + tid] = grel[c];
-  // one slot at a time (-1 = rows aggregated): the 16 inputs are gathered first (independent random
-  // loads in flight together), then scanned chunk by chunk
+  // Up to two payload slots per element are gathered once, together (one random record read per
+  // element; a second pass over the slots would miss the L2 again); wider payloads slot by slot.
+  constexpr int kRegSlots = 2;
+  uint64_t xr[kSPT][kRegSlots];
+  if (pw <= kRegSlots) {
+#pragma unroll
+    for (int c = 0; c < kSPT; ++c) {
+      const bool valid = c * kST + tid < tile_n;
+      const uint64_t* pr = payload + (size_t)idx_of[c] * pw;
+      if (pw == 2 && valid) {
+        const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(pr);  // 16-byte aligned: pw == 2
+        xr[c][0] = w.x;
+        xr[c][1] = w.y;
+      } else {
+        xr[c][0] = valid && pw >= 1 ? pr[0] : 0ull;
+        xr[c][1] = 0ull;
+      }
+    }
+  }
+  // one slot at a time (-1 = rows aggregated): the 16 inputs (gathered above, or now: independent
+  // random loads in flight together) go to LDS, then are scanned chunk by chunk
   for (int a = -1; a < na; ++a) {
     const int kind = a < 0 ? DG_AGG_COUNT : plan.kind[a];
     if (kind == DG_AGG_FLOAT_SUM) continue;  // k_fsum_runs: float32 in row order
@@ -534,7 +553,10 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ 
 #pragma unroll
       for (int c = 0; c < kSPT; ++c) {
         const bool valid = c * kST + tid < tile_n;
-        xv[c] = !valid ? ident : (a < 0 ? 1ull : payload[(size_t)idx_of[c] * pw + a]);
+        if (!valid) xv[c] = ident;
+        else if (a < 0) xv[c] = 1ull;
+        else if (pw <= kRegSlots) xv[c] = a == 0 ? xr[c][0] : xr[c][1];
+        else xv[c] = payload[(size_t)idx_of[c] * pw + a];
       }
 #pragma unroll
       for (int c = 0; c < kSPT; ++c) s_x[c * kST + tid] = xv[c];
