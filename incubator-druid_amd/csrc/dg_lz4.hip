@@ -336,50 +336,47 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     if (2 * tid < nj) s_jpre[2 * tid] = pre;
     if (2 * tid + 1 < nj) s_jpre[2 * tid + 1] = pre + l0;
     __syncthreads();
-    const int f0 = (int)(((int64_t)tot * tid) / kLzThreads), f1 = (int)(((int64_t)tot * (tid + 1)) / kLzThreads);
-    if (f0 < f1) {
-      int lo = 0, hi = nj - 1;  // last job with s_jpre <= f0
+    // flat positions interleaved over the threads (f = tid, tid + 1024, ...): a wave's 64 lanes take
+    // 64 consecutive positions, so the literal byte loads of a long run are one cache line per wave
+    // instruction and the E stores consecutive; each lane's job index only moves forward
+    auto find_job = [&](int f, int lo) {  // last job with s_jpre <= f, searching from lo
+      int hi = nj - 1;
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (s_jpre[mid] <= f0) lo = mid;
+        if (s_jpre[mid] <= f) lo = mid;
         else hi = mid - 1;
       }
-      int j = lo;
-      uint2 jb = s_job[j];
-      int jstart = s_jpre[j], jend = jstart + job_len(jb);
-      for (int f = f0; f < f1; f += 8) {
-        int xs[8], srcs[8];
-        uint32_t vals[8];
+      return lo;
+    };
+    int j = 0;
+    for (int fb = tid; fb < tot; fb += 8 * kLzThreads) {
+      int xs[8], srcs[8];
+      uint32_t vals[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          xs[u] = -1;
-          const int g = f + u;
-          if (g < f1) {
-            while (g >= jend) {
-              ++j;
-              jb = s_job[j];
-              jstart = s_jpre[j];
-              jend = jstart + job_len(jb);
-            }
-            const int k = g - jstart, o = (int)(jb.x & 0xFFFF);
-            xs[u] = o + k;
-            if (jb.y & 0x80000000u) {
-              const int d = (int)(jb.y & 0xFFFF);
-              srcs[u] = (d >= job_len(jb) || d == kClass) ? o + k - d : o - d + k % d;
-            } else {
-              srcs[u] = -1 - ((int)jb.y + k);  // literal: input offset, encoded negative
-            }
+      for (int u = 0; u < 8; ++u) {
+        xs[u] = -1;
+        const int g = fb + u * kLzThreads;
+        if (g < tot) {
+          if (g >= s_jpre[j] + job_len(s_job[j])) j = find_job(g, j);
+          const uint2 jb = s_job[j];
+          const int k = g - s_jpre[j], o = (int)(jb.x & 0xFFFF);
+          xs[u] = o + k;
+          if (jb.y & 0x80000000u) {
+            const int d = (int)(jb.y & 0xFFFF);
+            srcs[u] = (d >= job_len(jb) || d == kClass) ? o + k - d : o - d + k % d;
+          } else {
+            srcs[u] = -1 - ((int)jb.y + k);  // literal: input offset, encoded negative
           }
         }
+      }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (xs[u] >= 0 && srcs[u] < 0) vals[u] = gin[-1 - srcs[u]];
+      for (int u = 0; u < 8; ++u)
+        if (xs[u] >= 0 && srcs[u] < 0) vals[u] = gin[-1 - srcs[u]];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (xs[u] < 0) continue;
-          if (srcs[u] < 0) put_lit(S, xs[u], vals[u]);
-          else put_ptr(S, xs[u], srcs[u]);
-        }
+      for (int u = 0; u < 8; ++u) {
+        if (xs[u] < 0) continue;
+        if (srcs[u] < 0) put_lit(S, xs[u], vals[u]);
+        else put_ptr(S, xs[u], srcs[u]);
       }
     }
   }
@@ -492,8 +489,9 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         const uint32_t v = dv[k], d0 = v & 0xFFFF, d1 = v >> 16;
         const int a0 = x - (d0 < (uint32_t)kTail ? (int)d0 : 0);
         const int a1 = x + 1 - (d1 < (uint32_t)kTail ? (int)d1 : 0);
-        ta[k] = x < kTail ? s_e[eph(a0)] : 0xFF00u;
-        tb[k] = x < kTail ? s_e[eph(a1)] : 0xFF00u;
+        // a resolved entry (literal code) needs no target read
+        ta[k] = (x < kTail && d0 < (uint32_t)kTail) ? s_e[eph(a0)] : 0xFF00u;
+        tb[k] = (x < kTail && d1 < (uint32_t)kTail) ? s_e[eph(a1)] : 0xFF00u;
       }
       bool open = false;
 #pragma unroll

@@ -22,7 +22,7 @@ PHASES = ["stage", "parse+scan", "fill", "coop", "jump", "output"]
 
 def payloads(rng, k):
     n8 = BLOCK // 8
-    out = {"seqlong": [], "time": [], "normal": [], "uniform3": [], "ulong500": [], "zipfdbl": []}
+    out = {"seqlong": [], "time": [], "normal": [], "uniform3": [], "hyper3": [], "ulong500": [], "zipfdbl": []}
     for i in range(k):
         seq = np.arange(i * n8, (i + 1) * n8, dtype=np.int64)
         out["seqlong"].append((seq % 10000).astype("<i8").tobytes())
@@ -34,6 +34,8 @@ def payloads(rng, k):
         out["zipfdbl"].append(rng.choice(zk - 1, size=n8, p=zp / zp.sum()).astype("<f8").tobytes())
         ids = rng.integers(1, 100001, BLOCK // 3 + 1).astype("<u4").view(np.uint8).reshape(-1, 4)[:, :3]
         out["uniform3"].append(ids.tobytes()[:3 * 16384])
+        hyp = (np.arange(i * 16384, (i + 1) * 16384) % 100000).astype("<u4").view(np.uint8).reshape(-1, 4)[:, :3]
+        out["hyper3"].append(hyp.tobytes())
     return out
 
 
