@@ -838,26 +838,63 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
     for (int k = 0; k < l; ++k)
       if (fp.leaf_col[k] == c) first = false;
     if (!first) continue;
-    std::vector<int64_t> offs;
-    std::vector<int32_t> lens, tgts;
+    std::vector<int64_t> offs, row0s, p_off, p_row0;
+    std::vector<int32_t> lens, tgts, p_info, p_tgt;
+    const bool split = !c->bm_piece_first.empty();
     for (int k = l; k < nleaves; ++k) {
       if (fp.leaf_col[k] != c) continue;
       for (int32_t id : fp.leaf_ids[k]) {
         if (c->bm_len[id] == 0) continue;
+        if (split && c->bm_piece_first[id + 1] > c->bm_piece_first[id]) {  // a long bitmap: its pieces
+          for (int32_t q = c->bm_piece_first[id]; q < c->bm_piece_first[id + 1]; ++q) {
+            const BmPiece& pc = c->bm_pieces[q];
+            if (c->bitmap_roaring) {
+              p_off.push_back(pc.off);
+              p_row0.push_back(pc.row0);
+              p_info.push_back(pc.info);
+              p_tgt.push_back(k);
+            } else {
+              offs.push_back(pc.off);
+              lens.push_back(pc.len);
+              row0s.push_back(pc.row0);
+              tgts.push_back(k);
+            }
+          }
+          continue;
+        }
         offs.push_back(c->bm_off[id]);
         lens.push_back(c->bm_len[id]);
+        row0s.push_back(0);
         tgts.push_back(k);
       }
     }
+    if (!p_off.empty()) {  // Roaring containers of split bitmaps
+      const int np = (int)p_off.size();
+      int64_t *d_poff, *d_prow;
+      int32_t *d_pinfo, *d_ptgt;
+      int64_t* h_poff = up_take<int64_t>(cs, np, &d_poff, st);
+      int64_t* h_prow = up_take<int64_t>(cs, np, &d_prow, st);
+      int32_t* h_pinfo = up_take<int32_t>(cs, np, &d_pinfo, st);
+      int32_t* h_ptgt = up_take<int32_t>(cs, np, &d_ptgt, st);
+      if (!h_poff || !h_prow || !h_pinfo || !h_ptgt) return set_error(DG_ERR_OOM, "bitmap piece tables");
+      memcpy(h_poff, p_off.data(), np * 8);
+      memcpy(h_prow, p_row0.data(), np * 8);
+      memcpy(h_pinfo, p_info.data(), np * 4);
+      memcpy(h_ptgt, p_tgt.data(), np * 4);
+      DG_FLUSH(cs, st);
+      launch_roaring_pieces(c->bm_bytes.as<uint8_t>(), d_poff, d_prow, d_pinfo, d_ptgt, np, d_sets, (nwords + 2) * 32, st);
+    }
     if (offs.empty()) continue;
     const int nb = (int)offs.size();
-    int64_t* d_off;
+    int64_t *d_off, *d_row0;
     int32_t *d_len, *d_tgt;
     int64_t* h_off = up_take<int64_t>(cs, nb, &d_off, st);
+    int64_t* h_row0 = up_take<int64_t>(cs, nb, &d_row0, st);
     int32_t* h_len = up_take<int32_t>(cs, nb, &d_len, st);
     int32_t* h_tgt = up_take<int32_t>(cs, nb, &d_tgt, st);
-    if (!h_off || !h_len || !h_tgt) return set_error(DG_ERR_OOM, "bitmap tables");
+    if (!h_off || !h_row0 || !h_len || !h_tgt) return set_error(DG_ERR_OOM, "bitmap tables");
     memcpy(h_off, offs.data(), nb * 8);
+    memcpy(h_row0, row0s.data(), nb * 8);
     memcpy(h_len, lens.data(), nb * 4);
     memcpy(h_tgt, tgts.data(), nb * 4);
     if (c->bitmap_roaring) {
@@ -867,7 +904,7 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
       launch_roaring_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, d_err, (nwords + 2) * 32, st);
     } else {
       DG_FLUSH(cs, st);
-      launch_concise_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, nb, d_sets, (nwords + 2) * 32, st);
+      launch_concise_or(c->bm_bytes.as<uint8_t>(), d_off, d_len, d_tgt, d_row0, nb, d_sets, (nwords + 2) * 32, st);
     }
   }
   // row-predicate leaves: decode the column (its blocks, as the reference's post-filter reads them

@@ -198,6 +198,17 @@ struct BlockColumn {
   DevBuf block_ptrs;                   // const uint8_t*[nblocks]: raw slots (UNCOMPRESSED/NONE)
 };
 
+// A piece of a long serialized bitmap: Concise = a run of whole words starting at row `row0`;
+// Roaring = one container (info = cardinality - 1 | 1 << 31 for a run container).
+struct BmPiece {
+  int64_t off;   // byte offset of the piece's data inside the column's bm_bytes
+  int64_t row0;  // first row the piece covers
+  int32_t len;   // bytes
+  int32_t info;  // Roaring container: (card - 1) | run << 31; Concise: 0
+};
+constexpr int kConcisePieceWords = 4096;  // Concise bitmaps above 2x this are cut into pieces of it
+constexpr int kRoaringSplitBytes = 32768; // Roaring bitmaps above this are cut into containers
+
 constexpr int kOrderSlots = 8;
 
 struct Column {
@@ -214,6 +225,11 @@ struct Column {
   std::vector<int64_t> bm_off;         // byte offset of each bitmap inside bm_bytes (4-byte aligned)
   std::vector<int32_t> bm_len;
   DevBuf bm_bytes;
+  // long bitmaps split at attach so one bitmap's expansion spreads over many workgroups: bitmap i's
+  // pieces are bm_pieces[bm_piece_first[i] .. bm_piece_first[i + 1]) (empty = not split); empty
+  // vector = no bitmap of the column is split
+  std::vector<int32_t> bm_piece_first;
+  std::vector<BmPiece> bm_pieces;
   // dictionary orders handed in by dg_segment_set_dim_order (slot = 2 * DG_ORDER_* + inverted):
   // rank of every dictionary id under the StringComparator, comparator-equal values share a rank
   DevBuf order_rank[kOrderSlots];
@@ -297,8 +313,13 @@ void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStrea
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // VSizeLongSerde.getSerializedSize (VSizeLongSerde.java:61-65)
 inline int64_t vsize_serialized(int bits, int64_t n) { return (bits * n + 7) / 8 + 4; }
+// Concise words [off, off + len) whose first word starts at row row0 (null: 0), OR-ed into sets[target]
 void launch_concise_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
-                       int nbitmaps, uint32_t* const* d_sets, int64_t limit_bits, hipStream_t s);
+                       const int64_t* d_row0, int nbitmaps, uint32_t* const* d_sets, int64_t limit_bits, hipStream_t s);
+// single Roaring containers (pieces): data at off, rows from row0, info as BmPiece; four per workgroup
+void launch_roaring_pieces(const uint8_t* bm_base, const int64_t* d_off, const int64_t* d_row0, const int32_t* d_info,
+                           const int32_t* d_target, int npieces, uint32_t* const* d_sets, int64_t limit_bits,
+                           hipStream_t s);
 void launch_roaring_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
                        int nbitmaps, uint32_t* const* d_sets, int32_t* d_err, int64_t limit_bits, hipStream_t s);
 void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_sets, uint32_t* out, int64_t nrows,

@@ -81,13 +81,14 @@ __device__ void or_range(uint32_t* set, int64_t lo, int64_t hi, int64_t skip, in
 
 __global__ __launch_bounds__(256) void k_concise_or(const uint8_t* __restrict__ base, const int64_t* __restrict__ off,
                                                     const int32_t* __restrict__ len, const int32_t* __restrict__ target,
-                                                    uint32_t* const* __restrict__ sets, int64_t limit) {
+                                                    const int64_t* __restrict__ row0, uint32_t* const* __restrict__ sets,
+                                                    int64_t limit) {
   __shared__ int64_t s_tmp[8];
   const int b = blockIdx.x;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(base + off[b]);
   const int nw = len[b] >> 2;
   uint32_t* set = sets[target[b]];
-  int64_t carry = 0;
+  int64_t carry = row0 ? row0[b] : 0;  // a piece of a split bitmap starts mid-way
   for (int basew = 0; basew < nw; basew += 256) {
     const int i = basew + threadIdx.x;
     uint32_t w = 0;
@@ -115,9 +116,10 @@ __global__ __launch_bounds__(256) void k_concise_or(const uint8_t* __restrict__ 
 }
 
 void launch_concise_or(const uint8_t* bm_base, const int64_t* d_off, const int32_t* d_len, const int32_t* d_target,
-                       int nbitmaps, uint32_t* const* d_sets, int64_t limit, hipStream_t s) {
+                       const int64_t* d_row0, int nbitmaps, uint32_t* const* d_sets, int64_t limit, hipStream_t s) {
   if (nbitmaps <= 0) return;
-  hipLaunchKernelGGL(k_concise_or, dim3(nbitmaps), dim3(256), 0, s, bm_base, d_off, d_len, d_target, d_sets, limit);
+  hipLaunchKernelGGL(k_concise_or, dim3(nbitmaps), dim3(256), 0, s, bm_base, d_off, d_len, d_target, d_row0, d_sets,
+                     limit);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -253,6 +255,49 @@ __global__ __launch_bounds__(256) void k_filter_eval(const int32_t* __restrict__
   // wave reduce then one atomic per wave
   for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, 64);
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
+}
+
+// one Roaring container per wave (pieces of long bitmaps, split at attach): the container's rows are
+// OR-ed exactly as k_roaring_or does for a whole bitmap
+__global__ __launch_bounds__(256) void k_roaring_pieces(const uint8_t* __restrict__ base, const int64_t* __restrict__ off,
+                                                        const int64_t* __restrict__ row0s, const int32_t* __restrict__ info,
+                                                        const int32_t* __restrict__ target, int npieces,
+                                                        uint32_t* const* __restrict__ sets, int64_t limit) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= npieces) return;
+  const uint8_t* d = base + off[c];
+  const int64_t row0 = row0s[c];
+  const bool run = info[c] < 0;
+  const int card = (info[c] & 0x7FFFFFFF) + 1;
+  uint32_t* set = sets[target[c]];
+  if (run) {
+    const int nruns = (int)rd16(d);
+    for (int r = lane; r < nruns; r += 64) {
+      const int64_t st = row0 + rd16(d + 2 + 4 * r);
+      const int64_t ln = (int64_t)rd16(d + 4 + 4 * r) + 1;
+      or_range(set, st, st + ln, -1, limit);
+    }
+  } else if (card <= 4096) {
+    for (int k = lane; k < card; k += 64) {
+      const int64_t row = row0 + rd16(d + 2 * k);
+      if (row < limit) atomicOr(set + (row >> 5), 1u << (row & 31));
+    }
+  } else {
+    uint32_t* dst = set + (row0 >> 5);
+    for (int k = lane; k < 2048; k += 64) {
+      const uint32_t w = rd32(d + 4 * k);
+      if (w && row0 + 32ll * k < limit) atomicOr(dst + k, w);
+    }
+  }
+}
+
+void launch_roaring_pieces(const uint8_t* bm_base, const int64_t* d_off, const int64_t* d_row0, const int32_t* d_info,
+                           const int32_t* d_target, int npieces, uint32_t* const* d_sets, int64_t limit_bits,
+                           hipStream_t s) {
+  if (npieces <= 0) return;
+  hipLaunchKernelGGL(k_roaring_pieces, dim3((npieces + 3) / 4), dim3(256), 0, s, bm_base, d_off, d_row0, d_info,
+                     d_target, npieces, d_sets, limit_bits);
 }
 
 // ------------------------------------------------------------------------------------------------

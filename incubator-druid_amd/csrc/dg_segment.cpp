@@ -34,6 +34,7 @@
 
 namespace dg {
 
+
 namespace {
 
 int32_t be32(const uint8_t* p) {
@@ -174,6 +175,8 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps) {
 }
 
 namespace {
+static void index_bitmap_pieces(Column* c, const std::vector<uint8_t>& host);
+
 
 // Upload the blocks of a GenericIndexed of (compressed or raw) blocks.
 int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
@@ -516,8 +519,91 @@ int parse_string(Context* ctx, Column* c, Slice s) {
     }
     if (!c->bm_bytes.alloc(host.size())) return set_error(DG_ERR_OOM, "hipMalloc bitmaps");
     DG_HIP(hipMemcpy(c->bm_bytes.p, host.data(), host.size(), hipMemcpyHostToDevice));
+    index_bitmap_pieces(c, host);
   }
   return DG_OK;
+}
+
+// Long bitmaps are cut into pieces once, at attach, so a query expands one bitmap with many
+// workgroups: a Concise bitmap into runs of kConcisePieceWords words with the row each run starts
+// at (the sum of the earlier words' spans: 31 rows per literal, 31 * (blocks) per fill,
+// ConciseSetUtils.java:45-75), a Roaring bitmap into its containers (portable format: cookie,
+// [run bitmap], key / cardinality descriptors, [offsets], containers). A bitmap whose header does not
+// parse stays whole (the per-bitmap kernel reports it).
+static uint32_t le32(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+static uint32_t le16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+
+static bool roaring_containers(const uint8_t* p, int len, std::vector<BmPiece>* out, int64_t base_off) {
+  if (len < 8) return false;
+  const uint32_t cookie = le32(p);
+  int pos = 4, n = 0;
+  const uint8_t* runbits = nullptr;
+  bool has_off = true;
+  if ((cookie & 0xFFFFu) == 12347u) {
+    n = (int)(cookie >> 16) + 1;
+    runbits = p + pos;
+    pos += (n + 7) / 8;
+    has_off = n >= 4;
+  } else if (cookie == 12346u) {
+    n = (int)le32(p + 4);
+    pos = 8;
+  } else {
+    return false;
+  }
+  if (n <= 0 || pos + 4 * n > len) return false;
+  const uint8_t* desc = p + pos;
+  pos += 4 * n;
+  const uint8_t* offs = nullptr;
+  if (has_off) {
+    if (pos + 4 * n > len) return false;
+    offs = p + pos;
+    pos += 4 * n;
+  }
+  int cur = pos;
+  std::vector<BmPiece> v;
+  for (int c = 0; c < n; ++c) {
+    const int key = (int)le16(desc + 4 * c), card = (int)le16(desc + 4 * c + 2) + 1;
+    const bool run = runbits && ((runbits[c >> 3] >> (c & 7)) & 1);
+    const int start = offs ? (int)le32(offs + 4 * c) : cur;
+    if (start < 0 || start + 2 > len) return false;
+    const int sz = run ? 2 + 4 * (int)le16(p + start) : (card <= 4096 ? 2 * card : 8192);
+    if (start + sz > len) return false;
+    v.push_back(BmPiece{base_off + start, (int64_t)key << 16, sz, (int32_t)((uint32_t)(card - 1) | (run ? 0x80000000u : 0u))});
+    cur = start + sz;
+  }
+  out->insert(out->end(), v.begin(), v.end());
+  return true;
+}
+
+static void index_bitmap_pieces(Column* c, const std::vector<uint8_t>& host) {
+  const int n = (int)c->bm_off.size();
+  std::vector<int32_t> first(n + 1, 0);
+  std::vector<BmPiece> pieces;
+  for (int i = 0; i < n; ++i) {
+    first[i] = (int32_t)pieces.size();
+    const uint8_t* p = host.data() + c->bm_off[i];
+    const int len = c->bm_len[i];
+    if (!c->bitmap_roaring) {
+      const int nw = len / 4;
+      if (nw <= 2 * kConcisePieceWords) continue;
+      int64_t row = 0;
+      for (int w0 = 0; w0 < nw; w0 += kConcisePieceWords) {
+        const int cnt = std::min(kConcisePieceWords, nw - w0);
+        pieces.push_back(BmPiece{c->bm_off[i] + 4ll * w0, row, 4 * cnt, 0});
+        for (int k = w0; k < w0 + cnt; ++k) {
+          const uint32_t w = (uint32_t)be32(p + 4ll * k);
+          row += (w & 0x80000000u) ? 31 : 31ll * ((int64_t)(w & 0x01FFFFFFu) + 1);
+        }
+      }
+    } else if (len > kRoaringSplitBytes) {
+      roaring_containers(p, len, &pieces, c->bm_off[i]);
+    }
+  }
+  first[n] = (int32_t)pieces.size();
+  if (!pieces.empty()) {
+    c->bm_piece_first.swap(first);
+    c->bm_pieces.swap(pieces);
+  }
 }
 
 int64_t column_device_bytes(const Column& c) {
