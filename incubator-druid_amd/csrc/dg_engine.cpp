@@ -972,6 +972,8 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.expect_len = expect;
   j.ncp = b.cp_n[k];
   j.dec_len = b.dec_len[k];
+  j.wide = b.cp_wide[k];
+  j.pad = 0;
   return j;
 }
 
@@ -1082,9 +1084,14 @@ static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_
   // longest blocks first (token-dense blocks cost the most; workgroups dispatch in order, so this
   // is greedy LPT scheduling of the blocks over the CUs and shortens the ragged last wave). Only for
   // a few waves of blocks: with hundreds of waves the tail is noise and the host sort is not.
+  // wide blocks (more than 8192 sequences) go to their own launch of the decoder (twice the
+  // per-thread sequence registers)
+  const int nn = (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.wide; }) -
+                       db->jobs.begin());
 #ifndef DG_NO_LPT
-  if (n <= 16 * 256)
-    std::stable_sort(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; });
+  auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
+  if (nn <= 16 * 256) std::stable_sort(db->jobs.begin(), db->jobs.begin() + nn, by_ncp);
+  if (n - nn <= 16 * 256) std::stable_sort(db->jobs.begin() + nn, db->jobs.end(), by_ncp);
 #endif
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
@@ -1092,7 +1099,8 @@ static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_
   if (!h || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
-  launch_lz4_decode(d, n, d_err, st, d_prof);
+  launch_lz4_decode(d, nn, 0, d_err, st, d_prof);
+  launch_lz4_decode(d + nn, n - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
 
@@ -3234,6 +3242,7 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.comp_len.resize(n);
   b.cp_off.resize(n);
   b.cp_n.resize(n);
+  b.cp_wide.assign(n, 0);
   b.dec_len.resize(n);
   int64_t total = 0;
   for (int i = 0; i < n; ++i) {
@@ -3247,7 +3256,9 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
     std::vector<uint32_t> one;
-    const int d = lz4_index_block(blocks[i], lens[i], &one);
+    int wide = 0;
+    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide);
+    b.cp_wide[i] = (uint8_t)wide;
     b.cp_off[i] = (int64_t)cps.size();
     b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size();
     b.dec_len[i] = d < 0 ? 0 : d;

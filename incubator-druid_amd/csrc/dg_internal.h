@@ -41,9 +41,12 @@ struct ColView {
 constexpr int32_t kViewBigEndian = 1;
 
 // LZ4 sequence checkpoints: built once per block at attach (lz4_index_block), one entry per
-// kLzSeqPerCp sequences = the compressed offset where that sequence's token starts. They let the
-// decoder parse every interval of a block in parallel; the bytes themselves stay LZ4.
-constexpr int kLzSeqPerCp = 16;
+// kLzSeqPerCp sequences (2 * kLzSeqPerCp for the rare block with more than kLzMaxCps * kLzSeqPerCp
+// sequences) = the compressed offset where that sequence's token starts. They let the decoder
+// parse every interval of a block in parallel (one interval per thread); the bytes stay LZ4.
+constexpr int kLzSeqPerCp = 8;
+constexpr int kLzMaxSeqPerCp = 2 * kLzSeqPerCp;  // the decoder's per-thread register budget
+constexpr int kLzMaxCps = 1024;                  // one interval per decoder thread
 
 // One LZ4 block to decode (compressed bytes are 16-byte aligned in the device image).
 struct Lz4Job {
@@ -54,6 +57,8 @@ struct Lz4Job {
   int32_t expect_len;  // bytes that must come out (>= rows * width of the block)
   int32_t ncp;         // number of checkpoints; < 0: the block failed validation at attach
   int32_t dec_len;     // decoded length found at attach
+  int32_t wide;        // checkpoints every 2 * kLzSeqPerCp sequences (decoded by the wide kernel)
+  int32_t pad;
 };
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
@@ -80,7 +85,8 @@ struct VsJob {
 
 // Host-side validating parse of one LZ4 block (lz4-java safe-decompressor semantics): appends the
 // block's checkpoints to *cps and returns the decoded length, or -1 for a malformed block.
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps);
+// *wide: the block keeps every other checkpoint (more than kLzMaxCps * kLzSeqPerCp sequences).
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide);
 
 struct AggPlan {
   int32_t n;
@@ -190,6 +196,7 @@ struct BlockColumn {
   std::vector<int32_t> comp_len;
   std::vector<int64_t> cp_off;         // LZ4: first checkpoint of block b inside cps
   std::vector<int32_t> cp_n;           // LZ4: checkpoints of block b (-1: malformed block)
+  std::vector<uint8_t> cp_wide;        // LZ4: block b keeps a checkpoint every 2 * kLzSeqPerCp sequences
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
   int64_t index_bytes = 0;             // LZ4: bytes of the checkpoint index (read per query)
   DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)
@@ -307,8 +314,9 @@ int set_error(int code, const char* fmt, ...);
 int load_segment(Context* ctx, const char* dir, Segment** out);
 
 // kernel launchers (dg_kernels.hip)
-constexpr int kLz4ProfWords = 12;  // per-block phase stamps of the decoder (diagnostic builds of the call)
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (diagnostic builds of the call)
+// blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
+void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // VSizeLongSerde.getSerializedSize (VSizeLongSerde.java:61-65)

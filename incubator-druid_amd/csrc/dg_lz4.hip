@@ -8,9 +8,10 @@
 // [1 literal byte, 7-byte match] whose matches copy bytes earlier matches produced (copy chains up
 // to ~300 deep), so neither a lane walking the token stream nor match-by-match copying is fast. The
 // block is decoded in four data-parallel phases, all in LDS:
-//   1. parse: the attach-time checkpoint index (lz4_index_block: the token offset of every 16th
-//      sequence) gives every thread its own 16 sequences; it parses them from the staged input into
-//      registers (literal start, literal length, distance, match length);
+//   1. parse: the attach-time checkpoint index (lz4_index_block: the token offset of every 8th
+//      sequence, every 16th in blocks of more than 8192) gives every thread its own interval; it
+//      parses those sequences from the staged input into registers (literal start or bytes,
+//      literal length, distance, match length);
 //   2. a block scan of the threads' output lengths places every sequence; each output byte x gets a
 //      16-bit entry E[x] in LDS: a literal is 0xFF00 | byte, a match byte the distance to the byte
 //      it copies (LZ4 overlap semantics: src = start - dist + (k mod dist));
@@ -21,10 +22,8 @@
 // literals are re-read from the compressed block in HBM/L2). Entries >= 0xFF00 are literals, so a
 // distance must stay below 0xFF00: the last 256 output positions, whose distances can exceed it,
 // keep absolute source positions in a small tail table and are resolved by a short chase.
-// The sequential one-wave decoder (k_lz4_decode_seq) stays as a differential reference, DG_LZ4_SEQ=1.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 
 #include "dg_internal.h"
 
@@ -40,11 +39,12 @@ static_assert(kShortLit <= 4, "Tok::lv holds four literal bytes");
 constexpr int kLongFill = 48;                  // matches above this are filled cooperatively
 constexpr int kMaxJobs = 2048;
 constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
-constexpr int kJumpBatch = 8;                 // steps of a jump sweep whose reads are issued together
+constexpr int kJumpBatch = 4;                 // steps of a jump sweep whose reads are issued together
 constexpr int kMaxRounds = 20;                 // > log2(65536) + 1: pointer jumping always converges before
 constexpr int kClass = 8;                      // the value width whose distance-8 copy chains are scanned
 static_assert(kLz4InCap + 32 <= kBlockBytes * 2, "staged input must fit in the E array");
-static_assert(kLzThreads * kLzSeqPerCp >= kBlockBytes / 4, "a block can hold 16384 sequences");
+static_assert(kLzMaxCps == kLzThreads, "one checkpoint interval per thread");
+static_assert(kLzThreads * kLzMaxSeqPerCp >= kBlockBytes / 4, "a block can hold 16384 sequences");
 
 struct Tok {
   int lit;   // literal start (input offset)
@@ -74,7 +74,8 @@ __device__ __forceinline__ bool ext_len(const uint8_t* __restrict__ in, int n, i
   }
 }
 
-// Byte-wise parse (long lengths / windows that do not hold the offset).
+// Byte-wise parse (long lengths / windows that do not hold the offset); out of line: rare, and the
+// decoder's per-sequence loops are unrolled.
 __device__ __forceinline__ bool parse_tok_slow(const uint8_t* __restrict__ in, int n, int p, Tok& t) {
   if (p >= n) return false;
   const int tk = in[p];
@@ -189,10 +190,50 @@ __device__ __forceinline__ void put_ptr(const LzState& S, int x, int src) {
   else S.tsrc[x - kTail] = (uint16_t)src;
 }
 
-// value of output byte x once E and the tail table have converged (both hold literal codes)
+// value of output byte x once E and the tail table have converged (literal codes, or in E one hop
+// from one)
 __device__ __forceinline__ uint32_t lz_value(const LzState& S, int x) {
-  if (x < kTail) return S.e[eph(x)] & 0xFF;
+  if (x < kTail) {
+    uint32_t e = S.e[eph(x)];
+    if (e < (uint32_t)kTail) e = S.e[eph(x - (int)e)];  // class mode: one hop from the code
+    return e & 0xFF;
+  }
   return S.tsrc[x - kTail] & 0xFF;
+}
+
+// E entries of one sequence in the general form (out of line: the rare cases): literals that did not
+// get a job (table full; read from the compressed block in HBM, `lit` = input offset) or whose
+// bytes ride in `lv`, matches without a job, and sequences reaching the tail table.
+__device__ __noinline__ void fill_general(uint16_t* e, uint16_t* tsrc, uint32_t* tlit, const uint8_t* __restrict__ gin, int o, int L, int M, int d,
+                                          uint32_t lv, bool lit_inline, bool lit_here, bool match_here) {
+  const LzState S{e, tsrc, tlit};
+  if (lit_inline) {
+    for (int k = 0; k < L; ++k) put_lit(S, o + k, gin[lv + k]);
+  } else if (lit_here) {
+    for (int k = 0; k < L; ++k) put_lit(S, o + k, (lv >> (8 * k)) & 0xFF);
+  }
+  if (match_here) {
+    const int om = o + L;
+    int r = 0;
+    for (int k = 0; k < M; ++k) {
+      put_ptr(S, om + k, (d >= M || d == kClass) ? om + k - d : om - d + r);
+      if (++r == d) r = 0;
+    }
+  }
+}
+
+// Wave-aggregated slot allocation: each lane asking for n slots gets its first slot index.
+__device__ __forceinline__ int wave_alloc(int* counter, int n) {
+  int incl = n;  // inclusive prefix of n over the lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if ((int)(threadIdx.x & 63) >= o) incl += y;
+  }
+  const int total = __shfl(incl, 63, 64);
+  int base = 0;
+  if ((threadIdx.x & 63) == 63 && total) base = atomicAdd(counter, total);
+  return __shfl(base, 63, 64) + incl - n;
 }
 
 #define LZ_STAMP(k)                                                                           \
@@ -204,27 +245,29 @@ __device__ __forceinline__ uint32_t lz_value(const LzState& S, int x) {
 // match distance | 1 << 31 (kind 1)
 __device__ __forceinline__ int job_len(uint2 j) { return (int)(j.x >> 16) + 1; }
 
-template <bool PROF>
+template <bool PROF, int SEQ>
 __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
                                                            uint64_t* __restrict__ prof) {
   __shared__ __attribute__((aligned(16))) uint16_t s_e[kEWords];  // 130 KiB: staged input, then E
   __shared__ uint16_t s_tsrc[kTailN];
   __shared__ uint32_t s_tlit[kTailN / 32];
-  __shared__ uint2 s_job[kMaxJobs];
-  __shared__ int s_jpre[kMaxJobs];
-  __shared__ int s_njob, s_bad, s_c8;
+  __shared__ uint2 s_jobs_buf[kMaxJobs + kMaxJobs / 2];  // jobs, then their prefix sums; later the open list
+  uint2* s_job = s_jobs_buf;
+  int* s_jpre = reinterpret_cast<int*>(s_jobs_buf + kMaxJobs);
+  __shared__ int s_njob, s_bad, s_c8, s_nopen;
   __shared__ int s_tmp[kLzWaves];
 
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x;
   const int n = job.src_len, ncp = job.ncp;
-  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzThreads || job.dec_len > kBlockBytes ||
+  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.dec_len > kBlockBytes ||
       job.dec_len < job.expect_len) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
   LZ_STAMP(0);
   uint8_t* s_in = reinterpret_cast<uint8_t*>(s_e);
+  uint32_t* s_e32 = reinterpret_cast<uint32_t*>(s_e);
   const LzState S{s_e, s_tsrc, s_tlit};
   // ---- stage the compressed block (16-byte aligned and padded in the device image) ----
   {
@@ -242,14 +285,15 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   }
   __syncthreads();
   LZ_STAMP(1);
-  // ---- 1. parse my interval of kLzSeqPerCp sequences into registers ----
-  uint32_t r_L[kLzSeqPerCp], r_DM[kLzSeqPerCp], r_lv[kLzSeqPerCp];  // r_lv: literal bytes (L <= 4) or offset
+  // ---- 1. parse my interval (<= SEQ sequences: kLzSeqPerCp, or 2 * kLzSeqPerCp in a wide block)
+  // into registers ----
+  uint32_t r_L[SEQ], r_DM[SEQ], r_lv[SEQ];  // r_lv: literal bytes (L <= 4) or offset
   int cnt = 0, out_rel = 0;
   if (tid < ncp) {
     int pos = (int)job.cp[tid];
     const int end = tid + 1 < ncp ? (int)job.cp[tid + 1] : n;
 #pragma unroll
-    for (int s = 0; s < kLzSeqPerCp; ++s) {
+    for (int s = 0; s < SEQ; ++s) {
       if (pos < end) {
         Tok t;
         if (parse_tok(s_in, n, pos, t)) {
@@ -273,110 +317,217 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     if (tid == 0) atomicOr(err, 1);
     return;
   }
-  // ---- 2. E entries: short literals from registers, short matches as distances; longer runs
-  // become jobs for the cooperative pass (their literals come from the compressed block in HBM) ----
+  // ---- 2. long runs (literals > kShortLit bytes, matches > kLongFill) become jobs; the jobs'
+  // bytes form one flat range split evenly over the threads, and each thread reads the literal
+  // bytes of its range from the staged input into registers before any E entry is written over it.
+  // Then every thread writes the E entries of its own short runs (literal codes from the parse
+  // registers, distances) and of its job range. ----
   const uint8_t* __restrict__ gin = job.src;
-  int c8 = 0;  // my match bytes at distance 8 (class chains of 8-byte values, resolved by a scan below)
+  constexpr uint32_t kInlineLit = 0x80000000u, kInlineMatch = 0x40000000u;  // r_L flags: job table full
+  int c8 = 0;  // match bytes at distance 8 (class chains of 8-byte values, resolved by a scan below)
+  {  // (every lane of the wave takes part: slot allocation is wave-aggregated)
+    int o = base;
+#pragma unroll
+    for (int s = 0; s < SEQ; ++s) {
+      const bool act = s < cnt;  // (cnt = 0 beyond the checkpoints)
+      const int L = act ? (int)r_L[s] : 0;
+      const int d = (int)(r_DM[s] & 0xFFFF), M = act ? (int)(r_DM[s] >> 16) : 0;
+      const int nl = L > kShortLit, nm = M > kLongFill;
+      if (__ballot(nl | nm)) {  // job slots: one LDS atomic per wave
+        const int j = wave_alloc(&s_njob, nl + nm);
+        if (nl) {
+          if (j < kMaxJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(L - 1) << 16), r_lv[s]);
+          else r_L[s] |= kInlineLit;
+        }
+        if (nm) {
+          if (j + nl < kMaxJobs) s_job[j + nl] = make_uint2((uint32_t)(o + L) | ((uint32_t)(M - 1) << 16), (uint32_t)d | 0x80000000u);
+          else r_L[s] |= kInlineMatch;
+        }
+      }
+      c8 += d == kClass ? M : 0;
+      o += L + M;
+    }
+    for (int off = 32; off > 0; off >>= 1) c8 += __shfl_xor(c8, off, 64);  // wave sum, one LDS atomic
+    if ((tid & 63) == 0 && c8) atomicAdd(&s_c8, c8);
+  }
+  __syncthreads();
+  const int nj = min(s_njob, kMaxJobs);
+  int tot = 0;
+  if (nj > 0) {
+    int l0 = 0, l1 = 0;
+    if (2 * tid < nj) l0 = job_len(s_job[2 * tid]);
+    if (2 * tid + 1 < nj) l1 = job_len(s_job[2 * tid + 1]);
+    const int pre = block_scan_lz(l0 + l1, &tot, s_tmp);
+    if (2 * tid < nj) s_jpre[2 * tid] = pre;
+    if (2 * tid + 1 < nj) s_jpre[2 * tid + 1] = pre + l0;
+    __syncthreads();
+  }
+  // my contiguous range of the flat job bytes (<= 64: jobs cover distinct output positions)
+  const int per = (tot + kLzThreads - 1) / kLzThreads;
+  const int g0 = tid * per, gend = min(g0 + per, tot);
+  int j0 = 0;
+  if (g0 < gend) {  // last job with s_jpre <= g0
+    int lo = 0, hi = nj - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_jpre[mid] <= g0) lo = mid;
+      else hi = mid - 1;
+    }
+    j0 = lo;
+  }
+  uint32_t lit4[16];  // the literal bytes of my range, four per register
+#pragma unroll
+  for (int q = 0; q < 16; ++q) lit4[q] = 0;
+  // walk of my range over the jobs (jobs hold >= 5 bytes: at most one step per 4 positions)
+  int wj = j0, wjs = 0, wje = 0;
+  uint2 wjb = make_uint2(0, 0);
+  auto walk_reset = [&]() {
+    wj = j0;
+    wjs = s_jpre[wj];
+    wjb = s_job[wj];
+    wje = wjs + job_len(wjb);
+  };
+  auto walk_to = [&](int pos) {
+    if (pos >= wje) {
+      ++wj;
+      wjs = s_jpre[wj];
+      wjb = s_job[wj];
+      wje = wjs + job_len(wjb);
+    }
+  };
+  if (g0 < gend) {
+    walk_reset();
+    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(s_in);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int pq = g0 + 4 * q;
+      if (pq < gend) {
+        walk_to(pq);
+        uint32_t w = 0;
+        if (pq + 4 <= wje && pq + 4 <= gend) {  // four bytes of one job: one unaligned read
+          if (!(wjb.y & 0x80000000u)) {
+            const int src = (int)wjb.y + (pq - wjs);
+            w = __builtin_amdgcn_alignbyte(in32[(src >> 2) + 1], in32[src >> 2], src & 3);
+          }
+        } else {
+#pragma unroll 1
+          for (int i = 0; i < 4; ++i) {
+            if (pq + i < gend) {
+              walk_to(pq + i);
+              if (!(wjb.y & 0x80000000u)) w |= (uint32_t)s_in[wjb.y + (pq + i - wjs)] << (8 * i);
+            }
+          }
+        }
+        lit4[q] = w;
+      }
+    }
+  }
+  __syncthreads();  // every read of the staged input is done
+  // class mode (mostly distance-8 matches): E starts as all 8, and the fill skips distance-8 matches
+  const bool cls = s_c8 * 4 > total;
+  if (cls) {
+    uint4* e4 = reinterpret_cast<uint4*>(s_e);
+    const uint4 eight = make_uint4(0x00080008u, 0x00080008u, 0x00080008u, 0x00080008u);
+    for (int i = tid; i < kEWords / 8; i += kLzThreads) e4[i] = eight;
+    __syncthreads();
+  }
+  LZ_STAMP(3);
   if (tid < ncp) {
     int o = base;
 #pragma unroll
-    for (int s = 0; s < kLzSeqPerCp; ++s) {
+    for (int s = 0; s < SEQ; ++s) {
       if (s < cnt) {
-        const int L = (int)r_L[s];
+        const uint32_t lf = r_L[s];
+        const int L = (int)(lf & 0x3FFFFFFFu);
         const int d = (int)(r_DM[s] & 0xFFFF), M = (int)(r_DM[s] >> 16);
-        if (L <= kShortLit) {
-          const uint32_t lv = r_lv[s];
+        const bool fast = !(lf & (kInlineLit | kInlineMatch)) && o + L + M <= kTail;
+        if (fast) {  // the common case: plain E entries, no tail table
+          if (L <= kShortLit) {
+            const uint32_t lv = r_lv[s];
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (k < L) put_lit(S, o + k, (lv >> (8 * k)) & 0xFF);
-        } else {
-          const int j = atomicAdd(&s_njob, 1);
-          if (j < kMaxJobs) {
-            s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(L - 1) << 16), r_lv[s]);
-          } else {
-            for (int k = 0; k < L; ++k) put_lit(S, o + k, gin[r_lv[s] + k]);
+            for (int k = 0; k < kShortLit; ++k)
+              if (k < L) S.e[eph(o + k)] = (uint16_t)(0xFF00u | ((lv >> (8 * k)) & 0xFFu));
           }
+          if (M > 0 && M <= kLongFill && !(cls && d == kClass)) {
+            const int om = o + L;
+            if (d >= M || d == kClass) {  // one distance for the whole match (distance 8: class chains), by pairs
+              int x = om;
+              const int xe = om + M;
+              if (x & 1) S.e[eph(x++)] = (uint16_t)d;
+              const uint32_t dd = (uint32_t)d * 0x10001u;
+              for (; x + 2 <= xe; x += 2) s_e32[eph(x) >> 1] = dd;
+              if (x < xe) S.e[eph(x)] = (uint16_t)d;
+            } else {  // overlapping: byte k copies the first period, distance d * (1 + k / d)
+              int r = 0, dk = d;
+              for (int k = 0; k < M; ++k) {
+                S.e[eph(om + k)] = (uint16_t)dk;
+                if (++r == d) { r = 0; dk += d; }
+              }
+            }
+          }
+        } else {
+          fill_general(s_e, s_tsrc, s_tlit, gin, o, L, M, d, r_lv[s], (lf & kInlineLit) != 0, L <= kShortLit,
+                       (lf & kInlineMatch) != 0 || (M > 0 && M <= kLongFill));
         }
         o += L;
         if (M > 0) {
           if (d > o) s_bad = 1;
-          c8 += d == 8 ? M : 0;
-          int j = kMaxJobs;
-          if (M > kLongFill) {
-            j = atomicAdd(&s_njob, 1);
-            if (j < kMaxJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(M - 1) << 16), (uint32_t)d | 0x80000000u);
-          }
-          if (j >= kMaxJobs) {
-            if (d >= M || d == kClass) {  // distance 8: plain x - 8 (same value, same class chain)
-              for (int k = 0; k < M; ++k) put_ptr(S, o + k, o + k - d);
-            } else {
-              int r = 0;
-              for (int k = 0; k < M; ++k) {
-                put_ptr(S, o + k, o - d + r);
-                if (++r == d) r = 0;
-              }
-            }
-          }
           o += M;
         }
       }
     }
   }
-  if (c8) atomicAdd(&s_c8, c8);
-  __syncthreads();
-  LZ_STAMP(3);
-  // ---- cooperative pass: the jobs' bytes as one flat range, split evenly over the threads ----
-  const int nj = min(s_njob, kMaxJobs);
-  if (nj > 0) {
-    int l0 = 0, l1 = 0;
-    if (2 * tid < nj) l0 = job_len(s_job[2 * tid]);
-    if (2 * tid + 1 < nj) l1 = job_len(s_job[2 * tid + 1]);
-    int tot;
-    const int pre = block_scan_lz(l0 + l1, &tot, s_tmp);
-    if (2 * tid < nj) s_jpre[2 * tid] = pre;
-    if (2 * tid + 1 < nj) s_jpre[2 * tid + 1] = pre + l0;
-    __syncthreads();
-    // flat positions interleaved over the threads (f = tid, tid + 1024, ...): a wave's 64 lanes take
-    // 64 consecutive positions, so the literal byte loads of a long run are one cache line per wave
-    // instruction and the E stores consecutive; each lane's job index only moves forward
-    auto find_job = [&](int f, int lo) {  // last job with s_jpre <= f, searching from lo
-      int hi = nj - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_jpre[mid] <= f) lo = mid;
-        else hi = mid - 1;
-      }
-      return lo;
-    };
-    int j = 0;
-    for (int fb = tid; fb < tot; fb += 8 * kLzThreads) {
-      int xs[8], srcs[8];
-      uint32_t vals[8];
+  if (PROF && (tid & 63) == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + 16 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
+  if (g0 < gend) {  // my job range: literal codes from lit4, distances for long matches
+    walk_reset();
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        xs[u] = -1;
-        const int g = fb + u * kLzThreads;
-        if (g < tot) {
-          if (g >= s_jpre[j] + job_len(s_job[j])) j = find_job(g, j);
-          const uint2 jb = s_job[j];
-          const int k = g - s_jpre[j], o = (int)(jb.x & 0xFFFF);
-          xs[u] = o + k;
-          if (jb.y & 0x80000000u) {
-            const int d = (int)(jb.y & 0xFFFF);
-            srcs[u] = (d >= job_len(jb) || d == kClass) ? o + k - d : o - d + k % d;
+    for (int q = 0; q < 16; ++q) {
+      const int pq = g0 + 4 * q;
+      if (pq < gend) {
+        walk_to(pq);
+        const int o = (int)(wjb.x & 0xFFFF), x = o + (pq - wjs);
+        const bool lit = !(wjb.y & 0x80000000u);
+        const int d = (int)(wjb.y & 0xFFFF), M = job_len(wjb);
+        const bool flat = pq + 4 <= wje && pq + 4 <= gend && x + 4 <= kTail && (x & 127) <= 124;
+        if (flat && lit) {  // four literal codes in one 128-entry skew span
+          const uint32_t w = lit4[q];
+          const uint32_t c01 = 0xFF00FF00u | (w & 0xFFu) | ((w & 0xFF00u) << 8);
+          const uint32_t c23 = 0xFF00FF00u | ((w >> 16) & 0xFFu) | ((w >> 8) & 0xFF0000u);
+          if (!(x & 1)) {
+            s_e32[eph(x) >> 1] = c01;
+            s_e32[(eph(x) >> 1) + 1] = c23;
           } else {
-            srcs[u] = -1 - ((int)jb.y + k);  // literal: input offset, encoded negative
+            S.e[eph(x)] = (uint16_t)c01;
+            s_e32[(eph(x) + 1) >> 1] = (c01 >> 16) | (c23 << 16);
+            S.e[eph(x) + 3] = (uint16_t)(c23 >> 16);
+          }
+        } else if (flat && (d >= M || d == kClass)) {  // four entries of one distance
+          if (!(cls && d == kClass)) {
+            const uint32_t dd = (uint32_t)d * 0x10001u;
+            if (!(x & 1)) {
+              s_e32[eph(x) >> 1] = dd;
+              s_e32[(eph(x) >> 1) + 1] = dd;
+            } else {
+              S.e[eph(x)] = (uint16_t)d;
+              s_e32[(eph(x) + 1) >> 1] = dd;
+              S.e[eph(x) + 3] = (uint16_t)d;
+            }
+          }
+        } else {
+#pragma unroll 1
+          for (int i = 0; i < 4; ++i) {
+            if (pq + i < gend) {
+              walk_to(pq + i);
+              const int k = pq + i - wjs, oo = (int)(wjb.x & 0xFFFF);
+              if (wjb.y & 0x80000000u) {
+                const int dj = (int)(wjb.y & 0xFFFF);
+                put_ptr(S, oo + k, (dj >= job_len(wjb) || dj == kClass) ? oo + k - dj : oo - dj + k % dj);
+              } else {
+                put_lit(S, oo + k, (lit4[q] >> (8 * i)) & 0xFF);
+              }
+            }
           }
         }
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (xs[u] >= 0 && srcs[u] < 0) vals[u] = gin[-1 - srcs[u]];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (xs[u] < 0) continue;
-        if (srcs[u] < 0) put_lit(S, xs[u], vals[u]);
-        else put_ptr(S, xs[u], srcs[u]);
       }
     }
   }
@@ -386,129 +537,223 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     return;
   }
   LZ_STAMP(4);
-  // ---- 3. pointer jumping with value propagation over positions [0, min(total, kTail)):
-  // E[x] += E[x - E[x]] while that target holds a distance; once it holds a literal code, x takes
-  // the code itself, so later readers of x resolve in one step. My pairs stay in registers. ----
+  // ---- 3. resolution over positions [0, min(total, kTail)). Every E entry is a literal code or a
+  // distance to an earlier byte of the same value; jumping (E[x] += E[x - E[x]], or the target's
+  // code once it is a literal) rewrites distances until only literal codes remain.
+  //
+  // Class mode: a byte copied from 8 back (E == 8) has the value of the last byte before it in its
+  // residue class mod 8 whose entry is not 8 (its "terminal"). Value columns of 8-byte values
+  // (sequential longs, timestamps) are ~99 % distance-8 matches chaining through the whole block; in
+  // such blocks a carry scan gives every E == 8 entry the distance to its terminal and lists the
+  // terminals that are still distances (the few matches at other distances). Jumping over that list
+  // resolves the terminals (through the scanned entries, one hop per class chain), and one final
+  // sweep gives every scanned entry its terminal's code.
+  //
+  // Otherwise: wave w sweeps its own 4 KiB of positions in increasing order, so a position sees the
+  // updates of the earlier batches of its wave (LDS ops of one wave complete in order); the pairs
+  // still open after that first sweep are listed and later rounds only visit the list. Both lists
+  // live in the job tables' space; on overflow the rounds fall back to full sweeps. ----
   const int lim = min(total, kTail);
-  uint32_t* s_e32 = reinterpret_cast<uint32_t*>(s_e);
-  // positions in [lim, 2 * kPairs * kLzThreads) act as resolved literals
+  // positions in [lim, kTail) act as resolved literals
   if (lim < kTail) {
     for (int x = lim + tid; x < kTail; x += kLzThreads) s_e[eph(x)] = 0xFF00;
   }
-#ifndef DG_LZ_NOSCAN8
-  // ---- 2b. class chains: a byte copied from 8 back holds the value of the last "terminal" (a
-  // literal, or a byte of a match at another distance) of its residue class mod 8 before it. A
-  // carry scan over the block turns every distance-8 entry into the distance to that terminal, so
-  // the jumping below only has to chase the few other matches (8-byte value columns: sequential
-  // longs and timestamps are ~99.5 % distance-8 matches chaining through the whole block). ----
-  if (s_c8 * 4 > total) {
-    __syncthreads();
-    const int x0 = tid * 64;
-    // my 64 entries as pairs (read twice: keeping them in registers spills); positions >= lim read
-    // as literals
-    auto pair_at = [&](int q) { return x0 + 2 * q < lim ? s_e32[eph(x0 + 2 * q) >> 1] : 0xFF00FF00u; };
-    int last[kClass];
-#pragma unroll
-    for (int c = 0; c < kClass; ++c) last[c] = -1;
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int c = (2 * q) & 7;
-      const uint32_t v = pair_at(q);
-      if ((v & 0xFFFF) != (uint32_t)kClass) last[c] = x0 + 2 * q;
-      if ((v >> 16) != (uint32_t)kClass) last[c + 1] = x0 + 2 * q + 1;
-    }
-    // exclusive max-scan of the per-class last terminal over the threads (positions grow with tid)
-    const int lane = tid & 63, wave = tid >> 6;
-    int carry[kClass];
-    int* s_scan = s_jpre;  // free after the cooperative pass: [kLzWaves][kClass]
-#pragma unroll
-    for (int c = 0; c < kClass; ++c) {
-      int v = last[c];
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(v, o, 64);
-        if (lane >= o) v = max(v, y);
-      }
-      const int ex = __shfl_up(v, 1, 64);
-      carry[c] = lane ? ex : -1;
-      if (lane == 63) s_scan[wave * kClass + c] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < kClass; ++c)
-      for (int w = 0; w < wave; ++w) carry[c] = max(carry[c], s_scan[w * kClass + c]);
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int c = (2 * q) & 7, x = x0 + 2 * q;
-      const uint32_t v = pair_at(q);
-      uint32_t lo = v & 0xFFFF, hi = v >> 16;
-      if (lo == (uint32_t)kClass) {
-        if (carry[c] >= 0) lo = (uint32_t)(x - carry[c]);
-      } else {
-        carry[c] = x;
-      }
-      if (hi == (uint32_t)kClass) {
-        if (carry[c + 1] >= 0) hi = (uint32_t)(x + 1 - carry[c + 1]);
-      } else {
-        carry[c + 1] = x + 1;
-      }
-      const uint32_t nv = lo | (hi << 16);
-      if (nv != v && x < lim) s_e32[eph(x) >> 1] = nv;
-    }
-  }
-#endif
-  bool any = true;
-  int jump_rounds = 0;
-  // Rounds of jumping. Wave w sweeps its own 4 KiB of positions in increasing order, 64 pairs per
-  // step, so within a round a position already sees the updates of the earlier steps of its wave
-  // (LDS ops of one wave complete in order): chains collapse to the region start in one round, and
-  // the rounds only have to jump across the 16 regions. A batch of kJumpBatch steps issues its
-  // reads back to back; a resolved position reads itself; only changed pairs are written.
+  uint16_t* s_open = reinterpret_cast<uint16_t*>(s_job);  // pair indices, or positions in class mode
+  constexpr int kOpenCap = (kMaxJobs + kMaxJobs / 2) * (int)sizeof(uint2) / 2;
+  __shared__ uint32_t s_scan[kLzWaves * kClass];
+  if (tid == 0) s_nopen = 0;
+  __syncthreads();
   const int wv = tid >> 6, ln = tid & 63;
-  uint32_t done = 0;  // wave-uniform: batch b of my wave's region is fully resolved
-  for (int round = 0; __syncthreads_or(any); ++round) {
-    if (round > kMaxRounds) {  // unreachable for a valid block
-      if (tid == 0) atomicOr(err, 1);
-      return;
+  auto list_append = [&](bool op, int v) {  // wave-aggregated append to s_open
+    const uint64_t bal = __ballot(op);
+    if (bal) {
+      int at = 0;
+      if (ln == 0) at = atomicAdd(&s_nopen, __popcll(bal));
+      at = __shfl(at, 0, 64) +
+           (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+      if (op && at < kOpenCap) s_open[at] = (uint16_t)v;
     }
-    jump_rounds++;
-    any = false;
+  };
+  auto is_open = [](uint32_t v) { return (v & 0xFFFF) < (uint32_t)kTail || (v >> 16) < (uint32_t)kTail; };
+  // one jump step for an entry d whose target holds e
+  auto jstep = [](uint32_t d, uint32_t e) -> uint32_t {
+    return d >= (uint32_t)kTail ? d : (e >= (uint32_t)kTail ? e : d + e);
+  };
+  // full sweep of my wave's region, one step per open entry; with `mark`, the pairs still open
+  // afterwards are set in the open-pair bitmap s_obits (a step's 64 lanes are 64 consecutive pairs:
+  // its ballot is two bitmap words). Returns whether any of my entries is still open.
+  uint32_t* s_obits = reinterpret_cast<uint32_t*>(s_jobs_buf);  // kBlockBytes / 2 bits (non-class mode)
+  auto sweep = [&](bool mark) -> bool {
+    bool any = false;
 #pragma unroll 1
     for (int b = 0; b < kPairs / kJumpBatch; ++b) {
-      if ((done >> b) & 1u) continue;
       const int j0 = b * kJumpBatch;
       uint32_t dv[kJumpBatch], ta[kJumpBatch], tb[kJumpBatch];
+      bool need = false;
 #pragma unroll
       for (int k = 0; k < kJumpBatch; ++k) {
         const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
         dv[k] = x < kTail ? s_e32[eph(x) >> 1] : 0xFF00FF00u;
+        need |= is_open(dv[k]);
+      }
+      if (__ballot(need) == 0) {
+        if (mark && ln < 2 * kJumpBatch) s_obits[((wv * (kPairs * 64) + j0 * 64) >> 5) + ln] = 0u;
+        continue;
       }
 #pragma unroll
       for (int k = 0; k < kJumpBatch; ++k) {
         const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
-        const uint32_t v = dv[k], d0 = v & 0xFFFF, d1 = v >> 16;
-        const int a0 = x - (d0 < (uint32_t)kTail ? (int)d0 : 0);
-        const int a1 = x + 1 - (d1 < (uint32_t)kTail ? (int)d1 : 0);
-        // a resolved entry (literal code) needs no target read
-        ta[k] = (x < kTail && d0 < (uint32_t)kTail) ? s_e[eph(a0)] : 0xFF00u;
-        tb[k] = (x < kTail && d1 < (uint32_t)kTail) ? s_e[eph(a1)] : 0xFF00u;
+        const uint32_t d0 = dv[k] & 0xFFFF, d1 = dv[k] >> 16;
+        ta[k] = d0 < (uint32_t)kTail ? s_e[eph(x - (int)d0)] : 0xFF00u;
+        tb[k] = d1 < (uint32_t)kTail ? s_e[eph(x + 1 - (int)d1)] : 0xFF00u;
       }
-      bool open = false;
 #pragma unroll
       for (int k = 0; k < kJumpBatch; ++k) {
         const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
-        const uint32_t v = dv[k], d0 = v & 0xFFFF, d1 = v >> 16;
-        const uint32_t e0 = ta[k], e1 = tb[k];
-        const uint32_t n0 = d0 >= (uint32_t)kTail ? d0 : (e0 >= (uint32_t)kTail ? e0 : d0 + e0);
-        const uint32_t n1 = d1 >= (uint32_t)kTail ? d1 : (e1 >= (uint32_t)kTail ? e1 : d1 + e1);
-        const uint32_t nv = n0 | (n1 << 16);
-        if (nv != v) s_e32[eph(x) >> 1] = nv;
-        open |= n0 < (uint32_t)kTail || n1 < (uint32_t)kTail;
+        const uint32_t nv = jstep(dv[k] & 0xFFFF, ta[k]) | (jstep(dv[k] >> 16, tb[k]) << 16);
+        if (nv != dv[k]) s_e32[eph(x) >> 1] = nv;
+        const bool op = is_open(nv);
+        any |= op;
+        if (mark) {
+          const uint64_t bal = __ballot(op);
+          const int w0 = (wv * (kPairs * 64) + (j0 + k) * 64) >> 5;
+          if (ln == 0) s_obits[w0] = (uint32_t)bal;
+          if (ln == 32) s_obits[w0 + 1] = (uint32_t)(bal >> 32);
+        }
       }
-      if (__ballot(open) == 0) done |= 1u << b;
-      any |= open;
+    }
+    return any;
+  };
+  int jump_rounds = 0;
+  if (cls) {
+    // carry scan over my 64 positions [tid * 64, tid * 64 + 64). A terminal travels as key
+    // (position + 1) << 16 | its entry (0 = none yet); an E == 8 entry takes the terminal's literal
+    // code, or the distance to the terminal while that is still open.
+    const int x0 = tid * 64;
+    auto pair_at = [&](int q) { return x0 + 2 * q < lim ? s_e32[eph(x0 + 2 * q) >> 1] : 0xFF00FF00u; };
+    uint32_t last[kClass];
+#pragma unroll
+    for (int c = 0; c < kClass; ++c) last[c] = 0;
+#pragma unroll 1
+    for (int q0 = 0; q0 < 32; q0 += 4) {  // 4 pairs (one residue-class period) per step
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = q0 + j, c = 2 * j;
+        const uint32_t v = pair_at(q);
+        if ((v & 0xFFFF) != (uint32_t)kClass) last[c] = ((uint32_t)(x0 + 2 * q + 1) << 16) | (v & 0xFFFF);
+        if ((v >> 16) != (uint32_t)kClass) last[c + 1] = ((uint32_t)(x0 + 2 * q + 2) << 16) | (v >> 16);
+      }
+    }
+    uint32_t carry[kClass];
+#pragma unroll
+    for (int c = 0; c < kClass; ++c) {  // exclusive max-scan over the threads (positions grow with tid)
+      uint32_t v = last[c];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(v, o, 64);
+        if (ln >= o) v = max(v, y);
+      }
+      const uint32_t ex = __shfl_up(v, 1, 64);
+      carry[c] = ln ? ex : 0u;
+      if (ln == 63) s_scan[wv * kClass + c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < kClass; ++c)
+      for (int w = 0; w < wv; ++w) carry[c] = max(carry[c], s_scan[w * kClass + c]);
+    auto take = [](uint32_t key, int x) -> uint32_t {  // new entry of a distance-8 byte at x
+      const uint32_t tv = key & 0xFFFF;
+      return tv >= (uint32_t)kTail ? tv : (uint32_t)(x + 1) - (key >> 16);
+    };
+#pragma unroll 1
+    for (int q0 = 0; q0 < 32; q0 += 4)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = q0 + j, c = 2 * j, x = x0 + 2 * q;
+      const uint32_t v = pair_at(q);
+      uint32_t lo = v & 0xFFFF, hi = v >> 16;
+      const bool t0 = lo != (uint32_t)kClass, t1 = hi != (uint32_t)kClass;
+      if (!t0) {
+        if (carry[c]) lo = take(carry[c], x);
+      } else {
+        carry[c] = ((uint32_t)(x + 1) << 16) | lo;
+      }
+      if (!t1) {
+        if (carry[c + 1]) hi = take(carry[c + 1], x + 1);
+      } else {
+        carry[c + 1] = ((uint32_t)(x + 2) << 16) | hi;
+      }
+      const uint32_t nv = lo | (hi << 16);
+      if (nv != v) s_e32[eph(x) >> 1] = nv;  // x < lim whenever an entry changes
+      list_append(t0 && lo < (uint32_t)kTail, x);  // open terminals
+      list_append(t1 && hi < (uint32_t)kTail, x + 1);
+    }
+    __syncthreads();
+    const int no = s_nopen;
+    if (no <= kOpenCap) {
+      // terminal rounds over the list, then one sweep: every scanned entry reads its terminal's code
+      for (int round = 0;; ++round) {
+        if (round > kMaxRounds) {  // unreachable for a valid block
+          if (tid == 0) atomicOr(err, 1);
+          return;
+        }
+        jump_rounds++;
+        bool any = false;
+        for (int i = tid; i < no; i += kLzThreads) {
+          const int x = s_open[i];
+          const uint32_t d = s_e[eph(x)];
+          if (d < (uint32_t)kTail) {
+            const uint32_t nd = jstep(d, s_e[eph(x - (int)d)]);
+            s_e[eph(x)] = (uint16_t)nd;
+            any |= nd < (uint32_t)kTail;
+          }
+        }
+        if (!__syncthreads_or(any)) break;
+      }
+      // every scanned entry now holds a code or the distance to a terminal that holds one: the tail
+      // and the output take that last hop themselves (final_code)
+    } else {
+      for (int round = 0; __syncthreads_or(sweep(false)); ++round) {
+        jump_rounds++;
+        if (round > kMaxRounds) {
+          if (tid == 0) atomicOr(err, 1);
+          return;
+        }
+      }
+    }
+  } else {
+    jump_rounds = 1;
+    if (__syncthreads_or(sweep(true))) {
+      // later rounds: thread t takes bitmap word t (pairs 32t .. 32t + 31) and steps its open pairs
+      uint32_t m = s_obits[tid];
+      int cnt_open = __popc(m);
+      for (int round = 1;; ++round) {
+        if (round > kMaxRounds) {  // unreachable for a valid block
+          if (tid == 0) atomicOr(err, 1);
+          return;
+        }
+        jump_rounds++;
+        uint32_t keep = 0, mm = m;
+        while (mm) {
+          const int bit = __builtin_ctz(mm);
+          mm &= mm - 1;
+          const int x = 2 * (32 * tid + bit);
+          const uint32_t v = s_e32[eph(x) >> 1];
+          const uint32_t d0 = v & 0xFFFF, d1 = v >> 16;
+          const uint32_t e0 = d0 < (uint32_t)kTail ? s_e[eph(x - (int)d0)] : 0xFF00u;
+          const uint32_t e1 = d1 < (uint32_t)kTail ? s_e[eph(x + 1 - (int)d1)] : 0xFF00u;
+          const uint32_t nv = jstep(d0, e0) | (jstep(d1, e1) << 16);
+          if (nv != v) s_e32[eph(x) >> 1] = nv;
+          if (is_open(nv)) keep |= 1u << bit;
+        }
+        m = keep;
+        if (!__syncthreads_or(m != 0)) break;
+      }
+      if (PROF && cnt_open) atomicAdd(&s_nopen, cnt_open);  // (unused otherwise in this mode)
     }
   }
+  __syncthreads();
+  if (PROF && tid == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + 7] = (uint64_t)s_nopen;
   LZ_STAMP(5);
   if (PROF && tid == 0) {
     prof[(size_t)blockIdx.x * kLz4ProfWords + 8] = (uint64_t)jump_rounds;
@@ -516,6 +761,12 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     prof[(size_t)blockIdx.x * kLz4ProfWords + 10] = (uint64_t)nj;
     prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
   }
+  // the literal code of position y < kTail: E holds it, or (class mode) the distance to a byte that does
+  auto final_code = [&](int y) -> uint32_t {
+    uint32_t e = s_e[eph(y)];
+    if (e < (uint32_t)kTail) e = s_e[eph(y - (int)e)];
+    return e;
+  };
   // ---- tail: positions [kTail, total) hold absolute sources; rounds of jumping over the table ----
   if (total > kTail) {
     const int nt = total - kTail;
@@ -526,7 +777,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       if (tact) {
         const int src = s_tsrc[tid];
         if (src < kTail) {
-          nsrc = s_e[eph(src)];  // a literal code: E has converged
+          nsrc = final_code(src);
           res = true;
         } else {
           const int i2 = src - kTail;
@@ -549,7 +800,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       }
     }
   }
-  // ---- 4. output: every entry is now a literal code; 16 bytes per 16-byte store ----
+  // ---- 4. output: every entry is a literal code or one hop from one; 16 bytes per 16-byte store ----
   uint4* dst = reinterpret_cast<uint4*>(job.dst);
   const int nchunks = (total + 15) >> 4;
   for (int c = tid; c < nchunks; c += kLzThreads) {
@@ -557,9 +808,22 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     uint32_t w[4];
     if (x0 + 16 <= lim) {
       const uint32_t* ep = s_e32 + (eph(x0) >> 1);
+      uint32_t e[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) e[q] = ep[q];
+      const uint32_t all = e[0] & e[1] & e[2] & e[3] & e[4] & e[5] & e[6] & e[7];
+      if ((all & 0xFF00FF00u) != 0xFF00FF00u) {  // class mode: entries one hop from their code
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          uint32_t lo = e[q] & 0xFFFF, hi = e[q] >> 16;
+          if (lo < (uint32_t)kTail) lo = s_e[eph(x0 + 2 * q - (int)lo)];
+          if (hi < (uint32_t)kTail) hi = s_e[eph(x0 + 2 * q + 1 - (int)hi)];
+          e[q] = lo | (hi << 16);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint32_t e0 = ep[2 * q], e1 = ep[2 * q + 1];
+        const uint32_t e0 = e[2 * q], e1 = e[2 * q + 1];
         w[q] = (e0 & 0xFF) | ((e0 >> 8) & 0xFF00) | ((e1 & 0xFF) << 16) | ((e1 & 0xFF0000) << 8);
       }
     } else {
@@ -581,112 +845,15 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   }
 }
 
-// Sequential reference decoder (DG_LZ4_SEQ=1): one wave per block, compressed input and decoded output staged in LDS.
-// Tokens are parsed in order (the format is sequential); literal and match copies are spread over
-// the 64 lanes. Overlapping matches (offset < length) use the periodic form
-// out[op + k] = out[op - off + k % off], which only reads bytes before op, so the lanes never race.
-// ------------------------------------------------------------------------------------------------
-
-__global__ __launch_bounds__(64) void k_lz4_decode_seq(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[kBlockBytes + 64];
-  const Lz4Job job = jobs[blockIdx.x];
-  const int lane = threadIdx.x;
-  const int iend = job.src_len;
-  if (iend <= 0 || iend > kLz4InCap) {
-    if (lane == 0) atomicOr(err, 1);
-    return;
-  }
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(job.src);
-    uint4* dst = reinterpret_cast<uint4*>(s_in);
-    const int n16 = (iend + 15) >> 4;
-    for (int i = lane; i < n16; i += 64) dst[i] = src[i];
-  }
-  __syncthreads();
-  int ip = 0, op = 0;
-  bool bad = false;
-  for (;;) {
-    if (ip >= iend) {
-      bad = true;
-      break;
-    }
-    const int tok = __builtin_amdgcn_readfirstlane(s_in[ip]);
-    ip++;
-    int lit = tok >> 4;
-    if (lit == 15) {
-      int b;
-      do {
-        if (ip >= iend) {
-          bad = true;
-          break;
-        }
-        b = __builtin_amdgcn_readfirstlane(s_in[ip]);
-        ip++;
-        lit += b;
-      } while (b == 255);
-      if (bad) break;
-    }
-    if (lit > iend - ip || lit > kBlockBytes - op) {
-      bad = true;
-      break;
-    }
-    for (int k = lane; k < lit; k += 64) s_out[op + k] = s_in[ip + k];
-    ip += lit;
-    op += lit;
-    if (ip == iend) break;  // last sequence: literals only
-    if (iend - ip < 2) {
-      bad = true;
-      break;
-    }
-    const int off = __builtin_amdgcn_readfirstlane((int)s_in[ip] | ((int)s_in[ip + 1] << 8));
-    ip += 2;
-    int ml = tok & 15;
-    if (ml == 15) {
-      int b;
-      do {
-        if (ip >= iend) {
-          bad = true;
-          break;
-        }
-        b = __builtin_amdgcn_readfirstlane(s_in[ip]);
-        ip++;
-        ml += b;
-      } while (b == 255);
-      if (bad) break;
-    }
-    ml += 4;
-    if (off == 0 || off > op || ml > kBlockBytes - op) {
-      bad = true;
-      break;
-    }
-    __syncthreads();
-    if (off >= ml) {
-      for (int k = lane; k < ml; k += 64) s_out[op + k] = s_out[op - off + k];
-    } else {
-      for (int k = lane; k < ml; k += 64) s_out[op + k] = s_out[op - off + (k % off)];
-    }
-    op += ml;
-    __syncthreads();
-  }
-  __syncthreads();
-  if (bad || op < job.expect_len) {
-    if (lane == 0) atomicOr(err, 1);
-    return;
-  }
-  uint4* dst = reinterpret_cast<uint4*>(job.dst);
-  const uint4* src = reinterpret_cast<const uint4*>(s_out);
-  const int n16 = (op + 15) >> 4;
-  for (int i = lane; i < n16; i += 64) dst[i] = src[i];
-}
-
-
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
+void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
-  static const bool seq = getenv("DG_LZ4_SEQ") && getenv("DG_LZ4_SEQ")[0] == '1';
-  if (seq) hipLaunchKernelGGL(k_lz4_decode_seq, dim3(njobs), dim3(64), 0, s, d_jobs, d_err);
-  else if (d_prof) hipLaunchKernelGGL(k_lz4_decode<true>, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
-  else hipLaunchKernelGGL(k_lz4_decode<false>, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
+  if (wide) {
+    if (d_prof) hipLaunchKernelGGL((k_lz4_decode<true, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
+    else hipLaunchKernelGGL((k_lz4_decode<false, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
+  } else {
+    if (d_prof) hipLaunchKernelGGL((k_lz4_decode<true, kLzSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
+    else hipLaunchKernelGGL((k_lz4_decode<false, kLzSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
+  }
 }
 
 }  // namespace dg

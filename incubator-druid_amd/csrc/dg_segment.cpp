@@ -140,8 +140,10 @@ int log2i(int32_t v) {
 // Validating parse of one LZ4 block (the checks of lz4-java's LZ4SafeDecompressor / liblz4's
 // LZ4_decompress_safe: lengths inside the input, match distance inside the output produced so far,
 // output within one 64 KiB Druid block, CompressedPools.java:39). Records the token offset of every
-// kLzSeqPerCp-th sequence.
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps) {
+// kLzSeqPerCp-th sequence; a block with more than kLzMaxCps such checkpoints keeps every other one
+// (intervals of 2 * kLzSeqPerCp sequences), and one that still has more is rejected.
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide) {
+  const size_t first = cps->size();
   int pos = 0, out = 0;
   int64_t seq = 0;
   auto ext = [&](int* len) {
@@ -151,6 +153,17 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps) {
       *len += b;
       if (b != 255) return true;
     }
+  };
+  *wide = 0;
+  auto finish = [&](int dec) {
+    size_t m = cps->size() - first;
+    if (m > (size_t)kLzMaxCps) {
+      *wide = 1;
+      for (size_t i = 0; 2 * i < m; ++i) (*cps)[first + i] = (*cps)[first + 2 * i];
+      m = (m + 1) / 2;
+      cps->resize(first + m);
+    }
+    return m > (size_t)kLzMaxCps ? -1 : dec;
   };
   for (;;) {
     if (seq % kLzSeqPerCp == 0) cps->push_back((uint32_t)pos);
@@ -162,7 +175,7 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps) {
     if (L > n - pos || L > kBlockBytes - out) return -1;
     pos += L;
     out += L;
-    if (pos == n) return out;  // last sequence: literals only
+    if (pos == n) return finish(out);  // last sequence: literals only
     if (n - pos < 2) return -1;
     const int off = in[pos] | (in[pos + 1] << 8);
     pos += 2;
@@ -206,6 +219,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     // sequence checkpoints of every block (host threads over blocks; validated parse)
     col->cp_off.assign(blocks.n, 0);
     col->cp_n.assign(blocks.n, -1);
+    col->cp_wide.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
     const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -214,7 +228,9 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int t = 0; t < nt; ++t)
       th.emplace_back([&, t] {
         for (int32_t b = t; b < blocks.n; b += nt) {
-          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b]);
+          int wide = 0;
+          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide);
+          col->cp_wide[b] = (uint8_t)wide;
           col->dec_len[b] = d;
           col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size();
         }

@@ -8,6 +8,7 @@ mkdir -p $out/obj
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I../../include $*"
 $H -c -x hip dg_lz4.hip -o $out/obj/dg_lz4.o &
 $H -c -x hip dg_kernels.hip -o $out/obj/dg_kernels.o &
+$H -c -x hip dg_sort.hip -o $out/obj/dg_sort.o &
 $H -c dg_engine.cpp -o $out/obj/dg_engine.o &
 $H -c dg_segment.cpp -o $out/obj/dg_segment.o &
 wait

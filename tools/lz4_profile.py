@@ -17,7 +17,7 @@ N = importlib.import_module("incubator-druid_amd._native")
 S = importlib.import_module("incubator-druid_amd.segment")
 W = importlib.import_module("incubator-druid_amd.writer")
 BLOCK = 65536
-PHASES = ["stage", "parse+scan", "fill", "coop", "jump", "output"]
+PHASES = ["stage", "parse+scan", "jobs+read", "fill+write", "resolve", "output"]
 
 
 def payloads(rng, k):
@@ -47,11 +47,11 @@ def run(ctx, blocks):
     out = np.zeros(n * BLOCK, dtype=np.uint8)
     out_lens = (ctypes.c_int32 * n)()
     ms = ctypes.c_double()
-    prof = np.zeros(n * 12, dtype=np.uint64)
+    prof = np.zeros(n * 32, dtype=np.uint64)
     for _ in range(2):
         N.check(N.lib().dg_debug_lz4_decode(ctx.handle, ptrs, lens, n, out.ctypes.data, out_lens, ctypes.byref(ms),
                                             prof.ctypes.data))
-    p = prof.reshape(n, 12).astype(np.int64)
+    p = prof.reshape(n, 32).astype(np.int64)
     return ms.value, p
 
 
@@ -59,8 +59,10 @@ def report(name, ms, p):
     d = np.diff(p[:, :7], axis=1)
     print(f"{name:10s} blocks={len(p):4d} kernel={ms:7.3f} ms  in_bytes(avg)={p[:, 9].mean():7.0f} "
           f"jump_rounds(avg/max)={p[:, 8].mean():5.1f}/{p[:, 8].max():3d} coop_jobs={p[:, 10].mean():6.1f} "
-          f"cps={p[:, 11].mean():6.1f}")
+          f"cps={p[:, 11].mean():6.1f} listed={p[:, 7].mean():7.0f}")
     print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(PHASES, d.mean(axis=0))))
+    fw = p[:, 16:32] - p[:, 3:4]  # each wave's own end of the fill, from the start of the fill
+    print(f"   fill end per wave (mean over blocks): first={fw.min(axis=1).mean():8.0f} last={fw.max(axis=1).mean():8.0f}")
 
 
 def main():
