@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 4
+#define DG_ABI_VERSION 5
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -146,6 +146,17 @@ typedef struct {
  * processing/.../segment/CursorFactory.java:32-42).
  * Granularity: period_ms == 0 is ALL; otherwise a fixed-length UTC period with bucket starts at
  * origin_ms + k * period_ms (PeriodGranularity.truncateMillisPeriod, PeriodGranularity.java:411-428).
+ * Calendar granularities (months, years, periods in a time zone, compound periods: PeriodGranularity
+ * with Joda chronology arithmetic, PeriodGranularity.java:212-410) are given as the bucket list
+ * gran.getIterable(interval) yields (Granularity.java:176-240): bucket_starts[0..n_bucket_starts)
+ * = the starts followed by the end of the last bucket (strictly ascending, covering the interval),
+ * period_ms = 0; bucket k = [bucket_starts[k], bucket_starts[k + 1]). The Java shim computes it
+ * with the query's own Granularity object. In dg_keyspace / dg_merge such a granularity is the
+ * grid period_ms = 1 over bucket indices into that list.
+ * descending: CursorFactory.makeCursors(..., descending) (QueryableIndexStorageAdapter.java:378-424):
+ * cursors in descending time order and each cursor's rows last to first (order-dependent floatSum);
+ * timeseries / topN write their per-segment buckets in that order. groupBy ignores it (its engine
+ * always asks for ascending cursors, GroupByQueryEngineV2.java:108-115).
  */
 typedef struct {
   int64_t interval_start; /* [start, end) epoch millis */
@@ -157,6 +168,9 @@ typedef struct {
   const dg_agg* aggs;
   int32_t n_aggs;
   const volatile int32_t* cancel; /* optional; non-zero => DG_ERR_INTERRUPTED between kernels */
+  const int64_t* bucket_starts;   /* calendar granularity (see above); NULL = period_ms grid */
+  int32_t n_bucket_starts;
+  int32_t descending;
 } dg_scan;
 
 /* QueryMetrics counters (query/QueryMetrics.java:295-306) + device timings */

@@ -6,6 +6,8 @@ cannot be loaded the product path raises, it never silently runs on the CPU.
 from __future__ import annotations
 
 import ctypes
+
+import numpy as np
 import json
 import os
 from typing import List, Optional, Sequence
@@ -57,7 +59,8 @@ class dg_scan(ctypes.Structure):
                 ("period_ms", ctypes.c_int64), ("origin_ms", ctypes.c_int64),
                 ("filter", ctypes.POINTER(dg_filter)), ("n_filter", ctypes.c_int32),
                 ("aggs", ctypes.POINTER(dg_agg)), ("n_aggs", ctypes.c_int32),
-                ("cancel", ctypes.POINTER(ctypes.c_int32))]
+                ("cancel", ctypes.POINTER(ctypes.c_int32)), ("bucket_starts", ctypes.c_void_p),
+                ("n_bucket_starts", ctypes.c_int32), ("descending", ctypes.c_int32)]
 
 
 class dg_metrics(ctypes.Structure):
@@ -324,8 +327,17 @@ def make_scan(query, query_module, cancel: Optional[ctypes.c_int32] = None, segm
     keep.append(aggs)
     s = dg_scan()
     s.interval_start, s.interval_end = query.interval
-    s.period_ms = query.granularity.period_ms
-    s.origin_ms = query.granularity.origin_ms
+    gran = query.granularity
+    if gran.is_calendar:
+        # Granularity.getIterable(interval) of the query interval (the engine buckets by these starts)
+        starts = np.asarray(gran.bucket_starts(tuple(query.interval)), dtype=np.int64)
+        keep.append(starts)
+        s.bucket_starts = starts.ctypes.data
+        s.n_bucket_starts = len(starts)
+    else:
+        s.period_ms = gran.period_ms
+        s.origin_ms = gran.origin_ms
+    s.descending = int(bool(getattr(query, "descending", False)))
     if fp.array is not None:
         s.filter = ctypes.cast(fp.array, ctypes.POINTER(dg_filter))
         s.n_filter = len(fp.nodes)

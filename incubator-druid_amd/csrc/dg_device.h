@@ -29,6 +29,23 @@ __device__ __forceinline__ int64_t java_d2l(double d) {
   return (int64_t)d;
 }
 
+// bucket coordinate of timestamp t: t itself on a period grid, or (calendar granularity, caller-given
+// bucket starts b[0..n)) the index of the last start <= t (-1 before the first)
+__device__ __forceinline__ int64_t bucket_coord(const int64_t* __restrict__ b, int32_t n, int64_t t) {
+  if (!b) return t;
+  int lo = 0, len = n;
+  while (len > 0) {
+    const int h = len >> 1;
+    if (b[lo + h] <= t) {
+      lo += h + 1;
+      len -= h + 1;
+    } else {
+      len = h;
+    }
+  }
+  return (int64_t)lo - 1;
+}
+
 __device__ __forceinline__ const uint8_t* cv_ptr(const ColView& v, int64_t r) {
   const uint8_t* base = v.blocks[r >> v.log2_per];
   return base + (size_t)(r & ((1ll << v.log2_per) - 1)) * (size_t)v.width;

@@ -1198,17 +1198,81 @@ static int64_t floor_mod(int64_t a, int64_t b) {
 struct Cursors {
   bool any = false;       // interval overlaps the data interval
   int64_t t_lo = 0, t_hi = 0;  // actual interval
-  int64_t bucket0 = 0;    // first bucket start (period) / bucket time (ALL)
+  int64_t bucket0 = 0;    // first bucket start (period) / bucket time (ALL) / first bucket index (calendar)
   int64_t nbuckets = 0;
   bool need_time = false;
 };
 
-static Cursors plan_cursors(const Segment* seg, const dg_scan* q) {
+// Calendar granularity (months, years, zoned or compound periods): the caller's bucket starts
+// (Granularity.getIterable of the query interval, Granularity.java:176-240), b[0..nb] with bucket k
+// = [b[k], b[k + 1]). The scan is then run on a virtual grid of period 1 whose coordinates are bucket
+// indices; the kernels map a timestamp to its index by binary search (bucket_coord).
+struct Grain {
+  const int64_t* hb = nullptr;  // host bucket starts (nb + 1), null on a period grid
+  int32_t nb = 0;
+  const int64_t* db = nullptr;  // device copy (uploaded per call)
+  bool desc = false;            // descending cursors
+  int64_t coord(int64_t t) const {
+    return (int64_t)(std::upper_bound(hb, hb + nb + 1, t) - hb) - 1;
+  }
+  int64_t time_of(int64_t v) const { return hb ? hb[v] : v; }
+};
+
+// Validates the scan's granularity and returns the scan the engines run (calendar: period 1 over
+// bucket indices).
+static int prepare_scan(const dg_scan* in, dg_scan* out, Grain* g) {
+  *out = *in;
+  *g = Grain();
+  g->desc = in->descending != 0;
+  if (!in->bucket_starts) {
+    if (in->n_bucket_starts) return set_error(DG_ERR_ARG, "n_bucket_starts without bucket_starts");
+    if (in->period_ms < 0) return set_error(DG_ERR_ARG, "negative period");
+    return DG_OK;
+  }
+  const int64_t* b = in->bucket_starts;
+  const int32_t n = in->n_bucket_starts;
+  if (in->period_ms != 0) return set_error(DG_ERR_ARG, "bucket_starts with a period");
+  if (n < 2) return set_error(DG_ERR_ARG, "bucket_starts needs at least one bucket (start and end)");
+  for (int32_t k = 1; k < n; ++k)
+    if (b[k] <= b[k - 1]) return set_error(DG_ERR_ARG, "bucket_starts not strictly ascending at %d", k);
+  if (b[0] > in->interval_start || b[n - 1] < in->interval_end)
+    return set_error(DG_ERR_ARG, "bucket_starts do not cover the interval");
+  g->hb = b;
+  g->nb = n - 1;
+  out->period_ms = 1;
+  out->origin_ms = 0;
+  return DG_OK;
+}
+
+static int upload_grain(CallScratch* cs, Grain* g, hipStream_t st) {
+  if (!g->hb) return DG_OK;
+  int64_t* d;
+  int64_t* h = up_take<int64_t>(cs, (size_t)g->nb + 1, &d, st);
+  if (!h) return set_error(DG_ERR_OOM, "bucket starts");
+  memcpy(h, g->hb, sizeof(int64_t) * ((size_t)g->nb + 1));
+  g->db = d;
+  return DG_OK;
+}
+
+static Cursors plan_cursors(const Segment* seg, const dg_scan* q, const Grain& g) {
   Cursors c;
   if (seg->nrows == 0) return c;
   const int64_t P = q->period_ms;
-  auto bucket_start = [&](int64_t t) { return P ? t - floor_mod(t - q->origin_ms, P) : kMinInstant; };
   const int64_t data_s = seg->min_time;
+  if (g.hb) {
+    // dataInterval = [minTime, gran.bucketEnd(maxTime)) (QueryableIndexStorageAdapter.makeCursors)
+    const int64_t km = g.coord(seg->max_time);
+    const int64_t data_e = km < 0 ? g.hb[0] : (km >= g.nb ? kMaxInstant : g.hb[km + 1]);
+    if (!(q->interval_start < data_e && data_s < q->interval_end)) return c;
+    c.any = true;
+    c.t_lo = std::max(q->interval_start, data_s);
+    c.t_hi = std::min(q->interval_end, data_e);
+    c.bucket0 = g.coord(c.t_lo);
+    c.nbuckets = g.coord(c.t_hi - 1) - c.bucket0 + 1;
+    c.need_time = true;
+    return c;
+  }
+  auto bucket_start = [&](int64_t t) { return P ? t - floor_mod(t - q->origin_ms, P) : kMinInstant; };
   const int64_t data_e = P ? bucket_start(seg->max_time) + P : kMaxInstant;
   if (!(q->interval_start < data_e && data_s < q->interval_end)) return c;
   c.any = true;
@@ -1504,7 +1568,7 @@ static int upload_gb_jobs(CallScratch* cs, std::vector<GbJob>& gj, const std::ve
 // accumulator tables (the scan kernels accumulate floatSum in fp64 first; this pass replaces it).
 // Keys are already in (segment, bucket) order unless `sort`.
 static int fsum_pass(CallScratch* cs, std::vector<GbJob>& gj, const std::vector<int64_t>& rows, int key_bits, bool sort,
-                     const AggPlan& plan, hipStream_t st) {
+                     const AggPlan& plan, hipStream_t st, bool desc) {
   if (key_bits > 64) return set_error(DG_ERR_UNSUPPORTED, "floatSum cell key of %d bits", key_bits);
   GbJob* d_jobs;
   int32_t* d_tile;
@@ -1524,7 +1588,7 @@ static int fsum_pass(CallScratch* cs, std::vector<GbJob>& gj, const std::vector<
   launch_run_mark(&sb, head_pos, st);
   for (int a = 0; a < plan.n; ++a)
     if (plan.kind[a] == DG_AGG_FLOAT_SUM)
-      launch_fsum_runs(d_jobs, (int)gj.size(), ntiles, &sb, plan, a, head_pos, nullptr, 0, st);
+      launch_fsum_runs(d_jobs, (int)gj.size(), ntiles, &sb, plan, a, head_pos, nullptr, 0, st, desc ? 1 : 0);
   return DG_OK;
 }
 
@@ -1675,12 +1739,19 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   int rc = check_segments(segs, n, &ctx);
   if (rc) return rc;
   if (!q) return set_error(DG_ERR_ARG, "null scan");
+  dg_scan qs;
+  Grain gr;
+  rc = prepare_scan(q, &qs, &gr);
+  if (rc) return rc;
+  q = &qs;
   AggPlan plan;
   rc = make_plan(q, &plan);
   if (rc) return rc;
   CallGuard g(ctx);
   CallScratch* cs = g.cs;
   hipStream_t st = ctx->stream;
+  rc = upload_grain(cs, &gr, st);
+  if (rc) return rc;
   dg_metrics m;
   memset(&m, 0, sizeof m);
   const int na = plan.n, rec = na + 1;
@@ -1692,7 +1763,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
-    cur[i] = plan_cursors(seg, q);
+    cur[i] = plan_cursors(seg, q, gr);
     out_nb[i] = (int32_t)(cur[i].any ? cur[i].nbuckets : 0);
     m.segment_rows += seg->nrows;
     if (!cur[i].any) continue;
@@ -1708,6 +1779,8 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     j.t_hi = cur[i].t_hi;
     j.bucket0 = cur[i].bucket0;
     j.period = q->period_ms;
+    j.bounds = gr.db;
+    j.nbounds = gr.nb + 1;
     j.nbuckets = (int32_t)cur[i].nbuckets;
     j.time.kind = VIEW_ABSENT;
     if (cur[i].need_time) {
@@ -1770,6 +1843,8 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
       f.t_hi = jobs[i].t_hi;
       f.bucket0 = cur[i].bucket0;
       f.period = q->period_ms;
+      f.bounds = gr.db;
+      f.nbounds = gr.nb + 1;
       f.seg_slot = i;
       f.seg_shift = bb;
       f.bucket_bits = bb;
@@ -1778,7 +1853,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
       f.fs_mul = 1;
       frows[i] = jobs[i].nrows;
     }
-    rc = fsum_pass(cs, gj, frows, bb + bits_for(n), false, plan, st);
+    rc = fsum_pass(cs, gj, frows, bb + bits_for(n), false, plan, st, gr.desc);
     if (rc) return rc;
   }
   hipEventRecord(ctx->ev[4], st);
@@ -1795,8 +1870,9 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     if (!cur[i].any) continue;
     m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : reinterpret_cast<Segment*>(segs[i])->nrows;
     for (int64_t b = 0; b < cur[i].nbuckets; ++b) {
-      const int64_t o = (int64_t)i * bucket_cap + b;
-      out_time[o] = q->period_ms ? cur[i].bucket0 + b * q->period_ms : cur[i].t_lo;
+      // cursor order: a descending query emits the buckets last to first (:378-381)
+      const int64_t o = (int64_t)i * bucket_cap + (gr.desc ? cur[i].nbuckets - 1 - b : b);
+      out_time[o] = q->period_ms ? gr.time_of(cur[i].bucket0 + b * q->period_ms) : cur[i].t_lo;
       out_rows[o] = (int64_t)h_out[i][b * rec];
       m.selected_rows += out_rows[o];
       for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], h_out[i][b * rec + 1 + a]);
@@ -1854,6 +1930,11 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   int rc = check_segments(segs, n, &ctx);
   if (rc) return rc;
   if (!q || !t || !t->dimension) return set_error(DG_ERR_ARG, "null argument");
+  dg_scan qs;
+  Grain gr;
+  rc = prepare_scan(q, &qs, &gr);
+  if (rc) return rc;
+  q = &qs;
   // non-ALL granularity: one cursor (and result list) per bucket, TopNQueryEngine.java:80-104
   const int bcap = q->period_ms ? t->bucket_cap : 1;
   if (bcap <= 0) return set_error(DG_ERR_ARG, "bucket_cap");
@@ -1868,6 +1949,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   CallGuard g(ctx);
   CallScratch* cs = g.cs;
   hipStream_t st = ctx->stream;
+  rc = upload_grain(cs, &gr, st);
+  if (rc) return rc;
   dg_metrics m;
   memset(&m, 0, sizeof m);
   const int na = plan.n, rec = na + 1;
@@ -1879,7 +1962,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
-    cur[i] = plan_cursors(seg, q);
+    cur[i] = plan_cursors(seg, q, gr);
     m.segment_rows += seg->nrows;
     for (int b = 0; b < bcap; ++b) out_n[(int64_t)i * bcap + b] = -1;
     if (!cur[i].any) continue;
@@ -1944,6 +2027,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     jobs[i].key_card = q->period_ms ? (int32_t)card[i] : 0;
     jobs[i].bucket0 = cur[i].bucket0;
     jobs[i].period = q->period_ms;
+    jobs[i].bounds = gr.db;
+    jobs[i].nbounds = gr.nb + 1;
     jobs[i].out = dev_take<uint64_t>(cs, (size_t)nkeys * rec);
     if (!jobs[i].out) return set_error(DG_ERR_OOM, "topN table");
     const int64_t nb = (nkeys + (1ll << shift) - 1) >> shift;
@@ -2020,6 +2105,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       f.t_hi = jobs[i].t_hi;
       f.bucket0 = cur[i].bucket0;
       f.period = q->period_ms;
+      f.bounds = gr.db;
+      f.nbounds = gr.nb + 1;
       f.ndims = 1;
       f.dims[0] = jobs[i].key;  // VIEW_ABSENT for a missing dimension: id 0 (its null value)
       f.dim_bits[0] = ib;
@@ -2032,7 +2119,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       f.fs_mul = jobs[i].key_card;
       frows[i] = jobs[i].nrows;
     }
-    rc = fsum_pass(cs, gj, frows, bits_for(n) + bb + ib, true, plan, st);
+    rc = fsum_pass(cs, gj, frows, bits_for(n) + bb + ib, true, plan, st, gr.desc);
     if (rc) return rc;
   }
   // selection + gather of the candidates' records, all segments in one launch
@@ -2090,8 +2177,10 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       if (any_ties) gc = card[i];
       sel_seg.push_back(i);
       sel_bucket.push_back((int)b);
-      out_base.push_back((int64_t)i * bcap + b);
-      if (q->period_ms) t->out_bucket_time[(int64_t)i * bcap + b] = cur[i].bucket0 + b * q->period_ms;
+      // cursor order: a descending query emits the buckets last to first
+      const int64_t L = (int64_t)i * bcap + (q->period_ms && gr.desc ? cur[i].nbuckets - 1 - b : b);
+      out_base.push_back(L);
+      if (q->period_ms) t->out_bucket_time[L] = gr.time_of(cur[i].bucket0 + b * q->period_ms);
       jgcap.push_back(gc);
       jgoff.push_back(gtotal);
       gtotal += gc * (rec + 1) + (gc + 3) / 4;  // records + u16 builder order
@@ -2742,6 +2831,7 @@ struct dg_result {
   int64_t cap = 0;
   dg::KeyLayout lay{};
   int64_t bucket0 = 0, period = 0, universal = 0;
+  std::vector<int64_t> bounds;  // calendar granularity: the call's bucket starts (bucket index -> time)
   std::vector<std::shared_ptr<dg::MergedDict>> dicts;  // empty for a dg_merge result (cluster ids)
   std::vector<int32_t> cards;                         // dg_merge result: cluster dictionary sizes
   ~dg_result() {
@@ -2762,6 +2852,11 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   int rc = check_segments(segs, n, &ctx);
   if (rc) return rc;
   if (!q || !gb || !out) return set_error(DG_ERR_ARG, "null argument");
+  dg_scan qs;
+  Grain gr;
+  rc = prepare_scan(q, &qs, &gr);
+  if (rc) return rc;
+  q = &qs;  // (groupBy cursors are always ascending: GroupByQueryEngineV2.java:108-115)
   const int nd = gb->n_dims;
   if (nd < 0 || nd > kMaxGroupDims) return set_error(DG_ERR_UNSUPPORTED, "%d groupBy dimensions (max %d)", nd, kMaxGroupDims);
   if (n > kMaxCallSegs) return set_error(DG_ERR_UNSUPPORTED, "%d segments in one call (max %d)", n, kMaxCallSegs);
@@ -2771,6 +2866,8 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   CallGuard g(ctx);
   CallScratch* cs = g.cs;
   hipStream_t st = ctx->stream;
+  rc = upload_grain(cs, &gr, st);
+  if (rc) return rc;
   dg_metrics m;
   memset(&m, 0, sizeof m);
   const int na = plan.n, rec = na + 1;
@@ -2778,7 +2875,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   for (int i = 0; i < n; ++i) sv[i] = reinterpret_cast<Segment*>(segs[i]);
   std::vector<Cursors> cur(n);
   for (int i = 0; i < n; ++i) {
-    cur[i] = plan_cursors(sv[i], q);
+    cur[i] = plan_cursors(sv[i], q, gr);
     m.segment_rows += sv[i]->nrows;
   }
   // merged dictionaries (GroupByMergingQueryRunnerV2 merges by value; merged ids order like values)
@@ -2834,6 +2931,8 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     j.t_hi = cur[i].t_hi;
     j.bucket0 = gb0;
     j.period = q->period_ms;
+    j.bounds = gr.db;
+    j.nbounds = gr.nb + 1;
     j.bucket_shift = lay.bucket_shift;
     j.bucket_bits = lay.bucket_bits;
     j.ndims = nd;
@@ -2893,6 +2992,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   res->lay = lay;
   res->bucket0 = gb0;
   res->period = q->period_ms;
+  if (gr.hb) res->bounds.assign(gr.hb, gr.hb + gr.nb + 1);
   res->universal = q->interval_start;  // GroupByStrategyV2.getUniversalTimestamp (ALL granularity)
   res->dicts = md;
   res->keys = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * 8));
@@ -2969,7 +3069,9 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
   if (rc) return rc;
   if (bucket_time)
     for (int64_t i = 0; i < count; ++i)
-      bucket_time[i] = r->period ? r->bucket0 + bucket_time[i] * r->period : r->universal;
+      bucket_time[i] = !r->period ? r->universal
+                       : r->bounds.empty() ? r->bucket0 + bucket_time[i] * r->period
+                                           : r->bounds[r->bucket0 + bucket_time[i]];
   if (values && r->naggs)
     for (int64_t i = 0; i < count; ++i)
       for (int a = 0; a < r->naggs; ++a) values[i * r->naggs + a] = tmp[(size_t)a * count + i];

@@ -101,8 +101,11 @@ struct ScanJob {
   const uint32_t* bitset;   // null: every row passes the filter
   ColView time;             // VIEW_ABSENT when the time column is not needed
   int64_t t_lo, t_hi;       // rows with t in [t_lo, t_hi)
-  int64_t bucket0;          // start of the first bucket
-  int64_t period;           // 0 = ALL (single bucket)
+  int64_t bucket0;          // start of the first bucket (calendar: its index in `bounds`)
+  int64_t period;           // 0 = ALL (single bucket); calendar: 1
+  const int64_t* bounds;    // calendar granularity: ascending bucket starts (null: period grid)
+  int32_t nbounds;
+  int32_t desc;             // descending cursors (floatSum recurrence runs backwards)
   int32_t nbuckets;         // timeseries: buckets; topN: table keys (cardinality, x buckets when key_card)
   int32_t key_card;         // topN over granularity buckets: key = bucket * key_card + id (0: key = id)
   ColView vals[kMaxAggs];   // input column per aggregator
@@ -128,7 +131,10 @@ struct GbJob {
   ColView time;                 // VIEW_ABSENT when the time column is not needed
   int64_t t_lo, t_hi;           // rows with t in [t_lo, t_hi)
   int64_t bucket0;              // origin of the bucket index (shared by the call's segments in a merge)
-  int64_t period;               // 0 = ALL
+  int64_t period;               // 0 = ALL; calendar: 1 (bucket index = position in `bounds`)
+  const int64_t* bounds;        // calendar granularity: ascending bucket starts (null: period grid)
+  int32_t nbounds;
+  int32_t desc;                 // descending cursors: the floatSum pass runs each cell backwards
   int32_t seg_slot, seg_shift;  // key field of the segment (0 / 0 when the groups are merged)
   int32_t bucket_shift, bucket_bits;
   ColView dims[kMaxGroupDims];
@@ -432,7 +438,7 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
 // (FloatSumAggregator.combine). groupBy: into out_slots[(1 + agg) * cap + g]; per-segment engines
 // (out_slots == null): into the job's fs_out table.
 void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, AggPlan plan, int agg,
-                      const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s);
+                      const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s, int desc = 0);
 // device slot encoding -> ABI encoding (finalize) of the aggregator slots [1 + a][cap] of n_ptr[0] groups
 void launch_slots_finalize(uint64_t* slots, const uint32_t* n_ptr, int64_t cap, AggPlan plan, hipStream_t s);
 // SoA slots [rec][cap] -> AoS records [n][rec]

@@ -430,7 +430,7 @@ __device__ __forceinline__ bool row_selected(const ScanJob& j, int64_t r, int64_
   if (j.time.kind != VIEW_ABSENT) {
     const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, r));
     if (t < j.t_lo || t >= j.t_hi) return false;
-    *bucket = j.period ? (t - j.bucket0) / j.period : 0;
+    *bucket = j.period ? (bucket_coord(j.bounds, j.nbounds, t) - j.bucket0) / j.period : 0;
   } else {
     *bucket = 0;
   }
@@ -468,7 +468,8 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
     int64_t b0 = 0;
     if (j.period && j.time.kind != VIEW_ABSENT) {
       const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, row0));
-      b0 = t >= j.bucket0 ? (t - j.bucket0) / j.period : 0;
+      const int64_t v = bucket_coord(j.bounds, j.nbounds, t);
+      b0 = v >= j.bucket0 ? (v - j.bucket0) / j.period : 0;
     }
     s_b0 = b0;
   }
@@ -711,7 +712,8 @@ __device__ __forceinline__ void quad_keys(const ScanJob& j, int64_t r, uint32_t 
     uint64_t t[4];
     load_raw4(j.time, r, t);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) id[k] += (uint32_t)(((int64_t)t[k] - j.bucket0) / j.period) * (uint32_t)j.key_card;
+    for (int k = 0; k < 4; ++k)
+      id[k] += (uint32_t)((bucket_coord(j.bounds, j.nbounds, (int64_t)t[k]) - j.bucket0) / j.period) * (uint32_t)j.key_card;
   }
 }
 

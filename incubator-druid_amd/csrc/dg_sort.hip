@@ -104,7 +104,7 @@ __device__ __forceinline__ bool gb_select(const GbJob& j, int64_t r, int64_t* bu
   if (j.time.kind != VIEW_ABSENT) {
     const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, r));
     if (t < j.t_lo || t >= j.t_hi) return false;
-    if (j.period) *bucket = (t - j.bucket0) / j.period;
+    if (j.period) *bucket = (bucket_coord(j.bounds, j.nbounds, t) - j.bucket0) / j.period;
   }
   return true;
 }
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ head_pos, const uint64_t* __restrict__ payload,
                                                    int pw, int agg, uint64_t* __restrict__ out_slots, int64_t cap,
-                                                   int rec) {
+                                                   int rec, int desc) {
   __shared__ uint32_t s_base[kMaxCallSegs];
   const uint32_t n = n_ptr[0], ng = n_ptr[1];
   for (int x = threadIdx.x; x < njobs; x += 256) s_base[x] = jobs[x].tile_begin < ntiles ? tile_off[jobs[x].tile_begin] : n;
@@ -686,7 +686,9 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
     float total = 0.0f, sum = 0.0f;
     int cur = -1;
     bool first = true;
-    for (uint32_t i = i0; i < i1; ++i) {
+    // a descending cursor adds its rows last to first (QueryableIndexStorageAdapter.java:397-403)
+    for (uint32_t k = i0; k < i1; ++k) {
+      const uint32_t i = desc ? i1 - 1 - (k - i0) : k;
       const uint32_t idx = elem_ref(keys[i], refs, i, kshift);
       const int seg = locate_seg(s_base, njobs, idx);
       if (seg != cur) {
@@ -715,11 +717,11 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
 }
 
 void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, AggPlan plan, int agg,
-                      const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s) {
+                      const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s, int desc) {
   const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (sb->cap + 255) / 256));
   hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->tile_cnt, ntiles,
                      sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, sb->payload, sb->pw, agg,
-                     out_slots, cap, plan.n + 1);
+                     out_slots, cap, plan.n + 1, desc);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -339,16 +339,27 @@ class GroupByExchange:
             local.append(sorted(vals, key=R._java_key))
         gran = query.granularity
         span = None
+        # calendar granularity: the engines bucket on the query's bucket list (identical on every rank),
+        # keys carry bucket indices into it (dg_keyspace period 1)
+        self.starts = np.asarray(gran.bucket_starts(tuple(query.interval)), np.int64) if gran.is_calendar else None
+        if self.starts is not None:
+            coord = lambda t: int(np.searchsorted(self.starts, t, side="right")) - 1  # noqa: E731
+            bend = lambda t: int(self.starts[coord(t) + 1]) if coord(t) + 1 < len(self.starts) else Q.MAX_INSTANT  # noqa: E731
+            period = 1
+        else:
+            coord = lambda t: gran.bucket_start(t)  # noqa: E731
+            bend = lambda t: gran.bucket_start(t) + gran.period_ms  # noqa: E731
+            period = gran.period_ms
         if not gran.is_all:  # the grid of bucket indices every rank's result is re-keyed onto
             q0, q1 = query.interval
             for s in segments:
                 if s.num_rows == 0:
                     continue
-                data_e = gran.bucket_start(s.max_time) + gran.period_ms
+                data_e = bend(s.max_time)
                 if not (q0 < data_e and s.min_time < q1):
                     continue
-                lo = gran.bucket_start(max(q0, s.min_time))
-                hi = gran.bucket_start(min(q1, data_e) - 1)
+                lo = coord(max(q0, s.min_time))
+                hi = coord(min(q1, data_e) - 1)
                 span = (lo, hi) if span is None else (min(span[0], lo), max(span[1], hi))
         gathered: List = [None] * self.world
         dist.all_gather_object(gathered, {"dicts": local, "span": span})
@@ -366,8 +377,8 @@ class GroupByExchange:
             bucket0, nb = 0, 1
         else:
             bucket0 = min(s[0] for s in spans)
-            nb = (max(s[1] for s in spans) - bucket0) // gran.period_ms + 1
-        self.ks = KeySpace([len(d) for d in self.dicts], gran.period_ms, bucket0, nb, query.interval[0],
+            nb = (max(s[1] for s in spans) - bucket0) // period + 1
+        self.ks = KeySpace([len(d) for d in self.dicts], 0 if gran.is_all else period, bucket0, nb, query.interval[0],
                            [a.kind for a in query.aggregations])
         if self.ks.bits > 63:
             raise R.N.UnsupportedQuery(2, f"cluster groupBy key of {self.ks.bits} bits")
@@ -433,7 +444,10 @@ class GroupByExchange:
         self.dist.all_to_all_single(rkeys, keys.contiguous(), [int(x) for x in recv], [int(x) for x in send])
         self.dist.all_to_all_single(rslots, slots.contiguous(), [int(x) * self.rec for x in recv],
                                     [int(x) * self.rec for x in send])
-        return self.engine.merge(self.ks, rkeys, rslots, self.query, self.dicts)
+        res = self.engine.merge(self.ks, rkeys, rslots, self.query, self.dicts)
+        if self.starts is not None:
+            res.time_map = self.starts  # dg_merge times are bucket indices into the query's bucket list
+        return res
 
 
 def _to_bits(a, v) -> int:

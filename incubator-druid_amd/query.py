@@ -20,6 +20,7 @@ null string == "" and numeric nulls read as 0.
 from __future__ import annotations
 
 import datetime as _dt
+import functools
 import math
 import re
 import struct
@@ -80,26 +81,44 @@ _ISO_PERIOD = re.compile(r"P(?:(\d+)W)?(?:(\d+)D)?(?:T(?:(\d+)H)?(?:(\d+)M)?(?:(
 
 @dataclass(frozen=True)
 class Granularity:
-    """ALL (period_ms == 0) or a fixed-length UTC period with an origin.
+    """ALL (period_ms == 0), a fixed-length UTC period with an origin, or a calendar granularity.
 
-    bucketStart(t) = t - floorMod(t - origin, period) (PeriodGranularity.truncateMillisPeriod,
+    Fixed: bucketStart(t) = t - floorMod(t - origin, period) (PeriodGranularity.truncateMillisPeriod,
     PeriodGranularity.java:411-428, UTC so fixed-length days/hours/weeks); Joda weeks start on
     Monday, so WEEK carries origin 1969-12-29 (Monday) = -3 days.
+    Calendar (name "calendar"): any other PeriodGranularity — months / years, a time zone, compound
+    periods with calendar fields — bucketed through the Joda restatement of granularity.py; the
+    engine receives its bucket starts (dg_scan.bucket_starts).
     """
     period_ms: int = 0
     origin_ms: int = 0
     name: str = "all"
+    iso: str = ""                   # calendar: ISO-8601 period
+    tz: str = ""                    # calendar: time zone id ("" = UTC)
+    origin: Optional[int] = None    # calendar: the spec's origin (None = the zone's local epoch)
 
     @property
     def is_all(self) -> bool:
-        return self.period_ms == 0
+        return self.period_ms == 0 and self.name != "calendar"
+
+    @property
+    def is_calendar(self) -> bool:
+        return self.name == "calendar"
+
+    @property
+    def calendar(self):
+        return _calendar(self.iso, self.origin, self.tz or None)
 
     def bucket_start(self, t: int) -> int:
+        if self.is_calendar:
+            return self.calendar.truncate(t)
         if self.is_all:
             return MIN_INSTANT
         return t - ((t - self.origin_ms) % self.period_ms)
 
     def increment(self, t: int) -> int:
+        if self.is_calendar:
+            return self.calendar.increment(t)
         if self.is_all:
             return MAX_INSTANT
         return t + self.period_ms
@@ -112,6 +131,9 @@ class Granularity:
         s, e = interval
         if self.is_all:
             return [(s, e)]
+        if self.is_calendar:
+            b = self.calendar.iterable_starts(s, e)
+            return list(zip(b[:-1], b[1:]))
         out = []
         cur = self.bucket_start(s)
         while cur < e:
@@ -119,12 +141,39 @@ class Granularity:
             cur += self.period_ms
         return out
 
+    def bucket_starts(self, interval: Tuple[int, int]) -> List[int]:
+        """Calendar: starts of the buckets getIterable(interval) yields, then the end of the last."""
+        return self.calendar.iterable_starts(*interval)
+
     def to_json(self):
         if self.is_all:
             return "all"
+        if self.is_calendar:
+            js = {"type": "period", "period": self.iso}
+            if self.tz:
+                js["timeZone"] = self.tz
+            if self.origin is not None:
+                js["origin"] = format_time(self.origin)
+            return js
         if self.name in _PERIOD_MS:
             return self.name
         return {"type": "duration", "duration": self.period_ms, "origin": self.origin_ms}
+
+    @staticmethod
+    def period(iso: str, tz: Optional[str] = None, origin=None) -> "Granularity":
+        """PeriodGranularity(period, origin, timeZone): the fixed UTC form when it is exact, else calendar."""
+        from .granularity import parse_period
+        y, mo, w, d, h, mi, s, ms = parse_period(iso)
+        utc = tz in (None, "", "UTC", "Etc/UTC")
+        o = parse_time(origin) if origin is not None else None
+        single = sum(1 for v in (y, mo, w, d, h, mi, s, ms) if v) == 1
+        # hours with an origin before 1970 not on the hour: PeriodGranularity.java:313-315 floors to the hour
+        quirk = bool(h) and single and o is not None and o < 0 and o % 3_600_000 != 0
+        if utc and not (y or mo) and not quirk:
+            P = ((((w * 7 + d) * 24 + h) * 60 + mi) * 60 + s) * 1000 + ms
+            default_origin = -3 * 86_400_000 if (w == 1 and single) else 0  # P1W: Mondays
+            return Granularity(P, o if o is not None else default_origin, "period")
+        return Granularity(0, 0, "calendar", iso.upper(), "" if utc else tz, o)
 
     @staticmethod
     def of(spec) -> "Granularity":
@@ -138,6 +187,8 @@ class Granularity:
                 return ALL
             if k in _PERIOD_MS:
                 return Granularity(_PERIOD_MS[k], -3 * 86_400_000 if k == "week" else 0, k)
+            if k in _CALENDAR:  # Granularities.MONTH / QUARTER / YEAR (GranularityType.java)
+                return Granularity.period(_CALENDAR[k])
             raise ValueError(f"unsupported granularity {spec!r}")
         t = spec.get("type")
         if t == "all":
@@ -146,17 +197,17 @@ class Granularity:
             origin = parse_time(spec["origin"]) if spec.get("origin") is not None else 0
             return Granularity(int(spec["duration"]), origin, "duration")
         if t == "period":
-            if spec.get("timeZone") not in (None, "UTC", "Etc/UTC"):
-                raise ValueError("only UTC period granularities are supported")
-            m = _ISO_PERIOD.fullmatch(spec["period"])
-            if not m or not any(m.groups()):
-                raise ValueError(f"unsupported period {spec['period']!r} (months/years are not fixed-length)")
-            w, d, h, mi, s = (int(x or 0) for x in m.groups())
-            ms = ((((w * 7 + d) * 24 + h) * 60 + mi) * 60 + s) * 1000
-            default_origin = -3 * 86_400_000 if (w and not (d or h or mi or s)) else 0
-            origin = parse_time(spec["origin"]) if spec.get("origin") is not None else default_origin
-            return Granularity(ms, origin, "period")
+            return Granularity.period(spec["period"], spec.get("timeZone"), spec.get("origin"))
         raise ValueError(f"unsupported granularity {spec!r}")
+
+
+_CALENDAR = {"month": "P1M", "quarter": "P3M", "year": "P1Y"}
+
+
+@functools.lru_cache(maxsize=64)
+def _calendar(iso: str, origin: Optional[int], tz: Optional[str]):
+    from .granularity import PeriodGranularity
+    return PeriodGranularity(iso, origin, tz)
 
 
 ALL = Granularity(0, 0, "all")

@@ -124,7 +124,10 @@ def _bucket_cap(segs, query) -> int:
         lo = max(qs, s.min_time)
         hi = min(qe, g.bucket_end(s.max_time))
         if hi > lo:
-            cap = max(cap, (hi - g.bucket_start(lo) + g.period_ms - 1) // g.period_ms)
+            if g.is_calendar:  # buckets of the segment's actual interval on the query's bucket list
+                cap = max(cap, len(g.iterable((lo, hi))))
+            else:
+                cap = max(cap, (hi - g.bucket_start(lo) + g.period_ms - 1) // g.period_ms)
     return int(cap)
 
 
@@ -548,7 +551,10 @@ def merge_topn(query: Q.TopNQuery, per_segment: List[List[Q.Result]]) -> List[Q.
     for ts, _, r in flat:
         key = 0 if gran.is_all else gran.bucket_start(ts)
         merged[key] = topn_binary_fn(query, merged.get(key), r)
-    return [Q.Result(merged[k].timestamp, merged[k].value[:query.threshold]) for k in sorted(merged)]
+    out = [Q.Result(merged[k].timestamp, merged[k].value[:query.threshold]) for k in sorted(merged)]
+    # result ordering ResultGranularTimestampComparator.create(gran, descending) (TopNQueryQueryToolChest.java:132;
+    # a TopNQuery is never descending, TopNQuery.java:74)
+    return out[::-1] if getattr(query, "descending", False) else out
 
 
 # ----------------------------------------------------------------------------------------------
@@ -586,6 +592,7 @@ class GroupByResult:
         self.handle, self.query = handle, query
         self.groups = int(N.lib().dg_result_groups(handle))
         self._dicts = dictionaries
+        self.time_map: Optional[np.ndarray] = None  # bucket index -> time (a dg_merge over a calendar grid)
 
     def dictionary(self, d: int) -> List[Optional[str]]:
         if self._dicts is not None:
@@ -611,6 +618,8 @@ class GroupByResult:
         if count:
             N.check(N.lib().dg_result_fetch_groups(self.handle, start, count, t.ctypes.data, ids.ctypes.data,
                                                    vals.ctypes.data))
+        if self.time_map is not None:
+            t[:count] = self.time_map[t[:count]]
         ids = ids[:count * nd].reshape(count, nd) if nd else np.zeros((count, 0), np.int32)
         codes = [np.ascontiguousarray(ids[:, d]) for d in range(nd)]
         aggs = _decode_slots(q.aggregations, vals[:count * na].reshape(count, na)) if na else []

@@ -65,6 +65,194 @@ def o_empty_to_null(v):
     return None if v is None or v == "" else str(v)
 
 
+# ---- PeriodGranularity in a time zone / with calendar fields (restated on Python datetimes) ----
+# java-util/.../granularity/PeriodGranularity.java:58-74 (origin default: the zone's local epoch),
+# :212-221 increment = chronology.add(period, t, 1), :222-410 truncate, :432-445 isCompoundPeriod;
+# Joda ZonedChronology semantics: calendar fields (day and longer) work on local wall time and map
+# back with the original instant's offset when valid, else the earlier instant of an overlap / the
+# instant after a gap; time fields (< 12 h) keep the instant's offset.
+_O_UTC = __import__("datetime").timezone.utc
+_O_EPOCH = __import__("datetime").datetime(1970, 1, 1)
+_O_ISO = re.compile(r"P(?:(\d+)Y)?(?:(\d+)M)?(?:(\d+)W)?(?:(\d+)D)?(?:T(?:(\d+)H)?(?:(\d+)M)?(?:(\d+)(?:\.(\d{1,3}))?S)?)?")
+_O_UNIT = {2: 604_800_000, 3: 86_400_000, 4: 3_600_000, 5: 60_000, 6: 1000, 7: 1}
+
+
+class _OZone:
+    def __init__(self, name):
+        import datetime as dt
+        self.dt = dt
+        if not name or name.upper() in ("UTC", "ETC/UTC", "Z"):
+            self.tz = _O_UTC
+        elif re.fullmatch(r"[+-]\d{2}(:?\d{2})?", name):
+            mins = int(name[1:3]) * 60 + (int(name[-2:]) if len(name) > 3 else 0)
+            self.tz = dt.timezone(dt.timedelta(minutes=mins if name[0] == "+" else -mins))
+        else:
+            from zoneinfo import ZoneInfo
+            self.tz = ZoneInfo(name)
+
+    def wall(self, t):  # instant -> (naive local datetime, offset ms)
+        a = (_O_EPOCH.replace(tzinfo=_O_UTC) + self.dt.timedelta(milliseconds=t)).astimezone(self.tz)
+        off = int(a.utcoffset() / self.dt.timedelta(milliseconds=1))
+        return a.replace(tzinfo=None), off
+
+    def instant(self, wall, like=None):
+        """wall time -> instant: the original instant's offset if valid there (convertLocalToUTC(local,
+        false, original)), else fold=0 (earlier instant in an overlap, forward across a gap)."""
+        ms = int((wall - _O_EPOCH) / self.dt.timedelta(milliseconds=1))
+        if like is not None:
+            off = self.wall(like)[1]
+            if self.wall(ms - off)[1] == off:
+                return ms - off
+        off = wall.replace(tzinfo=self.tz, fold=0).utcoffset()
+        return ms - int(off / self.dt.timedelta(milliseconds=1))
+
+
+def _o_month_add(w, n):
+    import calendar
+    y, m = divmod(w.year * 12 + w.month - 1 + n, 12)
+    return w.replace(year=y, month=m + 1, day=min(w.day, calendar.monthrange(y, m + 1)[1]))
+
+
+class _OPeriod:
+    def __init__(self, iso, origin, tz):
+        g = _O_ISO.fullmatch(iso.upper()).groups()
+        self.f = [int(x or 0) for x in g[:7]] + [int((g[7] or "0").ljust(3, "0"))]
+        self.z = _OZone(tz)
+        self.has_origin = origin is not None
+        self.origin = origin if origin is not None else self.z.instant(_O_EPOCH)
+        self.compound = sum(1 for v in self.f if v) > 1
+
+    def add_field(self, i, t, n):
+        if n == 0:
+            return t
+        if i >= 4:
+            return t + n * _O_UNIT[i]
+        w = self.z.wall(t)[0]
+        if i <= 1:
+            w = _o_month_add(w, n * (12 if i == 0 else 1))
+        else:
+            w = w + self.z.dt.timedelta(milliseconds=n * _O_UNIT[i])
+        return self.z.instant(w)
+
+    def diff_field(self, i, t, o):
+        if i >= 4:  # elapsed units, Java division (toward zero)
+            q = abs(t - o) // _O_UNIT[i]
+            return q if t >= o else -q
+        a, b = self.z.wall(t)[0], self.z.wall(o)[0]
+        if i >= 2:
+            d = int((a - b) / self.z.dt.timedelta(milliseconds=1))
+            q = abs(d) // _O_UNIT[i]
+            return q if d >= 0 else -q
+        sign = 1
+        if a < b:
+            a, b, sign = b, a, -1
+        if i == 1:  # months: whole months elapsed (end-of-month rule of BasicMonthOfYearDateTimeField)
+            import calendar
+            n = (a.year - b.year) * 12 + a.month - b.month
+            if a.day == calendar.monthrange(a.year, a.month)[1] and b.day > a.day:
+                b = b.replace(day=a.day)
+            if (a - a.replace(day=1, hour=0, minute=0, second=0, microsecond=0)) < \
+                    (b - b.replace(day=1, hour=0, minute=0, second=0, microsecond=0)):
+                n -= 1
+            return sign * n
+        # years (BasicGJChronology.getYearDifference: leap-day balanced remainders)
+        import calendar
+        ra = a - a.replace(month=1, day=1, hour=0, minute=0, second=0, microsecond=0)
+        rb = b - b.replace(month=1, day=1, hour=0, minute=0, second=0, microsecond=0)
+        feb29 = self.z.dt.timedelta(days=59)
+        if rb >= feb29:
+            if calendar.isleap(b.year):
+                if not calendar.isleap(a.year):
+                    rb -= self.z.dt.timedelta(days=1)
+            elif ra >= feb29 and calendar.isleap(a.year):
+                ra -= self.z.dt.timedelta(days=1)
+        n = a.year - b.year - (1 if ra < rb else 0)
+        return sign * n
+
+    def increment(self, t, k=1):
+        for i, v in enumerate(self.f):
+            t = self.add_field(i, t, v * k)
+        return t
+
+    def aligned(self, i, t, n):
+        k = self.diff_field(i, t, self.origin)
+        k -= _jrem(k, n)
+        tt = self.add_field(i, self.origin, k)
+        return self.add_field(i, tt, -n) if t < tt else tt
+
+    def floor_wall(self, t, fn):  # roundFloor / set of a calendar field
+        return self.z.instant(fn(self.z.wall(t)[0]), t)
+
+    def floor_time(self, t, unit):  # roundFloor of a time field: keep the instant's offset
+        off = self.z.wall(t)[1]
+        return (t + off) // unit * unit - off
+
+    def truncate(self, t):
+        y, mo, w, d, h, mi, s, ms = self.f
+        dt0 = dict(hour=0, minute=0, second=0, microsecond=0)
+        if self.compound:
+            if not (y or mo) and isinstance(self.z.tz, type(_O_UTC)):  # truncateMillisPeriod
+                P = ((((w * 7 + d) * 24 + h) * 60 + mi) * 60 + s) * 1000 + ms
+                off = _jrem(t, P) - _jrem(self.origin, P)
+                return t - (off + P if off < 0 else off)
+            if t >= self.origin:
+                cur, nxt = self.origin, self.increment(self.origin)
+                while t >= nxt:
+                    cur, nxt = nxt, self.increment(nxt)
+                return cur
+            cur = self.increment(self.origin, -1)
+            while t < cur:
+                cur = self.increment(cur, -1)
+            return cur
+        if y:
+            return self.aligned(0, t, y) if (y > 1 or self.has_origin) else \
+                self.floor_wall(t, lambda x: x.replace(month=1, day=1, **dt0))
+        if mo:
+            return self.aligned(1, t, mo) if (mo > 1 or self.has_origin) else \
+                self.floor_wall(t, lambda x: x.replace(day=1, **dt0))
+        if w:
+            if w > 1 or self.has_origin:
+                return self.aligned(2, t, w)
+            t = self.floor_wall(t, lambda x: x.replace(**dt0))
+            return self.floor_wall(t, lambda x: x - self.z.dt.timedelta(days=x.isoweekday() - 1))
+        if d:
+            if d > 1 or self.has_origin:
+                return self.aligned(3, t, d)
+            return self.floor_wall(self.floor_time(t, 3_600_000), lambda x: x.replace(hour=0))
+        if h:
+            if h > 1 or self.has_origin:
+                k = self.diff_field(4, t, self.origin)
+                tt = self.origin + (k - _jrem(k, h)) * 3_600_000
+                if t < tt and self.origin > 0:
+                    return tt - h * 3_600_000
+                if t > tt and self.origin < 0:
+                    return self.floor_wall(self.floor_time(tt, 60_000), lambda x: x.replace(minute=0))
+                return tt
+            return self.floor_wall(self.floor_time(t, 60_000), lambda x: x.replace(minute=0))
+        if mi:
+            return self.aligned(5, t, mi) if (mi > 1 or self.has_origin) else \
+                self.floor_wall(self.floor_time(t, 1000), lambda x: x.replace(second=0))
+        if s:
+            return self.aligned(6, t, s) if (s > 1 or self.has_origin) else \
+                self.floor_wall(t, lambda x: x.replace(microsecond=0))
+        if ms > 1:
+            return self.aligned(7, t, ms)
+        return t
+
+
+@functools.lru_cache(maxsize=64)
+def _o_period(iso, origin, tz):
+    return _OPeriod(iso, origin, tz)
+
+
+def _o_cal(gran):
+    """The calendar restatement for a calendar-mode granularity of the tests' query objects (their
+    fields: ISO period, zone id, origin), None for ALL / fixed-length ones."""
+    if getattr(gran, "name", "") != "calendar":
+        return None
+    return _o_period(gran.iso, gran.origin, gran.tz or None)
+
+
 def o_bucket_start(gran, t: int) -> int:
     """Granularity.bucketStart of a UTC granularity.
     ALL: AllGranularity (every row in one bucket). duration: DurationGranularity.bucketStart
@@ -75,6 +263,9 @@ def o_bucket_start(gran, t: int) -> int:
     difference in whole units from the origin rounded toward zero, stepped back one period for
     timestamps before the aligned point — i.e. the floor relative to the origin; weeks start on
     Monday (dayOfWeek().set(t, 1), :279-281) = origin 1969-12-29."""
+    cal = _o_cal(gran)
+    if cal is not None:
+        return cal.truncate(t)
     P = gran.period_ms
     if P == 0:
         return _MIN_INSTANT
@@ -91,7 +282,14 @@ def o_bucket_start(gran, t: int) -> int:
     return tt - P if t < tt else tt
 
 
+def o_is_all(gran) -> bool:
+    return gran.period_ms == 0 and _o_cal(gran) is None
+
+
 def o_increment(gran, t: int) -> int:
+    cal = _o_cal(gran)
+    if cal is not None:
+        return cal.increment(t)
     return _MAX_INSTANT if gran.period_ms == 0 else t + gran.period_ms
 
 
@@ -99,7 +297,7 @@ def o_iterable(gran, interval):
     """Granularity.getIterable (java-util/.../granularity/Granularity.java:176-240): buckets from
     bucketStart(start) while < end; AllGranularity yields the interval itself."""
     s, e = interval
-    if gran.period_ms == 0:
+    if o_is_all(gran):
         return [(s, e)]
     out, cur = [], o_bucket_start(gran, s)
     while cur < e:
@@ -998,8 +1196,9 @@ def filter_mask(seg: OracleSegment, f) -> np.ndarray:
 # ----------------------------------------------------------------------------------------------
 # cursors / buckets
 # ----------------------------------------------------------------------------------------------
-def cursor_buckets(seg: OracleSegment, query) -> List[Tuple[int, int, int]]:
-    """(bucket_time, row_start, row_end) per cursor, makeCursors + CursorSequenceBuilder.build."""
+def cursor_buckets(seg: OracleSegment, query, descending: bool = False) -> List[Tuple[int, int, int]]:
+    """(bucket_time, row_start, row_end) per cursor, makeCursors + CursorSequenceBuilder.build;
+    descending: the bucket list reversed (QueryableIndexStorageAdapter.java:378-381)."""
     if seg.num_rows == 0:
         return []
     t = seg.time()
@@ -1017,7 +1216,14 @@ def cursor_buckets(seg: OracleSegment, query) -> List[Tuple[int, int, int]]:
         r0 = int(np.searchsorted(t, ts, side="left"))
         r1 = int(np.searchsorted(t, te, side="left"))
         out.append((bs if not gran.is_all else actual[0], r0, max(r0, r1)))
-    return out
+    return out[::-1] if descending else out
+
+
+def _cursor_rows(mask, r0, r1, descending):
+    """Rows of one cursor in its iteration order (a descending cursor walks its offset backwards,
+    DescendingTimestampCheckingOffset :655-690)."""
+    rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
+    return rows[::-1].copy() if descending else rows
 
 
 def _agg_input(seg: OracleSegment, agg) -> Optional[np.ndarray]:
@@ -1058,12 +1264,13 @@ def _py(v, out_type):
 # ----------------------------------------------------------------------------------------------
 def timeseries_segment(seg: OracleSegment, query) -> List:
     mask = filter_mask(seg, o_optimize(query.filter))
-    buckets = cursor_buckets(seg, query)
-    # one cursor per bucket; rows of every cursor are aggregated in row order (one C pass per aggregator,
-    # group = cursor index, identical to running each cursor's Aggregator loop on its own)
+    desc = bool(getattr(query, "descending", False))
+    buckets = cursor_buckets(seg, query, desc)
+    # one cursor per bucket; rows of every cursor are aggregated in cursor order (one C pass per
+    # aggregator, group = cursor index, identical to running each cursor's Aggregator loop on its own)
     rows_l, grp_l, counts = [], [], []
     for g, (bt, r0, r1) in enumerate(buckets):
-        rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
+        rows = _cursor_rows(mask, r0, r1, desc)
         rows_l.append(rows)
         grp_l.append(np.full(len(rows), g, np.int32))
         counts.append(len(rows))
@@ -1311,8 +1518,9 @@ def topn_segment(seg: OracleSegment, query) -> List:
     min_t = int(query.context.get("minTopNThreshold", 1000))
     T = query.threshold if query.threshold > min_t else min_t
     lo, hi = _dimension_id_range(seg, query, dictionary, T)
-    for bt, r0, r1 in cursor_buckets(seg, query):
-        rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
+    desc = bool(getattr(query, "descending", False))
+    for bt, r0, r1 in cursor_buckets(seg, query, desc):
+        rows = _cursor_rows(mask, r0, r1, desc)
         card = len(dictionary)
         gids = ids_all[rows]
         states = aggregate_groups(seg, query.aggregations, rows, gids, card)
@@ -1369,7 +1577,8 @@ def merge_topn(query, per_segment: List[List]) -> List:
         r = merged[k]
         # final truncation to the query threshold (Iterables.limit in the toolchest)
         out.append(Q.Result(r.timestamp, r.value[:query.threshold]))
-    return out
+    # ResultGranularTimestampComparator.create(gran, descending) (TopNQueryQueryToolChest.java:132)
+    return out[::-1] if getattr(query, "descending", False) else out
 
 
 # ----------------------------------------------------------------------------------------------
