@@ -973,7 +973,7 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.ncp = b.cp_n[k];
   j.dec_len = b.dec_len[k];
   j.wide = b.cp_wide[k];
-  j.pad = 0;
+  j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
   return j;
 }
 
@@ -1086,12 +1086,18 @@ static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_
   // a few waves of blocks: with hundreds of waves the tail is noise and the host sort is not.
   // wide blocks (more than 8192 sequences) go to their own launch of the decoder (twice the
   // per-thread sequence registers)
-  const int nn = (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.wide; }) -
+  // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
+  // blocks per CU); DG_LZ4_NO_LIGHT=1 sends them through the general decoder (A/B)
+  static const bool no_light = getenv("DG_LZ4_NO_LIGHT") != nullptr;
+  const int nh = no_light ? n
+                          : (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.light; }) -
+                                  db->jobs.begin());
+  const int nn = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
                        db->jobs.begin());
 #ifndef DG_NO_LPT
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
   if (nn <= 16 * 256) std::stable_sort(db->jobs.begin(), db->jobs.begin() + nn, by_ncp);
-  if (n - nn <= 16 * 256) std::stable_sort(db->jobs.begin() + nn, db->jobs.end(), by_ncp);
+  if (nh - nn <= 16 * 256) std::stable_sort(db->jobs.begin() + nn, db->jobs.begin() + nh, by_ncp);
 #endif
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
@@ -1099,8 +1105,9 @@ static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_
   if (!h || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
+  launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
   launch_lz4_decode(d, nn, 0, d_err, st, d_prof);
-  launch_lz4_decode(d + nn, n - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
+  launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
 
@@ -3345,6 +3352,7 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.cp_off.resize(n);
   b.cp_n.resize(n);
   b.cp_wide.assign(n, 0);
+  b.cp_light.assign(n, 0);
   b.dec_len.resize(n);
   int64_t total = 0;
   for (int i = 0; i < n; ++i) {
@@ -3358,9 +3366,10 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
     std::vector<uint32_t> one;
-    int wide = 0;
-    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide);
+    int wide = 0, light = 0;
+    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light);
     b.cp_wide[i] = (uint8_t)wide;
+    b.cp_light[i] = (uint8_t)light;
     b.cp_off[i] = (int64_t)cps.size();
     b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size();
     b.dec_len[i] = d < 0 ? 0 : d;

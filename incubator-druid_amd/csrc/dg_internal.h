@@ -58,8 +58,14 @@ struct Lz4Job {
   int32_t ncp;         // number of checkpoints; < 0: the block failed validation at attach
   int32_t dec_len;     // decoded length found at attach
   int32_t wide;        // checkpoints every 2 * kLzSeqPerCp sequences (decoded by the wide kernel)
-  int32_t pad;
+  int32_t light;       // few sequences, short copy chains: decoded by the light kernel (k_lz4_light)
 };
+
+// Light blocks (literal-heavy: random ids, high-entropy values): at most kLtMaxCps checkpoint
+// intervals and copy chains of at most kLtMaxDepth hops. k_lz4_light decodes them with a small
+// sequence table in LDS (many blocks per CU), resolving every output byte back to its literal.
+constexpr int kLtMaxCps = 256;
+constexpr int kLtMaxDepth = 16;
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
 struct LzfJob {
@@ -86,7 +92,8 @@ struct VsJob {
 // Host-side validating parse of one LZ4 block (lz4-java safe-decompressor semantics): appends the
 // block's checkpoints to *cps and returns the decoded length, or -1 for a malformed block.
 // *wide: the block keeps every other checkpoint (more than kLzMaxCps * kLzSeqPerCp sequences).
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide);
+// *light (optional): the block qualifies for the light decoder (kLtMaxCps / kLtMaxDepth).
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr);
 
 struct AggPlan {
   int32_t n;
@@ -203,6 +210,7 @@ struct BlockColumn {
   std::vector<int64_t> cp_off;         // LZ4: first checkpoint of block b inside cps
   std::vector<int32_t> cp_n;           // LZ4: checkpoints of block b (-1: malformed block)
   std::vector<uint8_t> cp_wide;        // LZ4: block b keeps a checkpoint every 2 * kLzSeqPerCp sequences
+  std::vector<uint8_t> cp_light;       // LZ4: block b goes to the light decoder
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
   int64_t index_bytes = 0;             // LZ4: bytes of the checkpoint index (read per query)
   DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)
@@ -323,6 +331,7 @@ int load_segment(Context* ctx, const char* dir, Segment** out);
 constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (diagnostic builds of the call)
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // VSizeLongSerde.getSerializedSize (VSizeLongSerde.java:61-65)

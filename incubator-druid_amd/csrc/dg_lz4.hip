@@ -845,6 +845,287 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Light decoder: blocks of at most kLtMaxCps checkpoint intervals (<= 2048 sequences) whose copy
+// chains are at most kLtMaxDepth hops long (attach-time classification, lz4_index_block). These are
+// the literal-heavy blocks of high-entropy columns (random dictionary ids, noisy doubles: one long
+// literal run, or ~700 sequences of ~90 literal bytes and a short match). Instead of a per-byte
+// entry image (the general decoder's 128 KiB of LDS, one block per CU) the workgroup keeps only the
+// staged input, then the sequence table in the same LDS (68 KiB: two blocks per CU), and resolves
+// every output byte directly: a byte inside a literal run is read from the compressed block (L2,
+// just staged), a match byte hops to its source position (at most kLtMaxDepth hops).
+//   1. stage the compressed block in LDS; thread t parses checkpoint interval t (<= 8 sequences);
+//   2. a block scan of the intervals' output lengths places every sequence: start, match start,
+//      literal input offset, distance (written over the staged input); a 64-byte-granular LUT maps a
+//      position to its first sequence;
+//   3. output: 16-byte chunks, one per thread per step (coalesced 16-byte stores). A chunk inside one
+//      literal run is five dword loads from the input; otherwise each byte is resolved hop by hop.
+// ------------------------------------------------------------------------------------------------
+constexpr int kLtThreads = 512;
+constexpr int kLtMaxSeq = kLtMaxCps * kLzSeqPerCp;  // 2048
+constexpr int kLtLut = kBlockBytes / 64;
+constexpr int kLtBufWords = (kLz4InCap + 32) / 4;  // staged input (+ zero pad), later the sequence table
+static_assert(kLtMaxCps <= kLtThreads, "one checkpoint interval per light-decoder thread");
+static_assert((kLtMaxSeq + 1 + 3 * kLtMaxSeq) * 4 + kLtMaxSeq * 2 <= kLtBufWords * 4, "table fits the input buffer");
+
+template <bool PROF>
+__global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+                                                          uint64_t* __restrict__ prof) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_buf[kLtBufWords];
+  __shared__ uint16_t s_lut[kLtLut];  // first sequence covering position 64 * i
+  __shared__ int s_tmp[kLtThreads / 64];
+  __shared__ int s_bad;
+  uint32_t* s_start = s_buf;                    // [kLtMaxSeq + 1] output start of every sequence, then the total
+  uint32_t* s_mst = s_buf + kLtMaxSeq + 1;      // [kLtMaxSeq] output start of its match
+  uint32_t* s_lit = s_mst + kLtMaxSeq;          // [kLtMaxSeq] input offset of its literals
+  int32_t* s_mb = reinterpret_cast<int32_t*>(s_lit + kLtMaxSeq);  // [kLtMaxSeq] input base of a resolved match, -1
+  uint16_t* s_dist = reinterpret_cast<uint16_t*>(s_mb + kLtMaxSeq);  // [kLtMaxSeq] match distance
+
+  const Lz4Job job = jobs[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = job.src_len, ncp = job.ncp;
+  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLtMaxCps || job.dec_len > kBlockBytes ||
+      job.dec_len < job.expect_len) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  LZ_STAMP(0);
+  // ---- stage the compressed block (16-byte aligned and padded in the device image) ----
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(job.src);
+    uint4* dst = reinterpret_cast<uint4*>(s_buf);
+    const int n16 = (n + 15) >> 4;
+    for (int i = tid; i < n16; i += kLtThreads) dst[i] = src[i];
+    if (tid == 0) {
+      dst[n16] = make_uint4(0, 0, 0, 0);
+      s_bad = 0;
+    }
+  }
+  __syncthreads();
+  LZ_STAMP(1);
+  const uint8_t* s_in = reinterpret_cast<const uint8_t*>(s_buf);
+  // ---- 1. parse my interval ----
+  int r_L[kLzSeqPerCp], r_M[kLzSeqPerCp], r_off[kLzSeqPerCp], r_lit[kLzSeqPerCp];
+  int cnt = 0, out_rel = 0;
+  bool bad = false;
+  if (tid < ncp) {
+    int pos = (int)job.cp[tid];
+    const int end = tid + 1 < ncp ? (int)job.cp[tid + 1] : n;
+#pragma unroll
+    for (int s = 0; s < kLzSeqPerCp; ++s) {
+      r_L[s] = r_M[s] = r_off[s] = r_lit[s] = 0;
+      if (pos < end) {
+        Tok t;
+        if (parse_tok(s_in, n, pos, t)) {
+          r_L[s] = t.L;
+          r_M[s] = t.M;
+          r_off[s] = t.off;
+          r_lit[s] = t.lit;
+          out_rel += t.L + t.M;
+          pos = t.next;
+          cnt = s + 1;
+        } else {
+          pos = -1;
+        }
+      }
+    }
+    bad = pos != end || (tid + 1 < ncp && cnt != kLzSeqPerCp);
+  }
+  // ---- 2. block scan of the intervals' output lengths -> sequence table (over the staged input) ----
+  int x = out_rel;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[wave] = x;
+  if (bad) s_bad = 1;
+  __syncthreads();  // also the end of every read of the staged input
+  LZ_STAMP(2);
+  int base = x - out_rel, total = 0;
+#pragma unroll
+  for (int w = 0; w < kLtThreads / 64; ++w) {
+    const int y = s_tmp[w];
+    base += w < wave ? y : 0;
+    total += y;
+  }
+  if (s_bad || total != job.dec_len) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  {
+    int o = base;
+#pragma unroll
+    for (int s = 0; s < kLzSeqPerCp; ++s) {
+      if (s < cnt) {
+        const int i = tid * kLzSeqPerCp + s;
+        s_start[i] = (uint32_t)o;
+        s_mst[i] = (uint32_t)(o + r_L[s]);
+        s_lit[i] = (uint32_t)r_lit[s];
+        s_dist[i] = (uint16_t)r_off[s];
+        s_mb[i] = -1;
+        if (r_M[s] > 0 && r_off[s] > o + r_L[s]) s_bad = 1;  // distance before the block start
+        // LUT entries of the 64-byte boundaries inside [o, o + L + M)
+        const int e = o + r_L[s] + r_M[s];
+        for (int k = (o + 63) >> 6; (k << 6) < e; ++k) s_lut[k] = (uint16_t)i;
+        o = e;
+      }
+    }
+    if (tid == ncp - 1) s_start[tid * kLzSeqPerCp + cnt] = (uint32_t)total;
+  }
+  __syncthreads();
+  if (s_bad) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  auto seq_of = [&](int pos) {
+    int s = s_lut[pos >> 6];
+    while ((int)s_start[s + 1] <= pos) ++s;
+    return s;
+  };
+  // ---- match resolution by sequence: a match whose first period (its source [ms - d, ms - d +
+  // min(M, d))) lies inside one literal run, or inside one resolved non-periodic match, copies
+  // input bytes base + (k mod d): record base (rounds, one per chain level; the rest stay per byte) ----
+  {
+    uint32_t todo = 0;  // my sequences with a match still to resolve
+#pragma unroll
+    for (int s = 0; s < kLzSeqPerCp; ++s) todo |= (s < cnt && r_M[s] > 0) ? 1u << s : 0u;
+    for (int round = 0; round < kLtMaxDepth; ++round) {
+      bool progress = false;
+#pragma unroll
+      for (int s = 0; s < kLzSeqPerCp; ++s) {
+        if (!((todo >> s) & 1u)) continue;
+        const int i = tid * kLzSeqPerCp + s;
+        const int ms = (int)s_mst[i], d = r_off[s], a = ms - d, len = min(r_M[s], d);
+        const int t = seq_of(a);
+        const int tst = (int)s_start[t], tms = (int)s_mst[t], ten = (int)s_start[t + 1];
+        int base = -1;
+        if (a + len <= tms) {
+          base = (int)s_lit[t] + (a - tst);
+        } else if (a >= tms && a + len <= ten) {
+          const int tb = s_mb[t], td = s_dist[t];
+          if (tb >= 0 && td >= ten - tms) base = tb + (a - tms);  // (a resolved, non-periodic match)
+          else if (tb < 0) continue;                             // (its source may resolve next round)
+        }
+        if (base >= 0) {
+          s_mb[i] = base;
+          progress = true;
+        }
+        todo &= ~(1u << s);  // resolved, or left to the per-byte path
+      }
+      if (!__syncthreads_or(progress)) break;  // (another thread's match may unlock one of mine)
+    }
+  }
+  __syncthreads();
+  LZ_STAMP(3);
+  // ---- 3. output: 16-byte chunks ----
+  const uint8_t* __restrict__ in = job.src;
+  const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
+  uint4* dst = reinterpret_cast<uint4*>(job.dst);
+  const int nchunks = (total + 15) >> 4;
+  bool fail = false;
+  for (int c0 = tid; c0 < nchunks; c0 += 2 * kLtThreads) {
+    // two chunks per step: their literal loads are issued together
+    int cs[2], src[2];
+    bool lit[2];
+    uint32_t v[2][5];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = c0 + u * kLtThreads;
+      cs[u] = c < nchunks ? seq_of(c << 4) : 0;
+      lit[u] = c < nchunks && (c << 4) + 16 <= (int)s_mst[cs[u]];
+      src[u] = lit[u] ? (int)s_lit[cs[u]] + ((c << 4) - (int)s_start[cs[u]]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) v[u][q] = lit[u] ? in32[(src[u] >> 2) + q] : 0u;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = c0 + u * kLtThreads;
+      if (c >= nchunks) break;
+      const int x0 = c << 4;
+      uint32_t w[4];
+      if (lit[u]) {  // inside one literal run
+        const int sh = src[u] & 3;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = sh ? __builtin_amdgcn_alignbyte(v[u][q + 1], v[u][q], sh) : v[u][q];
+      } else {  // every byte's literal position (LDS only), then the 16 bytes loaded together
+        int sp[16];
+        // the sequence under the cursor, reloaded only at sequence boundaries: literal bytes take
+        // their position arithmetically, match bytes hop (the previous match byte's source sequence
+        // is the first guess for the next one)
+        int s = cs[u];
+        int st = (int)s_start[s], ms = (int)s_mst[s], en = (int)s_start[s + 1], li = (int)s_lit[s], dd = s_dist[s];
+        int mb = s_mb[s];
+        int hs = s;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {  // (unrolled: sp stays in registers)
+          const int xi = x0 + i;
+          sp[i] = -1;
+          if (xi < total) {
+            while (xi >= en) {
+              ++s;
+              st = en;
+              ms = (int)s_mst[s];
+              en = (int)s_start[s + 1];
+              li = (int)s_lit[s];
+              dd = s_dist[s];
+              mb = s_mb[s];
+            }
+            if (xi < ms) {
+              sp[i] = li + (xi - st);
+            } else if (mb >= 0) {
+              const int k = xi - ms;
+              sp[i] = mb + (k < dd ? k : k % dd);
+            } else {
+              const int M = en - ms, k = xi - ms;
+              int y = dd >= M ? xi - dd : ms - dd + k % dd;
+              int sy = hs;
+#pragma unroll 1
+              for (int hop = 0; hop <= kLtMaxDepth && y >= 0; ++hop) {
+                if (y < (int)s_start[sy] || y >= (int)s_start[sy + 1]) sy = seq_of(y);
+                const int yst = (int)s_start[sy], yms = (int)s_mst[sy];
+                if (y < yms) {
+                  sp[i] = (int)s_lit[sy] + (y - yst);
+                  break;
+                }
+                const int yd = s_dist[sy], yM = (int)s_start[sy + 1] - yms, yk = y - yms;
+                const int yb = s_mb[sy];
+                if (yb >= 0) {
+                  sp[i] = yb + (yk < yd ? yk : yk % yd);
+                  break;
+                }
+                y = yd >= yM ? y - yd : yms - yd + yk % yd;
+              }
+              hs = sy;
+              if (sp[i] < 0) fail = true;
+            }
+          }
+        }
+        uint32_t b[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) b[i] = sp[i] >= 0 ? (uint32_t)in[sp[i]] : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = b[4 * q] | (b[4 * q + 1] << 8) | (b[4 * q + 2] << 16) | (b[4 * q + 3] << 24);
+      }
+      dst[c] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  if (fail) atomicOr(err, 1);
+  if (PROF) {
+    __syncthreads();
+    LZ_STAMP(4);
+    if (tid == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
+  }
+}
+
+void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
+  if (njobs <= 0) return;
+  if (d_prof) hipLaunchKernelGGL(k_lz4_light<true>, dim3(njobs), dim3(kLtThreads), 0, s, d_jobs, d_err, d_prof);
+  else hipLaunchKernelGGL(k_lz4_light<false>, dim3(njobs), dim3(kLtThreads), 0, s, d_jobs, d_err, nullptr);
+}
+
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
   if (wide) {

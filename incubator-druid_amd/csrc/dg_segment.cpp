@@ -142,8 +142,45 @@ int log2i(int32_t v) {
 // output within one 64 KiB Druid block, CompressedPools.java:39). Records the token offset of every
 // kLzSeqPerCp-th sequence; a block with more than kLzMaxCps such checkpoints keeps every other one
 // (intervals of 2 * kLzSeqPerCp sequences), and one that still has more is rejected.
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide) {
+// Longest copy chain of a validated block: a literal byte has depth 0, a match byte one more than the
+// byte it copies (overlapping matches copy from the match's first period). Stops above `cap`.
+static int lz4_max_depth(const uint8_t* in, int n, int cap) {
+  thread_local std::vector<uint8_t> dep(kBlockBytes);
+  int pos = 0, out = 0, mx = 0;
+  auto ext = [&](int* len) {
+    for (int b = 255; b == 255 && pos < n;) {
+      b = in[pos++];
+      *len += b;
+    }
+  };
+  for (;;) {
+    const int tok = in[pos++];
+    int L = tok >> 4;
+    if (L == 15) ext(&L);
+    memset(dep.data() + out, 0, (size_t)L);
+    out += L;
+    pos += L;
+    if (pos >= n) return mx;
+    const int off = in[pos] | (in[pos + 1] << 8);
+    pos += 2;
+    int M = tok & 15;
+    if (M == 15) ext(&M);
+    M += 4;
+    for (int k = 0, r = 0; k < M; ++k) {
+      const int src = off >= M ? out + k - off : out - off + r;
+      const int v = dep[src] + 1;
+      if (v > cap) return v;
+      dep[out + k] = (uint8_t)v;
+      mx = std::max(mx, v);
+      if (++r == off) r = 0;
+    }
+    out += M;
+  }
+}
+
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light) {
   const size_t first = cps->size();
+  if (light) *light = 0;
   int pos = 0, out = 0;
   int64_t seq = 0;
   auto ext = [&](int* len) {
@@ -163,7 +200,9 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
       m = (m + 1) / 2;
       cps->resize(first + m);
     }
-    return m > (size_t)kLzMaxCps ? -1 : dec;
+    if (m > (size_t)kLzMaxCps) return -1;
+    if (light && !*wide && m <= (size_t)kLtMaxCps) *light = lz4_max_depth(in, n, kLtMaxDepth) <= kLtMaxDepth;
+    return dec;
   };
   for (;;) {
     if (seq % kLzSeqPerCp == 0) cps->push_back((uint32_t)pos);
@@ -220,6 +259,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->cp_off.assign(blocks.n, 0);
     col->cp_n.assign(blocks.n, -1);
     col->cp_wide.assign(blocks.n, 0);
+    col->cp_light.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
     const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -228,9 +268,10 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int t = 0; t < nt; ++t)
       th.emplace_back([&, t] {
         for (int32_t b = t; b < blocks.n; b += nt) {
-          int wide = 0;
-          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide);
+          int wide = 0, light = 0;
+          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light);
           col->cp_wide[b] = (uint8_t)wide;
+          col->cp_light[b] = (uint8_t)light;
           col->dec_len[b] = d;
           col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size();
         }

@@ -135,3 +135,17 @@ def test_calendar_bucket_list_validation(R, Q, segs):
     rc = N.lib().dg_timeseries_run(R._handles(segs[:1]), 1, ctypes.byref(scan), 8, nb.ctypes.data, buf.ctypes.data,
                                    buf.ctypes.data, buf.ctypes.data, None)
     assert rc == 6  # DG_ERR_ARG
+
+
+def test_two_rank_exchange_calendar(R, Q, O, segs, osegs):
+    """Cross-device groupBy merge on a calendar grid: keys carry bucket indices into the query's
+    bucket list (dg_keyspace period 1), merged times map back through it."""
+    import test_merge_gpu as TM
+    D = importlib.import_module("incubator-druid_amd.distributed")
+    q = Q.GroupByQuery(intervals=IV, granularity={"type": "period", "period": "P1W", "timeZone": "America/Los_Angeles"},
+                       dimensions=["dimZipf"], aggregations=[Q.count("rows"), Q.long_sum("sumLongSequential"),
+                                                             Q.float_sum("fsum", "sumFloatNormal")])
+    parts = TM._run_ranks(R, D, Q, [segs[:1], segs[1:]], q)
+    exp = O.run(q, osegs)
+    assert len(exp) > 100
+    assert_results(q, TM._rows(Q, q, parts), exp)

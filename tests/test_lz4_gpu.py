@@ -184,3 +184,45 @@ def test_crafted_streams_pinned_by_system_liblz4(O):
         dst = ctypes.create_string_buffer(BLOCK + 16)
         n = lib.LZ4_decompress_safe(b, dst, len(b), BLOCK)
         assert n > 0 and dst.raw[:n] == O.lz4_decompress(b), name
+
+
+def _light_boundary(rng):
+    """Blocks at the light decoder's routing limits (<= 256 checkpoint intervals = 2048 sequences,
+    copy chains <= 16 hops): each case decodes bit-exactly on whichever decoder takes it."""
+    r = lambda k: rng.integers(0, 256, k).astype(np.uint8).tobytes()  # noqa: E731
+    cases = {}
+    for depth in (1, 16, 17, 40):  # every match copies the previous 64 bytes: chain depth = #matches
+        cases[f"chain{depth}"] = lz4_sequences([(r(64) if i == 0 else b"", 64, 64) for i in range(depth)], r(33))
+    for nseq in (2047, 2048, 2049):  # sequences incl. the last literal-only one
+        cases[f"seq{nseq}"] = lz4_sequences([(r(20), int(rng.integers(1, 20)), 4 + i % 3) for i in range(nseq - 1)],
+                                            r(7))
+    # long literal runs with short matches into earlier literals (random ids) and overlaps d < M
+    seqs, o = [], 0
+    while o < BLOCK - 2000:
+        L = int(rng.integers(20, 300))
+        m = int(rng.integers(4, 12))
+        d = int(rng.integers(1, min(o + L, 65535) + 1))
+        seqs.append((r(L), d, m))
+        o += L + m
+    cases["lit_heavy"] = lz4_sequences(seqs, r(BLOCK - o) if BLOCK - o < 2000 else r(3))
+    cases["rle_short"] = lz4_sequences([(b"\x01\x02\x03", 3, 5000), (r(10), 2, 9)], r(40))
+    return cases
+
+
+@pytest.mark.gpu
+def test_lz4_light_decoder_boundaries(O):
+    rng = np.random.default_rng(17)
+    cases = _light_boundary(rng)
+    blocks = list(cases.values()) * 3  # several per launch, mixed with the general decoder's blocks
+    got = gpu_decode(blocks)
+    for name, b, g in zip(list(cases) * 3, blocks, got):
+        assert g == O.lz4_decompress(b), name
+
+
+def test_light_boundary_streams_pinned_by_system_liblz4(O):
+    lib = ctypes.CDLL("liblz4.so.1")
+    rng = np.random.default_rng(17)
+    for name, b in _light_boundary(rng).items():
+        dst = ctypes.create_string_buffer(BLOCK + 16)
+        n = lib.LZ4_decompress_safe(b, dst, len(b), BLOCK)
+        assert n > 0 and dst.raw[:n] == O.lz4_decompress(b), name
