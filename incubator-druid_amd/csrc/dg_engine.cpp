@@ -977,20 +977,33 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   return j;
 }
 
+static int block_view(const BlockColumn& b, int kind, const char* name, CallScratch* cs, DecodeBatch* db, ColView* v,
+                      hipStream_t st);
+
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
   if (c->multi_value)
-    return set_error(DG_ERR_UNSUPPORTED, "%s: grouping on a multi-value dimension", c->name.c_str());
-  const BlockColumn& b = c->data;
+    return set_error(DG_ERR_UNSUPPORTED, "%s: multi-value dimension", c->name.c_str());
+  const int kind = c->type == DG_COL_LONG ? VIEW_LONG : c->type == DG_COL_DOUBLE ? VIEW_DOUBLE
+                   : c->type == DG_COL_FLOAT ? VIEW_FLOAT : VIEW_IDS;
+  return block_view(c->data, kind, c->name.c_str(), cs, db, v, st);
+}
+
+// a multi-value dimension: its value ids and the rows' value offsets
+static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st) {
+  int rc = block_view(c->data, VIEW_IDS, c->name.c_str(), cs, db, vals, st);
+  if (rc) return rc;
+  return block_view(c->mv_off, VIEW_IDS, c->name.c_str(), cs, db, offs, st);
+}
+
+static int block_view(const BlockColumn& b, int kind, const char* name, CallScratch* cs, DecodeBatch* db, ColView* v,
+                      hipStream_t st) {
   v->log2_per = b.log2_per;
   v->width = b.width;
   v->pad = b.big_endian ? kViewBigEndian : 0;
-  if (c->type == DG_COL_LONG) v->kind = VIEW_LONG;
-  else if (c->type == DG_COL_DOUBLE) v->kind = VIEW_DOUBLE;
-  else if (c->type == DG_COL_FLOAT) v->kind = VIEW_FLOAT;
-  else v->kind = VIEW_IDS;
+  v->kind = kind;
   db->bytes += b.stored_bytes + b.index_bytes;
   if (b.codec != CODEC_LZ4 && b.codec != CODEC_LZF && b.codec != CODEC_UNCOMPRESSED && b.codec != CODEC_NONE)
-    return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, c->name.c_str());
+    return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, name);
   uint8_t* slots = nullptr;
   if (b.codec == CODEC_LZ4 || b.codec == CODEC_LZF) {
     slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
@@ -2918,6 +2931,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   hipEventRecord(ctx->ev[0], st);
   std::vector<GbJob> gj(n);
   std::vector<int64_t> rows(n, 0);
+  bool any_multi = false;
   std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db;
   for (int i = 0; i < n; ++i) {
@@ -2945,7 +2959,13 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     j.ndims = nd;
     for (int d = 0; d < nd; ++d) {
       Column* c = seg->find(gb->dimensions[d]);
-      if (c) {
+      if (c && c->multi_value) {  // row value lists: every row groups under each of its values
+        rc = multi_view(c, cs, &db, &j.dims[d], &j.moff[d], st);
+        if (rc) return rc;
+        j.multi = 1;
+        any_multi = true;
+        j.remap[d] = md[d]->remap[i] ? md[d]->remap[i]->as<int32_t>() : nullptr;
+      } else if (c) {
         rc = column_view(c, cs, &db, &j.dims[d], st);
         if (rc) return rc;
         j.remap[d] = md[d]->remap[i] ? md[d]->remap[i]->as<int32_t>() : nullptr;
@@ -2974,6 +2994,18 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   int64_t total = 0;
   rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
   if (rc) return rc;
+  if (any_multi) {
+    // rows explode into one element per grouping: count them first to size the sort
+    uint32_t* d_cnt = dev_take<uint32_t>(cs, (size_t)std::max(ntiles, 1) + 4);
+    uint32_t* h_tot = host_take<uint32_t>(cs, 1);
+    if (!d_cnt || !h_tot) return set_error(DG_ERR_OOM, "groupBy element count");
+    DG_FLUSH(cs, st);
+    launch_gb_count(d_jobs, d_tile, ntiles, d_cnt, d_cnt + std::max(ntiles, 1), true, st);
+    DG_HIP(hipMemcpyAsync(h_tot, d_cnt + std::max(ntiles, 1), 4, hipMemcpyDeviceToHost, st));
+    rc = finish_call(cs, st);
+    if (rc) return rc;
+    total = *h_tot;  // (a 32-bit count: more elements than that are not representable anyway)
+  }
   SortBufs sb;
   rc = sort_bufs(cs, total, ntiles, key_bits, na, &sb);
   if (rc) return rc;
@@ -2981,7 +3013,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   if (!h_n) return set_error(DG_ERR_OOM, "groupBy counters");
   DG_FLUSH(cs, st);
   hipEventRecord(ctx->ev[3], st);
-  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st);
+  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi);
   hipEventRecord(ctx->ev[5], st);
   launch_radix_sort(&sb, key_bits, st);
   hipEventRecord(ctx->ev[6], st);

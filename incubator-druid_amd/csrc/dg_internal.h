@@ -144,7 +144,9 @@ struct GbJob {
   int32_t desc;                 // descending cursors: the floatSum pass runs each cell backwards
   int32_t seg_slot, seg_shift;  // key field of the segment (0 / 0 when the groups are merged)
   int32_t bucket_shift, bucket_bits;
-  ColView dims[kMaxGroupDims];
+  ColView dims[kMaxGroupDims];           // dictionary ids (a multi-value dimension: its value stream)
+  ColView moff[kMaxGroupDims];           // multi-value dimension: row value offsets (VIEW_ABSENT otherwise)
+  int32_t multi;                         // some dimension is multi-value: rows explode into groupings
   const int32_t* remap[kMaxGroupDims];  // local dictionary id -> merged id (null: identity)
   int32_t null_gid[kMaxGroupDims];      // merged id of the null value (a missing dimension's rows)
   int32_t dim_shift[kMaxGroupDims];
@@ -242,7 +244,8 @@ struct Column {
   std::vector<uint64_t> dict_hash;     // value_hash of every dictionary value (cross-segment merges)
   int bitmap_roaring = 0;
   bool has_bitmaps = false;
-  bool multi_value = false;            // row value lists not on the device: bitmap filters only
+  bool multi_value = false;            // row r's values: data[mv_off[r] .. mv_off[r + 1])
+  BlockColumn mv_off;                  // multi-value: rows + 1 value offsets (4-byte ints)
   std::vector<int64_t> bm_off;         // byte offset of each bitmap inside bm_bytes (4-byte aligned)
   std::vector<int32_t> bm_len;
   DevBuf bm_bytes;
@@ -428,8 +431,11 @@ constexpr int kMaxCallSegs = 1024;  // segments of one sort-based call (row-ref 
 inline int sort_tiles(int64_t n) { return (int)std::max<int64_t>(1, (n + kSortTile - 1) / kSortTile); }
 // selected rows -> (key, element index) in (segment, row) order + their aggregator inputs in
 // sb->payload; sb->n[0] = selected rows
+// selected rows (groupings of rows with multi-value dimensions) per keygen tile, and their total
+void launch_gb_count(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, uint32_t* tile_cnt, uint32_t* total,
+                     bool multi, hipStream_t s);
 void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
-                      hipStream_t s);
+                      hipStream_t s, bool multi = false);
 // stable LSD radix sort of sb->keys/refs[cur] on key bits [0, key_bits)
 void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s);
 // run heads of the sorted keys: sb->run_cnt = per-tile offsets, sb->n[1] = runs

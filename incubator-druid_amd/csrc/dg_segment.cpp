@@ -458,32 +458,77 @@ int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
   return DG_OK;
 }
 
-// Multi-value id parts (DictionaryEncodedColumnPartSerde.readMultiValuedColumn):
-// UNCOMPRESSED_MULTI_VALUE = VSizeColumnarMultiInts [0x01][numBytes][i32 size][size bytes]
-// (VSizeColumnarMultiInts.readFromByteBuffer); COMPRESSED + MULTI_VALUE_V3 =
-// [0x03][CompressedColumnarIntsSupplier offsets: 0x02, i32 total, i32 sizePer, u8 codec, GI]
-// [CompressedVSizeColumnarIntsSupplier values: 0x02, u8 numBytes, i32, i32, u8 codec, GI]
-// (V3CompressedVSizeColumnarMultiIntsSupplier.fromByteBuffer, CompressedColumnarIntsSupplier.fromByteBuffer).
-static int skip_multi_value_ids(Column* c, Slice* s, int version) {
+// Multi-value id parts (DictionaryEncodedColumnPartSerde.readMultiValuedColumn, :183-217), uploaded as
+// two block columns: mv_off (rows + 1 value offsets, 4-byte little-endian ints) and data (the value
+// ids). UNCOMPRESSED_MULTI_VALUE = VSizeColumnarMultiInts [0x01][numBytes][i32 size][payload: i32
+// count, count big-endian end byte offsets, big-endian numBytes values] (VSizeColumnarMultiInts.
+// readFromByteBuffer / get(index)): the offsets are converted at attach, the values read in place;
+// COMPRESSED + MULTI_VALUE_V3 = [0x03][CompressedColumnarIntsSupplier offsets: 0x02, i32 total,
+// i32 sizePer, u8 codec, GI][CompressedVSizeColumnarIntsSupplier values: 0x02, u8 numBytes, i32,
+// i32, u8 codec, GI] (V3CompressedVSizeColumnarMultiIntsSupplier.fromByteBuffer).
+static int parse_multi_value_ids(Context* ctx, Column* c, Slice* s, int version) {
+  BlockColumn& off = c->mv_off;
+  BlockColumn& val = c->data;
   if (version == 1) {
-    if (s->left() < 6 || s->p[0] != 0x01) return set_error(DG_ERR_FORMAT, "%s: bad VSize multi-ints", c->name.c_str());
+    if (s->left() < 10 || s->p[0] != 0x01) return set_error(DG_ERR_FORMAT, "%s: bad VSize multi-ints", c->name.c_str());
+    const int nb = s->p[1];
     const int32_t size = be32(s->p + 2);
-    if (size < 4 || s->left() < 6 + (int64_t)size) return set_error(DG_ERR_FORMAT, "%s: truncated multi-ints", c->name.c_str());
-    c->data.total = be32(s->p + 6);  // [i32 count] opens the payload
+    if (nb < 1 || nb > 4 || size < 4 || s->left() < 6 + (int64_t)size)
+      return set_error(DG_ERR_FORMAT, "%s: truncated multi-ints", c->name.c_str());
+    const uint8_t* pay = s->p + 6;
+    const int32_t count = be32(pay);
+    if (count < 0 || 4 + 4 * (int64_t)count > size) return set_error(DG_ERR_FORMAT, "%s: bad multi-ints count", c->name.c_str());
+    std::vector<int32_t> offs((size_t)count + 1, 0);
+    int64_t prev = 0;
+    for (int32_t r = 0; r < count; ++r) {
+      const int64_t e = be32(pay + 4 + 4 * (int64_t)r);
+      if (e < prev || e % nb || 4 + 4 * (int64_t)count + e > size)
+        return set_error(DG_ERR_FORMAT, "%s: bad multi-ints offsets", c->name.c_str());
+      offs[(size_t)r + 1] = (int32_t)(e / nb);
+      prev = e;
+    }
+    off.total = count + 1;
+    off.width = 4;
+    off.codec = CODEC_NONE;
+    int rc = upload_flat(&off, reinterpret_cast<const uint8_t*>(offs.data()),
+                         reinterpret_cast<const uint8_t*>(offs.data() + offs.size()));
+    if (rc) return rc;
+    val.width = nb;
+    val.total = (int32_t)(prev / nb);
+    val.codec = CODEC_NONE;
+    val.big_endian = 1;
+    const uint8_t* vp = pay + 4 + 4 * (int64_t)count;
+    rc = upload_flat(&val, vp, s->end);
+    if (rc) return rc;
     s->p += 6 + size;
     return DG_OK;
   }
   if (s->left() < 1 + 10 || s->p[0] != 0x03 || s->p[1] != 0x02)
     return set_error(DG_ERR_FORMAT, "%s: bad V3 multi-value ids", c->name.c_str());
-  c->data.total = be32(s->p + 2) - 1;  // rows + 1 offsets
+  off.total = be32(s->p + 2);
+  off.size_per = be32(s->p + 6);
+  off.codec = s->p[10];
+  off.width = 4;
+  off.log2_per = log2i(off.size_per);
   s->p += 1 + 10;
+  if (off.total < 1 || off.log2_per < 0 || (int64_t)off.size_per * 4 > kBlockBytes)
+    return set_error(DG_ERR_FORMAT, "%s: bad multi-value offsets header", c->name.c_str());
   GI offsets;
   if (!gi_read(*s, &offsets)) return set_error(DG_ERR_FORMAT, "%s: bad multi-value offsets", c->name.c_str());
+  int rc = upload_blocks(ctx, &off, offsets);
+  if (rc) return rc;
   if (s->left() < 11 || s->p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: bad multi-value values", c->name.c_str());
+  val.width = s->p[1];
+  val.total = be32(s->p + 2);
+  val.size_per = be32(s->p + 6);
+  val.codec = s->p[10];
+  val.log2_per = log2i(val.size_per);
   s->p += 11;
+  if (val.width < 1 || val.width > 4 || val.log2_per < 0)
+    return set_error(DG_ERR_FORMAT, "%s: bad multi-value values header", c->name.c_str());
   GI values;
   if (!gi_read(*s, &values)) return set_error(DG_ERR_FORMAT, "%s: bad multi-value value blocks", c->name.c_str());
-  return DG_OK;
+  return upload_blocks(ctx, &val, values);
 }
 
 int parse_string(Context* ctx, Column* c, Slice s) {
@@ -515,9 +560,8 @@ int parse_string(Context* ctx, Column* c, Slice s) {
   for (int32_t i = 0; i < dict.n; ++i) c->dict_hash[i] = c->dict_null[i] ? kNullValueHash : value_hash(c->dict[i]);
   BlockColumn& col = c->data;
   if (c->multi_value) {
-    // Row value lists are not uploaded: filters on the column run on its bitmap index, grouping on
-    // it is DG_ERR_UNSUPPORTED (column_view). Skip the id part to reach the bitmaps.
-    int rc = skip_multi_value_ids(c, &s, version);
+    // row value lists: filters run on the bitmap index, groupBy explodes the lists (dg_sort.hip)
+    int rc = parse_multi_value_ids(ctx, c, &s, version);
     if (rc) return rc;
   } else if (version == 0 || version == 3) {
     // UNCOMPRESSED_SINGLE_VALUE / UNCOMPRESSED_WITH_FLAGS: VSizeColumnarInts.readFromByteBuffer
@@ -664,7 +708,8 @@ static void index_bitmap_pieces(Column* c, const std::vector<uint8_t>& host) {
 }
 
 int64_t column_device_bytes(const Column& c) {
-  return (int64_t)(c.data.comp.n + c.data.raw.n + c.data.block_ptrs.n + c.bm_bytes.n);
+  return (int64_t)(c.data.comp.n + c.data.raw.n + c.data.block_ptrs.n + c.bm_bytes.n + c.mv_off.comp.n +
+                   c.mv_off.raw.n + c.mv_off.block_ptrs.n);
 }
 
 }  // namespace
@@ -789,9 +834,10 @@ int load_segment(Context* ctx, const char* dir, Segment** out) {
   if (!t || t->type != DG_COL_LONG) return set_error(DG_ERR_FORMAT, "%s: missing __time", dir);
   seg->nrows = t->data.total;
   for (auto& c : seg->columns) {
+    const int64_t rows = c->multi_value ? (int64_t)c->mv_off.total - 1 : c->data.total;
     if ((c->type == DG_COL_LONG || c->type == DG_COL_FLOAT || c->type == DG_COL_DOUBLE || c->type == DG_COL_STRING) &&
-        c->data.total != seg->nrows)
-      return set_error(DG_ERR_FORMAT, "%s: %d rows, segment has %lld", c->name.c_str(), c->data.total,
+        rows != seg->nrows)
+      return set_error(DG_ERR_FORMAT, "%s: %lld rows, segment has %lld", c->name.c_str(), (long long)rows,
                        (long long)seg->nrows);
   }
   int rc = read_time_bounds(seg.get());

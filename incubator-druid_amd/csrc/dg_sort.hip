@@ -124,6 +124,44 @@ __device__ __forceinline__ uint64_t gb_key(const GbJob& j, int64_t r, int64_t bu
   return k;
 }
 
+// Multi-value dimensions: a row groups under every combination of its dimensions' values (an empty
+// list = GROUP_BY_MISSING_VALUE, reported as null), the last dimension varying fastest
+// (GroupByQueryEngineV2.HashAggregateIterator.aggregateMultiValueDims :480-540,
+// StringGroupByColumnSelectorStrategy :47-57, :94-141). Row r's list of dimension d is
+// dims[d][moff[d][r] .. moff[d][r + 1]).
+__device__ __forceinline__ uint32_t gb_fanout(const GbJob& j, int64_t r) {
+  uint32_t n = 1;
+  for (int d = 0; d < j.ndims; ++d)
+    if (j.moff[d].kind != VIEW_ABSENT) {
+      const uint32_t a = load_id(j.moff[d], r), b = load_id(j.moff[d], r + 1);
+      n *= b > a ? b - a : 1u;
+    }
+  return n;
+}
+
+// key of grouping c (0 <= c < gb_fanout) of row r
+__device__ __forceinline__ uint64_t gb_key_multi(const GbJob& j, int64_t r, int64_t bucket, uint32_t c) {
+  uint64_t k = ((uint64_t)j.seg_slot << j.seg_shift) | ((uint64_t)bucket << j.bucket_shift);
+  for (int d = j.ndims - 1; d >= 0; --d) {
+    uint32_t g = (uint32_t)j.null_gid[d];
+    if (j.moff[d].kind != VIEW_ABSENT) {
+      const uint32_t a = load_id(j.moff[d], r), b = load_id(j.moff[d], r + 1);
+      if (b > a) {
+        const uint32_t m = b - a, i = c % m;
+        c /= m;
+        const uint32_t id = load_id(j.dims[d], (int64_t)a + i);
+        g = j.remap[d] ? (uint32_t)j.remap[d][id] : id;
+      }
+    } else if (j.dims[d].kind == VIEW_IDS) {
+      const uint32_t id = load_id(j.dims[d], r);
+      g = j.remap[d] ? (uint32_t)j.remap[d][id] : id;
+    }
+    k |= (uint64_t)g << j.dim_shift[d];
+  }
+  return k;
+}
+
+template <bool MULTI>
 __global__ __launch_bounds__(256) void k_gb_count(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                   uint32_t* __restrict__ cnt) {
   __shared__ uint32_t s_tmp[4];
@@ -133,7 +171,7 @@ __global__ __launch_bounds__(256) void k_gb_count(const GbJob* __restrict__ jobs
   uint32_t c = 0;
   for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
     int64_t b;
-    c += gb_select(j, r, &b) ? 1u : 0u;
+    if (gb_select(j, r, &b)) c += MULTI ? gb_fanout(j, r) : 1u;
   }
   const uint32_t t = block_sum_u32<256>(c, s_tmp);
   if (threadIdx.x == 0) cnt[blockIdx.x] = t;
@@ -150,6 +188,7 @@ __device__ __forceinline__ uint32_t elem_ref(uint64_t w, const uint32_t* refs, i
 // written at payload[index * pw] in the device slot encoding, in row order (coalesced column reads),
 // so the reduce after the sort gathers one payload record per element instead of one random read
 // per column.
+template <bool MULTI>
 __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                    const uint32_t* __restrict__ offs, uint64_t* __restrict__ keys,
                                                    uint32_t* __restrict__ refs, int kshift, AggPlan plan,
@@ -164,6 +203,23 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
     int64_t b = 0;
     const bool sel = r < r1 && gb_select(j, r, &b);
     uint32_t tot;
+    if (MULTI) {  // every grouping of the row is an element with the row's aggregator inputs
+      const uint32_t nf = sel ? gb_fanout(j, r) : 0u;
+      const uint32_t ex = block_scan_u32<256>(nf, &tot, s_tmp);
+      for (uint32_t e = 0; e < nf; ++e) {
+        const uint32_t idx = base + ex + e;
+        const uint64_t key = gb_key_multi(j, r, b, e);
+        if (refs) {
+          keys[idx] = key;
+          refs[idx] = idx;
+        } else {
+          keys[idx] = (key << kshift) | idx;
+        }
+        for (int a = 0; a < pw; ++a) payload[(size_t)idx * pw + a] = agg_in(j, plan, a, r);
+      }
+      base += tot;
+      continue;
+    }
     const uint32_t ex = block_scan_u32<256>(sel ? 1u : 0u, &tot, s_tmp);
     if (sel) {
       const uint32_t idx = base + ex;
@@ -179,16 +235,30 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
   }
 }
 
+void launch_gb_count(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, uint32_t* tile_cnt, uint32_t* total,
+                     bool multi, hipStream_t s) {
+  if (ntiles <= 0) {
+    (void)hipMemsetAsync(total, 0, 4, s);
+    return;
+  }
+  if (multi) hipLaunchKernelGGL(k_gb_count<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, tile_cnt);
+  else hipLaunchKernelGGL(k_gb_count<false>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, tile_cnt);
+  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, tile_cnt, ntiles, total);
+}
+
 void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
-                      hipStream_t s) {
+                      hipStream_t s, bool multi) {
   if (ntiles <= 0) {
     (void)hipMemsetAsync(sb->n, 0, 4, s);
     return;
   }
-  hipLaunchKernelGGL(k_gb_count, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt);
-  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, sb->tile_cnt, ntiles, sb->n);
-  hipLaunchKernelGGL(k_gb_keygen, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw);
+  launch_gb_count(d_jobs, d_tile_job, ntiles, sb->tile_cnt, sb->n, multi, s);
+  if (multi)
+    hipLaunchKernelGGL(k_gb_keygen<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw);
+  else
+    hipLaunchKernelGGL(k_gb_keygen<false>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -300,6 +300,15 @@ typedef struct {
   gindexed dict, bitmaps;
   int num_bytes;
   const uint8_t* vsize; /* uncompressed VSizeColumnarInts values (big-endian), or NULL */
+  /* multi-value ids: V3 = row offsets as CompressedColumnarInts (mv_total = rows + 1 ints, blocks of
+   * mv_size_per) + the values as CompressedVSizeColumnarInts in the fields above; VSizeColumnarMultiInts
+   * = mv_count rows, mv_ends (big-endian end byte offsets), mv_vals (big-endian values) */
+  int32_t mv_total, mv_size_per;
+  int mv_compression;
+  gindexed mv_blocks;
+  int32_t mv_count;
+  const uint8_t* mv_ends;
+  const uint8_t* mv_vals;
 } ocol;
 
 typedef struct {
@@ -429,18 +438,35 @@ static int parse_string(ocol* c, const uint8_t* p) {
   c->multi_value = (flags & 3) != 0;
   if (gi_read(&q, c->end, &c->dict)) return -1;
   if (c->multi_value) {
-    /* readMultiValuedColumn: only the bitmap index is restated (filters); skip the id part */
-    gindexed skip;
-    if (version == 1) { /* VSizeColumnarMultiInts [0x01][numBytes][i32 size][size bytes] */
+    /* readMultiValuedColumn (DictionaryEncodedColumnPartSerde.java:183-217) */
+    if (version == 1) {
+      /* VSizeColumnarMultiInts.readFromByteBuffer: [0x01][numBytes][i32 size][payload: i32 count,
+       * count big-endian end offsets (bytes into the values), the values as big-endian numBytes ints] */
       if (q[0] != 0x01) return -1;
-      q += 6 + be32(q + 2);
-    } else if (version == 2 && (flags & 2)) { /* V3: [0x03][offsets CompressedColumnarInts][values CompressedVSize] */
+      c->num_bytes = q[1];
+      const int32_t size = be32(q + 2);
+      if (c->num_bytes < 1 || c->num_bytes > 4 || size < 4) return -1;
+      c->mv_count = be32(q + 6);
+      if (c->mv_count < 0 || 4 + 4 * (int64_t)c->mv_count > size) return -1;
+      c->mv_ends = q + 10;
+      c->mv_vals = q + 10 + 4 * (int64_t)c->mv_count;
+      q += 6 + size;
+    } else if (version == 2 && (flags & 2)) {
+      /* V3CompressedVSizeColumnarMultiIntsSupplier.fromByteBuffer: [0x03][offsets: CompressedColumnarInts
+       * 0x02, i32 total, i32 sizePer, u8 codec, GI][values: CompressedVSizeColumnarInts] */
       if (q[0] != 0x03 || q[1] != 0x02) return -1;
+      c->mv_total = be32(q + 2);
+      c->mv_size_per = be32(q + 6);
+      c->mv_compression = q[10];
       q += 11;
-      if (gi_read(&q, c->end, &skip)) return -1;
+      if (gi_read(&q, c->end, &c->mv_blocks)) return -1;
       if (q[0] != 0x02) return -1;
+      c->num_bytes = q[1];
+      c->total = be32(q + 2);
+      c->size_per = be32(q + 6);
+      c->compression = q[10];
       q += 11;
-      if (gi_read(&q, c->end, &skip)) return -1;
+      if (gi_read(&q, c->end, &c->blocks)) return -1;
     } else {
       return -2;
     }
@@ -855,6 +881,80 @@ int or_dim_ids(void* h, const char* name, int32_t* out) {
   }
   free(buf);
   return done == c->total ? 0 : -1;
+}
+
+/* CompressedVSizeColumnarInts values of a column (its blocks / num_bytes / little_endian), n of them */
+static int read_vsize_ids(ocol* c, int64_t n, int32_t* out) {
+  uint8_t* buf = (uint8_t*)malloc(65536 + 16);
+  int64_t done = 0;
+  for (int32_t b = 0; b < c->blocks.n && done < n; ++b) {
+    memset(buf, 0, 65536 + 16);
+    int64_t got = decode_block(c, b, buf, 65536 + 16);
+    int64_t vals = c->size_per;
+    if (vals > n - done) vals = n - done;
+    if (got < vals * c->num_bytes) {
+      free(buf);
+      return -1;
+    }
+    for (int64_t k = 0; k < vals; ++k) {
+      const uint8_t* p = buf + k * c->num_bytes;
+      uint32_t v = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+      if (c->num_bytes < 4) v &= (1u << (8 * c->num_bytes)) - 1;
+      out[done + k] = (int32_t)v;
+    }
+    done += vals;
+  }
+  free(buf);
+  return done == n ? 0 : -1;
+}
+
+/* Row value lists of a multi-value dimension (V3CompressedVSizeColumnarMultiIntsSupplier.get(index):
+ * values offsets[index] .. offsets[index + 1]; VSizeColumnarMultiInts.get: the end byte offsets of
+ * rows index - 1 and index). offsets = rows + 1 ints; values NULL: *nvalues only. */
+int or_dim_multi(void* h, const char* name, int32_t* offsets, int32_t* values, int64_t* nvalues) {
+  oseg* s = (oseg*)h;
+  ocol* c = find_col(s, name);
+  if (!c || c->kind != OR_STRING || !c->multi_value) return -1;
+  const int64_t rows = s->nrows;
+  if (c->mv_ends) {
+    if (c->mv_count != rows) return -1;
+    int64_t prev = 0;
+    if (offsets) offsets[0] = 0;
+    for (int64_t r = 0; r < rows; ++r) {
+      const int64_t e = be32(c->mv_ends + 4 * r);
+      if (e < prev || e % c->num_bytes) return -1;
+      prev = e;
+      if (offsets) offsets[r + 1] = (int32_t)(e / c->num_bytes);
+    }
+    *nvalues = prev / c->num_bytes;
+    if (values)
+      for (int64_t k = 0; k < *nvalues; ++k) {
+        const uint8_t* p = c->mv_vals + k * c->num_bytes;
+        uint32_t v = 0;
+        for (int b = 0; b < c->num_bytes; ++b) v = (v << 8) | p[b];
+        values[k] = (int32_t)v;
+      }
+    return 0;
+  }
+  if (c->mv_total != rows + 1) return -1;
+  int32_t* off = offsets ? offsets : (int32_t*)malloc((size_t)(rows + 1) * 4);
+  ocol oc = *c; /* the offsets part: 4-byte little-endian ints */
+  oc.blocks = c->mv_blocks;
+  oc.compression = c->mv_compression;
+  oc.size_per = c->mv_size_per;
+  oc.num_bytes = 4;
+  int rc = read_vsize_ids(&oc, rows + 1, off);
+  if (!rc) {
+    for (int64_t r = 0; r < rows; ++r)
+      if (off[r + 1] < off[r] || off[0] != 0) rc = -1;
+  }
+  if (!rc) {
+    *nvalues = off[rows];
+    if (*nvalues > c->total) rc = -1;
+  }
+  if (!offsets) free(off);
+  if (rc || !values) return rc;
+  return read_vsize_ids(c, *nvalues, values);
 }
 
 /* rows of dictionary id `id`'s bitmap (BitmapIndexColumnPartSupplier.getBitmap) */

@@ -400,6 +400,7 @@ def lib():
         l.or_dim_value.restype = i32
         l.or_dim_value.argtypes = [vp, cp, i32, ctypes.POINTER(ctypes.c_void_p)]
         l.or_dim_ids.argtypes = [vp, cp, vp]
+        l.or_dim_multi.argtypes = [vp, cp, vp, vp, ctypes.POINTER(i64)]
         l.or_dim_bitmap.restype = i64
         l.or_dim_bitmap.argtypes = [vp, cp, i32, vp, i64]
         l.or_agg_init.argtypes = [ctypes.c_int, i32, vp]
@@ -541,6 +542,24 @@ class OracleSegment:
             if lib().or_dim_ids(self._h, dim.encode(), out.ctypes.data) != 0:
                 raise ValueError(f"cannot decode ids of {dim}")
             self._cache[key] = out
+        return self._cache[key]
+
+    def is_multi(self, dim: str) -> bool:
+        n = ctypes.c_int64()
+        return self.is_dim(dim) and lib().or_dim_multi(self._h, dim.encode(), None, None, ctypes.byref(n)) == 0
+
+    def multi(self, dim: str) -> Tuple[np.ndarray, np.ndarray]:
+        """Row value lists of a multi-value dimension: (offsets [rows + 1], values)."""
+        key = ("multi", dim)
+        if key not in self._cache:
+            n = ctypes.c_int64()
+            off = np.zeros(self.num_rows + 1, dtype=np.int32)
+            if lib().or_dim_multi(self._h, dim.encode(), off.ctypes.data, None, ctypes.byref(n)) != 0:
+                raise ValueError(f"cannot decode row lists of {dim}")
+            vals = np.zeros(max(n.value, 1), dtype=np.int32)
+            if lib().or_dim_multi(self._h, dim.encode(), off.ctypes.data, vals.ctypes.data, ctypes.byref(n)) != 0:
+                raise ValueError(f"cannot decode row lists of {dim}")
+            self._cache[key] = (off, vals[:n.value])
         return self._cache[key]
 
     def bitmap_rows(self, dim: str, idx: int) -> np.ndarray:
@@ -1587,24 +1606,53 @@ def merge_topn(query, per_segment: List[List]) -> List:
 def groupby_segment(seg: OracleSegment, query) -> List[Tuple[int, Tuple, Dict]]:
     mask = filter_mask(seg, o_optimize(query.filter))
     dims = query.dimensions
-    dicts, idcols = [], []
+    dicts, cols = [], []
     for d in dims:
-        if seg.is_dim(d):
+        if seg.is_dim(d) and seg.is_multi(d):
+            # a multi-value row groups under every value of its list; an empty list under
+            # GROUP_BY_MISSING_VALUE, reported as null (StringGroupByColumnSelectorStrategy.java:47-57,
+            # :130-141): the extra last id
+            off, vals = seg.multi(d)
+            dicts.append(list(seg.dictionary(d)) + [None])
+            cols.append((off.astype(np.int64), vals.astype(np.int64)))
+        elif seg.is_dim(d):
             dicts.append(seg.dictionary(d))
-            idcols.append(seg.ids(d).astype(np.int64))
+            cols.append(seg.ids(d).astype(np.int64))
         else:
             dicts.append([None])
-            idcols.append(np.zeros(seg.num_rows, np.int64))
+            cols.append(np.zeros(seg.num_rows, np.int64))
     out = []
     for bt, r0, r1 in cursor_buckets(seg, query):
         rows = np.nonzero(mask[r0:r1])[0].astype(np.int32) + r0
         if len(rows) == 0:
             continue
-        key = np.zeros(len(rows), dtype=np.int64)
-        for d, col in zip(dicts, idcols):
-            key = key * len(d) + col[rows]
+        # every row's groupings: the cartesian product of its dimensions' values, the last dimension
+        # fastest (GroupByQueryEngineV2.HashAggregateIterator.aggregateMultiValueDims :480-540)
+        m = [np.ones(len(rows), np.int64) if not isinstance(c, tuple) else
+             np.maximum(c[0][rows + 1] - c[0][rows], 1) for c in cols]
+        n_el = np.prod(np.stack(m), axis=0) if m else np.ones(len(rows), np.int64)
+        erows = np.repeat(rows, n_el)
+        first = np.repeat(np.cumsum(n_el) - n_el, n_el)
+        comb = np.arange(len(erows), dtype=np.int64) - first
+        er_i = np.repeat(np.arange(len(rows)), n_el)
+        parts = [None] * len(cols)
+        for di in range(len(cols) - 1, -1, -1):
+            c = cols[di]
+            md = m[di][er_i]
+            idx = comb % md
+            comb //= md
+            if isinstance(c, tuple):
+                off, vals = c
+                ln = off[erows + 1] - off[erows]
+                parts[di] = np.where(ln == 0, len(dicts[di]) - 1, vals[np.minimum(off[erows] + idx, len(vals) - 1)]
+                                     if len(vals) else 0)
+            else:
+                parts[di] = c[erows]
+        key = np.zeros(len(erows), dtype=np.int64)
+        for d, col in zip(dicts, parts):
+            key = key * len(d) + col
         uniq, inv = np.unique(key, return_inverse=True)
-        states = aggregate_groups(seg, query.aggregations, rows, inv.astype(np.int32), len(uniq))
+        states = aggregate_groups(seg, query.aggregations, erows.astype(np.int32), inv.astype(np.int32), len(uniq))
         for g, k in enumerate(uniq):
             vals = []
             kk = int(k)

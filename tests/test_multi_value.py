@@ -1,11 +1,13 @@
 """Multi-value string dimensions: the V3 compressed and
 UNCOMPRESSED_MULTI_VALUE id layouts are parsed at attach; filters on the column run on its bitmap
-index (a row matches when any of its values matches, an empty row is [null]); grouping on it is
+index (a row matches when any of its values matches, an empty row is [null]); groupBy explodes each
+row into every combination of its dimensions' values (GroupByQueryEngineV2.aggregateMultiValueDims
+:480-540: duplicates in a row's list count twice); topN over a multi-value dimension is
 DG_ERR_UNSUPPORTED (the Java factory keeps its CPU engine for those queries).
 
-CPU: the writer's bitmaps through the oracle's filter evaluation against the row-list semantics
-computed directly from the written rows. GPU: filter bitsets and filtered timeseries / topN /
-groupBy (grouping on other dimensions) through the engine vs the oracle."""
+CPU: the writer's bitmaps and row lists through the oracle's restatement against the rows as written.
+GPU: filter bitsets, filtered timeseries / topN / groupBy and groupBy on the multi-value dimensions
+through the engine vs the oracle."""
 import importlib
 
 import numpy as np
@@ -61,8 +63,9 @@ def _segment(W, path, rows, bitmap, comp, seed=3):
     n = len(rows)
     dic, ids = W.encode_multi_strings(rows)
     s_vals = [str(x) for x in rng.integers(0, 10, n)]
+    dic2, ids2 = W.encode_multi_strings([list(rng.choice(["x", "y", "z"], int(rng.integers(1, 3)))) for _ in range(n)])
     spec = W.SegmentSpec(timestamps=np.sort(rng.integers(0, 86_400_000, n)).astype(np.int64),
-                         dims={"tags": (dic, ids), "s": W.encode_strings(s_vals)},
+                         dims={"tags": (dic, ids), "s": W.encode_strings(s_vals), "tags2": (dic2, ids2)},
                          metrics={"m": ("long", rng.integers(0, 1000, n)), "x": ("double", rng.normal(10, 2, n))})
     return W.write_segment(path, spec, bitmap=bitmap, compression=comp, lz4_mode="fast"), s_vals
 
@@ -77,6 +80,10 @@ def test_oracle_filters_follow_row_lists(Q, O, W, tmp_path, layout):
         assert np.array_equal(O.filter_mask(o, f.optimize()), _expected_mask(O, Q, f, rows, s_vals)), f
     with pytest.raises(ValueError):
         o.ids("tags")
+    off, vals = o.multi("tags")  # the row lists restated from the id part (V3 / VSizeColumnarMultiInts)
+    d = o.dictionary("tags")
+    assert [[d[v] for v in vals[off[r]:off[r + 1]]] for r in range(len(rows))] == [sorted(r) if r else [None] for r in rows]
+    assert o.is_multi("tags") and not o.is_multi("s")
 
 
 @pytest.mark.gpu
@@ -104,3 +111,34 @@ def test_gpu_multi_value_filters(Q, O, W, tmp_path, layout):
     with pytest.raises(Exception):
         R.run_query(Q.TopNQuery(intervals=[(0, 1 << 40)], dimension="tags", metric="m", threshold=5,
                                 aggregations=aggs), [g])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_gpu_groupby_multi_value_dimensions(Q, O, W, tmp_path, layout):
+    """groupBy on multi-value dimensions: one grouping per value (per combination over several
+    multi-value dimensions), merged over segments of both layouts' row-list encodings."""
+    R = importlib.import_module("incubator-druid_amd.runners")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    paths = [_segment(W, str(tmp_path / f"mv{i}"), _rows(30_000, seed=7 + i), *layout, seed=4 + i)[0] for i in range(2)]
+    g = [S.GpuSegment(p) for p in paths]
+    o = [O.OracleSegment(p) for p in paths]
+    aggs = [Q.count("rows"), Q.long_sum("m", "m"), Q.AggregatorFactory("doubleSum", "x", "x"),
+            Q.AggregatorFactory("floatSum", "fx", "x"), Q.AggregatorFactory("longMin", "mn", "m")]
+    cases = [
+        dict(dimensions=["tags"]),
+        dict(dimensions=["tags", "s"]),
+        dict(dimensions=["s", "tags", "tags2"]),
+        dict(dimensions=["tags2", "tags"], filter=Q.OrDimFilter([Q.SelectorDimFilter("tags", "a"),
+                                                                Q.SelectorDimFilter("s", "3")])),
+        dict(dimensions=["tags"], granularity="hour", filter=Q.BoundDimFilter("m", "100", "700", ordering="numeric")),
+    ]
+    for kw in cases:
+        q = Q.GroupByQuery(intervals=[(0, 1 << 40)], aggregations=aggs, **kw)
+        exp = O.run(q, o)
+        assert_results(q, R.run_query(q, g), exp)
+        assert_results(q, R.run_query(q, g[:1]), O.run(q, o[:1]))
+    # a row counts once per value of its list (duplicates included)
+    q = Q.GroupByQuery(intervals=[(0, 1 << 40)], aggregations=[Q.count("rows")], dimensions=["tags"])
+    off, _ = o[0].multi("tags")
+    assert sum(r.event["rows"] for r in R.run_query(q, g[:1])) == int(off[-1])
