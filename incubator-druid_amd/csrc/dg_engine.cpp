@@ -1583,6 +1583,22 @@ static int upload_gb_jobs(CallScratch* cs, std::vector<GbJob>& gj, const std::ve
   return DG_OK;
 }
 
+// elements of a keygen over rows with multi-value dimensions (one per grouping), counted on the
+// device before the sort buffers are sized
+static int count_elements(CallScratch* cs, GbJob* d_jobs, int32_t* d_tile, int ntiles, int64_t* total, hipStream_t st) {
+  const int nt = std::max(ntiles, 1);
+  uint32_t* d_cnt = dev_take<uint32_t>(cs, (size_t)nt + 4);
+  uint32_t* h_tot = host_take<uint32_t>(cs, 1);
+  if (!d_cnt || !h_tot) return set_error(DG_ERR_OOM, "element count");
+  DG_FLUSH(cs, st);
+  launch_gb_count(d_jobs, d_tile, ntiles, d_cnt, d_cnt + nt, true, st);
+  DG_HIP(hipMemcpyAsync(h_tot, d_cnt + nt, 4, hipMemcpyDeviceToHost, st));
+  int rc = finish_call(cs, st);
+  if (rc) return rc;
+  *total = *h_tot;
+  return DG_OK;
+}
+
 // floatSum of the per-segment engines (timeseries, topN), as the reference computes it: every
 // (segment, bucket[, id]) cell's float32 sum in row order, written over the cell's slot in the
 // accumulator tables (the scan kernels accumulate floatSum in fp64 first; this pass replaces it).
@@ -1596,13 +1612,19 @@ static int fsum_pass(CallScratch* cs, std::vector<GbJob>& gj, const std::vector<
   int64_t total = 0;
   int rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
   if (rc) return rc;
+  bool multi = false;
+  for (const GbJob& g : gj) multi |= g.multi != 0;
+  if (multi) {
+    rc = count_elements(cs, d_jobs, d_tile, ntiles, &total, st);
+    if (rc) return rc;
+  }
   SortBufs sb;
   rc = sort_bufs(cs, total, ntiles, key_bits, plan.n, &sb);
   if (rc) return rc;
   uint32_t* head_pos = dev_take<uint32_t>(cs, (size_t)total + 16);
   if (!head_pos) return set_error(DG_ERR_OOM, "floatSum runs");
   DG_FLUSH(cs, st);
-  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st);
+  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, multi);
   if (sort) launch_radix_sort(&sb, key_bits, st);
   launch_run_heads(&sb, st);
   launch_run_mark(&sb, head_pos, st);
@@ -1979,6 +2001,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   std::vector<int64_t> card(n, 1), tiles_rows(n, 0);
   std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db;
+  bool any_multi = false;
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
@@ -2007,7 +2030,12 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     if (dc) {
       if (dim && !dc->order_set[t->dim_order])
         return set_error(DG_ERR_ARG, "order slot %d of %s not set (dg_segment_set_dim_order)", t->dim_order, t->dimension);
-      rc = column_view(dc, cs, &db, &j.key, st);
+      if (dc->multi_value) {  // every value of a row's list aggregates the row
+        rc = multi_view(dc, cs, &db, &j.key, &j.key_off, st);
+        any_multi = true;
+      } else {
+        rc = column_view(dc, cs, &db, &j.key, st);
+      }
       if (rc) return rc;
       card[i] = std::max<int64_t>((int64_t)dc->dict.size(), 1);
     } else {
@@ -2099,9 +2127,22 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       h_jobs[i] = fixed;
     }
   }
-  DG_FLUSH(cs, st);
-  launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
-                   d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
+  if (any_multi) {
+    // multi-value dimension: per-(row, value) atomics into identity-initialised tables
+    uint64_t* d_init;
+    uint64_t* h_init = up_take<uint64_t>(cs, rec, &d_init, st);
+    if (!h_init) return set_error(DG_ERR_OOM, "topN table init");
+    h_init[0] = 0;
+    for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
+    DG_FLUSH(cs, st);
+    for (int i = 0; i < n; ++i)
+      if (cur[i].any) launch_fill_u64(jobs[i].out, jobs[i].nbuckets, rec, d_init, st);
+    launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
+  } else {
+    DG_FLUSH(cs, st);
+    launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
+                     d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
+  }
   ht.mark("bins_launched");
   if (has_float_sum(plan)) {
     // floatSum as the reference adds it: float32, one row at a time per (cursor, dictionary id)
@@ -2129,6 +2170,9 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       f.nbounds = gr.nb + 1;
       f.ndims = 1;
       f.dims[0] = jobs[i].key;  // VIEW_ABSENT for a missing dimension: id 0 (its null value)
+      f.moff[0] = jobs[i].key_off;
+      f.multi = any_multi;
+      f.skip_empty = 1;
       f.dim_bits[0] = ib;
       f.bucket_shift = ib;
       f.bucket_bits = bb;
@@ -2994,17 +3038,9 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   int64_t total = 0;
   rc = upload_gb_jobs(cs, gj, rows, &d_jobs, &d_tile, &ntiles, &total, st);
   if (rc) return rc;
-  if (any_multi) {
-    // rows explode into one element per grouping: count them first to size the sort
-    uint32_t* d_cnt = dev_take<uint32_t>(cs, (size_t)std::max(ntiles, 1) + 4);
-    uint32_t* h_tot = host_take<uint32_t>(cs, 1);
-    if (!d_cnt || !h_tot) return set_error(DG_ERR_OOM, "groupBy element count");
-    DG_FLUSH(cs, st);
-    launch_gb_count(d_jobs, d_tile, ntiles, d_cnt, d_cnt + std::max(ntiles, 1), true, st);
-    DG_HIP(hipMemcpyAsync(h_tot, d_cnt + std::max(ntiles, 1), 4, hipMemcpyDeviceToHost, st));
-    rc = finish_call(cs, st);
+  if (any_multi) {  // rows explode into one element per grouping: count them first to size the sort
+    rc = count_elements(cs, d_jobs, d_tile, ntiles, &total, st);
     if (rc) return rc;
-    total = *h_tot;  // (a 32-bit count: more elements than that are not representable anyway)
   }
   SortBufs sb;
   rc = sort_bufs(cs, total, ntiles, key_bits, na, &sb);

@@ -117,7 +117,8 @@ struct ScanJob {
   int32_t key_card;         // topN over granularity buckets: key = bucket * key_card + id (0: key = id)
   ColView vals[kMaxAggs];   // input column per aggregator
   const uint32_t* agg_bits[kMaxAggs];  // FilteredAggregatorFactory row matcher per aggregator (null: all rows)
-  ColView key;              // topN: dimension ids
+  ColView key;              // topN: dimension ids (a multi-value dimension: its value stream)
+  ColView key_off;          // topN over a multi-value dimension: row value offsets (VIEW_ABSENT otherwise)
   uint64_t* out;            // accumulator table of this segment
 };
 
@@ -147,6 +148,7 @@ struct GbJob {
   ColView dims[kMaxGroupDims];           // dictionary ids (a multi-value dimension: its value stream)
   ColView moff[kMaxGroupDims];           // multi-value dimension: row value offsets (VIEW_ABSENT otherwise)
   int32_t multi;                         // some dimension is multi-value: rows explode into groupings
+  int32_t skip_empty;                    // an empty value list yields no element (topN) instead of null (groupBy)
   const int32_t* remap[kMaxGroupDims];  // local dictionary id -> merged id (null: identity)
   int32_t null_gid[kMaxGroupDims];      // merged id of the null value (a missing dimension's rows)
   int32_t dim_shift[kMaxGroupDims];

@@ -449,15 +449,22 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
   const int na = plan.n;
 
   if (TOPN) {
+    // topN over a multi-value dimension (PooledTopNAlgorithm.scanAndAggregate: every value of the
+    // row's list aggregates the row, an empty list none): atomics into the [keys][1 + naggs] table
+    const bool mv = j.key_off.kind != VIEW_ABSENT;
     for (int64_t r = row0 + threadIdx.x; r < row_end; r += 256) {
       int64_t b;
       if (!row_selected(j, r, &b)) continue;
-      const uint32_t id = load_id(j.key, r);
-      uint64_t* rec = j.out + (size_t)id * (na + 1);
-      atomicAdd(reinterpret_cast<unsigned long long*>(rec), 1ull);
+      const uint32_t k0 = mv ? load_id(j.key_off, r) : 0u, k1 = mv ? load_id(j.key_off, r + 1) : 1u;
+      for (uint32_t k = k0; k < k1; ++k) {
+        const uint32_t id = mv ? load_id(j.key, k) : (j.key.kind == VIEW_IDS ? load_id(j.key, r) : 0u);
+        const uint32_t key = j.key_card ? (uint32_t)b * (uint32_t)j.key_card + id : id;
+        uint64_t* rec = j.out + (size_t)key * (na + 1);
+        atomicAdd(reinterpret_cast<unsigned long long*>(rec), 1ull);
 #pragma unroll
-      for (int a = 0; a < kMaxAggs; ++a) {
-        if (a < na) atomic_op(plan.op[a], rec + 1 + a, agg_in(j, plan, a, r));
+        for (int a = 0; a < kMaxAggs; ++a) {
+          if (a < na) atomic_op(plan.op[a], rec + 1 + a, agg_in(j, plan, a, r));
+        }
       }
     }
     return;

@@ -134,7 +134,7 @@ __device__ __forceinline__ uint32_t gb_fanout(const GbJob& j, int64_t r) {
   for (int d = 0; d < j.ndims; ++d)
     if (j.moff[d].kind != VIEW_ABSENT) {
       const uint32_t a = load_id(j.moff[d], r), b = load_id(j.moff[d], r + 1);
-      n *= b > a ? b - a : 1u;
+      n *= b > a ? b - a : (j.skip_empty ? 0u : 1u);
     }
   return n;
 }

@@ -1531,7 +1531,8 @@ def topn_segment(seg: OracleSegment, query) -> List:
     out = []
     dim_present = seg.is_dim(query.dimension)
     dictionary = seg.dictionary(query.dimension) if dim_present else [None]
-    ids_all = seg.ids(query.dimension) if dim_present else np.zeros(seg.num_rows, np.int32)
+    multi = seg.multi(query.dimension) if dim_present and seg.is_multi(query.dimension) else None
+    ids_all = seg.ids(query.dimension) if dim_present and multi is None else np.zeros(seg.num_rows, np.int32)
     # TopNQueryQueryToolChest.preMergeQueryDecoration (:553-561): a threshold <= minTopNThreshold
     # (context value, else TopNQueryConfig.minTopNThreshold = 1000) runs per segment with that minimum
     min_t = int(query.context.get("minTopNThreshold", 1000))
@@ -1541,7 +1542,16 @@ def topn_segment(seg: OracleSegment, query) -> List:
     for bt, r0, r1 in cursor_buckets(seg, query, desc):
         rows = _cursor_rows(mask, r0, r1, desc)
         card = len(dictionary)
-        gids = ids_all[rows]
+        if multi is not None:
+            # a multi-value row aggregates into every value of its list, an empty list into none
+            # (PooledTopNAlgorithm.scanAndAggregate* loops over dimValues.size())
+            off, vals = multi
+            n_el = (off[rows + 1] - off[rows]).astype(np.int64)
+            pos = np.repeat(off[rows].astype(np.int64) - np.cumsum(n_el) + n_el, n_el) + np.arange(int(n_el.sum()))
+            rows = np.repeat(rows, n_el).astype(np.int32)
+            gids = vals[pos].astype(np.int32)
+        else:
+            gids = ids_all[rows]
         states = aggregate_groups(seg, query.aggregations, rows, gids, card)
         touched = np.zeros(card, dtype=bool)
         touched[gids] = True

@@ -2,12 +2,12 @@
 UNCOMPRESSED_MULTI_VALUE id layouts are parsed at attach; filters on the column run on its bitmap
 index (a row matches when any of its values matches, an empty row is [null]); groupBy explodes each
 row into every combination of its dimensions' values (GroupByQueryEngineV2.aggregateMultiValueDims
-:480-540: duplicates in a row's list count twice); topN over a multi-value dimension is
-DG_ERR_UNSUPPORTED (the Java factory keeps its CPU engine for those queries).
+:480-540: duplicates in a row's list count twice); topN aggregates a row into every value of its
+list (PooledTopNAlgorithm, an empty list into none).
 
 CPU: the writer's bitmaps and row lists through the oracle's restatement against the rows as written.
-GPU: filter bitsets, filtered timeseries / topN / groupBy and groupBy on the multi-value dimensions
-through the engine vs the oracle."""
+GPU: filter bitsets, filtered timeseries / topN / groupBy, and groupBy / topN on the multi-value
+dimensions through the engine vs the oracle."""
 import importlib
 
 import numpy as np
@@ -108,10 +108,12 @@ def test_gpu_multi_value_filters(Q, O, W, tmp_path, layout):
     q = Q.GroupByQuery(intervals=[(0, 1 << 40)], dimensions=["s"], aggregations=aggs,
                        filter=Q.InDimFilter("tags", ["a", "e"]))
     assert_results(q, R.run_query(q, [g]), O.run(q, [o]))
-    with pytest.raises(Exception):
-        R.run_query(Q.TopNQuery(intervals=[(0, 1 << 40)], dimension="tags", metric="m", threshold=5,
-                                aggregations=aggs), [g])
-
+    # topN over the multi-value dimension: every value of a row's list aggregates the row
+    for kw in (dict(metric="m"), dict(metric={"type": "dimension", "ordering": "lexicographic"}),
+               dict(metric="fx", granularity="hour")):
+        q = Q.TopNQuery(intervals=[(0, 1 << 40)], dimension="tags", threshold=4,
+                        aggregations=aggs + [Q.AggregatorFactory("floatSum", "fx", "x")], **kw)
+        assert_results(q, R.run_query(q, [g]), O.run(q, [o]))
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("layout", LAYOUTS)
