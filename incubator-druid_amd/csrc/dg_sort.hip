@@ -533,73 +533,47 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ 
                                                    int64_t cap, uint32_t* __restrict__ head_pos,
                                                    int64_t* __restrict__ carry_g, uint64_t* __restrict__ carry_slots,
                                                    int64_t* __restrict__ open_g) {
+  // Each wave reduces its own contiguous quarter of the tile (kWSeg elements, 16 chunks of 64): a
+  // segmented wave scan per chunk with the open run carried in registers, no barriers. A run that
+  // crosses a quarter boundary is finished like one crossing a tile boundary: the quarter holding
+  // its head writes it open (device encoding, listed in open_g), every later quarter's share goes to
+  // that quarter's carry slot (k_gb_carry folds it in, k_gb_open_finalize finalizes).
+  constexpr int kWSeg = kSortTile / 4;
   __shared__ uint64_t s_key[kSortTile + 2];  // [0] = element before the tile, [1 + x] = element x
-  __shared__ uint32_t s_ref[kSortTile];
-  __shared__ uint32_t s_tmp[4];
-  __shared__ uint64_t s_wv[4];
-  __shared__ int s_wf[4];
+  __shared__ uint32_t s_heads[4];
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) {
-    carry_g[blockIdx.x] = -1;
-    open_g[blockIdx.x] = -1;
+  const int64_t wt = (int64_t)blockIdx.x * 4 + wave;  // wave tile (carry / open slot)
+  if (lane == 0) {
+    carry_g[wt] = -1;
+    open_g[wt] = -1;
   }
   if (base >= n) return;
   const int tile_n = (int)min<int64_t>(kSortTile, (int64_t)n - base);
   const uint64_t kmask = kshift ? ((1ull << kshift) - 1ull) : 0ull;
-  for (int x = tid; x < tile_n; x += kST) {
-    const uint64_t w = keys[base + x];
+  const int wbase = wave * kWSeg;
+  uint32_t idx_of[kSPT];
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) {
+    const int x = wbase + c * 64 + lane;
+    uint64_t w = 0;
+    if (x < tile_n) w = keys[base + x];
     s_key[1 + x] = w >> kshift;
-    s_ref[x] = REFS ? refs[base + x] : (uint32_t)(w & kmask);
+    idx_of[c] = REFS ? (x < tile_n ? refs[base + x] : 0u) : (uint32_t)(w & kmask);
   }
   const bool has_next = base + kSortTile < n;
   if (tid == 0) {
     s_key[0] = base > 0 ? keys[base - 1] >> kshift : ~(keys[0] >> kshift);
     if (has_next) s_key[1 + kSortTile] = keys[base + kSortTile] >> kshift;
   }
-  __syncthreads();
-  const int na = plan.n, rec = na + 1;
-  const int64_t G0 = run_off[blockIdx.x];  // groups whose head lies in an earlier tile
-  // per element (chunk c, lane): run head / run end flags, group index (relative: -1 = the group
-  // carried in from an earlier tile), payload index
-  uint32_t hm = 0, tm = 0;
-  int32_t grel[kSPT];
-  uint32_t idx_of[kSPT];
-  int heads = 0;  // heads of the tile in the chunks before
-#pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
-    const int x = c * kST + tid;
-    const bool valid = x < tile_n;
-    const uint64_t k = s_key[1 + x];
-    const bool h = valid && k != s_key[x];
-    bool t = false;
-    if (valid) t = x + 1 < tile_n ? s_key[2 + x] != k : (!has_next || s_key[1 + kSortTile] != k);
-    hm |= (uint32_t)h << c;
-    tm |= (uint32_t)t << c;
-    uint32_t tot;
-    const uint32_t ex = block_scan_u32<kST>(h ? 1u : 0u, &tot, s_tmp);
-    grel[c] = heads + (int)ex + (h ? 1 : 0) - 1;
-    heads += (int)tot;
-    idx_of[c] = s_ref[valid ? x : 0];
-    if (h) {
-      out_keys[G0 + grel[c]] = k;
-      if (head_pos) head_pos[G0 + grel[c]] = (uint32_t)(base + x);
-    }
-  }
-  __syncthreads();  // the keys and refs are consumed: their LDS now holds inputs / group indices
-  uint64_t* s_x = s_key;            // [x] = the current slot's input of element x
-  int32_t* s_g = reinterpret_cast<int32_t*>(s_ref);  // [x] = relative group index of element x
-#pragma unroll
-  for (int c = 0; c < kSPT; ++c) s_g[c * kST + tid] = grel[c];
-  // Up to two payload slots per element are gathered once, together (one random record read per
-  // element; a second pass over the slots would miss the L2 again); wider payloads slot by slot.
+  // up to two payload slots per element, gathered once and together (random record reads in flight)
   constexpr int kRegSlots = 2;
   uint64_t xr[kSPT][kRegSlots];
   if (pw <= kRegSlots) {
 #pragma unroll
     for (int c = 0; c < kSPT; ++c) {
-      const bool valid = c * kST + tid < tile_n;
+      const bool valid = wbase + c * 64 + lane < tile_n;
       const uint64_t* pr = payload + (size_t)idx_of[c] * pw;
       if (pw == 2 && valid) {
         const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(pr);  // 16-byte aligned: pw == 2
@@ -611,59 +585,75 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ 
       }
     }
   }
-  // one slot at a time (-1 = rows aggregated): the 16 inputs (gathered above, or now: independent
-  // random loads in flight together) go to LDS, then are scanned chunk by chunk
+  __syncthreads();  // the tile's keys are in LDS
+  // run heads / ends of my elements, and the groups whose head lies before my quarter
+  uint32_t hm = 0, tm = 0;
+  uint32_t nh = 0;  // heads in my quarter
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) {
+    const int x = wbase + c * 64 + lane;
+    const bool valid = x < tile_n;
+    const uint64_t k = s_key[1 + x];
+    const bool h = valid && k != s_key[x];
+    bool t = false;
+    if (valid) t = x + 1 < tile_n ? s_key[2 + x] != k : (!has_next || s_key[1 + kSortTile] != k);
+    hm |= (uint32_t)h << c;
+    tm |= (uint32_t)t << c;
+    nh += (uint32_t)__popcll(__ballot(h));
+  }
+  if (lane == 0) s_heads[wave] = nh;
+  __syncthreads();
+  int64_t G = run_off[blockIdx.x];  // groups with a head before my quarter
+  for (int w = 0; w < wave; ++w) G += s_heads[w];
+  const int64_t Gq = G;
+  int32_t grel[kSPT];  // group of each element relative to Gq (-1: the group open before my quarter)
+  {
+    int heads = 0;
+#pragma unroll
+    for (int c = 0; c < kSPT; ++c) {
+      const bool h = (hm >> c) & 1u;
+      const uint64_t bal = __ballot(h);
+      const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      grel[c] = heads + below + (h ? 1 : 0) - 1;
+      heads += __popcll(bal);
+      if (h) {
+        const int x = wbase + c * 64 + lane;
+        out_keys[Gq + grel[c]] = s_key[1 + x];
+        if (head_pos) head_pos[Gq + grel[c]] = (uint32_t)(base + x);
+      }
+    }
+  }
+  const int na = plan.n, rec = na + 1;
+  const int wend = min(tile_n, wbase + kWSeg) - 1;  // my quarter's last element
   for (int a = -1; a < na; ++a) {
     const int kind = a < 0 ? DG_AGG_COUNT : plan.kind[a];
     if (kind == DG_AGG_FLOAT_SUM) continue;  // k_fsum_runs: float32 in row order
     const int op = a < 0 ? (int)OP_ADD_I64 : plan.op[a];
     const uint64_t ident = a < 0 ? 0ull : identity_of(op, kind);
-    {
-      uint64_t xv[kSPT];
+    uint64_t run = ident;  // the run open at the end of the previous chunk
 #pragma unroll
-      for (int c = 0; c < kSPT; ++c) {
-        const bool valid = c * kST + tid < tile_n;
-        if (!valid) xv[c] = ident;
-        else if (a < 0) xv[c] = 1ull;
-        else if (pw <= kRegSlots) xv[c] = a == 0 ? xr[c][0] : xr[c][1];
-        else xv[c] = payload[(size_t)idx_of[c] * pw + a];
-      }
-#pragma unroll
-      for (int c = 0; c < kSPT; ++c) s_x[c * kST + tid] = xv[c];
-    }
-    uint64_t run = ident;  // value of the run open at the end of the previous chunk
-#pragma unroll 1
     for (int c = 0; c < kSPT; ++c) {
-      const int x = c * kST + tid;
+      const int x = wbase + c * 64 + lane;
+      const bool valid = x < tile_n;
+      uint64_t xv;
+      if (!valid) xv = ident;
+      else if (a < 0) xv = 1ull;
+      else if (pw <= kRegSlots) xv = a == 0 ? xr[c][0] : xr[c][1];
+      else xv = payload[(size_t)idx_of[c] * pw + a];
       bool f;
-      uint64_t v = seg_scan_wave(op, s_x[x], (hm >> c) & 1u, &f);
-      if (lane == 63) {
-        s_wv[wave] = v;
-        s_wf[wave] = f;
-      }
-      __syncthreads();
-      uint64_t pre = run;  // what precedes my wave in the open run
-      uint64_t all = run;  // the open run at the end of the chunk
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const uint64_t wv = s_wv[w];
-        const uint64_t nx = s_wf[w] ? wv : combine_op(op, all, wv);
-        if (w < wave) pre = nx;
-        all = nx;
-      }
-      __syncthreads();
-      if (!f) v = combine_op(op, pre, v);
-      run = all;
-      if (x < tile_n) {
+      uint64_t v = seg_scan_wave(op, xv, (hm >> c) & 1u, &f);
+      if (!f) v = combine_op(op, run, v);
+      run = __shfl(v, 63, 64);
+      if (valid) {
         const bool t = (tm >> c) & 1u;
-        const int32_t gr = s_g[x];
-        if (t || x == tile_n - 1) {
-          if (gr >= 0) {  // a group of this tile: complete, or open at the tile's end
-            out_slots[(1 + a) * cap + G0 + gr] = t ? finalize_dev(kind, v) : v;
-            if (!t) open_g[blockIdx.x] = G0 + gr;
-          } else {  // the tile's share of a group that began earlier
-            carry_slots[(int64_t)blockIdx.x * rec + 1 + a] = v;
-            carry_g[blockIdx.x] = G0 - 1;
+        if (t || x == wend) {
+          const int32_t gr = grel[c];
+          if (gr >= 0) {  // a group headed in my quarter: complete, or open at the quarter's end
+            out_slots[(1 + a) * cap + Gq + gr] = t ? finalize_dev(kind, v) : v;
+            if (!t) open_g[wt] = Gq + gr;
+          } else {  // my quarter's share of a group headed earlier
+            carry_slots[wt * rec + 1 + a] = v;
+            carry_g[wt] = Gq - 1;
           }
         }
       }
@@ -719,9 +709,10 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
     hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
                        open_g);
-  const unsigned g = (unsigned)((nt + 255) / 256);
-  hipLaunchKernelGGL(k_gb_carry, dim3(g), dim3(256), 0, s, carry_g, carry_slots, (int64_t)nt, plan, out_slots, cap);
-  hipLaunchKernelGGL(k_gb_open_finalize, dim3(g), dim3(256), 0, s, open_g, (int64_t)nt, plan, out_slots, cap);
+  const int64_t nw = (int64_t)nt * 4;  // carry / open slots: one per wave quarter of a tile
+  const unsigned g = (unsigned)((nw + 255) / 256);
+  hipLaunchKernelGGL(k_gb_carry, dim3(g), dim3(256), 0, s, carry_g, carry_slots, nw, plan, out_slots, cap);
+  hipLaunchKernelGGL(k_gb_open_finalize, dim3(g), dim3(256), 0, s, open_g, nw, plan, out_slots, cap);
 }
 
 // ------------------------------------------------------------------------------------------------
