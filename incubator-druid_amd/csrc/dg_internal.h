@@ -428,6 +428,8 @@ void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, i
 constexpr int kTileRows = 2048;
 
 // dg_sort.hip
+constexpr int kMaxDigitBits = 8;  // radix digits of up to 8 bits (9-bit digits measured slower: 64-byte store runs)
+constexpr int kMaxBins = 1 << kMaxDigitBits;
 constexpr int kSortTile = 4096;  // elements per radix / run tile (256 threads x 16)
 constexpr int kMaxCallSegs = 1024;  // segments of one sort-based call (row-ref bases live in LDS)
 inline int sort_tiles(int64_t n) { return (int)std::max<int64_t>(1, (n + kSortTile - 1) / kSortTile); }

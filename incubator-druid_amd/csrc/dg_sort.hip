@@ -266,23 +266,23 @@ void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kST) void k_rs_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
                                                  int shift, int bits, uint32_t* __restrict__ hist, int ntiles) {
-  __shared__ uint32_t s_h[4 * 256];  // one histogram per wave (fewer same-address LDS atomics)
+  __shared__ uint32_t s_h[4 * kMaxBins];  // one histogram per wave (fewer same-address LDS atomics)
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
   const int nb = 1 << bits;
-  for (int i = threadIdx.x; i < 4 * 256; i += kST) s_h[i] = 0;
+  for (int i = threadIdx.x; i < 4 * kMaxBins; i += kST) s_h[i] = 0;
   __syncthreads();
   const int wave = threadIdx.x >> 6;
   if (base < n) {
 #pragma unroll 4
     for (int c = 0; c < kSPT; ++c) {
       const int64_t i = base + c * kST + threadIdx.x;
-      if (i < n) atomicAdd(&s_h[wave * 256 + (int)((keys[i] >> shift) & (uint64_t)(nb - 1))], 1u);
+      if (i < n) atomicAdd(&s_h[wave * kMaxBins + (int)((keys[i] >> shift) & (uint64_t)(nb - 1))], 1u);
     }
   }
   __syncthreads();
   for (int d = threadIdx.x; d < nb; d += kST)
-    hist[(size_t)d * ntiles + blockIdx.x] = s_h[d] + s_h[256 + d] + s_h[512 + d] + s_h[768 + d];
+    hist[(size_t)d * ntiles + blockIdx.x] = s_h[d] + s_h[kMaxBins + d] + s_h[2 * kMaxBins + d] + s_h[3 * kMaxBins + d];
 }
 
 // one workgroup per digit: exclusive scan of that digit's tile counts in place + the digit's total
@@ -328,8 +328,8 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
                                                     const uint32_t* __restrict__ bin_total, int ntiles) {
   __shared__ uint64_t s_k[kSortTile];
   __shared__ uint32_t s_v[REFS ? kSortTile : 1];
-  __shared__ uint32_t s_cnt[4 * 256];
-  __shared__ int64_t s_delta[256];  // global position of tile-sorted element i of digit d = s_delta[d] + i
+  __shared__ uint32_t s_cnt[4 * kMaxBins];
+  __shared__ int64_t s_delta[kMaxBins];  // global position of tile-sorted element i of digit d = s_delta[d] + i
   __shared__ uint32_t s_tmp[4];
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   const int nb = 1 << bits;
   const uint64_t dmask = (uint64_t)(nb - 1);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < 4 * 256; i += kST) s_cnt[i] = 0;
+  for (int i = tid; i < 4 * kMaxBins; i += kST) s_cnt[i] = 0;
   __syncthreads();
   uint64_t k[kSPT];
   uint32_t v[kSPT], rank[kSPT];
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
     k[c] = ok ? kin[base + x] : 0ull;
     if (REFS) v[c] = ok ? vin[base + x] : 0u;
   }
-  uint32_t* cnt = s_cnt + wave * 256;
+  uint32_t* cnt = s_cnt + wave * kMaxBins;
 #pragma unroll
   for (int c = 0; c < kSPT; ++c) {
     const bool ok = wbase + c * 64 + lane < tile_n;
@@ -367,18 +367,31 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   // per digit: tile offset (scan over digits of the tile's counts), wave offsets inside it, and the
   // digit's global base (earlier digits' totals + earlier tiles' counts of this digit)
   {
-    const uint32_t c0 = tid < nb ? s_cnt[tid] : 0u, c1 = tid < nb ? s_cnt[256 + tid] : 0u;
-    const uint32_t c2 = tid < nb ? s_cnt[512 + tid] : 0u, c3 = tid < nb ? s_cnt[768 + tid] : 0u;
+    // thread t: digits 2t and 2t + 1 (up to 512 digits)
+    uint32_t cw[2][4], ct[2], gt[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int d = 2 * tid + q;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) cw[q][w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
+      ct[q] = cw[q][0] + cw[q][1] + cw[q][2] + cw[q][3];
+      gt[q] = d < nb ? bin_total[d] : 0u;
+    }
     uint32_t tot;
-    const uint32_t toff = block_scan_u32<kST>(c0 + c1 + c2 + c3, &tot, s_tmp);
-    const uint32_t gtot = tid < nb ? bin_total[tid] : 0u;
-    const uint32_t gex = block_scan_u32<kST>(gtot, &tot, s_tmp);
-    if (tid < nb) {
-      s_cnt[tid] = toff;
-      s_cnt[256 + tid] = toff + c0;
-      s_cnt[512 + tid] = toff + c0 + c1;
-      s_cnt[768 + tid] = toff + c0 + c1 + c2;
-      s_delta[tid] = (int64_t)gex + (int64_t)hist[(size_t)tid * ntiles + blockIdx.x] - (int64_t)toff;
+    uint32_t toff = block_scan_u32<kST>(ct[0] + ct[1], &tot, s_tmp);
+    uint32_t gex = block_scan_u32<kST>(gt[0] + gt[1], &tot, s_tmp);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int d = 2 * tid + q;
+      if (d < nb) {
+        s_cnt[d] = toff;
+        s_cnt[kMaxBins + d] = toff + cw[q][0];
+        s_cnt[2 * kMaxBins + d] = toff + cw[q][0] + cw[q][1];
+        s_cnt[3 * kMaxBins + d] = toff + cw[q][0] + cw[q][1] + cw[q][2];
+        s_delta[d] = (int64_t)gex + (int64_t)hist[(size_t)d * ntiles + blockIdx.x] - (int64_t)toff;
+      }
+      toff += ct[q];
+      gex += gt[q];
     }
   }
   __syncthreads();
@@ -401,7 +414,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
 
 void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
   if (key_bits <= 0) return;
-  const int npass = (key_bits + 7) / 8;
+  const int npass = (key_bits + kMaxDigitBits - 1) / kMaxDigitBits;
   const int w = (key_bits + npass - 1) / npass;
   const int nt = sb->ntiles_sort;
   for (int p = 0, off = 0; p < npass; ++p, off += w) {
