@@ -341,14 +341,16 @@ def main():
     bytes_read = per_step("bytes_read")
     kernels = {}  # phase -> (kernel, algorithmic bytes per launch, launches per step, ms per step)
     if phases["decode"] > 0:
-        dk = "k_lzf_decode" if args.compression == "lzf" else "k_lz4_decode"
+        # LZ4: the light decoder (literal-heavy blocks) and the general one, both inside the phase
+        dk = "k_lzf_decode" if args.compression == "lzf" else "k_lz4_light+k_lz4_decode"
         kernels["decode"] = (dk if args.long_encoding == "longs" else dk + "+k_vsize_expand", bytes_read, 1,
                              phases["decode"])
     if isinstance(query, Q.GroupByQuery):
         phases.update({"keygen": per_step("keygen_ms"), "sort": per_step("sort_ms"), "reduce": per_step("reduce_ms")})
         passes = max(1, int(round(per_step("sort_passes"))))
         n_sel = selected_local
-        # one radix pass reads and writes every (key, row ref) once: 2 x 12 B per selected row
+        # one radix pass: the histogram reads every packed [key | row ref] word, the scatter reads and
+        # writes it once: 3 x 8 B per selected row
         kernels["sort"] = ("k_rs_hist+k_rs_binscan+k_rs_scatter", 24.0 * n_sel, passes, phases["sort"])
         kernels["keygen"] = ("k_gb_count+k_gb_keygen", n_sel * (3 + 3 + 12), 1, phases["keygen"])
     elif phases["aggregate"] > 0:

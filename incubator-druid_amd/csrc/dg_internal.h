@@ -166,7 +166,10 @@ struct SortBufs {
   uint64_t* keys[2];      // packed (refs null): [key | row ref in the low ref_bits bits]; else keys
   uint32_t* refs[2];      // row refs when the key and the ref do not fit one word, else null
   int ref_bits;           // packed: bits of the element index (the sort key starts there); else 0
-  uint64_t* payload;      // [cap][pw]: the aggregators' inputs of each element (device slot encoding)
+  uint64_t* payload;      // the aggregators' inputs of each element (device slot encoding): [cap][pw] by
+                          // element index, or (pcap != 0) [pw][pcap] by sorted position, carried by the sort
+  uint64_t* payload2;     // pcap != 0: the other buffer of the carried payload
+  int64_t pcap;
   int pw;
   int cur;                // which of the ping-pong buffers holds the result
   uint32_t* tile_cnt;     // keygen tiles: selected rows, then their offsets
@@ -441,6 +444,13 @@ void launch_gb_count(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles,
 void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
                       hipStream_t s, bool multi = false);
 // stable LSD radix sort of sb->keys/refs[cur] on key bits [0, key_bits)
+// bucketed sort (payload carried, sb->pcap != 0, packed keys): top kBucketBits key bits by LSD passes,
+// then each bucket (<= kBucketCap elements, else *overflow is set) sorted in LDS; false = not applicable.
+// bstart / bend: 1 << bucket_bits words each (bucket_bits <= kBucketBits).
+constexpr int kBucketBits = 17;  // at most this many bucket bits (chosen per query)
+constexpr int kBucketCap = 2048;
+bool sort_bucketed(SortBufs* sb, int key_bits, int bucket_bits, uint32_t* bstart, uint32_t* bend, uint32_t* overflow,
+                   hipStream_t s);
 void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s);
 // run heads of the sorted keys: sb->run_cnt = per-tile offsets, sb->n[1] = runs
 void launch_run_heads(SortBufs* sb, hipStream_t s);

@@ -82,6 +82,12 @@ __global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ a, int
   if (threadIdx.x == 0) *total = carry;
 }
 
+// payload word a of element / position i: by element index ([i][pw], pcap == 0) or carried by the
+// sort ([a][pcap], i = sorted position)
+__device__ __forceinline__ size_t pay_at(int pw, int64_t pcap, size_t i, int a) {
+  return pcap ? (size_t)a * (size_t)pcap + i : i * (size_t)pw + (size_t)a;
+}
+
 // segment of an element index (or row ref): the last job whose base <= it (bases ascend)
 __device__ __forceinline__ int locate_seg(const uint32_t* s_base, int njobs, uint32_t ref) {
   int lo = 0, hi = njobs - 1;
@@ -192,7 +198,7 @@ template <bool MULTI>
 __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                    const uint32_t* __restrict__ offs, uint64_t* __restrict__ keys,
                                                    uint32_t* __restrict__ refs, int kshift, AggPlan plan,
-                                                   uint64_t* __restrict__ payload, int pw) {
+                                                   uint64_t* __restrict__ payload, int pw, int64_t pcap) {
   __shared__ uint32_t s_tmp[4];
   const GbJob& j = jobs[tile_job[blockIdx.x]];
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
@@ -215,7 +221,7 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
         } else {
           keys[idx] = (key << kshift) | idx;
         }
-        for (int a = 0; a < pw; ++a) payload[(size_t)idx * pw + a] = agg_in(j, plan, a, r);
+        for (int a = 0; a < pw; ++a) payload[pay_at(pw, pcap, idx, a)] = agg_in(j, plan, a, r);
       }
       base += tot;
       continue;
@@ -229,7 +235,7 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
       } else {
         keys[idx] = (gb_key(j, r, b) << kshift) | idx;
       }
-      for (int a = 0; a < pw; ++a) payload[(size_t)idx * pw + a] = agg_in(j, plan, a, r);
+      for (int a = 0; a < pw; ++a) payload[pay_at(pw, pcap, idx, a)] = agg_in(j, plan, a, r);
     }
     base += tot;
   }
@@ -255,10 +261,10 @@ void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles
   launch_gb_count(d_jobs, d_tile_job, ntiles, sb->tile_cnt, sb->n, multi, s);
   if (multi)
     hipLaunchKernelGGL(k_gb_keygen<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw);
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->pcap);
   else
     hipLaunchKernelGGL(k_gb_keygen<false>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw);
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->pcap);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -412,25 +418,281 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   }
 }
 
-void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
-  if (key_bits <= 0) return;
-  const int npass = (key_bits + kMaxDigitBits - 1) / kMaxDigitBits;
-  const int w = (key_bits + npass - 1) / npass;
+// The same pass over packed words with the element's payload words carried along (sb->pcap != 0:
+// [pw][pcap] buffers): each payload word follows its key through the tile's LDS reorder, so the
+// stores stay coalesced and the payload ends up in sorted order.
+template <int PW>
+__global__ __launch_bounds__(kST) void k_rs_scatter_pay(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
+                                                        const uint64_t* __restrict__ pin, uint64_t* __restrict__ pout,
+                                                        int64_t pcap, const uint32_t* __restrict__ n_ptr, int shift,
+                                                        int bits, const uint32_t* __restrict__ hist,
+                                                        const uint32_t* __restrict__ bin_total, int ntiles) {
+  __shared__ uint64_t s_k[kSortTile];
+  __shared__ uint32_t s_cnt[4 * kMaxBins];
+  __shared__ int64_t s_delta[kMaxBins];
+  __shared__ uint32_t s_tmp[4];
+  const uint32_t n = *n_ptr;
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  if (base >= n) return;
+  const int tile_n = (int)min<int64_t>(kSortTile, (int64_t)n - base);
+  const int nb = 1 << bits;
+  const uint64_t dmask = (uint64_t)(nb - 1);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < 4 * kMaxBins; i += kST) s_cnt[i] = 0;
+  __syncthreads();
+  uint64_t k[kSPT];
+  uint32_t lp[kSPT];
+  const int wbase = wave * (kSortTile / 4);
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) {
+    const int x = wbase + c * 64 + lane;
+    k[c] = x < tile_n ? kin[base + x] : 0ull;
+  }
+  uint32_t* cnt = s_cnt + wave * kMaxBins;
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) {
+    const bool ok = wbase + c * 64 + lane < tile_n;
+    const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
+    const uint64_t peers = match_digit(d, bits, ok);
+    uint32_t prior = 0;
+    if (ok) prior = cnt[d];
+    lp[c] = prior + lanes_below(peers);  // rank among the wave's elements of digit d
+    if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  {
+    uint32_t cw[2][4], ct[2], gt[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int d = 2 * tid + q;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) cw[q][w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
+      ct[q] = cw[q][0] + cw[q][1] + cw[q][2] + cw[q][3];
+      gt[q] = d < nb ? bin_total[d] : 0u;
+    }
+    uint32_t tot;
+    uint32_t toff = block_scan_u32<kST>(ct[0] + ct[1], &tot, s_tmp);
+    uint32_t gex = block_scan_u32<kST>(gt[0] + gt[1], &tot, s_tmp);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int d = 2 * tid + q;
+      if (d < nb) {
+        s_cnt[d] = toff;
+        s_cnt[kMaxBins + d] = toff + cw[q][0];
+        s_cnt[2 * kMaxBins + d] = toff + cw[q][0] + cw[q][1];
+        s_cnt[3 * kMaxBins + d] = toff + cw[q][0] + cw[q][1] + cw[q][2];
+        s_delta[d] = (int64_t)gex + (int64_t)hist[(size_t)d * ntiles + blockIdx.x] - (int64_t)toff;
+      }
+      toff += ct[q];
+      gex += gt[q];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < kSPT; ++c) {
+    const bool ok = wbase + c * 64 + lane < tile_n;
+    const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
+    lp[c] = ok ? cnt[d] + lp[c] : 0xFFFFFFFFu;  // the element's place in the tile's digit order
+    if (ok) s_k[lp[c]] = k[c];
+  }
+  __syncthreads();
+  uint32_t pos[kSPT];  // global output position of tile-sorted element tid + j * kST
+#pragma unroll
+  for (int j = 0; j < kSPT; ++j) {
+    const int i = tid + j * kST;
+    pos[j] = 0;
+    if (i < tile_n) {
+      const uint64_t kk = s_k[i];
+      pos[j] = (uint32_t)(s_delta[(kk >> shift) & dmask] + i);
+      kout[pos[j]] = kk;
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < PW; ++w) {
+    uint64_t pv[kSPT];
+#pragma unroll
+    for (int c = 0; c < kSPT; ++c) {
+      const int x = wbase + c * 64 + lane;
+      pv[c] = x < tile_n ? pin[(size_t)w * pcap + base + x] : 0ull;
+    }
+    __syncthreads();  // every read of s_k (previous word) is done
+#pragma unroll
+    for (int c = 0; c < kSPT; ++c)
+      if (lp[c] != 0xFFFFFFFFu) s_k[lp[c]] = pv[c];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kSPT; ++j) {
+      const int i = tid + j * kST;
+      if (i < tile_n) pout[(size_t)w * pcap + pos[j]] = s_k[i];
+    }
+  }
+}
+
+// LSD passes over key bits [lo, hi) of the key field (above the element index bits), payload carried
+// when sb->pcap != 0
+static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
+  const int kb = hi - lo;
+  if (kb <= 0) return;
+  const int npass = (kb + kMaxDigitBits - 1) / kMaxDigitBits;
+  const int w = (kb + npass - 1) / npass;
   const int nt = sb->ntiles_sort;
-  for (int p = 0, off = 0; p < npass; ++p, off += w) {
-    const int bits = std::min(w, key_bits - off);
+  for (int p = 0, off = lo; p < npass; ++p, off += w) {
+    const int bits = std::min(w, hi - off);
     const int shift = sb->ref_bits + off;
     const int in = sb->cur, out = sb->cur ^ 1;
     hipLaunchKernelGGL(k_rs_hist, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->n, shift, bits, sb->hist, nt);
     hipLaunchKernelGGL(k_rs_binscan, dim3(1 << bits), dim3(1024), 0, s, sb->hist, nt, sb->bin_total);
-    if (sb->refs[in])
+    if (sb->pcap) {
+      switch (sb->pw) {
+#define DG_PAY_PASS(P)                                                                                               \
+  case P:                                                                                                            \
+    hipLaunchKernelGGL(k_rs_scatter_pay<P>, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->keys[out], sb->payload,     \
+                       sb->payload2, sb->pcap, sb->n, shift, bits, sb->hist, sb->bin_total, nt);                      \
+    break;
+        DG_PAY_PASS(0)
+        DG_PAY_PASS(1)
+        DG_PAY_PASS(2)
+        DG_PAY_PASS(3)
+        DG_PAY_PASS(4)
+#undef DG_PAY_PASS
+      }
+      std::swap(sb->payload, sb->payload2);
+    } else if (sb->refs[in]) {
       hipLaunchKernelGGL(k_rs_scatter<true>, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
                          sb->refs[out], sb->n, shift, bits, sb->hist, sb->bin_total, nt);
-    else
+    } else {
       hipLaunchKernelGGL(k_rs_scatter<false>, dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out], nullptr,
                          sb->n, shift, bits, sb->hist, sb->bin_total, nt);
+    }
     sb->cur = out;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// bucketed sort (high-cardinality keys): LSD passes carrying the payload over the top kBucketBits key
+// bits order the elements by bucket; then one workgroup per bucket sorts its (<= kBucketCap)
+// elements by the remaining key bits in LDS and permutes their payload inside the bucket's range.
+// The reduce then reads keys and payload sequentially (no random payload gather).
+// ------------------------------------------------------------------------------------------------
+__global__ void k_bucket_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, int bshift,
+                                uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
+  const uint32_t n = *n_ptr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t b = (uint32_t)(keys[i] >> bshift);
+    if (i == 0 || (uint32_t)(keys[i - 1] >> bshift) != b) bstart[b] = (uint32_t)i;
+    if (i + 1 == n || (uint32_t)(keys[i + 1] >> bshift) != b) bend[b] = (uint32_t)(i + 1);
+  }
+}
+
+template <int PW>
+__global__ __launch_bounds__(kST) void k_bucket_sort(uint64_t* __restrict__ keys, const uint64_t* __restrict__ pin,
+                                                     uint64_t* __restrict__ pout, int64_t pcap,
+                                                     const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+                                                     int lo_shift, int low_bits, uint32_t* __restrict__ overflow) {
+  __shared__ uint64_t s_w[2][kBucketCap];
+  __shared__ uint16_t s_p[2][kBucketCap];
+  __shared__ uint32_t s_cnt[4 * 256];
+  __shared__ uint32_t s_tmp[4];
+  const uint32_t lo = bstart[blockIdx.x], hi = bend[blockIdx.x];
+  const int m = (int)(hi - lo);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (m <= 0) return;
+  if (m > kBucketCap) {
+    if (tid == 0) atomicOr(overflow, 1u);
+    return;
+  }
+  for (int i = tid; i < m; i += kST) {
+    s_w[0][i] = keys[lo + i];
+    s_p[0][i] = (uint16_t)i;
+  }
+  constexpr int kQ = kBucketCap / 4;  // elements per wave quarter
+  int cur = 0;
+  const int npass = (low_bits + 7) / 8;
+  const int wbits = npass ? (low_bits + npass - 1) / npass : 0;
+  for (int p = 0, off = 0; p < npass; ++p, off += wbits) {
+    const int bits = min(wbits, low_bits - off);
+    const int nb = 1 << bits;
+    const int shift = lo_shift + off;
+    for (int i = tid; i < 4 * 256; i += kST) s_cnt[i] = 0;
+    __syncthreads();
+    uint32_t rank[kQ / 64];
+    uint32_t* cnt = s_cnt + wave * 256;
+#pragma unroll
+    for (int c = 0; c < kQ / 64; ++c) {  // wave w ranks its quarter [w * kQ, (w + 1) * kQ) in order
+      const int x = wave * kQ + c * 64 + lane;
+      const bool ok = x < m;
+      const uint32_t d = ok ? (uint32_t)((s_w[cur][x] >> shift) & (uint64_t)(nb - 1)) : 0u;
+      const uint64_t peers = match_digit(d, bits, ok);
+      uint32_t prior = 0;
+      if (ok) prior = cnt[d];
+      rank[c] = prior + lanes_below(peers);
+      if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    {
+      const uint32_t c0 = tid < nb ? s_cnt[tid] : 0u, c1 = tid < nb ? s_cnt[256 + tid] : 0u;
+      const uint32_t c2 = tid < nb ? s_cnt[512 + tid] : 0u, c3 = tid < nb ? s_cnt[768 + tid] : 0u;
+      uint32_t tot;
+      const uint32_t toff = block_scan_u32<kST>(c0 + c1 + c2 + c3, &tot, s_tmp);
+      if (tid < nb) {
+        s_cnt[tid] = toff;
+        s_cnt[256 + tid] = toff + c0;
+        s_cnt[512 + tid] = toff + c0 + c1;
+        s_cnt[768 + tid] = toff + c0 + c1 + c2;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < kQ / 64; ++c) {
+      const int x = wave * kQ + c * 64 + lane;
+      if (x < m) {
+        const uint64_t w = s_w[cur][x];
+        const uint32_t d = (uint32_t)((w >> shift) & (uint64_t)(nb - 1));
+        const uint32_t to = cnt[d] + rank[c];
+        s_w[cur ^ 1][to] = w;
+        s_p[cur ^ 1][to] = s_p[cur][x];
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  for (int i = tid; i < m; i += kST) {
+    keys[lo + i] = s_w[cur][i];
+    const size_t src = lo + s_p[cur][i];
+#pragma unroll
+    for (int w = 0; w < PW; ++w) pout[(size_t)w * pcap + lo + i] = pin[(size_t)w * pcap + src];
+  }
+}
+
+bool sort_bucketed(SortBufs* sb, int key_bits, int bucket_bits, uint32_t* bstart, uint32_t* bend, uint32_t* overflow,
+                   hipStream_t s) {
+  if (!sb->pcap || sb->refs[sb->cur] || key_bits <= bucket_bits || bucket_bits > kBucketBits) return false;
+  radix_passes(sb, key_bits - bucket_bits, key_bits, s);
+  const int bshift = sb->ref_bits + key_bits - bucket_bits;
+  (void)hipMemsetAsync(bstart, 0, sizeof(uint32_t) * ((size_t)1 << bucket_bits), s);
+  (void)hipMemsetAsync(bend, 0, sizeof(uint32_t) * ((size_t)1 << bucket_bits), s);
+  hipLaunchKernelGGL(k_bucket_bounds, dim3(4096), dim3(256), 0, s, sb->keys[sb->cur], sb->n, bshift, bstart, bend);
+  const int nbk = 1 << bucket_bits;
+  switch (sb->pw) {
+#define DG_BUCKET(P)                                                                                                  \
+  case P:                                                                                                             \
+    hipLaunchKernelGGL(k_bucket_sort<P>, dim3(nbk), dim3(kST), 0, s, sb->keys[sb->cur], sb->payload, sb->payload2,    \
+                       sb->pcap, bstart, bend, sb->ref_bits, key_bits - bucket_bits, overflow);                       \
+    break;
+    DG_BUCKET(0)
+    DG_BUCKET(1)
+    DG_BUCKET(2)
+    DG_BUCKET(3)
+    DG_BUCKET(4)
+#undef DG_BUCKET
+  }
+  std::swap(sb->payload, sb->payload2);
+  return true;
+}
+
+void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
+  if (key_bits <= 0) return;
+  radix_passes(sb, 0, key_bits, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -538,7 +800,7 @@ __device__ __forceinline__ uint64_t seg_scan_wave(int op, uint64_t v, bool head,
 }
 
 template <bool REFS>
-__global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw,
+__global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw, int64_t pcap,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ run_off, AggPlan plan,
@@ -587,6 +849,12 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ 
 #pragma unroll
     for (int c = 0; c < kSPT; ++c) {
       const bool valid = wbase + c * 64 + lane < tile_n;
+      if (pcap) {  // carried by the sort: sequential words at the sorted position
+        const size_t i = (size_t)(base + wbase + c * 64 + lane);
+        xr[c][0] = valid && pw >= 1 ? payload[i] : 0ull;
+        xr[c][1] = valid && pw >= 2 ? payload[(size_t)pcap + i] : 0ull;
+        continue;
+      }
       const uint64_t* pr = payload + (size_t)idx_of[c] * pw;
       if (pw == 2 && valid) {
         const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(pr);  // 16-byte aligned: pw == 2
@@ -652,7 +920,7 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ 
       if (!valid) xv = ident;
       else if (a < 0) xv = 1ull;
       else if (pw <= kRegSlots) xv = a == 0 ? xr[c][0] : xr[c][1];
-      else xv = payload[(size_t)idx_of[c] * pw + a];
+      else xv = payload[pcap ? pay_at(pw, pcap, (size_t)(base + x), a) : pay_at(pw, 0, idx_of[c], a)];
       bool f;
       uint64_t v = seg_scan_wave(op, xv, (hm >> c) & 1u, &f);
       if (!f) v = combine_op(op, run, v);
@@ -715,11 +983,11 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
   const int nt = sb->ntiles_sort;
   const uint32_t* refs = sb->refs[sb->cur];
   if (refs)
-    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
+    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->pcap, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
                        open_g);
   else
-    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
+    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->pcap, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
                        open_g);
   const int64_t nw = (int64_t)nt * 4;  // carry / open slots: one per wave quarter of a tile
@@ -749,7 +1017,7 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ head_pos, const uint64_t* __restrict__ payload,
-                                                   int pw, int agg, uint64_t* __restrict__ out_slots, int64_t cap,
+                                                   int pw, int64_t pcap, int agg, uint64_t* __restrict__ out_slots, int64_t cap,
                                                    int rec, int desc) {
   __shared__ uint32_t s_base[kMaxCallSegs];
   const uint32_t n = n_ptr[0], ng = n_ptr[1];
@@ -775,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
       }
       // the row's float input (identity 0.0f for a row its FilteredAggregator rejects: x + 0.0f == x
       // for every partial sum, which starts at +0.0f)
-      sum = sum + (float)__longlong_as_double((long long)payload[(size_t)idx * pw + agg]);
+      sum = sum + (float)__longlong_as_double((long long)payload[pay_at(pw, pcap, pcap ? i : idx, agg)]);
     }
     if (cur >= 0) total = first ? sum : total + sum;
     if (out_slots) {  // groupBy: the final ABI value
@@ -794,7 +1062,7 @@ void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, 
                       const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s, int desc) {
   const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (sb->cap + 255) / 256));
   hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->tile_cnt, ntiles,
-                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, sb->payload, sb->pw, agg,
+                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, sb->payload, sb->pw, sb->pcap, agg,
                      out_slots, cap, plan.n + 1, desc);
 }
 

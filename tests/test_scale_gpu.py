@@ -163,3 +163,39 @@ def test_cfg4_compound_filters_on_large_segments(R, Q, O, S, DG, tmp_path_factor
     for f in filters:
         q = Q.TimeseriesQuery(intervals=IV, aggregations=[Q.count("rows"), Q.long_sum("sumLongSequential")], filter=f)
         assert_results(q, R.run_query(q, g), O.run(q, o))
+
+
+_ORACLE_CACHE = {}
+
+
+@pytest.mark.parametrize("mode", ["bucketed", "bucket_bits_12", "overflow_fallback", "lsd"])
+def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
+    """The headline's shape (<= 4 aggregators) through each sort path: the opt-in bucketed sort (top
+    key bits by payload-carrying LSD passes, buckets sorted in LDS), smaller buckets, buckets too large
+    for the workgroup sort (the engine detects it and reruns the classic path) and the default LSD path."""
+    env = {"bucketed": {"DG_BUCKETED": "1"}, "bucket_bits_12": {"DG_BUCKET_BITS": "12"},
+           "overflow_fallback": {"DG_BUCKET_BITS": "8"}, "lsd": {"DG_NO_BUCKETED": "1"}}[mode]
+    for k in ("DG_BUCKET_BITS", "DG_NO_BUCKETED", "DG_BUCKETED"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g, o = cfg3
+    aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal"),
+            Q.float_sum("fsum", "sumFloatNormal")]
+    q = Q.GroupByQuery(intervals=IV, dimensions=["dimUniform", "dimHyperUnique"], aggregations=aggs)
+    part = R.groupby_per_device(g, q)[0]
+    if "exp" not in _ORACLE_CACHE:
+        _ORACLE_CACHE["exp"] = O.run(q, o)
+    exp = _ORACLE_CACHE["exp"]
+    assert len(part) == len(exp) > 1_000_000
+    t, keys, vals = _columns(exp, q.dimensions, aggs)
+    assert np.array_equal(part.times, t)
+    assert list(zip(*[list(c) for c in part.dims])) == keys
+    for a, col in zip(aggs, part.aggs):
+        e = vals[a.name]
+        if a.type == "doubleSum":
+            assert np.allclose(col, e, rtol=TOL["double"], atol=0)
+        elif a.type == "floatSum":
+            assert np.array_equal(col.astype(np.float32), e.astype(np.float32))
+        else:
+            assert np.array_equal(col, e.astype(col.dtype)), a.name
