@@ -800,7 +800,7 @@ __device__ __forceinline__ uint64_t seg_scan_wave(int op, uint64_t v, bool head,
 }
 
 template <bool REFS>
-__global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw, int64_t pcap,
+__global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw, int64_t pcap,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ run_off, AggPlan plan,
@@ -921,10 +921,20 @@ __global__ __launch_bounds__(kST) void k_gb_reduce(const uint64_t* __restrict__ 
       else if (a < 0) xv = 1ull;
       else if (pw <= kRegSlots) xv = a == 0 ? xr[c][0] : xr[c][1];
       else xv = payload[pcap ? pay_at(pw, pcap, (size_t)(base + x), a) : pay_at(pw, 0, idx_of[c], a)];
-      bool f;
-      uint64_t v = seg_scan_wave(op, xv, (hm >> c) & 1u, &f);
-      if (!f) v = combine_op(op, run, v);
-      run = __shfl(v, 63, 64);
+      uint64_t v = xv;
+      // a chunk of singleton groups (every element a run head and end: ~3 in 4 chunks at one group per
+      // row) needs no scan; otherwise the segmented scan with the open run carried in
+#ifndef DG_REDUCE_NOSKIP
+      const bool single = !valid || ((hm >> c) & (tm >> c) & 1u);
+#else
+      const bool single = false;
+#endif
+      if (__ballot(!single)) {
+        bool f;
+        v = seg_scan_wave(op, xv, (hm >> c) & 1u, &f);
+        if (!f) v = combine_op(op, run, v);
+        run = __shfl(v, 63, 64);
+      }
       if (valid) {
         const bool t = (tm >> c) & 1u;
         if (t || x == wend) {
