@@ -204,6 +204,31 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
   const int64_t r1 = min((int64_t)j.nrows, r0 + kTileRows);
   uint32_t base = offs[blockIdx.x];
+#ifndef DG_KEYGEN_NOFAST
+  constexpr bool kFast = true;
+#else
+  constexpr bool kFast = false;
+#endif
+  if (kFast && !MULTI && !j.bitset && j.time.kind == VIEW_ABSENT) {
+    // every row of the tile is selected (no filter, the interval covers the segment): element index =
+    // tile base + row offset, no per-block scan
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+      const uint32_t idx = base + (uint32_t)(r - r0);
+      const uint64_t key = gb_key(j, r, 0);
+      if (refs) {
+        keys[idx] = key;
+        refs[idx] = idx;
+      } else {
+        keys[idx] = (key << kshift) | idx;
+      }
+      if (pw == 2 && !pcap) {
+        *reinterpret_cast<ulonglong2*>(payload + (size_t)idx * 2) = make_ulonglong2(agg_in(j, plan, 0, r), agg_in(j, plan, 1, r));
+      } else {
+        for (int a = 0; a < pw; ++a) payload[pay_at(pw, pcap, idx, a)] = agg_in(j, plan, a, r);
+      }
+    }
+    return;
+  }
   for (int64_t rb = r0; rb < r1; rb += 256) {
     const int64_t r = rb + threadIdx.x;
     int64_t b = 0;
