@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 5
+#define DG_ABI_VERSION 6
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -303,6 +303,32 @@ typedef struct {
 
 int dg_groupby_run(dg_segment* const* segs, int32_t n_segs, const dg_scan* scan, const dg_groupby* g,
                    dg_result** out, dg_metrics* metrics);
+/* ---- groupBy limit push-down ----
+ * GroupByQuery.isApplyLimitPushDown (query/groupby/GroupByQuery.java:377-416: a limited DefaultLimitSpec
+ * whose ORDER BY columns are all grouping dimensions, no having spec, no subtotals) orders rows by
+ * getRowOrderingForPushDown (:423-528): the bucket time first (last with the sortByDimsFirst context
+ * flag on a non-ALL granularity), then the ORDER BY dimensions in their order, each under its
+ * StringComparator and direction (compareDimsForLimitPushDown :600-633), then the other dimensions
+ * ascending; the grouper keeps the first `limit` rows (LimitedBufferHashGrouper.java). dg_result_limit
+ * applies that to a dg_groupby_run / dg_merge result on the device: afterwards the result holds
+ * min(limit, groups) groups in that order (comparator-equal groups keep the result's natural order),
+ * fetched as before; dg_result_export refuses a limited result. */
+typedef struct {
+  int32_t dim;         /* index into dg_groupby.dimensions */
+  int32_t descending;  /* OrderByColumnSpec.Direction.DESCENDING */
+  const int32_t* rank; /* rank of every id of the result's dictionary of `dim` under the column's
+                          StringComparator (0 <= rank < cardinality, nulls first, comparator-equal
+                          values share a rank); NULL = LEXICOGRAPHIC, the id order itself */
+} dg_order_column;
+
+typedef struct {
+  const dg_order_column* columns;
+  int32_t n_columns;
+  int32_t limit;              /* > 0 */
+  int32_t sort_by_dims_first; /* query context sortByDimsFirst */
+} dg_limit;
+
+int dg_result_limit(dg_result* res, const dg_limit* spec);
 /* number of merged groups */
 int64_t dg_result_groups(const dg_result* res);
 /* groups [start, start + count), in result order (bucket time, then dimension values in Java

@@ -95,6 +95,15 @@ class dg_record_layout(ctypes.Structure):
                 ("record_size", ctypes.c_int32), ("big_endian", ctypes.c_int32)]
 
 
+class dg_order_column(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("descending", ctypes.c_int32), ("rank", ctypes.c_void_p)]
+
+
+class dg_limit(ctypes.Structure):
+    _fields_ = [("columns", ctypes.c_void_p), ("n_columns", ctypes.c_int32), ("limit", ctypes.c_int32),
+                ("sort_by_dims_first", ctypes.c_int32)]
+
+
 class dg_keyspace(ctypes.Structure):
     _fields_ = [("n_dims", ctypes.c_int32), ("card", ctypes.c_void_p), ("period_ms", ctypes.c_int64),
                 ("bucket0", ctypes.c_int64), ("n_buckets", ctypes.c_int64), ("universal_time", ctypes.c_int64),
@@ -110,7 +119,7 @@ EXPORTS = [
     "dg_segment_dim_dictionary", "dg_segment_set_dim_order", "dg_filter_bitmap", "dg_timeseries_run", "dg_topn_run", "dg_topn_merge", "dg_groupby_run",
     "dg_result_groups", "dg_result_fetch_groups", "dg_result_fetch_rows", "dg_result_dim_cardinality",
     "dg_result_dim_dictionary", "dg_result_release", "dg_keyspace_bits", "dg_result_export", "dg_keys_partition",
-    "dg_merge", "dg_records_pack", "dg_debug_lz4_decode",
+    "dg_merge", "dg_records_pack", "dg_debug_lz4_decode", "dg_result_limit",
 ]
 
 _lib = None
@@ -165,6 +174,7 @@ def lib():
         "dg_result_dim_cardinality": (i32, [vp, i32]),
         "dg_result_dim_dictionary": (ctypes.c_int, [vp, i32, vp, vp, P(i64)]),
         "dg_result_release": (None, [vp]),
+        "dg_result_limit": (ctypes.c_int, [vp, P(dg_limit)]),
         "dg_keyspace_bits": (ctypes.c_int, [P(dg_keyspace), P(i32)]),
         "dg_result_export": (ctypes.c_int, [vp, P(dg_keyspace), P(vp), vp, vp]),
         "dg_keys_partition": (ctypes.c_int, [vp, vp, i64, vp, i32, vp]),

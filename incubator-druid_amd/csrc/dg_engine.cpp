@@ -2904,6 +2904,7 @@ struct dg_result {
   std::vector<int64_t> bounds;  // calendar granularity: the call's bucket starts (bucket index -> time)
   std::vector<std::shared_ptr<dg::MergedDict>> dicts;  // empty for a dg_merge result (cluster ids)
   std::vector<int32_t> cards;                         // dg_merge result: cluster dictionary sizes
+  bool limited = false;                               // dg_result_limit: groups in the push-down order
   ~dg_result() {
     if (!ctx) return;
     std::lock_guard<std::mutex> g(ctx->mu);
@@ -3241,6 +3242,99 @@ int dg_result_dim_dictionary(const dg_result* r, int32_t dim, int64_t* offsets, 
   return DG_OK;
 }
 
+int dg_result_limit(dg_result* r, const dg_limit* spec) {
+  if (!r || !spec || spec->limit <= 0 || spec->n_columns < 0 || (spec->n_columns > 0 && !spec->columns))
+    return set_error(DG_ERR_ARG, "bad limit spec");
+  Context* ctx = r->ctx;
+  const KeyLayout& lay = r->lay;
+  // the push-down field order: time, ORDER BY dimensions (first mention), the other dimensions
+  // ascending; time last with sortByDimsFirst
+  LimitOrder o;
+  memset(&o, 0, sizeof o);
+  std::vector<int> field_dim;  // -1 = bucket
+  const bool time_last = spec->sort_by_dims_first != 0;
+  if (lay.bucket_bits && !time_last) field_dim.push_back(-1);
+  std::vector<int> desc(r->ndims, 0);
+  std::vector<const int32_t*> rank(r->ndims, nullptr);
+  std::vector<bool> used(r->ndims, false);
+  for (int c = 0; c < spec->n_columns; ++c) {
+    const dg_order_column& oc = spec->columns[c];
+    if (oc.dim < 0 || oc.dim >= r->ndims) return set_error(DG_ERR_ARG, "ORDER BY dimension %d of %d", oc.dim, r->ndims);
+    if (used[oc.dim]) continue;  // a later mention never decides (the first already compared equal)
+    used[oc.dim] = true;
+    desc[oc.dim] = oc.descending != 0;
+    rank[oc.dim] = oc.rank;
+    field_dim.push_back(oc.dim);
+  }
+  for (int d = 0; d < r->ndims; ++d)
+    if (!used[d]) field_dim.push_back(d);
+  if (lay.bucket_bits && time_last) field_dim.push_back(-1);
+  int key_bits = 0;
+  for (int f : field_dim) key_bits += f < 0 ? lay.bucket_bits : lay.dim_bits[f];
+  CallGuard g(ctx);
+  CallScratch* cs = g.cs;
+  hipStream_t st = ctx->stream;
+  int out = key_bits;
+  for (size_t f = 0; f < field_dim.size(); ++f) {
+    const int d = field_dim[f];
+    o.bits[o.nfields] = d < 0 ? lay.bucket_bits : lay.dim_bits[d];
+    o.in_shift[o.nfields] = d < 0 ? lay.bucket_shift : lay.dim_shift[d];
+    out -= o.bits[o.nfields];
+    o.out_shift[o.nfields] = out;
+    if (d >= 0) {
+      o.desc[o.nfields] = desc[d];
+      if (rank[d]) {  // caller's comparator ranks over the result's dictionary ids, checked and uploaded
+        const int32_t card = dg_result_dim_cardinality(r, d);
+        const int64_t top = o.bits[o.nfields] >= 31 ? INT32_MAX : (1ll << o.bits[o.nfields]);
+        for (int32_t i = 0; i < card; ++i)
+          if (rank[d][i] < 0 || rank[d][i] >= card || rank[d][i] >= top)
+            return set_error(DG_ERR_ARG, "rank %d of id %d of dimension %d outside [0, %d)", rank[d][i], i, d, card);
+        int32_t* dr;
+        int32_t* h = up_take<int32_t>(cs, (size_t)std::max(card, 1), &dr, st);
+        if (!h) return set_error(DG_ERR_OOM, "rank table");
+        memcpy(h, rank[d], sizeof(int32_t) * (size_t)card);
+        o.rank[o.nfields] = dr;
+      }
+    }
+    if (o.bits[o.nfields] > 0) o.nfields++;
+  }
+  const int64_t n = r->ngroups;
+  const int64_t m = std::min<int64_t>(spec->limit, n);
+  if (n == 0) {
+    r->limited = true;
+    return DG_OK;
+  }
+  SortBufs sb;
+  int rc = sort_bufs(cs, n, 1, key_bits, 0, &sb);
+  if (rc) return rc;
+  const int rec = r->naggs + 1;
+  DG_FLUSH(cs, st);
+  uint64_t* nk = static_cast<uint64_t*>(result_alloc(ctx, (size_t)m * 8));
+  uint64_t* ns = static_cast<uint64_t*>(result_alloc(ctx, (size_t)m * rec * 8));
+  if (!nk || !ns) {
+    result_free(ctx, nk);
+    result_free(ctx, ns);
+    return set_error(DG_ERR_OOM, "limited result of %lld groups", (long long)m);
+  }
+  launch_limit_load(r->keys, n, o, &sb, st);
+  launch_radix_sort(&sb, key_bits, st);
+  launch_limit_gather(&sb, m, r->keys, r->slots, r->cap, rec, nk, ns, m, st);
+  rc = finish_call(cs, st);
+  if (rc) {
+    result_free(ctx, nk);
+    result_free(ctx, ns);
+    return rc;
+  }
+  result_free(ctx, r->keys);
+  result_free(ctx, r->slots);
+  r->keys = nk;
+  r->slots = ns;
+  r->cap = m;
+  r->ngroups = m;
+  r->limited = true;
+  return DG_OK;
+}
+
 int32_t dg_result_dim_cardinality(const dg_result* r, int32_t dim) {
   if (!r || dim < 0 || dim >= r->ndims) return -1;
   if (r->dicts.empty()) return r->cards[dim];
@@ -3320,6 +3414,7 @@ int dg_keyspace_bits(const dg_keyspace* ks, int32_t* bits) {
 
 int dg_result_export(dg_result* r, const dg_keyspace* ks, const int32_t* const* maps, uint64_t* d_keys, uint64_t* d_slots) {
   if (!r) return set_error(DG_ERR_ARG, "null result");
+  if (r->limited) return set_error(DG_ERR_ARG, "a limited result is not in key order");
   KeyLayout lay;
   AggPlan plan;
   int rc = keyspace_layout(ks, &lay, &plan);

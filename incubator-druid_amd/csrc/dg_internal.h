@@ -490,6 +490,20 @@ void launch_gb_rekey(const uint64_t* in, int64_t n, KeyLayout lin, KeyLayout lou
 void launch_lower_bound(const uint64_t* keys, int64_t n, const uint64_t* split, int nsplit, int64_t* pos, hipStream_t s);
 // sort input of a merge (refs = record index, sb->n[0] = n)
 void launch_merge_load(const uint64_t* keys, int64_t n, SortBufs* sb, hipStream_t s);
+// limit push-down: key fields (bucket, dimensions) re-packed most significant first in the push-down
+// order; a field's value goes through its rank table (if any) and is complemented when descending
+struct LimitOrder {
+  int32_t nfields;
+  int32_t in_shift[kMaxGroupDims + 1];
+  int32_t bits[kMaxGroupDims + 1];
+  int32_t out_shift[kMaxGroupDims + 1];
+  int32_t desc[kMaxGroupDims + 1];
+  const int32_t* rank[kMaxGroupDims + 1];
+};
+void launch_limit_load(const uint64_t* keys, int64_t n, const LimitOrder& o, SortBufs* sb, hipStream_t s);
+// the first m elements of the sorted order: keys[ref] and the [rec][cap] slot-major records -> [rec][ocap]
+void launch_limit_gather(const SortBufs* sb, int64_t m, const uint64_t* keys, const uint64_t* slots, int64_t cap,
+                         int rec, uint64_t* okeys, uint64_t* oslots, int64_t ocap, hipStream_t s);
 // one record per run of the sorted merge input, partial values combined in order (device encoding,
 // SoA slots [rec][cap])
 void launch_merge_reduce(SortBufs* sb, const uint32_t* head_pos, const uint64_t* in_slots, AggPlan plan, int64_t cap,

@@ -1217,6 +1217,60 @@ void launch_merge_load(const uint64_t* keys, int64_t n, SortBufs* sb, hipStream_
                      sb->ref_bits, sb->n);
 }
 
+// ------------------------------------------------------------------------------------------------
+// limit push-down (GroupByQuery.getRowOrderingForPushDown, GroupByQuery.java:423-528): a result's
+// keys re-packed with their fields in the push-down order (comparator ranks, descending columns
+// complemented), sorted, and the first `limit` groups gathered in that order
+// ------------------------------------------------------------------------------------------------
+__global__ void k_limit_load(const uint64_t* __restrict__ keys, int64_t n, LimitOrder o, uint64_t* __restrict__ kout,
+                             uint32_t* __restrict__ rout, int kshift, uint32_t* __restrict__ n_out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) n_out[0] = (uint32_t)n;
+  for (int64_t i = t; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    uint64_t ord = 0;
+    for (int f = 0; f < o.nfields; ++f) {
+      const uint64_t m = (1ull << o.bits[f]) - 1ull;
+      uint64_t v = (k >> o.in_shift[f]) & m;
+      if (o.rank[f]) v = (uint64_t)(uint32_t)o.rank[f][v];
+      if (o.desc[f]) v = m - v;
+      ord |= v << o.out_shift[f];
+    }
+    if (rout) {
+      kout[i] = ord;
+      rout[i] = (uint32_t)i;
+    } else {
+      kout[i] = (ord << kshift) | (uint64_t)i;
+    }
+  }
+}
+
+void launch_limit_load(const uint64_t* keys, int64_t n, const LimitOrder& o, SortBufs* sb, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(16384, std::max<int64_t>(1, (n + 255) / 256));
+  hipLaunchKernelGGL(k_limit_load, dim3((unsigned)blocks), dim3(256), 0, s, keys, n, o, sb->keys[sb->cur],
+                     sb->refs[sb->cur], sb->ref_bits, sb->n);
+}
+
+__global__ void k_limit_gather(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ srefs, int kshift,
+                               int64_t m, const uint64_t* __restrict__ keys, const uint64_t* __restrict__ slots,
+                               int64_t cap, int rec, uint64_t* __restrict__ okeys, uint64_t* __restrict__ oslots,
+                               int64_t ocap) {
+  const uint64_t rmask = kshift ? (1ull << kshift) - 1ull : 0ull;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t src = srefs ? (int64_t)srefs[i] : (int64_t)(skeys[i] & rmask);
+    okeys[i] = keys[src];
+    for (int s = 0; s < rec; ++s) oslots[(size_t)s * ocap + i] = slots[(size_t)s * cap + src];
+  }
+}
+
+void launch_limit_gather(const SortBufs* sb, int64_t m, const uint64_t* keys, const uint64_t* slots, int64_t cap,
+                         int rec, uint64_t* okeys, uint64_t* oslots, int64_t ocap, hipStream_t s) {
+  if (m <= 0) return;
+  const int64_t blocks = std::min<int64_t>(16384, (m + 255) / 256);
+  hipLaunchKernelGGL(k_limit_gather, dim3((unsigned)blocks), dim3(256), 0, s, sb->keys[sb->cur], sb->refs[sb->cur],
+                     sb->ref_bits, m, keys, slots, cap, rec, okeys, oslots, ocap);
+}
+
 // AggregatorFactory.getCombiningFactory semantics on ABI-encoded partial values: the combining
 // aggregator starts from its identity and folds the partials in order (sums: LongSumAggregator /
 // DoubleSumAggregator / FloatSumAggregator.combine with float adds; min / max: Math.min / Math.max,

@@ -447,6 +447,10 @@ class GroupByExchange:
         res = self.engine.merge(self.ks, rkeys, rslots, self.query, self.dicts)
         if self.starts is not None:
             res.time_map = self.starts  # dg_merge times are bucket indices into the query's bucket list
+        # limit push-down: this rank's key range holds whole groups, and the ordering is on grouping
+        # fields only, so the cluster's first `limit` groups are among the ranks' first `limit`
+        if hasattr(res, "apply_limit_push_down"):  # (the CPU tests' host engine returns its rows whole)
+            res.apply_limit_push_down()
         return res
 
 

@@ -891,6 +891,44 @@ class GroupByQuery(BaseQuery):
                 dims.append(d)
         self.dimensions = dims
 
+    def _ctx_bool(self, key: str, default: bool) -> bool:
+        v = (self.context or {}).get(key, default)
+        if isinstance(v, str):  # QueryContexts.parseBoolean: Boolean.parseBoolean of a string
+            return v.strip().lower() == "true"
+        return bool(v)
+
+    def order_by_dims(self) -> Optional[List[int]]:
+        """Dimension index of every ORDER BY column (OrderByColumnSpec.getDimIndexForOrderBy), or None
+        when one sorts on a non-grouping field (DefaultLimitSpec.sortingOrderHasNonGroupingFields)."""
+        idx = []
+        for c in (self.limitSpec.columns if self.limitSpec else []):
+            if c.dimension not in self.dimensions:
+                return None
+            idx.append(self.dimensions.index(c.dimension))
+        return idx
+
+    def apply_limit_push_down(self) -> bool:
+        """GroupByQuery.determineApplyLimitPushDown / validateAndGetForceLimitPushDown
+        (query/groupby/GroupByQuery.java:352-416): a limited DefaultLimitSpec ordered by grouping
+        dimensions only, no having spec, applyLimitPushDown not switched off in the context. A forced
+        push-down (forceLimitPushDown) that sorts on aggregators is not pushed here: the reference
+        then truncates every segment's grouper by partial aggregates (approximate); this engine
+        returns the exact ordering instead."""
+        ls = self.limitSpec
+        force = self._ctx_bool("forceLimitPushDown", False)
+        if force:
+            if ls is None:
+                raise ValueError("When forcing limit push down, a limit spec must be provided.")
+            if ls.limit is None:
+                raise ValueError("When forcing limit push down, the provided limit spec must have a limit.")
+            if self.having is not None:
+                raise ValueError("Cannot force limit push down when a having spec is present.")
+        if ls is None or ls.limit is None:
+            return False
+        if not force and (not self._ctx_bool("applyLimitPushDown", True) or self.having is not None):
+            return False
+        return self.order_by_dims() is not None
+
     def to_json(self):
         js = self._base_json("groupBy")
         js["dimensions"] = list(self.dimensions)

@@ -625,6 +625,36 @@ class GroupByResult:
         aggs = _decode_slots(q.aggregations, vals[:count * na].reshape(count, na)) if na else []
         return GroupByPartial(t[:count], None, aggs, codes, [self.dictionary(d) for d in range(nd)], merged=True)
 
+    def apply_limit_push_down(self) -> bool:
+        """LimitedBufferHashGrouper's outcome on the device (dg_result_limit): when the query pushes
+        its limit down (GroupByQuery.isApplyLimitPushDown), keep the first `limit` groups in the
+        push-down row order (GroupByQuery.getRowOrderingForPushDown :423-528). Every dimension is
+        passed as a column: the ORDER BY ones with their comparator and direction, then the others
+        ascending under LEXICOGRAPHIC (UTF-8 byte order, which differs from the dictionary's Java
+        String order only for values beyond U+D7FF, so the id order is used when none has one)."""
+        q = self.query
+        if self.groups == 0 or not q.apply_limit_push_down():
+            return False
+        order = q.order_by_dims()
+        cols, keep, seen = [], [], set()
+        spec = [(d, c.direction == "descending", c.dimensionOrder) for d, c in zip(order, q.limitSpec.columns)]
+        spec += [(d, False, "lexicographic") for d in range(len(q.dimensions)) if d not in order]
+        for d, desc, ordering in spec:
+            if d in seen:
+                continue
+            seen.add(d)
+            rank = None
+            if ordering != "lexicographic" or _beyond_bmp_low(self.dictionary(d)):
+                rank = np.ascontiguousarray(O.DictionaryOrder(self.dictionary(d), ordering).rank, dtype=np.int32)
+                keep.append(rank)
+            cols.append(N.dg_order_column(d, int(desc), rank.ctypes.data if rank is not None else None))
+        arr = (N.dg_order_column * len(cols))(*cols)
+        lim = N.dg_limit(ctypes.cast(arr, ctypes.c_void_p), len(cols), int(q.limitSpec.limit),
+                         int(q._ctx_bool("sortByDimsFirst", False)))
+        N.check(N.lib().dg_result_limit(self.handle, ctypes.byref(lim)))
+        self.groups = int(N.lib().dg_result_groups(self.handle))
+        return True
+
     def release(self):
         if self.handle:
             N.lib().dg_result_release(self.handle)
@@ -637,10 +667,17 @@ class GroupByResult:
             pass
 
 
+def _beyond_bmp_low(values) -> bool:
+    """Whether any value holds a character whose UTF-8 order differs from its UTF-16 order."""
+    return any(v is not None and any(ord(ch) > 0xD7FF for ch in v) for v in values)
+
+
 def groupby_run(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
-                stats: Optional[RunStats] = None) -> GroupByResult:
+                stats: Optional[RunStats] = None, limit_push_down: bool = False) -> GroupByResult:
     """One dg_groupby_run over segments of ONE device: GroupByStrategyV2.mergeRunners over their
-    per-segment runners (GroupByMergingQueryRunnerV2.java:170-290), the groups left in HBM."""
+    per-segment runners (GroupByMergingQueryRunnerV2.java:170-290), the groups left in HBM. With
+    `limit_push_down`, a query that pushes its limit down keeps only its first `limit` groups
+    (GroupByResult.apply_limit_push_down); a result meant for the cross-device exchange stays whole."""
     if len(_group_by_device(segments)) != 1:
         raise ValueError("groupby_run: segments must share one device")
     nd = len(query.dimensions)
@@ -655,7 +692,10 @@ def groupby_run(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
                                    ctypes.byref(res), ctypes.byref(m)))
     if stats is not None:
         stats.add(m)
-    return GroupByResult(res, query)
+    out = GroupByResult(res, query)
+    if limit_push_down:
+        out.apply_limit_push_down()
+    return out
 
 
 def groupby_per_device(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
@@ -663,7 +703,7 @@ def groupby_per_device(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
     """The merged, ordered groups of every device's segments (one engine call per device)."""
     out = []
     for _, idx in _group_by_device(segments).items():
-        r = groupby_run([segments[i] for i in idx], query, stats)
+        r = groupby_run([segments[i] for i in idx], query, stats, limit_push_down=True)
         try:
             out.append(r.fetch())
         finally:
@@ -792,7 +832,34 @@ def merge_groupby(query: Q.GroupByQuery, partials: Sequence[GroupByPartial]) -> 
         for a, col in zip(query.aggregations, aggs):
             ev[a.name] = _py(col[r], a.output_type)
         rows.append(Q.Row(int(t[r]), ev))
+    if query.apply_limit_push_down():
+        # the partials hold (at least) the first `limit` groups of every device in the push-down
+        # order; across devices the cut is taken again in that order
+        rows = sorted(rows, key=_push_down_key(query))[:query.limitSpec.limit]
+    elif query._ctx_bool("sortByDimsFirst", False) and not query.granularity.is_all:
+        # getRowOrdering(false) with sortByDimsFirst: dimensions, then time (GroupByQuery.java:543-553)
+        rows.sort(key=lambda r: tuple(_java_key(r.event[d]) for d in query.dimensions))
     return postprocess_groupby(query, rows)
+
+
+def _push_down_key(query: Q.GroupByQuery):
+    """Sort key of GroupByQuery.getRowOrderingForPushDown (:423-528): ORDER BY dimensions under their
+    comparator and direction, the other dimensions ascending under LEXICOGRAPHIC, the time first (last
+    with sortByDimsFirst; absent for ALL)."""
+    fields, seen = [], set()
+    for c in query.limitSpec.columns:
+        fields.append((c.dimension, O.sort_key(c.dimensionOrder), c.direction == "descending"))
+        seen.add(c.dimension)
+    fields += [(d, O.sort_key("lexicographic"), False) for d in query.dimensions if d not in seen]
+    gran_all = query.granularity.is_all
+    dims_first = query._ctx_bool("sortByDimsFirst", False)
+
+    def key(r):
+        ks = tuple(O._Desc(f(r.event.get(n))) if desc else f(r.event.get(n)) for n, f, desc in fields)
+        if gran_all:
+            return ks
+        return ks + (r.timestamp,) if dims_first else (r.timestamp,) + ks
+    return key
 
 
 # ----------------------------------------------------------------------------------------------
@@ -847,13 +914,31 @@ def _having_eval(h: Q.HavingSpec, row: Q.Row) -> bool:
     return c > 0 if t == "greaterThan" else (c < 0 if t == "lessThan" else c == 0)
 
 
+def _limit_needs_sort(query: Q.GroupByQuery) -> bool:
+    """DefaultLimitSpec.build (orderby/DefaultLimitSpec.java:122-188): whether the natural order is
+    not good enough (then a sort by makeComparator, else just the limit)."""
+    ls = query.limitSpec
+    if len(query.dimensions) < len(ls.columns):
+        return True
+    aggs = {a.name for a in query.aggregations}
+    for i, c in enumerate(ls.columns):
+        if c.dimension in aggs:
+            return True
+        if c.dimension not in query.dimensions:
+            raise ValueError(f"Unknown column in order clause[{c.dimension}]")
+        # string dimensions: the natural comparator is LEXICOGRAPHIC
+        if c.direction != "ascending" or c.dimensionOrder != "lexicographic" or c.dimension != query.dimensions[i]:
+            return True
+    return not query.granularity.is_all and query._ctx_bool("sortByDimsFirst", False)
+
+
 def postprocess_groupby(query: Q.GroupByQuery, rows: List[Q.Row]) -> List[Q.Row]:
     if query.having is not None:
         rows = [r for r in rows if _having_eval(query.having, r)]
     ls = query.limitSpec
     if ls is None:
         return rows
-    if ls.columns:
+    if _limit_needs_sort(query):
         aggs = {a.name: a for a in query.aggregations}
         dims = set(query.dimensions)
         parts = []
@@ -867,7 +952,7 @@ def postprocess_groupby(query: Q.GroupByQuery, rows: List[Q.Row]) -> List[Q.Row]
             else:
                 raise ValueError(f"Unknown column in order clause[{c.dimension}]")
             parts.append((kf, c.direction == "descending"))
-        by_dims_first = bool(query.context.get("sortByDimsFirst", False))
+        by_dims_first = query._ctx_bool("sortByDimsFirst", False)
         gran_all = query.granularity.is_all
 
         def key(r):

@@ -1701,7 +1701,73 @@ def merge_groupby(query, per_segment: List[List]) -> List:
         ev.update(aggs)
         out.append(Q.Row(_universal_timestamp(query) if gran.is_all else k, ev))
     out.sort(key=lambda r: (r.timestamp, tuple(_jkey(r.event[d]) for d in query.dimensions)))
+    if o_limit_push_down(query):  # LimitedBufferHashGrouper: the first `limit` in the push-down order
+        out = sorted(out, key=functools.cmp_to_key(_push_down_ordering(query)))[:query.limitSpec.limit]
+    elif _o_ctx_bool(query, "sortByDimsFirst", False) and not o_is_all(gran):
+        # getRowOrdering(false) with sortByDimsFirst: compareDims, then the time (GroupByQuery.java:543-553)
+        out.sort(key=lambda r: tuple(_jkey(r.event[d]) for d in query.dimensions))
     return groupby_post_process(query, out)
+
+
+def _o_ctx_bool(query, key: str, default: bool) -> bool:
+    """QueryContexts.getAsBoolean: a Boolean, or Boolean.parseBoolean of a string."""
+    v = (getattr(query, "context", None) or {}).get(key, default)
+    return v.strip().lower() == "true" if isinstance(v, str) else bool(v)
+
+
+def o_limit_push_down(query) -> bool:
+    """GroupByQuery.determineApplyLimitPushDown (GroupByQuery.java:377-416) and the checks of
+    validateAndGetForceLimitPushDown (:352-375)."""
+    ls = getattr(query, "limitSpec", None)
+    having = getattr(query, "having", None)
+    force = _o_ctx_bool(query, "forceLimitPushDown", False)
+    if force and (ls is None or ls.limit is None or having is not None):
+        raise ValueError("invalid forceLimitPushDown")
+    if ls is None or ls.limit is None:
+        return False
+    if force:
+        # (forced with an aggregator ordering the reference truncates per segment by partial values;
+        # the engine does not push such an ordering down, and neither does this restatement)
+        return all(c.dimension in query.dimensions for c in ls.columns)
+    if not _o_ctx_bool(query, "applyLimitPushDown", True) or having is not None:
+        return False
+    return all(c.dimension in query.dimensions for c in ls.columns)  # !sortingOrderHasNonGroupingFields
+
+
+def _push_down_ordering(query):
+    """getRowOrderingForPushDown (GroupByQuery.java:423-528) + compareDimsForLimitPushDown (:600-633):
+    the ORDER BY dimensions with their comparator and direction, then the other dimensions ascending
+    under LEXICOGRAPHIC; the time before them (after with sortByDimsFirst), none for ALL."""
+    fields = []
+    in_order = set()
+    for c in query.limitSpec.columns:
+        fields.append((c.dimension, _STRING_COMPARATORS[c.dimensionOrder], c.direction == "descending"))
+        in_order.add(c.dimension)
+    for d in query.dimensions:
+        if d not in in_order:
+            fields.append((d, _STRING_COMPARATORS["lexicographic"], False))
+
+    def dims_cmp(x, y):
+        for name, cmp, rev in fields:
+            c = cmp(x.event.get(name), y.event.get(name))
+            if c:
+                return -c if rev else c
+        return 0
+
+    def time_cmp(x, y):
+        return (x.timestamp > y.timestamp) - (x.timestamp < y.timestamp)
+
+    if o_is_all(query.granularity):
+        return dims_cmp
+    chain = [dims_cmp, time_cmp] if _o_ctx_bool(query, "sortByDimsFirst", False) else [time_cmp, dims_cmp]
+
+    def ordering(x, y):
+        for f in chain:
+            c = f(x, y)
+            if c:
+                return c
+        return 0
+    return ordering
 
 
 # ---- GroupByQuery.postProcess: having (having/*HavingSpec.java) then DefaultLimitSpec
@@ -1794,9 +1860,23 @@ def groupby_post_process(query, rows: List) -> List:
     ls = getattr(query, "limitSpec", None)
     if ls is None:
         return rows
-    if not ls.columns:
-        return rows if ls.limit is None else rows[:ls.limit]  # LimitingFn
     aggs = {a.name: a for a in query.aggregations}
+    # DefaultLimitSpec.build (:122-188): re-sort only when the natural order is not good enough
+    need = len(query.dimensions) < len(ls.columns)
+    if not need:
+        for i, c in enumerate(ls.columns):
+            if c.dimension in aggs:
+                need = True
+                break
+            if c.dimension not in query.dimensions:
+                raise ValueError(f"Unknown column in order clause[{c.dimension}]")
+            if c.direction != "ascending" or c.dimensionOrder != "lexicographic" or c.dimension != query.dimensions[i]:
+                need = True  # (string dimensions: the natural comparator is LEXICOGRAPHIC)
+                break
+    if not need:
+        need = not o_is_all(query.granularity) and _o_ctx_bool(query, "sortByDimsFirst", False)
+    if not need:
+        return rows if ls.limit is None else rows[:ls.limit]  # LimitingFn
     comparators = []
     for c in ls.columns:  # makeComparator: post-aggs, then aggregators, then dimensions
         if c.dimension in aggs:
@@ -1813,7 +1893,7 @@ def groupby_post_process(query, rows: List) -> List:
     def time_cmp(x, y):
         return (x.timestamp > y.timestamp) - (x.timestamp < y.timestamp)
 
-    by_dims_first = bool(query.context.get("sortByDimsFirst", False))
+    by_dims_first = _o_ctx_bool(query, "sortByDimsFirst", False)
     chain = comparators + [time_cmp] if by_dims_first else [time_cmp] + comparators
 
     def ordering(x, y):

@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_structs():
     N = importlib.import_module("incubator-druid_amd._native")
-    assert N.lib().dg_abi_version() == 5
+    assert N.lib().dg_abi_version() == 6
     # struct layouts the header fixes (LP64)
     assert ctypes.sizeof(N.dg_filter) == 64
     assert ctypes.sizeof(N.dg_agg) == 32
@@ -35,6 +35,8 @@ def test_abi_version_and_structs():
     assert ctypes.sizeof(N.dg_metrics) == 104
     assert ctypes.sizeof(N.dg_topn_lists) == 40
     assert ctypes.sizeof(N.dg_topn) == 56
+    assert ctypes.sizeof(N.dg_order_column) == 16
+    assert ctypes.sizeof(N.dg_limit) == 24
 
 
 def test_gpu_kernels_are_gfx950_code_objects():
@@ -42,7 +44,7 @@ def test_gpu_kernels_are_gfx950_code_objects():
     data = open(N.LIB_PATH, "rb").read()
     assert b"gfx950" in data
     for k in (b"k_lz4_decode", b"k_concise_or", b"k_roaring_or", b"k_scan_agg", b"k_topn_radix", b"k_topn_compact", b"k_gb_keygen",
-              b"k_rs_scatter", b"k_gb_reduce", b"k_fsum_runs"):
+              b"k_rs_scatter", b"k_gb_reduce", b"k_fsum_runs", b"k_limit_load", b"k_limit_gather"):
         assert k in data, k
 
 
