@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 6
+#define DG_ABI_VERSION 7
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -207,6 +207,24 @@ int dg_context_set_stream(dg_context* ctx, void* hip_stream);
 /* ---- segments ---- */
 int dg_segment_attach(dg_context* ctx, const char* segment_dir, dg_segment** out);
 void dg_segment_release(dg_segment* seg);
+/* In-memory (realtime) segment: the rows of an IncrementalIndex queried like a persisted segment
+ * (IncrementalIndexStorageAdapter, processing/.../segment/incremental/IncrementalIndexStorageAdapter.java:
+ * the index's facts in its iteration order, TimeAndDims order: time ascending). Rows are copied into
+ * HBM as flat columns (__time from `timestamps`); a string dimension comes as the index's
+ * DimensionDictionary (values by id in insertion order, NULL or "" = null) plus one id per row and is
+ * re-sorted into the sorted-dictionary form (SortedDimensionDictionary) the engines use. Such a
+ * segment has no bitmap index: string filters run as row predicates on the ids (the adapter's
+ * ValueMatchers). Multi-value rows are not taken. Released with dg_segment_release. */
+typedef struct {
+  const char* name;
+  int32_t type;            /* DG_COL_LONG / DG_COL_FLOAT / DG_COL_DOUBLE / DG_COL_STRING */
+  int32_t card;            /* STRING: dictionary size */
+  const char* const* dict; /* STRING: value of every id */
+  const int32_t* ids;      /* STRING: [n_rows] ids into dict */
+  const void* values;      /* numeric: [n_rows] int64 / float / double */
+} dg_row_column;
+int dg_segment_from_rows(dg_context* ctx, int64_t n_rows, const int64_t* timestamps, int64_t interval_start,
+                         int64_t interval_end, const dg_row_column* columns, int32_t n_columns, dg_segment** out);
 int64_t dg_segment_num_rows(const dg_segment* seg);
 int dg_segment_interval(const dg_segment* seg, int64_t* start, int64_t* end);
 int dg_segment_time_bounds(const dg_segment* seg, int64_t* min_time, int64_t* max_time);

@@ -95,6 +95,11 @@ class dg_record_layout(ctypes.Structure):
                 ("record_size", ctypes.c_int32), ("big_endian", ctypes.c_int32)]
 
 
+class dg_row_column(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("type", ctypes.c_int32), ("card", ctypes.c_int32),
+                ("dict", ctypes.c_void_p), ("ids", ctypes.c_void_p), ("values", ctypes.c_void_p)]
+
+
 class dg_order_column(ctypes.Structure):
     _fields_ = [("dim", ctypes.c_int32), ("descending", ctypes.c_int32), ("rank", ctypes.c_void_p)]
 
@@ -120,6 +125,7 @@ EXPORTS = [
     "dg_result_groups", "dg_result_fetch_groups", "dg_result_fetch_rows", "dg_result_dim_cardinality",
     "dg_result_dim_dictionary", "dg_result_release", "dg_keyspace_bits", "dg_result_export", "dg_keys_partition",
     "dg_merge", "dg_records_pack", "dg_debug_lz4_decode", "dg_result_limit",
+    "dg_segment_from_rows",
 ]
 
 _lib = None
@@ -152,6 +158,7 @@ def lib():
         "dg_context_set_stream": (ctypes.c_int, [vp, vp]),
         "dg_segment_attach": (ctypes.c_int, [vp, cp, P(vp)]),
         "dg_segment_release": (None, [vp]),
+        "dg_segment_from_rows": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, i32, P(vp)]),
         "dg_segment_num_rows": (i64, [vp]),
         "dg_segment_interval": (ctypes.c_int, [vp, P(i64), P(i64)]),
         "dg_segment_time_bounds": (ctypes.c_int, [vp, P(i64), P(i64)]),

@@ -270,6 +270,8 @@ static int java_compare(const std::string& a, const std::string& b) {
   return ua.size() == ub.size() ? 0 : (ua.size() < ub.size() ? -1 : 1);
 }
 
+int java_compare_str(const char* a, const char* b) { return java_compare(std::string(a), std::string(b)); }
+
 // null-aware compare: null < anything
 static int cmp_nullable(bool an, const std::string& a, bool bn, const std::string& b) {
   if (an || bn) return an == bn ? 0 : (an ? -1 : 1);
@@ -748,7 +750,7 @@ static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos
         fp->preds.push_back(std::move(L));
         return DG_OK;
       }
-      if (c->type != DG_COL_STRING || !c->has_bitmaps)
+      if (c->type != DG_COL_STRING || (!c->has_bitmaps && c->multi_value))
         return set_error(DG_ERR_UNSUPPORTED, "filter on %s needs a bitmap index", f.dimension);
       std::vector<int32_t> ids;
       if (f.kind == DG_F_SELECTOR) {
@@ -786,6 +788,22 @@ static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos
       }
       if (ids.empty()) {
         fp->prog.push_back(-2);
+        return DG_OK;
+      }
+      if (!c->has_bitmaps) {
+        // no bitmap index (an in-memory segment): the matching ids become a row predicate, as
+        // IncrementalIndexStorageAdapter's cursors evaluate filter.makeMatcher per row
+        PredLeaf L;
+        memset(&L.p, 0, sizeof L.p);
+        L.p.kind = PRED_ID_SET;
+        L.col = c;
+        L.set.assign((c->dict.size() + 63) / 64, 0);
+        for (int32_t i : ids) L.set[i >> 6] |= (int64_t)(1ull << (i & 63));
+        fp->prog.push_back((int32_t)fp->leaf_ids.size());
+        fp->leaf_ids.emplace_back();
+        fp->leaf_col.push_back(nullptr);
+        fp->leaf_pred.push_back((int32_t)fp->preds.size());
+        fp->preds.push_back(std::move(L));
         return DG_OK;
       }
       fp->prog.push_back((int32_t)fp->leaf_ids.size());
@@ -1661,6 +1679,19 @@ int dg_segment_attach(dg_context* c, const char* dir, dg_segment** out) {
   hipSetDevice(ctx->device);
   Segment* seg = nullptr;
   int rc = load_segment(ctx, dir, &seg);
+  if (rc) return rc;
+  *out = reinterpret_cast<dg_segment*>(seg);
+  return DG_OK;
+}
+
+int dg_segment_from_rows(dg_context* c, int64_t n_rows, const int64_t* timestamps, int64_t interval_start,
+                         int64_t interval_end, const dg_row_column* columns, int32_t n_columns, dg_segment** out) {
+  Context* ctx = reinterpret_cast<Context*>(c);
+  if (!ctx || !out) return set_error(DG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  hipSetDevice(ctx->device);
+  Segment* seg = nullptr;
+  int rc = segment_from_rows(ctx, n_rows, timestamps, interval_start, interval_end, columns, n_columns, &seg);
   if (rc) return rc;
   *out = reinterpret_cast<dg_segment*>(seg);
   return DG_OK;

@@ -334,6 +334,9 @@ int set_error(int code, const char* fmt, ...);
 
 // segment loading (dg_segment.cpp)
 int load_segment(Context* ctx, const char* dir, Segment** out);
+int segment_from_rows(Context* ctx, int64_t nrows, const int64_t* ts, int64_t istart, int64_t iend,
+                      const dg_row_column* cols, int ncols, Segment** out);
+int java_compare_str(const char* a, const char* b);  // String.compareTo over UTF-8 bytes (dg_engine.cpp)
 
 // kernel launchers (dg_kernels.hip)
 constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (diagnostic builds of the call)
@@ -366,6 +369,7 @@ enum PredKind : int32_t {
   PRED_ORD_RANGE = 3,   // float/double column: Double.compare range on (double) value, as ordered keys
   PRED_BITS_SET = 4,    // float/double column: floatToIntBits / doubleToLongBits in the sorted set
   PRED_LONG_LEX = 5,    // long column: String.valueOf(value) vs UTF-8 bound strings (LEXICOGRAPHIC)
+  PRED_ID_SET = 6,      // string column without a bitmap index: row id's bit in `set` (64-bit words)
 };
 struct NumPred {
   int32_t kind;

@@ -345,7 +345,10 @@ __global__ __launch_bounds__(256) void k_num_pred(ColView v, int64_t nrows, NumP
   bool m = false;
   if (r < nrows && p.kind != PRED_FALSE) {
     const uint8_t* ptr = cv_ptr(v, r);
-    if (v.kind == VIEW_LONG) {
+    if (v.kind == VIEW_IDS) {
+      const uint32_t id = load_id(v, r);
+      m = p.kind == PRED_ID_SET && ((uint64_t)p.set[id >> 6] >> (id & 63)) & 1ull;
+    } else if (v.kind == VIEW_LONG) {
       const int64_t x = *reinterpret_cast<const int64_t*>(ptr);
       if (p.kind == PRED_LONG_RANGE) m = range_ok((x > p.lo) - (x < p.lo), (p.hi > x) - (p.hi < x), p);
       else if (p.kind == PRED_LONG_SET) m = in_sorted(p.set, p.nset, x);

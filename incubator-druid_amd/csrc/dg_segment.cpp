@@ -846,4 +846,103 @@ int load_segment(Context* ctx, const char* dir, Segment** out) {
   return DG_OK;
 }
 
+// In-memory segment from an IncrementalIndex's rows (IncrementalIndexStorageAdapter): every column a
+// flat array in HBM (codec NONE); string dictionaries re-sorted into Java String order (nulls first)
+// with the row ids remapped, so the engines see the sorted-dictionary contract of a persisted segment
+// (IncrementalIndexStorageAdapter also answers through the sorted lookup, StringDimensionIndexer's
+// SortedDimensionDictionary). No bitmap index: string filters run as row predicates on the ids, as
+// the adapter's ValueMatchers do (IncrementalIndexStorageAdapter.makeCursors -> filter.makeMatcher).
+int segment_from_rows(Context* ctx, int64_t nrows, const int64_t* ts, int64_t istart, int64_t iend,
+                      const dg_row_column* cols, int ncols, Segment** out) {
+  if (nrows < 0 || nrows > INT32_MAX - 1 || (nrows > 0 && !ts) || ncols < 0 || (ncols > 0 && !cols) || iend < istart)
+    return set_error(DG_ERR_ARG, "bad row arguments");
+  static std::atomic<uint64_t> serial{1ull << 62};
+  std::unique_ptr<Segment> seg(new Segment());
+  seg->ctx = ctx;
+  seg->uid = ++serial;
+  seg->dir = "<rows>";
+  seg->nrows = nrows;
+  seg->istart = istart;
+  seg->iend = iend;
+  for (int64_t r = 1; r < nrows; ++r)
+    if (ts[r] < ts[r - 1]) return set_error(DG_ERR_ARG, "row timestamps must ascend (the index's time order)");
+  auto add = [&](std::unique_ptr<Column> c) {
+    seg->device_bytes += column_device_bytes(*c);
+    seg->by_name[c->name] = c.get();
+    seg->columns.push_back(std::move(c));
+  };
+  auto flat = [&](Column* c, const void* p, int width) {
+    c->data.total = (int32_t)nrows;
+    c->data.width = width;
+    c->data.codec = CODEC_NONE;
+    static const int64_t zero[2] = {0, 0};
+    const uint8_t* b = nrows ? static_cast<const uint8_t*>(p) : reinterpret_cast<const uint8_t*>(zero);
+    return upload_flat(&c->data, b, b + (size_t)nrows * width);
+  };
+  {
+    std::unique_ptr<Column> t(new Column());
+    t->name = "__time";
+    t->type = DG_COL_LONG;
+    int rc = flat(t.get(), ts, 8);
+    if (rc) return rc;
+    add(std::move(t));
+  }
+  for (int i = 0; i < ncols; ++i) {
+    const dg_row_column& rc_ = cols[i];
+    if (!rc_.name || !*rc_.name || !strcmp(rc_.name, "__time") || seg->find(rc_.name))
+      return set_error(DG_ERR_ARG, "column %d: missing, reserved or repeated name", i);
+    std::unique_ptr<Column> c(new Column());
+    c->name = rc_.name;
+    c->type = rc_.type;
+    int rc = DG_OK;
+    if (rc_.type == DG_COL_LONG || rc_.type == DG_COL_DOUBLE || rc_.type == DG_COL_FLOAT) {
+      if (nrows && !rc_.values) return set_error(DG_ERR_ARG, "%s: null values", rc_.name);
+      rc = flat(c.get(), rc_.values, rc_.type == DG_COL_FLOAT ? 4 : 8);
+    } else if (rc_.type == DG_COL_STRING) {
+      const int32_t card = rc_.card;
+      if (card < 0 || (card > 0 && !rc_.dict) || (nrows && !rc_.ids)) return set_error(DG_ERR_ARG, "%s: bad dictionary", rc_.name);
+      // DimensionDictionary ids (insertion order) -> sorted ids; "" is null (default null handling)
+      std::vector<int32_t> order(card);
+      for (int32_t k = 0; k < card; ++k) order[k] = k;
+      auto is_null = [&](int32_t k) { return !rc_.dict[k] || !rc_.dict[k][0]; };
+      std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+        const bool an = is_null(a), bn = is_null(b);
+        if (an || bn) return an && !bn;
+        return java_compare_str(rc_.dict[a], rc_.dict[b]) < 0;
+      });
+      std::vector<int32_t> remap(card);
+      for (int32_t k = 0; k < card; ++k) {
+        const int32_t o = order[k];
+        if (k > 0) {
+          const int32_t p = order[k - 1];
+          const bool same = is_null(o) ? is_null(p) : (!is_null(p) && !strcmp(rc_.dict[o], rc_.dict[p]));
+          if (same) return set_error(DG_ERR_ARG, "%s: dictionary value repeated", rc_.name);
+        }
+        remap[o] = k;
+        c->dict.push_back(is_null(o) ? std::string() : std::string(rc_.dict[o]));
+        c->dict_null.push_back(is_null(o) ? 1 : 0);
+        c->dict_hash.push_back(is_null(o) ? kNullValueHash : value_hash(c->dict.back()));
+      }
+      std::vector<int32_t> ids((size_t)std::max<int64_t>(nrows, 1));
+      for (int64_t r = 0; r < nrows; ++r) {
+        const int32_t id = rc_.ids[r];
+        if (id < 0 || id >= card) return set_error(DG_ERR_ARG, "%s: row %lld id %d outside [0, %d)", rc_.name, (long long)r, id, card);
+        ids[r] = remap[id];
+      }
+      c->has_bitmaps = false;
+      rc = flat(c.get(), ids.data(), 4);
+    } else {
+      return set_error(DG_ERR_ARG, "%s: column type %d", rc_.name, rc_.type);
+    }
+    if (rc) return rc;
+    add(std::move(c));
+  }
+  if (nrows) {
+    seg->min_time = ts[0];
+    seg->max_time = ts[nrows - 1];
+  }
+  *out = seg.release();
+  return DG_OK;
+}
+
 }  // namespace dg

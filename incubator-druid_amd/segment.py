@@ -55,6 +55,17 @@ class GpuSegment:
         self.context = context or GpuContext.get(device)
         h = ctypes.c_void_p()
         N.check(N.lib().dg_segment_attach(self.context.handle, path.encode(), ctypes.byref(h)))
+        self._init(h, path)
+
+    @classmethod
+    def from_handle(cls, handle: ctypes.c_void_p, context: GpuContext, name: str) -> "GpuSegment":
+        """A segment the engine built otherwise (dg_segment_from_rows: an in-memory index)."""
+        seg = cls.__new__(cls)
+        seg.context = context
+        seg._init(handle, name)
+        return seg
+
+    def _init(self, h: ctypes.c_void_p, path: str):
         self.handle = h
         self.path = path
         GpuSegment._ids += 1
