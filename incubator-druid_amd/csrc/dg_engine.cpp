@@ -3175,9 +3175,9 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     // run heads are only needed by the floatSum row-order pass
     uint32_t* head_pos = has_float_sum(plan) ? dev_take<uint32_t>(cs, (size_t)ng + 16) : nullptr;
     const size_t nt = (size_t)sb.ntiles_sort;  // one carry / open group per tile
-    int64_t* carry_g = dev_take<int64_t>(cs, 4 * nt);  // one carry / open slot per wave quarter of a tile
-    int64_t* open_g = dev_take<int64_t>(cs, 4 * nt);
-    uint64_t* carry_slots = dev_take<uint64_t>(cs, 4 * nt * rec);
+    int64_t* carry_g = dev_take<int64_t>(cs, (size_t)kRedWaves * nt);  // one carry / open slot per wave share of a tile
+    int64_t* open_g = dev_take<int64_t>(cs, (size_t)kRedWaves * nt);
+    uint64_t* carry_slots = dev_take<uint64_t>(cs, (size_t)kRedWaves * nt * rec);
     if ((has_float_sum(plan) && !head_pos) || !carry_g || !open_g || !carry_slots)
       return set_error(DG_ERR_OOM, "groupBy reduce scratch");
     launch_gb_reduce(&sb, plan, res->keys, res->slots, ng, head_pos, carry_g, carry_slots, open_g, st);

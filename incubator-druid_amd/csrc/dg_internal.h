@@ -438,6 +438,12 @@ constexpr int kTileRows = 2048;
 constexpr int kMaxDigitBits = 8;  // radix digits of up to 8 bits (9-bit digits measured slower: 64-byte store runs)
 constexpr int kMaxBins = 1 << kMaxDigitBits;
 constexpr int kSortTile = 4096;  // elements per radix / run tile (256 threads x 16)
+// groupBy reduce: waves per sort tile (each reduces its own 4096 / kRedWaves elements; one carry /
+// open slot per wave)
+#ifndef DG_RED_WAVES
+#define DG_RED_WAVES 16
+#endif
+constexpr int kRedWaves = DG_RED_WAVES;
 constexpr int kMaxCallSegs = 1024;  // segments of one sort-based call (row-ref bases live in LDS)
 inline int sort_tiles(int64_t n) { return (int)std::max<int64_t>(1, (n + kSortTile - 1) / kSortTile); }
 // selected rows -> (key, element index) in (segment, row) order + their aggregator inputs in

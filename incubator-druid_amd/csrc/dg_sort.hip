@@ -824,8 +824,13 @@ __device__ __forceinline__ uint64_t seg_scan_wave(int op, uint64_t v, bool head,
   return v;
 }
 
+#ifndef DG_RED_MINW
+#define DG_RED_MINW 4
+#endif
+constexpr int kRT = 64 * kRedWaves;             // reduce threads per tile
+constexpr int kRSPT = kSortTile / kRT;          // elements per lane
 template <bool REFS>
-__global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw, int64_t pcap,
+__global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw, int64_t pcap,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ run_off, AggPlan plan,
@@ -833,18 +838,18 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
                                                    int64_t cap, uint32_t* __restrict__ head_pos,
                                                    int64_t* __restrict__ carry_g, uint64_t* __restrict__ carry_slots,
                                                    int64_t* __restrict__ open_g) {
-  // Each wave reduces its own contiguous quarter of the tile (kWSeg elements, 16 chunks of 64): a
+  // Each wave reduces its own contiguous share of the tile (kWSeg elements, kRSPT chunks of 64): a
   // segmented wave scan per chunk with the open run carried in registers, no barriers. A run that
-  // crosses a quarter boundary is finished like one crossing a tile boundary: the quarter holding
-  // its head writes it open (device encoding, listed in open_g), every later quarter's share goes to
-  // that quarter's carry slot (k_gb_carry folds it in, k_gb_open_finalize finalizes).
-  constexpr int kWSeg = kSortTile / 4;
+  // crosses a share boundary is finished like one crossing a tile boundary: the share holding
+  // its head writes it open (device encoding, listed in open_g), every later share's share goes to
+  // that share's carry slot (k_gb_carry folds it in, k_gb_open_finalize finalizes).
+  constexpr int kWSeg = kSortTile / kRedWaves;
   __shared__ uint64_t s_key[kSortTile + 2];  // [0] = element before the tile, [1 + x] = element x
-  __shared__ uint32_t s_heads[4];
+  __shared__ uint32_t s_heads[kRedWaves];
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t wt = (int64_t)blockIdx.x * 4 + wave;  // wave tile (carry / open slot)
+  const int64_t wt = (int64_t)blockIdx.x * kRedWaves + wave;  // wave tile (carry / open slot)
   if (lane == 0) {
     carry_g[wt] = -1;
     open_g[wt] = -1;
@@ -853,9 +858,9 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
   const int tile_n = (int)min<int64_t>(kSortTile, (int64_t)n - base);
   const uint64_t kmask = kshift ? ((1ull << kshift) - 1ull) : 0ull;
   const int wbase = wave * kWSeg;
-  uint32_t idx_of[kSPT];
+  uint32_t idx_of[kRSPT];
 #pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
+  for (int c = 0; c < kRSPT; ++c) {
     const int x = wbase + c * 64 + lane;
     uint64_t w = 0;
     if (x < tile_n) w = keys[base + x];
@@ -869,10 +874,10 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
   }
   // up to two payload slots per element, gathered once and together (random record reads in flight)
   constexpr int kRegSlots = 2;
-  uint64_t xr[kSPT][kRegSlots];
+  uint64_t xr[kRSPT][kRegSlots];
   if (pw <= kRegSlots) {
 #pragma unroll
-    for (int c = 0; c < kSPT; ++c) {
+    for (int c = 0; c < kRSPT; ++c) {
       const bool valid = wbase + c * 64 + lane < tile_n;
       if (pcap) {  // carried by the sort: sequential words at the sorted position
         const size_t i = (size_t)(base + wbase + c * 64 + lane);
@@ -880,7 +885,11 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
         xr[c][1] = valid && pw >= 2 ? payload[(size_t)pcap + i] : 0ull;
         continue;
       }
+#ifdef DG_REDUCE_SEQPAY  // A/B timing only (wrong results): the gather replaced by sequential reads
+      const uint64_t* pr = payload + (size_t)(base + wbase + c * 64 + lane) * pw;
+#else
       const uint64_t* pr = payload + (size_t)idx_of[c] * pw;
+#endif
       if (pw == 2 && valid) {
         const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(pr);  // 16-byte aligned: pw == 2
         xr[c][0] = w.x;
@@ -892,11 +901,11 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
     }
   }
   __syncthreads();  // the tile's keys are in LDS
-  // run heads / ends of my elements, and the groups whose head lies before my quarter
+  // run heads / ends of my elements, and the groups whose head lies before my share
   uint32_t hm = 0, tm = 0;
-  uint32_t nh = 0;  // heads in my quarter
+  uint32_t nh = 0;  // heads in my share
 #pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
+  for (int c = 0; c < kRSPT; ++c) {
     const int x = wbase + c * 64 + lane;
     const bool valid = x < tile_n;
     const uint64_t k = s_key[1 + x];
@@ -909,14 +918,14 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
   }
   if (lane == 0) s_heads[wave] = nh;
   __syncthreads();
-  int64_t G = run_off[blockIdx.x];  // groups with a head before my quarter
+  int64_t G = run_off[blockIdx.x];  // groups with a head before my share
   for (int w = 0; w < wave; ++w) G += s_heads[w];
   const int64_t Gq = G;
-  int32_t grel[kSPT];  // group of each element relative to Gq (-1: the group open before my quarter)
+  int32_t grel[kRSPT];  // group of each element relative to Gq (-1: the group open before my share)
   {
     int heads = 0;
 #pragma unroll
-    for (int c = 0; c < kSPT; ++c) {
+    for (int c = 0; c < kRSPT; ++c) {
       const bool h = (hm >> c) & 1u;
       const uint64_t bal = __ballot(h);
       const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
@@ -930,7 +939,7 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
     }
   }
   const int na = plan.n, rec = na + 1;
-  const int wend = min(tile_n, wbase + kWSeg) - 1;  // my quarter's last element
+  const int wend = min(tile_n, wbase + kWSeg) - 1;  // my share's last element
   for (int a = -1; a < na; ++a) {
     const int kind = a < 0 ? DG_AGG_COUNT : plan.kind[a];
     if (kind == DG_AGG_FLOAT_SUM) continue;  // k_fsum_runs: float32 in row order
@@ -938,7 +947,7 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
     const uint64_t ident = a < 0 ? 0ull : identity_of(op, kind);
     uint64_t run = ident;  // the run open at the end of the previous chunk
 #pragma unroll
-    for (int c = 0; c < kSPT; ++c) {
+    for (int c = 0; c < kRSPT; ++c) {
       const int x = wbase + c * 64 + lane;
       const bool valid = x < tile_n;
       uint64_t xv;
@@ -964,10 +973,13 @@ __global__ __launch_bounds__(kST, 2) void k_gb_reduce(const uint64_t* __restrict
         const bool t = (tm >> c) & 1u;
         if (t || x == wend) {
           const int32_t gr = grel[c];
-          if (gr >= 0) {  // a group headed in my quarter: complete, or open at the quarter's end
+          if (gr >= 0) {  // a group headed in my share: complete, or open at the share's end
+#ifdef DG_REDUCE_NOSTORE  // A/B timing only (wrong results): the slot stores dropped
+            if (v == 0x5a5a5a5a5a5a5a5aull)
+#endif
             out_slots[(1 + a) * cap + Gq + gr] = t ? finalize_dev(kind, v) : v;
             if (!t) open_g[wt] = Gq + gr;
-          } else {  // my quarter's share of a group headed earlier
+          } else {  // my share's share of a group headed earlier
             carry_slots[wt * rec + 1 + a] = v;
             carry_g[wt] = Gq - 1;
           }
@@ -1018,14 +1030,14 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
   const int nt = sb->ntiles_sort;
   const uint32_t* refs = sb->refs[sb->cur];
   if (refs)
-    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->pcap, sb->keys[sb->cur], refs,
+    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->pcap, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
                        open_g);
   else
-    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kST), 0, s, sb->payload, sb->pw, sb->pcap, sb->keys[sb->cur], refs,
+    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->pcap, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
                        open_g);
-  const int64_t nw = (int64_t)nt * 4;  // carry / open slots: one per wave quarter of a tile
+  const int64_t nw = (int64_t)nt * kRedWaves;  // carry / open slots: one per wave share of a tile
   const unsigned g = (unsigned)((nw + 255) / 256);
   hipLaunchKernelGGL(k_gb_carry, dim3(g), dim3(256), 0, s, carry_g, carry_slots, nw, plan, out_slots, cap);
   hipLaunchKernelGGL(k_gb_open_finalize, dim3(g), dim3(256), 0, s, open_g, nw, plan, out_slots, cap);
