@@ -887,6 +887,9 @@ __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* 
       }
 #ifdef DG_REDUCE_SEQPAY  // A/B timing only (wrong results): the gather replaced by sequential reads
       const uint64_t* pr = payload + (size_t)(base + wbase + c * 64 + lane) * pw;
+#elif defined(DG_REDUCE_LOCALPAY)  // A/B timing only: random within a window around the position
+      const uint64_t* pr = payload + (size_t)min<int64_t>((int64_t)(((base + wbase + c * 64 + lane) & ~((1ll << DG_REDUCE_LOCALPAY) - 1)) |
+                                                   (idx_of[c] & ((1u << DG_REDUCE_LOCALPAY) - 1))), (int64_t)n - 1) * pw;
 #else
       const uint64_t* pr = payload + (size_t)idx_of[c] * pw;
 #endif
@@ -901,6 +904,14 @@ __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* 
     }
   }
   __syncthreads();  // the tile's keys are in LDS
+#ifdef DG_REDUCE_PROBE_LOADS  // A/B timing only (wrong results): stop after the loads
+  {
+    uint64_t acc = 0;
+    for (int c = 0; c < kRSPT; ++c) acc ^= xr[c][0] ^ xr[c][1] ^ s_key[1 + wbase + c * 64 + lane];
+    if (acc == 0x5a5a5a5a5a5a5a5aull) out_keys[0] = acc;
+    return;
+  }
+#endif
   // run heads / ends of my elements, and the groups whose head lies before my share
   uint32_t hm = 0, tm = 0;
   uint32_t nh = 0;  // heads in my share
