@@ -191,7 +191,7 @@ def _light_boundary(rng):
     copy chains <= 16 hops): each case decodes bit-exactly on whichever decoder takes it."""
     r = lambda k: rng.integers(0, 256, k).astype(np.uint8).tobytes()  # noqa: E731
     cases = {}
-    for depth in (1, 16, 17, 40):  # every match copies the previous 64 bytes: chain depth = #matches
+    for depth in (1, 16, 17, 32, 33, 40):  # every match copies the previous 64 bytes: chain depth = #matches
         cases[f"chain{depth}"] = lz4_sequences([(r(64) if i == 0 else b"", 64, 64) for i in range(depth)], r(33))
     for nseq in (2047, 2048, 2049):  # sequences incl. the last literal-only one
         cases[f"seq{nseq}"] = lz4_sequences([(r(20), int(rng.integers(1, 20)), 4 + i % 3) for i in range(nseq - 1)],
@@ -206,7 +206,19 @@ def _light_boundary(rng):
         o += L + m
     cases["lit_heavy"] = lz4_sequences(seqs, r(BLOCK - o) if BLOCK - o < 2000 else r(3))
     cases["rle_short"] = lz4_sequences([(b"\x01\x02\x03", 3, 5000), (r(10), 2, 9)], r(40))
+    # the medium tier's limits (<= 1024 intervals = 8192 sequences, chains <= 16 hops): two literal
+    # bytes and a periodic 4-byte copy of them per sequence (depth 1); 8193 sequences are wide
+    for nseq in (8191, 8192, 8193):
+        cases[f"med{nseq}"] = lz4_sequences([(r(2), 2, 4 + i % 2) for i in range(nseq - 1)], r(5))
+    # noisy doubles (the headline's doubleSum column): ~7.5 K short sequences into earlier literals
+    vals = rng.normal(5000.0, 1.0, BLOCK // 8).astype("<f8").tobytes()
+    cases["normal_dbl"] = _lz4_hc(vals)
     return cases
+
+
+def _lz4_hc(raw: bytes) -> bytes:
+    import importlib
+    return importlib.import_module("incubator-druid_amd.writer").lz4_compress(raw, "hc")
 
 
 @pytest.mark.gpu
