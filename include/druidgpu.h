@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 7
+#define DG_ABI_VERSION 8
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -214,14 +214,17 @@ void dg_segment_release(dg_segment* seg);
  * DimensionDictionary (values by id in insertion order, NULL or "" = null) plus one id per row and is
  * re-sorted into the sorted-dictionary form (SortedDimensionDictionary) the engines use. Such a
  * segment has no bitmap index: string filters run as row predicates on the ids (the adapter's
- * ValueMatchers). Multi-value rows are not taken. Released with dg_segment_release. */
+ * ValueMatchers; a multi-value row matches when one of its values does, an empty row as null).
+ * Multi-value dimension: offsets[n_rows + 1] into ids (StringDimensionIndexer's encoded rows, values
+ * in the row's order; an empty row = no values). Released with dg_segment_release. */
 typedef struct {
   const char* name;
   int32_t type;            /* DG_COL_LONG / DG_COL_FLOAT / DG_COL_DOUBLE / DG_COL_STRING */
   int32_t card;            /* STRING: dictionary size */
   const char* const* dict; /* STRING: value of every id */
-  const int32_t* ids;      /* STRING: [n_rows] ids into dict */
+  const int32_t* ids;      /* STRING: [n_rows] ids into dict (multi-value: [offsets[n_rows]]) */
   const void* values;      /* numeric: [n_rows] int64 / float / double */
+  const int32_t* offsets;  /* STRING multi-value: [n_rows + 1] row starts into ids; NULL = one id per row */
 } dg_row_column;
 int dg_segment_from_rows(dg_context* ctx, int64_t n_rows, const int64_t* timestamps, int64_t interval_start,
                          int64_t interval_end, const dg_row_column* columns, int32_t n_columns, dg_segment** out);

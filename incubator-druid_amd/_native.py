@@ -97,7 +97,8 @@ class dg_record_layout(ctypes.Structure):
 
 class dg_row_column(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("type", ctypes.c_int32), ("card", ctypes.c_int32),
-                ("dict", ctypes.c_void_p), ("ids", ctypes.c_void_p), ("values", ctypes.c_void_p)]
+                ("dict", ctypes.c_void_p), ("ids", ctypes.c_void_p), ("values", ctypes.c_void_p),
+                ("offsets", ctypes.c_void_p)]
 
 
 class dg_order_column(ctypes.Structure):

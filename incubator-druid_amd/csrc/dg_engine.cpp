@@ -385,6 +385,7 @@ struct DecodeBatch {
   int64_t bytes = 0;  // algorithmic bytes read
 };
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
+static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st);
 static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr);
 
 // ------------------------------------------------------------------------------------------------
@@ -750,7 +751,7 @@ static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos
         fp->preds.push_back(std::move(L));
         return DG_OK;
       }
-      if (c->type != DG_COL_STRING || (!c->has_bitmaps && c->multi_value))
+      if (c->type != DG_COL_STRING)
         return set_error(DG_ERR_UNSUPPORTED, "filter on %s needs a bitmap index", f.dimension);
       std::vector<int32_t> ids;
       if (f.kind == DG_F_SELECTOR) {
@@ -799,6 +800,7 @@ static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos
         L.col = c;
         L.set.assign((c->dict.size() + 63) / 64, 0);
         for (int32_t i : ids) L.set[i >> 6] |= (int64_t)(1ull << (i & 63));
+        L.p.has_lo = c->multi_value && !c->dict.empty() && c->dict_null[0] && !ids.empty() && ids[0] == 0;
         fp->prog.push_back((int32_t)fp->leaf_ids.size());
         fp->leaf_ids.emplace_back();
         fp->leaf_col.push_back(nullptr);
@@ -931,9 +933,10 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
     if (fp.leaf_pred[l] < 0) continue;
     PredLeaf& L = fp.preds[fp.leaf_pred[l]];
     DecodeBatch db;
-    ColView v;
+    ColView v, voff;
     memset(&v, 0, sizeof v);
-    int rc2 = column_view(L.col, cs, &db, &v, st);
+    memset(&voff, 0, sizeof voff);
+    int rc2 = L.col->multi_value ? multi_view(L.col, cs, &db, &v, &voff, st) : column_view(L.col, cs, &db, &v, st);
     if (rc2) return rc2;
     if (!L.set.empty()) {
       int64_t* d_set;
@@ -958,7 +961,7 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
     rc2 = run_decodes(cs, &db, st);
     if (rc2) return rc2;
     DG_FLUSH(cs, st);
-    launch_num_pred(v, seg->nrows, L.p, h_sets[l], st);
+    launch_num_pred(v, voff, seg->nrows, L.p, h_sets[l], st);
   }
   const int plen = (int)fp.prog.size();
   int32_t* d_prog;

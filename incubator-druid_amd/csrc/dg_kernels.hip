@@ -340,12 +340,21 @@ __device__ __forceinline__ bool range_ok(int lc, int uc, const NumPred& p) {
   return lok && uok;
 }
 
-__global__ __launch_bounds__(256) void k_num_pred(ColView v, int64_t nrows, NumPred p, uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_num_pred(ColView v, ColView voff, int64_t nrows, NumPred p, uint32_t* __restrict__ out) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   bool m = false;
   if (r < nrows && p.kind != PRED_FALSE) {
     const uint8_t* ptr = cv_ptr(v, r);
-    if (v.kind == VIEW_IDS) {
+    if (v.kind == VIEW_IDS && voff.kind != VIEW_ABSENT) {
+      // a multi-value row matches when any of its values does; an empty row as the null value
+      // (DimensionSelector value matchers over IndexedInts: size 0 -> predicate(null))
+      const uint32_t b = load_id(voff, r), e = load_id(voff, r + 1);
+      if (b == e) m = p.has_lo != 0;
+      for (uint32_t k = b; k < e && !m; ++k) {
+        const uint32_t id = load_id(v, k);
+        m = ((uint64_t)p.set[id >> 6] >> (id & 63)) & 1ull;
+      }
+    } else if (v.kind == VIEW_IDS) {
       const uint32_t id = load_id(v, r);
       m = p.kind == PRED_ID_SET && ((uint64_t)p.set[id >> 6] >> (id & 63)) & 1ull;
     } else if (v.kind == VIEW_LONG) {
@@ -385,9 +394,9 @@ __global__ __launch_bounds__(256) void k_num_pred(ColView v, int64_t nrows, NumP
   }
 }
 
-void launch_num_pred(ColView v, int64_t nrows, NumPred p, uint32_t* out, hipStream_t s) {
+void launch_num_pred(ColView v, ColView voff, int64_t nrows, NumPred p, uint32_t* out, hipStream_t s) {
   if (nrows <= 0) return;
-  hipLaunchKernelGGL(k_num_pred, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, v, nrows, p, out);
+  hipLaunchKernelGGL(k_num_pred, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, v, voff, nrows, p, out);
 }
 
 void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_sets, uint32_t* out, int64_t nrows,

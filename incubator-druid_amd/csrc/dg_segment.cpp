@@ -923,14 +923,38 @@ int segment_from_rows(Context* ctx, int64_t nrows, const int64_t* ts, int64_t is
         c->dict_null.push_back(is_null(o) ? 1 : 0);
         c->dict_hash.push_back(is_null(o) ? kNullValueHash : value_hash(c->dict.back()));
       }
-      std::vector<int32_t> ids((size_t)std::max<int64_t>(nrows, 1));
-      for (int64_t r = 0; r < nrows; ++r) {
+      int64_t nv = nrows;
+      if (rc_.offsets) {  // multi-value rows: offsets must start at 0 and never decrease
+        if (rc_.offsets[0] != 0) return set_error(DG_ERR_ARG, "%s: offsets[0] != 0", rc_.name);
+        for (int64_t r = 0; r < nrows; ++r)
+          if (rc_.offsets[r + 1] < rc_.offsets[r]) return set_error(DG_ERR_ARG, "%s: offsets decrease at row %lld", rc_.name, (long long)r);
+        nv = rc_.offsets[nrows];
+        if (nv > 0 && !rc_.ids) return set_error(DG_ERR_ARG, "%s: null ids", rc_.name);
+      }
+      std::vector<int32_t> ids((size_t)std::max<int64_t>(nv, 1));
+      for (int64_t r = 0; r < nv; ++r) {
         const int32_t id = rc_.ids[r];
-        if (id < 0 || id >= card) return set_error(DG_ERR_ARG, "%s: row %lld id %d outside [0, %d)", rc_.name, (long long)r, id, card);
+        if (id < 0 || id >= card) return set_error(DG_ERR_ARG, "%s: value %lld id %d outside [0, %d)", rc_.name, (long long)r, id, card);
         ids[r] = remap[id];
       }
       c->has_bitmaps = false;
-      rc = flat(c.get(), ids.data(), 4);
+      if (rc_.offsets) {
+        c->multi_value = true;
+        c->mv_off.total = (int32_t)nrows + 1;
+        c->mv_off.width = 4;
+        c->mv_off.codec = CODEC_NONE;
+        rc = upload_flat(&c->mv_off, reinterpret_cast<const uint8_t*>(rc_.offsets),
+                         reinterpret_cast<const uint8_t*>(rc_.offsets + nrows + 1));
+        if (rc) return rc;
+        c->data.total = (int32_t)nv;
+        c->data.width = 4;
+        c->data.codec = CODEC_NONE;
+        static const int32_t zero[4] = {0, 0, 0, 0};
+        const uint8_t* b = nv ? reinterpret_cast<const uint8_t*>(ids.data()) : reinterpret_cast<const uint8_t*>(zero);
+        rc = upload_flat(&c->data, b, b + (size_t)nv * 4);
+      } else {
+        rc = flat(c.get(), ids.data(), 4);
+      }
     } else {
       return set_error(DG_ERR_ARG, "%s: column type %d", rc_.name, rc_.type);
     }

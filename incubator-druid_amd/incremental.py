@@ -7,6 +7,7 @@ and hands the rows to the engine with ``dg_segment_from_rows``:
 
 * dimension values are encoded per dimension in insertion order (``DimensionDictionary.add``,
   StringDimensionIndexer.java), "" and missing values are null (``NullHandling.emptyToNullIfNeeded``);
+  a list value is a multi-value row (sorted values, an empty list has no values);
 * with rollup, rows with equal (truncated timestamp, dimension values) fold into one fact whose metric
   columns combine the ingested values (``IncrementalIndex.addToFacts``; the ingestion aggregators
   longSum / doubleSum / floatSum / count / min / max). The timestamp is truncated by the index's
@@ -86,6 +87,7 @@ class IncrementalIndex:
         self._dicts: List[Dict[Optional[str], int]] = [dict() for _ in self.dimensions]
         self._values: List[List[Optional[str]]] = [[] for _ in self.dimensions]
         self._facts: Dict[tuple, list] = {}
+        self._multi = [False] * len(self.dimensions)  # hasMultipleValues
         self._order = 0
 
     def _id(self, d: int, v) -> int:
@@ -96,10 +98,25 @@ class IncrementalIndex:
             self._values[d].append(v)
         return i
 
+    def _encode(self, d: int, v) -> tuple:
+        """StringDimensionIndexer.processRowValsToUnsortedEncodedKeyComponent (:247-300): null / a
+        scalar -> one id; a list: empty -> no ids (null still enters the dictionary), else its values
+        sorted (MultiValueHandling SORTED_ARRAY, naturalNullsFirst) -> their ids."""
+        if isinstance(v, (list, tuple)):
+            vals = [None if x is None or x == "" else str(x) for x in v]
+            if not vals:
+                self._id(d, None)
+                return ()
+            if len(vals) > 1:
+                self._multi[d] = True
+                vals.sort(key=_java_key)
+            return tuple(self._id(d, x) for x in vals)
+        return (self._id(d, v),)
+
     def add(self, timestamp: int, event: Dict) -> int:
         """IncrementalIndex.add: returns the number of facts."""
         t = int(timestamp) if self.gran is None else self.gran.bucket_start(int(timestamp))
-        key = (t, tuple(self._id(d, event.get(name)) for d, name in enumerate(self.dimensions)))
+        key = (t, tuple(self._encode(d, event.get(name)) for d, name in enumerate(self.dimensions)))
         if not self.rollup:
             key = key + (self._order,)
         self._order += 1
@@ -121,15 +138,32 @@ class IncrementalIndex:
         return len(self._facts)
 
     def _ordered(self):
+        # IncrementalIndexRowComparator: time, then per dimension compareUnsortedEncodedKeyComponents
+        # (the row's value count first, then its values, String.compareTo with nulls first)
         def key(k):
-            dims = tuple(_java_key(self._values[d][i]) for d, i in enumerate(k[1]))
+            dims = tuple((len(ids), tuple(_java_key(self._values[d][i]) for i in ids)) for d, ids in enumerate(k[1]))
             return (k[0], dims) + ((k[2],) if len(k) > 2 else ())
         return sorted(self._facts.items(), key=lambda kv: key(kv[0]))
+
+    def _row_ids(self, d: int, ids: tuple):
+        """A single-valued dimension stores one id per row (an empty list as null)."""
+        if self._multi[d]:
+            return ids
+        return ids[0] if ids else self._dicts[d][None]
 
     def _columns(self):
         facts = self._ordered()
         ts = np.array([k[0] for k, _ in facts], dtype=np.int64)
-        ids = [np.array([k[1][d] for k, _ in facts], dtype=np.int32) for d in range(len(self.dimensions))]
+        ids = []
+        for d in range(len(self.dimensions)):
+            rows = [self._row_ids(d, k[1][d]) for k, _ in facts]
+            if self._multi[d]:
+                offs = np.zeros(len(rows) + 1, np.int32)
+                offs[1:] = np.cumsum([len(r) for r in rows])
+                flat = np.array([i for r in rows for i in r], dtype=np.int32)
+                ids.append((flat, offs))
+            else:
+                ids.append(np.array(rows, dtype=np.int32))
         mets = []
         for i, (name, kind, _f) in enumerate(self.metrics):
             typ = _KINDS[kind][0]
@@ -150,13 +184,15 @@ class IncrementalIndex:
         for d, name in enumerate(self.dimensions):
             vals = self._values[d]
             arr = (ctypes.c_char_p * max(len(vals), 1))(*[None if v is None else v.encode() for v in vals])
-            keep += [arr, ids[d]]
+            flat, offs = ids[d] if self._multi[d] else (ids[d], None)
+            flat = flat if len(flat) else np.zeros(1, np.int32)
+            keep += [arr, flat, offs]
             cols.append(N.dg_row_column(name.encode(), 4, len(vals), ctypes.cast(arr, ctypes.c_void_p),
-                                        ids[d].ctypes.data, None))
+                                        flat.ctypes.data, None, None if offs is None else offs.ctypes.data))
         for name, typ, v in mets:
             keep.append(v)
             cols.append(N.dg_row_column(name.encode(), {"long": 1, "float": 2, "double": 3}[typ], 0, None, None,
-                                        v.ctypes.data))
+                                        v.ctypes.data, None))
         carr = (N.dg_row_column * max(len(cols), 1))(*cols)
         iv = self._interval(ts)
         ctx = context or GpuContext.get(device)
@@ -175,6 +211,11 @@ class IncrementalIndex:
             order = sorted(range(len(vals)), key=lambda i: _java_key(vals[i]))
             remap = np.zeros(max(len(vals), 1), np.int32)
             remap[order] = np.arange(len(order), dtype=np.int32)
-            dims[name] = (["" if vals[i] is None else vals[i] for i in order], remap[ids[d]])
+            dct = ["" if vals[i] is None else vals[i] for i in order]
+            if self._multi[d]:  # IndexMergerV9: the multi-value column format, values in row order
+                flat, offs = ids[d]
+                dims[name] = (dct, [remap[flat[offs[r]:offs[r + 1]]] for r in range(len(offs) - 1)])
+            else:
+                dims[name] = (dct, remap[ids[d]])
         return SegmentSpec(timestamps=ts, dims=dims, metrics={n: (t, v) for n, t, v in mets},
                            interval=self._interval(ts))

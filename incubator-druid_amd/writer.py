@@ -414,7 +414,7 @@ def multi_string_column_part(dictionary: List[Optional[str]], rows: Sequence[np.
     V3CompressedVSizeColumnarMultiIntsSerializer.java:87-120); uncompressed = version
     UNCOMPRESSED_MULTI_VALUE with VSizeColumnarMultiInts ([0x01][numBytes][i32 size][i32 count]
     [count end byte offsets][big-endian values][4 - numBytes pad], VSizeColumnarMultiInts.fromIterable).
-    Value v's bitmap holds every row whose list contains v."""
+    Value v's bitmap holds every row whose list contains v (and the null value's, rows with no value)."""
     card = len(dictionary)
     dict_vals = [b"" if (v is None or v == "") else v.encode("utf-8") for v in dictionary]
     nb = num_bytes_for_max(card)
@@ -439,8 +439,13 @@ def multi_string_column_part(dictionary: List[Optional[str]], rows: Sequence[np.
     sf, sr = flat[order], row_of[order]
     bounds = np.searchsorted(sf, np.arange(card + 1))
     bms = []
+    # StringDimensionMergerV9.processMergedRow / :483: rows without values join the null value's
+    # bitmap when null is the dictionary's first value
+    empty_rows = np.nonzero(lens == 0)[0] if card and dictionary[0] in (None, "") else np.zeros(0, np.int64)
     for v in range(card):
         rws = np.unique(sr[bounds[v]:bounds[v + 1]])
+        if v == 0 and len(empty_rows):
+            rws = np.union1d(rws, empty_rows)
         if bitmap == "concise":
             bms.append(_tools.concise_encode(rws).astype(">i4").tobytes())
         else:

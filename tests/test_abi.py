@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_structs():
     N = importlib.import_module("incubator-druid_amd._native")
-    assert N.lib().dg_abi_version() == 7
+    assert N.lib().dg_abi_version() == 8
     # struct layouts the header fixes (LP64)
     assert ctypes.sizeof(N.dg_filter) == 64
     assert ctypes.sizeof(N.dg_agg) == 32
@@ -37,7 +37,7 @@ def test_abi_version_and_structs():
     assert ctypes.sizeof(N.dg_topn) == 56
     assert ctypes.sizeof(N.dg_order_column) == 16
     assert ctypes.sizeof(N.dg_limit) == 24
-    assert ctypes.sizeof(N.dg_row_column) == 40
+    assert ctypes.sizeof(N.dg_row_column) == 48
 
 
 def test_gpu_kernels_are_gfx950_code_objects():

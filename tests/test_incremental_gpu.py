@@ -23,7 +23,7 @@ METRICS = [("rows", "count", None), ("sumLong", "longSum", "l"), ("sumDouble", "
 def _index(seed, n, rollup=True, gran="minute"):
     I = importlib.import_module("incubator-druid_amd.incremental")
     rng = np.random.default_rng(seed)
-    idx = I.IncrementalIndex(["dimA", "dimB", "dimC"], METRICS, query_granularity=gran, rollup=rollup,
+    idx = I.IncrementalIndex(["dimA", "dimB", "dimC", "tags"], METRICS, query_granularity=gran, rollup=rollup,
                              interval=(0, 6 * 3_600_000))
     a_vals = ["zeta", "alpha", "", "Beta", "béta", "gamma", "10", "9", "\U0001f600x", "～"]
     t = np.sort(rng.integers(0, 6 * 3_600_000, n))
@@ -33,6 +33,8 @@ def _index(seed, n, rollup=True, gran="minute"):
               "l": int(rng.integers(-1000, 1000)), "d": float(rng.normal(100, 50)), "f": float(rng.normal(5000, 1))}
         if rng.random() < 0.6:
             ev["dimC"] = "c" + str(int(rng.integers(0, 30)))
+        k = int(rng.integers(0, 4))  # multi-value: 0-3 tags (an empty list has no values)
+        ev["tags"] = ["t" + str(int(x)) for x in rng.integers(0, 12, k)] if k != 1 or rng.random() < 0.5 else "t0"
         idx.add(int(t[i]), ev)
     return idx
 
@@ -53,6 +55,15 @@ def test_rollup_bookkeeping():
     assert spec.metrics["rows"][1].tolist() == [2, 2, 1]
     assert spec.metrics["s"][1].tolist() == [2, 7, 5]
     assert np.signbit(spec.metrics["m"][1][1]) and spec.metrics["m"][1][0] == 0.0
+    mv = I.IncrementalIndex(["t"], [("rows", "count", None)])
+    mv.add(0, {"t": ["b", "a"]})
+    mv.add(0, {"t": []})
+    mv.add(0, {"t": "a"})
+    mv.add(0, {"t": ["a", "b"]})  # the same sorted row as the first: rolled up
+    sp = mv.to_spec()
+    dct, rows = sp.dims["t"]
+    assert dct == ["", "a", "b"] and [r.tolist() for r in rows] == [[], [1], [1, 2]]  # by value count, then values
+    assert sp.metrics["rows"][1].tolist() == [1, 1, 2]
     no = I.IncrementalIndex(["x"], [("rows", "count", None)], rollup=False)
     for _ in range(3):
         no.add(5, {"x": "a"})
@@ -94,6 +105,15 @@ def _queries(Q):
                               filter=filters[6]))
     out.append(Q.GroupByQuery(intervals=iv, granularity="all", dimensions=["dimB", "dimA"], aggregations=aggs,
                               limitSpec={"type": "default", "columns": ["dimA"], "limit": 30}))
+    # the multi-value dimension: grouped (a row under each of its values, an empty row as null),
+    # topN per value, and filtered (a row matches when one of its values does)
+    out.append(Q.GroupByQuery(intervals=iv, granularity="hour", dimensions=["tags", "dimC"], aggregations=aggs))
+    out.append(Q.TopNQuery(intervals=iv, granularity="all", dimension="tags", metric="sumDouble", threshold=6,
+                           aggregations=aggs, filter=filters[2]))
+    for f in (Q.SelectorDimFilter("tags", "t3"), Q.SelectorDimFilter("tags", None), Q.InDimFilter("tags", ["t1", "t11", None]),
+              Q.NotDimFilter(Q.BoundDimFilter("tags", "t2", "t5"))):
+        out.append(Q.TimeseriesQuery(intervals=iv, granularity="hour", filter=f, aggregations=aggs))
+        out.append(Q.GroupByQuery(intervals=iv, granularity="all", dimensions=["dimA"], aggregations=aggs, filter=f))
     return out
 
 
