@@ -3334,7 +3334,18 @@ int dg_result_limit(dg_result* r, const dg_limit* spec) {
   }
   const int64_t n = r->ngroups;
   const int64_t m = std::min<int64_t>(spec->limit, n);
-  if (n == 0) {
+  // the push-down order is the result's own key order (no ORDER BY beyond an ascending LEXICOGRAPHIC
+  // prefix of the dimensions, time first): the first `limit` groups already are the answer
+  bool natural = true;
+  for (int f = 0, d = 0; f < (int)field_dim.size(); ++f) {
+    if (field_dim[f] < 0) {
+      natural &= f == 0;
+      continue;
+    }
+    natural &= field_dim[f] == d++ && !desc[field_dim[f]] && !rank[field_dim[f]];
+  }
+  if (n == 0 || natural) {
+    r->ngroups = m;
     r->limited = true;
     return DG_OK;
   }
