@@ -75,17 +75,17 @@ __device__ __forceinline__ uint32_t load_id(const ColView& v, int64_t r) {
 // Input of one aggregator for row r, encoded for its slot op.
 // Selector coercions follow LongColumnSelector / DoubleColumnSelector / FloatColumnSelector
 // (segment/DoubleColumnSelector.java:40-55): getLong of a double = (long) d, getFloat = (float) x, ...
-__device__ __forceinline__ uint64_t agg_input(int kind, const ColView& v, int64_t r) {
+// the aggregator input of a value at p (a view of kind vkind; p unused for VIEW_ABSENT)
+__device__ __forceinline__ uint64_t agg_input_at(int kind, int vkind, const uint8_t* p) {
   int64_t l = 0;
   double d = 0.0;
   float f = 0.0f;
-  if (kind != DG_AGG_COUNT && v.kind != VIEW_ABSENT) {
-    const uint8_t* p = cv_ptr(v, r);
-    if (v.kind == VIEW_LONG) {
+  if (kind != DG_AGG_COUNT && vkind != VIEW_ABSENT) {
+    if (vkind == VIEW_LONG) {
       l = *reinterpret_cast<const int64_t*>(p);
       d = (double)l;
       f = (float)l;
-    } else if (v.kind == VIEW_DOUBLE) {
+    } else if (vkind == VIEW_DOUBLE) {
       d = *reinterpret_cast<const double*>(p);
       l = java_d2l(d);
       f = (float)d;
@@ -107,6 +107,10 @@ __device__ __forceinline__ uint64_t agg_input(int kind, const ColView& v, int64_
     case DG_AGG_FLOAT_MIN: return f != f ? 0ull : ord_key((double)f);
     default: return f != f ? ~0ull : ord_key((double)f);  // FLOAT_MAX
   }
+}
+
+__device__ __forceinline__ uint64_t agg_input(int kind, const ColView& v, int64_t r) {
+  return agg_input_at(kind, v.kind, kind != DG_AGG_COUNT && v.kind != VIEW_ABSENT ? cv_ptr(v, r) : nullptr);
 }
 
 // ---- four consecutive rows r .. r + 3 (r % 4 == 0, all inside the view's block): one or a few
