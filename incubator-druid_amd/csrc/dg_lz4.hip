@@ -875,12 +875,6 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   __shared__ uint16_t s_lut[kLtLut];  // first sequence covering position 64 * i
   __shared__ int s_tmp[kLtThreads / 64];
   __shared__ int s_bad;
-  uint32_t* s_start = s_buf;                    // [kLtMaxSeq + 1] output start of every sequence, then the total
-  uint32_t* s_mst = s_buf + kLtMaxSeq + 1;      // [kLtMaxSeq] output start of its match
-  uint32_t* s_lit = s_mst + kLtMaxSeq;          // [kLtMaxSeq] input offset of its literals
-  int32_t* s_mb = reinterpret_cast<int32_t*>(s_lit + kLtMaxSeq);  // [kLtMaxSeq] input base of a resolved match, -1
-  uint16_t* s_dist = reinterpret_cast<uint16_t*>(s_mb + kLtMaxSeq);  // [kLtMaxSeq] match distance
-
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = job.src_len, ncp = job.ncp;
@@ -889,6 +883,20 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
     if (tid == 0) atomicOr(err, 1);
     return;
   }
+  // sequence table (sequence i = thread * kLzSeqPerCp + s): right after the staged input when both
+  // fit, so the output reads literals from LDS; otherwise over the input (literals from L2)
+  const int nsq = ncp * kLzSeqPerCp;
+  const int in_words = ((n + 15) >> 4) * 4 + 4;  // staged input + one zero uint4
+#ifndef DG_LT_NOKEEP
+  const bool keep_in = in_words + (nsq + 1) + 3 * nsq + (nsq + 1) / 2 <= kLtBufWords;
+#else
+  const bool keep_in = false;  // (A/B: literals always from L2)
+#endif
+  uint32_t* s_start = s_buf + (keep_in ? in_words : 0);  // [nsq + 1] output start of every sequence, then the total
+  uint32_t* s_mst = s_start + nsq + 1;                    // [nsq] output start of its match
+  uint32_t* s_lit = s_mst + nsq;                          // [nsq] input offset of its literals
+  int32_t* s_mb = reinterpret_cast<int32_t*>(s_lit + nsq);  // [nsq] input base of a resolved match, -1
+  uint16_t* s_dist = reinterpret_cast<uint16_t*>(s_mb + nsq);  // [nsq] match distance
   LZ_STAMP(0);
   // ---- stage the compressed block (16-byte aligned and padded in the device image) ----
   {
@@ -1039,7 +1047,8 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int q = 0; q < 5; ++q) v[u][q] = lit[u] ? in32[(src[u] >> 2) + q] : 0u;
+      for (int q = 0; q < 5; ++q)
+        v[u][q] = !lit[u] ? 0u : keep_in ? reinterpret_cast<const uint32_t*>(s_in)[(src[u] >> 2) + q] : in32[(src[u] >> 2) + q];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = c0 + u * kLtThreads;
@@ -1105,7 +1114,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
         }
         uint32_t b[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) b[i] = sp[i] >= 0 ? (uint32_t)in[sp[i]] : 0u;
+        for (int i = 0; i < 16; ++i) b[i] = sp[i] < 0 ? 0u : keep_in ? (uint32_t)s_in[sp[i]] : (uint32_t)in[sp[i]];
 #pragma unroll
         for (int q = 0; q < 4; ++q) w[q] = b[4 * q] | (b[4 * q + 1] << 8) | (b[4 * q + 2] << 16) | (b[4 * q + 3] << 24);
       }
