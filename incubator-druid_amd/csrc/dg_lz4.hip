@@ -1032,8 +1032,34 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   uint4* dst = reinterpret_cast<uint4*>(job.dst);
   const int nchunks = (total + 15) >> 4;
   bool fail = false;
-  for (int c0 = tid; c0 < nchunks; c0 += 2 * kLtThreads) {
+  // the source of output byte x: its literal position (a literal byte, a resolved match byte, or
+  // hop by hop back to one); -1 = longer chain than the light limit (malformed classification)
+  auto resolve = [&](int x) -> int {
+    const int s = seq_of(x);
+    const int st = (int)s_start[s], ms = (int)s_mst[s];
+    if (x < ms) return (int)s_lit[s] + (x - st);
+    const int dd = s_dist[s], mb = s_mb[s], k = x - ms;
+    if (mb >= 0) return mb + (k < dd ? k : k % dd);
+    const int M = (int)s_start[s + 1] - ms;
+    int y = dd >= M ? x - dd : ms - dd + k % dd;
+    int sy = s;
+#pragma unroll 1
+    for (int hop = 0; hop <= kLtMaxDepth && y >= 0; ++hop) {
+      if (y < (int)s_start[sy] || y >= (int)s_start[sy + 1]) sy = seq_of(y);
+      const int yst = (int)s_start[sy], yms = (int)s_mst[sy];
+      if (y < yms) return (int)s_lit[sy] + (y - yst);
+      const int yd = s_dist[sy], yM = (int)s_start[sy + 1] - yms, yk = y - yms;
+      const int yb = s_mb[sy];
+      if (yb >= 0) return yb + (yk < yd ? yk : yk % yd);
+      y = yd >= yM ? y - yd : yms - yd + yk % yd;
+    }
+    return -1;
+  };
+  uint32_t* dst32 = reinterpret_cast<uint32_t*>(job.dst);
+  const int nsteps = (nchunks + 2 * kLtThreads - 1) / (2 * kLtThreads);
+  for (int it = 0; it < nsteps; ++it) {  // (wave-uniform trip count: the per-byte pass shuffles)
     // two chunks per step: their literal loads are issued together
+    const int c0 = it * 2 * kLtThreads + tid;
     int cs[2], src[2];
     bool lit[2];
     uint32_t v[2][5];
@@ -1051,74 +1077,41 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
         v[u][q] = !lit[u] ? 0u : keep_in ? reinterpret_cast<const uint32_t*>(s_in)[(src[u] >> 2) + q] : in32[(src[u] >> 2) + q];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int c = c0 + u * kLtThreads;
-      if (c >= nchunks) break;
-      const int x0 = c << 4;
+      if (!lit[u]) continue;  // inside one literal run: one 16-byte store
+      const int sh = src[u] & 3;
       uint32_t w[4];
-      if (lit[u]) {  // inside one literal run
-        const int sh = src[u] & 3;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) w[q] = sh ? __builtin_amdgcn_alignbyte(v[u][q + 1], v[u][q], sh) : v[u][q];
-      } else {  // every byte's literal position (LDS only), then the 16 bytes loaded together
-        int sp[16];
-        // the sequence under the cursor, reloaded only at sequence boundaries: literal bytes take
-        // their position arithmetically, match bytes hop (the previous match byte's source sequence
-        // is the first guess for the next one)
-        int s = cs[u];
-        int st = (int)s_start[s], ms = (int)s_mst[s], en = (int)s_start[s + 1], li = (int)s_lit[s], dd = s_dist[s];
-        int mb = s_mb[s];
-        int hs = s;
+      for (int q = 0; q < 4; ++q) w[q] = sh ? __builtin_amdgcn_alignbyte(v[u][q + 1], v[u][q], sh) : v[u][q];
+      dst[c0 + u * kLtThreads] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    // the wave's other chunks, four at a time with one lane per byte: every byte resolves on its own
+    // (no per-byte serial walk in one lane), bytes pack into dwords across lanes
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {  // (unrolled: sp stays in registers)
-          const int xi = x0 + i;
-          sp[i] = -1;
-          if (xi < total) {
-            while (xi >= en) {
-              ++s;
-              st = en;
-              ms = (int)s_mst[s];
-              en = (int)s_start[s + 1];
-              li = (int)s_lit[s];
-              dd = s_dist[s];
-              mb = s_mb[s];
-            }
-            if (xi < ms) {
-              sp[i] = li + (xi - st);
-            } else if (mb >= 0) {
-              const int k = xi - ms;
-              sp[i] = mb + (k < dd ? k : k % dd);
-            } else {
-              const int M = en - ms, k = xi - ms;
-              int y = dd >= M ? xi - dd : ms - dd + k % dd;
-              int sy = hs;
-#pragma unroll 1
-              for (int hop = 0; hop <= kLtMaxDepth && y >= 0; ++hop) {
-                if (y < (int)s_start[sy] || y >= (int)s_start[sy + 1]) sy = seq_of(y);
-                const int yst = (int)s_start[sy], yms = (int)s_mst[sy];
-                if (y < yms) {
-                  sp[i] = (int)s_lit[sy] + (y - yst);
-                  break;
-                }
-                const int yd = s_dist[sy], yM = (int)s_start[sy + 1] - yms, yk = y - yms;
-                const int yb = s_mb[sy];
-                if (yb >= 0) {
-                  sp[i] = yb + (yk < yd ? yk : yk % yd);
-                  break;
-                }
-                y = yd >= yM ? y - yd : yms - yd + yk % yd;
-              }
-              hs = sy;
-              if (sp[i] < 0) fail = true;
-            }
+    for (int u = 0; u < 2; ++u) {
+      const int mine = c0 + u * kLtThreads;
+      uint64_t pend = __ballot(mine < nchunks && !lit[u]);
+      while (pend) {
+        int own[4] = {0, 0, 0, 0}, k = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (pend) {
+            own[q] = __builtin_ctzll(pend);
+            pend &= pend - 1;
+            k = q + 1;
           }
+        const int sub = lane >> 4, bi = lane & 15;
+        const int ol = sub == 0 ? own[0] : sub == 1 ? own[1] : sub == 2 ? own[2] : own[3];
+        const int cc = __shfl(mine, ol, 64);
+        const int x = (cc << 4) + bi;
+        uint32_t b = 0;
+        if (sub < k && x < total) {
+          const int sp = resolve(x);
+          if (sp < 0) fail = true;
+          else b = keep_in ? (uint32_t)s_in[sp] : (uint32_t)in[sp];
         }
-        uint32_t b[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) b[i] = sp[i] < 0 ? 0u : keep_in ? (uint32_t)s_in[sp[i]] : (uint32_t)in[sp[i]];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) w[q] = b[4 * q] | (b[4 * q + 1] << 8) | (b[4 * q + 2] << 16) | (b[4 * q + 3] << 24);
+        const uint32_t b1 = __shfl_down(b, 1, 64), b2 = __shfl_down(b, 2, 64), b3 = __shfl_down(b, 3, 64);
+        if (sub < k && (bi & 3) == 0) dst32[cc * 4 + (bi >> 2)] = b | (b1 << 8) | (b2 << 16) | (b3 << 24);
       }
-      dst[c] = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
   if (fail) atomicOr(err, 1);
