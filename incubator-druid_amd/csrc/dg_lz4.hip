@@ -1034,8 +1034,8 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   bool fail = false;
   // the source of output byte x: its literal position (a literal byte, a resolved match byte, or
   // hop by hop back to one); -1 = longer chain than the light limit (malformed classification)
-  auto resolve = [&](int x) -> int {
-    const int s = seq_of(x);
+  auto resolve = [&](int x, int s) -> int {  // s: a sequence starting at or before x
+    while ((int)s_start[s + 1] <= x) ++s;
     const int st = (int)s_start[s], ms = (int)s_mst[s];
     if (x < ms) return (int)s_lit[s] + (x - st);
     const int dd = s_dist[s], mb = s_mb[s], k = x - ms;
@@ -1102,10 +1102,11 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
         const int sub = lane >> 4, bi = lane & 15;
         const int ol = sub == 0 ? own[0] : sub == 1 ? own[1] : sub == 2 ? own[2] : own[3];
         const int cc = __shfl(mine, ol, 64);
+        const int s0 = __shfl(cs[u], ol, 64);  // the chunk's first sequence
         const int x = (cc << 4) + bi;
         uint32_t b = 0;
         if (sub < k && x < total) {
-          const int sp = resolve(x);
+          const int sp = resolve(x, s0);
           if (sp < 0) fail = true;
           else b = keep_in ? (uint32_t)s_in[sp] : (uint32_t)in[sp];
         }
