@@ -995,6 +995,7 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.dec_len = b.dec_len[k];
   j.wide = b.cp_wide[k];
   j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
+  j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
   return j;
 }
 
@@ -3626,6 +3627,7 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.cp_n.resize(n);
   b.cp_wide.assign(n, 0);
   b.cp_light.assign(n, 0);
+  b.cp_fine.assign(n, 0);
   b.dec_len.resize(n);
   int64_t total = 0;
   for (int i = 0; i < n; ++i) {
@@ -3639,12 +3641,13 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
     std::vector<uint32_t> one;
-    int wide = 0, light = 0;
-    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light);
+    int wide = 0, light = 0, nfine = 0;
+    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine);
     b.cp_wide[i] = (uint8_t)wide;
     b.cp_light[i] = (uint8_t)light;
+    b.cp_fine[i] = nfine;
     b.cp_off[i] = (int64_t)cps.size();
-    b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size();
+    b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size() - nfine;
     b.dec_len[i] = d < 0 ? 0 : d;
     out_lens[i] = d;
     if (d >= 0) cps.insert(cps.end(), one.begin(), one.end());

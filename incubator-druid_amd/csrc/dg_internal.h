@@ -58,13 +58,16 @@ struct Lz4Job {
   int32_t ncp;         // number of checkpoints; < 0: the block failed validation at attach
   int32_t dec_len;     // decoded length found at attach
   int32_t wide;        // checkpoints every 2 * kLzSeqPerCp sequences (decoded by the wide kernel)
-  int32_t light;       // few sequences, short copy chains: decoded by the light kernel (k_lz4_light)
+  int32_t light;       // few sequences, short copy chains: decoded by the light kernel (k_lz4_light);
+                       // > 0: sequences per light checkpoint (cp[ncp .. ncp + nfine) = the light checkpoints)
+  int32_t nfine;       // light checkpoints (one per light-decoder thread)
 };
 
 // Light blocks (literal-heavy: random ids, high-entropy values): at most kLtMaxCps checkpoint
 // intervals and copy chains of at most kLtMaxDepth hops. k_lz4_light decodes them with a small
 // sequence table in LDS (many blocks per CU), resolving every output byte back to its literal.
 constexpr int kLtMaxCps = 256;
+constexpr int kLtThreads = 512;  // light-decoder threads (at most one light checkpoint interval each)
 constexpr int kLtMaxDepth = 16;
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
@@ -93,7 +96,10 @@ struct VsJob {
 // block's checkpoints to *cps and returns the decoded length, or -1 for a malformed block.
 // *wide: the block keeps every other checkpoint (more than kLzMaxCps * kLzSeqPerCp sequences).
 // *light (optional): the block qualifies for the light decoder (kLtMaxCps / kLtMaxDepth).
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr);
+// *light = g > 0 when light: the block's checkpoints are followed by *nfine light checkpoints, one
+// every g sequences (g the fewest sequences per checkpoint that fit the light decoder's threads).
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr,
+                    int* nfine = nullptr);
 
 struct AggPlan {
   int32_t n;
@@ -217,7 +223,8 @@ struct BlockColumn {
   std::vector<int64_t> cp_off;         // LZ4: first checkpoint of block b inside cps
   std::vector<int32_t> cp_n;           // LZ4: checkpoints of block b (-1: malformed block)
   std::vector<uint8_t> cp_wide;        // LZ4: block b keeps a checkpoint every 2 * kLzSeqPerCp sequences
-  std::vector<uint8_t> cp_light;       // LZ4: block b goes to the light decoder
+  std::vector<uint8_t> cp_light;       // LZ4: block b goes to the light decoder (sequences per light checkpoint)
+  std::vector<int32_t> cp_fine;        // LZ4: light checkpoints of block b (after its cp_n checkpoints)
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
   int64_t index_bytes = 0;             // LZ4: bytes of the checkpoint index (read per query)
   DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)

@@ -861,7 +861,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 //   3. output: 16-byte chunks, one per thread per step (coalesced 16-byte stores). A chunk inside one
 //      literal run is five dword loads from the input; otherwise each byte is resolved hop by hop.
 // ------------------------------------------------------------------------------------------------
-constexpr int kLtThreads = 512;
 constexpr int kLtMaxSeq = kLtMaxCps * kLzSeqPerCp;  // 2048
 constexpr int kLtLut = kBlockBytes / 64;
 constexpr int kLtBufWords = (kLz4InCap + 32) / 4;  // staged input (+ zero pad), later the sequence table
@@ -877,15 +876,17 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   __shared__ int s_bad;
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = job.src_len, ncp = job.ncp;
-  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLtMaxCps || job.dec_len > kBlockBytes ||
-      job.dec_len < job.expect_len) {
+  // the light checkpoints: one interval of g sequences per thread
+  const int n = job.src_len, ncp = job.nfine, g = job.light;
+  const uint32_t* cpl = job.cp + job.ncp;
+  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLtThreads || g < 1 || g > kLzSeqPerCp || ncp * g > kLtMaxSeq + g ||
+      job.dec_len > kBlockBytes || job.dec_len < job.expect_len) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
-  // sequence table (sequence i = thread * kLzSeqPerCp + s): right after the staged input when both
-  // fit, so the output reads literals from LDS; otherwise over the input (literals from L2)
-  const int nsq = ncp * kLzSeqPerCp;
+  // sequence table (sequence i = thread * g + s): right after the staged input when both fit, so the
+  // output reads literals from LDS; otherwise over the input (literals from L2)
+  const int nsq = ncp * g;
   const int in_words = ((n + 15) >> 4) * 4 + 4;  // staged input + one zero uint4
 #ifndef DG_LT_NOKEEP
   const bool keep_in = in_words + (nsq + 1) + 3 * nsq + (nsq + 1) / 2 <= kLtBufWords;
@@ -917,12 +918,12 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   int cnt = 0, out_rel = 0;
   bool bad = false;
   if (tid < ncp) {
-    int pos = (int)job.cp[tid];
-    const int end = tid + 1 < ncp ? (int)job.cp[tid + 1] : n;
+    int pos = (int)cpl[tid];
+    const int end = tid + 1 < ncp ? (int)cpl[tid + 1] : n;
 #pragma unroll
     for (int s = 0; s < kLzSeqPerCp; ++s) {
       r_L[s] = r_M[s] = r_off[s] = r_lit[s] = 0;
-      if (pos < end) {
+      if (s < g && pos < end) {
         Tok t;
         if (parse_tok(s_in, n, pos, t)) {
           r_L[s] = t.L;
@@ -937,7 +938,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
         }
       }
     }
-    bad = pos != end || (tid + 1 < ncp && cnt != kLzSeqPerCp);
+    bad = pos != end || (tid + 1 < ncp && cnt != g);
   }
   // ---- 2. block scan of the intervals' output lengths -> sequence table (over the staged input) ----
   int x = out_rel;
@@ -966,7 +967,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
 #pragma unroll
     for (int s = 0; s < kLzSeqPerCp; ++s) {
       if (s < cnt) {
-        const int i = tid * kLzSeqPerCp + s;
+        const int i = tid * g + s;
         s_start[i] = (uint32_t)o;
         s_mst[i] = (uint32_t)(o + r_L[s]);
         s_lit[i] = (uint32_t)r_lit[s];
@@ -979,7 +980,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
         o = e;
       }
     }
-    if (tid == ncp - 1) s_start[tid * kLzSeqPerCp + cnt] = (uint32_t)total;
+    if (tid == ncp - 1) s_start[tid * g + cnt] = (uint32_t)total;
   }
   __syncthreads();
   if (s_bad) {
@@ -1003,7 +1004,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
 #pragma unroll
       for (int s = 0; s < kLzSeqPerCp; ++s) {
         if (!((todo >> s) & 1u)) continue;
-        const int i = tid * kLzSeqPerCp + s;
+        const int i = tid * g + s;
         const int ms = (int)s_mst[i], d = r_off[s], a = ms - d, len = min(r_M[s], d);
         const int t = seq_of(a);
         const int tst = (int)s_start[t], tms = (int)s_mst[t], ten = (int)s_start[t + 1];

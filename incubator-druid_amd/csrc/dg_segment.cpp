@@ -178,9 +178,10 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
   }
 }
 
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light) {
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine) {
   const size_t first = cps->size();
   if (light) *light = 0;
+  if (nfine) *nfine = 0;
   int pos = 0, out = 0;
   int64_t seq = 0;
   auto ext = [&](int* len) {
@@ -201,7 +202,29 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
       cps->resize(first + m);
     }
     if (m > (size_t)kLzMaxCps) return -1;
-    if (light && !*wide && m <= (size_t)kLtMaxCps) *light = lz4_max_depth(in, n, kLtMaxDepth) <= kLtMaxDepth;
+    if (light && !*wide && m <= (size_t)kLtMaxCps && lz4_max_depth(in, n, kLtMaxDepth) <= kLtMaxDepth) {
+      // light checkpoints: every g sequences, the fewest that fit one per light-decoder thread
+      const int g = (int)std::max<int64_t>(1, (seq + kLtThreads - 1) / kLtThreads);
+      if (nfine && g <= kLzSeqPerCp) {
+        int p = 0;
+        for (int64_t k = 0; k < seq; ++k) {
+          if (k % g == 0) {
+            cps->push_back((uint32_t)p);
+            ++*nfine;
+          }
+          const int tok = in[p++];
+          int L = tok >> 4;
+          if (L == 15) for (int b = 255; b == 255;) L += (b = in[p++]);
+          p += L;
+          if (p >= n) break;
+          p += 2;
+          if ((tok & 15) == 15) for (int b = 255; b == 255;) b = in[p++];
+        }
+        *light = g;
+      } else if (!nfine) {
+        *light = 1;
+      }
+    }
     return dec;
   };
   for (;;) {
@@ -260,6 +283,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->cp_n.assign(blocks.n, -1);
     col->cp_wide.assign(blocks.n, 0);
     col->cp_light.assign(blocks.n, 0);
+    col->cp_fine.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
     const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -268,12 +292,13 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int t = 0; t < nt; ++t)
       th.emplace_back([&, t] {
         for (int32_t b = t; b < blocks.n; b += nt) {
-          int wide = 0, light = 0;
-          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light);
+          int wide = 0, light = 0, nfine = 0;
+          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine);
           col->cp_wide[b] = (uint8_t)wide;
           col->cp_light[b] = (uint8_t)light;
+          col->cp_fine[b] = nfine;
           col->dec_len[b] = d;
-          col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size();
+          col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size() - nfine;
         }
       });
     for (auto& x : th) x.join();
