@@ -39,7 +39,10 @@ static_assert(kShortLit <= 4, "Tok::lv holds four literal bytes");
 constexpr int kLongFill = 48;                  // matches above this are filled cooperatively
 constexpr int kMaxJobs = 2048;
 constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
-constexpr int kJumpBatch = 4;                 // steps of a jump sweep whose reads are issued together
+#ifndef DG_LZ_JUMP_BATCH
+#define DG_LZ_JUMP_BATCH 4
+#endif
+constexpr int kJumpBatch = DG_LZ_JUMP_BATCH;  // steps of a jump sweep whose reads are issued together
 constexpr int kMaxRounds = 20;                 // > log2(65536) + 1: pointer jumping always converges before
 constexpr int kClass = 8;                      // the value width whose distance-8 copy chains are scanned
 static_assert(kLz4InCap + 32 <= kBlockBytes * 2, "staged input must fit in the E array");
