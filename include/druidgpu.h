@@ -70,8 +70,8 @@ extern "C" {
 #define DG_COL_LONG 1
 #define DG_COL_FLOAT 2
 #define DG_COL_DOUBLE 3
-#define DG_COL_STRING 4      /* single- or multi-value (V3 / UNCOMPRESSED_MULTI_VALUE: bitmap filters only,
-                                grouping on it -> DG_ERR_UNSUPPORTED) */
+#define DG_COL_STRING 4      /* single- or multi-value (V3, legacy compressed or uncompressed multi-value:
+                                filters, topN per value and groupBy explode all run on it) */
 #define DG_COL_UNSUPPORTED 5 /* complex / legacy non-V3 compressed multi-value / unsupported codec */
 
 /* aggregator kinds (query/aggregation/...AggregatorFactory.java) */
@@ -203,6 +203,14 @@ int dg_context_create(int device, dg_context** out);
 void dg_context_release(dg_context* ctx);
 /* Bind the context's work to an existing HIP stream (e.g. torch's current stream); NULL resets. */
 int dg_context_set_stream(dg_context* ctx, void* hip_stream);
+/* Resource limits of the context's calls (the processing-buffer budget a historical configures,
+ * DruidProcessingConfig / GroupByQueryConfig; exceeding one is answered DG_ERR_UNSUPPORTED before any
+ * buffer is sized, so the Java factory keeps its CPU engine). value <= 0 restores the default.
+ *   DG_LIMIT_GROUP_ELEMENTS: sort elements of one groupBy call (rows, or for multi-value dimensions
+ *   rows x the product of their value-list lengths, GroupByQueryEngineV2.java:480-540); never more
+ *   than 2^32 - 64 (element indices are 32-bit). */
+#define DG_LIMIT_GROUP_ELEMENTS 1
+int dg_context_set_limit(dg_context* ctx, int32_t which, int64_t value);
 
 /* ---- segments ---- */
 int dg_segment_attach(dg_context* ctx, const char* segment_dir, dg_segment** out);

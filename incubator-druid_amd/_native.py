@@ -22,6 +22,7 @@ ERRORS = {1: "DG_ERR_FORMAT", 2: "DG_ERR_UNSUPPORTED", 3: "DG_ERR_OOM", 4: "DG_E
 COL_MISSING, COL_LONG, COL_FLOAT, COL_DOUBLE, COL_STRING, COL_UNSUPPORTED = range(6)
 F_AND, F_OR, F_NOT, F_SELECTOR, F_IN, F_BOUND = 1, 2, 3, 4, 5, 6
 ORDER = {"lexicographic": 0, "numeric": 1}
+LIMIT_GROUP_ELEMENTS = 1
 
 
 class DruidGpuError(RuntimeError):
@@ -126,7 +127,7 @@ EXPORTS = [
     "dg_result_groups", "dg_result_fetch_groups", "dg_result_fetch_rows", "dg_result_dim_cardinality",
     "dg_result_dim_dictionary", "dg_result_release", "dg_keyspace_bits", "dg_result_export", "dg_keys_partition",
     "dg_merge", "dg_records_pack", "dg_debug_lz4_decode", "dg_result_limit",
-    "dg_segment_from_rows",
+    "dg_segment_from_rows", "dg_context_set_limit",
 ]
 
 _lib = None
@@ -157,6 +158,7 @@ def lib():
         "dg_context_create": (ctypes.c_int, [ctypes.c_int, P(vp)]),
         "dg_context_release": (None, [vp]),
         "dg_context_set_stream": (ctypes.c_int, [vp, vp]),
+        "dg_context_set_limit": (ctypes.c_int, [vp, i32, i64]),
         "dg_segment_attach": (ctypes.c_int, [vp, cp, P(vp)]),
         "dg_segment_release": (None, [vp]),
         "dg_segment_from_rows": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, i32, P(vp)]),

@@ -160,10 +160,12 @@ struct CallScratch {
   Pool dev;
   Pool host;
   UpPool up;
-  // per-call device error word (bit 0: corrupt LZ4 block, bit 1: corrupt Roaring bitmap), read once
+  // per-call device error word (bit 0: corrupt LZ4 block, bit 1: corrupt Roaring bitmap, bit 2:
+  // corrupt multi-value row lists), read once
   // at the call's final synchronisation instead of after every kernel
   int32_t* d_err = nullptr;
   int32_t* h_err = nullptr;
+  Context* ctx = nullptr;
   CallScratch() { host.pinned = true; }
   void reset() {
     dev.reset();
@@ -181,6 +183,7 @@ static CallScratch* scratch_of(Context* ctx) {
   auto it = s.find(ctx);
   if (it != s.end()) return it->second;
   CallScratch* c = new CallScratch();
+  c->ctx = ctx;
   s[ctx] = c;
   return c;
 }
@@ -225,7 +228,9 @@ static int finish_call(CallScratch* cs, hipStream_t st) {
   DG_HIP(hipStreamSynchronize(st));
   DG_HIP(hipGetLastError());
   if (cs->d_err && *cs->h_err)
-    return set_error(DG_ERR_FORMAT, (*cs->h_err & 1) ? "corrupt LZ4 block" : "corrupt Roaring bitmap");
+    return set_error(DG_ERR_FORMAT, (*cs->h_err & 1)   ? "corrupt LZ4 block"
+                                    : (*cs->h_err & 4) ? "corrupt multi-value row lists"
+                                                       : "corrupt Roaring bitmap");
   return DG_OK;
 }
 
@@ -379,6 +384,7 @@ struct DecodeBatch {
   std::vector<Lz4Job> jobs;
   std::vector<LzfJob> lzf_jobs;  // LZF blocks, decoded one wave per block
   std::vector<VsJob> expands;  // DELTA / TABLE blocks, expanded after the LZ4 decodes
+  std::vector<MvCheck> mv_checks;  // multi-value row lists, validated after the decodes
   int32_t expand_rows = 0;     // largest block of `expands` (grid width)
   int64_t* last_expanded = nullptr;
   uint8_t* last_slots = nullptr;  // decode slots of the last viewed LZ4 / LZF column
@@ -387,6 +393,7 @@ struct DecodeBatch {
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
 static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st);
 static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr);
+static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof);
 
 // ------------------------------------------------------------------------------------------------
 // numeric post-filters: Java's parsing of the filter's strings (host side, once per call)
@@ -1014,7 +1021,16 @@ static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColVie
 static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st) {
   int rc = block_view(c->data, VIEW_IDS, c->name.c_str(), cs, db, vals, st);
   if (rc) return rc;
-  return block_view(c->mv_off, VIEW_IDS, c->name.c_str(), cs, db, offs, st);
+  rc = block_view(c->mv_off, VIEW_IDS, c->name.c_str(), cs, db, offs, st);
+  if (rc) return rc;
+  MvCheck m;
+  m.vals = *vals;
+  m.offs = *offs;
+  m.rows = (int64_t)c->mv_off.total - 1;
+  m.nvals = c->data.total;
+  m.card = (int64_t)c->dict.size();
+  db->mv_checks.push_back(m);
+  return DG_OK;
 }
 
 static int block_view(const BlockColumn& b, int kind, const char* name, CallScratch* cs, DecodeBatch* db, ColView* v,
@@ -1111,7 +1127,29 @@ static int run_lzf(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
   return DG_OK;
 }
 
+static int run_mv_checks(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
+  if (db->mv_checks.empty()) return DG_OK;
+  const int n = (int)db->mv_checks.size();
+  MvCheck* d;
+  MvCheck* h = up_take<MvCheck>(cs, n, &d, st);
+  int32_t* d_err = call_err(cs, st);
+  if (!h || !d_err) return set_error(DG_ERR_OOM, "multi-value checks");
+  memcpy(h, db->mv_checks.data(), sizeof(MvCheck) * n);
+  DG_FLUSH(cs, st);
+  launch_mv_check(d, n, d_err, st);
+  db->mv_checks.clear();
+  // wait for the verdict before any kernel follows the row lists (an offset past the values would
+  // send the consumers' loads out of their buffers); multi-value scans are rare, one sync is cheap
+  return finish_call(cs, st);
+}
+
 static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof) {
+  int rcl = run_decodes_only(cs, db, st, d_prof);
+  if (rcl) return rcl;
+  return run_mv_checks(cs, db, st);
+}
+
+static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof) {
   int rcl = run_lzf(cs, db, st);
   if (rcl) return rcl;
   if (db->jobs.empty()) return run_expands(cs, db, st);
@@ -1390,6 +1428,18 @@ int dg_context_set_stream(dg_context* c, void* stream) {
   return DG_OK;
 }
 
+int dg_context_set_limit(dg_context* c, int32_t which, int64_t value) {
+  Context* ctx = reinterpret_cast<Context*>(c);
+  if (!ctx) return set_error(DG_ERR_ARG, "null context");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  switch (which) {
+    case DG_LIMIT_GROUP_ELEMENTS:
+      ctx->max_elements = value <= 0 ? ~0ull : (uint64_t)value;
+      return DG_OK;
+    default: return set_error(DG_ERR_ARG, "unknown limit %d", which);
+  }
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------------------------------------
@@ -1613,17 +1663,24 @@ static int upload_gb_jobs(CallScratch* cs, std::vector<GbJob>& gj, const std::ve
 
 // elements of a keygen over rows with multi-value dimensions (one per grouping), counted on the
 // device before the sort buffers are sized
-static int count_elements(CallScratch* cs, GbJob* d_jobs, int32_t* d_tile, int ntiles, int64_t* total, hipStream_t st) {
+// (counted in 64 bits: rows x the product of their value-list lengths can pass 2^32, and element
+// indices / sort offsets are 32-bit, so such a call is refused before anything is sized from it)
+static int count_elements(CallScratch* cs, GbJob* d_jobs, int32_t* d_tile, int ntiles, int64_t* total,
+                          hipStream_t st) {
   const int nt = std::max(ntiles, 1);
   uint32_t* d_cnt = dev_take<uint32_t>(cs, (size_t)nt + 4);
-  uint32_t* h_tot = host_take<uint32_t>(cs, 1);
-  if (!d_cnt || !h_tot) return set_error(DG_ERR_OOM, "element count");
+  unsigned long long* d_tot = dev_take<unsigned long long>(cs, 1);
+  unsigned long long* h_tot = host_take<unsigned long long>(cs, 1);
+  if (!d_cnt || !d_tot || !h_tot) return set_error(DG_ERR_OOM, "element count");
   DG_FLUSH(cs, st);
-  launch_gb_count(d_jobs, d_tile, ntiles, d_cnt, d_cnt + nt, true, st);
-  DG_HIP(hipMemcpyAsync(h_tot, d_cnt + nt, 4, hipMemcpyDeviceToHost, st));
+  launch_gb_count_total(d_jobs, d_tile, ntiles, d_cnt, d_tot, st);
+  DG_HIP(hipMemcpyAsync(h_tot, d_tot, 8, hipMemcpyDeviceToHost, st));
   int rc = finish_call(cs, st);
   if (rc) return rc;
-  *total = *h_tot;
+  const unsigned long long cap = std::min<unsigned long long>(cs->ctx->max_elements, (1ull << 32) - 64);
+  if (*h_tot > cap)
+    return set_error(DG_ERR_UNSUPPORTED, "multi-value grouping explodes into %llu elements (limit %llu)", *h_tot, cap);
+  *total = (int64_t)*h_tot;
   return DG_OK;
 }
 

@@ -297,6 +297,8 @@ struct Context {
   DevBuf scratch[6];
   DevBuf pinned_dummy;
   hipEvent_t ev[8] = {};
+  // dg_context_set_limit(DG_LIMIT_GROUP_ELEMENTS): most sort elements one groupBy call may build
+  uint64_t max_elements = ~0ull;
   std::vector<std::shared_ptr<MergedDict>> dict_cache;  // most recent last
   // device blocks of groupBy results: live (size by pointer) and released for reuse
   std::map<void*, size_t> block_size;
@@ -352,6 +354,15 @@ void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
+// one multi-value dimension's decoded row lists, validated before use (bit 2 of the error word)
+struct MvCheck {
+  ColView vals;
+  ColView offs;
+  int64_t rows;
+  int64_t nvals;  // values stored (the offsets may not pass it)
+  int64_t card;   // dictionary size (every value id must be below it)
+};
+void launch_mv_check(const MvCheck* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 // VSizeLongSerde.getSerializedSize (VSizeLongSerde.java:61-65)
 inline int64_t vsize_serialized(int bits, int64_t n) { return (bits * n + 7) / 8 + 4; }
 // Concise words [off, off + len) whose first word starts at row row0 (null: 0), OR-ed into sets[target]
@@ -460,6 +471,9 @@ inline int sort_tiles(int64_t n) { return (int)std::max<int64_t>(1, (n + kSortTi
 // selected rows (groupings of rows with multi-value dimensions) per keygen tile, and their total
 void launch_gb_count(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, uint32_t* tile_cnt, uint32_t* total,
                      bool multi, hipStream_t s);
+// multi-value element count: per-tile counts (0xFFFFFFFF = saturated) and their 64-bit total
+void launch_gb_count_total(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, uint32_t* tile_cnt,
+                           unsigned long long* total, hipStream_t s);
 void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
                       hipStream_t s, bool multi = false);
 // stable LSD radix sort of sb->keys/refs[cur] on key bits [0, key_bits)

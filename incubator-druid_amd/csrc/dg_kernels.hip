@@ -1363,6 +1363,30 @@ void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32
 }
 
 // ------------------------------------------------------------------------------------------------
+// Multi-value row lists, checked once decoded (the reference would fail on them with an
+// IndexOutOfBounds from SliceIndexedInts / the dictionary): offsets[0] == 0, non-decreasing,
+// offsets[rows] <= values, and every value id < the dictionary's cardinality. A bad list sets bit 2
+// of the call's error word (DG_ERR_FORMAT at the call's synchronisation) before any kernel reads it.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mv_check(const MvCheck* __restrict__ jobs, int32_t* __restrict__ err) {
+  const MvCheck j = jobs[blockIdx.y];
+  bool bad = false;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < j.rows; r += stride) {
+    const uint32_t a = load_id(j.offs, r), b = load_id(j.offs, r + 1);
+    bad |= b < a || (r == 0 && a != 0) || (r + 1 == j.rows && (int64_t)b > j.nvals);
+  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < j.nvals; i += stride)
+    bad |= (int64_t)load_id(j.vals, i) >= (int64_t)j.card;
+  if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(err, 4);
+}
+
+void launch_mv_check(const MvCheck* d_jobs, int njobs, int32_t* d_err, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(k_mv_check, dim3(256, (unsigned)njobs), dim3(256), 0, s, d_jobs, d_err);
+}
+
+// ------------------------------------------------------------------------------------------------
 // LZF blocks (CompressionStrategy.LZF, id 0x00 / LZF_VERSION columns): compress-lzf 1.0.4's chunk
 // stream ("ZV" + type 0 raw | type 1 liblzf, ChunkDecoder.decodeChunk). One wave per block: the
 // compressed block is staged into LDS with coalesced dword loads, the wave walks the tokens in

@@ -483,15 +483,36 @@ int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
   return DG_OK;
 }
 
+// CompressedVSizeColumnarIntsSupplier.fromByteBuffer (data/CompressedVSizeColumnarIntsSupplier.java:
+// 143-168): [0x02][u8 numBytes][i32 total][i32 sizePer][u8 codec][GenericIndexed blocks], values
+// little-endian numBytes wide inside a block (:254-353)
+static int parse_vsize_ints(Context* ctx, BlockColumn* col, Slice* s, const char* name, const char* what) {
+  if (s->left() < 11 || s->p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: bad %s", name, what);
+  col->width = s->p[1];
+  col->total = be32(s->p + 2);
+  col->size_per = be32(s->p + 6);
+  col->codec = s->p[10];
+  col->log2_per = log2i(col->size_per);
+  s->p += 11;
+  if (col->width < 1 || col->width > 4 || col->log2_per < 0 || col->total < 0 ||
+      (int64_t)col->size_per * col->width > kBlockBytes)
+    return set_error(DG_ERR_FORMAT, "%s: bad %s header", name, what);
+  GI blocks;
+  if (!gi_read(*s, &blocks)) return set_error(DG_ERR_FORMAT, "%s: bad %s blocks", name, what);
+  if ((int64_t)blocks.n * col->size_per < col->total) return set_error(DG_ERR_FORMAT, "%s: too few %s blocks", name, what);
+  return upload_blocks(ctx, col, blocks);
+}
+
 // Multi-value id parts (DictionaryEncodedColumnPartSerde.readMultiValuedColumn, :183-217), uploaded as
-// two block columns: mv_off (rows + 1 value offsets, 4-byte little-endian ints) and data (the value
+// two block columns: mv_off (rows + 1 value offsets, little-endian ints) and data (the value
 // ids). UNCOMPRESSED_MULTI_VALUE = VSizeColumnarMultiInts [0x01][numBytes][i32 size][payload: i32
 // count, count big-endian end byte offsets, big-endian numBytes values] (VSizeColumnarMultiInts.
 // readFromByteBuffer / get(index)): the offsets are converted at attach, the values read in place;
 // COMPRESSED + MULTI_VALUE_V3 = [0x03][CompressedColumnarIntsSupplier offsets: 0x02, i32 total,
 // i32 sizePer, u8 codec, GI][CompressedVSizeColumnarIntsSupplier values: 0x02, u8 numBytes, i32,
-// i32, u8 codec, GI] (V3CompressedVSizeColumnarMultiIntsSupplier.fromByteBuffer).
-static int parse_multi_value_ids(Context* ctx, Column* c, Slice* s, int version) {
+// i32, u8 codec, GI] (V3CompressedVSizeColumnarMultiIntsSupplier.fromByteBuffer); COMPRESSED +
+// MULTI_VALUE = the legacy form, both parts CompressedVSizeColumnarInts (offsets 1-4 bytes wide).
+static int parse_multi_value_ids(Context* ctx, Column* c, Slice* s, int version, bool legacy) {
   BlockColumn& off = c->mv_off;
   BlockColumn& val = c->data;
   if (version == 1) {
@@ -528,6 +549,17 @@ static int parse_multi_value_ids(Context* ctx, Column* c, Slice* s, int version)
     s->p += 6 + size;
     return DG_OK;
   }
+  if (legacy) {
+    // COMPRESSED + MULTI_VALUE (no V3 flag): CompressedVSizeColumnarMultiIntsSupplier.fromByteBuffer
+    // (:77-93) = [0x02][offsets: CompressedVSizeColumnarInts, numBytes for the values count][values:
+    // CompressedVSizeColumnarInts]; the offsets' width comes from their own header (1-4 bytes)
+    if (s->left() < 1 || s->p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: Unknown version[%d]", c->name.c_str(), s->left() ? s->p[0] : -1);
+    s->p += 1;
+    int rc = parse_vsize_ints(ctx, &off, s, c->name.c_str(), "multi-value offsets");
+    if (rc) return rc;
+    if (off.total < 1) return set_error(DG_ERR_FORMAT, "%s: bad multi-value offsets header", c->name.c_str());
+    return parse_vsize_ints(ctx, &val, s, c->name.c_str(), "multi-value values");
+  }
   if (s->left() < 1 + 10 || s->p[0] != 0x03 || s->p[1] != 0x02)
     return set_error(DG_ERR_FORMAT, "%s: bad V3 multi-value ids", c->name.c_str());
   off.total = be32(s->p + 2);
@@ -542,18 +574,7 @@ static int parse_multi_value_ids(Context* ctx, Column* c, Slice* s, int version)
   if (!gi_read(*s, &offsets)) return set_error(DG_ERR_FORMAT, "%s: bad multi-value offsets", c->name.c_str());
   int rc = upload_blocks(ctx, &off, offsets);
   if (rc) return rc;
-  if (s->left() < 11 || s->p[0] != 0x02) return set_error(DG_ERR_FORMAT, "%s: bad multi-value values", c->name.c_str());
-  val.width = s->p[1];
-  val.total = be32(s->p + 2);
-  val.size_per = be32(s->p + 6);
-  val.codec = s->p[10];
-  val.log2_per = log2i(val.size_per);
-  s->p += 11;
-  if (val.width < 1 || val.width > 4 || val.log2_per < 0)
-    return set_error(DG_ERR_FORMAT, "%s: bad multi-value values header", c->name.c_str());
-  GI values;
-  if (!gi_read(*s, &values)) return set_error(DG_ERR_FORMAT, "%s: bad multi-value value blocks", c->name.c_str());
-  return upload_blocks(ctx, &val, values);
+  return parse_vsize_ints(ctx, &val, s, c->name.c_str(), "multi-value values");
 }
 
 int parse_string(Context* ctx, Column* c, Slice s) {
@@ -568,8 +589,6 @@ int parse_string(Context* ctx, Column* c, Slice s) {
     flags = 1;
   }
   c->multi_value = (flags & 3) != 0;
-  if (c->multi_value && version == 2 && !(flags & 2))
-    return set_error(DG_ERR_UNSUPPORTED, "%s: legacy compressed multi-value ids", c->name.c_str());
   GI dict;
   if (!gi_read(s, &dict)) return set_error(DG_ERR_FORMAT, "%s: bad dictionary", c->name.c_str());
   c->dict.resize(dict.n);
@@ -586,7 +605,7 @@ int parse_string(Context* ctx, Column* c, Slice s) {
   BlockColumn& col = c->data;
   if (c->multi_value) {
     // row value lists: filters run on the bitmap index, groupBy explodes the lists (dg_sort.hip)
-    int rc = parse_multi_value_ids(ctx, c, &s, version);
+    int rc = parse_multi_value_ids(ctx, c, &s, version, version == 2 && !(flags & 2));
     if (rc) return rc;
   } else if (version == 0 || version == 3) {
     // UNCOMPRESSED_SINGLE_VALUE / UNCOMPRESSED_WITH_FLAGS: VSizeColumnarInts.readFromByteBuffer

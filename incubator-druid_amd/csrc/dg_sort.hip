@@ -135,14 +135,17 @@ __device__ __forceinline__ uint64_t gb_key(const GbJob& j, int64_t r, int64_t bu
 // (GroupByQueryEngineV2.HashAggregateIterator.aggregateMultiValueDims :480-540,
 // StringGroupByColumnSelectorStrategy :47-57, :94-141). Row r's list of dimension d is
 // dims[d][moff[d][r] .. moff[d][r + 1]).
+// The product is formed in 64 bits and saturates at 0xFFFFFFFF: a row (or tile) that reaches it
+// makes the element total >= 2^32, which the host rejects before sizing the sort.
 __device__ __forceinline__ uint32_t gb_fanout(const GbJob& j, int64_t r) {
-  uint32_t n = 1;
+  uint64_t n = 1;
   for (int d = 0; d < j.ndims; ++d)
     if (j.moff[d].kind != VIEW_ABSENT) {
       const uint32_t a = load_id(j.moff[d], r), b = load_id(j.moff[d], r + 1);
-      n *= b > a ? b - a : (j.skip_empty ? 0u : 1u);
+      n *= b > a ? (uint64_t)(b - a) : (j.skip_empty ? 0ull : 1ull);
+      n = n > 0xFFFFFFFFull ? 0xFFFFFFFFull : n;
     }
-  return n;
+  return (uint32_t)n;
 }
 
 // key of grouping c (0 <= c < gb_fanout) of row r
@@ -174,13 +177,40 @@ __global__ __launch_bounds__(256) void k_gb_count(const GbJob* __restrict__ jobs
   const GbJob& j = jobs[tile_job[blockIdx.x]];
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
   const int64_t r1 = min((int64_t)j.nrows, r0 + kTileRows);
-  uint32_t c = 0;
+  uint64_t c = 0;
   for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
     int64_t b;
     if (gb_select(j, r, &b)) c += MULTI ? gb_fanout(j, r) : 1u;
   }
-  const uint32_t t = block_sum_u32<256>(c, s_tmp);
-  if (threadIdx.x == 0) cnt[blockIdx.x] = t;
+  // per-thread sums saturate (8 rows each), the tile sum too: a saturated tile means >= 2^32 elements
+  const uint32_t t = block_sum_u32<256>((uint32_t)min<uint64_t>(c, 0xFFFFFFull), s_tmp);
+  const bool sat = __syncthreads_or(c > 0xFFFFFFull);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = sat ? 0xFFFFFFFFu : t;
+}
+
+// total of n u32 counts in 64 bits (the element count of a multi-value keygen, checked against 2^32)
+__global__ __launch_bounds__(1024) void k_sum_u64(const uint32_t* __restrict__ a, int n, unsigned long long* __restrict__ total) {
+  __shared__ unsigned long long s[16];
+  unsigned long long c = 0;
+  for (int i = threadIdx.x; i < n; i += 1024) c += a[i];
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 16; ++w) t += s[w];
+    *total = t;
+  }
+}
+
+void launch_gb_count_total(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, uint32_t* tile_cnt,
+                           unsigned long long* total, hipStream_t s) {
+  if (ntiles <= 0) {
+    (void)hipMemsetAsync(total, 0, 8, s);
+    return;
+  }
+  hipLaunchKernelGGL(k_gb_count<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, tile_cnt);
+  hipLaunchKernelGGL(k_sum_u64, dim3(1), dim3(1024), 0, s, tile_cnt, ntiles, total);
 }
 
 // element of the sort: packed = one word [key | row ref] (ref in the low sb->ref_bits bits, so equal

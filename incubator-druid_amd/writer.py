@@ -273,9 +273,10 @@ def numeric_column_part(values: np.ndarray, kind: str, compression: str, lz4_mod
     return header + _blocks_generic_indexed(_compress_blocks(raw, size_per * width, compression, lz4_mode))
 
 
-def ids_part(ids: np.ndarray, cardinality: int, compression: str, lz4_mode: str) -> bytes:
-    """CompressedVSizeColumnarIntsSerializer (little-endian values, numBytes from cardinality)."""
-    nb = num_bytes_for_max(cardinality)
+def ids_part(ids: np.ndarray, cardinality: int, compression: str, lz4_mode: str, num_bytes: Optional[int] = None) -> bytes:
+    """CompressedVSizeColumnarIntsSerializer (little-endian values, numBytes from cardinality; num_bytes
+    forces a wider id, e.g. the 4-byte form CompressedVSizeColumnarIntsSupplier reads as full ints)."""
+    nb = num_bytes or num_bytes_for_max(cardinality)
     size_per = max_ints_in_buffer_for_bytes(nb)
     ids32 = np.ascontiguousarray(ids, dtype="<u4")
     if nb == 4:
@@ -288,11 +289,11 @@ def ids_part(ids: np.ndarray, cardinality: int, compression: str, lz4_mode: str)
     return header + _blocks_generic_indexed(_compress_blocks(raw, size_per * nb, comp, lz4_mode))
 
 
-def vsize_ids_part(ids: np.ndarray, cardinality: int) -> bytes:
+def vsize_ids_part(ids: np.ndarray, cardinality: int, num_bytes: Optional[int] = None) -> bytes:
     """VSizeColumnarIntsSerializer (data/VSizeColumnarIntsSerializer.java:40-96): header
     [0x00][numBytes][i32 size], then each id as its low numBytes bytes big-endian, then
     4 - numBytes zero bytes so the reader's getInt never runs off the end."""
-    nb = num_bytes_for_max(cardinality)
+    nb = num_bytes or num_bytes_for_max(cardinality)
     be = np.ascontiguousarray(ids, dtype=">u4").view(np.uint8).reshape(-1, 4)[:, 4 - nb:].tobytes()
     payload = be + bytes(4 - nb)
     return struct.pack(">BBi", 0x00, nb, len(payload)) + payload
@@ -372,7 +373,7 @@ def roaring_bitmaps(ids: np.ndarray, cardinality: int) -> List[bytes]:
 
 
 def string_column_part(dictionary: List[Optional[str]], ids: np.ndarray, bitmap: str,
-                       compression: str, lz4_mode: str) -> bytes:
+                       compression: str, lz4_mode: str, num_bytes: Optional[int] = None) -> bytes:
     card = len(dictionary)
     dict_vals = [None if (v is None or v == "") else v.encode("utf-8") for v in dictionary]
     # null / "" are both stored as a zero-length value (NullHandling.replaceWithDefault)
@@ -383,11 +384,11 @@ def string_column_part(dictionary: List[Optional[str]], ids: np.ndarray, bitmap:
         # DictionaryEncodedColumnPartSerde.java:191-217)
         out = bytes([0x00])
         out += generic_indexed(dict_vals, sorted_flag=True)
-        out += vsize_ids_part(ids, card)
+        out += vsize_ids_part(ids, card, num_bytes)
     else:
         out = bytes([0x02]) + struct.pack(">i", 0)  # COMPRESSED, flags = 0 (single-value, bitmaps)
         out += generic_indexed(dict_vals, sorted_flag=True)
-        out += ids_part(ids, card, compression, lz4_mode)
+        out += ids_part(ids, card, compression, lz4_mode, num_bytes)
     if bitmap == "concise":
         bms = concise_bitmaps(ids, card)
     else:
@@ -407,7 +408,7 @@ def encode_multi_strings(rows: Sequence[Sequence[Optional[str]]]) -> Tuple[List[
 
 
 def multi_string_column_part(dictionary: List[Optional[str]], rows: Sequence[np.ndarray], bitmap: str,
-                             compression: str, lz4_mode: str) -> bytes:
+                             compression: str, lz4_mode: str, legacy: bool = False) -> bytes:
     """Multi-value dictionary-encoded column (DictionaryEncodedColumnPartSerde.java:183-217):
     compressed = version COMPRESSED + MULTI_VALUE_V3 flag, ids as V3CompressedVSizeColumnarMultiInts
     ([0x03][CompressedColumnarInts row start offsets + end][CompressedVSizeColumnarInts values],
@@ -420,7 +421,13 @@ def multi_string_column_part(dictionary: List[Optional[str]], rows: Sequence[np.
     nb = num_bytes_for_max(card)
     lens = np.array([len(r) for r in rows], dtype=np.int64)
     flat = np.concatenate([np.asarray(r, dtype=np.int32) for r in rows]) if len(rows) else np.zeros(0, np.int32)
-    if compression in ("uncompressed", "none"):
+    if legacy:  # blocks of the column's compression (NONE has no block form: UNCOMPRESSED blocks)
+        bc = "uncompressed" if compression == "none" else compression
+        out = bytes([0x02]) + struct.pack(">i", 0x1) + generic_indexed(dict_vals, sorted_flag=True)
+        offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        total = int(offsets[-1])
+        out += bytes([0x02]) + ids_part(offsets, total, bc, lz4_mode) + ids_part(flat, card, bc, lz4_mode)
+    elif compression in ("uncompressed", "none"):
         out = bytes([0x01]) + generic_indexed(dict_vals, sorted_flag=True)
         ends = np.cumsum(lens * nb).astype(">i4")
         values = np.ascontiguousarray(flat, dtype=">u4").view(np.uint8).reshape(-1, 4)[:, 4 - nb:].tobytes()
@@ -504,10 +511,13 @@ class SegmentSpec:
 
 
 def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", compression: str = "lz4",
-                  dim_compression: Optional[str] = None, lz4_mode: str = "hc", long_encoding: str = "longs") -> str:
+                  dim_compression: Optional[str] = None, lz4_mode: str = "hc", long_encoding: str = "longs",
+                  id_bytes: Optional[int] = None, legacy_multi_value: bool = False) -> str:
     """Write a v9 segment directory. Rows must already be in segment order (time-sorted).
     long_encoding: IndexSpec.longEncoding, "longs" (default) or "auto" (DELTA / TABLE / LONGS per column,
-    __time included: IndexMergerV9 serializes it with the same long encoding)."""
+    __time included: IndexMergerV9 serializes it with the same long encoding).
+    id_bytes: width of single-value dictionary ids (default: numBytes for the cardinality).
+    legacy_multi_value: compressed multi-value dimensions in the pre-V3 CompressedVSizeColumnarMultiInts form."""
     os.makedirs(out_dir, exist_ok=True)
     n = len(spec.timestamps)
     ts = np.asarray(spec.timestamps, dtype=np.int64)
@@ -525,13 +535,14 @@ def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", comp
             part = {"type": "stringDictionary", "bitmapSerdeFactory": _bitmap_json(bitmap),
                     "byteOrder": "LITTLE_ENDIAN"}
             files[name] = _descriptor("STRING", part, multi=True) + multi_string_column_part(
-                dictionary, [np.asarray(r, dtype=np.int32) for r in ids], bitmap, dim_comp, lz4_mode)
+                dictionary, [np.asarray(r, dtype=np.int32) for r in ids], bitmap, dim_comp, lz4_mode, legacy_multi_value)
             continue
         ids = np.asarray(ids, dtype=np.int32)
         if len(ids) != n:
             raise ValueError(f"dimension {name} has {len(ids)} rows, expected {n}")
         part = {"type": "stringDictionary", "bitmapSerdeFactory": _bitmap_json(bitmap), "byteOrder": "LITTLE_ENDIAN"}
-        files[name] = _descriptor("STRING", part) + string_column_part(dictionary, ids, bitmap, dim_comp, lz4_mode)
+        files[name] = _descriptor("STRING", part) + string_column_part(dictionary, ids, bitmap, dim_comp, lz4_mode,
+                                                                       id_bytes)
     for name, (kind, vals) in spec.metrics.items():
         vals = np.asarray(vals)
         if len(vals) != n:

@@ -305,6 +305,7 @@ typedef struct {
    * = mv_count rows, mv_ends (big-endian end byte offsets), mv_vals (big-endian values) */
   int32_t mv_total, mv_size_per;
   int mv_compression;
+  int mv_num_bytes; /* offsets' width: 4 for V3 (CompressedColumnarInts), numBytes of the legacy form */
   gindexed mv_blocks;
   int32_t mv_count;
   const uint8_t* mv_ends;
@@ -459,6 +460,25 @@ static int parse_string(ocol* c, const uint8_t* p) {
       c->mv_size_per = be32(q + 6);
       c->mv_compression = q[10];
       q += 11;
+      c->mv_num_bytes = 4;
+      if (gi_read(&q, c->end, &c->mv_blocks)) return -1;
+      if (q[0] != 0x02) return -1;
+      c->num_bytes = q[1];
+      c->total = be32(q + 2);
+      c->size_per = be32(q + 6);
+      c->compression = q[10];
+      q += 11;
+      if (gi_read(&q, c->end, &c->blocks)) return -1;
+    } else if (version == 2 && (flags & 1)) {
+      /* CompressedVSizeColumnarMultiIntsSupplier.fromByteBuffer (:77-93): [0x02][offsets:
+       * CompressedVSizeColumnarInts][values: CompressedVSizeColumnarInts] */
+      if (q[0] != 0x02 || q[1] != 0x02) return -1;
+      c->mv_num_bytes = q[2];
+      c->mv_total = be32(q + 3);
+      c->mv_size_per = be32(q + 7);
+      c->mv_compression = q[11];
+      if (c->mv_num_bytes < 1 || c->mv_num_bytes > 4) return -1;
+      q += 12;
       if (gi_read(&q, c->end, &c->mv_blocks)) return -1;
       if (q[0] != 0x02) return -1;
       c->num_bytes = q[1];
@@ -938,11 +958,11 @@ int or_dim_multi(void* h, const char* name, int32_t* offsets, int32_t* values, i
   }
   if (c->mv_total != rows + 1) return -1;
   int32_t* off = offsets ? offsets : (int32_t*)malloc((size_t)(rows + 1) * 4);
-  ocol oc = *c; /* the offsets part: 4-byte little-endian ints */
+  ocol oc = *c; /* the offsets part: little-endian ints (4 bytes for V3, numBytes for the legacy form) */
   oc.blocks = c->mv_blocks;
   oc.compression = c->mv_compression;
   oc.size_per = c->mv_size_per;
-  oc.num_bytes = 4;
+  oc.num_bytes = c->mv_num_bytes;
   int rc = read_vsize_ids(&oc, rows + 1, off);
   if (!rc) {
     for (int64_t r = 0; r < rows; ++r)

@@ -16,7 +16,10 @@ import pytest
 from compare import assert_results
 
 VALUES = ["a", "b", "c", "d", "e", "ff", "g10", "g9", "10", "9"]
-LAYOUTS = [("concise", "lz4"), ("roaring", "lz4"), ("concise", "uncompressed"), ("roaring", "none")]
+# (bitmap, compression, legacy): legacy = the pre-V3 compressed form (COMPRESSED + MULTI_VALUE,
+# CompressedVSizeColumnarMultiIntsSupplier: offsets as CompressedVSizeColumnarInts of 1-4 bytes)
+LAYOUTS = [("concise", "lz4", False), ("roaring", "lz4", False), ("concise", "uncompressed", False),
+           ("roaring", "none", False), ("concise", "lz4", True), ("roaring", "uncompressed", True)]
 
 
 def _rows(n, seed=2):
@@ -58,7 +61,7 @@ def _expected_mask(O, Q, f, rows, s_vals):
     return np.array([any(leaf(v) for v in (r or [None])) for r in vals])
 
 
-def _segment(W, path, rows, bitmap, comp, seed=3):
+def _segment(W, path, rows, bitmap, comp, legacy=False, seed=3):
     rng = np.random.default_rng(seed)
     n = len(rows)
     dic, ids = W.encode_multi_strings(rows)
@@ -67,7 +70,8 @@ def _segment(W, path, rows, bitmap, comp, seed=3):
     spec = W.SegmentSpec(timestamps=np.sort(rng.integers(0, 86_400_000, n)).astype(np.int64),
                          dims={"tags": (dic, ids), "s": W.encode_strings(s_vals), "tags2": (dic2, ids2)},
                          metrics={"m": ("long", rng.integers(0, 1000, n)), "x": ("double", rng.normal(10, 2, n))})
-    return W.write_segment(path, spec, bitmap=bitmap, compression=comp, lz4_mode="fast"), s_vals
+    return W.write_segment(path, spec, bitmap=bitmap, compression=comp, lz4_mode="fast",
+                           legacy_multi_value=legacy), s_vals
 
 
 @pytest.mark.parametrize("layout", LAYOUTS)
@@ -144,3 +148,55 @@ def test_gpu_groupby_multi_value_dimensions(Q, O, W, tmp_path, layout):
     q = Q.GroupByQuery(intervals=[(0, 1 << 40)], aggregations=[Q.count("rows")], dimensions=["tags"])
     off, _ = o[0].multi("tags")
     assert sum(r.event["rows"] for r in R.run_query(q, g[:1])) == int(off[-1])
+
+
+@pytest.mark.gpu
+def test_gpu_groupby_element_limit(Q, O, W, tmp_path):
+    """The multi-value explosion is counted in 64 bits before the sort is sized: a call whose
+    groupings pass the context's element limit (at most 2^32 - 64, element indices are 32-bit) is
+    refused with DG_ERR_UNSUPPORTED (the Java factory keeps its CPU engine) instead of wrapping."""
+    R = importlib.import_module("incubator-druid_amd.runners")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    N = importlib.import_module("incubator-druid_amd._native")
+    p, _ = _segment(W, str(tmp_path / "mv"), _rows(20_000, seed=11), "concise", "lz4", False)
+    ctx = S.GpuContext(0)
+    g, o = S.GpuSegment(p, context=ctx), O.OracleSegment(p)
+    q = Q.GroupByQuery(intervals=[(0, 1 << 40)], aggregations=[Q.count("rows")], dimensions=["tags", "tags2"])
+    exp = O.run(q, [o])
+    elements = sum(r.event["rows"] for r in exp)
+    try:
+        N.check(N.lib().dg_context_set_limit(ctx.handle, N.LIMIT_GROUP_ELEMENTS, elements))
+        assert_results(q, R.run_query(q, [g]), exp)  # exactly at the limit: runs
+        N.check(N.lib().dg_context_set_limit(ctx.handle, N.LIMIT_GROUP_ELEMENTS, elements - 1))
+        with pytest.raises(N.UnsupportedQuery, match="explodes"):
+            R.run_query(q, [g])
+    finally:
+        N.check(N.lib().dg_context_set_limit(ctx.handle, N.LIMIT_GROUP_ELEMENTS, 0))
+    assert_results(q, R.run_query(q, [g]), exp)
+
+
+@pytest.mark.gpu
+def test_gpu_legacy_multi_value_reference_segment(Q, O, v8_dir):
+    """The reference's own committed segment (IndexMergerV9CompatibilityTest) stores dim0 in the legacy
+    compressed multi-value form (DictionaryEncodedColumnPartSerde.java:376-377 ->
+    CompressedVSizeColumnarMultiIntsSupplier.java:77-93). Its rows are the test's events
+    (:99-126): ["dim00","dim01"], [null], ["dim00","dim01"] and three rows without dim0."""
+    R = importlib.import_module("incubator-druid_amd.runners")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    g, o = S.GpuSegment(v8_dir), O.OracleSegment(v8_dir)
+    iv = ["2014-01-01/2014-01-02"]
+    q = Q.GroupByQuery(intervals=iv, dimensions=["dim0"], aggregations=[Q.count("rows"), Q.long_sum("c", "count")])
+    got = R.run_query(q, [g])
+    assert [(r.event.get("dim0"), r.event["rows"]) for r in got] == [(None, 4), ("dim00", 2), ("dim01", 2)]
+    assert_results(q, got, O.run(q, [o]))
+    q = Q.GroupByQuery(intervals=iv, dimensions=["dim0", "dim1"], aggregations=[Q.count("rows")],
+                       filter=Q.SelectorDimFilter("dim0", "dim01"))
+    assert_results(q, R.run_query(q, [g]), O.run(q, [o]))
+    for f, n in ((Q.SelectorDimFilter("dim0", "dim00"), 2), (Q.SelectorDimFilter("dim0", None), 4),
+                 (Q.NotDimFilter(Q.SelectorDimFilter("dim0", "dim01")), 4)):
+        q = Q.TimeseriesQuery(intervals=iv, aggregations=[Q.count("rows")], filter=f)
+        got = R.run_query(q, [g])
+        assert got[0].value["rows"] == n
+        assert_results(q, got, O.run(q, [o]))
+    q = Q.TopNQuery(intervals=iv, dimension="dim0", metric="rows", threshold=3, aggregations=[Q.count("rows")])
+    assert_results(q, R.run_query(q, [g]), O.run(q, [o]))
