@@ -160,58 +160,110 @@ def _cpu_model():
 
 
 def _cpu_threads():
+    """Every core this process may run on (sched_getaffinity), as SURVEY §8(d) asks for."""
     try:
-        return max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16"))))
-    except (AttributeError, ValueError):
-        return max(1, min(os.cpu_count() or 1, 16))
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return max(1, os.cpu_count() or 1)
 
 
-def cpu_baseline_groupby(paths, query, threads):
+def _cpu_quota():
+    """The cgroup CPU quota in cores (cpu.max), or None when unlimited / unreadable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_groupby(paths, query, threads, want_groups=False):
     """oracle/libdruid_cpu.so: the reference's per-segment GroupByV2 loop (LZ4 decode, hash grouping,
-    merge by value, ordered result) in C -O3 -march=native, one segment per thread, on the whole
-    workload. Merged-dictionary maps are built before timing (the GPU engine caches them too)."""
+    merge by value, ordered result) in C -O3 -march=native over row chunks of the segments on
+    `threads` host threads, on the whole workload. Merged-dictionary maps are built before timing (the
+    GPU engine caches them too). want_groups: also return every merged group (key = merged id 1 << 32
+    | merged id 2, long sum, double sum) for the per-group comparison with the GPU result."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     lib = ctypes.CDLL(os.path.join(REPO, "oracle", "libdruid_cpu.so"))
     lib.cpu_groupby2.restype = ctypes.c_int64
-    lib.cpu_groupby2.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
-                                 ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
-                                 ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    vp = ctypes.c_void_p
+    lib.cpu_groupby2.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                 ctypes.c_char_p, ctypes.c_char_p, vp, vp, ctypes.c_int32,
+                                 ctypes.c_int, ctypes.POINTER(ctypes.c_double), vp, vp, vp, vp,
+                                 ctypes.POINTER(ctypes.c_double)]
     segs = [O.OracleSegment(p) for p in paths]
     d1, d2 = query.dimensions
-    maps = []
+    maps, merged_dicts = [], []
     for dim in (d1, d2):
         dicts = [s.dictionary(dim) for s in segs]
         merged = sorted(set().union(*map(set, dicts)), key=lambda v: (v is not None, (v or "").encode("utf-16-be")))
         index = {v: i for i, v in enumerate(merged)}
         maps.append(([np.array([index[v] for v in dd], dtype=np.int32) for dd in dicts], len(merged)))
+        merged_dicts.append(merged)
     (m1, card1), (m2, _) = maps
-    ptr1 = (ctypes.c_void_p * len(segs))(*[a.ctypes.data for a in m1])
-    ptr2 = (ctypes.c_void_p * len(segs))(*[a.ctypes.data for a in m2])
-    lib.or_open.restype = ctypes.c_void_p
+    ptr1 = (vp * len(segs))(*[a.ctypes.data for a in m1])
+    ptr2 = (vp * len(segs))(*[a.ctypes.data for a in m2])
+    lib.or_open.restype = vp
     lib.or_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
-    lib.or_close.argtypes = [ctypes.c_void_p]
+    lib.or_close.argtypes = [vp]
     err = ctypes.create_string_buffer(512)
     hs = [lib.or_open(p.encode(), err, 512) for p in paths]  # the engine library's own segment readers
     if not all(hs):
         raise IOError(err.value.decode())
-    handles = (ctypes.c_void_p * len(segs))(*hs)
+    handles = (vp * len(segs))(*hs)
     sums = (ctypes.c_double * 3)()
+    rows = sum(s.num_rows for s in segs)
+    out = None
+    if want_groups:
+        out = {"key": np.empty(rows, np.uint64), "lsum": np.empty(rows, np.int64), "dsum": np.empty(rows, np.float64)}
     ls, ds = query.aggregations[0].fieldName, query.aggregations[1].fieldName
+    secs = ctypes.c_double()
     t0 = time.perf_counter()
     ng = lib.cpu_groupby2(handles, len(segs), d1.encode(), d2.encode(), ls.encode(), ds.encode(), ptr1, ptr2, card1,
-                          threads, sums)
-    el = time.perf_counter() - t0
-    rows = sum(s.num_rows for s in segs)
+                          threads, sums, out["key"].ctypes.data if out else None, None,
+                          out["lsum"].ctypes.data if out else None, out["dsum"].ctypes.data if out else None,
+                          ctypes.byref(secs))
+    if ng < 0:
+        raise RuntimeError("cpu_groupby2 failed")
+    el = secs.value if secs.value > 0 else time.perf_counter() - t0
     for s, h in zip(segs, hs):
         s.close()
         lib.or_close(h)
-    return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"the whole step workload: {len(paths)} segments x {rows // len(paths)} rows, GroupByV2 "
-                      f"{d1} x {d2} longSum+doubleSum -> {ng} merged groups in {el:.2f} s "
-                      f"(oracle/cpu_engine.c + druid_oracle.c, C -O3 -march=native, {threads} threads, "
-                      f"LZ4 decoded per block inside the timing)",
-            "cpu_model": _cpu_model(), "groups": int(ng), "checks": [sums[0], sums[1], sums[2]]}
+    quota = _cpu_quota()
+    res = {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+           "sample": f"the whole step workload: {len(paths)} segments x {rows // len(paths)} rows, GroupByV2 "
+                     f"{d1} x {d2} longSum+doubleSum -> {ng} merged groups in {el:.2f} s "
+                     f"(oracle/cpu_engine.c + druid_oracle.c, C -O3 -march=native, {threads} threads over 1M-row "
+                     f"chunks, LZ4 decoded per block inside the timing)",
+           "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cores": threads,
+           "cgroup_quota_cores": quota, "groups": int(ng)}
+    if out is not None:
+        for k in out:
+            out[k] = out[k][:ng]
+        res["_groups"] = out
+        res["_dicts"] = merged_dicts
+    return res
+
+
+def compare_groups(part, dicts, cpu):
+    """Per-group equality of the GPU's merged result with the CPU engine's, over every group: the same
+    dimension values in the same order, long sums bit-exact, double sums within 1e-9 relative."""
+    g = cpu["_groups"]
+    n = len(part)
+    out = {"groups_equal": n == len(g["key"]), "dicts_equal": dicts == cpu["_dicts"]}
+    if not (out["groups_equal"] and out["dicts_equal"]):
+        out["per_group_equal"] = False
+        return out
+    keys = (part.codes[0].astype(np.uint64) << np.uint64(32)) | part.codes[1].astype(np.uint64)
+    out["keys_equal"] = bool(np.array_equal(keys, g["key"]))
+    out["long_sums_equal"] = bool(np.array_equal(np.asarray(part.aggs[0], dtype=np.int64), g["lsum"]))
+    a, b = np.asarray(part.aggs[1], dtype=np.float64), g["dsum"]
+    rel = np.abs(a - b) / np.maximum(np.maximum(np.abs(a), np.abs(b)), 1e-300)
+    rel[a == b] = 0.0
+    out["double_max_rel_err"] = float(rel.max()) if n else 0.0
+    out["doubles_within_1e-9"] = bool(out["double_max_rel_err"] <= 1e-9)
+    out["per_group_equal"] = out["keys_equal"] and out["long_sums_equal"] and out["doubles_within_1e-9"]
+    return out
 
 
 def cpu_baseline_oracle(query, path, rows, seconds, selected_fraction):
@@ -393,33 +445,43 @@ def main():
     }
     if isinstance(query, Q.GroupByQuery):
         line["groups_per_step"] = per_step("groups")
+    part = dicts = None
     if isinstance(query, Q.GroupByQuery) and dist is None:
         # the merged result, fetched to the host once (PCIe-inclusive; not part of `value`), and checked
         t1 = time.perf_counter()
         res = R.groupby_run(segs, query)
         part = res.fetch()
         fetch_s = time.perf_counter() - t1
+        dicts = [res.dictionary(d) for d in range(len(query.dimensions))]
         res.release()
         line["pcie_fetch"] = {"groups": len(part), "query_plus_fetch_ms": fetch_s * 1e3,
                               "rows_per_s_incl_fetch": scanned_local / fetch_s}
-        checks = [float(len(part)), float(np.sum(part.aggs[0], dtype=np.float64)),
-                  float(np.sum(part.aggs[1], dtype=np.float64))]
-        line["result_checks"] = {"groups": checks[0], "long_sum": checks[1], "double_sum": checks[2],
-                                 "sorted": bool(np.all(np.diff(part.codes[0].astype(np.int64) * (1 << 32) +
-                                                               part.codes[1].astype(np.int64)) > 0))}
-        del part
+        # result order: bucket time, then each dimension's merged id (strictly increasing, no duplicates)
+        order = np.lexsort(tuple(c.astype(np.int64) for c in reversed(part.codes)) + (part.times,)) \
+            if len(part) else np.zeros(0, np.int64)
+        same = np.ones(max(len(part) - 1, 0), dtype=bool)
+        for c in [part.times] + list(part.codes):
+            same &= c[1:] == c[:-1]
+        line["result_checks"] = {"groups": len(part),
+                                 "long_sum": int(np.sum(np.asarray(part.aggs[0], dtype=np.int64))),
+                                 "double_sum": float(np.sum(part.aggs[1], dtype=np.float64)),
+                                 "sorted": bool(np.array_equal(order, np.arange(len(part))) and not same.any())}
+        del order, same
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if args.config == "groupby":
-            cb = cpu_baseline_groupby(paths, query, _cpu_threads())
-            if "result_checks" in line:
+            cb = cpu_baseline_groupby(paths, query, _cpu_threads(), want_groups=part is not None)
+            if part is not None:
                 rc = line["result_checks"]
-                rc["cpu_groups_equal"] = cb["groups"] == int(rc["groups"])
-                rc["cpu_long_sum_equal"] = abs(cb["checks"][1] - rc["long_sum"]) <= 1e-6 * max(1.0, abs(rc["long_sum"]))
-                rc["cpu_double_sum_rel"] = abs(cb["checks"][2] - rc["double_sum"]) / max(1.0, abs(rc["double_sum"]))
+                rc.update(compare_groups(part, dicts, cb))
+                rc["cpu_long_sum"] = int(np.sum(cb["_groups"]["lsum"]))
+                rc["cpu_long_sum_equal"] = rc["cpu_long_sum"] == rc["long_sum"]
+            cb.pop("_groups", None)
+            cb.pop("_dicts", None)
             line["cpu_baseline"] = cb
         else:
             line["cpu_baseline"] = cpu_baseline_oracle(query, paths[0], rows_per, args.cpu_seconds,
                                                        selected_local / scanned_local if scanned_local else 1.0)
+    del part
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

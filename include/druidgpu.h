@@ -29,6 +29,8 @@
  *   dg_result_export / dg_keys_partition / dg_merge
  *                            <- QueryRunnerFactory.mergeRunners across devices (query/QueryRunnerFactory.java:62):
  *                               GroupByMergingQueryRunnerV2 semantics over the devices' merged groups
+ *   dg_groupby_merge_devices <- the same within one process: the library moves key ranges between devices itself
+ *   dg_timeseries_merge      <- TimeseriesBinaryFn fold of runners' results (query/timeseries/TimeseriesBinaryFn.java:67-70)
  *   dg_records_pack          <- BufferAggregator.get* record layout (query/aggregation/BufferAggregator.java:35-199)
  *
  * Segment arrays: every *_run takes n_segs segments that are attached to the SAME context (device)
@@ -52,7 +54,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 8
+#define DG_ABI_VERSION 9
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -414,6 +416,36 @@ int dg_keys_partition(dg_context* ctx, const uint64_t* d_keys, int64_t n, const 
  * dg_result_dim_cardinality is ks->card[d], and the dictionary is the caller's. */
 int dg_merge(dg_context* ctx, const dg_keyspace* ks, const uint64_t* d_keys, const uint64_t* d_slots, int64_t n,
              dg_result** out, dg_metrics* metrics);
+
+/* ---- in-process cross-device merge (QueryRunnerFactory.mergeRunners over the devices of ONE process,
+ * query/QueryRunnerFactory.java:62: a historical is one JVM whose processing pool drives every
+ * segment, ChainedExecutionQueryRunner.java:89-180; GroupByMergingQueryRunnerV2.java:170-290
+ * semantics) ----
+ * parts: n_parts dg_groupby_run results of one query, each on its own context (device), in merge
+ * order. The library builds the union of their merged dictionaries, re-keys every part into that key
+ * space on its own device (as dg_result_export), cuts the keys into n_targets ranges at splitters
+ * sampled from all parts (dg_keys_partition), moves every range to its target's device with peer
+ * copies over xGMI (hipMemcpyPeerAsync; a device copy when part and target share a device) and
+ * merges it there (dg_merge: equal keys combine in part order with the combining aggregators).
+ * outs[t] = key range t of the merged result, resident on targets[t]; concatenated in t order they
+ * are the whole merged, ordered result. The outputs fetch like dg_groupby_run results: their
+ * dg_result_dim_dictionary is the union dictionary. n_targets == 1: the whole merge on one device.
+ * Parts stay valid (the caller releases them). No transport from the caller is needed. */
+int dg_groupby_merge_devices(dg_result* const* parts, int32_t n_parts, dg_context* const* targets, int32_t n_targets,
+                             dg_result** outs, dg_metrics* metrics);
+
+/* TimeseriesBinaryFn fold (query/timeseries/TimeseriesBinaryFn.java:67-70) as the toolchest's
+ * mergeResults applies it over runners' results (ResultMergeQueryRunner: by time, then runner
+ * order): n_lists lists in dg_timeseries_run's output layout (list i holds n[i] buckets: times[i * cap
+ * + k], rows[...], values[(i * cap + k) * n_aggs ...]) — the segments of one call, or the lists of
+ * several devices' calls concatenated. Results of one granularity bucket combine with
+ * AggregatorFactory.combine (long wrap, float adds in float, Math.min/max with NaN and -0.0); ALL
+ * granularity keeps the earliest result's timestamp. skip_empty: skipEmptyBuckets drops buckets with
+ * zero rows before merging. Output: out_n merged buckets, ascending (descending when scan->descending),
+ * out_rows = rows aggregated per bucket. Host memory only. */
+int dg_timeseries_merge(const dg_scan* scan, int32_t n_lists, const int32_t* n, int32_t cap, const int64_t* times,
+                        const int64_t* rows, const uint64_t* values, int32_t skip_empty, int32_t out_cap, int32_t* out_n,
+                        int64_t* out_time, int64_t* out_rows, uint64_t* out_values);
 
 /* ---- BufferAggregator record layout (query/aggregation/BufferAggregator.java:35-199) ----
  * Writes n records of aggregate slots (n_aggs per record, the dg_*_run slot encoding) into Druid's

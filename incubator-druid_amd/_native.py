@@ -127,7 +127,7 @@ EXPORTS = [
     "dg_result_groups", "dg_result_fetch_groups", "dg_result_fetch_rows", "dg_result_dim_cardinality",
     "dg_result_dim_dictionary", "dg_result_release", "dg_keyspace_bits", "dg_result_export", "dg_keys_partition",
     "dg_merge", "dg_records_pack", "dg_debug_lz4_decode", "dg_result_limit",
-    "dg_segment_from_rows", "dg_context_set_limit",
+    "dg_segment_from_rows", "dg_context_set_limit", "dg_groupby_merge_devices", "dg_timeseries_merge",
 ]
 
 _lib = None
@@ -189,6 +189,8 @@ def lib():
         "dg_result_export": (ctypes.c_int, [vp, P(dg_keyspace), P(vp), vp, vp]),
         "dg_keys_partition": (ctypes.c_int, [vp, vp, i64, vp, i32, vp]),
         "dg_merge": (ctypes.c_int, [vp, P(dg_keyspace), vp, vp, i64, P(vp), P(dg_metrics)]),
+        "dg_groupby_merge_devices": (ctypes.c_int, [P(vp), i32, P(vp), i32, P(vp), P(dg_metrics)]),
+        "dg_timeseries_merge": (ctypes.c_int, [P(dg_scan), i32, vp, i32, vp, vp, vp, i32, i32, P(i32), vp, vp, vp]),
         "dg_records_pack": (ctypes.c_int, [vp, i64, P(dg_record_layout), vp]),
         "dg_debug_lz4_decode": (ctypes.c_int, [vp, P(vp), P(i32), i32, vp, P(i32), P(ctypes.c_double), vp]),
     }

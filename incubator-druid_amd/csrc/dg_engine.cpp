@@ -2997,6 +2997,7 @@ struct dg_result {
   std::vector<std::shared_ptr<dg::MergedDict>> dicts;  // empty for a dg_merge result (cluster ids)
   std::vector<int32_t> cards;                         // dg_merge result: cluster dictionary sizes
   bool limited = false;                               // dg_result_limit: groups in the push-down order
+  std::vector<int32_t> kinds;                         // DG_AGG_* of every aggregator (combine semantics)
   ~dg_result() {
     if (!ctx) return;
     std::lock_guard<std::mutex> g(ctx->mu);
@@ -3227,6 +3228,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   res->period = q->period_ms;
   if (gr.hb) res->bounds.assign(gr.hb, gr.hb + gr.nb + 1);
   res->universal = q->interval_start;  // GroupByStrategyV2.getUniversalTimestamp (ALL granularity)
+  res->kinds.assign(plan.kind, plan.kind + na);
   res->dicts = md;
   res->keys = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * 8));
   res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * rec * 8));
@@ -3619,6 +3621,7 @@ int dg_merge(dg_context* c, const dg_keyspace* ks, const uint64_t* d_keys, const
   res->bucket0 = ks->bucket0;
   res->period = ks->period_ms;
   res->universal = ks->universal_time;
+  res->kinds.assign(plan.kind, plan.kind + plan.n);
   res->cards.assign(ks->card, ks->card + ks->n_dims);
   dg_metrics m;
   memset(&m, 0, sizeof m);
@@ -3663,6 +3666,287 @@ int dg_merge(dg_context* c, const dg_keyspace* ks, const uint64_t* d_keys, const
   m.total_ms = ms_since(t0);
   if (metrics) *metrics = m;
   *out = res.release();
+  return DG_OK;
+}
+
+// ---- in-process cross-device merge (one process, several devices / contexts) ----
+}  // extern "C"
+
+namespace dg {
+
+// Union of the parts' merged dictionaries of one dimension (each sorted, Java String order, nulls
+// first) + for every part the map of its ids into the union (strictly increasing).
+static void union_dictionary(const std::vector<const MergedDict*>& ds, MergedDict* out, std::vector<std::vector<int32_t>>* maps) {
+  const size_t n = ds.size();
+  maps->assign(n, {});
+  std::vector<size_t> pos(n, 0);
+  for (size_t p = 0; p < n; ++p) (*maps)[p].resize(ds[p]->values.size());
+  for (;;) {
+    int best = -1;
+    for (size_t p = 0; p < n; ++p) {
+      if (pos[p] >= ds[p]->values.size()) continue;
+      if (best < 0 || cmp_nullable(ds[p]->is_null[pos[p]] != 0, ds[p]->values[pos[p]], ds[best]->is_null[pos[best]] != 0,
+                                   ds[best]->values[pos[best]]) < 0)
+        best = (int)p;
+    }
+    if (best < 0) break;
+    const bool nul = ds[best]->is_null[pos[best]] != 0;
+    const std::string v = ds[best]->values[pos[best]];
+    out->values.push_back(nul ? std::string() : v);
+    out->is_null.push_back(nul ? 1 : 0);
+    const int32_t id = (int32_t)out->values.size() - 1;
+    for (size_t p = 0; p < n; ++p)
+      while (pos[p] < ds[p]->values.size() &&
+             cmp_nullable(ds[p]->is_null[pos[p]] != 0, ds[p]->values[pos[p]], nul, v) == 0)
+        (*maps)[p][pos[p]++] = id;
+  }
+  out->null_gid = (!out->values.empty() && out->is_null[0]) ? 0 : -1;
+}
+
+struct CtxBlock {  // a device block from a context's result cache, returned on scope exit
+  Context* ctx = nullptr;
+  void* p = nullptr;
+  CtxBlock() = default;
+  CtxBlock(const CtxBlock&) = delete;
+  CtxBlock& operator=(const CtxBlock&) = delete;
+  bool take(Context* c, size_t bytes) {
+    ctx = c;
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    p = result_alloc(c, bytes);
+    return p != nullptr;
+  }
+  ~CtxBlock() {
+    if (!ctx || !p) return;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    result_free(ctx, p);
+  }
+};
+
+}  // namespace dg
+
+extern "C" {
+
+int dg_groupby_merge_devices(dg_result* const* parts, int32_t n_parts, dg_context* const* targets, int32_t n_targets,
+                             dg_result** outs, dg_metrics* metrics) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!parts || n_parts <= 0 || !targets || n_targets <= 0 || !outs) return set_error(DG_ERR_ARG, "bad arguments");
+  for (int32_t t = 0; t < n_targets; ++t) {
+    if (!targets[t]) return set_error(DG_ERR_ARG, "null target %d", t);
+    outs[t] = nullptr;
+  }
+  const dg_result* r0 = parts[0];
+  for (int32_t p = 0; p < n_parts; ++p) {
+    const dg_result* r = parts[p];
+    if (!r) return set_error(DG_ERR_ARG, "null part %d", p);
+    if (r->limited) return set_error(DG_ERR_ARG, "part %d is a limited result (not in key order)", p);
+    if (r->dicts.empty() || (int)r->dicts.size() != r->ndims)
+      return set_error(DG_ERR_ARG, "part %d is not a dg_groupby_run result", p);
+    if (r->ndims != r0->ndims || r->naggs != r0->naggs || r->kinds != r0->kinds || r->period != r0->period ||
+        r->bounds != r0->bounds || (!r->period && r->universal != r0->universal))
+      return set_error(DG_ERR_ARG, "part %d is not a result of the same query", p);
+  }
+  const int nd = r0->ndims, na = r0->naggs, rec = na + 1;
+  // one cluster key space: union dictionaries, bucket indices from the earliest part's origin
+  std::vector<std::shared_ptr<MergedDict>> udicts(nd);
+  std::vector<std::vector<std::vector<int32_t>>> maps(nd);  // [dim][part][id]
+  std::vector<int32_t> card(nd);
+  for (int d = 0; d < nd; ++d) {
+    std::vector<const MergedDict*> ds;
+    for (int32_t p = 0; p < n_parts; ++p) ds.push_back(parts[p]->dicts[d].get());
+    udicts[d] = std::make_shared<MergedDict>();
+    udicts[d]->dim = ds[0]->dim;
+    union_dictionary(ds, udicts[d].get(), &maps[d]);
+    card[d] = (int32_t)udicts[d]->values.size();
+  }
+  dg_keyspace ks;
+  memset(&ks, 0, sizeof ks);
+  ks.n_dims = nd;
+  ks.card = card.data();
+  ks.period_ms = r0->period;
+  ks.universal_time = r0->universal;
+  ks.n_aggs = na;
+  ks.agg_kinds = r0->kinds.data();
+  if (r0->period) {
+    int64_t b0 = INT64_MAX, end = INT64_MIN;
+    for (int32_t p = 0; p < n_parts; ++p) b0 = std::min(b0, parts[p]->bucket0);
+    for (int32_t p = 0; p < n_parts; ++p) {
+      const int64_t delta = (parts[p]->bucket0 - b0) / r0->period;
+      if ((parts[p]->bucket0 - b0) % r0->period) return set_error(DG_ERR_ARG, "part %d buckets off the grid", p);
+      end = std::max(end, delta + ((int64_t)1 << parts[p]->lay.bucket_bits));
+    }
+    ks.bucket0 = b0;
+    ks.n_buckets = std::max<int64_t>(end, 1);
+  }
+  int32_t kbits = 0;
+  int rc = dg_keyspace_bits(&ks, &kbits);
+  if (rc) return rc;
+  // every part re-keyed into the key space on its own device
+  std::vector<CtxBlock> xkeys(n_parts), xslots(n_parts);
+  std::vector<int64_t> np(n_parts);
+  for (int32_t p = 0; p < n_parts; ++p) {
+    dg_result* r = parts[p];
+    np[p] = r->ngroups;
+    if (!np[p]) continue;
+    if (!xkeys[p].take(r->ctx, (size_t)np[p] * 8) || !xslots[p].take(r->ctx, (size_t)np[p] * rec * 8))
+      return set_error(DG_ERR_OOM, "export buffers of part %d (%lld groups)", p, (long long)np[p]);
+    std::vector<const int32_t*> mp(nd);
+    for (int d = 0; d < nd; ++d) mp[d] = maps[d][p].data();
+    rc = dg_result_export(r, &ks, mp.data(), static_cast<uint64_t*>(xkeys[p].p), static_cast<uint64_t*>(xslots[p].p));
+    if (rc) return rc;
+  }
+  // key ranges: n_targets - 1 splitters from evenly spaced samples of every part (weighted by the
+  // part's size), identical cuts on every part, so equal keys meet on one target
+  std::vector<uint64_t> splits;
+  if (n_targets > 1) {
+    struct Smp {
+      uint64_t key;
+      double w;
+    };
+    std::vector<Smp> smp;
+    double total = 0;
+    for (int32_t p = 0; p < n_parts; ++p) {
+      if (!np[p]) continue;
+      const int64_t s = std::min<int64_t>(np[p], 4096), stride = np[p] / s;
+      std::vector<uint64_t> h((size_t)s);
+      Context* c = parts[p]->ctx;
+      {
+        std::lock_guard<std::mutex> g(c->mu);
+        hipSetDevice(c->device);
+        DG_HIP(hipMemcpy2D(h.data(), 8, xkeys[p].p, (size_t)stride * 8, 8, (size_t)s, hipMemcpyDeviceToHost));
+      }
+      for (uint64_t k : h) smp.push_back({k, (double)np[p] / (double)s});
+      total += (double)np[p];
+    }
+    std::sort(smp.begin(), smp.end(), [](const Smp& a, const Smp& b) { return a.key < b.key; });
+    double acc = 0;
+    size_t i = 0;
+    for (int32_t t = 1; t < n_targets; ++t) {
+      const double want = total * t / n_targets;
+      while (i < smp.size() && acc + smp[i].w <= want) acc += smp[i++].w;
+      splits.push_back(i < smp.size() ? smp[i].key : ~0ull);
+    }
+  }
+  std::vector<std::vector<int64_t>> cut(n_parts, std::vector<int64_t>(n_targets + 1, 0));
+  for (int32_t p = 0; p < n_parts; ++p) {
+    cut[p][n_targets] = np[p];
+    if (n_targets > 1 && np[p]) {
+      rc = dg_keys_partition(reinterpret_cast<dg_context*>(parts[p]->ctx), static_cast<uint64_t*>(xkeys[p].p), np[p],
+                             splits.data(), n_targets - 1, cut[p].data() + 1);
+      if (rc) return rc;
+    }
+  }
+  // every range moves to its target (peer copies over xGMI; a device copy on the same device) and
+  // is merged there in part order (equal keys combine in that order)
+  dg_metrics tot;
+  memset(&tot, 0, sizeof tot);
+  for (int32_t t = 0; t < n_targets; ++t) {
+    Context* tc = reinterpret_cast<Context*>(targets[t]);
+    int64_t n = 0;
+    for (int32_t p = 0; p < n_parts; ++p) n += cut[p][t + 1] - cut[p][t];
+    CtxBlock rk, rs;
+    if (n > 0 && (!rk.take(tc, (size_t)n * 8) || !rs.take(tc, (size_t)n * rec * 8)))
+      return set_error(DG_ERR_OOM, "receive buffers of target %d (%lld records)", t, (long long)n);
+    {
+      std::lock_guard<std::mutex> g(tc->mu);
+      hipSetDevice(tc->device);
+      int64_t at = 0;
+      for (int32_t p = 0; p < n_parts; ++p) {
+        const int64_t a = cut[p][t], m = cut[p][t + 1] - a;
+        if (m <= 0) continue;
+        const int sdev = parts[p]->ctx->device;
+        if (sdev != tc->device) {
+          int can = 0;
+          if (hipDeviceCanAccessPeer(&can, tc->device, sdev) == hipSuccess && can) {
+            hipError_t e = hipDeviceEnablePeerAccess(sdev, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return set_error(DG_ERR_DEVICE, "peer access %d -> %d", tc->device, sdev);
+            (void)hipGetLastError();
+          }
+        }
+        DG_HIP(hipMemcpyPeerAsync(static_cast<uint64_t*>(rk.p) + at, tc->device, static_cast<uint64_t*>(xkeys[p].p) + a,
+                                  sdev, (size_t)m * 8, tc->stream));
+        DG_HIP(hipMemcpyPeerAsync(static_cast<uint64_t*>(rs.p) + at * rec, tc->device,
+                                  static_cast<uint64_t*>(xslots[p].p) + a * rec, sdev, (size_t)m * rec * 8, tc->stream));
+        at += m;
+      }
+      DG_HIP(hipStreamSynchronize(tc->stream));
+    }
+    dg_metrics m;
+    rc = dg_merge(targets[t], &ks, static_cast<uint64_t*>(rk.p), static_cast<uint64_t*>(rs.p), n, &outs[t], &m);
+    if (rc) {
+      for (int32_t u = 0; u < t; ++u) {
+        dg_result_release(outs[u]);
+        outs[u] = nullptr;
+      }
+      return rc;
+    }
+    outs[t]->dicts = udicts;  // the union dictionaries: the merged result fetches like a groupBy result
+    outs[t]->bounds = r0->bounds;
+    tot.sort_ms += m.sort_ms;
+    tot.reduce_ms += m.reduce_ms;
+    tot.aggregate_ms += m.aggregate_ms;
+    tot.selected_rows += m.selected_rows;
+    tot.groups += m.groups;
+    tot.sort_passes = m.sort_passes;
+    tot.key_bits = m.key_bits;
+  }
+  tot.total_ms = ms_since(t0);
+  if (metrics) *metrics = tot;
+  return DG_OK;
+}
+
+// ---- timeseries merge (TimeseriesBinaryFn fold, host) ----
+int dg_timeseries_merge(const dg_scan* scan, int32_t n_lists, const int32_t* n, int32_t cap, const int64_t* times,
+                        const int64_t* rows, const uint64_t* values, int32_t skip_empty, int32_t out_cap,
+                        int32_t* out_n, int64_t* out_time, int64_t* out_rows, uint64_t* out_values) {
+  if (!scan || n_lists < 0 || cap < 0 || (n_lists && (!n || !times || !rows)) || !out_n || out_cap < 0)
+    return set_error(DG_ERR_ARG, "bad arguments");
+  const int na = scan->n_aggs;
+  if (na < 0 || na > kMaxAggs || (na && (!scan->aggs || (n_lists && !values)))) return set_error(DG_ERR_ARG, "bad aggregators");
+  for (int a = 0; a < na; ++a)
+    if (scan->aggs[a].kind < DG_AGG_COUNT || scan->aggs[a].kind > DG_AGG_FLOAT_MAX)
+      return set_error(DG_ERR_ARG, "aggregator kind %d", scan->aggs[a].kind);
+  const bool all = scan->period_ms == 0 && !scan->bucket_starts;
+  struct E {
+    int64_t t;
+    int32_t list, k;
+  };
+  std::vector<E> es;
+  for (int32_t i = 0; i < n_lists; ++i) {
+    if (n[i] > cap) return set_error(DG_ERR_ARG, "list %d holds %d > cap %d buckets", i, n[i], cap);
+    for (int32_t k = 0; k < n[i]; ++k) {
+      const int64_t at = (int64_t)i * cap + k;
+      if (skip_empty && rows[at] == 0) continue;
+      es.push_back({times[at], i, k});
+    }
+  }
+  // ResultMergeQueryRunner order: time, then the runners' order
+  std::stable_sort(es.begin(), es.end(), [](const E& a, const E& b) { return a.t != b.t ? a.t < b.t : a.list < b.list; });
+  std::vector<int64_t> mt, mr;
+  std::vector<uint64_t> mv;
+  for (size_t e = 0; e < es.size(); ++e) {
+    const int64_t at = (int64_t)es[e].list * cap + es[e].k;
+    const bool same = !mt.empty() && (all || mt.back() == es[e].t);
+    if (!same) {
+      mt.push_back(es[e].t);  // ALL: the earliest result's timestamp
+      mr.push_back(0);
+      for (int a = 0; a < na; ++a) mv.push_back(values[at * na + a]);
+    } else {
+      uint64_t* acc = mv.data() + (mt.size() - 1) * na;
+      for (int a = 0; a < na; ++a) acc[a] = combine_abi(scan->aggs[a].kind, acc[a], values[at * na + a]);
+    }
+    mr.back() += rows[at];
+  }
+  const int32_t m = (int32_t)mt.size();
+  if (m > out_cap) return set_error(DG_ERR_ARG, "%d merged buckets > out_cap %d", m, out_cap);
+  for (int32_t i = 0; i < m; ++i) {
+    const int32_t j = scan->descending ? m - 1 - i : i;  // descending queries list buckets latest first
+    if (out_time) out_time[i] = mt[j];
+    if (out_rows) out_rows[i] = mr[j];
+    if (out_values)
+      for (int a = 0; a < na; ++a) out_values[(int64_t)i * na + a] = mv[(size_t)j * na + a];
+  }
+  *out_n = m;
   return DG_OK;
 }
 

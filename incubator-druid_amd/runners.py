@@ -114,6 +114,55 @@ def timeseries_per_segment(segments: Sequence[GpuSegment], query: Q.TimeseriesQu
     return out
 
 
+def run_timeseries(segments: Sequence[GpuSegment], query: Q.TimeseriesQuery,
+                   stats: Optional[RunStats] = None) -> List[Q.Result]:
+    """QueryRunnerFactory.mergeRunners over segments on any devices: one dg_timeseries_run per device,
+    then every segment's bucket list (in segment order) folded natively by dg_timeseries_merge
+    (TimeseriesBinaryFn, ResultMergeQueryRunner order: time, then runner)."""
+    na = len(query.aggregations)
+    groups = list(_group_by_device(segments).items())
+    caps = {dev: _bucket_cap([segments[i] for i in idx], query) for dev, idx in groups}
+    cap = max(caps.values()) if caps else 1
+    n_all = len(segments)
+    nb = np.zeros(max(n_all, 1), dtype=np.int32)
+    times = np.zeros(max(n_all, 1) * cap, dtype=np.int64)
+    rows = np.zeros(max(n_all, 1) * cap, dtype=np.int64)
+    vals = np.zeros(max(n_all, 1) * cap * max(na, 1), dtype=np.uint64)
+    scan = keep = None
+    for dev, idx in groups:
+        segs = [segments[i] for i in idx]
+        c = caps[dev]
+        scan, keep = N.make_scan(query, Q, segments=segs)
+        n = len(segs)
+        d_nb = np.zeros(n, dtype=np.int32)
+        d_t = np.zeros(n * c, dtype=np.int64)
+        d_r = np.zeros(n * c, dtype=np.int64)
+        d_v = np.zeros(n * c * max(na, 1), dtype=np.uint64)
+        m = N.dg_metrics()
+        N.check(N.lib().dg_timeseries_run(_handles(segs), n, ctypes.byref(scan), c, d_nb.ctypes.data, d_t.ctypes.data,
+                                          d_r.ctypes.data, d_v.ctypes.data, ctypes.byref(m)))
+        if stats is not None:
+            stats.add(m)
+        for k, i in enumerate(idx):  # into the segment's slot of the call-wide lists
+            nb[i] = d_nb[k]
+            times[i * cap:i * cap + c] = d_t[k * c:(k + 1) * c]
+            rows[i * cap:i * cap + c] = d_r[k * c:(k + 1) * c]
+            vals[i * cap * na:(i * cap + c) * na] = d_v[k * c * na:(k + 1) * c * na]
+    if scan is None:
+        scan, keep = N.make_scan(query, Q, filters=False)
+    out_cap = max(n_all, 1) * cap
+    on = ctypes.c_int32()
+    o_t = np.zeros(out_cap, dtype=np.int64)
+    o_v = np.zeros(out_cap * max(na, 1), dtype=np.uint64)
+    N.check(N.lib().dg_timeseries_merge(ctypes.byref(scan), n_all, nb.ctypes.data, cap, times.ctypes.data,
+                                        rows.ctypes.data, vals.ctypes.data, int(query.skip_empty_buckets), out_cap,
+                                        ctypes.byref(on), o_t.ctypes.data, None, o_v.ctypes.data))
+    m = on.value
+    cols = _decode_slots(query.aggregations, o_v.reshape(-1, max(na, 1))[:m, :na])
+    return [Q.Result(int(o_t[b]), {a.name: _py(c[b], a.output_type) for a, c in zip(query.aggregations, cols)})
+            for b in range(m)]
+
+
 def _bucket_cap(segs, query) -> int:
     g = query.granularity
     if g.is_all:
@@ -711,6 +760,31 @@ def groupby_per_device(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
     return out
 
 
+def groupby_merge_devices(segments: Sequence[GpuSegment], query: Q.GroupByQuery, stats: Optional[RunStats] = None,
+                          targets: Optional[Sequence] = None) -> "GroupByResult | List[GroupByResult]":
+    """mergeRunners over segments of several devices in one process: one dg_groupby_run per device,
+    then dg_groupby_merge_devices moves key ranges between the devices itself (peer copies) and
+    merges them there. targets: contexts owning the key ranges (default: the first device's, one
+    result); with targets given, the list of per-target results in key order."""
+    parts = []
+    try:
+        for _, idx in _group_by_device(segments).items():
+            parts.append(groupby_run([segments[i] for i in idx], query, stats))
+        ctxs = [segments[0].context] if targets is None else list(targets)
+        outs = (ctypes.c_void_p * len(ctxs))()
+        hp = (ctypes.c_void_p * len(parts))(*[p.handle.value for p in parts])
+        ht = (ctypes.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+        m = N.dg_metrics()
+        N.check(N.lib().dg_groupby_merge_devices(hp, len(parts), ht, len(ctxs), outs, ctypes.byref(m)))
+        if stats is not None:
+            stats.add(m)
+    finally:
+        for p in parts:
+            p.release()
+    res = [GroupByResult(ctypes.c_void_p(o), query) for o in outs]
+    return res[0] if targets is None else res
+
+
 def groupby_per_segment(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
                         stats: Optional[RunStats] = None) -> List[GroupByPartial]:
     """What each segment's QueryRunner returns (createRunner(segment).run), one engine call each."""
@@ -1003,7 +1077,8 @@ class TimeseriesQueryRunnerFactory:
         return timeseries_per_segment(segments, query, stats)
 
     def run_merged(self, segments, query, stats=None):
-        return self.toolchest.merge(query, self.per_segment(segments, query, stats))
+        # every device's segments in one engine call, the buckets folded natively (dg_timeseries_merge)
+        return run_timeseries(segments, query, stats)
 
     def createRunner(self, segment):
         return SegmentQueryRunner(self, segment)
@@ -1032,8 +1107,16 @@ class GroupByQueryRunnerFactory(TimeseriesQueryRunnerFactory):
         return groupby_per_segment(segments, query, stats)
 
     def run_merged(self, segments, query, stats=None):
-        # the engine merges each device's segments (GroupByMergingQueryRunnerV2); devices by value
-        return self.toolchest.merge(query, groupby_per_device(segments, query, stats))
+        # the engine merges each device's segments (GroupByMergingQueryRunnerV2) and the devices'
+        # results by value on the device (dg_groupby_merge_devices: peer copies, no host merge)
+        if len(_group_by_device(segments)) == 1:
+            return self.toolchest.merge(query, groupby_per_device(segments, query, stats))
+        res = groupby_merge_devices(segments, query, stats)
+        try:
+            res.apply_limit_push_down()
+            return self.toolchest.merge(query, [res.fetch()])
+        finally:
+            res.release()
 
 
 FACTORIES = {Q.TimeseriesQuery: TimeseriesQueryRunnerFactory(), Q.TopNQuery: TopNQueryRunnerFactory(),

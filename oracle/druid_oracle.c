@@ -903,6 +903,49 @@ int or_dim_ids(void* h, const char* name, int32_t* out) {
   return done == c->total ? 0 : -1;
 }
 
+/* Rows [row0, row0 + n) of one column, decoding only the blocks that hold them (the CPU baseline's
+ * per-chunk reads, cpu_engine.c): a plain block-layout numeric column (LONGS encoding, LZ4 / LZF /
+ * UNCOMPRESSED blocks) as raw 8-byte values (`kind` OR_LONG / OR_DOUBLE, no coercion), or a
+ * single-value compressed dictionary-id column as int32 ids (kind OR_STRING). -1: other layouts. */
+int or_read_rows(void* h, const char* name, int kind, int64_t row0, int64_t n, void* out) {
+  oseg* s = (oseg*)h;
+  ocol* c = find_col(s, name);
+  if (!c || n < 0 || row0 < 0 || row0 + n > s->nrows) return -1;
+  const int ids = kind == OR_STRING;
+  if (ids ? (c->kind != OR_STRING || c->multi_value || c->vsize || !c->little_endian) : (c->kind != kind || c->long_enc != 0xFF))
+    return -1;
+  if (c->compression == 0xFE || c->size_per <= 0) return -1;
+  const int width = ids ? c->num_bytes : 8;
+  uint8_t* buf = (uint8_t*)malloc(65536 + 16);
+  int64_t r = row0;
+  int rc = 0;
+  while (r < row0 + n) {
+    const int32_t b = (int32_t)(r / c->size_per);
+    const int64_t first = (int64_t)b * c->size_per;
+    int64_t last = first + c->size_per;
+    if (last > row0 + n) last = row0 + n;
+    memset(buf, 0, 65536 + 16);
+    const int64_t got = b < c->blocks.n ? decode_block(c, b, buf, 65536 + 16) : -1;
+    if (got < (last - first) * width) {
+      rc = -1;
+      break;
+    }
+    for (int64_t k = r; k < last; ++k) {
+      const uint8_t* p = buf + (k - first) * width;
+      if (ids) {
+        uint32_t v = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+        if (width < 4) v &= (1u << (8 * width)) - 1;
+        ((int32_t*)out)[k - row0] = (int32_t)v;
+      } else {
+        memcpy((uint8_t*)out + (k - row0) * 8, p, 8);
+      }
+    }
+    r = last;
+  }
+  free(buf);
+  return rc;
+}
+
 /* CompressedVSizeColumnarInts values of a column (its blocks / num_bytes / little_endian), n of them */
 static int read_vsize_ids(ocol* c, int64_t n, int32_t* out) {
   uint8_t* buf = (uint8_t*)malloc(65536 + 16);
