@@ -391,12 +391,17 @@ def main():
     phases = {"bitmap": per_step("bitmap_ms"), "decode": per_step("decode_ms"), "aggregate": per_step("aggregate_ms"),
               "query_wall": per_step("total_ms")}
     bytes_read = per_step("bytes_read")
+    bytes_side = per_step("bytes_side")
     kernels = {}  # phase -> (kernel, algorithmic bytes per launch, launches per step, ms per step)
+    dk = "k_lzf_decode" if args.compression == "lzf" else "k_lz4_light+k_lz4_decode"
     if phases["decode"] > 0:
         # LZ4: the light decoder (literal-heavy blocks) and the general one, both inside the phase
-        dk = "k_lzf_decode" if args.compression == "lzf" else "k_lz4_light+k_lz4_decode"
-        kernels["decode"] = (dk if args.long_encoding == "longs" else dk + "+k_vsize_expand", bytes_read, 1,
+        kernels["decode"] = (dk if args.long_encoding == "longs" else dk + "+k_vsize_expand", bytes_read - bytes_side, 1,
                              phases["decode"])
+    if per_step("decode_side_ms") > 0:
+        # groupBy payload columns decoded in place on the side stream (overlapping keygen + sort)
+        phases["decode_payload_side"] = per_step("decode_side_ms")
+        kernels["decode_payload_side"] = (dk + " (payload, side stream)", bytes_side, 1, phases["decode_payload_side"])
     if isinstance(query, Q.GroupByQuery):
         phases.update({"keygen": per_step("keygen_ms"), "sort": per_step("sort_ms"), "reduce": per_step("reduce_ms")})
         passes = max(1, int(round(per_step("sort_passes"))))

@@ -192,6 +192,9 @@ typedef struct {
   int32_t sort_passes;
   int32_t key_bits;
   int64_t groups;            /* merged groups */
+  /* groupBy: payload columns decoded in place on the side stream, overlapping the key build + sort */
+  double decode_side_ms;     /* device time of those decodes (their own stream) */
+  int64_t bytes_side;        /* their algorithmic bytes (part of bytes_read) */
 } dg_metrics;
 
 /* Aggregate values are returned in 8-byte slots: int64 for count/long*, double for double*,

@@ -70,7 +70,8 @@ class dg_metrics(ctypes.Structure):
                 ("bitmap_ms", ctypes.c_double), ("decode_ms", ctypes.c_double),
                 ("aggregate_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("keygen_ms", ctypes.c_double), ("sort_ms", ctypes.c_double), ("reduce_ms", ctypes.c_double),
-                ("sort_passes", ctypes.c_int32), ("key_bits", ctypes.c_int32), ("groups", ctypes.c_int64)]
+                ("sort_passes", ctypes.c_int32), ("key_bits", ctypes.c_int32), ("groups", ctypes.c_int64),
+                ("decode_side_ms", ctypes.c_double), ("bytes_side", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1003,6 +1003,8 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.wide = b.cp_wide[k];
   j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
   j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
+  j.vstride = 0;
+  j.pad_ = 0;
   return j;
 }
 
@@ -1101,6 +1103,29 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
   return DG_OK;
 }
 
+// A plain 8-byte LZ4 value column decoded straight into column `a` of the groupBy payload records
+// ([rows][pw] words, row ref row_base + r): the value is its aggregator's input as is (longSum of a
+// long column, doubleSum of a double column), so the decoded block needs no second pass (the keygen
+// leaves that column alone). Returns false when the column is not of that form (the caller then
+// takes the ordinary view).
+static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int pw, int a, uint32_t row_base,
+                         DecodeBatch* db) {
+  const BlockColumn& b = c->data;
+  const bool ident = (agg_kind == DG_AGG_LONG_SUM && c->type == DG_COL_LONG) ||
+                     (agg_kind == DG_AGG_DOUBLE_SUM && c->type == DG_COL_DOUBLE);
+  if (!ident || c->multi_value || b.codec != CODEC_LZ4 || b.vbits || b.width != 8 || !payload) return false;
+  db->bytes += b.stored_bytes + b.index_bytes;
+  for (int32_t k = 0; k < b.nblocks; ++k) {
+    const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
+    if (rows <= 0) continue;
+    const int64_t r0 = (int64_t)row_base + (int64_t)k * b.size_per;
+    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(payload + (size_t)r0 * pw + a), (int32_t)(rows * 8));
+    j.vstride = pw * 8;
+    db->jobs.push_back(j);
+  }
+  return true;
+}
+
 static int run_expands(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
   if (db->expands.empty()) return DG_OK;
   const int n = (int)db->expands.size();
@@ -1160,18 +1185,14 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   // wide blocks (more than 8192 sequences) go to their own launch of the decoder (twice the
   // per-thread sequence registers)
   // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
-  // blocks per CU); DG_LZ4_NO_LIGHT=1 sends them through the general decoder (A/B)
-  static const bool no_light = getenv("DG_LZ4_NO_LIGHT") != nullptr;
-  const int nh = no_light ? n
-                          : (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.light; }) -
-                                  db->jobs.begin());
+  // blocks per CU)
+  const int nh = (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.light; }) -
+                       db->jobs.begin());
   const int nn = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
                        db->jobs.begin());
-#ifndef DG_NO_LPT
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
   if (nn <= 16 * 256) std::stable_sort(db->jobs.begin(), db->jobs.begin() + nn, by_ncp);
   if (nh - nn <= 16 * 256) std::stable_sort(db->jobs.begin() + nn, db->jobs.begin() + nh, by_ncp);
-#endif
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
   int32_t* d_err = call_err(cs, st);
@@ -1399,6 +1420,8 @@ int dg_context_create(int device, dg_context** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) hipEventCreate(&e);
+  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) ctx->side = nullptr;
+  for (auto& e : ctx->side_ev) hipEventCreate(&e);
   *out = reinterpret_cast<dg_context*>(ctx);
   return DG_OK;
 }
@@ -1408,7 +1431,12 @@ void dg_context_release(dg_context* c) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
+  if (ctx->side) {
+    hipStreamSynchronize(ctx->side);
+    hipStreamDestroy(ctx->side);
+  }
   for (auto& e : ctx->ev) hipEventDestroy(e);
+  for (auto& e : ctx->side_ev) hipEventDestroy(e);
   for (auto& b : ctx->free_blocks) hipFree(b.first);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1501,6 +1529,15 @@ int read_time_bounds(Segment* seg) {
 // ------------------------------------------------------------------------------------------------
 // common per-call setup
 // ------------------------------------------------------------------------------------------------
+// joins the side stream on every exit of a call that launched work on it (its kernels write into the
+// call's scratch, which the next call reuses)
+struct SideJoin {
+  hipStream_t s = nullptr;
+  ~SideJoin() {
+    if (s) hipStreamSynchronize(s);
+  }
+};
+
 struct CallGuard {
   Context* ctx;
   std::unique_lock<std::mutex> lock;
@@ -1606,8 +1643,7 @@ static bool has_float_sum(const AggPlan& plan) {
 
 // device buffers of a sort-based grouping of at most `cap` rows with keys of key_bits bits (call
 // scratch): one 8-byte word per element [key | row ref] when both fit, else keys + a u32 ref array
-static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bits, int pw, SortBufs* sb,
-                     bool carry_payload = false) {
+static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bits, int pw, SortBufs* sb) {
   memset(sb, 0, sizeof *sb);
   sb->cap = cap;
   sb->ntiles_sort = sort_tiles(cap);
@@ -1621,12 +1657,7 @@ static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bi
     if (!sb->keys[k] || (!packed && !sb->refs[k])) return set_error(DG_ERR_OOM, "sort buffers of %lld rows", (long long)cap);
   }
   sb->pw = pw;
-  if (carry_payload && packed) {  // [pw][c] words, ping-pong buffers moved by the sort
-    sb->pcap = (int64_t)c;
-    sb->payload = dev_take<uint64_t>(cs, c * (size_t)std::max(pw, 1));
-    sb->payload2 = dev_take<uint64_t>(cs, c * (size_t)std::max(pw, 1));
-    if (!sb->payload || !sb->payload2) return set_error(DG_ERR_OOM, "payload of %lld rows", (long long)cap);
-  } else if (pw > 0) {
+  if (pw > 0) {
     sb->payload = dev_take<uint64_t>(cs, c * (size_t)pw);
     if (!sb->payload) return set_error(DG_ERR_OOM, "payload of %lld rows", (long long)cap);
   }
@@ -3075,9 +3106,32 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   hipEventRecord(ctx->ev[0], st);
   std::vector<GbJob> gj(n);
   std::vector<int64_t> rows(n, 0);
+  // one element per row unless a grouping dimension is multi-value: then the payload is indexed by
+  // the row (row-ref mode) and sized before the decodes, so plain LZ4 value columns decode straight
+  // into it (payload_view)
   bool any_multi = false;
+  int64_t row_total = 0;
+  int ntiles_rows = 0;
+  std::vector<uint32_t> row_base(n, 0);
+  for (int i = 0; i < n; ++i) {
+    if (!cur[i].any) continue;
+    for (int d = 0; d < nd; ++d) {
+      const Column* c = sv[i]->find(gb->dimensions[d]);
+      any_multi |= c && c->multi_value;
+    }
+    row_base[i] = (uint32_t)row_total;
+    row_total += sv[i]->nrows;
+    ntiles_rows += (int)((sv[i]->nrows + kTileRows - 1) / kTileRows);
+  }
+  if (row_total >= (1ll << 32)) return set_error(DG_ERR_UNSUPPORTED, "%lld rows in one call (row refs are 32-bit)", (long long)row_total);
+  SortBufs sb;
+  if (!any_multi) {
+    rc = sort_bufs(cs, row_total, std::max(ntiles_rows, 1), key_bits, na, &sb);
+    if (rc) return rc;
+    sb.row_refs = 1;
+  }
   std::vector<const unsigned long long*> counts(n, nullptr);
-  DecodeBatch db;
+  DecodeBatch db, db_side;  // db_side: payload columns decoded in place (side stream)
   for (int i = 0; i < n; ++i) {
     GbJob& j = gj[i];
     memset(&j, 0, sizeof j);
@@ -3107,7 +3161,6 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
         rc = multi_view(c, cs, &db, &j.dims[d], &j.moff[d], st);
         if (rc) return rc;
         j.multi = 1;
-        any_multi = true;
         j.remap[d] = md[d]->remap[i] ? md[d]->remap[i]->as<int32_t>() : nullptr;
       } else if (c) {
         rc = column_view(c, cs, &db, &j.dims[d], st);
@@ -3121,17 +3174,45 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
       j.dim_bits[d] = lay.dim_bits[d];
     }
     for (int a = 0; a < na; ++a) {
+      const Column* ac = q->aggs[a].field ? seg->find(q->aggs[a].field) : nullptr;
+      if (!any_multi && ac && !(q->aggs[a].filter && q->aggs[a].n_filter > 0) &&
+          payload_view(ac, q->aggs[a].kind, sb.payload, na, a, row_base[i], &db_side)) {
+        j.inplace |= 1u << a;
+        j.vals[a].kind = VIEW_ABSENT;
+        continue;
+      }
       rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
       if (rc) return rc;
     }
     rows[i] = seg->nrows;
   }
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  // The payload columns only meet the keys at the reduce: they decode on the side stream while the
+  // main stream decodes the key columns, builds the keys and sorts them (the general LZ4 decoder is
+  // LDS / latency bound, the sort HBM bound, so the two overlap on the CUs).
+  SideJoin side_join;
+  const bool side = ctx->side && !db_side.jobs.empty();
+  if (side) {
+    if (!call_err(cs, st)) return set_error(DG_ERR_OOM, "error word");
+    DG_FLUSH(cs, st);  // everything staged so far leaves on the main stream first
+    hipEventRecord(ctx->side_ev[0], st);
+    DG_HIP(hipStreamWaitEvent(ctx->side, ctx->side_ev[0], 0));
+    side_join.s = ctx->side;
+    hipEventRecord(ctx->side_ev[1], ctx->side);
+    rc = run_decodes_only(cs, &db_side, ctx->side, nullptr);
+    if (rc) return rc;
+    hipEventRecord(ctx->side_ev[2], ctx->side);
+  } else {
+    db.jobs.insert(db.jobs.end(), db_side.jobs.begin(), db_side.jobs.end());
+    db.bytes += db_side.bytes;
+    db_side.bytes = 0;
+  }
   hipEventRecord(ctx->ev[1], st);
   rc = run_decodes(cs, &db, st);
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
-  m.bytes_read = db.bytes;
+  m.bytes_read = db.bytes + db_side.bytes;
+  m.bytes_side = db_side.bytes;
   GbJob* d_jobs;
   int32_t* d_tile;
   int ntiles = 0;
@@ -3141,81 +3222,21 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   if (any_multi) {  // rows explode into one element per grouping: count them first to size the sort
     rc = count_elements(cs, d_jobs, d_tile, ntiles, &total, st);
     if (rc) return rc;
+    rc = sort_bufs(cs, total, ntiles, key_bits, na, &sb);
+    if (rc) return rc;
   }
-  // high-cardinality keys whose top kBucketBits bits spread the elements into small buckets: the
-  // bucketed sort (payload carried, reduce without a random gather); else LSD passes over the whole
-  // key and the reduce gathers each element's payload record by its row ref
-  // (DG_BUCKETED / DG_NO_BUCKETED / DG_BUCKET_BITS: A/B and the tests' way to force the path, small
-  // buckets or the fallback)
-  // Bucket count: the fewest top key bits whose used prefixes (fields uniform over their used
-  // values, most significant first: bucket index, then the dimensions) put ~1300 elements or fewer
-  // in a bucket on average, so the largest stays under kBucketCap.
-  auto used_prefixes = [&](int B) {
-    int64_t distinct = 1;
-    int rem = B;
-    const int64_t nbuck = lay.bucket_bits ? (gend - gb0) / std::max<int64_t>(q->period_ms, 1) + 1 : 1;
-    std::vector<std::pair<int, int64_t>> fields;  // (bits, used values)
-    if (lay.bucket_bits) fields.push_back({lay.bucket_bits, nbuck});
-    for (int d = 0; d < nd; ++d) fields.push_back({lay.dim_bits[d], std::max<int64_t>((int64_t)md[d]->values.size(), 1)});
-    for (auto& f : fields) {
-      if (rem <= 0) break;
-      if (rem >= f.first) {
-        distinct *= f.second;
-        rem -= f.first;
-      } else {
-        const int64_t span = 1ll << (f.first - rem);
-        distinct *= (f.second + span - 1) / span;
-        rem = 0;
-      }
-    }
-    return std::max<int64_t>(distinct, 1);
-  };
-  const char* bb_env = getenv("DG_BUCKET_BITS");
-  int bbits = bb_env ? std::max(1, std::min(kBucketBits, atoi(bb_env))) : 0;
-  if (!bb_env)
-    for (int B = 12; B <= kBucketBits && !bbits; ++B)
-      if (total <= 1300 * used_prefixes(B)) bbits = B;
-  // Opt-in (DG_BUCKETED=1): measured on the headline it loses — three payload-carrying passes (1.06 ms
-  // each) + the bucket sort (2.3 ms) cost more than the random gather they remove (reduce 5.5 -> 4.5
-  // ms): 20.5 vs 18.5 ms/step on the same box.
-  const bool bucketed = (getenv("DG_BUCKETED") || bb_env) && !getenv("DG_NO_BUCKETED") && bbits > 0 &&
-                        key_bits > bbits + 2 && na <= 4 &&
-                        key_bits + bits_for(std::max<int64_t>(total, 1)) <= 64;
-  SortBufs sb;
-  rc = sort_bufs(cs, total, ntiles, key_bits, na, &sb, bucketed);
-  if (rc) return rc;
   uint32_t* h_n = host_take<uint32_t>(cs, 4);
-  uint32_t* d_bk = bucketed ? dev_take<uint32_t>(cs, ((size_t)2 << kBucketBits) + 4) : nullptr;
-  if (!h_n || (bucketed && !d_bk)) return set_error(DG_ERR_OOM, "groupBy counters");
-  uint32_t* d_ovf = bucketed ? d_bk + ((size_t)2 << kBucketBits) : nullptr;
-  if (d_ovf) DG_HIP(hipMemsetAsync(d_ovf, 0, 4, st));
+  if (!h_n) return set_error(DG_ERR_OOM, "groupBy counters");
   DG_FLUSH(cs, st);
   hipEventRecord(ctx->ev[3], st);
   launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi);
   hipEventRecord(ctx->ev[5], st);
-  if (!bucketed || !sort_bucketed(&sb, key_bits, bbits, d_bk, d_bk + ((size_t)1 << kBucketBits), d_ovf, st))
-    launch_radix_sort(&sb, key_bits, st);
+  launch_radix_sort(&sb, key_bits, st);
   hipEventRecord(ctx->ev[6], st);
   launch_run_heads(&sb, st);
   DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));
-  if (d_ovf) DG_HIP(hipMemcpyAsync(h_n + 2, d_ovf, 4, hipMemcpyDeviceToHost, st));
   rc = finish_call(cs, st);  // the result is sized by the group count
   if (rc) return rc;
-  if (d_ovf && h_n[2]) {
-    // a bucket was too large for the workgroup sort (skewed keys): run the classic path instead
-    sb.cur = 0;
-    sb.pcap = 0;
-    sb.payload2 = nullptr;
-    DG_FLUSH(cs, st);
-    launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi);
-    hipEventRecord(ctx->ev[5], st);
-    launch_radix_sort(&sb, key_bits, st);
-    hipEventRecord(ctx->ev[6], st);
-    launch_run_heads(&sb, st);
-    DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));
-    rc = finish_call(cs, st);
-    if (rc) return rc;
-  }
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
   const int64_t nsel = h_n[0], ng = h_n[1];
   std::unique_ptr<dg_result> res(new dg_result());
@@ -3243,13 +3264,20 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     uint64_t* carry_slots = dev_take<uint64_t>(cs, (size_t)kRedWaves * nt * rec);
     if ((has_float_sum(plan) && !head_pos) || !carry_g || !open_g || !carry_slots)
       return set_error(DG_ERR_OOM, "groupBy reduce scratch");
+    if (side) DG_HIP(hipStreamWaitEvent(st, ctx->side_ev[2], 0));  // the payload is decoded
     launch_gb_reduce(&sb, plan, res->keys, res->slots, ng, head_pos, carry_g, carry_slots, open_g, st);
     for (int a = 0; a < na; ++a)
       if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, ntiles, &sb, plan, a, head_pos, res->slots, ng, st);
   }
   hipEventRecord(ctx->ev[4], st);
+  if (side) DG_HIP(hipStreamWaitEvent(st, ctx->side_ev[2], 0));  // (no groups: no reduce waited)
   rc = finish_call(cs, st);
   if (rc) return rc;
+  if (side) {
+    float fs = 0;
+    hipEventElapsedTime(&fs, ctx->side_ev[1], ctx->side_ev[2]);
+    m.decode_side_ms = fs;
+  }
   for (int i = 0; i < n; ++i)
     if (cur[i].any) m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : sv[i]->nrows;
   m.selected_rows = nsel;

@@ -61,6 +61,11 @@ struct Lz4Job {
   int32_t light;       // few sequences, short copy chains: decoded by the light kernel (k_lz4_light);
                        // > 0: sequences per light checkpoint (cp[ncp .. ncp + nfine) = the light checkpoints)
   int32_t nfine;       // light checkpoints (one per light-decoder thread)
+  // 0: the block's bytes go to dst contiguously (a decode slot). > 0: the block holds 8-byte values
+  // and value v goes to dst + v * vstride (a column of the groupBy payload records, written in place);
+  // bytes past expect_len are then not written (they would land in the next segment's records)
+  int32_t vstride;
+  int32_t pad_;
 };
 
 // Light blocks (literal-heavy: random ids, high-entropy values): at most kLtMaxCps checkpoint
@@ -155,6 +160,7 @@ struct GbJob {
   ColView moff[kMaxGroupDims];           // multi-value dimension: row value offsets (VIEW_ABSENT otherwise)
   int32_t multi;                         // some dimension is multi-value: rows explode into groupings
   int32_t skip_empty;                    // an empty value list yields no element (topN) instead of null (groupBy)
+  uint32_t inplace;                      // row-ref mode: payload columns the LZ4 decoder wrote (bit a)
   const int32_t* remap[kMaxGroupDims];  // local dictionary id -> merged id (null: identity)
   int32_t null_gid[kMaxGroupDims];      // merged id of the null value (a missing dimension's rows)
   int32_t dim_shift[kMaxGroupDims];
@@ -172,10 +178,10 @@ struct SortBufs {
   uint64_t* keys[2];      // packed (refs null): [key | row ref in the low ref_bits bits]; else keys
   uint32_t* refs[2];      // row refs when the key and the ref do not fit one word, else null
   int ref_bits;           // packed: bits of the element index (the sort key starts there); else 0
-  uint64_t* payload;      // the aggregators' inputs of each element (device slot encoding): [cap][pw] by
-                          // element index, or (pcap != 0) [pw][pcap] by sorted position, carried by the sort
-  uint64_t* payload2;     // pcap != 0: the other buffer of the carried payload
-  int64_t pcap;
+  uint64_t* payload;      // the aggregators' inputs of each element (device slot encoding): [cap][pw]
+                          // by element reference
+  int row_refs;           // element reference = the row's index over the call (one element per row,
+                          // payload columns may be decoded in place); else the element index
   int pw;
   int cur;                // which of the ping-pong buffers holds the result
   uint32_t* tile_cnt;     // keygen tiles: selected rows, then their offsets
@@ -297,6 +303,10 @@ struct Context {
   DevBuf scratch[6];
   DevBuf pinned_dummy;
   hipEvent_t ev[8] = {};
+  // side stream: the groupBy payload columns decode on it while the main stream builds and sorts the
+  // keys (the two only meet at the reduce); side_ev[0] = its inputs are staged, [1..2] = decode span
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev[3] = {};
   // dg_context_set_limit(DG_LIMIT_GROUP_ELEMENTS): most sort elements one groupBy call may build
   uint64_t max_elements = ~0ull;
   std::vector<std::shared_ptr<MergedDict>> dict_cache;  // most recent last
@@ -477,13 +487,6 @@ void launch_gb_count_total(const GbJob* d_jobs, const int32_t* d_tile_job, int n
 void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
                       hipStream_t s, bool multi = false);
 // stable LSD radix sort of sb->keys/refs[cur] on key bits [0, key_bits)
-// bucketed sort (payload carried, sb->pcap != 0, packed keys): top kBucketBits key bits by LSD passes,
-// then each bucket (<= kBucketCap elements, else *overflow is set) sorted in LDS; false = not applicable.
-// bstart / bend: 1 << bucket_bits words each (bucket_bits <= kBucketBits).
-constexpr int kBucketBits = 17;  // at most this many bucket bits (chosen per query)
-constexpr int kBucketCap = 2048;
-bool sort_bucketed(SortBufs* sb, int key_bits, int bucket_bits, uint32_t* bstart, uint32_t* bend, uint32_t* overflow,
-                   hipStream_t s);
 void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s);
 // run heads of the sorted keys: sb->run_cnt = per-tile offsets, sb->n[1] = runs
 void launch_run_heads(SortBufs* sb, hipStream_t s);

@@ -163,15 +163,9 @@ __device__ int block_scan_lz(int v, int* total, int* s_tmp) {
 
 // E is skewed by one dword every 128 entries so that the threads of a wave, whose intervals start
 // ~128 output bytes apart in token-dense blocks, write different LDS banks.
-#ifndef DG_LZ_NOSKEW
 constexpr int kESkewShift = 7;
 constexpr int kEWords = kBlockBytes + (kBlockBytes >> kESkewShift) * 2;  // u16 entries incl. skew
 __device__ __forceinline__ int eph(int x) { return x + ((x >> kESkewShift) << 1); }
-#else
-constexpr int kESkewShift = 16;
-constexpr int kEWords = kBlockBytes;
-__device__ __forceinline__ int eph(int x) { return x; }
-#endif
 
 struct LzState {
   uint16_t* e;
@@ -247,6 +241,30 @@ __device__ __forceinline__ int wave_alloc(int* counter, int n) {
 // cooperative-copy job: x = output start | (len - 1) << 16, y = literal input offset (kind 0) or
 // match distance | 1 << 31 (kind 1)
 __device__ __forceinline__ int job_len(uint2 j) { return (int)(j.x >> 16) + 1; }
+
+// Output of decoded bytes [16c, 16c + 16): a 16-byte store into a slot, or with job.vstride the two
+// 8-byte values to their payload records (only values inside the block's expect_len)
+__device__ __forceinline__ void out16(const Lz4Job& job, int c, const uint32_t w[4]) {
+  if (!job.vstride) {
+    reinterpret_cast<uint4*>(job.dst)[c] = make_uint4(w[0], w[1], w[2], w[3]);
+    return;
+  }
+  const int v = 2 * c;
+  if ((v + 1) * 8 <= job.expect_len)
+    *reinterpret_cast<uint2*>(job.dst + (size_t)v * job.vstride) = make_uint2(w[0], w[1]);
+  if ((v + 2) * 8 <= job.expect_len)
+    *reinterpret_cast<uint2*>(job.dst + (size_t)(v + 1) * job.vstride) = make_uint2(w[2], w[3]);
+}
+
+// decoded bytes [x, x + 4) (x % 4 == 0) as one dword store (same placement rules as out16)
+__device__ __forceinline__ void out4(const Lz4Job& job, int x, uint32_t w) {
+  if (!job.vstride) {
+    reinterpret_cast<uint32_t*>(job.dst)[x >> 2] = w;
+    return;
+  }
+  if (((x >> 3) + 1) * 8 <= job.expect_len)
+    *reinterpret_cast<uint32_t*>(job.dst + (size_t)(x >> 3) * job.vstride + (x & 7)) = w;
+}
 
 template <bool PROF, int SEQ>
 __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
@@ -804,7 +822,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
   }
   // ---- 4. output: every entry is a literal code or one hop from one; 16 bytes per 16-byte store ----
-  uint4* dst = reinterpret_cast<uint4*>(job.dst);
   const int nchunks = (total + 15) >> 4;
   for (int c = tid; c < nchunks; c += kLzThreads) {
     const int x0 = c << 4;
@@ -840,7 +857,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         w[q] = acc;
       }
     }
-    dst[c] = make_uint4(w[0], w[1], w[2], w[3]);
+    out16(job, c, w);
   }
   if (PROF) {
     __syncthreads();
@@ -891,11 +908,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   // output reads literals from LDS; otherwise over the input (literals from L2)
   const int nsq = ncp * g;
   const int in_words = ((n + 15) >> 4) * 4 + 4;  // staged input + one zero uint4
-#ifndef DG_LT_NOKEEP
   const bool keep_in = in_words + (nsq + 1) + 3 * nsq + (nsq + 1) / 2 <= kLtBufWords;
-#else
-  const bool keep_in = false;  // (A/B: literals always from L2)
-#endif
   uint32_t* s_start = s_buf + (keep_in ? in_words : 0);  // [nsq + 1] output start of every sequence, then the total
   uint32_t* s_mst = s_start + nsq + 1;                    // [nsq] output start of its match
   uint32_t* s_lit = s_mst + nsq;                          // [nsq] input offset of its literals
@@ -1033,7 +1046,6 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   // ---- 3. output: 16-byte chunks ----
   const uint8_t* __restrict__ in = job.src;
   const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
-  uint4* dst = reinterpret_cast<uint4*>(job.dst);
   const int nchunks = (total + 15) >> 4;
   bool fail = false;
   // the source of output byte x: its literal position (a literal byte, a resolved match byte, or
@@ -1059,7 +1071,6 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
     }
     return -1;
   };
-  uint32_t* dst32 = reinterpret_cast<uint32_t*>(job.dst);
   const int nsteps = (nchunks + 2 * kLtThreads - 1) / (2 * kLtThreads);
   for (int it = 0; it < nsteps; ++it) {  // (wave-uniform trip count: the per-byte pass shuffles)
     // two chunks per step: their literal loads are issued together
@@ -1086,7 +1097,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
       uint32_t w[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) w[q] = sh ? __builtin_amdgcn_alignbyte(v[u][q + 1], v[u][q], sh) : v[u][q];
-      dst[c0 + u * kLtThreads] = make_uint4(w[0], w[1], w[2], w[3]);
+      out16(job, c0 + u * kLtThreads, w);
     }
     // the wave's other chunks, four at a time with one lane per byte: every byte resolves on its own
     // (no per-byte serial walk in one lane), bytes pack into dwords across lanes
@@ -1115,7 +1126,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
           else b = keep_in ? (uint32_t)s_in[sp] : (uint32_t)in[sp];
         }
         const uint32_t b1 = __shfl_down(b, 1, 64), b2 = __shfl_down(b, 2, 64), b3 = __shfl_down(b, 3, 64);
-        if (sub < k && (bi & 3) == 0) dst32[cc * 4 + (bi >> 2)] = b | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        if (sub < k && (bi & 3) == 0) out4(job, cc * 16 + bi, b | (b1 << 8) | (b2 << 16) | (b3 << 24));
       }
     }
   }

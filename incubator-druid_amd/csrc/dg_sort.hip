@@ -82,11 +82,9 @@ __global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ a, int
   if (threadIdx.x == 0) *total = carry;
 }
 
-// payload word a of element / position i: by element index ([i][pw], pcap == 0) or carried by the
-// sort ([a][pcap], i = sorted position)
-__device__ __forceinline__ size_t pay_at(int pw, int64_t pcap, size_t i, int a) {
-  return pcap ? (size_t)a * (size_t)pcap + i : i * (size_t)pw + (size_t)a;
-}
+// payload word a of the element with reference i ([i][pw] words: i = the element index, or in
+// row-ref mode the row's index over the call's segments)
+__device__ __forceinline__ size_t pay_at(int pw, size_t i, int a) { return i * (size_t)pw + (size_t)a; }
 
 // segment of an element index (or row ref): the last job whose base <= it (bases ascend)
 __device__ __forceinline__ int locate_seg(const uint32_t* s_base, int njobs, uint32_t ref) {
@@ -220,31 +218,42 @@ __device__ __forceinline__ uint32_t elem_ref(uint64_t w, const uint32_t* refs, i
 }
 
 // Selected rows in (segment, row) order get consecutive element indices; the element's sort word
-// carries its index (packed) or the ref array does. The aggregators' inputs of the element are
-// written at payload[index * pw] in the device slot encoding, in row order (coalesced column reads),
-// so the reduce after the sort gathers one payload record per element instead of one random read
-// per column.
+// carries its reference (packed) or the ref array does. The reference is the element index, or in
+// row-ref mode (`rowref`: no multi-value dimension, one element per row) the row's index over the
+// call's segments (row_base + r). The aggregators' inputs of the element are written at
+// payload[ref * pw] in the device slot encoding, in row order (coalesced column reads), so the
+// reduce after the sort gathers one payload record per element instead of one random read per
+// column. In row-ref mode the payload columns in `j.inplace` were written by the LZ4 decoder
+// itself (payload_view: the decoded value is the aggregator's input) and are left alone.
 template <bool MULTI>
 __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                    const uint32_t* __restrict__ offs, uint64_t* __restrict__ keys,
                                                    uint32_t* __restrict__ refs, int kshift, AggPlan plan,
-                                                   uint64_t* __restrict__ payload, int pw, int64_t pcap) {
+                                                   uint64_t* __restrict__ payload, int pw, int rowref) {
   __shared__ uint32_t s_tmp[4];
   const GbJob& j = jobs[tile_job[blockIdx.x]];
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
   const int64_t r1 = min((int64_t)j.nrows, r0 + kTileRows);
   uint32_t base = offs[blockIdx.x];
-#ifndef DG_KEYGEN_NOFAST
-  constexpr bool kFast = true;
-#else
-  constexpr bool kFast = false;
-#endif
-#ifndef DG_KEYGEN_NODIRECT
-  constexpr bool kDirect = true;
-#else
-  constexpr bool kDirect = false;
-#endif
-  if (kFast && !MULTI && !j.bitset && j.time.kind == VIEW_ABSENT) {
+  const uint32_t inplace = rowref ? j.inplace : 0u;
+  const bool all_inplace = pw > 0 && inplace == (pw >= 32 ? 0xFFFFFFFFu : (1u << pw) - 1u);
+  // the element's sort word(s) and payload record
+  auto emit = [&](uint32_t idx, uint32_t ref, uint64_t key, auto&& val) {
+    if (refs) {
+      keys[idx] = key;
+      refs[idx] = ref;
+    } else {
+      keys[idx] = (key << kshift) | ref;
+    }
+    if (all_inplace) return;
+    if (pw == 2 && !inplace) {
+      *reinterpret_cast<ulonglong2*>(payload + (size_t)ref * 2) = make_ulonglong2(val(0), val(1));
+    } else {
+      for (int a = 0; a < pw; ++a)
+        if (!((inplace >> a) & 1u)) payload[pay_at(pw, ref, a)] = val(a);
+    }
+  };
+  if (!MULTI && !j.bitset && j.time.kind == VIEW_ABSENT) {
     // every row of the tile is selected (no filter, the interval covers the segment): element index =
     // tile base + row offset, no per-block scan.
     // A tile (kTileRows, aligned) lies inside one block of every view (blocks hold >= 8192 rows):
@@ -255,8 +264,9 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
       direct &= j.dims[d].kind != VIEW_IDS ||
                 (!(j.dims[d].pad & kViewBigEndian) && (r0 >> j.dims[d].log2_per) == ((r1 - 1) >> j.dims[d].log2_per));
     for (int a = 0; a < pw; ++a)
-      direct &= j.vals[a].kind == VIEW_ABSENT || (r0 >> j.vals[a].log2_per) == ((r1 - 1) >> j.vals[a].log2_per);
-    if (direct && kDirect) {
+      direct &= ((inplace >> a) & 1u) || j.vals[a].kind == VIEW_ABSENT ||
+                (r0 >> j.vals[a].log2_per) == ((r1 - 1) >> j.vals[a].log2_per);
+    if (direct) {
       for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
         const uint32_t idx = base + (uint32_t)(r - r0);
         uint64_t key = ((uint64_t)j.seg_slot << j.seg_shift);
@@ -282,41 +292,19 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
           }
           key |= (uint64_t)g << j.dim_shift[d];
         }
-        if (refs) {
-          keys[idx] = key;
-          refs[idx] = idx;
-        } else {
-          keys[idx] = (key << kshift) | idx;
-        }
-        auto val = [&](int a) -> uint64_t {
+        emit(idx, rowref ? j.row_base + (uint32_t)r : idx, key, [&](int a) -> uint64_t {
           const ColView& v = j.vals[a];
           if (!agg_row(j.agg_bits[a], r)) return identity_of(plan.op[a], plan.kind[a]);
           if (plan.kind[a] == DG_AGG_COUNT || v.kind == VIEW_ABSENT) return agg_input_at(plan.kind[a], v.kind, nullptr);
           const int64_t blk = r0 >> v.log2_per;
           return agg_input_at(plan.kind[a], v.kind, v.blocks[blk] + (size_t)(r - (blk << v.log2_per)) * (size_t)v.width);
-        };
-        if (pw == 2 && !pcap) {
-          *reinterpret_cast<ulonglong2*>(payload + (size_t)idx * 2) = make_ulonglong2(val(0), val(1));
-        } else {
-          for (int a = 0; a < pw; ++a) payload[pay_at(pw, pcap, idx, a)] = val(a);
-        }
+        });
       }
       return;
     }
     for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
       const uint32_t idx = base + (uint32_t)(r - r0);
-      const uint64_t key = gb_key(j, r, 0);
-      if (refs) {
-        keys[idx] = key;
-        refs[idx] = idx;
-      } else {
-        keys[idx] = (key << kshift) | idx;
-      }
-      if (pw == 2 && !pcap) {
-        *reinterpret_cast<ulonglong2*>(payload + (size_t)idx * 2) = make_ulonglong2(agg_in(j, plan, 0, r), agg_in(j, plan, 1, r));
-      } else {
-        for (int a = 0; a < pw; ++a) payload[pay_at(pw, pcap, idx, a)] = agg_in(j, plan, a, r);
-      }
+      emit(idx, rowref ? j.row_base + (uint32_t)r : idx, gb_key(j, r, 0), [&](int a) { return agg_in(j, plan, a, r); });
     }
     return;
   }
@@ -328,31 +316,15 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
     if (MULTI) {  // every grouping of the row is an element with the row's aggregator inputs
       const uint32_t nf = sel ? gb_fanout(j, r) : 0u;
       const uint32_t ex = block_scan_u32<256>(nf, &tot, s_tmp);
-      for (uint32_t e = 0; e < nf; ++e) {
-        const uint32_t idx = base + ex + e;
-        const uint64_t key = gb_key_multi(j, r, b, e);
-        if (refs) {
-          keys[idx] = key;
-          refs[idx] = idx;
-        } else {
-          keys[idx] = (key << kshift) | idx;
-        }
-        for (int a = 0; a < pw; ++a) payload[pay_at(pw, pcap, idx, a)] = agg_in(j, plan, a, r);
-      }
+      for (uint32_t e = 0; e < nf; ++e)
+        emit(base + ex + e, base + ex + e, gb_key_multi(j, r, b, e), [&](int a) { return agg_in(j, plan, a, r); });
       base += tot;
       continue;
     }
     const uint32_t ex = block_scan_u32<256>(sel ? 1u : 0u, &tot, s_tmp);
-    if (sel) {
-      const uint32_t idx = base + ex;
-      if (refs) {
-        keys[idx] = gb_key(j, r, b);
-        refs[idx] = idx;
-      } else {
-        keys[idx] = (gb_key(j, r, b) << kshift) | idx;
-      }
-      for (int a = 0; a < pw; ++a) payload[pay_at(pw, pcap, idx, a)] = agg_in(j, plan, a, r);
-    }
+    if (sel)
+      emit(base + ex, rowref ? j.row_base + (uint32_t)r : base + ex, gb_key(j, r, b),
+           [&](int a) { return agg_in(j, plan, a, r); });
     base += tot;
   }
 }
@@ -377,10 +349,10 @@ void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles
   launch_gb_count(d_jobs, d_tile_job, ntiles, sb->tile_cnt, sb->n, multi, s);
   if (multi)
     hipLaunchKernelGGL(k_gb_keygen<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->pcap);
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, 0);
   else
     hipLaunchKernelGGL(k_gb_keygen<false>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->pcap);
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->row_refs);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -534,118 +506,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   }
 }
 
-// The same pass over packed words with the element's payload words carried along (sb->pcap != 0:
-// [pw][pcap] buffers): each payload word follows its key through the tile's LDS reorder, so the
-// stores stay coalesced and the payload ends up in sorted order.
-template <int PW>
-__global__ __launch_bounds__(kST) void k_rs_scatter_pay(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
-                                                        const uint64_t* __restrict__ pin, uint64_t* __restrict__ pout,
-                                                        int64_t pcap, const uint32_t* __restrict__ n_ptr, int shift,
-                                                        int bits, const uint32_t* __restrict__ hist,
-                                                        const uint32_t* __restrict__ bin_total, int ntiles) {
-  __shared__ uint64_t s_k[kSortTile];
-  __shared__ uint32_t s_cnt[4 * kMaxBins];
-  __shared__ int64_t s_delta[kMaxBins];
-  __shared__ uint32_t s_tmp[4];
-  const uint32_t n = *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  if (base >= n) return;
-  const int tile_n = (int)min<int64_t>(kSortTile, (int64_t)n - base);
-  const int nb = 1 << bits;
-  const uint64_t dmask = (uint64_t)(nb - 1);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < 4 * kMaxBins; i += kST) s_cnt[i] = 0;
-  __syncthreads();
-  uint64_t k[kSPT];
-  uint32_t lp[kSPT];
-  const int wbase = wave * (kSortTile / 4);
-#pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
-    const int x = wbase + c * 64 + lane;
-    k[c] = x < tile_n ? kin[base + x] : 0ull;
-  }
-  uint32_t* cnt = s_cnt + wave * kMaxBins;
-#pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
-    const bool ok = wbase + c * 64 + lane < tile_n;
-    const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
-    const uint64_t peers = match_digit(d, bits, ok);
-    uint32_t prior = 0;
-    if (ok) prior = cnt[d];
-    lp[c] = prior + lanes_below(peers);  // rank among the wave's elements of digit d
-    if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
-  }
-  __syncthreads();
-  {
-    uint32_t cw[2][4], ct[2], gt[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int d = 2 * tid + q;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) cw[q][w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
-      ct[q] = cw[q][0] + cw[q][1] + cw[q][2] + cw[q][3];
-      gt[q] = d < nb ? bin_total[d] : 0u;
-    }
-    uint32_t tot;
-    uint32_t toff = block_scan_u32<kST>(ct[0] + ct[1], &tot, s_tmp);
-    uint32_t gex = block_scan_u32<kST>(gt[0] + gt[1], &tot, s_tmp);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int d = 2 * tid + q;
-      if (d < nb) {
-        s_cnt[d] = toff;
-        s_cnt[kMaxBins + d] = toff + cw[q][0];
-        s_cnt[2 * kMaxBins + d] = toff + cw[q][0] + cw[q][1];
-        s_cnt[3 * kMaxBins + d] = toff + cw[q][0] + cw[q][1] + cw[q][2];
-        s_delta[d] = (int64_t)gex + (int64_t)hist[(size_t)d * ntiles + blockIdx.x] - (int64_t)toff;
-      }
-      toff += ct[q];
-      gex += gt[q];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
-    const bool ok = wbase + c * 64 + lane < tile_n;
-    const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
-    lp[c] = ok ? cnt[d] + lp[c] : 0xFFFFFFFFu;  // the element's place in the tile's digit order
-    if (ok) s_k[lp[c]] = k[c];
-  }
-  __syncthreads();
-  uint32_t pos[kSPT];  // global output position of tile-sorted element tid + j * kST
-#pragma unroll
-  for (int j = 0; j < kSPT; ++j) {
-    const int i = tid + j * kST;
-    pos[j] = 0;
-    if (i < tile_n) {
-      const uint64_t kk = s_k[i];
-      pos[j] = (uint32_t)(s_delta[(kk >> shift) & dmask] + i);
-      kout[pos[j]] = kk;
-    }
-  }
-#pragma unroll
-  for (int w = 0; w < PW; ++w) {
-    uint64_t pv[kSPT];
-#pragma unroll
-    for (int c = 0; c < kSPT; ++c) {
-      const int x = wbase + c * 64 + lane;
-      pv[c] = x < tile_n ? pin[(size_t)w * pcap + base + x] : 0ull;
-    }
-    __syncthreads();  // every read of s_k (previous word) is done
-#pragma unroll
-    for (int c = 0; c < kSPT; ++c)
-      if (lp[c] != 0xFFFFFFFFu) s_k[lp[c]] = pv[c];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kSPT; ++j) {
-      const int i = tid + j * kST;
-      if (i < tile_n) pout[(size_t)w * pcap + pos[j]] = s_k[i];
-    }
-  }
-}
-
-// LSD passes over key bits [lo, hi) of the key field (above the element index bits), payload carried
-// when sb->pcap != 0
+// LSD passes over key bits [lo, hi) of the key field (above the element index bits)
 static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
   const int kb = hi - lo;
   if (kb <= 0) return;
@@ -658,22 +519,7 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
     const int in = sb->cur, out = sb->cur ^ 1;
     hipLaunchKernelGGL(k_rs_hist, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->n, shift, bits, sb->hist, nt);
     hipLaunchKernelGGL(k_rs_binscan, dim3(1 << bits), dim3(1024), 0, s, sb->hist, nt, sb->bin_total);
-    if (sb->pcap) {
-      switch (sb->pw) {
-#define DG_PAY_PASS(P)                                                                                               \
-  case P:                                                                                                            \
-    hipLaunchKernelGGL(k_rs_scatter_pay<P>, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->keys[out], sb->payload,     \
-                       sb->payload2, sb->pcap, sb->n, shift, bits, sb->hist, sb->bin_total, nt);                      \
-    break;
-        DG_PAY_PASS(0)
-        DG_PAY_PASS(1)
-        DG_PAY_PASS(2)
-        DG_PAY_PASS(3)
-        DG_PAY_PASS(4)
-#undef DG_PAY_PASS
-      }
-      std::swap(sb->payload, sb->payload2);
-    } else if (sb->refs[in]) {
+    if (sb->refs[in]) {    } else if (sb->refs[in]) {
       hipLaunchKernelGGL(k_rs_scatter<true>, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
                          sb->refs[out], sb->n, shift, bits, sb->hist, sb->bin_total, nt);
     } else {
@@ -682,128 +528,6 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
     }
     sb->cur = out;
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// bucketed sort (high-cardinality keys): LSD passes carrying the payload over the top kBucketBits key
-// bits order the elements by bucket; then one workgroup per bucket sorts its (<= kBucketCap)
-// elements by the remaining key bits in LDS and permutes their payload inside the bucket's range.
-// The reduce then reads keys and payload sequentially (no random payload gather).
-// ------------------------------------------------------------------------------------------------
-__global__ void k_bucket_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, int bshift,
-                                uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
-  const uint32_t n = *n_ptr;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t b = (uint32_t)(keys[i] >> bshift);
-    if (i == 0 || (uint32_t)(keys[i - 1] >> bshift) != b) bstart[b] = (uint32_t)i;
-    if (i + 1 == n || (uint32_t)(keys[i + 1] >> bshift) != b) bend[b] = (uint32_t)(i + 1);
-  }
-}
-
-template <int PW>
-__global__ __launch_bounds__(kST) void k_bucket_sort(uint64_t* __restrict__ keys, const uint64_t* __restrict__ pin,
-                                                     uint64_t* __restrict__ pout, int64_t pcap,
-                                                     const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
-                                                     int lo_shift, int low_bits, uint32_t* __restrict__ overflow) {
-  __shared__ uint64_t s_w[2][kBucketCap];
-  __shared__ uint16_t s_p[2][kBucketCap];
-  __shared__ uint32_t s_cnt[4 * 256];
-  __shared__ uint32_t s_tmp[4];
-  const uint32_t lo = bstart[blockIdx.x], hi = bend[blockIdx.x];
-  const int m = (int)(hi - lo);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (m <= 0) return;
-  if (m > kBucketCap) {
-    if (tid == 0) atomicOr(overflow, 1u);
-    return;
-  }
-  for (int i = tid; i < m; i += kST) {
-    s_w[0][i] = keys[lo + i];
-    s_p[0][i] = (uint16_t)i;
-  }
-  constexpr int kQ = kBucketCap / 4;  // elements per wave quarter
-  int cur = 0;
-  const int npass = (low_bits + 7) / 8;
-  const int wbits = npass ? (low_bits + npass - 1) / npass : 0;
-  for (int p = 0, off = 0; p < npass; ++p, off += wbits) {
-    const int bits = min(wbits, low_bits - off);
-    const int nb = 1 << bits;
-    const int shift = lo_shift + off;
-    for (int i = tid; i < 4 * 256; i += kST) s_cnt[i] = 0;
-    __syncthreads();
-    uint32_t rank[kQ / 64];
-    uint32_t* cnt = s_cnt + wave * 256;
-#pragma unroll
-    for (int c = 0; c < kQ / 64; ++c) {  // wave w ranks its quarter [w * kQ, (w + 1) * kQ) in order
-      const int x = wave * kQ + c * 64 + lane;
-      const bool ok = x < m;
-      const uint32_t d = ok ? (uint32_t)((s_w[cur][x] >> shift) & (uint64_t)(nb - 1)) : 0u;
-      const uint64_t peers = match_digit(d, bits, ok);
-      uint32_t prior = 0;
-      if (ok) prior = cnt[d];
-      rank[c] = prior + lanes_below(peers);
-      if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
-    }
-    __syncthreads();
-    {
-      const uint32_t c0 = tid < nb ? s_cnt[tid] : 0u, c1 = tid < nb ? s_cnt[256 + tid] : 0u;
-      const uint32_t c2 = tid < nb ? s_cnt[512 + tid] : 0u, c3 = tid < nb ? s_cnt[768 + tid] : 0u;
-      uint32_t tot;
-      const uint32_t toff = block_scan_u32<kST>(c0 + c1 + c2 + c3, &tot, s_tmp);
-      if (tid < nb) {
-        s_cnt[tid] = toff;
-        s_cnt[256 + tid] = toff + c0;
-        s_cnt[512 + tid] = toff + c0 + c1;
-        s_cnt[768 + tid] = toff + c0 + c1 + c2;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < kQ / 64; ++c) {
-      const int x = wave * kQ + c * 64 + lane;
-      if (x < m) {
-        const uint64_t w = s_w[cur][x];
-        const uint32_t d = (uint32_t)((w >> shift) & (uint64_t)(nb - 1));
-        const uint32_t to = cnt[d] + rank[c];
-        s_w[cur ^ 1][to] = w;
-        s_p[cur ^ 1][to] = s_p[cur][x];
-      }
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
-  for (int i = tid; i < m; i += kST) {
-    keys[lo + i] = s_w[cur][i];
-    const size_t src = lo + s_p[cur][i];
-#pragma unroll
-    for (int w = 0; w < PW; ++w) pout[(size_t)w * pcap + lo + i] = pin[(size_t)w * pcap + src];
-  }
-}
-
-bool sort_bucketed(SortBufs* sb, int key_bits, int bucket_bits, uint32_t* bstart, uint32_t* bend, uint32_t* overflow,
-                   hipStream_t s) {
-  if (!sb->pcap || sb->refs[sb->cur] || key_bits <= bucket_bits || bucket_bits > kBucketBits) return false;
-  radix_passes(sb, key_bits - bucket_bits, key_bits, s);
-  const int bshift = sb->ref_bits + key_bits - bucket_bits;
-  (void)hipMemsetAsync(bstart, 0, sizeof(uint32_t) * ((size_t)1 << bucket_bits), s);
-  (void)hipMemsetAsync(bend, 0, sizeof(uint32_t) * ((size_t)1 << bucket_bits), s);
-  hipLaunchKernelGGL(k_bucket_bounds, dim3(4096), dim3(256), 0, s, sb->keys[sb->cur], sb->n, bshift, bstart, bend);
-  const int nbk = 1 << bucket_bits;
-  switch (sb->pw) {
-#define DG_BUCKET(P)                                                                                                  \
-  case P:                                                                                                             \
-    hipLaunchKernelGGL(k_bucket_sort<P>, dim3(nbk), dim3(kST), 0, s, sb->keys[sb->cur], sb->payload, sb->payload2,    \
-                       sb->pcap, bstart, bend, sb->ref_bits, key_bits - bucket_bits, overflow);                       \
-    break;
-    DG_BUCKET(0)
-    DG_BUCKET(1)
-    DG_BUCKET(2)
-    DG_BUCKET(3)
-    DG_BUCKET(4)
-#undef DG_BUCKET
-  }
-  std::swap(sb->payload, sb->payload2);
-  return true;
 }
 
 void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
@@ -921,7 +645,7 @@ __device__ __forceinline__ uint64_t seg_scan_wave(int op, uint64_t v, bool head,
 constexpr int kRT = 64 * kRedWaves;             // reduce threads per tile
 constexpr int kRSPT = kSortTile / kRT;          // elements per lane
 template <bool REFS>
-__global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw, int64_t pcap,
+__global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ run_off, AggPlan plan,
@@ -970,20 +694,7 @@ __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* 
 #pragma unroll
     for (int c = 0; c < kRSPT; ++c) {
       const bool valid = wbase + c * 64 + lane < tile_n;
-      if (pcap) {  // carried by the sort: sequential words at the sorted position
-        const size_t i = (size_t)(base + wbase + c * 64 + lane);
-        xr[c][0] = valid && pw >= 1 ? payload[i] : 0ull;
-        xr[c][1] = valid && pw >= 2 ? payload[(size_t)pcap + i] : 0ull;
-        continue;
-      }
-#ifdef DG_REDUCE_SEQPAY  // A/B timing only (wrong results): the gather replaced by sequential reads
-      const uint64_t* pr = payload + (size_t)(base + wbase + c * 64 + lane) * pw;
-#elif defined(DG_REDUCE_LOCALPAY)  // A/B timing only: random within a window around the position
-      const uint64_t* pr = payload + (size_t)min<int64_t>((int64_t)(((base + wbase + c * 64 + lane) & ~((1ll << DG_REDUCE_LOCALPAY) - 1)) |
-                                                   (idx_of[c] & ((1u << DG_REDUCE_LOCALPAY) - 1))), (int64_t)n - 1) * pw;
-#else
       const uint64_t* pr = payload + (size_t)idx_of[c] * pw;
-#endif
       if (pw == 2 && valid) {
         const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(pr);  // 16-byte aligned: pw == 2
         xr[c][0] = w.x;
@@ -995,14 +706,6 @@ __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* 
     }
   }
   __syncthreads();  // the tile's keys are in LDS
-#ifdef DG_REDUCE_PROBE_LOADS  // A/B timing only (wrong results): stop after the loads
-  {
-    uint64_t acc = 0;
-    for (int c = 0; c < kRSPT; ++c) acc ^= xr[c][0] ^ xr[c][1] ^ s_key[1 + wbase + c * 64 + lane];
-    if (acc == 0x5a5a5a5a5a5a5a5aull) out_keys[0] = acc;
-    return;
-  }
-#endif
   // run heads / ends of my elements, and the groups whose head lies before my share
   uint32_t hm = 0, tm = 0;
   uint32_t nh = 0;  // heads in my share
@@ -1056,15 +759,11 @@ __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* 
       if (!valid) xv = ident;
       else if (a < 0) xv = 1ull;
       else if (pw <= kRegSlots) xv = a == 0 ? xr[c][0] : xr[c][1];
-      else xv = payload[pcap ? pay_at(pw, pcap, (size_t)(base + x), a) : pay_at(pw, 0, idx_of[c], a)];
+      else xv = payload[pay_at(pw, idx_of[c], a)];
       uint64_t v = xv;
       // a chunk of singleton groups (every element a run head and end: ~3 in 4 chunks at one group per
       // row) needs no scan; otherwise the segmented scan with the open run carried in
-#ifndef DG_REDUCE_NOSKIP
       const bool single = !valid || ((hm >> c) & (tm >> c) & 1u);
-#else
-      const bool single = false;
-#endif
       if (__ballot(!single)) {
         bool f;
         v = seg_scan_wave(op, xv, (hm >> c) & 1u, &f);
@@ -1076,9 +775,6 @@ __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* 
         if (t || x == wend) {
           const int32_t gr = grel[c];
           if (gr >= 0) {  // a group headed in my share: complete, or open at the share's end
-#ifdef DG_REDUCE_NOSTORE  // A/B timing only (wrong results): the slot stores dropped
-            if (v == 0x5a5a5a5a5a5a5a5aull)
-#endif
             out_slots[(1 + a) * cap + Gq + gr] = t ? finalize_dev(kind, v) : v;
             if (!t) open_g[wt] = Gq + gr;
           } else {  // my share's share of a group headed earlier
@@ -1132,11 +828,11 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
   const int nt = sb->ntiles_sort;
   const uint32_t* refs = sb->refs[sb->cur];
   if (refs)
-    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->pcap, sb->keys[sb->cur], refs,
+    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
                        open_g);
   else
-    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->pcap, sb->keys[sb->cur], refs,
+    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
                        open_g);
   const int64_t nw = (int64_t)nt * kRedWaves;  // carry / open slots: one per wave share of a tile
@@ -1166,11 +862,13 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ head_pos, const uint64_t* __restrict__ payload,
-                                                   int pw, int64_t pcap, int agg, uint64_t* __restrict__ out_slots, int64_t cap,
+                                                   int pw, int rowref, int agg, uint64_t* __restrict__ out_slots, int64_t cap,
                                                    int rec, int desc) {
   __shared__ uint32_t s_base[kMaxCallSegs];
   const uint32_t n = n_ptr[0], ng = n_ptr[1];
-  for (int x = threadIdx.x; x < njobs; x += 256) s_base[x] = jobs[x].tile_begin < ntiles ? tile_off[jobs[x].tile_begin] : n;
+  // first reference of every segment: its row base (row-ref mode) or its first element index
+  for (int x = threadIdx.x; x < njobs; x += 256)
+    s_base[x] = rowref ? jobs[x].row_base : jobs[x].tile_begin < ntiles ? tile_off[jobs[x].tile_begin] : n;
   __syncthreads();
   for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += (int64_t)gridDim.x * 256) {
     const uint32_t i0 = head_pos[g], i1 = g + 1 < ng ? head_pos[g + 1] : n;
@@ -1192,7 +890,7 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
       }
       // the row's float input (identity 0.0f for a row its FilteredAggregator rejects: x + 0.0f == x
       // for every partial sum, which starts at +0.0f)
-      sum = sum + (float)__longlong_as_double((long long)payload[pay_at(pw, pcap, pcap ? i : idx, agg)]);
+      sum = sum + (float)__longlong_as_double((long long)payload[pay_at(pw, idx, agg)]);
     }
     if (cur >= 0) total = first ? sum : total + sum;
     if (out_slots) {  // groupBy: the final ABI value
@@ -1211,7 +909,7 @@ void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, 
                       const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s, int desc) {
   const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (sb->cap + 255) / 256));
   hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->tile_cnt, ntiles,
-                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, sb->payload, sb->pw, sb->pcap, agg,
+                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, sb->payload, sb->pw, sb->row_refs, agg,
                      out_slots, cap, plan.n + 1, desc);
 }
 

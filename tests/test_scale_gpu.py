@@ -165,29 +165,28 @@ def test_cfg4_compound_filters_on_large_segments(R, Q, O, S, DG, tmp_path_factor
         assert_results(q, R.run_query(q, g), O.run(q, o))
 
 
-_ORACLE_CACHE = {}
-
-
-@pytest.mark.parametrize("mode", ["bucketed", "bucket_bits_12", "overflow_fallback", "lsd"])
-def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
-    """The headline's shape (<= 4 aggregators) through each sort path: the opt-in bucketed sort (top
-    key bits by payload-carrying LSD passes, buckets sorted in LDS), smaller buckets, buckets too large
-    for the workgroup sort (the engine detects it and reruns the classic path) and the default LSD path."""
-    env = {"bucketed": {"DG_BUCKETED": "1"}, "bucket_bits_12": {"DG_BUCKET_BITS": "12"},
-           "overflow_fallback": {"DG_BUCKET_BITS": "8"}, "lsd": {"DG_NO_BUCKETED": "1"}}[mode]
-    for k in ("DG_BUCKET_BITS", "DG_NO_BUCKETED", "DG_BUCKETED"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("mode", ["inplace", "agg_filter", "interval"])
+def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode):
+    """The headline's shape through the keygen paths: longSum / doubleSum of plain LZ4 columns decoded
+    straight into the payload records (row-ref mode) next to a floatSum the keygen writes; a
+    FilteredAggregator (its column goes through the keygen, the other in place) with a row filter
+    (sparse rows: references stay row indices); and an interval cutting the segments (the per-row
+    time check path)."""
     g, o = cfg3
     aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal"),
             Q.float_sum("fsum", "sumFloatNormal")]
-    q = Q.GroupByQuery(intervals=IV, dimensions=["dimUniform", "dimHyperUnique"], aggregations=aggs)
+    iv, flt = IV, None
+    if mode == "agg_filter":
+        aggs[1] = Q.filtered(Q.long_sum("sumLongSequential"), Q.BoundDimFilter("dimHyperUnique", "2", "7"))
+        flt = Q.NotDimFilter(Q.BoundDimFilter("dimUniform", "50000", "60000"))
+    elif mode == "interval":
+        ts = np.concatenate([s.time() for s in o])
+        lo, hi = int(np.quantile(ts, 0.2)), int(np.quantile(ts, 0.7))
+        iv = [(lo, hi)]
+    q = Q.GroupByQuery(intervals=iv, dimensions=["dimUniform", "dimHyperUnique"], aggregations=aggs, filter=flt)
     part = R.groupby_per_device(g, q)[0]
-    if "exp" not in _ORACLE_CACHE:
-        _ORACLE_CACHE["exp"] = O.run(q, o)
-    exp = _ORACLE_CACHE["exp"]
-    assert len(part) == len(exp) > 1_000_000
+    exp = O.run(q, o)
+    assert len(part) == len(exp) > 200_000
     t, keys, vals = _columns(exp, q.dimensions, aggs)
     assert np.array_equal(part.times, t)
     assert list(zip(*[list(c) for c in part.dims])) == keys
