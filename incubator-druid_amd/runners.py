@@ -20,6 +20,7 @@ per-segment runners. Cross-device / cross-rank merging is in distributed.py.
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 import heapq
 import math
 from collections import OrderedDict, defaultdict
@@ -86,6 +87,9 @@ class RunStats:
 # ----------------------------------------------------------------------------------------------
 def timeseries_per_segment(segments: Sequence[GpuSegment], query: Q.TimeseriesQuery,
                            stats: Optional[RunStats] = None) -> List[List[Q.Result]]:
+    split = segment_queries(query, segments)
+    if split is not None:  # every segment on its own calendar chain
+        return [timeseries_per_segment([s], q, stats)[0] if q is not None else [] for s, q in zip(segments, split)]
     out: List[List[Q.Result]] = [[] for _ in segments]
     na = len(query.aggregations)
     for _, idx in _group_by_device(segments).items():
@@ -150,6 +154,15 @@ def run_timeseries(segments: Sequence[GpuSegment], query: Q.TimeseriesQuery,
             vals[i * cap * na:(i * cap + c) * na] = d_v[k * c * na:(k + 1) * c * na]
     if scan is None:
         scan, keep = N.make_scan(query, Q, filters=False)
+    g = query.granularity
+    if g.is_calendar:  # TimeseriesBinaryFn keys a result by gran.bucketStart(its timestamp)
+        starts = {}
+        for i in range(n_all):
+            for k in range(int(nb[i])):
+                t = int(times[i * cap + k])
+                if t not in starts:
+                    starts[t] = g.bucket_start(t)
+                times[i * cap + k] = starts[t]
     out_cap = max(n_all, 1) * cap
     on = ctypes.c_int32()
     o_t = np.zeros(out_cap, dtype=np.int64)
@@ -545,6 +558,9 @@ def topn_per_segment(segments: Sequence[GpuSegment], query: Q.TopNQuery,
                      stats: Optional[RunStats] = None) -> List[List[Q.Result]]:
     """Per-segment results (what each segment's QueryRunner returns), as Result lists."""
     _check_topn(query)
+    split = segment_queries(query, segments)
+    if split is not None:  # every segment on its own calendar chain
+        return [topn_per_segment([s], q, stats)[0] if q is not None else [] for s, q in zip(segments, split)]
     out: List[List[Q.Result]] = [[] for _ in segments]
     na = len(query.aggregations)
     for _, idx in _group_by_device(segments).items():
@@ -787,8 +803,10 @@ def groupby_merge_devices(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
 
 def groupby_per_segment(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
                         stats: Optional[RunStats] = None) -> List[GroupByPartial]:
-    """What each segment's QueryRunner returns (createRunner(segment).run), one engine call each."""
-    return [groupby_per_device([s], query, stats)[0] for s in segments]
+    """What each segment's QueryRunner returns (createRunner(segment).run), one engine call each
+    (a calendar granularity on the segment's own bucket chain, segment_queries)."""
+    split = segment_queries(query, segments) or [query] * len(segments)
+    return [groupby_per_device([s], q, stats)[0] for s, q in zip(segments, split) if q is not None]
 
 
 def merge_groupby_columnar(query: Q.GroupByQuery, partials: Sequence[GroupByPartial]):
@@ -1042,6 +1060,44 @@ def postprocess_groupby(query: Q.GroupByQuery, rows: List[Q.Row]) -> List[Q.Row]
 # ----------------------------------------------------------------------------------------------
 # factories (QueryRunnerFactory surface)
 # ----------------------------------------------------------------------------------------------
+def segment_queries(query, segments: Sequence[GpuSegment]):
+    """Calendar granularities: makeCursors iterates gran.getIterable(actualInterval) per segment
+    (QueryableIndexStorageAdapter.java:367-456; actualInterval = [max(query start, minTime),
+    min(query end, bucketEnd(maxTime)))), i.e. bucketStart(actual start) and increments from there.
+    With an origin whose day clamps (P1M from Jan 31: truncate gives Apr 30, the chain from the query
+    start Apr 28) that chain is not a slice of the query interval's, which the engine buckets every
+    segment of a call on. Returns None when every segment's chain lies on the query's list (the
+    batched path is exact); else one query per segment (None for a segment outside the interval)
+    whose interval is the segment's actual interval, so each runs on its own chain."""
+    g = query.granularity
+    if not g.is_calendar:
+        return None
+    qs, qe = query.interval
+    qlist = g.bucket_starts((qs, qe))
+    qpos = {t: i for i, t in enumerate(qlist)}
+    out, diverge = [], False
+    for s in segments:
+        lo, hi = max(qs, s.min_time), min(qe, g.bucket_end(s.max_time))
+        if s.num_rows == 0 or hi <= lo:
+            out.append(None)
+            continue
+        sl = g.bucket_starts((lo, hi))
+        i = qpos.get(sl[0])
+        diverge |= i is None or qlist[i:i + len(sl)] != sl
+        out.append(dataclasses.replace(query, intervals=[(lo, hi)]))
+    return out if diverge else None
+
+
+def _run_split(factory, segments, queries, query, stats):
+    """Per segment on its own bucket chain (segment_queries), merged by the toolchest (the
+    reference's per-segment runners + mergeResults)."""
+    per = []
+    for s, q in zip(segments, queries):
+        if q is not None:
+            per.extend(factory.per_segment([s], q, stats))
+    return factory.toolchest.merge(query, per)
+
+
 class SegmentQueryRunner:
     """QueryRunner for one segment (QueryRunnerFactory.createRunner)."""
 
@@ -1049,6 +1105,9 @@ class SegmentQueryRunner:
         self.factory, self.segment = factory, segment
 
     def run(self, query):
+        split = segment_queries(query, [self.segment])
+        if split is not None:
+            return _run_split(self.factory, [self.segment], split, query, None)
         return self.factory.toolchest.merge(query, self.factory.per_segment([self.segment], query))
 
 
@@ -1061,6 +1120,9 @@ class MergedQueryRunner:
         self.stats = RunStats()
 
     def run(self, query):
+        split = segment_queries(query, self.segments)
+        if split is not None:
+            return _run_split(self.factory, self.segments, split, query, self.stats)
         return self.factory.run_merged(self.segments, query, self.stats)
 
 

@@ -49,6 +49,10 @@ GRANS = [
     {"type": "period", "period": "P1W", "timeZone": "America/New_York", "origin": "2012-10-03T10:00:00Z"},
     {"type": "period", "period": "P1M2D", "timeZone": "America/Los_Angeles"},
     {"type": "period", "period": "P3M", "timeZone": "Europe/Berlin"},
+    # origins whose day clamps: each segment's chain (bucketStart of its first row, then increments)
+    # differs from the query interval's, so every segment runs on its own (runners.segment_queries)
+    {"type": "period", "period": "P1M", "origin": "2000-01-31T00:00:00Z"},
+    {"type": "period", "period": "P1M", "timeZone": "America/Los_Angeles", "origin": "2011-12-30T17:00:00Z"},
 ]
 
 
@@ -102,7 +106,8 @@ def test_timeseries_descending(R, Q, O, segs, osegs):
 
 
 def test_topn_calendar_granularity(R, Q, O, segs, osegs):
-    for gran in ("month", {"type": "period", "period": "P1W", "timeZone": "Asia/Kolkata"}):
+    for gran in ("month", {"type": "period", "period": "P1W", "timeZone": "Asia/Kolkata"},
+                 {"type": "period", "period": "P1M", "origin": "2000-01-31T00:00:00Z"}):
         q = Q.TopNQuery(intervals=IV, granularity=gran, dimension="dimZipf", metric="fsum", threshold=5,
                         aggregations=[Q.long_sum("sumLongSequential"), Q.float_sum("fsum", "sumFloatNormal"),
                                       Q.count("rows")])
@@ -112,7 +117,8 @@ def test_topn_calendar_granularity(R, Q, O, segs, osegs):
 
 
 def test_groupby_calendar_granularity(R, Q, O, segs, osegs):
-    for gran in ("quarter", {"type": "period", "period": "P1D", "timeZone": "America/Los_Angeles"}):
+    for gran in ("quarter", {"type": "period", "period": "P1D", "timeZone": "America/Los_Angeles"},
+                 {"type": "period", "period": "P1M", "origin": "2000-01-31T00:00:00Z"}):
         q = Q.GroupByQuery(intervals=IV, granularity=gran, dimensions=["dimZipf", "dimSequentialHalfNull"],
                            aggregations=[Q.count("rows"), Q.long_sum("sumLongSequential"),
                                          Q.float_sum("fsum", "sumFloatNormal")],

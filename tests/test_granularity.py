@@ -89,3 +89,27 @@ def test_host_and_oracle_restatements_agree(Q, O, spec):
     starts = g.bucket_starts((lo, lo + 200 * 86_400_000))
     assert starts == [b for b, _ in O.o_iterable(g, (lo, lo + 200 * 86_400_000))] + [starts[-1]]
     assert all(x < y for x, y in zip(starts, starts[1:]))
+
+
+def test_segment_bucket_chains_diverge_only_for_clamped_origins(Q):
+    """makeCursors buckets each segment on gran.getIterable(its actual interval): bucketStart of its
+    first row, then increments. With an origin on a day that clamps (P1M from Jan 31) that chain is
+    not the query interval's, and runners.segment_queries sends every segment down on its own."""
+    import importlib
+    R = importlib.import_module("incubator-druid_amd.runners")
+
+    class Seg:
+        def __init__(self, a, b):
+            self.min_time, self.max_time, self.num_rows = Q.parse_time(a), Q.parse_time(b), 10
+
+    segs = [Seg("2012-09-15", "2012-11-14"), Seg("2012-11-16", "2013-01-14"), Seg("2013-01-16", "2013-03-19")]
+    iv = ["2012-09-20T05:00:00Z/2013-03-15T00:00:00Z"]
+    for gran in ("month", "day", {"type": "period", "period": "P3M", "timeZone": "Europe/Berlin"}):
+        assert R.segment_queries(Q.TimeseriesQuery(intervals=iv, granularity=gran), segs) is None
+    q = Q.TimeseriesQuery(intervals=iv, granularity={"type": "period", "period": "P1M", "origin": "2000-01-31T00:00:00Z"})
+    split = R.segment_queries(q, segs)
+    assert [s.interval[0] for s in split] == [Q.parse_time(iv[0].split("/")[0]), segs[1].min_time, segs[2].min_time]
+    g = q.granularity
+    # segment 2's chain starts at Oct 31 (Jan 31 + 9 months), the query's has Oct 30 there
+    assert g.bucket_start(segs[1].min_time) == Q.parse_time("2012-10-31")
+    assert Q.parse_time("2012-10-30") in g.bucket_starts(q.interval)
