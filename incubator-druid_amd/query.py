@@ -96,6 +96,7 @@ class Granularity:
     iso: str = ""                   # calendar: ISO-8601 period
     tz: str = ""                    # calendar: time zone id ("" = UTC)
     origin: Optional[int] = None    # calendar: the spec's origin (None = the zone's local epoch)
+    exact_from: Optional[int] = None  # fixed grid of a period spec: exact only for t >= this (None: always)
 
     @property
     def is_all(self) -> bool:
@@ -157,23 +158,54 @@ class Granularity:
             return js
         if self.name in _PERIOD_MS:
             return self.name
+        if self.iso:  # a period spec bucketed on its fixed grid
+            js = {"type": "period", "period": self.iso}
+            if self.tz:
+                js["timeZone"] = self.tz
+            if self.origin is not None:
+                js["origin"] = format_time(self.origin)
+            return js
         return {"type": "duration", "duration": self.period_ms, "origin": self.origin_ms}
 
     @staticmethod
     def period(iso: str, tz: Optional[str] = None, origin=None) -> "Granularity":
-        """PeriodGranularity(period, origin, timeZone): the fixed UTC form when it is exact, else calendar."""
-        from .granularity import parse_period
+        """PeriodGranularity(period, origin, timeZone): the fixed grid when it is exact, else calendar.
+        Exact: a period without months / years in UTC or a fixed-offset zone ("+05:30"), where every
+        truncate branch (PeriodGranularity.java:222-330) is a floor on the grid of the period from the
+        origin (default: the zone's local epoch, 0 - offset; P1W: its Monday). Two quirks of the hours
+        branch (:313-326) are not: an origin < 0 off the local hour rounds to the hour (calendar), and
+        with an origin <= 0 a timestamp before the origin gets the aligned point AFTER it — exact on the
+        grid only at or after the origin, so the grid records `exact_from` and the runners switch to
+        the calendar restatement when the data reaches before it (compound periods likewise before 0)."""
+        from .granularity import Zone, parse_period
         y, mo, w, d, h, mi, s, ms = parse_period(iso)
         utc = tz in (None, "", "UTC", "Etc/UTC")
+        off = 0 if utc else Zone(tz).fixed  # fixed offset in ms, None for a zone with rules
         o = parse_time(origin) if origin is not None else None
         single = sum(1 for v in (y, mo, w, d, h, mi, s, ms) if v) == 1
-        # hours with an origin before 1970 not on the hour: PeriodGranularity.java:313-315 floors to the hour
-        quirk = bool(h) and single and o is not None and o < 0 and o % 3_600_000 != 0
-        if utc and not (y or mo) and not quirk:
+        hours_branch = bool(h) and single and (h > 1 or o is not None)
+        # hours with an origin before 1970 not on the (local) hour: PeriodGranularity.java:313-315 floors to the hour
+        quirk = bool(h) and single and o is not None and o < 0 and (o + (off or 0)) % 3_600_000 != 0
+        if off is not None and not (y or mo) and not quirk:
             P = ((((w * 7 + d) * 24 + h) * 60 + mi) * 60 + s) * 1000 + ms
-            default_origin = -3 * 86_400_000 if (w == 1 and single) else 0  # P1W: Mondays
-            return Granularity(P, o if o is not None else default_origin, "period")
+            default_origin = (-3 * 86_400_000 if (w == 1 and single) else 0) - off  # P1W: Mondays
+            org = o if o is not None else default_origin
+            exact_from = None
+            if not single:
+                # compound: truncateMillisPeriod (PeriodGranularity.java:411-428) = t - (t % P - origin % P,
+                # + P once if negative) with Java remainders: the grid's floor only for t >= 0 and a
+                # non-negative origin remainder
+                if math.fmod(org, P) < 0:
+                    return Granularity(0, 0, "calendar", iso.upper(), "" if utc else tz, o)
+                exact_from = 0
+            elif hours_branch and org <= 0:
+                exact_from = org
+            return Granularity(P, org, "period", iso.upper(), "" if utc else tz, o, exact_from)
         return Granularity(0, 0, "calendar", iso.upper(), "" if utc else tz, o)
+
+    def calendar_form(self) -> "Granularity":
+        """The same PeriodGranularity bucketed through the calendar restatement."""
+        return Granularity(0, 0, "calendar", self.iso, self.tz, self.origin)
 
     @staticmethod
     def of(spec) -> "Granularity":

@@ -1060,6 +1060,24 @@ def postprocess_groupby(query: Q.GroupByQuery, rows: List[Q.Row]) -> List[Q.Row]
 # ----------------------------------------------------------------------------------------------
 # factories (QueryRunnerFactory surface)
 # ----------------------------------------------------------------------------------------------
+def exact_granularity(query, segments: Sequence[GpuSegment]):
+    """A period granularity on the fixed grid that is exact only from some instant on
+    (Granularity.exact_from: the hours branch gives timestamps before its origin the aligned point
+    after them, PeriodGranularity.java:313-326; truncateMillisPeriod's Java remainders misalign
+    negative timestamps): when the data reaches before that instant, the query with the calendar
+    restatement instead, its interval clipped to the data so the bucket list stays finite."""
+    g = query.granularity
+    ef = getattr(g, "exact_from", None)
+    if ef is None:
+        return query
+    live = [s for s in segments if s.num_rows]
+    if not live or min(s.min_time for s in live) >= ef or query.interval[0] >= ef:
+        return query
+    lo = max(query.interval[0], min(s.min_time for s in live))
+    hi = min(query.interval[1], max(s.max_time for s in live) + 1)
+    return dataclasses.replace(query, intervals=[(lo, max(hi, lo + 1))], granularity=g.calendar_form())
+
+
 def segment_queries(query, segments: Sequence[GpuSegment]):
     """Calendar granularities: makeCursors iterates gran.getIterable(actualInterval) per segment
     (QueryableIndexStorageAdapter.java:367-456; actualInterval = [max(query start, minTime),
@@ -1105,6 +1123,7 @@ class SegmentQueryRunner:
         self.factory, self.segment = factory, segment
 
     def run(self, query):
+        query = exact_granularity(query, [self.segment])
         split = segment_queries(query, [self.segment])
         if split is not None:
             return _run_split(self.factory, [self.segment], split, query, None)
@@ -1120,6 +1139,7 @@ class MergedQueryRunner:
         self.stats = RunStats()
 
     def run(self, query):
+        query = exact_granularity(query, self.segments)
         split = segment_queries(query, self.segments)
         if split is not None:
             return _run_split(self.factory, self.segments, split, query, self.stats)

@@ -246,9 +246,11 @@ def _o_period(iso, origin, tz):
 
 
 def _o_cal(gran):
-    """The calendar restatement for a calendar-mode granularity of the tests' query objects (their
-    fields: ISO period, zone id, origin), None for ALL / fixed-length ones."""
-    if getattr(gran, "name", "") != "calendar":
+    """The PeriodGranularity restatement for any granularity given as a period spec (the tests'
+    query objects keep its fields: ISO period, zone id, origin) — calendar-mode ones and those the
+    engine buckets on a fixed grid alike, so the oracle never relies on the engine's choice of grid;
+    None for ALL, duration and the simple named granularities."""
+    if getattr(gran, "name", "") not in ("calendar", "period") or not getattr(gran, "iso", ""):
         return None
     return _o_period(gran.iso, gran.origin, gran.tz or None)
 

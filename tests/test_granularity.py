@@ -113,3 +113,49 @@ def test_segment_bucket_chains_diverge_only_for_clamped_origins(Q):
     # segment 2's chain starts at Oct 31 (Jan 31 + 9 months), the query's has Oct 30 there
     assert g.bucket_start(segs[1].min_time) == Q.parse_time("2012-10-31")
     assert Q.parse_time("2012-10-30") in g.bucket_starts(q.interval)
+
+
+def test_fixed_offset_zones_bucket_on_a_fixed_grid(Q):
+    """A fixed-offset zone ("+05:30") with a period without months / years is an exact fixed grid
+    (origin = the zone's local epoch), the same buckets as the calendar restatement, with no
+    per-query bucket list (whose size is capped)."""
+    rng = np.random.default_rng(3)
+    ts = rng.integers(-3 * 10**12, 3 * 10**12, 400)
+    for iso, tz, origin in (("P1D", "+05:30", None), ("PT1H", "-03:30", None), ("P1W", "+01:00", None),
+                            ("PT6H", "+05:45", None), ("P2D", "-08:00", "2012-03-04T05:06:07Z"),
+                            ("PT15M", "+05:30", None), ("PT1H30M", "-02:00", None)):
+        g = Q.Granularity.period(iso, tz, origin)
+        assert not g.is_calendar, (iso, tz)
+        cal = g.calendar_form()
+        for t in ts:
+            if g.exact_from is not None and t < g.exact_from:
+                continue
+            assert g.bucket_start(int(t)) == cal.bucket_start(int(t)), (iso, tz, int(t))
+    # a compound period whose origin has a negative Java remainder: truncateMillisPeriod is not the
+    # grid's floor, so it stays on the calendar restatement
+    assert Q.Granularity.period("PT1H30M", "+02:00").is_calendar
+
+
+def test_hours_branch_before_the_origin(Q):
+    """PeriodGranularity.truncate's hours branch (PeriodGranularity.java:313-326) with an origin <= 0:
+    a timestamp before the origin gets the aligned point AFTER it (PT2H, default origin 0: -1.5 h ->
+    0); after the origin it is the grid's floor. The fixed grid records this and the runners switch
+    to the calendar restatement when the data reaches before the origin."""
+    import importlib
+    R = importlib.import_module("incubator-druid_amd.runners")
+    g = Q.Granularity.period("PT2H")
+    assert g.exact_from == 0 and g.origin_ms == 0
+    cal = g.calendar_form()
+    assert cal.bucket_start(-5_400_000) == 0  # the quirk
+    assert cal.bucket_start(-7_200_000) == -7_200_000  # on the grid: itself
+    assert cal.bucket_start(5_400_000) == 0 == g.bucket_start(5_400_000)
+    assert Q.Granularity.period("PT1H").exact_from is None  # roundFloor branch
+
+    class Seg:
+        def __init__(self, a, b):
+            self.min_time, self.max_time, self.num_rows = a, b, 10
+
+    q = Q.TimeseriesQuery(intervals=["1960-01-01/1980-01-01"], granularity={"type": "period", "period": "PT2H"})
+    assert R.exact_granularity(q, [Seg(0, 10**9)]) is q  # data after the origin: the grid is exact
+    q2 = R.exact_granularity(q, [Seg(-10**9, 10**9)])
+    assert q2.granularity.is_calendar and q2.interval == (-10**9, 10**9 + 1)
