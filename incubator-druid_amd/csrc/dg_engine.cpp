@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -1537,6 +1538,28 @@ struct SideJoin {
     if (s) hipStreamSynchronize(s);
   }
 };
+
+// memcpy of several (dst, src, bytes) ranges over a few host threads (large result fetches: the
+// destination pages fault in on first touch, which one thread alone does slowly)
+static void par_copy(const std::vector<std::pair<void*, std::pair<const void*, size_t>>>& parts) {
+  size_t total = 0;
+  for (auto& p : parts) total += p.second.second;
+  const int nt = (int)std::min<size_t>(8, std::max<size_t>(1, total >> 23));
+  auto run = [&](int t) {
+    for (auto& p : parts) {
+      const size_t b = p.second.second, lo = b * t / nt, hi = b * (t + 1) / nt;
+      if (hi > lo) memcpy((char*)p.first + lo, (const char*)p.second.first + lo, hi - lo);
+    }
+  };
+  if (nt == 1) {
+    run(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(run, t);
+  run(0);
+  for (auto& x : th) x.join();
+}
 
 struct CallGuard {
   Context* ctx;
@@ -3312,33 +3335,68 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
   CallGuard g(r->ctx);
   CallScratch* cs = g.cs;
   hipStream_t st = r->ctx->stream;
-  const int nd = r->ndims;
-  if (bucket_time || ids) {
-    int64_t* d_b = dev_take<int64_t>(cs, (size_t)count);
-    int32_t* d_ids = dev_take<int32_t>(cs, (size_t)count * std::max(nd, 1));
-    if (!d_b || !d_ids) return set_error(DG_ERR_OOM, "fetch staging");
-    launch_gb_unpack(r->keys, start, count, r->lay, d_b, d_ids, st);
-    if (bucket_time) DG_HIP(hipMemcpyAsync(bucket_time, d_b, (size_t)count * 8, hipMemcpyDeviceToHost, st));
-    if (ids && nd) DG_HIP(hipMemcpyAsync(ids, d_ids, (size_t)count * nd * 4, hipMemcpyDeviceToHost, st));
+  const int nd = r->ndims, na = r->naggs;
+  // per group: time 8 B, ids 4 B each, values 8 B each, packed on the device and copied through two
+  // pinned staging chunks; the host copies chunk i into the caller's arrays (several threads) while
+  // chunk i + 1 crosses PCIe
+  const int64_t per = (bucket_time ? 8 : 0) + (ids ? 4 * (int64_t)nd : 0) + (values ? 8 * (int64_t)na : 0);
+  if (per == 0) return DG_OK;
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)64 << 20) / per));
+  const size_t cbytes = (size_t)(chunk * per + 64);
+  uint8_t* d_stage = dev_take<uint8_t>(cs, cbytes);
+  uint8_t* h_stage[2] = {host_take<uint8_t>(cs, cbytes), host_take<uint8_t>(cs, cbytes)};
+  if (!d_stage || !h_stage[0] || !h_stage[1]) return set_error(DG_ERR_OOM, "fetch staging");
+  const int64_t* d_bounds = nullptr;
+  if (r->period && !r->bounds.empty()) {
+    int64_t* db;
+    int64_t* hb = up_take<int64_t>(cs, r->bounds.size(), &db, st);
+    if (!hb) return set_error(DG_ERR_OOM, "bucket table");
+    memcpy(hb, r->bounds.data(), r->bounds.size() * 8);
+    d_bounds = db;
   }
-  std::vector<uint64_t> tmp;
-  if (values && r->naggs) {
-    tmp.resize((size_t)count * r->naggs);
-    for (int a = 0; a < r->naggs; ++a)
-      DG_HIP(hipMemcpyAsync(tmp.data() + (size_t)a * count, r->slots + (size_t)(1 + a) * r->cap + start, (size_t)count * 8,
-                            hipMemcpyDeviceToHost, st));
+  DG_FLUSH(cs, st);
+  hipEvent_t done[2] = {r->ctx->ev[6], r->ctx->ev[7]};
+  auto layout = [&](uint8_t* base, int64_t n, int64_t** t, int32_t** i, uint64_t** v) {
+    uint8_t* p = base;
+    *t = bucket_time ? reinterpret_cast<int64_t*>(p) : nullptr;
+    p += bucket_time ? 8 * n : 0;
+    *v = values ? reinterpret_cast<uint64_t*>(p) : nullptr;
+    p += values ? 8 * n * na : 0;
+    *i = ids ? reinterpret_cast<int32_t*>(p) : nullptr;
+  };
+  auto drain = [&](int k, int64_t c0, int64_t n) {  // chunk in h_stage[k] -> the caller's arrays
+    int64_t* t;
+    int32_t* i;
+    uint64_t* v;
+    layout(h_stage[k], n, &t, &i, &v);
+    std::vector<std::pair<void*, std::pair<const void*, size_t>>> parts;
+    if (t) parts.push_back({bucket_time + (c0 - start), {t, (size_t)n * 8}});
+    if (v && na) parts.push_back({values + (c0 - start) * na, {v, (size_t)n * na * 8}});
+    if (i && nd) parts.push_back({ids + (c0 - start) * nd, {i, (size_t)n * nd * 4}});
+    par_copy(parts);
+  };
+  int64_t prev0 = -1, prevn = 0;
+  int k = 0;
+  for (int64_t c0 = start; c0 < start + count; c0 += chunk, k ^= 1) {
+    const int64_t n = std::min<int64_t>(chunk, start + count - c0);
+    int64_t* t;
+    int32_t* i;
+    uint64_t* v;
+    layout(d_stage, n, &t, &i, &v);
+    launch_gb_fetch_pack(r->keys, r->slots, r->cap, c0, n, r->lay, na, r->universal, r->bucket0, r->period, d_bounds, t,
+                         nd ? i : nullptr, na ? v : nullptr, st);
+    DG_HIP(hipMemcpyAsync(h_stage[k], d_stage, (size_t)(n * per), hipMemcpyDeviceToHost, st));
+    DG_HIP(hipEventRecord(done[k], st));
+    if (prev0 >= 0) {
+      DG_HIP(hipEventSynchronize(done[k ^ 1]));
+      drain(k ^ 1, prev0, prevn);
+    }
+    prev0 = c0;
+    prevn = n;
   }
-  int rc = finish_call(cs, st);
-  if (rc) return rc;
-  if (bucket_time)
-    for (int64_t i = 0; i < count; ++i)
-      bucket_time[i] = !r->period ? r->universal
-                       : r->bounds.empty() ? r->bucket0 + bucket_time[i] * r->period
-                                           : r->bounds[r->bucket0 + bucket_time[i]];
-  if (values && r->naggs)
-    for (int64_t i = 0; i < count; ++i)
-      for (int a = 0; a < r->naggs; ++a) values[i * r->naggs + a] = tmp[(size_t)a * count + i];
-  return DG_OK;
+  DG_HIP(hipEventSynchronize(done[k ^ 1]));
+  drain(k ^ 1, prev0, prevn);
+  return finish_call(cs, st);
 }
 
 int dg_result_fetch_rows(dg_result* r, int64_t start, int64_t count, int64_t* rows) {

@@ -517,6 +517,10 @@ struct KeyLayout {
 };
 void launch_gb_unpack(const uint64_t* keys, int64_t start, int64_t count, KeyLayout lay, int64_t* bucket, int32_t* ids,
                       hipStream_t s);
+// groups [start, start + count) packed for one device-to-host copy: times, ids, AoS values (see dg_sort.hip)
+void launch_gb_fetch_pack(const uint64_t* keys, const uint64_t* slots, int64_t cap, int64_t start, int64_t count,
+                          KeyLayout lay, int naggs, int64_t universal, int64_t bucket0, int64_t period,
+                          const int64_t* bounds, int64_t* times, int32_t* ids, uint64_t* vals, hipStream_t s);
 // cross-device merge: keys of layout lin -> layout lout (bucket index + bucket_delta, ids through maps)
 struct RekeyMaps {
   const int32_t* m[kMaxGroupDims];

@@ -960,6 +960,37 @@ void launch_gb_unpack(const uint64_t* keys, int64_t start, int64_t count, KeyLay
   hipLaunchKernelGGL(k_gb_unpack, dim3((unsigned)blocks), dim3(256), 0, s, keys, start, count, lay, bucket, ids);
 }
 
+// groups [start, start + count) of a result packed for one host copy: bucket times [count] (ALL: the
+// universal time; grid: bucket0 + index * period; calendar: bounds[bucket0 + index]), dimension ids
+// [count][ndims], then the ABI values [count][naggs] (the slot-major rows of `slots` transposed);
+// a null region pointer skips it
+__global__ void k_gb_fetch_pack(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ slots, int64_t cap,
+                                int64_t start, int64_t count, KeyLayout lay, int naggs, int64_t universal,
+                                int64_t bucket0, int64_t period, const int64_t* __restrict__ bounds,
+                                int64_t* __restrict__ times, int32_t* __restrict__ ids, uint64_t* __restrict__ vals) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[start + i];
+    if (times) {
+      const int64_t b = lay.bucket_bits ? (int64_t)((k >> lay.bucket_shift) & ((1ull << lay.bucket_bits) - 1)) : 0;
+      times[i] = !period ? universal : bounds ? bounds[bucket0 + b] : bucket0 + b * period;
+    }
+    if (ids)
+      for (int d = 0; d < lay.ndims; ++d)
+        ids[i * lay.ndims + d] = lay.dim_bits[d] ? (int32_t)((k >> lay.dim_shift[d]) & ((1ull << lay.dim_bits[d]) - 1)) : 0;
+    if (vals)
+      for (int a = 0; a < naggs; ++a) vals[i * naggs + a] = slots[(size_t)(1 + a) * cap + start + i];
+  }
+}
+
+void launch_gb_fetch_pack(const uint64_t* keys, const uint64_t* slots, int64_t cap, int64_t start, int64_t count,
+                          KeyLayout lay, int naggs, int64_t universal, int64_t bucket0, int64_t period,
+                          const int64_t* bounds, int64_t* times, int32_t* ids, uint64_t* vals, hipStream_t s) {
+  if (count <= 0) return;
+  const int64_t blocks = std::min<int64_t>(16384, (count + 255) / 256);
+  hipLaunchKernelGGL(k_gb_fetch_pack, dim3((unsigned)blocks), dim3(256), 0, s, keys, slots, cap, start, count, lay, naggs,
+                     universal, bucket0, period, bounds, times, ids, vals);
+}
+
 // ------------------------------------------------------------------------------------------------
 // cross-device merge (QueryRunnerFactory.mergeRunners over the devices' merged groups): re-key a
 // result into the cluster key space, split it by key range, merge the received partials

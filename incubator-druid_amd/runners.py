@@ -42,14 +42,13 @@ from .segment import GpuSegment
 def _decode_slots(aggs: Sequence[Q.AggregatorFactory], slots: np.ndarray) -> List[np.ndarray]:
     """[n, naggs] uint64 ABI slots -> one typed column per aggregator."""
     out = []
-    for a, col in zip(aggs, slots.T):
-        col = np.ascontiguousarray(col)
+    for a, col in zip(aggs, slots.T):  # (strided views of the slot rows; floats are narrowed)
         if a.output_type == "long":
             out.append(col.view(np.int64))
         elif a.output_type == "double":
             out.append(col.view(np.float64))
         else:
-            out.append(col.astype(np.uint64).view(np.uint32)[0::2].view(np.float32))
+            out.append((col & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32))
     return out
 
 
@@ -677,16 +676,17 @@ class GroupByResult:
         q = self.query
         nd, na = len(q.dimensions), len(q.aggregations)
         count = self.groups - start if count is None else count
-        t = np.zeros(max(count, 1), dtype=np.int64)
-        ids = np.zeros(max(count * nd, 1), dtype=np.int32)
-        vals = np.zeros(max(count * na, 1), dtype=np.uint64)
+        # (np.empty: the library's staged copy is the first touch of these pages, spread over threads)
+        t = np.empty(max(count, 1), dtype=np.int64)
+        ids = np.empty(max(count * nd, 1), dtype=np.int32)
+        vals = np.empty(max(count * na, 1), dtype=np.uint64)
         if count:
-            N.check(N.lib().dg_result_fetch_groups(self.handle, start, count, t.ctypes.data, ids.ctypes.data,
-                                                   vals.ctypes.data))
+            N.check(N.lib().dg_result_fetch_groups(self.handle, start, count, t.ctypes.data,
+                                                   ids.ctypes.data if nd else None, vals.ctypes.data if na else None))
         if self.time_map is not None:
             t[:count] = self.time_map[t[:count]]
         ids = ids[:count * nd].reshape(count, nd) if nd else np.zeros((count, 0), np.int32)
-        codes = [np.ascontiguousarray(ids[:, d]) for d in range(nd)]
+        codes = [ids[:, d] for d in range(nd)]  # strided views of the [count][ndims] id rows
         aggs = _decode_slots(q.aggregations, vals[:count * na].reshape(count, na)) if na else []
         return GroupByPartial(t[:count], None, aggs, codes, [self.dictionary(d) for d in range(nd)], merged=True)
 
