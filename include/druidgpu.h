@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 9
+#define DG_ABI_VERSION 10
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -151,10 +151,18 @@ typedef struct {
  * Calendar granularities (months, years, periods in a time zone, compound periods: PeriodGranularity
  * with Joda chronology arithmetic, PeriodGranularity.java:212-410) are given as the bucket list
  * gran.getIterable(interval) yields (Granularity.java:176-240): bucket_starts[0..n_bucket_starts)
- * = the starts followed by the end of the last bucket (strictly ascending, covering the interval),
+ * = the starts followed by the end of the last bucket (strictly ascending, the last end at or past the
+ * interval end; the first start may lie after the interval start, rows before it are in no bucket),
  * period_ms = 0; bucket k = [bucket_starts[k], bucket_starts[k + 1]). The Java shim computes it
  * with the query's own Granularity object. In dg_keyspace / dg_merge such a granularity is the
  * grid period_ms = 1 over bucket indices into that list.
+ * seg_bounds (calendar only, optional): per segment of the call two instants, {gran.bucketStart(s),
+ * gran.bucketEnd(maxTime)} with s = max(interval start, minTime): where the segment's iterable starts
+ * and where its dataInterval ends (QueryableIndexStorageAdapter.java:367-372). Both truncate from
+ * the origin, so they can leave the listed buckets: bucketEnd past the end of the listed bucket that
+ * holds maxTime (an origin whose day clamps: P1M from Jan 31), bucketStart after s (the hours branch
+ * before its origin, PeriodGranularity.java:313-326: rows in [s, bucketStart(s)) are in no cursor).
+ * NULL = the listed bucket ends and no clipping at the start.
  * descending: CursorFactory.makeCursors(..., descending) (QueryableIndexStorageAdapter.java:378-424):
  * cursors in descending time order and each cursor's rows last to first (order-dependent floatSum);
  * timeseries / topN write their per-segment buckets in that order. groupBy ignores it (its engine
@@ -173,6 +181,7 @@ typedef struct {
   const int64_t* bucket_starts;   /* calendar granularity (see above); NULL = period_ms grid */
   int32_t n_bucket_starts;
   int32_t descending;
+  const int64_t* seg_bounds;      /* calendar granularity: 2 per segment (see above), or NULL */
 } dg_scan;
 
 /* QueryMetrics counters (query/QueryMetrics.java:295-306) + device timings */

@@ -61,7 +61,8 @@ class dg_scan(ctypes.Structure):
                 ("filter", ctypes.POINTER(dg_filter)), ("n_filter", ctypes.c_int32),
                 ("aggs", ctypes.POINTER(dg_agg)), ("n_aggs", ctypes.c_int32),
                 ("cancel", ctypes.POINTER(ctypes.c_int32)), ("bucket_starts", ctypes.c_void_p),
-                ("n_bucket_starts", ctypes.c_int32), ("descending", ctypes.c_int32)]
+                ("n_bucket_starts", ctypes.c_int32), ("descending", ctypes.c_int32),
+                ("seg_bounds", ctypes.c_void_p)]
 
 
 class dg_metrics(ctypes.Structure):
@@ -357,6 +358,12 @@ def make_scan(query, query_module, cancel: Optional[ctypes.c_int32] = None, segm
         keep.append(starts)
         s.bucket_starts = starts.ctypes.data
         s.n_bucket_starts = len(starts)
+        if segments:  # per segment: where its iterable starts, where its dataInterval ends
+            qs = query.interval[0]
+            b = np.asarray([[gran.bucket_start(max(qs, sg.min_time)), gran.bucket_end(sg.max_time)] if sg.num_rows
+                            else [0, 0] for sg in segments], np.int64).reshape(-1)
+            keep.append(b)
+            s.seg_bounds = b.ctypes.data
     else:
         s.period_ms = gran.period_ms
         s.origin_ms = gran.origin_ms

@@ -1337,8 +1337,10 @@ static int prepare_scan(const dg_scan* in, dg_scan* out, Grain* g) {
   if (n < 2) return set_error(DG_ERR_ARG, "bucket_starts needs at least one bucket (start and end)");
   for (int32_t k = 1; k < n; ++k)
     if (b[k] <= b[k - 1]) return set_error(DG_ERR_ARG, "bucket_starts not strictly ascending at %d", k);
-  if (b[0] > in->interval_start || b[n - 1] < in->interval_end)
-    return set_error(DG_ERR_ARG, "bucket_starts do not cover the interval");
+  // the list may start after the interval (bucketStart of the interval start can lie after it:
+  // the hours branch before its origin, PeriodGranularity.java:313-326): rows before b[0] are in
+  // no cursor (makeCursors clips each cursor to its bucket)
+  if (b[n - 1] < in->interval_end) return set_error(DG_ERR_ARG, "bucket_starts do not cover the interval");
   g->hb = b;
   g->nb = n - 1;
   out->period_ms = 1;
@@ -1356,19 +1358,24 @@ static int upload_grain(CallScratch* cs, Grain* g, hipStream_t st) {
   return DG_OK;
 }
 
-static Cursors plan_cursors(const Segment* seg, const dg_scan* q, const Grain& g) {
+static Cursors plan_cursors(const Segment* seg, int seg_index, const dg_scan* q, const Grain& g) {
   Cursors c;
   if (seg->nrows == 0) return c;
   const int64_t P = q->period_ms;
   const int64_t data_s = seg->min_time;
   if (g.hb) {
-    // dataInterval = [minTime, gran.bucketEnd(maxTime)) (QueryableIndexStorageAdapter.makeCursors)
+    // dataInterval = [minTime, gran.bucketEnd(maxTime)) (QueryableIndexStorageAdapter.makeCursors):
+    // the caller's bucketEnd when given, else the end of the listed bucket holding maxTime
     const int64_t km = g.coord(seg->max_time);
-    const int64_t data_e = km < 0 ? g.hb[0] : (km >= g.nb ? kMaxInstant : g.hb[km + 1]);
+    const int64_t data_e = q->seg_bounds ? q->seg_bounds[2 * seg_index + 1]
+                                         : (km < 0 ? g.hb[0] : (km >= g.nb ? kMaxInstant : g.hb[km + 1]));
     if (!(q->interval_start < data_e && data_s < q->interval_end)) return c;
-    c.any = true;
-    c.t_lo = std::max(q->interval_start, data_s);
+    // the segment's cursors start at its iterable's first bucket (gran.bucketStart of the actual start)
+    const int64_t it0 = q->seg_bounds ? q->seg_bounds[2 * seg_index] : g.hb[0];
+    c.t_lo = std::max(std::max(q->interval_start, data_s), std::max(it0, g.hb[0]));
     c.t_hi = std::min(q->interval_end, data_e);
+    if (c.t_lo >= c.t_hi) return c;
+    c.any = true;
     c.bucket0 = g.coord(c.t_lo);
     c.nbuckets = g.coord(c.t_hi - 1) - c.bucket0 + 1;
     c.need_time = true;
@@ -1957,7 +1964,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
-    cur[i] = plan_cursors(seg, q, gr);
+    cur[i] = plan_cursors(seg, i, q, gr);
     out_nb[i] = (int32_t)(cur[i].any ? cur[i].nbuckets : 0);
     m.segment_rows += seg->nrows;
     if (!cur[i].any) continue;
@@ -2157,7 +2164,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
-    cur[i] = plan_cursors(seg, q, gr);
+    cur[i] = plan_cursors(seg, i, q, gr);
     m.segment_rows += seg->nrows;
     for (int b = 0; b < bcap; ++b) out_n[(int64_t)i * bcap + b] = -1;
     if (!cur[i].any) continue;
@@ -3093,7 +3100,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   for (int i = 0; i < n; ++i) sv[i] = reinterpret_cast<Segment*>(segs[i]);
   std::vector<Cursors> cur(n);
   for (int i = 0; i < n; ++i) {
-    cur[i] = plan_cursors(sv[i], q, gr);
+    cur[i] = plan_cursors(sv[i], i, q, gr);
     m.segment_rows += sv[i]->nrows;
   }
   // merged dictionaries (GroupByMergingQueryRunnerV2 merges by value; merged ids order like values)

@@ -820,6 +820,12 @@ def merge_groupby_columnar(query: Q.GroupByQuery, partials: Sequence[GroupByPart
         return parts[0].times, parts[0].dims, parts[0].aggs
     times = np.concatenate([p.times for p in parts])
     keys_t = times if not gran.is_all else np.zeros(len(times), np.int64)
+    if gran.is_calendar and len(times):
+        # segments on their own bucket chains (segment_queries): the toolchest's mergeResults orders
+        # and combines rows by gran.bucketStart(timestamp) and emits that start
+        # (GroupByQuery.getRowOrdering(true), GroupByQuery.java:575-576; GroupByBinaryFnV2.java:78-81)
+        u, inv = np.unique(times, return_inverse=True)
+        keys_t = np.array([gran.bucket_start(int(x)) for x in u], np.int64)[inv]
     dim_codes = []
     dim_values = []
     coded = all(p.codes is not None for p in parts)

@@ -27,11 +27,11 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_structs():
     N = importlib.import_module("incubator-druid_amd._native")
-    assert N.lib().dg_abi_version() == 9
+    assert N.lib().dg_abi_version() == 10
     # struct layouts the header fixes (LP64)
     assert ctypes.sizeof(N.dg_filter) == 64
     assert ctypes.sizeof(N.dg_agg) == 32
-    assert ctypes.sizeof(N.dg_scan) == 88
+    assert ctypes.sizeof(N.dg_scan) == 96
     assert ctypes.sizeof(N.dg_metrics) == 120
     assert ctypes.sizeof(N.dg_topn_lists) == 40
     assert ctypes.sizeof(N.dg_topn) == 56

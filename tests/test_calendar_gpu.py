@@ -183,7 +183,7 @@ def test_fixed_grid_periods_around_the_epoch(R, Q, O, epoch_segs, gran):
                           aggregations=[Q.count("rows"), Q.long_sum("sumLongSequential"),
                                         Q.float_sum("fsum", "sumFloatNormal")])
     exp = O.run(q, o)
-    assert len(exp) > 10
+    assert len(exp) >= 4  # (P1D: five days)
     assert_results(q, R.run_query(q, g), exp)
     _exact_float(R.run_query(q, g), exp, "fsum")
     qg = Q.GroupByQuery(intervals=["1969-12-29/1970-01-03"], granularity=gran, dimensions=["dimZipf"],
