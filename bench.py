@@ -286,6 +286,26 @@ def cpu_baseline_oracle(query, path, rows, seconds, selected_fraction):
                       f"{selected_fraction:.4g}", "cpu_model": _cpu_model()}
 
 
+def pmc_traffic(args, kname):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes of this same bench
+    command (profiles/pmc_<config>.json, written by tools/prof_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE rocprofv3 runs). FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM: gfx950 tallies a
+    wide streaming read's 128-B requests at 64 B; the decoders stage their blocks with 16-B loads);
+    the raw value is kept beside it."""
+    f = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"pmc_{args.config}.json")
+    if not os.path.exists(f):
+        return {}
+    pm = json.load(open(f))
+    ks = [k for k in pm["kernels"] if any(k.startswith(n) or f"::{n}" in k for n in kname.split("+"))]
+    if not ks:
+        return {}
+    calls = sum(pm["kernels"][k]["calls"] for k in ks)
+    fetch = sum(pm["kernels"][k]["fetch_bytes"] for k in ks) / calls
+    write = sum(pm["kernels"][k]["write_bytes"] for k in ks) / calls
+    return {"traffic": 2 * fetch + write, "traffic_fetch_raw": fetch, "traffic_write": write,
+            "traffic_source": os.path.join("profiles", os.path.basename(f)) + f" ({pm.get('label', '')})"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -402,6 +422,12 @@ def main():
         # groupBy payload columns decoded in place on the side stream (overlapping keygen + sort)
         phases["decode_payload_side"] = per_step("decode_side_ms")
         kernels["decode_payload_side"] = (dk + " (payload, side stream)", bytes_side, 1, phases["decode_payload_side"])
+    if per_step("lz4_general_ms") > 0:
+        # the general LZ4 decoder alone (token-dense blocks; main and side stream): its own HIP-event span
+        # per stream, its blocks' stored bytes; a "launch" here is one kernel launch, as rocprofv3 counts
+        phases["lz4_general"] = per_step("lz4_general_ms")
+        kernels["lz4_general"] = ("k_lz4_decode", per_step("lz4_general_bytes"),
+                                  max(per_step("lz4_general_launches"), 1.0), phases["lz4_general"])
     if isinstance(query, Q.GroupByQuery):
         phases.update({"keygen": per_step("keygen_ms"), "sort": per_step("sort_ms"), "reduce": per_step("reduce_ms")})
         passes = max(1, int(round(per_step("sort_passes"))))
@@ -417,7 +443,10 @@ def main():
     if phases["bitmap"] > 0:
         kernels["bitmap"] = ("k_concise_or+k_filter_eval" if args.bitmap == "concise" else "k_roaring_or+k_filter_eval",
                              None, 1, phases["bitmap"])
-    dom = max(kernels, key=lambda k: kernels[k][3]) if kernels else None
+    # the dominant kernel: the longest single-kernel span (phases that group several kernels, like the
+    # decode phase or the side-stream payload decode, are reported in phases_ms)
+    single = {k: v for k, v in kernels.items() if k in ("lz4_general", "aggregate", "bitmap", "sort", "keygen")}
+    dom = max(single or kernels, key=lambda k: (single or kernels)[k][3]) if kernels else None
     roofline = None
     if dom is not None:
         kname, kbytes, launches, kms = kernels[dom]
@@ -427,6 +456,7 @@ def main():
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
                     "bytes_per_launch": kbytes / launches if kbytes else None, "avg_launch_ms": per_launch_ms,
                     "launches_per_step": launches}
+        roofline.update(pmc_traffic(args, kname))
     line = {
         "metric": "filtered rows aggregated/sec",
         "value": value,
@@ -441,7 +471,8 @@ def main():
         "dtype": "int64/f64",
         "data": "synthetic (basic schema columns, seeded numpy generator, written as Druid v9 segments)",
         "config": {"workload": desc, "config": args.config, "rows_per_segment": rows_per, "segments_per_gpu": nseg,
-                   "compression": args.compression, "bitmap": args.bitmap, "long_encoding": args.long_encoding,
+                   "compression": args.compression, "lz4_mode": args.lz4_mode, "bitmap": args.bitmap,
+                   "long_encoding": args.long_encoding,
                    "parallelism": f"segments sharded over {world} GPU(s)"},
         "roofline": roofline,
         "phases_ms": phases,

@@ -204,6 +204,12 @@ typedef struct {
   /* groupBy: payload columns decoded in place on the side stream, overlapping the key build + sort */
   double decode_side_ms;     /* device time of those decodes (their own stream) */
   int64_t bytes_side;        /* their algorithmic bytes (part of bytes_read) */
+  /* the general LZ4 decoder (token-dense blocks), both streams: device time of its launches, the
+     stored bytes and number of the blocks it decoded, and its launches */
+  double lz4_general_ms;
+  int64_t lz4_general_bytes;
+  int32_t lz4_general_blocks;
+  int32_t lz4_general_launches;
 } dg_metrics;
 
 /* Aggregate values are returned in 8-byte slots: int64 for count/long*, double for double*,

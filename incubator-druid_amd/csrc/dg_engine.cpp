@@ -390,7 +390,19 @@ struct DecodeBatch {
   int64_t* last_expanded = nullptr;
   uint8_t* last_slots = nullptr;  // decode slots of the last viewed LZ4 / LZF column
   int64_t bytes = 0;  // algorithmic bytes read
+  // the general decoder's launches bracketed by these events (when set), and its blocks' stored bytes
+  hipEvent_t gen_a = nullptr, gen_b = nullptr;
+  int64_t gen_bytes = 0;
+  int32_t gen_blocks = 0;
+  int32_t gen_launches = 0;
 };
+// device time of the general decoder's launches of a batch (0 if it launched none)
+static double gen_ms(const DecodeBatch& db) {
+  if (!db.gen_blocks || !db.gen_a) return 0;
+  float f = 0;
+  hipEventElapsedTime(&f, db.gen_a, db.gen_b);
+  return f;
+}
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
 static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st);
 static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr);
@@ -1201,8 +1213,13 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
   launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
+  for (int i = 0; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
+  db->gen_blocks += nh;
+  db->gen_launches += (nn > 0) + (nh - nn > 0);
+  if (db->gen_a && nh) hipEventRecord(db->gen_a, st);
   launch_lz4_decode(d, nn, 0, d_err, st, d_prof);
   launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
+  if (db->gen_a && nh) hipEventRecord(db->gen_b, st);
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
 
@@ -1430,6 +1447,7 @@ int dg_context_create(int device, dg_context** out) {
   for (auto& e : ctx->ev) hipEventCreate(&e);
   if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) ctx->side = nullptr;
   for (auto& e : ctx->side_ev) hipEventCreate(&e);
+  for (auto& e : ctx->gen_ev) hipEventCreate(&e);
   *out = reinterpret_cast<dg_context*>(ctx);
   return DG_OK;
 }
@@ -1445,6 +1463,7 @@ void dg_context_release(dg_context* c) {
   }
   for (auto& e : ctx->ev) hipEventDestroy(e);
   for (auto& e : ctx->side_ev) hipEventDestroy(e);
+  for (auto& e : ctx->gen_ev) hipEventDestroy(e);
   for (auto& b : ctx->free_blocks) hipFree(b.first);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1961,6 +1980,8 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   std::vector<int64_t> tiles_rows(n, 0);
   std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db;
+  db.gen_a = ctx->gen_ev[0];
+  db.gen_b = ctx->gen_ev[1];
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
@@ -2085,6 +2106,10 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
   m.bitmap_ms = f1;
   m.decode_ms = f2;
+  m.lz4_general_ms = gen_ms(db);
+  m.lz4_general_bytes = db.gen_bytes;
+  m.lz4_general_blocks = db.gen_blocks;
+  m.lz4_general_launches = db.gen_launches;
   m.aggregate_ms = f3;
   m.total_ms = ms_since(t0);
   if (metrics) *metrics = m;
@@ -2160,6 +2185,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   std::vector<int64_t> card(n, 1), tiles_rows(n, 0);
   std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db;
+  db.gen_a = ctx->gen_ev[0];
+  db.gen_b = ctx->gen_ev[1];
   bool any_multi = false;
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
@@ -2681,6 +2708,10 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
   m.bitmap_ms = f1;
   m.decode_ms = f2;
+  m.lz4_general_ms = gen_ms(db);
+  m.lz4_general_bytes = db.gen_bytes;
+  m.lz4_general_blocks = db.gen_blocks;
+  m.lz4_general_launches = db.gen_launches;
   m.aggregate_ms = f3;
   m.total_ms = ms_since(t0);
   ht.mark("done");
@@ -3162,6 +3193,10 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   }
   std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db, db_side;  // db_side: payload columns decoded in place (side stream)
+  db.gen_a = ctx->gen_ev[0];
+  db.gen_b = ctx->gen_ev[1];
+  db_side.gen_a = ctx->gen_ev[2];
+  db_side.gen_b = ctx->gen_ev[3];
   for (int i = 0; i < n; ++i) {
     GbJob& j = gj[i];
     memset(&j, 0, sizeof j);
@@ -3320,6 +3355,10 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   hipEventElapsedTime(&f6, ctx->ev[6], ctx->ev[4]);
   m.bitmap_ms = f1;
   m.decode_ms = f2;
+  m.lz4_general_ms = gen_ms(db) + gen_ms(db_side);
+  m.lz4_general_bytes = db.gen_bytes + db_side.gen_bytes;
+  m.lz4_general_blocks = db.gen_blocks + db_side.gen_blocks;
+  m.lz4_general_launches = db.gen_launches + db_side.gen_launches;
   m.aggregate_ms = f3;
   m.keygen_ms = f4;
   m.sort_ms = f5;

@@ -307,6 +307,8 @@ struct Context {
   // keys (the two only meet at the reduce); side_ev[0] = its inputs are staged, [1..2] = decode span
   hipStream_t side = nullptr;
   hipEvent_t side_ev[3] = {};
+  // the general LZ4 decoder's own span on each stream (main, side): its roofline figure (dg_metrics)
+  hipEvent_t gen_ev[4] = {};
   // dg_context_set_limit(DG_LIMIT_GROUP_ELEMENTS): most sort elements one groupBy call may build
   uint64_t max_elements = ~0ull;
   std::vector<std::shared_ptr<MergedDict>> dict_cache;  // most recent last
