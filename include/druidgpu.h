@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 10
+#define DG_ABI_VERSION 11
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -491,6 +491,11 @@ int dg_records_pack(const uint64_t* slots, int64_t n, const dg_record_layout* la
  * s_memtime stamps of the decoder's phases + counters (tools/lz4_profile.py prints them). */
 int dg_debug_lz4_decode(dg_context* ctx, const uint8_t* const* blocks, const int32_t* lens, int32_t n, uint8_t* out,
                         int32_t* out_lens, double* ms, uint64_t* prof);
+
+/* Which HIP decoder the attach-time classification routes one raw LZ4 block to (host only, no
+ * device work): *kind = -1 malformed (fails validation), 0 general (k_lz4_decode), 1 general with
+ * wide checkpoints, 2 light (k_lz4_light), 3 window (k_lz4_window). Since ABI 11. */
+int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind);
 
 #ifdef __cplusplus
 }

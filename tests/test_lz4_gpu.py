@@ -238,3 +238,101 @@ def test_light_boundary_streams_pinned_by_system_liblz4(O):
         dst = ctypes.create_string_buffer(BLOCK + 16)
         n = lib.LZ4_decompress_safe(b, dst, len(b), BLOCK)
         assert n > 0 and dst.raw[:n] == O.lz4_decompress(b), name
+
+
+def _window_cases(rng):
+    """Blocks for the window decoder (k_lz4_window: copies from at most 8 bytes back plus a few
+    "holes" copied from farther): 8-byte value runs at distance 8, distances 1..7 (dividing 8 or
+    not), far copies whose holes chain through earlier holes, long literal runs and a decoded
+    length that is not a multiple of 8 (a partial last qword)."""
+    r = lambda k: rng.integers(0, 256, k).astype(np.uint8).tobytes()  # noqa: E731
+    cases = {}
+    n8 = BLOCK // 8
+    seq = np.arange(n8, dtype=np.int64)
+    cases["seqlong"] = _lz4_hc((seq % 10000).astype("<i8").tobytes())
+    cases["time"] = _lz4_hc(np.round(seq * 1.3333 + 1388534400000).astype("<i8").tobytes())
+    cases["seqlong_partial"] = _lz4_hc((seq[:n8 - 3] % 10000).astype("<i8").tobytes() + b"\x01\x02\x03\x04\x05")
+
+    def values(k, seqs):  # k values: one new low byte per value, the other 7 copied from 8 back
+        for _ in range(k):
+            seqs.append((r(1), 8, 7))
+        return 8 * k
+
+    # far copies: every ~600 bytes a far match (holes), the next one often copying an earlier
+    # hole (depth 2..3), then 8 literal bytes overwrite every class of the window
+    seqs, o, far = [(r(8), 8, 8)], 16, []
+    while o < BLOCK - 800:
+        o += values(int(rng.integers(40, 80)), seqs)
+        if far and rng.random() < 0.6:
+            src = far[int(rng.integers(0, len(far)))]
+            d, m = o - src, 6
+        else:
+            d, m = int(rng.integers(9, min(o, 4000))), int(rng.integers(4, 12))
+        seqs.append((b"", d, m))
+        far.append(o)
+        o += m
+        seqs.append((r(8), 8, 8))
+        o += 16
+    o += values((BLOCK - 16 - o) // 8, seqs)
+    cases["holes"] = lz4_sequences(seqs, r(BLOCK - o))
+    # distances 1, 2, 4 (window unchanged after 8 bytes) and 3, 5, 6, 7 (walked byte by byte)
+    seqs, o = [(r(8), 8, 8)], 16
+    while o < BLOCK - 1200:
+        o += values(int(rng.integers(5, 30)), seqs)
+        d = int(rng.choice([1, 2, 3, 4, 5, 6, 7]))
+        m = int(rng.integers(4, 400 if d in (1, 2, 4) else 60))
+        seqs.append((r(int(rng.integers(0, 3))), d, m))
+        o += len(seqs[-1][0]) + m
+    cases["short_dist"] = lz4_sequences(seqs, r(7))
+    # a long literal run first, long distance-8 runs (repeated values), then an odd tail
+    seqs, o = [(r(300), 8, 1000)], 1300
+    while o < BLOCK - 4000:
+        o += values(int(rng.integers(10, 50)), seqs)
+        m = int(rng.integers(8, 3000))
+        seqs.append((r(2), 8, m))
+        o += 2 + m
+    o += values((BLOCK - 100 - o) // 8, seqs)
+    cases["long_runs8"] = lz4_sequences(seqs, r(BLOCK - o - 3))  # decoded length 65533
+    return cases
+
+
+def test_window_classification():
+    """CPU: the attach-time classification routes the window cases to the window decoder and the
+    headline's noisy doubles / random ids elsewhere."""
+    N = importlib.import_module("incubator-druid_amd._native")
+    rng = np.random.default_rng(23)
+
+    def kind(b):
+        k = ctypes.c_int32()
+        N.check(N.lib().dg_debug_lz4_classify(b, len(b), ctypes.byref(k)))
+        return k.value
+
+    for name, b in _window_cases(rng).items():
+        assert kind(b) == 3, name
+    assert kind(_lz4_hc(rng.normal(5000.0, 1.0, BLOCK // 8).astype("<f8").tobytes())) == 0
+    ids = b"".join(int(x).to_bytes(4, "little")[:3] for x in rng.integers(1, 100001, BLOCK // 3 + 1))[:BLOCK]
+    assert kind(_lz4_hc(ids)) == 2
+    assert kind(b"\x00\x01") == -1
+
+
+def test_window_streams_pinned_by_system_liblz4(O):
+    lib = ctypes.CDLL("liblz4.so.1")
+    rng = np.random.default_rng(23)
+    for name, b in _window_cases(rng).items():
+        dst = ctypes.create_string_buffer(BLOCK + 16)
+        n = lib.LZ4_decompress_safe(b, dst, len(b), BLOCK)
+        assert n > 0 and dst.raw[:n] == O.lz4_decompress(b), name
+
+
+@pytest.mark.gpu
+def test_lz4_window_decoder_bit_exact(O):
+    rng = np.random.default_rng(23)
+    cases = _window_cases(rng)
+    blocks = list(cases.values()) * 4  # several per launch
+    got = gpu_decode(blocks)
+    for name, b, g in zip(list(cases) * 4, blocks, got):
+        exp = O.lz4_decompress(b)
+        if g != exp:
+            bad = [i for i in range(min(len(g or b""), len(exp))) if g[i] != exp[i]][:8] if g else None
+            raise AssertionError(f"{name}: decoded {None if g is None else len(g)} vs {len(exp)} bytes, "
+                                 f"first differences at {bad}")

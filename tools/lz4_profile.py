@@ -18,6 +18,15 @@ S = importlib.import_module("incubator-druid_amd.segment")
 W = importlib.import_module("incubator-druid_amd.writer")
 BLOCK = 65536
 PHASES = ["stage", "parse+scan", "jobs+read", "fill+write", "resolve", "output"]
+# k_lz4_window (blocks whose copies come from <= 8 bytes back): its own phases
+WIN_PHASES = ["stage", "parse+scan", "transfer", "fn-scan", "sources", "output"]
+KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light", 3: "window"}
+
+
+def classify(block):
+    k = ctypes.c_int32()
+    N.check(N.lib().dg_debug_lz4_classify(block, len(block), ctypes.byref(k)))
+    return KINDS[k.value]
 
 
 def payloads(rng, k):
@@ -55,12 +64,22 @@ def run(ctx, blocks):
     return ms.value, p
 
 
-def report(name, ms, p):
+def report(name, ms, p, decoder=""):
     d = np.diff(p[:, :7], axis=1)
-    print(f"{name:10s} blocks={len(p):4d} kernel={ms:7.3f} ms  in_bytes(avg)={p[:, 9].mean():7.0f} "
+    print(f"{name:10s} [{decoder}] blocks={len(p):4d} kernel={ms:7.3f} ms  in_bytes(avg)={p[:, 9].mean():7.0f} "
           f"jump_rounds(avg/max)={p[:, 8].mean():5.1f}/{p[:, 8].max():3d} coop_jobs={p[:, 10].mean():6.1f} "
           f"cps={p[:, 11].mean():6.1f} listed={p[:, 7].mean():7.0f}")
-    print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(PHASES, d.mean(axis=0))))
+    names = WIN_PHASES if decoder == "window" else PHASES
+    print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(names, d.mean(axis=0))))
+    if decoder == "window":  # per-wave end of the table walk, the barrier after it, from stamp 4
+        we = p[:, 16:24] - p[:, 4:5]  # waves 0-7
+        oe = p[:, 24:32] - p[:, 5:6]
+        print(f"   table walk end per wave (waves 0-7): first={we.min(axis=1).mean():8.0f} last={we.max(axis=1).mean():8.0f}  "
+              f"barrier={np.mean(p[:, 12] - p[:, 4]):8.0f}  rounds(avg)={p[:, 8].mean():4.1f}")
+        print(f"   output end per wave (waves 0-7): first={oe.min(axis=1).mean():8.0f} last={oe.max(axis=1).mean():8.0f} "
+              f"wave0={oe[:, 0].mean():8.0f}")
+    if decoder != "general":
+        return
     fw = p[:, 16:32] - p[:, 3:4]  # each wave's own end of the fill, from the start of the fill
     print(f"   fill end per wave (mean over blocks): first={fw.min(axis=1).mean():8.0f} last={fw.max(axis=1).mean():8.0f}")
 
@@ -68,14 +87,17 @@ def report(name, ms, p):
 def main():
     ctx = S.GpuContext.get(0)
     rng = np.random.default_rng(1)
-    pays = payloads(rng, 92)
+    # 1024 blocks of a kind: four per CU, so most blocks run with the decoder's code already in the
+    # instruction cache (92 blocks = one cold block per CU)
+    pays = payloads(rng, int(os.environ.get("LZ4_PROFILE_BLOCKS", "1024")))
     comp = {k: [W.lz4_compress(x, "hc") for x in v] for k, v in pays.items()}
     kinds = sys.argv[1:] or list(comp)
     for k, blocks in comp.items():
         if k not in kinds:
             continue
         ms, p = run(ctx, blocks)
-        report(k, ms, p)
+        kinds = sorted({classify(b) for b in blocks})
+        report(k, ms, p, "/".join(kinds))
     if sys.argv[1:] and "mix" not in kinds:
         return
     mix = []
