@@ -494,7 +494,7 @@ int dg_debug_lz4_decode(dg_context* ctx, const uint8_t* const* blocks, const int
 
 /* Which HIP decoder the attach-time classification routes one raw LZ4 block to (host only, no
  * device work): *kind = -1 malformed (fails validation), 0 general (k_lz4_decode), 1 general with
- * wide checkpoints, 2 light (k_lz4_light), 3 window (k_lz4_window). Since ABI 11. */
+ * wide checkpoints, 2 light (k_lz4_light). Since ABI 11. */
 int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind);
 
 #ifdef __cplusplus

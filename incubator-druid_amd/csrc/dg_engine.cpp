@@ -1017,7 +1017,7 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
   j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
   j.vstride = 0;
-  j.win = b.cp_win.empty() ? 0 : b.cp_win[k];
+  j.pad_ = 0;
   return j;
 }
 
@@ -1199,17 +1199,12 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   // per-thread sequence registers)
   // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
   // blocks per CU)
-  // window blocks (copies from at most 8 bytes back: sequential longs, timestamps) go first, to the
-  // window decoder (k_lz4_window: no per-byte entry image), narrow then wide
-  auto part = [&](int lo, int hi, bool (*pred)(const Lz4Job&)) {
-    return (int)(std::stable_partition(db->jobs.begin() + lo, db->jobs.begin() + hi, pred) - db->jobs.begin());
-  };
-  const int nh = part(0, n, [](const Lz4Job& j) { return !j.light; });
-  const int nw = part(0, nh, [](const Lz4Job& j) { return j.win != 0; });
-  const int nwn = part(0, nw, [](const Lz4Job& j) { return !j.wide; });
-  const int nn = part(nw, nh, [](const Lz4Job& j) { return !j.wide; });
+  const int nh = (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.light; }) -
+                       db->jobs.begin());
+  const int nn = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
+                       db->jobs.begin());
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
-  if (nn - nw <= 16 * 256) std::stable_sort(db->jobs.begin() + nw, db->jobs.begin() + nn, by_ncp);
+  if (nn <= 16 * 256) std::stable_sort(db->jobs.begin(), db->jobs.begin() + nn, by_ncp);
   if (nh - nn <= 16 * 256) std::stable_sort(db->jobs.begin() + nn, db->jobs.begin() + nh, by_ncp);
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
@@ -1220,13 +1215,10 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
   for (int i = 0; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
   db->gen_blocks += nh;
-  db->gen_launches += (nwn > 0) + (nw - nwn > 0) + (nn - nw > 0) + (nh - nn > 0);
+  db->gen_launches += (nn > 0) + (nh - nn > 0);
   if (db->gen_a && nh) hipEventRecord(db->gen_a, st);
-  auto pr = [&](int at) { return d_prof ? d_prof + (size_t)at * kLz4ProfWords : nullptr; };
-  launch_lz4_window(d, nwn, 0, d_err, st, pr(0));
-  launch_lz4_window(d + nwn, nw - nwn, 1, d_err, st, pr(nwn));
-  launch_lz4_decode(d + nw, nn - nw, 0, d_err, st, pr(nw));
-  launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, pr(nn));
+  launch_lz4_decode(d, nn, 0, d_err, st, d_prof);
+  launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
   if (db->gen_a && nh) hipEventRecord(db->gen_b, st);
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
@@ -4098,9 +4090,9 @@ int dg_timeseries_merge(const dg_scan* scan, int32_t n_lists, const int32_t* n, 
 extern "C" int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind) {
   if (!block || len <= 0 || len > kBlockBytes + 2048 || !kind) return set_error(DG_ERR_ARG, "bad arguments");
   std::vector<uint32_t> one;
-  int wide = 0, light = 0, nfine = 0, win = 0;
-  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine, &win);
-  *kind = d < 0 ? -1 : light ? 2 : win ? 3 : wide ? 1 : 0;
+  int wide = 0, light = 0, nfine = 0;
+  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine);
+  *kind = d < 0 ? -1 : light ? 2 : wide ? 1 : 0;
   return DG_OK;
 }
 
@@ -4118,7 +4110,6 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.cp_wide.assign(n, 0);
   b.cp_light.assign(n, 0);
   b.cp_fine.assign(n, 0);
-  b.cp_win.assign(n, 0);
   b.dec_len.resize(n);
   int64_t total = 0;
   for (int i = 0; i < n; ++i) {
@@ -4132,12 +4123,11 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
     std::vector<uint32_t> one;
-    int wide = 0, light = 0, nfine = 0, win = 0;
-    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine, &win);
+    int wide = 0, light = 0, nfine = 0;
+    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine);
     b.cp_wide[i] = (uint8_t)wide;
     b.cp_light[i] = (uint8_t)light;
     b.cp_fine[i] = nfine;
-    b.cp_win[i] = (uint8_t)win;
     b.cp_off[i] = (int64_t)cps.size();
     b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size() - nfine;
     b.dec_len[i] = d < 0 ? 0 : d;

@@ -65,16 +65,8 @@ struct Lz4Job {
   // and value v goes to dst + v * vstride (a column of the groupBy payload records, written in place);
   // bytes past expect_len are then not written (they would land in the next segment's records)
   int32_t vstride;
-  int32_t win;         // copies mostly from <= 8 bytes back: decoded by the window kernel (k_lz4_window)
+  int32_t pad_;
 };
-
-// Window blocks (token-dense blocks of 8-byte or 4-byte values: sequential longs, timestamps): every
-// match byte copies from at most 8 bytes back except for copies from at most kWinFar "far" source
-// positions (far matches, and near copies reaching before their checkpoint interval); no checkpoint
-// interval walks more than kWinMaxWork bytes. Classified at attach by following the decoder's walks
-// (lz4_index_block).
-constexpr int kWinFar = 1024;
-constexpr int kWinMaxWork = 512;
 
 // Light blocks (literal-heavy: random ids, high-entropy values): at most kLtMaxCps checkpoint
 // intervals and copy chains of at most kLtMaxDepth hops. k_lz4_light decodes them with a small
@@ -111,10 +103,8 @@ struct VsJob {
 // *light (optional): the block qualifies for the light decoder (kLtMaxCps / kLtMaxDepth).
 // *light = g > 0 when light: the block's checkpoints are followed by *nfine light checkpoints, one
 // every g sequences (g the fewest sequences per checkpoint that fit the light decoder's threads).
-// *win (optional): a non-light block that qualifies for the window decoder (kWinFar, kWinMaxWork
-// per checkpoint interval).
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr,
-                    int* nfine = nullptr, int* win = nullptr);
+                    int* nfine = nullptr);
 
 struct AggPlan {
   int32_t n;
@@ -241,7 +231,6 @@ struct BlockColumn {
   std::vector<uint8_t> cp_wide;        // LZ4: block b keeps a checkpoint every 2 * kLzSeqPerCp sequences
   std::vector<uint8_t> cp_light;       // LZ4: block b goes to the light decoder (sequences per light checkpoint)
   std::vector<int32_t> cp_fine;        // LZ4: light checkpoints of block b (after its cp_n checkpoints)
-  std::vector<uint8_t> cp_win;         // LZ4: block b goes to the window decoder
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
   int64_t index_bytes = 0;             // LZ4: bytes of the checkpoint index (read per query)
   DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)
@@ -375,7 +364,6 @@ constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (dia
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
-void launch_lz4_window(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // one multi-value dimension's decoded row lists, validated before use (bit 2 of the error word)

@@ -887,530 +887,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
-// Window decoder: token-dense blocks whose match bytes copy from at most 8 bytes back, apart from at
-// most kWinFar "far" sources (attach-time classification, lz4_window_ok). Columns of 8-byte values
-// (sequential longs, timestamps: [1-2 literal bytes, 6-7 byte match at distance 8] per value) are
-// such blocks: every byte is a function of the 8 bytes before it, so the decoder needs no per-byte
-// entry image and no pointer jumping over the block.
-//   1. stage the block in LDS; thread t parses checkpoint interval t into registers (as k_lz4_decode);
-//      a block scan places the intervals;
-//   2. each thread walks its interval with a symbolic window, one entry per residue class of the
-//      position mod 8: a known byte, a far reference (the value of a marked earlier position) or
-//      untouched (= the incoming window's entry of that class). Far references come from far matches
-//      and from near copies whose source entry is untouched, so an untouched class is always the
-//      identity and the final window is the interval's transfer function;
-//   3. a block scan composes the transfer functions (an untouched class takes the earlier entry),
-//      giving every thread its incoming window;
-//   4. threads holding marked positions walk again from their incoming window and record each one's
-//      entry in a table (indexed by the position's rank in the bitmap); pointer jumping over the table
-//      resolves its far references (a chain only goes to smaller positions: <= log2(kWinFar) + 1
-//      rounds);
-//   5. a last walk with every byte known: after byte 8q + 7 the window holds exactly bytes
-//      [8q, 8q + 8), and the thread holding that byte stores the qword from registers (a payload value
-//      of the groupBy records, or 8 bytes of a slot).
-// The window is packed: its bytes in a u64 (byte c = class c), the known / far classes as u64 byte
-// masks, the far sources as 16-bit fields. Each thread's sequences live in three 16-element register
-// vectors indexed by the (uniform) sequence number.
-// ------------------------------------------------------------------------------------------------
-constexpr uint32_t kWKnown = 0x80000000u;  // table entry: | byte
-constexpr uint32_t kWFar = 0x40000000u;    // table entry: | source position
-constexpr int kWSrcWords = kBlockBytes / 32;
-typedef __attribute__((ext_vector_type(16))) uint32_t v16u32;
-
-__device__ __forceinline__ uint64_t rotl64(uint64_t v, int sh) { return sh ? (v << sh) | (v >> (64 - sh)) : v; }
-
-// k mod d for 0 <= k < 2^16, 1 <= d <= 8, without an integer division
-__device__ __forceinline__ int mod_small(int k, int d) {
-  if ((d & (d - 1)) == 0) return k & (d - 1);
-  int q = (int)((float)k * __frcp_rn((float)d));
-  int r = k - q * d;
-  r = r < 0 ? r + d : r;
-  return r >= d ? r - d : r;
-}
-__device__ __forceinline__ uint64_t bmask(int n) { return n >= 8 ? ~0ull : (1ull << (8 * n)) - 1; }
-
-struct Win {        // symbolic window (transfer-function walks)
-  uint64_t kb;      // known bytes
-  uint64_t K, F;    // byte masks of the known / far classes (untouched: neither)
-  uint32_t fs[4];   // far source of class c: 16-bit field c & 1 of fs[c >> 1]
-};
-
-__device__ __forceinline__ uint32_t w_fs_get(const Win& w, int c) {
-  uint32_t f0 = w.fs[0], f1 = w.fs[1], f2 = w.fs[2], f3 = w.fs[3];
-  asm("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));  // (registers: no select-of-loads into a stack copy)
-  const int r = c >> 1;
-  const uint32_t v = r == 0 ? f0 : r == 1 ? f1 : r == 2 ? f2 : f3;
-  return (c & 1) ? v >> 16 : v & 0xFFFFu;
-}
-
-__device__ __forceinline__ void w_fs_set(Win& w, int c, uint32_t src) {
-  const uint32_t keep = (c & 1) ? 0x0000FFFFu : 0xFFFF0000u, put = (c & 1) ? src << 16 : src;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) w.fs[r] = (c >> 1) == r ? (w.fs[r] & keep) | put : w.fs[r];
-}
-
-// n <= 8 known bytes (v, little-endian) at positions x, x + 1, ...
-__device__ __forceinline__ void w_put_bytes(Win& w, int x, int n, uint64_t v) {
-  const int sh = 8 * (x & 7);
-  const uint64_t m = rotl64(bmask(n), sh);
-  w.kb = (w.kb & ~m) | (rotl64(v, sh) & m);
-  w.K |= m;
-  w.F &= ~m;
-}
-
-__device__ __forceinline__ void w_put_far(Win& w, int x, uint32_t src) {
-  const uint64_t m = 0xFFull << (8 * (x & 7));
-  w.K &= ~m;
-  w.F |= m;
-  w_fs_set(w, x & 7, src);
-}
-
-// position x copies the entry of class cs (a position inside this walk)
-__device__ __forceinline__ void w_copy(Win& w, int x, int cs) {
-  const int c = x & 7;
-  const uint64_t m = 0xFFull << (8 * c);
-  if ((w.F >> (8 * cs)) & 1) {
-    w_put_far(w, x, w_fs_get(w, cs));
-  } else {
-    w_put_bytes(w, x, 1, (w.kb >> (8 * cs)) & 0xFF);
-  }
-  (void)m;
-}
-
-// B := (A then B): the classes B leaves untouched take A's entries
-__device__ __forceinline__ void w_compose(const Win& A, Win& B) {
-  const uint64_t S = ~(B.K | B.F);
-  const uint64_t fa = S & A.F;
-  B.kb = (B.kb & B.K) | (A.kb & ~B.K);
-  B.K |= S & A.K;
-  B.F |= fa;
-  if (fa) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t hm = ((fa >> (16 * r)) & 1 ? 0xFFFFu : 0u) | ((fa >> (16 * r + 8)) & 1 ? 0xFFFF0000u : 0u);
-      B.fs[r] = (A.fs[r] & hm) | (B.fs[r] & ~hm);
-    }
-  }
-}
-
-__device__ __forceinline__ void w_shfl_up(const Win& a, Win& r, int off) {
-  r.kb = __shfl_up(a.kb, off, 64);
-  r.K = __shfl_up(a.K, off, 64);
-  r.F = __shfl_up(a.F, off, 64);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r.fs[i] = __shfl_up(a.fs[i], off, 64);
-}
-
-struct WinCtx {
-  uint8_t* dst;
-  int vstride, expect_len, total;
-  const uint8_t* s_in;
-  uint32_t* s_src;   // marked source positions (bitmap)
-  uint16_t* s_rank;  // marked positions before each bitmap word
-  uint32_t* s_val;   // table entry of every marked position, by rank
-};
-
-__device__ __forceinline__ int w_rank(const WinCtx& C, int p) {
-  return (int)C.s_rank[p >> 5] + __popc(C.s_src[p >> 5] & ((1u << (p & 31)) - 1u));
-}
-
-__device__ __forceinline__ void w_mark(const WinCtx& C, int p) { atomicOr(&C.s_src[p >> 5], 1u << (p & 31)); }
-
-// does [a, e) hold a marked position?
-__device__ __forceinline__ bool w_has_src(const WinCtx& C, int a, int e) {
-  if (e <= a) return false;
-  const int w0 = a >> 5, w1 = (e - 1) >> 5;
-  for (int w = w0; w <= w1; ++w) {
-    uint32_t m = C.s_src[w];
-    if (w == w0) m &= ~0u << (a & 31);
-    if (w == w1 && ((e & 31) != 0)) m &= (1u << (e & 31)) - 1u;
-    if (m) return true;
-  }
-  return false;
-}
-
-// n <= 8 literal bytes starting k bytes into a literal run (lv: its bytes when L <= kShortLit, else its
-// input offset in the staged block)
-__device__ __forceinline__ uint64_t w_lit_bytes(const WinCtx& C, int L, uint32_t lv, int k, int n) {
-  if (L <= kShortLit) return (uint64_t)(k < 4 ? lv >> (8 * k) : 0u) & bmask(n);
-  const int p = (int)lv + k;
-  const uint32_t* in32 = reinterpret_cast<const uint32_t*>(C.s_in);
-  const int a = p >> 2, sh = (p & 3) * 8;
-  const uint32_t w0 = in32[a], w1 = in32[a + 1], w2 = in32[a + 2];
-  const uint64_t lo = ((uint64_t)w1 << 32) | w0;
-  const uint64_t v = sh ? (lo >> sh) | ((uint64_t)w2 << (64 - sh)) : lo;
-  return v & bmask(n);
-}
-
-// qword q = decoded bytes [8q, 8q + 8) = the window after byte 8q + 7
-__device__ __forceinline__ void wo_emit(const WinCtx& C, int q, uint64_t wb) {
-  if (C.vstride) {  // payload values past expect_len belong to the next segment
-    if ((q << 3) + 8 <= C.expect_len) gst8(C.dst + (size_t)q * C.vstride, (uint32_t)wb, (uint32_t)(wb >> 32));
-  } else {
-    gst8(C.dst + (q << 3), (uint32_t)wb, (uint32_t)(wb >> 32));
-  }
-}
-
-// marks [p, p + n) (word-level atomics)
-__device__ __forceinline__ void w_mark_range(const WinCtx& C, int p, int n) {
-#pragma unroll 1
-  while (n > 0) {
-    const int b = p & 31, k = min(n, 32 - b);
-    atomicOr(&C.s_src[p >> 5], (k == 32 ? ~0u : (1u << k) - 1u) << b);
-    p += k;
-    n -= k;
-  }
-}
-
-// the last n <= 8 bytes of a far match [om, om + M) at distance d > 8: far references to their
-// sources (in the first period when the match overlaps itself)
-__device__ __forceinline__ void w_far_tail(Win& w, int om, int M, int d) {
-  const int n = min(M, 8), x0 = om + M - n;
-  const uint64_t m = rotl64(bmask(n), 8 * (x0 & 7));
-  w.K &= ~m;
-  w.F |= m;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    if ((m >> (8 * c)) & 1) {
-      const int x = x0 + ((c - x0) & 7);
-      const int src = d >= M ? x - d : om - d + (x - om) % d;
-      const uint32_t keep = (c & 1) ? 0x0000FFFFu : 0xFFFF0000u, put = (c & 1) ? (uint32_t)src << 16 : (uint32_t)src;
-      w.fs[c >> 1] = (w.fs[c >> 1] & keep) | put;
-    }
-  }
-}
-
-// The sequence [o, e) through the symbolic window w (transfer-function walk when TRANSFER: an entry
-// copied from an untouched class becomes a far reference to its source, which is marked).
-template <bool TRANSFER>
-__device__ __forceinline__ void w_seq(Win& w, int o, int L, uint32_t lv, int M, int d, const WinCtx& C) {
-  const int om = o + L;
-  {  // the last (at most 8) literal bytes at once
-    const int n = min(L, 8);
-    if (n > 0) w_put_bytes(w, om - n, n, w_lit_bytes(C, L, lv, L - n, n));
-  }
-  if (M <= 0) return;
-  if (d <= 8) {
-    // near copies, byte by byte until the window stops changing (a distance dividing 8: after 8
-    // bytes; distance 8: at once)
-    const int n1 = d == 8 ? 0 : (d & (d - 1)) == 0 ? min(M, 8) : M;
-#pragma unroll 1
-    for (int k = 0; k < n1; ++k) {
-      const int x = om + k, cs = (x - d) & 7;
-      if (TRANSFER && !(((w.K | w.F) >> (8 * cs)) & 1)) {
-        w_put_far(w, x, (uint32_t)(x - d));
-        w_mark(C, x - d);
-      } else {
-        w_copy(w, x, cs);
-      }
-    }
-  } else {  // far copies, sourced in the match's first period
-    w_far_tail(w, om, M, d);
-    if (TRANSFER) w_mark_range(C, om - d, min(M, d));
-  }
-}
-
-// Table entries of the marked positions inside the sequence [o, e), from the window w before it (every
-// class defined: the true incoming window of the interval plus the sequences before).
-__device__ __forceinline__ void w_seq_table(const Win& w, int o, int L, uint32_t lv, int M, int d, const WinCtx& C) {
-  const int om = o + L, e = om + M;
-  auto entry_of_class = [&](int c) -> uint32_t {
-    if (!((w.F >> (8 * c)) & 1)) return kWKnown | (uint32_t)((w.kb >> (8 * c)) & 0xFF);
-    return kWFar | w_fs_get(w, c);
-  };
-#pragma unroll 1
-  for (int wd = o >> 5; wd <= (e - 1) >> 5; ++wd) {
-    const uint32_t word = C.s_src[wd];
-    uint32_t bits = word;
-    if (wd == o >> 5) bits &= ~0u << (o & 31);
-    if (wd == (e - 1) >> 5 && (e & 31)) bits &= (1u << (e & 31)) - 1u;
-    if (!bits) continue;
-    int r = (int)C.s_rank[wd] + __popc(word & ((1u << __builtin_ctz(bits)) - 1u));
-#pragma unroll 1
-    for (; bits; bits &= bits - 1, ++r) {
-      const int x = 32 * wd + __builtin_ctz(bits);
-      uint32_t v;
-      if (x < om) {
-        v = kWKnown | (uint32_t)w_lit_bytes(C, L, lv, x - o, 1);
-      } else if (d > 8) {
-        v = kWFar | (uint32_t)(d >= M ? x - d : om - d + (x - om) % d);
-      } else {
-        const int p = om - d + mod_small(x - om, d);  // the first period: a literal of this sequence or before it
-        v = p >= o ? kWKnown | (uint32_t)w_lit_bytes(C, L, lv, p - o, 1) : entry_of_class(p & 7);
-      }
-      C.s_val[r] = v;
-    }
-  }
-}
-
-// One sequence of the output pass: wb = the true window (every byte known).
-__device__ __forceinline__ void wo_seq(uint64_t& wb, int o, int L, uint32_t lv, int M, int d, const WinCtx& C) {
-  const int om = o + L, e = om + M;
-  auto put = [&](int x, int n, uint64_t v) {
-    const int sh = 8 * (x & 7);
-    const uint64_t m = rotl64(bmask(n), sh);
-    wb = (wb & ~m) | (rotl64(v, sh) & m);
-  };
-  // literals: up to the next qword boundary at a time
-#pragma unroll 1
-  for (int x = o; x < om;) {
-    const int n = min(om - x, 8 - (x & 7));
-    put(x, n, w_lit_bytes(C, L, lv, x - o, n));
-    x += n;
-    if ((x & 7) == 0) wo_emit(C, (x >> 3) - 1, wb);
-  }
-  if (M <= 0) return;
-  int x = om;
-  if (d < 8) {  // byte by byte until the window stops changing
-    const int n1 = (d & (d - 1)) == 0 ? min(M, 8) : M;
-#pragma unroll 1
-    for (; x < om + n1; ++x) {
-      put(x, 1, (wb >> (8 * ((x - d) & 7))) & 0xFF);
-      if ((x & 7) == 7) wo_emit(C, x >> 3, wb);
-    }
-  } else if (d > 8) {
-#pragma unroll 1
-    for (int k = 0; k < M; ++k, ++x) {
-      const uint32_t v = C.s_val[w_rank(C, d >= M ? x - d : om - d + k % d)];
-      put(x, 1, v & 0xFF);
-      if ((x & 7) == 7) wo_emit(C, x >> 3, wb);
-    }
-  }
-#pragma unroll 1
-  for (int y = x | 7; y < e; y += 8) wo_emit(C, y >> 3, wb);  // the window no longer changes
-}
-
-template <bool PROF, int SEQ>
-__global__ __launch_bounds__(kLzThreads) void k_lz4_window(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
-                                                           uint64_t* __restrict__ prof) {
-  static_assert(SEQ <= 16, "sequences of an interval: one 16-element register vector");
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[kLz4InCap + 32];
-  __shared__ uint32_t s_src[kWSrcWords];
-  __shared__ uint16_t s_rank[kWSrcWords];
-  __shared__ uint32_t s_val[kWinFar];
-  __shared__ Win s_wt[kLzWaves];  // wave transfer functions, then wave incoming windows
-  __shared__ int s_bad;
-  __shared__ int s_tmp[kLzWaves];
-
-  const Lz4Job job = jobs[blockIdx.x];
-  const int tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
-  const int n = job.src_len, ncp = job.ncp;
-  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || (job.wide != 0) != (SEQ > kLzSeqPerCp) ||
-      job.dec_len > kBlockBytes || job.dec_len < job.expect_len) {
-    if (tid == 0) atomicOr(err, 1);
-    return;
-  }
-  LZ_STAMP(0);
-  {
-    uint4* dst = reinterpret_cast<uint4*>(s_in);
-    const int n16 = (n + 15) >> 4;
-    for (int i = tid; i < n16; i += kLzThreads) dst[i] = gld16(job.src + 16 * (size_t)i);
-    if (tid == 0) {
-      dst[n16] = make_uint4(0, 0, 0, 0);
-      s_bad = 0;
-    }
-    for (int i = tid; i < kWSrcWords; i += kLzThreads) s_src[i] = 0;
-  }
-  __syncthreads();
-  LZ_STAMP(1);
-  // ---- 1. parse my interval into registers ----
-  v16u32 VL, VD, VV;  // literal length, distance | match length << 16, literal bytes (L <= 4) or offset
-  int cnt = 0, out_rel = 0;
-  bool bad = false;
-  if (tid < ncp) {
-    int pos = (int)gld4(job.cp + tid);
-    const int end = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
-#pragma unroll
-    for (int s = 0; s < SEQ; ++s) {
-      VL[s] = VD[s] = VV[s] = 0;
-      if (pos >= 0 && pos < end) {
-        Tok t;
-        if (parse_tok(s_in, n, pos, t)) {
-          VL[s] = (uint32_t)t.L;
-          VD[s] = (uint32_t)t.off | ((uint32_t)t.M << 16);
-          VV[s] = t.L <= kShortLit ? t.lv : (uint32_t)t.lit;
-          bad |= t.M > 0 && t.off > out_rel + t.L;  // a distance before the interval: checked below
-          out_rel += t.L + t.M;
-          pos = t.next;
-          cnt = s + 1;
-        } else {
-          pos = -1;
-        }
-      }
-    }
-    if (pos != end) s_bad = 1;
-  }
-  int total;
-  const int base = block_scan_lz(out_rel, &total, s_tmp);
-  if (bad) {  // distances reaching before my interval: valid only when they stay inside the block
-    int o = base;
-#pragma unroll 1
-    for (int s = 0; s < cnt; ++s) {
-      const int L = (int)VL[s], d = (int)(VD[s] & 0xFFFF), M = (int)(VD[s] >> 16);
-      if (M > 0 && d > o + L) s_bad = 1;
-      o += L + M;
-    }
-  }
-  __syncthreads();
-  if (s_bad || total != job.dec_len) {
-    if (tid == 0) atomicOr(err, 1);
-    return;
-  }
-  LZ_STAMP(2);
-  const WinCtx C{job.dst, job.vstride, job.expect_len, total, s_in, s_src, s_rank, s_val};
-  // ---- 2. my transfer function (and the marked positions) ----
-  Win T;
-  T.kb = T.K = T.F = 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) T.fs[r] = 0;
-  {
-    int o = base;
-#pragma unroll 1
-    for (int s = 0; s < SEQ; ++s) {  // (a uniform trip count: s indexes the register vectors uniformly)
-      if (s < cnt) {
-        const int L = (int)VL[s], d = (int)(VD[s] & 0xFFFF), M = (int)(VD[s] >> 16);
-        w_seq<true>(T, o, L, VV[s], M, d, C);
-        o += L + M;
-      }
-    }
-  }
-  LZ_STAMP(3);
-  // ---- 3. block scan of the transfer functions: incoming window of every thread ----
-  Win X;  // exclusive prefix within my wave, then my incoming window
-  {
-    Win P = T;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      Win A;
-      w_shfl_up(P, A, off);
-      if (ln >= off) w_compose(A, P);
-    }
-    if (ln == 63) s_wt[wv] = P;
-    w_shfl_up(P, X, 1);
-    if (ln == 0) X.K = X.F = 0;
-  }
-  int nsrc;
-  {  // ranks of the marked positions: exclusive prefix of the bitmap words' popcounts
-    static_assert(kWSrcWords == 2 * kLzThreads, "two bitmap words per thread");
-    __syncthreads();  // every position is marked
-    const int c0 = __popc(s_src[2 * tid]), c1 = __popc(s_src[2 * tid + 1]);
-    const int pre = block_scan_lz(c0 + c1, &nsrc, s_tmp);  // (its barriers also publish s_wt)
-    s_rank[2 * tid] = (uint16_t)pre;
-    s_rank[2 * tid + 1] = (uint16_t)(pre + c0);
-  }
-  if (nsrc > kWinFar) {  // never, for a block the classification admitted
-    if (tid == 0) atomicOr(err, 1);
-    return;
-  }
-  if (wv == 0) {  // exclusive scan of the wave totals (lanes < kLzWaves)
-    Win Q;
-    if (ln < kLzWaves) {
-      Q = s_wt[ln];
-    } else {
-      Q.kb = Q.K = Q.F = 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Q.fs[r] = 0;
-    }
-#pragma unroll
-    for (int off = 1; off < kLzWaves; off <<= 1) {
-      Win A;
-      w_shfl_up(Q, A, off);
-      if (ln >= off) w_compose(A, Q);
-    }
-    Win E;
-    w_shfl_up(Q, E, 1);
-    if (ln == 0) E.K = E.F = 0;
-    if (ln < kLzWaves) s_wt[ln] = E;
-  }
-  __syncthreads();
-  {
-    const Win Wv = s_wt[wv];
-    w_compose(Wv, X);
-  }
-  LZ_STAMP(4);
-  // ---- 4. table entries of the marked positions in my interval, then pointer jumping ----
-  if (nsrc > 0 && w_has_src(C, base, base + out_rel)) {
-    Win Y = X;
-    int o = base;
-#pragma unroll 1
-    for (int s = 0; s < SEQ; ++s) {
-      if (s < cnt) {
-        const int L = (int)VL[s], d = (int)(VD[s] & 0xFFFF), M = (int)(VD[s] >> 16);
-        if (w_has_src(C, o, o + L + M)) w_seq_table(Y, o, L, VV[s], M, d, C);
-        w_seq<false>(Y, o, L, VV[s], M, d, C);
-        o += L + M;
-      }
-    }
-  }
-  if (PROF && ln == 0 && wv < 8) prof[(size_t)blockIdx.x * kLz4ProfWords + 16 + wv] = __builtin_amdgcn_s_memtime();
-  __syncthreads();
-  if (PROF && tid == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + 12] = __builtin_amdgcn_s_memtime();
-  int nrounds = 0;
-  for (int round = 0; nsrc > 0; ++round) {
-    nrounds++;
-    bool open = false;
-    for (int i = tid; i < nsrc; i += kLzThreads) {
-      const uint32_t v = s_val[i];
-      if (v & kWFar) {
-        const uint32_t u = s_val[w_rank(C, (int)(v & 0xFFFF))];
-        if (u != v) s_val[i] = u;  // (an ancestor's entry: known, or a far reference further back)
-        open |= (u & kWFar) != 0;
-      }
-    }
-    if (!__syncthreads_or(open)) break;
-    if (round > 11) {  // > log2(kWinFar) + 1: unreachable
-      if (tid == 0) atomicOr(err, 1);
-      return;
-    }
-  }
-  LZ_STAMP(5);
-  // ---- 5. output: my interval from its (now known) incoming window, one store per qword ----
-  uint64_t wb = X.kb;
-  if (X.F) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if ((X.F >> (8 * c)) & 1) {
-        const uint64_t v = s_val[w_rank(C, (int)w_fs_get(X, c))] & 0xFF;
-        wb = (wb & ~(0xFFull << (8 * c))) | (v << (8 * c));
-      }
-  }
-  {
-    int o = base;
-#pragma unroll 1
-    for (int s = 0; s < SEQ; ++s) {
-      if (s < cnt) {
-        const int L = (int)VL[s], d = (int)(VD[s] & 0xFFFF), M = (int)(VD[s] >> 16);
-        wo_seq(wb, o, L, VV[s], M, d, C);
-        o += L + M;
-      }
-    }
-  }
-  if (tid == ncp - 1 && (total & 7)) wo_emit(C, total >> 3, wb);  // the last, partial qword
-  if (PROF && ln == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + 24 + (wv & 7)] = __builtin_amdgcn_s_memtime();
-  if (PROF) {
-    __syncthreads();
-    LZ_STAMP(6);
-    if (tid == 0) {
-      prof[(size_t)blockIdx.x * kLz4ProfWords + 7] = (uint64_t)nsrc;
-      prof[(size_t)blockIdx.x * kLz4ProfWords + 8] = (uint64_t)nrounds;
-      prof[(size_t)blockIdx.x * kLz4ProfWords + 9] = (uint64_t)n;
-      prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
-    }
-  }
-}
-
-void launch_lz4_window(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
-  if (njobs <= 0) return;
-  if (wide) {
-    if (d_prof) hipLaunchKernelGGL((k_lz4_window<true, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
-    else hipLaunchKernelGGL((k_lz4_window<false, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
-  } else {
-    if (d_prof) hipLaunchKernelGGL((k_lz4_window<true, kLzSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
-    else hipLaunchKernelGGL((k_lz4_window<false, kLzSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // Light decoder: blocks of at most kLtMaxCps checkpoint intervals (<= 2048 sequences) whose copy
 // chains are at most kLtMaxDepth hops long (attach-time classification, lz4_index_block). These are
 // the literal-heavy blocks of high-entropy columns (random dictionary ids, noisy doubles: one long

@@ -178,75 +178,10 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
   }
 }
 
-// Window-decoder eligibility (k_lz4_window, dg_lz4.hip), following the decoder's walks. Its table
-// holds the positions that far references point to: the first period of every match at a distance
-// > 8, and the source of every near copy (distance < 8, walked byte by byte) whose residue class the
-// walk of the copy's checkpoint interval has not written yet (the source lies before the interval,
-// or is a distance-8 copy of a byte that does); the block qualifies with at most kWinFar of them (a chain of far
-// references only goes to smaller positions, so pointer jumping over the table needs at most
-// log2(kWinFar) + 1 rounds). The work of an interval counts the bytes the decoder walks one by one:
-// literals, matches at distances that do not divide 8 and far matches; a match at a distance
-// dividing 8 leaves the window unchanged after its first 8 bytes (distance 8: from its first), so
-// only its qword stores count.
-static bool lz4_window_ok(const uint8_t* in, int n, int seq_per_cp) {
-  thread_local std::vector<uint8_t> mark(kBlockBytes);
-  std::fill(mark.begin(), mark.end(), 0);
-  int pos = 0, out = 0, marked = 0, work = 0;
-  unsigned touched = 0;  // residue classes the interval's walk has written
-  int64_t seq = 0;
-  auto ext = [&](int* len) {
-    for (int b = 255; b == 255 && pos < n;) {
-      b = in[pos++];
-      *len += b;
-    }
-  };
-  auto put_mark = [&](int p) {
-    marked += !mark[p];
-    mark[p] = 1;
-  };
-  for (;;) {
-    if (seq % seq_per_cp == 0) {
-      if (work > kWinMaxWork) return false;
-      work = 0;
-      touched = 0;
-    }
-    seq++;
-    const int tok = in[pos++];
-    int L = tok >> 4;
-    if (L == 15) ext(&L);
-    work += L;
-    for (int k = std::max(0, L - 8); k < L; ++k) touched |= 1u << ((out + k) & 7);
-    out += L;
-    pos += L;
-    if (pos >= n) return work <= kWinMaxWork;
-    const int off = in[pos] | (in[pos + 1] << 8);
-    pos += 2;
-    int M = tok & 15;
-    if (M == 15) ext(&M);
-    M += 4;
-    if (off <= 8) {
-      const int n1 = off == 8 ? 0 : ((off & (off - 1)) == 0 ? std::min(M, 8) : M);
-      work += n1 + (M - n1) / 8 + 1;
-      for (int k = 0; k < n1; ++k) {
-        const int x = out + k;
-        if (!((touched >> ((x - off) & 7)) & 1)) put_mark(x - off);
-        touched |= 1u << (x & 7);
-      }
-    } else {
-      work += M;
-      for (int k = 0; k < std::min(M, off); ++k) put_mark(out - off + k);
-      for (int k = std::max(0, M - 8); k < M; ++k) touched |= 1u << ((out + k) & 7);
-    }
-    if (marked > kWinFar) return false;
-    out += M;
-  }
-}
-
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine, int* win) {
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine) {
   const size_t first = cps->size();
   if (light) *light = 0;
   if (nfine) *nfine = 0;
-  if (win) *win = 0;
   int pos = 0, out = 0;
   int64_t seq = 0;
   auto ext = [&](int* len) {
@@ -290,9 +225,6 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
         *light = 1;
       }
     }
-#ifndef DG_LZ4_NO_WINDOW  // (A/B variant builds: every token-dense block on the general decoder)
-    if (win && !(light && *light) && lz4_window_ok(in, n, *wide ? 2 * kLzSeqPerCp : kLzSeqPerCp)) *win = 1;
-#endif
     return dec;
   };
   for (;;) {
@@ -352,7 +284,6 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->cp_wide.assign(blocks.n, 0);
     col->cp_light.assign(blocks.n, 0);
     col->cp_fine.assign(blocks.n, 0);
-    col->cp_win.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
     const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -361,12 +292,11 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int t = 0; t < nt; ++t)
       th.emplace_back([&, t] {
         for (int32_t b = t; b < blocks.n; b += nt) {
-          int wide = 0, light = 0, nfine = 0, win = 0;
-          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine, &win);
+          int wide = 0, light = 0, nfine = 0;
+          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine);
           col->cp_wide[b] = (uint8_t)wide;
           col->cp_light[b] = (uint8_t)light;
           col->cp_fine[b] = nfine;
-          col->cp_win[b] = (uint8_t)win;
           col->dec_len[b] = d;
           col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size() - nfine;
         }

@@ -240,11 +240,11 @@ def test_light_boundary_streams_pinned_by_system_liblz4(O):
         assert n > 0 and dst.raw[:n] == O.lz4_decompress(b), name
 
 
-def _window_cases(rng):
-    """Blocks for the window decoder (k_lz4_window: copies from at most 8 bytes back plus a few
-    "holes" copied from farther): 8-byte value runs at distance 8, distances 1..7 (dividing 8 or
-    not), far copies whose holes chain through earlier holes, long literal runs and a decoded
-    length that is not a multiple of 8 (a partial last qword)."""
+def _value_run_cases(rng):
+    """Blocks of 8-byte value runs (the general decoder's class mode: copies at distance 8 chaining
+    through the block): sequential longs and timestamps, distances 1..7 (dividing 8 or not) inside
+    the runs, far copies sourcing earlier far copies, long literal runs, long distance-8 runs and a
+    decoded length that is not a multiple of 8."""
     r = lambda k: rng.integers(0, 256, k).astype(np.uint8).tobytes()  # noqa: E731
     cases = {}
     n8 = BLOCK // 8
@@ -258,8 +258,8 @@ def _window_cases(rng):
             seqs.append((r(1), 8, 7))
         return 8 * k
 
-    # far copies: every ~600 bytes a far match (holes), the next one often copying an earlier
-    # hole (depth 2..3), then 8 literal bytes overwrite every class of the window
+    # far copies: every ~600 bytes a far match, the next one often copying an earlier one's bytes
+    # (chains of far copies), then 8 literal bytes
     seqs, o, far = [(r(8), 8, 8)], 16, []
     while o < BLOCK - 800:
         o += values(int(rng.integers(40, 80)), seqs)
@@ -274,8 +274,8 @@ def _window_cases(rng):
         seqs.append((r(8), 8, 8))
         o += 16
     o += values((BLOCK - 16 - o) // 8, seqs)
-    cases["holes"] = lz4_sequences(seqs, r(BLOCK - o))
-    # distances 1, 2, 4 (window unchanged after 8 bytes) and 3, 5, 6, 7 (walked byte by byte)
+    cases["far_chains"] = lz4_sequences(seqs, r(BLOCK - o))
+    # distances 1, 2, 4 (periods dividing 8) and 3, 5, 6, 7 inside the value runs
     seqs, o = [(r(8), 8, 8)], 16
     while o < BLOCK - 1200:
         o += values(int(rng.integers(5, 30)), seqs)
@@ -296,9 +296,9 @@ def _window_cases(rng):
     return cases
 
 
-def test_window_classification():
-    """CPU: the attach-time classification routes the window cases to the window decoder and the
-    headline's noisy doubles / random ids elsewhere."""
+def test_lz4_classification():
+    """CPU: the attach-time classification routes value runs to the general decoder (class mode),
+    random dictionary ids to the light decoder, and rejects malformed blocks."""
     N = importlib.import_module("incubator-druid_amd._native")
     rng = np.random.default_rng(23)
 
@@ -307,27 +307,27 @@ def test_window_classification():
         N.check(N.lib().dg_debug_lz4_classify(b, len(b), ctypes.byref(k)))
         return k.value
 
-    for name, b in _window_cases(rng).items():
-        assert kind(b) == 3, name
+    for name, b in _value_run_cases(rng).items():
+        assert kind(b) in (0, 1), name
     assert kind(_lz4_hc(rng.normal(5000.0, 1.0, BLOCK // 8).astype("<f8").tobytes())) == 0
     ids = b"".join(int(x).to_bytes(4, "little")[:3] for x in rng.integers(1, 100001, BLOCK // 3 + 1))[:BLOCK]
     assert kind(_lz4_hc(ids)) == 2
     assert kind(b"\x00\x01") == -1
 
 
-def test_window_streams_pinned_by_system_liblz4(O):
+def test_value_run_streams_pinned_by_system_liblz4(O):
     lib = ctypes.CDLL("liblz4.so.1")
     rng = np.random.default_rng(23)
-    for name, b in _window_cases(rng).items():
+    for name, b in _value_run_cases(rng).items():
         dst = ctypes.create_string_buffer(BLOCK + 16)
         n = lib.LZ4_decompress_safe(b, dst, len(b), BLOCK)
         assert n > 0 and dst.raw[:n] == O.lz4_decompress(b), name
 
 
 @pytest.mark.gpu
-def test_lz4_window_decoder_bit_exact(O):
+def test_lz4_value_runs_bit_exact(O):
     rng = np.random.default_rng(23)
-    cases = _window_cases(rng)
+    cases = _value_run_cases(rng)
     blocks = list(cases.values()) * 4  # several per launch
     got = gpu_decode(blocks)
     for name, b, g in zip(list(cases) * 4, blocks, got):

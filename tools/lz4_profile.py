@@ -18,9 +18,7 @@ S = importlib.import_module("incubator-druid_amd.segment")
 W = importlib.import_module("incubator-druid_amd.writer")
 BLOCK = 65536
 PHASES = ["stage", "parse+scan", "jobs+read", "fill+write", "resolve", "output"]
-# k_lz4_window (blocks whose copies come from <= 8 bytes back): its own phases
-WIN_PHASES = ["stage", "parse+scan", "transfer", "fn-scan", "sources", "output"]
-KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light", 3: "window"}
+KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light"}
 
 
 def classify(block):
@@ -69,15 +67,7 @@ def report(name, ms, p, decoder=""):
     print(f"{name:10s} [{decoder}] blocks={len(p):4d} kernel={ms:7.3f} ms  in_bytes(avg)={p[:, 9].mean():7.0f} "
           f"jump_rounds(avg/max)={p[:, 8].mean():5.1f}/{p[:, 8].max():3d} coop_jobs={p[:, 10].mean():6.1f} "
           f"cps={p[:, 11].mean():6.1f} listed={p[:, 7].mean():7.0f}")
-    names = WIN_PHASES if decoder == "window" else PHASES
-    print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(names, d.mean(axis=0))))
-    if decoder == "window":  # per-wave end of the table walk, the barrier after it, from stamp 4
-        we = p[:, 16:24] - p[:, 4:5]  # waves 0-7
-        oe = p[:, 24:32] - p[:, 5:6]
-        print(f"   table walk end per wave (waves 0-7): first={we.min(axis=1).mean():8.0f} last={we.max(axis=1).mean():8.0f}  "
-              f"barrier={np.mean(p[:, 12] - p[:, 4]):8.0f}  rounds(avg)={p[:, 8].mean():4.1f}")
-        print(f"   output end per wave (waves 0-7): first={oe.min(axis=1).mean():8.0f} last={oe.max(axis=1).mean():8.0f} "
-              f"wave0={oe[:, 0].mean():8.0f}")
+    print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(PHASES, d.mean(axis=0))))
     if decoder != "general":
         return
     fw = p[:, 16:32] - p[:, 3:4]  # each wave's own end of the fill, from the start of the fill
