@@ -288,11 +288,11 @@ def cpu_baseline_oracle(query, path, rows, seconds, selected_fraction):
 
 def pmc_traffic(args, kname):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes of this same bench
-    command (profiles/pmc_<config>.json, written by tools/prof_summary.py from separate FETCH_SIZE and
+    command (bench_pmc/pmc_<config>.json, written by tools/prof_summary.py from separate FETCH_SIZE and
     WRITE_SIZE rocprofv3 runs). FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM: gfx950 tallies a
     wide streaming read's 128-B requests at 64 B; the decoders stage their blocks with 16-B loads);
-    the raw value is kept beside it."""
-    f = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"pmc_{args.config}.json")
+    the raw value is kept beside it. (bench_pmc/ travels with the tree to the GPU box; profiles/ does not.)"""
+    f = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench_pmc", f"pmc_{args.config}.json")
     if not os.path.exists(f):
         return {}
     pm = json.load(open(f))
@@ -303,7 +303,7 @@ def pmc_traffic(args, kname):
     fetch = sum(pm["kernels"][k]["fetch_bytes"] for k in ks) / calls
     write = sum(pm["kernels"][k]["write_bytes"] for k in ks) / calls
     return {"traffic": 2 * fetch + write, "traffic_fetch_raw": fetch, "traffic_write": write,
-            "traffic_source": os.path.join("profiles", os.path.basename(f)) + f" ({pm.get('label', '')})"}
+            "traffic_source": os.path.join("bench_pmc", os.path.basename(f)) + f" ({pm.get('label', '')})"}
 
 
 def main():
@@ -441,8 +441,9 @@ def main():
         kernels["aggregate"] = ("k_topn_bin_*" if args.config.startswith("topn") else "k_scan_agg",
                                 scanned_local * per_row, 1, phases["aggregate"])
     if phases["bitmap"] > 0:
+        # serialized bitmap bytes of the matched values + every row bitset written and read once
         kernels["bitmap"] = ("k_concise_or+k_filter_eval" if args.bitmap == "concise" else "k_roaring_or+k_filter_eval",
-                             None, 1, phases["bitmap"])
+                             per_step("bitmap_bytes") or None, 1, phases["bitmap"])
     # the dominant kernel: the longest single-kernel span (phases that group several kernels, like the
     # decode phase or the side-stream payload decode, are reported in phases_ms)
     single = {k: v for k, v in kernels.items() if k in ("lz4_general", "aggregate", "bitmap", "sort", "keygen")}

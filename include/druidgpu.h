@@ -210,6 +210,8 @@ typedef struct {
   int64_t lz4_general_bytes;
   int32_t lz4_general_blocks;
   int32_t lz4_general_launches;
+  /* filter bitmaps: serialized bitmap bytes read + row bitsets written and read (since ABI 11) */
+  int64_t bitmap_bytes;
 } dg_metrics;
 
 /* Aggregate values are returned in 8-byte slots: int64 for count/long*, double for double*,

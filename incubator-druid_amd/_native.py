@@ -74,7 +74,8 @@ class dg_metrics(ctypes.Structure):
                 ("sort_passes", ctypes.c_int32), ("key_bits", ctypes.c_int32), ("groups", ctypes.c_int64),
                 ("decode_side_ms", ctypes.c_double), ("bytes_side", ctypes.c_int64),
                 ("lz4_general_ms", ctypes.c_double), ("lz4_general_bytes", ctypes.c_int64),
-                ("lz4_general_blocks", ctypes.c_int32), ("lz4_general_launches", ctypes.c_int32)]
+                ("lz4_general_blocks", ctypes.c_int32), ("lz4_general_launches", ctypes.c_int32),
+                ("bitmap_bytes", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

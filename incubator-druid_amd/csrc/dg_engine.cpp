@@ -167,6 +167,9 @@ struct CallScratch {
   int32_t* d_err = nullptr;
   int32_t* h_err = nullptr;
   Context* ctx = nullptr;
+  // algorithmic bytes of the call's filter bitmaps (dg_metrics.bitmap_bytes): serialized bitmaps
+  // read + every row bitset written and read once
+  int64_t bitmap_bytes = 0;
   CallScratch() { host.pinned = true; }
   void reset() {
     dev.reset();
@@ -174,6 +177,7 @@ struct CallScratch {
     up.reset();
     d_err = nullptr;
     h_err = nullptr;
+    bitmap_bytes = 0;
   }
 };
 
@@ -885,6 +889,7 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
       if (fp.leaf_col[k] != c) continue;
       for (int32_t id : fp.leaf_ids[k]) {
         if (c->bm_len[id] == 0) continue;
+        cs->bitmap_bytes += c->bm_len[id];
         if (split && c->bm_piece_first[id + 1] > c->bm_piece_first[id]) {  // a long bitmap: its pieces
           for (int32_t q = c->bm_piece_first[id]; q < c->bm_piece_first[id + 1]; ++q) {
             const BmPiece& pc = c->bm_pieces[q];
@@ -982,7 +987,9 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
     if (rc2) return rc2;
     DG_FLUSH(cs, st);
     launch_num_pred(v, voff, seg->nrows, L.p, h_sets[l], st);
+    cs->bitmap_bytes += seg->nrows * (int64_t)std::max(v.width, 1);  // the predicate's column
   }
+  cs->bitmap_bytes += (2 * (int64_t)nleaves + 1) * nwords * 4;  // leaf bitsets written + read, the result
   const int plen = (int)fp.prog.size();
   int32_t* d_prog;
   int32_t* h_prog = up_take<int32_t>(cs, plen + 2, &d_prog, st);  // + the zeroed 8-byte count
@@ -2105,6 +2112,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
   hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
   m.bitmap_ms = f1;
+  m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
   m.lz4_general_ms = gen_ms(db);
   m.lz4_general_bytes = db.gen_bytes;
@@ -2707,6 +2715,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
   hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
   m.bitmap_ms = f1;
+  m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
   m.lz4_general_ms = gen_ms(db);
   m.lz4_general_bytes = db.gen_bytes;
@@ -3354,6 +3363,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   hipEventElapsedTime(&f5, ctx->ev[5], ctx->ev[6]);
   hipEventElapsedTime(&f6, ctx->ev[6], ctx->ev[4]);
   m.bitmap_ms = f1;
+  m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
   m.lz4_general_ms = gen_ms(db) + gen_ms(db_side);
   m.lz4_general_bytes = db.gen_bytes + db_side.gen_bytes;

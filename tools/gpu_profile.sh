@@ -2,7 +2,7 @@
 # rocprofv3 evidence for a bench line: kernel trace + stats, then separate PMC passes for HBM bytes
 # (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950). The segments are written first, outside
 # the profiler. Each GPU step has its own time limit; the summary goes to gpurun_out/prof_<tag>.txt and
-# gpurun_out/pmc_<config>.json (commit as profiles/pmc_<config>.json: bench.py's roofline.traffic).
+# gpurun_out/pmc_<config>.json (commit as bench_pmc/pmc_<config>.json: bench.py's roofline.traffic).
 # usage: CONFIG=groupby TAG=r03_v3 STEPS=10 tools/gpu_profile.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -2,7 +2,7 @@
 launch from the separate FETCH_SIZE / WRITE_SIZE passes. The table shows FETCH_SIZE raw and doubled
 (MI355X_MICROARCH.md: gfx950's correction, valid for wide streaming reads only; random gathers are
 left raw). With a second argument it also writes the per-kernel totals as JSON (bench.py reads
-profiles/pmc_<config>.json for its roofline.traffic).
+bench_pmc/pmc_<config>.json for its roofline.traffic).
 
 usage: prof_summary.py [gpurun_out dir] [out.json] [label]"""
 import collections
