@@ -1720,7 +1720,7 @@ static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bi
   sb->tile_cnt = dev_take<uint32_t>(cs, (size_t)std::max(ntiles_keygen, 1));
   sb->n = dev_take<uint32_t>(cs, 4);
   sb->hist = dev_take<uint32_t>(cs, (size_t)kMaxBins * sb->ntiles_sort);
-  sb->bin_total = dev_take<uint32_t>(cs, kMaxBins);
+  sb->bin_total = dev_take<uint32_t>(cs, (size_t)kMaxBins * 8 + 8);  // per-pass digit totals + tile counters (radix_passes)
   sb->run_cnt = dev_take<uint32_t>(cs, (size_t)sb->ntiles_sort);
   if (!sb->tile_cnt || !sb->n || !sb->hist || !sb->bin_total || !sb->run_cnt) return set_error(DG_ERR_OOM, "sort tables");
   return DG_OK;

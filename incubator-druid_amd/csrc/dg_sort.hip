@@ -356,43 +356,33 @@ void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles
 }
 
 // ------------------------------------------------------------------------------------------------
-// stable LSD radix sort (key words [+ u32 refs]), tiles of kSortTile consecutive elements
+// stable LSD radix sort (key words [+ u32 refs]), tiles of kSortTile consecutive elements, one sweep
+// per pass: a pass is a single kernel whose tiles find their digits' global offsets by decoupled
+// look-back over the earlier tiles' published counts, and which counts the next pass's digits of the
+// keys it stores; only the first pass's digit totals need a read of the keys of their own
+// (k_rs_hist0). No per-pass histogram read, no separate scan.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kST) void k_rs_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
-                                                 int shift, int bits, uint32_t* __restrict__ hist, int ntiles) {
-  __shared__ uint32_t s_h[4 * kMaxBins];  // one histogram per wave (fewer same-address LDS atomics)
-  const uint32_t n = *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  const int nb = 1 << bits;
-  for (int i = threadIdx.x; i < 4 * kMaxBins; i += kST) s_h[i] = 0;
-  __syncthreads();
-  const int wave = threadIdx.x >> 6;
-  if (base < n) {
-#pragma unroll 4
-    for (int c = 0; c < kSPT; ++c) {
-      const int64_t i = base + c * kST + threadIdx.x;
-      if (i < n) atomicAdd(&s_h[wave * kMaxBins + (int)((keys[i] >> shift) & (uint64_t)(nb - 1))], 1u);
-    }
-  }
-  __syncthreads();
-  for (int d = threadIdx.x; d < nb; d += kST)
-    hist[(size_t)d * ntiles + blockIdx.x] = s_h[d] + s_h[kMaxBins + d] + s_h[2 * kMaxBins + d] + s_h[3 * kMaxBins + d];
-}
+constexpr int kRsMaxPasses = 8;                       // 64 key bits at >= 8 bits per digit (totals[] rows)
+constexpr uint32_t kLbAgg = 1u << 30;                 // look-back status: the tile's own count
+constexpr uint32_t kLbPre = 2u << 30;                 // ... the inclusive prefix up to the tile
+constexpr uint32_t kLbVal = (1u << 30) - 1;
 
-// one workgroup per digit: exclusive scan of that digit's tile counts in place + the digit's total
-__global__ __launch_bounds__(1024) void k_rs_binscan(uint32_t* __restrict__ hist, int ntiles, uint32_t* __restrict__ bin_total) {
-  __shared__ uint32_t s_tmp[16];
-  uint32_t* h = hist + (size_t)blockIdx.x * ntiles;
-  uint32_t carry = 0;
-  for (int base = 0; base < ntiles; base += 1024) {
-    const int i = base + threadIdx.x;
-    const uint32_t v = i < ntiles ? h[i] : 0u;
-    uint32_t t;
-    const uint32_t ex = block_scan_u32<1024>(v, &t, s_tmp);
-    if (i < ntiles) h[i] = carry + ex;
-    carry += t;
+// the first pass's digit totals: totals[d] += elements whose digit (bits above shift) is d
+__global__ __launch_bounds__(kST) void k_rs_hist0(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
+                                                  int shift, int bits, uint32_t* __restrict__ totals) {
+  __shared__ uint32_t s_h[4][kMaxBins];  // one histogram per wave (fewer same-address LDS atomics)
+  const int tid = threadIdx.x, wave = tid >> 6;
+  for (int i = tid; i < 4 * kMaxBins; i += kST) (&s_h[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t n = *n_ptr;
+  const uint64_t mask = (1ull << bits) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * kST + tid; i < (int64_t)n; i += (int64_t)gridDim.x * kST)
+    atomicAdd(&s_h[wave][(int)((keys[i] >> shift) & mask)], 1u);
+  __syncthreads();
+  for (int d = tid; d < (1 << bits); d += kST) {
+    const uint32_t c = s_h[0][d] + s_h[1][d] + s_h[2][d] + s_h[3][d];
+    if (c) atomicAdd(&totals[d], c);
   }
-  if (threadIdx.x == 0) bin_total[blockIdx.x] = carry;
 }
 
 // lanes of the wave whose digit equals mine (ballot per digit bit), restricted to valid lanes
@@ -410,30 +400,39 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Wave w of a tile owns its elements [w * 1024, (w + 1) * 1024) in 16 chunks of 64. Each element is
-// ranked among the earlier elements of its wave with the same digit (chunk order, then lane order =
-// element order); the tile is then reordered by digit in LDS, so the global stores of a wave run
-// along each digit's contiguous output range (coalesced) instead of scattering lane by lane.
+// One LSD pass. Tiles take their index from a counter as they start, so a tile only waits for tiles
+// that are running or done. Wave w of a tile owns its elements [w * 1024, (w + 1) * 1024) in 16 chunks
+// of 64. Each element is ranked among the earlier elements of its wave with the same digit (chunk
+// order, then lane order = element order). Thread d publishes the tile's count of digit d, adds the
+// earlier tiles' counts walking back until one has published its inclusive prefix, and publishes its
+// own. The tile is then reordered by digit in LDS, so the global stores of a wave run along each
+// digit's contiguous output range (coalesced) instead of scattering lane by lane.
 template <bool REFS>
 __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     const uint32_t* __restrict__ n_ptr, int shift, int bits,
-                                                    const uint32_t* __restrict__ hist,
-                                                    const uint32_t* __restrict__ bin_total, int ntiles) {
+                                                    const uint32_t* __restrict__ totals, uint32_t* __restrict__ status,
+                                                    uint32_t* __restrict__ tile_ctr, int nshift, int nbits,
+                                                    uint32_t* __restrict__ ntotals) {
   __shared__ uint64_t s_k[kSortTile];
   __shared__ uint32_t s_v[REFS ? kSortTile : 1];
   __shared__ uint32_t s_cnt[4 * kMaxBins];
+  __shared__ uint32_t s_next[kMaxBins];  // the next pass's digit counts of the tile
   __shared__ int64_t s_delta[kMaxBins];  // global position of tile-sorted element i of digit d = s_delta[d] + i
   __shared__ uint32_t s_tmp[4];
+  __shared__ int s_tile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
+  for (int i = tid; i < 4 * kMaxBins; i += kST) s_cnt[i] = 0;
+  for (int i = tid; i < kMaxBins; i += kST) s_next[i] = 0;
+  __syncthreads();
+  const int tile = s_tile;
   const uint32_t n = *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  if (base >= n) return;
+  const int64_t base = (int64_t)tile * kSortTile;
+  if (base >= n) return;  // (every later tile is past the end too: none waits for this one)
   const int tile_n = (int)min<int64_t>(kSortTile, (int64_t)n - base);
   const int nb = 1 << bits;
   const uint64_t dmask = (uint64_t)(nb - 1);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < 4 * kMaxBins; i += kST) s_cnt[i] = 0;
-  __syncthreads();
   uint64_t k[kSPT];
   uint32_t v[kSPT], rank[kSPT];
   const int wbase = wave * (kSortTile / 4);
@@ -458,34 +457,60 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
     if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
   }
   __syncthreads();
-  // per digit: tile offset (scan over digits of the tile's counts), wave offsets inside it, and the
-  // digit's global base (earlier digits' totals + earlier tiles' counts of this digit)
+  // thread d: digit d's count in the tile, its wave offsets, the earlier tiles' counts (look-back) and
+  // the digit's global base (the earlier digits' totals)
   {
-    // thread t: digits 2t and 2t + 1 (up to 512 digits)
-    uint32_t cw[2][4], ct[2], gt[2];
+    static_assert(kMaxBins <= kST, "one digit per thread");
+    const int d = tid;
+    uint32_t cw[4], ct = 0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int d = 2 * tid + q;
+    for (int w = 0; w < 4; ++w) {
+      cw[w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
+      ct += cw[w];
+    }
+    uint32_t excl = 0;
+    if (d < nb) {
+      uint32_t* st = status + (size_t)tile * nb + d;
+      if (tile == 0) {
+        __hip_atomic_store(st, kLbPre | ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_store(st, kLbAgg | ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // eight earlier tiles at a time (independent loads), newest first, up to the first one
+        // with its inclusive prefix; a tile not published yet (it has started: it publishes its
+        // count without waiting) is loaded again
+        constexpr int kLb = 8;
+        for (int j = tile - 1; j >= 0;) {
+          uint32_t sv[kLb];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) cw[q][w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
-      ct[q] = cw[q][0] + cw[q][1] + cw[q][2] + cw[q][3];
-      gt[q] = d < nb ? bin_total[d] : 0u;
+          for (int q = 0; q < kLb; ++q)
+            sv[q] = j - q >= 0 ? __hip_atomic_load(status + (size_t)(j - q) * nb + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : kLbPre;
+          int q = 0;
+          bool prefix = false;
+          for (; q < kLb; ++q) {
+            if ((sv[q] >> 30) == 0) break;
+            excl += sv[q] & kLbVal;
+            if (sv[q] & kLbPre) {
+              prefix = true;
+              break;
+            }
+          }
+          if (prefix) break;
+          j -= q;
+          if (q < kLb) __builtin_amdgcn_s_sleep(1);
+        }
+        __hip_atomic_store(st, kLbPre | (excl + ct), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     uint32_t tot;
-    uint32_t toff = block_scan_u32<kST>(ct[0] + ct[1], &tot, s_tmp);
-    uint32_t gex = block_scan_u32<kST>(gt[0] + gt[1], &tot, s_tmp);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int d = 2 * tid + q;
-      if (d < nb) {
-        s_cnt[d] = toff;
-        s_cnt[kMaxBins + d] = toff + cw[q][0];
-        s_cnt[2 * kMaxBins + d] = toff + cw[q][0] + cw[q][1];
-        s_cnt[3 * kMaxBins + d] = toff + cw[q][0] + cw[q][1] + cw[q][2];
-        s_delta[d] = (int64_t)gex + (int64_t)hist[(size_t)d * ntiles + blockIdx.x] - (int64_t)toff;
-      }
-      toff += ct[q];
-      gex += gt[q];
+    const uint32_t toff = block_scan_u32<kST>(ct, &tot, s_tmp);
+    const uint32_t gex = block_scan_u32<kST>(d < nb ? totals[d] : 0u, &tot, s_tmp);
+    if (d < nb) {
+      s_cnt[d] = toff;
+      s_cnt[kMaxBins + d] = toff + cw[0];
+      s_cnt[2 * kMaxBins + d] = toff + cw[0] + cw[1];
+      s_cnt[3 * kMaxBins + d] = toff + cw[0] + cw[1] + cw[2];
+      s_delta[d] = (int64_t)gex + (int64_t)excl - (int64_t)toff;
     }
   }
   __syncthreads();
@@ -498,11 +523,18 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
     if (REFS) s_v[lp] = v[c];
   }
   __syncthreads();
+  const uint64_t nmask = (1ull << nbits) - 1;
   for (int i = tid; i < tile_n; i += kST) {
     const uint64_t kk = s_k[i];
     const int64_t pos = s_delta[(kk >> shift) & dmask] + i;
     kout[pos] = kk;
     if (REFS) vout[pos] = s_v[i];
+    if (ntotals) atomicAdd(&s_next[(kk >> nshift) & nmask], 1u);
+  }
+  if (ntotals) {  // the next pass's digit totals (complete once this pass's kernel is)
+    __syncthreads();
+    for (int dd = tid; dd < (1 << nbits); dd += kST)
+      if (s_next[dd]) atomicAdd(&ntotals[dd], s_next[dd]);
   }
 }
 
@@ -513,18 +545,27 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
   const int npass = (kb + kMaxDigitBits - 1) / kMaxDigitBits;
   const int w = (kb + npass - 1) / npass;
   const int nt = sb->ntiles_sort;
+  uint32_t* totals = sb->bin_total;                            // [npass][kMaxBins]
+  uint32_t* ctr = sb->bin_total + kRsMaxPasses * kMaxBins;     // [npass] tile counters
+  (void)hipMemsetAsync(sb->bin_total, 0, (kRsMaxPasses * kMaxBins + kRsMaxPasses) * sizeof(uint32_t), s);
+  // the first pass's digit totals from one read of the keys; every pass's scatter counts the next
+  // pass's digits of the keys it stores
+  hipLaunchKernelGGL(k_rs_hist0, dim3(std::min(nt, 4096)), dim3(kST), 0, s, sb->keys[sb->cur], sb->n,
+                     sb->ref_bits + lo, std::min(kb, w), totals);
   for (int p = 0, off = lo; p < npass; ++p, off += w) {
     const int bits = std::min(w, hi - off);
     const int shift = sb->ref_bits + off;
+    const int nbits = p + 1 < npass ? std::min(w, hi - off - w) : 0;
+    uint32_t* nt_tot = p + 1 < npass ? totals + (size_t)(p + 1) * kMaxBins : nullptr;
     const int in = sb->cur, out = sb->cur ^ 1;
-    hipLaunchKernelGGL(k_rs_hist, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->n, shift, bits, sb->hist, nt);
-    hipLaunchKernelGGL(k_rs_binscan, dim3(1 << bits), dim3(1024), 0, s, sb->hist, nt, sb->bin_total);
-    if (sb->refs[in]) {    } else if (sb->refs[in]) {
+    (void)hipMemsetAsync(sb->hist, 0, (size_t)(1 << bits) * nt * sizeof(uint32_t), s);  // look-back status
+    if (sb->refs[in]) {
       hipLaunchKernelGGL(k_rs_scatter<true>, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
-                         sb->refs[out], sb->n, shift, bits, sb->hist, sb->bin_total, nt);
+                         sb->refs[out], sb->n, shift, bits, totals + (size_t)p * kMaxBins, sb->hist, ctr + p,
+                         shift + w, nbits, nt_tot);
     } else {
       hipLaunchKernelGGL(k_rs_scatter<false>, dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out], nullptr,
-                         sb->n, shift, bits, sb->hist, sb->bin_total, nt);
+                         sb->n, shift, bits, totals + (size_t)p * kMaxBins, sb->hist, ctr + p, shift + w, nbits, nt_tot);
     }
     sb->cur = out;
   }
@@ -532,6 +573,7 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
 
 void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
   if (key_bits <= 0) return;
+  static_assert(64 / kMaxDigitBits <= kRsMaxPasses, "passes of a 64-bit key");
   radix_passes(sb, 0, key_bits, s);
 }
 
