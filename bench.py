@@ -296,7 +296,9 @@ def pmc_traffic(args, kname):
     if not os.path.exists(f):
         return {}
     pm = json.load(open(f))
-    ks = [k for k in pm["kernels"] if any(k.startswith(n) or f"::{n}" in k for n in kname.split("+"))]
+    # kernel names as "a+b", each a prefix of the demangled name (after the namespace) or "prefix*"
+    names = [n.rstrip("*") for n in kname.split("+")]
+    ks = [k for k in pm["kernels"] if any(k.startswith(n) or f"::{n}" in k for n in names)]
     if not ks:
         return {}
     calls = sum(pm["kernels"][k]["calls"] for k in ks)
