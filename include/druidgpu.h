@@ -74,7 +74,7 @@ extern "C" {
 #define DG_COL_DOUBLE 3
 #define DG_COL_STRING 4      /* single- or multi-value (V3, legacy compressed or uncompressed multi-value:
                                 filters, topN per value and groupBy explode all run on it) */
-#define DG_COL_UNSUPPORTED 5 /* complex / legacy non-V3 compressed multi-value / unsupported codec */
+#define DG_COL_UNSUPPORTED 5 /* complex column / unsupported codec */
 
 /* aggregator kinds (query/aggregation/...AggregatorFactory.java) */
 #define DG_AGG_COUNT 0
