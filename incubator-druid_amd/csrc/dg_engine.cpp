@@ -1024,7 +1024,7 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
   j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
   j.vstride = 0;
-  j.pad_ = 0;
+  j.dense = b.cp_dense.empty() ? 0 : b.cp_dense[k];
   return j;
 }
 
@@ -1206,12 +1206,19 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   // per-thread sequence registers)
   // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
   // blocks per CU)
+  // dense blocks (token-dense, short runs: k_lz4_dense, two blocks per CU) go first
+  // (DG_LZ4_NO_DENSE=1: every dense block to the general decoder, for same-box A/B and tests)
+  const char* no_dense = getenv("DG_LZ4_NO_DENSE");
+  if (no_dense && *no_dense && *no_dense != '0')
+    for (Lz4Job& j : db->jobs) j.dense = 0;
   const int nh = (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.light; }) -
                        db->jobs.begin());
-  const int nn = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
+  const int nd = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return j.dense != 0; }) -
+                       db->jobs.begin());
+  const int nn = (int)(std::stable_partition(db->jobs.begin() + nd, db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
                        db->jobs.begin());
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
-  if (nn <= 16 * 256) std::stable_sort(db->jobs.begin(), db->jobs.begin() + nn, by_ncp);
+  if (nn - nd <= 16 * 256) std::stable_sort(db->jobs.begin() + nd, db->jobs.begin() + nn, by_ncp);
   if (nh - nn <= 16 * 256) std::stable_sort(db->jobs.begin() + nn, db->jobs.begin() + nh, by_ncp);
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
@@ -1220,11 +1227,13 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
   launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
+  // the token-dense decoders (dense + general) are timed together: "general" in the metrics
   for (int i = 0; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
   db->gen_blocks += nh;
-  db->gen_launches += (nn > 0) + (nh - nn > 0);
+  db->gen_launches += (nd > 0) + (nn - nd > 0) + (nh - nn > 0);
   if (db->gen_a && nh) hipEventRecord(db->gen_a, st);
-  launch_lz4_decode(d, nn, 0, d_err, st, d_prof);
+  launch_lz4_dense(d, nd, d_err, st, d_prof);
+  launch_lz4_decode(d + nd, nn - nd, 0, d_err, st, d_prof ? d_prof + (size_t)nd * kLz4ProfWords : nullptr);
   launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
   if (db->gen_a && nh) hipEventRecord(db->gen_b, st);
   return run_expands(cs, db, st);  // errors surface at finish_call
@@ -1719,10 +1728,11 @@ static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bi
   }
   sb->tile_cnt = dev_take<uint32_t>(cs, (size_t)std::max(ntiles_keygen, 1));
   sb->n = dev_take<uint32_t>(cs, 4);
-  sb->hist = dev_take<uint32_t>(cs, (size_t)kMaxBins * sb->ntiles_sort);
-  sb->bin_total = dev_take<uint32_t>(cs, (size_t)kMaxBins * 8 + 8);  // per-pass digit totals + tile counters (radix_passes)
+  sb->lb_status = dev_take<uint64_t>(cs, (size_t)kMaxBins * sb->ntiles_sort);
+  // per-pass digit totals + tile counters (radix_passes)
+  sb->bin_total = dev_take<uint32_t>(cs, (size_t)kMaxBins * kRsMaxPasses + kRsMaxPasses);
   sb->run_cnt = dev_take<uint32_t>(cs, (size_t)sb->ntiles_sort);
-  if (!sb->tile_cnt || !sb->n || !sb->hist || !sb->bin_total || !sb->run_cnt) return set_error(DG_ERR_OOM, "sort tables");
+  if (!sb->tile_cnt || !sb->n || !sb->lb_status || !sb->bin_total || !sb->run_cnt) return set_error(DG_ERR_OOM, "sort tables");
   return DG_OK;
 }
 
@@ -4100,9 +4110,10 @@ int dg_timeseries_merge(const dg_scan* scan, int32_t n_lists, const int32_t* n, 
 extern "C" int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind) {
   if (!block || len <= 0 || len > kBlockBytes + 2048 || !kind) return set_error(DG_ERR_ARG, "bad arguments");
   std::vector<uint32_t> one;
-  int wide = 0, light = 0, nfine = 0;
-  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine);
-  *kind = d < 0 ? -1 : light ? 2 : wide ? 1 : 0;
+  int wide = 0, light = 0, nfine = 0, dense = 0;
+  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine, &dense);
+  // -1 malformed, 0 general, 1 general (wide), 2 light, 3 dense (rounds), 4 dense (class scan)
+  *kind = d < 0 ? -1 : light ? 2 : dense ? 2 + dense : wide ? 1 : 0;
   return DG_OK;
 }
 
@@ -4119,6 +4130,7 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.cp_n.resize(n);
   b.cp_wide.assign(n, 0);
   b.cp_light.assign(n, 0);
+  b.cp_dense.assign(n, 0);
   b.cp_fine.assign(n, 0);
   b.dec_len.resize(n);
   int64_t total = 0;
@@ -4133,10 +4145,11 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
     std::vector<uint32_t> one;
-    int wide = 0, light = 0, nfine = 0;
-    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine);
+    int wide = 0, light = 0, nfine = 0, dense = 0;
+    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine, &dense);
     b.cp_wide[i] = (uint8_t)wide;
     b.cp_light[i] = (uint8_t)light;
+    b.cp_dense[i] = (uint8_t)(light ? 0 : dense);
     b.cp_fine[i] = nfine;
     b.cp_off[i] = (int64_t)cps.size();
     b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size() - nfine;

@@ -65,7 +65,8 @@ struct Lz4Job {
   // and value v goes to dst + v * vstride (a column of the groupBy payload records, written in place);
   // bytes past expect_len are then not written (they would land in the next segment's records)
   int32_t vstride;
-  int32_t pad_;
+  int32_t dense;       // token-dense block for k_lz4_dense (attach-time classification): 0 no, 1 match
+                       // rounds only, 2 distance-8 class scan + rounds (kDnMode*)
 };
 
 // Light blocks (literal-heavy: random ids, high-entropy values): at most kLtMaxCps checkpoint
@@ -74,6 +75,18 @@ struct Lz4Job {
 constexpr int kLtMaxCps = 256;
 constexpr int kLtThreads = 512;  // light-decoder threads (at most one light checkpoint interval each)
 constexpr int kLtMaxDepth = 16;
+
+// Dense blocks (token-dense value columns: sequential longs, timestamps, noisy doubles): at most
+// kLzMaxCps checkpoint intervals (two per thread), matches of at most kDnMaxRun bytes, at most kDnMaxLongLit literal runs longer than kDnShortLit,
+// and every match resolvable within kDnMaxRounds rounds (lz4_dense_mode simulates the kernel's
+// resolution order at attach). k_lz4_dense decodes them into a byte image + a resolved-bit map in LDS
+// (72 KiB: two blocks per CU).
+constexpr int kDnThreads = 512;
+constexpr int kDnMaxRun = 255;        // longest match
+constexpr int kDnShortLit = 32;       // longer literal runs are copied by the whole workgroup ...
+constexpr int kDnMaxLongLit = 256;    // ... at most this many per block
+constexpr int kDnMaxRounds = 64;
+enum : int32_t { kDnModeNone = 0, kDnModeRounds = 1, kDnModeClass = 2 };
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
 struct LzfJob {
@@ -104,7 +117,11 @@ struct VsJob {
 // *light = g > 0 when light: the block's checkpoints are followed by *nfine light checkpoints, one
 // every g sequences (g the fewest sequences per checkpoint that fit the light decoder's threads).
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr,
-                    int* nfine = nullptr);
+                    int* nfine = nullptr, int* dense = nullptr);
+// The k_lz4_dense mode of a validated, non-wide block (kDnMode*): rounds or class mode when every
+// run fits kDnMaxRun and the kernel's resolution (distance-8 class scan in class mode, then rounds of
+// matches whose source bytes are resolved) finishes within kDnMaxRounds rounds; else kDnModeNone.
+int lz4_dense_mode(const uint8_t* in, int n);
 
 struct AggPlan {
   int32_t n;
@@ -186,8 +203,9 @@ struct SortBufs {
   int cur;                // which of the ping-pong buffers holds the result
   uint32_t* tile_cnt;     // keygen tiles: selected rows, then their offsets
   uint32_t* n;            // [0] selected rows, [1] groups
-  uint32_t* hist;         // radix histograms [bins][tiles]
-  uint32_t* bin_total;    // [256]
+  uint64_t* lb_status;    // radix look-back status per (tile, digit) of one pass: flag in the top two bits,
+                          // the tile's digit count or inclusive prefix below (prefixes reach n: 64-bit)
+  uint32_t* bin_total;    // [kRsMaxPasses][kMaxBins] digit totals + [kRsMaxPasses] tile counters
   uint32_t* run_cnt;      // per sort tile: run heads, then their offsets
   int64_t cap;            // element capacity (rows of the call)
   int ntiles_sort;        // sort tiles of `cap`
@@ -230,6 +248,7 @@ struct BlockColumn {
   std::vector<int32_t> cp_n;           // LZ4: checkpoints of block b (-1: malformed block)
   std::vector<uint8_t> cp_wide;        // LZ4: block b keeps a checkpoint every 2 * kLzSeqPerCp sequences
   std::vector<uint8_t> cp_light;       // LZ4: block b goes to the light decoder (sequences per light checkpoint)
+  std::vector<uint8_t> cp_dense;       // LZ4: block b goes to the dense decoder (kDnMode*)
   std::vector<int32_t> cp_fine;        // LZ4: light checkpoints of block b (after its cp_n checkpoints)
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
   int64_t index_bytes = 0;             // LZ4: bytes of the checkpoint index (read per query)
@@ -364,6 +383,7 @@ constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (dia
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+void launch_lz4_dense(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // one multi-value dimension's decoded row lists, validated before use (bit 2 of the error word)
@@ -469,6 +489,7 @@ constexpr int kTileRows = 2048;
 // dg_sort.hip
 constexpr int kMaxDigitBits = 8;  // radix digits of up to 8 bits (9-bit digits measured slower: 64-byte store runs)
 constexpr int kMaxBins = 1 << kMaxDigitBits;
+constexpr int kRsMaxPasses = 8;  // 64 key bits at >= 8 bits per digit (rows of SortBufs::bin_total)
 constexpr int kSortTile = 4096;  // elements per radix / run tile (256 threads x 16)
 // groupBy reduce: waves per sort tile (each reduces its own 4096 / kRedWaves elements; one carry /
 // open slot per wave)

@@ -1157,6 +1157,381 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Dense decoder: token-dense blocks whose runs are short (attach-time classification,
+// lz4_dense_mode): sequential longs and timestamps (~8 K sequences of one literal byte and a 7-byte
+// copy at distance 8, copy chains through the whole block) and noisy doubles (~7.5 K sequences of ~5
+// literal bytes and a ~4-byte copy at a random distance, chains of <= ~24 hops). Instead of the
+// general decoder's 16-bit entry per output byte (128 KiB of LDS, one block per CU), the block is
+// resolved in place in a byte image of the output + one resolved bit per byte (72 KiB: two blocks per
+// CU), and every thread keeps its own sequences in registers:
+//   1. stage the compressed block in LDS; thread t parses checkpoint intervals 2t, 2t + 1 (<= 16
+//      sequences) into registers; a block scan of the output lengths places them;
+//   2. literal bytes go to the image (read from the compressed block in L2: the staged input is now
+//      dead, the image overlays it) and their resolved bits are set;
+//   3. class mode: a byte copied from 8 back has the value of the last byte of its residue class mod 8
+//      that is not such a copy (its terminal). A block-wide max-scan over the threads' last terminal
+//      per class gives every thread the terminals before its range; it then walks its range with an
+//      8-byte window of class values and writes every distance-8 byte whose terminal is resolved;
+//   4. rounds: every other match whose source bytes (its first period) are all resolved copies them
+//      and sets its bits; class mode re-walks the ranges still holding unresolved distance-8 bytes
+//      after a round that resolved terminals. The attach-time simulation bounds the rounds;
+//   5. the image goes out in 16-byte chunks (out16: slots, or 8-byte values to the payload records).
+// ------------------------------------------------------------------------------------------------
+constexpr int kDnWaves = kDnThreads / 64;
+constexpr int kDnSeq = 2 * kLzSeqPerCp;                 // sequences per thread (two checkpoint intervals)
+constexpr int kDnResWords = kBlockBytes / 32;           // resolved bits
+constexpr int kDnBufWords = kBlockBytes / 4 + kDnResWords;  // image + resolved bits; first the staged input
+static_assert(kDnBufWords * 4 >= kLz4InCap + 16, "the staged input fits the image + bit map");
+static_assert(kDnThreads * 2 >= kLzMaxCps, "two checkpoint intervals per dense-decoder thread");
+
+// OR of the bits of positions [a, b) into the resolved map, one LDS atomic per word touched
+__device__ __forceinline__ void res_set(uint32_t* s_res, int a, int b) {
+  while (a < b) {
+    const int w = a >> 5, lo = a & 31, hi = min(b - (w << 5), 32);
+    const uint32_t m = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+    atomicOr(&s_res[w], m);
+    a = (w + 1) << 5;
+  }
+}
+
+// all bits of positions [a, b) set
+__device__ __forceinline__ bool res_all(const uint32_t* s_res, int a, int b) {
+  bool ok = true;
+  while (a < b && ok) {
+    const int w = a >> 5, lo = a & 31, hi = min(b - (w << 5), 32);
+    const uint32_t m = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+    ok = (s_res[w] & m) == m;
+    a = (w + 1) << 5;
+  }
+  return ok;
+}
+
+template <bool PROF>
+__global__ __launch_bounds__(kDnThreads, 4) void k_lz4_dense(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+                                                             uint64_t* __restrict__ prof) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_buf[kDnBufWords];
+  __shared__ int s_tmp[kDnWaves];
+  __shared__ uint32_t s_cls[kDnWaves * kClass];
+  __shared__ uint32_t s_lj[3 * kDnMaxLongLit];  // long literal runs: output start, input offset, length
+  __shared__ int s_bad, s_nlj;
+  const Lz4Job job = jobs[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = job.src_len, ncp = job.ncp;
+  const bool cls = job.dense == kDnModeClass;
+  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.wide || job.dec_len > kBlockBytes ||
+      job.dec_len < job.expect_len) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  LZ_STAMP(0);
+  // ---- stage the compressed block (16-byte aligned and padded in the device image) ----
+  {
+    uint4* dst = reinterpret_cast<uint4*>(s_buf);
+    const int n16 = (n + 15) >> 4;
+    for (int i = tid; i < n16; i += kDnThreads) dst[i] = gld16(job.src + 16 * (size_t)i);
+    if (tid == 0) {
+      dst[n16] = make_uint4(0, 0, 0, 0);
+      s_bad = 0;
+      s_nlj = 0;
+    }
+  }
+  __syncthreads();
+  LZ_STAMP(1);
+  // ---- 1. parse my two intervals into registers. Sequence s: r_a = distance | literal length << 16,
+  // r_b = match start | match length << 17 (output positions, relative until the scan), r_lit =
+  // literal input offset ----
+  const uint8_t* s_in = reinterpret_cast<const uint8_t*>(s_buf);
+  uint32_t r_a[kDnSeq], r_b[kDnSeq], r_lit[kDnSeq];
+  int out_rel = 0;
+  bool bad = false;
+#pragma unroll
+  for (int s = 0; s < kDnSeq; ++s) r_a[s] = r_b[s] = r_lit[s] = 0;
+  if (2 * tid < ncp) {
+    int pos = (int)gld4(job.cp + 2 * tid);
+    const int end = 2 * tid + 2 < ncp ? (int)gld4(job.cp + 2 * tid + 2) : n;
+#pragma unroll
+    for (int s = 0; s < kDnSeq; ++s) {
+      if (pos < end) {
+        Tok t;
+        if (parse_tok(s_in, n, pos, t) && t.M <= kDnMaxRun && t.L < 65536) {
+          r_a[s] = (uint32_t)t.off | ((uint32_t)t.L << 16);
+          r_b[s] = (uint32_t)(out_rel + t.L) | ((uint32_t)t.M << 17);
+          r_lit[s] = (uint32_t)t.lit;
+          out_rel += t.L + t.M;
+          pos = t.next;
+        } else {
+          pos = -1;
+        }
+      }
+    }
+    bad = pos != end;
+  }
+  int x = out_rel;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[wave] = x;
+  if (bad) s_bad = 1;
+  __syncthreads();  // also the end of every read of the staged input
+  int base = x - out_rel, total = 0;
+#pragma unroll
+  for (int w = 0; w < kDnWaves; ++w) {
+    const int y = s_tmp[w];
+    base += w < wave ? y : 0;
+    total += y;
+  }
+  LZ_STAMP(2);
+  if (s_bad || total != job.dec_len) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+#pragma unroll
+  for (int s = 0; s < kDnSeq; ++s)
+    r_b[s] += (uint32_t)base;  // (an absent sequence: an empty one at my range's start)
+  uint8_t* s_img = reinterpret_cast<uint8_t*>(s_buf);
+  uint32_t* s_res = s_buf + kBlockBytes / 4;
+  for (int i = tid; i < kDnResWords; i += kDnThreads) s_res[i] = 0;
+  __syncthreads();
+  // ---- 2. literal bytes (from the compressed block in L2: the staged input is dead, the image
+  // overlays it) -> image + resolved bits; long runs go to a list copied by the whole block. The
+  // matches still to resolve: `unres` (rounds) and, in class mode, the distance-8 ones `pend8` ----
+  uint32_t unres = 0, pend8 = 0;
+  {
+    int o = base;
+#pragma unroll
+    for (int s = 0; s < kDnSeq; ++s) {
+      const int L = (int)(r_a[s] >> 16), d = (int)(r_a[s] & 0xFFFF), M = (int)(r_b[s] >> 17);
+      if (L > kDnShortLit) {
+        const int j = atomicAdd(&s_nlj, 1);
+        if (j < kDnMaxLongLit) {
+          s_lj[3 * j] = (uint32_t)o;
+          s_lj[3 * j + 1] = r_lit[s];
+          s_lj[3 * j + 2] = (uint32_t)L;
+        } else {
+          s_bad = 1;  // (more than the attach-time classification allows)
+        }
+      } else if (L > 0) {
+        const int lit = (int)r_lit[s], a0 = lit & ~3, nd = ((lit & 3) + L + 3) >> 2;
+#pragma unroll 1
+        for (int q = 0; q < nd; ++q) {
+          const uint32_t w = gld4(job.src + a0 + 4 * q);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int k = a0 + 4 * q + b - lit;
+            if (k >= 0 && k < L) s_img[o + k] = (uint8_t)(w >> (8 * b));
+          }
+        }
+        res_set(s_res, o, o + L);
+      }
+      if (M > 0) {
+        if (d > o + L) s_bad = 1;  // a copy from before the block
+        if (cls && d == kClass) pend8 |= 1u << s;
+        else unres |= 1u << s;
+      }
+      o += L + M;
+    }
+  }
+  __syncthreads();
+  if (s_bad) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  if (s_nlj > 0) {  // the long literal runs, every thread a byte of each (then their bits, by word)
+    const int nlj = s_nlj;
+    for (int j = 0; j < nlj; ++j) {
+      const int o = (int)s_lj[3 * j], lit = (int)s_lj[3 * j + 1], L = (int)s_lj[3 * j + 2];
+      for (int i = tid; i < L; i += kDnThreads) s_img[o + i] = (uint8_t)gld1(job.src + lit + i);
+      for (int w = (o >> 5) + tid; w <= ((o + L - 1) >> 5); w += kDnThreads) res_set(s_res, max(o, w << 5), min(o + L, (w + 1) << 5));
+    }
+    __syncthreads();
+  }
+  LZ_STAMP(3);
+  // ---- 3. class mode: terminals per residue class mod 8 ----
+  uint32_t carry[kClass];  // position + 1 of the last terminal before my range, per class (0: none)
+#pragma unroll
+  for (int c = 0; c < kClass; ++c) carry[c] = 0;
+  // walk of my range: writes every pending distance-8 byte whose terminal is resolved (a run of
+  // k >= 8 bytes sets its classes from its last 8 bytes)
+  auto class_walk = [&]() {
+#pragma unroll
+    for (int s = 0; s < kDnSeq; ++s) {
+      asm volatile("" : "+v"(r_a[s]));
+      asm volatile("" : "+v"(r_b[s]));
+    }
+    uint64_t win = 0;  // byte c: value of class c's current terminal
+    uint32_t valid = 0;
+#pragma unroll
+    for (int c = 0; c < kClass; ++c) {
+      const int y = (int)carry[c] - 1;
+      if (y >= 0 && ((s_res[y >> 5] >> (y & 31)) & 1u)) {
+        win |= (uint64_t)s_img[y] << (8 * c);
+        valid |= 1u << c;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < kDnSeq; ++s) {
+      const int L = (int)(r_a[s] >> 16), d = (int)(r_a[s] & 0xFFFF);
+      const int xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
+      // literals: resolved terminals (the last 8 bytes of the run decide the window)
+      if (L > 0) {
+        const int o = xm - L;
+#pragma unroll 1
+        for (int k = max(0, L - 8); k < L; ++k) {
+          const int y = o + k, c = y & 7;
+          win = (win & ~(0xFFull << (8 * c))) | ((uint64_t)s_img[y] << (8 * c));
+          valid |= 1u << c;
+        }
+      }
+      if (M > 0) {
+        if (d == kClass) {
+          if ((pend8 >> s) & 1u) {
+            bool all = true;
+#pragma unroll 1
+            for (int k = 0; k < M; ++k) {
+              const int y = xm + k, c = y & 7;
+              if ((valid >> c) & 1u) s_img[y] = (uint8_t)(win >> (8 * c));
+              else all = false;
+            }
+            if (all) {
+              res_set(s_res, xm, xm + M);
+              pend8 &= ~(1u << s);
+            }
+          }
+        } else {  // another distance: a terminal, resolved or not
+          const bool res = !((unres >> s) & 1u);
+#pragma unroll 1
+          for (int k = max(0, M - 8); k < M; ++k) {
+            const int y = xm + k, c = y & 7;
+            if (res) {
+              win = (win & ~(0xFFull << (8 * c))) | ((uint64_t)s_img[y] << (8 * c));
+              valid |= 1u << c;
+            } else {
+              valid &= ~(1u << c);
+            }
+          }
+        }
+      }
+    }
+  };
+  if (cls) {
+    // my last terminal per class (position + 1), from my sequences' literal runs and non-class matches
+    uint32_t last[kClass];
+#pragma unroll
+    for (int c = 0; c < kClass; ++c) last[c] = 0;
+#pragma unroll
+    for (int s = 0; s < kDnSeq; ++s) {
+      const int L = (int)(r_a[s] >> 16), d = (int)(r_a[s] & 0xFFFF);
+      const int xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
+      const int o = xm - L, e = xm + (d == kClass ? 0 : M);  // terminals: [o, e)
+      if (e > o) {
+#pragma unroll
+        for (int c = 0; c < kClass; ++c) {
+          const int p = (e - 1) - (((e - 1) - c) & 7);  // last position of class c in [.., e)
+          if (p >= o) last[c] = (uint32_t)(p + 1);
+        }
+      }
+    }
+    // exclusive max-scan over the threads (positions grow with the thread index)
+#pragma unroll
+    for (int c = 0; c < kClass; ++c) {
+      uint32_t v = last[c];
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(v, off, 64);
+        if (lane >= off) v = max(v, y);
+      }
+      const uint32_t ex = __shfl_up(v, 1, 64);
+      carry[c] = lane ? ex : 0u;
+      if (lane == 63) s_cls[wave * kClass + c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < kClass; ++c)
+      for (int w = 0; w < wave; ++w) carry[c] = max(carry[c], s_cls[w * kClass + c]);
+    if (pend8) class_walk();
+  }
+  LZ_STAMP(4);
+  // ---- 4. rounds ----
+  int rounds = 0;
+  for (;; ++rounds) {
+    if (!__syncthreads_or((unres | pend8) != 0)) break;
+    if (rounds > kDnMaxRounds + 1) {  // beyond the attach-time bound: not a block of this kind
+      if (tid == 0) atomicOr(err, 1);
+      return;
+    }
+    // the sequence registers are re-read every round (no loop-invariant copies of their fields: the
+    // kernel must stay within 128 VGPRs for two blocks per CU)
+#pragma unroll
+    for (int s = 0; s < kDnSeq; ++s) {
+      asm volatile("" : "+v"(r_a[s]));
+      asm volatile("" : "+v"(r_b[s]));
+    }
+    bool progress = false;
+    if (unres) {
+#pragma unroll
+      for (int s = 0; s < kDnSeq; ++s) {
+        if ((unres >> s) & 1u) {
+          const int d = (int)(r_a[s] & 0xFFFF), xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
+          const int a = xm - d, len = min(M, d);
+          if (res_all(s_res, a, a + len)) {
+            // (a bit seen set by another wave this round: its bytes were written before it)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll 1
+            for (int k = 0, r = 0; k < M; ++k) {  // LZ4 overlap: byte k copies the first period
+              s_img[xm + k] = s_img[a + r];
+              if (++r == d) r = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            res_set(s_res, xm, xm + M);
+            unres &= ~(1u << s);
+            progress = true;
+          }
+        }
+      }
+    }
+    if (cls) {
+      // terminals resolved this round reach their distance-8 followers (in any thread's range)
+      if (__syncthreads_or(progress) && pend8) class_walk();
+    }
+  }
+  LZ_STAMP(5);
+  if (PROF && tid == 0) {
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 8] = (uint64_t)rounds;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 9] = (uint64_t)n;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 10] = (uint64_t)s_nlj;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
+  }
+  // ---- 5. output: 16-byte chunks of the image ----
+  const int nchunks = (total + 15) >> 4;
+  const uint4* img16 = reinterpret_cast<const uint4*>(s_buf);
+  for (int c = tid; c < nchunks; c += kDnThreads) {
+    const uint4 v = img16[c];
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const int rem = total - 16 * c;
+    if (rem < 16) {  // bytes past the block's end are zero
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int keep = min(max(rem - 4 * q, 0), 4);
+        w[q] &= keep == 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+      }
+    }
+    out16(job, c, w);
+  }
+  if (PROF) {
+    __syncthreads();
+    LZ_STAMP(6);
+  }
+}
+
+void launch_lz4_dense(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
+  if (njobs <= 0) return;
+  if (d_prof) hipLaunchKernelGGL(k_lz4_dense<true>, dim3(njobs), dim3(kDnThreads), 0, s, d_jobs, d_err, d_prof);
+  else hipLaunchKernelGGL(k_lz4_dense<false>, dim3(njobs), dim3(kDnThreads), 0, s, d_jobs, d_err, nullptr);
+}
+
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
   if (d_prof) hipLaunchKernelGGL(k_lz4_light<true>, dim3(njobs), dim3(kLtThreads), 0, s, d_jobs, d_err, d_prof);

@@ -178,10 +178,88 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
   }
 }
 
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine) {
+// Simulation of k_lz4_dense's resolution order (dg_lz4.hip) on a validated block: literal bytes are
+// resolved at round 0; in class mode (distance-8 copies are more than a quarter of the output, as the
+// kernel's class scan assumes) a distance-8 byte resolves with its class terminal (the last earlier
+// byte of its residue class mod 8 that is not a distance-8 copy); every other match resolves one
+// round after the last of its source bytes (its first period). The kernel resolves at least this
+// fast (its rounds also see same-round results), so the block is dense when every run fits
+// kDnMaxRun and the last match resolves by round kDnMaxRounds.
+int lz4_dense_mode(const uint8_t* in, int n) {
+  thread_local std::vector<uint8_t> rd(kBlockBytes);
+  struct Seq {
+    int L, M, d;
+  };
+  thread_local std::vector<Seq> seqs;
+  seqs.clear();
+  int pos = 0, out = 0, c8 = 0, nlong = 0;
+  auto ext = [&](int* len) {
+    for (int b = 255; b == 255 && pos < n;) {
+      b = in[pos++];
+      *len += b;
+    }
+  };
+  for (;;) {
+    if (pos >= n) return kDnModeNone;
+    const int tok = in[pos++];
+    int L = tok >> 4;
+    if (L == 15) ext(&L);
+    pos += L;
+    if (L > 65535 || pos > n) return kDnModeNone;
+    if (L > kDnShortLit && ++nlong > kDnMaxLongLit) return kDnModeNone;
+    if (pos == n) {
+      seqs.push_back({L, 0, 0});
+      out += L;
+      break;
+    }
+    if (n - pos < 2) return kDnModeNone;
+    const int d = in[pos] | (in[pos + 1] << 8);
+    pos += 2;
+    int M = tok & 15;
+    if (M == 15) ext(&M);
+    M += 4;
+    if (M > kDnMaxRun || d == 0 || d > out + L || out + L + M > kBlockBytes) return kDnModeNone;
+    seqs.push_back({L, M, d});
+    if (d == 8) c8 += M;
+    out += L + M;
+  }
+  if (seqs.size() > (size_t)kLzMaxCps * kLzSeqPerCp) return kDnModeNone;
+  const bool cls = (int64_t)c8 * 4 > out;
+  int last[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  int x = 0, mx = 0;
+  for (const Seq& q : seqs) {
+    for (int k = 0; k < q.L; ++k, ++x) {
+      rd[x] = 0;
+      last[x & 7] = x;
+    }
+    if (!q.M) continue;
+    if (cls && q.d == 8) {
+      for (int k = 0; k < q.M; ++k, ++x) {
+        const int t = last[x & 7];
+        if (t < 0) return kDnModeNone;
+        rd[x] = rd[t];
+      }
+      continue;
+    }
+    int r = 0;
+    const int a = x - q.d;
+    for (int k = 0; k < std::min(q.M, q.d); ++k) r = std::max<int>(r, rd[a + k]);
+    r += 1;
+    if (r > kDnMaxRounds) return kDnModeNone;
+    mx = std::max(mx, r);
+    for (int k = 0; k < q.M; ++k, ++x) {
+      rd[x] = (uint8_t)r;
+      last[x & 7] = x;
+    }
+  }
+  return cls ? kDnModeClass : kDnModeRounds;
+}
+
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine, int* dense) {
   const size_t first = cps->size();
   if (light) *light = 0;
   if (nfine) *nfine = 0;
+  if (dense) *dense = 0;
   int pos = 0, out = 0;
   int64_t seq = 0;
   auto ext = [&](int* len) {
@@ -202,6 +280,7 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
       cps->resize(first + m);
     }
     if (m > (size_t)kLzMaxCps) return -1;
+    if (dense && !*wide) *dense = lz4_dense_mode(in, n);
     if (light && !*wide && m <= (size_t)kLtMaxCps && lz4_max_depth(in, n, kLtMaxDepth) <= kLtMaxDepth) {
       // light checkpoints: every g sequences, the fewest that fit one per light-decoder thread
       const int g = (int)std::max<int64_t>(1, (seq + kLtThreads - 1) / kLtThreads);
@@ -283,6 +362,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->cp_n.assign(blocks.n, -1);
     col->cp_wide.assign(blocks.n, 0);
     col->cp_light.assign(blocks.n, 0);
+    col->cp_dense.assign(blocks.n, 0);
     col->cp_fine.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
@@ -292,10 +372,12 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int t = 0; t < nt; ++t)
       th.emplace_back([&, t] {
         for (int32_t b = t; b < blocks.n; b += nt) {
-          int wide = 0, light = 0, nfine = 0;
-          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine);
+          int wide = 0, light = 0, nfine = 0, dense = 0;
+          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine,
+                                        &dense);
           col->cp_wide[b] = (uint8_t)wide;
           col->cp_light[b] = (uint8_t)light;
+          col->cp_dense[b] = (uint8_t)(light ? 0 : dense);
           col->cp_fine[b] = nfine;
           col->dec_len[b] = d;
           col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size() - nfine;

@@ -362,10 +362,11 @@ void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles
 // keys it stores; only the first pass's digit totals need a read of the keys of their own
 // (k_rs_hist0). No per-pass histogram read, no separate scan.
 // ------------------------------------------------------------------------------------------------
-constexpr int kRsMaxPasses = 8;                       // 64 key bits at >= 8 bits per digit (totals[] rows)
-constexpr uint32_t kLbAgg = 1u << 30;                 // look-back status: the tile's own count
-constexpr uint32_t kLbPre = 2u << 30;                 // ... the inclusive prefix up to the tile
-constexpr uint32_t kLbVal = (1u << 30) - 1;
+// look-back status words are 64-bit: an inclusive prefix counts every earlier element of the digit,
+// up to n (< 2^32), so it cannot share a 32-bit word with the flag
+constexpr uint64_t kLbAgg = 1ull << 62;                // look-back status: the tile's own count
+constexpr uint64_t kLbPre = 2ull << 62;                // ... the inclusive prefix up to the tile
+constexpr uint64_t kLbVal = (1ull << 62) - 1;
 
 // the first pass's digit totals: totals[d] += elements whose digit (bits above shift) is d
 __global__ __launch_bounds__(kST) void k_rs_hist0(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
@@ -411,7 +412,7 @@ template <bool REFS>
 __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     const uint32_t* __restrict__ n_ptr, int shift, int bits,
-                                                    const uint32_t* __restrict__ totals, uint32_t* __restrict__ status,
+                                                    const uint32_t* __restrict__ totals, uint64_t* __restrict__ status,
                                                     uint32_t* __restrict__ tile_ctr, int nshift, int nbits,
                                                     uint32_t* __restrict__ ntotals) {
   __shared__ uint64_t s_k[kSortTile];
@@ -468,9 +469,9 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
       cw[w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
       ct += cw[w];
     }
-    uint32_t excl = 0;
+    uint64_t excl = 0;
     if (d < nb) {
-      uint32_t* st = status + (size_t)tile * nb + d;
+      uint64_t* st = status + (size_t)tile * nb + d;
       if (tile == 0) {
         __hip_atomic_store(st, kLbPre | ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
@@ -480,7 +481,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
         // count without waiting) is loaded again
         constexpr int kLb = 8;
         for (int j = tile - 1; j >= 0;) {
-          uint32_t sv[kLb];
+          uint64_t sv[kLb];
 #pragma unroll
           for (int q = 0; q < kLb; ++q)
             sv[q] = j - q >= 0 ? __hip_atomic_load(status + (size_t)(j - q) * nb + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -488,7 +489,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
           int q = 0;
           bool prefix = false;
           for (; q < kLb; ++q) {
-            if ((sv[q] >> 30) == 0) break;
+            if ((sv[q] >> 62) == 0) break;
             excl += sv[q] & kLbVal;
             if (sv[q] & kLbPre) {
               prefix = true;
@@ -547,7 +548,7 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
   const int nt = sb->ntiles_sort;
   uint32_t* totals = sb->bin_total;                            // [npass][kMaxBins]
   uint32_t* ctr = sb->bin_total + kRsMaxPasses * kMaxBins;     // [npass] tile counters
-  (void)hipMemsetAsync(sb->bin_total, 0, (kRsMaxPasses * kMaxBins + kRsMaxPasses) * sizeof(uint32_t), s);
+  (void)hipMemsetAsync(sb->bin_total, 0, ((size_t)kRsMaxPasses * kMaxBins + kRsMaxPasses) * sizeof(uint32_t), s);
   // the first pass's digit totals from one read of the keys; every pass's scatter counts the next
   // pass's digits of the keys it stores
   hipLaunchKernelGGL(k_rs_hist0, dim3(std::min(nt, 4096)), dim3(kST), 0, s, sb->keys[sb->cur], sb->n,
@@ -558,14 +559,14 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
     const int nbits = p + 1 < npass ? std::min(w, hi - off - w) : 0;
     uint32_t* nt_tot = p + 1 < npass ? totals + (size_t)(p + 1) * kMaxBins : nullptr;
     const int in = sb->cur, out = sb->cur ^ 1;
-    (void)hipMemsetAsync(sb->hist, 0, (size_t)(1 << bits) * nt * sizeof(uint32_t), s);  // look-back status
+    (void)hipMemsetAsync(sb->lb_status, 0, (size_t)(1 << bits) * nt * sizeof(uint64_t), s);  // look-back status
     if (sb->refs[in]) {
       hipLaunchKernelGGL(k_rs_scatter<true>, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
-                         sb->refs[out], sb->n, shift, bits, totals + (size_t)p * kMaxBins, sb->hist, ctr + p,
+                         sb->refs[out], sb->n, shift, bits, totals + (size_t)p * kMaxBins, sb->lb_status, ctr + p,
                          shift + w, nbits, nt_tot);
     } else {
       hipLaunchKernelGGL(k_rs_scatter<false>, dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out], nullptr,
-                         sb->n, shift, bits, totals + (size_t)p * kMaxBins, sb->hist, ctr + p, shift + w, nbits, nt_tot);
+                         sb->n, shift, bits, totals + (size_t)p * kMaxBins, sb->lb_status, ctr + p, shift + w, nbits, nt_tot);
     }
     sb->cur = out;
   }

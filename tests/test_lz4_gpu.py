@@ -43,6 +43,17 @@ def lz4_sequences(seqs, last_literals: bytes) -> bytes:
     return bytes(out)
 
 
+@pytest.fixture(params=["default", "no_dense"])
+def route(request, monkeypatch):
+    """Decode every block both ways: dense blocks on k_lz4_dense (default) and on the general decoder
+    (DG_LZ4_NO_DENSE=1, read by the library per call)."""
+    if request.param == "no_dense":
+        monkeypatch.setenv("DG_LZ4_NO_DENSE", "1")
+    else:
+        monkeypatch.delenv("DG_LZ4_NO_DENSE", raising=False)
+    return request.param
+
+
 def gpu_decode(blocks):
     N = importlib.import_module("incubator-druid_amd._native")
     S = importlib.import_module("incubator-druid_amd.segment")
@@ -127,7 +138,7 @@ def _crafted(rng):
 
 
 @pytest.mark.gpu
-def test_lz4_column_patterns_bit_exact(O, W):
+def test_lz4_column_patterns_bit_exact(route, O, W):
     rng = np.random.default_rng(11)
     blocks, names = [], []
     for name, raw in _column_payloads(rng).items():
@@ -140,7 +151,7 @@ def test_lz4_column_patterns_bit_exact(O, W):
 
 
 @pytest.mark.gpu
-def test_lz4_crafted_streams_bit_exact(O):
+def test_lz4_crafted_streams_bit_exact(route, O):
     rng = np.random.default_rng(5)
     cases = _crafted(rng)
     blocks = list(cases.values())
@@ -166,7 +177,7 @@ def test_lz4_malformed_blocks_rejected(O):
 
 
 @pytest.mark.gpu
-def test_lz4_many_blocks_one_launch(O, W):
+def test_lz4_many_blocks_one_launch(route, O, W):
     """A batch larger than the CU count, mixed block kinds, decoded in one launch."""
     rng = np.random.default_rng(3)
     pays = list(_column_payloads(rng).values())
@@ -222,7 +233,7 @@ def _lz4_hc(raw: bytes) -> bytes:
 
 
 @pytest.mark.gpu
-def test_lz4_light_decoder_boundaries(O):
+def test_lz4_light_decoder_boundaries(route, O):
     rng = np.random.default_rng(17)
     cases = _light_boundary(rng)
     blocks = list(cases.values()) * 3  # several per launch, mixed with the general decoder's blocks
@@ -307,9 +318,19 @@ def test_lz4_classification():
         N.check(N.lib().dg_debug_lz4_classify(b, len(b), ctypes.byref(k)))
         return k.value
 
+    # -1 malformed, 0/1 general (wide), 2 light, 3 dense (rounds), 4 dense (distance-8 class scan)
     for name, b in _value_run_cases(rng).items():
-        assert kind(b) in (0, 1), name
-    assert kind(_lz4_hc(rng.normal(5000.0, 1.0, BLOCK // 8).astype("<f8").tobytes())) == 0
+        assert kind(b) in (0, 1, 3, 4), name
+    n8 = BLOCK // 8
+    seq = np.arange(n8, dtype=np.int64)
+    assert kind(_lz4_hc((seq % 10000).astype("<i8").tobytes())) == 4
+    assert kind(_lz4_hc(np.round(seq * 1.3333 + 1388534400000).astype("<i8").tobytes())) == 4
+    assert kind(_lz4_hc(rng.normal(5000.0, 1.0, BLOCK // 8).astype("<f8").tobytes())) == 3
+    cases = _dense_boundary(np.random.default_rng(29))
+    assert all(kind(cases[f"lit{L}"]) in (3, 4) for L in (32, 33, 1000))
+    assert kind(cases["longlits256"]) in (3, 4) and kind(cases["longlits257"]) not in (3, 4)
+    assert kind(cases["match255"]) in (3, 4) and kind(cases["match256"]) not in (3, 4)
+    assert kind(cases["rounds64"]) == 3 and kind(cases["rounds65"]) not in (3, 4)
     ids = b"".join(int(x).to_bytes(4, "little")[:3] for x in rng.integers(1, 100001, BLOCK // 3 + 1))[:BLOCK]
     assert kind(_lz4_hc(ids)) == 2
     assert kind(b"\x00\x01") == -1
@@ -325,7 +346,7 @@ def test_value_run_streams_pinned_by_system_liblz4(O):
 
 
 @pytest.mark.gpu
-def test_lz4_value_runs_bit_exact(O):
+def test_lz4_value_runs_bit_exact(route, O):
     rng = np.random.default_rng(23)
     cases = _value_run_cases(rng)
     blocks = list(cases.values()) * 4  # several per launch
@@ -336,3 +357,91 @@ def test_lz4_value_runs_bit_exact(O):
             bad = [i for i in range(min(len(g or b""), len(exp))) if g[i] != exp[i]][:8] if g else None
             raise AssertionError(f"{name}: decoded {None if g is None else len(g)} vs {len(exp)} bytes, "
                                  f"first differences at {bad}")
+
+
+def _dense_boundary(rng):
+    """Blocks at the dense decoder's routing limits (matches of at most 255 bytes, at most 256 literal
+    runs over 32 bytes, matches resolved within 64 rounds, at most 1024 checkpoint intervals) and its
+    class-scan corner cases."""
+    r = lambda k: rng.integers(0, 256, k).astype(np.uint8).tobytes()  # noqa: E731
+    cases = {}
+
+    def filler(o, seqs, until):  # short sequences of fresh literals + a copy of the last 4 bytes
+        while o < until:
+            seqs.append((r(4), 4, 4))
+            o += 8
+        return o
+
+    for L in (32, 33, 1000):  # a literal run of 33+ bytes is copied by the whole workgroup
+        seqs = [(r(L), 17, 40)]
+        o = filler(L + 40, seqs, BLOCK - 600)
+        cases[f"lit{L}"] = lz4_sequences(seqs, r(BLOCK - o))
+    for k in (256, 257):  # at most 256 such runs per dense block
+        seqs, o = [], 0
+        for i in range(k):
+            seqs.append((r(40), 20, 4))
+            o += 44
+            o = filler(o, seqs, o + 40)
+        o = filler(o, seqs, BLOCK - 24)
+        cases[f"longlits{k}"] = lz4_sequences(seqs, r(BLOCK - o))
+    for M in (255, 256):
+        seqs = [(r(64), 50, M)]
+        o = filler(64 + M, seqs, BLOCK - 600)
+        cases[f"match{M}"] = lz4_sequences(seqs, r(BLOCK - o))
+    # a chain of k matches, each copying the previous one (depth k), in a block of short sequences
+    for k in (64, 65):
+        seqs, o = [(r(16), 8, 4)], 20
+        o = filler(o, seqs, 4000)
+        prev = None
+        for i in range(k):
+            if prev is None:  # the chain's first copy reads its own literals (depth 1)
+                o += 8
+                seqs.append((r(8), 8, 6))
+            else:
+                o += 3
+                seqs.append((r(3), o - prev, 6))
+            prev = o
+            o += 6
+            o = filler(o, seqs, o + 64)
+        o = filler(o, seqs, BLOCK - 600)
+        cases[f"rounds{k}"] = lz4_sequences(seqs, r(BLOCK - o))
+    # class mode whose distance-8 runs start from a periodic copy (distance 1) and from far copies
+    # that are themselves resolved only in later rounds (terminals resolved late)
+    seqs, o = [(b"\x05\x00\x00", 1, 5)], 8
+    far = []
+    while o < BLOCK - 1200:
+        for _ in range(int(rng.integers(20, 60))):
+            seqs.append((r(1), 8, 7))
+            o += 8
+        if far and rng.random() < 0.7:
+            d = o - far[int(rng.integers(0, len(far)))]
+        else:
+            d = int(rng.integers(9, o))
+        seqs.append((b"", d, 8))
+        far.append(o)
+        o += 8
+    for _ in range((BLOCK - 16 - o) // 8):
+        seqs.append((r(1), 8, 7))
+        o += 8
+    cases["class_late_terminals"] = lz4_sequences(seqs, r(BLOCK - o))
+    # 8192 sequences (1024 intervals, the last thread's pair full) and a short block of 5 sequences
+    cases["seq8192"] = lz4_sequences([(r(3), 3, 4) for i in range(8191)], r(5))
+    cases["seq5"] = lz4_sequences([(r(9), 8, 7)] * 4, r(5))
+    return cases
+
+
+def test_dense_boundary_streams_pinned_by_system_liblz4(O):
+    lib = ctypes.CDLL("liblz4.so.1")
+    for name, b in _dense_boundary(np.random.default_rng(29)).items():
+        dst = ctypes.create_string_buffer(BLOCK + 16)
+        n = lib.LZ4_decompress_safe(b, dst, len(b), BLOCK)
+        assert n > 0 and dst.raw[:n] == O.lz4_decompress(b), name
+
+
+@pytest.mark.gpu
+def test_lz4_dense_boundaries_bit_exact(route, O):
+    cases = _dense_boundary(np.random.default_rng(29))
+    blocks = list(cases.values()) * 3
+    got = gpu_decode(blocks)
+    for name, b, g in zip(list(cases) * 3, blocks, got):
+        assert g == O.lz4_decompress(b), name

@@ -18,7 +18,7 @@ S = importlib.import_module("incubator-druid_amd.segment")
 W = importlib.import_module("incubator-druid_amd.writer")
 BLOCK = 65536
 PHASES = ["stage", "parse+scan", "jobs+read", "fill+write", "resolve", "output"]
-KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light"}
+KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light", 3: "dense", 4: "dense-class"}
 
 
 def classify(block):
@@ -86,8 +86,7 @@ def main():
         if k not in kinds:
             continue
         ms, p = run(ctx, blocks)
-        kinds = sorted({classify(b) for b in blocks})
-        report(k, ms, p, "/".join(kinds))
+        report(k, ms, p, "/".join(sorted({classify(b) for b in blocks})))
     if sys.argv[1:] and "mix" not in kinds:
         return
     mix = []
