@@ -75,7 +75,9 @@ class dg_metrics(ctypes.Structure):
                 ("decode_side_ms", ctypes.c_double), ("bytes_side", ctypes.c_int64),
                 ("lz4_general_ms", ctypes.c_double), ("lz4_general_bytes", ctypes.c_int64),
                 ("lz4_general_blocks", ctypes.c_int32), ("lz4_general_launches", ctypes.c_int32),
-                ("bitmap_bytes", ctypes.c_int64)]
+                ("bitmap_bytes", ctypes.c_int64), ("reduce_kernel_ms", ctypes.c_double),
+                ("lz4_dense_ms", ctypes.c_double), ("lz4_dense_bytes", ctypes.c_int64),
+                ("lz4_dense_blocks", ctypes.c_int32), ("lz4_dense_launches", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

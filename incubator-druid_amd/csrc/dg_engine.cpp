@@ -399,6 +399,11 @@ struct DecodeBatch {
   int64_t gen_bytes = 0;
   int32_t gen_blocks = 0;
   int32_t gen_launches = 0;
+  // the same for the dense decoder
+  hipEvent_t dense_a = nullptr, dense_b = nullptr;
+  int64_t dense_bytes = 0;
+  int32_t dense_blocks = 0;
+  int32_t dense_launches = 0;
 };
 // device time of the general decoder's launches of a batch (0 if it launched none)
 static double gen_ms(const DecodeBatch& db) {
@@ -406,6 +411,30 @@ static double gen_ms(const DecodeBatch& db) {
   float f = 0;
   hipEventElapsedTime(&f, db.gen_a, db.gen_b);
   return f;
+}
+static double dense_ms(const DecodeBatch& db) {
+  if (!db.dense_blocks || !db.dense_a) return 0;
+  float f = 0;
+  hipEventElapsedTime(&f, db.dense_a, db.dense_b);
+  return f;
+}
+// the decode-timing events of a call's main (side = false) or side batch
+static void decode_events(Context* ctx, DecodeBatch* db, bool side) {
+  db->gen_a = ctx->gen_ev[side ? 2 : 0];
+  db->gen_b = ctx->gen_ev[side ? 3 : 1];
+  db->dense_a = ctx->gen_ev[side ? 6 : 4];
+  db->dense_b = ctx->gen_ev[side ? 7 : 5];
+}
+// a call's decode metrics from its main and side batches
+static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_metrics* m) {
+  m->lz4_general_ms = gen_ms(db) + gen_ms(side);
+  m->lz4_general_bytes = db.gen_bytes + side.gen_bytes;
+  m->lz4_general_blocks = db.gen_blocks + side.gen_blocks;
+  m->lz4_general_launches = db.gen_launches + side.gen_launches;
+  m->lz4_dense_ms = dense_ms(db) + dense_ms(side);
+  m->lz4_dense_bytes = db.dense_bytes + side.dense_bytes;
+  m->lz4_dense_blocks = db.dense_blocks + side.dense_blocks;
+  m->lz4_dense_launches = db.dense_launches + side.dense_launches;
 }
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
 static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st);
@@ -1227,15 +1256,19 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
   launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
-  // the token-dense decoders (dense + general) are timed together: "general" in the metrics
-  for (int i = 0; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
-  db->gen_blocks += nh;
-  db->gen_launches += (nd > 0) + (nn - nd > 0) + (nh - nn > 0);
-  if (db->gen_a && nh) hipEventRecord(db->gen_a, st);
+  for (int i = 0; i < nd; ++i) db->dense_bytes += db->jobs[i].src_len;
+  db->dense_blocks += nd;
+  db->dense_launches += nd > 0;
+  if (db->dense_a && nd) hipEventRecord(db->dense_a, st);
   launch_lz4_dense(d, nd, d_err, st, d_prof);
+  if (db->dense_a && nd) hipEventRecord(db->dense_b, st);
+  for (int i = nd; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
+  db->gen_blocks += nh - nd;
+  db->gen_launches += (nn - nd > 0) + (nh - nn > 0);
+  if (db->gen_a && nh > nd) hipEventRecord(db->gen_a, st);
   launch_lz4_decode(d + nd, nn - nd, 0, d_err, st, d_prof ? d_prof + (size_t)nd * kLz4ProfWords : nullptr);
   launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
-  if (db->gen_a && nh) hipEventRecord(db->gen_b, st);
+  if (db->gen_a && nh > nd) hipEventRecord(db->gen_b, st);
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
 
@@ -1997,8 +2030,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   std::vector<int64_t> tiles_rows(n, 0);
   std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db;
-  db.gen_a = ctx->gen_ev[0];
-  db.gen_b = ctx->gen_ev[1];
+  decode_events(ctx, &db, false);
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
@@ -2124,10 +2156,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
-  m.lz4_general_ms = gen_ms(db);
-  m.lz4_general_bytes = db.gen_bytes;
-  m.lz4_general_blocks = db.gen_blocks;
-  m.lz4_general_launches = db.gen_launches;
+  decode_metrics(db, DecodeBatch(), &m);
   m.aggregate_ms = f3;
   m.total_ms = ms_since(t0);
   if (metrics) *metrics = m;
@@ -2203,8 +2232,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   std::vector<int64_t> card(n, 1), tiles_rows(n, 0);
   std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db;
-  db.gen_a = ctx->gen_ev[0];
-  db.gen_b = ctx->gen_ev[1];
+  decode_events(ctx, &db, false);
   bool any_multi = false;
   hipEventRecord(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
@@ -2727,10 +2755,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
-  m.lz4_general_ms = gen_ms(db);
-  m.lz4_general_bytes = db.gen_bytes;
-  m.lz4_general_blocks = db.gen_blocks;
-  m.lz4_general_launches = db.gen_launches;
+  decode_metrics(db, DecodeBatch(), &m);
   m.aggregate_ms = f3;
   m.total_ms = ms_since(t0);
   ht.mark("done");
@@ -3212,10 +3237,8 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   }
   std::vector<const unsigned long long*> counts(n, nullptr);
   DecodeBatch db, db_side;  // db_side: payload columns decoded in place (side stream)
-  db.gen_a = ctx->gen_ev[0];
-  db.gen_b = ctx->gen_ev[1];
-  db_side.gen_a = ctx->gen_ev[2];
-  db_side.gen_b = ctx->gen_ev[3];
+  decode_events(ctx, &db, false);
+  decode_events(ctx, &db_side, true);
   for (int i = 0; i < n; ++i) {
     GbJob& j = gj[i];
     memset(&j, 0, sizeof j);
@@ -3339,6 +3362,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * rec * 8));
   res->cap = ng;
   if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "groupBy result of %lld groups", (long long)ng);
+  bool reduce_timed = false;
   if (ng > 0) {
     // run heads are only needed by the floatSum row-order pass
     uint32_t* head_pos = has_float_sum(plan) ? dev_take<uint32_t>(cs, (size_t)ng + 16) : nullptr;
@@ -3349,6 +3373,8 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     if ((has_float_sum(plan) && !head_pos) || !carry_g || !open_g || !carry_slots)
       return set_error(DG_ERR_OOM, "groupBy reduce scratch");
     if (side) DG_HIP(hipStreamWaitEvent(st, ctx->side_ev[2], 0));  // the payload is decoded
+    hipEventRecord(ctx->ev[7], st);
+    reduce_timed = true;
     launch_gb_reduce(&sb, plan, res->keys, res->slots, ng, head_pos, carry_g, carry_slots, open_g, st);
     for (int a = 0; a < na; ++a)
       if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, ntiles, &sb, plan, a, head_pos, res->slots, ng, st);
@@ -3375,14 +3401,16 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
-  m.lz4_general_ms = gen_ms(db) + gen_ms(db_side);
-  m.lz4_general_bytes = db.gen_bytes + db_side.gen_bytes;
-  m.lz4_general_blocks = db.gen_blocks + db_side.gen_blocks;
-  m.lz4_general_launches = db.gen_launches + db_side.gen_launches;
+  decode_metrics(db, db_side, &m);
   m.aggregate_ms = f3;
   m.keygen_ms = f4;
   m.sort_ms = f5;
   m.reduce_ms = f6;  // includes the group-count read-back between the sort and the reduce
+  if (reduce_timed) {
+    float fr = 0;
+    hipEventElapsedTime(&fr, ctx->ev[7], ctx->ev[4]);
+    m.reduce_kernel_ms = fr;
+  }
   m.sort_passes = key_bits > 0 ? (key_bits + 7) / 8 : 0;
   m.key_bits = key_bits;
   m.groups = ng;

@@ -65,8 +65,7 @@ struct Lz4Job {
   // and value v goes to dst + v * vstride (a column of the groupBy payload records, written in place);
   // bytes past expect_len are then not written (they would land in the next segment's records)
   int32_t vstride;
-  int32_t dense;       // token-dense block for k_lz4_dense (attach-time classification): 0 no, 1 match
-                       // rounds only, 2 distance-8 class scan + rounds (kDnMode*)
+  int32_t dense;       // token-dense block for k_lz4_dense (attach-time classification, kDnMode*)
 };
 
 // Light blocks (literal-heavy: random ids, high-entropy values): at most kLtMaxCps checkpoint
@@ -76,17 +75,17 @@ constexpr int kLtMaxCps = 256;
 constexpr int kLtThreads = 512;  // light-decoder threads (at most one light checkpoint interval each)
 constexpr int kLtMaxDepth = 16;
 
-// Dense blocks (token-dense value columns: sequential longs, timestamps, noisy doubles): at most
-// kLzMaxCps checkpoint intervals (two per thread), matches of at most kDnMaxRun bytes, at most kDnMaxLongLit literal runs longer than kDnShortLit,
-// and every match resolvable within kDnMaxRounds rounds (lz4_dense_mode simulates the kernel's
-// resolution order at attach). k_lz4_dense decodes them into a byte image + a resolved-bit map in LDS
-// (72 KiB: two blocks per CU).
-constexpr int kDnThreads = 512;
+// Dense blocks (token-dense, short matches at scattered distances: noisy doubles): at most kLzMaxCps
+// checkpoint intervals (one per thread), matches of at most kDnMaxRun bytes, at most kDnMaxLongLit
+// literal runs longer than kDnShortLit, and every match resolved within kDnMaxRounds rounds
+// (lz4_dense_mode simulates the kernel's resolution at attach). k_lz4_dense decodes them into a byte
+// image + a resolved-bit map in LDS beside the staged input.
+constexpr int kDnThreads = 1024;
 constexpr int kDnMaxRun = 255;        // longest match
 constexpr int kDnShortLit = 32;       // longer literal runs are copied by the whole workgroup ...
 constexpr int kDnMaxLongLit = 256;    // ... at most this many per block
 constexpr int kDnMaxRounds = 64;
-enum : int32_t { kDnModeNone = 0, kDnModeRounds = 1, kDnModeClass = 2 };
+enum : int32_t { kDnModeNone = 0, kDnModeRounds = 1 };
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
 struct LzfJob {
@@ -118,9 +117,8 @@ struct VsJob {
 // every g sequences (g the fewest sequences per checkpoint that fit the light decoder's threads).
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr,
                     int* nfine = nullptr, int* dense = nullptr);
-// The k_lz4_dense mode of a validated, non-wide block (kDnMode*): rounds or class mode when every
-// run fits kDnMaxRun and the kernel's resolution (distance-8 class scan in class mode, then rounds of
-// matches whose source bytes are resolved) finishes within kDnMaxRounds rounds; else kDnModeNone.
+// The k_lz4_dense mode of a validated, non-wide block (kDnMode*): kDnModeRounds when it fits the dense
+// decoder's limits (above) and its matches resolve within kDnMaxRounds rounds; else kDnModeNone.
 int lz4_dense_mode(const uint8_t* in, int n);
 
 struct AggPlan {
@@ -326,8 +324,9 @@ struct Context {
   // keys (the two only meet at the reduce); side_ev[0] = its inputs are staged, [1..2] = decode span
   hipStream_t side = nullptr;
   hipEvent_t side_ev[3] = {};
-  // the general LZ4 decoder's own span on each stream (main, side): its roofline figure (dg_metrics)
-  hipEvent_t gen_ev[4] = {};
+  // the general and the dense LZ4 decoders' own spans on each stream: [0, 1] general main, [2, 3]
+  // general side, [4, 5] dense main, [6, 7] dense side (their roofline figures, dg_metrics)
+  hipEvent_t gen_ev[8] = {};
   // dg_context_set_limit(DG_LIMIT_GROUP_ELEMENTS): most sort elements one groupBy call may build
   uint64_t max_elements = ~0ull;
   std::vector<std::shared_ptr<MergedDict>> dict_cache;  // most recent last

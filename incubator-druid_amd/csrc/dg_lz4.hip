@@ -244,6 +244,24 @@ __device__ __noinline__ void fill_general(uint16_t* e, uint16_t* tsrc, uint32_t*
   }
 }
 
+// max(v, v of the lane DPP control `ctrl` names), rows outside `rmask` and invalid lanes unchanged
+template <int CTRL, int RMASK>
+__device__ __forceinline__ uint32_t dpp_max_step(uint32_t old, uint32_t v) {
+  return max(old, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RMASK, 0xf, false));
+}
+
+// inclusive max-scan over the 64 lanes of a wave: row shifts 1/2/4/8, then the row broadcasts of
+// lanes 15 and 31 (no LDS round trips)
+__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v) {
+  v = dpp_max_step<0x111, 0xf>(v, v);  // row_shr:1
+  v = dpp_max_step<0x112, 0xf>(v, v);  // row_shr:2
+  v = dpp_max_step<0x114, 0xf>(v, v);  // row_shr:4
+  v = dpp_max_step<0x118, 0xf>(v, v);  // row_shr:8
+  v = dpp_max_step<0x142, 0xa>(v, v);  // row_bcast:15 into rows 1, 3
+  v = dpp_max_step<0x143, 0xc>(v, v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+
 // Wave-aggregated slot allocation: each lane asking for n slots gets its first slot index.
 __device__ __forceinline__ int wave_alloc(int* counter, int n) {
   int incl = n;  // inclusive prefix of n over the lanes
@@ -672,7 +690,9 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     // (position + 1) << 16 | its entry (0 = none yet); an E == 8 entry takes the terminal's literal
     // code, or the distance to the terminal while that is still open.
     const int x0 = tid * 64;
-    auto pair_at = [&](int q) { return x0 + 2 * q < lim ? s_e32[eph(x0 + 2 * q) >> 1] : 0xFF00FF00u; };
+    // my 64 positions lie in one skew span (64 | 128): pair q is dword eb + q of E
+    const int eb = (x0 >> 1) + (x0 >> kESkewShift);
+    auto pair_at = [&](int q) { return x0 + 2 * q < lim ? s_e32[eb + q] : 0xFF00FF00u; };
     uint32_t last[kClass];
 #pragma unroll
     for (int c = 0; c < kClass; ++c) last[c] = 0;
@@ -689,20 +709,21 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     uint32_t carry[kClass];
 #pragma unroll
     for (int c = 0; c < kClass; ++c) {  // exclusive max-scan over the threads (positions grow with tid)
-      uint32_t v = last[c];
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(v, o, 64);
-        if (ln >= o) v = max(v, y);
-      }
-      const uint32_t ex = __shfl_up(v, 1, 64);
-      carry[c] = ln ? ex : 0u;
+      const uint32_t v = wave_max_scan(last[c]);
+      carry[c] = dpp_max_step<0x138, 0xf>(0u, v);  // wave_shr:1 (lane 0 gets 0)
       if (ln == 63) s_scan[wv * kClass + c] = v;
     }
     __syncthreads();
+    {  // the earlier waves' totals: lane l reads class l % 8 of waves l / 8 and 8 + l / 8, then a
+       // max over the lanes of one class; no loop of dependent LDS reads
+      static_assert(kLzWaves == 16 && kClass == 8, "s_scan = two entries per lane");
+      uint32_t v = max((ln >> 3) < wv ? s_scan[ln] : 0u, 8 + (ln >> 3) < wv ? s_scan[64 + ln] : 0u);
+      v = max(v, (uint32_t)__shfl_xor((int)v, 8, 64));
+      v = max(v, (uint32_t)__shfl_xor((int)v, 16, 64));
+      v = max(v, (uint32_t)__shfl_xor((int)v, 32, 64));
 #pragma unroll
-    for (int c = 0; c < kClass; ++c)
-      for (int w = 0; w < wv; ++w) carry[c] = max(carry[c], s_scan[w * kClass + c]);
+      for (int c = 0; c < kClass; ++c) carry[c] = max(carry[c], (uint32_t)__builtin_amdgcn_readlane((int)v, c));
+    }
     auto take = [](uint32_t key, int x) -> uint32_t {  // new entry of a distance-8 byte at x
       const uint32_t tv = key & 0xFFFF;
       return tv >= (uint32_t)kTail ? tv : (uint32_t)(x + 1) - (key >> 16);
@@ -726,7 +747,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         carry[c + 1] = ((uint32_t)(x + 2) << 16) | hi;
       }
       const uint32_t nv = lo | (hi << 16);
-      if (nv != v) s_e32[eph(x) >> 1] = nv;  // x < lim whenever an entry changes
+      if (nv != v) s_e32[eb + q] = nv;  // x < lim whenever an entry changes
       list_append(t0 && lo < (uint32_t)kTail, x);  // open terminals
       list_append(t1 && hi < (uint32_t)kTail, x + 1);
     }
@@ -775,18 +796,33 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
           return;
         }
         jump_rounds++;
+        // four open pairs per step, their reads issued together (a step may read a pair another
+        // step of this round already advanced: jumping only converges faster)
         uint32_t keep = 0, mm = m;
+        const int xb = 64 * tid, eb = eph(xb) >> 1;  // my 64 positions lie in one skew span
         while (mm) {
-          const int bit = __builtin_ctz(mm);
-          mm &= mm - 1;
-          const int x = 2 * (32 * tid + bit);
-          const uint32_t v = s_e32[eph(x) >> 1];
-          const uint32_t d0 = v & 0xFFFF, d1 = v >> 16;
-          const uint32_t e0 = d0 < (uint32_t)kTail ? s_e[eph(x - (int)d0)] : 0xFF00u;
-          const uint32_t e1 = d1 < (uint32_t)kTail ? s_e[eph(x + 1 - (int)d1)] : 0xFF00u;
-          const uint32_t nv = jstep(d0, e0) | (jstep(d1, e1) << 16);
-          if (nv != v) s_e32[eph(x) >> 1] = nv;
-          if (is_open(nv)) keep |= 1u << bit;
+          int bit[4];
+          uint32_t v[4], e0[4], e1[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            bit[k] = mm ? __builtin_ctz(mm) : -1;
+            mm &= mm - 1;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = bit[k] >= 0 ? s_e32[eb + bit[k]] : 0xFF00FF00u;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int x = xb + 2 * bit[k];
+            const uint32_t d0 = v[k] & 0xFFFF, d1 = v[k] >> 16;
+            e0[k] = d0 < (uint32_t)kTail ? s_e[eph(x - (int)d0)] : 0xFF00u;
+            e1[k] = d1 < (uint32_t)kTail ? s_e[eph(x + 1 - (int)d1)] : 0xFF00u;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t nv = jstep(v[k] & 0xFFFF, e0[k]) | (jstep(v[k] >> 16, e1[k]) << 16);
+            if (nv != v[k]) s_e32[eb + bit[k]] = nv;  // (bit < 0: v is two codes, unchanged)
+            if (bit[k] >= 0 && is_open(nv)) keep |= 1u << bit[k];
+          }
         }
         m = keep;
         if (!__syncthreads_or(m != 0)) break;
@@ -809,42 +845,13 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     if (e < (uint32_t)kTail) e = s_e[eph(y - (int)e)];
     return e;
   };
-  // ---- tail: positions [kTail, total) hold absolute sources; rounds of jumping over the table ----
-  if (total > kTail) {
-    const int nt = total - kTail;
-    bool tact = tid < nt && !((s_tlit[tid >> 5] >> (tid & 31)) & 1u);
-    for (int round = 0;; ++round) {
-      uint32_t nsrc = 0;
-      bool res = false;
-      if (tact) {
-        const int src = s_tsrc[tid];
-        if (src < kTail) {
-          nsrc = final_code(src);
-          res = true;
-        } else {
-          const int i2 = src - kTail;
-          nsrc = s_tsrc[i2];
-          res = (s_tlit[i2 >> 5] >> (i2 & 31)) & 1u;
-        }
-      }
-      __syncthreads();
-      if (tact) {
-        s_tsrc[tid] = (uint16_t)nsrc;
-        if (res) {
-          atomicOr(&s_tlit[tid >> 5], 1u << (tid & 31));
-          tact = false;
-        }
-      }
-      if (!__syncthreads_or(tact)) break;
-      if (round > 10) {  // 256 positions: 9 rounds suffice
-        if (tid == 0) atomicOr(err, 1);
-        return;
-      }
-    }
-  }
-  // ---- 4. output: every entry is a literal code or one hop from one; 16 bytes per 16-byte store ----
+  // ---- tail: positions [kTail, total) hold absolute sources. The last wave alone jumps over the
+  // table (its LDS ops complete in order, so a round's reads precede its writes without a barrier)
+  // while the other waves write the chunks below kTail; the tail's chunks follow one barrier. ----
   const int nchunks = (total + 15) >> 4;
-  for (int c = tid; c < nchunks; c += kLzThreads) {
+  const bool has_tail = total > kTail;
+  const int nbody = has_tail ? (kTail >> 4) : nchunks;  // chunks below kTail (kTail % 16 == 0)
+  auto out_chunk = [&](int c) {
     const int x0 = c << 4;
     uint32_t w[4];
     if (x0 + 16 <= lim) {
@@ -879,6 +886,59 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       }
     }
     out16(job, c, w);
+  };
+  if (has_tail && wv == kLzWaves - 1) {
+    const int nt = total - kTail;
+    auto lit_at = [&](int i) { return (s_tlit[i >> 5] >> (i & 31)) & 1u; };
+    uint32_t act = 0;  // bit k: position ln + 64 k still a source
+#pragma unroll
+    for (int k = 0; k < kTailN / 64; ++k) {
+      const int i = ln + 64 * k;
+      if (i < nt && !lit_at(i)) act |= 1u << k;
+    }
+    for (int round = 0; __ballot(act != 0); ++round) {
+      if (round > 10) {  // 256 positions: 9 rounds suffice
+        s_bad = 1;
+        break;
+      }
+      uint32_t nsrc[kTailN / 64], res = 0;
+#pragma unroll
+      for (int k = 0; k < kTailN / 64; ++k) {
+        nsrc[k] = 0;
+        if ((act >> k) & 1u) {
+          const int src = s_tsrc[ln + 64 * k];
+          if (src < kTail) {
+            nsrc[k] = final_code(src);
+            res |= 1u << k;
+          } else {
+            const int i2 = src - kTail;
+            nsrc[k] = s_tsrc[i2];
+            res |= lit_at(i2) << k;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kTailN / 64; ++k) {
+        if ((act >> k) & 1u) {
+          const int i = ln + 64 * k;
+          s_tsrc[i] = (uint16_t)nsrc[k];
+          if ((res >> k) & 1u) atomicOr(&s_tlit[i >> 5], 1u << (i & 31));
+        }
+      }
+      act &= ~res;
+    }
+  } else {
+    // ---- 4. output: every entry is a literal code or one hop from one; 16 bytes per 16-byte store ----
+    const int nthr = has_tail ? kLzThreads - 64 : kLzThreads;
+    for (int c = tid; c < nbody; c += nthr) out_chunk(c);
+  }
+  if (has_tail) {
+    __syncthreads();
+    if (s_bad) {
+      if (tid == 0) atomicOr(err, 1);
+      return;
+    }
+    for (int c = nbody + tid; c < nchunks; c += kLzThreads) out_chunk(c);
   }
   if (PROF) {
     __syncthreads();
@@ -1158,32 +1218,28 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense decoder: token-dense blocks whose runs are short (attach-time classification,
-// lz4_dense_mode): sequential longs and timestamps (~8 K sequences of one literal byte and a 7-byte
-// copy at distance 8, copy chains through the whole block) and noisy doubles (~7.5 K sequences of ~5
-// literal bytes and a ~4-byte copy at a random distance, chains of <= ~24 hops). Instead of the
-// general decoder's 16-bit entry per output byte (128 KiB of LDS, one block per CU), the block is
-// resolved in place in a byte image of the output + one resolved bit per byte (72 KiB: two blocks per
-// CU), and every thread keeps its own sequences in registers:
-//   1. stage the compressed block in LDS; thread t parses checkpoint intervals 2t, 2t + 1 (<= 16
-//      sequences) into registers; a block scan of the output lengths places them;
-//   2. literal bytes go to the image (read from the compressed block in L2: the staged input is now
-//      dead, the image overlays it) and their resolved bits are set;
-//   3. class mode: a byte copied from 8 back has the value of the last byte of its residue class mod 8
-//      that is not such a copy (its terminal). A block-wide max-scan over the threads' last terminal
-//      per class gives every thread the terminals before its range; it then walks its range with an
-//      8-byte window of class values and writes every distance-8 byte whose terminal is resolved;
-//   4. rounds: every other match whose source bytes (its first period) are all resolved copies them
-//      and sets its bits; class mode re-walks the ranges still holding unresolved distance-8 bytes
-//      after a round that resolved terminals. The attach-time simulation bounds the rounds;
-//   5. the image goes out in 16-byte chunks (out16: slots, or 8-byte values to the payload records).
+// Dense decoder: token-dense blocks of short matches at scattered distances (attach-time
+// classification, lz4_dense_mode): noisy doubles (~7.5 K sequences of ~5 literal bytes and a ~4-byte
+// copy at a random distance, copy chains of <= ~24 hops). Blocks of 8-byte value runs (sequential
+// longs, timestamps: copies at distance 8 chaining through the whole block) stay on the general
+// decoder's class mode. Instead of the general decoder's 16-bit entry per output byte, the block is
+// resolved in place in a byte image of the output + one resolved bit per byte, beside the staged
+// input (which stays: literals are copied LDS to LDS). One thread per checkpoint interval (<= 8
+// sequences, kept in registers):
+//   1. stage the compressed block; parse; a block scan of the output lengths places the sequences;
+//   2. literal bytes go to the image and their bits are set (runs over kDnShortLit bytes are copied
+//      by the whole workgroup);
+//   3. rounds: every match whose source bytes (its first period) are all resolved copies them and
+//      sets its bits (a thread's reads for all its matches issued together); the attach-time
+//      simulation bounds the rounds (kDnMaxRounds);
+//   4. the image goes out in 16-byte chunks (out16: slots, or 8-byte values to the payload records).
 // ------------------------------------------------------------------------------------------------
 constexpr int kDnWaves = kDnThreads / 64;
-constexpr int kDnSeq = 2 * kLzSeqPerCp;                 // sequences per thread (two checkpoint intervals)
-constexpr int kDnResWords = kBlockBytes / 32;           // resolved bits
-constexpr int kDnBufWords = kBlockBytes / 4 + kDnResWords;  // image + resolved bits; first the staged input
-static_assert(kDnBufWords * 4 >= kLz4InCap + 16, "the staged input fits the image + bit map");
-static_assert(kDnThreads * 2 >= kLzMaxCps, "two checkpoint intervals per dense-decoder thread");
+constexpr int kDnSeq = kLzSeqPerCp;                      // sequences per thread (one checkpoint interval)
+constexpr int kDnResWords = kBlockBytes / 32;            // resolved bits
+constexpr int kDnInWords = (kLz4InCap + 32) / 4;         // staged input (+ zero pad)
+static_assert(kDnThreads >= kLzMaxCps, "one checkpoint interval per dense-decoder thread");
+
 
 // OR of the bits of positions [a, b) into the resolved map, one LDS atomic per word touched
 __device__ __forceinline__ void res_set(uint32_t* s_res, int a, int b) {
@@ -1207,49 +1263,71 @@ __device__ __forceinline__ bool res_all(const uint32_t* s_res, int a, int b) {
   return ok;
 }
 
+__device__ __forceinline__ uint32_t bits_of(int a, int b) {  // positions [a, b) of one 32-bit word, a <= b <= a + 32
+  const int lo = a & 31, hi = lo + (b - a);
+  return (hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+}
+
+// the residue classes mod 8 of positions [a, a + k)
+__device__ __forceinline__ uint32_t classes_of(int a, int k) {
+  if (k >= 8) return 0xFFu;
+  const uint32_t m = (1u << k) - 1u;
+  return ((m << (a & 7)) | (m >> (8 - (a & 7)))) & 0xFFu;
+}
+
 template <bool PROF>
-__global__ __launch_bounds__(kDnThreads, 4) void k_lz4_dense(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
-                                                             uint64_t* __restrict__ prof) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_buf[kDnBufWords];
+__global__ __launch_bounds__(kDnThreads) void k_lz4_dense(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+                                                          uint64_t* __restrict__ prof) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_in32[kDnInWords];    // staged compressed block
+  __shared__ __attribute__((aligned(16))) uint32_t s_img32[kBlockBytes / 4];  // decoded image
+  __shared__ uint32_t s_res[kDnResWords];                                   // resolved bits
+  __shared__ uint32_t s_aux[3 * kDnMaxLongLit];  // long literal runs: output start, input offset, length
   __shared__ int s_tmp[kDnWaves];
-  __shared__ uint32_t s_cls[kDnWaves * kClass];
-  __shared__ uint32_t s_lj[3 * kDnMaxLongLit];  // long literal runs: output start, input offset, length
   __shared__ int s_bad, s_nlj;
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = job.src_len, ncp = job.ncp;
-  const bool cls = job.dense == kDnModeClass;
-  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.wide || job.dec_len > kBlockBytes ||
+  if (job.dense != kDnModeRounds || n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.wide || job.dec_len > kBlockBytes ||
       job.dec_len < job.expect_len) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
   LZ_STAMP(0);
-  // ---- stage the compressed block (16-byte aligned and padded in the device image) ----
+  uint8_t* s_in = reinterpret_cast<uint8_t*>(s_in32);
+  uint8_t* s_img = reinterpret_cast<uint8_t*>(s_img32);
+  // ---- stage the compressed block (16-byte aligned and padded in the device image): every load of a
+  // thread issued before the first store ----
   {
-    uint4* dst = reinterpret_cast<uint4*>(s_buf);
+    uint4* dst = reinterpret_cast<uint4*>(s_in32);
     const int n16 = (n + 15) >> 4;
-    for (int i = tid; i < n16; i += kDnThreads) dst[i] = gld16(job.src + 16 * (size_t)i);
+    constexpr int kPer = (kLz4InCap + 16 * kDnThreads - 1) / (16 * kDnThreads);
+    uint4 v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (tid + k * kDnThreads < n16) v[k] = gld16(job.src + 16 * (size_t)(tid + k * kDnThreads));
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (tid + k * kDnThreads < n16) dst[tid + k * kDnThreads] = v[k];
     if (tid == 0) {
       dst[n16] = make_uint4(0, 0, 0, 0);
       s_bad = 0;
       s_nlj = 0;
     }
+    for (int i = tid; i < kDnResWords; i += kDnThreads) s_res[i] = 0;
   }
   __syncthreads();
   LZ_STAMP(1);
-  // ---- 1. parse my two intervals into registers. Sequence s: r_a = distance | literal length << 16,
+  // ---- 1. parse my interval into registers. Sequence s: r_a = distance | literal length << 16,
   // r_b = match start | match length << 17 (output positions, relative until the scan), r_lit =
   // literal input offset ----
-  const uint8_t* s_in = reinterpret_cast<const uint8_t*>(s_buf);
   uint32_t r_a[kDnSeq], r_b[kDnSeq], r_lit[kDnSeq];
-  int out_rel = 0;
-  bool bad = false;
 #pragma unroll
   for (int s = 0; s < kDnSeq; ++s) r_a[s] = r_b[s] = r_lit[s] = 0;
-  if (2 * tid < ncp) {
-    int pos = (int)gld4(job.cp + 2 * tid);
-    const int end = 2 * tid + 2 < ncp ? (int)gld4(job.cp + 2 * tid + 2) : n;
+  int out_rel = 0;
+  bool bad = false;
+  if (tid < ncp) {
+    int pos = (int)gld4(job.cp + tid);
+    const int end = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
 #pragma unroll
     for (int s = 0; s < kDnSeq; ++s) {
       if (pos < end) {
@@ -1275,7 +1353,7 @@ __global__ __launch_bounds__(kDnThreads, 4) void k_lz4_dense(const Lz4Job* __res
   }
   if (lane == 63) s_tmp[wave] = x;
   if (bad) s_bad = 1;
-  __syncthreads();  // also the end of every read of the staged input
+  __syncthreads();
   int base = x - out_rel, total = 0;
 #pragma unroll
   for (int w = 0; w < kDnWaves; ++w) {
@@ -1289,49 +1367,38 @@ __global__ __launch_bounds__(kDnThreads, 4) void k_lz4_dense(const Lz4Job* __res
     return;
   }
 #pragma unroll
-  for (int s = 0; s < kDnSeq; ++s)
-    r_b[s] += (uint32_t)base;  // (an absent sequence: an empty one at my range's start)
-  uint8_t* s_img = reinterpret_cast<uint8_t*>(s_buf);
-  uint32_t* s_res = s_buf + kBlockBytes / 4;
-  for (int i = tid; i < kDnResWords; i += kDnThreads) s_res[i] = 0;
-  __syncthreads();
-  // ---- 2. literal bytes (from the compressed block in L2: the staged input is dead, the image
-  // overlays it) -> image + resolved bits; long runs go to a list copied by the whole block. The
-  // matches still to resolve: `unres` (rounds) and, in class mode, the distance-8 ones `pend8` ----
-  uint32_t unres = 0, pend8 = 0;
-  {
-    int o = base;
+  for (int s = 0; s < kDnSeq; ++s) r_b[s] += (uint32_t)base;  // (an absent sequence: empty, at my range's end)
+  // ---- 2. literal bytes -> image + resolved bits; `unres`: my matches still to resolve ----
+  uint32_t unres = 0;
 #pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {
-      const int L = (int)(r_a[s] >> 16), d = (int)(r_a[s] & 0xFFFF), M = (int)(r_b[s] >> 17);
-      if (L > kDnShortLit) {
-        const int j = atomicAdd(&s_nlj, 1);
-        if (j < kDnMaxLongLit) {
-          s_lj[3 * j] = (uint32_t)o;
-          s_lj[3 * j + 1] = r_lit[s];
-          s_lj[3 * j + 2] = (uint32_t)L;
-        } else {
-          s_bad = 1;  // (more than the attach-time classification allows)
-        }
-      } else if (L > 0) {
-        const int lit = (int)r_lit[s], a0 = lit & ~3, nd = ((lit & 3) + L + 3) >> 2;
+  for (int s = 0; s < kDnSeq; ++s) {
+    const int L = (int)(r_a[s] >> 16), d = (int)(r_a[s] & 0xFFFF);
+    const int xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17), o = xm - L, lit = (int)r_lit[s];
+    if (L > kDnShortLit) {
+      const int j = atomicAdd(&s_nlj, 1);
+      if (j < kDnMaxLongLit) {
+        s_aux[3 * j] = (uint32_t)o;
+        s_aux[3 * j + 1] = (uint32_t)lit;
+        s_aux[3 * j + 2] = (uint32_t)L;
+      } else {
+        s_bad = 1;  // (more than the attach-time classification allows)
+      }
+    } else if (L > 0) {
+      // up to kDnShortLit bytes: dwords of the staged input, realigned, written bytewise
 #pragma unroll 1
-        for (int q = 0; q < nd; ++q) {
-          const uint32_t w = gld4(job.src + a0 + 4 * q);
+      for (int k0 = 0; k0 < L; k0 += 8) {
+        const int q = (lit + k0) >> 2, sh = (lit + k0) & 3;
+        const uint32_t a0 = s_in32[q], a1 = s_in32[q + 1], a2 = s_in32[q + 2];
+        const uint32_t v0 = __builtin_amdgcn_alignbyte(a1, a0, sh), v1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const int k = a0 + 4 * q + b - lit;
-            if (k >= 0 && k < L) s_img[o + k] = (uint8_t)(w >> (8 * b));
-          }
-        }
-        res_set(s_res, o, o + L);
+        for (int k = 0; k < 8; ++k)
+          if (k0 + k < L) s_img[o + k0 + k] = (uint8_t)((k < 4 ? v0 : v1) >> (8 * (k & 3)));
       }
-      if (M > 0) {
-        if (d > o + L) s_bad = 1;  // a copy from before the block
-        if (cls && d == kClass) pend8 |= 1u << s;
-        else unres |= 1u << s;
-      }
-      o += L + M;
+      res_set(s_res, o, xm);
+    }
+    if (M > 0) {
+      if (d > xm) s_bad = 1;  // a copy from before the block
+      unres |= 1u << s;
     }
   }
   __syncthreads();
@@ -1342,159 +1409,102 @@ __global__ __launch_bounds__(kDnThreads, 4) void k_lz4_dense(const Lz4Job* __res
   if (s_nlj > 0) {  // the long literal runs, every thread a byte of each (then their bits, by word)
     const int nlj = s_nlj;
     for (int j = 0; j < nlj; ++j) {
-      const int o = (int)s_lj[3 * j], lit = (int)s_lj[3 * j + 1], L = (int)s_lj[3 * j + 2];
-      for (int i = tid; i < L; i += kDnThreads) s_img[o + i] = (uint8_t)gld1(job.src + lit + i);
+      const int o = (int)s_aux[3 * j], lit = (int)s_aux[3 * j + 1], L = (int)s_aux[3 * j + 2];
+      for (int i = tid; i < L; i += kDnThreads) s_img[o + i] = s_in[lit + i];
       for (int w = (o >> 5) + tid; w <= ((o + L - 1) >> 5); w += kDnThreads) res_set(s_res, max(o, w << 5), min(o + L, (w + 1) << 5));
     }
     __syncthreads();
   }
   LZ_STAMP(3);
-  // ---- 3. class mode: terminals per residue class mod 8 ----
-  uint32_t carry[kClass];  // position + 1 of the last terminal before my range, per class (0: none)
-#pragma unroll
-  for (int c = 0; c < kClass; ++c) carry[c] = 0;
-  // walk of my range: writes every pending distance-8 byte whose terminal is resolved (a run of
-  // k >= 8 bytes sets its classes from its last 8 bytes)
-  auto class_walk = [&]() {
-#pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {
-      asm volatile("" : "+v"(r_a[s]));
-      asm volatile("" : "+v"(r_b[s]));
-    }
-    uint64_t win = 0;  // byte c: value of class c's current terminal
-    uint32_t valid = 0;
-#pragma unroll
-    for (int c = 0; c < kClass; ++c) {
-      const int y = (int)carry[c] - 1;
-      if (y >= 0 && ((s_res[y >> 5] >> (y & 31)) & 1u)) {
-        win |= (uint64_t)s_img[y] << (8 * c);
-        valid |= 1u << c;
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {
-      const int L = (int)(r_a[s] >> 16), d = (int)(r_a[s] & 0xFFFF);
-      const int xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
-      // literals: resolved terminals (the last 8 bytes of the run decide the window)
-      if (L > 0) {
-        const int o = xm - L;
-#pragma unroll 1
-        for (int k = max(0, L - 8); k < L; ++k) {
-          const int y = o + k, c = y & 7;
-          win = (win & ~(0xFFull << (8 * c))) | ((uint64_t)s_img[y] << (8 * c));
-          valid |= 1u << c;
-        }
-      }
-      if (M > 0) {
-        if (d == kClass) {
-          if ((pend8 >> s) & 1u) {
-            bool all = true;
-#pragma unroll 1
-            for (int k = 0; k < M; ++k) {
-              const int y = xm + k, c = y & 7;
-              if ((valid >> c) & 1u) s_img[y] = (uint8_t)(win >> (8 * c));
-              else all = false;
-            }
-            if (all) {
-              res_set(s_res, xm, xm + M);
-              pend8 &= ~(1u << s);
-            }
-          }
-        } else {  // another distance: a terminal, resolved or not
-          const bool res = !((unres >> s) & 1u);
-#pragma unroll 1
-          for (int k = max(0, M - 8); k < M; ++k) {
-            const int y = xm + k, c = y & 7;
-            if (res) {
-              win = (win & ~(0xFFull << (8 * c))) | ((uint64_t)s_img[y] << (8 * c));
-              valid |= 1u << c;
-            } else {
-              valid &= ~(1u << c);
-            }
-          }
-        }
-      }
-    }
-  };
-  if (cls) {
-    // my last terminal per class (position + 1), from my sequences' literal runs and non-class matches
-    uint32_t last[kClass];
-#pragma unroll
-    for (int c = 0; c < kClass; ++c) last[c] = 0;
-#pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {
-      const int L = (int)(r_a[s] >> 16), d = (int)(r_a[s] & 0xFFFF);
-      const int xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
-      const int o = xm - L, e = xm + (d == kClass ? 0 : M);  // terminals: [o, e)
-      if (e > o) {
-#pragma unroll
-        for (int c = 0; c < kClass; ++c) {
-          const int p = (e - 1) - (((e - 1) - c) & 7);  // last position of class c in [.., e)
-          if (p >= o) last[c] = (uint32_t)(p + 1);
-        }
-      }
-    }
-    // exclusive max-scan over the threads (positions grow with the thread index)
-#pragma unroll
-    for (int c = 0; c < kClass; ++c) {
-      uint32_t v = last[c];
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(v, off, 64);
-        if (lane >= off) v = max(v, y);
-      }
-      const uint32_t ex = __shfl_up(v, 1, 64);
-      carry[c] = lane ? ex : 0u;
-      if (lane == 63) s_cls[wave * kClass + c] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < kClass; ++c)
-      for (int w = 0; w < wave; ++w) carry[c] = max(carry[c], s_cls[w * kClass + c]);
-    if (pend8) class_walk();
-  }
-  LZ_STAMP(4);
-  // ---- 4. rounds ----
   int rounds = 0;
+  // ---- 3'. rounds: each match whose source bytes (its first period) are resolved copies them;
+  // a thread's reads for all its matches go out together ----
   for (;; ++rounds) {
-    if (!__syncthreads_or((unres | pend8) != 0)) break;
+    if (!__syncthreads_or(unres != 0)) break;
     if (rounds > kDnMaxRounds + 1) {  // beyond the attach-time bound: not a block of this kind
       if (tid == 0) atomicOr(err, 1);
       return;
     }
-    // the sequence registers are re-read every round (no loop-invariant copies of their fields: the
-    // kernel must stay within 128 VGPRs for two blocks per CU)
 #pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {
+    for (int s = 0; s < kDnSeq; ++s) {  // (no loop-invariant copies of the fields: VGPR budget)
       asm volatile("" : "+v"(r_a[s]));
       asm volatile("" : "+v"(r_b[s]));
+      asm volatile("" : "+v"(r_lit[s]));
     }
-    bool progress = false;
-    if (unres) {
+    uint32_t rw[kDnSeq][2];
+#pragma unroll
+    for (int s = 0; s < kDnSeq; ++s) {
+      rw[s][0] = rw[s][1] = 0;
+      if ((unres >> s) & 1u) {
+        const int d = (int)(r_a[s] & 0xFFFF), xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
+        const int a = xm - d, e = a + min(M, d);
+        rw[s][0] = s_res[a >> 5];
+        rw[s][1] = s_res[(e - 1) >> 5];
+      }
+    }
+    uint32_t ok = 0;
+#pragma unroll
+    for (int s = 0; s < kDnSeq; ++s) {
+      if ((unres >> s) & 1u) {
+        const int d = (int)(r_a[s] & 0xFFFF), xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
+        const int a = xm - d, e = a + min(M, d);
+        bool y;
+        if ((a >> 5) == ((e - 1) >> 5)) {
+          const uint32_t m = bits_of(a, e);
+          y = (rw[s][0] & m) == m;
+        } else if ((a >> 5) + 1 == ((e - 1) >> 5)) {
+          const uint32_t m0 = bits_of(a, (a | 31) + 1), m1 = bits_of((e - 1) & ~31, e);
+          y = (rw[s][0] & m0) == m0 && (rw[s][1] & m1) == m1;
+        } else {
+          y = res_all(s_res, a, e);
+        }
+        ok |= y ? 1u << s : 0u;
+      }
+    }
+    if (ok) {
+      // (a bit seen set by another wave this round: the bytes were written before it)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      uint32_t sw[kDnSeq][3];  // sources of the short non-overlapping copies: three dwords
 #pragma unroll
       for (int s = 0; s < kDnSeq; ++s) {
-        if ((unres >> s) & 1u) {
+        sw[s][0] = sw[s][1] = sw[s][2] = 0;
+        const int d = (int)(r_a[s] & 0xFFFF), M = (int)(r_b[s] >> 17);
+        if (((ok >> s) & 1u) && d >= M && M <= 8) {
+          const int aw = ((int)(r_b[s] & 0x1FFFF) - d) >> 2;
+          sw[s][0] = s_img32[aw];
+          sw[s][1] = s_img32[aw + 1];
+          sw[s][2] = s_img32[aw + 2];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < kDnSeq; ++s) {
+        if ((ok >> s) & 1u) {
           const int d = (int)(r_a[s] & 0xFFFF), xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
-          const int a = xm - d, len = min(M, d);
-          if (res_all(s_res, a, a + len)) {
-            // (a bit seen set by another wave this round: its bytes were written before it)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          const int a = xm - d;
+          if (d >= M && M <= 8) {
+            const int sh = a & 3;
+            const uint32_t v0 = __builtin_amdgcn_alignbyte(sw[s][1], sw[s][0], sh);
+            const uint32_t v1 = __builtin_amdgcn_alignbyte(sw[s][2], sw[s][1], sh);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (k < M) s_img[xm + k] = (uint8_t)((k < 4 ? v0 : v1) >> (8 * (k & 3)));
+          } else {
 #pragma unroll 1
             for (int k = 0, r = 0; k < M; ++k) {  // LZ4 overlap: byte k copies the first period
               s_img[xm + k] = s_img[a + r];
               if (++r == d) r = 0;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            res_set(s_res, xm, xm + M);
-            unres &= ~(1u << s);
-            progress = true;
           }
         }
       }
-    }
-    if (cls) {
-      // terminals resolved this round reach their distance-8 followers (in any thread's range)
-      if (__syncthreads_or(progress) && pend8) class_walk();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+      for (int s = 0; s < kDnSeq; ++s)
+        if ((ok >> s) & 1u) {
+          const int xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
+          res_set(s_res, xm, xm + M);
+        }
+      unres &= ~ok;
     }
   }
   LZ_STAMP(5);
@@ -1504,9 +1514,10 @@ __global__ __launch_bounds__(kDnThreads, 4) void k_lz4_dense(const Lz4Job* __res
     prof[(size_t)blockIdx.x * kLz4ProfWords + 10] = (uint64_t)s_nlj;
     prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
   }
-  // ---- 5. output: 16-byte chunks of the image ----
+  __syncthreads();
+  // ---- 4. output: 16-byte chunks of the image ----
   const int nchunks = (total + 15) >> 4;
-  const uint4* img16 = reinterpret_cast<const uint4*>(s_buf);
+  const uint4* img16 = reinterpret_cast<const uint4*>(s_img32);
   for (int c = tid; c < nchunks; c += kDnThreads) {
     const uint4 v = img16[c];
     uint32_t w[4] = {v.x, v.y, v.z, v.w};

@@ -179,12 +179,11 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
 }
 
 // Simulation of k_lz4_dense's resolution order (dg_lz4.hip) on a validated block: literal bytes are
-// resolved at round 0; in class mode (distance-8 copies are more than a quarter of the output, as the
-// kernel's class scan assumes) a distance-8 byte resolves with its class terminal (the last earlier
-// byte of its residue class mod 8 that is not a distance-8 copy); every other match resolves one
-// round after the last of its source bytes (its first period). The kernel resolves at least this
-// fast (its rounds also see same-round results), so the block is dense when every run fits
-// kDnMaxRun and the last match resolves by round kDnMaxRounds.
+// resolved at round 0, and every match resolves one round after the last of its source bytes (its
+// first period). The kernel resolves at least this fast (a round also sees some same-round results),
+// so the block is dense when every match fits kDnMaxRun, at most kDnMaxLongLit literal runs are
+// longer than kDnShortLit, and the last match resolves by round kDnMaxRounds. Blocks of 8-byte value
+// runs (distance-8 copies over a quarter of the output) stay on the general decoder's class mode.
 int lz4_dense_mode(const uint8_t* in, int n) {
   thread_local std::vector<uint8_t> rd(kBlockBytes);
   struct Seq {
@@ -223,36 +222,18 @@ int lz4_dense_mode(const uint8_t* in, int n) {
     if (d == 8) c8 += M;
     out += L + M;
   }
-  if (seqs.size() > (size_t)kLzMaxCps * kLzSeqPerCp) return kDnModeNone;
-  const bool cls = (int64_t)c8 * 4 > out;
-  int last[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-  int x = 0, mx = 0;
+  if (seqs.size() > (size_t)kLzMaxCps * kLzSeqPerCp || (int64_t)c8 * 4 > out) return kDnModeNone;
+  int x = 0;
   for (const Seq& q : seqs) {
-    for (int k = 0; k < q.L; ++k, ++x) {
-      rd[x] = 0;
-      last[x & 7] = x;
-    }
+    for (int k = 0; k < q.L; ++k) rd[x++] = 0;
     if (!q.M) continue;
-    if (cls && q.d == 8) {
-      for (int k = 0; k < q.M; ++k, ++x) {
-        const int t = last[x & 7];
-        if (t < 0) return kDnModeNone;
-        rd[x] = rd[t];
-      }
-      continue;
-    }
     int r = 0;
     const int a = x - q.d;
     for (int k = 0; k < std::min(q.M, q.d); ++k) r = std::max<int>(r, rd[a + k]);
-    r += 1;
-    if (r > kDnMaxRounds) return kDnModeNone;
-    mx = std::max(mx, r);
-    for (int k = 0; k < q.M; ++k, ++x) {
-      rd[x] = (uint8_t)r;
-      last[x & 7] = x;
-    }
+    if (++r > kDnMaxRounds) return kDnModeNone;
+    for (int k = 0; k < q.M; ++k) rd[x++] = (uint8_t)r;
   }
-  return cls ? kDnModeClass : kDnModeRounds;
+  return kDnModeRounds;
 }
 
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine, int* dense) {

@@ -318,19 +318,20 @@ def test_lz4_classification():
         N.check(N.lib().dg_debug_lz4_classify(b, len(b), ctypes.byref(k)))
         return k.value
 
-    # -1 malformed, 0/1 general (wide), 2 light, 3 dense (rounds), 4 dense (distance-8 class scan)
+    # -1 malformed, 0/1 general (wide), 2 light, 3 dense
     for name, b in _value_run_cases(rng).items():
-        assert kind(b) in (0, 1, 3, 4), name
+        assert kind(b) in (0, 1), name  # 8-byte value runs: the general decoder's class mode
     n8 = BLOCK // 8
     seq = np.arange(n8, dtype=np.int64)
-    assert kind(_lz4_hc((seq % 10000).astype("<i8").tobytes())) == 4
-    assert kind(_lz4_hc(np.round(seq * 1.3333 + 1388534400000).astype("<i8").tobytes())) == 4
+    assert kind(_lz4_hc((seq % 10000).astype("<i8").tobytes())) == 0
+    assert kind(_lz4_hc(np.round(seq * 1.3333 + 1388534400000).astype("<i8").tobytes())) == 0
     assert kind(_lz4_hc(rng.normal(5000.0, 1.0, BLOCK // 8).astype("<f8").tobytes())) == 3
     cases = _dense_boundary(np.random.default_rng(29))
-    assert all(kind(cases[f"lit{L}"]) in (3, 4) for L in (32, 33, 1000))
-    assert kind(cases["longlits256"]) in (3, 4) and kind(cases["longlits257"]) not in (3, 4)
-    assert kind(cases["match255"]) in (3, 4) and kind(cases["match256"]) not in (3, 4)
-    assert kind(cases["rounds64"]) == 3 and kind(cases["rounds65"]) not in (3, 4)
+    assert all(kind(cases[f"lit{L}"]) == 3 for L in (32, 33, 1000))
+    assert kind(cases["longlits256"]) == 3 and kind(cases["longlits257"]) != 3
+    assert kind(cases["match255"]) == 3 and kind(cases["match256"]) != 3
+    assert kind(cases["rounds64"]) == 3 and kind(cases["rounds65"]) != 3
+    assert kind(cases["seq8192"]) == 3 and kind(cases["class_late_terminals"]) in (0, 1)
     ids = b"".join(int(x).to_bytes(4, "little")[:3] for x in rng.integers(1, 100001, BLOCK // 3 + 1))[:BLOCK]
     assert kind(_lz4_hc(ids)) == 2
     assert kind(b"\x00\x01") == -1
