@@ -160,11 +160,15 @@ def _cpu_model():
 
 
 def _cpu_threads():
-    """Every core this process may run on (sched_getaffinity), as SURVEY §8(d) asks for."""
+    """The cores this process can actually use: its affinity set (sched_getaffinity, as SURVEY §8(d)
+    asks for), capped by the cgroup CPU quota (a 16-core quota on a 256-thread affinity set runs 16
+    cores' worth of work, however many threads are spawned)."""
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        aff = max(1, len(os.sched_getaffinity(0)))
     except AttributeError:
-        return max(1, os.cpu_count() or 1)
+        aff = max(1, os.cpu_count() or 1)
+    q = _cpu_quota()
+    return max(1, min(aff, int(q))) if q else aff
 
 
 def _cpu_quota():
@@ -176,73 +180,297 @@ def _cpu_quota():
         return None
 
 
+def _cpu_lib():
+    """oracle/libdruid_cpu.so (C -O3 -march=native restatement of the reference's per-segment loops)."""
+    lib = ctypes.CDLL(os.path.join(REPO, "oracle", "libdruid_cpu.so"))
+    vp, i32, i64, cp = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_char_p
+    lib.or_open.restype = vp
+    lib.or_open.argtypes = [cp, cp, ctypes.c_int]
+    lib.or_close.argtypes = [vp]
+    lib.cpu_groupby2.restype = i64
+    lib.cpu_groupby2.argtypes = [ctypes.POINTER(vp), ctypes.c_int, cp, cp, cp, cp, vp, vp, i32, ctypes.c_int,
+                                 i64, i64, i64, i32, ctypes.POINTER(ctypes.c_double), vp, vp, vp, vp,
+                                 ctypes.POINTER(ctypes.c_double)]
+    lib.cpu_timeseries.restype = ctypes.c_int
+    lib.cpu_timeseries.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp, vp,
+                                   ctypes.c_int, i64, i64, i64, i64, i64, i32, ctypes.c_int, vp, vp, vp, vp,
+                                   ctypes.POINTER(ctypes.c_double)]
+    lib.cpu_topn.restype = ctypes.c_int
+    lib.cpu_topn.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp, vp, ctypes.c_int,
+                             cp, vp, ctypes.c_int, vp, vp, ctypes.c_int, i32, i32, vp, vp,
+                             ctypes.POINTER(ctypes.c_double)]
+    return lib
+
+
+class _CpuSegments:
+    """The segments opened by the CPU engine's own reader (and the oracle's, for dictionaries)."""
+
+    def __init__(self, paths):
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        self.O = O
+        self.lib = _cpu_lib()
+        self.osegs = [O.OracleSegment(p) for p in paths]
+        err = ctypes.create_string_buffer(512)
+        hs = [self.lib.or_open(p.encode(), err, 512) for p in paths]
+        if not all(hs):
+            raise IOError(err.value.decode())
+        self.hs = hs
+        self.handles = (ctypes.c_void_p * len(hs))(*hs)
+        self.rows = sum(s.num_rows for s in self.osegs)
+        self._keep = []
+
+    def close(self):
+        for s, h in zip(self.osegs, self.hs):
+            s.close()
+            self.lib.or_close(h)
+
+    def merged(self, dim):
+        """Merged dictionary (Java String order, nulls first) and per-segment local -> merged id maps."""
+        dicts = [s.dictionary(dim) for s in self.osegs]
+        merged = sorted(set().union(*map(set, dicts)), key=lambda v: (v is not None, (v or "").encode("utf-16-be")))
+        index = {v: i for i, v in enumerate(merged)}
+        maps = [np.array([index[v] for v in dd], dtype=np.int32) for dd in dicts]
+        return merged, maps
+
+    def filter_program(self, filt):
+        """The query filter (DimFilter.optimize) as the engine's postfix program over bitmap leaves, with
+        every leaf's dictionary ids per segment (-1 terminated): selector / in / bound leaves under
+        And / Or / Not (Filter.getBitmapResult)."""
+        O = self.O
+        Q = importlib.import_module("incubator-druid_amd.query")
+        f = O.o_optimize(filt) if filt is not None else None
+        prog, leaves = [], []
+
+        def walk(node):
+            if isinstance(node, (Q.AndDimFilter, Q.OrDimFilter)):
+                op = -1 if isinstance(node, Q.AndDimFilter) else -2
+                for k, ch in enumerate(node.fields):
+                    walk(ch)
+                    if k:
+                        prog.append(op)
+            elif isinstance(node, Q.NotDimFilter):
+                walk(node.field)
+                prog.append(-3)
+            else:
+                leaves.append(node)
+                prog.append(len(leaves) - 1)
+
+        if f is not None:
+            walk(f)
+        ids = []
+        for seg in self.osegs:
+            for lf in leaves:
+                sel = O.filter_id_set(seg, lf) if seg.is_dim(lf.dimension) else []
+                a = np.array(list(sel) + [-1], dtype=np.int32)
+                self._keep.append(a)
+                ids.append(a.ctypes.data)
+        dims = [lf.dimension.encode() for lf in leaves]
+        self._keep += [dims]
+        P = (ctypes.c_int32 * max(len(prog), 1))(*prog)
+        D = (ctypes.c_char_p * max(len(dims), 1))(*dims)
+        I = (ctypes.c_void_p * max(len(ids), 1))(*ids)
+        self._keep += [P, D, I]
+        return P, len(prog), D, I, len(leaves)
+
+
+def _query_buckets(query, segs):
+    """Granularity buckets of a timeseries / groupBy query over the segments: (t_lo, t_hi, origin,
+    period, bucket0, nbuckets); ALL = one bucket (fixed UTC periods only, as the benched queries use)."""
+    t_lo, t_hi = query.interval
+    g = query.granularity
+    if g.is_all:
+        return t_lo, t_hi, 0, 0, 0, 1
+    P, org = g.period_ms, g.origin_ms
+    lo = min(s.interval[0] for s in segs)
+    hi = max(s.interval[1] for s in segs)
+    b0 = (max(lo, t_lo) - org) // P
+    b1 = (min(hi, t_hi) - 1 - org) // P
+    return t_lo, t_hi, org, P, b0, int(b1 - b0 + 1)
+
+
+def _baseline_line(value, threads, kind, sample, extra=None):
+    d = {"value": value, "unit": "rows/s", "cores": threads, "kind": kind, "sample": sample, "cpu_model": _cpu_model(),
+         "nproc": os.cpu_count(), "cgroup_quota_cores": _cpu_quota()}
+    if extra:
+        d.update(extra)
+    return d
+
+
+def cpu_baseline_timeseries(paths, query, threads):
+    """oracle/cpu_engine.c cpu_timeseries on the whole step workload: the filter's bitmaps per segment,
+    then the TimeseriesQueryEngine loop over 1 M-row chunks on `threads` cores (LZ4 decoded inside the
+    timing). Returns (baseline line, {bucket timestamp: (rows, [agg values])})."""
+    cs = _CpuSegments(paths)
+    try:
+        P, nprog, D, I, nleaf = cs.filter_program(query.filter)
+        t_lo, t_hi, org, per, b0, nb = _query_buckets(query, cs.osegs)
+        aggs = query.aggregations
+        kinds = (ctypes.c_int32 * len(aggs))(*[a.kind for a in aggs])
+        cols = (ctypes.c_char_p * len(aggs))(*[(a.fieldName or "").encode() for a in aggs])
+        rows = np.zeros(nb, np.int64)
+        state = np.zeros(nb * len(aggs), np.uint64)
+        secs = ctypes.c_double()
+        rc = cs.lib.cpu_timeseries(cs.handles, len(paths), threads, P, nprog, D, I, nleaf, t_lo, t_hi, org, per, b0, nb,
+                                   len(aggs), kinds, cols, rows.ctypes.data, state.ctypes.data, ctypes.byref(secs))
+        if rc:
+            raise RuntimeError("cpu_timeseries failed")
+        out = {}
+        for b in range(nb):
+            if rows[b] or query.granularity.is_all:
+                vals = []
+                for k, a in enumerate(aggs):
+                    v = state[k * nb + b]
+                    vals.append(float(v.view(np.float64)) if a.output_type == "double" else int(v.view(np.int64)))
+                ts = t_lo if query.granularity.is_all else org + (b0 + b) * per
+                out[ts] = (int(rows[b]), vals)
+        sel = int(rows.sum())
+        line = _baseline_line(cs.rows / secs.value, threads, "port",
+                              f"the whole step workload: {len(paths)} segments x {cs.rows // len(paths)} rows, "
+                              f"{sel} selected rows in {secs.value:.3f} s (oracle/cpu_engine.c cpu_timeseries, C -O3 "
+                              f"-march=native, {threads} threads over 1M-row chunks, bitmap filter + LZ4 decode inside "
+                              f"the timing); value = scanned rows/s",
+                              {"selected_rows_per_s": sel / secs.value})
+        return line, out
+    finally:
+        cs.close()
+
+
+def check_timeseries(gpu, cpu, query):
+    """Per-bucket equality of the GPU's merged timeseries result with the CPU engine's: the same
+    non-empty buckets, counts / long aggregators bit-exact, double aggregators within 1e-9 relative."""
+    g = {}
+    for r in gpu:
+        vals = [r.value[a.name] for a in query.aggregations]
+        if query.granularity.is_all or any(v != 0 for v in vals):
+            g[r.timestamp] = vals
+    c = {ts: v for ts, (n, v) in cpu.items()}
+    if query.granularity.is_all:  # one bucket (its timestamp is the cursor's start, not checked here)
+        g = {0: v for v in g.values()}
+        c = {0: v for v in c.values()}
+    out = {"buckets": len(c), "buckets_equal": sorted(g) == sorted(c)}
+    longs_ok, maxrel = True, 0.0
+    for ts in set(g) & set(c):
+        for a, x, y in zip(query.aggregations, g[ts], c[ts]):
+            if a.output_type == "double":
+                if x != y:
+                    rel = abs(x - y) / max(abs(x), abs(y), 1e-300)
+                    if rel == rel:
+                        maxrel = max(maxrel, rel)
+                    else:
+                        maxrel = float("inf")
+            elif int(x) != int(y):
+                longs_ok = False
+    out["longs_equal"] = longs_ok
+    out["double_max_rel_err"] = maxrel
+    out["doubles_within_1e-9"] = maxrel <= 1e-9
+    out["per_bucket_equal"] = out["buckets_equal"] and longs_ok and out["doubles_within_1e-9"]
+    return out
+
+
+def cpu_baseline_topn(paths, query, threads):
+    """oracle/cpu_engine.c cpu_topn (numeric metric): PooledTopNAlgorithm per segment on `threads`
+    cores (one segment per thread, as ChainedExecutionQueryRunner), top max(threshold, 1000) per segment,
+    TopNBinaryFn fold in segment order. Returns (baseline line, [(value, [agg values])])."""
+    cs = _CpuSegments(paths)
+    try:
+        P, nprog, D, I, nleaf = cs.filter_program(query.filter)
+        merged, maps = cs.merged(query.dimension)
+        R = (ctypes.c_void_p * len(maps))(*[m.ctypes.data for m in maps])
+        aggs = query.aggregations
+        kinds = (ctypes.c_int32 * len(aggs))(*[a.kind for a in aggs])
+        cols = (ctypes.c_char_p * len(aggs))(*[(a.fieldName or "").encode() for a in aggs])
+        metric = [a.name for a in aggs].index(query.metric.metric)
+        ids = np.zeros(query.threshold, np.int32)
+        vals = np.zeros(query.threshold * len(aggs), np.uint64)
+        secs = ctypes.c_double()
+        n = cs.lib.cpu_topn(cs.handles, len(paths), threads, P, nprog, D, I, nleaf, query.dimension.encode(), R, len(aggs),
+                            kinds, cols, metric, query.threshold, int(query.context.get("minTopNThreshold", 1000)),
+                            ids.ctypes.data, vals.ctypes.data, ctypes.byref(secs))
+        if n < 0:
+            raise RuntimeError("cpu_topn failed")
+        out = []
+        for i in range(n):
+            vs = []
+            for k, a in enumerate(aggs):
+                v = vals[i * len(aggs) + k]
+                vs.append(float(v.view(np.float64)) if a.output_type == "double" else int(v.view(np.int64)))
+            out.append((merged[ids[i]], vs))
+        line = _baseline_line(cs.rows / secs.value, min(threads, len(paths)), "port",
+                              f"the whole step workload: {len(paths)} segments x {cs.rows // len(paths)} rows in "
+                              f"{secs.value:.3f} s (oracle/cpu_engine.c cpu_topn, C -O3 -march=native, one segment per "
+                              f"thread like ChainedExecutionQueryRunner: {min(threads, len(paths))} of {threads} cores "
+                              f"busy, LZ4 decode inside the timing)")
+        return line, out
+    finally:
+        cs.close()
+
+
+def check_topn(gpu, cpu, query):
+    """The GPU's final topN list vs the CPU engine's: same dimension values in the same order, long
+    aggregators bit-exact, doubles within 1e-9 relative."""
+    rows = gpu[0].value if gpu else []
+    out = {"entries": len(rows), "values_equal": [r[query.dimension] for r in rows] == [v for v, _ in cpu]}
+    longs_ok, maxrel = True, 0.0
+    for r, (_, vs) in zip(rows, cpu):
+        for a, y in zip(query.aggregations, vs):
+            x = r[a.name]
+            if a.output_type == "double":
+                if x != y:
+                    maxrel = max(maxrel, abs(x - y) / max(abs(x), abs(y), 1e-300))
+            elif int(x) != int(y):
+                longs_ok = False
+    out["longs_equal"] = longs_ok
+    out["double_max_rel_err"] = maxrel
+    out["doubles_within_1e-9"] = maxrel <= 1e-9
+    out["per_entry_equal"] = out["values_equal"] and longs_ok and out["doubles_within_1e-9"]
+    return out
+
+
 def cpu_baseline_groupby(paths, query, threads, want_groups=False):
     """oracle/libdruid_cpu.so: the reference's per-segment GroupByV2 loop (LZ4 decode, hash grouping,
     merge by value, ordered result) in C -O3 -march=native over row chunks of the segments on
     `threads` host threads, on the whole workload. Merged-dictionary maps are built before timing (the
-    GPU engine caches them too). want_groups: also return every merged group (key = merged id 1 << 32
-    | merged id 2, long sum, double sum) for the per-group comparison with the GPU result."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as O
-    lib = ctypes.CDLL(os.path.join(REPO, "oracle", "libdruid_cpu.so"))
-    lib.cpu_groupby2.restype = ctypes.c_int64
-    vp = ctypes.c_void_p
-    lib.cpu_groupby2.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
-                                 ctypes.c_char_p, ctypes.c_char_p, vp, vp, ctypes.c_int32,
-                                 ctypes.c_int, ctypes.POINTER(ctypes.c_double), vp, vp, vp, vp,
-                                 ctypes.POINTER(ctypes.c_double)]
-    segs = [O.OracleSegment(p) for p in paths]
-    d1, d2 = query.dimensions
-    maps, merged_dicts = [], []
-    for dim in (d1, d2):
-        dicts = [s.dictionary(dim) for s in segs]
-        merged = sorted(set().union(*map(set, dicts)), key=lambda v: (v is not None, (v or "").encode("utf-16-be")))
-        index = {v: i for i, v in enumerate(merged)}
-        maps.append(([np.array([index[v] for v in dd], dtype=np.int32) for dd in dicts], len(merged)))
-        merged_dicts.append(merged)
-    (m1, card1), (m2, _) = maps
-    ptr1 = (vp * len(segs))(*[a.ctypes.data for a in m1])
-    ptr2 = (vp * len(segs))(*[a.ctypes.data for a in m2])
-    lib.or_open.restype = vp
-    lib.or_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
-    lib.or_close.argtypes = [vp]
-    err = ctypes.create_string_buffer(512)
-    hs = [lib.or_open(p.encode(), err, 512) for p in paths]  # the engine library's own segment readers
-    if not all(hs):
-        raise IOError(err.value.decode())
-    handles = (vp * len(segs))(*hs)
-    sums = (ctypes.c_double * 3)()
-    rows = sum(s.num_rows for s in segs)
-    out = None
-    if want_groups:
-        out = {"key": np.empty(rows, np.uint64), "lsum": np.empty(rows, np.int64), "dsum": np.empty(rows, np.float64)}
-    ls, ds = query.aggregations[0].fieldName, query.aggregations[1].fieldName
-    secs = ctypes.c_double()
-    t0 = time.perf_counter()
-    ng = lib.cpu_groupby2(handles, len(segs), d1.encode(), d2.encode(), ls.encode(), ds.encode(), ptr1, ptr2, card1,
-                          threads, sums, out["key"].ctypes.data if out else None, None,
-                          out["lsum"].ctypes.data if out else None, out["dsum"].ctypes.data if out else None,
-                          ctypes.byref(secs))
-    if ng < 0:
-        raise RuntimeError("cpu_groupby2 failed")
-    el = secs.value if secs.value > 0 else time.perf_counter() - t0
-    for s, h in zip(segs, hs):
-        s.close()
-        lib.or_close(h)
-    quota = _cpu_quota()
-    res = {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
-           "sample": f"the whole step workload: {len(paths)} segments x {rows // len(paths)} rows, GroupByV2 "
-                     f"{d1} x {d2} longSum+doubleSum -> {ng} merged groups in {el:.2f} s "
-                     f"(oracle/cpu_engine.c + druid_oracle.c, C -O3 -march=native, {threads} threads over 1M-row "
-                     f"chunks, LZ4 decoded per block inside the timing)",
-           "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cores": threads,
-           "cgroup_quota_cores": quota, "groups": int(ng)}
-    if out is not None:
-        for k in out:
-            out[k] = out[k][:ng]
-        res["_groups"] = out
-        res["_dicts"] = merged_dicts
-    return res
+    GPU engine caches them too). want_groups: also return every merged group (key = (bucket index x
+    card1 + merged id 1) << 32 | merged id 2, long sum, double sum) for the per-group comparison."""
+    cs = _CpuSegments(paths)
+    try:
+        d1, d2 = query.dimensions
+        (merged1, m1), (merged2, m2) = cs.merged(d1), cs.merged(d2)
+        card1 = len(merged1)
+        ptr1 = (ctypes.c_void_p * len(paths))(*[a.ctypes.data for a in m1])
+        ptr2 = (ctypes.c_void_p * len(paths))(*[a.ctypes.data for a in m2])
+        _, _, org, per, b0, nb = _query_buckets(query, cs.osegs)
+        sums = (ctypes.c_double * 3)()
+        rows = cs.rows
+        out = None
+        if want_groups:
+            out = {"key": np.empty(rows, np.uint64), "lsum": np.empty(rows, np.int64), "dsum": np.empty(rows, np.float64)}
+        ls, ds = query.aggregations[0].fieldName, query.aggregations[1].fieldName
+        secs = ctypes.c_double()
+        ng = cs.lib.cpu_groupby2(cs.handles, len(paths), d1.encode(), d2.encode(), ls.encode(), ds.encode(), ptr1, ptr2,
+                                 card1, threads, org, per, b0, nb, sums, out["key"].ctypes.data if out else None, None,
+                                 out["lsum"].ctypes.data if out else None, out["dsum"].ctypes.data if out else None,
+                                 ctypes.byref(secs))
+        if ng < 0:
+            raise RuntimeError("cpu_groupby2 failed")
+        el = secs.value
+        gran = "ALL" if not per else f"{per} ms buckets"
+        res = _baseline_line(rows / el, threads, "port",
+                             f"the whole step workload: {len(paths)} segments x {rows // len(paths)} rows, GroupByV2 "
+                             f"{d1} x {d2} ({gran}) longSum+doubleSum -> {ng} merged groups in {el:.2f} s "
+                             f"(oracle/cpu_engine.c + druid_oracle.c, C -O3 -march=native, {threads} threads over 1M-row "
+                             f"chunks, LZ4 decoded per block inside the timing)",
+                             {"affinity_cores": len(os.sched_getaffinity(0)), "groups": int(ng)})
+        if out is not None:
+            for k in out:
+                out[k] = out[k][:ng]
+            res["_groups"] = out
+            res["_dicts"] = [merged1, merged2]
+            res["_buckets"] = (org, per, b0, card1)
+        return res
+    finally:
+        cs.close()
 
 
 def compare_groups(part, dicts, cpu):
@@ -254,7 +482,11 @@ def compare_groups(part, dicts, cpu):
     if not (out["groups_equal"] and out["dicts_equal"]):
         out["per_group_equal"] = False
         return out
-    keys = (part.codes[0].astype(np.uint64) << np.uint64(32)) | part.codes[1].astype(np.uint64)
+    org, per, b0, card1 = cpu["_buckets"]
+    hi = part.codes[0].astype(np.uint64)
+    if per:
+        hi = ((part.times.astype(np.int64) - org) // per - b0).astype(np.uint64) * np.uint64(card1) + hi
+    keys = (hi << np.uint64(32)) | part.codes[1].astype(np.uint64)
     out["keys_equal"] = bool(np.array_equal(keys, g["key"]))
     out["long_sums_equal"] = bool(np.array_equal(np.asarray(part.aggs[0], dtype=np.int64), g["lsum"]))
     a, b = np.asarray(part.aggs[1], dtype=np.float64), g["dsum"]
@@ -425,19 +657,33 @@ def main():
         phases["decode_payload_side"] = per_step("decode_side_ms")
         kernels["decode_payload_side"] = (dk + " (payload, side stream)", bytes_side, 1, phases["decode_payload_side"])
     if per_step("lz4_general_ms") > 0:
-        # the general LZ4 decoder alone (token-dense blocks; main and side stream): its own HIP-event span
-        # per stream, its blocks' stored bytes; a "launch" here is one kernel launch, as rocprofv3 counts
+        # the general LZ4 decoder alone (token-dense blocks of 8-byte value runs; main and side stream): its
+        # own HIP-event span per stream, its blocks' stored bytes; a "launch" is one kernel launch, as
+        # rocprofv3 counts
         phases["lz4_general"] = per_step("lz4_general_ms")
         kernels["lz4_general"] = ("k_lz4_decode", per_step("lz4_general_bytes"),
                                   max(per_step("lz4_general_launches"), 1.0), phases["lz4_general"])
+    if per_step("lz4_dense_ms") > 0:
+        # the dense LZ4 decoder (token-dense blocks of scattered short copies), the same way
+        phases["lz4_dense"] = per_step("lz4_dense_ms")
+        kernels["lz4_dense"] = ("k_lz4_dense", per_step("lz4_dense_bytes"), max(per_step("lz4_dense_launches"), 1.0),
+                                phases["lz4_dense"])
     if isinstance(query, Q.GroupByQuery):
-        phases.update({"keygen": per_step("keygen_ms"), "sort": per_step("sort_ms"), "reduce": per_step("reduce_ms")})
+        phases.update({"keygen": per_step("keygen_ms"), "sort": per_step("sort_ms"), "reduce": per_step("reduce_ms"),
+                       "reduce_kernels": per_step("reduce_kernel_ms")})
         passes = max(1, int(round(per_step("sort_passes"))))
         n_sel = selected_local
-        # one radix pass: the histogram reads every packed [key | row ref] word, the scatter reads and
-        # writes it once: 3 x 8 B per selected row
-        kernels["sort"] = ("k_rs_hist+k_rs_binscan+k_rs_scatter", 24.0 * n_sel, passes, phases["sort"])
-        kernels["keygen"] = ("k_gb_count+k_gb_keygen", n_sel * (3 + 3 + 12), 1, phases["keygen"])
+        groups = per_step("groups")
+        # the first pass's digit totals read every packed [key | row ref] word once (k_rs_hist0); every
+        # one-sweep pass reads and writes it once (k_rs_scatter): 8 + 16 x passes B per selected row
+        kernels["sort"] = ("k_rs_hist0+k_rs_scatter", n_sel * (8.0 + 16.0 * passes), passes + 1, phases["sort"])
+        # keygen: the two 3-byte ids of the row in, its 8-byte sort word out
+        kernels["keygen"] = ("k_gb_keygen", n_sel * (3 + 3 + 8), 1, phases["keygen"])
+        # reduce (its kernels alone): the sorted words and the payload records in, per group its key and
+        # (1 + aggregators) 8-byte slots out
+        pw = len(query.aggregations)
+        kernels["reduce"] = ("k_gb_reduce+k_gb_carry+k_gb_open_finalize", n_sel * (8.0 + 8.0 * pw) + groups * 8.0 * (2 + pw),
+                             1, phases["reduce_kernels"])
     elif phases["aggregate"] > 0:
         per_row = {"topn": 3 + 8 + 8}.get(args.config, 8)
         kernels["aggregate"] = ("k_topn_bin_*" if args.config.startswith("topn") else "k_scan_agg",
@@ -448,7 +694,8 @@ def main():
                              per_step("bitmap_bytes") or None, 1, phases["bitmap"])
     # the dominant kernel: the longest single-kernel span (phases that group several kernels, like the
     # decode phase or the side-stream payload decode, are reported in phases_ms)
-    single = {k: v for k, v in kernels.items() if k in ("lz4_general", "aggregate", "bitmap", "sort", "keygen")}
+    single = {k: v for k, v in kernels.items()
+              if k in ("lz4_general", "lz4_dense", "aggregate", "bitmap", "sort", "keygen", "reduce")}
     dom = max(single or kernels, key=lambda k: (single or kernels)[k][3]) if kernels else None
     roofline = None
     if dom is not None:
@@ -507,19 +754,42 @@ def main():
                                  "sorted": bool(gt.all())}
         del gt, eq
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if args.config == "groupby":
-            cb = cpu_baseline_groupby(paths, query, _cpu_threads(), want_groups=part is not None)
+        # the CPU baseline on the box's usable cores, and the result of the benched query checked
+        # against it (or against the oracle) after the timed loop
+        threads = _cpu_threads()
+        if isinstance(query, Q.GroupByQuery):
+            cb = cpu_baseline_groupby(paths, query, threads, want_groups=part is not None)
             if part is not None:
                 rc = line["result_checks"]
                 rc.update(compare_groups(part, dicts, cb))
                 rc["cpu_long_sum"] = int(np.sum(cb["_groups"]["lsum"]))
                 rc["cpu_long_sum_equal"] = rc["cpu_long_sum"] == rc["long_sum"]
-            cb.pop("_groups", None)
-            cb.pop("_dicts", None)
+            for k in ("_groups", "_dicts", "_buckets"):
+                cb.pop(k, None)
             line["cpu_baseline"] = cb
-        else:
+        elif isinstance(query, Q.TimeseriesQuery):
+            gpu_res = step(R.RunStats())
+            cb, cres = cpu_baseline_timeseries(paths, query, threads)
+            line["cpu_baseline"] = cb
+            line["result_checks"] = check_timeseries(gpu_res, cres, query)
+        elif isinstance(query, Q.TopNQuery) and query.metric.type == "numeric":
+            gpu_res = step(R.RunStats())
+            cb, cres = cpu_baseline_topn(paths, query, threads)
+            line["cpu_baseline"] = cb
+            line["result_checks"] = check_topn(gpu_res, cres, query)
+        else:  # dimension-ordered topN: the oracle (one thread) is both the baseline and the check
+            gpu_res = step(R.RunStats())
             line["cpu_baseline"] = cpu_baseline_oracle(query, paths[0], rows_per, args.cpu_seconds,
                                                        selected_local / scanned_local if scanned_local else 1.0)
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle as O
+            osegs = [O.OracleSegment(p) for p in paths]
+            exp = O.run(query, osegs)
+            for sg in osegs:
+                sg.close()
+            same = [[r[query.dimension] for r in x.value] for x in gpu_res] == [[r[query.dimension] for r in x.value] for x in exp]
+            line["result_checks"] = {"entries": sum(len(x.value) for x in gpu_res), "values_equal_oracle": same,
+                                     "results_equal_oracle": same and [x.value for x in gpu_res] == [x.value for x in exp]}
     del part
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -1268,6 +1268,19 @@ __device__ __forceinline__ uint32_t bits_of(int a, int b) {  // positions [a, b)
   return (hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
 }
 
+// OR the low `len` (<= 8) bytes of w into the zero-initialised image at byte position x: at most three
+// dword ORs (bytes of other runs in the same dwords are disjoint)
+__device__ __forceinline__ void img_or(uint32_t* s_img32, int x, int len, uint64_t w) {
+  if (len < 8) w &= (1ull << (8 * len)) - 1ull;
+  const int sh = (x & 3) * 8, q = x >> 2;
+  const uint32_t d0 = (uint32_t)(w << sh);
+  const uint32_t d1 = (uint32_t)((sh ? (w >> (32 - sh)) : (w >> 32)));
+  const uint32_t d2 = sh ? (uint32_t)(w >> (64 - sh)) : 0u;
+  if (d0) atomicOr(&s_img32[q], d0);
+  if (d1) atomicOr(&s_img32[q + 1], d1);
+  if (d2) atomicOr(&s_img32[q + 2], d2);
+}
+
 // the residue classes mod 8 of positions [a, a + k)
 __device__ __forceinline__ uint32_t classes_of(int a, int k) {
   if (k >= 8) return 0xFFu;
@@ -1314,6 +1327,8 @@ __global__ __launch_bounds__(kDnThreads) void k_lz4_dense(const Lz4Job* __restri
       s_nlj = 0;
     }
     for (int i = tid; i < kDnResWords; i += kDnThreads) s_res[i] = 0;
+    uint4* img4 = reinterpret_cast<uint4*>(s_img32);
+    for (int i = tid; i < kBlockBytes / 16; i += kDnThreads) img4[i] = make_uint4(0, 0, 0, 0);  // (bytes are ORed in)
   }
   __syncthreads();
   LZ_STAMP(1);
@@ -1390,9 +1405,7 @@ __global__ __launch_bounds__(kDnThreads) void k_lz4_dense(const Lz4Job* __restri
         const int q = (lit + k0) >> 2, sh = (lit + k0) & 3;
         const uint32_t a0 = s_in32[q], a1 = s_in32[q + 1], a2 = s_in32[q + 2];
         const uint32_t v0 = __builtin_amdgcn_alignbyte(a1, a0, sh), v1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k0 + k < L) s_img[o + k0 + k] = (uint8_t)((k < 4 ? v0 : v1) >> (8 * (k & 3)));
+        img_or(s_img32, o + k0, min(8, L - k0), (uint64_t)v0 | ((uint64_t)v1 << 32));
       }
       res_set(s_res, o, xm);
     }
@@ -1410,12 +1423,13 @@ __global__ __launch_bounds__(kDnThreads) void k_lz4_dense(const Lz4Job* __restri
     const int nlj = s_nlj;
     for (int j = 0; j < nlj; ++j) {
       const int o = (int)s_aux[3 * j], lit = (int)s_aux[3 * j + 1], L = (int)s_aux[3 * j + 2];
-      for (int i = tid; i < L; i += kDnThreads) s_img[o + i] = s_in[lit + i];
+      for (int i = tid; i < L; i += kDnThreads) atomicOr(&s_img32[(o + i) >> 2], (uint32_t)s_in[lit + i] << (8 * ((o + i) & 3)));
       for (int w = (o >> 5) + tid; w <= ((o + L - 1) >> 5); w += kDnThreads) res_set(s_res, max(o, w << 5), min(o + L, (w + 1) << 5));
     }
     __syncthreads();
   }
   LZ_STAMP(3);
+  LZ_STAMP(4);
   int rounds = 0;
   // ---- 3'. rounds: each match whose source bytes (its first period) are resolved copies them;
   // a thread's reads for all its matches go out together ----
@@ -1485,13 +1499,11 @@ __global__ __launch_bounds__(kDnThreads) void k_lz4_dense(const Lz4Job* __restri
             const int sh = a & 3;
             const uint32_t v0 = __builtin_amdgcn_alignbyte(sw[s][1], sw[s][0], sh);
             const uint32_t v1 = __builtin_amdgcn_alignbyte(sw[s][2], sw[s][1], sh);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if (k < M) s_img[xm + k] = (uint8_t)((k < 4 ? v0 : v1) >> (8 * (k & 3)));
+            img_or(s_img32, xm, M, (uint64_t)v0 | ((uint64_t)v1 << 32));
           } else {
 #pragma unroll 1
             for (int k = 0, r = 0; k < M; ++k) {  // LZ4 overlap: byte k copies the first period
-              s_img[xm + k] = s_img[a + r];
+              atomicOr(&s_img32[(xm + k) >> 2], (uint32_t)s_img[a + r] << (8 * ((xm + k) & 3)));
               if (++r == d) r = 0;
             }
           }
