@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <chrono>
 #include <thread>
+#include <functional>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -3915,6 +3916,19 @@ int dg_groupby_merge_devices(dg_result* const* parts, int32_t n_parts, dg_contex
     if (!targets[t]) return set_error(DG_ERR_ARG, "null target %d", t);
     outs[t] = nullptr;
   }
+  // every error return after the targets' merges have started releases what they produced
+  struct OutsGuard {
+    dg_result** outs;
+    int32_t n;
+    bool ok = false;
+    ~OutsGuard() {
+      if (ok) return;
+      for (int32_t t = 0; t < n; ++t) {
+        dg_result_release(outs[t]);
+        outs[t] = nullptr;
+      }
+    }
+  } guard{outs, n_targets};
   const dg_result* r0 = parts[0];
   for (int32_t p = 0; p < n_parts; ++p) {
     const dg_result* r = parts[p];
@@ -3961,20 +3975,46 @@ int dg_groupby_merge_devices(dg_result* const* parts, int32_t n_parts, dg_contex
   int32_t kbits = 0;
   int rc = dg_keyspace_bits(&ks, &kbits);
   if (rc) return rc;
+  // Work items of the phases below run concurrently, one host thread each (ChainedExecutionQueryRunner
+  // runs the segment runners on the processing pool; here every device's work goes out at once and
+  // each context's own mutex serialises calls that share a device). An item's error (code and the
+  // thread's dg_last_error text) is handed back to the calling thread.
+  struct ItemErr {
+    int rc = DG_OK;
+    std::string msg;
+  };
+  auto run_items = [](int n, const std::function<int(int)>& fn, std::vector<ItemErr>* errs) -> int {
+    errs->assign(n, ItemErr());
+    std::vector<std::thread> th;
+    for (int i = 1; i < n; ++i)
+      th.emplace_back([&, i] {
+        (*errs)[i].rc = fn(i);
+        if ((*errs)[i].rc) (*errs)[i].msg = dg_last_error();
+      });
+    if (n > 0) {
+      (*errs)[0].rc = fn(0);
+      if ((*errs)[0].rc) (*errs)[0].msg = dg_last_error();
+    }
+    for (auto& x : th) x.join();
+    for (auto& e : *errs)
+      if (e.rc) return set_error(e.rc, "%s", e.msg.c_str());
+    return DG_OK;
+  };
+  std::vector<ItemErr> errs;
   // every part re-keyed into the key space on its own device
   std::vector<CtxBlock> xkeys(n_parts), xslots(n_parts);
   std::vector<int64_t> np(n_parts);
-  for (int32_t p = 0; p < n_parts; ++p) {
+  rc = run_items(n_parts, [&](int p) -> int {
     dg_result* r = parts[p];
     np[p] = r->ngroups;
-    if (!np[p]) continue;
+    if (!np[p]) return DG_OK;
     if (!xkeys[p].take(r->ctx, (size_t)np[p] * 8) || !xslots[p].take(r->ctx, (size_t)np[p] * rec * 8))
       return set_error(DG_ERR_OOM, "export buffers of part %d (%lld groups)", p, (long long)np[p]);
     std::vector<const int32_t*> mp(nd);
     for (int d = 0; d < nd; ++d) mp[d] = maps[d][p].data();
-    rc = dg_result_export(r, &ks, mp.data(), static_cast<uint64_t*>(xkeys[p].p), static_cast<uint64_t*>(xslots[p].p));
-    if (rc) return rc;
-  }
+    return dg_result_export(r, &ks, mp.data(), static_cast<uint64_t*>(xkeys[p].p), static_cast<uint64_t*>(xslots[p].p));
+  }, &errs);
+  if (rc) return rc;
   // key ranges: n_targets - 1 splitters from evenly spaced samples of every part (weighted by the
   // part's size), identical cuts on every part, so equal keys meet on one target
   std::vector<uint64_t> splits;
@@ -4008,19 +4048,18 @@ int dg_groupby_merge_devices(dg_result* const* parts, int32_t n_parts, dg_contex
     }
   }
   std::vector<std::vector<int64_t>> cut(n_parts, std::vector<int64_t>(n_targets + 1, 0));
-  for (int32_t p = 0; p < n_parts; ++p) {
+  rc = run_items(n_parts, [&](int p) -> int {
     cut[p][n_targets] = np[p];
-    if (n_targets > 1 && np[p]) {
-      rc = dg_keys_partition(reinterpret_cast<dg_context*>(parts[p]->ctx), static_cast<uint64_t*>(xkeys[p].p), np[p],
-                             splits.data(), n_targets - 1, cut[p].data() + 1);
-      if (rc) return rc;
-    }
-  }
-  // every range moves to its target (peer copies over xGMI; a device copy on the same device) and
-  // is merged there in part order (equal keys combine in that order)
-  dg_metrics tot;
-  memset(&tot, 0, sizeof tot);
-  for (int32_t t = 0; t < n_targets; ++t) {
+    if (n_targets > 1 && np[p])
+      return dg_keys_partition(reinterpret_cast<dg_context*>(parts[p]->ctx), static_cast<uint64_t*>(xkeys[p].p), np[p],
+                               splits.data(), n_targets - 1, cut[p].data() + 1);
+    return DG_OK;
+  }, &errs);
+  if (rc) return rc;
+  // every range moves to its target (peer copies over xGMI; a device copy on the same device) and is
+  // merged there in part order (equal keys combine in that order); the targets work concurrently
+  std::vector<dg_metrics> tm(n_targets);
+  rc = run_items(n_targets, [&](int t) -> int {
     Context* tc = reinterpret_cast<Context*>(targets[t]);
     int64_t n = 0;
     for (int32_t p = 0; p < n_parts; ++p) n += cut[p][t + 1] - cut[p][t];
@@ -4039,7 +4078,8 @@ int dg_groupby_merge_devices(dg_result* const* parts, int32_t n_parts, dg_contex
           int can = 0;
           if (hipDeviceCanAccessPeer(&can, tc->device, sdev) == hipSuccess && can) {
             hipError_t e = hipDeviceEnablePeerAccess(sdev, 0);
-            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return set_error(DG_ERR_DEVICE, "peer access %d -> %d", tc->device, sdev);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+              return set_error(DG_ERR_DEVICE, "peer access %d -> %d", tc->device, sdev);
             (void)hipGetLastError();
           }
         }
@@ -4051,27 +4091,27 @@ int dg_groupby_merge_devices(dg_result* const* parts, int32_t n_parts, dg_contex
       }
       DG_HIP(hipStreamSynchronize(tc->stream));
     }
-    dg_metrics m;
-    rc = dg_merge(targets[t], &ks, static_cast<uint64_t*>(rk.p), static_cast<uint64_t*>(rs.p), n, &outs[t], &m);
-    if (rc) {
-      for (int32_t u = 0; u < t; ++u) {
-        dg_result_release(outs[u]);
-        outs[u] = nullptr;
-      }
-      return rc;
-    }
+    const int mrc = dg_merge(targets[t], &ks, static_cast<uint64_t*>(rk.p), static_cast<uint64_t*>(rs.p), n, &outs[t], &tm[t]);
+    if (mrc) return mrc;
     outs[t]->dicts = udicts;  // the union dictionaries: the merged result fetches like a groupBy result
     outs[t]->bounds = r0->bounds;
-    tot.sort_ms += m.sort_ms;
-    tot.reduce_ms += m.reduce_ms;
-    tot.aggregate_ms += m.aggregate_ms;
-    tot.selected_rows += m.selected_rows;
-    tot.groups += m.groups;
-    tot.sort_passes = m.sort_passes;
-    tot.key_bits = m.key_bits;
+    return DG_OK;
+  }, &errs);
+  if (rc) return rc;
+  dg_metrics tot;
+  memset(&tot, 0, sizeof tot);
+  for (int32_t t = 0; t < n_targets; ++t) {
+    tot.sort_ms += tm[t].sort_ms;
+    tot.reduce_ms += tm[t].reduce_ms;
+    tot.aggregate_ms += tm[t].aggregate_ms;
+    tot.selected_rows += tm[t].selected_rows;
+    tot.groups += tm[t].groups;
+    tot.sort_passes = tm[t].sort_passes;
+    tot.key_bits = tm[t].key_bits;
   }
   tot.total_ms = ms_since(t0);
   if (metrics) *metrics = tot;
+  guard.ok = true;
   return DG_OK;
 }
 

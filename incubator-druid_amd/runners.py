@@ -20,6 +20,7 @@ per-segment runners. Cross-device / cross-rank merging is in distributed.py.
 from __future__ import annotations
 
 import ctypes
+import time
 import dataclasses
 import heapq
 import math
@@ -74,8 +75,11 @@ class RunStats:
     def __init__(self):
         self.calls: List[Dict] = []
 
-    def add(self, m: N.dg_metrics):
-        self.calls.append(m.as_dict())
+    def add(self, m: N.dg_metrics, span=None):
+        d = m.as_dict()
+        if span is not None:  # host wall clock (time.perf_counter) at the call's start and end
+            d["t_start"], d["t_end"] = span
+        self.calls.append(d)
 
     def total(self, key):
         return sum(c[key] for c in self.calls)
@@ -753,10 +757,11 @@ def groupby_run(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
     g.n_dims = nd
     res = ctypes.c_void_p()
     m = N.dg_metrics()
+    t0 = time.perf_counter()
     N.check(N.lib().dg_groupby_run(_handles(segments), len(segments), ctypes.byref(scan), ctypes.byref(g),
                                    ctypes.byref(res), ctypes.byref(m)))
     if stats is not None:
-        stats.add(m)
+        stats.add(m, (t0, time.perf_counter()))
     out = GroupByResult(res, query)
     if limit_push_down:
         out.apply_limit_push_down()
@@ -776,17 +781,33 @@ def groupby_per_device(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
     return out
 
 
+def _per_device_concurrently(groups, fn):
+    """fn(segment indices of one device) for every device at once, one host thread each, results in
+    device order (ChainedExecutionQueryRunner submits every runner to the processing pool; the native
+    calls release the GIL, so the devices' kernels are in flight together)."""
+    items = list(groups.values())
+    if len(items) == 1:
+        return [fn(items[0])]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=len(items)) as ex:
+        futs = [ex.submit(fn, idx) for idx in items]
+        return [f.result() for f in futs]
+
+
 def groupby_merge_devices(segments: Sequence[GpuSegment], query: Q.GroupByQuery, stats: Optional[RunStats] = None,
-                          targets: Optional[Sequence] = None) -> "GroupByResult | List[GroupByResult]":
-    """mergeRunners over segments of several devices in one process: one dg_groupby_run per device,
-    then dg_groupby_merge_devices moves key ranges between the devices itself (peer copies) and
-    merges them there. targets: contexts owning the key ranges (default: the first device's, one
-    result); with targets given, the list of per-target results in key order."""
+                          targets: Optional[Sequence] = None) -> "List[GroupByResult]":
+    """mergeRunners over segments of several devices in one process: one dg_groupby_run per device, all
+    devices at once, then dg_groupby_merge_devices moves key ranges between the devices itself (peer
+    copies) and merges them there, every target concurrently. targets: the contexts owning the key
+    ranges (default: every participating device's context, so no device funnels the others' groups);
+    returns the per-target results in key order."""
+    groups = _group_by_device(segments)
     parts = []
     try:
-        for _, idx in _group_by_device(segments).items():
-            parts.append(groupby_run([segments[i] for i in idx], query, stats))
-        ctxs = [segments[0].context] if targets is None else list(targets)
+        def one(idx):
+            return groupby_run([segments[i] for i in idx], query, stats)
+        parts = _per_device_concurrently(groups, one)
+        ctxs = [segments[idx[0]].context for idx in groups.values()] if targets is None else list(targets)
         outs = (ctypes.c_void_p * len(ctxs))()
         hp = (ctypes.c_void_p * len(parts))(*[p.handle.value for p in parts])
         ht = (ctypes.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
@@ -797,8 +818,7 @@ def groupby_merge_devices(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
     finally:
         for p in parts:
             p.release()
-    res = [GroupByResult(ctypes.c_void_p(o), query) for o in outs]
-    return res[0] if targets is None else res
+    return [GroupByResult(ctypes.c_void_p(o), query) for o in outs]
 
 
 def groupby_per_segment(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
@@ -1201,10 +1221,12 @@ class GroupByQueryRunnerFactory(TimeseriesQueryRunnerFactory):
             return self.toolchest.merge(query, groupby_per_device(segments, query, stats))
         res = groupby_merge_devices(segments, query, stats)
         try:
-            res.apply_limit_push_down()
-            return self.toolchest.merge(query, [res.fetch()])
+            for r in res:  # (each key range keeps its first `limit` groups; the toolchest re-limits)
+                r.apply_limit_push_down()
+            return self.toolchest.merge(query, [r.fetch() for r in res])
         finally:
-            res.release()
+            for r in res:
+                r.release()
 
 
 FACTORIES = {Q.TimeseriesQuery: TimeseriesQueryRunnerFactory(), Q.TopNQuery: TopNQueryRunnerFactory(),

@@ -737,7 +737,7 @@ int cpu_topn(void** segs, int nseg, int nthreads, const int32_t* prog, int nprog
   c.nlist = (int32_t*)calloc((size_t)(nseg > 0 ? nseg : 1), sizeof(int32_t));
   run_threads(nthreads < nseg ? nthreads : (nseg > 0 ? nseg : 1), tn_seg_worker, &c);
   /* TopNBinaryFn fold in segment order: combine equal values, keep the query's threshold */
-  tn_ent* acc = (tn_ent*)malloc(sizeof(tn_ent) * (size_t)(c.seg_threshold + threshold + 1));
+  tn_ent* acc = (tn_ent*)malloc(sizeof(tn_ent) * (size_t)(2 * c.seg_threshold + threshold + 1));  /* (a list + the next) */
   int32_t na = 0;
   for (int s = 0; s < nseg && !c.err; ++s) {
     tn_ent* l = c.lists[s];

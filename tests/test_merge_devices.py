@@ -154,3 +154,40 @@ def test_merge_devices_granularity_and_filters(Q, O, two_contexts):
         q = Q.TimeseriesQuery(intervals=IV, granularity=gran, aggregations=aggs + [Q.float_sum("fs", "sumFloatNormal")],
                               filter=Q.NotDimFilter(Q.SelectorDimFilter("dimUniform", "3")))
         assert_results(q, R.run_query(q, g), O.run(q, o))
+
+
+@pytest.mark.gpu
+def test_merge_devices_runs_concurrently_and_spreads_targets(Q, O, two_contexts):
+    """The in-process mergeRunners issues every context's dg_groupby_run at once (their host call spans
+    overlap: both were in flight on the GPU together) and by default every participating context owns a
+    key range of the merged result (nothing funnels into the first device)."""
+    R = importlib.import_module("incubator-druid_amd.runners")
+    (ca, cb), g, o = two_contexts
+    aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal")]
+    q = Q.GroupByQuery(intervals=IV, dimensions=["dimUniform", "dimHyperUnique"], aggregations=aggs)
+    exp = O.run(q, o)
+    overlapped = False
+    for _ in range(3):  # (thread start-up order can serialise one attempt)
+        stats = R.RunStats()
+        parts = R.groupby_merge_devices(g, q, stats)
+        try:
+            runs = [c for c in stats.calls if "t_start" in c]
+            assert len(runs) == 2 and len(parts) == 2
+            overlapped |= max(c["t_start"] for c in runs) < min(c["t_end"] for c in runs)
+            assert all(p.groups > 300_000 for p in parts)
+            got = [p.fetch() for p in parts]
+        finally:
+            for p in parts:
+                p.release()
+        keys = [tuple(r.event[d] for d in q.dimensions) for r in exp]
+        assert [k for p in got for k in zip(*[list(c) for c in p.dims])] == keys
+        for i, a in enumerate(aggs):
+            col = np.concatenate([p.aggs[i] for p in got])
+            e = np.array([r.event[a.name] for r in exp])
+            if a.type == "doubleSum":
+                assert np.allclose(col, e, rtol=TOL["double"], atol=0)
+            else:
+                assert np.array_equal(col, e.astype(col.dtype))
+        if overlapped:
+            break
+    assert overlapped

@@ -198,3 +198,38 @@ def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode):
             assert np.array_equal(col.astype(np.float32), e.astype(np.float32))
         else:
             assert np.array_equal(col, e.astype(col.dtype)), a.name
+
+
+def test_cfg1_selector_timeseries_on_lz4_hc_segments(R, Q, O, cfg2):
+    """BASELINE configs[0]'s exact query (TimeseriesBenchmark basic: SelectorDimFilter dimSequential =
+    '399', count + longSum(sumLongSequential) + doubleSum(sumFloatNormal), ALL granularity) on the
+    750k-row LZ4-HC segments of config 2, one by one and merged."""
+    g, o = cfg2
+    q = Q.TimeseriesQuery(intervals=IV, filter=Q.SelectorDimFilter("dimSequential", "399"),
+                          aggregations=[Q.count("rows"), Q.long_sum("sumLongSequential"),
+                                        Q.double_sum("sumFloatNormal")])
+    for s_g, s_o in zip(g, o):
+        got, exp = R.run_query(q, [s_g]), O.run(q, [s_o])
+        assert exp[0].value["rows"] == 750  # every 1,000th row
+        assert_results(q, got, exp)
+    assert_results(q, R.run_query(q, g), O.run(q, o))
+
+
+@pytest.mark.parametrize("bitmap", ["concise", "roaring"])
+def test_cfg4_compound_filter_on_a_full_size_segment(R, Q, O, S, DG, tmp_path_factory, bitmap):
+    """BASELINE configs[3]'s compound filter on one GPU's full 12.5M-row share (one segment, the
+    filter's dimensions), bit-exact against the oracle's row selection, and its timeseries count."""
+    base = tmp_path_factory.mktemp(f"cfg4full_{bitmap}")
+    p = DG.write_basic_segment(str(base / "seg"), 12_500_000, seed=9999, bitmap=bitmap, lz4_mode="hc",
+                               dims=["dimSequential", "dimZipf", "dimUniform"], metrics=["rows"])
+    gs, os_ = S.GpuSegment(p), O.OracleSegment(p)
+    f = Q.OrDimFilter([Q.AndDimFilter([Q.BoundDimFilter("dimSequential", "100", "200"),
+                                       Q.InDimFilter("dimZipf", ["1", "2", "3"])]),
+                       Q.SelectorDimFilter("dimUniform", "199"),
+                       Q.NotDimFilter(Q.SelectorDimFilter("dimZipf", "7"))])
+    words, cnt = gs.filter_bitmap(f.optimize(), Q)
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:gs.num_rows].astype(bool)
+    exp = O.filter_mask(os_, f.optimize())
+    assert cnt == int(exp.sum()) and np.array_equal(bits, exp)
+    q = Q.TimeseriesQuery(intervals=IV, aggregations=[Q.count("rows")], filter=f)
+    assert_results(q, R.run_query(q, [gs]), O.run(q, [os_]))
