@@ -1764,7 +1764,8 @@ static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bi
   sb->n = dev_take<uint32_t>(cs, 4);
   sb->lb_status = dev_take<uint64_t>(cs, (size_t)kMaxBins * sb->ntiles_sort);
   // per-pass digit totals + tile counters (radix_passes)
-  sb->bin_total = dev_take<uint32_t>(cs, (size_t)kMaxBins * kRsMaxPasses + kRsMaxPasses);
+  // + one tile counter for the groupBy reduce's look-back
+  sb->bin_total = dev_take<uint32_t>(cs, (size_t)kMaxBins * kRsMaxPasses + kRsMaxPasses + 1);
   sb->run_cnt = dev_take<uint32_t>(cs, (size_t)sb->ntiles_sort);
   if (!sb->tile_cnt || !sb->n || !sb->lb_status || !sb->bin_total || !sb->run_cnt) return set_error(DG_ERR_OOM, "sort tables");
   return DG_OK;
@@ -3341,17 +3342,13 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   hipEventRecord(ctx->ev[5], st);
   launch_radix_sort(&sb, key_bits, st);
   hipEventRecord(ctx->ev[6], st);
-  launch_run_heads(&sb, st);
-  DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));
-  rc = finish_call(cs, st);  // the result is sized by the group count
-  if (rc) return rc;
-  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
-  const int64_t nsel = h_n[0], ng = h_n[1];
+  // the result is laid out for the sort's capacity (>= the groups): the reduce counts the groups itself
+  // (look-back over tiles), so there is no host read-back between the sort and the reduce
+  const int64_t cap = std::max<int64_t>(sb.cap, 1);
   std::unique_ptr<dg_result> res(new dg_result());
   res->ctx = ctx;
   res->ndims = nd;
   res->naggs = na;
-  res->ngroups = ng;
   res->lay = lay;
   res->bucket0 = gb0;
   res->period = q->period_ms;
@@ -3359,14 +3356,14 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   res->universal = q->interval_start;  // GroupByStrategyV2.getUniversalTimestamp (ALL granularity)
   res->kinds.assign(plan.kind, plan.kind + na);
   res->dicts = md;
-  res->keys = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * 8));
-  res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)ng * rec * 8));
-  res->cap = ng;
-  if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "groupBy result of %lld groups", (long long)ng);
+  res->keys = static_cast<uint64_t*>(result_alloc(ctx, (size_t)cap * 8));
+  res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)cap * rec * 8));
+  res->cap = cap;
+  if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "groupBy result of %lld records", (long long)cap);
   bool reduce_timed = false;
-  if (ng > 0) {
+  {
     // run heads are only needed by the floatSum row-order pass
-    uint32_t* head_pos = has_float_sum(plan) ? dev_take<uint32_t>(cs, (size_t)ng + 16) : nullptr;
+    uint32_t* head_pos = has_float_sum(plan) ? dev_take<uint32_t>(cs, (size_t)cap + 16) : nullptr;
     const size_t nt = (size_t)sb.ntiles_sort;  // one carry / open group per tile
     int64_t* carry_g = dev_take<int64_t>(cs, (size_t)kRedWaves * nt);  // one carry / open slot per wave share of a tile
     int64_t* open_g = dev_take<int64_t>(cs, (size_t)kRedWaves * nt);
@@ -3376,14 +3373,17 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     if (side) DG_HIP(hipStreamWaitEvent(st, ctx->side_ev[2], 0));  // the payload is decoded
     hipEventRecord(ctx->ev[7], st);
     reduce_timed = true;
-    launch_gb_reduce(&sb, plan, res->keys, res->slots, ng, head_pos, carry_g, carry_slots, open_g, st);
+    launch_gb_reduce(&sb, plan, res->keys, res->slots, cap, head_pos, carry_g, carry_slots, open_g, st);
     for (int a = 0; a < na; ++a)
-      if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, ntiles, &sb, plan, a, head_pos, res->slots, ng, st);
+      if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, ntiles, &sb, plan, a, head_pos, res->slots, cap, st);
   }
   hipEventRecord(ctx->ev[4], st);
-  if (side) DG_HIP(hipStreamWaitEvent(st, ctx->side_ev[2], 0));  // (no groups: no reduce waited)
+  DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));  // selected rows, groups
   rc = finish_call(cs, st);
   if (rc) return rc;
+  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  const int64_t nsel = h_n[0], ng = h_n[1];
+  res->ngroups = ng;
   if (side) {
     float fs = 0;
     hipEventElapsedTime(&fs, ctx->side_ev[1], ctx->side_ev[2]);
@@ -3406,7 +3406,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   m.aggregate_ms = f3;
   m.keygen_ms = f4;
   m.sort_ms = f5;
-  m.reduce_ms = f6;  // includes the group-count read-back between the sort and the reduce
+  m.reduce_ms = f6;  // includes the wait for the side-stream payload decode
   if (reduce_timed) {
     float fr = 0;
     hipEventElapsedTime(&fr, ctx->ev[7], ctx->ev[4]);

@@ -690,8 +690,9 @@ constexpr int kRSPT = kSortTile / kRT;          // elements per lane
 template <bool REFS>
 __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
-                                                   int kshift, const uint32_t* __restrict__ n_ptr,
-                                                   const uint32_t* __restrict__ run_off, AggPlan plan,
+                                                   int kshift, uint32_t* __restrict__ n_ptr,
+                                                   uint64_t* __restrict__ status, uint32_t* __restrict__ tile_ctr,
+                                                   AggPlan plan,
                                                    uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_slots,
                                                    int64_t cap, uint32_t* __restrict__ head_pos,
                                                    int64_t* __restrict__ carry_g, uint64_t* __restrict__ carry_slots,
@@ -701,13 +702,22 @@ __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* 
   // crosses a share boundary is finished like one crossing a tile boundary: the share holding
   // its head writes it open (device encoding, listed in open_g), every later share's share goes to
   // that share's carry slot (k_gb_carry folds it in, k_gb_open_finalize finalizes).
+  // The groups before a tile are counted by decoupled look-back over the earlier tiles' run-head
+  // counts (tiles take their index from a counter as they start, so a tile only waits on running
+  // ones); the last tile publishes the group count (n_ptr[1]). No separate run-count pass over the
+  // keys, no host read-back before the reduce: the result is laid out for `cap` (>= groups) records.
   constexpr int kWSeg = kSortTile / kRedWaves;
   __shared__ uint64_t s_key[kSortTile + 2];  // [0] = element before the tile, [1 + x] = element x
   __shared__ uint32_t s_heads[kRedWaves];
-  const uint32_t n = *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  __shared__ int s_tile;
+  __shared__ int64_t s_gbase;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t wt = (int64_t)blockIdx.x * kRedWaves + wave;  // wave tile (carry / open slot)
+  if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
+  __syncthreads();
+  const int tile = s_tile;
+  const uint32_t n = n_ptr[0];
+  const int64_t base = (int64_t)tile * kSortTile;
+  const int64_t wt = (int64_t)tile * kRedWaves + wave;  // wave tile (carry / open slot)
   if (lane == 0) {
     carry_g[wt] = -1;
     open_g[wt] = -1;
@@ -766,7 +776,42 @@ __global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* 
   }
   if (lane == 0) s_heads[wave] = nh;
   __syncthreads();
-  int64_t G = run_off[blockIdx.x];  // groups with a head before my share
+  if (tid == 0) {  // look-back: the groups headed in earlier tiles
+    uint64_t cnt = 0;
+    for (int w = 0; w < kRedWaves; ++w) cnt += s_heads[w];
+    uint64_t excl = 0;
+    uint64_t* st = status + tile;
+    if (tile == 0) {
+      __hip_atomic_store(st, kLbPre | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(st, kLbAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      constexpr int kLb = 8;
+      for (int j = tile - 1; j >= 0;) {
+        uint64_t sv[kLb];
+#pragma unroll
+        for (int q = 0; q < kLb; ++q)
+          sv[q] = j - q >= 0 ? __hip_atomic_load(status + (j - q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
+        int q = 0;
+        bool prefix = false;
+        for (; q < kLb; ++q) {
+          if ((sv[q] >> 62) == 0) break;
+          excl += sv[q] & kLbVal;
+          if (sv[q] & kLbPre) {
+            prefix = true;
+            break;
+          }
+        }
+        if (prefix) break;
+        j -= q;
+        if (q < kLb) __builtin_amdgcn_s_sleep(1);
+      }
+      __hip_atomic_store(st, kLbPre | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (base + kSortTile >= (int64_t)n) n_ptr[1] = (uint32_t)(excl + cnt);  // the last tile: the group count
+    s_gbase = (int64_t)excl;
+  }
+  __syncthreads();
+  int64_t G = s_gbase;  // groups with a head before my share
   for (int w = 0; w < wave; ++w) G += s_heads[w];
   const int64_t Gq = G;
   int32_t grel[kRSPT];  // group of each element relative to Gq (-1: the group open before my share)
@@ -870,14 +915,19 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
                       uint32_t* head_pos, int64_t* carry_g, uint64_t* carry_slots, int64_t* open_g, hipStream_t s) {
   const int nt = sb->ntiles_sort;
   const uint32_t* refs = sb->refs[sb->cur];
+  // the look-back status (the sort's, free again) and the tile counter; the group count starts at 0
+  uint32_t* ctr = sb->bin_total + (size_t)kRsMaxPasses * kMaxBins + kRsMaxPasses;
+  (void)hipMemsetAsync(sb->lb_status, 0, (size_t)nt * sizeof(uint64_t), s);
+  (void)hipMemsetAsync(ctr, 0, sizeof(uint32_t), s);
+  (void)hipMemsetAsync(sb->n + 1, 0, sizeof(uint32_t), s);
   if (refs)
     hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
-                       sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
-                       open_g);
+                       sb->ref_bits, sb->n, sb->lb_status, ctr, plan, out_keys, out_slots, cap, head_pos, carry_g,
+                       carry_slots, open_g);
   else
     hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
-                       sb->ref_bits, sb->n, sb->run_cnt, plan, out_keys, out_slots, cap, head_pos, carry_g, carry_slots,
-                       open_g);
+                       sb->ref_bits, sb->n, sb->lb_status, ctr, plan, out_keys, out_slots, cap, head_pos, carry_g,
+                       carry_slots, open_g);
   const int64_t nw = (int64_t)nt * kRedWaves;  // carry / open slots: one per wave share of a tile
   const unsigned g = (unsigned)((nw + 255) / 256);
   hipLaunchKernelGGL(k_gb_carry, dim3(g), dim3(256), 0, s, carry_g, carry_slots, nw, plan, out_slots, cap);
