@@ -51,6 +51,17 @@ __device__ __forceinline__ const uint8_t* cv_ptr(const ColView& v, int64_t r) {
   return base + (size_t)(r & ((1ll << v.log2_per) - 1)) * (size_t)v.width;
 }
 
+// The cursor time of row r (the scan's __time view): a block whose rows all share one bucket and lie
+// inside the interval is not decoded; its pointer is tagged (low bit) and points at one representative
+// timestamp (the block's first row time), which gives every row of the block the same bucket and
+// interval verdict as its own time would.
+__device__ __forceinline__ int64_t load_time(const ColView& v, int64_t r) {
+  const uintptr_t b = reinterpret_cast<uintptr_t>(v.blocks[r >> v.log2_per]);
+  if (b & 1u) return *reinterpret_cast<const int64_t*>(b & ~(uintptr_t)1);
+  return *reinterpret_cast<const int64_t*>(reinterpret_cast<const uint8_t*>(b) +
+                                           (size_t)(r & ((1ll << v.log2_per) - 1)) * 8);
+}
+
 // a width-byte big-endian id read as little-endian -> its value (VSizeColumnarInts.get, :124-127)
 __device__ __forceinline__ uint32_t id_bswap(uint32_t x, int width) {
   const uint32_t b = __builtin_bswap32(x);
@@ -158,6 +169,22 @@ __device__ __forceinline__ void load_ids4(const ColView& v, int64_t r, uint32_t 
 #pragma unroll
     for (int k = 0; k < 4; ++k) id[k] = id_bswap(id[k], v.width);
   }
+}
+
+// cursor times of rows r .. r + 3 (r % 4 == 0, inside one block; see load_time)
+__device__ __forceinline__ void load_time4(const ColView& v, int64_t r, uint64_t t[4]) {
+  const uintptr_t b = reinterpret_cast<uintptr_t>(v.blocks[r >> v.log2_per]);
+  if (b & 1u) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(b & ~(uintptr_t)1);
+    t[0] = t[1] = t[2] = t[3] = x;
+    return;
+  }
+  const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(b) + (size_t)(r & ((1ll << v.log2_per) - 1)) * 8);
+  const uint4 a = p[0], c = p[1];
+  t[0] = (uint64_t)a.x | ((uint64_t)a.y << 32);
+  t[1] = (uint64_t)a.z | ((uint64_t)a.w << 32);
+  t[2] = (uint64_t)c.x | ((uint64_t)c.y << 32);
+  t[3] = (uint64_t)c.z | ((uint64_t)c.w << 32);
 }
 
 // raw 8-byte lanes of a numeric view for rows r .. r + 3 (float views: 4-byte values in the low half)

@@ -1466,6 +1466,65 @@ static Cursors plan_cursors(const Segment* seg, int seg_index, const dg_scan* q,
   return c;
 }
 
+// The cursor's __time view of a scan (ScanJob / GbJob .time: bucket and interval of every row). An
+// LZ4 LONGS block whose rows all fall in one bucket and inside [t_lo, t_hi) is not decoded: its block
+// pointer is tagged and points at one representative time (load_time), which gives each of its rows
+// the verdict its own time would. Rows are time-sorted (IndexMergerV9 / IncrementalIndex order), so
+// block k's rows lie in [first[k], first[k + 1]] (the blocks' first-row times, read at attach) and the
+// last block's in [first[k], maxTime]; the view falls back to decoding every block when the first
+// times do not ascend. grid0: a bucket start at or before t_lo (period grids); g: calendar buckets.
+static int time_view(const Segment* seg, const Column* c, const Cursors& cu, int64_t period, const Grain& g,
+                     CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
+  const BlockColumn& b = c->data;
+  const bool plain = b.codec == CODEC_LZ4 && !b.vbits && b.width == 8 && (int32_t)b.first8.size() == b.nblocks &&
+                     b.nblocks > 0 && !c->multi_value;
+  bool sorted = plain;
+  for (int32_t k = 1; sorted && k < b.nblocks; ++k) sorted = b.first8[k - 1] <= b.first8[k];
+  if (sorted) sorted = b.first8[b.nblocks - 1] <= seg->max_time;
+  const char* off = getenv("DG_NO_TIME_SKIP");  // (same-box A/B and tests: decode every block)
+  if (!sorted || (off && *off && *off != '0')) return column_view(c, cs, db, v, st);
+  auto bucket = [&](int64_t t) -> int64_t {
+    if (g.hb) return g.coord(t);
+    return period ? (t - cu.bucket0) / period : 0;  // (t >= t_lo >= bucket0)
+  };
+  std::vector<uint8_t> uni(b.nblocks, 0);
+  int32_t ndec = 0;
+  for (int32_t k = 0; k < b.nblocks; ++k) {
+    const int64_t lo = b.first8[k], hi = k + 1 < b.nblocks ? b.first8[k + 1] : seg->max_time;
+    uni[k] = lo >= cu.t_lo && hi < cu.t_hi && bucket(lo) == bucket(hi);
+    ndec += !uni[k];
+  }
+  v->log2_per = b.log2_per;
+  v->width = b.width;
+  v->pad = 0;
+  v->kind = VIEW_LONG;
+  uint8_t* slots = ndec ? dev_take<uint8_t>(cs, (size_t)ndec * kBlockBytes + 64) : nullptr;
+  int64_t* d_const;
+  int64_t* h_const = up_take<int64_t>(cs, std::max(b.nblocks, 1), &d_const, st);
+  const uint8_t** d_ptrs;
+  const uint8_t** h_ptrs = up_take<const uint8_t*>(cs, std::max(b.nblocks, 1), &d_ptrs, st);
+  if ((ndec && !slots) || !h_const || !h_ptrs) return set_error(DG_ERR_OOM, "time view");
+  if (ndec) db->last_slots = slots;
+  int32_t at = 0;
+  for (int32_t k = 0; k < b.nblocks; ++k) {
+    const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
+    if (uni[k]) {
+      h_const[k] = b.first8[k];
+      h_ptrs[k] = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(d_const + k) | 1u);
+      continue;
+    }
+    uint8_t* slot = slots + (size_t)at++ * kBlockBytes;
+    h_ptrs[k] = slot;
+    if (rows > 0) {
+      db->jobs.push_back(lz4_job(b, k, slot, (int32_t)(rows * 8)));
+      db->bytes += b.comp_len[k];
+    }
+  }
+  v->blocks = d_ptrs;
+  return DG_OK;
+}
+
+
 // ------------------------------------------------------------------------------------------------
 // ABI: library & context
 // ------------------------------------------------------------------------------------------------
@@ -2057,7 +2116,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     j.nbuckets = (int32_t)cur[i].nbuckets;
     j.time.kind = VIEW_ABSENT;
     if (cur[i].need_time) {
-      rc = column_view(seg->find("__time"), cs, &db, &j.time, st);
+      rc = time_view(seg, seg->find("__time"), cur[i], q->period_ms, gr, cs, &db, &j.time, st);
       if (rc) return rc;
     }
     for (int a = 0; a < na; ++a) {
@@ -2258,7 +2317,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     j.t_hi = cur[i].t_hi;
     j.time.kind = VIEW_ABSENT;
     if (cur[i].need_time) {
-      rc = column_view(seg->find("__time"), cs, &db, &j.time, st);
+      rc = time_view(seg, seg->find("__time"), cur[i], q->period_ms, gr, cs, &db, &j.time, st);
       if (rc) return rc;
     }
     if (dc) {
@@ -3252,7 +3311,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     j.bitset = bits;
     j.time.kind = VIEW_ABSENT;
     if (cur[i].need_time) {
-      rc = column_view(seg->find("__time"), cs, &db, &j.time, st);
+      rc = time_view(seg, seg->find("__time"), cur[i], q->period_ms, gr, cs, &db, &j.time, st);
       if (rc) return rc;
     }
     j.t_lo = cur[i].t_lo;

@@ -249,6 +249,8 @@ struct BlockColumn {
   std::vector<uint8_t> cp_dense;       // LZ4: block b goes to the dense decoder (kDnMode*)
   std::vector<int32_t> cp_fine;        // LZ4: light checkpoints of block b (after its cp_n checkpoints)
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
+  std::vector<int64_t> first8;         // LZ4: the first 8 decoded bytes of block b (int64 LE: its first
+                                       // row's value in a LONGS column), from the attach-time parse
   int64_t index_bytes = 0;             // LZ4: bytes of the checkpoint index (read per query)
   DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)
   DevBuf cps;                          // LZ4: uint32 checkpoints of every block

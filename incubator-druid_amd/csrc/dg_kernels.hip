@@ -440,7 +440,7 @@ constexpr int kBins = 32;
 __device__ __forceinline__ bool row_selected(const ScanJob& j, int64_t r, int64_t* bucket) {
   if (j.bitset && !((j.bitset[r >> 5] >> (r & 31)) & 1u)) return false;
   if (j.time.kind != VIEW_ABSENT) {
-    const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, r));
+    const int64_t t = load_time(j.time, r);
     if (t < j.t_lo || t >= j.t_hi) return false;
     *bucket = j.period ? (bucket_coord(j.bounds, j.nbounds, t) - j.bucket0) / j.period : 0;
   } else {
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
   if (threadIdx.x == 0) {
     int64_t b0 = 0;
     if (j.period && j.time.kind != VIEW_ABSENT) {
-      const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, row0));
+      const int64_t t = load_time(j.time, row0);
       const int64_t v = bucket_coord(j.bounds, j.nbounds, t);
       b0 = v >= j.bucket0 ? (v - j.bucket0) / j.period : 0;
     }
@@ -569,7 +569,7 @@ __device__ __forceinline__ unsigned quad_selected(const ScanJob& j, int64_t r) {
   if (j.bitset) m = (j.bitset[r >> 5] >> (r & 31)) & 0xF;
   if (m && j.time.kind != VIEW_ABSENT) {
     uint64_t t[4];
-    load_raw4(j.time, r, t);
+    load_time4(j.time, r, t);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if ((int64_t)t[k] < j.t_lo || (int64_t)t[k] >= j.t_hi) m &= ~(1u << k);
@@ -729,7 +729,7 @@ __device__ __forceinline__ void quad_keys(const ScanJob& j, int64_t r, uint32_t 
   load_ids4(j.key, r, id);
   if (j.key_card) {
     uint64_t t[4];
-    load_raw4(j.time, r, t);
+    load_time4(j.time, r, t);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       id[k] += (uint32_t)((bucket_coord(j.bounds, j.nbounds, (int64_t)t[k]) - j.bucket0) / j.period) * (uint32_t)j.key_card;

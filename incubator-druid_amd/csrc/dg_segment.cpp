@@ -236,6 +236,39 @@ int lz4_dense_mode(const uint8_t* in, int n) {
   return kDnModeRounds;
 }
 
+// The first 8 decoded bytes of a validated block (its first sequences only), or false when it
+// decodes to fewer.
+static bool lz4_first8(const uint8_t* in, int n, int64_t* out) {
+  uint8_t buf[8];
+  int o = 0, p = 0;
+  auto ext = [&](int* len) {
+    for (int b = 255; b == 255 && p < n;) {
+      b = in[p++];
+      *len += b;
+    }
+  };
+  while (o < 8) {
+    if (p >= n) return false;
+    const int tok = in[p++];
+    int L = tok >> 4;
+    if (L == 15) ext(&L);
+    if (L > n - p) return false;
+    for (int k = 0; k < L && o < 8; ++k) buf[o++] = in[p + k];
+    p += L;
+    if (o >= 8 || p >= n || n - p < 2) break;
+    const int d = in[p] | (in[p + 1] << 8);
+    p += 2;
+    int M = tok & 15;
+    if (M == 15) ext(&M);
+    M += 4;
+    if (d == 0 || d > o) return false;
+    for (int k = 0; k < M && o < 8; ++k, ++o) buf[o] = buf[o - d];
+  }
+  if (o < 8) return false;
+  memcpy(out, buf, 8);
+  return true;
+}
+
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine, int* dense) {
   const size_t first = cps->size();
   if (light) *light = 0;
@@ -346,6 +379,8 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->cp_dense.assign(blocks.n, 0);
     col->cp_fine.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
+    col->first8.assign(blocks.n, 0);
+    std::vector<uint8_t> has8(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
     const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const int nt = blocks.n >= 64 ? nth : 1;
@@ -361,10 +396,13 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
           col->cp_dense[b] = (uint8_t)(light ? 0 : dense);
           col->cp_fine[b] = nfine;
           col->dec_len[b] = d;
+          if (d >= 8) has8[b] = lz4_first8(host.data() + col->comp_off[b], col->comp_len[b], &col->first8[b]);
           col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size() - nfine;
         }
       });
     for (auto& x : th) x.join();
+    for (int32_t b = 0; b < blocks.n; ++b)
+      if (!has8[b]) col->first8.clear();  // (then no block's first value is known)
     std::vector<uint32_t> all;
     for (int32_t b = 0; b < blocks.n; ++b) {
       col->cp_off[b] = (int64_t)all.size();

@@ -106,7 +106,7 @@ __device__ __forceinline__ bool gb_select(const GbJob& j, int64_t r, int64_t* bu
   if (j.bitset && !((j.bitset[r >> 5] >> (r & 31)) & 1u)) return false;
   *bucket = 0;
   if (j.time.kind != VIEW_ABSENT) {
-    const int64_t t = *reinterpret_cast<const int64_t*>(cv_ptr(j.time, r));
+    const int64_t t = load_time(j.time, r);
     if (t < j.t_lo || t >= j.t_hi) return false;
     if (j.period) *bucket = (bucket_coord(j.bounds, j.nbounds, t) - j.bucket0) / j.period;
   }
