@@ -180,10 +180,17 @@ __global__ __launch_bounds__(256) void k_gb_count(const GbJob* __restrict__ jobs
     int64_t b;
     if (gb_select(j, r, &b)) c += MULTI ? gb_fanout(j, r) : 1u;
   }
-  // per-thread sums saturate (8 rows each), the tile sum too: a saturated tile means >= 2^32 elements
-  const uint32_t t = block_sum_u32<256>((uint32_t)min<uint64_t>(c, 0xFFFFFFull), s_tmp);
-  const bool sat = __syncthreads_or(c > 0xFFFFFFull);
-  if (threadIdx.x == 0) cnt[blockIdx.x] = sat ? 0xFFFFFFFFu : t;
+  // the tile's sum in 64 bits (a row's fan-out is the product of its value-list lengths: a few rows can
+  // pass 2^32 between them); only the stored 32-bit count saturates, which marks >= 2^32 elements
+  __shared__ unsigned long long s_sum[4];
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+    cnt[blockIdx.x] = t >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t;
+  }
+  (void)s_tmp;
 }
 
 // total of n u32 counts in 64 bits (the element count of a multi-value keygen, checked against 2^32)

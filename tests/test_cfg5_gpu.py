@@ -141,3 +141,35 @@ def test_two_rank_merge(Q, O, R, cfg5):
     exp = O.run(qt, o)
     assert_results(qt, out[0], exp)
     assert_results(qt, out[1], exp)
+
+
+@pytest.mark.parametrize("kind", ["timeseries", "groupby", "topn"])
+def test_uniform_time_blocks_are_not_decoded(R, cfg5, kind, monkeypatch):
+    """__time blocks whose rows share one hourly bucket (almost every block of these time-sorted
+    segments) are not decoded: the scan reads fewer stored bytes than with every block decoded
+    (DG_NO_TIME_SKIP=1), and the results are identical, also with an interval cutting blocks."""
+    B, g, o = cfg5
+    Q = importlib.import_module("incubator-druid_amd.query")
+    lo, hi = g[0].min_time + 1_234_567, g[-1].max_time - 7_654_321
+    for iv in (["1970-01-01/2020-01-01"], [(lo, hi)]):
+        if kind == "timeseries":
+            q = Q.TimeseriesQuery(intervals=iv, granularity="hour", aggregations=[Q.count("rows"),
+                                                                                   Q.long_sum("sumLongSequential")])
+        elif kind == "groupby":
+            q = Q.GroupByQuery(intervals=iv, granularity="hour", dimensions=["dimZipf"],
+                               aggregations=[Q.count("rows"), Q.double_sum("sumFloatNormal")])
+        else:
+            q = Q.TopNQuery(intervals=iv, granularity="hour", dimension="dimZipf", metric="rows", threshold=5,
+                            aggregations=[Q.count("rows")])
+        runs = {}
+        for mode in ("skip", "decode"):
+            if mode == "decode":
+                monkeypatch.setenv("DG_NO_TIME_SKIP", "1")
+            else:
+                monkeypatch.delenv("DG_NO_TIME_SKIP", raising=False)
+            stats = R.RunStats()
+            runs[mode] = (R.run_query(q, g, stats), sum(c["bytes_read"] for c in stats.calls))
+        monkeypatch.delenv("DG_NO_TIME_SKIP", raising=False)
+        (a, bytes_skip), (b, bytes_all) = runs["skip"], runs["decode"]
+        assert bytes_skip < bytes_all, (bytes_skip, bytes_all)
+        assert_results(q, a, b)
