@@ -283,4 +283,14 @@ __device__ __forceinline__ uint64_t agg_in(const Job& j, const AggPlan& plan, in
   return agg_row(j.agg_bits[a], r) ? agg_input(plan.kind[a], j.vals[a], r) : identity_of(plan.op[a], plan.kind[a]);
 }
 
+// agg_in for the timeseries scan: rows of a block the decoder already aggregated (kViewFused view,
+// tagged block pointer) contribute the identity
+template <class Job>
+__device__ __forceinline__ uint64_t agg_in_scan(const Job& j, const AggPlan& plan, int a, int64_t r) {
+  const ColView& v = j.vals[a];
+  if ((v.pad & kViewFused) && (reinterpret_cast<uintptr_t>(v.blocks[r >> v.log2_per]) & 1u))
+    return identity_of(plan.op[a], plan.kind[a]);
+  return agg_in(j, plan, a, r);
+}
+
 }  // namespace dg

@@ -400,11 +400,12 @@ struct DecodeBatch {
   int64_t gen_bytes = 0;
   int32_t gen_blocks = 0;
   int32_t gen_launches = 0;
-  // the same for the dense decoder
-  hipEvent_t dense_a = nullptr, dense_b = nullptr;
-  int64_t dense_bytes = 0;
-  int32_t dense_blocks = 0;
-  int32_t dense_launches = 0;
+  int64_t fused_blocks = 0;  // blocks whose decode was fused with their aggregator (fused_agg_view)
+  // the same for the class-8 decoder
+  hipEvent_t c8_a = nullptr, c8_b = nullptr;
+  int64_t c8_bytes = 0;
+  int32_t c8_blocks = 0;
+  int32_t c8_launches = 0;
 };
 // device time of the general decoder's launches of a batch (0 if it launched none)
 static double gen_ms(const DecodeBatch& db) {
@@ -413,18 +414,18 @@ static double gen_ms(const DecodeBatch& db) {
   hipEventElapsedTime(&f, db.gen_a, db.gen_b);
   return f;
 }
-static double dense_ms(const DecodeBatch& db) {
-  if (!db.dense_blocks || !db.dense_a) return 0;
+static double c8_ms(const DecodeBatch& db) {
+  if (!db.c8_blocks || !db.c8_a) return 0;
   float f = 0;
-  hipEventElapsedTime(&f, db.dense_a, db.dense_b);
+  hipEventElapsedTime(&f, db.c8_a, db.c8_b);
   return f;
 }
 // the decode-timing events of a call's main (side = false) or side batch
 static void decode_events(Context* ctx, DecodeBatch* db, bool side) {
   db->gen_a = ctx->gen_ev[side ? 2 : 0];
   db->gen_b = ctx->gen_ev[side ? 3 : 1];
-  db->dense_a = ctx->gen_ev[side ? 6 : 4];
-  db->dense_b = ctx->gen_ev[side ? 7 : 5];
+  db->c8_a = ctx->gen_ev[side ? 6 : 4];
+  db->c8_b = ctx->gen_ev[side ? 7 : 5];
 }
 // a call's decode metrics from its main and side batches
 static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_metrics* m) {
@@ -432,10 +433,11 @@ static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_me
   m->lz4_general_bytes = db.gen_bytes + side.gen_bytes;
   m->lz4_general_blocks = db.gen_blocks + side.gen_blocks;
   m->lz4_general_launches = db.gen_launches + side.gen_launches;
-  m->lz4_dense_ms = dense_ms(db) + dense_ms(side);
-  m->lz4_dense_bytes = db.dense_bytes + side.dense_bytes;
-  m->lz4_dense_blocks = db.dense_blocks + side.dense_blocks;
-  m->lz4_dense_launches = db.dense_launches + side.dense_launches;
+  m->lz4_fused_blocks = db.fused_blocks + side.fused_blocks;
+  m->lz4_c8_ms = c8_ms(db) + c8_ms(side);
+  m->lz4_c8_bytes = db.c8_bytes + side.c8_bytes;
+  m->lz4_c8_blocks = db.c8_blocks + side.c8_blocks;
+  m->lz4_c8_launches = db.c8_launches + side.c8_launches;
 }
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
 static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st);
@@ -1054,7 +1056,9 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
   j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
   j.vstride = 0;
-  j.dense = b.cp_dense.empty() ? 0 : b.cp_dense[k];
+  j.c8 = b.cp_c8.empty() ? 0 : b.cp_c8[k];
+  j.red_dst = nullptr;
+  j.red_op = j.red_kind = j.red_vkind = j.red_pad = 0;
   return j;
 }
 
@@ -1236,14 +1240,14 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   // per-thread sequence registers)
   // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
   // blocks per CU)
-  // dense blocks (token-dense, short runs: k_lz4_dense, two blocks per CU) go first
-  // (DG_LZ4_NO_DENSE=1: every dense block to the general decoder, for same-box A/B and tests)
-  const char* no_dense = getenv("DG_LZ4_NO_DENSE");
-  if (no_dense && *no_dense && *no_dense != '0')
-    for (Lz4Job& j : db->jobs) j.dense = 0;
+  // class-8 blocks (8-byte value runs: k_lz4_c8) go first
+  // (DG_LZ4_NO_C8=1: those blocks to the general decoder, for same-box A/B and tests)
+  const char* no_c8 = getenv("DG_LZ4_NO_C8");
+  if (no_c8 && *no_c8 && *no_c8 != '0')
+    for (Lz4Job& j : db->jobs) j.c8 = 0;
   const int nh = (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.light; }) -
                        db->jobs.begin());
-  const int nd = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return j.dense != 0; }) -
+  const int nd = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return j.c8 != 0; }) -
                        db->jobs.begin());
   const int nn = (int)(std::stable_partition(db->jobs.begin() + nd, db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
                        db->jobs.begin());
@@ -1257,12 +1261,12 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
   launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
-  for (int i = 0; i < nd; ++i) db->dense_bytes += db->jobs[i].src_len;
-  db->dense_blocks += nd;
-  db->dense_launches += nd > 0;
-  if (db->dense_a && nd) hipEventRecord(db->dense_a, st);
-  launch_lz4_dense(d, nd, d_err, st, d_prof);
-  if (db->dense_a && nd) hipEventRecord(db->dense_b, st);
+  for (int i = 0; i < nd; ++i) db->c8_bytes += db->jobs[i].src_len;
+  db->c8_blocks += nd;
+  db->c8_launches += nd > 0;
+  if (db->c8_a && nd) hipEventRecord(db->c8_a, st);
+  launch_lz4_c8(d, nd, d_err, st, d_prof);
+  if (db->c8_a && nd) hipEventRecord(db->c8_b, st);
   for (int i = nd; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
   db->gen_blocks += nh - nd;
   db->gen_launches += (nn - nd > 0) + (nh - nn > 0);
@@ -1473,8 +1477,13 @@ static Cursors plan_cursors(const Segment* seg, int seg_index, const dg_scan* q,
 // block k's rows lie in [first[k], first[k + 1]] (the blocks' first-row times, read at attach) and the
 // last block's in [first[k], maxTime]; the view falls back to decoding every block when the first
 // times do not ascend. grid0: a bucket start at or before t_lo (period grids); g: calendar buckets.
-static int time_view(const Segment* seg, const Column* c, const Cursors& cu, int64_t period, const Grain& g,
-                     CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
+// Per __time block: the bucket (the scan's index, row_selected's formula) its rows share inside the
+// interval, or -1 when they may span buckets or leave it. Empty when the blocks' first times cannot
+// bound their rows (not plain LZ4 LONGS, first times not ascending, or DG_NO_TIME_SKIP).
+static std::vector<int64_t> time_block_buckets(const Segment* seg, const Column* c, const Cursors& cu, int64_t period,
+                                               const Grain& g) {
+  std::vector<int64_t> tb;
+  if (!c) return tb;
   const BlockColumn& b = c->data;
   const bool plain = b.codec == CODEC_LZ4 && !b.vbits && b.width == 8 && (int32_t)b.first8.size() == b.nblocks &&
                      b.nblocks > 0 && !c->multi_value;
@@ -1482,16 +1491,27 @@ static int time_view(const Segment* seg, const Column* c, const Cursors& cu, int
   for (int32_t k = 1; sorted && k < b.nblocks; ++k) sorted = b.first8[k - 1] <= b.first8[k];
   if (sorted) sorted = b.first8[b.nblocks - 1] <= seg->max_time;
   const char* off = getenv("DG_NO_TIME_SKIP");  // (same-box A/B and tests: decode every block)
-  if (!sorted || (off && *off && *off != '0')) return column_view(c, cs, db, v, st);
+  if (!sorted || (off && *off && *off != '0')) return tb;
   auto bucket = [&](int64_t t) -> int64_t {
-    if (g.hb) return g.coord(t);
-    return period ? (t - cu.bucket0) / period : 0;  // (t >= t_lo >= bucket0)
+    const int64_t v = g.hb ? g.coord(t) : t;
+    return period ? (v - cu.bucket0) / period : 0;
   };
+  tb.assign(b.nblocks, -1);
+  for (int32_t k = 0; k < b.nblocks; ++k) {
+    const int64_t lo = b.first8[k], hi = k + 1 < b.nblocks ? b.first8[k + 1] : seg->max_time;
+    if (lo >= cu.t_lo && hi < cu.t_hi && bucket(lo) == bucket(hi)) tb[k] = bucket(lo);
+  }
+  return tb;
+}
+
+static int time_view(const Column* c, const std::vector<int64_t>& tb, CallScratch* cs,
+                     DecodeBatch* db, ColView* v, hipStream_t st) {
+  if (tb.empty()) return column_view(c, cs, db, v, st);
+  const BlockColumn& b = c->data;
   std::vector<uint8_t> uni(b.nblocks, 0);
   int32_t ndec = 0;
   for (int32_t k = 0; k < b.nblocks; ++k) {
-    const int64_t lo = b.first8[k], hi = k + 1 < b.nblocks ? b.first8[k + 1] : seg->max_time;
-    uni[k] = lo >= cu.t_lo && hi < cu.t_hi && bucket(lo) == bucket(hi);
+    uni[k] = tb[k] >= 0;
     ndec += !uni[k];
   }
   v->log2_per = b.log2_per;
@@ -1765,6 +1785,79 @@ static int agg_view(Segment* seg, const dg_agg& a, CallScratch* cs, DecodeBatch*
   if (c->type == DG_COL_STRING || c->type == DG_COL_UNSUPPORTED)
     return set_error(DG_ERR_UNSUPPORTED, "aggregating non-numeric column %s", a.field);
   return column_view(c, cs, db, v, st);
+}
+
+// Timeseries decode fused with aggregation (BlockLayoutColumnarLongsSupplier.java:64-90 reads each
+// decompressed block in the loop that consumes it): the LZ4 blocks of an 8-byte long / double input
+// whose rows share one bucket inside the interval (time_block_buckets; every block when the cursor
+// needs no time) are reduced by the decoder itself into the bucket's slot (Lz4Job.red_*), nothing is
+// written; their view pointers are tagged (kViewFused) so the scan takes the identity for those rows.
+// Other blocks (light blocks, blocks straddling a bucket edge) are decoded into slots as usual. Only
+// for an unfiltered scan and an unfiltered aggregator other than floatSum (its row-order fp32
+// recurrence) and count. `out` = the segment's [buckets][rec] accumulators, initialised before the
+// decoders run. Returns 1 when the aggregator does not qualify (the caller builds the plain view).
+static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::vector<int64_t>& tb, bool one_bucket,
+                          uint64_t* out, int rec, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
+  const char* off = getenv("DG_NO_FUSE");  // (same-box A/B and tests: decode every block)
+  if ((off && *off && *off != '0') || (a.filter && a.n_filter > 0) || a.kind == DG_AGG_COUNT ||
+      a.kind == DG_AGG_FLOAT_SUM || !a.field)
+    return 1;
+  const Column* c = seg->find(a.field);
+  const Column* tc = seg->find("__time");
+  if (!c || c->multi_value || (c->type != DG_COL_LONG && c->type != DG_COL_DOUBLE)) return 1;
+  const BlockColumn& b = c->data;
+  if (b.codec != CODEC_LZ4 || b.vbits || b.width != 8 || b.nblocks <= 0) return 1;
+  if (!one_bucket && (tb.empty() || !tc)) return 1;
+  const int64_t ts = one_bucket ? 1 : tc->data.size_per;
+  std::vector<int64_t> bk(b.nblocks, -1);
+  int32_t nfused = 0;
+  for (int32_t k = 0; k < b.nblocks; ++k) {
+    const int64_t r0 = (int64_t)k * b.size_per, r1 = std::min<int64_t>((int64_t)b.total, r0 + b.size_per);
+    if (r1 <= r0 || (!b.cp_light.empty() && b.cp_light[k])) continue;
+    if (one_bucket) {
+      bk[k] = 0;
+    } else {
+      const int64_t t0 = r0 / ts, t1 = (r1 - 1) / ts;
+      if (t1 >= (int64_t)tb.size()) continue;
+      int64_t bu = tb[t0];
+      for (int64_t t = t0 + 1; t <= t1 && bu >= 0; ++t)
+        if (tb[t] != bu) bu = -1;
+      bk[k] = bu;
+    }
+    nfused += bk[k] >= 0;
+  }
+  if (!nfused) return 1;
+  v->log2_per = b.log2_per;
+  v->width = b.width;
+  v->pad = kViewFused;
+  v->kind = c->type == DG_COL_LONG ? VIEW_LONG : VIEW_DOUBLE;
+  db->bytes += b.stored_bytes + b.index_bytes;
+  const int32_t ndec = b.nblocks - nfused;
+  uint8_t* slots = ndec ? dev_take<uint8_t>(cs, (size_t)ndec * kBlockBytes + 64) : nullptr;
+  const uint8_t** d_ptrs;
+  const uint8_t** h_ptrs = up_take<const uint8_t*>(cs, b.nblocks, &d_ptrs, st);
+  if ((ndec && !slots) || !h_ptrs) return set_error(DG_ERR_OOM, "fused view");
+  if (ndec) db->last_slots = slots;
+  int32_t at = 0;
+  for (int32_t k = 0; k < b.nblocks; ++k) {
+    const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
+    if (bk[k] >= 0) {
+      h_ptrs[k] = reinterpret_cast<const uint8_t*>((uintptr_t)1);  // tagged: never dereferenced
+      Lz4Job j = lz4_job(b, k, nullptr, (int32_t)(rows * 8));
+      j.red_dst = out + (size_t)bk[k] * rec + 1 + slot;
+      j.red_op = slot_op(a.kind);
+      j.red_kind = a.kind;
+      j.red_vkind = v->kind;
+      db->jobs.push_back(j);
+      db->fused_blocks++;
+      continue;
+    }
+    uint8_t* dst = slots + (size_t)at++ * kBlockBytes;
+    h_ptrs[k] = dst;
+    if (rows > 0) db->jobs.push_back(lz4_job(b, k, dst, (int32_t)(rows * 8)));
+  }
+  v->blocks = d_ptrs;
+  return DG_OK;
 }
 
 // per-segment tile assignment
@@ -2090,6 +2183,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   std::vector<ScanJob> jobs(n);
   std::vector<int64_t> tiles_rows(n, 0);
   std::vector<const unsigned long long*> counts(n, nullptr);
+  const bool fsum = has_float_sum(plan);
   DecodeBatch db;
   decode_events(ctx, &db, false);
   hipEventRecord(ctx->ev[0], st);
@@ -2115,32 +2209,40 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     j.nbounds = gr.nb + 1;
     j.nbuckets = (int32_t)cur[i].nbuckets;
     j.time.kind = VIEW_ABSENT;
+    const Column* tcol = seg->find("__time");
+    std::vector<int64_t> tb;
     if (cur[i].need_time) {
-      rc = time_view(seg, seg->find("__time"), cur[i], q->period_ms, gr, cs, &db, &j.time, st);
-      if (rc) return rc;
-    }
-    for (int a = 0; a < na; ++a) {
-      rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
+      tb = time_block_buckets(seg, tcol, cur[i], q->period_ms, gr);
+      rc = time_view(tcol, tb, cs, &db, &j.time, st);
       if (rc) return rc;
     }
     j.out = dev_take<uint64_t>(cs, (size_t)cur[i].nbuckets * rec);
     if (!j.out) return set_error(DG_ERR_OOM, "accumulators");
+    for (int a = 0; a < na; ++a) {
+      rc = 1;
+      if (!bits && !fsum)
+        rc = fused_agg_view(seg, q->aggs[a], a, tb, !cur[i].need_time, j.out, rec, cs, &db, &j.vals[a], st);
+      if (rc == 1) rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
+      if (rc) return rc;
+    }
     tiles_rows[i] = seg->nrows;
-    for (int k = 0; k < n; ++k) (void)k;
   }
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  // init accumulators (before the decoders: fused blocks combine into them)
+  uint64_t* d_init;
+  uint64_t* h_init = up_take<uint64_t>(cs, rec, &d_init, st);
+  if (!h_init) return set_error(DG_ERR_OOM, "accumulator init");
+  h_init[0] = 0;
+  for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
+  DG_FLUSH(cs, st);
+  for (int i = 0; i < n; ++i)
+    if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, d_init, st);
   hipEventRecord(ctx->ev[1], st);
   rc = run_decodes(cs, &db, st);
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
   m.bytes_read = db.bytes;
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
-  // init accumulators
-  uint64_t* d_init;
-  uint64_t* h_init = up_take<uint64_t>(cs, rec, &d_init, st);
-  if (!h_init) return set_error(DG_ERR_OOM, "accumulator init");
-  h_init[0] = 0;
-  for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
   std::vector<int32_t> begin;
   int ntiles = 0;
   for (int i = 0; i < n; ++i)
@@ -2153,11 +2255,9 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   if (!h_jobs) return set_error(DG_ERR_OOM, "scan jobs");
   memcpy(h_jobs, jobs.data(), sizeof(ScanJob) * n);
   DG_FLUSH(cs, st);
-  for (int i = 0; i < n; ++i)
-    if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, d_init, st);
   hipEventRecord(ctx->ev[3], st);
   launch_scan_agg(d_jobs, d_tile, ntiles, plan, 0, st);
-  if (has_float_sum(plan)) {
+  if (fsum) {
     // floatSum as the reference adds it: float32, one row at a time per cursor (bucket)
     std::vector<GbJob> gj(n);
     std::vector<int64_t> frows(n, 0);
@@ -2317,7 +2417,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     j.t_hi = cur[i].t_hi;
     j.time.kind = VIEW_ABSENT;
     if (cur[i].need_time) {
-      rc = time_view(seg, seg->find("__time"), cur[i], q->period_ms, gr, cs, &db, &j.time, st);
+      rc = time_view(seg->find("__time"), time_block_buckets(seg, seg->find("__time"), cur[i], q->period_ms, gr), cs, &db, &j.time, st);
       if (rc) return rc;
     }
     if (dc) {
@@ -3311,7 +3411,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     j.bitset = bits;
     j.time.kind = VIEW_ABSENT;
     if (cur[i].need_time) {
-      rc = time_view(seg, seg->find("__time"), cur[i], q->period_ms, gr, cs, &db, &j.time, st);
+      rc = time_view(seg->find("__time"), time_block_buckets(seg, seg->find("__time"), cur[i], q->period_ms, gr), cs, &db, &j.time, st);
       if (rc) return rc;
     }
     j.t_lo = cur[i].t_lo;
@@ -4237,10 +4337,10 @@ int dg_timeseries_merge(const dg_scan* scan, int32_t n_lists, const int32_t* n, 
 extern "C" int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind) {
   if (!block || len <= 0 || len > kBlockBytes + 2048 || !kind) return set_error(DG_ERR_ARG, "bad arguments");
   std::vector<uint32_t> one;
-  int wide = 0, light = 0, nfine = 0, dense = 0;
-  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine, &dense);
-  // -1 malformed, 0 general, 1 general (wide), 2 light, 3 dense (rounds), 4 dense (class scan)
-  *kind = d < 0 ? -1 : light ? 2 : dense ? 2 + dense : wide ? 1 : 0;
+  int wide = 0, light = 0, nfine = 0, c8 = 0;
+  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine, &c8);
+  // -1 malformed, 0 general, 1 general (wide), 2 light, 4 class-8 (3: the removed dense decoder)
+  *kind = d < 0 ? -1 : light ? 2 : c8 ? 4 : wide ? 1 : 0;
   return DG_OK;
 }
 
@@ -4257,7 +4357,7 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.cp_n.resize(n);
   b.cp_wide.assign(n, 0);
   b.cp_light.assign(n, 0);
-  b.cp_dense.assign(n, 0);
+  b.cp_c8.assign(n, 0);
   b.cp_fine.assign(n, 0);
   b.dec_len.resize(n);
   int64_t total = 0;
@@ -4272,11 +4372,11 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
     std::vector<uint32_t> one;
-    int wide = 0, light = 0, nfine = 0, dense = 0;
-    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine, &dense);
+    int wide = 0, light = 0, nfine = 0, c8 = 0;
+    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine, &c8);
     b.cp_wide[i] = (uint8_t)wide;
     b.cp_light[i] = (uint8_t)light;
-    b.cp_dense[i] = (uint8_t)(light ? 0 : dense);
+    b.cp_c8[i] = (uint8_t)(light ? 0 : c8);
     b.cp_fine[i] = nfine;
     b.cp_off[i] = (int64_t)cps.size();
     b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size() - nfine;

@@ -30,7 +30,9 @@ enum ViewKind : int32_t { VIEW_ABSENT = 0, VIEW_LONG = 1, VIEW_FLOAT = 2, VIEW_D
 enum SlotOp : int32_t { OP_ADD_I64 = 0, OP_ADD_F64 = 1, OP_MIN_U64 = 2, OP_MAX_U64 = 3 };
 
 // A column as the kernels see it: value(row) lives at blocks[row >> log2_per] + (row & mask) * width.
-// flags: kViewBigEndian = dictionary ids stored big-endian (uncompressed VSizeColumnarInts).
+// flags: kViewBigEndian = dictionary ids stored big-endian (uncompressed VSizeColumnarInts);
+// kViewFused = an aggregator's input whose tagged blocks (low pointer bit) the decoder already
+// aggregated (Lz4Job.red_*): the scan takes the aggregator's identity for their rows.
 struct ColView {
   const uint8_t* const* blocks;
   int32_t log2_per;
@@ -39,6 +41,7 @@ struct ColView {
   int32_t pad;  // flags
 };
 constexpr int32_t kViewBigEndian = 1;
+constexpr int32_t kViewFused = 2;
 
 // LZ4 sequence checkpoints: built once per block at attach (lz4_index_block), one entry per
 // kLzSeqPerCp sequences (2 * kLzSeqPerCp for the rare block with more than kLzMaxCps * kLzSeqPerCp
@@ -65,7 +68,16 @@ struct Lz4Job {
   // and value v goes to dst + v * vstride (a column of the groupBy payload records, written in place);
   // bytes past expect_len are then not written (they would land in the next segment's records)
   int32_t vstride;
-  int32_t dense;       // token-dense block for k_lz4_dense (attach-time classification, kDnMode*)
+  int32_t c8;          // class-8 block: decoded by k_lz4_c8 (attach-time classification, lz4_c8_mode)
+  // Decode fused with a timeseries aggregator (the block's rows share one bucket, no filter): instead
+  // of writing its 8-byte values the decoder folds them with red_op (agg_input_raw(red_kind,
+  // red_vkind, value)) and combines the block's result into the bucket's slot *red_dst atomically.
+  // Null: the block is written out.
+  uint64_t* red_dst;
+  int32_t red_op;
+  int32_t red_kind;
+  int32_t red_vkind;
+  int32_t red_pad;
 };
 
 // Light blocks (literal-heavy: random ids, high-entropy values): at most kLtMaxCps checkpoint
@@ -75,17 +87,13 @@ constexpr int kLtMaxCps = 256;
 constexpr int kLtThreads = 512;  // light-decoder threads (at most one light checkpoint interval each)
 constexpr int kLtMaxDepth = 16;
 
-// Dense blocks (token-dense, short matches at scattered distances: noisy doubles): at most kLzMaxCps
-// checkpoint intervals (one per thread), matches of at most kDnMaxRun bytes, at most kDnMaxLongLit
-// literal runs longer than kDnShortLit, and every match resolved within kDnMaxRounds rounds
-// (lz4_dense_mode simulates the kernel's resolution at attach). k_lz4_dense decodes them into a byte
-// image + a resolved-bit map in LDS beside the staged input.
-constexpr int kDnThreads = 1024;
-constexpr int kDnMaxRun = 255;        // longest match
-constexpr int kDnShortLit = 32;       // longer literal runs are copied by the whole workgroup ...
-constexpr int kDnMaxLongLit = 256;    // ... at most this many per block
-constexpr int kDnMaxRounds = 64;
-enum : int32_t { kDnModeNone = 0, kDnModeRounds = 1 };
+// Class-8 blocks (Lz4Job.c8): nearly every match copies from exactly 8 bytes back
+// (8-byte values that change in a few low bytes per row: sequential or slowly varying longs, sorted
+// times); the bytes of the other matches ("exceptions") number at most kC8MaxExc, and no checkpoint
+// interval decodes to more than kC8MaxSpan bytes. k_lz4_c8 decodes them with a scan over the eight
+// residue classes (lz4_c8_mode classifies at attach).
+constexpr int kC8MaxSpan = 512;
+constexpr int kC8MaxExc = 512;
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
 struct LzfJob {
@@ -115,11 +123,11 @@ struct VsJob {
 // *light (optional): the block qualifies for the light decoder (kLtMaxCps / kLtMaxDepth).
 // *light = g > 0 when light: the block's checkpoints are followed by *nfine light checkpoints, one
 // every g sequences (g the fewest sequences per checkpoint that fit the light decoder's threads).
+// *c8 (optional): the block qualifies for the class-8 decoder (lz4_c8_mode).
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr,
-                    int* nfine = nullptr, int* dense = nullptr);
-// The k_lz4_dense mode of a validated, non-wide block (kDnMode*): kDnModeRounds when it fits the dense
-// decoder's limits (above) and its matches resolve within kDnMaxRounds rounds; else kDnModeNone.
-int lz4_dense_mode(const uint8_t* in, int n);
+                    int* nfine = nullptr, int* c8 = nullptr);
+// true when a validated, non-wide block qualifies for k_lz4_c8 (class-8 blocks, above)
+bool lz4_c8_mode(const uint8_t* in, int n);
 
 struct AggPlan {
   int32_t n;
@@ -246,7 +254,7 @@ struct BlockColumn {
   std::vector<int32_t> cp_n;           // LZ4: checkpoints of block b (-1: malformed block)
   std::vector<uint8_t> cp_wide;        // LZ4: block b keeps a checkpoint every 2 * kLzSeqPerCp sequences
   std::vector<uint8_t> cp_light;       // LZ4: block b goes to the light decoder (sequences per light checkpoint)
-  std::vector<uint8_t> cp_dense;       // LZ4: block b goes to the dense decoder (kDnMode*)
+  std::vector<uint8_t> cp_c8;          // LZ4: block b goes to the class-8 decoder
   std::vector<int32_t> cp_fine;        // LZ4: light checkpoints of block b (after its cp_n checkpoints)
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
   std::vector<int64_t> first8;         // LZ4: the first 8 decoded bytes of block b (int64 LE: its first
@@ -326,8 +334,8 @@ struct Context {
   // keys (the two only meet at the reduce); side_ev[0] = its inputs are staged, [1..2] = decode span
   hipStream_t side = nullptr;
   hipEvent_t side_ev[3] = {};
-  // the general and the dense LZ4 decoders' own spans on each stream: [0, 1] general main, [2, 3]
-  // general side, [4, 5] dense main, [6, 7] dense side (their roofline figures, dg_metrics)
+  // the general and the class-8 LZ4 decoders' own spans on each stream: [0, 1] general main, [2, 3]
+  // general side, [4, 5] class-8 main, [6, 7] class-8 side (their roofline figures, dg_metrics)
   hipEvent_t gen_ev[8] = {};
   // dg_context_set_limit(DG_LIMIT_GROUP_ELEMENTS): most sort elements one groupBy call may build
   uint64_t max_elements = ~0ull;
@@ -384,7 +392,7 @@ constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (dia
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
-void launch_lz4_dense(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+void launch_lz4_c8(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // one multi-value dimension's decoded row lists, validated before use (bit 2 of the error word)

@@ -534,7 +534,7 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
     cnt++;
 #pragma unroll
     for (int a = 0; a < kMaxAggs; ++a) {
-      if (a < na) acc[a] = combine_op(plan.op[a], acc[a], agg_in(j, plan, a, r));
+      if (a < na) acc[a] = combine_op(plan.op[a], acc[a], agg_in_scan(j, plan, a, r));
     }
   }
   flush(cur);

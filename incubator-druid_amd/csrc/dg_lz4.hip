@@ -26,6 +26,7 @@
 
 
 #include "dg_internal.h"
+#include "dg_device.h"
 
 namespace dg {
 
@@ -286,8 +287,17 @@ __device__ __forceinline__ int wave_alloc(int* counter, int n) {
 __device__ __forceinline__ int job_len(uint2 j) { return (int)(j.x >> 16) + 1; }
 
 // Output of decoded bytes [16c, 16c + 16): a 16-byte store into a slot, or with job.vstride the two
-// 8-byte values to their payload records (only values inside the block's expect_len)
-__device__ __forceinline__ void out16(const Lz4Job& job, int c, const uint32_t w[4]) {
+// 8-byte values to their payload records (only values inside the block's expect_len), or with
+// job.red_dst the two values folded into the thread's aggregate `acc` (nothing written)
+__device__ __forceinline__ void out16(const Lz4Job& job, int c, const uint32_t w[4], uint64_t& acc) {
+  if (job.red_dst) {
+    const int v = 2 * c;
+    if ((v + 1) * 8 <= job.expect_len)
+      acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, (uint64_t)w[0] | ((uint64_t)w[1] << 32)));
+    if ((v + 2) * 8 <= job.expect_len)
+      acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, (uint64_t)w[2] | ((uint64_t)w[3] << 32)));
+    return;
+  }
   if (!job.vstride) {
     gst16(job.dst + 16 * (size_t)c, w[0], w[1], w[2], w[3]);
     return;
@@ -306,6 +316,23 @@ __device__ __forceinline__ void out4(const Lz4Job& job, int x, uint32_t w) {
   if (((x >> 3) + 1) * 8 <= job.expect_len) gst4(job.dst + (size_t)(x >> 3) * job.vstride + (x & 7), w);
 }
 
+// The fused block's aggregate: the workgroup's per-thread values folded (wave shuffles, then one
+// slot per wave in s_red) and combined into the bucket's slot with one atomic. Every thread calls it.
+__device__ __forceinline__ void red_finish(const Lz4Job& job, uint64_t acc, uint64_t* s_red, int nwaves) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    acc = combine_op(job.red_op, acc, (uint64_t)__shfl_xor((unsigned long long)acc, o, 64));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s_red[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = s_red[0];
+    for (int k = 1; k < nwaves; ++k) t = combine_op(job.red_op, t, s_red[k]);
+    atomic_op(job.red_op, job.red_dst, t);
+  }
+}
+
 template <bool PROF, int SEQ>
 __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
                                                            uint64_t* __restrict__ prof) {
@@ -317,6 +344,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   int* s_jpre = reinterpret_cast<int*>(s_jobs_buf + kMaxJobs);
   __shared__ int s_njob, s_bad, s_c8, s_nopen;
   __shared__ int s_tmp[kLzWaves];
+  __shared__ uint64_t s_red[kLzWaves];
 
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x;
@@ -851,6 +879,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   const int nchunks = (total + 15) >> 4;
   const bool has_tail = total > kTail;
   const int nbody = has_tail ? (kTail >> 4) : nchunks;  // chunks below kTail (kTail % 16 == 0)
+  uint64_t racc = job.red_dst ? identity_of(job.red_op, job.red_kind) : 0ull;
   auto out_chunk = [&](int c) {
     const int x0 = c << 4;
     uint32_t w[4];
@@ -885,7 +914,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         w[q] = acc;
       }
     }
-    out16(job, c, w);
+    out16(job, c, w, racc);
   };
   if (has_tail && wv == kLzWaves - 1) {
     const int nt = total - kTail;
@@ -940,6 +969,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
     for (int c = nbody + tid; c < nchunks; c += kLzThreads) out_chunk(c);
   }
+  if (job.red_dst) red_finish(job, racc, s_red, kLzWaves);
   if (PROF) {
     __syncthreads();
     LZ_STAMP(6);
@@ -1127,6 +1157,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   const uint8_t* __restrict__ in = job.src;
   const int nchunks = (total + 15) >> 4;
   bool fail = false;
+  uint64_t lt_acc = 0;  // (unused: the engine fuses only blocks of the general and class-8 decoders)
   // the source of output byte x: its literal position (a literal byte, a resolved match byte, or
   // hop by hop back to one); -1 = longer chain than the light limit (malformed classification)
   auto resolve = [&](int x, int s) -> int {  // s: a sequence starting at or before x
@@ -1176,7 +1207,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
       uint32_t w[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) w[q] = sh ? __builtin_amdgcn_alignbyte(v[u][q + 1], v[u][q], sh) : v[u][q];
-      out16(job, c0 + u * kLtThreads, w);
+      out16(job, c0 + u * kLtThreads, w, lt_acc);
     }
     // the wave's other chunks, four at a time with one lane per byte: every byte resolves on its own
     // (no per-byte serial walk in one lane), bytes pack into dwords across lanes
@@ -1218,319 +1249,352 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense decoder: token-dense blocks of short matches at scattered distances (attach-time
-// classification, lz4_dense_mode): noisy doubles (~7.5 K sequences of ~5 literal bytes and a ~4-byte
-// copy at a random distance, copy chains of <= ~24 hops). Blocks of 8-byte value runs (sequential
-// longs, timestamps: copies at distance 8 chaining through the whole block) stay on the general
-// decoder's class mode. Instead of the general decoder's 16-bit entry per output byte, the block is
-// resolved in place in a byte image of the output + one resolved bit per byte, beside the staged
-// input (which stays: literals are copied LDS to LDS). One thread per checkpoint interval (<= 8
-// sequences, kept in registers):
-//   1. stage the compressed block; parse; a block scan of the output lengths places the sequences;
-//   2. literal bytes go to the image and their bits are set (runs over kDnShortLit bytes are copied
-//      by the whole workgroup);
-//   3. rounds: every match whose source bytes (its first period) are all resolved copies them and
-//      sets its bits (a thread's reads for all its matches issued together); the attach-time
-//      simulation bounds the rounds (kDnMaxRounds);
-//   4. the image goes out in 16-byte chunks (out16: slots, or 8-byte values to the payload records).
+// Class-8 decoder (blocks of 8-byte values that change in a few low bytes per row: sequential longs,
+// sorted timestamps; lz4_c8_mode). When a match copies from exactly 8 bytes back, output byte x equals
+// the last byte written at or before x in its residue class x mod 8, so a "class register" of 8
+// entries is all the state the decoder needs: a literal byte writes its class, a distance-8 copy
+// leaves the register unchanged, and the 8 bytes of qword v are the register after position 8v + 7.
+// Bytes of matches at other distances ("exceptions", a few hundred per block at most) write their
+// class with a value found later. An entry is 16 bits: a byte value, or 0x8000 | the ordinal of the
+// exception byte that wrote it. Thread t owns checkpoint interval t (<= 8 sequences) and every qword
+// whose last byte lies in it:
+//   1. parse: output length, exception count and class transfer (classes written, the last entry of
+//      each; positions relative to the interval start);
+//   2. block scan of lengths / exception counts; transfer rotated to absolute classes; block scan of
+//      transfers (later writes win) = the register entering each interval;
+//   3. exceptions: each finds the entry its source position (taken before its match's start) holds,
+//      by replaying the owning interval from its entering register; pointer jumping over the
+//      exception -> exception links (log of the chain length) leaves every exception a value;
+//   4. re-walk from the entering register (exception entries replaced by their values), writing each
+//      completed qword into the LDS image; 5. 16-byte chunks of the image to the slot / payload
+//      records / fused aggregate.
+// ~8 sequences and ~8 qwords per thread in registers, against the general decoder's per-byte image.
 // ------------------------------------------------------------------------------------------------
-constexpr int kDnWaves = kDnThreads / 64;
-constexpr int kDnSeq = kLzSeqPerCp;                      // sequences per thread (one checkpoint interval)
-constexpr int kDnResWords = kBlockBytes / 32;            // resolved bits
-constexpr int kDnInWords = (kLz4InCap + 32) / 4;         // staged input (+ zero pad)
-static_assert(kDnThreads >= kLzMaxCps, "one checkpoint interval per dense-decoder thread");
+constexpr int kC8Threads = kLzMaxCps;  // one checkpoint interval per thread
+constexpr int kC8Waves = kC8Threads / 64;
+constexpr int kC8InWords = (kLz4InCap + 32) / 4;  // staged input (+ zero pad)
+constexpr uint64_t kC8Exc4 = 0x8000800080008000ull;
 
+__device__ __forceinline__ uint32_t c8_lit(const uint8_t* s_in, const Tok& t, int k) {
+  return t.L <= 4 ? (t.lv >> (8 * k)) & 0xFFu : (uint32_t)s_in[t.lit + k];
+}
 
-// OR of the bits of positions [a, b) into the resolved map, one LDS atomic per word touched
-__device__ __forceinline__ void res_set(uint32_t* s_res, int a, int b) {
-  while (a < b) {
-    const int w = a >> 5, lo = a & 31, hi = min(b - (w << 5), 32);
-    const uint32_t m = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-    atomicOr(&s_res[w], m);
-    a = (w + 1) << 5;
+// the class register: entries of classes 0-3 in lo, 4-7 in hi (16 bits each)
+struct C8Reg {
+  uint64_t lo, hi;
+};
+__device__ __forceinline__ void c8_put(C8Reg& r, int x, uint32_t e) {
+  const int c = x & 7, sh = (c & 3) * 16;
+  const uint64_t m = ~(0xFFFFull << sh), v = (uint64_t)e << sh;
+  if (c < 4) r.lo = (r.lo & m) | v;
+  else r.hi = (r.hi & m) | v;
+}
+__device__ __forceinline__ uint32_t c8_get(const C8Reg& r, int x) {
+  const int c = x & 7;
+  return (uint32_t)(((c < 4 ? r.lo : r.hi) >> ((c & 3) * 16)) & 0xFFFF);
+}
+// 16-bit lanes of the 4-bit class mask m
+__device__ __forceinline__ uint64_t c8_lanes(uint32_t m) {
+  return ((m & 1) ? 0xFFFFull : 0) | ((m & 2) ? 0xFFFFull << 16 : 0) | ((m & 4) ? 0xFFFFull << 32 : 0) |
+         ((m & 8) ? 0xFFFFull << 48 : 0);
+}
+// a then b (b's entries win in b's classes)
+__device__ __forceinline__ void c8_compose(C8Reg& a, uint32_t& am, const C8Reg& b, uint32_t bm) {
+  a.lo = (a.lo & ~c8_lanes(bm & 15)) | b.lo;
+  a.hi = (a.hi & ~c8_lanes(bm >> 4)) | b.hi;
+  am |= bm;
+}
+// 8 byte values from a register of resolved entries
+__device__ __forceinline__ uint64_t c8_bytes(const C8Reg& r) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    v |= ((r.lo >> (16 * c)) & 0xFF) << (8 * c);
+    v |= ((r.hi >> (16 * c)) & 0xFF) << (8 * (c + 4));
   }
-}
-
-// all bits of positions [a, b) set
-__device__ __forceinline__ bool res_all(const uint32_t* s_res, int a, int b) {
-  bool ok = true;
-  while (a < b && ok) {
-    const int w = a >> 5, lo = a & 31, hi = min(b - (w << 5), 32);
-    const uint32_t m = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-    ok = (s_res[w] & m) == m;
-    a = (w + 1) << 5;
-  }
-  return ok;
-}
-
-__device__ __forceinline__ uint32_t bits_of(int a, int b) {  // positions [a, b) of one 32-bit word, a <= b <= a + 32
-  const int lo = a & 31, hi = lo + (b - a);
-  return (hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-}
-
-// OR the low `len` (<= 8) bytes of w into the zero-initialised image at byte position x: at most three
-// dword ORs (bytes of other runs in the same dwords are disjoint)
-__device__ __forceinline__ void img_or(uint32_t* s_img32, int x, int len, uint64_t w) {
-  if (len < 8) w &= (1ull << (8 * len)) - 1ull;
-  const int sh = (x & 3) * 8, q = x >> 2;
-  const uint32_t d0 = (uint32_t)(w << sh);
-  const uint32_t d1 = (uint32_t)((sh ? (w >> (32 - sh)) : (w >> 32)));
-  const uint32_t d2 = sh ? (uint32_t)(w >> (64 - sh)) : 0u;
-  if (d0) atomicOr(&s_img32[q], d0);
-  if (d1) atomicOr(&s_img32[q + 1], d1);
-  if (d2) atomicOr(&s_img32[q + 2], d2);
-}
-
-// the residue classes mod 8 of positions [a, a + k)
-__device__ __forceinline__ uint32_t classes_of(int a, int k) {
-  if (k >= 8) return 0xFFu;
-  const uint32_t m = (1u << k) - 1u;
-  return ((m << (a & 7)) | (m >> (8 - (a & 7)))) & 0xFFu;
+  return v;
 }
 
 template <bool PROF>
-__global__ __launch_bounds__(kDnThreads) void k_lz4_dense(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
-                                                          uint64_t* __restrict__ prof) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_in32[kDnInWords];    // staged compressed block
-  __shared__ __attribute__((aligned(16))) uint32_t s_img32[kBlockBytes / 4];  // decoded image
-  __shared__ uint32_t s_res[kDnResWords];                                   // resolved bits
-  __shared__ uint32_t s_aux[3 * kDnMaxLongLit];  // long literal runs: output start, input offset, length
-  __shared__ int s_tmp[kDnWaves];
-  __shared__ int s_bad, s_nlj;
+__global__ __launch_bounds__(kC8Threads) void k_lz4_c8(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+                                                       uint64_t* __restrict__ prof) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_in32[kC8InWords];  // staged compressed block
+  // the decoded image; until step 4 it holds the intervals' entering registers and starts
+  __shared__ __attribute__((aligned(16))) uint64_t s_img[kBlockBytes / 8];
+  __shared__ uint16_t s_esrc[kC8MaxExc];  // exception byte -> its source position
+  __shared__ uint16_t s_link[kC8MaxExc];  // exception byte -> entry (value, or a link to another)
+  __shared__ int s_tmp[kC8Waves];
+  __shared__ uint64_t s_wlo[kC8Waves], s_whi[kC8Waves];
+  __shared__ uint32_t s_wm[kC8Waves];
+  __shared__ uint64_t s_red[kC8Waves];
+  __shared__ int s_bad;
+  static_assert(kC8Threads * 20 <= kBlockBytes, "entering registers + starts fit the image");
+  C8Reg* s_ent = reinterpret_cast<C8Reg*>(s_img);                           // [kC8Threads]
+  uint32_t* s_start = reinterpret_cast<uint32_t*>(s_img + 2 * kC8Threads);  // base | ebase << 17
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = job.src_len, ncp = job.ncp;
-  if (job.dense != kDnModeRounds || n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.wide || job.dec_len > kBlockBytes ||
-      job.dec_len < job.expect_len) {
+  if (!job.c8 || n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kC8Threads || job.wide ||
+      job.dec_len > kBlockBytes || job.dec_len < job.expect_len) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
   LZ_STAMP(0);
   uint8_t* s_in = reinterpret_cast<uint8_t*>(s_in32);
-  uint8_t* s_img = reinterpret_cast<uint8_t*>(s_img32);
-  // ---- stage the compressed block (16-byte aligned and padded in the device image): every load of a
-  // thread issued before the first store ----
   {
     uint4* dst = reinterpret_cast<uint4*>(s_in32);
     const int n16 = (n + 15) >> 4;
-    constexpr int kPer = (kLz4InCap + 16 * kDnThreads - 1) / (16 * kDnThreads);
+    constexpr int kPer = (kLz4InCap + 16 * kC8Threads - 1) / (16 * kC8Threads);
     uint4 v[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
-      if (tid + k * kDnThreads < n16) v[k] = gld16(job.src + 16 * (size_t)(tid + k * kDnThreads));
+      if (tid + k * kC8Threads < n16) v[k] = gld16(job.src + 16 * (size_t)(tid + k * kC8Threads));
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
-      if (tid + k * kDnThreads < n16) dst[tid + k * kDnThreads] = v[k];
+      if (tid + k * kC8Threads < n16) dst[tid + k * kC8Threads] = v[k];
     if (tid == 0) {
       dst[n16] = make_uint4(0, 0, 0, 0);
       s_bad = 0;
-      s_nlj = 0;
     }
-    for (int i = tid; i < kDnResWords; i += kDnThreads) s_res[i] = 0;
-    uint4* img4 = reinterpret_cast<uint4*>(s_img32);
-    for (int i = tid; i < kBlockBytes / 16; i += kDnThreads) img4[i] = make_uint4(0, 0, 0, 0);  // (bytes are ORed in)
   }
   __syncthreads();
   LZ_STAMP(1);
-  // ---- 1. parse my interval into registers. Sequence s: r_a = distance | literal length << 16,
-  // r_b = match start | match length << 17 (output positions, relative until the scan), r_lit =
-  // literal input offset ----
-  uint32_t r_a[kDnSeq], r_b[kDnSeq], r_lit[kDnSeq];
-#pragma unroll
-  for (int s = 0; s < kDnSeq; ++s) r_a[s] = r_b[s] = r_lit[s] = 0;
-  int out_rel = 0;
+  const int p0 = tid < ncp ? (int)gld4(job.cp + tid) : n;
+  const int end = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
+  // ---- 1. transfer of my interval (relative classes), length, exception count ----
+  C8Reg tr = {0, 0};
+  uint32_t tm = 0;
+  int len = 0, ne = 0;
   bool bad = false;
-  if (tid < ncp) {
-    int pos = (int)gld4(job.cp + tid);
-    const int end = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
-#pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {
-      if (pos < end) {
-        Tok t;
-        if (parse_tok(s_in, n, pos, t) && t.M <= kDnMaxRun && t.L < 65536) {
-          r_a[s] = (uint32_t)t.off | ((uint32_t)t.L << 16);
-          r_b[s] = (uint32_t)(out_rel + t.L) | ((uint32_t)t.M << 17);
-          r_lit[s] = (uint32_t)t.lit;
-          out_rel += t.L + t.M;
-          pos = t.next;
-        } else {
-          pos = -1;
-        }
+  {
+    int pos = p0;
+    for (int s = 0; s < kLzSeqPerCp && pos < end; ++s) {
+      Tok t;
+      if (!parse_tok(s_in, n, pos, t)) {
+        bad = true;
+        break;
       }
+      for (int k = max(0, t.L - 8); k < t.L; ++k) {  // (earlier bytes of the run: overwritten)
+        c8_put(tr, len + k, c8_lit(s_in, t, k));
+        tm |= 1u << ((len + k) & 7);
+      }
+      len += t.L;
+      if (t.M && t.off != 8) {
+        for (int k = max(0, t.M - 8); k < t.M; ++k) {
+          c8_put(tr, len + k, 0x8000u | (uint32_t)(ne + k));
+          tm |= 1u << ((len + k) & 7);
+        }
+        ne += t.M;
+      }
+      len += t.M;
+      pos = t.next;
     }
-    bad = pos != end;
+    if (tid < ncp && pos != end) bad = true;
   }
-  int x = out_rel;
+  // ---- 2. block scan of (length | exception count << 18) ----
+  int base, ebase, total, nexc;
+  {
+    const int mine = len | (ne << 18);
+    int x = mine;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) s_tmp[wave] = x;
+    if (bad) s_bad = 1;
+    __syncthreads();
+    int pre = x - mine, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kC8Waves; ++w) {
+      const int y = s_tmp[w];
+      pre += w < wave ? y : 0;
+      tot += y;
+    }
+    base = pre & ((1 << 18) - 1);
+    ebase = pre >> 18;
+    total = tot & ((1 << 18) - 1);
+    nexc = tot >> 18;
   }
-  if (lane == 63) s_tmp[wave] = x;
-  if (bad) s_bad = 1;
-  __syncthreads();
-  int base = x - out_rel, total = 0;
-#pragma unroll
-  for (int w = 0; w < kDnWaves; ++w) {
-    const int y = s_tmp[w];
-    base += w < wave ? y : 0;
-    total += y;
+  if (s_bad || total != job.dec_len || nexc > kC8MaxExc) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
   }
   LZ_STAMP(2);
-  if (s_bad || total != job.dec_len) {
-    if (tid == 0) atomicOr(err, 1);
-    return;
+  // exception ordinals absolute; classes absolute (rotate the 8 entries by base mod 8)
+  tr.lo += ((tr.lo & kC8Exc4) >> 15) * (uint64_t)ebase;
+  tr.hi += ((tr.hi & kC8Exc4) >> 15) * (uint64_t)ebase;
+  {
+    int r = base & 7;
+    if (r >= 4) {
+      const uint64_t t = tr.lo;
+      tr.lo = tr.hi;
+      tr.hi = t;
+      r -= 4;
+    }
+    if (r) {
+      const int sh = 16 * r;
+      const uint64_t lo = (tr.lo << sh) | (tr.hi >> (64 - sh)), hi = (tr.hi << sh) | (tr.lo >> (64 - sh));
+      tr.lo = lo;
+      tr.hi = hi;
+    }
+    const int rb = base & 7;
+    tm = ((tm << rb) | (tm >> (8 - rb))) & 0xFFu;
   }
+  // block scan of the transfers: inclusive in the wave, then the earlier waves' totals
+  C8Reg inc = tr;
+  uint32_t im = tm;
 #pragma unroll
-  for (int s = 0; s < kDnSeq; ++s) r_b[s] += (uint32_t)base;  // (an absent sequence: empty, at my range's end)
-  // ---- 2. literal bytes -> image + resolved bits; `unres`: my matches still to resolve ----
-  uint32_t unres = 0;
-#pragma unroll
-  for (int s = 0; s < kDnSeq; ++s) {
-    const int L = (int)(r_a[s] >> 16), d = (int)(r_a[s] & 0xFFFF);
-    const int xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17), o = xm - L, lit = (int)r_lit[s];
-    if (L > kDnShortLit) {
-      const int j = atomicAdd(&s_nlj, 1);
-      if (j < kDnMaxLongLit) {
-        s_aux[3 * j] = (uint32_t)o;
-        s_aux[3 * j + 1] = (uint32_t)lit;
-        s_aux[3 * j + 2] = (uint32_t)L;
-      } else {
-        s_bad = 1;  // (more than the attach-time classification allows)
-      }
-    } else if (L > 0) {
-      // up to kDnShortLit bytes: dwords of the staged input, realigned, written bytewise
-#pragma unroll 1
-      for (int k0 = 0; k0 < L; k0 += 8) {
-        const int q = (lit + k0) >> 2, sh = (lit + k0) & 3;
-        const uint32_t a0 = s_in32[q], a1 = s_in32[q + 1], a2 = s_in32[q + 2];
-        const uint32_t v0 = __builtin_amdgcn_alignbyte(a1, a0, sh), v1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
-        img_or(s_img32, o + k0, min(8, L - k0), (uint64_t)v0 | ((uint64_t)v1 << 32));
-      }
-      res_set(s_res, o, xm);
+  for (int o = 1; o < 64; o <<= 1) {
+    C8Reg p;
+    p.lo = __shfl_up((unsigned long long)inc.lo, o, 64);
+    p.hi = __shfl_up((unsigned long long)inc.hi, o, 64);
+    uint32_t pm = __shfl_up(im, o, 64);
+    if (lane >= o) {
+      c8_compose(p, pm, inc, im);
+      inc = p;
+      im = pm;
     }
-    if (M > 0) {
-      if (d > xm) s_bad = 1;  // a copy from before the block
-      unres |= 1u << s;
-    }
+  }
+  C8Reg ent;
+  ent.lo = __shfl_up((unsigned long long)inc.lo, 1, 64);
+  ent.hi = __shfl_up((unsigned long long)inc.hi, 1, 64);
+  uint32_t em = __shfl_up(im, 1, 64);
+  if (lane == 0) {
+    ent.lo = ent.hi = 0;
+    em = 0;
+  }
+  if (lane == 63) {
+    s_wlo[wave] = inc.lo;
+    s_whi[wave] = inc.hi;
+    s_wm[wave] = im;
   }
   __syncthreads();
-  if (s_bad) {
-    if (tid == 0) atomicOr(err, 1);
-    return;
-  }
-  if (s_nlj > 0) {  // the long literal runs, every thread a byte of each (then their bits, by word)
-    const int nlj = s_nlj;
-    for (int j = 0; j < nlj; ++j) {
-      const int o = (int)s_aux[3 * j], lit = (int)s_aux[3 * j + 1], L = (int)s_aux[3 * j + 2];
-      for (int i = tid; i < L; i += kDnThreads) atomicOr(&s_img32[(o + i) >> 2], (uint32_t)s_in[lit + i] << (8 * ((o + i) & 3)));
-      for (int w = (o >> 5) + tid; w <= ((o + L - 1) >> 5); w += kDnThreads) res_set(s_res, max(o, w << 5), min(o + L, (w + 1) << 5));
+  {
+    C8Reg pre = {0, 0};
+    uint32_t pm = 0;
+    for (int w = 0; w < wave; ++w) {
+      const C8Reg b = {s_wlo[w], s_whi[w]};
+      c8_compose(pre, pm, b, s_wm[w]);
     }
-    __syncthreads();
+    c8_compose(pre, pm, ent, em);
+    ent = pre;
   }
-  LZ_STAMP(3);
-  LZ_STAMP(4);
-  int rounds = 0;
-  // ---- 3'. rounds: each match whose source bytes (its first period) are resolved copies them;
-  // a thread's reads for all its matches go out together ----
-  for (;; ++rounds) {
-    if (!__syncthreads_or(unres != 0)) break;
-    if (rounds > kDnMaxRounds + 1) {  // beyond the attach-time bound: not a block of this kind
+  // ---- 3. exceptions: source positions, entries at the sources, pointer jumping ----
+  if (nexc) {
+    s_ent[tid] = ent;
+    s_start[tid] = (uint32_t)base | ((uint32_t)ebase << 17);
+    if (ne) {  // my exception bytes' sources
+      int pos = p0, x = base, ei = ebase;
+      for (int s = 0; s < kLzSeqPerCp && pos < end; ++s) {
+        Tok t;
+        parse_tok(s_in, n, pos, t);
+        x += t.L;
+        if (t.M && t.off != 8) {
+          const int d = t.off;
+          for (int k = 0; k < t.M; ++k, ++ei) {
+            const int src = (d >= t.M || k < d) ? x + k - d : x - d + k % d;
+            bad |= src < 0;
+            s_esrc[ei] = (uint16_t)max(src, 0);
+          }
+        }
+        x += t.M;
+        pos = t.next;
+      }
+    }
+    if (bad) s_bad = 1;
+    __syncthreads();
+    if (s_bad) {
       if (tid == 0) atomicOr(err, 1);
       return;
     }
-#pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {  // (no loop-invariant copies of the fields: VGPR budget)
-      asm volatile("" : "+v"(r_a[s]));
-      asm volatile("" : "+v"(r_b[s]));
-      asm volatile("" : "+v"(r_lit[s]));
-    }
-    uint32_t rw[kDnSeq][2];
-#pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {
-      rw[s][0] = rw[s][1] = 0;
-      if ((unres >> s) & 1u) {
-        const int d = (int)(r_a[s] & 0xFFFF), xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
-        const int a = xm - d, e = a + min(M, d);
-        rw[s][0] = s_res[a >> 5];
-        rw[s][1] = s_res[(e - 1) >> 5];
+    for (int e = tid; e < nexc; e += kC8Threads) {
+      const int y = s_esrc[e];
+      int lo = 0, hi = ncp - 1;  // the last interval starting at or before y
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)(s_start[mid] & ((1u << 17) - 1)) <= y) lo = mid;
+        else hi = mid - 1;
       }
-    }
-    uint32_t ok = 0;
-#pragma unroll
-    for (int s = 0; s < kDnSeq; ++s) {
-      if ((unres >> s) & 1u) {
-        const int d = (int)(r_a[s] & 0xFFFF), xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
-        const int a = xm - d, e = a + min(M, d);
-        bool y;
-        if ((a >> 5) == ((e - 1) >> 5)) {
-          const uint32_t m = bits_of(a, e);
-          y = (rw[s][0] & m) == m;
-        } else if ((a >> 5) + 1 == ((e - 1) >> 5)) {
-          const uint32_t m0 = bits_of(a, (a | 31) + 1), m1 = bits_of((e - 1) & ~31, e);
-          y = (rw[s][0] & m0) == m0 && (rw[s][1] & m1) == m1;
+      C8Reg r = s_ent[lo];
+      int x = (int)(s_start[lo] & ((1u << 17) - 1)), ei = (int)(s_start[lo] >> 17);
+      int pos = (int)gld4(job.cp + lo);
+      const int pe = lo + 1 < ncp ? (int)gld4(job.cp + lo + 1) : n;
+      for (int s = 0; s < kLzSeqPerCp && pos < pe && x <= y; ++s) {
+        Tok t;
+        parse_tok(s_in, n, pos, t);
+        for (int k = 0; k < t.L && x <= y; ++k, ++x) c8_put(r, x, c8_lit(s_in, t, k));
+        if (x > y) break;
+        if (t.M && t.off != 8) {
+          for (int k = 0; k < t.M && x <= y; ++k, ++x, ++ei) c8_put(r, x, 0x8000u | (uint32_t)ei);
         } else {
-          y = res_all(s_res, a, e);
+          x += t.M;
         }
-        ok |= y ? 1u << s : 0u;
+        pos = t.next;
+      }
+      s_link[e] = (uint16_t)c8_get(r, y);
+    }
+    __syncthreads();
+    for (int round = 0;; ++round) {
+      bool open = false;
+      for (int e = tid; e < nexc; e += kC8Threads) {
+        const uint32_t l = s_link[e];
+        if (l & 0x8000u) {
+          const uint32_t l2 = s_link[l & 0x7FFFu];  // (an earlier exception: links never cycle)
+          s_link[e] = (uint16_t)l2;
+          open |= (l2 & 0x8000u) != 0;
+        }
+      }
+      if (!__syncthreads_or(open)) break;
+      if (round > 10) {  // 2^11 > kC8MaxExc: a longer chain means a malformed link
+        if (tid == 0) atomicOr(err, 1);
+        return;
       }
     }
-    if (ok) {
-      // (a bit seen set by another wave this round: the bytes were written before it)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      uint32_t sw[kDnSeq][3];  // sources of the short non-overlapping copies: three dwords
+    // my entering register's exception entries -> their values
 #pragma unroll
-      for (int s = 0; s < kDnSeq; ++s) {
-        sw[s][0] = sw[s][1] = sw[s][2] = 0;
-        const int d = (int)(r_a[s] & 0xFFFF), M = (int)(r_b[s] >> 17);
-        if (((ok >> s) & 1u) && d >= M && M <= 8) {
-          const int aw = ((int)(r_b[s] & 0x1FFFF) - d) >> 2;
-          sw[s][0] = s_img32[aw];
-          sw[s][1] = s_img32[aw + 1];
-          sw[s][2] = s_img32[aw + 2];
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < kDnSeq; ++s) {
-        if ((ok >> s) & 1u) {
-          const int d = (int)(r_a[s] & 0xFFFF), xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
-          const int a = xm - d;
-          if (d >= M && M <= 8) {
-            const int sh = a & 3;
-            const uint32_t v0 = __builtin_amdgcn_alignbyte(sw[s][1], sw[s][0], sh);
-            const uint32_t v1 = __builtin_amdgcn_alignbyte(sw[s][2], sw[s][1], sh);
-            img_or(s_img32, xm, M, (uint64_t)v0 | ((uint64_t)v1 << 32));
-          } else {
-#pragma unroll 1
-            for (int k = 0, r = 0; k < M; ++k) {  // LZ4 overlap: byte k copies the first period
-              atomicOr(&s_img32[(xm + k) >> 2], (uint32_t)s_img[a + r] << (8 * ((xm + k) & 3)));
-              if (++r == d) r = 0;
-            }
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#pragma unroll
-      for (int s = 0; s < kDnSeq; ++s)
-        if ((ok >> s) & 1u) {
-          const int xm = (int)(r_b[s] & 0x1FFFF), M = (int)(r_b[s] >> 17);
-          res_set(s_res, xm, xm + M);
-        }
-      unres &= ~ok;
+    for (int c = 0; c < 8; ++c) {
+      const uint32_t e = c8_get(ent, c);
+      if (e & 0x8000u) c8_put(ent, c, s_link[e & 0x7FFFu]);
     }
   }
-  LZ_STAMP(5);
-  if (PROF && tid == 0) {
-    prof[(size_t)blockIdx.x * kLz4ProfWords + 8] = (uint64_t)rounds;
-    prof[(size_t)blockIdx.x * kLz4ProfWords + 9] = (uint64_t)n;
-    prof[(size_t)blockIdx.x * kLz4ProfWords + 10] = (uint64_t)s_nlj;
-    prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
+  LZ_STAMP(3);
+  __syncthreads();  // (the image region held the entering registers)
+  // ---- 4. re-walk: completed qwords into the image ----
+  if (tid < ncp) {
+    uint64_t S = c8_bytes(ent);
+    int pos = p0, x = base, ei = ebase;
+    for (int s = 0; s < kLzSeqPerCp && pos < end; ++s) {
+      Tok t;
+      parse_tok(s_in, n, pos, t);
+      for (int k = 0; k < t.L; ++k, ++x) {
+        const int c = (x & 7) * 8;
+        S = (S & ~(0xFFull << c)) | ((uint64_t)c8_lit(s_in, t, k) << c);
+        if ((x & 7) == 7) s_img[x >> 3] = S;
+      }
+      if (t.M && t.off != 8) {
+        for (int k = 0; k < t.M; ++k, ++x, ++ei) {
+          const int c = (x & 7) * 8;
+          S = (S & ~(0xFFull << c)) | ((uint64_t)(s_link[ei] & 0xFF) << c);
+          if ((x & 7) == 7) s_img[x >> 3] = S;
+        }
+      } else if (t.M) {
+        for (int y = x | 7; y < x + t.M; y += 8) s_img[y >> 3] = S;
+        x += t.M;
+      }
+      pos = t.next;
+    }
+    // the block's partial last qword (its bytes past the end zeroed)
+    if (x == total && (total & 7)) s_img[total >> 3] = S & ((1ull << (8 * (total & 7))) - 1);
   }
   __syncthreads();
-  // ---- 4. output: 16-byte chunks of the image ----
+  LZ_STAMP(4);
+  LZ_STAMP(5);
+  // ---- 5. output: 16-byte chunks of the image ----
   const int nchunks = (total + 15) >> 4;
-  const uint4* img16 = reinterpret_cast<const uint4*>(s_img32);
-  for (int c = tid; c < nchunks; c += kDnThreads) {
+  const uint4* img16 = reinterpret_cast<const uint4*>(s_img);
+  uint64_t racc = job.red_dst ? identity_of(job.red_op, job.red_kind) : 0ull;
+  for (int c = tid; c < nchunks; c += kC8Threads) {
     const uint4 v = img16[c];
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
     const int rem = total - 16 * c;
@@ -1541,18 +1605,19 @@ __global__ __launch_bounds__(kDnThreads) void k_lz4_dense(const Lz4Job* __restri
         w[q] &= keep == 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
       }
     }
-    out16(job, c, w);
+    out16(job, c, w, racc);
   }
+  if (job.red_dst) red_finish(job, racc, s_red, kC8Waves);
   if (PROF) {
     __syncthreads();
     LZ_STAMP(6);
   }
 }
 
-void launch_lz4_dense(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
+void launch_lz4_c8(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
-  if (d_prof) hipLaunchKernelGGL(k_lz4_dense<true>, dim3(njobs), dim3(kDnThreads), 0, s, d_jobs, d_err, d_prof);
-  else hipLaunchKernelGGL(k_lz4_dense<false>, dim3(njobs), dim3(kDnThreads), 0, s, d_jobs, d_err, nullptr);
+  if (d_prof) hipLaunchKernelGGL(k_lz4_c8<true>, dim3(njobs), dim3(kC8Threads), 0, s, d_jobs, d_err, d_prof);
+  else hipLaunchKernelGGL(k_lz4_c8<false>, dim3(njobs), dim3(kC8Threads), 0, s, d_jobs, d_err, nullptr);
 }
 
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {

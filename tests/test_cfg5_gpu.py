@@ -173,3 +173,48 @@ def test_uniform_time_blocks_are_not_decoded(R, cfg5, kind, monkeypatch):
         (a, bytes_skip), (b, bytes_all) = runs["skip"], runs["decode"]
         assert bytes_skip < bytes_all, (bytes_skip, bytes_all)
         assert_results(q, a, b)
+
+
+@pytest.mark.parametrize("shape", ["hourly", "hourly_cut", "all", "day_desc", "filtered"])
+def test_fused_decode_aggregate(Q, O, R, cfg5, shape, monkeypatch):
+    """Timeseries decode fused with aggregation: the LZ4 value blocks whose rows share one bucket are
+    folded by the decoder into the bucket's slot (no decoded image written, the scan skips their
+    rows). Results equal the unfused path (DG_NO_FUSE=1) and the oracle, for every aggregator kind of
+    configs[4]a (longSum, doubleSum, longMax, doubleMin), an interval cutting blocks, ALL granularity
+    (one bucket: every value block fused), a descending day query, and a filtered query (not fused)."""
+    B, g, o = cfg5
+    base = B.make_query(Q, "ts_hourly")
+    aggs = base.aggregations + [Q.long_min("lmin", "maxLongUniform"), Q.double_max("dmax", "sumFloatNormal")]
+    lo, hi = g[0].min_time + 1_234_567, g[-1].max_time - 7_654_321
+    iv = ["1970-01-01/2020-01-01"]
+    kw = {}
+    if shape == "hourly":
+        q = Q.TimeseriesQuery(intervals=iv, granularity="hour", aggregations=aggs)
+    elif shape == "hourly_cut":
+        q = Q.TimeseriesQuery(intervals=[(lo, hi)], granularity="hour", aggregations=aggs)
+    elif shape == "all":
+        q = Q.TimeseriesQuery(intervals=iv, granularity="all", aggregations=aggs)
+    elif shape == "day_desc":
+        q = Q.TimeseriesQuery(intervals=[(lo, hi)], granularity="day", aggregations=aggs, descending=True)
+    else:
+        q = Q.TimeseriesQuery(intervals=iv, granularity="hour", aggregations=aggs,
+                              filter=Q.BoundDimFilter("dimSequential", "100", "500"))
+    runs = {}
+    for mode in ("fused", "plain"):
+        if mode == "plain":
+            monkeypatch.setenv("DG_NO_FUSE", "1")
+        else:
+            monkeypatch.delenv("DG_NO_FUSE", raising=False)
+        stats = R.RunStats()
+        runs[mode] = (R.run_query(q, g, stats), stats.total("lz4_fused_blocks"))
+    monkeypatch.delenv("DG_NO_FUSE", raising=False)
+    (a, nf), (b, n0) = runs["fused"], runs["plain"]
+    assert n0 == 0
+    if shape == "filtered":
+        assert nf == 0
+    else:
+        # configs[4]a's value columns: 4 columns x ~183 blocks per 1.5 M-row segment; only blocks at
+        # bucket edges (and light blocks) are decoded
+        assert nf > (0.97 if shape == "all" else 0.5) * 4 * NSEG * (ROWS // 8192), nf
+    assert_results(q, a, b)
+    assert_results(q, a, O.run(q, o))
