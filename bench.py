@@ -647,10 +647,9 @@ def main():
     bytes_read = per_step("bytes_read")
     bytes_side = per_step("bytes_side")
     kernels = {}  # phase -> (kernel, algorithmic bytes per launch, launches per step, ms per step)
-    dk = "k_lzf_decode" if args.compression == "lzf" else "k_lz4_light+k_lz4_c8+k_lz4_decode"
+    dk = "k_lzf_decode" if args.compression == "lzf" else "k_lz4_light+k_lz4_decode"
     if phases["decode"] > 0:
-        # LZ4: the light (literal-heavy blocks), class-8 (8-byte value runs) and general decoders, all
-        # inside the phase
+        # LZ4: the light decoder (literal-heavy blocks) and the general one, both inside the phase
         kernels["decode"] = (dk if args.long_encoding == "longs" else dk + "+k_vsize_expand", bytes_read - bytes_side, 1,
                              phases["decode"])
     if per_step("decode_side_ms") > 0:
@@ -664,14 +663,8 @@ def main():
         phases["lz4_general"] = per_step("lz4_general_ms")
         kernels["lz4_general"] = ("k_lz4_decode", per_step("lz4_general_bytes"),
                                   max(per_step("lz4_general_launches"), 1.0), phases["lz4_general"])
-    if per_step("lz4_c8_ms") > 0:
-        # the class-8 LZ4 decoder (8-byte value runs: sequential longs, timestamps), the same way
-        phases["lz4_c8"] = per_step("lz4_c8_ms")
-        kernels["lz4_c8"] = ("k_lz4_c8", per_step("lz4_c8_bytes"), max(per_step("lz4_c8_launches"), 1.0),
-                             phases["lz4_c8"])
     # LZ4 blocks per step by decoder (and those whose decode was fused with their aggregator)
-    lz4_blocks = {"general": per_step("lz4_general_blocks"), "class8": per_step("lz4_c8_blocks"),
-                  "fused": per_step("lz4_fused_blocks")}
+    lz4_blocks = {"general": per_step("lz4_general_blocks"), "fused": per_step("lz4_fused_blocks")}
     if isinstance(query, Q.GroupByQuery):
         phases.update({"keygen": per_step("keygen_ms"), "sort": per_step("sort_ms"), "reduce": per_step("reduce_ms"),
                        "reduce_kernels": per_step("reduce_kernel_ms")})
@@ -699,7 +692,7 @@ def main():
     # the dominant kernel: the longest single-kernel span (phases that group several kernels, like the
     # decode phase or the side-stream payload decode, are reported in phases_ms)
     single = {k: v for k, v in kernels.items()
-              if k in ("lz4_general", "lz4_c8", "aggregate", "bitmap", "sort", "keygen", "reduce")}
+              if k in ("lz4_general", "aggregate", "bitmap", "sort", "keygen", "reduce")}
     dom = max(single or kernels, key=lambda k: (single or kernels)[k][3]) if kernels else None
     roofline = None
     if dom is not None:

@@ -204,7 +204,7 @@ typedef struct {
   /* groupBy: payload columns decoded in place on the side stream, overlapping the key build + sort */
   double decode_side_ms;     /* device time of those decodes (their own stream) */
   int64_t bytes_side;        /* their algorithmic bytes (part of bytes_read) */
-  /* the general LZ4 decoder (token-dense blocks the class-8 decoder does not take), both streams: device
+  /* the general LZ4 decoder (token-dense blocks: 8-byte value runs, noisy doubles), both streams: device
      time of its launches, the stored bytes and number of the blocks it decoded, and its launches */
   double lz4_general_ms;
   int64_t lz4_general_bytes;
@@ -218,12 +218,6 @@ typedef struct {
   /* since ABI 13: timeseries LZ4 blocks whose decode was fused with their aggregator (the decoder
      folded the block's values into its bucket's slot and wrote no decoded image) */
   int64_t lz4_fused_blocks;
-  /* the class-8 LZ4 decoder (k_lz4_c8: blocks whose matches copy from 8 bytes back, bar a few): device
-     time of its launches, stored bytes and number of its blocks, and its launches */
-  double lz4_c8_ms;
-  int64_t lz4_c8_bytes;
-  int32_t lz4_c8_blocks;
-  int32_t lz4_c8_launches;
 } dg_metrics;
 
 /* Aggregate values are returned in 8-byte slots: int64 for count/long*, double for double*,

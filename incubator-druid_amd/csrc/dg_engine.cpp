@@ -401,11 +401,6 @@ struct DecodeBatch {
   int32_t gen_blocks = 0;
   int32_t gen_launches = 0;
   int64_t fused_blocks = 0;  // blocks whose decode was fused with their aggregator (fused_agg_view)
-  // the same for the class-8 decoder
-  hipEvent_t c8_a = nullptr, c8_b = nullptr;
-  int64_t c8_bytes = 0;
-  int32_t c8_blocks = 0;
-  int32_t c8_launches = 0;
 };
 // device time of the general decoder's launches of a batch (0 if it launched none)
 static double gen_ms(const DecodeBatch& db) {
@@ -414,18 +409,10 @@ static double gen_ms(const DecodeBatch& db) {
   hipEventElapsedTime(&f, db.gen_a, db.gen_b);
   return f;
 }
-static double c8_ms(const DecodeBatch& db) {
-  if (!db.c8_blocks || !db.c8_a) return 0;
-  float f = 0;
-  hipEventElapsedTime(&f, db.c8_a, db.c8_b);
-  return f;
-}
 // the decode-timing events of a call's main (side = false) or side batch
 static void decode_events(Context* ctx, DecodeBatch* db, bool side) {
   db->gen_a = ctx->gen_ev[side ? 2 : 0];
   db->gen_b = ctx->gen_ev[side ? 3 : 1];
-  db->c8_a = ctx->gen_ev[side ? 6 : 4];
-  db->c8_b = ctx->gen_ev[side ? 7 : 5];
 }
 // a call's decode metrics from its main and side batches
 static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_metrics* m) {
@@ -434,10 +421,6 @@ static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_me
   m->lz4_general_blocks = db.gen_blocks + side.gen_blocks;
   m->lz4_general_launches = db.gen_launches + side.gen_launches;
   m->lz4_fused_blocks = db.fused_blocks + side.fused_blocks;
-  m->lz4_c8_ms = c8_ms(db) + c8_ms(side);
-  m->lz4_c8_bytes = db.c8_bytes + side.c8_bytes;
-  m->lz4_c8_blocks = db.c8_blocks + side.c8_blocks;
-  m->lz4_c8_launches = db.c8_launches + side.c8_launches;
 }
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
 static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st);
@@ -1056,7 +1039,7 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
   j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
   j.vstride = 0;
-  j.c8 = b.cp_c8.empty() ? 0 : b.cp_c8[k];
+  j.pad_ = 0;
   j.red_dst = nullptr;
   j.red_op = j.red_kind = j.red_vkind = j.red_pad = 0;
   return j;
@@ -1240,19 +1223,12 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   // per-thread sequence registers)
   // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
   // blocks per CU)
-  // class-8 blocks (8-byte value runs: k_lz4_c8) go first
-  // (DG_LZ4_NO_C8=1: those blocks to the general decoder, for same-box A/B and tests)
-  const char* no_c8 = getenv("DG_LZ4_NO_C8");
-  if (no_c8 && *no_c8 && *no_c8 != '0')
-    for (Lz4Job& j : db->jobs) j.c8 = 0;
   const int nh = (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.light; }) -
                        db->jobs.begin());
-  const int nd = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return j.c8 != 0; }) -
-                       db->jobs.begin());
-  const int nn = (int)(std::stable_partition(db->jobs.begin() + nd, db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
+  const int nn = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
                        db->jobs.begin());
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
-  if (nn - nd <= 16 * 256) std::stable_sort(db->jobs.begin() + nd, db->jobs.begin() + nn, by_ncp);
+  if (nn <= 16 * 256) std::stable_sort(db->jobs.begin(), db->jobs.begin() + nn, by_ncp);
   if (nh - nn <= 16 * 256) std::stable_sort(db->jobs.begin() + nn, db->jobs.begin() + nh, by_ncp);
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
@@ -1261,19 +1237,13 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
   launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
-  for (int i = 0; i < nd; ++i) db->c8_bytes += db->jobs[i].src_len;
-  db->c8_blocks += nd;
-  db->c8_launches += nd > 0;
-  if (db->c8_a && nd) hipEventRecord(db->c8_a, st);
-  launch_lz4_c8(d, nd, d_err, st, d_prof);
-  if (db->c8_a && nd) hipEventRecord(db->c8_b, st);
-  for (int i = nd; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
-  db->gen_blocks += nh - nd;
-  db->gen_launches += (nn - nd > 0) + (nh - nn > 0);
-  if (db->gen_a && nh > nd) hipEventRecord(db->gen_a, st);
-  launch_lz4_decode(d + nd, nn - nd, 0, d_err, st, d_prof ? d_prof + (size_t)nd * kLz4ProfWords : nullptr);
+  for (int i = 0; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
+  db->gen_blocks += nh;
+  db->gen_launches += (nn > 0) + (nh - nn > 0);
+  if (db->gen_a && nh) hipEventRecord(db->gen_a, st);
+  launch_lz4_decode(d, nn, 0, d_err, st, d_prof);
   launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
-  if (db->gen_a && nh > nd) hipEventRecord(db->gen_b, st);
+  if (db->gen_a && nh) hipEventRecord(db->gen_b, st);
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
 
@@ -4337,10 +4307,10 @@ int dg_timeseries_merge(const dg_scan* scan, int32_t n_lists, const int32_t* n, 
 extern "C" int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind) {
   if (!block || len <= 0 || len > kBlockBytes + 2048 || !kind) return set_error(DG_ERR_ARG, "bad arguments");
   std::vector<uint32_t> one;
-  int wide = 0, light = 0, nfine = 0, c8 = 0;
-  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine, &c8);
-  // -1 malformed, 0 general, 1 general (wide), 2 light, 4 class-8 (3: the removed dense decoder)
-  *kind = d < 0 ? -1 : light ? 2 : c8 ? 4 : wide ? 1 : 0;
+  int wide = 0, light = 0, nfine = 0;
+  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine);
+  // -1 malformed, 0 general, 1 general (wide), 2 light
+  *kind = d < 0 ? -1 : light ? 2 : wide ? 1 : 0;
   return DG_OK;
 }
 
@@ -4357,7 +4327,6 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.cp_n.resize(n);
   b.cp_wide.assign(n, 0);
   b.cp_light.assign(n, 0);
-  b.cp_c8.assign(n, 0);
   b.cp_fine.assign(n, 0);
   b.dec_len.resize(n);
   int64_t total = 0;
@@ -4372,11 +4341,10 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
     std::vector<uint32_t> one;
-    int wide = 0, light = 0, nfine = 0, c8 = 0;
-    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine, &c8);
+    int wide = 0, light = 0, nfine = 0;
+    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine);
     b.cp_wide[i] = (uint8_t)wide;
     b.cp_light[i] = (uint8_t)light;
-    b.cp_c8[i] = (uint8_t)(light ? 0 : c8);
     b.cp_fine[i] = nfine;
     b.cp_off[i] = (int64_t)cps.size();
     b.cp_n[i] = d < 0 ? -1 : (int32_t)one.size() - nfine;

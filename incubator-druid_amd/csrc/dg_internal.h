@@ -68,7 +68,7 @@ struct Lz4Job {
   // and value v goes to dst + v * vstride (a column of the groupBy payload records, written in place);
   // bytes past expect_len are then not written (they would land in the next segment's records)
   int32_t vstride;
-  int32_t c8;          // class-8 block: decoded by k_lz4_c8 (attach-time classification, lz4_c8_mode)
+  int32_t pad_;
   // Decode fused with a timeseries aggregator (the block's rows share one bucket, no filter): instead
   // of writing its 8-byte values the decoder folds them with red_op (agg_input_raw(red_kind,
   // red_vkind, value)) and combines the block's result into the bucket's slot *red_dst atomically.
@@ -86,14 +86,6 @@ struct Lz4Job {
 constexpr int kLtMaxCps = 256;
 constexpr int kLtThreads = 512;  // light-decoder threads (at most one light checkpoint interval each)
 constexpr int kLtMaxDepth = 16;
-
-// Class-8 blocks (Lz4Job.c8): nearly every match copies from exactly 8 bytes back
-// (8-byte values that change in a few low bytes per row: sequential or slowly varying longs, sorted
-// times); the bytes of the other matches ("exceptions") number at most kC8MaxExc, and no checkpoint
-// interval decodes to more than kC8MaxSpan bytes. k_lz4_c8 decodes them with a scan over the eight
-// residue classes (lz4_c8_mode classifies at attach).
-constexpr int kC8MaxSpan = 512;
-constexpr int kC8MaxExc = 512;
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
 struct LzfJob {
@@ -123,11 +115,8 @@ struct VsJob {
 // *light (optional): the block qualifies for the light decoder (kLtMaxCps / kLtMaxDepth).
 // *light = g > 0 when light: the block's checkpoints are followed by *nfine light checkpoints, one
 // every g sequences (g the fewest sequences per checkpoint that fit the light decoder's threads).
-// *c8 (optional): the block qualifies for the class-8 decoder (lz4_c8_mode).
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr,
-                    int* nfine = nullptr, int* c8 = nullptr);
-// true when a validated, non-wide block qualifies for k_lz4_c8 (class-8 blocks, above)
-bool lz4_c8_mode(const uint8_t* in, int n);
+                    int* nfine = nullptr);
 
 struct AggPlan {
   int32_t n;
@@ -254,7 +243,6 @@ struct BlockColumn {
   std::vector<int32_t> cp_n;           // LZ4: checkpoints of block b (-1: malformed block)
   std::vector<uint8_t> cp_wide;        // LZ4: block b keeps a checkpoint every 2 * kLzSeqPerCp sequences
   std::vector<uint8_t> cp_light;       // LZ4: block b goes to the light decoder (sequences per light checkpoint)
-  std::vector<uint8_t> cp_c8;          // LZ4: block b goes to the class-8 decoder
   std::vector<int32_t> cp_fine;        // LZ4: light checkpoints of block b (after its cp_n checkpoints)
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
   std::vector<int64_t> first8;         // LZ4: the first 8 decoded bytes of block b (int64 LE: its first
@@ -334,9 +322,9 @@ struct Context {
   // keys (the two only meet at the reduce); side_ev[0] = its inputs are staged, [1..2] = decode span
   hipStream_t side = nullptr;
   hipEvent_t side_ev[3] = {};
-  // the general and the class-8 LZ4 decoders' own spans on each stream: [0, 1] general main, [2, 3]
-  // general side, [4, 5] class-8 main, [6, 7] class-8 side (their roofline figures, dg_metrics)
-  hipEvent_t gen_ev[8] = {};
+  // the general LZ4 decoder's own span on each stream: [0, 1] main, [2, 3] side (its roofline
+  // figures, dg_metrics)
+  hipEvent_t gen_ev[4] = {};
   // dg_context_set_limit(DG_LIMIT_GROUP_ELEMENTS): most sort elements one groupBy call may build
   uint64_t max_elements = ~0ull;
   std::vector<std::shared_ptr<MergedDict>> dict_cache;  // most recent last
@@ -392,7 +380,6 @@ constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (dia
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
-void launch_lz4_c8(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // one multi-value dimension's decoded row lists, validated before use (bit 2 of the error word)

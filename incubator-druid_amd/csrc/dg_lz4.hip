@@ -1157,7 +1157,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   const uint8_t* __restrict__ in = job.src;
   const int nchunks = (total + 15) >> 4;
   bool fail = false;
-  uint64_t lt_acc = 0;  // (unused: the engine fuses only blocks of the general and class-8 decoders)
+  uint64_t lt_acc = 0;  // (unused: the engine fuses only blocks of the general decoder)
   // the source of output byte x: its literal position (a literal byte, a resolved match byte, or
   // hop by hop back to one); -1 = longer chain than the light limit (malformed classification)
   auto resolve = [&](int x, int s) -> int {  // s: a sequence starting at or before x
@@ -1246,378 +1246,6 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
     LZ_STAMP(4);
     if (tid == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Class-8 decoder (blocks of 8-byte values that change in a few low bytes per row: sequential longs,
-// sorted timestamps; lz4_c8_mode). When a match copies from exactly 8 bytes back, output byte x equals
-// the last byte written at or before x in its residue class x mod 8, so a "class register" of 8
-// entries is all the state the decoder needs: a literal byte writes its class, a distance-8 copy
-// leaves the register unchanged, and the 8 bytes of qword v are the register after position 8v + 7.
-// Bytes of matches at other distances ("exceptions", a few hundred per block at most) write their
-// class with a value found later. An entry is 16 bits: a byte value, or 0x8000 | the ordinal of the
-// exception byte that wrote it. Thread t owns checkpoint interval t (<= 8 sequences) and every qword
-// whose last byte lies in it:
-//   1. parse: output length, exception count and class transfer (classes written, the last entry of
-//      each; positions relative to the interval start);
-//   2. block scan of lengths / exception counts; transfer rotated to absolute classes; block scan of
-//      transfers (later writes win) = the register entering each interval;
-//   3. exceptions: each finds the entry its source position (taken before its match's start) holds,
-//      by replaying the owning interval from its entering register; pointer jumping over the
-//      exception -> exception links (log of the chain length) leaves every exception a value;
-//   4. re-walk from the entering register (exception entries replaced by their values), writing each
-//      completed qword into the LDS image; 5. 16-byte chunks of the image to the slot / payload
-//      records / fused aggregate.
-// ~8 sequences and ~8 qwords per thread in registers, against the general decoder's per-byte image.
-// ------------------------------------------------------------------------------------------------
-constexpr int kC8Threads = kLzMaxCps;  // one checkpoint interval per thread
-constexpr int kC8Waves = kC8Threads / 64;
-constexpr int kC8InWords = (kLz4InCap + 32) / 4;  // staged input (+ zero pad)
-constexpr uint64_t kC8Exc4 = 0x8000800080008000ull;
-
-__device__ __forceinline__ uint32_t c8_lit(const uint8_t* s_in, const Tok& t, int k) {
-  return t.L <= 4 ? (t.lv >> (8 * k)) & 0xFFu : (uint32_t)s_in[t.lit + k];
-}
-
-// the class register: entries of classes 0-3 in lo, 4-7 in hi (16 bits each)
-struct C8Reg {
-  uint64_t lo, hi;
-};
-__device__ __forceinline__ void c8_put(C8Reg& r, int x, uint32_t e) {
-  const int c = x & 7, sh = (c & 3) * 16;
-  const uint64_t m = ~(0xFFFFull << sh), v = (uint64_t)e << sh;
-  if (c < 4) r.lo = (r.lo & m) | v;
-  else r.hi = (r.hi & m) | v;
-}
-__device__ __forceinline__ uint32_t c8_get(const C8Reg& r, int x) {
-  const int c = x & 7;
-  return (uint32_t)(((c < 4 ? r.lo : r.hi) >> ((c & 3) * 16)) & 0xFFFF);
-}
-// 16-bit lanes of the 4-bit class mask m
-__device__ __forceinline__ uint64_t c8_lanes(uint32_t m) {
-  return ((m & 1) ? 0xFFFFull : 0) | ((m & 2) ? 0xFFFFull << 16 : 0) | ((m & 4) ? 0xFFFFull << 32 : 0) |
-         ((m & 8) ? 0xFFFFull << 48 : 0);
-}
-// a then b (b's entries win in b's classes)
-__device__ __forceinline__ void c8_compose(C8Reg& a, uint32_t& am, const C8Reg& b, uint32_t bm) {
-  a.lo = (a.lo & ~c8_lanes(bm & 15)) | b.lo;
-  a.hi = (a.hi & ~c8_lanes(bm >> 4)) | b.hi;
-  am |= bm;
-}
-// 8 byte values from a register of resolved entries
-__device__ __forceinline__ uint64_t c8_bytes(const C8Reg& r) {
-  uint64_t v = 0;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    v |= ((r.lo >> (16 * c)) & 0xFF) << (8 * c);
-    v |= ((r.hi >> (16 * c)) & 0xFF) << (8 * (c + 4));
-  }
-  return v;
-}
-
-template <bool PROF>
-__global__ __launch_bounds__(kC8Threads) void k_lz4_c8(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
-                                                       uint64_t* __restrict__ prof) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_in32[kC8InWords];  // staged compressed block
-  // the decoded image; until step 4 it holds the intervals' entering registers and starts
-  __shared__ __attribute__((aligned(16))) uint64_t s_img[kBlockBytes / 8];
-  __shared__ uint16_t s_esrc[kC8MaxExc];  // exception byte -> its source position
-  __shared__ uint16_t s_link[kC8MaxExc];  // exception byte -> entry (value, or a link to another)
-  __shared__ int s_tmp[kC8Waves];
-  __shared__ uint64_t s_wlo[kC8Waves], s_whi[kC8Waves];
-  __shared__ uint32_t s_wm[kC8Waves];
-  __shared__ uint64_t s_red[kC8Waves];
-  __shared__ int s_bad;
-  static_assert(kC8Threads * 20 <= kBlockBytes, "entering registers + starts fit the image");
-  C8Reg* s_ent = reinterpret_cast<C8Reg*>(s_img);                           // [kC8Threads]
-  uint32_t* s_start = reinterpret_cast<uint32_t*>(s_img + 2 * kC8Threads);  // base | ebase << 17
-  const Lz4Job job = jobs[blockIdx.x];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = job.src_len, ncp = job.ncp;
-  if (!job.c8 || n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kC8Threads || job.wide ||
-      job.dec_len > kBlockBytes || job.dec_len < job.expect_len) {
-    if (tid == 0) atomicOr(err, 1);
-    return;
-  }
-  LZ_STAMP(0);
-  uint8_t* s_in = reinterpret_cast<uint8_t*>(s_in32);
-  {
-    uint4* dst = reinterpret_cast<uint4*>(s_in32);
-    const int n16 = (n + 15) >> 4;
-    constexpr int kPer = (kLz4InCap + 16 * kC8Threads - 1) / (16 * kC8Threads);
-    uint4 v[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-      if (tid + k * kC8Threads < n16) v[k] = gld16(job.src + 16 * (size_t)(tid + k * kC8Threads));
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-      if (tid + k * kC8Threads < n16) dst[tid + k * kC8Threads] = v[k];
-    if (tid == 0) {
-      dst[n16] = make_uint4(0, 0, 0, 0);
-      s_bad = 0;
-    }
-  }
-  __syncthreads();
-  LZ_STAMP(1);
-  const int p0 = tid < ncp ? (int)gld4(job.cp + tid) : n;
-  const int end = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
-  // ---- 1. transfer of my interval (relative classes), length, exception count ----
-  C8Reg tr = {0, 0};
-  uint32_t tm = 0;
-  int len = 0, ne = 0;
-  bool bad = false;
-  {
-    int pos = p0;
-    for (int s = 0; s < kLzSeqPerCp && pos < end; ++s) {
-      Tok t;
-      if (!parse_tok(s_in, n, pos, t)) {
-        bad = true;
-        break;
-      }
-      for (int k = max(0, t.L - 8); k < t.L; ++k) {  // (earlier bytes of the run: overwritten)
-        c8_put(tr, len + k, c8_lit(s_in, t, k));
-        tm |= 1u << ((len + k) & 7);
-      }
-      len += t.L;
-      if (t.M && t.off != 8) {
-        for (int k = max(0, t.M - 8); k < t.M; ++k) {
-          c8_put(tr, len + k, 0x8000u | (uint32_t)(ne + k));
-          tm |= 1u << ((len + k) & 7);
-        }
-        ne += t.M;
-      }
-      len += t.M;
-      pos = t.next;
-    }
-    if (tid < ncp && pos != end) bad = true;
-  }
-  // ---- 2. block scan of (length | exception count << 18) ----
-  int base, ebase, total, nexc;
-  {
-    const int mine = len | (ne << 18);
-    int x = mine;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) s_tmp[wave] = x;
-    if (bad) s_bad = 1;
-    __syncthreads();
-    int pre = x - mine, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kC8Waves; ++w) {
-      const int y = s_tmp[w];
-      pre += w < wave ? y : 0;
-      tot += y;
-    }
-    base = pre & ((1 << 18) - 1);
-    ebase = pre >> 18;
-    total = tot & ((1 << 18) - 1);
-    nexc = tot >> 18;
-  }
-  if (s_bad || total != job.dec_len || nexc > kC8MaxExc) {
-    if (tid == 0) atomicOr(err, 1);
-    return;
-  }
-  LZ_STAMP(2);
-  // exception ordinals absolute; classes absolute (rotate the 8 entries by base mod 8)
-  tr.lo += ((tr.lo & kC8Exc4) >> 15) * (uint64_t)ebase;
-  tr.hi += ((tr.hi & kC8Exc4) >> 15) * (uint64_t)ebase;
-  {
-    int r = base & 7;
-    if (r >= 4) {
-      const uint64_t t = tr.lo;
-      tr.lo = tr.hi;
-      tr.hi = t;
-      r -= 4;
-    }
-    if (r) {
-      const int sh = 16 * r;
-      const uint64_t lo = (tr.lo << sh) | (tr.hi >> (64 - sh)), hi = (tr.hi << sh) | (tr.lo >> (64 - sh));
-      tr.lo = lo;
-      tr.hi = hi;
-    }
-    const int rb = base & 7;
-    tm = ((tm << rb) | (tm >> (8 - rb))) & 0xFFu;
-  }
-  // block scan of the transfers: inclusive in the wave, then the earlier waves' totals
-  C8Reg inc = tr;
-  uint32_t im = tm;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    C8Reg p;
-    p.lo = __shfl_up((unsigned long long)inc.lo, o, 64);
-    p.hi = __shfl_up((unsigned long long)inc.hi, o, 64);
-    uint32_t pm = __shfl_up(im, o, 64);
-    if (lane >= o) {
-      c8_compose(p, pm, inc, im);
-      inc = p;
-      im = pm;
-    }
-  }
-  C8Reg ent;
-  ent.lo = __shfl_up((unsigned long long)inc.lo, 1, 64);
-  ent.hi = __shfl_up((unsigned long long)inc.hi, 1, 64);
-  uint32_t em = __shfl_up(im, 1, 64);
-  if (lane == 0) {
-    ent.lo = ent.hi = 0;
-    em = 0;
-  }
-  if (lane == 63) {
-    s_wlo[wave] = inc.lo;
-    s_whi[wave] = inc.hi;
-    s_wm[wave] = im;
-  }
-  __syncthreads();
-  {
-    C8Reg pre = {0, 0};
-    uint32_t pm = 0;
-    for (int w = 0; w < wave; ++w) {
-      const C8Reg b = {s_wlo[w], s_whi[w]};
-      c8_compose(pre, pm, b, s_wm[w]);
-    }
-    c8_compose(pre, pm, ent, em);
-    ent = pre;
-  }
-  // ---- 3. exceptions: source positions, entries at the sources, pointer jumping ----
-  if (nexc) {
-    s_ent[tid] = ent;
-    s_start[tid] = (uint32_t)base | ((uint32_t)ebase << 17);
-    if (ne) {  // my exception bytes' sources
-      int pos = p0, x = base, ei = ebase;
-      for (int s = 0; s < kLzSeqPerCp && pos < end; ++s) {
-        Tok t;
-        parse_tok(s_in, n, pos, t);
-        x += t.L;
-        if (t.M && t.off != 8) {
-          const int d = t.off;
-          for (int k = 0; k < t.M; ++k, ++ei) {
-            const int src = (d >= t.M || k < d) ? x + k - d : x - d + k % d;
-            bad |= src < 0;
-            s_esrc[ei] = (uint16_t)max(src, 0);
-          }
-        }
-        x += t.M;
-        pos = t.next;
-      }
-    }
-    if (bad) s_bad = 1;
-    __syncthreads();
-    if (s_bad) {
-      if (tid == 0) atomicOr(err, 1);
-      return;
-    }
-    for (int e = tid; e < nexc; e += kC8Threads) {
-      const int y = s_esrc[e];
-      int lo = 0, hi = ncp - 1;  // the last interval starting at or before y
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((int)(s_start[mid] & ((1u << 17) - 1)) <= y) lo = mid;
-        else hi = mid - 1;
-      }
-      C8Reg r = s_ent[lo];
-      int x = (int)(s_start[lo] & ((1u << 17) - 1)), ei = (int)(s_start[lo] >> 17);
-      int pos = (int)gld4(job.cp + lo);
-      const int pe = lo + 1 < ncp ? (int)gld4(job.cp + lo + 1) : n;
-      for (int s = 0; s < kLzSeqPerCp && pos < pe && x <= y; ++s) {
-        Tok t;
-        parse_tok(s_in, n, pos, t);
-        for (int k = 0; k < t.L && x <= y; ++k, ++x) c8_put(r, x, c8_lit(s_in, t, k));
-        if (x > y) break;
-        if (t.M && t.off != 8) {
-          for (int k = 0; k < t.M && x <= y; ++k, ++x, ++ei) c8_put(r, x, 0x8000u | (uint32_t)ei);
-        } else {
-          x += t.M;
-        }
-        pos = t.next;
-      }
-      s_link[e] = (uint16_t)c8_get(r, y);
-    }
-    __syncthreads();
-    for (int round = 0;; ++round) {
-      bool open = false;
-      for (int e = tid; e < nexc; e += kC8Threads) {
-        const uint32_t l = s_link[e];
-        if (l & 0x8000u) {
-          const uint32_t l2 = s_link[l & 0x7FFFu];  // (an earlier exception: links never cycle)
-          s_link[e] = (uint16_t)l2;
-          open |= (l2 & 0x8000u) != 0;
-        }
-      }
-      if (!__syncthreads_or(open)) break;
-      if (round > 10) {  // 2^11 > kC8MaxExc: a longer chain means a malformed link
-        if (tid == 0) atomicOr(err, 1);
-        return;
-      }
-    }
-    // my entering register's exception entries -> their values
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const uint32_t e = c8_get(ent, c);
-      if (e & 0x8000u) c8_put(ent, c, s_link[e & 0x7FFFu]);
-    }
-  }
-  LZ_STAMP(3);
-  __syncthreads();  // (the image region held the entering registers)
-  // ---- 4. re-walk: completed qwords into the image ----
-  if (tid < ncp) {
-    uint64_t S = c8_bytes(ent);
-    int pos = p0, x = base, ei = ebase;
-    for (int s = 0; s < kLzSeqPerCp && pos < end; ++s) {
-      Tok t;
-      parse_tok(s_in, n, pos, t);
-      for (int k = 0; k < t.L; ++k, ++x) {
-        const int c = (x & 7) * 8;
-        S = (S & ~(0xFFull << c)) | ((uint64_t)c8_lit(s_in, t, k) << c);
-        if ((x & 7) == 7) s_img[x >> 3] = S;
-      }
-      if (t.M && t.off != 8) {
-        for (int k = 0; k < t.M; ++k, ++x, ++ei) {
-          const int c = (x & 7) * 8;
-          S = (S & ~(0xFFull << c)) | ((uint64_t)(s_link[ei] & 0xFF) << c);
-          if ((x & 7) == 7) s_img[x >> 3] = S;
-        }
-      } else if (t.M) {
-        for (int y = x | 7; y < x + t.M; y += 8) s_img[y >> 3] = S;
-        x += t.M;
-      }
-      pos = t.next;
-    }
-    // the block's partial last qword (its bytes past the end zeroed)
-    if (x == total && (total & 7)) s_img[total >> 3] = S & ((1ull << (8 * (total & 7))) - 1);
-  }
-  __syncthreads();
-  LZ_STAMP(4);
-  LZ_STAMP(5);
-  // ---- 5. output: 16-byte chunks of the image ----
-  const int nchunks = (total + 15) >> 4;
-  const uint4* img16 = reinterpret_cast<const uint4*>(s_img);
-  uint64_t racc = job.red_dst ? identity_of(job.red_op, job.red_kind) : 0ull;
-  for (int c = tid; c < nchunks; c += kC8Threads) {
-    const uint4 v = img16[c];
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    const int rem = total - 16 * c;
-    if (rem < 16) {  // bytes past the block's end are zero
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int keep = min(max(rem - 4 * q, 0), 4);
-        w[q] &= keep == 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
-      }
-    }
-    out16(job, c, w, racc);
-  }
-  if (job.red_dst) red_finish(job, racc, s_red, kC8Waves);
-  if (PROF) {
-    __syncthreads();
-    LZ_STAMP(6);
-  }
-}
-
-void launch_lz4_c8(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
-  if (njobs <= 0) return;
-  if (d_prof) hipLaunchKernelGGL(k_lz4_c8<true>, dim3(njobs), dim3(kC8Threads), 0, s, d_jobs, d_err, d_prof);
-  else hipLaunchKernelGGL(k_lz4_c8<false>, dim3(njobs), dim3(kC8Threads), 0, s, d_jobs, d_err, nullptr);
 }
 
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {

@@ -178,44 +178,6 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
   }
 }
 
-// Class-8 classification (k_lz4_c8): at least one match at distance 8, the bytes of matches at other
-// distances ("exceptions") at most kC8MaxExc, and every run of kLzSeqPerCp sequences (one checkpoint
-// interval) decoding to at most kC8MaxSpan bytes.
-bool lz4_c8_mode(const uint8_t* in, int n) {
-  int pos = 0, out = 0, span = 0, n8 = 0, nexc = 0;
-  int64_t seq = 0;
-  auto ext = [&](int* len) {
-    for (int b = 255; b == 255 && pos < n;) {
-      b = in[pos++];
-      *len += b;
-    }
-  };
-  for (;;) {
-    if (pos >= n) return false;
-    if (seq++ % kLzSeqPerCp == 0) span = 0;
-    const int tok = in[pos++];
-    int L = tok >> 4;
-    if (L == 15) ext(&L);
-    pos += L;
-    span += L;
-    out += L;
-    if (pos > n || span > kC8MaxSpan || out > kBlockBytes) return false;
-    if (pos == n) break;
-    if (n - pos < 2) return false;
-    const int d = in[pos] | (in[pos + 1] << 8);
-    pos += 2;
-    int M = tok & 15;
-    if (M == 15) ext(&M);
-    M += 4;
-    span += M;
-    if (d == 0 || d > out || span > kC8MaxSpan || out + M > kBlockBytes) return false;
-    if (d == 8) ++n8;
-    else if ((nexc += M) > kC8MaxExc) return false;
-    out += M;
-  }
-  return n8 > 0 && seq <= (int64_t)kLzMaxCps * kLzSeqPerCp;
-}
-
 // The first 8 decoded bytes of a validated block (its first sequences only), or false when it
 // decodes to fewer.
 static bool lz4_first8(const uint8_t* in, int n, int64_t* out) {
@@ -249,11 +211,10 @@ static bool lz4_first8(const uint8_t* in, int n, int64_t* out) {
   return true;
 }
 
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine, int* c8) {
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine) {
   const size_t first = cps->size();
   if (light) *light = 0;
   if (nfine) *nfine = 0;
-  if (c8) *c8 = 0;
   int pos = 0, out = 0;
   int64_t seq = 0;
   auto ext = [&](int* len) {
@@ -274,7 +235,6 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
       cps->resize(first + m);
     }
     if (m > (size_t)kLzMaxCps) return -1;
-    if (c8 && !*wide) *c8 = lz4_c8_mode(in, n);
     if (light && !*wide && m <= (size_t)kLtMaxCps && lz4_max_depth(in, n, kLtMaxDepth) <= kLtMaxDepth) {
       // light checkpoints: every g sequences, the fewest that fit one per light-decoder thread
       const int g = (int)std::max<int64_t>(1, (seq + kLtThreads - 1) / kLtThreads);
@@ -356,7 +316,6 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->cp_n.assign(blocks.n, -1);
     col->cp_wide.assign(blocks.n, 0);
     col->cp_light.assign(blocks.n, 0);
-    col->cp_c8.assign(blocks.n, 0);
     col->cp_fine.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
     col->first8.assign(blocks.n, 0);
@@ -368,12 +327,10 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int t = 0; t < nt; ++t)
       th.emplace_back([&, t] {
         for (int32_t b = t; b < blocks.n; b += nt) {
-          int wide = 0, light = 0, nfine = 0, c8 = 0;
-          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine,
-                                        &c8);
+          int wide = 0, light = 0, nfine = 0;
+          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine);
           col->cp_wide[b] = (uint8_t)wide;
           col->cp_light[b] = (uint8_t)light;
-          col->cp_c8[b] = (uint8_t)(light ? 0 : c8);
           col->cp_fine[b] = nfine;
           col->dec_len[b] = d;
           if (d >= 8) has8[b] = lz4_first8(host.data() + col->comp_off[b], col->comp_len[b], &col->first8[b]);

@@ -43,15 +43,10 @@ def lz4_sequences(seqs, last_literals: bytes) -> bytes:
     return bytes(out)
 
 
-@pytest.fixture(params=["default", "general"])
-def route(request, monkeypatch):
-    """Decode every block both ways: class-8 blocks on k_lz4_c8 (default) and on the general decoder
-    (DG_LZ4_NO_C8=1, read by the library per call)."""
-    if request.param == "general":
-        monkeypatch.setenv("DG_LZ4_NO_C8", "1")
-    else:
-        monkeypatch.delenv("DG_LZ4_NO_C8", raising=False)
-    return request.param
+@pytest.fixture
+def route():
+    """The library's routing of blocks to its decoders (light / general), read per call."""
+    return "default"
 
 
 def gpu_decode(blocks):
@@ -308,9 +303,9 @@ def _value_run_cases(rng):
 
 
 def test_lz4_classification():
-    """CPU: the attach-time classification routes 8-byte value runs (sequential longs, timestamps) to
-    the class-8 decoder, noisy doubles to the general decoder, random dictionary ids to the light
-    decoder, and rejects malformed blocks."""
+    """CPU: the attach-time classification routes token-dense blocks (8-byte value runs, noisy
+    doubles) to the general decoder, random dictionary ids to the light decoder, and rejects malformed
+    blocks."""
     N = importlib.import_module("incubator-druid_amd._native")
     rng = np.random.default_rng(23)
 
@@ -319,21 +314,18 @@ def test_lz4_classification():
         N.check(N.lib().dg_debug_lz4_classify(b, len(b), ctypes.byref(k)))
         return k.value
 
-    # -1 malformed, 0/1 general (wide), 2 light, 4 class-8
+    # -1 malformed, 0/1 general (wide), 2 light
     for name, b in _value_run_cases(rng).items():
-        assert kind(b) in (0, 1, 4), name
+        assert kind(b) in (0, 1), name
     n8 = BLOCK // 8
     seq = np.arange(n8, dtype=np.int64)
-    assert kind(_lz4_hc((seq % 10000).astype("<i8").tobytes())) == 4
-    assert kind(_lz4_hc(np.round(seq * 1.3333 + 1388534400000).astype("<i8").tobytes())) == 4
-    c8 = _c8_boundary(np.random.default_rng(31))
-    for name in ("c8_plain", "c8_partial", "c8_exc_far", "c8_exc_short", "c8_exc_chain", "c8_exc512", "c8_span512",
-                 "c8_longlit"):
-        assert kind(c8[name]) == 4, name
-    assert kind(c8["c8_exc513"]) != 4 and kind(c8["c8_span513"]) != 4
+    assert kind(_lz4_hc((seq % 10000).astype("<i8").tobytes())) == 0
+    assert kind(_lz4_hc(np.round(seq * 1.3333 + 1388534400000).astype("<i8").tobytes())) == 0
+    for name, b in _c8_boundary(np.random.default_rng(31)).items():
+        assert kind(b) in (0, 1), name
     assert kind(_lz4_hc(rng.normal(5000.0, 1.0, BLOCK // 8).astype("<f8").tobytes())) == 0
     for name, b in _dense_boundary(np.random.default_rng(29)).items():
-        assert kind(b) in (0, 1, 2, 4), name
+        assert kind(b) in (0, 1, 2), name
     ids = b"".join(int(x).to_bytes(4, "little")[:3] for x in rng.integers(1, 100001, BLOCK // 3 + 1))[:BLOCK]
     assert kind(_lz4_hc(ids)) == 2
     assert kind(b"\x00\x01") == -1
@@ -451,10 +443,11 @@ def test_lz4_dense_boundaries_bit_exact(route, O):
 
 
 def _c8_boundary(rng):
-    """Blocks for the class-8 decoder: 8-byte value runs (a step = 1-2 new low bytes + a 6-7-byte copy
-    from 8 back) with a partial last qword, exceptions (matches at other distances: far, overlapping
-    short, chained through each other), and its routing limits (512 exception bytes, 512 output bytes
-    per checkpoint interval of 8 sequences)."""
+    """8-byte value runs (a step = 1-2 new low bytes + a 6-7-byte copy from 8 back) with a partial last
+    qword and "exceptions" (matches at other distances: far, overlapping short, chained through each
+    other), around the limits of the (removed, measured no faster) class-8 decoder: 512 exception
+    bytes, 512 output bytes per checkpoint interval of 8 sequences. The general decoder's class mode
+    decodes them."""
     r = lambda k: rng.integers(0, 256, k).astype(np.uint8).tobytes()  # noqa: E731
 
     def steps(k, seqs):
@@ -526,7 +519,7 @@ def test_c8_boundary_streams_pinned_by_system_liblz4(O):
 
 
 @pytest.mark.gpu
-def test_lz4_c8_boundaries_bit_exact(route, O):
+def test_lz4_value_run_exceptions_bit_exact(route, O):
     cases = _c8_boundary(np.random.default_rng(31))
     blocks = list(cases.values()) * 3
     got = gpu_decode(blocks)

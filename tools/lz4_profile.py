@@ -18,7 +18,7 @@ S = importlib.import_module("incubator-druid_amd.segment")
 W = importlib.import_module("incubator-druid_amd.writer")
 BLOCK = 65536
 PHASES = ["stage", "parse+scan", "jobs+read", "fill+write", "resolve", "output"]
-KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light", 4: "class8"}
+KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light"}
 
 
 def classify(block):
