@@ -1041,7 +1041,7 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.vstride = 0;
   j.pad_ = 0;
   j.red_dst = nullptr;
-  j.red_op = j.red_kind = j.red_vkind = j.red_pad = 0;
+  j.red_op = j.red_kind = j.red_vkind = j.red_code = 0;
   return j;
 }
 
@@ -1818,6 +1818,9 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
       j.red_op = slot_op(a.kind);
       j.red_kind = a.kind;
       j.red_vkind = v->kind;
+      j.red_code = v->kind == VIEW_LONG ? (a.kind == DG_AGG_LONG_SUM ? kRedLongSum : a.kind == DG_AGG_LONG_MAX ? kRedLongMax
+                                           : a.kind == DG_AGG_LONG_MIN ? kRedLongMin : kRedGeneric)
+                                        : (a.kind == DG_AGG_DOUBLE_SUM ? kRedDoubleSum : kRedGeneric);
       db->jobs.push_back(j);
       db->fused_blocks++;
       continue;

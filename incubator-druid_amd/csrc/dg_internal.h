@@ -77,8 +77,11 @@ struct Lz4Job {
   int32_t red_op;
   int32_t red_kind;
   int32_t red_vkind;
-  int32_t red_pad;
+  int32_t red_code;  // kRed*: the fold in the value's own type (generic: agg_input_raw + combine_op)
 };
+// folds of a fused decode (Lz4Job.red_code): int64 sum / max / min of a long column, double sum of a
+// double column in their native types (converted to the slot encoding once per block); others generic
+enum : int32_t { kRedGeneric = 0, kRedLongSum = 1, kRedDoubleSum = 2, kRedLongMax = 3, kRedLongMin = 4 };
 
 // Light blocks (literal-heavy: random ids, high-entropy values): at most kLtMaxCps checkpoint
 // intervals and copy chains of at most kLtMaxDepth hops. k_lz4_light decodes them with a small

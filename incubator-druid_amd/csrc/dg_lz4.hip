@@ -292,10 +292,37 @@ __device__ __forceinline__ int job_len(uint2 j) { return (int)(j.x >> 16) + 1; }
 __device__ __forceinline__ void out16(const Lz4Job& job, int c, const uint32_t w[4], uint64_t& acc) {
   if (job.red_dst) {
     const int v = 2 * c;
-    if ((v + 1) * 8 <= job.expect_len)
-      acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, (uint64_t)w[0] | ((uint64_t)w[1] << 32)));
-    if ((v + 2) * 8 <= job.expect_len)
-      acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, (uint64_t)w[2] | ((uint64_t)w[3] << 32)));
+    const bool has0 = (v + 1) * 8 <= job.expect_len, has1 = (v + 2) * 8 <= job.expect_len;
+    const uint64_t x0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), x1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+    switch (job.red_code) {
+      case kRedLongSum:
+        acc += (has0 ? x0 : 0) + (has1 ? x1 : 0);
+        break;
+      case kRedDoubleSum: {
+        double a = __longlong_as_double((long long)acc);
+        if (has0) a += __longlong_as_double((long long)x0);
+        if (has1) a += __longlong_as_double((long long)x1);
+        acc = (uint64_t)__double_as_longlong(a);
+        break;
+      }
+      case kRedLongMax: {
+        long long a = (long long)acc;
+        if (has0) a = max(a, (long long)x0);
+        if (has1) a = max(a, (long long)x1);
+        acc = (uint64_t)a;
+        break;
+      }
+      case kRedLongMin: {
+        long long a = (long long)acc;
+        if (has0) a = min(a, (long long)x0);
+        if (has1) a = min(a, (long long)x1);
+        acc = (uint64_t)a;
+        break;
+      }
+      default:
+        if (has0) acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, x0));
+        if (has1) acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, x1));
+    }
     return;
   }
   if (!job.vstride) {
@@ -316,9 +343,21 @@ __device__ __forceinline__ void out4(const Lz4Job& job, int x, uint32_t w) {
   if (((x >> 3) + 1) * 8 <= job.expect_len) gst4(job.dst + (size_t)(x >> 3) * job.vstride + (x & 7), w);
 }
 
+// the fold's starting value in the encoding out16 accumulates in (red_code)
+__device__ __forceinline__ uint64_t red_identity(const Lz4Job& job) {
+  switch (job.red_code) {
+    case kRedLongSum:
+    case kRedDoubleSum: return 0;
+    case kRedLongMax: return (uint64_t)INT64_MIN;
+    case kRedLongMin: return (uint64_t)INT64_MAX;
+    default: return identity_of(job.red_op, job.red_kind);
+  }
+}
+
 // The fused block's aggregate: the workgroup's per-thread values folded (wave shuffles, then one
 // slot per wave in s_red) and combined into the bucket's slot with one atomic. Every thread calls it.
 __device__ __forceinline__ void red_finish(const Lz4Job& job, uint64_t acc, uint64_t* s_red, int nwaves) {
+  if (job.red_code == kRedLongMax || job.red_code == kRedLongMin) acc ^= kSign;  // -> the slot encoding
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
     acc = combine_op(job.red_op, acc, (uint64_t)__shfl_xor((unsigned long long)acc, o, 64));
@@ -879,7 +918,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   const int nchunks = (total + 15) >> 4;
   const bool has_tail = total > kTail;
   const int nbody = has_tail ? (kTail >> 4) : nchunks;  // chunks below kTail (kTail % 16 == 0)
-  uint64_t racc = job.red_dst ? identity_of(job.red_op, job.red_kind) : 0ull;
+  uint64_t racc = job.red_dst ? red_identity(job) : 0ull;
   auto out_chunk = [&](int c) {
     const int x0 = c << 4;
     uint32_t w[4];
