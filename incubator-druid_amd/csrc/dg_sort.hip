@@ -369,11 +369,20 @@ void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles
 // keys it stores; only the first pass's digit totals need a read of the keys of their own
 // (k_rs_hist0). No per-pass histogram read, no separate scan.
 // ------------------------------------------------------------------------------------------------
-// look-back status words are 64-bit: an inclusive prefix counts every earlier element of the digit,
-// up to n (< 2^32), so it cannot share a 32-bit word with the flag
-constexpr uint64_t kLbAgg = 1ull << 62;                // look-back status: the tile's own count
-constexpr uint64_t kLbPre = 2ull << 62;                // ... the inclusive prefix up to the tile
-constexpr uint64_t kLbVal = (1ull << 62) - 1;
+// look-back status words: a flag in the top two bits (the tile's own count / the inclusive prefix up
+// to the tile) and a count below. An inclusive prefix counts every earlier element of the digit, up to
+// n: 32-bit words (30-bit counts) when the call's capacity is below 2^30 elements, 64-bit words
+// otherwise (n < 2^32) — the narrow words halve the look-back traffic of every pass
+template <class W>
+struct Lb {
+  static constexpr int kShift = 8 * sizeof(W) - 2;
+  static constexpr W kAgg = (W)1 << kShift;
+  static constexpr W kPre = (W)2 << kShift;
+  static constexpr W kVal = ((W)1 << kShift) - 1;
+};
+constexpr uint64_t kLbAgg = Lb<uint64_t>::kAgg;  // (the groupBy reduce's per-tile look-back)
+constexpr uint64_t kLbPre = Lb<uint64_t>::kPre;
+constexpr uint64_t kLbVal = Lb<uint64_t>::kVal;
 
 // the first pass's digit totals: totals[d] += elements whose digit (bits above shift) is d
 __global__ __launch_bounds__(kST) void k_rs_hist0(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
@@ -415,11 +424,11 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // earlier tiles' counts walking back until one has published its inclusive prefix, and publishes its
 // own. The tile is then reordered by digit in LDS, so the global stores of a wave run along each
 // digit's contiguous output range (coalesced) instead of scattering lane by lane.
-template <bool REFS>
+template <bool REFS, class W>
 __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     const uint32_t* __restrict__ n_ptr, int shift, int bits,
-                                                    const uint32_t* __restrict__ totals, uint64_t* __restrict__ status,
+                                                    const uint32_t* __restrict__ totals, W* __restrict__ status,
                                                     uint32_t* __restrict__ tile_ctr, int nshift, int nbits,
                                                     uint32_t* __restrict__ ntotals) {
   __shared__ uint64_t s_k[kSortTile];
@@ -478,27 +487,27 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
     }
     uint64_t excl = 0;
     if (d < nb) {
-      uint64_t* st = status + (size_t)tile * nb + d;
+      W* st = status + (size_t)tile * nb + d;
       if (tile == 0) {
-        __hip_atomic_store(st, kLbPre | ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st, Lb<W>::kPre | (W)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
-        __hip_atomic_store(st, kLbAgg | ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st, Lb<W>::kAgg | (W)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // eight earlier tiles at a time (independent loads), newest first, up to the first one
         // with its inclusive prefix; a tile not published yet (it has started: it publishes its
         // count without waiting) is loaded again
         constexpr int kLb = 8;
         for (int j = tile - 1; j >= 0;) {
-          uint64_t sv[kLb];
+          W sv[kLb];
 #pragma unroll
           for (int q = 0; q < kLb; ++q)
             sv[q] = j - q >= 0 ? __hip_atomic_load(status + (size_t)(j - q) * nb + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : kLbPre;
+                               : Lb<W>::kPre;
           int q = 0;
           bool prefix = false;
           for (; q < kLb; ++q) {
-            if ((sv[q] >> 62) == 0) break;
-            excl += sv[q] & kLbVal;
-            if (sv[q] & kLbPre) {
+            if ((sv[q] >> Lb<W>::kShift) == 0) break;
+            excl += sv[q] & Lb<W>::kVal;
+            if (sv[q] & Lb<W>::kPre) {
               prefix = true;
               break;
             }
@@ -507,7 +516,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
           j -= q;
           if (q < kLb) __builtin_amdgcn_s_sleep(1);
         }
-        __hip_atomic_store(st, kLbPre | (excl + ct), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st, Lb<W>::kPre | (W)(excl + ct), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     uint32_t tot;
@@ -566,15 +575,25 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
     const int nbits = p + 1 < npass ? std::min(w, hi - off - w) : 0;
     uint32_t* nt_tot = p + 1 < npass ? totals + (size_t)(p + 1) * kMaxBins : nullptr;
     const int in = sb->cur, out = sb->cur ^ 1;
-    (void)hipMemsetAsync(sb->lb_status, 0, (size_t)(1 << bits) * nt * sizeof(uint64_t), s);  // look-back status
-    if (sb->refs[in]) {
-      hipLaunchKernelGGL(k_rs_scatter<true>, dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
-                         sb->refs[out], sb->n, shift, bits, totals + (size_t)p * kMaxBins, sb->lb_status, ctr + p,
-                         shift + w, nbits, nt_tot);
-    } else {
-      hipLaunchKernelGGL(k_rs_scatter<false>, dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out], nullptr,
-                         sb->n, shift, bits, totals + (size_t)p * kMaxBins, sb->lb_status, ctr + p, shift + w, nbits, nt_tot);
-    }
+    // 30-bit counts hold every prefix (n <= cap); DG_SORT_WIDE_STATUS=1: 64-bit words regardless (tests)
+    const char* wide = getenv("DG_SORT_WIDE_STATUS");
+    const bool narrow = sb->cap < ((int64_t)1 << 30) && !(wide && *wide && *wide != '0');
+    (void)hipMemsetAsync(sb->lb_status, 0, (size_t)(1 << bits) * nt * (narrow ? 4 : 8), s);  // look-back status
+    uint32_t* st32 = reinterpret_cast<uint32_t*>(sb->lb_status);
+    uint64_t* st64 = sb->lb_status;
+    const uint32_t* tp = totals + (size_t)p * kMaxBins;
+    if (sb->refs[in] && narrow)
+      hipLaunchKernelGGL((k_rs_scatter<true, uint32_t>), dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
+                         sb->refs[out], sb->n, shift, bits, tp, st32, ctr + p, shift + w, nbits, nt_tot);
+    else if (sb->refs[in])
+      hipLaunchKernelGGL((k_rs_scatter<true, uint64_t>), dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
+                         sb->refs[out], sb->n, shift, bits, tp, st64, ctr + p, shift + w, nbits, nt_tot);
+    else if (narrow)
+      hipLaunchKernelGGL((k_rs_scatter<false, uint32_t>), dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out],
+                         nullptr, sb->n, shift, bits, tp, st32, ctr + p, shift + w, nbits, nt_tot);
+    else
+      hipLaunchKernelGGL((k_rs_scatter<false, uint64_t>), dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out],
+                         nullptr, sb->n, shift, bits, tp, st64, ctr + p, shift + w, nbits, nt_tot);
     sb->cur = out;
   }
 }

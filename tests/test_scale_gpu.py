@@ -113,7 +113,14 @@ def _columns(rows, dims, aggs):
     return t, keys, vals
 
 
-def test_cfg3_groupby_high_cardinality_matches_oracle(R, Q, O, cfg3):
+@pytest.mark.parametrize("status", ["narrow", "wide"])
+def test_cfg3_groupby_high_cardinality_matches_oracle(R, Q, O, cfg3, status, monkeypatch):
+    """1.2 M groups vs the oracle, with the radix look-back status in 32-bit words (the default below
+    2^30 elements) and in 64-bit words (DG_SORT_WIDE_STATUS=1, the path of larger calls)."""
+    if status == "wide":
+        monkeypatch.setenv("DG_SORT_WIDE_STATUS", "1")
+    else:
+        monkeypatch.delenv("DG_SORT_WIDE_STATUS", raising=False)
     g, o = cfg3
     assert g[0].dictionary("dimUniform") != g[1].dictionary("dimUniform")
     aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal"),
