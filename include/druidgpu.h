@@ -212,8 +212,8 @@ typedef struct {
   int32_t lz4_general_launches;
   /* filter bitmaps: serialized bitmap bytes read + row bitsets written and read (since ABI 11) */
   int64_t bitmap_bytes;
-  /* since ABI 12: the groupBy reduce kernels alone (reduce_ms also holds the group-count read-back and
-     the wait for the side-stream payload decode) */
+  /* since ABI 12: the groupBy reduce kernels alone (reduce_ms also holds the wait for the side-stream
+     payload decode) */
   double reduce_kernel_ms;
   /* since ABI 13: timeseries LZ4 blocks whose decode was fused with their aggregator (the decoder
      folded the block's values into its bucket's slot and wrote no decoded image) */
