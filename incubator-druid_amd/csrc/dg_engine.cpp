@@ -2202,14 +2202,10 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   }
   if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
   // init accumulators (before the decoders: fused blocks combine into them)
-  uint64_t* d_init;
-  uint64_t* h_init = up_take<uint64_t>(cs, rec, &d_init, st);
-  if (!h_init) return set_error(DG_ERR_OOM, "accumulator init");
-  h_init[0] = 0;
-  for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
-  DG_FLUSH(cs, st);
+  SlotInit init{};
+  for (int a = 0; a < na; ++a) init.v[1 + a] = identity_host(plan.kind[a]);
   for (int i = 0; i < n; ++i)
-    if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, d_init, st);
+    if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, init, st);
   hipEventRecord(ctx->ev[1], st);
   rc = run_decodes(cs, &db, st);
   if (rc) return rc;
@@ -2495,14 +2491,11 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   }
   if (any_multi) {
     // multi-value dimension: per-(row, value) atomics into identity-initialised tables
-    uint64_t* d_init;
-    uint64_t* h_init = up_take<uint64_t>(cs, rec, &d_init, st);
-    if (!h_init) return set_error(DG_ERR_OOM, "topN table init");
-    h_init[0] = 0;
-    for (int a = 0; a < na; ++a) h_init[1 + a] = identity_host(plan.kind[a]);
+    SlotInit init{};
+    for (int a = 0; a < na; ++a) init.v[1 + a] = identity_host(plan.kind[a]);
     DG_FLUSH(cs, st);
     for (int i = 0; i < n; ++i)
-      if (cur[i].any) launch_fill_u64(jobs[i].out, jobs[i].nbuckets, rec, d_init, st);
+      if (cur[i].any) launch_fill_u64(jobs[i].out, jobs[i].nbuckets, rec, init, st);
     launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
   } else {
     DG_FLUSH(cs, st);

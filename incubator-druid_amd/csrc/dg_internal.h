@@ -434,7 +434,11 @@ struct NumPred {
 // voff: row value offsets of a multi-value id column (VIEW_ABSENT otherwise); PRED_ID_SET over a
 // multi-value column: has_lo = whether an empty row (the null value) matches
 void launch_num_pred(ColView v, ColView voff, int64_t nrows, NumPred p, uint32_t* out, hipStream_t s);
-void launch_fill_u64(uint64_t* p, int64_t n_rows_of_slots, int slots_per_row, const uint64_t* d_init, hipStream_t s);
+// one record of accumulator slots, passed by value (a kernel argument: no staging copy)
+struct SlotInit {
+  uint64_t v[kMaxAggs + 1];
+};
+void launch_fill_u64(uint64_t* p, int64_t n_rows_of_slots, int slots_per_row, const SlotInit& init, hipStream_t s);
 void launch_scan_agg(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, int topn, hipStream_t s);
 // topN aggregation with LDS-private dictionary-id ranges: workgroup (p, s) owns ids
 // [p * range, (p + 1) * range) of segment s, scans every row of the segment and writes its range of

@@ -411,18 +411,18 @@ void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_
 // ------------------------------------------------------------------------------------------------
 // accumulator init
 // ------------------------------------------------------------------------------------------------
-__global__ void k_fill_u64(uint64_t* __restrict__ p, int64_t rows, int slots, const uint64_t* __restrict__ init) {
+__global__ void k_fill_u64(uint64_t* __restrict__ p, int64_t rows, int slots, SlotInit init) {
   const int64_t n = rows * slots;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    p[i] = init[i % slots];
+    p[i] = init.v[i % slots];
 }
 
-void launch_fill_u64(uint64_t* p, int64_t rows, int slots, const uint64_t* d_init, hipStream_t s) {
+void launch_fill_u64(uint64_t* p, int64_t rows, int slots, const SlotInit& init, hipStream_t s) {
   const int64_t n = rows * slots;
   if (n <= 0) return;
   int grid = (int)((n + 255) / 256);
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(k_fill_u64, dim3(grid), dim3(256), 0, s, p, rows, slots, d_init);
+  hipLaunchKernelGGL(k_fill_u64, dim3(grid), dim3(256), 0, s, p, rows, slots, init);
 }
 
 // ------------------------------------------------------------------------------------------------

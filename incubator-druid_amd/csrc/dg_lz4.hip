@@ -365,10 +365,15 @@ __device__ __forceinline__ void red_finish(const Lz4Job& job, uint64_t acc, uint
   __syncthreads();
   if ((threadIdx.x & 63) == 0) s_red[w] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t t = s_red[0];
-    for (int k = 1; k < nwaves; ++k) t = combine_op(job.red_op, t, s_red[k]);
-    atomic_op(job.red_op, job.red_dst, t);
+  if (w == 0) {  // the waves' results folded by the first wave's lanes, one atomic
+    const int l = threadIdx.x;
+    // lanes past the waves: a copy of wave 0's value for min / max (idempotent), +0 for the sums (the
+    // sums' identity in the slot encoding, like identity_of)
+    uint64_t t = l < nwaves ? s_red[l] : (job.red_op == OP_ADD_I64 || job.red_op == OP_ADD_F64 ? 0ull : s_red[0]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+      t = combine_op(job.red_op, t, (uint64_t)__shfl_xor((unsigned long long)t, o, 64));
+    if (l == 0) atomic_op(job.red_op, job.red_dst, t);
   }
 }
 

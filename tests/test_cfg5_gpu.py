@@ -175,13 +175,14 @@ def test_uniform_time_blocks_are_not_decoded(R, cfg5, kind, monkeypatch):
         assert_results(q, a, b)
 
 
-@pytest.mark.parametrize("shape", ["hourly", "hourly_cut", "all", "day_desc", "filtered"])
+@pytest.mark.parametrize("shape", ["hourly", "hourly_cut", "all", "day_desc", "pt6h_tz", "filtered"])
 def test_fused_decode_aggregate(Q, O, R, cfg5, shape, monkeypatch):
     """Timeseries decode fused with aggregation: the LZ4 value blocks whose rows share one bucket are
     folded by the decoder into the bucket's slot (no decoded image written, the scan skips their
     rows). Results equal the unfused path (DG_NO_FUSE=1) and the oracle, for every aggregator kind of
     configs[4]a (longSum, doubleSum, longMax, doubleMin), an interval cutting blocks, ALL granularity
-    (one bucket: every value block fused), a descending day query, and a filtered query (not fused)."""
+    (one bucket: every value block fused), a descending day query, calendar buckets in a +05:45 zone,
+    and a filtered query (not fused)."""
     B, g, o = cfg5
     base = B.make_query(Q, "ts_hourly")
     aggs = base.aggregations + [Q.long_min("lmin", "maxLongUniform"), Q.double_max("dmax", "sumFloatNormal")]
@@ -196,6 +197,9 @@ def test_fused_decode_aggregate(Q, O, R, cfg5, shape, monkeypatch):
         q = Q.TimeseriesQuery(intervals=iv, granularity="all", aggregations=aggs)
     elif shape == "day_desc":
         q = Q.TimeseriesQuery(intervals=[(lo, hi)], granularity="day", aggregations=aggs, descending=True)
+    elif shape == "pt6h_tz":  # calendar buckets (caller-given bucket starts): a zone with a 45-minute offset
+        q = Q.TimeseriesQuery(intervals=iv, aggregations=aggs,
+                              granularity={"type": "period", "period": "PT6H", "timeZone": "Asia/Kathmandu"})
     else:
         q = Q.TimeseriesQuery(intervals=iv, granularity="hour", aggregations=aggs,
                               filter=Q.BoundDimFilter("dimSequential", "100", "500"))
