@@ -577,7 +577,8 @@ def main():
     paths = ensure_segments(args.data_dir, rank, nseg, rows_per, args.compression, args.bitmap, args.lz4_mode, cols,
                             partitioned=args.config in ("ts_hourly", "groupby_hourly"), workers=args.write_workers,
                             long_encoding=args.long_encoding)
-    segs = [S.GpuSegment(p, device=local_rank) for p in paths]
+    device = D.device_index() if world > 1 else local_rank
+    segs = [S.GpuSegment(p, device=device) for p in paths]
     query = make_query(Q, args.config)
 
     gdict = None

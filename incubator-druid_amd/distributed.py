@@ -45,10 +45,20 @@ def init_from_env(prefer_nccl: bool = True):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     backend = "nccl" if (prefer_nccl and torch.cuda.is_available()) else "gloo"
+    # DG_DIST_BACKEND=gloo: the collectives on the host (rehearsal of the multi-rank path with several
+    # ranks on one GPU, which RCCL refuses: "Duplicate GPU detected")
+    backend = os.environ.get("DG_DIST_BACKEND", backend)
     if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(device_index())
     dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return dist
+
+
+def device_index() -> int:
+    """This rank's GPU: LOCAL_RANK, or DG_BENCH_DEVICE when set (every rank on that one device: a
+    rehearsal with DG_DIST_BACKEND=gloo on a one-GPU box)."""
+    forced = os.environ.get("DG_BENCH_DEVICE")
+    return int(forced) if forced not in (None, "") else int(os.environ.get("LOCAL_RANK", "0"))
 
 
 def _device(dist):
@@ -435,15 +445,17 @@ class GroupByExchange:
         bounds = np.concatenate([[0], pos, [n]]).astype(np.int64)
         send = np.diff(bounds)
         dev = keys.device
-        cnt_in = torch.from_numpy(send.astype(np.int64)).to(_device(self.dist))
+        cdev = _device(self.dist)  # where the collective's tensors live (the GPU under RCCL)
+        cnt_in = torch.from_numpy(send.astype(np.int64)).to(cdev)
         cnt_out = torch.empty_like(cnt_in)
         self.dist.all_to_all_single(cnt_out, cnt_in)
         recv = cnt_out.cpu().numpy().astype(np.int64)
-        rkeys = torch.empty(int(recv.sum()), dtype=torch.int64, device=dev)
-        rslots = torch.empty(int(recv.sum()) * self.rec, dtype=torch.int64, device=dev)
-        self.dist.all_to_all_single(rkeys, keys.contiguous(), [int(x) for x in recv], [int(x) for x in send])
-        self.dist.all_to_all_single(rslots, slots.contiguous(), [int(x) * self.rec for x in recv],
+        rkeys = torch.empty(int(recv.sum()), dtype=torch.int64, device=cdev)
+        rslots = torch.empty(int(recv.sum()) * self.rec, dtype=torch.int64, device=cdev)
+        self.dist.all_to_all_single(rkeys, keys.contiguous().to(cdev), [int(x) for x in recv], [int(x) for x in send])
+        self.dist.all_to_all_single(rslots, slots.contiguous().to(cdev), [int(x) * self.rec for x in recv],
                                     [int(x) * self.rec for x in send])
+        rkeys, rslots = rkeys.to(dev), rslots.to(dev)  # (no copies when the collective ran on the GPU)
         res = self.engine.merge(self.ks, rkeys, rslots, self.query, self.dicts)
         if self.starts is not None:
             res.time_map = self.starts  # dg_merge times are bucket indices into the query's bucket list
