@@ -218,6 +218,9 @@ typedef struct {
   /* since ABI 13: timeseries LZ4 blocks whose decode was fused with their aggregator (the decoder
      folded the block's values into its bucket's slot and wrote no decoded image) */
   int64_t lz4_fused_blocks;
+  /* the wall time the general decoder ran on either stream (the union of its main- and side-stream
+     spans; lz4_general_ms is their sum) */
+  double lz4_general_wall_ms;
 } dg_metrics;
 
 /* Aggregate values are returned in 8-byte slots: int64 for count/long*, double for double*,

@@ -76,7 +76,7 @@ class dg_metrics(ctypes.Structure):
                 ("lz4_general_ms", ctypes.c_double), ("lz4_general_bytes", ctypes.c_int64),
                 ("lz4_general_blocks", ctypes.c_int32), ("lz4_general_launches", ctypes.c_int32),
                 ("bitmap_bytes", ctypes.c_int64), ("reduce_kernel_ms", ctypes.c_double),
-                ("lz4_fused_blocks", ctypes.c_int64)]
+                ("lz4_fused_blocks", ctypes.c_int64), ("lz4_general_wall_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -415,8 +415,20 @@ static void decode_events(Context* ctx, DecodeBatch* db, bool side) {
   db->gen_b = ctx->gen_ev[side ? 3 : 1];
 }
 // a call's decode metrics from its main and side batches
-static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_metrics* m) {
+static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_metrics* m, hipEvent_t base) {
   m->lz4_general_ms = gen_ms(db) + gen_ms(side);
+  // the wall time the general decoder ran on either stream: the union of the two spans (from the
+  // call's first event)
+  m->lz4_general_wall_ms = m->lz4_general_ms;
+  if (db.gen_blocks && side.gen_blocks && db.gen_a && side.gen_a && base) {
+    float s1 = 0, e1 = 0, s2 = 0, e2 = 0;
+    hipEventElapsedTime(&s1, base, db.gen_a);
+    hipEventElapsedTime(&e1, base, db.gen_b);
+    hipEventElapsedTime(&s2, base, side.gen_a);
+    hipEventElapsedTime(&e2, base, side.gen_b);
+    const double overlap = std::max(0.0, (double)std::min(e1, e2) - (double)std::max(s1, s2));
+    m->lz4_general_wall_ms = (double)(e1 - s1) + (double)(e2 - s2) - overlap;
+  }
   m->lz4_general_bytes = db.gen_bytes + side.gen_bytes;
   m->lz4_general_blocks = db.gen_blocks + side.gen_blocks;
   m->lz4_general_launches = db.gen_launches + side.gen_launches;
@@ -2286,7 +2298,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
-  decode_metrics(db, DecodeBatch(), &m);
+  decode_metrics(db, DecodeBatch(), &m, nullptr);
   m.aggregate_ms = f3;
   m.total_ms = ms_since(t0);
   if (metrics) *metrics = m;
@@ -2882,7 +2894,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
-  decode_metrics(db, DecodeBatch(), &m);
+  decode_metrics(db, DecodeBatch(), &m, nullptr);
   m.aggregate_ms = f3;
   m.total_ms = ms_since(t0);
   ht.mark("done");
@@ -3196,6 +3208,10 @@ static int merged_dict(Context* ctx, Segment* const* segs, int n, const std::str
     }
     for (int i = 0; i < n; ++i) {
       if (host[i].empty()) continue;
+      // a segment whose dictionary is the merged one keeps its ids: no table (no lookup per row)
+      bool identity = true;
+      for (size_t k = 0; identity && k < host[i].size(); ++k) identity = host[i][k] == (int32_t)k;
+      if (identity) continue;
       md->remap[i].reset(new DevBuf());
       if (!md->remap[i]->alloc(host[i].size() * 4)) return set_error(DG_ERR_OOM, "hipMalloc dictionary map");
       DG_HIP(hipMemcpy(md->remap[i]->p, host[i].data(), host[i].size() * 4, hipMemcpyHostToDevice));
@@ -3527,7 +3543,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
-  decode_metrics(db, db_side, &m);
+  decode_metrics(db, db_side, &m, ctx->ev[0]);
   m.aggregate_ms = f3;
   m.keygen_ms = f4;
   m.sort_ms = f5;

@@ -32,7 +32,7 @@ def test_abi_version_and_structs():
     assert ctypes.sizeof(N.dg_filter) == 64
     assert ctypes.sizeof(N.dg_agg) == 32
     assert ctypes.sizeof(N.dg_scan) == 96
-    assert ctypes.sizeof(N.dg_metrics) == 168
+    assert ctypes.sizeof(N.dg_metrics) == 176
     assert ctypes.sizeof(N.dg_topn_lists) == 40
     assert ctypes.sizeof(N.dg_topn) == 56
     assert ctypes.sizeof(N.dg_order_column) == 16
