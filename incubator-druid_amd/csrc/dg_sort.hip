@@ -260,9 +260,17 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
         if (!((inplace >> a) & 1u)) payload[pay_at(pw, ref, a)] = val(a);
     }
   };
-  if (!MULTI && !j.bitset && j.time.kind == VIEW_ABSENT) {
-    // every row of the tile is selected (no filter, the interval covers the segment): element index =
-    // tile base + row offset, no per-block scan.
+  // every row of the tile selected: no filter, and the interval covers the segment or the tile's
+  // __time block is a uniform one (time_view: its rows all inside the interval, in one bucket)
+  bool all_rows = !MULTI && !j.bitset;
+  int64_t tbucket = 0;
+  if (all_rows && j.time.kind != VIEW_ABSENT) {
+    const int64_t tk = r0 >> j.time.log2_per;
+    all_rows = (reinterpret_cast<uintptr_t>(j.time.blocks[tk]) & 1u) && tk == ((r1 - 1) >> j.time.log2_per);
+    if (all_rows) all_rows = gb_select(j, r0, &tbucket);
+  }
+  if (all_rows) {
+    // element index = tile base + row offset, no per-block scan.
     // A tile (kTileRows, aligned) lies inside one block of every view (blocks hold >= 8192 rows):
     // each column's block pointer is then read once per tile (a scalar load) instead of per row, and
     // 3-byte ids are two aligned dword loads instead of three byte loads.
@@ -274,32 +282,54 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
       direct &= ((inplace >> a) & 1u) || j.vals[a].kind == VIEW_ABSENT ||
                 (r0 >> j.vals[a].log2_per) == ((r1 - 1) >> j.vals[a].log2_per);
     if (direct) {
-      for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
-        const uint32_t idx = base + (uint32_t)(r - r0);
-        uint64_t key = ((uint64_t)j.seg_slot << j.seg_shift);
-        for (int d = 0; d < j.ndims; ++d) {
-          const ColView& v = j.dims[d];
-          uint32_t g = (uint32_t)j.null_gid[d];
-          if (v.kind == VIEW_IDS) {
-            const int64_t blk = r0 >> v.log2_per;
-            const uint8_t* bp = v.blocks[blk];
-            const uint32_t off = (uint32_t)(r - (blk << v.log2_per)) * (uint32_t)v.width;
-            uint32_t id;
-            if (v.width == 3) {  // the slot / flat allocation extends past the last id's dword
-              const uint32_t* w = reinterpret_cast<const uint32_t*>(bp + (off & ~3u));
-              id = __builtin_amdgcn_alignbyte(w[1], w[0], off & 3u) & 0xFFFFFFu;
-            } else if (v.width == 1) {
-              id = bp[off];
-            } else if (v.width == 2) {
-              id = *reinterpret_cast<const uint16_t*>(bp + off);
-            } else {
-              id = *reinterpret_cast<const uint32_t*>(bp + off);
+      // kB rows per thread (one batch: the whole tile), each dimension's id loads of the batch in flight
+      // together, then its dictionary-map lookups together
+      constexpr int kB = kTileRows / 256;
+      static_assert(kTileRows % 256 == 0, "whole batches per tile");
+      uint64_t key[kB];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) key[u] = ((uint64_t)j.seg_slot << j.seg_shift) | ((uint64_t)tbucket << j.bucket_shift);
+      for (int d = 0; d < j.ndims; ++d) {
+        const ColView& v = j.dims[d];
+        uint32_t g[kB];
+        if (v.kind == VIEW_IDS) {
+          const int64_t blk = r0 >> v.log2_per;
+          const uint8_t* bp = v.blocks[blk];
+          uint32_t id[kB];
+#pragma unroll
+          for (int u = 0; u < kB; ++u) {
+            const int64_t r = r0 + threadIdx.x + 256 * u;
+            id[u] = 0;
+            if (r < r1) {
+              const uint32_t off = (uint32_t)(r - (blk << v.log2_per)) * (uint32_t)v.width;
+              if (v.width == 3) {  // the slot / flat allocation extends past the last id's dword
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(bp + (off & ~3u));
+                id[u] = __builtin_amdgcn_alignbyte(w[1], w[0], off & 3u) & 0xFFFFFFu;
+              } else if (v.width == 1) {
+                id[u] = bp[off];
+              } else if (v.width == 2) {
+                id[u] = *reinterpret_cast<const uint16_t*>(bp + off);
+              } else {
+                id[u] = *reinterpret_cast<const uint32_t*>(bp + off);
+              }
             }
-            g = j.remap[d] ? (uint32_t)j.remap[d][id] : id;
           }
-          key |= (uint64_t)g << j.dim_shift[d];
+          const int32_t* rm = j.remap[d];
+#pragma unroll
+          for (int u = 0; u < kB; ++u) g[u] = rm ? (uint32_t)rm[id[u]] : id[u];  // (rows past r1: id 0, a valid index)
+        } else {
+#pragma unroll
+          for (int u = 0; u < kB; ++u) g[u] = (uint32_t)j.null_gid[d];
         }
-        emit(idx, rowref ? j.row_base + (uint32_t)r : idx, key, [&](int a) -> uint64_t {
+#pragma unroll
+        for (int u = 0; u < kB; ++u) key[u] |= (uint64_t)g[u] << j.dim_shift[d];
+      }
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const int64_t r = r0 + threadIdx.x + 256 * u;
+        if (r >= r1) continue;
+        const uint32_t idx = base + (uint32_t)(r - r0);
+        emit(idx, rowref ? j.row_base + (uint32_t)r : idx, key[u], [&](int a) -> uint64_t {
           const ColView& v = j.vals[a];
           if (!agg_row(j.agg_bits[a], r)) return identity_of(plan.op[a], plan.kind[a]);
           if (plan.kind[a] == DG_AGG_COUNT || v.kind == VIEW_ABSENT) return agg_input_at(plan.kind[a], v.kind, nullptr);
@@ -311,7 +341,7 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
     }
     for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
       const uint32_t idx = base + (uint32_t)(r - r0);
-      emit(idx, rowref ? j.row_base + (uint32_t)r : idx, gb_key(j, r, 0), [&](int a) { return agg_in(j, plan, a, r); });
+      emit(idx, rowref ? j.row_base + (uint32_t)r : idx, gb_key(j, r, tbucket), [&](int a) { return agg_in(j, plan, a, r); });
     }
     return;
   }
