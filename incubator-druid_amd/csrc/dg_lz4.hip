@@ -60,11 +60,15 @@ constexpr int kLzWaves = kLzThreads / 64;
 constexpr int kLz4InCap = kBlockBytes + 2048;  // >= LZ4_compressBound(65536) = 65809
 constexpr int kTail = 0xFF00;                  // E codes >= kTail are literals; positions >= kTail use the tail table
 constexpr int kTailN = kBlockBytes - kTail;    // 256
+constexpr uint32_t kTailLit = 0x10000u;        // tail table word: a literal byte (else an absolute source)
 constexpr int kShortLit = 4;                   // literal runs up to this ride in the parse registers
 static_assert(kShortLit <= 4, "Tok::lv holds four literal bytes");
 constexpr int kLongFill = 48;                  // matches above this are filled cooperatively
 constexpr int kMaxJobs = 2048;
 constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
+#ifndef DG_LZ_BATCH_APPEND
+#define DG_LZ_BATCH_APPEND 1  // the class scan's open terminals listed once per thread (0: per pair, A/B)
+#endif
 #ifndef DG_LZ_JUMP_BATCH
 #define DG_LZ_JUMP_BATCH 4
 #endif
@@ -164,15 +168,26 @@ __device__ __forceinline__ bool parse_tok(const uint8_t* __restrict__ in, int n,
   return t.off != 0;
 }
 
+// inclusive add-scan over the 64 lanes of a wave: row shifts 1/2/4/8, then the row broadcasts of
+// lanes 15 and 31 (DPP: no LDS round trips, unlike a __shfl_up ladder)
+template <int CTRL, int RMASK>
+__device__ __forceinline__ int dpp_add_step(int v) {
+  return v + __builtin_amdgcn_update_dpp(0, v, CTRL, RMASK, 0xf, false);
+}
+__device__ __forceinline__ int wave_add_scan(int v) {
+  v = dpp_add_step<0x111, 0xf>(v);  // row_shr:1
+  v = dpp_add_step<0x112, 0xf>(v);  // row_shr:2
+  v = dpp_add_step<0x114, 0xf>(v);  // row_shr:4
+  v = dpp_add_step<0x118, 0xf>(v);  // row_shr:8
+  v = dpp_add_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v = dpp_add_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+
 // block-wide (1024 threads) exclusive scan; total via *total
 __device__ int block_scan_lz(int v, int* total, int* s_tmp) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  const int x = wave_add_scan(v);
   if (lane == 63) s_tmp[wave] = x;
   __syncthreads();
   int wave_off = 0, tot = 0;
@@ -193,24 +208,25 @@ constexpr int kESkewShift = 7;
 constexpr int kEWords = kBlockBytes + (kBlockBytes >> kESkewShift) * 2;  // u16 entries incl. skew
 __device__ __forceinline__ int eph(int x) { return x + ((x >> kESkewShift) << 1); }
 
+// The fill writes E at every position, the tail's too: a literal code, or the distance when it is
+// below kTail. A tail position whose distance is not (a match reaching the block's first bytes) gets
+// E = 0 and its absolute source in the tail table. Before the tail's rounds its wave turns the tail's
+// E entries into tail-table words (absolute sources, or kTailLit | byte), so the fill's common path
+// serves the tail's sequences too.
 struct LzState {
   uint16_t* e;
-  uint16_t* tsrc;
-  uint32_t* tlit;
+  uint32_t* tsrc;  // tail positions: absolute source, or kTailLit | the literal byte
 };
 
-__device__ __forceinline__ void put_lit(const LzState& S, int x, int v) {
-  if (x < kTail) {
-    S.e[eph(x)] = (uint16_t)(0xFF00 | v);
-  } else {
-    S.tsrc[x - kTail] = (uint16_t)v;
-    atomicOr(&S.tlit[(x - kTail) >> 5], 1u << ((x - kTail) & 31));
-  }
-}
+__device__ __forceinline__ void put_lit(const LzState& S, int x, int v) { S.e[eph(x)] = (uint16_t)(0xFF00 | v); }
 
 __device__ __forceinline__ void put_ptr(const LzState& S, int x, int src) {
-  if (x < kTail) S.e[eph(x)] = (uint16_t)(x - src);
-  else S.tsrc[x - kTail] = (uint16_t)src;
+  if (x - src < kTail) {
+    S.e[eph(x)] = (uint16_t)(x - src);
+  } else {
+    S.e[eph(x)] = 0;
+    S.tsrc[x - kTail] = (uint32_t)src;
+  }
 }
 
 // value of output byte x once E and the tail table have converged (literal codes, or in E one hop
@@ -226,10 +242,18 @@ __device__ __forceinline__ uint32_t lz_value(const LzState& S, int x) {
 
 // E entries of one sequence in the general form (out of line: the rare cases): literals that did not
 // get a job (table full; read from the compressed block in HBM, `lit` = input offset) or whose
-// bytes ride in `lv`, matches without a job, and sequences reaching the tail table.
-__device__ __noinline__ void fill_general(uint16_t* e, uint16_t* tsrc, uint32_t* tlit, const uint8_t* __restrict__ gin, int o, int L, int M, int d,
+// bytes ride in `lv`, matches without a job, and tail matches at distances >= kTail.
+#ifndef DG_LZ_FILL_INLINE
+#define DG_LZ_FILL_INLINE 0  // (A/B: the rare-case fill inlined at its call sites)
+#endif
+#if DG_LZ_FILL_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+void fill_general(uint16_t* e, uint32_t* tsrc, const uint8_t* __restrict__ gin, int o, int L, int M, int d,
                                           uint32_t lv, bool lit_inline, bool lit_here, bool match_here) {
-  const LzState S{e, tsrc, tlit};
+  const LzState S{e, tsrc};
   if (lit_inline) {
     for (int k = 0; k < L; ++k) put_lit(S, o + k, (int)gld1(gin + lv + k));
   } else if (lit_here) {
@@ -265,17 +289,21 @@ __device__ __forceinline__ uint32_t wave_max_scan(uint32_t v) {
 
 // Wave-aggregated slot allocation: each lane asking for n slots gets its first slot index.
 __device__ __forceinline__ int wave_alloc(int* counter, int n) {
-  int incl = n;  // inclusive prefix of n over the lanes
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o, 64);
-    if ((int)(threadIdx.x & 63) >= o) incl += y;
-  }
-  const int total = __shfl(incl, 63, 64);
+  const int incl = wave_add_scan(n);  // inclusive prefix of n over the lanes
+  const int total = __builtin_amdgcn_readlane(incl, 63);
   int base = 0;
   if ((threadIdx.x & 63) == 63 && total) base = atomicAdd(counter, total);
-  return __shfl(base, 63, 64) + incl - n;
+  return __builtin_amdgcn_readlane(base, 63) + incl - n;
 }
+
+#ifndef DG_LZ_WAVE_STAMP
+#define DG_LZ_WAVE_STAMP 3  // (diagnostic builds: the point whose per-wave times fill prof[16..31])
+#endif
+#define LZ_WAVE_STAMP(k)                                                                                  \
+  do {                                                                                                    \
+    if (PROF && DG_LZ_WAVE_STAMP == (k) && (tid & 63) == 0)                                               \
+      prof[(size_t)blockIdx.x * kLz4ProfWords + 16 + (tid >> 6)] = __builtin_amdgcn_s_memtime();          \
+  } while (0)
 
 #define LZ_STAMP(k)                                                                           \
   do {                                                                                        \
@@ -381,8 +409,7 @@ template <bool PROF, int SEQ>
 __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
                                                            uint64_t* __restrict__ prof) {
   __shared__ __attribute__((aligned(16))) uint16_t s_e[kEWords];  // 130 KiB: staged input, then E
-  __shared__ uint16_t s_tsrc[kTailN];
-  __shared__ uint32_t s_tlit[kTailN / 32];
+  __shared__ uint32_t s_tsrc[kTailN];
   __shared__ uint2 s_jobs_buf[kMaxJobs + kMaxJobs / 2];  // jobs, then their prefix sums; later the open list
   uint2* s_job = s_jobs_buf;
   int* s_jpre = reinterpret_cast<int*>(s_jobs_buf + kMaxJobs);
@@ -401,7 +428,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   LZ_STAMP(0);
   uint8_t* s_in = reinterpret_cast<uint8_t*>(s_e);
   uint32_t* s_e32 = reinterpret_cast<uint32_t*>(s_e);
-  const LzState S{s_e, s_tsrc, s_tlit};
+  const LzState S{s_e, s_tsrc};
   // ---- stage the compressed block (16-byte aligned and padded in the device image) ----
   {
     uint4* dst = reinterpret_cast<uint4*>(s_in);
@@ -413,7 +440,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       s_bad = 0;
       s_c8 = 0;
     }
-    if (tid < kTailN / 32) s_tlit[tid] = 0;
   }
   __syncthreads();
   LZ_STAMP(1);
@@ -442,6 +468,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
     if (pos != end) s_bad = 1;
   }
+  LZ_WAVE_STAMP(0);
   int total;
   const int base = block_scan_lz(out_rel, &total, s_tmp);  // its barriers end every read of s_in
   LZ_STAMP(2);
@@ -458,23 +485,27 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   constexpr uint32_t kInlineLit = 0x80000000u, kInlineMatch = 0x40000000u;  // r_L flags: job table full
   int c8 = 0;  // match bytes at distance 8 (class chains of 8-byte values, resolved by a scan below)
   {  // (every lane of the wave takes part: slot allocation is wave-aggregated)
+    // my job slots: one wave-aggregated allocation for all my sequences (one LDS atomic per wave)
+    int need = 0;
+#pragma unroll
+    for (int s = 0; s < SEQ; ++s)
+      if (s < cnt) need += ((int)r_L[s] > kShortLit) + ((int)(r_DM[s] >> 16) > kLongFill);
+    int j = __ballot(need) ? wave_alloc(&s_njob, need) : 0;
     int o = base;
 #pragma unroll
     for (int s = 0; s < SEQ; ++s) {
       const bool act = s < cnt;  // (cnt = 0 beyond the checkpoints)
       const int L = act ? (int)r_L[s] : 0;
       const int d = (int)(r_DM[s] & 0xFFFF), M = act ? (int)(r_DM[s] >> 16) : 0;
-      const int nl = L > kShortLit, nm = M > kLongFill;
-      if (__ballot(nl | nm)) {  // job slots: one LDS atomic per wave
-        const int j = wave_alloc(&s_njob, nl + nm);
-        if (nl) {
-          if (j < kMaxJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(L - 1) << 16), r_lv[s]);
-          else r_L[s] |= kInlineLit;
-        }
-        if (nm) {
-          if (j + nl < kMaxJobs) s_job[j + nl] = make_uint2((uint32_t)(o + L) | ((uint32_t)(M - 1) << 16), (uint32_t)d | 0x80000000u);
-          else r_L[s] |= kInlineMatch;
-        }
+      if (L > kShortLit) {
+        if (j < kMaxJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(L - 1) << 16), r_lv[s]);
+        else r_L[s] |= kInlineLit;
+        ++j;
+      }
+      if (M > kLongFill) {
+        if (j < kMaxJobs) s_job[j] = make_uint2((uint32_t)(o + L) | ((uint32_t)(M - 1) << 16), (uint32_t)d | 0x80000000u);
+        else r_L[s] |= kInlineMatch;
+        ++j;
       }
       c8 += d == kClass ? M : 0;
       o += L + M;
@@ -482,6 +513,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     for (int off = 32; off > 0; off >>= 1) c8 += __shfl_xor(c8, off, 64);  // wave sum, one LDS atomic
     if ((tid & 63) == 0 && c8) atomicAdd(&s_c8, c8);
   }
+  LZ_WAVE_STAMP(1);
   __syncthreads();
   const int nj = min(s_njob, kMaxJobs);
   int tot = 0;
@@ -554,6 +586,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       }
     }
   }
+  LZ_WAVE_STAMP(2);
   __syncthreads();  // every read of the staged input is done
   // class mode (mostly distance-8 matches): E starts as all 8, and the fill skips distance-8 matches
   const bool cls = s_c8 * 4 > total;
@@ -564,6 +597,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     __syncthreads();
   }
   LZ_STAMP(3);
+  uint64_t tfg = 0;  // (PROF: cycles in fill_general)
   if (tid < ncp) {
     int o = base;
 #pragma unroll
@@ -572,7 +606,8 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         const uint32_t lf = r_L[s];
         const int L = (int)(lf & 0x3FFFFFFFu);
         const int d = (int)(r_DM[s] & 0xFFFF), M = (int)(r_DM[s] >> 16);
-        const bool fast = !(lf & (kInlineLit | kInlineMatch)) && o + L + M <= kTail;
+        // (a tail sequence's entries stay below kTail when d + M does: d * (1 + k / d) <= d + k)
+        const bool fast = !(lf & (kInlineLit | kInlineMatch)) && (o + L + M <= kTail || d + M < kTail);
         if (fast) {  // the common case: plain E entries, no tail table
           if (L <= kShortLit) {
             const uint32_t lv = r_lv[s];
@@ -598,8 +633,10 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
             }
           }
         } else {
-          fill_general(s_e, s_tsrc, s_tlit, gin, o, L, M, d, r_lv[s], (lf & kInlineLit) != 0, L <= kShortLit,
+          const uint64_t tf0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
+          fill_general(s_e, s_tsrc, gin, o, L, M, d, r_lv[s], (lf & kInlineLit) != 0, L <= kShortLit,
                        (lf & kInlineMatch) != 0 || (M > 0 && M <= kLongFill));
+          if (PROF) tfg += __builtin_amdgcn_s_memtime() - tf0;
         }
         o += L;
         if (M > 0) {
@@ -609,7 +646,8 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       }
     }
   }
-  if (PROF && (tid & 63) == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + 16 + (tid >> 6)] = __builtin_amdgcn_s_memtime();
+  LZ_WAVE_STAMP(3);
+  if (PROF && tid == ncp - 1) prof[(size_t)blockIdx.x * kLz4ProfWords + 14] = tfg;
   if (g0 < gend) {  // my job range: literal codes from lit4, distances for long matches
     walk_reset();
 #pragma unroll
@@ -696,6 +734,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   if (tid == 0) s_nopen = 0;
   __syncthreads();
   const int wv = tid >> 6, ln = tid & 63;
+#if !DG_LZ_BATCH_APPEND
   auto list_append = [&](bool op, int v) {  // wave-aggregated append to s_open
     const uint64_t bal = __ballot(op);
     if (bal) {
@@ -706,6 +745,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       if (op && at < kOpenCap) s_open[at] = (uint16_t)v;
     }
   };
+#endif
   auto is_open = [](uint32_t v) { return (v & 0xFFFF) < (uint32_t)kTail || (v >> 16) < (uint32_t)kTail; };
   // one jump step for an entry d whose target holds e
   auto jstep = [](uint32_t d, uint32_t e) -> uint32_t {
@@ -786,6 +826,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       if (ln == 63) s_scan[wv * kClass + c] = v;
     }
     __syncthreads();
+    LZ_STAMP(12);
     {  // the earlier waves' totals: lane l reads class l % 8 of waves l / 8 and 8 + l / 8, then a
        // max over the lanes of one class; no loop of dependent LDS reads
       static_assert(kLzWaves == 16 && kClass == 8, "s_scan = two entries per lane");
@@ -796,6 +837,9 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 #pragma unroll
       for (int c = 0; c < kClass; ++c) carry[c] = max(carry[c], (uint32_t)__builtin_amdgcn_readlane((int)v, c));
     }
+#if DG_LZ_BATCH_APPEND
+    uint64_t omask = 0;  // my open terminals (bit = position - x0)
+#endif
     auto take = [](uint32_t key, int x) -> uint32_t {  // new entry of a distance-8 byte at x
       const uint32_t tv = key & 0xFFFF;
       return tv >= (uint32_t)kTail ? tv : (uint32_t)(x + 1) - (key >> 16);
@@ -820,10 +864,27 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       }
       const uint32_t nv = lo | (hi << 16);
       if (nv != v) s_e32[eb + q] = nv;  // x < lim whenever an entry changes
+#if DG_LZ_BATCH_APPEND
+      omask |= (uint64_t)(t0 && lo < (uint32_t)kTail) << (2 * q);
+      omask |= (uint64_t)(t1 && hi < (uint32_t)kTail) << (2 * q + 1);
+#else
       list_append(t0 && lo < (uint32_t)kTail, x);  // open terminals
       list_append(t1 && hi < (uint32_t)kTail, x + 1);
+#endif
     }
+#if DG_LZ_BATCH_APPEND
+    {
+      const int nm = __popcll(omask);
+      if (__ballot(nm)) {
+        int at = wave_alloc(&s_nopen, nm);
+        for (; omask; omask &= omask - 1, ++at)
+          if (at < kOpenCap) s_open[at] = (uint16_t)(x0 + __builtin_ctzll(omask));
+      }
+    }
+#endif
+    LZ_WAVE_STAMP(4);
     __syncthreads();
+    LZ_STAMP(13);
     const int no = s_nopen;
     if (no <= kOpenCap) {
       // terminal rounds over the list, then one sweep: every scanned entry reads its terminal's code
@@ -858,7 +919,10 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
   } else {
     jump_rounds = 1;
-    if (__syncthreads_or(sweep(true))) {
+    const bool open1 = __syncthreads_or(sweep(true));
+    LZ_STAMP(12);
+    LZ_STAMP(13);
+    if (open1) {
       // later rounds: thread t takes bitmap word t (pairs 32t .. 32t + 31) and steps its open pairs
       uint32_t m = s_obits[tid];
       int cnt_open = __popc(m);
@@ -962,8 +1026,17 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   };
   if (has_tail && wv == kLzWaves - 1) {
     const int nt = total - kTail;
-    auto lit_at = [&](int i) { return (s_tlit[i >> 5] >> (i & 31)) & 1u; };
+    auto lit_at = [&](int i) { return s_tsrc[i] >> 16; };
     uint32_t act = 0;  // bit k: position ln + 64 k still a source
+#pragma unroll
+    for (int k = 0; k < kTailN / 64; ++k) {  // the tail's E entries -> tail-table words
+      const int i = ln + 64 * k;
+      if (i < nt) {
+        const uint32_t e = s_e[eph(kTail + i)];
+        if (e >= (uint32_t)kTail) s_tsrc[i] = kTailLit | (e & 0xFFu);
+        else if (e) s_tsrc[i] = (uint32_t)(kTail + i - (int)e);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < kTailN / 64; ++k) {
       const int i = ln + 64 * k;
@@ -981,22 +1054,17 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         if ((act >> k) & 1u) {
           const int src = s_tsrc[ln + 64 * k];
           if (src < kTail) {
-            nsrc[k] = final_code(src);
+            nsrc[k] = kTailLit | (final_code(src) & 0xFFu);
             res |= 1u << k;
           } else {
-            const int i2 = src - kTail;
-            nsrc[k] = s_tsrc[i2];
-            res |= lit_at(i2) << k;
+            nsrc[k] = s_tsrc[src - kTail];  // a flagged literal, or its source
+            res |= (nsrc[k] >> 16) << k;
           }
         }
       }
 #pragma unroll
       for (int k = 0; k < kTailN / 64; ++k) {
-        if ((act >> k) & 1u) {
-          const int i = ln + 64 * k;
-          s_tsrc[i] = (uint16_t)nsrc[k];
-          if ((res >> k) & 1u) atomicOr(&s_tlit[i >> 5], 1u << (i & 31));
-        }
+        if ((act >> k) & 1u) s_tsrc[ln + 64 * k] = nsrc[k];
       }
       act &= ~res;
     }
@@ -1005,6 +1073,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     const int nthr = has_tail ? kLzThreads - 64 : kLzThreads;
     for (int c = tid; c < nbody; c += nthr) out_chunk(c);
   }
+  LZ_WAVE_STAMP(5);
   if (has_tail) {
     __syncthreads();
     if (s_bad) {
@@ -1111,12 +1180,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
     bad = pos != end || (tid + 1 < ncp && cnt != g);
   }
   // ---- 2. block scan of the intervals' output lengths -> sequence table (over the staged input) ----
-  int x = out_rel;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  const int x = wave_add_scan(out_rel);
   if (lane == 63) s_tmp[wave] = x;
   if (bad) s_bad = 1;
   __syncthreads();  // also the end of every read of the staged input

@@ -70,8 +70,13 @@ def report(name, ms, p, decoder=""):
     print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(PHASES, d.mean(axis=0))))
     if decoder != "general":
         return
-    fw = p[:, 16:32] - p[:, 3:4]  # each wave's own end of the fill, from the start of the fill
-    print(f"   fill end per wave (mean over blocks): first={fw.min(axis=1).mean():8.0f} last={fw.max(axis=1).mean():8.0f}")
+    sub = {"scan1": p[:, 12] - p[:, 4], "scan2": p[:, 13] - p[:, 12], "rounds": p[:, 5] - p[:, 13]}
+    print("   resolve (mean): " + "  ".join(f"{nm}={v.mean():8.0f}" for nm, v in sub.items()))
+    base = int(os.environ.get("LZ4_WAVE_BASE", "3"))  # the phase start of the build's DG_LZ_WAVE_STAMP point
+    fw = p[:, 16:32] - p[:, base:base + 1]  # each wave's own end of the phase, from the phase start
+    print(f"   phase end per wave (mean over blocks): first={fw.min(axis=1).mean():8.0f} last={fw.max(axis=1).mean():8.0f}")
+    print(f"   fill_general cycles in the last interval's wave: {p[:, 14].mean():8.0f}")
+    print("   phase end by wave index: " + " ".join(f"{v:.0f}" for v in fw.mean(axis=0)))
 
 
 def main():
