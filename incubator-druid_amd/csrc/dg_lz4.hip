@@ -66,6 +66,9 @@ static_assert(kShortLit <= 4, "Tok::lv holds four literal bytes");
 constexpr int kLongFill = 48;                  // matches above this are filled cooperatively
 constexpr int kMaxJobs = 2048;
 constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
+#ifndef DG_LZ_STAGED
+#define DG_LZ_STAGED 1  // non-class resolution in position-ordered stages (0: sweep + rounds, A/B)
+#endif
 #ifndef DG_LZ_BATCH_APPEND
 #define DG_LZ_BATCH_APPEND 1  // the class scan's open terminals listed once per thread (0: per pair, A/B)
 #endif
@@ -796,6 +799,62 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
     return any;
   };
+#if DG_LZ_STAGED
+  // Staged resolution in position order: stage s takes the 2 * kLzThreads pairs after stage s - 1, all
+  // of whose entries are literal codes by then, so a target before the stage is one read from its
+  // code. A target inside the stage (distance < the stage) is followed for up to kStageSteps more
+  // jumps (no barrier: entries only ever get closer to their code, so any value read is valid); pairs
+  // still open are set in the open-pair bitmap for the rounds below. One barrier per stage.
+  auto staged = [&]() -> bool {
+    constexpr int kStage = 2 * kLzThreads;  // pairs per stage
+    constexpr int kStageSteps = 6;
+    const int npairs = (lim + 1) >> 1;
+    bool any = false;
+#pragma unroll 1
+    for (int p0 = 0; p0 < npairs; p0 += kStage) {
+      uint32_t v[2], nv[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int x = 2 * (p0 + k * kLzThreads + tid);
+        v[k] = x < kTail ? s_e32[eph(x) >> 1] : 0xFF00FF00u;
+        nv[k] = v[k];
+      }
+#pragma unroll 1
+      for (int it = 0; it <= kStageSteps; ++it) {
+        uint32_t ta[2], tb[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int x = 2 * (p0 + k * kLzThreads + tid);
+          const uint32_t d0 = nv[k] & 0xFFFF, d1 = nv[k] >> 16;
+          ta[k] = d0 < (uint32_t)kTail ? s_e[eph(x - (int)d0)] : 0xFF00u;
+          tb[k] = d1 < (uint32_t)kTail ? s_e[eph(x + 1 - (int)d1)] : 0xFF00u;
+        }
+        bool open = false;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          nv[k] = jstep(nv[k] & 0xFFFF, ta[k]) | (jstep(nv[k] >> 16, tb[k]) << 16);
+          open |= is_open(nv[k]);
+        }
+        if (!__ballot(open)) break;
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int x = 2 * (p0 + k * kLzThreads + tid);
+        if (nv[k] != v[k]) s_e32[eph(x) >> 1] = nv[k];  // (x < kTail whenever an entry changes)
+        const bool op = is_open(nv[k]);
+        any |= op;
+        const uint64_t bal = __ballot(op);  // 64 consecutive pairs: two bitmap words
+        const int w0 = (p0 + k * kLzThreads + wv * 64) >> 5;
+        if (ln == 0) s_obits[w0] = (uint32_t)bal;
+        if (ln == 32) s_obits[w0 + 1] = (uint32_t)(bal >> 32);
+      }
+      __syncthreads();
+    }
+    // bitmap words past the last stage: nothing open
+    for (int w = ((npairs + kStage - 1) / kStage) * (kStage / 32) + tid; w < kLzThreads; w += kLzThreads) s_obits[w] = 0u;
+    return any;
+  };
+#endif
   int jump_rounds = 0;
   if (cls) {
     // carry scan over my 64 positions [tid * 64, tid * 64 + 64). A terminal travels as key
@@ -919,7 +978,11 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
   } else {
     jump_rounds = 1;
+#if DG_LZ_STAGED
+    const bool open1 = __syncthreads_or(staged());
+#else
     const bool open1 = __syncthreads_or(sweep(true));
+#endif
     LZ_STAMP(12);
     LZ_STAMP(13);
     if (open1) {
@@ -1068,7 +1131,8 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       }
       act &= ~res;
     }
-  } else {
+  }
+  if (!(has_tail && wv == kLzWaves - 1)) {
     // ---- 4. output: every entry is a literal code or one hop from one; 16 bytes per 16-byte store ----
     const int nthr = has_tail ? kLzThreads - 64 : kLzThreads;
     for (int c = tid; c < nbody; c += nthr) out_chunk(c);

@@ -141,7 +141,8 @@ int log2i(int32_t v) {
 // LZ4_decompress_safe: lengths inside the input, match distance inside the output produced so far,
 // output within one 64 KiB Druid block, CompressedPools.java:39). Records the token offset of every
 // kLzSeqPerCp-th sequence; a block with more than kLzMaxCps such checkpoints keeps every other one
-// (intervals of 2 * kLzSeqPerCp sequences), and one that still has more is rejected.
+// (intervals of 2 * kLzSeqPerCp sequences), and one that still has more is rejected. A general
+// (not light) block with fewer sequences gets intervals of ceil(sequences / kLzMaxCps) instead.
 // Longest copy chain of a validated block: a literal byte has depth 0, a match byte one more than the
 // byte it copies (overlapping matches copy from the match's first period). Stops above `cap`.
 static int lz4_max_depth(const uint8_t* in, int n, int cap) {
@@ -226,6 +227,24 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
     }
   };
   *wide = 0;
+  // checkpoints every g sequences from the block's start (appended after cps[first + ...])
+  auto push_every = [&](int64_t g) {
+    int p = 0, m = 0;
+    for (int64_t k = 0; k < seq; ++k) {
+      if (k % g == 0) {
+        cps->push_back((uint32_t)p);
+        ++m;
+      }
+      const int tok = in[p++];
+      int L = tok >> 4;
+      if (L == 15) for (int b = 255; b == 255;) L += (b = in[p++]);
+      p += L;
+      if (p >= n) break;
+      p += 2;
+      if ((tok & 15) == 15) for (int b = 255; b == 255;) b = in[p++];
+    }
+    return m;
+  };
   auto finish = [&](int dec) {
     size_t m = cps->size() - first;
     if (m > (size_t)kLzMaxCps) {
@@ -239,23 +258,19 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
       // light checkpoints: every g sequences, the fewest that fit one per light-decoder thread
       const int g = (int)std::max<int64_t>(1, (seq + kLtThreads - 1) / kLtThreads);
       if (nfine && g <= kLzSeqPerCp) {
-        int p = 0;
-        for (int64_t k = 0; k < seq; ++k) {
-          if (k % g == 0) {
-            cps->push_back((uint32_t)p);
-            ++*nfine;
-          }
-          const int tok = in[p++];
-          int L = tok >> 4;
-          if (L == 15) for (int b = 255; b == 255;) L += (b = in[p++]);
-          p += L;
-          if (p >= n) break;
-          p += 2;
-          if ((tok & 15) == 15) for (int b = 255; b == 255;) b = in[p++];
-        }
+        *nfine = push_every(g);
         *light = g;
       } else if (!nfine) {
         *light = 1;
+      }
+    }
+    if (!*wide && !(light && *light)) {
+      // a general block of fewer than kLzMaxCps * kLzSeqPerCp sequences: intervals of the fewest
+      // sequences that still give one per decoder thread, so every wave parses and fills
+      const int64_t g = std::max<int64_t>(1, (seq + kLzMaxCps - 1) / kLzMaxCps);
+      if (g < kLzSeqPerCp) {
+        cps->resize(first);
+        push_every(g);
       }
     }
     return dec;
