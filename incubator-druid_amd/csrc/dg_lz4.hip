@@ -66,6 +66,9 @@ static_assert(kShortLit <= 4, "Tok::lv holds four literal bytes");
 constexpr int kLongFill = 48;                  // matches above this are filled cooperatively
 constexpr int kMaxJobs = 2048;
 constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
+#ifndef DG_LZ_STAGE_K
+#define DG_LZ_STAGE_K 2  // pairs per thread in a resolution stage
+#endif
 #ifndef DG_LZ_STAGED
 #define DG_LZ_STAGED 1  // non-class resolution in position-ordered stages (0: sweep + rounds, A/B)
 #endif
@@ -806,24 +809,25 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   // jumps (no barrier: entries only ever get closer to their code, so any value read is valid); pairs
   // still open are set in the open-pair bitmap for the rounds below. One barrier per stage.
   auto staged = [&]() -> bool {
-    constexpr int kStage = 2 * kLzThreads;  // pairs per stage
+    constexpr int kSK = DG_LZ_STAGE_K;  // pairs per thread per stage
+    constexpr int kStage = kSK * kLzThreads;  // pairs per stage
     constexpr int kStageSteps = 6;
     const int npairs = (lim + 1) >> 1;
     bool any = false;
 #pragma unroll 1
     for (int p0 = 0; p0 < npairs; p0 += kStage) {
-      uint32_t v[2], nv[2];
+      uint32_t v[kSK], nv[kSK];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
+      for (int k = 0; k < kSK; ++k) {
         const int x = 2 * (p0 + k * kLzThreads + tid);
         v[k] = x < kTail ? s_e32[eph(x) >> 1] : 0xFF00FF00u;
         nv[k] = v[k];
       }
 #pragma unroll 1
       for (int it = 0; it <= kStageSteps; ++it) {
-        uint32_t ta[2], tb[2];
+        uint32_t ta[kSK], tb[kSK];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kSK; ++k) {
           const int x = 2 * (p0 + k * kLzThreads + tid);
           const uint32_t d0 = nv[k] & 0xFFFF, d1 = nv[k] >> 16;
           ta[k] = d0 < (uint32_t)kTail ? s_e[eph(x - (int)d0)] : 0xFF00u;
@@ -831,14 +835,14 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         }
         bool open = false;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kSK; ++k) {
           nv[k] = jstep(nv[k] & 0xFFFF, ta[k]) | (jstep(nv[k] >> 16, tb[k]) << 16);
           open |= is_open(nv[k]);
         }
         if (!__ballot(open)) break;
       }
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
+      for (int k = 0; k < kSK; ++k) {
         const int x = 2 * (p0 + k * kLzThreads + tid);
         if (nv[k] != v[k]) s_e32[eph(x) >> 1] = nv[k];  // (x < kTail whenever an entry changes)
         const bool op = is_open(nv[k]);
