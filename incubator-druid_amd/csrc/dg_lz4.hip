@@ -67,7 +67,10 @@ constexpr int kLongFill = 48;                  // matches above this are filled 
 constexpr int kMaxJobs = 2048;
 constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1024 = 65536 positions
 #ifndef DG_LZ_STAGE_K
-#define DG_LZ_STAGE_K 2  // pairs per thread in a resolution stage
+#define DG_LZ_STAGE_K 1  // pairs per thread in a resolution stage (1 measured faster than 2 and 4)
+#endif
+#ifndef DG_LZ_STAGE_STEPS
+#define DG_LZ_STAGE_STEPS 24  // extra jumps inside a stage before an entry is left to the rounds (3 / 6 / 12 / 24: 24 fastest)
 #endif
 #ifndef DG_LZ_STAGED
 #define DG_LZ_STAGED 1  // non-class resolution in position-ordered stages (0: sweep + rounds, A/B)
@@ -803,7 +806,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     return any;
   };
 #if DG_LZ_STAGED
-  // Staged resolution in position order: stage s takes the 2 * kLzThreads pairs after stage s - 1, all
+  // Staged resolution in position order: stage s takes the kLzThreads pairs after stage s - 1, all
   // of whose entries are literal codes by then, so a target before the stage is one read from its
   // code. A target inside the stage (distance < the stage) is followed for up to kStageSteps more
   // jumps (no barrier: entries only ever get closer to their code, so any value read is valid); pairs
@@ -811,7 +814,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   auto staged = [&]() -> bool {
     constexpr int kSK = DG_LZ_STAGE_K;  // pairs per thread per stage
     constexpr int kStage = kSK * kLzThreads;  // pairs per stage
-    constexpr int kStageSteps = 6;
+    constexpr int kStageSteps = DG_LZ_STAGE_STEPS;
     const int npairs = (lim + 1) >> 1;
     bool any = false;
 #pragma unroll 1
