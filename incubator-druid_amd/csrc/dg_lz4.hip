@@ -9,19 +9,20 @@
 // to ~300 deep), so neither a lane walking the token stream nor match-by-match copying is fast. The
 // block is decoded in four data-parallel phases, all in LDS:
 //   1. parse: the attach-time checkpoint index (lz4_index_block: the token offset of every 8th
-//      sequence, every 16th in blocks of more than 8192) gives every thread its own interval; it
-//      parses those sequences from the staged input into registers (literal start or bytes,
-//      literal length, distance, match length);
+//      sequence, every 16th in blocks of more than 8192, every ceil(n / 1024)th in blocks of n <
+//      8192) gives every thread its own interval; it parses those sequences from the staged input
+//      into registers (literal start or bytes, literal length, distance, match length);
 //   2. a block scan of the threads' output lengths places every sequence; each output byte x gets a
 //      16-bit entry E[x] in LDS: a literal is 0xFF00 | byte, a match byte the distance to the byte
 //      it copies (LZ4 overlap semantics: src = start - dist + (k mod dist));
-//   3. pointer jumping: E[x] += E[x - E[x]] until x - E[x] is a literal (log2(chain depth) rounds;
-//      updates are asynchronous, any value read is a valid ancestor distance);
+//   3. resolution: E[x] += E[x - E[x]] until x - E[x] is a literal (updates are asynchronous, any
+//      value read is a valid ancestor distance) — a carry scan over residue classes for blocks of
+//      distance-8 chains, position-ordered stages (then pointer-jumping rounds) otherwise;
 //   4. out[x] = low byte of the literal at x - E[x], written as 16-byte stores.
 // The staged input and E share one 128 KiB LDS array (the parse finishes before E is written;
 // literals are re-read from the compressed block in HBM/L2). Entries >= 0xFF00 are literals, so a
 // distance must stay below 0xFF00: the last 256 output positions, whose distances can exceed it,
-// keep absolute source positions in a small tail table and are resolved by a short chase.
+// are moved into a small tail table of absolute sources and resolved by a short chase.
 #include <hip/hip_runtime.h>
 
 
