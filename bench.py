@@ -18,6 +18,9 @@ The other configs (--config) are secondary lines / parity shapes: topn (configs[
 (configs[0]), filtered (configs[3], one GPU's share), ts_hourly / groupby_hourly (configs[4]).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config groupby|topn|...]
+
+--gpus N > 1 starts N ranks itself (launch_ranks) unless a launcher already did (WORLD_SIZE set,
+which must equal N); LOCAL_RANK picks the GPU (DG_BENCH_DEVICE overrides it for a one-GPU rehearsal).
 """
 import argparse
 import ctypes
@@ -540,6 +543,58 @@ def pmc_traffic(args, kname):
             "traffic_source": os.path.join("bench_pmc", os.path.basename(f)) + f" ({pm.get('label', '')})"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, script=None) -> int:
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N child processes of this
+    script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), the way
+    ChainedExecutionQueryRunner.java:89-180 fans segment runners out over the processing pool. The
+    parent never touches the GPU and never execs: it waits for the ranks, rank 0 prints the JSON line
+    (stdout is inherited), and the first failing rank stops the others and sets the exit code."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.2)
+    return rc
+
+
+def rank_env(args):
+    """(world, rank, local_rank) of this process. Under a launcher (WORLD_SIZE set, e.g.
+    torch.distributed.run) the world must be --gpus; without one, --gpus 1 is the single process."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus != 1:
+            raise SystemExit("rank_env: --gpus > 1 needs the ranks started by launch_ranks")
+        return 1, 0, 0
+    if int(world) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    return int(world), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -558,14 +613,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--write-workers", type=int, default=8, help="processes writing the synthetic segments")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))  # before torch or the engine is imported
+    world, rank, local_rank = rank_env(args)
 
     Q = importlib.import_module("incubator-druid_amd.query")
     R = importlib.import_module("incubator-druid_amd.runners")
     S = importlib.import_module("incubator-druid_amd.segment")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         D = importlib.import_module("incubator-druid_amd.distributed")

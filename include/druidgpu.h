@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 13
+#define DG_ABI_VERSION 14
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -66,6 +66,8 @@ extern "C" {
 #define DG_ERR_ARG 6         /* IllegalArgumentException */
 #define DG_ERR_DEVICE 7      /* HIP runtime failure */
 #define DG_ERR_NOT_FOUND 8   /* SegmentMissingException (TimeseriesQueryEngine.java:42-46) */
+#define DG_ERR_TIMEOUT 9     /* QueryInterruptedException(TimeoutException): "Query timeout" (ChainedExecutionQueryRunner.java:164-167,
+                                QueryInterruptedException.java:46) */
 
 /* column types (ValueType, processing/.../segment/column/ValueType.java) */
 #define DG_COL_MISSING 0
@@ -177,11 +179,19 @@ typedef struct {
   int32_t n_filter;
   const dg_agg* aggs;
   int32_t n_aggs;
-  const volatile int32_t* cancel; /* optional; non-zero => DG_ERR_INTERRUPTED between kernels */
+  /* optional cancellation flag (Thread.interrupt / QueryWatcher cancel, BaseQuery.checkInterrupted,
+     BaseQuery.java:46-51): polled between every launch group and while the call waits for the device;
+     non-zero => DG_ERR_INTERRUPTED. Work already queued on the device finishes before the call
+     returns, so the context is ready for its next call. */
+  const volatile int32_t* cancel;
   const int64_t* bucket_starts;   /* calendar granularity (see above); NULL = period_ms grid */
   int32_t n_bucket_starts;
   int32_t descending;
   const int64_t* seg_bounds;      /* calendar granularity: 2 per segment (see above), or NULL */
+  /* since ABI 14: the query context's "timeout" in ms (QueryContexts.getTimeout, ChainedExecutionQueryRunner
+     futures.get(timeout), ChainedExecutionQueryRunner.java:150-167), measured from the call's start and
+     checked where `cancel` is; <= 0: none. Past it => DG_ERR_TIMEOUT. */
+  int64_t timeout_ms;
 } dg_scan;
 
 /* QueryMetrics counters (query/QueryMetrics.java:295-306) + device timings */

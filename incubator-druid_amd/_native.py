@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("DRUID_AMD_LIB") or os.path.join(_HERE, "lib", "libdru
 
 DG_OK = 0
 ERRORS = {1: "DG_ERR_FORMAT", 2: "DG_ERR_UNSUPPORTED", 3: "DG_ERR_OOM", 4: "DG_ERR_INTERRUPTED",
-          5: "DG_ERR_TABLE_FULL", 6: "DG_ERR_ARG", 7: "DG_ERR_DEVICE", 8: "DG_ERR_NOT_FOUND"}
+          5: "DG_ERR_TABLE_FULL", 6: "DG_ERR_ARG", 7: "DG_ERR_DEVICE", 8: "DG_ERR_NOT_FOUND", 9: "DG_ERR_TIMEOUT"}
+ERR_INTERRUPTED, ERR_TIMEOUT = 4, 9
 COL_MISSING, COL_LONG, COL_FLOAT, COL_DOUBLE, COL_STRING, COL_UNSUPPORTED = range(6)
 F_AND, F_OR, F_NOT, F_SELECTOR, F_IN, F_BOUND = 1, 2, 3, 4, 5, 6
 ORDER = {"lexicographic": 0, "numeric": 1}
@@ -62,7 +63,7 @@ class dg_scan(ctypes.Structure):
                 ("aggs", ctypes.POINTER(dg_agg)), ("n_aggs", ctypes.c_int32),
                 ("cancel", ctypes.POINTER(ctypes.c_int32)), ("bucket_starts", ctypes.c_void_p),
                 ("n_bucket_starts", ctypes.c_int32), ("descending", ctypes.c_int32),
-                ("seg_bounds", ctypes.c_void_p)]
+                ("seg_bounds", ctypes.c_void_p), ("timeout_ms", ctypes.c_int64)]
 
 
 class dg_metrics(ctypes.Structure):
@@ -382,4 +383,6 @@ def make_scan(query, query_module, cancel: Optional[ctypes.c_int32] = None, segm
     if cancel is not None:
         s.cancel = ctypes.pointer(cancel)
         keep.append(cancel)
+    # QueryContexts.getTimeout: the context's "timeout" (ms; 0 = none)
+    s.timeout_ms = int((getattr(query, "context", None) or {}).get("timeout", 0) or 0)
     return s, keep

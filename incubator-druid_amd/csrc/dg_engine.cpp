@@ -31,8 +31,10 @@ namespace dg {
 // errors
 // ------------------------------------------------------------------------------------------------
 static thread_local char g_err[1024] = "";
+static thread_local uint64_t g_err_count = 0;  // set_error calls on this thread (CallGuard: did the call fail?)
 
 int set_error(int code, const char* fmt, ...) {
+  ++g_err_count;
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof g_err, fmt, ap);
@@ -158,7 +160,40 @@ struct UpPool {
   }
 };
 
+// Interruption of a query call: the scan's cancel flag (Thread.interrupt / QueryWatcher.cancel,
+// BaseQuery.checkInterrupted, BaseQuery.java:46-51) and the context's timeout measured from the call's
+// start (ChainedExecutionQueryRunner.java:150-167: futures.get(timeout) -> QueryInterruptedException(
+// TimeoutException)). Checked between launch groups and while finish_call waits for the device.
+struct Interrupt {
+  const volatile int32_t* cancel = nullptr;
+  bool timed = false;
+  int64_t timeout_ms = 0;
+  std::chrono::steady_clock::time_point deadline;
+  Interrupt(const dg_scan* q, std::chrono::steady_clock::time_point t0) {
+    if (!q) return;
+    cancel = q->cancel;
+    if (q->timeout_ms > 0) {
+      timed = true;
+      timeout_ms = q->timeout_ms;
+      deadline = t0 + std::chrono::milliseconds(q->timeout_ms);
+    }
+  }
+  bool active() const { return cancel || timed; }
+  int check() const {
+    if (cancel && *cancel) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+    if (timed && std::chrono::steady_clock::now() >= deadline)
+      return set_error(DG_ERR_TIMEOUT, "query timeout (%lld ms)", (long long)timeout_ms);
+    return DG_OK;
+  }
+};
+#define DG_CHECK_INTERRUPT(intr)       \
+  do {                                 \
+    const int _irc = (intr).check();   \
+    if (_irc) return _irc;             \
+  } while (0)
+
 struct CallScratch {
+  const Interrupt* intr = nullptr;  // the running query call's (null outside query calls)
   Pool dev;
   Pool host;
   UpPool up;
@@ -179,6 +214,7 @@ struct CallScratch {
     d_err = nullptr;
     h_err = nullptr;
     bitmap_bytes = 0;
+    intr = nullptr;
   }
 };
 
@@ -227,11 +263,26 @@ static int32_t* call_err(CallScratch* cs, hipStream_t st) {
   return cs->d_err;
 }
 
-// Enqueue the error-word read-back, wait for the stream, and turn device-side errors into codes.
+// Enqueue the error-word read-back, wait for the stream, and turn device-side errors into codes. In a
+// query call with a cancel flag or a timeout the wait polls them: once one fires, the queued work still
+// drains (it owns the context's scratch) and the call then returns the interruption.
 static int finish_call(CallScratch* cs, hipStream_t st) {
   DG_FLUSH(cs, st);
   if (cs->d_err) DG_HIP(hipMemcpyAsync(cs->h_err, cs->d_err, 4, hipMemcpyDeviceToHost, st));
-  DG_HIP(hipStreamSynchronize(st));
+  if (cs->intr && cs->intr->active()) {
+    int irc = DG_OK;
+    for (int spin = 0;; ++spin) {
+      const hipError_t e = hipStreamQuery(st);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) return set_error(DG_ERR_DEVICE, "hipStreamQuery: %s", hipGetErrorString(e));
+      if (!irc) irc = cs->intr->check();
+      if (spin < 256) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    if (irc) return irc;
+  } else {
+    DG_HIP(hipStreamSynchronize(st));
+  }
   DG_HIP(hipGetLastError());
   if (cs->d_err && *cs->h_err)
     return set_error(DG_ERR_FORMAT, (*cs->h_err & 1)   ? "corrupt LZ4 block"
@@ -1038,7 +1089,8 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
 // column decode: returns a ColView, scheduling LZ4 block decodes into scratch when needed
 // ------------------------------------------------------------------------------------------------
 
-static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect) {
+// run_ok: run blocks go to k_lz4_run (run_decode_enabled(), read once per column by the caller)
+static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, bool run_ok) {
   Lz4Job j;
   j.src = b.comp.as<uint8_t>() + b.comp_off[k];
   j.dst = dst;
@@ -1051,7 +1103,10 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
   j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
   j.vstride = 0;
-  j.pad_ = 0;
+  const bool run = run_ok && !b.run_off.empty() && b.run_off[k] >= 0;
+  j.rx = run ? b.runx.as<uint8_t>() + b.run_off[k] : nullptr;
+  j.run_n = run ? b.run_n[k] : 0;
+  j.run_far = run ? b.run_far[k] : 0;
   j.red_dst = nullptr;
   j.red_op = j.red_kind = j.red_vkind = j.red_code = 0;
   return j;
@@ -1094,6 +1149,7 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
   if (b.codec != CODEC_LZ4 && b.codec != CODEC_LZF && b.codec != CODEC_UNCOMPRESSED && b.codec != CODEC_NONE)
     return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, name);
   uint8_t* slots = nullptr;
+  const bool run_ok = b.codec == CODEC_LZ4 && run_decode_enabled();
   if (b.codec == CODEC_LZ4 || b.codec == CODEC_LZF) {
     slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
     if (!slots) return set_error(DG_ERR_OOM, "decode scratch");
@@ -1124,7 +1180,7 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
     if (slots) {
       const int64_t expect = b.vbits ? (b.vbits * rows + 7) / 8 : rows * b.width;
       if (b.codec == CODEC_LZ4) {
-        db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect));
+        db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect, run_ok));
       } else {
         LzfJob lj;
         lj.src = b.comp.as<uint8_t>() + b.comp_off[k];
@@ -1164,11 +1220,12 @@ static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int p
                      (agg_kind == DG_AGG_DOUBLE_SUM && c->type == DG_COL_DOUBLE);
   if (!ident || c->multi_value || b.codec != CODEC_LZ4 || b.vbits || b.width != 8 || !payload) return false;
   db->bytes += b.stored_bytes + b.index_bytes;
+  const bool run_ok = run_decode_enabled();
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (rows <= 0) continue;
     const int64_t r0 = (int64_t)row_base + (int64_t)k * b.size_per;
-    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(payload + (size_t)r0 * pw + a), (int32_t)(rows * 8));
+    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(payload + (size_t)r0 * pw + a), (int32_t)(rows * 8), run_ok);
     j.vstride = pw * 8;
     db->jobs.push_back(j);
   }
@@ -1235,27 +1292,33 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   // per-thread sequence registers)
   // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
   // blocks per CU)
-  const int nh = (int)(std::stable_partition(db->jobs.begin(), db->jobs.end(), [](const Lz4Job& j) { return !j.light; }) -
-                       db->jobs.begin());
-  const int nn = (int)(std::stable_partition(db->jobs.begin(), db->jobs.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
-                       db->jobs.begin());
+  // run blocks (value runs with a run index) first, to k_lz4_run
+  auto& J = db->jobs;
+  const int nr = (int)(std::stable_partition(J.begin(), J.end(), [](const Lz4Job& j) { return j.rx != nullptr; }) - J.begin());
+  const int nh = (int)(std::stable_partition(J.begin() + nr, J.end(), [](const Lz4Job& j) { return !j.light; }) - J.begin());
+  const int nn = (int)(std::stable_partition(J.begin() + nr, J.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
+                       J.begin());
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
-  if (nn <= 16 * 256) std::stable_sort(db->jobs.begin(), db->jobs.begin() + nn, by_ncp);
-  if (nh - nn <= 16 * 256) std::stable_sort(db->jobs.begin() + nn, db->jobs.begin() + nh, by_ncp);
+  if (nn - nr <= 16 * 256) std::stable_sort(J.begin() + nr, J.begin() + nn, by_ncp);
+  if (nh - nn <= 16 * 256) std::stable_sort(J.begin() + nn, J.begin() + nh, by_ncp);
+  int run_lds = 0;
+  for (int i = 0; i < nr; ++i) run_lds = std::max(run_lds, run_lds_bytes(J[i].src_len, J[i].run_far));
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
   int32_t* d_err = call_err(cs, st);
   if (!h || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
-  memcpy(h, db->jobs.data(), sizeof(Lz4Job) * n);
+  memcpy(h, J.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
+  launch_lz4_run(d, nr, run_lds, d_err, st);
   launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
-  for (int i = 0; i < nh; ++i) db->gen_bytes += db->jobs[i].src_len;
-  db->gen_blocks += nh;
-  db->gen_launches += (nn > 0) + (nh - nn > 0);
-  if (db->gen_a && nh) hipEventRecord(db->gen_a, st);
-  launch_lz4_decode(d, nn, 0, d_err, st, d_prof);
+  const int ng = nh - nr;  // general-decoder blocks
+  for (int i = nr; i < nh; ++i) db->gen_bytes += J[i].src_len;
+  db->gen_blocks += ng;
+  db->gen_launches += (nn > nr) + (nh - nn > 0);
+  if (db->gen_a && ng) hipEventRecord(db->gen_a, st);
+  launch_lz4_decode(d + nr, nn - nr, 0, d_err, st, d_prof ? d_prof + (size_t)nr * kLz4ProfWords : nullptr);
   launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
-  if (db->gen_a && nh) hipEventRecord(db->gen_b, st);
+  if (db->gen_a && ng) hipEventRecord(db->gen_b, st);
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
 
@@ -1508,6 +1571,7 @@ static int time_view(const Column* c, const std::vector<int64_t>& tb, CallScratc
   if ((ndec && !slots) || !h_const || !h_ptrs) return set_error(DG_ERR_OOM, "time view");
   if (ndec) db->last_slots = slots;
   int32_t at = 0;
+  const bool run_ok = run_decode_enabled();
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (uni[k]) {
@@ -1518,8 +1582,9 @@ static int time_view(const Column* c, const std::vector<int64_t>& tb, CallScratc
     uint8_t* slot = slots + (size_t)at++ * kBlockBytes;
     h_ptrs[k] = slot;
     if (rows > 0) {
-      db->jobs.push_back(lz4_job(b, k, slot, (int32_t)(rows * 8)));
-      db->bytes += b.comp_len[k];
+      db->jobs.push_back(lz4_job(b, k, slot, (int32_t)(rows * 8), run_ok));
+      const Lz4Job& j = db->jobs.back();
+      db->bytes += b.comp_len[k] + (j.rx ? run_index_bytes(j.run_n, j.run_far) : 4 * (int64_t)(j.ncp + j.nfine));
     }
   }
   v->blocks = d_ptrs;
@@ -1641,7 +1706,7 @@ int read_time_bounds(Segment* seg) {
     for (int k = 0; k < 2; ++k) {
       int32_t blk = k == 0 ? 0 : last;
       int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)blk * b.size_per);
-      db.jobs.push_back(lz4_job(b, blk, slots + (size_t)k * kBlockBytes, (int32_t)(rows * 8)));
+      db.jobs.push_back(lz4_job(b, blk, slots + (size_t)k * kBlockBytes, (int32_t)(rows * 8), run_decode_enabled()));
     }
     int rc0 = run_decodes(cs, &db, st);
     if (rc0) return rc0;
@@ -1702,9 +1767,20 @@ struct CallGuard {
   Context* ctx;
   std::unique_lock<std::mutex> lock;
   CallScratch* cs;
-  explicit CallGuard(Context* c) : ctx(c), lock(c->mu), cs(scratch_of(c)) {
+  uint64_t errs0;
+  explicit CallGuard(Context* c) : ctx(c), lock(c->mu), cs(scratch_of(c)), errs0(g_err_count) {
     hipSetDevice(c->device);
     cs->reset();
+  }
+  // a call that fails (interrupted, timed out, or any error after launches) drains both streams before
+  // it returns: queued kernels and copies still use the call's scratch and staging, which the next call
+  // of the context reuses
+  ~CallGuard() {
+    if (g_err_count != errs0) {
+      hipStreamSynchronize(ctx->stream);
+      if (ctx->side) hipStreamSynchronize(ctx->side);
+    }
+    cs->intr = nullptr;
   }
 };
 
@@ -1743,7 +1819,6 @@ static int check_segments(dg_segment* const* segs, int32_t n, Context** ctx) {
   return DG_OK;
 }
 
-static bool cancelled(const dg_scan* q) { return q->cancel && *q->cancel; }
 
 // resolve an aggregator's input column into a view (absent column reads 0) and, for a
 // FilteredAggregatorFactory, its filter into a row bitset (the ValueMatcher of
@@ -1793,9 +1868,12 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
   const int64_t ts = one_bucket ? 1 : tc->data.size_per;
   std::vector<int64_t> bk(b.nblocks, -1);
   int32_t nfused = 0;
+  const bool run_ok = run_decode_enabled();
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t r0 = (int64_t)k * b.size_per, r1 = std::min<int64_t>((int64_t)b.total, r0 + b.size_per);
-    if (r1 <= r0 || (!b.cp_light.empty() && b.cp_light[k])) continue;
+    // (light blocks are decoded by k_lz4_light, which does not fold; a run block folds in k_lz4_run)
+    const bool run = run_ok && !b.run_off.empty() && b.run_off[k] >= 0;
+    if (r1 <= r0 || (!run && !b.cp_light.empty() && b.cp_light[k])) continue;
     if (one_bucket) {
       bk[k] = 0;
     } else {
@@ -1825,7 +1903,7 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (bk[k] >= 0) {
       h_ptrs[k] = reinterpret_cast<const uint8_t*>((uintptr_t)1);  // tagged: never dereferenced
-      Lz4Job j = lz4_job(b, k, nullptr, (int32_t)(rows * 8));
+      Lz4Job j = lz4_job(b, k, nullptr, (int32_t)(rows * 8), run_ok);
       j.red_dst = out + (size_t)bk[k] * rec + 1 + slot;
       j.red_op = slot_op(a.kind);
       j.red_kind = a.kind;
@@ -1839,7 +1917,7 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
     }
     uint8_t* dst = slots + (size_t)at++ * kBlockBytes;
     h_ptrs[k] = dst;
-    if (rows > 0) db->jobs.push_back(lz4_job(b, k, dst, (int32_t)(rows * 8)));
+    if (rows > 0) db->jobs.push_back(lz4_job(b, k, dst, (int32_t)(rows * 8), run_ok));
   }
   v->blocks = d_ptrs;
   return DG_OK;
@@ -2158,6 +2236,8 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   if (rc) return rc;
   CallGuard g(ctx);
   CallScratch* cs = g.cs;
+  Interrupt intr(q, t0);
+  cs->intr = &intr;
   hipStream_t st = ctx->stream;
   rc = upload_grain(cs, &gr, st);
   if (rc) return rc;
@@ -2212,7 +2292,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     }
     tiles_rows[i] = seg->nrows;
   }
-  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  DG_CHECK_INTERRUPT(intr);
   // init accumulators (before the decoders: fused blocks combine into them)
   SlotInit init{};
   for (int a = 0; a < na; ++a) init.v[1 + a] = identity_host(plan.kind[a]);
@@ -2223,7 +2303,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
   m.bytes_read = db.bytes;
-  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  DG_CHECK_INTERRUPT(intr);
   std::vector<int32_t> begin;
   int ntiles = 0;
   for (int i = 0; i < n; ++i)
@@ -2238,6 +2318,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   DG_FLUSH(cs, st);
   hipEventRecord(ctx->ev[3], st);
   launch_scan_agg(d_jobs, d_tile, ntiles, plan, 0, st);
+  DG_CHECK_INTERRUPT(intr);
   if (fsum) {
     // floatSum as the reference adds it: float32, one row at a time per cursor (bucket)
     std::vector<GbJob> gj(n);
@@ -2363,6 +2444,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   if (rc) return rc;
   CallGuard g(ctx);
   CallScratch* cs = g.cs;
+  Interrupt intr(q, t0);
+  cs->intr = &intr;
   hipStream_t st = ctx->stream;
   rc = upload_grain(cs, &gr, st);
   if (rc) return rc;
@@ -2426,7 +2509,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     j.out = nullptr;  // allocated below with the bins
     tiles_rows[i] = seg->nrows;
   }
-  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  DG_CHECK_INTERRUPT(intr);
   hipEventRecord(ctx->ev[1], st);
   ht.mark("planned");
   rc = run_decodes(cs, &db, st);
@@ -3286,6 +3369,21 @@ struct dg_result {
   }
 };
 
+// A result under construction inside a call, whose CallGuard holds the context's lock: on an error
+// return its blocks go back to the cache here (~dg_result would take the lock again).
+struct ResultDrop {
+  void operator()(dg_result* r) const {
+    if (!r) return;
+    if (r->ctx) {
+      dg::result_free(r->ctx, r->keys);
+      dg::result_free(r->ctx, r->slots);
+    }
+    r->ctx = nullptr;
+    delete r;
+  }
+};
+using PendingResult = std::unique_ptr<dg_result, ResultDrop>;
+
 extern "C" {
 
 int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_groupby* gb, dg_result** out,
@@ -3308,6 +3406,8 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   if (rc) return rc;
   CallGuard g(ctx);
   CallScratch* cs = g.cs;
+  Interrupt intr(q, t0);
+  cs->intr = &intr;
   hipStream_t st = ctx->stream;
   rc = upload_grain(cs, &gr, st);
   if (rc) return rc;
@@ -3436,7 +3536,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     }
     rows[i] = seg->nrows;
   }
-  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
+  DG_CHECK_INTERRUPT(intr);
   // The payload columns only meet the keys at the reduce: they decode on the side stream while the
   // main stream decodes the key columns, builds the keys and sorts them (the general LZ4 decoder is
   // LDS / latency bound, the sort HBM bound, so the two overlap on the CUs).
@@ -3461,6 +3561,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   rc = run_decodes(cs, &db, st);
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
+  DG_CHECK_INTERRUPT(intr);
   m.bytes_read = db.bytes + db_side.bytes;
   m.bytes_side = db_side.bytes;
   GbJob* d_jobs;
@@ -3483,10 +3584,11 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   hipEventRecord(ctx->ev[5], st);
   launch_radix_sort(&sb, key_bits, st);
   hipEventRecord(ctx->ev[6], st);
+  DG_CHECK_INTERRUPT(intr);
   // the result is laid out for the sort's capacity (>= the groups): the reduce counts the groups itself
   // (look-back over tiles), so there is no host read-back between the sort and the reduce
   const int64_t cap = std::max<int64_t>(sb.cap, 1);
-  std::unique_ptr<dg_result> res(new dg_result());
+  PendingResult res(new dg_result());
   res->ctx = ctx;
   res->ndims = nd;
   res->naggs = na;
@@ -3520,11 +3622,33 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   }
   hipEventRecord(ctx->ev[4], st);
   DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));  // selected rows, groups
-  rc = finish_call(cs, st);
+  rc = finish_call(cs, st);  // (polls the cancel flag / timeout while the device works)
   if (rc) return rc;
-  if (cancelled(q)) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
   const int64_t nsel = h_n[0], ng = h_n[1];
   res->ngroups = ng;
+  // The result was laid out for the call's rows; when the groups are far fewer (filtered or few-group
+  // queries) it is compacted to them and the row-sized blocks go back to the context's cache.
+  if (ng * 2 < cap && (size_t)cap * rec * 8 >= ((size_t)1 << 20)) {
+    const int64_t c2 = std::max<int64_t>(ng, 1);
+    uint64_t* k2 = static_cast<uint64_t*>(result_alloc(ctx, (size_t)c2 * 8));
+    uint64_t* s2 = static_cast<uint64_t*>(result_alloc(ctx, (size_t)c2 * rec * 8));
+    if (k2 && s2) {
+      if (ng > 0) {
+        DG_HIP(hipMemcpyAsync(k2, res->keys, (size_t)ng * 8, hipMemcpyDeviceToDevice, st));
+        DG_HIP(hipMemcpy2DAsync(s2, (size_t)c2 * 8, res->slots, (size_t)cap * 8, (size_t)ng * 8, (size_t)rec,
+                                hipMemcpyDeviceToDevice, st));
+        DG_HIP(hipStreamSynchronize(st));
+      }
+      result_free(ctx, res->keys);
+      result_free(ctx, res->slots);
+      res->keys = k2;
+      res->slots = s2;
+      res->cap = c2;
+    } else {  // no room for the compact copy: keep the row-sized result
+      result_free(ctx, k2);
+      result_free(ctx, s2);
+    }
+  }
   if (side) {
     float fs = 0;
     hipEventElapsedTime(&fs, ctx->side_ev[1], ctx->side_ev[2]);
@@ -3935,7 +4059,7 @@ int dg_merge(dg_context* c, const dg_keyspace* ks, const uint64_t* d_keys, const
   CallGuard g(ctx);
   CallScratch* cs = g.cs;
   hipStream_t st = ctx->stream;
-  std::unique_ptr<dg_result> res(new dg_result());
+  PendingResult res(new dg_result());
   res->ctx = ctx;
   res->ndims = ks->n_dims;
   res->naggs = plan.n;
@@ -4321,8 +4445,11 @@ extern "C" int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t*
   std::vector<uint32_t> one;
   int wide = 0, light = 0, nfine = 0;
   const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine);
-  // -1 malformed, 0 general, 1 general (wide), 2 light
-  *kind = d < 0 ? -1 : light ? 2 : wide ? 1 : 0;
+  std::vector<uint8_t> rx;
+  int nint = 0, nfar = 0;
+  const bool run = d > 0 && lz4_run_index(block, len, d, &rx, &nint, &nfar);
+  // -1 malformed, 0 general, 1 general (wide), 2 light, 3 run
+  *kind = d < 0 ? -1 : run ? 3 : light ? 2 : wide ? 1 : 0;
   return DG_OK;
 }
 
@@ -4341,6 +4468,10 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.cp_light.assign(n, 0);
   b.cp_fine.assign(n, 0);
   b.dec_len.resize(n);
+  b.run_off.assign(n, -1);
+  b.run_n.assign(n, 0);
+  b.run_far.assign(n, 0);
+  std::vector<uint8_t> rall;
   int64_t total = 0;
   for (int i = 0; i < n; ++i) {
     if (lens[i] <= 0 || lens[i] > kBlockBytes + 2048) return set_error(DG_ERR_ARG, "block %d length %d", i, lens[i]);
@@ -4363,18 +4494,23 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
     b.dec_len[i] = d < 0 ? 0 : d;
     out_lens[i] = d;
     if (d >= 0) cps.insert(cps.end(), one.begin(), one.end());
+    const size_t at = rall.size();
+    if (d > 0 && lz4_run_index(blocks[i], lens[i], d, &rall, &b.run_n[i], &b.run_far[i])) b.run_off[i] = (int64_t)at;
   }
   if (cps.empty()) cps.push_back(0);
   CallGuard g(ctx);
   hipStream_t st = ctx->stream;
   if (!b.comp.alloc(host.size()) || !b.cps.alloc(cps.size() * 4)) return set_error(DG_ERR_OOM, "debug decode");
+  if (!rall.empty() && !b.runx.alloc(rall.size())) return set_error(DG_ERR_OOM, "debug decode");
   DG_HIP(hipMemcpy(b.comp.p, host.data(), host.size(), hipMemcpyHostToDevice));
   DG_HIP(hipMemcpy(b.cps.p, cps.data(), cps.size() * 4, hipMemcpyHostToDevice));
+  if (!rall.empty()) DG_HIP(hipMemcpy(b.runx.p, rall.data(), rall.size(), hipMemcpyHostToDevice));
+  const bool run_ok = run_decode_enabled();
   DecodeBatch db;
   uint8_t* slots = dev_take<uint8_t>(g.cs, (size_t)n * kBlockBytes + 64);
   if (!slots) return set_error(DG_ERR_OOM, "debug decode slots");
   for (int i = 0; i < n; ++i)
-    if (out_lens[i] >= 0) db.jobs.push_back(lz4_job(b, i, slots + (size_t)i * kBlockBytes, out_lens[i]));
+    if (out_lens[i] >= 0) db.jobs.push_back(lz4_job(b, i, slots + (size_t)i * kBlockBytes, out_lens[i], run_ok));
   uint64_t* d_prof = nullptr;
   if (prof) {
     d_prof = dev_take<uint64_t>(g.cs, (size_t)n * kLz4ProfWords);

@@ -68,7 +68,10 @@ struct Lz4Job {
   // and value v goes to dst + v * vstride (a column of the groupBy payload records, written in place);
   // bytes past expect_len are then not written (they would land in the next segment's records)
   int32_t vstride;
-  int32_t pad_;
+  // run block (k_lz4_run): the block's run index (lz4_run_index) and its shape; null: another decoder
+  const uint8_t* rx;
+  int32_t run_n;    // intervals (one per k_lz4_run thread)
+  int32_t run_far;  // bytes of the far-copy table after the intervals
   // Decode fused with a timeseries aggregator (the block's rows share one bucket, no filter): instead
   // of writing its 8-byte values the decoder folds them with red_op (agg_input_raw(red_kind,
   // red_vkind, value)) and combines the block's result into the bucket's slot *red_dst atomically.
@@ -89,6 +92,28 @@ enum : int32_t { kRedGeneric = 0, kRedLongSum = 1, kRedDoubleSum = 2, kRedLongMa
 constexpr int kLtMaxCps = 256;
 constexpr int kLtThreads = 512;  // light-decoder threads (at most one light checkpoint interval each)
 constexpr int kLtMaxDepth = 16;
+
+// Run blocks: LZ4 blocks of 8-byte value runs (sequential longs, timestamps, constant columns) whose
+// matches copy from at most 8 bytes back, except a few far copies. The attach-time run index cuts the
+// block into intervals of >= kRunTarget output bytes at sequence boundaries and stores, per interval,
+// its token offset, its output start and the 8 output bytes before it (its window); every far copy's
+// bytes are listed once. k_lz4_run then decodes each interval independently in one thread: the last
+// 8 output bytes ride in a register, a near copy is a shift of it, and every aligned 8-byte value is
+// emitted as it completes. Index layout per block (16-byte aligned): u64 win[n], u32 tok[n] (token
+// offset | far-table offset << 17), u16 out[n], zero pad to 16, the far table, zero pad to 16.
+constexpr int kRunThreads = 256;   // one interval per thread (kBlockBytes / kRunTarget intervals at most)
+constexpr int kRunTarget = 256;    // output bytes per interval, at least (the last one excepted)
+constexpr int kRunFarMax = 4096;   // far-copy bytes a run block may list
+constexpr int kRunMaxRun = 1024;   // longest literal run / match of a run block (one thread's serial work)
+constexpr int kRunLdsMax = 40960;  // staged input + far table of one run block (four workgroups per CU)
+static_assert(kBlockBytes / kRunTarget <= kRunThreads, "one interval per k_lz4_run thread");
+inline int run_index_bytes(int nint, int nfar) { return ((14 * nint + 15) & ~15) + ((nfar + 15) & ~15); }
+inline int run_lds_bytes(int n, int nfar) { return ((n + 15) & ~15) + 16 + ((nfar + 15) & ~15) + 16; }
+// Run index of one validated LZ4 block decoding to dec_len bytes, appended to *idx (16-byte aligned);
+// returns false (nothing appended) when the block is not a run block.
+bool lz4_run_index(const uint8_t* in, int n, int dec_len, std::vector<uint8_t>* idx, int* nint, int* nfar);
+// the run decoder is on unless DG_NO_RUN_DECODE is set (same-box A/B, tests of the other decoders)
+bool run_decode_enabled();
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
 struct LzfJob {
@@ -250,7 +275,12 @@ struct BlockColumn {
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
   std::vector<int64_t> first8;         // LZ4: the first 8 decoded bytes of block b (int64 LE: its first
                                        // row's value in a LONGS column), from the attach-time parse
-  int64_t index_bytes = 0;             // LZ4: bytes of the checkpoint index (read per query)
+  int64_t index_bytes = 0;             // LZ4: bytes of the index a query reads (checkpoints; run index
+                                       // of run blocks instead)
+  std::vector<int64_t> run_off;        // LZ4: block b's run index inside runx (-1: not a run block)
+  std::vector<int32_t> run_n;          // LZ4: its intervals
+  std::vector<int32_t> run_far;        // LZ4: its far-copy bytes
+  DevBuf runx;                         // LZ4: run indexes of the run blocks
   DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)
   DevBuf cps;                          // LZ4: uint32 checkpoints of every block
   DevBuf raw;                          // UNCOMPRESSED: 64 KiB slot per block; NONE: flat values
@@ -383,6 +413,8 @@ constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (dia
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+// run blocks (rx set); lds = the largest run_lds_bytes of the launch's blocks
+void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int lds, int32_t* d_err, hipStream_t s);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // one multi-value dimension's decoded row lists, validated before use (bit 2 of the error word)

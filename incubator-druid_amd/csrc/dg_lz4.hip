@@ -1428,6 +1428,176 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Run decoder: blocks of 8-byte value runs with a run index (lz4_run_index, dg_internal.h). Columns of
+// sequential longs and timestamps are ~8 K sequences of [1-2 literal bytes, a 6-7-byte copy from 8
+// bytes back] whose copy chains run through the whole block: the general decoder resolves them with a
+// 128 KiB per-byte entry image, one block per CU. Here the attach-time index gives every interval of
+// >= kRunTarget output bytes the 8 bytes before it, so each thread decodes its interval alone: the
+// last 8 output bytes live in one 64-bit register (`win`, oldest byte lowest), a literal or far-copy
+// chunk is shifted in from LDS, a copy from d <= 8 bytes back is the window's last d bytes repeated,
+// and every 8-byte-aligned value is emitted as it completes (a slot store, a payload record, or the
+// fused aggregator's fold). Only the compressed block and the far table are staged in LDS (<= 40 KiB:
+// four workgroups per CU); no barrier after staging.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lds_rd8(const uint32_t* __restrict__ s32, int p) {
+  const int a = p >> 2, sh = (p & 3) << 3;
+  const uint64_t w01 = (uint64_t)s32[a] | ((uint64_t)s32[a + 1] << 32);
+  const uint32_t w2 = s32[a + 2];
+  return sh ? ((w01 >> sh) | ((uint64_t)w2 << (64 - sh))) : w01;
+}
+
+// one 8-byte value v of a run block: its fold (fused), payload record, or slot qword
+// (a slot takes every qword of the block; payload records and folds only the block's rows)
+__device__ __forceinline__ void run_emit(const Lz4Job& job, int v, uint64_t x, uint64_t& acc) {
+  if (!job.red_dst && !job.vstride) {
+    gst8(job.dst + (size_t)v * 8, (uint32_t)x, (uint32_t)(x >> 32));
+    return;
+  }
+  if ((v + 1) * 8 > job.expect_len) return;
+  if (job.red_dst) {
+    switch (job.red_code) {
+      case kRedLongSum: acc += x; break;
+      case kRedDoubleSum:
+        acc = (uint64_t)__double_as_longlong(__longlong_as_double((long long)acc) + __longlong_as_double((long long)x));
+        break;
+      case kRedLongMax: acc = (uint64_t)max((long long)acc, (long long)x); break;
+      case kRedLongMin: acc = (uint64_t)min((long long)acc, (long long)x); break;
+      default: acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, x));
+    }
+    return;
+  }
+  gst8(job.dst + (size_t)v * job.vstride, (uint32_t)x, (uint32_t)(x >> 32));
+}
+
+__global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint4 s_run[];
+  __shared__ uint64_t s_red[kRunThreads / 64];
+  const Lz4Job job = jobs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int n = job.src_len, ni = job.run_n, nfar = job.run_far;
+  if (n <= 0 || ni <= 0 || ni > kRunThreads || nfar < 0 || nfar > kRunFarMax ||
+      16 * (((n + 15) >> 4) + ((nfar + 15) >> 4) + 2) > kRunLdsMax ||
+      job.dec_len <= 0 || (job.dec_len & 7) || job.dec_len > kBlockBytes || job.dec_len < job.expect_len) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  // ---- stage the compressed block, then the far table (both 16-byte aligned and padded) ----
+  const int n16 = (n + 15) >> 4, f16 = (nfar + 15) >> 4;
+  const uint8_t* far_g = job.rx + ((14 * ni + 15) & ~15);
+  for (int i = tid; i < n16 + 1 + f16 + 1; i += kRunThreads) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (i < n16) v = gld16(job.src + 16 * (size_t)i);
+    else if (i > n16 && i <= n16 + f16) v = gld16(far_g + 16 * (size_t)(i - n16 - 1));
+    s_run[i] = v;
+  }
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_run);
+  const uint8_t* s8 = reinterpret_cast<const uint8_t*>(s_run);
+  const int far0 = 16 * (n16 + 1);
+  uint64_t acc = job.red_dst ? red_identity(job) : 0ull;
+  bool bad = false;
+  // my interval's index entry (read before the barrier)
+  uint64_t win = 0;
+  uint32_t tf = 0;
+  int o = 0, oend = 0;
+  if (tid < ni) {
+    win = (uint64_t)gld4(job.rx + 8 * (size_t)tid) | ((uint64_t)gld4(job.rx + 8 * (size_t)tid + 4) << 32);
+    tf = gld4(job.rx + 8 * (size_t)ni + 4 * (size_t)tid);
+    const uint16_t* ost = reinterpret_cast<const uint16_t*>(job.rx + 12 * (size_t)ni);
+    o = ost[tid];
+    oend = tid + 1 < ni ? (int)ost[tid + 1] : job.dec_len;
+  }
+  __syncthreads();
+  if (tid < ni) {
+    int p = (int)(tf & 0x1FFFFu), fp = far0 + (int)(tf >> 17);
+    // shift k (1..8) bytes, the low bytes of x, into the window; emit a completed aligned value
+    auto push = [&](uint64_t x, int k) {
+      win = k == 8 ? x : ((win >> (8 * k)) | (x << (64 - 8 * k)));
+      o += k;
+      if ((o & 7) == 0) run_emit(job, (o >> 3) - 1, win, acc);
+    };
+    auto ext = [&](int& q, int& len) {  // LZ4 extended length (bytes up to the first != 255)
+      for (int b = 255; b == 255;) {
+        if (q >= n) {
+          bad = true;
+          return;
+        }
+        b = s8[q++];
+        len += b;
+      }
+    };
+#pragma unroll 1
+    while (o < oend && !bad) {
+      const uint64_t w = lds_rd8(s32, p);
+      const int tk = (int)(w & 0xFF);
+      int L = tk >> 4, M = tk & 15, q = p + 1;
+      if (L == 15) ext(q, L);
+      if (L > oend - o) {
+        bad = true;
+        break;
+      }
+      // literals: from the token's window when they and the distance fit in it, else from LDS
+      if (L > 0) {
+        if (tk < 0x60) {  // L <= 5: the token window holds them
+          const uint64_t lv = w >> 8;
+          const int k1 = min(L, 8 - (o & 7));
+          push(lv, k1);
+          if (L > k1) push(lv >> (8 * k1), L - k1);
+        } else {
+          int lp = q, rem = L;
+#pragma unroll 1
+          while (rem > 0) {
+            const int k = min(rem, 8 - (o & 7));
+            push(lds_rd8(s32, lp), k);
+            lp += k;
+            rem -= k;
+          }
+        }
+      }
+      q += L;
+      if (q >= n) {  // the last sequence: literals only
+        if (q > n || o != job.dec_len) bad = true;
+        break;
+      }
+      const int d = tk < 0x60 ? (int)((w >> (8 * (1 + L))) & 0xFFFF) : (int)(lds_rd8(s32, q) & 0xFFFF);
+      q += 2;
+      if (M == 15) ext(q, M);
+      M += 4;
+      if (d == 0 || d > o || M > oend - o) {
+        bad = true;
+        break;
+      }
+      if (d <= 8) {  // near copy: the window's last d bytes, repeated
+#pragma unroll 1
+        while (M > 0) {
+          const int k = min(M, 8 - (o & 7));
+          uint64_t r = win >> (64 - 8 * d);
+          for (int per = d; per < 8; per <<= 1) r |= r << (8 * per);
+          push(r, k);
+          M -= k;
+        }
+      } else {  // far copy: its bytes from the far table
+#pragma unroll 1
+        while (M > 0) {
+          const int k = min(M, 8 - (o & 7));
+          push(lds_rd8(s32, fp), k);
+          fp += k;
+          M -= k;
+        }
+      }
+      p = q;
+    }
+    if (o != oend) bad = true;
+  }
+  if (bad) atomicOr(err, 1);
+  if (job.red_dst) red_finish(job, acc, s_red, kRunThreads / 64);
+}
+
+void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int lds, int32_t* d_err, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(k_lz4_run, dim3(njobs), dim3(kRunThreads), lds, s, d_jobs, d_err);
+}
+
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
   if (d_prof) hipLaunchKernelGGL(k_lz4_light<true>, dim3(njobs), dim3(kLtThreads), 0, s, d_jobs, d_err, d_prof);

@@ -26,6 +26,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -297,6 +298,79 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
   }
 }
 
+bool run_decode_enabled() {
+  const char* off = getenv("DG_NO_RUN_DECODE");
+  return !(off && *off && *off != '0');
+}
+
+// The run index of a validated block (layout: dg_internal.h, kRunThreads): the block is decoded once
+// on the host, cut into intervals of at least kRunTarget output bytes at sequence starts, and every
+// interval records its token offset, its output start and the 8 output bytes before it; the bytes
+// of matches reaching further back than 8 bytes (far copies) are listed in sequence order.
+bool lz4_run_index(const uint8_t* in, int n, int dec_len, std::vector<uint8_t>* idx, int* nint, int* nfar) {
+  *nint = 0;
+  *nfar = 0;
+  if (dec_len <= 0 || dec_len % 8 || dec_len > kBlockBytes || run_lds_bytes(n, 0) > kRunLdsMax) return false;
+  thread_local std::vector<uint8_t> out(kBlockBytes);
+  std::vector<uint64_t> win;
+  std::vector<uint32_t> tok;
+  std::vector<uint16_t> ost;
+  std::vector<uint8_t> far;
+  int pos = 0, o = 0, cur = 0;
+  auto ext = [&](int* len) {
+    for (;;) {
+      if (pos >= n) return false;
+      const int b = in[pos++];
+      *len += b;
+      if (b != 255) return true;
+    }
+  };
+  for (bool first = true;; first = false) {
+    if (first || o - cur >= kRunTarget) {  // a new interval at this sequence
+      cur = o;
+      uint64_t w = 0;
+      if (o >= 8) memcpy(&w, out.data() + o - 8, 8);
+      win.push_back(w);
+      tok.push_back((uint32_t)pos | ((uint32_t)far.size() << 17));
+      ost.push_back((uint16_t)o);
+    }
+    if (pos >= n) return false;
+    const int t = in[pos++];
+    int L = t >> 4;
+    if (L == 15 && !ext(&L)) return false;
+    if (L > kRunMaxRun || L > n - pos || L > dec_len - o) return false;
+    memcpy(out.data() + o, in + pos, (size_t)L);
+    pos += L;
+    o += L;
+    if (pos == n) break;  // last sequence: literals only
+    if (n - pos < 2) return false;
+    const int d = in[pos] | (in[pos + 1] << 8);
+    pos += 2;
+    int M = t & 15;
+    if (M == 15 && !ext(&M)) return false;
+    M += 4;
+    if (d == 0 || d > o || M > kRunMaxRun || M > dec_len - o) return false;
+    for (int k = 0; k < M; ++k) out[o + k] = out[o + k - d];
+    if (d > 8) {
+      far.insert(far.end(), out.begin() + o, out.begin() + o + M);
+      if ((int)far.size() > kRunFarMax) return false;
+    }
+    o += M;
+  }
+  const int ni = (int)tok.size();
+  if (o != dec_len || ni > kRunThreads || run_lds_bytes(n, (int)far.size()) > kRunLdsMax) return false;
+  const size_t at = idx->size();
+  idx->resize(at + (size_t)run_index_bytes(ni, (int)far.size()), 0);
+  uint8_t* p = idx->data() + at;
+  memcpy(p, win.data(), 8 * (size_t)ni);
+  memcpy(p + 8 * (size_t)ni, tok.data(), 4 * (size_t)ni);
+  memcpy(p + 12 * (size_t)ni, ost.data(), 2 * (size_t)ni);
+  if (!far.empty()) memcpy(p + ((14 * (size_t)ni + 15) & ~(size_t)15), far.data(), far.size());
+  *nint = ni;
+  *nfar = (int)far.size();
+  return true;
+}
+
 namespace {
 static void index_bitmap_pieces(Column* c, const std::vector<uint8_t>& host);
 
@@ -336,6 +410,10 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->first8.assign(blocks.n, 0);
     std::vector<uint8_t> has8(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
+    std::vector<std::vector<uint8_t>> runs(blocks.n);
+    col->run_n.assign(blocks.n, 0);
+    col->run_far.assign(blocks.n, 0);
+    col->run_off.assign(blocks.n, -1);
     const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const int nt = blocks.n >= 64 ? nth : 1;
     std::vector<std::thread> th;
@@ -350,20 +428,35 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
           col->dec_len[b] = d;
           if (d >= 8) has8[b] = lz4_first8(host.data() + col->comp_off[b], col->comp_len[b], &col->first8[b]);
           col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size() - nfine;
+          if (d > 0 && lz4_run_index(host.data() + col->comp_off[b], col->comp_len[b], d, &runs[b], &col->run_n[b],
+                                     &col->run_far[b]))
+            col->run_off[b] = 0;
         }
       });
     for (auto& x : th) x.join();
     for (int32_t b = 0; b < blocks.n; ++b)
       if (!has8[b]) col->first8.clear();  // (then no block's first value is known)
     std::vector<uint32_t> all;
+    std::vector<uint8_t> rall;
+    col->index_bytes = 0;
     for (int32_t b = 0; b < blocks.n; ++b) {
       col->cp_off[b] = (int64_t)all.size();
       if (col->cp_n[b] > 0) all.insert(all.end(), per[b].begin(), per[b].end());
+      if (col->run_off[b] >= 0) {  // a query reads the run index of a run block, not its checkpoints
+        col->run_off[b] = (int64_t)rall.size();
+        rall.insert(rall.end(), runs[b].begin(), runs[b].end());
+        col->index_bytes += (int64_t)runs[b].size();
+      } else if (col->cp_n[b] > 0) {
+        col->index_bytes += 4 * (int64_t)per[b].size();
+      }
     }
     if (all.empty()) all.push_back(0);
-    col->index_bytes = (int64_t)all.size() * 4;
     if (!col->cps.alloc(all.size() * 4)) return set_error(DG_ERR_OOM, "hipMalloc lz4 index");
     DG_HIP(hipMemcpy(col->cps.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+    if (!rall.empty()) {
+      if (!col->runx.alloc(rall.size())) return set_error(DG_ERR_OOM, "hipMalloc lz4 run index");
+      DG_HIP(hipMemcpy(col->runx.p, rall.data(), rall.size(), hipMemcpyHostToDevice));
+    }
     return DG_OK;
   }
   if (col->codec == CODEC_UNCOMPRESSED) {

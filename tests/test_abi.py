@@ -27,11 +27,12 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_structs():
     N = importlib.import_module("incubator-druid_amd._native")
-    assert N.lib().dg_abi_version() == 13
+    assert N.lib().dg_abi_version() == 14
     # struct layouts the header fixes (LP64)
     assert ctypes.sizeof(N.dg_filter) == 64
     assert ctypes.sizeof(N.dg_agg) == 32
-    assert ctypes.sizeof(N.dg_scan) == 96
+    assert ctypes.sizeof(N.dg_scan) == 104
+    assert N.dg_scan.timeout_ms.offset == 96
     assert ctypes.sizeof(N.dg_metrics) == 176
     assert ctypes.sizeof(N.dg_topn_lists) == 40
     assert ctypes.sizeof(N.dg_topn) == 56
@@ -44,7 +45,7 @@ def test_gpu_kernels_are_gfx950_code_objects():
     N = importlib.import_module("incubator-druid_amd._native")
     data = open(N.LIB_PATH, "rb").read()
     assert b"gfx950" in data
-    for k in (b"k_lz4_decode", b"k_concise_or", b"k_roaring_or", b"k_scan_agg", b"k_topn_radix", b"k_topn_compact", b"k_gb_keygen",
+    for k in (b"k_lz4_decode", b"k_lz4_run", b"k_concise_or", b"k_roaring_or", b"k_scan_agg", b"k_topn_radix", b"k_topn_compact", b"k_gb_keygen",
               b"k_rs_scatter", b"k_gb_reduce", b"k_fsum_runs", b"k_limit_load", b"k_limit_gather"):
         assert k in data, k
 
