@@ -405,9 +405,17 @@ int64_t dg_result_groups(const dg_result* res);
  * String order, nulls first): bucket_time[count] (ALL granularity: the universal timestamp = the
  * query interval's start, GroupByStrategyV2.getUniversalTimestamp :125-138), ids[count * n_dims]
  * = indices into the result's merged dictionary of each dimension, values[count * n_aggs] in the
- * slot encoding of dg_timeseries_run. Any output pointer may be NULL. */
+ * slot encoding of dg_timeseries_run. Any output pointer may be NULL (under ALL granularity the
+ * caller knows every bucket time and passes NULL). Destinations in pinned host memory (dg_host_alloc,
+ * or memory the caller registered with HIP) receive the columns by DMA straight from the device;
+ * others through the library's pinned staging. */
 int dg_result_fetch_groups(dg_result* res, int64_t start, int64_t count, int64_t* bucket_time, int32_t* ids,
                            uint64_t* values);
+/* Pinned host memory for result delivery (since ABI 14): the shim allocates its result buffers once
+ * and wraps them as direct ByteBuffers (JNI NewDirectByteBuffer), the way the processing pool's
+ * buffers are allocated once at startup (OffheapBufferGenerator.java:53 allocateDirect). */
+int dg_host_alloc(int64_t bytes, void** out);
+void dg_host_free(void* p);
 /* rows aggregated into each group of [start, start + count) */
 int dg_result_fetch_rows(dg_result* res, int64_t start, int64_t count, int64_t* rows);
 /* merged dictionary of dimension `dim` (the union of the segments' dictionaries, Java String

@@ -135,7 +135,7 @@ EXPORTS = [
     "dg_result_dim_dictionary", "dg_result_release", "dg_keyspace_bits", "dg_result_export", "dg_keys_partition",
     "dg_merge", "dg_records_pack", "dg_debug_lz4_decode", "dg_result_limit",
     "dg_segment_from_rows", "dg_context_set_limit", "dg_groupby_merge_devices", "dg_timeseries_merge",
-    "dg_debug_lz4_classify",
+    "dg_debug_lz4_classify", "dg_host_alloc", "dg_host_free",
 ]
 
 _lib = None
@@ -202,6 +202,8 @@ def lib():
         "dg_records_pack": (ctypes.c_int, [vp, i64, P(dg_record_layout), vp]),
         "dg_debug_lz4_decode": (ctypes.c_int, [vp, P(vp), P(i32), i32, vp, P(i32), P(ctypes.c_double), vp]),
         "dg_debug_lz4_classify": (ctypes.c_int, [vp, i32, P(i32)]),
+        "dg_host_alloc": (ctypes.c_int, [i64, P(vp)]),
+        "dg_host_free": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(l, name)

@@ -33,6 +33,16 @@ namespace dg {
 static thread_local char g_err[1024] = "";
 static thread_local uint64_t g_err_count = 0;  // set_error calls on this thread (CallGuard: did the call fail?)
 
+static thread_local hipError_t g_launch_err = hipSuccess;
+void note_launch_error(hipError_t e) {
+  if (g_launch_err == hipSuccess) g_launch_err = e;
+}
+hipError_t take_launch_error() {
+  const hipError_t e = g_launch_err;
+  g_launch_err = hipSuccess;
+  return e;
+}
+
 int set_error(int code, const char* fmt, ...) {
   ++g_err_count;
   va_list ap;
@@ -284,6 +294,7 @@ static int finish_call(CallScratch* cs, hipStream_t st) {
     DG_HIP(hipStreamSynchronize(st));
   }
   DG_HIP(hipGetLastError());
+  DG_HIP(take_launch_error());
   if (cs->d_err && *cs->h_err)
     return set_error(DG_ERR_FORMAT, (*cs->h_err & 1)   ? "corrupt LZ4 block"
                                     : (*cs->h_err & 4) ? "corrupt multi-value row lists"
@@ -1518,32 +1529,28 @@ static Cursors plan_cursors(const Segment* seg, int seg_index, const dg_scan* q,
 // The cursor's __time view of a scan (ScanJob / GbJob .time: bucket and interval of every row). An
 // LZ4 LONGS block whose rows all fall in one bucket and inside [t_lo, t_hi) is not decoded: its block
 // pointer is tagged and points at one representative time (load_time), which gives each of its rows
-// the verdict its own time would. Rows are time-sorted (IndexMergerV9 / IncrementalIndex order), so
-// block k's rows lie in [first[k], first[k + 1]] (the blocks' first-row times, read at attach) and the
-// last block's in [first[k], maxTime]; the view falls back to decoding every block when the first
-// times do not ascend. grid0: a bucket start at or before t_lo (period grids); g: calendar buckets.
-// Per __time block: the bucket (the scan's index, row_selected's formula) its rows share inside the
-// interval, or -1 when they may span buckets or leave it. Empty when the blocks' first times cannot
-// bound their rows (not plain LZ4 LONGS, first times not ascending, or DG_NO_TIME_SKIP).
+// the verdict its own time would. Block k's rows lie in [min8[k], max8[k]] (its smallest and largest
+// row time, from the attach-time host decode of __time), so no assumption on the row order is needed.
+// g: calendar buckets. Per __time block: the bucket (the scan's index, row_selected's formula) its rows
+// share inside the interval, or -1 when they may span buckets or leave it. Empty when the blocks' time
+// ranges are unknown (not plain LZ4 LONGS, a segment from rows, or DG_NO_TIME_SKIP).
 static std::vector<int64_t> time_block_buckets(const Segment* seg, const Column* c, const Cursors& cu, int64_t period,
                                                const Grain& g) {
   std::vector<int64_t> tb;
   if (!c) return tb;
   const BlockColumn& b = c->data;
-  const bool plain = b.codec == CODEC_LZ4 && !b.vbits && b.width == 8 && (int32_t)b.first8.size() == b.nblocks &&
-                     b.nblocks > 0 && !c->multi_value;
-  bool sorted = plain;
-  for (int32_t k = 1; sorted && k < b.nblocks; ++k) sorted = b.first8[k - 1] <= b.first8[k];
-  if (sorted) sorted = b.first8[b.nblocks - 1] <= seg->max_time;
+  (void)seg;
+  const bool plain = b.codec == CODEC_LZ4 && !b.vbits && b.width == 8 && (int32_t)b.min8.size() == b.nblocks &&
+                     (int32_t)b.max8.size() == b.nblocks && b.nblocks > 0 && !c->multi_value;
   const char* off = getenv("DG_NO_TIME_SKIP");  // (same-box A/B and tests: decode every block)
-  if (!sorted || (off && *off && *off != '0')) return tb;
+  if (!plain || (off && *off && *off != '0')) return tb;
   auto bucket = [&](int64_t t) -> int64_t {
     const int64_t v = g.hb ? g.coord(t) : t;
     return period ? (v - cu.bucket0) / period : 0;
   };
   tb.assign(b.nblocks, -1);
   for (int32_t k = 0; k < b.nblocks; ++k) {
-    const int64_t lo = b.first8[k], hi = k + 1 < b.nblocks ? b.first8[k + 1] : seg->max_time;
+    const int64_t lo = b.min8[k], hi = b.max8[k];
     if (lo >= cu.t_lo && hi < cu.t_hi && bucket(lo) == bucket(hi)) tb[k] = bucket(lo);
   }
   return tb;
@@ -1575,7 +1582,7 @@ static int time_view(const Column* c, const std::vector<int64_t>& tb, CallScratc
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (uni[k]) {
-      h_const[k] = b.first8[k];
+      h_const[k] = b.min8[k];  // (any time of the block's rows: they share the bucket and the interval verdict)
       h_ptrs[k] = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(d_const + k) | 1u);
       continue;
     }
@@ -1771,6 +1778,7 @@ struct CallGuard {
   explicit CallGuard(Context* c) : ctx(c), lock(c->mu), cs(scratch_of(c)), errs0(g_err_count) {
     hipSetDevice(c->device);
     cs->reset();
+    (void)take_launch_error();  // (a previous call's, already reported or abandoned)
   }
   // a call that fails (interrupted, timed out, or any error after launches) drains both streams before
   // it returns: queued kernels and copies still use the call's scratch and staging, which the next call
@@ -3698,9 +3706,48 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
   const int nd = r->ndims, na = r->naggs;
   // per group: time 8 B, ids 4 B each, values 8 B each, packed on the device and copied through two
   // pinned staging chunks; the host copies chunk i into the caller's arrays (several threads) while
-  // chunk i + 1 crosses PCIe
+  // chunk i + 1 crosses PCIe. Pinned destinations take each chunk's columns by DMA instead.
   const int64_t per = (bucket_time ? 8 : 0) + (ids ? 4 * (int64_t)nd : 0) + (values ? 8 * (int64_t)na : 0);
   if (per == 0) return DG_OK;
+  auto pinned = [](const void* p) {
+    if (!p) return true;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return a.type == hipMemoryTypeHost;
+  };
+  if (pinned(bucket_time) && pinned(ids) && pinned(values)) {
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)256 << 20) / per));
+    uint8_t* d_stage = dev_take<uint8_t>(cs, (size_t)(chunk * per + 64));
+    if (!d_stage) return set_error(DG_ERR_OOM, "fetch staging");
+    const int64_t* d_bounds = nullptr;
+    if (r->period && !r->bounds.empty()) {
+      int64_t* db;
+      int64_t* hb = up_take<int64_t>(cs, r->bounds.size(), &db, st);
+      if (!hb) return set_error(DG_ERR_OOM, "bucket table");
+      memcpy(hb, r->bounds.data(), r->bounds.size() * 8);
+      d_bounds = db;
+    }
+    DG_FLUSH(cs, st);
+    for (int64_t c0 = start; c0 < start + count; c0 += chunk) {
+      const int64_t n = std::min<int64_t>(chunk, start + count - c0);
+      uint8_t* p = d_stage;
+      int64_t* t = bucket_time ? reinterpret_cast<int64_t*>(p) : nullptr;
+      p += bucket_time ? 8 * n : 0;
+      uint64_t* v = values && na ? reinterpret_cast<uint64_t*>(p) : nullptr;
+      p += v ? 8 * n * na : 0;
+      int32_t* i = ids && nd ? reinterpret_cast<int32_t*>(p) : nullptr;
+      launch_gb_fetch_pack(r->keys, r->slots, r->cap, c0, n, r->lay, na, r->universal, r->bucket0, r->period, d_bounds, t,
+                           i, v, st);
+      const int64_t o = c0 - start;
+      if (t) DG_HIP(hipMemcpyAsync(bucket_time + o, t, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+      if (v) DG_HIP(hipMemcpyAsync(values + o * na, v, (size_t)(n * na) * 8, hipMemcpyDeviceToHost, st));
+      if (i) DG_HIP(hipMemcpyAsync(ids + o * nd, i, (size_t)(n * nd) * 4, hipMemcpyDeviceToHost, st));
+    }
+    return finish_call(cs, st);
+  }
   const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)64 << 20) / per));
   const size_t cbytes = (size_t)(chunk * per + 64);
   uint8_t* d_stage = dev_take<uint8_t>(cs, cbytes);
@@ -3757,6 +3804,21 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
   DG_HIP(hipEventSynchronize(done[k ^ 1]));
   drain(k ^ 1, prev0, prevn);
   return finish_call(cs, st);
+}
+
+int dg_host_alloc(int64_t bytes, void** out) {
+  if (!out || bytes < 0) return set_error(DG_ERR_ARG, "bad arguments");
+  *out = nullptr;
+  if (hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 64), hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return set_error(DG_ERR_OOM, "hipHostMalloc %lld", (long long)bytes);
+  }
+  return DG_OK;
+}
+
+void dg_host_free(void* p) {
+  if (p) hipHostFree(p);
 }
 
 int dg_result_fetch_rows(dg_result* r, int64_t start, int64_t count, int64_t* rows) {

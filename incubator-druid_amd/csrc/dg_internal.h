@@ -112,6 +112,8 @@ inline int run_lds_bytes(int n, int nfar) { return ((n + 15) & ~15) + 16 + ((nfa
 // Run index of one validated LZ4 block decoding to dec_len bytes, appended to *idx (16-byte aligned);
 // returns false (nothing appended) when the block is not a run block.
 bool lz4_run_index(const uint8_t* in, int n, int dec_len, std::vector<uint8_t>* idx, int* nint, int* nfar);
+// Host decode of a validated LZ4 block into out (kBlockBytes); returns the decoded length or -1.
+int lz4_decode_host(const uint8_t* in, int n, uint8_t* out);
 // the run decoder is on unless DG_NO_RUN_DECODE is set (same-box A/B, tests of the other decoders)
 bool run_decode_enabled();
 
@@ -273,8 +275,10 @@ struct BlockColumn {
   std::vector<uint8_t> cp_light;       // LZ4: block b goes to the light decoder (sequences per light checkpoint)
   std::vector<int32_t> cp_fine;        // LZ4: light checkpoints of block b (after its cp_n checkpoints)
   std::vector<int32_t> dec_len;        // LZ4: decoded bytes of block b
-  std::vector<int64_t> first8;         // LZ4: the first 8 decoded bytes of block b (int64 LE: its first
-                                       // row's value in a LONGS column), from the attach-time parse
+  bool time_col = false;               // the __time column: min8 / max8 are recorded at attach
+  std::vector<int64_t> min8, max8;     // __time LZ4 LONGS: smallest / largest row time of block b (host
+                                       // decode at attach; the cursor's uniform-block skip needs no
+                                       // assumption on the row order inside a block)
   int64_t index_bytes = 0;             // LZ4: bytes of the index a query reads (checkpoints; run index
                                        // of run blocks instead)
   std::vector<int64_t> run_off;        // LZ4: block b's run index inside runx (-1: not a run block)
@@ -407,6 +411,11 @@ int load_segment(Context* ctx, const char* dir, Segment** out);
 int segment_from_rows(Context* ctx, int64_t nrows, const int64_t* ts, int64_t istart, int64_t iend,
                       const dg_row_column* cols, int ncols, Segment** out);
 int java_compare_str(const char* a, const char* b);  // String.compareTo over UTF-8 bytes (dg_engine.cpp)
+
+// a failed enqueue inside a void launcher (e.g. the memset of look-back status): recorded per thread,
+// returned as DG_ERR_DEVICE by the call's finish_call (dg_engine.cpp)
+void note_launch_error(hipError_t e);
+hipError_t take_launch_error();
 
 // kernel launchers (dg_kernels.hip)
 constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (diagnostic builds of the call)

@@ -73,12 +73,6 @@ constexpr int kPairs = 32;                     // E pairs per thread: 2 * 32 * 1
 #ifndef DG_LZ_STAGE_STEPS
 #define DG_LZ_STAGE_STEPS 24  // extra jumps inside a stage before an entry is left to the rounds (3 / 6 / 12 / 24: 24 fastest)
 #endif
-#ifndef DG_LZ_STAGED
-#define DG_LZ_STAGED 1  // non-class resolution in position-ordered stages (0: sweep + rounds, A/B)
-#endif
-#ifndef DG_LZ_BATCH_APPEND
-#define DG_LZ_BATCH_APPEND 1  // the class scan's open terminals listed once per thread (0: per pair, A/B)
-#endif
 #ifndef DG_LZ_JUMP_BATCH
 #define DG_LZ_JUMP_BATCH 4
 #endif
@@ -253,14 +247,7 @@ __device__ __forceinline__ uint32_t lz_value(const LzState& S, int x) {
 // E entries of one sequence in the general form (out of line: the rare cases): literals that did not
 // get a job (table full; read from the compressed block in HBM, `lit` = input offset) or whose
 // bytes ride in `lv`, matches without a job, and tail matches at distances >= kTail.
-#ifndef DG_LZ_FILL_INLINE
-#define DG_LZ_FILL_INLINE 0  // (A/B: the rare-case fill inlined at its call sites)
-#endif
-#if DG_LZ_FILL_INLINE
-__device__ __forceinline__
-#else
 __device__ __noinline__
-#endif
 void fill_general(uint16_t* e, uint32_t* tsrc, const uint8_t* __restrict__ gin, int o, int L, int M, int d,
                                           uint32_t lv, bool lit_inline, bool lit_here, bool match_here) {
   const LzState S{e, tsrc};
@@ -744,28 +731,15 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   if (tid == 0) s_nopen = 0;
   __syncthreads();
   const int wv = tid >> 6, ln = tid & 63;
-#if !DG_LZ_BATCH_APPEND
-  auto list_append = [&](bool op, int v) {  // wave-aggregated append to s_open
-    const uint64_t bal = __ballot(op);
-    if (bal) {
-      int at = 0;
-      if (ln == 0) at = atomicAdd(&s_nopen, __popcll(bal));
-      at = __shfl(at, 0, 64) +
-           (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-      if (op && at < kOpenCap) s_open[at] = (uint16_t)v;
-    }
-  };
-#endif
   auto is_open = [](uint32_t v) { return (v & 0xFFFF) < (uint32_t)kTail || (v >> 16) < (uint32_t)kTail; };
   // one jump step for an entry d whose target holds e
   auto jstep = [](uint32_t d, uint32_t e) -> uint32_t {
     return d >= (uint32_t)kTail ? d : (e >= (uint32_t)kTail ? e : d + e);
   };
-  // full sweep of my wave's region, one step per open entry; with `mark`, the pairs still open
-  // afterwards are set in the open-pair bitmap s_obits (a step's 64 lanes are 64 consecutive pairs:
-  // its ballot is two bitmap words). Returns whether any of my entries is still open.
+  // full sweep of my wave's region, one step per open entry (the class scan's fallback when its list of
+  // open terminals overflows). Returns whether any of my entries is still open.
   uint32_t* s_obits = reinterpret_cast<uint32_t*>(s_jobs_buf);  // kBlockBytes / 2 bits (non-class mode)
-  auto sweep = [&](bool mark) -> bool {
+  auto sweep = [&]() -> bool {
     bool any = false;
 #pragma unroll 1
     for (int b = 0; b < kPairs / kJumpBatch; ++b) {
@@ -778,10 +752,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         dv[k] = x < kTail ? s_e32[eph(x) >> 1] : 0xFF00FF00u;
         need |= is_open(dv[k]);
       }
-      if (__ballot(need) == 0) {
-        if (mark && ln < 2 * kJumpBatch) s_obits[((wv * (kPairs * 64) + j0 * 64) >> 5) + ln] = 0u;
-        continue;
-      }
+      if (__ballot(need) == 0) continue;
 #pragma unroll
       for (int k = 0; k < kJumpBatch; ++k) {
         const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
@@ -794,19 +765,11 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
         const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
         const uint32_t nv = jstep(dv[k] & 0xFFFF, ta[k]) | (jstep(dv[k] >> 16, tb[k]) << 16);
         if (nv != dv[k]) s_e32[eph(x) >> 1] = nv;
-        const bool op = is_open(nv);
-        any |= op;
-        if (mark) {
-          const uint64_t bal = __ballot(op);
-          const int w0 = (wv * (kPairs * 64) + (j0 + k) * 64) >> 5;
-          if (ln == 0) s_obits[w0] = (uint32_t)bal;
-          if (ln == 32) s_obits[w0 + 1] = (uint32_t)(bal >> 32);
-        }
+        any |= is_open(nv);
       }
     }
     return any;
   };
-#if DG_LZ_STAGED
   // Staged resolution in position order: stage s takes the kLzThreads pairs after stage s - 1, all
   // of whose entries are literal codes by then, so a target before the stage is one read from its
   // code. A target inside the stage (distance < the stage) is followed for up to kStageSteps more
@@ -862,7 +825,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     for (int w = ((npairs + kStage - 1) / kStage) * (kStage / 32) + tid; w < kLzThreads; w += kLzThreads) s_obits[w] = 0u;
     return any;
   };
-#endif
   int jump_rounds = 0;
   if (cls) {
     // carry scan over my 64 positions [tid * 64, tid * 64 + 64). A terminal travels as key
@@ -904,9 +866,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 #pragma unroll
       for (int c = 0; c < kClass; ++c) carry[c] = max(carry[c], (uint32_t)__builtin_amdgcn_readlane((int)v, c));
     }
-#if DG_LZ_BATCH_APPEND
     uint64_t omask = 0;  // my open terminals (bit = position - x0)
-#endif
     auto take = [](uint32_t key, int x) -> uint32_t {  // new entry of a distance-8 byte at x
       const uint32_t tv = key & 0xFFFF;
       return tv >= (uint32_t)kTail ? tv : (uint32_t)(x + 1) - (key >> 16);
@@ -931,15 +891,9 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       }
       const uint32_t nv = lo | (hi << 16);
       if (nv != v) s_e32[eb + q] = nv;  // x < lim whenever an entry changes
-#if DG_LZ_BATCH_APPEND
-      omask |= (uint64_t)(t0 && lo < (uint32_t)kTail) << (2 * q);
+      omask |= (uint64_t)(t0 && lo < (uint32_t)kTail) << (2 * q);  // open terminals
       omask |= (uint64_t)(t1 && hi < (uint32_t)kTail) << (2 * q + 1);
-#else
-      list_append(t0 && lo < (uint32_t)kTail, x);  // open terminals
-      list_append(t1 && hi < (uint32_t)kTail, x + 1);
-#endif
     }
-#if DG_LZ_BATCH_APPEND
     {
       const int nm = __popcll(omask);
       if (__ballot(nm)) {
@@ -948,7 +902,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
           if (at < kOpenCap) s_open[at] = (uint16_t)(x0 + __builtin_ctzll(omask));
       }
     }
-#endif
     LZ_WAVE_STAMP(4);
     __syncthreads();
     LZ_STAMP(13);
@@ -976,7 +929,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
       // every scanned entry now holds a code or the distance to a terminal that holds one: the tail
       // and the output take that last hop themselves (final_code)
     } else {
-      for (int round = 0; __syncthreads_or(sweep(false)); ++round) {
+      for (int round = 0; __syncthreads_or(sweep()); ++round) {
         jump_rounds++;
         if (round > kMaxRounds) {
           if (tid == 0) atomicOr(err, 1);
@@ -986,11 +939,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
   } else {
     jump_rounds = 1;
-#if DG_LZ_STAGED
     const bool open1 = __syncthreads_or(staged());
-#else
-    const bool open1 = __syncthreads_or(sweep(true));
-#endif
     LZ_STAMP(12);
     LZ_STAMP(13);
     if (open1) {

@@ -180,39 +180,6 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
   }
 }
 
-// The first 8 decoded bytes of a validated block (its first sequences only), or false when it
-// decodes to fewer.
-static bool lz4_first8(const uint8_t* in, int n, int64_t* out) {
-  uint8_t buf[8];
-  int o = 0, p = 0;
-  auto ext = [&](int* len) {
-    for (int b = 255; b == 255 && p < n;) {
-      b = in[p++];
-      *len += b;
-    }
-  };
-  while (o < 8) {
-    if (p >= n) return false;
-    const int tok = in[p++];
-    int L = tok >> 4;
-    if (L == 15) ext(&L);
-    if (L > n - p) return false;
-    for (int k = 0; k < L && o < 8; ++k) buf[o++] = in[p + k];
-    p += L;
-    if (o >= 8 || p >= n || n - p < 2) break;
-    const int d = in[p] | (in[p + 1] << 8);
-    p += 2;
-    int M = tok & 15;
-    if (M == 15) ext(&M);
-    M += 4;
-    if (d == 0 || d > o) return false;
-    for (int k = 0; k < M && o < 8; ++k, ++o) buf[o] = buf[o - d];
-  }
-  if (o < 8) return false;
-  memcpy(out, buf, 8);
-  return true;
-}
-
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine) {
   const size_t first = cps->size();
   if (light) *light = 0;
@@ -295,6 +262,38 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
     M += 4;
     if (off == 0 || off > out || M > kBlockBytes - out) return -1;
     out += M;
+  }
+}
+
+int lz4_decode_host(const uint8_t* in, int n, uint8_t* out) {
+  int pos = 0, o = 0;
+  auto ext = [&](int* len) {
+    for (;;) {
+      if (pos >= n) return false;
+      const int b = in[pos++];
+      *len += b;
+      if (b != 255) return true;
+    }
+  };
+  for (;;) {
+    if (pos >= n) return -1;
+    const int t = in[pos++];
+    int L = t >> 4;
+    if (L == 15 && !ext(&L)) return -1;
+    if (L > n - pos || L > kBlockBytes - o) return -1;
+    memcpy(out + o, in + pos, (size_t)L);
+    pos += L;
+    o += L;
+    if (pos == n) return o;
+    if (n - pos < 2) return -1;
+    const int d = in[pos] | (in[pos + 1] << 8);
+    pos += 2;
+    int M = t & 15;
+    if (M == 15 && !ext(&M)) return -1;
+    M += 4;
+    if (d == 0 || d > o || M > kBlockBytes - o) return -1;
+    for (int k = 0; k < M; ++k) out[o + k] = out[o + k - d];
+    o += M;
   }
 }
 
@@ -407,13 +406,17 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->cp_light.assign(blocks.n, 0);
     col->cp_fine.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
-    col->first8.assign(blocks.n, 0);
-    std::vector<uint8_t> has8(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
     std::vector<std::vector<uint8_t>> runs(blocks.n);
     col->run_n.assign(blocks.n, 0);
     col->run_far.assign(blocks.n, 0);
     col->run_off.assign(blocks.n, -1);
+    const bool minmax = col->time_col && col->width == 8 && !col->vbits;
+    if (minmax) {
+      col->min8.assign(blocks.n, 0);
+      col->max8.assign(blocks.n, 0);
+    }
+    std::vector<uint8_t> has_mm(blocks.n, 0);
     const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const int nt = blocks.n >= 64 ? nth : 1;
     std::vector<std::thread> th;
@@ -426,16 +429,34 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
           col->cp_light[b] = (uint8_t)light;
           col->cp_fine[b] = nfine;
           col->dec_len[b] = d;
-          if (d >= 8) has8[b] = lz4_first8(host.data() + col->comp_off[b], col->comp_len[b], &col->first8[b]);
           col->cp_n[b] = d < 0 ? -1 : (int32_t)per[b].size() - nfine;
           if (d > 0 && lz4_run_index(host.data() + col->comp_off[b], col->comp_len[b], d, &runs[b], &col->run_n[b],
                                      &col->run_far[b]))
             col->run_off[b] = 0;
+          if (minmax && d >= 8) {  // the block's smallest and largest row time (its rows only)
+            thread_local std::vector<uint8_t> dec(kBlockBytes);
+            const int64_t rows = std::min<int64_t>(col->size_per, (int64_t)col->total - (int64_t)b * col->size_per);
+            if (rows > 0 && lz4_decode_host(host.data() + col->comp_off[b], col->comp_len[b], dec.data()) >= rows * 8) {
+              int64_t mn = INT64_MAX, mx = INT64_MIN;
+              for (int64_t r = 0; r < rows; ++r) {
+                int64_t v;
+                memcpy(&v, dec.data() + 8 * r, 8);
+                mn = std::min(mn, v);
+                mx = std::max(mx, v);
+              }
+              col->min8[b] = mn;
+              col->max8[b] = mx;
+              has_mm[b] = 1;
+            }
+          }
         }
       });
     for (auto& x : th) x.join();
-    for (int32_t b = 0; b < blocks.n; ++b)
-      if (!has8[b]) col->first8.clear();  // (then no block's first value is known)
+    for (int32_t b = 0; minmax && b < blocks.n; ++b)
+      if (!has_mm[b]) {  // (then no block's time range is known: every block is decoded)
+        col->min8.clear();
+        col->max8.clear();
+      }
     std::vector<uint32_t> all;
     std::vector<uint8_t> rall;
     col->index_bytes = 0;
@@ -612,6 +633,7 @@ int parse_numeric(Context* ctx, Column* c, Slice s, int width) {
   GI blocks;
   if (!gi_read(s, &blocks)) return set_error(DG_ERR_FORMAT, "%s: bad block index", c->name.c_str());
   if ((int64_t)blocks.n * col.size_per < col.total) return set_error(DG_ERR_FORMAT, "%s: too few blocks", c->name.c_str());
+  col.time_col = c->name == "__time";
   int rc = upload_blocks(ctx, &col, blocks);
   if (rc || !col.vbits) return rc;
   // every block must hold the packed bytes of its rows (the expansion reads exactly those)

@@ -33,6 +33,15 @@
 
 namespace dg {
 
+// Zero a device range before a kernel that reads it as look-back status / counters; on failure the
+// dependent kernel is not launched (un-zeroed status words could make a look-back wait forever) and
+// the error surfaces at the call's finish_call (take_launch_error).
+static bool zero_async(void* p, size_t n, hipStream_t s) {
+  const hipError_t e = hipMemsetAsync(p, 0, n, s);
+  if (e != hipSuccess) note_launch_error(e);
+  return e == hipSuccess;
+}
+
 constexpr int kST = 256;                 // threads of the sort / run kernels
 constexpr int kSPT = kSortTile / kST;    // 16 elements per thread
 
@@ -211,7 +220,7 @@ __global__ __launch_bounds__(1024) void k_sum_u64(const uint32_t* __restrict__ a
 void launch_gb_count_total(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, uint32_t* tile_cnt,
                            unsigned long long* total, hipStream_t s) {
   if (ntiles <= 0) {
-    (void)hipMemsetAsync(total, 0, 8, s);
+    zero_async(total, 8, s);
     return;
   }
   hipLaunchKernelGGL(k_gb_count<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, tile_cnt);
@@ -369,7 +378,7 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
 void launch_gb_count(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, uint32_t* tile_cnt, uint32_t* total,
                      bool multi, hipStream_t s) {
   if (ntiles <= 0) {
-    (void)hipMemsetAsync(total, 0, 4, s);
+    zero_async(total, 4, s);
     return;
   }
   if (multi) hipLaunchKernelGGL(k_gb_count<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, tile_cnt);
@@ -380,7 +389,7 @@ void launch_gb_count(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles,
 void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
                       hipStream_t s, bool multi) {
   if (ntiles <= 0) {
-    (void)hipMemsetAsync(sb->n, 0, 4, s);
+    zero_async(sb->n, 4, s);
     return;
   }
   launch_gb_count(d_jobs, d_tile_job, ntiles, sb->tile_cnt, sb->n, multi, s);
@@ -594,7 +603,7 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
   const int nt = sb->ntiles_sort;
   uint32_t* totals = sb->bin_total;                            // [npass][kMaxBins]
   uint32_t* ctr = sb->bin_total + kRsMaxPasses * kMaxBins;     // [npass] tile counters
-  (void)hipMemsetAsync(sb->bin_total, 0, ((size_t)kRsMaxPasses * kMaxBins + kRsMaxPasses) * sizeof(uint32_t), s);
+  if (!zero_async(sb->bin_total, ((size_t)kRsMaxPasses * kMaxBins + kRsMaxPasses) * sizeof(uint32_t), s)) return;
   // the first pass's digit totals from one read of the keys; every pass's scatter counts the next
   // pass's digits of the keys it stores
   hipLaunchKernelGGL(k_rs_hist0, dim3(std::min(nt, 4096)), dim3(kST), 0, s, sb->keys[sb->cur], sb->n,
@@ -608,7 +617,7 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
     // 30-bit counts hold every prefix (n <= cap); DG_SORT_WIDE_STATUS=1: 64-bit words regardless (tests)
     const char* wide = getenv("DG_SORT_WIDE_STATUS");
     const bool narrow = sb->cap < ((int64_t)1 << 30) && !(wide && *wide && *wide != '0');
-    (void)hipMemsetAsync(sb->lb_status, 0, (size_t)(1 << bits) * nt * (narrow ? 4 : 8), s);  // look-back status
+    if (!zero_async(sb->lb_status, (size_t)(1 << bits) * nt * (narrow ? 4 : 8), s)) return;  // look-back status
     uint32_t* st32 = reinterpret_cast<uint32_t*>(sb->lb_status);
     uint64_t* st64 = sb->lb_status;
     const uint32_t* tp = totals + (size_t)p * kMaxBins;
@@ -738,25 +747,16 @@ __device__ __forceinline__ uint64_t seg_scan_wave(int op, uint64_t v, bool head,
   return v;
 }
 
-#ifndef DG_RED_MINW
-#define DG_RED_MINW 4
-#endif
+constexpr int kRedMinW = 4;  // waves per EU the reduce is compiled for (87 VGPRs)
 constexpr int kRT = 64 * kRedWaves;             // reduce threads per tile
 constexpr int kRSPT = kSortTile / kRT;          // elements per lane
 // A workgroup barrier for LDS only: waits for this wave's LDS operations, not its global loads, so the
 // reduce's random payload gathers stay in flight across the head count and the look-back (a
-// __syncthreads would wait for them: s_waitcnt vmcnt(0) before s_barrier). DG_RED_FULL_SYNC: the plain
-// barrier (same-box A/B).
-__device__ __forceinline__ void red_barrier() {
-#ifdef DG_RED_FULL_SYNC
-  __syncthreads();
-#else
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
-}
+// __syncthreads would wait for them: s_waitcnt vmcnt(0) before s_barrier; measured equal or slower).
+__device__ __forceinline__ void red_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <bool REFS>
-__global__ __launch_bounds__(kRT, DG_RED_MINW) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw,
+__global__ __launch_bounds__(kRT, kRedMinW) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, uint32_t* __restrict__ n_ptr,
                                                    uint64_t* __restrict__ status, uint32_t* __restrict__ tile_ctr,
@@ -992,9 +992,9 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
   // (a separate k_run_count pass + scan for the tile offsets measured the same, same box: 14.17-14.29
   // vs 14.22-14.25 ms per headline step)
   uint32_t* ctr = sb->bin_total + (size_t)kRsMaxPasses * kMaxBins + kRsMaxPasses;
-  (void)hipMemsetAsync(sb->lb_status, 0, (size_t)nt * sizeof(uint64_t), s);
-  (void)hipMemsetAsync(ctr, 0, sizeof(uint32_t), s);
-  (void)hipMemsetAsync(sb->n + 1, 0, sizeof(uint32_t), s);
+  if (!zero_async(sb->lb_status, (size_t)nt * sizeof(uint64_t), s)) return;
+  if (!zero_async(ctr, sizeof(uint32_t), s)) return;
+  if (!zero_async(sb->n + 1, sizeof(uint32_t), s)) return;
   if (refs)
     hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->lb_status, ctr, plan, out_keys, out_slots, cap, head_pos,

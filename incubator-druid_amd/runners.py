@@ -89,16 +89,18 @@ class RunStats:
 # timeseries
 # ----------------------------------------------------------------------------------------------
 def timeseries_per_segment(segments: Sequence[GpuSegment], query: Q.TimeseriesQuery,
-                           stats: Optional[RunStats] = None) -> List[List[Q.Result]]:
+                           stats: Optional[RunStats] = None,
+                           cancel: Optional[ctypes.c_int32] = None) -> List[List[Q.Result]]:
     split = segment_queries(query, segments)
     if split is not None:  # every segment on its own calendar chain
-        return [timeseries_per_segment([s], q, stats)[0] if q is not None else [] for s, q in zip(segments, split)]
+        return [timeseries_per_segment([s], q, stats, cancel)[0] if q is not None else []
+                for s, q in zip(segments, split)]
     out: List[List[Q.Result]] = [[] for _ in segments]
     na = len(query.aggregations)
     for _, idx in _group_by_device(segments).items():
         segs = [segments[i] for i in idx]
         cap = _bucket_cap(segs, query)
-        scan, keep = N.make_scan(query, Q, segments=segs)
+        scan, keep = N.make_scan(query, Q, segments=segs, cancel=cancel)
         n = len(segs)
         nb = np.zeros(n, dtype=np.int32)
         times = np.zeros(n * cap, dtype=np.int64)
@@ -651,6 +653,41 @@ class GroupByPartial:
         return len(self.times)
 
 
+class PinnedPool:
+    """Pinned host memory for result delivery (dg_host_alloc), allocated once and reused: the shim's
+    direct ByteBuffers (the processing pool allocates its buffers once at startup,
+    OffheapBufferGenerator.java:53). Fetches into it go by DMA, no staging copy on the host."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = ctypes.c_void_p()
+        N.check(N.lib().dg_host_alloc(int(nbytes), ctypes.byref(self.ptr)))
+        self.nbytes, self.off = int(nbytes), 0
+
+    def reset(self):
+        self.off = 0
+
+    def take(self, dtype, n: int) -> np.ndarray:
+        dt = np.dtype(dtype)
+        self.off = (self.off + 63) & ~63
+        nb = n * dt.itemsize
+        if self.off + nb > self.nbytes:
+            raise MemoryError(f"pinned pool of {self.nbytes} bytes: {self.off + nb} needed")
+        buf = (ctypes.c_char * nb).from_address(self.ptr.value + self.off)
+        self.off += nb
+        return np.frombuffer(buf, dtype=dt, count=n)
+
+    def close(self):
+        if self.ptr:
+            N.lib().dg_host_free(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
+            pass
+
+
 class GroupByResult:
     """A dg_result: the merged groups of one dg_groupby_run (or of a dg_merge across devices, whose
     ids index the caller's cluster dictionaries), resident in HBM until fetched."""
@@ -676,17 +713,29 @@ class GroupByResult:
         return [raw[int(offs[i]):int(offs[i + 1])].decode("utf-8") if offs[i + 1] > offs[i] else None
                 for i in range(card)]
 
-    def fetch(self, start: int = 0, count: Optional[int] = None) -> "GroupByPartial":
+    def fetch(self, start: int = 0, count: Optional[int] = None, pool: "Optional[PinnedPool]" = None) -> "GroupByPartial":
+        """Groups [start, start + count) to the host. Under ALL granularity no bucket times cross PCIe
+        (every group's is the universal timestamp, the query interval's start). pool: pinned host
+        memory (dg_host_alloc) the columns land in by DMA; the partial's arrays are views of it."""
         q = self.query
         nd, na = len(q.dimensions), len(q.aggregations)
         count = self.groups - start if count is None else count
-        # (np.empty: the library's staged copy is the first touch of these pages, spread over threads)
-        t = np.empty(max(count, 1), dtype=np.int64)
-        ids = np.empty(max(count * nd, 1), dtype=np.int32)
-        vals = np.empty(max(count * na, 1), dtype=np.uint64)
+        all_gran = q.granularity.is_all and self.time_map is None
+        if pool is not None:
+            pool.reset()
+            t = None if all_gran else pool.take(np.int64, max(count, 1))
+            ids = pool.take(np.int32, max(count * nd, 1))
+            vals = pool.take(np.uint64, max(count * na, 1))
+        else:
+            # (np.empty: the library's staged copy is the first touch of these pages, spread over threads)
+            t = None if all_gran else np.empty(max(count, 1), dtype=np.int64)
+            ids = np.empty(max(count * nd, 1), dtype=np.int32)
+            vals = np.empty(max(count * na, 1), dtype=np.uint64)
         if count:
-            N.check(N.lib().dg_result_fetch_groups(self.handle, start, count, t.ctypes.data,
+            N.check(N.lib().dg_result_fetch_groups(self.handle, start, count, t.ctypes.data if t is not None else None,
                                                    ids.ctypes.data if nd else None, vals.ctypes.data if na else None))
+        if all_gran:  # GroupByStrategyV2.getUniversalTimestamp (:125-138), one value for every group
+            t = np.broadcast_to(np.int64(q.interval[0]), (count,))
         if self.time_map is not None:
             t[:count] = self.time_map[t[:count]]
         ids = ids[:count * nd].reshape(count, nd) if nd else np.zeros((count, 0), np.int32)
@@ -742,15 +791,18 @@ def _beyond_bmp_low(values) -> bool:
 
 
 def groupby_run(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
-                stats: Optional[RunStats] = None, limit_push_down: bool = False) -> GroupByResult:
+                stats: Optional[RunStats] = None, limit_push_down: bool = False,
+                cancel: Optional[ctypes.c_int32] = None) -> GroupByResult:
     """One dg_groupby_run over segments of ONE device: GroupByStrategyV2.mergeRunners over their
     per-segment runners (GroupByMergingQueryRunnerV2.java:170-290), the groups left in HBM. With
     `limit_push_down`, a query that pushes its limit down keeps only its first `limit` groups
-    (GroupByResult.apply_limit_push_down); a result meant for the cross-device exchange stays whole."""
+    (GroupByResult.apply_limit_push_down); a result meant for the cross-device exchange stays whole.
+    cancel: a flag another thread may set (Thread.interrupt): the call then fails DG_ERR_INTERRUPTED;
+    the query context's "timeout" (ms) fails it with DG_ERR_TIMEOUT."""
     if len(_group_by_device(segments)) != 1:
         raise ValueError("groupby_run: segments must share one device")
     nd = len(query.dimensions)
-    scan, keep = N.make_scan(query, Q, segments=segments)
+    scan, keep = N.make_scan(query, Q, segments=segments, cancel=cancel)
     dims = (ctypes.c_char_p * max(nd, 1))(*[d.encode() for d in query.dimensions])
     g = N.dg_groupby()
     g.dimensions = ctypes.cast(dims, ctypes.POINTER(ctypes.c_char_p))
@@ -781,17 +833,32 @@ def groupby_per_device(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
     return out
 
 
-def _per_device_concurrently(groups, fn):
+def _per_device_concurrently(groups, fn, release=None):
     """fn(segment indices of one device) for every device at once, one host thread each, results in
     device order (ChainedExecutionQueryRunner submits every runner to the processing pool; the native
-    calls release the GIL, so the devices' kernels are in flight together)."""
+    calls release the GIL, so the devices' kernels are in flight together). Every future is waited
+    for; if one fails, `release` frees the results of the others before the first error is raised
+    (ChainedExecutionQueryRunner cancels the pending futures the same way, :158-167)."""
     items = list(groups.values())
     if len(items) == 1:
         return [fn(items[0])]
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(max_workers=len(items)) as ex:
         futs = [ex.submit(fn, idx) for idx in items]
-        return [f.result() for f in futs]
+        results, err = [], None
+        for f in futs:
+            try:
+                results.append(f.result())
+            except BaseException as e:  # noqa: BLE001 (re-raised below, after the cleanup)
+                results.append(None)
+                err = err or e
+    if err is not None:
+        if release is not None:
+            for r in results:
+                if r is not None:
+                    release(r)
+        raise err
+    return results
 
 
 def groupby_merge_devices(segments: Sequence[GpuSegment], query: Q.GroupByQuery, stats: Optional[RunStats] = None,
@@ -806,7 +873,7 @@ def groupby_merge_devices(segments: Sequence[GpuSegment], query: Q.GroupByQuery,
     try:
         def one(idx):
             return groupby_run([segments[i] for i in idx], query, stats)
-        parts = _per_device_concurrently(groups, one)
+        parts = _per_device_concurrently(groups, one, release=lambda r: r.release())
         ctxs = [segments[idx[0]].context for idx in groups.values()] if targets is None else list(targets)
         outs = (ctypes.c_void_p * len(ctxs))()
         hp = (ctypes.c_void_p * len(parts))(*[p.handle.value for p in parts])

@@ -222,3 +222,91 @@ def test_fused_decode_aggregate(Q, O, R, cfg5, shape, monkeypatch):
         assert nf > (0.97 if shape == "all" else 0.5) * 4 * NSEG * (ROWS // 8192), nf
     assert_results(q, a, b)
     assert_results(q, a, O.run(q, o))
+
+
+@pytest.fixture(scope="module")
+def signed_seg(tmp_path_factory, W):
+    """One 600 k-row LZ4 segment of signed values: sequential longs running from -300 000 upwards (value
+    runs through the sign change: run blocks), wide random longs, and doubles of both signs."""
+    rng = np.random.default_rng(77)
+    n = 600_000
+    ts = np.arange(n, dtype=np.int64) * 3  # 30 minutes of rows
+    spec = W.SegmentSpec(timestamps=ts, interval=(0, 3 * n),
+                         dims={"d": W.encode_int_strings(rng.integers(0, 50, n))},
+                         metrics={"seq": ("long", np.arange(n, dtype=np.int64) - 300_000),
+                                  "wide": ("long", rng.integers(-(1 << 62), 1 << 62, n)),
+                                  "dbl": ("double", rng.normal(-250.0, 1000.0, n))})
+    p = W.write_segment(str(tmp_path_factory.mktemp("signed") / "seg"), spec)
+    S = importlib.import_module("incubator-druid_amd.segment")
+    import oracle as O
+    return S.GpuSegment(p), O.OracleSegment(p)
+
+
+@pytest.mark.parametrize("route", ["run", "no_run"])
+def test_fused_folds_signed_and_cross_type(Q, O, R, signed_seg, route, monkeypatch):
+    """Every fold of a fused decode over negative values: longMin / longMax / longSum (native int64),
+    doubleSum, and the generic folds (doubleMax, doubleMin, longSum over a double column = Java's
+    (long) cast, doubleSum over a long column), on the run decoder and on the general decoder
+    (DG_NO_RUN_DECODE=1), against the unfused path and the oracle."""
+    g, o = signed_seg
+    if route == "no_run":
+        monkeypatch.setenv("DG_NO_RUN_DECODE", "1")
+    aggs = [Q.count("rows"), Q.long_min("smin", "seq"), Q.long_max("smax", "seq"), Q.long_sum("ssum", "seq"),
+            Q.long_min("wmin", "wide"), Q.long_max("wmax", "wide"), Q.long_sum("wsum", "wide"),
+            Q.double_sum("dsum", "dbl"), Q.double_max("dmax", "dbl"), Q.double_min("dmin", "dbl"),
+            Q.long_sum("lsum_of_dbl", "dbl"), Q.double_sum("dsum_of_seq", "seq")]
+    for gran in ("all", "minute"):
+        q = Q.TimeseriesQuery(intervals=["1970-01-01/2020-01-01"], granularity=gran, aggregations=aggs)
+        runs = {}
+        for mode in ("fused", "plain"):
+            if mode == "plain":
+                monkeypatch.setenv("DG_NO_FUSE", "1")
+            else:
+                monkeypatch.delenv("DG_NO_FUSE", raising=False)
+            stats = R.RunStats()
+            runs[mode] = (R.run_query(q, [g], stats), stats.total("lz4_fused_blocks"))
+        monkeypatch.delenv("DG_NO_FUSE", raising=False)
+        (a, nf), (b, n0) = runs["fused"], runs["plain"]
+        assert n0 == 0 and nf > 0, (nf, n0)
+        assert_results(q, a, b)
+        assert_results(q, a, O.run(q, [o]))
+
+
+def test_time_skip_needs_no_row_order_inside_blocks(Q, R, W, tmp_path, monkeypatch):
+    """The uniform-block skip bounds a __time block by its smallest and largest row time (recorded at
+    attach), not by its neighbours' first rows, so rows shuffled inside their blocks still land in
+    their own hour: the same per-hour counts and sums as decoding every block (DG_NO_TIME_SKIP=1)
+    and as bucketing every row on the host."""
+    rng = np.random.default_rng(5)
+    nblk, per = 48, 8192
+    span = 1_500_000  # ms per block: most blocks inside one hour, some across an hour boundary
+    ts = np.concatenate([rng.permutation(np.arange(k * span, (k + 1) * span, span // per)[:per]) for k in range(nblk)])
+    # the segment's first and last rows stay its min and max time (StorageAdapter.getMinTime / getMaxTime)
+    i0, i1 = int(np.argmin(ts[:per])), len(ts) - per + int(np.argmax(ts[-per:]))
+    ts[[0, i0]] = ts[[i0, 0]]
+    ts[[-1, i1]] = ts[[i1, -1]]
+    vals = rng.integers(-1000, 1000, len(ts))
+    spec = W.SegmentSpec(timestamps=ts.astype(np.int64), interval=(0, nblk * span),
+                         dims={"d": W.encode_int_strings(rng.integers(0, 5, len(ts)))},
+                         metrics={"v": ("long", vals.astype(np.int64))})
+    S = importlib.import_module("incubator-druid_amd.segment")
+    seg = S.GpuSegment(W.write_segment(str(tmp_path / "seg"), spec))
+    q = Q.TimeseriesQuery(intervals=["1970-01-01/2020-01-01"], granularity="hour",
+                          aggregations=[Q.count("rows"), Q.long_sum("s", "v")])
+    runs = {}
+    for mode in ("skip", "decode"):
+        if mode == "decode":
+            monkeypatch.setenv("DG_NO_TIME_SKIP", "1")
+        else:
+            monkeypatch.delenv("DG_NO_TIME_SKIP", raising=False)
+        stats = R.RunStats()
+        runs[mode] = (R.run_query(q, [seg], stats), sum(c["bytes_read"] for c in stats.calls))
+    monkeypatch.delenv("DG_NO_TIME_SKIP", raising=False)
+    (a, bytes_skip), (b, bytes_all) = runs["skip"], runs["decode"]
+    assert bytes_skip < bytes_all, (bytes_skip, bytes_all)
+    assert_results(q, a, b)
+    hour = ts // 3_600_000
+    exp = {int(h) * 3_600_000: (int((hour == h).sum()), int(vals[hour == h].sum())) for h in np.unique(hour)}
+    got = {r.timestamp: (r.value["rows"], r.value["s"]) for r in a if r.value["rows"]}
+    assert got == exp
+    seg.close()

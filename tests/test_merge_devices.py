@@ -159,7 +159,8 @@ def test_merge_devices_granularity_and_filters(Q, O, two_contexts):
 @pytest.mark.gpu
 def test_merge_devices_runs_concurrently_and_spreads_targets(Q, O, two_contexts):
     """The in-process mergeRunners issues every context's dg_groupby_run at once (their host call spans
-    overlap: both were in flight on the GPU together) and by default every participating context owns a
+    overlap: the two calls were issued concurrently, each from its own thread; whether their kernels
+    overlapped on the device is not measured here) and by default every participating context owns a
     key range of the merged result (nothing funnels into the first device)."""
     R = importlib.import_module("incubator-druid_amd.runners")
     (ca, cb), g, o = two_contexts
