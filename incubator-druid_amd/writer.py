@@ -512,16 +512,18 @@ class SegmentSpec:
 
 def write_segment(out_dir: str, spec: SegmentSpec, bitmap: str = "concise", compression: str = "lz4",
                   dim_compression: Optional[str] = None, lz4_mode: str = "hc", long_encoding: str = "longs",
-                  id_bytes: Optional[int] = None, legacy_multi_value: bool = False) -> str:
+                  id_bytes: Optional[int] = None, legacy_multi_value: bool = False, check_sorted: bool = True) -> str:
     """Write a v9 segment directory. Rows must already be in segment order (time-sorted).
     long_encoding: IndexSpec.longEncoding, "longs" (default) or "auto" (DELTA / TABLE / LONGS per column,
     __time included: IndexMergerV9 serializes it with the same long encoding).
     id_bytes: width of single-value dictionary ids (default: numBytes for the cardinality).
-    legacy_multi_value: compressed multi-value dimensions in the pre-V3 CompressedVSizeColumnarMultiInts form."""
+    legacy_multi_value: compressed multi-value dimensions in the pre-V3 CompressedVSizeColumnarMultiInts form.
+    check_sorted=False: write rows out of time order (robustness tests of the engine only; IndexMergerV9
+    never writes such a segment)."""
     os.makedirs(out_dir, exist_ok=True)
     n = len(spec.timestamps)
     ts = np.asarray(spec.timestamps, dtype=np.int64)
-    if n and np.any(np.diff(ts) < 0):
+    if check_sorted and n and np.any(np.diff(ts) < 0):
         raise ValueError("segment rows must be sorted by __time")
     dim_comp = dim_compression or ("uncompressed" if compression == "none" else
                                    "lzf" if compression == "lzf_v1" else compression)
