@@ -1224,7 +1224,7 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
 // long column, doubleSum of a double column), so the decoded block needs no second pass (the keygen
 // leaves that column alone). Returns false when the column is not of that form (the caller then
 // takes the ordinary view).
-static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int pw, int a, uint32_t row_base,
+static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int pw, int64_t ps, int a, uint32_t row_base,
                          DecodeBatch* db) {
   const BlockColumn& b = c->data;
   const bool ident = (agg_kind == DG_AGG_LONG_SUM && c->type == DG_COL_LONG) ||
@@ -1236,8 +1236,9 @@ static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int p
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (rows <= 0) continue;
     const int64_t r0 = (int64_t)row_base + (int64_t)k * b.size_per;
-    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(payload + (size_t)r0 * pw + a), (int32_t)(rows * 8), run_ok);
-    j.vstride = pw * 8;
+    uint64_t* dst = ps ? payload + (size_t)a * ps + r0 : payload + (size_t)r0 * pw + a;
+    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(dst), (int32_t)(rows * 8), run_ok);
+    j.vstride = ps ? 8 : pw * 8;
     db->jobs.push_back(j);
   }
   return true;
@@ -1979,6 +1980,8 @@ static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bi
     if (!sb->keys[k] || (!packed && !sb->refs[k])) return set_error(DG_ERR_OOM, "sort buffers of %lld rows", (long long)cap);
   }
   sb->pw = pw;
+  const char* soa = getenv("DG_PAYLOAD_SOA");  // (A/B: payload columns instead of records)
+  sb->pstride = (soa && *soa && *soa != '0') ? (int64_t)c : 0;
   if (pw > 0) {
     sb->payload = dev_take<uint64_t>(cs, c * (size_t)pw);
     if (!sb->payload) return set_error(DG_ERR_OOM, "payload of %lld rows", (long long)cap);
@@ -3534,7 +3537,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     for (int a = 0; a < na; ++a) {
       const Column* ac = q->aggs[a].field ? seg->find(q->aggs[a].field) : nullptr;
       if (!any_multi && ac && !(q->aggs[a].filter && q->aggs[a].n_filter > 0) &&
-          payload_view(ac, q->aggs[a].kind, sb.payload, na, a, row_base[i], &db_side)) {
+          payload_view(ac, q->aggs[a].kind, sb.payload, na, sb.pstride, a, row_base[i], &db_side)) {
         j.inplace |= 1u << a;
         j.vals[a].kind = VIEW_ABSENT;
         continue;
@@ -3590,7 +3593,11 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   hipEventRecord(ctx->ev[3], st);
   launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi);
   hipEventRecord(ctx->ev[5], st);
-  launch_radix_sort(&sb, key_bits, st);
+  // DG_GB_DENSE=1 (same-box A/B): a direct-indexed table over the packed key space instead of sort +
+  // reduce, for keys of at most 26 bits without floatSum (its row-order recurrence needs the sort)
+  const char* dn = getenv("DG_GB_DENSE");
+  const bool dense = dn && *dn && *dn != '0' && !any_multi && !sb.refs[0] && key_bits <= 26 && !has_float_sum(plan);
+  if (!dense) launch_radix_sort(&sb, key_bits, st);
   hipEventRecord(ctx->ev[6], st);
   DG_CHECK_INTERRUPT(intr);
   // the result is laid out for the sort's capacity (>= the groups): the reduce counts the groups itself
@@ -3612,7 +3619,16 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   res->cap = cap;
   if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "groupBy result of %lld records", (long long)cap);
   bool reduce_timed = false;
-  {
+  if (dense) {
+    const int64_t tsize = (int64_t)1 << std::max(key_bits, 1);
+    uint64_t* table = dev_take<uint64_t>(cs, (size_t)tsize * rec);
+    uint32_t* tcnt = dev_take<uint32_t>(cs, (size_t)((tsize + 1023) / 1024) + 2);
+    if (!table || !tcnt) return set_error(DG_ERR_OOM, "dense groupBy table of %lld slots", (long long)tsize);
+    if (side) DG_HIP(hipStreamWaitEvent(st, ctx->side_ev[2], 0));  // the payload is decoded
+    hipEventRecord(ctx->ev[7], st);
+    reduce_timed = true;
+    launch_gb_dense(&sb, plan, table, tsize, res->keys, res->slots, cap, tcnt, st);
+  } else {
     // run heads are only needed by the floatSum row-order pass
     uint32_t* head_pos = has_float_sum(plan) ? dev_take<uint32_t>(cs, (size_t)cap + 16) : nullptr;
     const size_t nt = (size_t)sb.ntiles_sort;  // one carry / open group per tile
