@@ -498,8 +498,8 @@ static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_me
 }
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
 static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st);
-static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr);
-static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof);
+static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof = nullptr, bool overlap = false);
+static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof, bool overlap = false);
 
 // ------------------------------------------------------------------------------------------------
 // numeric post-filters: Java's parsing of the filter's strings (host side, once per call)
@@ -1224,7 +1224,7 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
 // long column, doubleSum of a double column), so the decoded block needs no second pass (the keygen
 // leaves that column alone). Returns false when the column is not of that form (the caller then
 // takes the ordinary view).
-static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int pw, int64_t ps, int a, uint32_t row_base,
+static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int pw, int a, uint32_t row_base,
                          DecodeBatch* db) {
   const BlockColumn& b = c->data;
   const bool ident = (agg_kind == DG_AGG_LONG_SUM && c->type == DG_COL_LONG) ||
@@ -1236,9 +1236,8 @@ static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int p
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (rows <= 0) continue;
     const int64_t r0 = (int64_t)row_base + (int64_t)k * b.size_per;
-    uint64_t* dst = ps ? payload + (size_t)a * ps + r0 : payload + (size_t)r0 * pw + a;
-    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(dst), (int32_t)(rows * 8), run_ok);
-    j.vstride = ps ? 8 : pw * 8;
+    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(payload + (size_t)r0 * pw + a), (int32_t)(rows * 8), run_ok);
+    j.vstride = pw * 8;
     db->jobs.push_back(j);
   }
   return true;
@@ -1286,13 +1285,15 @@ static int run_mv_checks(CallScratch* cs, DecodeBatch* db, hipStream_t st) {
   return finish_call(cs, st);
 }
 
-static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof) {
-  int rcl = run_decodes_only(cs, db, st, d_prof);
+static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof, bool overlap) {
+  int rcl = run_decodes_only(cs, db, st, d_prof, overlap);
   if (rcl) return rcl;
   return run_mv_checks(cs, db, st);
 }
 
-static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof) {
+// overlap (a call whose side stream is otherwise idle: timeseries, topN): the short decoders (run, light)
+// go to the side stream beside the general decoder's launch on `st`, joined before `st` continues
+static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof, bool overlap) {
   int rcl = run_lzf(cs, db, st);
   if (rcl) return rcl;
   if (db->jobs.empty()) return run_expands(cs, db, st);
@@ -1321,8 +1322,17 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   if (!h || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
   memcpy(h, J.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
-  launch_lz4_run(d, nr, run_lds, d_err, st);
-  launch_lz4_light(d + nh, n - nh, d_err, st, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
+  Context* ctx = cs->ctx;
+  const bool ovl = overlap && ctx && ctx->side && st == ctx->stream && nh > nr && (nr > 0 || n > nh) && !d_prof;
+  hipStream_t ss = st;
+  if (ovl) {
+    hipEventRecord(ctx->ovl_ev[0], st);
+    DG_HIP(hipStreamWaitEvent(ctx->side, ctx->ovl_ev[0], 0));
+    ss = ctx->side;
+  }
+  launch_lz4_run(d, nr, run_lds, d_err, ss);
+  launch_lz4_light(d + nh, n - nh, d_err, ss, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
+  if (ovl) hipEventRecord(ctx->ovl_ev[1], ss);
   const int ng = nh - nr;  // general-decoder blocks
   for (int i = nr; i < nh; ++i) db->gen_bytes += J[i].src_len;
   db->gen_blocks += ng;
@@ -1331,6 +1341,7 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   launch_lz4_decode(d + nr, nn - nr, 0, d_err, st, d_prof ? d_prof + (size_t)nr * kLz4ProfWords : nullptr);
   launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
   if (db->gen_a && ng) hipEventRecord(db->gen_b, st);
+  if (ovl) DG_HIP(hipStreamWaitEvent(st, ctx->ovl_ev[1], 0));
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
 
@@ -1632,6 +1643,7 @@ int dg_context_create(int device, dg_context** out) {
   if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) ctx->side = nullptr;
   for (auto& e : ctx->side_ev) hipEventCreate(&e);
   for (auto& e : ctx->gen_ev) hipEventCreate(&e);
+  for (auto& e : ctx->ovl_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   *out = reinterpret_cast<dg_context*>(ctx);
   return DG_OK;
 }
@@ -1648,6 +1660,7 @@ void dg_context_release(dg_context* c) {
   for (auto& e : ctx->ev) hipEventDestroy(e);
   for (auto& e : ctx->side_ev) hipEventDestroy(e);
   for (auto& e : ctx->gen_ev) hipEventDestroy(e);
+  for (auto& e : ctx->ovl_ev) hipEventDestroy(e);
   for (auto& b : ctx->free_blocks) hipFree(b.first);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1980,8 +1993,6 @@ static int sort_bufs(CallScratch* cs, int64_t cap, int ntiles_keygen, int key_bi
     if (!sb->keys[k] || (!packed && !sb->refs[k])) return set_error(DG_ERR_OOM, "sort buffers of %lld rows", (long long)cap);
   }
   sb->pw = pw;
-  const char* soa = getenv("DG_PAYLOAD_SOA");  // (A/B: payload columns instead of records)
-  sb->pstride = (soa && *soa && *soa != '0') ? (int64_t)c : 0;
   if (pw > 0) {
     sb->payload = dev_take<uint64_t>(cs, c * (size_t)pw);
     if (!sb->payload) return set_error(DG_ERR_OOM, "payload of %lld rows", (long long)cap);
@@ -2233,6 +2244,7 @@ int dg_filter_bitmap(dg_segment* s, const dg_filter* filter, int32_t n_filter, u
 int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int32_t bucket_cap, int32_t* out_nb,
                       int64_t* out_time, int64_t* out_rows, uint64_t* out_values, dg_metrics* metrics) {
   auto t0 = std::chrono::steady_clock::now();
+  HostTrace ht;
   Context* ctx;
   int rc = check_segments(segs, n, &ctx);
   if (rc) return rc;
@@ -2304,15 +2316,17 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     tiles_rows[i] = seg->nrows;
   }
   DG_CHECK_INTERRUPT(intr);
+  ht.mark("planned");
   // init accumulators (before the decoders: fused blocks combine into them)
   SlotInit init{};
   for (int a = 0; a < na; ++a) init.v[1 + a] = identity_host(plan.kind[a]);
   for (int i = 0; i < n; ++i)
     if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, init, st);
   hipEventRecord(ctx->ev[1], st);
-  rc = run_decodes(cs, &db, st);
+  rc = run_decodes(cs, &db, st, nullptr, true);
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
+  ht.mark("decode_launched");
   m.bytes_read = db.bytes;
   DG_CHECK_INTERRUPT(intr);
   std::vector<int32_t> begin;
@@ -2369,7 +2383,9 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     h_out[i] = host_take<uint64_t>(cs, (size_t)cur[i].nbuckets * rec);
     DG_HIP(hipMemcpyAsync(h_out[i], jobs[i].out, (size_t)cur[i].nbuckets * rec * 8, hipMemcpyDeviceToHost, st));
   }
+  ht.mark("agg_launched");
   rc = finish_call(cs, st);
+  ht.mark("synced");
   if (rc) return rc;
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
@@ -2523,7 +2539,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   DG_CHECK_INTERRUPT(intr);
   hipEventRecord(ctx->ev[1], st);
   ht.mark("planned");
-  rc = run_decodes(cs, &db, st);
+  rc = run_decodes(cs, &db, st, nullptr, true);
   ht.mark("decode_launched");
   if (rc) return rc;
   hipEventRecord(ctx->ev[2], st);
@@ -3537,7 +3553,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     for (int a = 0; a < na; ++a) {
       const Column* ac = q->aggs[a].field ? seg->find(q->aggs[a].field) : nullptr;
       if (!any_multi && ac && !(q->aggs[a].filter && q->aggs[a].n_filter > 0) &&
-          payload_view(ac, q->aggs[a].kind, sb.payload, na, sb.pstride, a, row_base[i], &db_side)) {
+          payload_view(ac, q->aggs[a].kind, sb.payload, na, a, row_base[i], &db_side)) {
         j.inplace |= 1u << a;
         j.vals[a].kind = VIEW_ABSENT;
         continue;
@@ -3593,11 +3609,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   hipEventRecord(ctx->ev[3], st);
   launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi);
   hipEventRecord(ctx->ev[5], st);
-  // DG_GB_DENSE=1 (same-box A/B): a direct-indexed table over the packed key space instead of sort +
-  // reduce, for keys of at most 26 bits without floatSum (its row-order recurrence needs the sort)
-  const char* dn = getenv("DG_GB_DENSE");
-  const bool dense = dn && *dn && *dn != '0' && !any_multi && !sb.refs[0] && key_bits <= 26 && !has_float_sum(plan);
-  if (!dense) launch_radix_sort(&sb, key_bits, st);
+  launch_radix_sort(&sb, key_bits, st);
   hipEventRecord(ctx->ev[6], st);
   DG_CHECK_INTERRUPT(intr);
   // the result is laid out for the sort's capacity (>= the groups): the reduce counts the groups itself
@@ -3619,16 +3631,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   res->cap = cap;
   if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "groupBy result of %lld records", (long long)cap);
   bool reduce_timed = false;
-  if (dense) {
-    const int64_t tsize = (int64_t)1 << std::max(key_bits, 1);
-    uint64_t* table = dev_take<uint64_t>(cs, (size_t)tsize * rec);
-    uint32_t* tcnt = dev_take<uint32_t>(cs, (size_t)((tsize + 1023) / 1024) + 2);
-    if (!table || !tcnt) return set_error(DG_ERR_OOM, "dense groupBy table of %lld slots", (long long)tsize);
-    if (side) DG_HIP(hipStreamWaitEvent(st, ctx->side_ev[2], 0));  // the payload is decoded
-    hipEventRecord(ctx->ev[7], st);
-    reduce_timed = true;
-    launch_gb_dense(&sb, plan, table, tsize, res->keys, res->slots, cap, tcnt, st);
-  } else {
+  {
     // run heads are only needed by the floatSum row-order pass
     uint32_t* head_pos = has_float_sum(plan) ? dev_take<uint32_t>(cs, (size_t)cap + 16) : nullptr;
     const size_t nt = (size_t)sb.ntiles_sort;  // one carry / open group per tile

@@ -225,7 +225,6 @@ struct SortBufs {
   int row_refs;           // element reference = the row's index over the call (one element per row,
                           // payload columns may be decoded in place); else the element index
   int pw;
-  int64_t pstride;        // 0: payload records [ref][pw]; > 0: payload columns [a][pstride] (DG_PAYLOAD_SOA, A/B)
   int cur;                // which of the ping-pong buffers holds the result
   uint32_t* tile_cnt;     // keygen tiles: selected rows, then their offsets
   uint32_t* n;            // [0] selected rows, [1] groups
@@ -363,6 +362,9 @@ struct Context {
   // the general LZ4 decoder's own span on each stream: [0, 1] main, [2, 3] side (its roofline
   // figures, dg_metrics)
   hipEvent_t gen_ev[4] = {};
+  // a small call's short decoders (run, light) on the side stream beside the general decoder:
+  // [0] their jobs are staged, [1] they are done (no timing)
+  hipEvent_t ovl_ev[2] = {};
   // dg_context_set_limit(DG_LIMIT_GROUP_ELEMENTS): most sort elements one groupBy call may build
   uint64_t max_elements = ~0ull;
   std::vector<std::shared_ptr<MergedDict>> dict_cache;  // most recent last
@@ -572,12 +574,6 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
 // (out_slots == null): into the job's fs_out table.
 void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, AggPlan plan, int agg,
                       const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s, int desc = 0);
-// dense-key groupBy (A/B, DG_GB_DENSE=1): table [1 + naggs][tsize] over the packed key space, one atomic
-// per (selected row, slot) from the keygen's row-order elements, then the non-empty slots compacted in
-// key order into out_keys / out_slots (SoA, cap) and the group count into sb->n[1]. tile_cnt:
-// (tsize + 1023) / 1024 + 1 words.
-void launch_gb_dense(SortBufs* sb, AggPlan plan, uint64_t* table, int64_t tsize, uint64_t* out_keys, uint64_t* out_slots,
-                     int64_t cap, uint32_t* tile_cnt, hipStream_t s);
 // device slot encoding -> ABI encoding (finalize) of the aggregator slots [1 + a][cap] of n_ptr[0] groups
 void launch_slots_finalize(uint64_t* slots, const uint32_t* n_ptr, int64_t cap, AggPlan plan, hipStream_t s);
 // SoA slots [rec][cap] -> AoS records [n][rec]

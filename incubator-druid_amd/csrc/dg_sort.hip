@@ -91,11 +91,10 @@ __global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ a, int
   if (threadIdx.x == 0) *total = carry;
 }
 
-// payload word a of the element with reference i (i = the element index, or in row-ref mode the row's
-// index over the call's segments): records [i][pw], or with ps > 0 columns [a][ps]
-__device__ __forceinline__ size_t pay_at(int pw, int64_t ps, size_t i, int a) {
-  return ps ? (size_t)a * (size_t)ps + i : i * (size_t)pw + (size_t)a;
-}
+// payload word a of the element with reference i ([i][pw] words: i = the element index, or in
+// row-ref mode the row's index over the call's segments). Records, not columns: the reduce gathers one
+// 16-byte record per element (payload columns: two random 8-byte reads, measured slower)
+__device__ __forceinline__ size_t pay_at(int pw, size_t i, int a) { return i * (size_t)pw + (size_t)a; }
 
 // segment of an element index (or row ref): the last job whose base <= it (bases ascend)
 __device__ __forceinline__ int locate_seg(const uint32_t* s_base, int njobs, uint32_t ref) {
@@ -247,7 +246,7 @@ template <bool MULTI>
 __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                    const uint32_t* __restrict__ offs, uint64_t* __restrict__ keys,
                                                    uint32_t* __restrict__ refs, int kshift, AggPlan plan,
-                                                   uint64_t* __restrict__ payload, int pw, int64_t ps, int rowref) {
+                                                   uint64_t* __restrict__ payload, int pw, int rowref) {
   __shared__ uint32_t s_tmp[4];
   const GbJob& j = jobs[tile_job[blockIdx.x]];
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
@@ -264,11 +263,11 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
       keys[idx] = (key << kshift) | ref;
     }
     if (all_inplace) return;
-    if (pw == 2 && !inplace && !ps) {
+    if (pw == 2 && !inplace) {
       *reinterpret_cast<ulonglong2*>(payload + (size_t)ref * 2) = make_ulonglong2(val(0), val(1));
     } else {
       for (int a = 0; a < pw; ++a)
-        if (!((inplace >> a) & 1u)) payload[pay_at(pw, ps, ref, a)] = val(a);
+        if (!((inplace >> a) & 1u)) payload[pay_at(pw, ref, a)] = val(a);
     }
   };
   // every row of the tile selected: no filter, and the interval covers the segment or the tile's
@@ -397,10 +396,10 @@ void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles
   launch_gb_count(d_jobs, d_tile_job, ntiles, sb->tile_cnt, sb->n, multi, s);
   if (multi)
     hipLaunchKernelGGL(k_gb_keygen<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->pstride, 0);
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, 0);
   else
     hipLaunchKernelGGL(k_gb_keygen<false>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->pstride, sb->row_refs);
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->row_refs);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -758,7 +757,7 @@ constexpr int kRSPT = kSortTile / kRT;          // elements per lane
 __device__ __forceinline__ void red_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <bool REFS>
-__global__ __launch_bounds__(kRT, kRedMinW) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw, int64_t ps,
+__global__ __launch_bounds__(kRT, kRedMinW) void k_gb_reduce(const uint64_t* __restrict__ payload, int pw,
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, uint32_t* __restrict__ n_ptr,
                                                    uint64_t* __restrict__ status, uint32_t* __restrict__ tile_ctr,
@@ -822,11 +821,8 @@ __global__ __launch_bounds__(kRT, kRedMinW) void k_gb_reduce(const uint64_t* __r
 #pragma unroll
     for (int c = 0; c < kRSPT; ++c) {
       const bool valid = wbase + c * 64 + lane < tile_n;
-      const uint64_t* pr = payload + (size_t)idx_of[c] * (ps ? 1 : pw);
-      if (ps) {  // payload columns: one read per column
-        xr[c][0] = valid && pw >= 1 ? pr[0] : 0ull;
-        xr[c][1] = valid && pw >= 2 ? pr[ps] : 0ull;
-      } else if (pw == 2 && valid) {
+      const uint64_t* pr = payload + (size_t)idx_of[c] * pw;
+      if (pw == 2 && valid) {
         const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(pr);  // 16-byte aligned: pw == 2
         xr[c][0] = w.x;
         xr[c][1] = w.y;
@@ -925,7 +921,7 @@ __global__ __launch_bounds__(kRT, kRedMinW) void k_gb_reduce(const uint64_t* __r
       if (!valid) xv = ident;
       else if (a < 0) xv = 1ull;
       else if (pw <= kRegSlots) xv = a == 0 ? xr[c][0] : xr[c][1];
-      else xv = payload[pay_at(pw, ps, idx_of[c], a)];
+      else xv = payload[pay_at(pw, idx_of[c], a)];
       uint64_t v = xv;
       // a chunk of singleton groups (every element a run head and end: ~3 in 4 chunks at one group per
       // row) needs no scan; otherwise the segmented scan with the open run carried in
@@ -1001,11 +997,11 @@ void launch_gb_reduce(SortBufs* sb, AggPlan plan, uint64_t* out_keys, uint64_t* 
   if (!zero_async(ctr, sizeof(uint32_t), s)) return;
   if (!zero_async(sb->n + 1, sizeof(uint32_t), s)) return;
   if (refs)
-    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->pstride, sb->keys[sb->cur], refs,
+    hipLaunchKernelGGL(k_gb_reduce<true>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->lb_status, ctr, plan, out_keys, out_slots, cap, head_pos,
                        carry_g, carry_slots, open_g);
   else
-    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->pstride, sb->keys[sb->cur], refs,
+    hipLaunchKernelGGL(k_gb_reduce<false>, dim3(nt), dim3(kRT), 0, s, sb->payload, sb->pw, sb->keys[sb->cur], refs,
                        sb->ref_bits, sb->n, sb->lb_status, ctr, plan, out_keys, out_slots, cap, head_pos,
                        carry_g, carry_slots, open_g);
   const int64_t nw = (int64_t)nt * kRedWaves;  // carry / open slots: one per wave share of a tile
@@ -1035,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
                                                    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ refs,
                                                    int kshift, const uint32_t* __restrict__ n_ptr,
                                                    const uint32_t* __restrict__ head_pos, const uint64_t* __restrict__ payload,
-                                                   int pw, int64_t ps, int rowref, int agg, uint64_t* __restrict__ out_slots, int64_t cap,
+                                                   int pw, int rowref, int agg, uint64_t* __restrict__ out_slots, int64_t cap,
                                                    int rec, int desc) {
   __shared__ uint32_t s_base[kMaxCallSegs];
   const uint32_t n = n_ptr[0], ng = n_ptr[1];
@@ -1063,7 +1059,7 @@ __global__ __launch_bounds__(256) void k_fsum_runs(const GbJob* __restrict__ job
       }
       // the row's float input (identity 0.0f for a row its FilteredAggregator rejects: x + 0.0f == x
       // for every partial sum, which starts at +0.0f)
-      sum = sum + (float)__longlong_as_double((long long)payload[pay_at(pw, ps, idx, agg)]);
+      sum = sum + (float)__longlong_as_double((long long)payload[pay_at(pw, idx, agg)]);
     }
     if (cur >= 0) total = first ? sum : total + sum;
     if (out_slots) {  // groupBy: the final ABI value
@@ -1082,103 +1078,8 @@ void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, 
                       const uint32_t* head_pos, uint64_t* out_slots, int64_t cap, hipStream_t s, int desc) {
   const int64_t blocks = std::min<int64_t>(8192, std::max<int64_t>(1, (sb->cap + 255) / 256));
   hipLaunchKernelGGL(k_fsum_runs, dim3((unsigned)blocks), dim3(256), 0, s, d_jobs, njobs, sb->tile_cnt, ntiles,
-                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, sb->payload, sb->pw, sb->pstride, sb->row_refs, agg,
+                     sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, sb->n, head_pos, sb->payload, sb->pw, sb->row_refs, agg,
                      out_slots, cap, plan.n + 1, desc);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Dense-key groupBy (same-box A/B against the sort path, DG_GB_DENSE=1; GroupByQueryEngineV2's array
-// aggregation, GroupByQueryEngineV2.java:189-233, over the whole packed key space): one table slot per
-// possible key, [1 + naggs][tsize] in the device slot encoding; every selected row adds itself with one
-// agent-scope atomic per slot (rows, then each aggregator's input from the payload), then the
-// non-empty slots are compacted in key order into the result (keys + slot-major ABI values).
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gb_dense_acc(const uint64_t* __restrict__ elems, const uint32_t* __restrict__ n_ptr,
-                                                      int ref_bits, const uint64_t* __restrict__ payload, int pw, int64_t ps,
-                                                      AggPlan plan, uint64_t* __restrict__ table, int64_t tsize) {
-  const uint32_t n = n_ptr[0];
-  const uint64_t rmask = (1ull << ref_bits) - 1;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < (int64_t)n; i += (int64_t)gridDim.x * 256) {
-    const uint64_t e = elems[i];
-    const uint64_t key = e >> ref_bits, ref = e & rmask;
-    if ((int64_t)key >= tsize) continue;  // (cannot happen: the table spans the key bits)
-    atomicAdd(reinterpret_cast<unsigned long long*>(table + key), 1ull);
-    for (int a = 0; a < plan.n; ++a) atomic_op(plan.op[a], table + (size_t)(1 + a) * tsize + key, payload[pay_at(pw, ps, ref, a)]);
-  }
-}
-
-// non-empty slots per 1024-slot tile
-__global__ __launch_bounds__(256) void k_gb_dense_count(const uint64_t* __restrict__ rows, int64_t tsize, uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t s_c;
-  if (threadIdx.x == 0) s_c = 0;
-  __syncthreads();
-  const int64_t t0 = (int64_t)blockIdx.x * 1024;
-  uint32_t c = 0;
-  for (int k = 0; k < 4; ++k) {
-    const int64_t i = t0 + k * 256 + threadIdx.x;
-    c += i < tsize && rows[i] != 0;
-  }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0) atomicAdd(&s_c, c);
-  __syncthreads();
-  if (threadIdx.x == 0) cnt[blockIdx.x] = s_c;
-}
-
-// tile t's non-empty slots, in key order, at groups offs[t] ..; total groups -> n_ptr[1]
-__global__ __launch_bounds__(256) void k_gb_dense_emit(const uint64_t* __restrict__ table, int64_t tsize,
-                                                       const uint32_t* __restrict__ offs, AggPlan plan,
-                                                       uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_slots,
-                                                       int64_t cap, uint32_t* __restrict__ n_ptr, int ntiles,
-                                                       const uint32_t* __restrict__ total) {
-  __shared__ uint32_t s_w[4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t t0 = (int64_t)blockIdx.x * 1024;
-  uint32_t g = offs[blockIdx.x];
-  for (int k = 0; k < 4; ++k) {
-    const int64_t i = t0 + k * 256 + threadIdx.x;
-    const bool live = i < tsize && table[i] != 0;
-    const uint64_t bal = __ballot(live);
-    if (lane == 0) s_w[wave] = (uint32_t)__popcll(bal);
-    __syncthreads();
-    uint32_t before = 0, all = 0;
-    for (int w = 0; w < 4; ++w) {
-      before += w < wave ? s_w[w] : 0u;
-      all += s_w[w];
-    }
-    if (live) {
-      const uint32_t at = g + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-      out_keys[at] = (uint64_t)i;
-      out_slots[at] = table[i];
-      for (int a = 0; a < plan.n; ++a)
-        out_slots[(size_t)(1 + a) * cap + at] = finalize_dev(plan.kind[a], table[(size_t)(1 + a) * tsize + i]);
-    }
-    g += all;
-    __syncthreads();
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) n_ptr[1] = *total;
-}
-
-// the table's identities: rows 0, every aggregator slot its op's identity (device slot encoding)
-__global__ __launch_bounds__(256) void k_gb_dense_init(uint64_t* __restrict__ table, int64_t tsize, AggPlan plan) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < tsize; i += (int64_t)gridDim.x * 256) {
-    table[i] = 0;
-    for (int a = 0; a < plan.n; ++a) table[(size_t)(1 + a) * tsize + i] = identity_of(plan.op[a], plan.kind[a]);
-  }
-}
-
-void launch_gb_dense(SortBufs* sb, AggPlan plan, uint64_t* table, int64_t tsize, uint64_t* out_keys, uint64_t* out_slots,
-                     int64_t cap, uint32_t* tile_cnt, hipStream_t s) {
-  hipLaunchKernelGGL(k_gb_dense_init, dim3((unsigned)std::min<int64_t>(16384, (tsize + 255) / 256)), dim3(256), 0, s, table,
-                     tsize, plan);
-  const int64_t blocks = std::min<int64_t>(16384, std::max<int64_t>(1, (sb->cap + 255) / 256));
-  hipLaunchKernelGGL(k_gb_dense_acc, dim3((unsigned)blocks), dim3(256), 0, s, sb->keys[sb->cur], sb->n, sb->ref_bits,
-                     sb->payload, sb->pw, sb->pstride, plan, table, tsize);
-  const int nt = (int)((tsize + 1023) / 1024);
-  hipLaunchKernelGGL(k_gb_dense_count, dim3(nt), dim3(256), 0, s, table, tsize, tile_cnt);
-  uint32_t* total = tile_cnt + nt;
-  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, tile_cnt, nt, total);
-  hipLaunchKernelGGL(k_gb_dense_emit, dim3(nt), dim3(256), 0, s, table, tsize, tile_cnt, plan, out_keys, out_slots, cap,
-                     sb->n, nt, total);
 }
 
 // ------------------------------------------------------------------------------------------------

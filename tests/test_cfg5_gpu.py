@@ -311,12 +311,3 @@ def test_time_skip_needs_no_row_order_inside_blocks(Q, R, W, tmp_path, monkeypat
     assert got == exp
     seg.close()
 
-
-@pytest.mark.parametrize("variant", ["DG_GB_DENSE", "DG_PAYLOAD_SOA"])
-def test_groupby_ab_variants_match_oracle(Q, O, R, cfg5, variant, monkeypatch):
-    """The groupBy A/B variants (a dense direct-indexed table instead of sort + reduce; payload columns
-    instead of records) give the oracle's result on configs[4]b's query."""
-    B, g, o = cfg5
-    monkeypatch.setenv(variant, "1")
-    q = B.make_query(Q, "groupby_hourly")
-    assert_results(q, R.run_query(q, g), O.run(q, o))
