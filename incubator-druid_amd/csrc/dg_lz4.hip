@@ -825,61 +825,6 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     for (int w = ((npairs + kStage - 1) / kStage) * (kStage / 32) + tid; w < kLzThreads; w += kLzThreads) s_obits[w] = 0u;
     return any;
   };
-#if DG_LZ_CHASE
-  // Chase resolution: wave wv walks its own 4 KiB of positions in increasing order, kJumpBatch pairs
-  // per lane at a time; every open entry jumps (E[x] += E[x - E[x]], or takes the target's code), written
-  // back at every step so that other chases meet compressed chains, until it holds a literal code. No
-  // barrier: any value read is a valid ancestor distance and every jump moves strictly back. Entries
-  // still open after kChaseSteps (pathological chains) are set in the open-pair bitmap for the rounds.
-  auto chase = [&]() -> bool {
-    constexpr int kChaseSteps = 32;
-    bool any = false;
-#pragma unroll 1
-    for (int b = 0; b < kPairs / kJumpBatch; ++b) {
-      const int j0 = b * kJumpBatch;
-      uint32_t dv[kJumpBatch];
-#pragma unroll
-      for (int k = 0; k < kJumpBatch; ++k) {
-        const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
-        dv[k] = x < kTail ? s_e32[eph(x) >> 1] : 0xFF00FF00u;
-      }
-#pragma unroll 1
-      for (int it = 0; it < kChaseSteps; ++it) {
-        bool open = false;
-#pragma unroll
-        for (int k = 0; k < kJumpBatch; ++k) open |= is_open(dv[k]);
-        if (!__ballot(open)) break;
-        uint32_t ta[kJumpBatch], tb[kJumpBatch];
-#pragma unroll
-        for (int k = 0; k < kJumpBatch; ++k) {
-          const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
-          const uint32_t d0 = dv[k] & 0xFFFF, d1 = dv[k] >> 16;
-          ta[k] = d0 < (uint32_t)kTail ? s_e[eph(x - (int)d0)] : 0xFF00u;
-          tb[k] = d1 < (uint32_t)kTail ? s_e[eph(x + 1 - (int)d1)] : 0xFF00u;
-        }
-#pragma unroll
-        for (int k = 0; k < kJumpBatch; ++k) {
-          const int x = 2 * (wv * (kPairs * 64) + (j0 + k) * 64 + ln);
-          const uint32_t nv = jstep(dv[k] & 0xFFFF, ta[k]) | (jstep(dv[k] >> 16, tb[k]) << 16);
-          if (nv != dv[k]) {
-            dv[k] = nv;
-            s_e32[eph(x) >> 1] = nv;  // (x < kTail whenever an entry changes)
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kJumpBatch; ++k) {
-        const bool op = is_open(dv[k]);
-        any |= op;
-        const uint64_t bal = __ballot(op);  // 64 consecutive pairs: two bitmap words
-        const int w0 = (wv * (kPairs * 64) + (j0 + k) * 64) >> 5;
-        if (ln == 0) s_obits[w0] = (uint32_t)bal;
-        if (ln == 32) s_obits[w0 + 1] = (uint32_t)(bal >> 32);
-      }
-    }
-    return any;
-  };
-#endif
   int jump_rounds = 0;
   if (cls) {
     // carry scan over my 64 positions [tid * 64, tid * 64 + 64). A terminal travels as key
@@ -994,11 +939,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     }
   } else {
     jump_rounds = 1;
-#if DG_LZ_CHASE
-    const bool open1 = __syncthreads_or(chase());
-#else
     const bool open1 = __syncthreads_or(staged());
-#endif
     LZ_STAMP(12);
     LZ_STAMP(13);
     if (open1) {
