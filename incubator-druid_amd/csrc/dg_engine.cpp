@@ -4579,6 +4579,7 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
     if (d > 0 && lz4_run_index(blocks[i], lens[i], d, &rall, &b.run_n[i], &b.run_far[i])) b.run_off[i] = (int64_t)at;
   }
   if (cps.empty()) cps.push_back(0);
+  if (!rall.empty()) rall.resize(rall.size() + 16, 0);  // (k_lz4_run reads 12 bytes at a time)
   CallGuard g(ctx);
   hipStream_t st = ctx->stream;
   if (!b.comp.alloc(host.size()) || !b.cps.alloc(cps.size() * 4)) return set_error(DG_ERR_OOM, "debug decode");

@@ -1384,86 +1384,71 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restri
 // 128 KiB per-byte entry image, one block per CU. Here the attach-time index gives every interval of
 // >= kRunTarget output bytes the 8 bytes before it, so each thread decodes its interval alone: the
 // last 8 output bytes live in one 64-bit register (`win`, oldest byte lowest), a literal or far-copy
-// chunk is shifted in from LDS, a copy from d <= 8 bytes back is the window's last d bytes repeated,
-// and every 8-byte-aligned value is emitted as it completes (a slot store, a payload record, or the
-// fused aggregator's fold). Only the compressed block and the far table are staged in LDS (<= 40 KiB:
-// four workgroups per CU); no barrier after staging.
+// chunk is shifted in from the compressed block (L1/L2: a thread reads its own ~128 contiguous bytes),
+// a copy from d <= 8 bytes back is the window's last d bytes repeated, and every 8-byte-aligned value is
+// complete the moment it is emitted. Values go to the block's image in LDS (64 KiB: two blocks per CU)
+// and leave in coalesced stores after one barrier (a slot, or the payload records' 8-byte field: 64 lanes
+// fill 64 consecutive records), or are folded into the fused aggregator (no image).
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t lds_rd8(const uint32_t* __restrict__ s32, int p) {
-  const int a = p >> 2, sh = (p & 3) << 3;
-  const uint64_t w01 = (uint64_t)s32[a] | ((uint64_t)s32[a + 1] << 32);
-  const uint32_t w2 = s32[a + 2];
+// 8 bytes of global memory at byte offset p of a 4-byte aligned buffer (three aligned dword loads)
+__device__ __forceinline__ uint64_t g_rd8(const uint8_t* __restrict__ base, int p) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(base) + (p >> 2);
+  const int sh = (p & 3) << 3;
+  const uint64_t w01 = (uint64_t)gld4(q) | ((uint64_t)gld4(q + 1) << 32);
+  const uint32_t w2 = gld4(q + 2);
   return sh ? ((w01 >> sh) | ((uint64_t)w2 << (64 - sh))) : w01;
 }
 
-// one 8-byte value v of a run block: its fold (fused), payload record, or slot qword
-// (a slot takes every qword of the block; payload records and folds only the block's rows)
-__device__ __forceinline__ void run_emit(const Lz4Job& job, int v, uint64_t x, uint64_t& acc) {
-  if (!job.red_dst && !job.vstride) {
-    gst8(job.dst + (size_t)v * 8, (uint32_t)x, (uint32_t)(x >> 32));
-    return;
+// fold of one 8-byte value into a fused decode's accumulator (red_code)
+__device__ __forceinline__ void run_fold(const Lz4Job& job, uint64_t x, uint64_t& acc) {
+  switch (job.red_code) {
+    case kRedLongSum: acc += x; break;
+    case kRedDoubleSum:
+      acc = (uint64_t)__double_as_longlong(__longlong_as_double((long long)acc) + __longlong_as_double((long long)x));
+      break;
+    case kRedLongMax: acc = (uint64_t)max((long long)acc, (long long)x); break;
+    case kRedLongMin: acc = (uint64_t)min((long long)acc, (long long)x); break;
+    default: acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, x));
   }
-  if ((v + 1) * 8 > job.expect_len) return;
-  if (job.red_dst) {
-    switch (job.red_code) {
-      case kRedLongSum: acc += x; break;
-      case kRedDoubleSum:
-        acc = (uint64_t)__double_as_longlong(__longlong_as_double((long long)acc) + __longlong_as_double((long long)x));
-        break;
-      case kRedLongMax: acc = (uint64_t)max((long long)acc, (long long)x); break;
-      case kRedLongMin: acc = (uint64_t)min((long long)acc, (long long)x); break;
-      default: acc = combine_op(job.red_op, acc, agg_input_raw(job.red_kind, job.red_vkind, x));
-    }
-    return;
-  }
-  gst8(job.dst + (size_t)v * job.vstride, (uint32_t)x, (uint32_t)(x >> 32));
 }
 
+constexpr int kRunVals = kBlockBytes / 8;
+
 __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
-  extern __shared__ __attribute__((aligned(16))) uint4 s_run[];
+  __shared__ __attribute__((aligned(16))) uint64_t s_val[kRunVals];  // the block's decoded image
   __shared__ uint64_t s_red[kRunThreads / 64];
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x;
   const int n = job.src_len, ni = job.run_n, nfar = job.run_far;
   if (n <= 0 || ni <= 0 || ni > kRunThreads || nfar < 0 || nfar > kRunFarMax ||
-      16 * (((n + 15) >> 4) + ((nfar + 15) >> 4) + 2) > kRunLdsMax ||
-      job.dec_len <= 0 || (job.dec_len & 7) || job.dec_len > kBlockBytes || job.dec_len < job.expect_len) {
+      16 * (((n + 15) >> 4) + ((nfar + 15) >> 4) + 2) > kRunLdsMax || job.dec_len <= 0 || (job.dec_len & 7) ||
+      job.dec_len > kBlockBytes || job.dec_len < job.expect_len) {
     if (tid == 0) atomicOr(err, 1);
     return;
   }
-  // ---- stage the compressed block, then the far table (both 16-byte aligned and padded) ----
-  const int n16 = (n + 15) >> 4, f16 = (nfar + 15) >> 4;
-  const uint8_t* far_g = job.rx + ((14 * ni + 15) & ~15);
-  for (int i = tid; i < n16 + 1 + f16 + 1; i += kRunThreads) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (i < n16) v = gld16(job.src + 16 * (size_t)i);
-    else if (i > n16 && i <= n16 + f16) v = gld16(far_g + 16 * (size_t)(i - n16 - 1));
-    s_run[i] = v;
-  }
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s_run);
-  const uint8_t* s8 = reinterpret_cast<const uint8_t*>(s_run);
-  const int far0 = 16 * (n16 + 1);
-  uint64_t acc = job.red_dst ? red_identity(job) : 0ull;
+  const uint8_t* __restrict__ in = job.src;                          // 16-byte aligned, zero padded
+  const uint8_t* __restrict__ far = job.rx + ((14 * ni + 15) & ~15);  // 16-byte aligned, zero padded
+  const bool fold = job.red_dst != nullptr;
+  uint64_t acc = fold ? red_identity(job) : 0ull;
   bool bad = false;
-  // my interval's index entry (read before the barrier)
-  uint64_t win = 0;
-  uint32_t tf = 0;
-  int o = 0, oend = 0;
   if (tid < ni) {
-    win = (uint64_t)gld4(job.rx + 8 * (size_t)tid) | ((uint64_t)gld4(job.rx + 8 * (size_t)tid + 4) << 32);
-    tf = gld4(job.rx + 8 * (size_t)ni + 4 * (size_t)tid);
+    uint64_t win = (uint64_t)gld4(job.rx + 8 * (size_t)tid) | ((uint64_t)gld4(job.rx + 8 * (size_t)tid + 4) << 32);
+    const uint32_t tf = gld4(job.rx + 8 * (size_t)ni + 4 * (size_t)tid);
     const uint16_t* ost = reinterpret_cast<const uint16_t*>(job.rx + 12 * (size_t)ni);
-    o = ost[tid];
-    oend = tid + 1 < ni ? (int)ost[tid + 1] : job.dec_len;
-  }
-  __syncthreads();
-  if (tid < ni) {
-    int p = (int)(tf & 0x1FFFFu), fp = far0 + (int)(tf >> 17);
-    // shift k (1..8) bytes, the low bytes of x, into the window; emit a completed aligned value
+    int o = ost[tid];
+    const int oend = tid + 1 < ni ? (int)ost[tid + 1] : job.dec_len;
+    int p = (int)(tf & 0x1FFFFu), fp = (int)(tf >> 17);
+    // shift k (1..8) bytes, the low bytes of x, into the window; a completed aligned value is emitted
     auto push = [&](uint64_t x, int k) {
       win = k == 8 ? x : ((win >> (8 * k)) | (x << (64 - 8 * k)));
       o += k;
-      if ((o & 7) == 0) run_emit(job, (o >> 3) - 1, win, acc);
+      if ((o & 7) == 0) {
+        if (fold) {
+          if (o <= job.expect_len) run_fold(job, win, acc);
+        } else {
+          s_val[(o >> 3) - 1] = win;
+        }
+      }
     };
     auto ext = [&](int& q, int& len) {  // LZ4 extended length (bytes up to the first != 255)
       for (int b = 255; b == 255;) {
@@ -1471,13 +1456,13 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
           bad = true;
           return;
         }
-        b = s8[q++];
+        b = (int)gld1(in + q++);
         len += b;
       }
     };
 #pragma unroll 1
     while (o < oend && !bad) {
-      const uint64_t w = lds_rd8(s32, p);
+      const uint64_t w = g_rd8(in, p);
       const int tk = (int)(w & 0xFF);
       int L = tk >> 4, M = tk & 15, q = p + 1;
       if (L == 15) ext(q, L);
@@ -1485,7 +1470,7 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
         bad = true;
         break;
       }
-      // literals: from the token's window when they and the distance fit in it, else from LDS
+      // literals: from the token's window when they and the distance fit in it, else from the block
       if (L > 0) {
         if (tk < 0x60) {  // L <= 5: the token window holds them
           const uint64_t lv = w >> 8;
@@ -1497,7 +1482,7 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
 #pragma unroll 1
           while (rem > 0) {
             const int k = min(rem, 8 - (o & 7));
-            push(lds_rd8(s32, lp), k);
+            push(g_rd8(in, lp), k);
             lp += k;
             rem -= k;
           }
@@ -1508,7 +1493,7 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
         if (q > n || o != job.dec_len) bad = true;
         break;
       }
-      const int d = tk < 0x60 ? (int)((w >> (8 * (1 + L))) & 0xFFFF) : (int)(lds_rd8(s32, q) & 0xFFFF);
+      const int d = tk < 0x60 ? (int)((w >> (8 * (1 + L))) & 0xFFFF) : (int)(g_rd8(in, q) & 0xFFFF);
       q += 2;
       if (M == 15) ext(q, M);
       M += 4;
@@ -1529,7 +1514,7 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
 #pragma unroll 1
         while (M > 0) {
           const int k = min(M, 8 - (o & 7));
-          push(lds_rd8(s32, fp), k);
+          push(g_rd8(far, fp), k);
           fp += k;
           M -= k;
         }
@@ -1539,12 +1524,36 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
     if (o != oend) bad = true;
   }
   if (bad) atomicOr(err, 1);
-  if (job.red_dst) red_finish(job, acc, s_red, kRunThreads / 64);
+  if (fold) {
+    red_finish(job, acc, s_red, kRunThreads / 64);
+    return;
+  }
+  __syncthreads();
+  // the block's values out: a slot takes every value of the block, payload records only its rows
+  if (!job.vstride) {
+    const int nq = job.dec_len >> 4;  // 16-byte stores (dec_len % 8 == 0)
+    const uint4* s16 = reinterpret_cast<const uint4*>(s_val);
+    for (int c = tid; c < nq; c += kRunThreads) {
+      const uint4 v = s16[c];
+      gst16(job.dst + 16 * (size_t)c, v.x, v.y, v.z, v.w);
+    }
+    if ((job.dec_len & 8) && tid == 0) {
+      const uint64_t v = s_val[(job.dec_len >> 3) - 1];
+      gst8(job.dst + (size_t)job.dec_len - 8, (uint32_t)v, (uint32_t)(v >> 32));
+    }
+  } else {
+    const int nv = job.expect_len >> 3;
+    for (int v = tid; v < nv; v += kRunThreads) {
+      const uint64_t x = s_val[v];
+      gst8(job.dst + (size_t)v * job.vstride, (uint32_t)x, (uint32_t)(x >> 32));
+    }
+  }
 }
 
 void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int lds, int32_t* d_err, hipStream_t s) {
+  (void)lds;
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_lz4_run, dim3(njobs), dim3(kRunThreads), lds, s, d_jobs, d_err);
+  hipLaunchKernelGGL(k_lz4_run, dim3(njobs), dim3(kRunThreads), 0, s, d_jobs, d_err);
 }
 
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {

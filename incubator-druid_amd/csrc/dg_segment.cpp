@@ -475,6 +475,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     if (!col->cps.alloc(all.size() * 4)) return set_error(DG_ERR_OOM, "hipMalloc lz4 index");
     DG_HIP(hipMemcpy(col->cps.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
     if (!rall.empty()) {
+      rall.resize(rall.size() + 16, 0);  // (k_lz4_run reads 12 bytes at a time: slack after the last table)
       if (!col->runx.alloc(rall.size())) return set_error(DG_ERR_OOM, "hipMalloc lz4 run index");
       DG_HIP(hipMemcpy(col->runx.p, rall.data(), rall.size(), hipMemcpyHostToDevice));
     }
