@@ -1100,6 +1100,12 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
 // column decode: returns a ColView, scheduling LZ4 block decodes into scratch when needed
 // ------------------------------------------------------------------------------------------------
 
+// A literal-only LZ4 block is its own decoded image (lz4_literal_start): the view points at its literal
+// bytes in HBM (16-byte aligned at attach) and no decoder runs for it; null for other blocks.
+static const uint8_t* literal_block(const BlockColumn& b, int32_t k) {
+  return (!b.lit_off.empty() && b.lit_off[k] >= 0) ? b.comp.as<uint8_t>() + b.lit_off[k] : nullptr;
+}
+
 // run_ok: run blocks go to k_lz4_run (run_decode_enabled(), read once per column by the caller)
 static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, bool run_ok) {
   Lz4Job j;
@@ -1183,12 +1189,14 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     // the packed (or plain) bytes of block k: an LZ4 slot, an uncompressed slot or a NONE range
     const uint8_t* src;
-    if (slots) src = slots + (size_t)k * kBlockBytes;
+    const uint8_t* lit = literal_block(b, k);
+    if (lit) src = lit;
+    else if (slots) src = slots + (size_t)k * kBlockBytes;
     else if (b.codec == CODEC_UNCOMPRESSED) src = b.raw.as<uint8_t>() + (size_t)k * kBlockBytes;
     else src = b.raw.as<uint8_t>() + (size_t)k * (size_t)b.size_per * b.vbits / 8;
     h_ptrs[k] = expanded ? reinterpret_cast<const uint8_t*>(expanded + (size_t)k * b.size_per) : src;
     if (rows <= 0) continue;
-    if (slots) {
+    if (slots && !lit) {
       const int64_t expect = b.vbits ? (b.vbits * rows + 7) / 8 : rows * b.width;
       if (b.codec == CODEC_LZ4) {
         db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect, run_ok));
@@ -1230,6 +1238,7 @@ static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int p
   const bool ident = (agg_kind == DG_AGG_LONG_SUM && c->type == DG_COL_LONG) ||
                      (agg_kind == DG_AGG_DOUBLE_SUM && c->type == DG_COL_DOUBLE);
   if (!ident || c->multi_value || b.codec != CODEC_LZ4 || b.vbits || b.width != 8 || !payload) return false;
+  if (!b.lit_off.empty()) return false;  // (literal-only blocks are viewed in place: the keygen copies them)
   db->bytes += b.stored_bytes + b.index_bytes;
   const bool run_ok = run_decode_enabled();
   for (int32_t k = 0; k < b.nblocks; ++k) {
@@ -1598,6 +1607,11 @@ static int time_view(const Column* c, const std::vector<int64_t>& tb, CallScratc
       h_ptrs[k] = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(d_const + k) | 1u);
       continue;
     }
+    if (const uint8_t* lit = literal_block(b, k)) {  // its own decoded image
+      h_ptrs[k] = lit;
+      db->bytes += b.comp_len[k];
+      continue;
+    }
     uint8_t* slot = slots + (size_t)at++ * kBlockBytes;
     h_ptrs[k] = slot;
     if (rows > 0) {
@@ -1724,16 +1738,21 @@ int read_time_bounds(Segment* seg) {
     // decode only the first and last block
     uint8_t* slots = dev_take<uint8_t>(cs, 2 * (size_t)kBlockBytes + 64);
     int32_t last = (int32_t)((seg->nrows - 1) >> b.log2_per);
+    const uint8_t* img[2];
     for (int k = 0; k < 2; ++k) {
       int32_t blk = k == 0 ? 0 : last;
       int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)blk * b.size_per);
-      db.jobs.push_back(lz4_job(b, blk, slots + (size_t)k * kBlockBytes, (int32_t)(rows * 8), run_decode_enabled()));
+      img[k] = literal_block(b, blk);
+      if (!img[k]) {
+        img[k] = slots + (size_t)k * kBlockBytes;
+        db.jobs.push_back(lz4_job(b, blk, slots + (size_t)k * kBlockBytes, (int32_t)(rows * 8), run_decode_enabled()));
+      }
     }
     int rc0 = run_decodes(cs, &db, st);
     if (rc0) return rc0;
     int64_t idx_last = (seg->nrows - 1) & ((1ll << b.log2_per) - 1);
-    DG_HIP(hipMemcpyAsync(h, slots, 8, hipMemcpyDeviceToHost, st));
-    DG_HIP(hipMemcpyAsync(h + 1, slots + kBlockBytes + idx_last * 8, 8, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h, img[0], 8, hipMemcpyDeviceToHost, st));
+    DG_HIP(hipMemcpyAsync(h + 1, img[1] + idx_last * 8, 8, hipMemcpyDeviceToHost, st));
   } else {
     std::vector<const uint8_t*> ptrs(b.nblocks);
     DG_HIP(hipMemcpy(ptrs.data(), b.block_ptrs.p, sizeof(void*) * b.nblocks, hipMemcpyDeviceToHost));
@@ -1895,7 +1914,7 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
     const int64_t r0 = (int64_t)k * b.size_per, r1 = std::min<int64_t>((int64_t)b.total, r0 + b.size_per);
     // (light blocks are decoded by k_lz4_light, which does not fold; a run block folds in k_lz4_run)
     const bool run = run_ok && !b.run_off.empty() && b.run_off[k] >= 0;
-    if (r1 <= r0 || (!run && !b.cp_light.empty() && b.cp_light[k])) continue;
+    if (r1 <= r0 || literal_block(b, k) || (!run && !b.cp_light.empty() && b.cp_light[k])) continue;
     if (one_bucket) {
       bk[k] = 0;
     } else {
@@ -1935,6 +1954,10 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
                                         : (a.kind == DG_AGG_DOUBLE_SUM ? kRedDoubleSum : kRedGeneric);
       db->jobs.push_back(j);
       db->fused_blocks++;
+      continue;
+    }
+    if (const uint8_t* lit = literal_block(b, k)) {  // its own decoded image
+      h_ptrs[k] = lit;
       continue;
     }
     uint8_t* dst = slots + (size_t)at++ * kBlockBytes;

@@ -112,6 +112,9 @@ inline int run_lds_bytes(int n, int nfar) { return ((n + 15) & ~15) + 16 + ((nfa
 // Run index of one validated LZ4 block decoding to dec_len bytes, appended to *idx (16-byte aligned);
 // returns false (nothing appended) when the block is not a run block.
 bool lz4_run_index(const uint8_t* in, int n, int dec_len, std::vector<uint8_t>* idx, int* nint, int* nfar);
+// Literal-only LZ4 block (a single sequence of literals, as LZ4 writes incompressible data): the
+// offset of its literal bytes (= its decoded image), or -1.
+int lz4_literal_start(const uint8_t* in, int n);
 // Host decode of a validated LZ4 block into out (kBlockBytes); returns the decoded length or -1.
 int lz4_decode_host(const uint8_t* in, int n, uint8_t* out);
 // the run decoder is on unless DG_NO_RUN_DECODE is set (same-box A/B, tests of the other decoders)
@@ -281,6 +284,9 @@ struct BlockColumn {
                                        // assumption on the row order inside a block)
   int64_t index_bytes = 0;             // LZ4: bytes of the index a query reads (checkpoints; run index
                                        // of run blocks instead)
+  std::vector<int64_t> lit_off;        // LZ4: literal-only block b's literal bytes inside comp (16-byte
+                                       // aligned: its decoded image, viewed in place), -1 otherwise;
+                                       // empty: no literal-only block
   std::vector<int64_t> run_off;        // LZ4: block b's run index inside runx (-1: not a run block)
   std::vector<int32_t> run_n;          // LZ4: its intervals
   std::vector<int32_t> run_far;        // LZ4: its far-copy bytes

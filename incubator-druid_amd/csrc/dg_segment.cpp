@@ -297,6 +297,20 @@ int lz4_decode_host(const uint8_t* in, int n, uint8_t* out) {
   }
 }
 
+int lz4_literal_start(const uint8_t* in, int n) {
+  if (n < 2) return -1;
+  int q = 1, L = in[0] >> 4;
+  if (in[0] & 15) return -1;  // (a match length: not the block's only, last sequence)
+  if (L == 15) {
+    for (int b = 255; b == 255;) {
+      if (q >= n) return -1;
+      b = in[q++];
+      L += b;
+    }
+  }
+  return L > 0 && L <= kBlockBytes && q + L == n ? q : -1;
+}
+
 bool run_decode_enabled() {
   const char* off = getenv("DG_NO_RUN_DECODE");
   return !(off && *off && *off != '0');
@@ -381,13 +395,23 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->comp_off.resize(blocks.n);
     col->comp_len.resize(blocks.n);
     int64_t total = 0;
+    col->lit_off.clear();
     for (int32_t b = 0; b < blocks.n; ++b) {
       const uint8_t* p;
       int32_t len = blocks.get(b, &p);
       if (len <= 0) return set_error(DG_ERR_FORMAT, "empty or out-of-range compressed block %d", b);
-      col->comp_off[b] = total;
+      // a literal-only LZ4 block (one sequence of literals: incompressible data) is placed so that its
+      // literal bytes, its decoded image, start 16-byte aligned: views point at them, nothing decodes
+      const int ls = col->codec == CODEC_LZ4 ? lz4_literal_start(p, len) : -1;
+      if (ls >= 0) {
+        if (col->lit_off.empty()) col->lit_off.assign(blocks.n, -1);
+        col->comp_off[b] = ((total + ls + 15) & ~(int64_t)15) - ls;
+        col->lit_off[b] = col->comp_off[b] + ls;
+      } else {
+        col->comp_off[b] = total;
+      }
       col->comp_len[b] = len;
-      total += (len + 15) & ~15;
+      total = (col->comp_off[b] + len + 15) & ~(int64_t)15;
     }
     std::vector<uint8_t> host((size_t)total + 16, 0);
     for (int32_t b = 0; b < blocks.n; ++b) {
