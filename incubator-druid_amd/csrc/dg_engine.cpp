@@ -1106,8 +1106,9 @@ static const uint8_t* literal_block(const BlockColumn& b, int32_t k) {
   return (!b.lit_off.empty() && b.lit_off[k] >= 0) ? b.comp.as<uint8_t>() + b.lit_off[k] : nullptr;
 }
 
-// run_ok: run blocks go to k_lz4_run (run_decode_enabled(), read once per column by the caller)
-static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, bool run_ok) {
+// routes: decode_routes(), read once per column by the caller (run blocks to k_lz4_run, flow blocks to
+// k_lz4_decode_flow)
+static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, int routes) {
   Lz4Job j;
   j.src = b.comp.as<uint8_t>() + b.comp_off[k];
   j.dst = dst;
@@ -1116,11 +1117,14 @@ static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t exp
   j.expect_len = expect;
   j.ncp = b.cp_n[k];
   j.dec_len = b.dec_len[k];
-  j.wide = b.cp_wide[k];
+  const bool flow = (routes & kRouteFlow) && !b.lvl_off.empty() && b.lvl_off[k] >= 0 && (b.cp_wide[k] & kLzFlow);
+  j.wide = (b.cp_wide[k] & 1) | (flow ? kLzFlow : 0);
+  j.lvl = flow ? b.lvls.as<uint8_t>() + b.lvl_off[k] : nullptr;
+  j.nlvl = flow ? b.lvl_n[k] : 0;
   j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
   j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
   j.vstride = 0;
-  const bool run = run_ok && !b.run_off.empty() && b.run_off[k] >= 0;
+  const bool run = (routes & kRouteRun) && !b.run_off.empty() && b.run_off[k] >= 0;
   j.rx = run ? b.runx.as<uint8_t>() + b.run_off[k] : nullptr;
   j.run_n = run ? b.run_n[k] : 0;
   j.run_far = run ? b.run_far[k] : 0;
@@ -1166,7 +1170,7 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
   if (b.codec != CODEC_LZ4 && b.codec != CODEC_LZF && b.codec != CODEC_UNCOMPRESSED && b.codec != CODEC_NONE)
     return set_error(DG_ERR_UNSUPPORTED, "codec 0x%02x of %s", b.codec, name);
   uint8_t* slots = nullptr;
-  const bool run_ok = b.codec == CODEC_LZ4 && run_decode_enabled();
+  const int routes = b.codec == CODEC_LZ4 ? decode_routes() : 0;
   if (b.codec == CODEC_LZ4 || b.codec == CODEC_LZF) {
     slots = dev_take<uint8_t>(cs, (size_t)b.nblocks * kBlockBytes + 64);
     if (!slots) return set_error(DG_ERR_OOM, "decode scratch");
@@ -1199,7 +1203,7 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
     if (slots && !lit) {
       const int64_t expect = b.vbits ? (b.vbits * rows + 7) / 8 : rows * b.width;
       if (b.codec == CODEC_LZ4) {
-        db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect, run_ok));
+        db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect, routes));
       } else {
         LzfJob lj;
         lj.src = b.comp.as<uint8_t>() + b.comp_off[k];
@@ -1240,12 +1244,12 @@ static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int p
   if (!ident || c->multi_value || b.codec != CODEC_LZ4 || b.vbits || b.width != 8 || !payload) return false;
   if (!b.lit_off.empty()) return false;  // (literal-only blocks are viewed in place: the keygen copies them)
   db->bytes += b.stored_bytes + b.index_bytes;
-  const bool run_ok = run_decode_enabled();
+  const int routes = decode_routes();
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (rows <= 0) continue;
     const int64_t r0 = (int64_t)row_base + (int64_t)k * b.size_per;
-    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(payload + (size_t)r0 * pw + a), (int32_t)(rows * 8), run_ok);
+    Lz4Job j = lz4_job(b, k, reinterpret_cast<uint8_t*>(payload + (size_t)r0 * pw + a), (int32_t)(rows * 8), routes);
     j.vstride = pw * 8;
     db->jobs.push_back(j);
   }
@@ -1315,14 +1319,19 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
   // blocks per CU)
   // run blocks (value runs with a run index) first, to k_lz4_run
+  // flow blocks (k_lz4_decode_flow) after the other general blocks, each kind narrow then wide
   auto& J = db->jobs;
   const int nr = (int)(std::stable_partition(J.begin(), J.end(), [](const Lz4Job& j) { return j.rx != nullptr; }) - J.begin());
   const int nh = (int)(std::stable_partition(J.begin() + nr, J.end(), [](const Lz4Job& j) { return !j.light; }) - J.begin());
-  const int nn = (int)(std::stable_partition(J.begin() + nr, J.begin() + nh, [](const Lz4Job& j) { return !j.wide; }) -
-                       J.begin());
+  auto by_kind = [](const Lz4Job& a, const Lz4Job& b) { return a.wide < b.wide; };  // wide: bit 0 | kLzFlow
+  std::stable_sort(J.begin() + nr, J.begin() + nh, by_kind);
+  int kb[5] = {nr, nr, nr, nr, nh};  // kb[w] .. kb[w + 1]: the general blocks of wide == w
+  for (int w = 1; w < 4; ++w)
+    kb[w] = (int)(std::lower_bound(J.begin() + nr, J.begin() + nh, w, [](const Lz4Job& j, int v) { return j.wide < v; }) -
+                  J.begin());
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
-  if (nn - nr <= 16 * 256) std::stable_sort(J.begin() + nr, J.begin() + nn, by_ncp);
-  if (nh - nn <= 16 * 256) std::stable_sort(J.begin() + nn, J.begin() + nh, by_ncp);
+  for (int w = 0; w < 4; ++w)
+    if (kb[w + 1] - kb[w] <= 16 * 256) std::stable_sort(J.begin() + kb[w], J.begin() + kb[w + 1], by_ncp);
   int run_lds = 0;
   for (int i = 0; i < nr; ++i) run_lds = std::max(run_lds, run_lds_bytes(J[i].src_len, J[i].run_far));
   Lz4Job* d;
@@ -1345,10 +1354,10 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   const int ng = nh - nr;  // general-decoder blocks
   for (int i = nr; i < nh; ++i) db->gen_bytes += J[i].src_len;
   db->gen_blocks += ng;
-  db->gen_launches += (nn > nr) + (nh - nn > 0);
+  for (int w = 0; w < 4; ++w) db->gen_launches += kb[w + 1] > kb[w];
   if (db->gen_a && ng) hipEventRecord(db->gen_a, st);
-  launch_lz4_decode(d + nr, nn - nr, 0, d_err, st, d_prof ? d_prof + (size_t)nr * kLz4ProfWords : nullptr);
-  launch_lz4_decode(d + nn, nh - nn, 1, d_err, st, d_prof ? d_prof + (size_t)nn * kLz4ProfWords : nullptr);
+  for (int w = 0; w < 4; ++w)
+    launch_lz4_decode(d + kb[w], kb[w + 1] - kb[w], w, d_err, st, d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
   if (db->gen_a && ng) hipEventRecord(db->gen_b, st);
   if (ovl) DG_HIP(hipStreamWaitEvent(st, ctx->ovl_ev[1], 0));
   return run_expands(cs, db, st);  // errors surface at finish_call
@@ -1599,7 +1608,7 @@ static int time_view(const Column* c, const std::vector<int64_t>& tb, CallScratc
   if ((ndec && !slots) || !h_const || !h_ptrs) return set_error(DG_ERR_OOM, "time view");
   if (ndec) db->last_slots = slots;
   int32_t at = 0;
-  const bool run_ok = run_decode_enabled();
+  const int routes = decode_routes();
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (uni[k]) {
@@ -1615,7 +1624,7 @@ static int time_view(const Column* c, const std::vector<int64_t>& tb, CallScratc
     uint8_t* slot = slots + (size_t)at++ * kBlockBytes;
     h_ptrs[k] = slot;
     if (rows > 0) {
-      db->jobs.push_back(lz4_job(b, k, slot, (int32_t)(rows * 8), run_ok));
+      db->jobs.push_back(lz4_job(b, k, slot, (int32_t)(rows * 8), routes));
       const Lz4Job& j = db->jobs.back();
       db->bytes += b.comp_len[k] + (j.rx ? run_index_bytes(j.run_n, j.run_far) : 4 * (int64_t)(j.ncp + j.nfine));
     }
@@ -1745,7 +1754,7 @@ int read_time_bounds(Segment* seg) {
       img[k] = literal_block(b, blk);
       if (!img[k]) {
         img[k] = slots + (size_t)k * kBlockBytes;
-        db.jobs.push_back(lz4_job(b, blk, slots + (size_t)k * kBlockBytes, (int32_t)(rows * 8), run_decode_enabled()));
+        db.jobs.push_back(lz4_job(b, blk, slots + (size_t)k * kBlockBytes, (int32_t)(rows * 8), decode_routes()));
       }
     }
     int rc0 = run_decodes(cs, &db, st);
@@ -1909,11 +1918,11 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
   const int64_t ts = one_bucket ? 1 : tc->data.size_per;
   std::vector<int64_t> bk(b.nblocks, -1);
   int32_t nfused = 0;
-  const bool run_ok = run_decode_enabled();
+  const int routes = decode_routes();
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t r0 = (int64_t)k * b.size_per, r1 = std::min<int64_t>((int64_t)b.total, r0 + b.size_per);
     // (light blocks are decoded by k_lz4_light, which does not fold; a run block folds in k_lz4_run)
-    const bool run = run_ok && !b.run_off.empty() && b.run_off[k] >= 0;
+    const bool run = (routes & kRouteRun) && !b.run_off.empty() && b.run_off[k] >= 0;
     if (r1 <= r0 || literal_block(b, k) || (!run && !b.cp_light.empty() && b.cp_light[k])) continue;
     if (one_bucket) {
       bk[k] = 0;
@@ -1944,7 +1953,7 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (bk[k] >= 0) {
       h_ptrs[k] = reinterpret_cast<const uint8_t*>((uintptr_t)1);  // tagged: never dereferenced
-      Lz4Job j = lz4_job(b, k, nullptr, (int32_t)(rows * 8), run_ok);
+      Lz4Job j = lz4_job(b, k, nullptr, (int32_t)(rows * 8), routes);
       j.red_dst = out + (size_t)bk[k] * rec + 1 + slot;
       j.red_op = slot_op(a.kind);
       j.red_kind = a.kind;
@@ -1962,7 +1971,7 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
     }
     uint8_t* dst = slots + (size_t)at++ * kBlockBytes;
     h_ptrs[k] = dst;
-    if (rows > 0) db->jobs.push_back(lz4_job(b, k, dst, (int32_t)(rows * 8), run_ok));
+    if (rows > 0) db->jobs.push_back(lz4_job(b, k, dst, (int32_t)(rows * 8), routes));
   }
   v->blocks = d_ptrs;
   return DG_OK;
@@ -4548,12 +4557,13 @@ extern "C" int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t*
   if (!block || len <= 0 || len > kBlockBytes + 2048 || !kind) return set_error(DG_ERR_ARG, "bad arguments");
   std::vector<uint32_t> one;
   int wide = 0, light = 0, nfine = 0;
-  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine);
+  std::vector<uint8_t> lv;
+  const int d = lz4_index_block(block, len, &one, &wide, &light, &nfine, &lv);
   std::vector<uint8_t> rx;
   int nint = 0, nfar = 0;
   const bool run = d > 0 && lz4_run_index(block, len, d, &rx, &nint, &nfar);
-  // -1 malformed, 0 general, 1 general (wide), 2 light, 3 run
-  *kind = d < 0 ? -1 : run ? 3 : light ? 2 : wide ? 1 : 0;
+  // -1 malformed, 0 general, 1 general (wide), 2 light, 3 run, 4 flow (narrow or wide)
+  *kind = d < 0 ? -1 : run ? 3 : light ? 2 : (wide & kLzFlow) ? 4 : wide ? 1 : 0;
   return DG_OK;
 }
 
@@ -4575,7 +4585,9 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.run_off.assign(n, -1);
   b.run_n.assign(n, 0);
   b.run_far.assign(n, 0);
-  std::vector<uint8_t> rall;
+  b.lvl_off.assign(n, -1);
+  b.lvl_n.assign(n, 0);
+  std::vector<uint8_t> rall, lall;
   int64_t total = 0;
   for (int i = 0; i < n; ++i) {
     if (lens[i] <= 0 || lens[i] > kBlockBytes + 2048) return set_error(DG_ERR_ARG, "block %d length %d", i, lens[i]);
@@ -4588,8 +4600,13 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);
     std::vector<uint32_t> one;
-    int wide = 0, light = 0, nfine = 0;
-    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine);
+    int wide = 0, light = 0, nfine = 0, nlvl = 0;
+    const size_t lat = lall.size();
+    const int d = lz4_index_block(blocks[i], lens[i], &one, &wide, &light, &nfine, &lall, &nlvl);
+    if (lall.size() > lat) {
+      b.lvl_off[i] = (int64_t)lat;
+      b.lvl_n[i] = nlvl;
+    }
     b.cp_wide[i] = (uint8_t)wide;
     b.cp_light[i] = (uint8_t)light;
     b.cp_fine[i] = nfine;
@@ -4607,15 +4624,17 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   hipStream_t st = ctx->stream;
   if (!b.comp.alloc(host.size()) || !b.cps.alloc(cps.size() * 4)) return set_error(DG_ERR_OOM, "debug decode");
   if (!rall.empty() && !b.runx.alloc(rall.size())) return set_error(DG_ERR_OOM, "debug decode");
+  if (!lall.empty() && !b.lvls.alloc(lall.size())) return set_error(DG_ERR_OOM, "debug decode");
   DG_HIP(hipMemcpy(b.comp.p, host.data(), host.size(), hipMemcpyHostToDevice));
   DG_HIP(hipMemcpy(b.cps.p, cps.data(), cps.size() * 4, hipMemcpyHostToDevice));
   if (!rall.empty()) DG_HIP(hipMemcpy(b.runx.p, rall.data(), rall.size(), hipMemcpyHostToDevice));
-  const bool run_ok = run_decode_enabled();
+  if (!lall.empty()) DG_HIP(hipMemcpy(b.lvls.p, lall.data(), lall.size(), hipMemcpyHostToDevice));
+  const int routes = decode_routes();
   DecodeBatch db;
   uint8_t* slots = dev_take<uint8_t>(g.cs, (size_t)n * kBlockBytes + 64);
   if (!slots) return set_error(DG_ERR_OOM, "debug decode slots");
   for (int i = 0; i < n; ++i)
-    if (out_lens[i] >= 0) db.jobs.push_back(lz4_job(b, i, slots + (size_t)i * kBlockBytes, out_lens[i], run_ok));
+    if (out_lens[i] >= 0) db.jobs.push_back(lz4_job(b, i, slots + (size_t)i * kBlockBytes, out_lens[i], routes));
   uint64_t* d_prof = nullptr;
   if (prof) {
     d_prof = dev_take<uint64_t>(g.cs, (size_t)n * kLz4ProfWords);

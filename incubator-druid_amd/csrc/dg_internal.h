@@ -72,6 +72,9 @@ struct Lz4Job {
   const uint8_t* rx;
   int32_t run_n;    // intervals (one per k_lz4_run thread)
   int32_t run_far;  // bytes of the far-copy table after the intervals
+  // flow block (wide & kLzFlow): its schedule (lz4_flow_schedule) and highest level
+  const uint8_t* lvl;
+  int32_t nlvl;
   // Decode fused with a timeseries aggregator (the block's rows share one bucket, no filter): instead
   // of writing its 8-byte values the decoder folds them with red_op (agg_input_raw(red_kind,
   // red_vkind, value)) and combines the block's result into the bucket's slot *red_dst atomically.
@@ -117,8 +120,19 @@ bool lz4_run_index(const uint8_t* in, int n, int dec_len, std::vector<uint8_t>* 
 int lz4_literal_start(const uint8_t* in, int n);
 // Host decode of a validated LZ4 block into out (kBlockBytes); returns the decoded length or -1.
 int lz4_decode_host(const uint8_t* in, int n, uint8_t* out);
-// the run decoder is on unless DG_NO_RUN_DECODE is set (same-box A/B, tests of the other decoders)
-bool run_decode_enabled();
+// Decoder routes a query may take (read once per column): kRouteRun = run blocks go to k_lz4_run
+// (off with DG_NO_RUN_DECODE), kRouteFlow = flow blocks go to k_lz4_decode_flow (off with
+// DG_NO_FLOW_DECODE); same-box A/B and the tests of the other decoders turn them off
+constexpr int kRouteRun = 1, kRouteFlow = 2;
+int decode_routes();
+
+// Flow blocks (Lz4Job.wide & kLzFlow, set at attach): general blocks of at most kLzMaxCps intervals
+// that are not distance-8 class chains (at most a quarter of their bytes copied from 8 back) and whose
+// copy chains are at most kFlowMaxDepth hops deep. The attach-time schedule ranks every match by its
+// copy-chain level; k_lz4_decode_flow writes the literals into a byte image in LDS, then the matches
+// level by level, each level's matches spread evenly over the threads.
+constexpr int kLzFlow = 2;
+constexpr int kFlowMaxDepth = 64;
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
 struct LzfJob {
@@ -144,12 +158,17 @@ struct VsJob {
 
 // Host-side validating parse of one LZ4 block (lz4-java safe-decompressor semantics): appends the
 // block's checkpoints to *cps and returns the decoded length, or -1 for a malformed block.
-// *wide: the block keeps every other checkpoint (more than kLzMaxCps * kLzSeqPerCp sequences).
+// *wide: bit 0 = the block keeps every other checkpoint (more than kLzMaxCps * kLzSeqPerCp sequences),
+// kLzFlow = a flow block (decoded by k_lz4_decode_flow).
 // *light (optional): the block qualifies for the light decoder (kLtMaxCps / kLtMaxDepth).
 // *light = g > 0 when light: the block's checkpoints are followed by *nfine light checkpoints, one
 // every g sequences (g the fewest sequences per checkpoint that fit the light decoder's threads).
+// levels (optional): a flow block's schedule is appended (lz4_flow_schedule: per checkpoint interval
+// kLzSeqPerCp u16 ranks of its matches in (level, position) order and kLzSeqPerCp u16 forwarded
+// distances; then the u16 start of every level's ranks, padded to 16 bytes) and *nlvl = its highest
+// level; without it no block is a flow block.
 int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light = nullptr,
-                    int* nfine = nullptr);
+                    int* nfine = nullptr, std::vector<uint8_t>* levels = nullptr, int* nlvl = nullptr);
 
 struct AggPlan {
   int32_t n;
@@ -291,6 +310,9 @@ struct BlockColumn {
   std::vector<int32_t> run_n;          // LZ4: its intervals
   std::vector<int32_t> run_far;        // LZ4: its far-copy bytes
   DevBuf runx;                         // LZ4: run indexes of the run blocks
+  std::vector<int64_t> lvl_off;        // LZ4: flow block b's level schedule inside lvls (-1: none)
+  std::vector<int32_t> lvl_n;          // LZ4: its highest level
+  DevBuf lvls;                         // LZ4: level schedules of the flow blocks
   DevBuf comp;                         // LZ4: packed compressed blocks (16-byte aligned)
   DevBuf cps;                          // LZ4: uint32 checkpoints of every block
   DevBuf raw;                          // UNCOMPRESSED: 64 KiB slot per block; NONE: flat values

@@ -1111,6 +1111,351 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
+// Flow decoder: general blocks of at most 8,192 sequences that are not distance-8 class chains and
+// whose copy chains are at most kFlowMaxDepth hops deep (attach-time classification, lz4_index_block):
+// the literal-heavy, short-match blocks of noisy doubles (~7,500 sequences of ~5 literal bytes and a
+// 4-byte copy from ~5 KiB back), zipfian doubles and uniform longs. k_lz4_decode spends most of its time
+// on per-byte entries (write 64 K of them, then resolve them all in position-ordered stages); here the
+// workgroup decodes straight into the block's byte image in LDS, in the order of the attach-time
+// schedule (lz4_flow_schedule: a match whose source lies inside one earlier match's output copies from
+// that match's source instead — forwarded distance; its level is one more than the highest level among
+// the bytes it copies, literal bytes are level 0; every match has its rank in (level, position) order):
+//   1. stage + parse + scan as in k_lz4_decode (every thread: one checkpoint interval in registers) and
+//      zero the image;
+//   2. level 0: every thread ORs its short literal runs into the image, long runs are split evenly over
+//      the threads (as in k_lz4_decode);
+//   3. the staged input is dead: every thread writes its matches (start, forwarded distance, length)
+//      into a table over it, at their ranks — each level's matches are then one contiguous range;
+//   4. levels 1 .. nlvl, one barrier each: thread t copies matches t, t + 1024, ... of the level's range
+//      (their sources are complete);
+//   5. output: 16-byte chunks of the image, coalesced stores (or out16's payload / fused paths).
+// A copy reads its source dwords (one more than the destination dwords it covers) and funnels them to
+// the destination's alignment; whole destination dwords are plain stores, the partial ones at its ends
+// LDS atomic ORs into the zeroed image (a neighbouring run owns the other bytes). LDS: staged input
+// (later the match table) 66 KiB + image 64 KiB + literal jobs 12 KiB: one block per CU, like
+// k_lz4_decode.
+// ------------------------------------------------------------------------------------------------
+constexpr int kFlowJobs = 1024;     // cooperative literal runs per block
+constexpr int kFlowLongLit = 16;    // literal runs longer than this are split over the threads
+constexpr int kFlowPad = 4;         // dwords before the staged input and the image: a copy's first
+                                    // source dword may start up to 3 bytes before its source
+constexpr int kFlowInWords = kFlowPad + (kLz4InCap + 32) / 4 + 8;  // (+ the unconditional reads past a copy)
+constexpr int kFlowOutWords = kFlowPad + kBlockBytes / 4 + 8;
+constexpr int kFlowMaxMatches = kLzMaxCps * kLzSeqPerCp;  // the match table's rows (over the staged input)
+static_assert(kFlowMaxMatches * 8 <= kFlowInWords * 4, "the match table fits the staged input");
+
+__device__ __forceinline__ void lds_or(uint32_t* p, uint32_t v) {
+  __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_ld8(const uint32_t* a, int p) {
+  return reinterpret_cast<const uint8_t*>(a + kFlowPad)[p];
+}
+
+// destination dword j (image word kFlowPad + j) gets bytes b0 .. b1 - 1 of w: an LDS atomic OR into the
+// zeroed image (a neighbouring run may own the dword's other bytes)
+__device__ __forceinline__ void flow_put(uint32_t* o32, int j, int b0, int b1, uint32_t w) {
+  const uint32_t m = (0xFFFFFFFFu << (8 * b0)) & (0xFFFFFFFFu >> (8 * (4 - b1)));
+  lds_or(o32 + kFlowPad + j, w & m);
+}
+
+// the byte mask of destination dword t (0 .. NJ - 1) of a run [dst, dst + len) whose first dword is
+// dst >> 2: full inside, cut at the run's two ends, empty past it
+__device__ __forceinline__ uint32_t run_mask(int t, int dst, int len) {
+  const int nj = ((dst + len - 1) >> 2) - (dst >> 2) + 1;
+  uint32_t m = t == 0 ? 0xFFFFFFFFu << (8 * (dst & 3)) : 0xFFFFFFFFu;
+  if (t == nj - 1) m &= 0xFFFFFFFFu >> (8 * (3 - ((dst + len - 1) & 3)));
+  return t < nj ? m : 0u;
+}
+
+// bytes [dst, dst + len) of the image o32 <- bytes [src, src + len) of i32 (padded LDS byte arrays,
+// 1 <= len <= 4 * (NJ - 1) + 1): NJ + 1 source dwords, then NJ masked ORs into the destination dwords
+// (nothing past the copy's end), all unconditional — one LDS round trip. Inside one array the source
+// must end before the destination starts (it is read before anything is written).
+template <int NJ>
+__device__ __forceinline__ void flow_copyn(uint32_t* o32, int dst, const uint32_t* i32, int src, int len) {
+  const int j0 = dst >> 2;
+  const int q0 = 4 * j0 + (src - dst) + 4 * kFlowPad;  // padded offset of dword j0's first source byte
+  const int k0 = q0 >> 2, sh = q0 & 3;
+  uint32_t sw[NJ + 1];
+#pragma unroll
+  for (int t = 0; t <= NJ; ++t) sw[t] = i32[k0 + t];
+#pragma unroll
+  for (int t = 0; t < NJ; ++t)
+    lds_or(o32 + kFlowPad + j0 + t, __builtin_amdgcn_alignbyte(sw[t + 1], sw[t], sh) & run_mask(t, dst, len));
+}
+
+// the first min(M, 16) bytes of an overlapping match (d < 16, d < M): out[om + k] = out[om - d + k mod d].
+// A period dividing 8 (the common ones: byte runs, repeated 8-byte values) is read as 8 bytes and
+// doubled in a register; other periods are gathered byte by byte.
+__device__ __forceinline__ void flow_head(uint32_t* o32, int om, int d, int M) {
+  const int h = min(M, 16);
+  uint32_t v[4];  // the head's bytes, little-endian
+  if (d <= 8 && (d & (d - 1)) == 0) {
+    const int q = om - d + 4 * kFlowPad, k = q >> 2, sh = q & 3;
+    const uint32_t w0 = o32[k], w1 = o32[k + 1], w2 = o32[k + 2];
+    uint64_t x = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+    x = d == 8 ? x : (x & ((1ull << (8 * d)) - 1));
+    for (int per = d; per < 8; per <<= 1) x |= x << (8 * per);
+    v[0] = v[2] = (uint32_t)x;
+    v[1] = v[3] = (uint32_t)(x >> 32);
+  } else {
+    v[0] = v[1] = v[2] = v[3] = 0u;
+    int r = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      v[k >> 2] |= lds_ld8(o32, om - d + r) << (8 * (k & 3));
+      if (++r == d) r = 0;
+    }
+  }
+  const int a = om & 3, j0 = om >> 2;
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    const uint32_t lo = t > 0 ? v[t - 1] : 0u, hi = t < 4 ? v[t] : 0u;
+    const uint32_t w = a == 0 ? hi : __builtin_amdgcn_alignbyte(hi, lo, 4 - a);  // bytes 4t - a ..
+    lds_or(o32 + kFlowPad + j0 + t, w & run_mask(t, om, h));
+  }
+}
+
+// one match (its source complete) in 16-byte pieces: the first piece a plain copy from d back (or, when
+// it overlaps itself, the gathered head), every later piece a plain copy from D back, D the first
+// multiple of d of at least 16 bytes (the bytes repeat with period d, and a piece's source ends before
+// it starts). Pieces in order: a piece may read what the earlier ones wrote.
+__device__ __forceinline__ void flow_match(uint32_t* o32, int om, int d, int M) {
+  if (d >= min(M, 16)) flow_copyn<5>(o32, om, o32, om - d, min(M, 16));
+  else flow_head(o32, om, d, M);
+  if (M > 16) {
+    int D = d;
+    while (D < 16) D += d;
+#pragma unroll 1
+    for (int k = 16; k < M; k += 16) flow_copyn<5>(o32, om + k, o32, om + k - D, min(16, M - k));
+  }
+}
+
+// a copy of any length from the staged input (16-byte pieces)
+__device__ __forceinline__ void flow_copy(uint32_t* o32, int dst, const uint32_t* i32, int src, int len) {
+#pragma unroll 1
+  for (int k = 0; k < len; k += 16) flow_copyn<5>(o32, dst + k, i32, src + k, min(16, len - k));
+}
+
+template <bool PROF>
+__global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+                                                                uint64_t* __restrict__ prof) {
+  constexpr int SEQ = kLzSeqPerCp;
+  __shared__ __attribute__((aligned(16))) uint32_t s_in32[kFlowInWords];    // staged input (after the pad)
+  __shared__ __attribute__((aligned(16))) uint32_t s_out32[kFlowOutWords];  // the decoded image (after the pad)
+  __shared__ uint2 s_job[kFlowJobs];  // long literal runs: output start | (L - 1) << 16, input offset
+  __shared__ int s_jpre[kFlowJobs];
+  __shared__ int s_lvl[kFlowMaxDepth + 1];  // s_lvl[k - 1] .. s_lvl[k]: the table rows of level k
+  __shared__ int s_njob, s_bad;
+  __shared__ int s_tmp[kLzWaves];
+  __shared__ uint64_t s_red[kLzWaves];
+  uint2* s_tab = reinterpret_cast<uint2*>(s_in32);  // the match table, after the literals
+
+  const Lz4Job job = jobs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int n = job.src_len, ncp = job.ncp;
+  if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.dec_len > kBlockBytes ||
+      job.dec_len < job.expect_len || !job.lvl || job.nlvl < 0 || job.nlvl > kFlowMaxDepth) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  LZ_STAMP(0);
+  const uint8_t* s_in = reinterpret_cast<const uint8_t*>(s_in32 + kFlowPad);
+  // my matches' table rows (u16 each, 0xFFFF: none) and the levels' row ranges
+  const uint4 rk4 = tid < ncp ? gld16(job.lvl + (size_t)tid * 4 * SEQ) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  const uint4 fd4 = tid < ncp ? gld16(job.lvl + (size_t)tid * 4 * SEQ + 2 * SEQ) : make_uint4(0u, 0u, 0u, 0u);
+  if (tid <= job.nlvl) {
+    const uint8_t* st = job.lvl + 4 * SEQ * (size_t)ncp;
+    s_lvl[tid] = (int)(gld4(st + 2 * tid - 2 * (tid & 1)) >> (16 * (tid & 1))) & 0xFFFF;
+  }
+  {
+    uint4* dst = reinterpret_cast<uint4*>(s_in32 + kFlowPad);
+    const int n16 = (n + 15) >> 4;
+    for (int i = tid; i < n16; i += kLzThreads) dst[i] = gld16(job.src + 16 * (size_t)i);
+    uint4* img = reinterpret_cast<uint4*>(s_out32 + kFlowPad);
+    for (int i = tid; i < kBlockBytes / 16; i += kLzThreads) img[i] = make_uint4(0, 0, 0, 0);
+    if (tid == 0) {
+      dst[n16] = make_uint4(0, 0, 0, 0);
+      s_njob = 0;
+      s_bad = 0;
+    }
+  }
+  __syncthreads();
+  LZ_STAMP(1);
+  // ---- 1. parse my interval into registers (as k_lz4_decode) ----
+  uint32_t r_L[SEQ], r_DM[SEQ], r_lv[SEQ];  // r_lv: literal bytes (L <= 4) or the literal input offset
+#pragma unroll
+  for (int s = 0; s < SEQ; ++s) r_L[s] = r_DM[s] = r_lv[s] = 0;
+  int cnt = 0, out_rel = 0;
+  if (tid < ncp) {
+    int pos = (int)gld4(job.cp + tid);
+    const int end = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
+#pragma unroll
+    for (int s = 0; s < SEQ; ++s) {
+      if (pos < end) {
+        Tok t;
+        if (parse_tok(s_in, n, pos, t)) {
+          r_L[s] = (uint32_t)t.L;
+          r_DM[s] = (uint32_t)t.off | ((uint32_t)t.M << 16);
+          r_lv[s] = t.L <= kShortLit ? t.lv : (uint32_t)t.lit;
+          out_rel += t.L + t.M;
+          pos = t.next;
+          cnt = s + 1;
+        } else {
+          pos = -1;
+        }
+      }
+    }
+    if (pos != end) s_bad = 1;
+  }
+  int total;
+  const int base = block_scan_lz(out_rel, &total, s_tmp);
+  LZ_STAMP(2);
+  if (s_bad || total != job.dec_len) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  const uint32_t rkw[4] = {rk4.x, rk4.y, rk4.z, rk4.w}, fdw[4] = {fd4.x, fd4.y, fd4.z, fd4.w};
+  auto rank = [&](int s) { return (int)((rkw[s >> 1] >> (16 * (s & 1))) & 0xFFFFu); };
+  auto fdist = [&](int s) { return (fdw[s >> 1] >> (16 * (s & 1))) & 0xFFFFu; };  // the forwarded distance
+  // ---- 2. level 0: literals into the image; long runs become jobs split evenly over the threads ----
+  constexpr uint32_t kOwnLit = 0x80000000u;  // r_L flag: a long run the job table had no room for
+  {
+    int need = 0;
+#pragma unroll
+    for (int s = 0; s < SEQ; ++s)
+      if (s < cnt) need += (int)r_L[s] > kFlowLongLit;
+    int j = __ballot(need) ? wave_alloc(&s_njob, need) : 0;
+    int o = base;
+#pragma unroll
+    for (int s = 0; s < SEQ; ++s) {
+      if (s < cnt) {
+        const int L = (int)r_L[s], d = (int)(r_DM[s] & 0xFFFF), M = (int)(r_DM[s] >> 16);
+        if (L > kFlowLongLit) {
+          if (j < kFlowJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(L - 1) << 16), r_lv[s]);
+          else r_L[s] |= kOwnLit;
+          ++j;
+        } else if (L > kShortLit) {
+          flow_copyn<5>(s_out32, o, s_in32, (int)r_lv[s], L);
+        } else if (L > 0) {  // the literal bytes ride in r_lv: one or two dwords of the image
+          const int a = o & 3;
+          const uint64_t x = (uint64_t)(L == 4 ? r_lv[s] : (r_lv[s] & ((1u << (8 * L)) - 1u))) << (8 * a);
+          flow_put(s_out32, o >> 2, a, min(a + L, 4), (uint32_t)x);
+          if (a + L > 4) flow_put(s_out32, (o >> 2) + 1, 0, a + L - 4, (uint32_t)(x >> 32));
+        }
+        // (a forwarded distance reaches further back, to the same bytes: the schedule's own invariants)
+        if (M > 0 && (d > o + L || rank(s) >= kFlowMaxMatches || (int)fdist(s) > o + L ||
+                      (d >= M ? (int)fdist(s) < d : (int)fdist(s) != d)))
+          s_bad = 1;
+        o += L + M;
+      }
+    }
+  }
+  __syncthreads();
+  const int nj = min(s_njob, kFlowJobs);
+  if (nj > 0) {
+    int l0 = 0, l1 = 0;
+    if (2 * tid < nj) l0 = job_len(s_job[2 * tid]);
+    if (2 * tid + 1 < nj) l1 = job_len(s_job[2 * tid + 1]);
+    int tot;
+    const int pre = block_scan_lz(l0 + l1, &tot, s_tmp);
+    if (2 * tid < nj) s_jpre[2 * tid] = pre;
+    if (2 * tid + 1 < nj) s_jpre[2 * tid + 1] = pre + l0;
+    __syncthreads();
+    // my contiguous range of the flat job bytes, copied piece by piece (a piece lies in one run)
+    const int per = (tot + kLzThreads - 1) / kLzThreads;
+    const int g0 = tid * per, gend = min(g0 + per, tot);
+    if (g0 < gend) {
+      int lo = 0, hi = nj - 1;
+      while (lo < hi) {  // last job with s_jpre <= g0
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_jpre[mid] <= g0) lo = mid;
+        else hi = mid - 1;
+      }
+#pragma unroll 1
+      for (int g = g0, wj = lo; g < gend; ++wj) {
+        const int js = s_jpre[wj];
+        const uint2 jb = s_job[wj];
+        const int je = js + job_len(jb);
+        const int len = min(gend, je) - g;
+        flow_copy(s_out32, (int)(jb.x & 0xFFFF) + (g - js), s_in32, (int)jb.y + (g - js), len);
+        g += len;
+      }
+    }
+  }
+  if (tid < ncp) {  // long runs the job table had no room for: their own thread copies them. From
+                    // here on r_L holds the sequence's match start.
+    int o = base;
+#pragma unroll
+    for (int s = 0; s < SEQ; ++s) {
+      if (s < cnt) {
+        const int L = (int)(r_L[s] & ~kOwnLit);
+        if (r_L[s] & kOwnLit) flow_copy(s_out32, o, s_in32, (int)r_lv[s], L);
+        r_L[s] = (uint32_t)(o + L);
+        o += L + (int)(r_DM[s] >> 16);
+      }
+    }
+  }
+  LZ_STAMP(3);
+  __syncthreads();  // every literal is in the image; the staged input is dead
+  if (s_bad || s_lvl[job.nlvl] > kFlowMaxMatches) {
+    if (tid == 0) atomicOr(err, 1);
+    return;
+  }
+  // ---- 3. my matches into the table at their ranks: start | distance << 16, length ----
+#pragma unroll
+  for (int s = 0; s < SEQ; ++s)
+    if (s < cnt && (r_DM[s] >> 16) > 0) s_tab[rank(s)] = make_uint2(r_L[s] | (fdist(s) << 16), r_DM[s] >> 16);
+  __syncthreads();
+  LZ_STAMP(4);
+  // ---- 4. matches level by level (every source byte is of a lower level: complete) ----
+  uint64_t t_busy = 0, t_wait = 0;  // (PROF: this wave's cycles copying / waiting at the level barriers)
+#pragma unroll 1
+  for (int k = 1; k <= job.nlvl; ++k) {
+    const uint64_t t0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
+    const int r1 = s_lvl[k];
+#pragma unroll 1
+    for (int r = s_lvl[k - 1] + tid; r < r1; r += kLzThreads) {
+      const uint2 m = s_tab[r];
+      flow_match(s_out32, (int)(m.x & 0xFFFF), (int)(m.x >> 16), (int)m.y);
+    }
+    if (PROF) {
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      t_busy += t1 - t0;
+      __syncthreads();
+      t_wait += __builtin_amdgcn_s_memtime() - t1;
+    } else {
+      __syncthreads();
+    }
+  }
+  if (PROF && (tid & 63) == 0) {
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 16 + (tid >> 6)] = t_busy;
+    if (tid == 0) prof[(size_t)blockIdx.x * kLz4ProfWords + 12] = t_wait;
+  }
+  LZ_STAMP(5);
+  if (PROF && tid == 0) {
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 8] = (uint64_t)job.nlvl;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 9] = (uint64_t)n;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 10] = (uint64_t)nj;
+    prof[(size_t)blockIdx.x * kLz4ProfWords + 11] = (uint64_t)ncp;
+  }
+  // ---- 4. output: 16 bytes per 16-byte store (bytes past the block's end are zero) ----
+  uint64_t racc = job.red_dst ? red_identity(job) : 0ull;
+  const int nchunks = (total + 15) >> 4;
+  for (int c = tid; c < nchunks; c += kLzThreads) {
+    const uint4 v = reinterpret_cast<const uint4*>(s_out32 + kFlowPad)[c];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    out16(job, c, w, racc);
+  }
+  if (job.red_dst) red_finish(job, racc, s_red, kLzWaves);
+  if (PROF) {
+    __syncthreads();
+    LZ_STAMP(6);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Light decoder: blocks of at most kLtMaxCps checkpoint intervals (<= 2048 sequences) whose copy
 // chains are at most kLtMaxDepth hops long (attach-time classification, lz4_index_block). These are
 // the literal-heavy blocks of high-entropy columns (random dictionary ids, noisy doubles: one long
@@ -1564,6 +1909,11 @@ void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream
 
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
+  if (wide & kLzFlow) {  // (flow blocks are never wide)
+    if (d_prof) hipLaunchKernelGGL(k_lz4_decode_flow<true>, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
+    else hipLaunchKernelGGL(k_lz4_decode_flow<false>, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
+    return;
+  }
   if (wide) {
     if (d_prof) hipLaunchKernelGGL((k_lz4_decode<true, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
     else hipLaunchKernelGGL((k_lz4_decode<false, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);

@@ -180,12 +180,99 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
   }
 }
 
-int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine) {
+// The flow decoder's schedule of a validated block (kLzSeqPerCp sequences per checkpoint interval, g of
+// them used). Source forwarding: a match (not overlapping itself) whose source lies entirely inside the
+// output of one earlier such match copies the same bytes from that match's source, repeatedly — LZ4 HC
+// chains a 4-byte pattern through every earlier occurrence, so this shortens the chains (noisy doubles:
+// 24 -> 8 levels). Every match then gets its copy-chain level — one more than the highest level among
+// the bytes of its (forwarded) source; literal bytes are level 0 — and its rank in the block's matches
+// ordered by (level, position). Appended per interval: kLzSeqPerCp u16 ranks (0xFFFF: no match) and
+// kLzSeqPerCp u16 forwarded distances; then the u16 start of every level's ranks (nlvl + 1 of them, zero
+// padded to 16 bytes). Returns the highest level, or -1 above `cap` (nothing appended).
+static int lz4_flow_schedule(const uint8_t* in, int n, int64_t g, int cap, std::vector<uint8_t>* lv) {
+  struct Mt {
+    int om, M, fsrc, d;
+  };
+  thread_local std::vector<uint8_t> lev(kBlockBytes);
+  thread_local std::vector<int32_t> owner(kBlockBytes);  // the match that produced a byte, -1: a literal
+  thread_local std::vector<Mt> ms;
+  thread_local std::vector<int32_t> seqm;  // per sequence: its match's index in ms, -1: none
+  ms.clear();
+  seqm.clear();
+  int pos = 0, out = 0, mx = 0;
+  auto ext = [&](int* len) {
+    for (int b = 255; b == 255 && pos < n;) {
+      b = in[pos++];
+      *len += b;
+    }
+  };
+  for (;;) {
+    const int tok = in[pos++];
+    int L = tok >> 4;
+    if (L == 15) ext(&L);
+    memset(lev.data() + out, 0, (size_t)L);
+    std::fill(owner.begin() + out, owner.begin() + out + L, -1);
+    out += L;
+    pos += L;
+    if (pos >= n) {
+      seqm.push_back(-1);
+      break;
+    }
+    const int off = in[pos] | (in[pos + 1] << 8);
+    pos += 2;
+    int M = tok & 15;
+    if (M == 15) ext(&M);
+    M += 4;
+    int src = out - off;
+    if (off >= M) {  // forward through earlier non-overlapping matches holding the whole source
+      for (;;) {
+        const int j = owner[src];
+        if (j < 0 || ms[j].d < ms[j].M || src + M > ms[j].om + ms[j].M) break;
+        src = ms[j].fsrc + (src - ms[j].om);
+      }
+    }
+    const int span = std::min(out - src, M);
+    int v = 0;
+    for (int k = 0; k < span; ++k) v = std::max(v, (int)lev[src + k]);
+    if (++v > cap) return -1;
+    memset(lev.data() + out, v, (size_t)M);
+    std::fill(owner.begin() + out, owner.begin() + out + M, (int32_t)ms.size());
+    seqm.push_back((int32_t)ms.size());
+    ms.push_back(Mt{out, M, src, off});
+    mx = std::max(mx, v);
+    out += M;
+  }
+  std::vector<int> cnt(mx + 2, 0);
+  for (const Mt& m : ms) cnt[lev[m.om]]++;
+  std::vector<uint16_t> next(mx + 2, 0), st(mx + 1, 0);
+  for (int k = 1, acc = 0; k <= mx; ++k) {
+    next[k] = (uint16_t)acc;
+    acc += cnt[k];
+    st[k] = (uint16_t)acc;  // st[k - 1] .. st[k]: the ranks of level k
+  }
+  const int64_t m = ((int64_t)seqm.size() + g - 1) / g;
+  const size_t at = lv->size(), rec = 4 * kLzSeqPerCp;  // per interval: ranks, then distances
+  lv->resize(at + (size_t)m * rec + (((size_t)(mx + 1) * 2 + 15) & ~(size_t)15), 0);
+  for (int64_t i = 0; i < m; ++i)
+    for (int q = 0; q < kLzSeqPerCp; ++q) {
+      uint16_t* r = reinterpret_cast<uint16_t*>(lv->data() + at + (size_t)i * rec);
+      const int64_t sq = i * g + q;
+      const int j = q < g && sq < (int64_t)seqm.size() ? seqm[sq] : -1;
+      r[q] = j < 0 ? (uint16_t)0xFFFF : next[lev[ms[j].om]]++;
+      r[kLzSeqPerCp + q] = j < 0 ? (uint16_t)0 : (uint16_t)(ms[j].om - ms[j].fsrc);
+    }
+  memcpy(lv->data() + at + (size_t)m * rec, st.data(), (size_t)(mx + 1) * 2);
+  return mx;
+}
+
+int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* wide, int* light, int* nfine,
+                    std::vector<uint8_t>* levels, int* nlvl) {
+  if (nlvl) *nlvl = 0;
   const size_t first = cps->size();
   if (light) *light = 0;
   if (nfine) *nfine = 0;
   int pos = 0, out = 0;
-  int64_t seq = 0;
+  int64_t seq = 0, c8 = 0;  // c8: bytes copied from 8 back (distance-8 class chains)
   auto ext = [&](int* len) {
     for (;;) {
       if (pos >= n) return false;
@@ -232,6 +319,7 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
         *light = 1;
       }
     }
+    int64_t gi = *wide ? kLzMaxSeqPerCp : kLzSeqPerCp;  // sequences per checkpoint interval
     if (!*wide && !(light && *light)) {
       // a general block of fewer than kLzMaxCps * kLzSeqPerCp sequences: intervals of the fewest
       // sequences that still give one per decoder thread, so every wave parses and fills
@@ -239,6 +327,16 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
       if (g < kLzSeqPerCp) {
         cps->resize(first);
         push_every(g);
+        gi = g;
+      }
+    }
+    // a general block (not wide) that is not a class chain and whose copy chains are short: the flow
+    // decoder, with its schedule
+    if (levels && !*wide && !(light && *light) && c8 * 4 <= dec) {
+      const int mx = lz4_flow_schedule(in, n, gi, kFlowMaxDepth, levels);
+      if (mx >= 0) {
+        *wide |= kLzFlow;
+        if (nlvl) *nlvl = mx;
       }
     }
     return dec;
@@ -262,6 +360,7 @@ int lz4_index_block(const uint8_t* in, int n, std::vector<uint32_t>* cps, int* w
     M += 4;
     if (off == 0 || off > out || M > kBlockBytes - out) return -1;
     out += M;
+    if (off == 8) c8 += M;
   }
 }
 
@@ -311,9 +410,12 @@ int lz4_literal_start(const uint8_t* in, int n) {
   return L > 0 && L <= kBlockBytes && q + L == n ? q : -1;
 }
 
-bool run_decode_enabled() {
-  const char* off = getenv("DG_NO_RUN_DECODE");
-  return !(off && *off && *off != '0');
+int decode_routes() {
+  auto off = [](const char* v) {
+    const char* e = getenv(v);
+    return e && *e && *e != '0';
+  };
+  return (off("DG_NO_RUN_DECODE") ? 0 : kRouteRun) | (off("DG_NO_FLOW_DECODE") ? 0 : kRouteFlow);
 }
 
 // The run index of a validated block (layout: dg_internal.h, kRunThreads): the block is decoded once
@@ -431,7 +533,9 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     col->cp_fine.assign(blocks.n, 0);
     col->dec_len.assign(blocks.n, 0);
     std::vector<std::vector<uint32_t>> per(blocks.n);
-    std::vector<std::vector<uint8_t>> runs(blocks.n);
+    std::vector<std::vector<uint8_t>> runs(blocks.n), lvls(blocks.n);
+    col->lvl_off.assign(blocks.n, -1);
+    col->lvl_n.assign(blocks.n, 0);
     col->run_n.assign(blocks.n, 0);
     col->run_far.assign(blocks.n, 0);
     col->run_off.assign(blocks.n, -1);
@@ -447,9 +551,11 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
     for (int t = 0; t < nt; ++t)
       th.emplace_back([&, t] {
         for (int32_t b = t; b < blocks.n; b += nt) {
-          int wide = 0, light = 0, nfine = 0;
-          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine);
+          int wide = 0, light = 0, nfine = 0, nlvl = 0;
+          const int d = lz4_index_block(host.data() + col->comp_off[b], col->comp_len[b], &per[b], &wide, &light, &nfine,
+                                        &lvls[b], &nlvl);
           col->cp_wide[b] = (uint8_t)wide;
+          col->lvl_n[b] = nlvl;
           col->cp_light[b] = (uint8_t)light;
           col->cp_fine[b] = nfine;
           col->dec_len[b] = d;
@@ -482,7 +588,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
         col->max8.clear();
       }
     std::vector<uint32_t> all;
-    std::vector<uint8_t> rall;
+    std::vector<uint8_t> rall, lall;
     col->index_bytes = 0;
     for (int32_t b = 0; b < blocks.n; ++b) {
       col->cp_off[b] = (int64_t)all.size();
@@ -493,7 +599,18 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
         col->index_bytes += (int64_t)runs[b].size();
       } else if (col->cp_n[b] > 0) {
         col->index_bytes += 4 * (int64_t)per[b].size();
+        if (!lvls[b].empty()) col->index_bytes += (int64_t)lvls[b].size();  // + a flow block's schedule
       }
+      if ((col->cp_wide[b] & kLzFlow) && !lvls[b].empty()) {
+        col->lvl_off[b] = (int64_t)lall.size();
+        lall.insert(lall.end(), lvls[b].begin(), lvls[b].end());
+      } else {
+        col->cp_wide[b] &= (uint8_t)~kLzFlow;
+      }
+    }
+    if (!lall.empty()) {
+      if (!col->lvls.alloc(lall.size())) return set_error(DG_ERR_OOM, "hipMalloc lz4 level schedules");
+      DG_HIP(hipMemcpy(col->lvls.p, lall.data(), lall.size(), hipMemcpyHostToDevice));
     }
     if (all.empty()) all.push_back(0);
     if (!col->cps.alloc(all.size() * 4)) return set_error(DG_ERR_OOM, "hipMalloc lz4 index");

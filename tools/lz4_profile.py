@@ -18,7 +18,7 @@ S = importlib.import_module("incubator-druid_amd.segment")
 W = importlib.import_module("incubator-druid_amd.writer")
 BLOCK = 65536
 PHASES = ["stage", "parse+scan", "jobs+read", "fill+write", "resolve", "output"]
-KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light"}
+KINDS = {-1: "malformed", 0: "general", 1: "general-wide", 2: "light", 3: "run", 4: "flow"}
 
 
 def classify(block):
@@ -68,6 +68,10 @@ def report(name, ms, p, decoder=""):
           f"jump_rounds(avg/max)={p[:, 8].mean():5.1f}/{p[:, 8].max():3d} coop_jobs={p[:, 10].mean():6.1f} "
           f"cps={p[:, 11].mean():6.1f} listed={p[:, 7].mean():7.0f}")
     print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(PHASES, d.mean(axis=0))))
+    if "flow" in decoder:
+        busy = p[:, 16:32]
+        print(f"   levels: busy cycles per wave (mean over blocks) max={busy.max(axis=1).mean():8.0f} "
+              f"mean={busy.mean():8.0f}; wave 0 barrier wait={p[:, 12].mean():8.0f}")
     if decoder != "general":
         return
     sub = {"scan1": p[:, 12] - p[:, 4], "scan2": p[:, 13] - p[:, 12], "rounds": p[:, 5] - p[:, 13]}
