@@ -423,6 +423,9 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
     return;
   }
   LZ_STAMP(0);
+  // my interval's token offsets, loaded with the staging (not after it)
+  const int cp0 = tid < ncp ? (int)gld4(job.cp + tid) : 0;
+  const int cp1 = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
   uint8_t* s_in = reinterpret_cast<uint8_t*>(s_e);
   uint32_t* s_e32 = reinterpret_cast<uint32_t*>(s_e);
   const LzState S{s_e, s_tsrc};
@@ -445,8 +448,8 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   uint32_t r_L[SEQ], r_DM[SEQ], r_lv[SEQ];  // r_lv: literal bytes (L <= 4) or offset
   int cnt = 0, out_rel = 0;
   if (tid < ncp) {
-    int pos = (int)gld4(job.cp + tid);
-    const int end = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
+    int pos = cp0;
+    const int end = cp1;
 #pragma unroll
     for (int s = 0; s < SEQ; ++s) {
       if (pos < end) {
@@ -1137,6 +1140,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 // ------------------------------------------------------------------------------------------------
 constexpr int kFlowJobs = 1024;     // cooperative literal runs per block
 constexpr int kFlowLongLit = 16;    // literal runs longer than this are split over the threads
+constexpr int kFlowRegLit = 8;      // literal runs up to this ride in the parse registers
 constexpr int kFlowPad = 4;         // dwords before the staged input and the image: a copy's first
                                     // source dword may start up to 3 bytes before its source
 constexpr int kFlowInWords = kFlowPad + (kLz4InCap + 32) / 4 + 8;  // (+ the unconditional reads past a copy)
@@ -1151,20 +1155,13 @@ __device__ __forceinline__ uint32_t lds_ld8(const uint32_t* a, int p) {
   return reinterpret_cast<const uint8_t*>(a + kFlowPad)[p];
 }
 
-// destination dword j (image word kFlowPad + j) gets bytes b0 .. b1 - 1 of w: an LDS atomic OR into the
-// zeroed image (a neighbouring run may own the dword's other bytes)
-__device__ __forceinline__ void flow_put(uint32_t* o32, int j, int b0, int b1, uint32_t w) {
-  const uint32_t m = (0xFFFFFFFFu << (8 * b0)) & (0xFFFFFFFFu >> (8 * (4 - b1)));
-  lds_or(o32 + kFlowPad + j, w & m);
-}
-
 // the byte mask of destination dword t (0 .. NJ - 1) of a run [dst, dst + len) whose first dword is
-// dst >> 2: full inside, cut at the run's two ends, empty past it
+// dst >> 2: its bytes below the run's end (k = the run's end - 4t, clamped to 0 .. 4), and in dword 0 from
+// the run's start
 __device__ __forceinline__ uint32_t run_mask(int t, int dst, int len) {
-  const int nj = ((dst + len - 1) >> 2) - (dst >> 2) + 1;
-  uint32_t m = t == 0 ? 0xFFFFFFFFu << (8 * (dst & 3)) : 0xFFFFFFFFu;
-  if (t == nj - 1) m &= 0xFFFFFFFFu >> (8 * (3 - ((dst + len - 1) & 3)));
-  return t < nj ? m : 0u;
+  const int k = min(max((dst & 3) + len - 4 * t, 0), 4);
+  const uint32_t m = (uint32_t)((1ull << (8 * k)) - 1ull);
+  return t == 0 ? m & (0xFFFFFFFFu << (8 * (dst & 3))) : m;
 }
 
 // bytes [dst, dst + len) of the image o32 <- bytes [src, src + len) of i32 (padded LDS byte arrays,
@@ -1237,6 +1234,46 @@ __device__ __forceinline__ void flow_copy(uint32_t* o32, int dst, const uint32_t
   for (int k = 0; k < len; k += 16) flow_copyn<5>(o32, dst + k, i32, src + k, min(16, len - k));
 }
 
+// The flow decoder's parse: one 16-byte window (four aligned dword reads, one LDS round trip) holds a
+// token, up to 8 literal bytes and the distance; the literal bytes ride along in lv / lv_hi (L <= 8).
+// Longer runs, extended lengths: parse_tok_slow.
+__device__ __forceinline__ bool parse_tok8(const uint8_t* __restrict__ in, int n, int p, Tok& t, uint32_t& lv_hi) {
+  if (p >= n) return false;
+  const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
+  const int a = p >> 2, sh = p & 3;
+  const uint32_t d0 = in32[a], d1 = in32[a + 1], d2 = in32[a + 2], d3 = in32[a + 3];
+  const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, sh), b1 = __builtin_amdgcn_alignbyte(d2, d1, sh),
+                 b2 = __builtin_amdgcn_alignbyte(d3, d2, sh);  // bytes p .. p + 11
+  const int tk = (int)(b0 & 0xFF);
+  const int L = tk >> 4, M = tk & 15;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(b1, b0, 1), hi = __builtin_amdgcn_alignbyte(b2, b1, 1);  // bytes 1 .. 8
+  if (L > 8 || M == 15) {
+    const bool ok = parse_tok_slow(in, n, p, t);
+    t.lv = lo;
+    lv_hi = hi;
+    return ok;
+  }
+  const int q = p + 1 + L;
+  t.lit = p + 1;
+  t.L = L;
+  t.lv = lo;
+  lv_hi = hi;
+  if (q > n) return false;
+  if (q == n) {
+    t.off = 0;
+    t.M = 0;
+    t.next = n;
+    return true;
+  }
+  if (q + 2 > n) return false;
+  const int k = L + 1;  // the distance: window bytes k, k + 1 (k <= 9)
+  const uint64_t w01 = (uint64_t)b0 | ((uint64_t)b1 << 32), w12 = (uint64_t)b1 | ((uint64_t)b2 << 32);
+  t.off = (int)((k <= 6 ? (w01 >> (8 * k)) : (w12 >> (8 * (k - 4)))) & 0xFFFF);
+  t.M = M + 4;
+  t.next = q + 2;
+  return t.off != 0;
+}
+
 template <bool PROF>
 __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
                                                                 uint64_t* __restrict__ prof) {
@@ -1264,6 +1301,9 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   // my matches' table rows (u16 each, 0xFFFF: none) and the levels' row ranges
   const uint4 rk4 = tid < ncp ? gld16(job.lvl + (size_t)tid * 4 * SEQ) : make_uint4(~0u, ~0u, ~0u, ~0u);
   const uint4 fd4 = tid < ncp ? gld16(job.lvl + (size_t)tid * 4 * SEQ + 2 * SEQ) : make_uint4(0u, 0u, 0u, 0u);
+  // my interval's token offsets, loaded with the staging (not after it)
+  const int cp0 = tid < ncp ? (int)gld4(job.cp + tid) : 0;
+  const int cp1 = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
   if (tid <= job.nlvl) {
     const uint8_t* st = job.lvl + 4 * SEQ * (size_t)ncp;
     s_lvl[tid] = (int)(gld4(st + 2 * tid - 2 * (tid & 1)) >> (16 * (tid & 1))) & 0xFFFF;
@@ -1283,21 +1323,24 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   __syncthreads();
   LZ_STAMP(1);
   // ---- 1. parse my interval into registers (as k_lz4_decode) ----
-  uint32_t r_L[SEQ], r_DM[SEQ], r_lv[SEQ];  // r_lv: literal bytes (L <= 4) or the literal input offset
+  // r_lv / r_lvh: the literal bytes (L <= kFlowRegLit), or in r_lv the literal input offset
+  uint32_t r_L[SEQ], r_DM[SEQ], r_lv[SEQ], r_lvh[SEQ];
 #pragma unroll
-  for (int s = 0; s < SEQ; ++s) r_L[s] = r_DM[s] = r_lv[s] = 0;
+  for (int s = 0; s < SEQ; ++s) r_L[s] = r_DM[s] = r_lv[s] = r_lvh[s] = 0;
   int cnt = 0, out_rel = 0;
   if (tid < ncp) {
-    int pos = (int)gld4(job.cp + tid);
-    const int end = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
+    int pos = cp0;
+    const int end = cp1;
 #pragma unroll
     for (int s = 0; s < SEQ; ++s) {
       if (pos < end) {
         Tok t;
-        if (parse_tok(s_in, n, pos, t)) {
+        uint32_t hi;
+        if (parse_tok8(s_in, n, pos, t, hi)) {
           r_L[s] = (uint32_t)t.L;
           r_DM[s] = (uint32_t)t.off | ((uint32_t)t.M << 16);
-          r_lv[s] = t.L <= kShortLit ? t.lv : (uint32_t)t.lit;
+          r_lv[s] = t.L <= kFlowRegLit ? t.lv : (uint32_t)t.lit;
+          r_lvh[s] = hi;
           out_rel += t.L + t.M;
           pos = t.next;
           cnt = s + 1;
@@ -1335,22 +1378,26 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
           if (j < kFlowJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(L - 1) << 16), r_lv[s]);
           else r_L[s] |= kOwnLit;
           ++j;
-        } else if (L > kShortLit) {
+        } else if (L > kFlowRegLit) {
           flow_copyn<5>(s_out32, o, s_in32, (int)r_lv[s], L);
-        } else if (L > 0) {  // the literal bytes ride in r_lv: one or two dwords of the image
+        } else if (L > 0) {  // the literal bytes ride in r_lv / r_lvh: cut to L bytes, up to three ORs, no reads
           const int a = o & 3;
-          const uint64_t x = (uint64_t)(L == 4 ? r_lv[s] : (r_lv[s] & ((1u << (8 * L)) - 1u))) << (8 * a);
-          flow_put(s_out32, o >> 2, a, min(a + L, 4), (uint32_t)x);
-          if (a + L > 4) flow_put(s_out32, (o >> 2) + 1, 0, a + L - 4, (uint32_t)(x >> 32));
+          const uint64_t x = ((uint64_t)r_lv[s] | ((uint64_t)r_lvh[s] << 32)) & (~0ull >> (64 - 8 * L));
+          const uint64_t xs = x << (8 * a);
+          lds_or(s_out32 + kFlowPad + (o >> 2), (uint32_t)xs);
+          if (a + L > 4) lds_or(s_out32 + kFlowPad + (o >> 2) + 1, (uint32_t)(xs >> 32));
+          if (a + L > 8) lds_or(s_out32 + kFlowPad + (o >> 2) + 2, (uint32_t)(x >> (64 - 8 * a)));
         }
-        // (a forwarded distance reaches further back, to the same bytes: the schedule's own invariants)
-        if (M > 0 && (d > o + L || rank(s) >= kFlowMaxMatches || (int)fdist(s) > o + L ||
-                      (d >= M ? (int)fdist(s) < d : (int)fdist(s) != d)))
+        // a match's (forwarded) source inside the block, its table row inside the table (the attach-time
+        // parse validated the stream; these keep a damaged index from reaching outside the image)
+        if (M > 0 && ((unsigned)(d - 1) >= (unsigned)(o + L) || (unsigned)(fdist(s) - 1) >= (unsigned)(o + L) ||
+                      rank(s) >= kFlowMaxMatches))
           s_bad = 1;
         o += L + M;
       }
     }
   }
+  LZ_STAMP(13);
   __syncthreads();
   const int nj = min(s_njob, kFlowJobs);
   if (nj > 0) {
@@ -1362,6 +1409,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
     if (2 * tid < nj) s_jpre[2 * tid] = pre;
     if (2 * tid + 1 < nj) s_jpre[2 * tid + 1] = pre + l0;
     __syncthreads();
+    LZ_STAMP(14);
     // my contiguous range of the flat job bytes, copied piece by piece (a piece lies in one run)
     const int per = (tot + kLzThreads - 1) / kLzThreads;
     const int g0 = tid * per, gend = min(g0 + per, tot);
@@ -1383,6 +1431,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
       }
     }
   }
+  LZ_STAMP(15);
   if (tid < ncp) {  // long runs the job table had no room for: their own thread copies them. From
                     // here on r_L holds the sequence's match start.
     int o = base;

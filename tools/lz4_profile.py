@@ -69,6 +69,9 @@ def report(name, ms, p, decoder=""):
           f"cps={p[:, 11].mean():6.1f} listed={p[:, 7].mean():7.0f}")
     print("   cycles/phase (mean): " + "  ".join(f"{nm}={v:8.0f}" for nm, v in zip(PHASES, d.mean(axis=0))))
     if "flow" in decoder:
+        sub = {"literals": p[:, 13] - p[:, 2], "job_scan": p[:, 14] - p[:, 13], "job_copy": p[:, 15] - p[:, 14],
+               "own": p[:, 3] - p[:, 15]}
+        print("   literal phase (wave 0, mean): " + "  ".join(f"{nm}={v.mean():8.0f}" for nm, v in sub.items()))
         busy = p[:, 16:32]
         print(f"   levels: busy cycles per wave (mean over blocks) max={busy.max(axis=1).mean():8.0f} "
               f"mean={busy.mean():8.0f}; wave 0 barrier wait={p[:, 12].mean():8.0f}")
