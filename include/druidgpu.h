@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 14
+#define DG_ABI_VERSION 15
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -416,6 +416,12 @@ int dg_result_fetch_groups(dg_result* res, int64_t start, int64_t count, int64_t
  * buffers are allocated once at startup (OffheapBufferGenerator.java:53 allocateDirect). */
 int dg_host_alloc(int64_t bytes, void** out);
 void dg_host_free(void* p);
+/* Phase timing (since ABI 15, process-wide, on by default): the dg_metrics *_ms phase times come from
+ * GPU timestamps the calls record between their launch groups. A small query pays ~25 us for them
+ * (configs[0]), so a caller timing queries end to end turns them off and samples phases in separate
+ * calls (the phase fields then read 0). No reference counterpart: the reference's per-query metrics
+ * (QueryMetrics reportSegmentTime etc.) are host wall times. */
+int dg_set_phase_timing(int32_t on);
 /* rows aggregated into each group of [start, start + count) */
 int dg_result_fetch_rows(dg_result* res, int64_t start, int64_t count, int64_t* rows);
 /* merged dictionary of dimension `dim` (the union of the segments' dictionaries, Java String

@@ -135,7 +135,7 @@ EXPORTS = [
     "dg_result_dim_dictionary", "dg_result_release", "dg_keyspace_bits", "dg_result_export", "dg_keys_partition",
     "dg_merge", "dg_records_pack", "dg_debug_lz4_decode", "dg_result_limit",
     "dg_segment_from_rows", "dg_context_set_limit", "dg_groupby_merge_devices", "dg_timeseries_merge",
-    "dg_debug_lz4_classify", "dg_host_alloc", "dg_host_free",
+    "dg_debug_lz4_classify", "dg_host_alloc", "dg_host_free", "dg_set_phase_timing",
 ]
 
 _lib = None
@@ -204,6 +204,7 @@ def lib():
         "dg_debug_lz4_classify": (ctypes.c_int, [vp, i32, P(i32)]),
         "dg_host_alloc": (ctypes.c_int, [i64, P(vp)]),
         "dg_host_free": (None, [vp]),
+        "dg_set_phase_timing": (ctypes.c_int, [ctypes.c_int32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(l, name)

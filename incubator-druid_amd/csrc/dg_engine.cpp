@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <thread>
 #include <functional>
@@ -212,6 +213,11 @@ struct CallScratch {
   // at the call's final synchronisation instead of after every kernel
   int32_t* d_err = nullptr;
   int32_t* h_err = nullptr;
+  // the call's filtered-row counts (build_bitset): one zeroed staged block, read back once with the
+  // error word at the call's final synchronisation instead of one copy per filter
+  unsigned long long* cnt_d = nullptr;
+  unsigned long long* cnt_h = nullptr;
+  int cnt_used = 0;
   Context* ctx = nullptr;
   // algorithmic bytes of the call's filter bitmaps (dg_metrics.bitmap_bytes): serialized bitmaps
   // read + every row bitset written and read once
@@ -223,6 +229,9 @@ struct CallScratch {
     up.reset();
     d_err = nullptr;
     h_err = nullptr;
+    cnt_d = nullptr;
+    cnt_h = nullptr;
+    cnt_used = 0;
     bitmap_bytes = 0;
     intr = nullptr;
   }
@@ -262,6 +271,47 @@ static T* up_take(CallScratch* cs, size_t count, T** dev, hipStream_t st) {
     if (!(cs)->up.flush(st)) return ::dg::set_error(DG_ERR_DEVICE, "staged upload failed"); \
   } while (0)
 
+// A phase-timing event (dg_metrics' *_ms fields). dg_set_phase_timing(0) or DG_NO_PHASE_EVENTS=1 leaves
+// them out (the phase times then read 0): a small query pays ~25 us for the timestamps.
+static std::atomic<bool> g_phase_timing{true};
+static bool phase_events_off() {
+  static const bool env_off = [] {
+    const char* v = getenv("DG_NO_PHASE_EVENTS");
+    return v && *v && *v != '0';
+  }();
+  return env_off || !g_phase_timing.load(std::memory_order_relaxed);
+}
+static void phase_event(hipEvent_t e, hipStream_t st) {
+  if (!phase_events_off()) hipEventRecord(e, st);
+}
+static hipError_t phase_elapsed(float* ms, hipEvent_t a, hipEvent_t b) {
+  if (phase_events_off()) {
+    *ms = 0.f;
+    return hipSuccess;
+  }
+  return hipEventElapsedTime(ms, a, b);
+}
+
+// a zeroed device word for a filter's row count and its host copy (valid after finish_call); null when
+// the call's count block is full (the caller then reads its count itself)
+static unsigned long long* count_slot(CallScratch* cs, hipStream_t st, unsigned long long** host) {
+  constexpr int kCountSlots = 64;
+  if (!cs->cnt_d) {
+    unsigned long long* z = up_take<unsigned long long>(cs, kCountSlots, &cs->cnt_d, st);
+    cs->cnt_h = host_take<unsigned long long>(cs, kCountSlots);
+    if (!z || !cs->cnt_h) {
+      cs->cnt_d = nullptr;
+      return nullptr;
+    }
+    memset(z, 0, 8 * kCountSlots);
+  }
+  if (cs->cnt_used >= kCountSlots) return nullptr;
+  *host = cs->cnt_h + cs->cnt_used;
+  return cs->cnt_d + cs->cnt_used++;
+}
+
+constexpr size_t kStagedAccBytes = 64 << 10;  // accumulator tables up to this start in the call's upload
+
 static int32_t* call_err(CallScratch* cs, hipStream_t st) {
   if (!cs->d_err) {
     int32_t* z = up_take<int32_t>(cs, 1, &cs->d_err, st);  // zeroed by the next flush
@@ -278,6 +328,7 @@ static int32_t* call_err(CallScratch* cs, hipStream_t st) {
 // drains (it owns the context's scratch) and the call then returns the interruption.
 static int finish_call(CallScratch* cs, hipStream_t st) {
   DG_FLUSH(cs, st);
+  if (cs->cnt_used) DG_HIP(hipMemcpyAsync(cs->cnt_h, cs->cnt_d, 8 * (size_t)cs->cnt_used, hipMemcpyDeviceToHost, st));
   if (cs->d_err) DG_HIP(hipMemcpyAsync(cs->h_err, cs->d_err, 4, hipMemcpyDeviceToHost, st));
   if (cs->intr && cs->intr->active()) {
     int irc = DG_OK;
@@ -468,7 +519,7 @@ struct DecodeBatch {
 static double gen_ms(const DecodeBatch& db) {
   if (!db.gen_blocks || !db.gen_a) return 0;
   float f = 0;
-  hipEventElapsedTime(&f, db.gen_a, db.gen_b);
+  phase_elapsed(&f, db.gen_a, db.gen_b);
   return f;
 }
 // the decode-timing events of a call's main (side = false) or side batch
@@ -484,10 +535,10 @@ static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_me
   m->lz4_general_wall_ms = m->lz4_general_ms;
   if (db.gen_blocks && side.gen_blocks && db.gen_a && side.gen_a && base) {
     float s1 = 0, e1 = 0, s2 = 0, e2 = 0;
-    hipEventElapsedTime(&s1, base, db.gen_a);
-    hipEventElapsedTime(&e1, base, db.gen_b);
-    hipEventElapsedTime(&s2, base, side.gen_a);
-    hipEventElapsedTime(&e2, base, side.gen_b);
+    phase_elapsed(&s1, base, db.gen_a);
+    phase_elapsed(&e1, base, db.gen_b);
+    phase_elapsed(&s2, base, side.gen_a);
+    phase_elapsed(&e2, base, side.gen_b);
     const double overlap = std::max(0.0, (double)std::min(e1, e2) - (double)std::max(s1, s2));
     m->lz4_general_wall_ms = (double)(e1 - s1) + (double)(e2 - s2) - overlap;
   }
@@ -933,7 +984,7 @@ static int plan_node(const Segment* seg, const dg_filter* nodes, int n, int* pos
 }
 
 // Build the row bitset of `filter` for segment `seg` on the device. *out = nullptr means "all rows".
-// The bitset's cardinality lands in the pinned word *count once the stream reaches this point
+// The bitset's cardinality lands in the pinned word *count once finish_call has synchronised
 // (nullptr when there is no filter: every row). Nothing here synchronises.
 static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, int n_filter, uint32_t** out,
                         const unsigned long long** count, hipStream_t st) {
@@ -956,6 +1007,19 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
   if (maxd > 16) return set_error(DG_ERR_UNSUPPORTED, "filter nesting too deep");
   const int64_t nwords = (seg->nrows + 31) / 32;
   const int nleaves = (int)fp.leaf_ids.size();
+  // the program and the row count staged first: the leaves' upload carries them
+  const int plen = (int)fp.prog.size();
+  int32_t* d_prog;
+  int32_t* h_prog = up_take<int32_t>(cs, plen + 2, &d_prog, st);  // (+ a zeroed count word when no slot)
+  if (!h_prog) return set_error(DG_ERR_OOM, "filter program");
+  memcpy(h_prog, fp.prog.data(), plen * 4);
+  unsigned long long* h_count = nullptr;
+  unsigned long long* d_count = count_slot(cs, st, &h_count);
+  const bool own_count = d_count == nullptr;
+  if (own_count) {
+    d_count = reinterpret_cast<unsigned long long*>(d_prog + ((plen + 1) & ~1));
+    memset(h_prog + ((plen + 1) & ~1), 0, 8);
+  }
   uint32_t** d_sets;
   uint32_t** h_sets = up_take<uint32_t*>(cs, std::max(nleaves, 1), &d_sets, st);
   uint32_t* leaf_mem = dev_take<uint32_t>(cs, (size_t)std::max(nleaves, 1) * (nwords + 2));
@@ -1079,18 +1143,14 @@ static int build_bitset(Segment* seg, CallScratch* cs, const dg_filter* filter, 
     cs->bitmap_bytes += seg->nrows * (int64_t)std::max(v.width, 1);  // the predicate's column
   }
   cs->bitmap_bytes += (2 * (int64_t)nleaves + 1) * nwords * 4;  // leaf bitsets written + read, the result
-  const int plen = (int)fp.prog.size();
-  int32_t* d_prog;
-  int32_t* h_prog = up_take<int32_t>(cs, plen + 2, &d_prog, st);  // + the zeroed 8-byte count
-  if (!h_prog) return set_error(DG_ERR_OOM, "filter program");
-  memcpy(h_prog, fp.prog.data(), plen * 4);
-  unsigned long long* d_count = reinterpret_cast<unsigned long long*>(d_prog + ((plen + 1) & ~1));
-  memset(h_prog + ((plen + 1) & ~1), 0, 8);
   uint32_t* result = dev_take<uint32_t>(cs, (size_t)nwords + 2);
   DG_FLUSH(cs, st);
   launch_filter_eval(d_prog, plen, d_sets, result, seg->nrows, d_count, st);
-  unsigned long long* h_count = host_take<unsigned long long>(cs, 1);
-  DG_HIP(hipMemcpyAsync(h_count, d_count, 8, hipMemcpyDeviceToHost, st));
+  if (own_count) {
+    h_count = host_take<unsigned long long>(cs, 1);
+    if (!h_count) return set_error(DG_ERR_OOM, "filter count");
+    DG_HIP(hipMemcpyAsync(h_count, d_count, 8, hipMemcpyDeviceToHost, st));
+  }
   *count = h_count;
   *out = result;
   return DG_OK;
@@ -1355,10 +1415,10 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   for (int i = nr; i < nh; ++i) db->gen_bytes += J[i].src_len;
   db->gen_blocks += ng;
   for (int w = 0; w < 4; ++w) db->gen_launches += kb[w + 1] > kb[w];
-  if (db->gen_a && ng) hipEventRecord(db->gen_a, st);
+  if (db->gen_a && ng) phase_event(db->gen_a, st);
   for (int w = 0; w < 4; ++w)
     launch_lz4_decode(d + kb[w], kb[w + 1] - kb[w], w, d_err, st, d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
-  if (db->gen_a && ng) hipEventRecord(db->gen_b, st);
+  if (db->gen_a && ng) phase_event(db->gen_b, st);
   if (ovl) DG_HIP(hipStreamWaitEvent(st, ctx->ovl_ev[1], 0));
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
@@ -2304,9 +2364,10 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   std::vector<int64_t> tiles_rows(n, 0);
   std::vector<const unsigned long long*> counts(n, nullptr);
   const bool fsum = has_float_sum(plan);
+  std::vector<char> staged_acc(n, 0);
   DecodeBatch db;
   decode_events(ctx, &db, false);
-  hipEventRecord(ctx->ev[0], st);
+  phase_event(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
     cur[i] = plan_cursors(seg, i, q, gr);
@@ -2336,7 +2397,17 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
       rc = time_view(tcol, tb, cs, &db, &j.time, st);
       if (rc) return rc;
     }
-    j.out = dev_take<uint64_t>(cs, (size_t)cur[i].nbuckets * rec);
+    // the accumulators: a small table starts as identities in the call's upload (no fill kernel)
+    const size_t outn = (size_t)cur[i].nbuckets * rec;
+    if (outn * 8 <= kStagedAccBytes) {
+      uint64_t* h = up_take<uint64_t>(cs, outn, &j.out, st);
+      if (!h) return set_error(DG_ERR_OOM, "accumulators");
+      for (int64_t b = 0; b < cur[i].nbuckets; ++b)
+        for (int k = 0; k < rec; ++k) h[b * rec + k] = k == 0 ? 0ull : identity_host(plan.kind[k - 1]);
+      staged_acc[i] = 1;
+    } else {
+      j.out = dev_take<uint64_t>(cs, outn);
+    }
     if (!j.out) return set_error(DG_ERR_OOM, "accumulators");
     for (int a = 0; a < na; ++a) {
       rc = 1;
@@ -2353,14 +2424,8 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   SlotInit init{};
   for (int a = 0; a < na; ++a) init.v[1 + a] = identity_host(plan.kind[a]);
   for (int i = 0; i < n; ++i)
-    if (cur[i].any) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, init, st);
-  hipEventRecord(ctx->ev[1], st);
-  rc = run_decodes(cs, &db, st, nullptr, true);
-  if (rc) return rc;
-  hipEventRecord(ctx->ev[2], st);
-  ht.mark("decode_launched");
-  m.bytes_read = db.bytes;
-  DG_CHECK_INTERRUPT(intr);
+    if (cur[i].any && !staged_acc[i]) launch_fill_u64(jobs[i].out, cur[i].nbuckets, rec, init, st);
+  // the scan's tile table and jobs staged before the decode: one upload carries them with its jobs
   std::vector<int32_t> begin;
   int ntiles = 0;
   for (int i = 0; i < n; ++i)
@@ -2372,8 +2437,15 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   ScanJob* h_jobs = up_take<ScanJob>(cs, n, &d_jobs, st);
   if (!h_jobs) return set_error(DG_ERR_OOM, "scan jobs");
   memcpy(h_jobs, jobs.data(), sizeof(ScanJob) * n);
-  DG_FLUSH(cs, st);
-  hipEventRecord(ctx->ev[3], st);
+  phase_event(ctx->ev[1], st);
+  rc = run_decodes(cs, &db, st, nullptr, true);
+  if (rc) return rc;
+  phase_event(ctx->ev[2], st);
+  ht.mark("decode_launched");
+  m.bytes_read = db.bytes;
+  DG_CHECK_INTERRUPT(intr);
+  DG_FLUSH(cs, st);  // (a no-op unless the decode staged nothing)
+  phase_event(ctx->ev[3], st);
   launch_scan_agg(d_jobs, d_tile, ntiles, plan, 0, st);
   DG_CHECK_INTERRUPT(intr);
   if (fsum) {
@@ -2407,7 +2479,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     rc = fsum_pass(cs, gj, frows, bb + bits_for(n), false, plan, st, gr.desc);
     if (rc) return rc;
   }
-  hipEventRecord(ctx->ev[4], st);
+  phase_event(ctx->ev[4], st);
   // results
   std::vector<uint64_t*> h_out(n, nullptr);
   for (int i = 0; i < n; ++i) {
@@ -2432,9 +2504,9 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     }
   }
   float f1 = 0, f2 = 0, f3 = 0;
-  hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
-  hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
-  hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
+  phase_elapsed(&f1, ctx->ev[0], ctx->ev[1]);
+  phase_elapsed(&f2, ctx->ev[1], ctx->ev[2]);
+  phase_elapsed(&f3, ctx->ev[3], ctx->ev[4]);
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
@@ -2518,7 +2590,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   DecodeBatch db;
   decode_events(ctx, &db, false);
   bool any_multi = false;
-  hipEventRecord(ctx->ev[0], st);
+  phase_event(ctx->ev[0], st);
   for (int i = 0; i < n; ++i) {
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
     cur[i] = plan_cursors(seg, i, q, gr);
@@ -2569,13 +2641,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     tiles_rows[i] = seg->nrows;
   }
   DG_CHECK_INTERRUPT(intr);
-  hipEventRecord(ctx->ev[1], st);
+  phase_event(ctx->ev[1], st);
   ht.mark("planned");
-  rc = run_decodes(cs, &db, st, nullptr, true);
-  ht.mark("decode_launched");
-  if (rc) return rc;
-  hipEventRecord(ctx->ev[2], st);
-  m.bytes_read = db.bytes;
   // dictionary-id bins: every segment's table [card][rec] is written whole by the bin reduce
   const int shift = topn_bin_shift(na);
   std::vector<int32_t> bin_first(n, 0), bin_seg;
@@ -2621,7 +2688,6 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   ScanJob* h_jobs = up_take<ScanJob>(cs, n, &d_jobs, st);
   if (!h_jobs) return set_error(DG_ERR_OOM, "scan jobs");
   memcpy(h_jobs, jobs.data(), sizeof(ScanJob) * n);
-  hipEventRecord(ctx->ev[3], st);
   // missing-dimension segments: the key view is absent; load_id would fault, so route them
   // through a 1-entry table with a zero id view
   for (int i = 0; i < n; ++i) {
@@ -2643,63 +2709,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       h_jobs[i] = fixed;
     }
   }
-  if (any_multi) {
-    // multi-value dimension: per-(row, value) atomics into identity-initialised tables
-    SlotInit init{};
-    for (int a = 0; a < na; ++a) init.v[1 + a] = identity_host(plan.kind[a]);
-    DG_FLUSH(cs, st);
-    for (int i = 0; i < n; ++i)
-      if (cur[i].any) launch_fill_u64(jobs[i].out, jobs[i].nbuckets, rec, init, st);
-    launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
-  } else {
-    DG_FLUSH(cs, st);
-    launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
-                     d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
-  }
-  ht.mark("bins_launched");
-  if (has_float_sum(plan)) {
-    // floatSum as the reference adds it: float32, one row at a time per (cursor, dictionary id)
-    // position of the pooled buffer (PooledTopNAlgorithm.aggregateDimValue -> FloatSumBufferAggregator)
-    std::vector<GbJob> gj(n);
-    std::vector<int64_t> frows(n, 0);
-    int64_t maxb = 1, maxc = 1;
-    for (int i = 0; i < n; ++i)
-      if (cur[i].any) {
-        maxb = std::max<int64_t>(maxb, q->period_ms ? cur[i].nbuckets : 1);
-        maxc = std::max<int64_t>(maxc, card[i]);
-      }
-    const int bb = q->period_ms ? bits_for(maxb) : 0, ib = bits_for(maxc);
-    for (int i = 0; i < n; ++i) {
-      GbJob& f = gj[i];
-      memset(&f, 0, sizeof f);
-      if (!cur[i].any) continue;
-      f.bitset = jobs[i].bitset;
-      f.time = jobs[i].time;
-      f.t_lo = jobs[i].t_lo;
-      f.t_hi = jobs[i].t_hi;
-      f.bucket0 = cur[i].bucket0;
-      f.period = q->period_ms;
-      f.bounds = gr.db;
-      f.nbounds = gr.nb + 1;
-      f.ndims = 1;
-      f.dims[0] = jobs[i].key;  // VIEW_ABSENT for a missing dimension: id 0 (its null value)
-      f.moff[0] = jobs[i].key_off;
-      f.multi = any_multi;
-      f.skip_empty = 1;
-      f.dim_bits[0] = ib;
-      f.bucket_shift = ib;
-      f.bucket_bits = bb;
-      f.seg_slot = i;
-      f.seg_shift = ib + bb;
-      gb_copy_aggs(&f, jobs[i]);
-      f.fs_out = jobs[i].out;
-      f.fs_mul = jobs[i].key_card;
-      frows[i] = jobs[i].nrows;
-    }
-    rc = fsum_pass(cs, gj, frows, bits_for(n) + bb + ib, true, plan, st, gr.desc);
-    if (rc) return rc;
-  }
-  // selection + gather of the candidates' records, all segments in one launch
+  // selection + gather of the candidates' records, all segments in one launch (staged before the
+  // decode: its upload carries the bins', the scan's and the selection's tables)
   const int mk = dim ? DG_AGG_COUNT : plan.kind[t->metric_agg];
   const int metric_agg = dim ? 0 : t->metric_agg;
   const int metric_op = (slot_op(mk) << 8) | mk;
@@ -2803,13 +2814,75 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     sel[k].ncand = reinterpret_cast<int32_t*>(d_selmem + sel_words * k + 4);
     sel[k].hist = reinterpret_cast<uint32_t*>(d_selmem + sel_words * k + 5);
   }
+  if (ns) memcpy(h_sel, sel.data(), sizeof(TopnSelJob) * ns);
+  rc = run_decodes(cs, &db, st, nullptr, true);
+  ht.mark("decode_launched");
+  if (rc) return rc;
+  phase_event(ctx->ev[2], st);
+  m.bytes_read = db.bytes;
+  phase_event(ctx->ev[3], st);
+  if (any_multi) {
+    // multi-value dimension: per-(row, value) atomics into identity-initialised tables
+    SlotInit init{};
+    for (int a = 0; a < na; ++a) init.v[1 + a] = identity_host(plan.kind[a]);
+    DG_FLUSH(cs, st);
+    for (int i = 0; i < n; ++i)
+      if (cur[i].any) launch_fill_u64(jobs[i].out, jobs[i].nbuckets, rec, init, st);
+    launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
+  } else {
+    DG_FLUSH(cs, st);
+    launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
+                     d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
+  }
+  ht.mark("bins_launched");
+  if (has_float_sum(plan)) {
+    // floatSum as the reference adds it: float32, one row at a time per (cursor, dictionary id)
+    // position of the pooled buffer (PooledTopNAlgorithm.aggregateDimValue -> FloatSumBufferAggregator)
+    std::vector<GbJob> gj(n);
+    std::vector<int64_t> frows(n, 0);
+    int64_t maxb = 1, maxc = 1;
+    for (int i = 0; i < n; ++i)
+      if (cur[i].any) {
+        maxb = std::max<int64_t>(maxb, q->period_ms ? cur[i].nbuckets : 1);
+        maxc = std::max<int64_t>(maxc, card[i]);
+      }
+    const int bb = q->period_ms ? bits_for(maxb) : 0, ib = bits_for(maxc);
+    for (int i = 0; i < n; ++i) {
+      GbJob& f = gj[i];
+      memset(&f, 0, sizeof f);
+      if (!cur[i].any) continue;
+      f.bitset = jobs[i].bitset;
+      f.time = jobs[i].time;
+      f.t_lo = jobs[i].t_lo;
+      f.t_hi = jobs[i].t_hi;
+      f.bucket0 = cur[i].bucket0;
+      f.period = q->period_ms;
+      f.bounds = gr.db;
+      f.nbounds = gr.nb + 1;
+      f.ndims = 1;
+      f.dims[0] = jobs[i].key;  // VIEW_ABSENT for a missing dimension: id 0 (its null value)
+      f.moff[0] = jobs[i].key_off;
+      f.multi = any_multi;
+      f.skip_empty = 1;
+      f.dim_bits[0] = ib;
+      f.bucket_shift = ib;
+      f.bucket_bits = bb;
+      f.seg_slot = i;
+      f.seg_shift = ib + bb;
+      gb_copy_aggs(&f, jobs[i]);
+      f.fs_out = jobs[i].out;
+      f.fs_mul = jobs[i].key_card;
+      frows[i] = jobs[i].nrows;
+    }
+    rc = fsum_pass(cs, gj, frows, bits_for(n) + bb + ib, true, plan, st, gr.desc);
+    if (rc) return rc;
+  }
   if (ns) {
-    memcpy(h_sel, sel.data(), sizeof(TopnSelJob) * ns);
     DG_FLUSH(cs, st);
     launch_topn_select(d_sel, ns, max_card, na, metric_agg, metric_op, t->inverted, sel_threshold, st);
     ht.mark("select_launched");
   }
-  hipEventRecord(ctx->ev[4], st);
+  phase_event(ctx->ev[4], st);
   uint64_t* h_selmem = host_take<uint64_t>(cs, sel_words * (size_t)std::max(ns, 1));
   uint64_t* h_gath = host_take<uint64_t>(cs, (size_t)std::max<int64_t>(gtotal, 1));
   if (!h_selmem || !h_gath) return set_error(DG_ERR_OOM, "topN read-back");
@@ -3030,9 +3103,9 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   }
   ht.mark("replayed");
   float f1 = 0, f2 = 0, f3 = 0;
-  hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
-  hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
-  hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
+  phase_elapsed(&f1, ctx->ev[0], ctx->ev[1]);
+  phase_elapsed(&f2, ctx->ev[1], ctx->ev[2]);
+  phase_elapsed(&f3, ctx->ev[3], ctx->ev[4]);
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
@@ -3510,7 +3583,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   lay.bucket_bits = (q->period_ms && anyc) ? bits_for((gend - gb0) / q->period_ms) : 0;
   const int key_bits = shift + lay.bucket_bits;
   if (key_bits > 64) return set_error(DG_ERR_UNSUPPORTED, "groupBy key of %d bits", key_bits);
-  hipEventRecord(ctx->ev[0], st);
+  phase_event(ctx->ev[0], st);
   std::vector<GbJob> gj(n);
   std::vector<int64_t> rows(n, 0);
   // one element per row unless a grouping dimension is multi-value: then the payload is indexed by
@@ -3604,22 +3677,22 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   if (side) {
     if (!call_err(cs, st)) return set_error(DG_ERR_OOM, "error word");
     DG_FLUSH(cs, st);  // everything staged so far leaves on the main stream first
-    hipEventRecord(ctx->side_ev[0], st);
+    phase_event(ctx->side_ev[0], st);
     DG_HIP(hipStreamWaitEvent(ctx->side, ctx->side_ev[0], 0));
     side_join.s = ctx->side;
-    hipEventRecord(ctx->side_ev[1], ctx->side);
+    phase_event(ctx->side_ev[1], ctx->side);
     rc = run_decodes_only(cs, &db_side, ctx->side, nullptr);
     if (rc) return rc;
-    hipEventRecord(ctx->side_ev[2], ctx->side);
+    phase_event(ctx->side_ev[2], ctx->side);
   } else {
     db.jobs.insert(db.jobs.end(), db_side.jobs.begin(), db_side.jobs.end());
     db.bytes += db_side.bytes;
     db_side.bytes = 0;
   }
-  hipEventRecord(ctx->ev[1], st);
+  phase_event(ctx->ev[1], st);
   rc = run_decodes(cs, &db, st);
   if (rc) return rc;
-  hipEventRecord(ctx->ev[2], st);
+  phase_event(ctx->ev[2], st);
   DG_CHECK_INTERRUPT(intr);
   m.bytes_read = db.bytes + db_side.bytes;
   m.bytes_side = db_side.bytes;
@@ -3638,11 +3711,11 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   uint32_t* h_n = host_take<uint32_t>(cs, 4);
   if (!h_n) return set_error(DG_ERR_OOM, "groupBy counters");
   DG_FLUSH(cs, st);
-  hipEventRecord(ctx->ev[3], st);
+  phase_event(ctx->ev[3], st);
   launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi);
-  hipEventRecord(ctx->ev[5], st);
+  phase_event(ctx->ev[5], st);
   launch_radix_sort(&sb, key_bits, st);
-  hipEventRecord(ctx->ev[6], st);
+  phase_event(ctx->ev[6], st);
   DG_CHECK_INTERRUPT(intr);
   // the result is laid out for the sort's capacity (>= the groups): the reduce counts the groups itself
   // (look-back over tiles), so there is no host read-back between the sort and the reduce
@@ -3673,13 +3746,13 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     if ((has_float_sum(plan) && !head_pos) || !carry_g || !open_g || !carry_slots)
       return set_error(DG_ERR_OOM, "groupBy reduce scratch");
     if (side) DG_HIP(hipStreamWaitEvent(st, ctx->side_ev[2], 0));  // the payload is decoded
-    hipEventRecord(ctx->ev[7], st);
+    phase_event(ctx->ev[7], st);
     reduce_timed = true;
     launch_gb_reduce(&sb, plan, res->keys, res->slots, cap, head_pos, carry_g, carry_slots, open_g, st);
     for (int a = 0; a < na; ++a)
       if (plan.kind[a] == DG_AGG_FLOAT_SUM) launch_fsum_runs(d_jobs, n, ntiles, &sb, plan, a, head_pos, res->slots, cap, st);
   }
-  hipEventRecord(ctx->ev[4], st);
+  phase_event(ctx->ev[4], st);
   DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));  // selected rows, groups
   rc = finish_call(cs, st);  // (polls the cancel flag / timeout while the device works)
   if (rc) return rc;
@@ -3710,19 +3783,19 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   }
   if (side) {
     float fs = 0;
-    hipEventElapsedTime(&fs, ctx->side_ev[1], ctx->side_ev[2]);
+    phase_elapsed(&fs, ctx->side_ev[1], ctx->side_ev[2]);
     m.decode_side_ms = fs;
   }
   for (int i = 0; i < n; ++i)
     if (cur[i].any) m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : sv[i]->nrows;
   m.selected_rows = nsel;
   float f1 = 0, f2 = 0, f3 = 0, f4 = 0, f5 = 0, f6 = 0;
-  hipEventElapsedTime(&f1, ctx->ev[0], ctx->ev[1]);
-  hipEventElapsedTime(&f2, ctx->ev[1], ctx->ev[2]);
-  hipEventElapsedTime(&f3, ctx->ev[3], ctx->ev[4]);
-  hipEventElapsedTime(&f4, ctx->ev[3], ctx->ev[5]);
-  hipEventElapsedTime(&f5, ctx->ev[5], ctx->ev[6]);
-  hipEventElapsedTime(&f6, ctx->ev[6], ctx->ev[4]);
+  phase_elapsed(&f1, ctx->ev[0], ctx->ev[1]);
+  phase_elapsed(&f2, ctx->ev[1], ctx->ev[2]);
+  phase_elapsed(&f3, ctx->ev[3], ctx->ev[4]);
+  phase_elapsed(&f4, ctx->ev[3], ctx->ev[5]);
+  phase_elapsed(&f5, ctx->ev[5], ctx->ev[6]);
+  phase_elapsed(&f6, ctx->ev[6], ctx->ev[4]);
   m.bitmap_ms = f1;
   m.bitmap_bytes = cs->bitmap_bytes;
   m.decode_ms = f2;
@@ -3733,7 +3806,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   m.reduce_ms = f6;  // includes the wait for the side-stream payload decode
   if (reduce_timed) {
     float fr = 0;
-    hipEventElapsedTime(&fr, ctx->ev[7], ctx->ev[4]);
+    phase_elapsed(&fr, ctx->ev[7], ctx->ev[4]);
     m.reduce_kernel_ms = fr;
   }
   m.sort_passes = key_bits > 0 ? (key_bits + 7) / 8 : 0;
@@ -4197,22 +4270,22 @@ int dg_merge(dg_context* c, const dg_keyspace* ks, const uint64_t* d_keys, const
     res->slots = static_cast<uint64_t*>(result_alloc(ctx, (size_t)n * rec * 8));
     res->cap = n;
     if (!res->keys || !res->slots) return set_error(DG_ERR_OOM, "merged result of %lld records", (long long)n);
-    hipEventRecord(ctx->ev[3], st);
+    phase_event(ctx->ev[3], st);
     launch_merge_load(d_keys, n, &sb, st);
     launch_radix_sort(&sb, key_bits, st);
-    hipEventRecord(ctx->ev[5], st);
+    phase_event(ctx->ev[5], st);
     launch_run_heads(&sb, st);
     launch_run_mark(&sb, head_pos, st);
     launch_merge_reduce(&sb, head_pos, d_slots, plan, n, res->keys, res->slots, st);
     launch_slots_finalize(res->slots, sb.n + 1, n, plan, st);
     DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));
-    hipEventRecord(ctx->ev[4], st);
+    phase_event(ctx->ev[4], st);
     rc = finish_call(cs, st);
     if (rc) return rc;
     ng = h_n[1];
     float fs = 0, fr = 0;
-    hipEventElapsedTime(&fs, ctx->ev[3], ctx->ev[5]);
-    hipEventElapsedTime(&fr, ctx->ev[5], ctx->ev[4]);
+    phase_elapsed(&fs, ctx->ev[3], ctx->ev[5]);
+    phase_elapsed(&fr, ctx->ev[5], ctx->ev[4]);
     m.sort_ms = fs;
     m.reduce_ms = fr;
     m.aggregate_ms = fs + fr;
@@ -4553,6 +4626,11 @@ int dg_timeseries_merge(const dg_scan* scan, int32_t n_lists, const int32_t* n, 
 // ------------------------------------------------------------------------------------------------
 // diagnostics: decode arbitrary LZ4 blocks through the engine's attach-time index + HIP decoder
 // ------------------------------------------------------------------------------------------------
+extern "C" int dg_set_phase_timing(int32_t on) {
+  g_phase_timing.store(on != 0, std::memory_order_relaxed);
+  return DG_OK;
+}
+
 extern "C" int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind) {
   if (!block || len <= 0 || len > kBlockBytes + 2048 || !kind) return set_error(DG_ERR_ARG, "bad arguments");
   std::vector<uint32_t> one;
@@ -4641,14 +4719,14 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
     if (!d_prof) return set_error(DG_ERR_OOM, "debug decode profile");
     DG_HIP(hipMemsetAsync(d_prof, 0, (size_t)n * kLz4ProfWords * 8, st));
   }
-  hipEventRecord(ctx->ev[0], st);
+  phase_event(ctx->ev[0], st);
   int rc = run_decodes(g.cs, &db, st, d_prof);
   if (rc) return rc;
-  hipEventRecord(ctx->ev[1], st);
+  phase_event(ctx->ev[1], st);
   rc = finish_call(g.cs, st);
   if (rc) return rc;
   float f = 0;
-  hipEventElapsedTime(&f, ctx->ev[0], ctx->ev[1]);
+  phase_elapsed(&f, ctx->ev[0], ctx->ev[1]);
   if (ms) *ms = f;
   DG_HIP(hipMemcpy(out, slots, (size_t)n * kBlockBytes, hipMemcpyDeviceToHost));
   if (prof) DG_HIP(hipMemcpy(prof, d_prof, (size_t)db.jobs.size() * kLz4ProfWords * 8, hipMemcpyDeviceToHost));

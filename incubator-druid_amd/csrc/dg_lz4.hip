@@ -1234,30 +1234,35 @@ __device__ __forceinline__ void flow_copy(uint32_t* o32, int dst, const uint32_t
   for (int k = 0; k < len; k += 16) flow_copyn<5>(o32, dst + k, i32, src + k, min(16, len - k));
 }
 
-// The flow decoder's parse: one 16-byte window (four aligned dword reads, one LDS round trip) holds a
-// token, up to 8 literal bytes and the distance; the literal bytes ride along in lv / lv_hi (L <= 8).
-// Longer runs, extended lengths: parse_tok_slow.
+// The flow decoder's parse: one 20-byte window (five aligned dword reads, one LDS round trip) holds a
+// token, its literal length extension byte, up to 8 literal bytes (they ride along in lv / lv_hi) and,
+// for runs of up to 14 bytes, the distance; a distance or match length extension byte past the window
+// is one more read. Only an extension of 255 or more (a run or match of 270+ bytes) takes the byte-wise
+// parse_tok_slow.
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t* in32, int q) { return (in32[q >> 2] >> (8 * (q & 3))) & 0xFFu; }
+
 __device__ __forceinline__ bool parse_tok8(const uint8_t* __restrict__ in, int n, int p, Tok& t, uint32_t& lv_hi) {
   if (p >= n) return false;
   const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
   const int a = p >> 2, sh = p & 3;
-  const uint32_t d0 = in32[a], d1 = in32[a + 1], d2 = in32[a + 2], d3 = in32[a + 3];
+  const uint32_t d0 = in32[a], d1 = in32[a + 1], d2 = in32[a + 2], d3 = in32[a + 3], d4 = in32[a + 4];
   const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, sh), b1 = __builtin_amdgcn_alignbyte(d2, d1, sh),
-                 b2 = __builtin_amdgcn_alignbyte(d3, d2, sh);  // bytes p .. p + 11
+                 b2 = __builtin_amdgcn_alignbyte(d3, d2, sh), b3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+  // bytes p .. p + 15 as b0..b3 (the 17th byte, p + 16, is not needed from the window)
   const int tk = (int)(b0 & 0xFF);
-  const int L = tk >> 4, M = tk & 15;
-  const uint32_t lo = __builtin_amdgcn_alignbyte(b1, b0, 1), hi = __builtin_amdgcn_alignbyte(b2, b1, 1);  // bytes 1 .. 8
-  if (L > 8 || M == 15) {
-    const bool ok = parse_tok_slow(in, n, p, t);
-    t.lv = lo;
-    lv_hi = hi;
-    return ok;
+  int L = tk >> 4, M = tk & 15;
+  lv_hi = __builtin_amdgcn_alignbyte(b2, b1, 1);  // bytes 5 .. 8
+  t.lv = __builtin_amdgcn_alignbyte(b1, b0, 1);   // bytes 1 .. 4
+  int q = p + 1;
+  if (L == 15) {
+    const int e = (int)((b0 >> 8) & 0xFF);
+    if (e == 255) return parse_tok_slow(in, n, p, t);
+    L += e;
+    q = p + 2;
   }
-  const int q = p + 1 + L;
-  t.lit = p + 1;
+  t.lit = q;
   t.L = L;
-  t.lv = lo;
-  lv_hi = hi;
+  q += L;
   if (q > n) return false;
   if (q == n) {
     t.off = 0;
@@ -1266,12 +1271,31 @@ __device__ __forceinline__ bool parse_tok8(const uint8_t* __restrict__ in, int n
     return true;
   }
   if (q + 2 > n) return false;
-  const int k = L + 1;  // the distance: window bytes k, k + 1 (k <= 9)
-  const uint64_t w01 = (uint64_t)b0 | ((uint64_t)b1 << 32), w12 = (uint64_t)b1 | ((uint64_t)b2 << 32);
-  t.off = (int)((k <= 6 ? (w01 >> (8 * k)) : (w12 >> (8 * (k - 4)))) & 0xFFFF);
+  const int k = q - p;  // the distance: window bytes k, k + 1
+  int off;
+  if (k <= 14) {
+    const uint64_t lo = (uint64_t)b0 | ((uint64_t)b1 << 32), hi = (uint64_t)b2 | ((uint64_t)b3 << 32);
+    off = (int)((k <= 6 ? lo >> (8 * k) : k < 8 ? (lo >> (8 * k)) | (hi << (64 - 8 * k)) : hi >> (8 * (k - 8))) & 0xFFFF);
+  } else {
+    off = (int)(lds_byte(in32, q) | (lds_byte(in32, q + 1) << 8));
+  }
+  q += 2;
+  if (M == 15) {
+    if (q >= n) return false;
+    const int e = (int)lds_byte(in32, q);
+    if (e == 255) {
+      const uint32_t lv = t.lv;
+      const bool ok = parse_tok_slow(in, n, p, t);
+      t.lv = lv;  // (parse_tok_slow keeps only runs of <= 4 literal bytes)
+      return ok;
+    }
+    M += e;
+    q += 1;
+  }
+  t.off = off;
   t.M = M + 4;
-  t.next = q + 2;
-  return t.off != 0;
+  t.next = q;
+  return off != 0;
 }
 
 template <bool PROF>
@@ -1299,13 +1323,16 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   LZ_STAMP(0);
   const uint8_t* s_in = reinterpret_cast<const uint8_t*>(s_in32 + kFlowPad);
   // my matches' table rows (u16 each, 0xFFFF: none) and the levels' row ranges
-  const uint4 rk4 = tid < ncp ? gld16(job.lvl + (size_t)tid * 4 * SEQ) : make_uint4(~0u, ~0u, ~0u, ~0u);
-  const uint4 fd4 = tid < ncp ? gld16(job.lvl + (size_t)tid * 4 * SEQ + 2 * SEQ) : make_uint4(0u, 0u, 0u, 0u);
-  // my interval's token offsets, loaded with the staging (not after it)
+  // my interval's schedule (match ranks, forwarded distances, token offsets) and checkpoints, loaded
+  // with the staging (not after it)
+  const uint8_t* my = job.lvl + (size_t)tid * 6 * SEQ;
+  const uint4 rk4 = tid < ncp ? gld16(my) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  const uint4 fd4 = tid < ncp ? gld16(my + 2 * SEQ) : make_uint4(0u, 0u, 0u, 0u);
+  const uint4 tk4 = tid < ncp ? gld16(my + 4 * SEQ) : make_uint4(~0u, ~0u, ~0u, ~0u);
   const int cp0 = tid < ncp ? (int)gld4(job.cp + tid) : 0;
   const int cp1 = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
   if (tid <= job.nlvl) {
-    const uint8_t* st = job.lvl + 4 * SEQ * (size_t)ncp;
+    const uint8_t* st = job.lvl + 6 * SEQ * (size_t)ncp;
     s_lvl[tid] = (int)(gld4(st + 2 * tid - 2 * (tid & 1)) >> (16 * (tid & 1))) & 0xFFFF;
   }
   {
@@ -1327,29 +1354,32 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   uint32_t r_L[SEQ], r_DM[SEQ], r_lv[SEQ], r_lvh[SEQ];
 #pragma unroll
   for (int s = 0; s < SEQ; ++s) r_L[s] = r_DM[s] = r_lv[s] = r_lvh[s] = 0;
+  // the interval's tokens parsed independently (token offsets from the schedule), then checked to
+  // chain: each token ends where the next begins, the last where the next interval does
   int cnt = 0, out_rel = 0;
   if (tid < ncp) {
-    int pos = cp0;
-    const int end = cp1;
+    const uint32_t tkw[4] = {tk4.x, tk4.y, tk4.z, tk4.w};
+    bool ok = true;
+    int prev_next = cp0;
 #pragma unroll
     for (int s = 0; s < SEQ; ++s) {
-      if (pos < end) {
-        Tok t;
-        uint32_t hi;
-        if (parse_tok8(s_in, n, pos, t, hi)) {
-          r_L[s] = (uint32_t)t.L;
-          r_DM[s] = (uint32_t)t.off | ((uint32_t)t.M << 16);
-          r_lv[s] = t.L <= kFlowRegLit ? t.lv : (uint32_t)t.lit;
-          r_lvh[s] = hi;
-          out_rel += t.L + t.M;
-          pos = t.next;
-          cnt = s + 1;
-        } else {
-          pos = -1;
-        }
+      const uint32_t dlt = (tkw[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
+      if (dlt != 0xFFFFu) {
+        const int pos = cp0 + (int)dlt;
+        Tok t{};
+        uint32_t hi = 0;
+        const bool parsed = parse_tok8(s_in, n, pos, t, hi);  // (independent of the previous token)
+        ok &= parsed & (pos == prev_next);
+        r_L[s] = (uint32_t)t.L;
+        r_DM[s] = (uint32_t)t.off | ((uint32_t)t.M << 16);
+        r_lv[s] = t.L <= kFlowRegLit ? t.lv : (uint32_t)t.lit;
+        r_lvh[s] = hi;
+        out_rel += t.L + t.M;
+        prev_next = t.next;
+        cnt = s + 1;
       }
     }
-    if (pos != end) s_bad = 1;
+    if (!ok || prev_next != cp1) s_bad = 1;
   }
   int total;
   const int base = block_scan_lz(out_rel, &total, s_tmp);

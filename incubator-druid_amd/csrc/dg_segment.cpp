@@ -186,9 +186,11 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
 // chains a 4-byte pattern through every earlier occurrence, so this shortens the chains (noisy doubles:
 // 24 -> 8 levels). Every match then gets its copy-chain level — one more than the highest level among
 // the bytes of its (forwarded) source; literal bytes are level 0 — and its rank in the block's matches
-// ordered by (level, position). Appended per interval: kLzSeqPerCp u16 ranks (0xFFFF: no match) and
-// kLzSeqPerCp u16 forwarded distances; then the u16 start of every level's ranks (nlvl + 1 of them, zero
-// padded to 16 bytes). Returns the highest level, or -1 above `cap` (nothing appended).
+// ordered by (level, position). Appended per interval: kLzSeqPerCp u16 ranks (0xFFFF: no match),
+// kLzSeqPerCp u16 forwarded distances and kLzSeqPerCp u16 token offsets from the interval's first
+// token (0xFFFF: no such sequence; the decoder parses an interval's tokens independently); then the u16
+// start of every level's ranks (nlvl + 1 of them, zero padded to 16 bytes). Returns the highest level,
+// or -1 above `cap` or when a token lies 64 KiB or more past its interval's first (nothing appended).
 static int lz4_flow_schedule(const uint8_t* in, int n, int64_t g, int cap, std::vector<uint8_t>* lv) {
   struct Mt {
     int om, M, fsrc, d;
@@ -197,8 +199,10 @@ static int lz4_flow_schedule(const uint8_t* in, int n, int64_t g, int cap, std::
   thread_local std::vector<int32_t> owner(kBlockBytes);  // the match that produced a byte, -1: a literal
   thread_local std::vector<Mt> ms;
   thread_local std::vector<int32_t> seqm;  // per sequence: its match's index in ms, -1: none
+  thread_local std::vector<int32_t> seqp;  // per sequence: its token's offset
   ms.clear();
   seqm.clear();
+  seqp.clear();
   int pos = 0, out = 0, mx = 0;
   auto ext = [&](int* len) {
     for (int b = 255; b == 255 && pos < n;) {
@@ -207,6 +211,7 @@ static int lz4_flow_schedule(const uint8_t* in, int n, int64_t g, int cap, std::
     }
   };
   for (;;) {
+    seqp.push_back(pos);
     const int tok = in[pos++];
     int L = tok >> 4;
     if (L == 15) ext(&L);
@@ -251,15 +256,20 @@ static int lz4_flow_schedule(const uint8_t* in, int n, int64_t g, int cap, std::
     st[k] = (uint16_t)acc;  // st[k - 1] .. st[k]: the ranks of level k
   }
   const int64_t m = ((int64_t)seqm.size() + g - 1) / g;
-  const size_t at = lv->size(), rec = 4 * kLzSeqPerCp;  // per interval: ranks, then distances
+  for (int64_t i = 0; i < m; ++i)  // token offsets as u16 deltas from the interval's first token
+    for (int64_t q = 1; q < g && i * g + q < (int64_t)seqp.size(); ++q)
+      if (seqp[i * g + q] - seqp[i * g] >= 0xFFFF) return -1;
+  const size_t at = lv->size(), rec = 6 * kLzSeqPerCp;  // per interval: ranks, distances, token deltas
   lv->resize(at + (size_t)m * rec + (((size_t)(mx + 1) * 2 + 15) & ~(size_t)15), 0);
   for (int64_t i = 0; i < m; ++i)
     for (int q = 0; q < kLzSeqPerCp; ++q) {
       uint16_t* r = reinterpret_cast<uint16_t*>(lv->data() + at + (size_t)i * rec);
       const int64_t sq = i * g + q;
-      const int j = q < g && sq < (int64_t)seqm.size() ? seqm[sq] : -1;
+      const bool here = q < g && sq < (int64_t)seqm.size();
+      const int j = here ? seqm[sq] : -1;
       r[q] = j < 0 ? (uint16_t)0xFFFF : next[lev[ms[j].om]]++;
       r[kLzSeqPerCp + q] = j < 0 ? (uint16_t)0 : (uint16_t)(ms[j].om - ms[j].fsrc);
+      r[2 * kLzSeqPerCp + q] = here ? (uint16_t)(seqp[sq] - seqp[i * g]) : (uint16_t)0xFFFF;
     }
   memcpy(lv->data() + at + (size_t)m * rec, st.data(), (size_t)(mx + 1) * 2);
   return mx;
