@@ -1837,9 +1837,24 @@ __device__ __forceinline__ void run_fold(const Lz4Job& job, uint64_t x, uint64_t
 }
 
 constexpr int kRunVals = kBlockBytes / 8;
+constexpr int kRunStageBlocks = 512;  // launches up to this many blocks stage their input (latency mode)
 
+// 8 bytes of an LDS byte array at byte offset p (three aligned dword reads)
+__device__ __forceinline__ uint64_t l_rd8(const uint32_t* __restrict__ a, int p) {
+  const uint32_t* q = a + (p >> 2);
+  const int sh = p & 3;
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+  return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+}
+
+// STAGE (launches of at most kRunStageBlocks blocks, which leave most CUs idle): the compressed block and
+// its far table are staged in LDS first, so each interval's serial chain waits on LDS instead of L2/HBM
+// (a block's latency, not the launch's throughput, is the cost there); 104 KiB of LDS, one block per
+// CU. Otherwise the thread reads its ~128 contiguous input bytes from L1/L2 and two blocks share a CU.
+template <bool STAGE>
 __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
   __shared__ __attribute__((aligned(16))) uint64_t s_val[kRunVals];  // the block's decoded image
+  __shared__ __attribute__((aligned(16))) uint32_t s_in[STAGE ? kRunLdsMax / 4 + 8 : 4];  // staged input, far table
   __shared__ uint64_t s_red[kRunThreads / 64];
   const Lz4Job job = jobs[blockIdx.x];
   const int tid = threadIdx.x;
@@ -1852,15 +1867,40 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
   }
   const uint8_t* __restrict__ in = job.src;                          // 16-byte aligned, zero padded
   const uint8_t* __restrict__ far = job.rx + ((14 * ni + 15) & ~15);  // 16-byte aligned, zero padded
+  const int n16 = (n + 15) >> 4;
+  if constexpr (STAGE) {
+    const int f16 = (nfar + 15) >> 4;
+    uint4* st = reinterpret_cast<uint4*>(s_in);
+    for (int i = tid; i < n16 + f16 + 1; i += kRunThreads)
+      st[i] = i < n16 ? gld16(in + 16 * (size_t)i) : i < n16 + f16 ? gld16(far + 16 * (size_t)(i - n16)) : make_uint4(0, 0, 0, 0);
+  }
+  auto rd8_in = [&](int q) -> uint64_t {
+    if constexpr (STAGE) return l_rd8(s_in, q);
+    else return g_rd8(in, q);
+  };
+  auto rd8_far = [&](int q) -> uint64_t {
+    if constexpr (STAGE) return l_rd8(s_in + 4 * n16, q);
+    else return g_rd8(far, q);
+  };
+  auto rd1_in = [&](int q) -> int {
+    if constexpr (STAGE) return (int)((s_in[q >> 2] >> (8 * (q & 3))) & 0xFF);
+    else return (int)gld1(in + q);
+  };
   const bool fold = job.red_dst != nullptr;
   uint64_t acc = fold ? red_identity(job) : 0ull;
   bool bad = false;
-  if (tid < ni) {
-    uint64_t win = (uint64_t)gld4(job.rx + 8 * (size_t)tid) | ((uint64_t)gld4(job.rx + 8 * (size_t)tid + 4) << 32);
-    const uint32_t tf = gld4(job.rx + 8 * (size_t)ni + 4 * (size_t)tid);
+  uint64_t win = 0;
+  uint32_t tf = 0;
+  int o = 0, oend = 0;
+  if (tid < ni) {  // (loaded beside the staging)
+    win = (uint64_t)gld4(job.rx + 8 * (size_t)tid) | ((uint64_t)gld4(job.rx + 8 * (size_t)tid + 4) << 32);
+    tf = gld4(job.rx + 8 * (size_t)ni + 4 * (size_t)tid);
     const uint16_t* ost = reinterpret_cast<const uint16_t*>(job.rx + 12 * (size_t)ni);
-    int o = ost[tid];
-    const int oend = tid + 1 < ni ? (int)ost[tid + 1] : job.dec_len;
+    o = ost[tid];
+    oend = tid + 1 < ni ? (int)ost[tid + 1] : job.dec_len;
+  }
+  if constexpr (STAGE) __syncthreads();
+  if (tid < ni) {
     int p = (int)(tf & 0x1FFFFu), fp = (int)(tf >> 17);
     // shift k (1..8) bytes, the low bytes of x, into the window; a completed aligned value is emitted
     auto push = [&](uint64_t x, int k) {
@@ -1880,13 +1920,13 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
           bad = true;
           return;
         }
-        b = (int)gld1(in + q++);
+        b = rd1_in(q++);
         len += b;
       }
     };
 #pragma unroll 1
     while (o < oend && !bad) {
-      const uint64_t w = g_rd8(in, p);
+      const uint64_t w = rd8_in(p);
       const int tk = (int)(w & 0xFF);
       int L = tk >> 4, M = tk & 15, q = p + 1;
       if (L == 15) ext(q, L);
@@ -1906,7 +1946,7 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
 #pragma unroll 1
           while (rem > 0) {
             const int k = min(rem, 8 - (o & 7));
-            push(g_rd8(in, lp), k);
+            push(rd8_in(lp), k);
             lp += k;
             rem -= k;
           }
@@ -1917,7 +1957,7 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
         if (q > n || o != job.dec_len) bad = true;
         break;
       }
-      const int d = tk < 0x60 ? (int)((w >> (8 * (1 + L))) & 0xFFFF) : (int)(g_rd8(in, q) & 0xFFFF);
+      const int d = tk < 0x60 ? (int)((w >> (8 * (1 + L))) & 0xFFFF) : (int)(rd8_in(q) & 0xFFFF);
       q += 2;
       if (M == 15) ext(q, M);
       M += 4;
@@ -1938,7 +1978,7 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
 #pragma unroll 1
         while (M > 0) {
           const int k = min(M, 8 - (o & 7));
-          push(g_rd8(far, fp), k);
+          push(rd8_far(fp), k);
           fp += k;
           M -= k;
         }
@@ -1977,7 +2017,11 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
 void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int lds, int32_t* d_err, hipStream_t s) {
   (void)lds;
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_lz4_run, dim3(njobs), dim3(kRunThreads), 0, s, d_jobs, d_err);
+  // DG_RUN_STAGE=0 / 1 forces the mode (tests run every run block through both)
+  const char* force = getenv("DG_RUN_STAGE");
+  const bool stage = force && *force ? *force != '0' : njobs <= kRunStageBlocks;
+  if (stage) hipLaunchKernelGGL(k_lz4_run<true>, dim3(njobs), dim3(kRunThreads), 0, s, d_jobs, d_err);
+  else hipLaunchKernelGGL(k_lz4_run<false>, dim3(njobs), dim3(kRunThreads), 0, s, d_jobs, d_err);
 }
 
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {

@@ -43,18 +43,21 @@ def lz4_sequences(seqs, last_literals: bytes) -> bytes:
     return bytes(out)
 
 
-@pytest.fixture(params=["default", "no_run", "no_flow"])
+@pytest.fixture(params=["default", "no_run", "no_flow", "run_l2"])
 def route(request, monkeypatch):
     """The library's routing of blocks to its decoders (run / light / flow / general), read per call;
     with DG_NO_RUN_DECODE=1 the run blocks (8-byte value runs) go to the general decoders instead, and
     with DG_NO_FLOW_DECODE=1 the flow blocks (short copy chains) go to k_lz4_decode, so every decoder
-    sees the same streams."""
-    monkeypatch.delenv("DG_NO_RUN_DECODE", raising=False)
-    monkeypatch.delenv("DG_NO_FLOW_DECODE", raising=False)
+    sees the same streams. k_lz4_run stages its input in LDS in small launches (these tests'); run_l2
+    (DG_RUN_STAGE=0) forces its large-launch mode, reading the input from L1/L2."""
+    for v in ("DG_NO_RUN_DECODE", "DG_NO_FLOW_DECODE", "DG_RUN_STAGE"):
+        monkeypatch.delenv(v, raising=False)
     if request.param == "no_run":
         monkeypatch.setenv("DG_NO_RUN_DECODE", "1")
     elif request.param == "no_flow":
         monkeypatch.setenv("DG_NO_FLOW_DECODE", "1")
+    elif request.param == "run_l2":
+        monkeypatch.setenv("DG_RUN_STAGE", "0")
     return request.param
 
 
