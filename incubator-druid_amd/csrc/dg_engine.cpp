@@ -144,6 +144,14 @@ struct UpPool {
     flushed = off;
     return true;
   }
+  // do device addresses [lo, hi) lie in one chunk
+  bool one_chunk(const void* lo, const void* hi) const {
+    for (const auto& c : chunks) {
+      const char* d = static_cast<const char*>(c.d);
+      if (static_cast<const char*>(lo) >= d && static_cast<const char*>(hi) <= d + c.n) return true;
+    }
+    return false;
+  }
   void* take(size_t n, void** dev, hipStream_t st) {
     n = (n + 255) & ~(size_t)255;
     if (cur >= chunks.size() || off + n > chunks[cur].n) {
@@ -218,6 +226,14 @@ struct CallScratch {
   unsigned long long* cnt_d = nullptr;
   unsigned long long* cnt_h = nullptr;
   int cnt_used = 0;
+  // device -> host reads of staged (upload-pool) words due at the call's final synchronisation:
+  // finish_call moves them with one copy of the span holding them all
+  struct LateRead {
+    void* h;
+    const void* d;
+    size_t n;
+  };
+  std::vector<LateRead> late;
   Context* ctx = nullptr;
   // algorithmic bytes of the call's filter bitmaps (dg_metrics.bitmap_bytes): serialized bitmaps
   // read + every row bitset written and read once
@@ -232,6 +248,7 @@ struct CallScratch {
     cnt_d = nullptr;
     cnt_h = nullptr;
     cnt_used = 0;
+    late.clear();
     bitmap_bytes = 0;
     intr = nullptr;
   }
@@ -328,8 +345,30 @@ static int32_t* call_err(CallScratch* cs, hipStream_t st) {
 // drains (it owns the context's scratch) and the call then returns the interruption.
 static int finish_call(CallScratch* cs, hipStream_t st) {
   DG_FLUSH(cs, st);
-  if (cs->cnt_used) DG_HIP(hipMemcpyAsync(cs->cnt_h, cs->cnt_d, 8 * (size_t)cs->cnt_used, hipMemcpyDeviceToHost, st));
-  if (cs->d_err) DG_HIP(hipMemcpyAsync(cs->h_err, cs->d_err, 4, hipMemcpyDeviceToHost, st));
+  auto& late = cs->late;
+  if (cs->cnt_used) late.push_back({cs->cnt_h, cs->cnt_d, 8 * (size_t)cs->cnt_used});
+  if (cs->d_err) late.push_back({cs->h_err, cs->d_err, 4});
+  // the late reads with one copy of the span holding them, when it is compact (they are staged words of
+  // one upload chunk, a few KiB apart); else one copy each
+  uint8_t* span_h = nullptr;
+  const uint8_t* lo = nullptr;
+  size_t span = 0, sum = 0;
+  if (late.size() > 1) {
+    const uint8_t* hi = nullptr;
+    for (const auto& r : late) {
+      const uint8_t* d = static_cast<const uint8_t*>(r.d);
+      lo = !lo || d < lo ? d : lo;
+      hi = !hi || d + r.n > hi ? d + r.n : hi;
+      sum += r.n;
+    }
+    span = (size_t)(hi - lo);
+    if (span <= 2 * sum + (64 << 10) && cs->up.one_chunk(lo, hi)) span_h = host_take<uint8_t>(cs, span);
+  }
+  if (span_h) {
+    DG_HIP(hipMemcpyAsync(span_h, lo, span, hipMemcpyDeviceToHost, st));
+  } else {
+    for (const auto& r : late) DG_HIP(hipMemcpyAsync(r.h, r.d, r.n, hipMemcpyDeviceToHost, st));
+  }
   if (cs->intr && cs->intr->active()) {
     int irc = DG_OK;
     for (int spin = 0;; ++spin) {
@@ -344,6 +383,9 @@ static int finish_call(CallScratch* cs, hipStream_t st) {
   } else {
     DG_HIP(hipStreamSynchronize(st));
   }
+  if (span_h)
+    for (const auto& r : late) memcpy(r.h, span_h + (static_cast<const uint8_t*>(r.d) - lo), r.n);
+  late.clear();
   DG_HIP(hipGetLastError());
   DG_HIP(take_launch_error());
   if (cs->d_err && *cs->h_err)
@@ -2485,7 +2527,9 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
     h_out[i] = host_take<uint64_t>(cs, (size_t)cur[i].nbuckets * rec);
-    DG_HIP(hipMemcpyAsync(h_out[i], jobs[i].out, (size_t)cur[i].nbuckets * rec * 8, hipMemcpyDeviceToHost, st));
+    if (!h_out[i]) return set_error(DG_ERR_OOM, "results");
+    if (staged_acc[i]) cs->late.push_back({h_out[i], jobs[i].out, (size_t)cur[i].nbuckets * rec * 8});
+    else DG_HIP(hipMemcpyAsync(h_out[i], jobs[i].out, (size_t)cur[i].nbuckets * rec * 8, hipMemcpyDeviceToHost, st));
   }
   ht.mark("agg_launched");
   rc = finish_call(cs, st);
