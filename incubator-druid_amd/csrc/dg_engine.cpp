@@ -3717,7 +3717,11 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   // main stream decodes the key columns, builds the keys and sorts them (the general LZ4 decoder is
   // LDS / latency bound, the sort HBM bound, so the two overlap on the CUs).
   SideJoin side_join;
-  const bool side = ctx->side && !db_side.jobs.empty();
+  static const bool no_side = [] {  // DG_NO_SIDE=1: everything on the main stream (same-box A/B)
+    const char* v = getenv("DG_NO_SIDE");
+    return v && *v && *v != '0';
+  }();
+  const bool side = ctx->side && !db_side.jobs.empty() && !no_side;
   if (side) {
     if (!call_err(cs, st)) return set_error(DG_ERR_OOM, "error word");
     DG_FLUSH(cs, st);  // everything staged so far leaves on the main stream first
