@@ -1434,8 +1434,6 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
   for (int w = 0; w < 4; ++w)
     if (kb[w + 1] - kb[w] <= 16 * 256) std::stable_sort(J.begin() + kb[w], J.begin() + kb[w + 1], by_ncp);
-  int run_lds = 0;
-  for (int i = 0; i < nr; ++i) run_lds = std::max(run_lds, run_lds_bytes(J[i].src_len, J[i].run_far));
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
   int32_t* d_err = call_err(cs, st);
@@ -1450,7 +1448,12 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
     DG_HIP(hipStreamWaitEvent(ctx->side, ctx->ovl_ev[0], 0));
     ss = ctx->side;
   }
-  launch_lz4_run(d, nr, run_lds, d_err, ss);
+  // staging the input in LDS (104 KiB per block) pays where the run decoder has the CUs to itself: a
+  // main-stream launch with nothing beside it stages always, a launch on the side stream next to the main
+  // stream's general decoder only when it is small (latency), and a call decoding on the side stream
+  // beside the main stream's sort never (it would wait for whole CUs)
+  const int stage = ctx && st == ctx->side ? 0 : ss == st ? 2 : 1;
+  launch_lz4_run(d, nr, stage, d_err, ss);
   launch_lz4_light(d + nh, n - nh, d_err, ss, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
   if (ovl) hipEventRecord(ctx->ovl_ev[1], ss);
   const int ng = nh - nr;  // general-decoder blocks
@@ -4714,14 +4717,14 @@ extern "C" int dg_debug_lz4_decode(dg_context* c, const uint8_t* const* blocks, 
   b.lvl_off.assign(n, -1);
   b.lvl_n.assign(n, 0);
   std::vector<uint8_t> rall, lall;
-  int64_t total = 0;
+  int64_t total = kCompSlack;
   for (int i = 0; i < n; ++i) {
     if (lens[i] <= 0 || lens[i] > kBlockBytes + 2048) return set_error(DG_ERR_ARG, "block %d length %d", i, lens[i]);
     b.comp_off[i] = total;
     b.comp_len[i] = lens[i];
     total += (lens[i] + 15) & ~15;
   }
-  std::vector<uint8_t> host((size_t)total + 16, 0);
+  std::vector<uint8_t> host((size_t)total + kCompSlack, 0);
   std::vector<uint32_t> cps;
   for (int i = 0; i < n; ++i) {
     memcpy(host.data() + b.comp_off[i], blocks[i], (size_t)lens[i]);

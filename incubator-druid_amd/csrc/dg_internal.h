@@ -133,6 +133,8 @@ int decode_routes();
 // level by level, each level's matches spread evenly over the threads.
 constexpr int kLzFlow = 2;
 constexpr int kFlowMaxDepth = 64;
+constexpr int kFlowRecBytes = 48;  // schedule bytes per checkpoint interval (lz4_flow_schedule)
+constexpr int kCompSlack = 64;     // bytes of zeros before and after a column's packed LZ4 blocks
 
 // One LZF block (compress-lzf chunk stream, CompressionStrategy.LZFDecompressor) -> dst.
 struct LzfJob {
@@ -453,8 +455,10 @@ constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (dia
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
 void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
-// run blocks (rx set); lds = the largest run_lds_bytes of the launch's blocks
-void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int lds, int32_t* d_err, hipStream_t s);
+// run blocks (rx set); stage: 0 = read the input from L1/L2 (64 KiB of LDS per block, two per CU: beside
+// another stream's LDS-heavy kernels), 1 = stage it in LDS when the launch is small (latency mode),
+// 2 = stage it (a launch that has the GPU to itself)
+void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int stage, int32_t* d_err, hipStream_t s);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // one multi-value dimension's decoded row lists, validated before use (bit 2 of the error word)

@@ -1244,8 +1244,10 @@ __device__ __forceinline__ uint32_t lds_byte(const uint32_t* in32, int q) { retu
 __device__ __forceinline__ bool parse_tok8(const uint8_t* __restrict__ in, int n, int p, Tok& t, uint32_t& lv_hi) {
   if (p >= n) return false;
   const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
+  auto word = [&](int i) -> uint32_t { return in32[i]; };
+  auto byte = [&](int q) -> uint32_t { return lds_byte(in32, q); };
   const int a = p >> 2, sh = p & 3;
-  const uint32_t d0 = in32[a], d1 = in32[a + 1], d2 = in32[a + 2], d3 = in32[a + 3], d4 = in32[a + 4];
+  const uint32_t d0 = word(a), d1 = word(a + 1), d2 = word(a + 2), d3 = word(a + 3), d4 = word(a + 4);
   const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, sh), b1 = __builtin_amdgcn_alignbyte(d2, d1, sh),
                  b2 = __builtin_amdgcn_alignbyte(d3, d2, sh), b3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
   // bytes p .. p + 15 as b0..b3 (the 17th byte, p + 16, is not needed from the window)
@@ -1277,12 +1279,12 @@ __device__ __forceinline__ bool parse_tok8(const uint8_t* __restrict__ in, int n
     const uint64_t lo = (uint64_t)b0 | ((uint64_t)b1 << 32), hi = (uint64_t)b2 | ((uint64_t)b3 << 32);
     off = (int)((k <= 6 ? lo >> (8 * k) : k < 8 ? (lo >> (8 * k)) | (hi << (64 - 8 * k)) : hi >> (8 * (k - 8))) & 0xFFFF);
   } else {
-    off = (int)(lds_byte(in32, q) | (lds_byte(in32, q + 1) << 8));
+    off = (int)(byte(q) | (byte(q + 1) << 8));
   }
   q += 2;
   if (M == 15) {
     if (q >= n) return false;
-    const int e = (int)lds_byte(in32, q);
+    const int e = (int)byte(q);
     if (e == 255) {
       const uint32_t lv = t.lv;
       const bool ok = parse_tok_slow(in, n, p, t);
@@ -1325,14 +1327,14 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   // my matches' table rows (u16 each, 0xFFFF: none) and the levels' row ranges
   // my interval's schedule (match ranks, forwarded distances, token offsets) and checkpoints, loaded
   // with the staging (not after it)
-  const uint8_t* my = job.lvl + (size_t)tid * 6 * SEQ;
+  const uint8_t* my = job.lvl + (size_t)tid * kFlowRecBytes;
   const uint4 rk4 = tid < ncp ? gld16(my) : make_uint4(~0u, ~0u, ~0u, ~0u);
   const uint4 fd4 = tid < ncp ? gld16(my + 2 * SEQ) : make_uint4(0u, 0u, 0u, 0u);
   const uint4 tk4 = tid < ncp ? gld16(my + 4 * SEQ) : make_uint4(~0u, ~0u, ~0u, ~0u);
   const int cp0 = tid < ncp ? (int)gld4(job.cp + tid) : 0;
   const int cp1 = tid + 1 < ncp ? (int)gld4(job.cp + tid + 1) : n;
   if (tid <= job.nlvl) {
-    const uint8_t* st = job.lvl + 6 * SEQ * (size_t)ncp;
+    const uint8_t* st = job.lvl + kFlowRecBytes * (size_t)ncp;
     s_lvl[tid] = (int)(gld4(st + 2 * tid - 2 * (tid & 1)) >> (16 * (tid & 1))) & 0xFFFF;
   }
   {
@@ -2014,12 +2016,11 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
   }
 }
 
-void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int lds, int32_t* d_err, hipStream_t s) {
-  (void)lds;
+void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int stage_mode, int32_t* d_err, hipStream_t s) {
   if (njobs <= 0) return;
   // DG_RUN_STAGE=0 / 1 forces the mode (tests run every run block through both)
   const char* force = getenv("DG_RUN_STAGE");
-  const bool stage = force && *force ? *force != '0' : njobs <= kRunStageBlocks;
+  const bool stage = force && *force ? *force != '0' : stage_mode == 2 || (stage_mode == 1 && njobs <= kRunStageBlocks);
   if (stage) hipLaunchKernelGGL(k_lz4_run<true>, dim3(njobs), dim3(kRunThreads), 0, s, d_jobs, d_err);
   else hipLaunchKernelGGL(k_lz4_run<false>, dim3(njobs), dim3(kRunThreads), 0, s, d_jobs, d_err);
 }

@@ -186,9 +186,9 @@ static int lz4_max_depth(const uint8_t* in, int n, int cap) {
 // chains a 4-byte pattern through every earlier occurrence, so this shortens the chains (noisy doubles:
 // 24 -> 8 levels). Every match then gets its copy-chain level — one more than the highest level among
 // the bytes of its (forwarded) source; literal bytes are level 0 — and its rank in the block's matches
-// ordered by (level, position). Appended per interval: kLzSeqPerCp u16 ranks (0xFFFF: no match),
-// kLzSeqPerCp u16 forwarded distances and kLzSeqPerCp u16 token offsets from the interval's first
-// token (0xFFFF: no such sequence; the decoder parses an interval's tokens independently); then the u16
+// ordered by (level, position). Appended per interval (kFlowRecBytes): kLzSeqPerCp u16 ranks (0xFFFF: no
+// match), kLzSeqPerCp u16 forwarded distances and kLzSeqPerCp u16 token offsets from the interval's
+// first token (0xFFFF: no such sequence; the decoder parses an interval's tokens independently); then the u16
 // start of every level's ranks (nlvl + 1 of them, zero padded to 16 bytes). Returns the highest level,
 // or -1 above `cap` or when a token lies 64 KiB or more past its interval's first (nothing appended).
 static int lz4_flow_schedule(const uint8_t* in, int n, int64_t g, int cap, std::vector<uint8_t>* lv) {
@@ -259,7 +259,7 @@ static int lz4_flow_schedule(const uint8_t* in, int n, int64_t g, int cap, std::
   for (int64_t i = 0; i < m; ++i)  // token offsets as u16 deltas from the interval's first token
     for (int64_t q = 1; q < g && i * g + q < (int64_t)seqp.size(); ++q)
       if (seqp[i * g + q] - seqp[i * g] >= 0xFFFF) return -1;
-  const size_t at = lv->size(), rec = 6 * kLzSeqPerCp;  // per interval: ranks, distances, token deltas
+  const size_t at = lv->size(), rec = kFlowRecBytes;  // per interval: ranks, distances, token deltas, levels
   lv->resize(at + (size_t)m * rec + (((size_t)(mx + 1) * 2 + 15) & ~(size_t)15), 0);
   for (int64_t i = 0; i < m; ++i)
     for (int q = 0; q < kLzSeqPerCp; ++q) {
@@ -506,7 +506,8 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
   if (col->codec == CODEC_LZ4 || col->codec == CODEC_LZF) {
     col->comp_off.resize(blocks.n);
     col->comp_len.resize(blocks.n);
-    int64_t total = 0;
+    int64_t total = kCompSlack;  // (slack before the first block and after the last: the decoders read
+                                 // whole dwords around a token or a literal run, from global memory too)
     col->lit_off.clear();
     for (int32_t b = 0; b < blocks.n; ++b) {
       const uint8_t* p;
@@ -525,7 +526,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
       col->comp_len[b] = len;
       total = (col->comp_off[b] + len + 15) & ~(int64_t)15;
     }
-    std::vector<uint8_t> host((size_t)total + 16, 0);
+    std::vector<uint8_t> host((size_t)total + kCompSlack, 0);
     for (int32_t b = 0; b < blocks.n; ++b) {
       const uint8_t* p;
       int32_t len = blocks.get(b, &p);
