@@ -3893,6 +3893,40 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
     }
     return a.type == hipMemoryTypeHost;
   };
+  // pinned destinations the device can address: the pack kernel writes the columns straight into them
+  // over PCIe (posted writes from every CU; no staging, no DMA copy). DG_FETCH_ZC=0: the staged DMA path.
+  auto dev_ptr = [](void* h) -> void* {
+    if (!h) return nullptr;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    return d;
+  };
+  static const bool zc_off = [] {
+    const char* v = getenv("DG_FETCH_ZC");
+    return v && *v == '0';
+  }();
+  if (!zc_off && pinned(bucket_time) && pinned(ids) && pinned(values)) {
+    int64_t* dt = static_cast<int64_t*>(dev_ptr(bucket_time));
+    int32_t* di = static_cast<int32_t*>(dev_ptr(ids));
+    uint64_t* dv = static_cast<uint64_t*>(dev_ptr(values));
+    if ((!bucket_time || dt) && (!ids || di) && (!values || dv)) {
+      const int64_t* d_bounds = nullptr;
+      if (r->period && !r->bounds.empty()) {
+        int64_t* db;
+        int64_t* hb = up_take<int64_t>(cs, r->bounds.size(), &db, st);
+        if (!hb) return set_error(DG_ERR_OOM, "bucket table");
+        memcpy(hb, r->bounds.data(), r->bounds.size() * 8);
+        d_bounds = db;
+      }
+      DG_FLUSH(cs, st);
+      launch_gb_fetch_pack(r->keys, r->slots, r->cap, start, count, r->lay, na, r->universal, r->bucket0, r->period, d_bounds,
+                           dt, nd ? di : nullptr, na ? dv : nullptr, st);
+      return finish_call(cs, st);
+    }
+  }
   if (pinned(bucket_time) && pinned(ids) && pinned(values)) {
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, ((int64_t)256 << 20) / per));
     uint8_t* d_stage = dev_take<uint8_t>(cs, (size_t)(chunk * per + 64));
