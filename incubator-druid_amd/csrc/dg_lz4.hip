@@ -1125,8 +1125,9 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 // the bytes it copies, literal bytes are level 0; every match has its rank in (level, position) order):
 //   1. stage + parse + scan as in k_lz4_decode (every thread: one checkpoint interval in registers) and
 //      zero the image;
-//   2. level 0: every thread ORs its short literal runs into the image, long runs are split evenly over
-//      the threads (as in k_lz4_decode);
+//   2. level 0: every thread ORs its literal runs of up to 8 bytes into the image from its parse
+//      registers; every 16-byte piece of a longer run is a job, and thread t then copies job t from the
+//      staged input;
 //   3. the staged input is dead: every thread writes its matches (start, forwarded distance, length)
 //      into a table over it, at their ranks — each level's matches are then one contiguous range;
 //   4. levels 1 .. nlvl, one barrier each: thread t copies matches t, t + 1024, ... of the level's range
@@ -1135,12 +1136,11 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
 // A copy reads its source dwords (one more than the destination dwords it covers) and funnels them to
 // the destination's alignment; whole destination dwords are plain stores, the partial ones at its ends
 // LDS atomic ORs into the zeroed image (a neighbouring run owns the other bytes). LDS: staged input
-// (later the match table) 66 KiB + image 64 KiB + literal jobs 12 KiB: one block per CU, like
+// (later the match table) 66 KiB + image 64 KiB + literal jobs 8 KiB: one block per CU, like
 // k_lz4_decode.
 // ------------------------------------------------------------------------------------------------
-constexpr int kFlowJobs = 1024;     // cooperative literal runs per block
-constexpr int kFlowLongLit = 16;    // literal runs longer than this are split over the threads
-constexpr int kFlowRegLit = 8;      // literal runs up to this ride in the parse registers
+constexpr int kFlowJobs = 1024;     // literal-run jobs per block (one per thread)
+constexpr int kFlowRegLit = 8;      // literal runs up to this ride in the parse registers; longer ones are jobs
 constexpr int kFlowPad = 4;         // dwords before the staged input and the image: a copy's first
                                     // source dword may start up to 3 bytes before its source
 constexpr int kFlowInWords = kFlowPad + (kLz4InCap + 32) / 4 + 8;  // (+ the unconditional reads past a copy)
@@ -1306,8 +1306,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   constexpr int SEQ = kLzSeqPerCp;
   __shared__ __attribute__((aligned(16))) uint32_t s_in32[kFlowInWords];    // staged input (after the pad)
   __shared__ __attribute__((aligned(16))) uint32_t s_out32[kFlowOutWords];  // the decoded image (after the pad)
-  __shared__ uint2 s_job[kFlowJobs];  // long literal runs: output start | (L - 1) << 16, input offset
-  __shared__ int s_jpre[kFlowJobs];
+  __shared__ uint2 s_job[kFlowJobs];  // literal runs past the registers: output start | (L - 1) << 16, input offset
   __shared__ int s_lvl[kFlowMaxDepth + 1];  // s_lvl[k - 1] .. s_lvl[k]: the table rows of level k
   __shared__ int s_njob, s_bad;
   __shared__ int s_tmp[kLzWaves];
@@ -1396,22 +1395,29 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   // ---- 2. level 0: literals into the image; long runs become jobs split evenly over the threads ----
   constexpr uint32_t kOwnLit = 0x80000000u;  // r_L flag: a long run the job table had no room for
   {
+    // a run past the registers: one job per 16 bytes of it
+    auto pieces = [](int L) { return L > kFlowRegLit ? (L + 15) >> 4 : 0; };
     int need = 0;
 #pragma unroll
     for (int s = 0; s < SEQ; ++s)
-      if (s < cnt) need += (int)r_L[s] > kFlowLongLit;
+      if (s < cnt) need += pieces((int)r_L[s]);
     int j = __ballot(need) ? wave_alloc(&s_njob, need) : 0;
     int o = base;
 #pragma unroll
     for (int s = 0; s < SEQ; ++s) {
       if (s < cnt) {
         const int L = (int)r_L[s], d = (int)(r_DM[s] & 0xFFFF), M = (int)(r_DM[s] >> 16);
-        if (L > kFlowLongLit) {
-          if (j < kFlowJobs) s_job[j] = make_uint2((uint32_t)o | ((uint32_t)(L - 1) << 16), r_lv[s]);
-          else r_L[s] |= kOwnLit;
-          ++j;
-        } else if (L > kFlowRegLit) {
-          flow_copyn<5>(s_out32, o, s_in32, (int)r_lv[s], L);
+        if (L > kFlowRegLit) {
+          const int nq = pieces(L);
+          // (every slot below the table's end is written — the job threads read slots 0 .. min(jobs,
+          // table) - 1 — and a run that does not fit whole is also copied by its own thread: its
+          // pieces that got a slot write the same bytes again, an OR of equal values)
+#pragma unroll 1
+          for (int q = 0; q < nq && j + q < kFlowJobs; ++q)
+            s_job[j + q] = make_uint2((uint32_t)(o + 16 * q) | ((uint32_t)(min(16, L - 16 * q) - 1) << 16),
+                                      r_lv[s] + 16u * (uint32_t)q);
+          if (j + nq > kFlowJobs) r_L[s] |= kOwnLit;
+          j += nq;
         } else if (L > 0) {  // the literal bytes ride in r_lv / r_lvh: cut to L bytes, up to three ORs, no reads
           const int a = o & 3;
           const uint64_t x = ((uint64_t)r_lv[s] | ((uint64_t)r_lvh[s] << 32)) & (~0ull >> (64 - 8 * L));
@@ -1431,37 +1437,12 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   }
   LZ_STAMP(13);
   __syncthreads();
+  // every 16-byte piece of a literal run longer than the registers hold is one job: thread t copies job t
   const int nj = min(s_njob, kFlowJobs);
-  if (nj > 0) {
-    int l0 = 0, l1 = 0;
-    if (2 * tid < nj) l0 = job_len(s_job[2 * tid]);
-    if (2 * tid + 1 < nj) l1 = job_len(s_job[2 * tid + 1]);
-    int tot;
-    const int pre = block_scan_lz(l0 + l1, &tot, s_tmp);
-    if (2 * tid < nj) s_jpre[2 * tid] = pre;
-    if (2 * tid + 1 < nj) s_jpre[2 * tid + 1] = pre + l0;
-    __syncthreads();
-    LZ_STAMP(14);
-    // my contiguous range of the flat job bytes, copied piece by piece (a piece lies in one run)
-    const int per = (tot + kLzThreads - 1) / kLzThreads;
-    const int g0 = tid * per, gend = min(g0 + per, tot);
-    if (g0 < gend) {
-      int lo = 0, hi = nj - 1;
-      while (lo < hi) {  // last job with s_jpre <= g0
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_jpre[mid] <= g0) lo = mid;
-        else hi = mid - 1;
-      }
-#pragma unroll 1
-      for (int g = g0, wj = lo; g < gend; ++wj) {
-        const int js = s_jpre[wj];
-        const uint2 jb = s_job[wj];
-        const int je = js + job_len(jb);
-        const int len = min(gend, je) - g;
-        flow_copy(s_out32, (int)(jb.x & 0xFFFF) + (g - js), s_in32, (int)jb.y + (g - js), len);
-        g += len;
-      }
-    }
+  LZ_STAMP(14);
+  if (tid < nj) {
+    const uint2 jb = s_job[tid];
+    flow_copyn<5>(s_out32, (int)(jb.x & 0xFFFF), s_in32, (int)jb.y, job_len(jb));
   }
   LZ_STAMP(15);
   if (tid < ncp) {  // long runs the job table had no room for: their own thread copies them. From
