@@ -2945,18 +2945,27 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   rc = finish_call(cs, st);
   ht.mark("synced");
   if (rc) return rc;
-  for (int k = 0; k < ns; ++k) {  // unpack [id, rec slots] records into ids + rec-strided slots
-    h_ncand[k] = *reinterpret_cast<const int32_t*>(h_selmem + sel_words * k + 4);
+  for (int k = 0; k < ns; ++k) h_ncand[k] = *reinterpret_cast<const int32_t*>(h_selmem + sel_words * k + 4);
+  // k_topn_order left a list's records in output order (`sorted_at`); the replays that walk the
+  // candidates in id order unpack them first (ids + rec-strided slots, back in id order)
+  auto ordered = [&](int k) { return h_ncand[k] > 0 && h_ncand[k] <= jgcap[k] && h_ncand[k] <= kTopnOrderCap; };
+  auto order_of = [&](int k) { return reinterpret_cast<const uint16_t*>(h_gath + jgoff[k] + jgcap[k] * (rec + 1)); };
+  auto sorted_at = [&](int k, int e) { return h_gath + jgoff[k] + (int64_t)e * (rec + 1); };  // [id, rec slots]
+  auto unpack = [&](int k) -> int {
+    if (h_cand[k]) return DG_OK;
     const int64_t g = std::min<int64_t>(jgcap[k], h_ncand[k]);
     h_cand[k] = host_take<int32_t>(cs, (size_t)std::max<int64_t>(jgcap[k], 1));
     h_tab[k] = host_take<uint64_t>(cs, (size_t)std::max<int64_t>(jgcap[k], 1) * rec);
     if (!h_cand[k] || !h_tab[k]) return set_error(DG_ERR_OOM, "topN read-back");
     const uint64_t* src = h_gath + jgoff[k];
-    for (int64_t c = 0; c < g; ++c) {
-      h_cand[k][c] = (int32_t)src[c * (rec + 1)];
-      memcpy(h_tab[k] + c * rec, src + c * (rec + 1) + 1, 8 * (size_t)rec);
+    const uint16_t* ord = ordered(k) ? order_of(k) : nullptr;
+    for (int64_t e = 0; e < g; ++e) {
+      const int64_t c = ord ? ord[e] : e;
+      h_cand[k][c] = (int32_t)src[e * (rec + 1)];
+      memcpy(h_tab[k] + c * rec, src + e * (rec + 1) + 1, 8 * (size_t)rec);
     }
-  }
+    return DG_OK;
+  };
   ht.mark("unpacked");
   // rare: more candidates than the speculative read-back held (many ties at the K-th key)
   bool again = false;
@@ -2989,6 +2998,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   ht.mark("overflow_checked");
   // replay TopNNumericResultBuilder over the candidates in id (= dimension value) order
   for (int k = 0; k < ns; ++k) {
+    if (k == 1) ht.mark("replayed_seg0");
     const int i = sel_seg[k];
     m.selected_rows += (int64_t)h_state[sel_words * k + 1];
     const int nc = h_ncand[k];
@@ -3006,16 +3016,23 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       const int32_t* hr = dim_rank_host[i];
       auto rank_of = [&](int c) { return hr ? hr[h_cand[k][c]] : 0; };
       std::vector<int> res;
-      if (!dim_ties[i]) {  // distinct ranks: the K smallest, ascending
-        if (nc > 0 && nc <= jgcap[k] && nc <= kTopnOrderCap) {
-          const uint16_t* ord = reinterpret_cast<const uint16_t*>(h_gath + jgoff[k] + jgcap[k] * (rec + 1));
-          for (int e = 0; e < std::min(nc, K); ++e) res.push_back(ord[e]);
-        } else {
-          res.resize(nc);
-          for (int c = 0; c < nc; ++c) res[c] = c;
-          std::sort(res.begin(), res.end(), [&](int a, int b) { return rank_of(a) < rank_of(b); });
-          if ((int)res.size() > K) res.resize(K);
+      if (!dim_ties[i] && ordered(k)) {  // distinct ranks: the K smallest, ascending = the first K in order
+        const int nout = std::min(nc, K);
+        out_n[out_base[k]] = nout;
+        for (int e = 0; e < nout; ++e) {
+          const int64_t o = out_base[k] * t->threshold + (int64_t)e;
+          const uint64_t* r = sorted_at(k, e);
+          out_ids[o] = (int32_t)r[0];
+          for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], r[2 + a]);
         }
+        continue;
+      }
+      if ((rc = unpack(k))) return rc;
+      if (!dim_ties[i]) {
+        res.resize(nc);
+        for (int c = 0; c < nc; ++c) res[c] = c;
+        std::sort(res.begin(), res.end(), [&](int a, int b) { return rank_of(a) < rank_of(b); });
+        if ((int)res.size() > K) res.resize(K);
       } else {  // java.util.PriorityQueue, literally (OpenJDK 8 siftUp / siftDown)
         const Column* dc = reinterpret_cast<Segment*>(segs[i])->find(t->dimension);
         auto is_null = [&](int c) { return !dc || dc->dict_null[h_cand[k][c]]; };
@@ -3063,38 +3080,40 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       continue;
     }
     std::vector<E> v;
-    if (nc > 0 && nc <= jgcap[k] && nc <= kTopnOrderCap) {
-      // k_topn_order sorted the candidates by (key desc, id asc); keep every key > kth and, of the
-      // kth ties, those the builder's queue keeps (see below), already in output order
-      const uint16_t* ord = reinterpret_cast<const uint16_t*>(h_gath + jgoff[k] + jgcap[k] * (rec + 1));
-      auto key_at = [&](int c) { return metric_key_host(h_tab[k][(size_t)c * rec + 1 + t->metric_agg], mk, t->inverted); };
+    if (ordered(k)) {
+      // k_topn_order sorted the candidates by (key desc, id asc) and left their records in that
+      // order; keep every key > kth and, of the kth ties, those the builder's queue keeps (see
+      // below), already in output order
+      const uint16_t* ord = order_of(k);
+      auto key_at = [&](int e) { return metric_key_host(sorted_at(k, e)[2 + t->metric_agg], mk, t->inverted); };
       const int r = std::min(nc, K) - 1;
-      const uint64_t kth = key_at(ord[r]);
-      bool exact = key_at(ord[nc - 1]) >= kth;  // nothing below the K-th key
-      int g = 0, gF = 0;
-      while (g < nc && key_at(ord[g]) > kth) gF += ord[g++] < K;
+      const uint64_t kth = key_at(r);
+      bool exact = key_at(nc - 1) >= kth;  // nothing below the K-th key
       if (exact) {
-        for (int e = 0; e < g; ++e) v.push_back(E{0, h_cand[k][ord[e]], (int32_t)ord[e]});
+        int g = 0, gF = 0;
+        while (g < nc && key_at(g) > kth) gF += ord[g++] < K;
         int skip = g - gF;  // ties popped by later pushes into the full queue, oldest first
-        for (int e = g; e < nc && (int)v.size() < K; ++e) {
+        int nout = 0;
+        auto emit = [&](int e) {
+          const int64_t o = out_base[k] * t->threshold + (int64_t)nout++;
+          const uint64_t* rr = sorted_at(k, e);
+          out_ids[o] = (int32_t)rr[0];
+          for (int a = 0; a < na; ++a) out_values[o * na + a] = finalize_slot(plan.kind[a], rr[2 + a]);
+        };
+        for (int e = 0; e < g; ++e) emit(e);
+        for (int e = g; e < nc && nout < K; ++e) {
           if (ord[e] >= K) continue;  // a tie after the queue filled is never pushed
           if (skip > 0) {
             skip--;
             continue;
           }
-          v.push_back(E{0, h_cand[k][ord[e]], (int32_t)ord[e]});
+          emit(e);
         }
-        out_n[out_base[k]] = (int32_t)v.size();
-        for (size_t e = 0; e < v.size(); ++e) {
-          const int64_t o = out_base[k] * t->threshold + (int64_t)e;
-          out_ids[o] = v[e].id;
-          for (int a = 0; a < na; ++a)
-            out_values[o * na + a] = finalize_slot(plan.kind[a], h_tab[k][(size_t)v[e].idx * rec + 1 + a]);
-        }
+        out_n[out_base[k]] = (int32_t)nout;
         continue;
       }
-      v.clear();
     }
+    if ((rc = unpack(k))) return rc;
     std::vector<E> all(nc);
     for (int c = 0; c < nc; ++c)
       all[c] = E{metric_key_host(h_tab[k][(size_t)c * rec + 1 + t->metric_agg], mk, t->inverted), h_cand[k][c], c};
@@ -3264,12 +3283,16 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
   struct Ent {
     int32_t list;
     int64_t key;
-    uint64_t mkey;  // comparator key of the metric (Long/Double/Float.compare, inverted)
-    size_t vo;      // first value slot in `vals`
+    uint64_t mkey;       // comparator key of the metric (Long/Double/Float.compare, inverted)
+    uint64_t h;          // identity hash of the dimension value (see ident)
+    const uint64_t* v;   // value slots: the caller's list row until combined, then a row of `vals`
   };
   int64_t total = 0;
   for (int l = 0; l < nl; ++l) total += std::max(in->list_n[l], 0);
+  // rows of combined values (copy on first combine; at most one per entry)
   std::vector<uint64_t> vals((size_t)std::max<int64_t>(total, 1) * std::max(na, 1));
+  size_t vo = 0;
+  auto owned = [&](const uint64_t* v) { return v >= vals.data() && v < vals.data() + vals.size(); };
   // dimension value of an entry: (is null, bytes)
   auto value_of = [&](const Ent& e, std::string_view* sv) -> bool {
     const Column* c = lcol[e.list];
@@ -3341,20 +3364,20 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
   };
   std::vector<Ent> acc, cur;
   bool have = false;
-  size_t vo = 0;
+  const int ma = t->metric_agg, inv = t->inverted;
   for (int l = 0; l < nl; ++l) {
     const int cnt = in->list_n[l];
     if (cnt < 0) continue;  // no cursor: no result from this segment
     cur.resize(cnt);
-    for (int e = 0; e < cnt; ++e) {
-      const int64_t o = (int64_t)l * in->stride + e;
-      cur[e].list = l;
-      cur[e].key = in->keys[o];
-      cur[e].vo = vo;
-      memcpy(vals.data() + vo, in->values + o * na, 8 * (size_t)na);
-      cur[e].mkey = abi_metric_key(mk, vals[vo + t->metric_agg], t->inverted);
-      vo += na;
+    const int64_t* ks = in->keys + (int64_t)l * in->stride;
+    const uint64_t* vs = in->values + (int64_t)l * in->stride * na;
+    for (int e = 0; e < cnt; ++e) {  // the entries reference the caller's rows (no copy)
+      const uint64_t* v = vs + (int64_t)e * na;
+      cur[e] = Ent{l, ks[e], abi_metric_key(mk, v[ma], inv), 0, v};
     }
+    // the value hashes in a pass of their own: independent dictionary reads the core overlaps (one
+    // random read per entry; interleaved with the table probes they were serialized)
+    for (int e = 0; e < cnt; ++e) cur[e].h = ident(cur[e]);
     if (!have) {
       acc.swap(cur);
       have = true;
@@ -3363,7 +3386,7 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
     // retVals (LinkedHashMap): r1's entries, then r2's new values; shared values combined in place
     table_reset(acc.size() + cur.size());
     auto find_or_insert = [&](const Ent& e, int32_t idx) -> int32_t {
-      const uint64_t h = ident(e);
+      const uint64_t h = e.h;
       for (size_t q = h & tmask;; q = (q + 1) & tmask) {
         if (slot_of[q] < 0) {
           slot_of[q] = idx;
@@ -3378,8 +3401,14 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
       const int32_t hit = find_or_insert(e, (int32_t)acc.size());
       if (hit >= 0) {
         Ent& a = acc[hit];
-        for (int k = 0; k < na; ++k) vals[a.vo + k] = combine_abi(plan.kind[k], vals[a.vo + k], vals[e.vo + k]);
-        a.mkey = abi_metric_key(mk, vals[a.vo + t->metric_agg], t->inverted);
+        if (!owned(a.v)) {
+          memcpy(vals.data() + vo, a.v, 8 * (size_t)na);
+          a.v = vals.data() + vo;
+          vo += na;
+        }
+        uint64_t* w = const_cast<uint64_t*>(a.v);
+        for (int k = 0; k < na; ++k) w[k] = combine_abi(plan.kind[k], w[k], e.v[k]);
+        a.mkey = abi_metric_key(mk, w[ma], inv);
       } else {
         acc.push_back(e);
       }
@@ -3391,7 +3420,7 @@ int dg_topn_merge(dg_segment* const* segs, const dg_scan* q, const dg_topn* t, c
   for (int e = 0; e < nout; ++e) {
     if (out_list) out_list[e] = acc[e].list;
     if (out_keys) out_keys[e] = acc[e].key;
-    if (out_values) memcpy(out_values + (size_t)e * na, vals.data() + acc[e].vo, 8 * (size_t)na);
+    if (out_values) memcpy(out_values + (size_t)e * na, acc[e].v, 8 * (size_t)na);
   }
   return DG_OK;
 }

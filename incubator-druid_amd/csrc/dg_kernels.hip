@@ -1247,8 +1247,8 @@ __global__ __launch_bounds__(1024) void k_topn_order(const TopnSelJob* __restric
   __shared__ uint64_t s_key[kOrderCap];
   __shared__ uint16_t s_pos[kOrderCap];
   const TopnSelJob& jb = jobs[blockIdx.x];
-  const int n = min(*jb.ncand, jb.gather_cap);
-  if (n > kOrderCap || n <= 0) return;
+  const int n = *jb.ncand;
+  if (n > kOrderCap || n > jb.gather_cap || n <= 0) return;  // the host replays in id order then
   int P = 1;
   while (P < n) P <<= 1;
   const int rec = naggs + 1;
@@ -1281,6 +1281,23 @@ __global__ __launch_bounds__(1024) void k_topn_order(const TopnSelJob* __restric
     }
   }
   for (int c = threadIdx.x; c < n; c += 1024) jb.order[c] = s_pos[c];
+  // the gathered records permuted into that order, in place, one record word at a time (every
+  // read of the word before the barrier, every write after it): the host reads its lists in order
+  const int rw = rec + 1;
+  for (int w = 0; w < rw; ++w) {
+    uint64_t v[kOrderCap / 1024];
+#pragma unroll
+    for (int j = 0; j < kOrderCap / 1024; ++j) {
+      const int c = threadIdx.x + j * 1024;
+      v[j] = c < n ? jb.gathered[(size_t)s_pos[c] * rw + w] : 0ull;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kOrderCap / 1024; ++j) {
+      const int c = threadIdx.x + j * 1024;
+      if (c < n) jb.gathered[(size_t)c * rw + w] = v[j];
+    }
+  }
 }
 
 void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, int naggs, int metric, int metric_op,

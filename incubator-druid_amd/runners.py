@@ -453,9 +453,14 @@ def topn_merge_raw(query: Q.TopNQuery, cnt: np.ndarray, keys: np.ndarray, vals: 
         return None
     order = np.array(sorted(live, key=lambda i: (int(ts[i]), i)), dtype=np.int64)
     n = len(order)
-    o_cnt = np.ascontiguousarray(cnt[order].astype(np.int32))
-    o_keys = np.ascontiguousarray(keys.reshape(-1, K)[order].astype(np.int64))
-    o_vals = np.ascontiguousarray(vals.reshape(-1, K, max(na, 1))[order])
+    if n == len(cnt) and not np.any(order != np.arange(n)):  # every list, already in merge order
+        o_cnt = np.ascontiguousarray(cnt, dtype=np.int32)
+        o_keys = np.ascontiguousarray(keys, dtype=np.int64)
+        o_vals = np.ascontiguousarray(vals)
+    else:
+        o_cnt = np.ascontiguousarray(cnt[order].astype(np.int32))
+        o_keys = np.ascontiguousarray(keys.reshape(-1, K)[order].astype(np.int64))
+        o_vals = np.ascontiguousarray(vals.reshape(-1, K, max(na, 1))[order])
     lists = N.dg_topn_lists()
     lists.n_lists = n
     lists.list_n = o_cnt.ctypes.data

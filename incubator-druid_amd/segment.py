@@ -79,6 +79,8 @@ class GpuSegment:
         self.min_time, self.max_time = s.value, e.value
         self._dicts: Dict[str, List[Optional[str]]] = {}
         self._orders: Dict[Tuple[str, int], O.DictionaryOrder] = {}
+        self._types: Dict[str, int] = {}  # a segment's columns never change once attached / built
+        self._values: Dict[str, Dict[int, Optional[str]]] = {}  # dim_value lookups already made
 
     # -- StorageAdapter-ish facts ------------------------------------------------------------
     def columns(self) -> List[str]:
@@ -86,7 +88,10 @@ class GpuSegment:
         return [L.dg_segment_column_name(self.handle, i).decode() for i in range(L.dg_segment_num_columns(self.handle))]
 
     def column_type(self, name: str) -> int:
-        return N.lib().dg_segment_column_type(self.handle, name.encode())
+        t = self._types.get(name)
+        if t is None:
+            t = self._types[name] = N.lib().dg_segment_column_type(self.handle, name.encode())
+        return t
 
     def device_bytes(self) -> int:
         return int(N.lib().dg_segment_device_bytes(self.handle))
@@ -135,13 +140,19 @@ class GpuSegment:
         d = self._dicts.get(dim)
         if d is not None:
             return d[idx]
+        seen = self._values.get(dim)
+        if seen is not None and idx in seen:
+            return seen[idx]
         if self.column_type(dim) != N.COL_STRING:
             return None
         p, n = ctypes.c_void_p(), ctypes.c_int32()
         N.check(N.lib().dg_segment_dim_value(self.handle, dim.encode(), int(idx), ctypes.byref(p), ctypes.byref(n)))
-        if n.value <= 0:
-            return None
-        return ctypes.string_at(p.value, n.value).decode("utf-8")
+        v = ctypes.string_at(p.value, n.value).decode("utf-8") if n.value > 0 else None
+        if seen is None:
+            seen = self._values[dim] = {}
+        if len(seen) < 65536:  # the ids a query's results name again (topN heads), bounded
+            seen[int(idx)] = v
+        return v
 
     def filter_bitmap(self, flt, query_module) -> Tuple[np.ndarray, int]:
         """Filter.getBitmapResult as a dense row bitset (uint32 words) + cardinality."""
