@@ -1441,7 +1441,11 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   memcpy(h, J.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
   Context* ctx = cs->ctx;
-  const bool ovl = overlap && ctx && ctx->side && st == ctx->stream && nh > nr && (nr > 0 || n > nh) && !d_prof;
+  static const bool no_ovl = [] {
+    const char* v = getenv("DG_NO_OVERLAP");  // (same-box A/B: every decoder on the call's stream)
+    return v && *v && *v != '0';
+  }();
+  const bool ovl = overlap && !no_ovl && ctx && ctx->side && st == ctx->stream && nh > nr && (nr > 0 || n > nh) && !d_prof;
   hipStream_t ss = st;
   if (ovl) {
     hipEventRecord(ctx->ovl_ev[0], st);

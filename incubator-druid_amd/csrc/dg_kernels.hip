@@ -459,6 +459,14 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
   const int64_t row0 = (int64_t)(tile - j.tile_begin) * kTileRows;
   const int64_t row_end = min((int64_t)j.nrows, row0 + kTileRows);
   const int na = plan.n;
+  // a tile whose filter bitset is empty selects nothing: one load of its 64 words, then done (a
+  // selective filter leaves most tiles empty; the bits past the segment's last row only keep it)
+  static_assert(kTileRows == 32 * 64 && kTileRows % 32 == 0, "one bitset word per thread of the first wave");
+  if (j.bitset) {
+    const int nw = (int)((row_end - row0 + 31) >> 5);
+    const uint32_t w = (int)threadIdx.x < nw ? j.bitset[(row0 >> 5) + threadIdx.x] : 0u;
+    if (!__syncthreads_or(w != 0u)) return;
+  }
 
   if (TOPN) {
     // topN over a multi-value dimension (PooledTopNAlgorithm.scanAndAggregate: every value of the
