@@ -1457,8 +1457,15 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   // stream's general decoder only when it is small (latency), and a call decoding on the side stream
   // beside the main stream's sort never (it would wait for whole CUs)
   const int stage = ctx && st == ctx->side ? 0 : ss == st ? 2 : 1;
+  // with the run blocks beside it, the light blocks follow the general decoder on `st` (the run
+  // decoder alone is the longer leg: topN's side stream was run + light while `st` idled)
+  static const int light_env = [] {
+    const char* v = getenv("DG_LIGHT_MAIN");  // (same-box A/B: 1 = light blocks on `st`, 0 = beside)
+    return v && *v ? (*v != '0' ? 1 : 0) : -1;
+  }();
+  const bool light_main = ovl && nr > 0 && light_env != 0;
   launch_lz4_run(d, nr, stage, d_err, ss);
-  launch_lz4_light(d + nh, n - nh, d_err, ss, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
+  if (!light_main) launch_lz4_light(d + nh, n - nh, d_err, ss, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
   if (ovl) hipEventRecord(ctx->ovl_ev[1], ss);
   const int ng = nh - nr;  // general-decoder blocks
   for (int i = nr; i < nh; ++i) db->gen_bytes += J[i].src_len;
@@ -1468,6 +1475,7 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   for (int w = 0; w < 4; ++w)
     launch_lz4_decode(d + kb[w], kb[w + 1] - kb[w], w, d_err, st, d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
   if (db->gen_a && ng) phase_event(db->gen_b, st);
+  if (light_main) launch_lz4_light(d + nh, n - nh, d_err, st, nullptr);
   if (ovl) DG_HIP(hipStreamWaitEvent(st, ctx->ovl_ev[1], 0));
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
