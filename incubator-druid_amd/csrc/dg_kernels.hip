@@ -1029,12 +1029,16 @@ __device__ __forceinline__ uint64_t metric_key(uint64_t slot, int op, int kind, 
 }
 
 // Replay the radix digit choices of levels [0, levels) from the histograms: wave-parallel (64 lanes x
-// 4 bins, descending digit order), result in (*prefix, *mask). Called by one full wave.
-__device__ void replay_digits(const uint32_t* __restrict__ hist, int levels, int64_t threshold, uint64_t* prefix_out,
-                              uint64_t* mask_out) {
+// 4 bins, descending digit order), result in (*prefix, *mask). Called by one full wave. The replay
+// ends early at a level whose chosen bucket is needed whole (its count = the keys still to take):
+// exactly `threshold` keys are >= the prefix with zero low bits, so that is the K-th key bound and
+// the deeper levels are not needed; returns the levels replayed.
+__device__ int replay_digits(const uint32_t* __restrict__ hist, int levels, int64_t threshold, uint64_t* prefix_out,
+                             uint64_t* mask_out) {
   const int lane = threadIdx.x & 63;
   uint64_t prefix = 0, mask = 0;
   int64_t krem = threshold;
+  int used = levels;
   for (int q = 0; q < levels; ++q) {
     const int shift = 56 - 8 * q;
     int64_t h[4], sum = 0;
@@ -1054,6 +1058,7 @@ __device__ void replay_digits(const uint32_t* __restrict__ hist, int levels, int
     const unsigned long long bm = __ballot(hit);
     int digit = 0;
     int64_t nk = krem;
+    int whole = 0;
     if (hit) {
       int64_t cum = excl;
 #pragma unroll
@@ -1061,6 +1066,7 @@ __device__ void replay_digits(const uint32_t* __restrict__ hist, int levels, int
         if (cum + h[j] >= krem) {
           digit = 255 - (lane * 4 + j);
           nk = krem - cum;
+          whole = h[j] == nk;
           break;
         }
         cum += h[j];
@@ -1070,13 +1076,19 @@ __device__ void replay_digits(const uint32_t* __restrict__ hist, int levels, int
       const int src = __ffsll((long long)bm) - 1;
       digit = __shfl(digit, src, 64);
       nk = __shfl(nk, src, 64);
+      whole = __shfl(whole, src, 64);
     }
     prefix |= (uint64_t)digit << shift;
     mask |= 255ull << shift;
     krem = nk;
+    if (whole) {
+      used = q + 1;
+      break;
+    }
   }
   *prefix_out = prefix;
   *mask_out = mask;
+  return used;
 }
 
 // DimensionTopNMetricSpec key of a touched id: smaller dictionary rank = larger key; 0 = not eligible
@@ -1140,19 +1152,22 @@ __global__ __launch_bounds__(kSelBlock) void k_topn_keys(const TopnSelJob* __res
 __global__ __launch_bounds__(kSelBlock) void k_topn_radix(const TopnSelJob* __restrict__ jobs, int level, int threshold) {
   __shared__ unsigned int s_hist[256];
   __shared__ uint64_t s_prefix, s_mask;
+  __shared__ int s_used;
   const TopnSelJob& jb = jobs[blockIdx.y];
   if ((int64_t)blockIdx.x * kSelBlock >= jb.card) return;
   if ((int64_t)jb.state[2] <= threshold) return;  // everything touched is a candidate
   if (threadIdx.x < 64) {
     uint64_t p, m;
-    replay_digits(jb.hist, level, threshold, &p, &m);
+    const int used = replay_digits(jb.hist, level, threshold, &p, &m);
     if (threadIdx.x == 0) {
       s_prefix = p;
       s_mask = m;
+      s_used = used;
     }
   }
   if (threadIdx.x < 256) s_hist[threadIdx.x] = 0;
   __syncthreads();
+  if (s_used < level) return;  // the bound is final (replay_digits): no deeper histogram
   const int64_t i = (int64_t)blockIdx.x * kSelBlock + threadIdx.x;
   const int shift = 56 - 8 * level;
   if (i < jb.card) {
