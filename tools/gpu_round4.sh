@@ -28,7 +28,7 @@ print('roofline', {k: b['roofline'][k] for k in ('kernel','achieved','frac','avg
 print('checks', b.get('result_checks')); print('cpu', {k: b['cpu_baseline'][k] for k in ('value','cores')})" ;;
     secondary)
       for cfg in ${CONFIGS:-timeseries topn filtered ts_hourly groupby_hourly topn_numeric topn_alphanumeric}; do
-        timeout -k 10 900 python -u bench.py --config "$cfg" --steps 10 --warmup 2 \
+        timeout -k 10 900 python -u bench.py --config "$cfg" --steps ${SEC_STEPS:-10} --warmup 2 \
           > gpurun_out/${TAG}_bench_$cfg.json 2> gpurun_out/${TAG}_bench_$cfg.err || { echo "$cfg failed"; tail -5 gpurun_out/${TAG}_bench_$cfg.err; exit 4; }
         python3 -c "
 import json; b=json.loads(open('gpurun_out/${TAG}_bench_$cfg.json').read().strip().splitlines()[-1])
