@@ -1275,9 +1275,48 @@ __global__ __launch_bounds__(1024) void k_topn_order(const TopnSelJob* __restric
   int P = 1;
   while (P < n) P <<= 1;
   const int rec = naggs + 1;
-  for (int c = threadIdx.x; c < P; c += 1024) {
+  auto key_of = [&](int c) {
     const uint64_t* g = jb.gathered + (size_t)c * (rec + 1);
-    s_key[c] = c >= n ? 0ull : jb.dim_mode ? dim_key(jb, (int64_t)g[0]) : metric_key(g[1 + 1 + metric], op, kind, inverted);
+    return c >= n ? 0ull : jb.dim_mode ? dim_key(jb, (int64_t)g[0]) : metric_key(g[1 + 1 + metric], op, kind, inverted);
+  };
+  if (P <= 1024) {
+    // one element per thread: the compare-exchange stages of stride < 64 between the lanes of a
+    // wave (shuffles, no barrier), the wider ones through LDS (45 of the 55 stages of P = 1024 stay
+    // in registers). Threads >= P pair among themselves (c ^ stride >= P) and are never written.
+    const int c = threadIdx.x;
+    uint64_t k = c < P ? key_of(c) : 0ull;
+    int pos = c;
+    for (int size = 2; size <= P; size <<= 1) {
+      const bool up = (c & size) == 0;
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        uint64_t ko;
+        int po;
+        if (stride >= 64) {
+          s_key[c] = k;
+          s_pos[c] = (uint16_t)pos;
+          __syncthreads();
+          ko = s_key[c ^ stride];
+          po = s_pos[c ^ stride];
+          __syncthreads();
+        } else {
+          ko = __shfl_xor((unsigned long long)k, stride, 64);
+          po = __shfl_xor(pos, stride, 64);
+        }
+        // the same network as below: the lower index of a pair keeps the element that comes first
+        // (larger key, or equal key and smaller position) when `up`, the other one otherwise
+        const bool lower = (c & stride) == 0;
+        const bool mine_first = k != ko ? k > ko : pos < po;
+        if (mine_first != (lower == up)) {
+          k = ko;
+          pos = po;
+        }
+      }
+    }
+    s_pos[c] = (uint16_t)pos;
+    __syncthreads();
+  } else {
+  for (int c = threadIdx.x; c < P; c += 1024) {
+    s_key[c] = key_of(c);
     s_pos[c] = (uint16_t)c;
   }
   __syncthreads();
@@ -1302,6 +1341,7 @@ __global__ __launch_bounds__(1024) void k_topn_order(const TopnSelJob* __restric
       }
       __syncthreads();
     }
+  }
   }
   for (int c = threadIdx.x; c < n; c += 1024) jb.order[c] = s_pos[c];
   // the gathered records permuted into that order, in place, one record word at a time (every
