@@ -289,20 +289,25 @@ static T* up_take(CallScratch* cs, size_t count, T** dev, hipStream_t st) {
   } while (0)
 
 // A phase-timing event (dg_metrics' *_ms fields). dg_set_phase_timing(0) or DG_NO_PHASE_EVENTS=1 leaves
-// them out (the phase times then read 0): a small query pays ~25 us for the timestamps.
+// them out (the phase times then read 0): a small query pays ~25 us for the timestamps. Only timing
+// events go through phase_event: an event another stream waits on is always recorded (hipEventRecord).
+// The switch is read once per call (CallGuard sets t_phase_on), so a toggle from another thread while a
+// call runs cannot make it read elapsed times of events it never recorded.
 static std::atomic<bool> g_phase_timing{true};
+static thread_local bool t_phase_on = true;
+// an engine switch (environment, read per call so tests can flip it): set and not "0"
+static bool env_on(const char* name) {
+  const char* v = getenv(name);
+  return v && *v && *v != '0';
+}
 static bool phase_events_off() {
-  static const bool env_off = [] {
-    const char* v = getenv("DG_NO_PHASE_EVENTS");
-    return v && *v && *v != '0';
-  }();
-  return env_off || !g_phase_timing.load(std::memory_order_relaxed);
+  return env_on("DG_NO_PHASE_EVENTS") || !g_phase_timing.load(std::memory_order_relaxed);
 }
 static void phase_event(hipEvent_t e, hipStream_t st) {
-  if (!phase_events_off()) hipEventRecord(e, st);
+  if (t_phase_on) hipEventRecord(e, st);
 }
 static hipError_t phase_elapsed(float* ms, hipEvent_t a, hipEvent_t b) {
-  if (phase_events_off()) {
+  if (!t_phase_on) {
     *ms = 0.f;
     return hipSuccess;
   }
@@ -1441,10 +1446,7 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   memcpy(h, J.data(), sizeof(Lz4Job) * n);
   DG_FLUSH(cs, st);
   Context* ctx = cs->ctx;
-  static const bool no_ovl = [] {
-    const char* v = getenv("DG_NO_OVERLAP");  // (same-box A/B: every decoder on the call's stream)
-    return v && *v && *v != '0';
-  }();
+  const bool no_ovl = env_on("DG_NO_OVERLAP");  // (same-box A/B and tests: every decoder on the call's stream)
   const bool ovl = overlap && !no_ovl && ctx && ctx->side && st == ctx->stream && nh > nr && (nr > 0 || n > nh) && !d_prof;
   hipStream_t ss = st;
   if (ovl) {
@@ -1459,8 +1461,8 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   const int stage = ctx && st == ctx->side ? 0 : ss == st ? 2 : 1;
   // with the run blocks beside it, the light blocks follow the general decoder on `st` (the run
   // decoder alone is the longer leg: topN's side stream was run + light while `st` idled)
-  static const int light_env = [] {
-    const char* v = getenv("DG_LIGHT_MAIN");  // (same-box A/B: 1 = light blocks on `st`, 0 = beside)
+  const int light_env = [] {
+    const char* v = getenv("DG_LIGHT_MAIN");  // (same-box A/B and tests: 1 = light blocks on `st`, 0 = beside)
     return v && *v ? (*v != '0' ? 1 : 0) : -1;
   }();
   const bool light_main = ovl && nr > 0 && light_env != 0;
@@ -1937,6 +1939,7 @@ struct CallGuard {
   explicit CallGuard(Context* c) : ctx(c), lock(c->mu), cs(scratch_of(c)), errs0(g_err_count) {
     hipSetDevice(c->device);
     cs->reset();
+    t_phase_on = !phase_events_off();
     (void)take_launch_error();  // (a previous call's, already reported or abandoned)
   }
   // a call that fails (interrupted, timed out, or any error after launches) drains both streams before
@@ -3761,21 +3764,20 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   // main stream decodes the key columns, builds the keys and sorts them (the general LZ4 decoder is
   // LDS / latency bound, the sort HBM bound, so the two overlap on the CUs).
   SideJoin side_join;
-  static const bool no_side = [] {  // DG_NO_SIDE=1: everything on the main stream (same-box A/B)
-    const char* v = getenv("DG_NO_SIDE");
-    return v && *v && *v != '0';
-  }();
+  const bool no_side = env_on("DG_NO_SIDE");  // everything on the main stream (same-box A/B and tests)
   const bool side = ctx->side && !db_side.jobs.empty() && !no_side;
   if (side) {
     if (!call_err(cs, st)) return set_error(DG_ERR_OOM, "error word");
     DG_FLUSH(cs, st);  // everything staged so far leaves on the main stream first
-    phase_event(ctx->side_ev[0], st);
+    // side_ev[0] (side waits for the flush and the zeroed error word) and side_ev[2] (the reduce waits
+    // for the payload) order the streams: recorded on every call, phase timing or not
+    DG_HIP(hipEventRecord(ctx->side_ev[0], st));
     DG_HIP(hipStreamWaitEvent(ctx->side, ctx->side_ev[0], 0));
     side_join.s = ctx->side;
     phase_event(ctx->side_ev[1], ctx->side);
     rc = run_decodes_only(cs, &db_side, ctx->side, nullptr);
     if (rc) return rc;
-    phase_event(ctx->side_ev[2], ctx->side);
+    DG_HIP(hipEventRecord(ctx->side_ev[2], ctx->side));
   } else {
     db.jobs.insert(db.jobs.end(), db_side.jobs.begin(), db_side.jobs.end());
     db.bytes += db_side.bytes;
@@ -3945,7 +3947,7 @@ int dg_result_fetch_groups(dg_result* r, int64_t start, int64_t count, int64_t* 
     }
     return d;
   };
-  static const bool zc_off = [] {
+  const bool zc_off = [] {  // (same-box A/B and tests)
     const char* v = getenv("DG_FETCH_ZC");
     return v && *v == '0';
   }();

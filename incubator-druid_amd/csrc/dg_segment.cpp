@@ -593,6 +593,15 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
         }
       });
     for (auto& x : th) x.join();
+    // a literal-only block is read in place (no decoder, so no device check of its decoded length):
+    // its literals must cover its rows (packed vbits columns are checked by parse_numeric)
+    for (int32_t b = 0; !col->lit_off.empty() && !col->vbits && b < blocks.n; ++b) {
+      if (col->lit_off[b] < 0) continue;
+      const int64_t rows = std::min<int64_t>(col->size_per, (int64_t)col->total - (int64_t)b * col->size_per);
+      if (rows > 0 && (int64_t)col->dec_len[b] < rows * col->width)
+        return set_error(DG_ERR_FORMAT, "literal-only block %d holds %d of %lld bytes", b, col->dec_len[b],
+                         (long long)(rows * col->width));
+    }
     for (int32_t b = 0; minmax && b < blocks.n; ++b)
       if (!has_mm[b]) {  // (then no block's time range is known: every block is decoded)
         col->min8.clear();

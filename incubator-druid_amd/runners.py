@@ -667,8 +667,22 @@ class PinnedPool:
         self.ptr = ctypes.c_void_p()
         N.check(N.lib().dg_host_alloc(int(nbytes), ctypes.byref(self.ptr)))
         self.nbytes, self.off = int(nbytes), 0
+        self._holder = None  # weak reference to the partial whose arrays are views of this memory
+
+    def _check_free(self, what: str):
+        if self._holder is not None and self._holder() is not None:
+            raise RuntimeError(f"PinnedPool.{what}: the memory is still in use by a fetched partial (drop it first)")
+        self._holder = None
+
+    def hold(self, partial) -> None:
+        """Mark the pool as backing `partial` (one fetch at a time): reset() and close() refuse while it
+        lives, and the partial keeps the pool alive."""
+        import weakref
+        self._holder = weakref.ref(partial)
+        partial._pool = self
 
     def reset(self):
+        self._check_free("reset")
         self.off = 0
 
     def take(self, dtype, n: int) -> np.ndarray:
@@ -683,6 +697,7 @@ class PinnedPool:
 
     def close(self):
         if self.ptr:
+            self._check_free("close")
             N.lib().dg_host_free(self.ptr)
             self.ptr = ctypes.c_void_p()
 
@@ -746,7 +761,10 @@ class GroupByResult:
         ids = ids[:count * nd].reshape(count, nd) if nd else np.zeros((count, 0), np.int32)
         codes = [ids[:, d] for d in range(nd)]  # strided views of the [count][ndims] id rows
         aggs = _decode_slots(q.aggregations, vals[:count * na].reshape(count, na)) if na else []
-        return GroupByPartial(t[:count], None, aggs, codes, [self.dictionary(d) for d in range(nd)], merged=True)
+        part = GroupByPartial(t[:count], None, aggs, codes, [self.dictionary(d) for d in range(nd)], merged=True)
+        if pool is not None:
+            pool.hold(part)
+        return part
 
     def apply_limit_push_down(self) -> bool:
         """LimitedBufferHashGrouper's outcome on the device (dg_result_limit): when the query pushes

@@ -70,6 +70,37 @@ def test_corrupt_segments_rejected(tmp_path, DG):
     N.lib().dg_segment_release(h)
 
 
+def test_short_literal_only_block_rejected(tmp_path, W):
+    """A literal-only LZ4 block is read in place (no decoder runs, so nothing checks its decoded length
+    on the device): when its literals do not cover its rows the attach fails with DG_ERR_FORMAT instead
+    of letting the views read past the block. Random longs compress to literal-only blocks; the
+    column's row total is raised by 100 so its last block (1,808 rows written) claims 1,908."""
+    N = importlib.import_module("incubator-druid_amd._native")
+    S = importlib.import_module("incubator-druid_amd.segment")
+    n = 10_000
+    rng = np.random.default_rng(5)
+    spec = W.SegmentSpec(timestamps=np.arange(n, dtype=np.int64), interval=(0, n),
+                         dims={"d": W.encode_int_strings(np.arange(n) % 7)},
+                         metrics={"noise": ("long", rng.integers(-(1 << 62), 1 << 62, n))})
+    good = W.write_segment(str(tmp_path / "good"), spec)
+    ctx = S.GpuContext.get(0)
+    h = ctypes.c_void_p()
+    assert N.lib().dg_segment_attach(ctx.handle, good.encode(), ctypes.byref(h)) == 0
+    N.lib().dg_segment_release(h)
+
+    def longer_total(data, cols):
+        start, _ = cols["noise"]
+        jl = struct.unpack(">i", bytes(data[start:start + 4]))[0]
+        p = start + 4 + jl  # [u8 version 2][i32 total][i32 sizePer][u8 codec]...
+        assert struct.unpack(">i", bytes(data[p + 1:p + 5]))[0] == n
+        data[p + 1:p + 5] = struct.pack(">i", n + 100)
+
+    bad = _patch(good, str(tmp_path / "short"), longer_total)
+    h = ctypes.c_void_p()
+    rc = N.lib().dg_segment_attach(ctx.handle, bad.encode(), ctypes.byref(h))
+    assert rc == 1 and "literal-only block" in N.lib().dg_last_error().decode(), (rc, N.lib().dg_last_error())
+
+
 def test_corrupt_multi_value_row_lists(tmp_path, Q, W):
     """Multi-value row lists are validated on the device once decoded (offsets start at 0, never
     decrease and stay within the values; every value id is below the dictionary size) before any

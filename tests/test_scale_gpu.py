@@ -172,13 +172,22 @@ def test_cfg4_compound_filters_on_large_segments(R, Q, O, S, DG, tmp_path_factor
         assert_results(q, R.run_query(q, g), O.run(q, o))
 
 
-@pytest.mark.parametrize("mode", ["inplace", "agg_filter", "interval"])
-def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode):
+@pytest.mark.parametrize("mode", ["inplace", "agg_filter", "interval", "phase_off", "no_side", "fetch_pinned",
+                                  "fetch_staged"])
+def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
     """The headline's shape through the keygen paths: longSum / doubleSum of plain LZ4 columns decoded
     straight into the payload records (row-ref mode) next to a floatSum the keygen writes; a
     FilteredAggregator (its column goes through the keygen, the other in place) with a row filter
     (sparse rows: references stay row indices); and an interval cutting the segments (the per-row
-    time check path)."""
+    time check path). Then the engine's run-time switches on the in-place path: phase timing off (the
+    bench's timed steps: the side-stream payload decode must still be joined before the reduce), the
+    payload decoded on the main stream (DG_NO_SIDE=1), and the groups fetched into pinned host memory
+    by the pack kernel (zero-copy) or through the staged DMA copy (DG_FETCH_ZC=0)."""
+    N = importlib.import_module("incubator-druid_amd._native")
+    if mode == "no_side":
+        monkeypatch.setenv("DG_NO_SIDE", "1")
+    if mode == "fetch_staged":
+        monkeypatch.setenv("DG_FETCH_ZC", "0")
     g, o = cfg3
     aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal"),
             Q.float_sum("fsum", "sumFloatNormal")]
@@ -191,7 +200,21 @@ def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode):
         lo, hi = int(np.quantile(ts, 0.2)), int(np.quantile(ts, 0.7))
         iv = [(lo, hi)]
     q = Q.GroupByQuery(intervals=iv, dimensions=["dimUniform", "dimHyperUnique"], aggregations=aggs, filter=flt)
-    part = R.groupby_per_device(g, q)[0]
+    pool = None
+    if mode == "phase_off":
+        N.lib().dg_set_phase_timing(0)
+        try:
+            for _ in range(2):  # (a second call: the first call's events are stale, not unrecorded)
+                part = R.groupby_per_device(g, q)[0]
+        finally:
+            N.lib().dg_set_phase_timing(1)
+    elif mode.startswith("fetch_"):
+        pool = R.PinnedPool(len(o[0].time()) * 2 * (4 * 2 + 8 * len(aggs)) + (1 << 20))
+        res = R.groupby_run(g, q)
+        part = res.fetch(pool=pool)
+        res.release()
+    else:
+        part = R.groupby_per_device(g, q)[0]
     exp = O.run(q, o)
     assert len(part) == len(exp) > 200_000
     t, keys, vals = _columns(exp, q.dimensions, aggs)
@@ -205,6 +228,26 @@ def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode):
             assert np.array_equal(col.astype(np.float32), e.astype(np.float32))
         else:
             assert np.array_equal(col, e.astype(col.dtype)), a.name
+    if pool is not None:
+        with pytest.raises(RuntimeError, match="still in use"):
+            pool.close()  # the partial's arrays are views of the pool
+        del part, col
+        pool.close()
+
+
+@pytest.mark.parametrize("switch", [("DG_NO_OVERLAP", "1"), ("DG_LIGHT_MAIN", "0"), ("DG_LIGHT_MAIN", "1")])
+def test_cfg2_decoder_stream_switches(R, Q, O, cfg2, switch, monkeypatch):
+    """The decoder stream placements of a timeseries / topN call: every decoder on the call's stream
+    (DG_NO_OVERLAP=1), and the light blocks beside the run decoder on the side stream (DG_LIGHT_MAIN=0)
+    or after the general decoder on the call's stream (=1, the default), against the oracle."""
+    monkeypatch.setenv(*switch)
+    g, o = cfg2
+    aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal")]
+    for q in (Q.TopNQuery(intervals=IV, dimension="dimUniform", metric="sumFloatNormal", threshold=10,
+                          aggregations=aggs[1:]),
+              Q.TimeseriesQuery(intervals=IV, filter=Q.SelectorDimFilter("dimSequential", "399"), aggregations=aggs),
+              Q.TimeseriesQuery(intervals=IV, granularity="minute", aggregations=aggs)):
+        assert_results(q, R.run_query(q, g), O.run(q, o))
 
 
 def test_cfg1_selector_timeseries_on_lz4_hc_segments(R, Q, O, cfg2):
