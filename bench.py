@@ -523,6 +523,117 @@ def cpu_baseline_oracle(query, path, rows, seconds, selected_fraction):
                       f"{selected_fraction:.4g}", "cpu_model": _cpu_model()}
 
 
+# ------------------------------------------------------------------------------------------------
+# N-rank result checks (world > 1): order-independent properties of the final, exchanged result against
+# every rank's local CPU-engine result (GroupByMergingQueryRunnerV2.java:170-290, TimeseriesBinaryFn.java:
+# 67-70, TopNBinaryFn.java:75-135), so the first multi-GPU run checks its own answer.
+# ------------------------------------------------------------------------------------------------
+SAMPLE_BITS = 10  # groups whose key hashes to 0 mod 2^SAMPLE_BITS are compared one by one
+
+
+def sample_mask(t, c1, c2):
+    """Deterministic 1-in-1024 sample of groupBy keys (bucket time, cluster id 1, cluster id 2)."""
+    m = np.uint64
+    h = (np.asarray(t).astype(np.int64).view(np.uint64) * m(0x9E3779B97F4A7C15)) ^ \
+        (np.asarray(c1).astype(m) * m(0xC2B2AE3D27D4EB4F)) ^ (np.asarray(c2).astype(m) * m(0x165667B19E3779F9))
+    h ^= h >> m(29)
+    return (h & m((1 << SAMPLE_BITS) - 1)) == 0
+
+
+def _lex_lt(a, b):
+    return tuple(a) < tuple(b)
+
+
+def rank_groupby_summary(final, cpu_groups, cpu_dicts, cpu_buckets, maps, local_dicts, universal, gpu_local_groups):
+    """One rank's facts for evaluate_dist_groupby: `final` = this rank's key range of the exchanged result
+    (times, cluster ids, [long sums, double sums]); cpu_groups = the CPU engine's groups over this rank's
+    segments (key = (bucket * card1 + merged id 1) << 32 | merged id 2, lsum, dsum), re-keyed to cluster
+    ids with the exchange's maps."""
+    t, c1, c2 = (np.asarray(final["times"], np.int64), np.asarray(final["c1"], np.int64),
+                 np.asarray(final["c2"], np.int64))
+    ls, ds = np.asarray(final["lsum"], np.int64), np.asarray(final["dsum"], np.float64)
+    n = len(t)
+    srt = True
+    if n > 1:  # strictly increasing (time, id1, id2)
+        gt = np.zeros(n - 1, bool)
+        eq = np.ones(n - 1, bool)
+        for c in (t, c1, c2):
+            gt |= eq & (c[1:] > c[:-1])
+            eq &= c[1:] == c[:-1]
+        srt = bool(gt.all())
+    org, per, b0, card1 = cpu_buckets
+    key = np.asarray(cpu_groups["key"], np.uint64)
+    m2 = (key & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    hi = (key >> np.uint64(32)).astype(np.int64)
+    m1, b = hi % card1, hi // card1
+    ct = (org + (b0 + b) * per) if per else np.full(len(key), universal, np.int64)
+    k1, k2 = maps[0][m1].astype(np.int64), maps[1][m2].astype(np.int64)
+    gs, cs_ = sample_mask(t, c1, c2), sample_mask(ct, k1, k2)
+    return {
+        "n_final": n, "lsum_final": int(ls.sum()), "dsum_final": float(ds.sum()), "sorted_final": srt,
+        "first": [int(t[0]), int(c1[0]), int(c2[0])] if n else None,
+        "last": [int(t[-1]), int(c1[-1]), int(c2[-1])] if n else None,
+        "gpu_local_groups": int(gpu_local_groups), "cpu_local_groups": int(len(key)),
+        "cpu_lsum": int(np.asarray(cpu_groups["lsum"], np.int64).sum()),
+        "cpu_dsum": float(np.asarray(cpu_groups["dsum"], np.float64).sum()),
+        "dicts_equal": [list(d) for d in cpu_dicts] == [list(d) for d in local_dicts],
+        "gpu_sample": [a[gs] for a in (t, c1, c2, ls, ds)],
+        "cpu_sample": [ct[cs_], k1[cs_], k2[cs_], np.asarray(cpu_groups["lsum"], np.int64)[cs_],
+                       np.asarray(cpu_groups["dsum"], np.float64)[cs_]],
+    }
+
+
+def evaluate_dist_groupby(summaries):
+    """rank 0: the exchanged result against the ranks' CPU results. Exact: the long-sum total, each
+    rank's pre-exchange group count, the ranges (each strictly increasing, rank r's last key below rank
+    r + 1's first), the sampled groups one by one (keys, long sums); the total group count lies between
+    the largest rank's and the sum of the ranks' counts; double sums within 1e-9 relative."""
+    S = summaries
+    groups = sum(x["n_final"] for x in S)
+    cpu_counts = [x["cpu_local_groups"] for x in S]
+    out = {"groups": groups, "ranks": len(S)}
+    out["local_counts_equal"] = all(x["gpu_local_groups"] == x["cpu_local_groups"] for x in S)
+    out["dicts_equal"] = all(x["dicts_equal"] for x in S)
+    out["group_count_in_bounds"] = max(cpu_counts) <= groups <= sum(cpu_counts)
+    wrap = lambda v: int(np.array([v % (1 << 64)], np.uint64).view(np.int64)[0])  # noqa: E731 (int64 sums wrap)
+    out["long_sum"] = wrap(sum(x["lsum_final"] for x in S))
+    out["long_sum_equal"] = out["long_sum"] == wrap(sum(x["cpu_lsum"] for x in S))
+    dg, dc = sum(x["dsum_final"] for x in S), sum(x["cpu_dsum"] for x in S)
+    out["double_sum_rel_err"] = abs(dg - dc) / max(abs(dg), abs(dc), 1e-300)
+    out["double_sum_within_1e-9"] = out["double_sum_rel_err"] <= 1e-9
+    out["ranges_sorted"] = all(x["sorted_final"] for x in S)
+    ne = [x for x in S if x["n_final"]]
+    out["ranges_disjoint_ascending"] = all(_lex_lt(a["last"], b["first"]) for a, b in zip(ne, ne[1:]))
+    # sampled groups: CPU records of every rank combined by key (sources in rank order, as dg_merge)
+    cat = [np.concatenate([np.asarray(x["cpu_sample"][i]) for x in S]) for i in range(5)]
+    order = np.lexsort((cat[2], cat[1], cat[0]))
+    t, c1, c2, ls, ds = (a[order] for a in cat)
+    if len(t):
+        new = np.ones(len(t), bool)
+        new[1:] = (t[1:] != t[:-1]) | (c1[1:] != c1[:-1]) | (c2[1:] != c2[:-1])
+        starts = np.flatnonzero(new)
+        t, c1, c2 = t[starts], c1[starts], c2[starts]
+        ls = np.add.reduceat(ls, starts)
+        ds = np.add.reduceat(ds, starts)
+    g = [np.concatenate([np.asarray(x["gpu_sample"][i]) for x in S]) for i in range(5)]
+    out["sample_groups"] = int(len(g[0]))
+    same = len(g[0]) == len(t) and all(np.array_equal(a, b) for a, b in zip(g[:3], (t, c1, c2)))
+    out["sample_keys_equal"] = bool(same)
+    out["sample_long_sums_equal"] = bool(same and np.array_equal(g[3], ls))
+    rel = 0.0
+    if same and len(t):
+        a, b = g[4].astype(np.float64), ds
+        r = np.abs(a - b) / np.maximum(np.maximum(np.abs(a), np.abs(b)), 1e-300)
+        r[a == b] = 0.0
+        rel = float(r.max())
+    out["sample_double_max_rel_err"] = rel
+    out["sample_equal"] = bool(same and out["sample_long_sums_equal"] and rel <= 1e-9)
+    out["all_equal"] = all(out[k] for k in ("local_counts_equal", "dicts_equal", "group_count_in_bounds",
+                                             "long_sum_equal", "double_sum_within_1e-9", "ranges_sorted",
+                                             "ranges_disjoint_ascending", "sample_equal"))
+    return out
+
+
 def pmc_traffic(args, kname):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes of this same bench
     command (bench_pmc/pmc_<config>.json, written by tools/prof_summary.py from separate FETCH_SIZE and
@@ -613,6 +724,7 @@ def main():
     ap.add_argument("--data-dir", default=os.environ.get("DRUID_AMD_BENCH_DATA", "/tmp/druid_amd_bench"))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-result-checks", action="store_true", help="N ranks: skip the CPU-engine result checks")
     ap.add_argument("--write-workers", type=int, default=8, help="processes writing the synthetic segments")
     args = ap.parse_args()
     if args.gpus < 1:
@@ -715,7 +827,13 @@ def main():
                           else sum(c[k] for c in calls) / steps)
     selected_local = per_step("selected_rows")
     scanned_local = sum(s.num_rows for s in segs)
-    value = selected_local * world * steps / elapsed  # every rank holds the same shape of data (weak scaling)
+    selected_all, scanned_all = selected_local, scanned_local
+    if dist is not None:  # the rows every rank actually aggregated (not this rank's count x world)
+        t = torch.tensor([selected_local, float(scanned_local)], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t)
+        selected_all, scanned_all = float(t[0].item()), float(t[1].item())
+    value = selected_all * steps / elapsed
     phases = {"bitmap": per_step("bitmap_ms"), "decode": per_step("decode_ms"), "aggregate": per_step("aggregate_ms"),
               "query_wall": per_step("total_ms")}
     bytes_read = per_step("bytes_read")
@@ -800,11 +918,11 @@ def main():
         "phases_ms": phases,
         "phases_source": f"{psteps} untimed steps after the timed ones, with phase timestamps (dg_set_phase_timing); "
                          "the timed steps run without them",
-        "selected_rows_per_step": selected_local * world,
-        "scanned_rows_per_s": scanned_local * world * steps / elapsed,
+        "selected_rows_per_step": selected_all,
+        "scanned_rows_per_s": scanned_all * steps / elapsed,
         "stored_bytes_per_step": bytes_read,
         "lz4_blocks_per_step": lz4_blocks,
-        "rows_scanned_per_step": scanned_local * world,
+        "rows_scanned_per_step": scanned_all,
     }
     if isinstance(query, Q.GroupByQuery):
         line["groups_per_step"] = per_step("groups")
@@ -876,6 +994,47 @@ def main():
             same = [[r[query.dimension] for r in x.value] for x in gpu_res] == [[r[query.dimension] for r in x.value] for x in exp]
             line["result_checks"] = {"entries": sum(len(x.value) for x in gpu_res), "values_equal_oracle": same,
                                      "results_equal_oracle": same and [x.value for x in gpu_res] == [x.value for x in exp]}
+    if dist is not None and not args.no_result_checks:
+        # N ranks: the final result checked against every rank's CPU-engine result (after the timing; one
+        # process per GPU, so the host cores are split between the node's ranks)
+        threads = max(1, _cpu_threads() // int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+        t_chk = time.perf_counter()
+        if isinstance(query, Q.GroupByQuery) and len(query.dimensions) == 2 and len(query.aggregations) == 2:
+            res = R.groupby_run(segs, query)
+            gpu_local = res.groups
+            merged = gmerge.exchange(res)
+            res.release()
+            fp = merged.fetch()
+            merged.release()
+            final = {"times": np.broadcast_to(fp.times, (len(fp),)), "c1": fp.codes[0], "c2": fp.codes[1],
+                     "lsum": fp.aggs[0], "dsum": fp.aggs[1]}
+            cb = cpu_baseline_groupby(paths, query, threads, want_groups=True)
+            summ = rank_groupby_summary(final, cb["_groups"], cb["_dicts"], cb["_buckets"], gmerge.maps, gmerge.local,
+                                        query.interval[0], gpu_local)
+            del fp, final, cb
+            gathered = [None] * world
+            dist.all_gather_object(gathered, summ)
+            if rank == 0:
+                line["result_checks"] = evaluate_dist_groupby(gathered)
+            del gathered, summ
+        elif isinstance(query, Q.TimeseriesQuery):
+            gpu_res = step(R.RunStats())  # (all-reduced on every rank)
+            _, cres = cpu_baseline_timeseries(paths, query, threads)
+            local = [Q.Result(ts, {a.name: v for a, v in zip(query.aggregations, vals)}) for ts, (_, vals) in cres.items()]
+            red = D.allreduce_timeseries(dist, query, local, ts_buckets)
+            cdict = {r.timestamp: (0, [r.value[a.name] for a in query.aggregations]) for r in red}
+            line["result_checks"] = dict(check_timeseries(gpu_res, cdict, query),
+                                         against="every rank's CPU engine result, all-reduced")
+        elif isinstance(query, Q.TopNQuery) and query.metric.type == "numeric":
+            allp = [None] * world
+            dist.all_gather_object(allp, paths)
+            gpu_res = step(R.RunStats())  # (rank 0 holds the folded result)
+            if rank == 0:  # the CPU engine over every rank's segments (one node: their files are here)
+                _, cres = cpu_baseline_topn([p for g in allp for p in g], query, _cpu_threads())
+                line["result_checks"] = dict(check_topn(gpu_res, cres, query),
+                                             against="the CPU engine over every rank's segments, rank-major")
+        if rank == 0 and "result_checks" in line:
+            line["result_checks"]["check_s"] = time.perf_counter() - t_chk
     del part
     if isinstance(query, Q.GroupByQuery) and dist is None:
         pool.close()

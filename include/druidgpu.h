@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 15
+#define DG_ABI_VERSION 16
 
 /* status codes (the JNI shim maps them to the reference's exceptions) */
 #define DG_OK 0
@@ -231,6 +231,10 @@ typedef struct {
   /* the wall time the general decoder ran on either stream (the union of its main- and side-stream
      spans; lz4_general_ms is their sum) */
   double lz4_general_wall_ms;
+  /* since ABI 16: of the general decoder's blocks, those decoded by its flow kernel (k_lz4_decode_flow)
+     and their stored bytes; the rest went to k_lz4_decode */
+  int64_t lz4_flow_blocks;
+  int64_t lz4_flow_bytes;
 } dg_metrics;
 
 /* Aggregate values are returned in 8-byte slots: int64 for count/long*, double for double*,
@@ -531,6 +535,23 @@ int dg_debug_lz4_decode(dg_context* ctx, const uint8_t* const* blocks, const int
  * device work): *kind = -1 malformed (fails validation), 0 general (k_lz4_decode), 1 general with
  * wide checkpoints, 2 light (k_lz4_light). Since ABI 11. */
 int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind);
+
+/* Measurement probes (since ABI 16): what the device and its host link deliver to plain kernels and
+ * copies, timed with HIP events over `iters` repetitions after one warm-up; *ms = average per
+ * repetition. Buffers are allocated and freed inside the call.
+ *   DG_PROBE_COPY      n bytes read and n bytes written by a grid-stride 16-byte copy kernel (HBM)
+ *   DG_PROBE_D2H       n bytes device -> pinned host memory (hipMemcpyAsync, DMA)
+ *   DG_PROBE_H2D       n bytes pinned host memory -> device
+ *   DG_PROBE_GATHER    n elements: an 8-byte word read in order, a 16-byte record gathered at a pseudo-random
+ *                      row (a permutation), four 8-byte stores in order (the groupBy reduce's memory floor)
+ *   DG_PROBE_ZC_WRITE  n bytes written by a kernel straight into pinned host memory (zero-copy over the link,
+ *                      the dg_result_fetch_groups path) */
+#define DG_PROBE_COPY 0
+#define DG_PROBE_D2H 1
+#define DG_PROBE_H2D 2
+#define DG_PROBE_GATHER 3
+#define DG_PROBE_ZC_WRITE 4
+int dg_debug_probe(int32_t device, int32_t kind, int64_t n, int32_t iters, double* ms);
 
 #ifdef __cplusplus
 }

@@ -77,7 +77,8 @@ class dg_metrics(ctypes.Structure):
                 ("lz4_general_ms", ctypes.c_double), ("lz4_general_bytes", ctypes.c_int64),
                 ("lz4_general_blocks", ctypes.c_int32), ("lz4_general_launches", ctypes.c_int32),
                 ("bitmap_bytes", ctypes.c_int64), ("reduce_kernel_ms", ctypes.c_double),
-                ("lz4_fused_blocks", ctypes.c_int64), ("lz4_general_wall_ms", ctypes.c_double)]
+                ("lz4_fused_blocks", ctypes.c_int64), ("lz4_general_wall_ms", ctypes.c_double),
+                ("lz4_flow_blocks", ctypes.c_int64), ("lz4_flow_bytes", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -135,7 +136,7 @@ EXPORTS = [
     "dg_result_dim_dictionary", "dg_result_release", "dg_keyspace_bits", "dg_result_export", "dg_keys_partition",
     "dg_merge", "dg_records_pack", "dg_debug_lz4_decode", "dg_result_limit",
     "dg_segment_from_rows", "dg_context_set_limit", "dg_groupby_merge_devices", "dg_timeseries_merge",
-    "dg_debug_lz4_classify", "dg_host_alloc", "dg_host_free", "dg_set_phase_timing",
+    "dg_debug_lz4_classify", "dg_host_alloc", "dg_host_free", "dg_set_phase_timing", "dg_debug_probe",
 ]
 
 _lib = None
@@ -205,6 +206,8 @@ def lib():
         "dg_host_alloc": (ctypes.c_int, [i64, P(vp)]),
         "dg_host_free": (None, [vp]),
         "dg_set_phase_timing": (ctypes.c_int, [ctypes.c_int32]),
+        "dg_debug_probe": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                          P(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(l, name)

@@ -560,6 +560,7 @@ struct DecodeBatch {
   int64_t gen_bytes = 0;
   int32_t gen_blocks = 0;
   int32_t gen_launches = 0;
+  int64_t flow_blocks = 0, flow_bytes = 0;  // of the general blocks, those of k_lz4_decode_flow
   int64_t fused_blocks = 0;  // blocks whose decode was fused with their aggregator (fused_agg_view)
 };
 // device time of the general decoder's launches of a batch (0 if it launched none)
@@ -593,6 +594,8 @@ static void decode_metrics(const DecodeBatch& db, const DecodeBatch& side, dg_me
   m->lz4_general_blocks = db.gen_blocks + side.gen_blocks;
   m->lz4_general_launches = db.gen_launches + side.gen_launches;
   m->lz4_fused_blocks = db.fused_blocks + side.fused_blocks;
+  m->lz4_flow_blocks = db.flow_blocks + side.flow_blocks;
+  m->lz4_flow_bytes = db.flow_bytes + side.flow_bytes;
 }
 static int column_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st);
 static int multi_view(const Column* c, CallScratch* cs, DecodeBatch* db, ColView* vals, ColView* offs, hipStream_t st);
@@ -1470,7 +1473,13 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   if (!light_main) launch_lz4_light(d + nh, n - nh, d_err, ss, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
   if (ovl) hipEventRecord(ctx->ovl_ev[1], ss);
   const int ng = nh - nr;  // general-decoder blocks
-  for (int i = nr; i < nh; ++i) db->gen_bytes += J[i].src_len;
+  for (int i = nr; i < nh; ++i) {
+    db->gen_bytes += J[i].src_len;
+    if (J[i].wide & kLzFlow) {
+      db->flow_blocks++;
+      db->flow_bytes += J[i].src_len;
+    }
+  }
   db->gen_blocks += ng;
   for (int w = 0; w < 4; ++w) db->gen_launches += kb[w + 1] > kb[w];
   if (db->gen_a && ng) phase_event(db->gen_a, st);
@@ -1782,7 +1791,24 @@ int dg_context_create(int device, dg_context** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) hipEventCreate(&e);
-  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) ctx->side = nullptr;
+  // DG_SIDE_CUS=k (same-box A/B): the side stream restricted to k CUs spread evenly over the chip;
+  // DG_SPLIT_CUS=1 also keeps the main stream off them
+  const char* side_cus = getenv("DG_SIDE_CUS");
+  const int kcu = side_cus ? atoi(side_cus) : 0;
+  if (kcu > 0 && kcu < 256) {
+    uint32_t m[8] = {0}, comp[8] = {0};
+    for (int i = 0; i < 256; ++i) {
+      if ((i * kcu) % 256 < kcu) m[i / 32] |= 1u << (i % 32);
+      else comp[i / 32] |= 1u << (i % 32);
+    }
+    if (hipExtStreamCreateWithCUMask(&ctx->side, 8, m) != hipSuccess) ctx->side = nullptr;
+    if (env_on("DG_SPLIT_CUS")) {
+      hipStreamDestroy(ctx->stream);
+      DG_HIP(hipExtStreamCreateWithCUMask(&ctx->stream, 8, comp));
+    }
+  } else if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
+    ctx->side = nullptr;
+  }
   for (auto& e : ctx->side_ev) hipEventCreate(&e);
   for (auto& e : ctx->gen_ev) hipEventCreate(&e);
   for (auto& e : ctx->ovl_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -3612,6 +3638,7 @@ extern "C" {
 int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_groupby* gb, dg_result** out,
                    dg_metrics* metrics) {
   auto t0 = std::chrono::steady_clock::now();
+  HostTrace ht;
   Context* ctx;
   int rc = check_segments(segs, n, &ctx);
   if (rc) return rc;
@@ -3674,6 +3701,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   lay.bucket_bits = (q->period_ms && anyc) ? bits_for((gend - gb0) / q->period_ms) : 0;
   const int key_bits = shift + lay.bucket_bits;
   if (key_bits > 64) return set_error(DG_ERR_UNSUPPORTED, "groupBy key of %d bits", key_bits);
+  ht.mark("dicts");
   phase_event(ctx->ev[0], st);
   std::vector<GbJob> gj(n);
   std::vector<int64_t> rows(n, 0);
@@ -3759,6 +3787,7 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     }
     rows[i] = seg->nrows;
   }
+  ht.mark("views");
   DG_CHECK_INTERRUPT(intr);
   // The payload columns only meet the keys at the reduce: they decode on the side stream while the
   // main stream decodes the key columns, builds the keys and sorts them (the general LZ4 decoder is
@@ -3783,10 +3812,12 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     db.bytes += db_side.bytes;
     db_side.bytes = 0;
   }
+  ht.mark("side_launched");
   phase_event(ctx->ev[1], st);
   rc = run_decodes(cs, &db, st);
   if (rc) return rc;
   phase_event(ctx->ev[2], st);
+  ht.mark("main_decode_launched");
   DG_CHECK_INTERRUPT(intr);
   m.bytes_read = db.bytes + db_side.bytes;
   m.bytes_side = db_side.bytes;
@@ -3848,8 +3879,10 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   }
   phase_event(ctx->ev[4], st);
   DG_HIP(hipMemcpyAsync(h_n, sb.n, 8, hipMemcpyDeviceToHost, st));  // selected rows, groups
+  ht.mark("reduce_launched");
   rc = finish_call(cs, st);  // (polls the cancel flag / timeout while the device works)
   if (rc) return rc;
+  ht.mark("synced");
   const int64_t nsel = h_n[0], ng = h_n[1];
   res->ngroups = ng;
   // The result was laid out for the call's rows; when the groups are far fewer (filtered or few-group
@@ -4757,6 +4790,64 @@ int dg_timeseries_merge(const dg_scan* scan, int32_t n_lists, const int32_t* n, 
 extern "C" int dg_set_phase_timing(int32_t on) {
   g_phase_timing.store(on != 0, std::memory_order_relaxed);
   return DG_OK;
+}
+
+extern "C" int dg_debug_probe(int32_t device, int32_t kind, int64_t n, int32_t iters, double* ms) {
+  if (!ms || n <= 0 || iters <= 0 || kind < DG_PROBE_COPY || kind > DG_PROBE_ZC_WRITE)
+    return set_error(DG_ERR_ARG, "bad probe arguments");
+  DG_HIP(hipSetDevice(device));
+  hipStream_t st;
+  DG_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  void *a = nullptr, *b = nullptr, *h = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = DG_OK;
+  auto dev_alloc = [&](void** p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess; };
+  const bool gather = kind == DG_PROBE_GATHER;
+  if (gather && n >= (1ll << 32)) rc = set_error(DG_ERR_ARG, "probe: gather of %lld rows (32-bit rows)", (long long)n);
+  const size_t bytes = gather ? 0 : (size_t)((n + 15) & ~15ll);
+  bool ok = rc == DG_OK;
+  if (ok && gather) ok = dev_alloc(&a, (size_t)n * 8) && dev_alloc(&b, (size_t)n * 16) && dev_alloc(&h, (size_t)n * 32);
+  else if (ok && kind == DG_PROBE_COPY) ok = dev_alloc(&a, bytes) && dev_alloc(&b, bytes);
+  else if (ok) ok = dev_alloc(&a, bytes) && hipHostMalloc(&h, bytes, hipHostMallocDefault) == hipSuccess;
+  if (ok && kind == DG_PROBE_ZC_WRITE) ok = hipHostGetDevicePointer(&b, h, 0) == hipSuccess;
+  if (!ok && rc == DG_OK) rc = set_error(DG_ERR_OOM, "probe buffers of %lld", (long long)n);
+  if (rc == DG_OK) {
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    if (gather) launch_probe_fill(static_cast<uint64_t*>(a), b, n, st);
+    else if (kind != DG_PROBE_H2D) hipMemsetAsync(a, 1, bytes, st);
+    auto once = [&] {
+      switch (kind) {
+        case DG_PROBE_COPY: launch_probe_copy(a, b, (int64_t)bytes, st); break;
+        case DG_PROBE_D2H: hipMemcpyAsync(h, a, bytes, hipMemcpyDeviceToHost, st); break;
+        case DG_PROBE_H2D: hipMemcpyAsync(a, h, bytes, hipMemcpyHostToDevice, st); break;
+        case DG_PROBE_GATHER: launch_probe_gather(static_cast<const uint64_t*>(a), b, n, static_cast<uint64_t*>(h), st); break;
+        default: launch_probe_copy(a, b, (int64_t)bytes, st); break;  // (a -> pinned host memory, mapped)
+      }
+    };
+    once();  // warm-up
+    hipEventRecord(e0, st);
+    for (int i = 0; i < iters; ++i) once();
+    hipEventRecord(e1, st);
+    if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess) {
+      rc = set_error(DG_ERR_DEVICE, "probe failed");
+    } else {
+      float f = 0;
+      hipEventElapsedTime(&f, e0, e1);
+      *ms = (double)f / iters;
+    }
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  if (a) hipFree(a);
+  if (gather || kind == DG_PROBE_COPY) {
+    if (b) hipFree(b);
+    if (h && gather) hipFree(h);
+  } else if (h) {
+    hipHostFree(h);
+  }
+  hipStreamDestroy(st);
+  return rc;
 }
 
 extern "C" int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind) {

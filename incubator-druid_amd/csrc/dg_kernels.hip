@@ -1612,3 +1612,55 @@ void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStrea
 }
 
 }  // namespace dg
+
+// ------------------------------------------------------------------------------------------------
+// measurement probes (dg_debug_probe): what this box's HBM and host link deliver to plain kernels and
+// copies, for bench.py's roofline ("also report vs a measured device copy-bandwidth")
+// ------------------------------------------------------------------------------------------------
+namespace dg {
+
+// stream copy: every byte read once and written once, 16-byte accesses, grid-stride
+__global__ __launch_bounds__(256) void k_probe_copy(const uint4* __restrict__ in, uint4* __restrict__ out, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = in[i];
+}
+
+// the groupBy reduce's memory floor: per element one sequential 8-byte word (a sorted [key | row]
+// word), one 16-byte record gathered at its row, four sequential 8-byte stores (key + the three slots
+// of a group, slot-major) — k_gb_reduce's loads and stores without its segmented scan
+__global__ __launch_bounds__(256) void k_probe_gather(const uint64_t* __restrict__ words, const uint4* __restrict__ rec,
+                                                     int64_t n, uint64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t w = words[i];
+    const uint4 r = rec[w & ((1ull << 32) - 1)];
+    out[i] = w >> 32;
+    out[n + i] = 1;
+    out[2 * n + i] = ((uint64_t)r.y << 32) | r.x;
+    out[3 * n + i] = ((uint64_t)r.w << 32) | r.z;
+  }
+}
+
+// words[i] = (i << 32) | (i * m mod n): a permutation of the rows (m odd and prime to n), so the
+// gathers land on pseudo-random records like the reduce's sorted row references
+__global__ void k_probe_fill(uint64_t* __restrict__ words, uint4* __restrict__ rec, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = ((uint64_t)i * 2654435761ull) % (uint64_t)n;  // (i < 2^32: no overflow)
+    words[i] = ((uint64_t)i << 32) | r;
+    rec[i] = make_uint4((uint32_t)i, 1u, (uint32_t)(i * 3), 2u);
+  }
+}
+
+void launch_probe_copy(const void* in, void* out, int64_t bytes, hipStream_t s) {
+  const int64_t n16 = bytes / 16;
+  hipLaunchKernelGGL(k_probe_copy, dim3(256 * 16), dim3(256), 0, s, static_cast<const uint4*>(in), static_cast<uint4*>(out), n16);
+}
+
+void launch_probe_gather(const uint64_t* words, const void* rec, int64_t n, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_probe_gather, dim3(256 * 16), dim3(256), 0, s, words, static_cast<const uint4*>(rec), n, out);
+}
+
+void launch_probe_fill(uint64_t* words, void* rec, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_probe_fill, dim3(256 * 16), dim3(256), 0, s, words, static_cast<uint4*>(rec), n);
+}
+
+}  // namespace dg

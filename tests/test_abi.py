@@ -27,13 +27,13 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_structs():
     N = importlib.import_module("incubator-druid_amd._native")
-    assert N.lib().dg_abi_version() == 15
+    assert N.lib().dg_abi_version() == 16
     # struct layouts the header fixes (LP64)
     assert ctypes.sizeof(N.dg_filter) == 64
     assert ctypes.sizeof(N.dg_agg) == 32
     assert ctypes.sizeof(N.dg_scan) == 104
     assert N.dg_scan.timeout_ms.offset == 96
-    assert ctypes.sizeof(N.dg_metrics) == 176
+    assert ctypes.sizeof(N.dg_metrics) == 192
     assert ctypes.sizeof(N.dg_topn_lists) == 40
     assert ctypes.sizeof(N.dg_topn) == 56
     assert ctypes.sizeof(N.dg_order_column) == 16

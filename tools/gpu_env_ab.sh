@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 CONFIG=${CONFIG:-groupby}
 for round in 1 2; do
   for v in none ${VARIANTS:-}; do
-    e=""; [ "$v" = none ] || e="$v"
+    e=""; [ "$v" = none ] || e="${v//,/ }"
     env $e timeout -k 10 600 python -u bench.py --config $CONFIG --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline \
       > gpurun_out/envab_$round.json 2> gpurun_out/envab_$round.err || { tail -5 gpurun_out/envab_$round.err; exit 3; }
     python3 -c "
