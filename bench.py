@@ -202,7 +202,7 @@ def _cpu_lib():
                                    ctypes.POINTER(ctypes.c_double)]
     lib.cpu_topn.restype = ctypes.c_int
     lib.cpu_topn.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp, vp, ctypes.c_int,
-                             cp, vp, ctypes.c_int, vp, vp, ctypes.c_int, i32, i32, vp, vp,
+                             cp, vp, ctypes.c_int, vp, vp, ctypes.c_int, i32, i32, vp, i32, vp, vp,
                              ctypes.POINTER(ctypes.c_double)]
     return lib
 
@@ -374,9 +374,12 @@ def check_timeseries(gpu, cpu, query):
 
 
 def cpu_baseline_topn(paths, query, threads):
-    """oracle/cpu_engine.c cpu_topn (numeric metric): PooledTopNAlgorithm per segment on `threads`
-    cores (one segment per thread, as ChainedExecutionQueryRunner), top max(threshold, 1000) per segment,
-    TopNBinaryFn fold in segment order. Returns (baseline line, [(value, [agg values])])."""
+    """oracle/cpu_engine.c cpu_topn: PooledTopNAlgorithm per segment on `threads` cores (one segment per
+    thread, as ChainedExecutionQueryRunner), top max(threshold, 1000) per segment, TopNBinaryFn fold in
+    segment order. A numeric metric orders by the aggregator; a DimensionTopNMetricSpec by the value's
+    rank under its comparator (the merged dictionary ranked here, before the timing, by the oracle's
+    StringComparators restatement), with the LEXICOGRAPHIC optimizer's id cut when it applies (no
+    previousStop, no filter, segments inside the interval). Returns (baseline line, [(value, [aggs])])."""
     cs = _CpuSegments(paths)
     try:
         P, nprog, D, I, nleaf = cs.filter_program(query.filter)
@@ -385,12 +388,29 @@ def cpu_baseline_topn(paths, query, threads):
         aggs = query.aggregations
         kinds = (ctypes.c_int32 * len(aggs))(*[a.kind for a in aggs])
         cols = (ctypes.c_char_p * len(aggs))(*[(a.fieldName or "").encode() for a in aggs])
-        metric = [a.name for a in aggs].index(query.metric.metric)
+        min_t = int(query.context.get("minTopNThreshold", 1000))
+        rank, id_limit, metric = None, 0, 0
+        spec = query.metric
+        if spec.type == "dimension":
+            if spec.previous_stop is not None:
+                raise ValueError("cpu_topn: previousStop is not restated")
+            import functools
+            cmp = cs.O.topn_comparator(spec)  # (InvertedTopNMetricSpec's inverse included)
+            order = sorted(range(len(merged)),
+                           key=functools.cmp_to_key(lambda a, b: cmp(merged[a], merged[b]) or (a > b) - (a < b)))
+            rank = np.empty(len(merged), np.int32)
+            rank[np.asarray(order, dtype=np.int64)] = np.arange(len(merged), dtype=np.int32)
+            covered = all(query.interval[0] <= s.interval[0] and s.interval[1] <= query.interval[1] for s in cs.osegs)
+            if spec.ordering == "lexicographic" and not spec.inverted and query.filter is None and covered:
+                id_limit = max(query.threshold, min_t)
+        else:
+            metric = [a.name for a in aggs].index(spec.metric)
         ids = np.zeros(query.threshold, np.int32)
         vals = np.zeros(query.threshold * len(aggs), np.uint64)
         secs = ctypes.c_double()
         n = cs.lib.cpu_topn(cs.handles, len(paths), threads, P, nprog, D, I, nleaf, query.dimension.encode(), R, len(aggs),
-                            kinds, cols, metric, query.threshold, int(query.context.get("minTopNThreshold", 1000)),
+                            kinds, cols, metric, query.threshold, min_t,
+                            rank.ctypes.data if rank is not None else None, id_limit,
                             ids.ctypes.data, vals.ctypes.data, ctypes.byref(secs))
         if n < 0:
             raise RuntimeError("cpu_topn failed")
@@ -644,16 +664,74 @@ def pmc_traffic(args, kname):
     if not os.path.exists(f):
         return {}
     pm = json.load(open(f))
-    # kernel names as "a+b", each a prefix of the demangled name (after the namespace) or "prefix*"
-    names = [n.rstrip("*") for n in kname.split("+")]
-    ks = [k for k in pm["kernels"] if any(k.startswith(n) or f"::{n}" in k for n in names)]
+    ks = match_kernels(pm["kernels"], kname)
     if not ks:
         return {}
     calls = sum(pm["kernels"][k]["calls"] for k in ks)
     fetch = sum(pm["kernels"][k]["fetch_bytes"] for k in ks) / calls
     write = sum(pm["kernels"][k]["write_bytes"] for k in ks) / calls
+    tcalls = sum(pm["kernels"][k].get("trace_calls", pm["kernels"][k]["calls"]) for k in ks)
+    avg_ns = sum(pm["kernels"][k]["avg_ns"] * pm["kernels"][k].get("trace_calls", pm["kernels"][k]["calls"])
+                 for k in ks) / max(tcalls, 1)
     return {"traffic": 2 * fetch + write, "traffic_fetch_raw": fetch, "traffic_write": write,
+            "rocprof_avg_launch_ms": avg_ns / 1e6, "rocprof_kernels": sorted(k.split("(")[0] for k in ks),
             "traffic_source": os.path.join("bench_pmc", os.path.basename(f)) + f" ({pm.get('label', '')})"}
+
+
+def match_kernels(kernels, kname):
+    """Profiled kernel names (demangled, e.g. "void dg::k_lz4_decode_flow<false>(...)") of a roofline
+    kernel spec "a+b": each part is an exact kernel name (any template arguments), or a prefix when it
+    ends in "*"."""
+    out = []
+    for k in kernels:
+        base = k.split("(")[0].split("<")[0].split("::")[-1]
+        for n in kname.split("+"):
+            n = n.strip()
+            if (n.endswith("*") and base.startswith(n[:-1])) or base == n:
+                out.append(k)
+                break
+    return out
+
+
+def device_probes(NAT, device, line):
+    """What this GPU and its host link deliver to plain kernels and copies (dg_debug_probe, HIP events;
+    after the timed region): a 2 GiB read + 2 GiB write stream copy (the measured HBM ceiling, SURVEY
+    §8(d)), 1 GiB DMA copies each way and zero-copy kernel writes into pinned host memory (the groupBy
+    fetch path), and for a groupBy line the reduce's memory floor — one ordered 8-byte word, one 16-byte
+    record gathered at a pseudo-random row and four ordered 8-byte stores per element, for as many
+    elements as the step's selected rows. The roofline line gets its kernel's fraction of the measured
+    copy bandwidth next to the fraction of the 8 TB/s spec."""
+    L = NAT.lib()
+
+    def probe(kind, n, iters):
+        ms = ctypes.c_double()
+        NAT.check(L.dg_debug_probe(device, kind, int(n), iters, ctypes.byref(ms)))
+        return ms.value
+
+    out = {}
+    gib = 1 << 30
+    ms = probe(0, 2 * gib, 20)
+    out["copy_gb_s"] = 2 * 2 * gib / (ms / 1e3) / 1e9  # bytes read + written
+    for name, kind in (("d2h_gb_s", 1), ("h2d_gb_s", 2), ("zero_copy_write_gb_s", 4)):
+        out[name] = gib / (probe(kind, gib, 5) / 1e3) / 1e9
+    rf = line.get("roofline") or {}
+    if rf.get("achieved"):
+        rf["measured_copy_gb_s"] = out["copy_gb_s"]
+        rf["frac_of_measured_copy"] = rf["achieved"] / out["copy_gb_s"]
+    if line.get("groups_per_step"):
+        n = int(line["selected_rows_per_step"] / max(line["n_gpus"], 1))
+        if 0 < n < (1 << 32):
+            g = probe(3, n, 5)
+            red = line["phases_ms"].get("reduce_kernels")
+            out["reduce_floor"] = {"elements": n, "gather_floor_ms": g, "reduce_kernels_ms": red,
+                                   "reduce_over_floor": red / g if red else None,
+                                   "floor": "per element: 8 B ordered read, 16 B record gathered at a pseudo-random "
+                                            "row, 4 x 8 B ordered writes (k_gb_reduce's loads and stores alone)"}
+    if line.get("pcie_fetch"):
+        pf = line["pcie_fetch"]
+        pf["link_d2h_gb_s"] = out["d2h_gb_s"]
+        pf["link_zero_copy_write_gb_s"] = out["zero_copy_write_gb_s"]
+    return out
 
 
 def _free_port() -> int:
@@ -725,6 +803,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-result-checks", action="store_true", help="N ranks: skip the CPU-engine result checks")
+    ap.add_argument("--no-probes", action="store_true", help="skip the device copy / link / gather probes")
     ap.add_argument("--write-workers", type=int, default=8, help="processes writing the synthetic segments")
     args = ap.parse_args()
     if args.gpus < 1:
@@ -854,7 +933,9 @@ def main():
         # rocprofv3 counts
         # (the phase: the wall time it ran on either stream; the roofline below: per launch)
         phases["lz4_general"] = per_step("lz4_general_wall_ms")
-        kernels["lz4_general"] = ("k_lz4_decode", per_step("lz4_general_bytes"),
+        fb, gb = per_step("lz4_flow_blocks"), per_step("lz4_general_blocks")
+        gname = "k_lz4_decode_flow" if fb >= gb else "k_lz4_decode" if fb == 0 else "k_lz4_decode+k_lz4_decode_flow"
+        kernels["lz4_general"] = (gname, per_step("lz4_general_bytes"),
                                   max(per_step("lz4_general_launches"), 1.0), per_step("lz4_general_ms"))
     # LZ4 blocks per step by decoder (and those whose decode was fused with their aggregator)
     lz4_blocks = {"general": per_step("lz4_general_blocks"), "fused": per_step("lz4_fused_blocks")}
@@ -891,12 +972,23 @@ def main():
     if dom is not None:
         kname, kbytes, launches, kms = kernels[dom]
         per_launch_ms = kms / launches
-        achieved = (kbytes / launches) / (per_launch_ms / 1e3) / 1e9 if kbytes else None
-        roofline = {"bound": "hbm", "kernel": kname, "phase": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
-                    "bytes_per_launch": kbytes / launches if kbytes else None, "avg_launch_ms": per_launch_ms,
-                    "launches_per_step": launches}
+        bpl = kbytes / launches if kbytes else None
+        roofline = {"bound": "hbm", "kernel": kname, "phase": dom, "achieved": None, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": None, "traffic": None, "bytes_per_launch": bpl,
+                    "hip_event_avg_launch_ms": per_launch_ms, "launches_per_step": launches}
         roofline.update(pmc_traffic(args, kname))
+        # achieved = algorithmic bytes per launch / average launch time: the rocprofv3 average of the
+        # committed profile of this command when there is one (bench_pmc/, the figure a reader recomputes
+        # from profiles/), else this run's HIP-event span; both are reported
+        prof_ms = roofline.get("rocprof_avg_launch_ms")
+        avg_ms = prof_ms if prof_ms else per_launch_ms
+        roofline["avg_launch_ms"] = avg_ms
+        roofline["avg_launch_source"] = "rocprofv3 kernel trace (traffic_source)" if prof_ms else "HIP events, this run"
+        if bpl:
+            roofline["achieved"] = bpl / (avg_ms / 1e3) / 1e9
+            roofline["frac"] = roofline["achieved"] / HBM_PEAK_GBS
+            roofline["achieved_hip_events"] = bpl / (per_launch_ms / 1e3) / 1e9
+            roofline["frac_hip_events"] = roofline["achieved_hip_events"] / HBM_PEAK_GBS
     line = {
         "metric": "filtered rows aggregated/sec",
         "value": value,
@@ -936,16 +1028,22 @@ def main():
         t1 = time.perf_counter()
         res = R.groupby_run(segs, query)
         t2 = time.perf_counter()
-        part = res.fetch(pool=pool)
+        dicts = [res.dictionary(d) for d in range(len(query.dimensions))]  # (host: the values as Python strings)
+        res._dicts = dicts
+        t2b = time.perf_counter()
+        part = res.fetch(pool=pool)  # dg_result_fetch_groups: the pack kernel writes the pinned columns
         t3 = time.perf_counter()
         fetch_s = t3 - t1
-        dicts = [res.dictionary(d) for d in range(len(query.dimensions))]
         res.release()
-        line["pcie_fetch"] = {"groups": len(part), "query_plus_fetch_ms": fetch_s * 1e3, "fetch_ms": (t3 - t2) * 1e3,
+        line["pcie_fetch"] = {"groups": len(part), "query_plus_fetch_ms": fetch_s * 1e3, "fetch_ms": (t3 - t2b) * 1e3,
+                              "dictionary_ms": (t2b - t2) * 1e3,
                               "bytes_fetched": len(part) * per_group,
-                              "fetch_gb_s": len(part) * per_group / max(t3 - t2, 1e-9) / 1e9,
+                              "fetch_gb_s": len(part) * per_group / max(t3 - t2b, 1e-9) / 1e9,
                               "rows_per_s_incl_fetch": scanned_local / fetch_s,
-                              "destination": "pinned host memory (dg_host_alloc, allocated before the timing)"}
+                              "destination": "pinned host memory (dg_host_alloc, allocated before the timing), "
+                                             "written by the pack kernel over the link (zero-copy)",
+                              "split": "fetch_ms = dg_result_fetch_groups (+ numpy views); dictionary_ms = the "
+                                       "merged dictionaries' values materialised as host strings"}
         # result order: bucket time, then each dimension's merged id, strictly increasing
         gt = np.zeros(max(len(part) - 1, 0), dtype=bool)
         eq = np.ones(max(len(part) - 1, 0), dtype=bool)
@@ -976,24 +1074,11 @@ def main():
             cb, cres = cpu_baseline_timeseries(paths, query, threads)
             line["cpu_baseline"] = cb
             line["result_checks"] = check_timeseries(gpu_res, cres, query)
-        elif isinstance(query, Q.TopNQuery) and query.metric.type == "numeric":
+        elif isinstance(query, Q.TopNQuery):
             gpu_res = step(R.RunStats())
             cb, cres = cpu_baseline_topn(paths, query, threads)
             line["cpu_baseline"] = cb
             line["result_checks"] = check_topn(gpu_res, cres, query)
-        else:  # dimension-ordered topN: the oracle (one thread) is both the baseline and the check
-            gpu_res = step(R.RunStats())
-            line["cpu_baseline"] = cpu_baseline_oracle(query, paths[0], rows_per, args.cpu_seconds,
-                                                       selected_local / scanned_local if scanned_local else 1.0)
-            sys.path.insert(0, os.path.join(REPO, "oracle"))
-            import oracle as O
-            osegs = [O.OracleSegment(p) for p in paths]
-            exp = O.run(query, osegs)
-            for sg in osegs:
-                sg.close()
-            same = [[r[query.dimension] for r in x.value] for x in gpu_res] == [[r[query.dimension] for r in x.value] for x in exp]
-            line["result_checks"] = {"entries": sum(len(x.value) for x in gpu_res), "values_equal_oracle": same,
-                                     "results_equal_oracle": same and [x.value for x in gpu_res] == [x.value for x in exp]}
     if dist is not None and not args.no_result_checks:
         # N ranks: the final result checked against every rank's CPU-engine result (after the timing; one
         # process per GPU, so the host cores are split between the node's ranks)
@@ -1025,7 +1110,7 @@ def main():
             cdict = {r.timestamp: (0, [r.value[a.name] for a in query.aggregations]) for r in red}
             line["result_checks"] = dict(check_timeseries(gpu_res, cdict, query),
                                          against="every rank's CPU engine result, all-reduced")
-        elif isinstance(query, Q.TopNQuery) and query.metric.type == "numeric":
+        elif isinstance(query, Q.TopNQuery):
             allp = [None] * world
             dist.all_gather_object(allp, paths)
             gpu_res = step(R.RunStats())  # (rank 0 holds the folded result)
@@ -1038,6 +1123,8 @@ def main():
     del part
     if isinstance(query, Q.GroupByQuery) and dist is None:
         pool.close()
+    if rank == 0 and not args.no_probes:
+        line["device_probes"] = device_probes(NAT, device, line)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

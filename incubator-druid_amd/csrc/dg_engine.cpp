@@ -561,6 +561,9 @@ struct DecodeBatch {
   int32_t gen_blocks = 0;
   int32_t gen_launches = 0;
   int64_t flow_blocks = 0, flow_bytes = 0;  // of the general blocks, those of k_lz4_decode_flow
+  // blocks planned as tasks (add_tasks), per decoder kind, and their stored bytes
+  std::vector<Lz4Task> tasks[kKinds];
+  int64_t task_bytes[kKinds] = {0, 0, 0, 0, 0, 0};
   int64_t fused_blocks = 0;  // blocks whose decode was fused with their aggregator (fused_agg_view)
 };
 // device time of the general decoder's launches of a batch (0 if it launched none)
@@ -1216,31 +1219,45 @@ static const uint8_t* literal_block(const BlockColumn& b, int32_t k) {
   return (!b.lit_off.empty() && b.lit_off[k] >= 0) ? b.comp.as<uint8_t>() + b.lit_off[k] : nullptr;
 }
 
-// routes: decode_routes(), read once per column by the caller (run blocks to k_lz4_run, flow blocks to
-// k_lz4_decode_flow)
-static Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, int routes) {
-  Lz4Job j;
-  j.src = b.comp.as<uint8_t>() + b.comp_off[k];
-  j.dst = dst;
-  j.cp = b.cps.as<uint32_t>() + b.cp_off[k];
-  j.src_len = b.comp_len[k];
-  j.expect_len = expect;
-  j.ncp = b.cp_n[k];
-  j.dec_len = b.dec_len[k];
-  const bool flow = (routes & kRouteFlow) && !b.lvl_off.empty() && b.lvl_off[k] >= 0 && (b.cp_wide[k] & kLzFlow);
-  j.wide = (b.cp_wide[k] & 1) | (flow ? kLzFlow : 0);
-  j.lvl = flow ? b.lvls.as<uint8_t>() + b.lvl_off[k] : nullptr;
-  j.nlvl = flow ? b.lvl_n[k] : 0;
-  j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
-  j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
-  j.vstride = 0;
-  const bool run = (routes & kRouteRun) && !b.run_off.empty() && b.run_off[k] >= 0;
-  j.rx = run ? b.runx.as<uint8_t>() + b.run_off[k] : nullptr;
-  j.run_n = run ? b.run_n[k] : 0;
-  j.run_far = run ? b.run_far[k] : 0;
-  j.red_dst = nullptr;
-  j.red_op = j.red_kind = j.red_vkind = j.red_code = 0;
-  return j;
+// Whether a column's LZ4 blocks can be planned as tasks (its attach-time tables hold the default routes).
+static bool taskable(const BlockColumn& b, int routes) {
+  return b.codec == CODEC_LZ4 && routes == (kRouteRun | kRouteFlow) && b.job_desc.p && b.kind_dev.p;
+}
+
+// The column's LZ4 blocks k in [k0, k1) of every decoder kind (literal-only and empty blocks are in no
+// list) as one task per kind: block k decodes to dst_base + k * dst_step (vstride: into records), or
+// folds into *red (fused) when red is given. O(kinds * log blocks) host work.
+struct FoldSpec {
+  uint64_t* dst;
+  int32_t op, kind, vkind, code;
+};
+static void add_tasks(DecodeBatch* db, const BlockColumn& b, int32_t k0, int32_t k1, uint8_t* dst_base, int64_t dst_step,
+                      int32_t vstride, const FoldSpec* red, bool with_light = true) {
+  for (int kd = 0; kd < kKinds; ++kd) {
+    if (kd == kKindLight && !with_light) continue;
+    const auto& l = b.kind_list[kd];
+    const int32_t i0 = (int32_t)(std::lower_bound(l.begin(), l.end(), k0) - l.begin());
+    const int32_t i1 = (int32_t)(std::lower_bound(l.begin(), l.end(), k1) - l.begin());
+    if (i1 <= i0) continue;
+    Lz4Task t;
+    memset(&t, 0, sizeof t);
+    t.desc = b.job_desc.as<Lz4Job>();
+    t.list = b.kind_dev.as<int32_t>() + b.kind_at[kd];
+    t.i0 = i0;
+    t.n = i1 - i0;
+    t.dst_base = dst_base;
+    t.dst_step = dst_step;
+    t.vstride = vstride;
+    if (red) {
+      t.red_dst = red->dst;
+      t.red_op = red->op;
+      t.red_kind = red->kind;
+      t.red_vkind = red->vkind;
+      t.red_code = red->code;
+    }
+    db->tasks[kd].push_back(t);
+    db->task_bytes[kd] += b.kind_bytes[kd][i1] - b.kind_bytes[kd][i0];
+  }
 }
 
 static int block_view(const BlockColumn& b, int kind, const char* name, CallScratch* cs, DecodeBatch* db, ColView* v,
@@ -1299,6 +1316,8 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
   const uint8_t** d_ptrs;
   const uint8_t** h_ptrs = up_take<const uint8_t*>(cs, std::max(b.nblocks, 1), &d_ptrs, st);
   if (!h_ptrs || !d_ptrs) return set_error(DG_ERR_OOM, "decode scratch");
+  const bool tasks = taskable(b, routes);  // every LZ4 block decodes to its slot k: one task per kind
+  if (tasks) add_tasks(db, b, 0, b.nblocks, slots, kBlockBytes, 0, nullptr);
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     // the packed (or plain) bytes of block k: an LZ4 slot, an uncompressed slot or a NONE range
@@ -1310,7 +1329,7 @@ static int block_view(const BlockColumn& b, int kind, const char* name, CallScra
     else src = b.raw.as<uint8_t>() + (size_t)k * (size_t)b.size_per * b.vbits / 8;
     h_ptrs[k] = expanded ? reinterpret_cast<const uint8_t*>(expanded + (size_t)k * b.size_per) : src;
     if (rows <= 0) continue;
-    if (slots && !lit) {
+    if (slots && !lit && !tasks) {
       const int64_t expect = b.vbits ? (b.vbits * rows + 7) / 8 : rows * b.width;
       if (b.codec == CODEC_LZ4) {
         db->jobs.push_back(lz4_job(b, k, const_cast<uint8_t*>(src), (int32_t)expect, routes));
@@ -1355,6 +1374,11 @@ static bool payload_view(const Column* c, int agg_kind, uint64_t* payload, int p
   if (!b.lit_off.empty()) return false;  // (literal-only blocks are viewed in place: the keygen copies them)
   db->bytes += b.stored_bytes + b.index_bytes;
   const int routes = decode_routes();
+  if (taskable(b, routes)) {  // block k's values go to the records of rows row_base + k * size_per ..
+    add_tasks(db, b, 0, b.nblocks, reinterpret_cast<uint8_t*>(payload + (size_t)row_base * pw + a),
+              (int64_t)b.size_per * pw * 8, pw * 8, nullptr);
+    return true;
+  }
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (rows <= 0) continue;
@@ -1419,17 +1443,25 @@ static int run_decodes(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_
 static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, uint64_t* d_prof, bool overlap) {
   int rcl = run_lzf(cs, db, st);
   if (rcl) return rcl;
-  if (db->jobs.empty()) return run_expands(cs, db, st);
+  int tb[kKinds], nt = 0;  // task blocks per kind, tasks
+  int64_t ttb = 0;
+  for (int kd = 0; kd < kKinds; ++kd) {
+    tb[kd] = 0;
+    for (const Lz4Task& t : db->tasks[kd]) tb[kd] += t.n;
+    nt += (int)db->tasks[kd].size();
+    ttb += tb[kd];
+  }
+  if (db->jobs.empty() && !ttb) return run_expands(cs, db, st);
   const int n = (int)db->jobs.size();
-  // longest blocks first (token-dense blocks cost the most; workgroups dispatch in order, so this
-  // is greedy LPT scheduling of the blocks over the CUs and shortens the ragged last wave). Only for
-  // a few waves of blocks: with hundreds of waves the tail is noise and the host sort is not.
-  // wide blocks (more than 8192 sequences) go to their own launch of the decoder (twice the
-  // per-thread sequence registers)
-  // light blocks (literal-heavy, short chains) go last, to the light decoder (k_lz4_light, many
-  // blocks per CU)
-  // run blocks (value runs with a run index) first, to k_lz4_run
-  // flow blocks (k_lz4_decode_flow) after the other general blocks, each kind narrow then wide
+  // per-block jobs (the few blocks a call plans one by one: skipped / fused time buckets, other
+  // routes), partitioned by decoder the way the tasks are kinded:
+  // run blocks (value runs with a run index) first, to k_lz4_run;
+  // then the general blocks, each kind narrow then wide, flow blocks (k_lz4_decode_flow) after the
+  // others; wide blocks (more than 8192 sequences) go to their own launch (twice the per-thread
+  // sequence registers); longest first (token-dense blocks cost the most; workgroups dispatch in order,
+  // so this is greedy LPT scheduling of the blocks over the CUs and shortens the ragged last wave), for
+  // a few waves of blocks only: with hundreds of waves the tail is noise and the host sort is not;
+  // light blocks (literal-heavy, short chains) last, to the light decoder (many blocks per CU).
   auto& J = db->jobs;
   const int nr = (int)(std::stable_partition(J.begin(), J.end(), [](const Lz4Job& j) { return j.rx != nullptr; }) - J.begin());
   const int nh = (int)(std::stable_partition(J.begin() + nr, J.end(), [](const Lz4Job& j) { return !j.light; }) - J.begin());
@@ -1442,15 +1474,57 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   auto by_ncp = [](const Lz4Job& a, const Lz4Job& b) { return a.ncp > b.ncp; };
   for (int w = 0; w < 4; ++w)
     if (kb[w + 1] - kb[w] <= 16 * 256) std::stable_sort(J.begin() + kb[w], J.begin() + kb[w + 1], by_ncp);
+  int jb[kKinds], jn[kKinds];  // per kind: its per-block jobs J[jb .. jb + jn)
+  jb[kKindRun] = 0;
+  jn[kKindRun] = nr;
+  for (int w = 0; w < 4; ++w) {
+    jb[kKindGen0 + w] = kb[w];
+    jn[kKindGen0 + w] = kb[w + 1] - kb[w];
+  }
+  jb[kKindLight] = nh;
+  jn[kKindLight] = n - nh;
+  // one staged upload: the jobs, the tasks, and per kind the launch blocks' task map + each task's
+  // first launch block
   Lz4Job* d;
   Lz4Job* h = up_take<Lz4Job>(cs, n, &d, st);
+  Lz4Task* d_tasks = nullptr;
+  Lz4Task* h_tasks = nt ? up_take<Lz4Task>(cs, nt, &d_tasks, st) : nullptr;
+  int32_t* d_first = nullptr;
+  int32_t* h_first = nt ? up_take<int32_t>(cs, nt, &d_first, st) : nullptr;
+  int32_t* d_of = nullptr;
+  int32_t* h_of = ttb ? up_take<int32_t>(cs, (size_t)ttb, &d_of, st) : nullptr;
   int32_t* d_err = call_err(cs, st);
-  if (!h || !d_err) return set_error(DG_ERR_OOM, "lz4 jobs");
+  if (!h || !d_err || (nt && (!h_tasks || !h_first)) || (ttb && !h_of)) return set_error(DG_ERR_OOM, "lz4 jobs");
   memcpy(h, J.data(), sizeof(Lz4Job) * n);
+  Lz4Launch L[kKinds];
+  int t_at = 0;
+  int64_t of_at = 0;
+  for (int kd = 0; kd < kKinds; ++kd) {
+    L[kd].jobs = d + jb[kd];
+    L[kd].tasks = d_tasks;
+    L[kd].task_of = d_of ? d_of + of_at : nullptr;
+    L[kd].task_first = d_first;
+    L[kd].njobs = jn[kd];
+    L[kd].pad = 0;
+    int first = jn[kd];
+    for (const Lz4Task& t : db->tasks[kd]) {
+      h_tasks[t_at] = t;
+      h_first[t_at] = first;
+      std::fill(h_of + of_at, h_of + of_at + t.n, t_at);
+      of_at += t.n;
+      first += t.n;
+      t_at++;
+    }
+  }
   DG_FLUSH(cs, st);
+  int cnt[kKinds];  // launch blocks per kind
+  for (int kd = 0; kd < kKinds; ++kd) cnt[kd] = jn[kd] + tb[kd];
+  const int n_run = cnt[kKindRun], n_light = cnt[kKindLight];
+  int ng = 0;
+  for (int w = 0; w < 4; ++w) ng += cnt[kKindGen0 + w];
   Context* ctx = cs->ctx;
   const bool no_ovl = env_on("DG_NO_OVERLAP");  // (same-box A/B and tests: every decoder on the call's stream)
-  const bool ovl = overlap && !no_ovl && ctx && ctx->side && st == ctx->stream && nh > nr && (nr > 0 || n > nh) && !d_prof;
+  const bool ovl = overlap && !no_ovl && ctx && ctx->side && st == ctx->stream && ng > 0 && (n_run > 0 || n_light > 0) && !d_prof;
   hipStream_t ss = st;
   if (ovl) {
     hipEventRecord(ctx->ovl_ev[0], st);
@@ -1468,11 +1542,11 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
     const char* v = getenv("DG_LIGHT_MAIN");  // (same-box A/B and tests: 1 = light blocks on `st`, 0 = beside)
     return v && *v ? (*v != '0' ? 1 : 0) : -1;
   }();
-  const bool light_main = ovl && nr > 0 && light_env != 0;
-  launch_lz4_run(d, nr, stage, d_err, ss);
-  if (!light_main) launch_lz4_light(d + nh, n - nh, d_err, ss, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
+  const bool light_main = ovl && n_run > 0 && light_env != 0;
+  launch_lz4_run(L[kKindRun], n_run, stage, d_err, ss);
+  if (!light_main)
+    launch_lz4_light(L[kKindLight], n_light, d_err, ss, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
   if (ovl) hipEventRecord(ctx->ovl_ev[1], ss);
-  const int ng = nh - nr;  // general-decoder blocks
   for (int i = nr; i < nh; ++i) {
     db->gen_bytes += J[i].src_len;
     if (J[i].wide & kLzFlow) {
@@ -1480,13 +1554,21 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
       db->flow_bytes += J[i].src_len;
     }
   }
+  for (int w = 0; w < 4; ++w) {
+    db->gen_bytes += db->task_bytes[kKindGen0 + w];
+    if (w & kLzFlow) {
+      db->flow_blocks += tb[kKindGen0 + w];
+      db->flow_bytes += db->task_bytes[kKindGen0 + w];
+    }
+  }
   db->gen_blocks += ng;
-  for (int w = 0; w < 4; ++w) db->gen_launches += kb[w + 1] > kb[w];
+  for (int w = 0; w < 4; ++w) db->gen_launches += cnt[kKindGen0 + w] > 0;
   if (db->gen_a && ng) phase_event(db->gen_a, st);
   for (int w = 0; w < 4; ++w)
-    launch_lz4_decode(d + kb[w], kb[w + 1] - kb[w], w, d_err, st, d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
+    launch_lz4_decode(L[kKindGen0 + w], cnt[kKindGen0 + w], w, d_err, st,
+                      d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
   if (db->gen_a && ng) phase_event(db->gen_b, st);
-  if (light_main) launch_lz4_light(d + nh, n - nh, d_err, st, nullptr);
+  if (light_main) launch_lz4_light(L[kKindLight], n_light, d_err, st, nullptr);
   if (ovl) DG_HIP(hipStreamWaitEvent(st, ctx->ovl_ev[1], 0));
   return run_expands(cs, db, st);  // errors surface at finish_call
 }
@@ -2095,18 +2177,33 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
   if ((ndec && !slots) || !h_ptrs) return set_error(DG_ERR_OOM, "fused view");
   if (ndec) db->last_slots = slots;
   int32_t at = 0;
+  FoldSpec fold;
+  fold.op = slot_op(a.kind);
+  fold.kind = a.kind;
+  fold.vkind = v->kind;
+  fold.code = v->kind == VIEW_LONG ? (a.kind == DG_AGG_LONG_SUM ? kRedLongSum : a.kind == DG_AGG_LONG_MAX ? kRedLongMax
+                                      : a.kind == DG_AGG_LONG_MIN ? kRedLongMin : kRedGeneric)
+                                   : (a.kind == DG_AGG_DOUBLE_SUM ? kRedDoubleSum : kRedGeneric);
+  const bool tasks = taskable(b, routes);
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
     if (bk[k] >= 0) {
       h_ptrs[k] = reinterpret_cast<const uint8_t*>((uintptr_t)1);  // tagged: never dereferenced
+      fold.dst = out + (size_t)bk[k] * rec + 1 + slot;
+      if (tasks) {  // the run of blocks folding into this bucket: one task per kind (light blocks never fold)
+        int32_t k1 = k + 1;
+        while (k1 < b.nblocks && bk[k1] == bk[k]) h_ptrs[k1++] = reinterpret_cast<const uint8_t*>((uintptr_t)1);
+        add_tasks(db, b, k, k1, nullptr, 0, 0, &fold, false);
+        db->fused_blocks += k1 - k;
+        k = k1 - 1;
+        continue;
+      }
       Lz4Job j = lz4_job(b, k, nullptr, (int32_t)(rows * 8), routes);
-      j.red_dst = out + (size_t)bk[k] * rec + 1 + slot;
-      j.red_op = slot_op(a.kind);
-      j.red_kind = a.kind;
-      j.red_vkind = v->kind;
-      j.red_code = v->kind == VIEW_LONG ? (a.kind == DG_AGG_LONG_SUM ? kRedLongSum : a.kind == DG_AGG_LONG_MAX ? kRedLongMax
-                                           : a.kind == DG_AGG_LONG_MIN ? kRedLongMin : kRedGeneric)
-                                        : (a.kind == DG_AGG_DOUBLE_SUM ? kRedDoubleSum : kRedGeneric);
+      j.red_dst = fold.dst;
+      j.red_op = fold.op;
+      j.red_kind = fold.kind;
+      j.red_vkind = fold.vkind;
+      j.red_code = fold.code;
       db->jobs.push_back(j);
       db->fused_blocks++;
       continue;
@@ -3809,6 +3906,10 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     DG_HIP(hipEventRecord(ctx->side_ev[2], ctx->side));
   } else {
     db.jobs.insert(db.jobs.end(), db_side.jobs.begin(), db_side.jobs.end());
+    for (int kd = 0; kd < kKinds; ++kd) {
+      db.tasks[kd].insert(db.tasks[kd].end(), db_side.tasks[kd].begin(), db_side.tasks[kd].end());
+      db.task_bytes[kd] += db_side.task_bytes[kd];
+    }
     db.bytes += db_side.bytes;
     db_side.bytes = 0;
   }

@@ -85,6 +85,33 @@ struct Lz4Job {
   int32_t red_vkind;
   int32_t red_code;  // kRed*: the fold in the value's own type (generic: agg_input_raw + combine_op)
 };
+// A run of one column's LZ4 blocks of one decoder kind, decoded in one launch. Built per call in O(1)
+// from the column's attach-time tables: block k = list[i] for i in [i0, i0 + n) (the column's blocks of
+// that kind, ascending), its job = desc[k] (every query-independent Lz4Job field, expect_len = the bytes
+// of its rows) with dst = dst_base + k * dst_step (null dst_base: a fused fold writes nothing), vstride
+// and the fused fold (red_*) from the task.
+struct Lz4Task {
+  const Lz4Job* desc;
+  const int32_t* list;
+  int32_t i0, n;
+  uint8_t* dst_base;
+  int64_t dst_step;
+  uint64_t* red_dst;
+  int32_t vstride, red_op, red_kind, red_vkind, red_code, pad;
+};
+// A decoder launch: blocks [0, njobs) are per-block jobs, the rest belong to tasks (task_of[b - njobs] =
+// the task of block b, task_first[t] = the launch block of task t's first block).
+struct Lz4Launch {
+  const Lz4Job* jobs;
+  const Lz4Task* tasks;
+  const int32_t* task_of;
+  const int32_t* task_first;
+  int32_t njobs;
+  int32_t pad;
+};
+// decoder kinds of a block under the default routes (the partition run_decodes_only launches by)
+enum : int32_t { kKindRun = 0, kKindGen0 = 1, kKindLight = 5, kKinds = 6 };  // kKindGen0 + wide: general
+
 // folds of a fused decode (Lz4Job.red_code): int64 sum / max / min of a long column, double sum of a
 // double column in their native types (converted to the slot encoding once per block); others generic
 enum : int32_t { kRedGeneric = 0, kRedLongSum = 1, kRedDoubleSum = 2, kRedLongMax = 3, kRedLongMin = 4 };
@@ -125,6 +152,9 @@ int lz4_decode_host(const uint8_t* in, int n, uint8_t* out);
 // DG_NO_FLOW_DECODE); same-box A/B and the tests of the other decoders turn them off
 constexpr int kRouteRun = 1, kRouteFlow = 2;
 int decode_routes();
+struct BlockColumn;
+// the job of LZ4 block k of a column (dst, expect and the routes given; no fused fold)
+Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, int routes);
 
 // Flow blocks (Lz4Job.wide & kLzFlow, set at attach): general blocks of at most kLzMaxCps intervals
 // that are not distance-8 class chains (at most a quarter of their bytes copied from 8 back) and whose
@@ -319,6 +349,15 @@ struct BlockColumn {
   DevBuf cps;                          // LZ4: uint32 checkpoints of every block
   DevBuf raw;                          // UNCOMPRESSED: 64 KiB slot per block; NONE: flat values
   DevBuf block_ptrs;                   // const uint8_t*[nblocks]: raw slots (UNCOMPRESSED/NONE)
+  // LZ4 decode tables (attach time, default routes): every block's query-independent job (device,
+  // Lz4Job[nblocks]) and, per decoder kind, the blocks of that kind ascending (host + device, at
+  // kind_at[kind] in kind_dev) with the prefix sums of their stored bytes / run-index or checkpoint
+  // bytes. Literal-only and empty blocks are in no list.
+  DevBuf job_desc;
+  DevBuf kind_dev;
+  std::vector<int32_t> kind_list[kKinds];
+  std::vector<int64_t> kind_bytes[kKinds];  // [i] = stored bytes of list[0 .. i)
+  int64_t kind_at[kKinds] = {0, 0, 0, 0, 0, 0};
 };
 
 // A piece of a long serialized bitmap: Concise = a run of whole words starting at row `row0`;
@@ -453,12 +492,12 @@ hipError_t take_launch_error();
 // kernel launchers (dg_kernels.hip)
 constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (diagnostic builds of the call)
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
-void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+void launch_lz4_decode(const Lz4Launch& L, int nblocks, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+void launch_lz4_light(const Lz4Launch& L, int nblocks, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 // run blocks (rx set); stage: 0 = read the input from L1/L2 (64 KiB of LDS per block, two per CU: beside
 // another stream's LDS-heavy kernels), 1 = stage it in LDS when the launch is small (latency mode),
 // 2 = stage it (a launch that has the GPU to itself)
-void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int stage, int32_t* d_err, hipStream_t s);
+void launch_lz4_run(const Lz4Launch& L, int nblocks, int stage, int32_t* d_err, hipStream_t s);
 void launch_lzf_decode(const LzfJob* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 void launch_vsize_expand(const VsJob* d_jobs, int njobs, int32_t max_rows, int32_t* d_err, hipStream_t s);
 // one multi-value dimension's decoded row lists, validated before use (bit 2 of the error word)

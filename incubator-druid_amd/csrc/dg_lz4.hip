@@ -402,8 +402,25 @@ __device__ __forceinline__ void red_finish(const Lz4Job& job, uint64_t acc, uint
   }
 }
 
+// the job of launch block b: a per-block job, or its task's block with the task's destination and fold
+__device__ __forceinline__ Lz4Job fetch_job(const Lz4Launch& L, int b) {
+  if (b < L.njobs) return L.jobs[b];
+  const int t = L.task_of[b - L.njobs];
+  const Lz4Task& T = L.tasks[t];
+  const int k = T.list[T.i0 + (b - L.task_first[t])];
+  Lz4Job j = T.desc[k];
+  j.dst = T.dst_base ? T.dst_base + (int64_t)k * T.dst_step : nullptr;
+  j.vstride = T.vstride;
+  j.red_dst = T.red_dst;
+  j.red_op = T.red_op;
+  j.red_kind = T.red_kind;
+  j.red_vkind = T.red_vkind;
+  j.red_code = T.red_code;
+  return j;
+}
+
 template <bool PROF, int SEQ>
-__global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+__global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Launch L, int32_t* __restrict__ err,
                                                            uint64_t* __restrict__ prof) {
   __shared__ __attribute__((aligned(16))) uint16_t s_e[kEWords];  // 130 KiB: staged input, then E
   __shared__ uint32_t s_tsrc[kTailN];
@@ -414,7 +431,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode(const Lz4Job* __restr
   __shared__ int s_tmp[kLzWaves];
   __shared__ uint64_t s_red[kLzWaves];
 
-  const Lz4Job job = jobs[blockIdx.x];
+  const Lz4Job job = fetch_job(L, blockIdx.x);
   const int tid = threadIdx.x;
   const int n = job.src_len, ncp = job.ncp;
   if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.dec_len > kBlockBytes ||
@@ -1301,7 +1318,7 @@ __device__ __forceinline__ bool parse_tok8(const uint8_t* __restrict__ in, int n
 }
 
 template <bool PROF>
-__global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+__global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Launch L, int32_t* __restrict__ err,
                                                                 uint64_t* __restrict__ prof) {
   constexpr int SEQ = kLzSeqPerCp;
   __shared__ __attribute__((aligned(16))) uint32_t s_in32[kFlowInWords];    // staged input (after the pad)
@@ -1313,7 +1330,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Job* __
   __shared__ uint64_t s_red[kLzWaves];
   uint2* s_tab = reinterpret_cast<uint2*>(s_in32);  // the match table, after the literals
 
-  const Lz4Job job = jobs[blockIdx.x];
+  const Lz4Job job = fetch_job(L, blockIdx.x);
   const int tid = threadIdx.x;
   const int n = job.src_len, ncp = job.ncp;
   if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.dec_len > kBlockBytes ||
@@ -1540,13 +1557,13 @@ static_assert(kLtMaxCps <= kLtThreads, "one checkpoint interval per light-decode
 static_assert((kLtMaxSeq + 1 + 3 * kLtMaxSeq) * 4 + kLtMaxSeq * 2 <= kLtBufWords * 4, "table fits the input buffer");
 
 template <bool PROF>
-__global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err,
+__global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Launch L, int32_t* __restrict__ err,
                                                           uint64_t* __restrict__ prof) {
   __shared__ __attribute__((aligned(16))) uint32_t s_buf[kLtBufWords];
   __shared__ uint16_t s_lut[kLtLut];  // first sequence covering position 64 * i
   __shared__ int s_tmp[kLtThreads / 64];
   __shared__ int s_bad;
-  const Lz4Job job = jobs[blockIdx.x];
+  const Lz4Job job = fetch_job(L, blockIdx.x);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // the light checkpoints: one interval of g sequences per thread
   const int n = job.src_len, ncp = job.nfine, g = job.light;
@@ -1835,11 +1852,11 @@ __device__ __forceinline__ uint64_t l_rd8(const uint32_t* __restrict__ a, int p)
 // (a block's latency, not the launch's throughput, is the cost there); 104 KiB of LDS, one block per
 // CU. Otherwise the thread reads its ~128 contiguous input bytes from L1/L2 and two blocks share a CU.
 template <bool STAGE>
-__global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restrict__ jobs, int32_t* __restrict__ err) {
+__global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Launch L, int32_t* __restrict__ err) {
   __shared__ __attribute__((aligned(16))) uint64_t s_val[kRunVals];  // the block's decoded image
   __shared__ __attribute__((aligned(16))) uint32_t s_in[STAGE ? kRunLdsMax / 4 + 8 : 4];  // staged input, far table
   __shared__ uint64_t s_red[kRunThreads / 64];
-  const Lz4Job job = jobs[blockIdx.x];
+  const Lz4Job job = fetch_job(L, blockIdx.x);
   const int tid = threadIdx.x;
   const int n = job.src_len, ni = job.run_n, nfar = job.run_far;
   if (n <= 0 || ni <= 0 || ni > kRunThreads || nfar < 0 || nfar > kRunFarMax ||
@@ -1997,34 +2014,34 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Job* __restric
   }
 }
 
-void launch_lz4_run(const Lz4Job* d_jobs, int njobs, int stage_mode, int32_t* d_err, hipStream_t s) {
+void launch_lz4_run(const Lz4Launch& L, int njobs, int stage_mode, int32_t* d_err, hipStream_t s) {
   if (njobs <= 0) return;
   // DG_RUN_STAGE=0 / 1 forces the mode (tests run every run block through both)
   const char* force = getenv("DG_RUN_STAGE");
   const bool stage = force && *force ? *force != '0' : stage_mode == 2 || (stage_mode == 1 && njobs <= kRunStageBlocks);
-  if (stage) hipLaunchKernelGGL(k_lz4_run<true>, dim3(njobs), dim3(kRunThreads), 0, s, d_jobs, d_err);
-  else hipLaunchKernelGGL(k_lz4_run<false>, dim3(njobs), dim3(kRunThreads), 0, s, d_jobs, d_err);
+  if (stage) hipLaunchKernelGGL(k_lz4_run<true>, dim3(njobs), dim3(kRunThreads), 0, s, L, d_err);
+  else hipLaunchKernelGGL(k_lz4_run<false>, dim3(njobs), dim3(kRunThreads), 0, s, L, d_err);
 }
 
-void launch_lz4_light(const Lz4Job* d_jobs, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
+void launch_lz4_light(const Lz4Launch& L, int njobs, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
-  if (d_prof) hipLaunchKernelGGL(k_lz4_light<true>, dim3(njobs), dim3(kLtThreads), 0, s, d_jobs, d_err, d_prof);
-  else hipLaunchKernelGGL(k_lz4_light<false>, dim3(njobs), dim3(kLtThreads), 0, s, d_jobs, d_err, nullptr);
+  if (d_prof) hipLaunchKernelGGL(k_lz4_light<true>, dim3(njobs), dim3(kLtThreads), 0, s, L, d_err, d_prof);
+  else hipLaunchKernelGGL(k_lz4_light<false>, dim3(njobs), dim3(kLtThreads), 0, s, L, d_err, nullptr);
 }
 
-void launch_lz4_decode(const Lz4Job* d_jobs, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
+void launch_lz4_decode(const Lz4Launch& L, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
   if (wide & kLzFlow) {  // (flow blocks are never wide)
-    if (d_prof) hipLaunchKernelGGL(k_lz4_decode_flow<true>, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
-    else hipLaunchKernelGGL(k_lz4_decode_flow<false>, dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
+    if (d_prof) hipLaunchKernelGGL(k_lz4_decode_flow<true>, dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, d_prof);
+    else hipLaunchKernelGGL(k_lz4_decode_flow<false>, dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, nullptr);
     return;
   }
   if (wide) {
-    if (d_prof) hipLaunchKernelGGL((k_lz4_decode<true, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
-    else hipLaunchKernelGGL((k_lz4_decode<false, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
+    if (d_prof) hipLaunchKernelGGL((k_lz4_decode<true, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, d_prof);
+    else hipLaunchKernelGGL((k_lz4_decode<false, kLzMaxSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, nullptr);
   } else {
-    if (d_prof) hipLaunchKernelGGL((k_lz4_decode<true, kLzSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, d_prof);
-    else hipLaunchKernelGGL((k_lz4_decode<false, kLzSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, d_jobs, d_err, nullptr);
+    if (d_prof) hipLaunchKernelGGL((k_lz4_decode<true, kLzSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, d_prof);
+    else hipLaunchKernelGGL((k_lz4_decode<false, kLzSeqPerCp>), dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, nullptr);
   }
 }
 

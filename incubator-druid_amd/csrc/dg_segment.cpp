@@ -496,9 +496,68 @@ bool lz4_run_index(const uint8_t* in, int n, int dec_len, std::vector<uint8_t>* 
   return true;
 }
 
+// routes: decode_routes(), read once per column by the caller (run blocks to k_lz4_run, flow blocks to
+// k_lz4_decode_flow)
+Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, int routes) {
+  Lz4Job j;
+  j.src = b.comp.as<uint8_t>() + b.comp_off[k];
+  j.dst = dst;
+  j.cp = b.cps.as<uint32_t>() + b.cp_off[k];
+  j.src_len = b.comp_len[k];
+  j.expect_len = expect;
+  j.ncp = b.cp_n[k];
+  j.dec_len = b.dec_len[k];
+  const bool flow = (routes & kRouteFlow) && !b.lvl_off.empty() && b.lvl_off[k] >= 0 && (b.cp_wide[k] & kLzFlow);
+  j.wide = (b.cp_wide[k] & 1) | (flow ? kLzFlow : 0);
+  j.lvl = flow ? b.lvls.as<uint8_t>() + b.lvl_off[k] : nullptr;
+  j.nlvl = flow ? b.lvl_n[k] : 0;
+  j.light = b.cp_light.empty() ? 0 : b.cp_light[k];
+  j.nfine = b.cp_fine.empty() ? 0 : b.cp_fine[k];
+  j.vstride = 0;
+  const bool run = (routes & kRouteRun) && !b.run_off.empty() && b.run_off[k] >= 0;
+  j.rx = run ? b.runx.as<uint8_t>() + b.run_off[k] : nullptr;
+  j.run_n = run ? b.run_n[k] : 0;
+  j.run_far = run ? b.run_far[k] : 0;
+  j.red_dst = nullptr;
+  j.red_op = j.red_kind = j.red_vkind = j.red_code = 0;
+  return j;
+}
+
 namespace {
 static void index_bitmap_pieces(Column* c, const std::vector<uint8_t>& host);
 
+
+// The column's attach-time decode tables (BlockColumn.job_desc / kind_list): a query then plans its
+// LZ4 decodes as a few Lz4Tasks per column instead of one job per block.
+static int decode_tables(BlockColumn* col) {
+  const int32_t nb = col->nblocks;
+  std::vector<Lz4Job> desc((size_t)std::max(nb, 1));
+  memset(desc.data(), 0, desc.size() * sizeof(Lz4Job));
+  for (auto& l : col->kind_list) l.clear();
+  for (int32_t k = 0; k < nb; ++k) {
+    const int64_t rows = std::min<int64_t>(col->size_per, (int64_t)col->total - (int64_t)k * col->size_per);
+    const int64_t expect = col->vbits ? (col->vbits * rows + 7) / 8 : rows * col->width;
+    desc[k] = lz4_job(*col, k, nullptr, (int32_t)std::max<int64_t>(expect, 0), kRouteRun | kRouteFlow);
+    if (rows <= 0 || (!col->lit_off.empty() && col->lit_off[k] >= 0)) continue;
+    const Lz4Job& j = desc[k];
+    const int kind = j.rx ? kKindRun : j.light ? kKindLight : kKindGen0 + j.wide;
+    col->kind_list[kind].push_back(k);
+  }
+  std::vector<int32_t> all;
+  for (int kd = 0; kd < kKinds; ++kd) {
+    col->kind_at[kd] = (int64_t)all.size();
+    all.insert(all.end(), col->kind_list[kd].begin(), col->kind_list[kd].end());
+    auto& pb = col->kind_bytes[kd];
+    pb.assign(col->kind_list[kd].size() + 1, 0);
+    for (size_t i = 0; i < col->kind_list[kd].size(); ++i) pb[i + 1] = pb[i] + col->comp_len[col->kind_list[kd][i]];
+  }
+  if (all.empty()) all.push_back(0);
+  if (!col->job_desc.alloc(desc.size() * sizeof(Lz4Job)) || !col->kind_dev.alloc(all.size() * 4))
+    return set_error(DG_ERR_OOM, "hipMalloc lz4 decode tables");
+  DG_HIP(hipMemcpy(col->job_desc.p, desc.data(), desc.size() * sizeof(Lz4Job), hipMemcpyHostToDevice));
+  DG_HIP(hipMemcpy(col->kind_dev.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+  return DG_OK;
+}
 
 // Upload the blocks of a GenericIndexed of (compressed or raw) blocks.
 int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
@@ -640,7 +699,7 @@ int upload_blocks(Context* ctx, BlockColumn* col, const GI& blocks) {
       if (!col->runx.alloc(rall.size())) return set_error(DG_ERR_OOM, "hipMalloc lz4 run index");
       DG_HIP(hipMemcpy(col->runx.p, rall.data(), rall.size(), hipMemcpyHostToDevice));
     }
-    return DG_OK;
+    return col->codec == CODEC_LZ4 ? decode_tables(col) : DG_OK;
   }
   if (col->codec == CODEC_UNCOMPRESSED) {
     size_t bytes = (size_t)blocks.n * kBlockBytes;

@@ -37,7 +37,12 @@
  * cpu_topn — PooledTopNAlgorithm per segment (dense aggregation per dictionary id, top
  *   max(threshold, 1000) by the metric, TopNQueryQueryToolChest.java:553-561) and the TopNBinaryFn
  *   fold over the segments in order with the query's threshold (TopNBinaryFn.java:75-135), by merged
- *   (value-ordered) ids; the metric is a numeric aggregator (descending, ties by value).
+ *   (value-ordered) ids; the metric is a numeric aggregator (descending, ties by value), or with
+ *   `merged_rank` the dimension's own order (DimensionTopNMetricSpec, TopNLexicographicResultBuilder:
+ *   ascending rank of the value under the LEXICOGRAPHIC / ALPHANUMERIC / NUMERIC comparator, computed by
+ *   the caller; equal ranks by value order) and `id_limit` > 0 the LEXICOGRAPHIC optimizer's cut: only
+ *   local ids below it aggregate (BaseTopNAlgorithm.java:296-326 after
+ *   DimensionTopNMetricSpec.configureOptimizer, DimensionTopNMetricSpec.java:117-124).
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -617,6 +622,8 @@ typedef struct {
   const int32_t* kinds;
   const char* const* cols;
   int32_t seg_threshold;
+  const int32_t* merged_rank; /* dimension order: rank of every merged id (NULL: the numeric metric) */
+  int32_t id_limit;           /* > 0: local ids at or above it do not aggregate */
   tn_ent** lists;
   int32_t* nlist;
   int64_t next;
@@ -665,6 +672,7 @@ static void* tn_seg_worker(void* arg) {
     for (int64_t r = 0; r < n && !err; ++r) {
       if (bits && !((bits[r >> 6] >> (r & 63)) & 1)) continue;
       const int32_t g = ids[r];
+      if (c->id_limit > 0 && g >= c->id_limit) continue;
       touched[g] = 1;
       for (int a = 0; a < c->nagg; ++a) {
         uint64_t* sa = st + (size_t)a * card + g;
@@ -691,7 +699,7 @@ static void* tn_seg_worker(void* arg) {
       memset(&e, 0, sizeof e);
       e.id = c->remap[s][g];
       for (int a = 0; a < c->nagg; ++a) e.v[a] = st[(size_t)a * card + g];
-      e.metric = tn_metric(c->kinds[c->metric], e.v[c->metric]);
+      e.metric = c->merged_rank ? -(double)c->merged_rank[e.id] : tn_metric(c->kinds[c->metric], e.v[c->metric]);
       all[m++] = e;
     }
     qsort(all, (size_t)m, sizeof(tn_ent), tn_cmp);
@@ -712,8 +720,8 @@ static void* tn_seg_worker(void* arg) {
 int cpu_topn(void** segs, int nseg, int nthreads, const int32_t* prog, int nprog, const char* const* leaf_dims,
              const int32_t* const* leaf_ids, int nleaf, const char* dim, const int32_t* const* remap, int nagg,
              const int32_t* kinds, const char* const* cols, int metric, int32_t threshold, int32_t min_threshold,
-             int32_t* out_ids, uint64_t* out_vals, double* seconds) {
-  if (nagg > 8 || metric < 0 || metric >= nagg || threshold < 1) return -1;
+             const int32_t* merged_rank, int32_t id_limit, int32_t* out_ids, uint64_t* out_vals, double* seconds) {
+  if (nagg > 8 || (!merged_rank && (metric < 0 || metric >= nagg)) || threshold < 1) return -1;
   if (nthreads < 1) nthreads = 1;
   const double t0 = now_s();
   tn_ctx c;
@@ -733,6 +741,8 @@ int cpu_topn(void** segs, int nseg, int nthreads, const int32_t* prog, int nprog
   c.kinds = kinds;
   c.cols = cols;
   c.seg_threshold = threshold > min_threshold ? threshold : min_threshold;
+  c.merged_rank = merged_rank;
+  c.id_limit = id_limit;
   c.lists = (tn_ent**)calloc((size_t)(nseg > 0 ? nseg : 1), sizeof(tn_ent*));
   c.nlist = (int32_t*)calloc((size_t)(nseg > 0 ? nseg : 1), sizeof(int32_t));
   run_threads(nthreads < nseg ? nthreads : (nseg > 0 ? nseg : 1), tn_seg_worker, &c);
@@ -754,7 +764,7 @@ int cpu_topn(void** segs, int nseg, int nthreads, const int32_t* prog, int nprog
       while (j < n0 && acc[j].id != l[i].id) ++j;
       if (j < n0) {
         for (int a = 0; a < nagg; ++a) or_agg_combine(kinds[a], 1, &acc[j].v[a], &l[i].v[a]);
-        acc[j].metric = tn_metric(kinds[metric], acc[j].v[metric]);
+        if (!merged_rank) acc[j].metric = tn_metric(kinds[metric], acc[j].v[metric]);
       } else {
         acc[na++] = l[i];
       }

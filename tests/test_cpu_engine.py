@@ -62,6 +62,26 @@ def test_cpu_topn_matches_oracle(B, O, Q, basic_dirs):
     assert checks["per_entry_equal"] and checks["entries"] == 10, checks
 
 
+@pytest.mark.parametrize("ordering", ["lexicographic", "alphanumeric", "numeric", "inverted_numeric"])
+def test_cpu_topn_dimension_orders_match_oracle(B, O, Q, basic_dirs, ordering):
+    """DimensionTopNMetricSpec orderings (TopNBenchmark's numericSort / alphanumericSort shapes, the
+    LEXICOGRAPHIC optimizer's id cut, an InvertedTopNMetricSpec around NUMERIC) on the C engine vs the
+    oracle."""
+    paths = _segs(basic_dirs)
+    spec = {"type": "dimension", "ordering": ordering.split("_")[-1], "previousStop": None}
+    if ordering.startswith("inverted"):
+        spec = {"type": "inverted", "metric": spec}
+    query = Q.TopNQuery(intervals=["1970-01-01/2020-01-01"], dimension="dimUniform", metric=spec, threshold=10,
+                        aggregations=[Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal")])
+    _, cres = B.cpu_baseline_topn(paths, query, 2)
+    osegs = [O.OracleSegment(p) for p in paths]
+    exp = O.run(query, osegs)
+    for s in osegs:
+        s.close()
+    checks = B.check_topn(exp, cres, query)
+    assert checks["per_entry_equal"] and checks["entries"] == 10, checks
+
+
 @pytest.mark.parametrize("gran", ["all", "minute"])
 def test_cpu_groupby_matches_oracle(B, O, Q, basic_dirs, gran):
     paths = _segs(basic_dirs)
