@@ -188,9 +188,17 @@ struct Interrupt {
   bool timed = false;
   int64_t timeout_ms = 0;
   std::chrono::steady_clock::time_point deadline;
+  // DG_DEBUG_CANCEL_AT=k (tests): the call's k-th check finds its cancel flag set — written here, as
+  // another thread would, at a fixed point of the call (k = 2: after its first launch group)
+  int cancel_at = 0;
+  mutable int checks = 0;
   Interrupt(const dg_scan* q, std::chrono::steady_clock::time_point t0) {
     if (!q) return;
     cancel = q->cancel;
+    if (cancel) {
+      const char* v = getenv("DG_DEBUG_CANCEL_AT");
+      cancel_at = v ? atoi(v) : 0;
+    }
     if (q->timeout_ms > 0) {
       timed = true;
       timeout_ms = q->timeout_ms;
@@ -199,6 +207,7 @@ struct Interrupt {
   }
   bool active() const { return cancel || timed; }
   int check() const {
+    if (cancel_at > 0 && ++checks >= cancel_at) *const_cast<volatile int32_t*>(cancel) = 1;
     if (cancel && *cancel) return set_error(DG_ERR_INTERRUPTED, "query cancelled");
     if (timed && std::chrono::steady_clock::now() >= deadline)
       return set_error(DG_ERR_TIMEOUT, "query timeout (%lld ms)", (long long)timeout_ms);

@@ -10,8 +10,6 @@ import ctypes
 import importlib
 import os
 import sys
-import threading
-import time
 
 import pytest
 
@@ -64,12 +62,6 @@ def _after_interrupt_still_exact(Q, O, R, B, g, o):
         assert_results(q, R.run_query(q, g), O.run(q, o))
 
 
-def _cancel_later(flag, delay_s):
-    t = threading.Timer(delay_s, lambda: setattr(flag, "value", 1))
-    t.start()
-    return t
-
-
 def test_cancel_before_the_call(Q, O, R, N, data):
     B, g, o = data
     for name in ("groupby_hourly", "ts_hourly"):
@@ -82,9 +74,13 @@ def test_cancel_before_the_call(Q, O, R, N, data):
     _after_interrupt_still_exact(Q, O, R, B, g, o)
 
 
+@pytest.mark.parametrize("at", [2, 3])
 @pytest.mark.parametrize("name", ["groupby_hourly", "ts_hourly"])
-def test_cancel_during_the_call(Q, O, R, N, data, name):
-    """The flag set by another thread while a 32 M-row call runs on the device."""
+def test_cancel_during_the_call(Q, O, R, N, data, name, at, monkeypatch):
+    """The flag set while a 32 M-row call is in flight, at a fixed point: DG_DEBUG_CANCEL_AT=k makes the
+    call's k-th check find it set (written by the engine as another thread would): 2 = after the first
+    launch group (the decoders queued), 3 = after the keygen / sort or the scan are queued. The call
+    drains what it queued and fails DG_ERR_INTERRUPTED; the flag is the caller's, now 1."""
     B, g, o = data
     q = B.make_query(Q, name)
     heavy = list(g) * HEAVY
@@ -93,15 +89,11 @@ def test_cancel_during_the_call(Q, O, R, N, data, name):
     r = run(ctypes.c_int32(0))  # warm (merged dictionaries cached, scratch grown): the call completes
     if name.startswith("groupby"):
         r.release()
-    t0 = time.perf_counter()
-    run(ctypes.c_int32(0))
-    full_s = time.perf_counter() - t0
+    monkeypatch.setenv("DG_DEBUG_CANCEL_AT", str(at))
     flag = ctypes.c_int32(0)
-    timer = _cancel_later(flag, min(0.002, full_s / 4))
-    try:
-        _expect_code(N, lambda: run(flag), N.ERR_INTERRUPTED)
-    finally:
-        timer.cancel()
+    _expect_code(N, lambda: run(flag), N.ERR_INTERRUPTED)
+    assert flag.value == 1
+    monkeypatch.delenv("DG_DEBUG_CANCEL_AT")
     _after_interrupt_still_exact(Q, O, R, B, g, o)
 
 
