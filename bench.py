@@ -667,12 +667,14 @@ def pmc_traffic(args, kname):
     ks = match_kernels(pm["kernels"], kname)
     if not ks:
         return {}
-    calls = sum(pm["kernels"][k]["calls"] for k in ks)
-    fetch = sum(pm["kernels"][k]["fetch_bytes"] for k in ks) / calls
-    write = sum(pm["kernels"][k]["write_bytes"] for k in ks) / calls
-    tcalls = sum(pm["kernels"][k].get("trace_calls", pm["kernels"][k]["calls"]) for k in ks)
-    avg_ns = sum(pm["kernels"][k]["avg_ns"] * pm["kernels"][k].get("trace_calls", pm["kernels"][k]["calls"])
-                 for k in ks) / max(tcalls, 1)
+    # a spec of several kernels ("a+b", "prefix*") is one logical launch of each: per launch, the kernels'
+    # bytes and times add up (every kernel of such a spec launches as often as the others)
+    K = pm["kernels"]
+    calls = max(K[k]["calls"] for k in ks)
+    fetch = sum(K[k]["fetch_bytes"] for k in ks) / calls
+    write = sum(K[k]["write_bytes"] for k in ks) / calls
+    tcalls = max(K[k].get("trace_calls", K[k]["calls"]) for k in ks)
+    avg_ns = sum(K[k]["avg_ns"] * K[k].get("trace_calls", K[k]["calls"]) for k in ks) / max(tcalls, 1)
     return {"traffic": 2 * fetch + write, "traffic_fetch_raw": fetch, "traffic_write": write,
             "rocprof_avg_launch_ms": avg_ns / 1e6, "rocprof_kernels": sorted(k.split("(")[0] for k in ks),
             "traffic_source": os.path.join("bench_pmc", os.path.basename(f)) + f" ({pm.get('label', '')})"}
@@ -947,14 +949,16 @@ def main():
         groups = per_step("groups")
         # the first pass's digit totals read every packed [key | row ref] word once (k_rs_hist0); every
         # one-sweep pass reads and writes it once (k_rs_scatter): 8 + 16 x passes B per selected row
-        kernels["sort"] = ("k_rs_hist0+k_rs_scatter", n_sel * (8.0 + 16.0 * passes), passes + 1, phases["sort"])
+        # the roofline kernel is one pass's scatter (passes launches per step); the first pass's digit totals
+        # (k_rs_hist0, one read of the words) are inside the phase
+        kernels["sort"] = ("k_rs_scatter", n_sel * 16.0 * passes, passes, phases["sort"])
         # keygen: the two 3-byte ids of the row in, its 8-byte sort word out
         kernels["keygen"] = ("k_gb_keygen", n_sel * (3 + 3 + 8), 1, phases["keygen"])
         # reduce (its kernels alone): the sorted words and the payload records in, per group its key and
         # (1 + aggregators) 8-byte slots out
         pw = len(query.aggregations)
-        kernels["reduce"] = ("k_gb_reduce+k_gb_carry+k_gb_open_finalize", n_sel * (8.0 + 8.0 * pw) + groups * 8.0 * (2 + pw),
-                             1, phases["reduce_kernels"])
+        # (k_gb_carry / k_gb_open_finalize, a few us per step, are inside the phase but not the roofline kernel)
+        kernels["reduce"] = ("k_gb_reduce", n_sel * (8.0 + 8.0 * pw) + groups * 8.0 * (2 + pw), 1, phases["reduce_kernels"])
     elif phases["aggregate"] > 0:
         per_row = {"topn": 3 + 8 + 8}.get(args.config, 8)
         kernels["aggregate"] = ("k_topn_bin_*" if args.config.startswith("topn") else "k_scan_agg",

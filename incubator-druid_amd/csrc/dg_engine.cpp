@@ -3900,7 +3900,9 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   // LDS / latency bound, the sort HBM bound, so the two overlap on the CUs).
   SideJoin side_join;
   const bool no_side = env_on("DG_NO_SIDE");  // everything on the main stream (same-box A/B and tests)
-  const bool side = ctx->side && !db_side.jobs.empty() && !no_side;
+  bool side_work = !db_side.jobs.empty();
+  for (const auto& t : db_side.tasks) side_work |= !t.empty();
+  const bool side = ctx->side && side_work && !no_side;
   if (side) {
     if (!call_err(cs, st)) return set_error(DG_ERR_OOM, "error word");
     DG_FLUSH(cs, st);  // everything staged so far leaves on the main stream first

@@ -609,7 +609,12 @@ void launch_topn_select(const TopnSelJob* d_jobs, int njobs, int64_t max_card, i
 constexpr int kTileRows = 2048;
 
 // dg_sort.hip
-constexpr int kMaxDigitBits = 8;  // radix digits of up to 8 bits (9-bit digits measured slower: 64-byte store runs)
+// radix digits of up to 8 bits (9-bit digits on 4096-element tiles measured slower: 64-byte store runs);
+// DG_RS_DIGIT_BITS: A/B builds
+#ifndef DG_RS_DIGIT_BITS
+#define DG_RS_DIGIT_BITS 8
+#endif
+constexpr int kMaxDigitBits = DG_RS_DIGIT_BITS;
 constexpr int kMaxBins = 1 << kMaxDigitBits;
 constexpr int kRsMaxPasses = 8;  // 64 key bits at >= 8 bits per digit (rows of SortBufs::bin_total)
 constexpr int kSortTile = 4096;  // elements per radix / run tile (256 threads x 16)

@@ -44,6 +44,12 @@ static bool zero_async(void* p, size_t n, hipStream_t s) {
 
 constexpr int kST = 256;                 // threads of the sort / run kernels
 constexpr int kSPT = kSortTile / kST;    // 16 elements per thread
+// radix scatter tiles: DG_RS_TILE_MUL sort tiles each (A/B builds; 1 = the sort tile)
+#ifndef DG_RS_TILE_MUL
+#define DG_RS_TILE_MUL 1
+#endif
+constexpr int kRsTile = kSortTile * DG_RS_TILE_MUL;
+constexpr int kRsSPT = kRsTile / kST;
 
 // exclusive scan of one u32 per thread over an NT-thread workgroup; *total = workgroup sum
 template <int NT>
@@ -471,8 +477,8 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
                                                     const uint32_t* __restrict__ totals, W* __restrict__ status,
                                                     uint32_t* __restrict__ tile_ctr, int nshift, int nbits,
                                                     uint32_t* __restrict__ ntotals) {
-  __shared__ uint64_t s_k[kSortTile];
-  __shared__ uint32_t s_v[REFS ? kSortTile : 1];
+  __shared__ uint64_t s_k[kRsTile];
+  __shared__ uint32_t s_v[REFS ? kRsTile : 1];
   __shared__ uint32_t s_cnt[4 * kMaxBins];
   __shared__ uint32_t s_next[kMaxBins];  // the next pass's digit counts of the tile
   __shared__ int64_t s_delta[kMaxBins];  // global position of tile-sorted element i of digit d = s_delta[d] + i
@@ -485,16 +491,16 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   __syncthreads();
   const int tile = s_tile;
   const uint32_t n = *n_ptr;
-  const int64_t base = (int64_t)tile * kSortTile;
+  const int64_t base = (int64_t)tile * kRsTile;
   if (base >= n) return;  // (every later tile is past the end too: none waits for this one)
-  const int tile_n = (int)min<int64_t>(kSortTile, (int64_t)n - base);
+  const int tile_n = (int)min<int64_t>(kRsTile, (int64_t)n - base);
   const int nb = 1 << bits;
   const uint64_t dmask = (uint64_t)(nb - 1);
-  uint64_t k[kSPT];
-  uint32_t v[kSPT], rank[kSPT];
-  const int wbase = wave * (kSortTile / 4);
+  uint64_t k[kRsSPT];
+  uint32_t v[kRsSPT], rank[kRsSPT];
+  const int wbase = wave * (kRsTile / 4);
 #pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
+  for (int c = 0; c < kRsSPT; ++c) {
     const int x = wbase + c * 64 + lane;
     const bool ok = x < tile_n;
     k[c] = ok ? kin[base + x] : 0ull;
@@ -502,7 +508,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   }
   uint32_t* cnt = s_cnt + wave * kMaxBins;
 #pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
+  for (int c = 0; c < kRsSPT; ++c) {
     const bool ok = wbase + c * 64 + lane < tile_n;
     const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
     const uint64_t peers = match_digit(d, bits, ok);
@@ -514,65 +520,81 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
     if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
   }
   __syncthreads();
-  // thread d: digit d's count in the tile, its wave offsets, the earlier tiles' counts (look-back) and
-  // the digit's global base (the earlier digits' totals)
+  // thread t: digits t * kDPT .. + kDPT: each one's count in the tile, its wave offsets, the earlier
+  // tiles' counts (look-back) and the digit's global base (the earlier digits' totals)
   {
-    static_assert(kMaxBins <= kST, "one digit per thread");
-    const int d = tid;
-    uint32_t cw[4], ct = 0;
+    constexpr int kDPT = kMaxBins > kST ? kMaxBins / kST : 1;
+    static_assert(kMaxBins <= kST || kMaxBins % kST == 0, "digits per thread");
+    uint32_t cw[kDPT][4], ct[kDPT];
+    uint64_t excl[kDPT];
+    uint32_t csum = 0, gsum = 0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      cw[w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
-      ct += cw[w];
-    }
-    uint64_t excl = 0;
-    if (d < nb) {
+    for (int j = 0; j < kDPT; ++j) {
+      const int d = tid * kDPT + j;
+      ct[j] = 0;
+      excl[j] = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        cw[j][w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
+        ct[j] += cw[j][w];
+      }
+      csum += ct[j];
+      gsum += d < nb ? totals[d] : 0u;
+      if (d >= nb) continue;
       W* st = status + (size_t)tile * nb + d;
       if (tile == 0) {
-        __hip_atomic_store(st, Lb<W>::kPre | (W)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        __hip_atomic_store(st, Lb<W>::kAgg | (W)ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // eight earlier tiles at a time (independent loads), newest first, up to the first one
-        // with its inclusive prefix; a tile not published yet (it has started: it publishes its
-        // count without waiting) is loaded again
-        constexpr int kLb = 8;
-        for (int j = tile - 1; j >= 0;) {
-          W sv[kLb];
-#pragma unroll
-          for (int q = 0; q < kLb; ++q)
-            sv[q] = j - q >= 0 ? __hip_atomic_load(status + (size_t)(j - q) * nb + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : Lb<W>::kPre;
-          int q = 0;
-          bool prefix = false;
-          for (; q < kLb; ++q) {
-            if ((sv[q] >> Lb<W>::kShift) == 0) break;
-            excl += sv[q] & Lb<W>::kVal;
-            if (sv[q] & Lb<W>::kPre) {
-              prefix = true;
-              break;
-            }
-          }
-          if (prefix) break;
-          j -= q;
-          if (q < kLb) __builtin_amdgcn_s_sleep(1);
-        }
-        __hip_atomic_store(st, Lb<W>::kPre | (W)(excl + ct), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st, Lb<W>::kPre | (W)ct[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
       }
+      __hip_atomic_store(st, Lb<W>::kAgg | (W)ct[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // eight earlier tiles at a time (independent loads), newest first, up to the first one with its
+      // inclusive prefix; a tile not published yet (it has started: it publishes its count without
+      // waiting) is loaded again
+      constexpr int kLb = 8;
+      uint64_t ex = 0;
+      for (int jt = tile - 1; jt >= 0;) {
+        W sv[kLb];
+#pragma unroll
+        for (int q = 0; q < kLb; ++q)
+          sv[q] = jt - q >= 0 ? __hip_atomic_load(status + (size_t)(jt - q) * nb + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : Lb<W>::kPre;
+        int q = 0;
+        bool prefix = false;
+        for (; q < kLb; ++q) {
+          if ((sv[q] >> Lb<W>::kShift) == 0) break;
+          ex += sv[q] & Lb<W>::kVal;
+          if (sv[q] & Lb<W>::kPre) {
+            prefix = true;
+            break;
+          }
+        }
+        if (prefix) break;
+        jt -= q;
+        if (q < kLb) __builtin_amdgcn_s_sleep(1);
+      }
+      excl[j] = ex;
+      __hip_atomic_store(st, Lb<W>::kPre | (W)(ex + ct[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint32_t tot;
-    const uint32_t toff = block_scan_u32<kST>(ct, &tot, s_tmp);
-    const uint32_t gex = block_scan_u32<kST>(d < nb ? totals[d] : 0u, &tot, s_tmp);
-    if (d < nb) {
-      s_cnt[d] = toff;
-      s_cnt[kMaxBins + d] = toff + cw[0];
-      s_cnt[2 * kMaxBins + d] = toff + cw[0] + cw[1];
-      s_cnt[3 * kMaxBins + d] = toff + cw[0] + cw[1] + cw[2];
-      s_delta[d] = (int64_t)gex + (int64_t)excl - (int64_t)toff;
+    uint32_t toff = block_scan_u32<kST>(csum, &tot, s_tmp);
+    uint32_t gex = block_scan_u32<kST>(gsum, &tot, s_tmp);
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+      const int d = tid * kDPT + j;
+      if (d < nb) {
+        s_cnt[d] = toff;
+        s_cnt[kMaxBins + d] = toff + cw[j][0];
+        s_cnt[2 * kMaxBins + d] = toff + cw[j][0] + cw[j][1];
+        s_cnt[3 * kMaxBins + d] = toff + cw[j][0] + cw[j][1] + cw[j][2];
+        s_delta[d] = (int64_t)gex + (int64_t)excl[j] - (int64_t)toff;
+        toff += ct[j];
+        gex += totals[d];
+      }
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < kSPT; ++c) {
+  for (int c = 0; c < kRsSPT; ++c) {
     if (wbase + c * 64 + lane >= tile_n) continue;
     const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
     const uint32_t lp = cnt[d] + rank[c];
@@ -601,7 +623,7 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
   if (kb <= 0) return;
   const int npass = (kb + kMaxDigitBits - 1) / kMaxDigitBits;
   const int w = (kb + npass - 1) / npass;
-  const int nt = sb->ntiles_sort;
+  const int nt = (sb->ntiles_sort + DG_RS_TILE_MUL - 1) / DG_RS_TILE_MUL;  // scatter tiles
   uint32_t* totals = sb->bin_total;                            // [npass][kMaxBins]
   uint32_t* ctr = sb->bin_total + kRsMaxPasses * kMaxBins;     // [npass] tile counters
   if (!zero_async(sb->bin_total, ((size_t)kRsMaxPasses * kMaxBins + kRsMaxPasses) * sizeof(uint32_t), s)) return;

@@ -5,7 +5,7 @@ name=$1; shift
 cd "$(dirname "$0")/../incubator-druid_amd/csrc"
 out=../lib/variants/$name
 mkdir -p $out/obj
-H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I../../include $*"
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-value -Wno-unused-result -I../../include $*"
 $H -c -x hip dg_lz4.hip -o $out/obj/dg_lz4.o &
 $H -c -x hip dg_kernels.hip -o $out/obj/dg_kernels.o &
 $H -c -x hip dg_sort.hip -o $out/obj/dg_sort.o &
