@@ -1552,6 +1552,15 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
     return v && *v ? (*v != '0' ? 1 : 0) : -1;
   }();
   const bool light_main = ovl && n_run > 0 && light_env != 0;
+  // DG_GEN_FIRST=1 (same-box A/B): on a stream of its own, the general decoder before the run decoder
+  const bool gen_first = ss == st && env_on("DG_GEN_FIRST");
+  if (gen_first) {
+    if (db->gen_a && ng) phase_event(db->gen_a, st);
+    for (int w = 0; w < 4; ++w)
+      launch_lz4_decode(L[kKindGen0 + w], cnt[kKindGen0 + w], w, d_err, st,
+                        d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
+    if (db->gen_a && ng) phase_event(db->gen_b, st);
+  }
   launch_lz4_run(L[kKindRun], n_run, stage, d_err, ss);
   if (!light_main)
     launch_lz4_light(L[kKindLight], n_light, d_err, ss, d_prof ? d_prof + (size_t)nh * kLz4ProfWords : nullptr);
@@ -1572,11 +1581,13 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
   }
   db->gen_blocks += ng;
   for (int w = 0; w < 4; ++w) db->gen_launches += cnt[kKindGen0 + w] > 0;
-  if (db->gen_a && ng) phase_event(db->gen_a, st);
-  for (int w = 0; w < 4; ++w)
-    launch_lz4_decode(L[kKindGen0 + w], cnt[kKindGen0 + w], w, d_err, st,
-                      d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
-  if (db->gen_a && ng) phase_event(db->gen_b, st);
+  if (!gen_first) {
+    if (db->gen_a && ng) phase_event(db->gen_a, st);
+    for (int w = 0; w < 4; ++w)
+      launch_lz4_decode(L[kKindGen0 + w], cnt[kKindGen0 + w], w, d_err, st,
+                        d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
+    if (db->gen_a && ng) phase_event(db->gen_b, st);
+  }
   if (light_main) launch_lz4_light(L[kKindLight], n_light, d_err, st, nullptr);
   if (ovl) DG_HIP(hipStreamWaitEvent(st, ctx->ovl_ev[1], 0));
   return run_expands(cs, db, st);  // errors surface at finish_call
@@ -1882,24 +1893,7 @@ int dg_context_create(int device, dg_context** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) hipEventCreate(&e);
-  // DG_SIDE_CUS=k (same-box A/B): the side stream restricted to k CUs spread evenly over the chip;
-  // DG_SPLIT_CUS=1 also keeps the main stream off them
-  const char* side_cus = getenv("DG_SIDE_CUS");
-  const int kcu = side_cus ? atoi(side_cus) : 0;
-  if (kcu > 0 && kcu < 256) {
-    uint32_t m[8] = {0}, comp[8] = {0};
-    for (int i = 0; i < 256; ++i) {
-      if ((i * kcu) % 256 < kcu) m[i / 32] |= 1u << (i % 32);
-      else comp[i / 32] |= 1u << (i % 32);
-    }
-    if (hipExtStreamCreateWithCUMask(&ctx->side, 8, m) != hipSuccess) ctx->side = nullptr;
-    if (env_on("DG_SPLIT_CUS")) {
-      hipStreamDestroy(ctx->stream);
-      DG_HIP(hipExtStreamCreateWithCUMask(&ctx->stream, 8, comp));
-    }
-  } else if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
-    ctx->side = nullptr;
-  }
+  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) ctx->side = nullptr;
   for (auto& e : ctx->side_ev) hipEventCreate(&e);
   for (auto& e : ctx->gen_ev) hipEventCreate(&e);
   for (auto& e : ctx->ovl_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
