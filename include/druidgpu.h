@@ -545,12 +545,17 @@ int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind);
  *   DG_PROBE_GATHER    n elements: an 8-byte word read in order, a 16-byte record gathered at a pseudo-random
  *                      row (a permutation), four 8-byte stores in order (the groupBy reduce's memory floor)
  *   DG_PROBE_ZC_WRITE  n bytes written by a kernel straight into pinned host memory (zero-copy over the link,
- *                      the dg_result_fetch_groups path) */
+ *                      the dg_result_fetch_groups path)
+ *   DG_PROBE_SORT      the groupBy sort alone: n packed [key | element index] words with the headline's key
+ *                      shape (two uniform 17-bit dictionary ids below 100000), sorted by the engine's radix
+ *                      passes (timed alone; the input is rewritten before each repetition) and checked
+ *                      ascending afterwards (DG_ERR_DEVICE when not). */
 #define DG_PROBE_COPY 0
 #define DG_PROBE_D2H 1
 #define DG_PROBE_H2D 2
 #define DG_PROBE_GATHER 3
 #define DG_PROBE_ZC_WRITE 4
+#define DG_PROBE_SORT 5
 int dg_debug_probe(int32_t device, int32_t kind, int64_t n, int32_t iters, double* ms);
 
 #ifdef __cplusplus

@@ -4899,11 +4899,16 @@ extern "C" int dg_set_phase_timing(int32_t on) {
 }
 
 extern "C" int dg_debug_probe(int32_t device, int32_t kind, int64_t n, int32_t iters, double* ms) {
-  if (!ms || n <= 0 || iters <= 0 || kind < DG_PROBE_COPY || kind > DG_PROBE_ZC_WRITE)
+  if (!ms || n <= 0 || iters <= 0 || kind < DG_PROBE_COPY || kind > DG_PROBE_SORT)
     return set_error(DG_ERR_ARG, "bad probe arguments");
   DG_HIP(hipSetDevice(device));
   hipStream_t st;
   DG_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  if (kind == DG_PROBE_SORT) {
+    const int rcs = probe_sort(n, iters, ms, st);
+    hipStreamDestroy(st);
+    return rcs;
+  }
   void *a = nullptr, *b = nullptr, *h = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = DG_OK;

@@ -512,6 +512,8 @@ struct MvCheck {
 void launch_probe_copy(const void* in, void* out, int64_t bytes, hipStream_t s);
 void launch_probe_gather(const uint64_t* words, const void* rec, int64_t n, uint64_t* out, hipStream_t s);
 void launch_probe_fill(uint64_t* words, void* rec, int64_t n, hipStream_t s);
+// DG_PROBE_SORT: n words sorted iters times by launch_radix_sort (events around the sort only)
+int probe_sort(int64_t n, int iters, double* ms, hipStream_t st);
 void launch_mv_check(const MvCheck* d_jobs, int njobs, int32_t* d_err, hipStream_t s);
 // VSizeLongSerde.getSerializedSize (VSizeLongSerde.java:61-65)
 inline int64_t vsize_serialized(int bits, int64_t n) { return (bits * n + 7) / 8 + 4; }

@@ -1319,7 +1319,7 @@ __device__ __forceinline__ bool parse_tok8(const uint8_t* __restrict__ in, int n
 
 template <bool PROF>
 __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Launch L, int32_t* __restrict__ err,
-                                                                uint64_t* __restrict__ prof) {
+                                                                uint64_t* __restrict__ prof, int nblocks) {
   constexpr int SEQ = kLzSeqPerCp;
   __shared__ __attribute__((aligned(16))) uint32_t s_in32[kFlowInWords];    // staged input (after the pad)
   __shared__ __attribute__((aligned(16))) uint32_t s_out32[kFlowOutWords];  // the decoded image (after the pad)
@@ -1330,7 +1330,12 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Launch 
   __shared__ uint64_t s_red[kLzWaves];
   uint2* s_tab = reinterpret_cast<uint2*>(s_in32);  // the match table, after the literals
 
-  const Lz4Job job = fetch_job(L, blockIdx.x);
+  // a grid smaller than the launch's blocks is persistent: workgroup w decodes blocks w, w + grid, ...
+  // and keeps its CU (and its 139 KiB of LDS) for the whole launch
+#pragma unroll 1
+  for (int blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+  if (blk != (int)blockIdx.x) __syncthreads();  // the previous block's output has left the image
+  const Lz4Job job = fetch_job(L, blk);
   const int tid = threadIdx.x;
   const int n = job.src_len, ncp = job.ncp;
   if (n <= 0 || n > kLz4InCap || ncp <= 0 || ncp > kLzMaxCps || job.dec_len > kBlockBytes ||
@@ -1531,6 +1536,7 @@ __global__ __launch_bounds__(kLzThreads) void k_lz4_decode_flow(const Lz4Launch 
   if (PROF) {
     __syncthreads();
     LZ_STAMP(6);
+  }
   }
 }
 
@@ -2032,8 +2038,12 @@ void launch_lz4_light(const Lz4Launch& L, int njobs, int32_t* d_err, hipStream_t
 void launch_lz4_decode(const Lz4Launch& L, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
   if (njobs <= 0) return;
   if (wide & kLzFlow) {  // (flow blocks are never wide)
-    if (d_prof) hipLaunchKernelGGL(k_lz4_decode_flow<true>, dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, d_prof);
-    else hipLaunchKernelGGL(k_lz4_decode_flow<false>, dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, nullptr);
+    // DG_FLOW_WGS=k (same-box A/B): at most k persistent workgroups
+    const char* wgs = getenv("DG_FLOW_WGS");
+    const int k = wgs && *wgs ? atoi(wgs) : 0;
+    const int grid = k > 0 && !d_prof ? std::min(njobs, k) : njobs;
+    if (d_prof) hipLaunchKernelGGL(k_lz4_decode_flow<true>, dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, d_prof, njobs);
+    else hipLaunchKernelGGL(k_lz4_decode_flow<false>, dim3(grid), dim3(kLzThreads), 0, s, L, d_err, nullptr, njobs);
     return;
   }
   if (wide) {

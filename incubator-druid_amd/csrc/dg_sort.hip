@@ -28,6 +28,7 @@
 // Integer results are exact; doubleSum partials combine in a different order than the reference's
 // row loop (within the 1e-9 relative tolerance north_star states).
 #include <hip/hip_runtime.h>
+#include <cstring>
 
 #include "dg_device.h"
 
@@ -48,8 +49,14 @@ constexpr int kSPT = kSortTile / kST;    // 16 elements per thread
 #ifndef DG_RS_TILE_MUL
 #define DG_RS_TILE_MUL 1
 #endif
+// radix scatter threads (A/B builds; 256 = the sort kernels' kST)
+#ifndef DG_RS_THREADS
+#define DG_RS_THREADS 256
+#endif
 constexpr int kRsTile = kSortTile * DG_RS_TILE_MUL;
-constexpr int kRsSPT = kRsTile / kST;
+constexpr int kRsT = DG_RS_THREADS;
+constexpr int kRsW = kRsT / 64;  // waves of a scatter tile
+constexpr int kRsSPT = kRsTile / kRsT;
 
 // exclusive scan of one u32 per thread over an NT-thread workgroup; *total = workgroup sum
 template <int NT>
@@ -471,7 +478,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // own. The tile is then reordered by digit in LDS, so the global stores of a wave run along each
 // digit's contiguous output range (coalesced) instead of scattering lane by lane.
 template <bool REFS, class W>
-__global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+__global__ __launch_bounds__(kRsT) void k_rs_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     const uint32_t* __restrict__ n_ptr, int shift, int bits,
                                                     const uint32_t* __restrict__ totals, W* __restrict__ status,
@@ -479,15 +486,15 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
                                                     uint32_t* __restrict__ ntotals) {
   __shared__ uint64_t s_k[kRsTile];
   __shared__ uint32_t s_v[REFS ? kRsTile : 1];
-  __shared__ uint32_t s_cnt[4 * kMaxBins];
+  __shared__ uint32_t s_cnt[kRsW * kMaxBins];
   __shared__ uint32_t s_next[kMaxBins];  // the next pass's digit counts of the tile
   __shared__ int64_t s_delta[kMaxBins];  // global position of tile-sorted element i of digit d = s_delta[d] + i
-  __shared__ uint32_t s_tmp[4];
+  __shared__ uint32_t s_tmp[kRsW];
   __shared__ int s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
-  for (int i = tid; i < 4 * kMaxBins; i += kST) s_cnt[i] = 0;
-  for (int i = tid; i < kMaxBins; i += kST) s_next[i] = 0;
+  for (int i = tid; i < kRsW * kMaxBins; i += kRsT) s_cnt[i] = 0;
+  for (int i = tid; i < kMaxBins; i += kRsT) s_next[i] = 0;
   __syncthreads();
   const int tile = s_tile;
   const uint32_t n = *n_ptr;
@@ -498,7 +505,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   const uint64_t dmask = (uint64_t)(nb - 1);
   uint64_t k[kRsSPT];
   uint32_t v[kRsSPT], rank[kRsSPT];
-  const int wbase = wave * (kRsTile / 4);
+  const int wbase = wave * (kRsTile / kRsW);
 #pragma unroll
   for (int c = 0; c < kRsSPT; ++c) {
     const int x = wbase + c * 64 + lane;
@@ -523,9 +530,9 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   // thread t: digits t * kDPT .. + kDPT: each one's count in the tile, its wave offsets, the earlier
   // tiles' counts (look-back) and the digit's global base (the earlier digits' totals)
   {
-    constexpr int kDPT = kMaxBins > kST ? kMaxBins / kST : 1;
-    static_assert(kMaxBins <= kST || kMaxBins % kST == 0, "digits per thread");
-    uint32_t cw[kDPT][4], ct[kDPT];
+    constexpr int kDPT = kMaxBins > kRsT ? kMaxBins / kRsT : 1;
+    static_assert(kMaxBins <= kRsT || kMaxBins % kRsT == 0, "digits per thread");
+    uint32_t cw[kDPT][kRsW], ct[kDPT];
     uint64_t excl[kDPT];
     uint32_t csum = 0, gsum = 0;
 #pragma unroll
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
       ct[j] = 0;
       excl[j] = 0;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < kRsW; ++w) {
         cw[j][w] = d < nb ? s_cnt[w * kMaxBins + d] : 0u;
         ct[j] += cw[j][w];
       }
@@ -550,9 +557,16 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
       // eight earlier tiles at a time (independent loads), newest first, up to the first one with its
       // inclusive prefix; a tile not published yet (it has started: it publishes its count without
       // waiting) is loaded again
-      constexpr int kLb = 8;
+#ifndef DG_RS_LB
+#define DG_RS_LB 8
+#endif
+      constexpr int kLb = DG_RS_LB;
       uint64_t ex = 0;
+#ifdef DG_RS_NO_LOOKBACK  // (timing probe builds only: every tile takes offset 0 — the sort is wrong)
+      for (int jt = -1; jt >= 0;) {
+#else
       for (int jt = tile - 1; jt >= 0;) {
+#endif
         W sv[kLb];
 #pragma unroll
         for (int q = 0; q < kLb; ++q)
@@ -576,16 +590,18 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
       __hip_atomic_store(st, Lb<W>::kPre | (W)(ex + ct[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint32_t tot;
-    uint32_t toff = block_scan_u32<kST>(csum, &tot, s_tmp);
-    uint32_t gex = block_scan_u32<kST>(gsum, &tot, s_tmp);
+    uint32_t toff = block_scan_u32<kRsT>(csum, &tot, s_tmp);
+    uint32_t gex = block_scan_u32<kRsT>(gsum, &tot, s_tmp);
 #pragma unroll
     for (int j = 0; j < kDPT; ++j) {
       const int d = tid * kDPT + j;
       if (d < nb) {
-        s_cnt[d] = toff;
-        s_cnt[kMaxBins + d] = toff + cw[j][0];
-        s_cnt[2 * kMaxBins + d] = toff + cw[j][0] + cw[j][1];
-        s_cnt[3 * kMaxBins + d] = toff + cw[j][0] + cw[j][1] + cw[j][2];
+        uint32_t wo = toff;
+#pragma unroll
+        for (int w = 0; w < kRsW; ++w) {
+          s_cnt[w * kMaxBins + d] = wo;
+          wo += cw[j][w];
+        }
         s_delta[d] = (int64_t)gex + (int64_t)excl[j] - (int64_t)toff;
         toff += ct[j];
         gex += totals[d];
@@ -603,7 +619,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   }
   __syncthreads();
   const uint64_t nmask = (1ull << nbits) - 1;
-  for (int i = tid; i < tile_n; i += kST) {
+  for (int i = tid; i < tile_n; i += kRsT) {
     const uint64_t kk = s_k[i];
     const int64_t pos = s_delta[(kk >> shift) & dmask] + i;
     kout[pos] = kk;
@@ -612,7 +628,7 @@ __global__ __launch_bounds__(kST) void k_rs_scatter(const uint64_t* __restrict__
   }
   if (ntotals) {  // the next pass's digit totals (complete once this pass's kernel is)
     __syncthreads();
-    for (int dd = tid; dd < (1 << nbits); dd += kST)
+    for (int dd = tid; dd < (1 << nbits); dd += kRsT)
       if (s_next[dd]) atomicAdd(&ntotals[dd], s_next[dd]);
   }
 }
@@ -645,16 +661,16 @@ static void radix_passes(SortBufs* sb, int lo, int hi, hipStream_t s) {
     uint64_t* st64 = sb->lb_status;
     const uint32_t* tp = totals + (size_t)p * kMaxBins;
     if (sb->refs[in] && narrow)
-      hipLaunchKernelGGL((k_rs_scatter<true, uint32_t>), dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
+      hipLaunchKernelGGL((k_rs_scatter<true, uint32_t>), dim3(nt), dim3(kRsT), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
                          sb->refs[out], sb->n, shift, bits, tp, st32, ctr + p, shift + w, nbits, nt_tot);
     else if (sb->refs[in])
-      hipLaunchKernelGGL((k_rs_scatter<true, uint64_t>), dim3(nt), dim3(kST), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
+      hipLaunchKernelGGL((k_rs_scatter<true, uint64_t>), dim3(nt), dim3(kRsT), 0, s, sb->keys[in], sb->refs[in], sb->keys[out],
                          sb->refs[out], sb->n, shift, bits, tp, st64, ctr + p, shift + w, nbits, nt_tot);
     else if (narrow)
-      hipLaunchKernelGGL((k_rs_scatter<false, uint32_t>), dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out],
+      hipLaunchKernelGGL((k_rs_scatter<false, uint32_t>), dim3(nt), dim3(kRsT), 0, s, sb->keys[in], nullptr, sb->keys[out],
                          nullptr, sb->n, shift, bits, tp, st32, ctr + p, shift + w, nbits, nt_tot);
     else
-      hipLaunchKernelGGL((k_rs_scatter<false, uint64_t>), dim3(nt), dim3(kST), 0, s, sb->keys[in], nullptr, sb->keys[out],
+      hipLaunchKernelGGL((k_rs_scatter<false, uint64_t>), dim3(nt), dim3(kRsT), 0, s, sb->keys[in], nullptr, sb->keys[out],
                          nullptr, sb->n, shift, bits, tp, st64, ctr + p, shift + w, nbits, nt_tot);
     sb->cur = out;
   }
@@ -664,6 +680,82 @@ void launch_radix_sort(SortBufs* sb, int key_bits, hipStream_t s) {
   if (key_bits <= 0) return;
   static_assert(64 / kMaxDigitBits <= kRsMaxPasses, "passes of a 64-bit key");
   radix_passes(sb, 0, key_bits, s);
+}
+
+// DG_PROBE_SORT: the headline's sort words — [id0 (17 bits) | id1 (17 bits) | element index], the ids
+// uniform below 100000 (splitmix64 of the index) — and a check that the sorted words ascend
+__global__ void k_probe_sort_fill(uint64_t* __restrict__ keys, int64_t n, int ref_bits) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const uint64_t key = (((z & 0xFFFFFFFFull) % 100000ull) << 17) | ((z >> 32) % 100000ull);
+    keys[i] = (key << ref_bits) | (uint64_t)i;
+  }
+}
+__global__ void k_probe_sort_check(const uint64_t* __restrict__ keys, int64_t n, uint32_t* __restrict__ bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (keys[i] >= keys[i + 1]) atomicAdd(bad, 1u);
+}
+
+int probe_sort(int64_t n, int iters, double* ms, hipStream_t st) {
+  if (n <= 0 || n >= (1ll << 30)) return set_error(DG_ERR_ARG, "probe: sort of %lld elements", (long long)n);
+  SortBufs sb;
+  memset(&sb, 0, sizeof sb);
+  sb.cap = n;
+  sb.ntiles_sort = sort_tiles(n);
+  int rb = 1;
+  while ((1ll << rb) < n) ++rb;
+  sb.ref_bits = rb;
+  const int key_bits = 34;
+  void* mem[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  const size_t sz[5] = {((size_t)n + 16) * 8, ((size_t)n + 16) * 8, (size_t)kMaxBins * sb.ntiles_sort * 8,
+                        ((size_t)kMaxBins * kRsMaxPasses + kRsMaxPasses + 1) * 4, 16};
+  int rc = DG_OK;
+  for (int i = 0; i < 5 && rc == DG_OK; ++i)
+    if (hipMalloc(&mem[i], sz[i]) != hipSuccess) rc = set_error(DG_ERR_OOM, "probe: sort buffers of %lld", (long long)n);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (rc == DG_OK) {
+    sb.keys[0] = static_cast<uint64_t*>(mem[0]);
+    sb.keys[1] = static_cast<uint64_t*>(mem[1]);
+    sb.lb_status = static_cast<uint64_t*>(mem[2]);
+    sb.bin_total = static_cast<uint32_t*>(mem[3]);
+    sb.n = static_cast<uint32_t*>(mem[4]);
+    const uint32_t nn[4] = {(uint32_t)n, 0u, 0u, 0u};
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    double tot = 0;
+    for (int it = 0; it <= iters && rc == DG_OK; ++it) {  // (repetition 0: warm-up)
+      sb.cur = 0;
+      hipMemcpyAsync(sb.n, nn, 16, hipMemcpyHostToDevice, st);
+      hipLaunchKernelGGL(k_probe_sort_fill, dim3(4096), dim3(256), 0, st, sb.keys[0], n, rb);
+      hipEventRecord(e0, st);
+      launch_radix_sort(&sb, key_bits, st);
+      hipEventRecord(e1, st);
+      hipMemsetAsync(sb.n + 1, 0, 4, st);
+      hipLaunchKernelGGL(k_probe_sort_check, dim3(4096), dim3(256), 0, st, sb.keys[sb.cur], n, sb.n + 1);
+      uint32_t bad = 0;
+      hipMemcpyAsync(&bad, sb.n + 1, 4, hipMemcpyDeviceToHost, st);
+      if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess) {
+        rc = set_error(DG_ERR_DEVICE, "probe: sort failed");
+#ifndef DG_RS_NO_LOOKBACK
+      } else if (bad) {
+        rc = set_error(DG_ERR_DEVICE, "probe: %u sorted words out of order", bad);
+#endif
+      } else if (it > 0) {
+        float f = 0;
+        hipEventElapsedTime(&f, e0, e1);
+        tot += f;
+      }
+    }
+    if (rc == DG_OK) *ms = tot / iters;
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  for (void* m : mem)
+    if (m) hipFree(m);
+  return rc;
 }
 
 // ------------------------------------------------------------------------------------------------
