@@ -1552,13 +1552,24 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
     return v && *v ? (*v != '0' ? 1 : 0) : -1;
   }();
   const bool light_main = ovl && n_run > 0 && light_env != 0;
-  // DG_GEN_FIRST=1 (same-box A/B): on a stream of its own, the general decoder before the run decoder
-  const bool gen_first = ss == st && env_on("DG_GEN_FIRST");
+  // A groupBy's payload decode on the side stream, beside the main stream's key decode, keygen and sort
+  // (round 6): the general decoder first, as kFlowSideWgs persistent workgroups. A flow workgroup
+  // needs a whole CU (139 KiB of LDS, every VGPR), which frees only when every smaller workgroup of
+  // the other stream on it has finished: one workgroup per block waits for whole CUs again and again
+  // (decoder 5.3 ms beside the sort, 1.5 ms alone); launched first, the persistent grid takes its
+  // CUs once and keeps them, and the other stream runs on the rest (same box: 10.27-10.32 ->
+  // 9.93-9.97 ms per headline step, profiles/r06_v16_ab_gen_first.log).
+  // DG_GEN_FIRST=0/1 and DG_FLOW_WGS=k (0: one workgroup per block) override (same-box A/B, tests).
+  const bool beside_sort = ctx && st == ctx->side;
+  const char* gf = getenv("DG_GEN_FIRST");
+  const bool gen_first = ss == st && (gf && *gf ? *gf != '0' : beside_sort);
+  const char* fw = getenv("DG_FLOW_WGS");
+  const int flow_wgs = fw && *fw ? atoi(fw) : beside_sort ? kFlowSideWgs : 0;
   if (gen_first) {
     if (db->gen_a && ng) phase_event(db->gen_a, st);
     for (int w = 0; w < 4; ++w)
       launch_lz4_decode(L[kKindGen0 + w], cnt[kKindGen0 + w], w, d_err, st,
-                        d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
+                        d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr, flow_wgs);
     if (db->gen_a && ng) phase_event(db->gen_b, st);
   }
   launch_lz4_run(L[kKindRun], n_run, stage, d_err, ss);
@@ -1585,7 +1596,7 @@ static int run_decodes_only(CallScratch* cs, DecodeBatch* db, hipStream_t st, ui
     if (db->gen_a && ng) phase_event(db->gen_a, st);
     for (int w = 0; w < 4; ++w)
       launch_lz4_decode(L[kKindGen0 + w], cnt[kKindGen0 + w], w, d_err, st,
-                        d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr);
+                        d_prof ? d_prof + (size_t)kb[w] * kLz4ProfWords : nullptr, flow_wgs);
     if (db->gen_a && ng) phase_event(db->gen_b, st);
   }
   if (light_main) launch_lz4_light(L[kKindLight], n_light, d_err, st, nullptr);

@@ -162,6 +162,7 @@ Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, in
 // copy-chain level; k_lz4_decode_flow writes the literals into a byte image in LDS, then the matches
 // level by level, each level's matches spread evenly over the threads.
 constexpr int kLzFlow = 2;
+constexpr int kFlowSideWgs = 192;  // persistent flow-decoder workgroups beside the groupBy sort (dg_engine.cpp)
 constexpr int kFlowMaxDepth = 64;
 constexpr int kFlowRecBytes = 48;  // schedule bytes per checkpoint interval (lz4_flow_schedule)
 constexpr int kCompSlack = 64;     // bytes of zeros before and after a column's packed LZ4 blocks
@@ -492,7 +493,9 @@ hipError_t take_launch_error();
 // kernel launchers (dg_kernels.hip)
 constexpr int kLz4ProfWords = 32;  // per-block phase stamps of the decoder (diagnostic builds of the call)
 // blocks of one kind: wide (2 * kLzSeqPerCp sequences per checkpoint) or not
-void launch_lz4_decode(const Lz4Launch& L, int nblocks, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
+// flow blocks (wide & kLzFlow): flow_wgs > 0 caps the grid at that many persistent workgroups
+void launch_lz4_decode(const Lz4Launch& L, int nblocks, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr,
+                       int flow_wgs = 0);
 void launch_lz4_light(const Lz4Launch& L, int nblocks, int32_t* d_err, hipStream_t s, uint64_t* d_prof = nullptr);
 // run blocks (rx set); stage: 0 = read the input from L1/L2 (64 KiB of LDS per block, two per CU: beside
 // another stream's LDS-heavy kernels), 1 = stage it in LDS when the launch is small (latency mode),

@@ -2035,13 +2035,11 @@ void launch_lz4_light(const Lz4Launch& L, int njobs, int32_t* d_err, hipStream_t
   else hipLaunchKernelGGL(k_lz4_light<false>, dim3(njobs), dim3(kLtThreads), 0, s, L, d_err, nullptr);
 }
 
-void launch_lz4_decode(const Lz4Launch& L, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof) {
+void launch_lz4_decode(const Lz4Launch& L, int njobs, int wide, int32_t* d_err, hipStream_t s, uint64_t* d_prof,
+                       int flow_wgs) {
   if (njobs <= 0) return;
   if (wide & kLzFlow) {  // (flow blocks are never wide)
-    // DG_FLOW_WGS=k (same-box A/B): at most k persistent workgroups
-    const char* wgs = getenv("DG_FLOW_WGS");
-    const int k = wgs && *wgs ? atoi(wgs) : 0;
-    const int grid = k > 0 && !d_prof ? std::min(njobs, k) : njobs;
+    const int grid = flow_wgs > 0 && !d_prof ? std::min(njobs, flow_wgs) : njobs;
     if (d_prof) hipLaunchKernelGGL(k_lz4_decode_flow<true>, dim3(njobs), dim3(kLzThreads), 0, s, L, d_err, d_prof, njobs);
     else hipLaunchKernelGGL(k_lz4_decode_flow<false>, dim3(grid), dim3(kLzThreads), 0, s, L, d_err, nullptr, njobs);
     return;

@@ -446,8 +446,18 @@ __global__ __launch_bounds__(kST) void k_rs_hist0(const uint64_t* __restrict__ k
   __syncthreads();
   const uint32_t n = *n_ptr;
   const uint64_t mask = (1ull << bits) - 1;
-  for (int64_t i = (int64_t)blockIdx.x * kST + tid; i < (int64_t)n; i += (int64_t)gridDim.x * kST)
-    atomicAdd(&s_h[wave][(int)((keys[i] >> shift) & mask)], 1u);
+  // four independent loads in flight per thread (one per iteration left the read latency-bound)
+  constexpr int kU = 4;
+  const int64_t stride = (int64_t)gridDim.x * kST;
+  int64_t i = (int64_t)blockIdx.x * kST + tid;
+  for (; i + (kU - 1) * stride < (int64_t)n; i += kU * stride) {
+    uint64_t w[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) w[u] = keys[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) atomicAdd(&s_h[wave][(int)((w[u] >> shift) & mask)], 1u);
+  }
+  for (; i < (int64_t)n; i += stride) atomicAdd(&s_h[wave][(int)((keys[i] >> shift) & mask)], 1u);
   __syncthreads();
   for (int d = tid; d < (1 << bits); d += kST) {
     const uint32_t c = s_h[0][d] + s_h[1][d] + s_h[2][d] + s_h[3][d];
@@ -492,20 +502,21 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const uint64_t* __restrict_
   __shared__ uint32_t s_tmp[kRsW];
   __shared__ int s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t n = *n_ptr;  // (in flight with the tile counter: one round trip before the key loads)
   if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
   for (int i = tid; i < kRsW * kMaxBins; i += kRsT) s_cnt[i] = 0;
   for (int i = tid; i < kMaxBins; i += kRsT) s_next[i] = 0;
   __syncthreads();
   const int tile = s_tile;
-  const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)tile * kRsTile;
   if (base >= n) return;  // (every later tile is past the end too: none waits for this one)
   const int tile_n = (int)min<int64_t>(kRsTile, (int64_t)n - base);
   const int nb = 1 << bits;
   const uint64_t dmask = (uint64_t)(nb - 1);
+  const uint64_t nmask = (1ull << nbits) - 1;
+  const int wbase = wave * (kRsTile / kRsW);
   uint64_t k[kRsSPT];
   uint32_t v[kRsSPT], rank[kRsSPT];
-  const int wbase = wave * (kRsTile / kRsW);
 #pragma unroll
   for (int c = 0; c < kRsSPT; ++c) {
     const int x = wbase + c * 64 + lane;
@@ -618,13 +629,17 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const uint64_t* __restrict_
     if (REFS) s_v[lp] = v[c];
   }
   __syncthreads();
-  const uint64_t nmask = (1ull << nbits) - 1;
-  for (int i = tid; i < tile_n; i += kRsT) {
-    const uint64_t kk = s_k[i];
-    const int64_t pos = s_delta[(kk >> shift) & dmask] + i;
-    kout[pos] = kk;
-    if (REFS) vout[pos] = s_v[i];
-    if (ntotals) atomicAdd(&s_next[(kk >> nshift) & nmask], 1u);
+  // (unrolled: the LDS reads of every store are independent)
+#pragma unroll
+  for (int c = 0; c < kRsSPT; ++c) {
+    const int i = c * kRsT + tid;
+    if (i < tile_n) {
+      const uint64_t kk = s_k[i];
+      const int64_t pos = s_delta[(kk >> shift) & dmask] + i;
+      kout[pos] = kk;
+      if (REFS) vout[pos] = s_v[i];
+      if (ntotals) atomicAdd(&s_next[(kk >> nshift) & nmask], 1u);
+    }
   }
   if (ntotals) {  // the next pass's digit totals (complete once this pass's kernel is)
     __syncthreads();
@@ -723,20 +738,20 @@ int probe_sort(int64_t n, int iters, double* ms, hipStream_t st) {
     sb.bin_total = static_cast<uint32_t*>(mem[3]);
     sb.n = static_cast<uint32_t*>(mem[4]);
     const uint32_t nn[4] = {(uint32_t)n, 0u, 0u, 0u};
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
     double tot = 0;
     for (int it = 0; it <= iters && rc == DG_OK; ++it) {  // (repetition 0: warm-up)
       sb.cur = 0;
-      hipMemcpyAsync(sb.n, nn, 16, hipMemcpyHostToDevice, st);
+      (void)hipMemcpyAsync(sb.n, nn, 16, hipMemcpyHostToDevice, st);
       hipLaunchKernelGGL(k_probe_sort_fill, dim3(4096), dim3(256), 0, st, sb.keys[0], n, rb);
-      hipEventRecord(e0, st);
+      (void)hipEventRecord(e0, st);
       launch_radix_sort(&sb, key_bits, st);
-      hipEventRecord(e1, st);
-      hipMemsetAsync(sb.n + 1, 0, 4, st);
+      (void)hipEventRecord(e1, st);
+      (void)hipMemsetAsync(sb.n + 1, 0, 4, st);
       hipLaunchKernelGGL(k_probe_sort_check, dim3(4096), dim3(256), 0, st, sb.keys[sb.cur], n, sb.n + 1);
       uint32_t bad = 0;
-      hipMemcpyAsync(&bad, sb.n + 1, 4, hipMemcpyDeviceToHost, st);
+      (void)hipMemcpyAsync(&bad, sb.n + 1, 4, hipMemcpyDeviceToHost, st);
       if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess) {
         rc = set_error(DG_ERR_DEVICE, "probe: sort failed");
 #ifndef DG_RS_NO_LOOKBACK
@@ -745,16 +760,16 @@ int probe_sort(int64_t n, int iters, double* ms, hipStream_t st) {
 #endif
       } else if (it > 0) {
         float f = 0;
-        hipEventElapsedTime(&f, e0, e1);
+        (void)hipEventElapsedTime(&f, e0, e1);
         tot += f;
       }
     }
     if (rc == DG_OK) *ms = tot / iters;
   }
-  if (e0) hipEventDestroy(e0);
-  if (e1) hipEventDestroy(e1);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
   for (void* m : mem)
-    if (m) hipFree(m);
+    if (m) (void)hipFree(m);
   return rc;
 }
 
@@ -895,10 +910,10 @@ __global__ __launch_bounds__(kRT, kRedMinW) void k_gb_reduce(const uint64_t* __r
   __shared__ int s_tile;
   __shared__ int64_t s_gbase;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t n = n_ptr[0];  // (in flight with the tile counter)
   if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
   __syncthreads();
   const int tile = s_tile;
-  const uint32_t n = n_ptr[0];
   const int64_t base = (int64_t)tile * kSortTile;
   const int64_t wt = (int64_t)tile * kRedWaves + wave;  // wave tile (carry / open slot)
   if (lane == 0) {

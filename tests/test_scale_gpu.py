@@ -173,7 +173,7 @@ def test_cfg4_compound_filters_on_large_segments(R, Q, O, S, DG, tmp_path_factor
 
 
 @pytest.mark.parametrize("mode", ["inplace", "agg_filter", "interval", "phase_off", "no_side", "fetch_pinned",
-                                  "fetch_staged"])
+                                  "fetch_staged", "flow_wgs_7", "per_block_run_first"])
 def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
     """The headline's shape through the keygen paths: longSum / doubleSum of plain LZ4 columns decoded
     straight into the payload records (row-ref mode) next to a floatSum the keygen writes; a
@@ -181,13 +181,20 @@ def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
     (sparse rows: references stay row indices); and an interval cutting the segments (the per-row
     time check path). Then the engine's run-time switches on the in-place path: phase timing off (the
     bench's timed steps: the side-stream payload decode must still be joined before the reduce), the
-    payload decoded on the main stream (DG_NO_SIDE=1), and the groups fetched into pinned host memory
-    by the pack kernel (zero-copy) or through the staged DMA copy (DG_FETCH_ZC=0)."""
+    payload decoded on the main stream (DG_NO_SIDE=1), the side stream's persistent flow decoder with
+    7 workgroups (DG_FLOW_WGS=7: every workgroup decodes many blocks) or one workgroup per block after
+    the run decoder (DG_FLOW_WGS=0, DG_GEN_FIRST=0: the round-5 placement), and the groups fetched into
+    pinned host memory by the pack kernel (zero-copy) or through the staged DMA copy (DG_FETCH_ZC=0)."""
     N = importlib.import_module("incubator-druid_amd._native")
     if mode == "no_side":
         monkeypatch.setenv("DG_NO_SIDE", "1")
     if mode == "fetch_staged":
         monkeypatch.setenv("DG_FETCH_ZC", "0")
+    if mode == "flow_wgs_7":
+        monkeypatch.setenv("DG_FLOW_WGS", "7")
+    if mode == "per_block_run_first":
+        monkeypatch.setenv("DG_FLOW_WGS", "0")
+        monkeypatch.setenv("DG_GEN_FIRST", "0")
     g, o = cfg3
     aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal"),
             Q.float_sum("fsum", "sumFloatNormal")]
@@ -235,11 +242,14 @@ def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
         pool.close()
 
 
-@pytest.mark.parametrize("switch", [("DG_NO_OVERLAP", "1"), ("DG_LIGHT_MAIN", "0"), ("DG_LIGHT_MAIN", "1")])
+@pytest.mark.parametrize("switch", [("DG_NO_OVERLAP", "1"), ("DG_LIGHT_MAIN", "0"), ("DG_LIGHT_MAIN", "1"),
+                                    ("DG_FLOW_WGS", "5"), ("DG_GEN_FIRST", "1")])
 def test_cfg2_decoder_stream_switches(R, Q, O, cfg2, switch, monkeypatch):
     """The decoder stream placements of a timeseries / topN call: every decoder on the call's stream
     (DG_NO_OVERLAP=1), and the light blocks beside the run decoder on the side stream (DG_LIGHT_MAIN=0)
-    or after the general decoder on the call's stream (=1, the default), against the oracle."""
+    or after the general decoder on the call's stream (=1, the default), the flow decoder as 5
+    persistent workgroups (DG_FLOW_WGS=5) and launched before the run decoder (DG_GEN_FIRST=1), against
+    the oracle."""
     monkeypatch.setenv(*switch)
     g, o = cfg2
     aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal")]
