@@ -971,7 +971,15 @@ def main():
     # decode phase or the side-stream payload decode, are reported in phases_ms)
     single = {k: v for k, v in kernels.items()
               if k in ("lz4_general", "aggregate", "bitmap", "sort", "keygen", "reduce")}
-    dom = max(single or kernels, key=lambda k: (single or kernels)[k][3]) if kernels else None
+
+    def step_ms(k):
+        # the kernel's own time per step: its rocprofv3 average x launches per step when the committed
+        # profile of this command has it (a phase's HIP-event span also holds its helper kernels and
+        # memsets: the sort phase holds k_rs_hist0), else the phase's HIP-event time
+        kname, _, launches, kms = (single or kernels)[k]
+        avg = pmc_traffic(args, kname).get("rocprof_avg_launch_ms")
+        return avg * launches if avg else kms
+    dom = max(single or kernels, key=step_ms) if kernels else None
     roofline = None
     if dom is not None:
         kname, kbytes, launches, kms = kernels[dom]
@@ -979,7 +987,9 @@ def main():
         bpl = kbytes / launches if kbytes else None
         roofline = {"bound": "hbm", "kernel": kname, "phase": dom, "achieved": None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": None, "traffic": None, "bytes_per_launch": bpl,
-                    "hip_event_avg_launch_ms": per_launch_ms, "launches_per_step": launches}
+                    "hip_event_avg_launch_ms": per_launch_ms, "launches_per_step": launches,
+                    "dominant_by": "kernel ms per step (rocprofv3 average x launches when profiled, else HIP events)",
+                    "kernel_ms_per_step": {k: round(step_ms(k), 4) for k in (single or kernels)}}
         roofline.update(pmc_traffic(args, kname))
         # achieved = algorithmic bytes per launch / average launch time: the rocprofv3 average of the
         # committed profile of this command when there is one (bench_pmc/, the figure a reader recomputes

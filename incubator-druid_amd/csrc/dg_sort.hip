@@ -83,6 +83,29 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* total, 
 }
 
 template <int NT>
+__device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* total, uint64_t* s_tmp) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[wave] = x;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const uint64_t y = s_tmp[w];
+    off += w < wave ? y : 0ull;
+    tot += y;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + x - v;
+}
+
+template <int NT>
 __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* s_tmp) {
   uint32_t t;
   block_scan_u32<NT>(v, &t, s_tmp);
@@ -499,12 +522,19 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const uint64_t* __restrict_
   __shared__ uint32_t s_cnt[kRsW * kMaxBins];
   __shared__ uint32_t s_next[kMaxBins];  // the next pass's digit counts of the tile
   __shared__ int64_t s_delta[kMaxBins];  // global position of tile-sorted element i of digit d = s_delta[d] + i
-  __shared__ uint32_t s_tmp[kRsW];
+  __shared__ uint64_t s_tmp64[kRsW];
   __shared__ int s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t n = *n_ptr;  // (in flight with the tile counter: one round trip before the key loads)
   if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
-  for (int i = tid; i < kRsW * kMaxBins; i += kRsT) s_cnt[i] = 0;
+  // during the ranking the tile buffer is free: per wave and digit, the mask of the chunk's lanes
+  // holding that digit (one LDS OR per chunk instead of a ballot per digit bit)
+  uint64_t* s_peer = reinterpret_cast<uint64_t*>(s_k);
+  static_assert(kRsW * kMaxBins <= kRsTile, "peer masks fit the tile buffer");
+  for (int i = tid; i < kRsW * kMaxBins; i += kRsT) {
+    s_cnt[i] = 0;
+    s_peer[i] = 0;
+  }
   for (int i = tid; i < kMaxBins; i += kRsT) s_next[i] = 0;
   __syncthreads();
   const int tile = s_tile;
@@ -525,17 +555,27 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const uint64_t* __restrict_
     if (REFS) v[c] = ok ? vin[base + x] : 0u;
   }
   uint32_t* cnt = s_cnt + wave * kMaxBins;
+  uint64_t* peer = s_peer + wave * kMaxBins;
 #pragma unroll
   for (int c = 0; c < kRsSPT; ++c) {
     const bool ok = wbase + c * 64 + lane < tile_n;
     const uint32_t d = (uint32_t)((k[c] >> shift) & dmask);
-    const uint64_t peers = match_digit(d, bits, ok);
+    // every lane ORs its bit into its digit's mask, then reads the mask back: the lanes with my digit
+    // (a wave's LDS operations complete in issue order: every OR lands before the read)
+    if (ok) __hip_atomic_fetch_or(peer + d, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint64_t peers = 0;
     uint32_t prior = 0;
-    if (ok) prior = cnt[d];
+    if (ok) {
+      peers = peer[d];
+      prior = cnt[d];
+    }
     rank[c] = prior + lanes_below(peers);
-    // the highest lane of each digit group advances the wave's count (a wave's LDS operations
-    // complete in issue order, so every lane above read the count before this write)
-    if (ok && 63 - __clzll((long long)peers) == lane) cnt[d] = prior + (uint32_t)__popcll(peers);
+    // the highest lane of each digit group advances the wave's count and clears the mask (every lane
+    // above read both before these writes)
+    if (ok && 63 - __clzll((long long)peers) == lane) {
+      cnt[d] = prior + (uint32_t)__popcll(peers);
+      peer[d] = 0;
+    }
   }
   __syncthreads();
   // thread t: digits t * kDPT .. + kDPT: each one's count in the tile, its wave offsets, the earlier
@@ -600,9 +640,10 @@ __global__ __launch_bounds__(kRsT) void k_rs_scatter(const uint64_t* __restrict_
       excl[j] = ex;
       __hip_atomic_store(st, Lb<W>::kPre | (W)(ex + ct[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    uint32_t tot;
-    uint32_t toff = block_scan_u32<kRsT>(csum, &tot, s_tmp);
-    uint32_t gex = block_scan_u32<kRsT>(gsum, &tot, s_tmp);
+    // both exclusive scans in one (the tile's counts in the low word: at most kRsTile, no carry)
+    uint64_t tot;
+    const uint64_t both = block_scan_u64<kRsT>(((uint64_t)gsum << 32) | csum, &tot, s_tmp64);
+    uint32_t toff = (uint32_t)both, gex = (uint32_t)(both >> 32);
 #pragma unroll
     for (int j = 0; j < kDPT; ++j) {
       const int d = tid * kDPT + j;
