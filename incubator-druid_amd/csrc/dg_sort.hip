@@ -335,40 +335,53 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
       uint64_t key[kB];
 #pragma unroll
       for (int u = 0; u < kB; ++u) key[u] = ((uint64_t)j.seg_slot << j.seg_shift) | ((uint64_t)tbucket << j.bucket_shift);
-      for (int d = 0; d < j.ndims; ++d) {
+      // dimension d's ids of the batch, then their merged ids (rows past r1: id 0, a valid index)
+      auto load_ids = [&](int d, uint32_t* id) {
         const ColView& v = j.dims[d];
-        uint32_t g[kB];
-        if (v.kind == VIEW_IDS) {
-          const int64_t blk = r0 >> v.log2_per;
-          const uint8_t* bp = v.blocks[blk];
-          uint32_t id[kB];
+        if (v.kind != VIEW_IDS) return;
+        const int64_t blk = r0 >> v.log2_per;
+        const uint8_t* bp = v.blocks[blk];
 #pragma unroll
-          for (int u = 0; u < kB; ++u) {
-            const int64_t r = r0 + threadIdx.x + 256 * u;
-            id[u] = 0;
-            if (r < r1) {
-              const uint32_t off = (uint32_t)(r - (blk << v.log2_per)) * (uint32_t)v.width;
-              if (v.width == 3) {  // the slot / flat allocation extends past the last id's dword
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(bp + (off & ~3u));
-                id[u] = __builtin_amdgcn_alignbyte(w[1], w[0], off & 3u) & 0xFFFFFFu;
-              } else if (v.width == 1) {
-                id[u] = bp[off];
-              } else if (v.width == 2) {
-                id[u] = *reinterpret_cast<const uint16_t*>(bp + off);
-              } else {
-                id[u] = *reinterpret_cast<const uint32_t*>(bp + off);
-              }
+        for (int u = 0; u < kB; ++u) {
+          const int64_t r = r0 + threadIdx.x + 256 * u;
+          id[u] = 0;
+          if (r < r1) {
+            const uint32_t off = (uint32_t)(r - (blk << v.log2_per)) * (uint32_t)v.width;
+            if (v.width == 3) {  // the slot / flat allocation extends past the last id's dword
+              const uint32_t* w = reinterpret_cast<const uint32_t*>(bp + (off & ~3u));
+              id[u] = __builtin_amdgcn_alignbyte(w[1], w[0], off & 3u) & 0xFFFFFFu;
+            } else if (v.width == 1) {
+              id[u] = bp[off];
+            } else if (v.width == 2) {
+              id[u] = *reinterpret_cast<const uint16_t*>(bp + off);
+            } else {
+              id[u] = *reinterpret_cast<const uint32_t*>(bp + off);
             }
           }
-          const int32_t* rm = j.remap[d];
+        }
+      };
+      auto merge_ids = [&](int d, uint32_t* id) {
+        const int32_t* rm = j.remap[d];
+        if (j.dims[d].kind != VIEW_IDS) {
 #pragma unroll
-          for (int u = 0; u < kB; ++u) g[u] = rm ? (uint32_t)rm[id[u]] : id[u];  // (rows past r1: id 0, a valid index)
-        } else {
-#pragma unroll
-          for (int u = 0; u < kB; ++u) g[u] = (uint32_t)j.null_gid[d];
+          for (int u = 0; u < kB; ++u) key[u] |= (uint64_t)(uint32_t)j.null_gid[d] << j.dim_shift[d];
+          return;
         }
 #pragma unroll
-        for (int u = 0; u < kB; ++u) key[u] |= (uint64_t)g[u] << j.dim_shift[d];
+        for (int u = 0; u < kB; ++u) key[u] |= (uint64_t)(rm ? (uint32_t)rm[id[u]] : id[u]) << j.dim_shift[d];
+      };
+      if (j.ndims == 2) {  // (the common two-dimension key: both columns' loads in flight, then both maps)
+        uint32_t id0[kB], id1[kB];
+        load_ids(0, id0);
+        load_ids(1, id1);
+        merge_ids(0, id0);
+        merge_ids(1, id1);
+      } else {
+        for (int d = 0; d < j.ndims; ++d) {
+          uint32_t id[kB];
+          load_ids(d, id);
+          merge_ids(d, id);
+        }
       }
 #pragma unroll
       for (int u = 0; u < kB; ++u) {

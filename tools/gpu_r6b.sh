@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r06}
-timeout -k 10 900 python -u -m pytest tests/test_scale_gpu.py tests/test_lz4_gpu.py -m gpu -x -q \
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_scale_gpu.py tests/test_lz4_gpu.py} -m gpu -x -q \
   -k "${KEXPR:-cfg3_groupby_sort_paths or decoder_stream_switches or lz4}" --timeout 300 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?
