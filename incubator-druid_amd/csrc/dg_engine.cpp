@@ -2562,6 +2562,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   std::vector<const unsigned long long*> counts(n, nullptr);
   const bool fsum = has_float_sum(plan);
   std::vector<char> staged_acc(n, 0);
+  bool any_part = false;
   DecodeBatch db;
   decode_events(ctx, &db, false);
   phase_event(ctx->ev[0], st);
@@ -2606,6 +2607,11 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
       j.out = dev_take<uint64_t>(cs, outn);
     }
     if (!j.out) return set_error(DG_ERR_OOM, "accumulators");
+    if (cur[i].nbuckets == 1) {  // one bucket: per-tile records + one fold (k_scan_combine), no atomics
+      j.part = dev_take<uint64_t>(cs, (size_t)std::max<int64_t>((seg->nrows + kTileRows - 1) / kTileRows, 1) * rec);
+      if (!j.part) return set_error(DG_ERR_OOM, "scan partials");
+      any_part = true;
+    }
     for (int a = 0; a < na; ++a) {
       rc = 1;
       if (!bits && !fsum)
@@ -2644,6 +2650,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   DG_FLUSH(cs, st);  // (a no-op unless the decode staged nothing)
   phase_event(ctx->ev[3], st);
   launch_scan_agg(d_jobs, d_tile, ntiles, plan, 0, st);
+  if (any_part) launch_scan_combine(d_jobs, n, plan, st);
   DG_CHECK_INTERRUPT(intr);
   if (fsum) {
     // floatSum as the reference adds it: float32, one row at a time per cursor (bucket)

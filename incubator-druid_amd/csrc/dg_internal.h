@@ -228,6 +228,10 @@ struct ScanJob {
   ColView key;              // topN: dimension ids (a multi-value dimension: its value stream)
   ColView key_off;          // topN over a multi-value dimension: row value offsets (VIEW_ABSENT otherwise)
   uint64_t* out;            // accumulator table of this segment
+  // one-bucket timeseries (round 6): the tiles' records [tiles][1 + naggs], stored plainly and folded
+  // into `out` by k_scan_combine — hundreds of tiles' atomics on one record serialised (configs[0]:
+  // 1,464 on one line) — null: per-tile atomics into `out`
+  uint64_t* part;
 };
 
 // groupBy by sort (dg_sort.hip) and the floatSum row-order pass. One job per segment of the call.
@@ -564,6 +568,8 @@ struct SlotInit {
 };
 void launch_fill_u64(uint64_t* p, int64_t n_rows_of_slots, int slots_per_row, const SlotInit& init, hipStream_t s);
 void launch_scan_agg(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, AggPlan plan, int topn, hipStream_t s);
+// the tiles' records of the jobs with `part` folded into `out` (one workgroup per job, tree order)
+void launch_scan_combine(const ScanJob* d_jobs, int njobs, AggPlan plan, hipStream_t s);
 // topN aggregation with LDS-private dictionary-id ranges: workgroup (p, s) owns ids
 // [p * range, (p + 1) * range) of segment s, scans every row of the segment and writes its range of
 // the record table with plain stores (no HBM atomics). Applicable when the table needs at most

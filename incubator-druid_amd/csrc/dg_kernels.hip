@@ -252,9 +252,16 @@ __global__ __launch_bounds__(256) void k_filter_eval(const int32_t* __restrict__
     out[w] = r;
     local += __popc(r);
   }
-  // wave reduce then one atomic per wave
+  // wave reduce, the workgroup's waves in LDS, then one atomic per workgroup (a grid of at most 512:
+  // thousands of atomics on one word serialise)
+  __shared__ unsigned long long s_c[4];
   for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, 64);
-  if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
+  if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long c = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+    if (c) atomicAdd(count, c);
+  }
 }
 
 // one Roaring container per wave (pieces of long bitmaps, split at attach): the container's rows are
@@ -403,7 +410,7 @@ void launch_filter_eval(const int32_t* d_prog, int prog_len, uint32_t* const* d_
                         unsigned long long* d_count, hipStream_t s) {
   const int64_t nwords = (nrows + 31) >> 5;
   int grid = (int)((nwords + 255) / 256);
-  if (grid > 2048) grid = 2048;
+  if (grid > 512) grid = 512;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(k_filter_eval, dim3(grid), dim3(256), 0, s, d_prog, prog_len, d_sets, out, nrows, d_count);
 }
@@ -465,7 +472,13 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
   if (j.bitset) {
     const int nw = (int)((row_end - row0 + 31) >> 5);
     const uint32_t w = (int)threadIdx.x < nw ? j.bitset[(row0 >> 5) + threadIdx.x] : 0u;
-    if (!__syncthreads_or(w != 0u)) return;
+    if (!__syncthreads_or(w != 0u)) {
+      if (!TOPN && j.part && (int)threadIdx.x <= na) {  // (an empty tile's record: identities)
+        const int s = threadIdx.x;
+        j.part[(size_t)(tile - j.tile_begin) * (na + 1) + s] = s == 0 ? 0ull : identity_of(plan.op[s - 1], plan.kind[s - 1]);
+      }
+      return;
+    }
   }
 
   if (TOPN) {
@@ -547,6 +560,10 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
   }
   flush(cur);
   __syncthreads();
+  if (j.part) {  // one bucket: the tile's record, plain stores (k_scan_combine folds the tiles)
+    if ((int)threadIdx.x <= na) j.part[(size_t)(tile - j.tile_begin) * (na + 1) + threadIdx.x] = s_bins[0][threadIdx.x];
+    return;
+  }
   for (int i = threadIdx.x; i < kBins * (na + 1); i += 256) {
     const int bin = i / (na + 1), s = i % (na + 1);
     const int64_t bucket = b0 + bin;
@@ -561,6 +578,40 @@ void launch_scan_agg(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntile
   if (ntiles <= 0) return;
   if (topn) hipLaunchKernelGGL(k_scan_agg<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, plan);
   else hipLaunchKernelGGL(k_scan_agg<false>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, plan);
+}
+
+// A one-bucket job's tile records folded slot by slot (each thread a strided run of tiles, then a wave
+// tree, then the four waves in order) and combined into the record that may already hold the fused
+// decoders' folds (TimeseriesBinaryFn / AggregatorFactory.combine: the slot's own combine op).
+__global__ __launch_bounds__(256) void k_scan_combine(const ScanJob* __restrict__ jobs, AggPlan plan) {
+  __shared__ uint64_t s_w[4];
+  const ScanJob& j = jobs[blockIdx.x];
+  if (!j.part) return;
+  const int na = plan.n, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nt = (int)((j.nrows + kTileRows - 1) / kTileRows);
+  for (int s = 0; s <= na; ++s) {
+    const int op = s == 0 ? OP_ADD_I64 : plan.op[s - 1];
+    const uint64_t id = s == 0 ? 0ull : identity_of(op, plan.kind[s - 1]);
+    uint64_t acc = id;
+    for (int t = threadIdx.x; t < nt; t += 256) acc = combine_op(op, acc, j.part[(size_t)t * (na + 1) + s]);
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t y = __shfl_down(acc, o, 64);
+      acc = lane + o < 64 ? combine_op(op, acc, y) : acc;
+    }
+    if (lane == 0) s_w[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t v = s_w[0];
+      for (int w = 1; w < 4; ++w) v = combine_op(op, v, s_w[w]);
+      j.out[s] = combine_op(op, j.out[s], v);
+    }
+    __syncthreads();
+  }
+}
+
+void launch_scan_combine(const ScanJob* d_jobs, int njobs, AggPlan plan, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(k_scan_combine, dim3(njobs), dim3(256), 0, s, d_jobs, plan);
 }
 
 // ------------------------------------------------------------------------------------------------
