@@ -3007,8 +3007,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     sel.push_back(sj);
   }
   const int ns = (int)sel.size();
-  // staged zero block: per selection state[4] | ncand (+pad) | hist[8][256] words
-  const size_t sel_words = 4 + 1 + 8 * 256 / 2;
+  // staged zero block: per selection state[4] | ncand (+pad) | radix state[9][4] | hist[8][256] words
+  const size_t sel_words = 4 + 1 + 36 + 8 * 256 / 2;
   uint64_t* d_selmem;
   uint64_t* h_selz = up_take<uint64_t>(cs, sel_words * std::max(ns, 1), &d_selmem, st);
   TopnSelJob* d_sel;
@@ -3018,7 +3018,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   for (int k = 0; k < ns; ++k) {
     sel[k].state = d_selmem + sel_words * k;
     sel[k].ncand = reinterpret_cast<int32_t*>(d_selmem + sel_words * k + 4);
-    sel[k].hist = reinterpret_cast<uint32_t*>(d_selmem + sel_words * k + 5);
+    sel[k].rstate = d_selmem + sel_words * k + 5;
+    sel[k].hist = reinterpret_cast<uint32_t*>(d_selmem + sel_words * k + 41);
   }
   if (ns) memcpy(h_sel, sel.data(), sizeof(TopnSelJob) * ns);
   rc = run_decodes(cs, &db, st, nullptr, true);
@@ -3093,7 +3094,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   uint64_t* h_gath = host_take<uint64_t>(cs, (size_t)std::max<int64_t>(gtotal, 1));
   if (!h_selmem || !h_gath) return set_error(DG_ERR_OOM, "topN read-back");
   if (ns) {
-    DG_HIP(hipMemcpyAsync(h_selmem, d_selmem, 8 * sel_words * (size_t)ns, hipMemcpyDeviceToHost, st));
+    // (state + ncand of each selection, not its histograms)
+    DG_HIP(hipMemcpy2DAsync(h_selmem, 8 * sel_words, d_selmem, 8 * sel_words, 8 * 5, (size_t)ns, hipMemcpyDeviceToHost, st));
     DG_HIP(hipMemcpyAsync(h_gath, d_gath, 8 * (size_t)gtotal, hipMemcpyDeviceToHost, st));
   }
   std::vector<int32_t> h_ncand_v(std::max(ns, 1));

@@ -601,6 +601,8 @@ struct TopnSelJob {
   uint64_t* gathered;     // [gather_cap][2 + naggs]: id, then the record of cand[0 .. gather_cap)
   uint64_t* keys;         // [card] metric keys (0 = untouched)
   uint32_t* hist;         // [8][256] radix histograms (zeroed by the host)
+  uint64_t* rstate;       // [9][4] the radix choice after k levels: prefix, mask, keys still to take, done
+                          // (k_topn_radix level k writes entry k, so each level replays one histogram)
   int32_t* blkcnt;        // [ceil(card / 1024)] candidates per workgroup
   uint16_t* order;        // [gather_cap] gather positions in builder order (filled when ncand <= 4096)
   int32_t gather_cap;

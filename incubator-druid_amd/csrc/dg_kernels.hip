@@ -1079,67 +1079,81 @@ __device__ __forceinline__ uint64_t metric_key(uint64_t slot, int op, int kind, 
   return inverted ? ~k : k;
 }
 
-// Replay the radix digit choices of levels [0, levels) from the histograms: wave-parallel (64 lanes x
-// 4 bins, descending digit order), result in (*prefix, *mask). Called by one full wave. The replay
-// ends early at a level whose chosen bucket is needed whole (its count = the keys still to take):
-// exactly `threshold` keys are >= the prefix with zero low bits, so that is the K-th key bound and
-// the deeper levels are not needed; returns the levels replayed.
-__device__ int replay_digits(const uint32_t* __restrict__ hist, int levels, int64_t threshold, uint64_t* prefix_out,
-                             uint64_t* mask_out) {
+// One level of the radix digit choice from its histogram (wave-parallel: 64 lanes x 4 bins, descending
+// digit order) on a running choice (prefix, mask, keys still to take); returns whether the chosen
+// bucket is needed whole (its count = the keys still to take: exactly `threshold` keys are then >= the
+// prefix with zero low bits, so that is the K-th key bound and the deeper levels are not needed).
+// Called by one full wave.
+__device__ bool replay_one(const uint32_t* __restrict__ hist, int q, uint64_t* prefix, uint64_t* mask, int64_t* krem) {
   const int lane = threadIdx.x & 63;
-  uint64_t prefix = 0, mask = 0;
-  int64_t krem = threshold;
-  int used = levels;
-  for (int q = 0; q < levels; ++q) {
-    const int shift = 56 - 8 * q;
-    int64_t h[4], sum = 0;
+  const int shift = 56 - 8 * q;
+  int64_t h[4], sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = hist[q * 256 + 255 - (lane * 4 + j)];
+    sum += h[j];
+  }
+  int64_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  const int64_t excl = incl - sum;
+  const bool hit = excl < *krem && incl >= *krem;
+  const unsigned long long bm = __ballot(hit);
+  int digit = 0, whole = 0;
+  int64_t nk = *krem;
+  if (hit) {
+    int64_t cum = excl;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      h[j] = hist[q * 256 + 255 - (lane * 4 + j)];
-      sum += h[j];
-    }
-    int64_t incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    const int64_t excl = incl - sum;
-    const bool hit = excl < krem && incl >= krem;
-    const unsigned long long bm = __ballot(hit);
-    int digit = 0;
-    int64_t nk = krem;
-    int whole = 0;
-    if (hit) {
-      int64_t cum = excl;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (cum + h[j] >= krem) {
-          digit = 255 - (lane * 4 + j);
-          nk = krem - cum;
-          whole = h[j] == nk;
-          break;
-        }
-        cum += h[j];
+      if (cum + h[j] >= *krem) {
+        digit = 255 - (lane * 4 + j);
+        nk = *krem - cum;
+        whole = h[j] == nk;
+        break;
       }
-    }
-    if (bm) {
-      const int src = __ffsll((long long)bm) - 1;
-      digit = __shfl(digit, src, 64);
-      nk = __shfl(nk, src, 64);
-      whole = __shfl(whole, src, 64);
-    }
-    prefix |= (uint64_t)digit << shift;
-    mask |= 255ull << shift;
-    krem = nk;
-    if (whole) {
-      used = q + 1;
-      break;
+      cum += h[j];
     }
   }
-  *prefix_out = prefix;
-  *mask_out = mask;
-  return used;
+  if (bm) {
+    const int src = __ffsll((long long)bm) - 1;
+    digit = __shfl(digit, src, 64);
+    nk = __shfl(nk, src, 64);
+    whole = __shfl(whole, src, 64);
+  }
+  *prefix |= (uint64_t)digit << shift;
+  *mask |= 255ull << shift;
+  *krem = nk;
+  return whole != 0;
+}
+
+// the radix choice after `level` levels: entry level - 1 of jb.rstate (written by the previous level's
+// kernel) plus one replayed histogram; workgroup 0 stores it as entry `level` for the next kernel.
+// Called by one full wave; returns whether the choice is final.
+__device__ bool radix_state(const TopnSelJob& jb, int level, int threshold, uint64_t* p_out, uint64_t* m_out) {
+  uint64_t p = 0, m = 0;
+  int64_t krem = threshold;
+  bool done = false;
+  if (level > 1) {
+    const uint64_t* sa = jb.rstate + 4 * (level - 1);
+    p = sa[0];
+    m = sa[1];
+    krem = (int64_t)sa[2];
+    done = sa[3] != 0;
+  }
+  if (!done) done = replay_one(jb.hist, level - 1, &p, &m, &krem);
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && level < 8) {
+    uint64_t* sb = jb.rstate + 4 * level;
+    sb[0] = p;
+    sb[1] = m;
+    sb[2] = (uint64_t)krem;
+    sb[3] = done ? 1ull : 0ull;
+  }
+  *p_out = p;
+  *m_out = m;
+  return done;
 }
 
 // DimensionTopNMetricSpec key of a touched id: smaller dictionary rank = larger key; 0 = not eligible
@@ -1209,16 +1223,16 @@ __global__ __launch_bounds__(kSelBlock) void k_topn_radix(const TopnSelJob* __re
   if ((int64_t)jb.state[2] <= threshold) return;  // everything touched is a candidate
   if (threadIdx.x < 64) {
     uint64_t p, m;
-    const int used = replay_digits(jb.hist, level, threshold, &p, &m);
+    const bool done = radix_state(jb, level, threshold, &p, &m);
     if (threadIdx.x == 0) {
       s_prefix = p;
       s_mask = m;
-      s_used = used;
+      s_used = done ? 0 : level;
     }
   }
   if (threadIdx.x < 256) s_hist[threadIdx.x] = 0;
   __syncthreads();
-  if (s_used < level) return;  // the bound is final (replay_digits): no deeper histogram
+  if (s_used < level) return;  // the bound is final (a bucket taken whole): no deeper histogram
   const int64_t i = (int64_t)blockIdx.x * kSelBlock + threadIdx.x;
   const int shift = 56 - 8 * level;
   if (i < jb.card) {
@@ -1232,7 +1246,7 @@ __global__ __launch_bounds__(kSelBlock) void k_topn_radix(const TopnSelJob* __re
 __device__ __forceinline__ uint64_t sel_kth(const TopnSelJob& jb, int threshold, uint64_t* s_kth) {
   if (threadIdx.x < 64) {
     uint64_t p = 0, m = 0;
-    if ((int64_t)jb.state[2] > threshold) replay_digits(jb.hist, 8, threshold, &p, &m);
+    if ((int64_t)jb.state[2] > threshold) radix_state(jb, 8, threshold, &p, &m);  // levels 0..6 stored, 7 replayed
     if (threadIdx.x == 0) *s_kth = p;
   }
   __syncthreads();
