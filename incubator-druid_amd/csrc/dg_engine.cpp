@@ -1239,6 +1239,8 @@ static bool taskable(const BlockColumn& b, int routes) {
 struct FoldSpec {
   uint64_t* dst;
   int32_t op, kind, vkind, code;
+  const uint32_t* bits;  // a filtered scan's row bitset (null: every row folds)
+  int32_t rpb;           // rows per block
 };
 static void add_tasks(DecodeBatch* db, const BlockColumn& b, int32_t k0, int32_t k1, uint8_t* dst_base, int64_t dst_step,
                       int32_t vstride, const FoldSpec* red, bool with_light = true) {
@@ -1263,6 +1265,8 @@ static void add_tasks(DecodeBatch* db, const BlockColumn& b, int32_t k0, int32_t
       t.red_kind = red->kind;
       t.red_vkind = red->vkind;
       t.red_code = red->code;
+      t.red_bits = red->bits;
+      t.red_rpb = red->rpb;
     }
     db->tasks[kd].push_back(t);
     db->task_bytes[kd] += b.kind_bytes[kd][i1] - b.kind_bytes[kd][i0];
@@ -2141,12 +2145,16 @@ static int agg_view(Segment* seg, const dg_agg& a, CallScratch* cs, DecodeBatch*
 // whose rows share one bucket inside the interval (time_block_buckets; every block when the cursor
 // needs no time) are reduced by the decoder itself into the bucket's slot (Lz4Job.red_*), nothing is
 // written; their view pointers are tagged (kViewFused) so the scan takes the identity for those rows.
-// Other blocks (light blocks, blocks straddling a bucket edge) are decoded into slots as usual. Only
-// for an unfiltered scan and an unfiltered aggregator other than floatSum (its row-order fp32
-// recurrence) and count. `out` = the segment's [buckets][rec] accumulators, initialised before the
-// decoders run. Returns 1 when the aggregator does not qualify (the caller builds the plain view).
+// Other blocks (light blocks, blocks straddling a bucket edge) are decoded into slots as usual. For an
+// unfiltered aggregator other than floatSum (its row-order fp32 recurrence) and count; a filtered scan
+// (round 6) folds only the rows of its row bitset `bits`. `out` = the segment's [buckets][rec]
+// accumulators, initialised before the decoders run. *whole: every block of the column folds (the
+// scan then reads nothing of it). Returns 1 when the aggregator does not qualify (the caller builds
+// the plain view).
 static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::vector<int64_t>& tb, bool one_bucket,
-                          uint64_t* out, int rec, CallScratch* cs, DecodeBatch* db, ColView* v, hipStream_t st) {
+                          uint64_t* out, int rec, const uint32_t* bits, bool* whole, CallScratch* cs, DecodeBatch* db,
+                          ColView* v, hipStream_t st) {
+  *whole = false;
   const char* off = getenv("DG_NO_FUSE");  // (same-box A/B and tests: decode every block)
   if ((off && *off && *off != '0') || (a.filter && a.n_filter > 0) || a.kind == DG_AGG_COUNT ||
       a.kind == DG_AGG_FLOAT_SUM || !a.field)
@@ -2179,6 +2187,7 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
     nfused += bk[k] >= 0;
   }
   if (!nfused) return 1;
+  *whole = nfused == b.nblocks;
   v->log2_per = b.log2_per;
   v->width = b.width;
   v->pad = kViewFused;
@@ -2198,6 +2207,8 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
   fold.code = v->kind == VIEW_LONG ? (a.kind == DG_AGG_LONG_SUM ? kRedLongSum : a.kind == DG_AGG_LONG_MAX ? kRedLongMax
                                       : a.kind == DG_AGG_LONG_MIN ? kRedLongMin : kRedGeneric)
                                    : (a.kind == DG_AGG_DOUBLE_SUM ? kRedDoubleSum : kRedGeneric);
+  fold.bits = bits;
+  fold.rpb = (int32_t)b.size_per;
   const bool tasks = taskable(b, routes);
   for (int32_t k = 0; k < b.nblocks; ++k) {
     const int64_t rows = std::min<int64_t>(b.size_per, (int64_t)b.total - (int64_t)k * b.size_per);
@@ -2218,6 +2229,8 @@ static int fused_agg_view(Segment* seg, const dg_agg& a, int slot, const std::ve
       j.red_kind = fold.kind;
       j.red_vkind = fold.vkind;
       j.red_code = fold.code;
+      j.red_bits = bits;
+      j.red_row0 = (int64_t)k * b.size_per;
       db->jobs.push_back(j);
       db->fused_blocks++;
       continue;
@@ -2561,7 +2574,7 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   std::vector<int64_t> tiles_rows(n, 0);
   std::vector<const unsigned long long*> counts(n, nullptr);
   const bool fsum = has_float_sum(plan);
-  std::vector<char> staged_acc(n, 0);
+  std::vector<char> staged_acc(n, 0), skip_scan(n, 0);
   bool any_part = false;
   DecodeBatch db;
   decode_events(ctx, &db, false);
@@ -2607,19 +2620,26 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
       j.out = dev_take<uint64_t>(cs, outn);
     }
     if (!j.out) return set_error(DG_ERR_OOM, "accumulators");
-    if (cur[i].nbuckets == 1) {  // one bucket: per-tile records + one fold (k_scan_combine), no atomics
+    // A one-bucket scan that needs no row time and whose every aggregator is a plain count or folded
+    // whole by the decoders reads nothing row by row: no scan tiles; its rows and counts are the
+    // filter's row count (the interval covers the segment) or the segment's rows, set after the call.
+    bool no_rows = cur[i].nbuckets == 1 && !cur[i].need_time && !fsum;
+    for (int a = 0; a < na; ++a) {
+      rc = 1;
+      bool whole = false;
+      if (!fsum)
+        rc = fused_agg_view(seg, q->aggs[a], a, tb, !cur[i].need_time, j.out, rec, bits, &whole, cs, &db, &j.vals[a], st);
+      if (rc == 1) rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
+      if (rc) return rc;
+      no_rows &= whole || (q->aggs[a].kind == DG_AGG_COUNT && !(q->aggs[a].filter && q->aggs[a].n_filter > 0));
+    }
+    skip_scan[i] = no_rows ? 1 : 0;
+    if (!no_rows && cur[i].nbuckets == 1) {  // one bucket: per-tile records + one fold (k_scan_combine)
       j.part = dev_take<uint64_t>(cs, (size_t)std::max<int64_t>((seg->nrows + kTileRows - 1) / kTileRows, 1) * rec);
       if (!j.part) return set_error(DG_ERR_OOM, "scan partials");
       any_part = true;
     }
-    for (int a = 0; a < na; ++a) {
-      rc = 1;
-      if (!bits && !fsum)
-        rc = fused_agg_view(seg, q->aggs[a], a, tb, !cur[i].need_time, j.out, rec, cs, &db, &j.vals[a], st);
-      if (rc == 1) rc = agg_view(seg, q->aggs[a], cs, &db, &j.vals[a], &j.agg_bits[a], st);
-      if (rc) return rc;
-    }
-    tiles_rows[i] = seg->nrows;
+    tiles_rows[i] = no_rows ? 0 : seg->nrows;
   }
   DG_CHECK_INTERRUPT(intr);
   ht.mark("planned");
@@ -2699,7 +2719,13 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   if (rc) return rc;
   for (int i = 0; i < n; ++i) {
     if (!cur[i].any) continue;
-    m.pre_filtered_rows += counts[i] ? (int64_t)*counts[i] : reinterpret_cast<Segment*>(segs[i])->nrows;
+    const int64_t pre = counts[i] ? (int64_t)*counts[i] : reinterpret_cast<Segment*>(segs[i])->nrows;
+    m.pre_filtered_rows += pre;
+    if (skip_scan[i]) {  // no scan: the bucket's rows and plain counts are the selected rows
+      h_out[i][0] = (uint64_t)pre;
+      for (int a = 0; a < na; ++a)
+        if (plan.kind[a] == DG_AGG_COUNT) h_out[i][1 + a] = (uint64_t)pre;
+    }
     for (int64_t b = 0; b < cur[i].nbuckets; ++b) {
       // cursor order: a descending query emits the buckets last to first (:378-381)
       const int64_t o = (int64_t)i * bucket_cap + (gr.desc ? cur[i].nbuckets - 1 - b : b);

@@ -84,6 +84,10 @@ struct Lz4Job {
   int32_t red_kind;
   int32_t red_vkind;
   int32_t red_code;  // kRed*: the fold in the value's own type (generic: agg_input_raw + combine_op)
+  // a filtered scan's fold (round 6): only the rows whose bit is set in the segment's row bitset
+  // red_bits (null: every row) fold; value v of the block is row red_row0 + v
+  const uint32_t* red_bits;
+  int64_t red_row0;
 };
 // A run of one column's LZ4 blocks of one decoder kind, decoded in one launch. Built per call in O(1)
 // from the column's attach-time tables: block k = list[i] for i in [i0, i0 + n) (the column's blocks of
@@ -97,7 +101,9 @@ struct Lz4Task {
   uint8_t* dst_base;
   int64_t dst_step;
   uint64_t* red_dst;
-  int32_t vstride, red_op, red_kind, red_vkind, red_code, pad;
+  int32_t vstride, red_op, red_kind, red_vkind, red_code;
+  int32_t red_rpb;           // rows per block (the fold's row of value v of block k: k * red_rpb + v)
+  const uint32_t* red_bits;  // the fold's row bitset (null: every row)
 };
 // A decoder launch: blocks [0, njobs) are per-block jobs, the rest belong to tasks (task_of[b - njobs] =
 // the task of block b, task_first[t] = the launch block of task t's first block).

@@ -314,10 +314,18 @@ __device__ __forceinline__ int job_len(uint2 j) { return (int)(j.x >> 16) + 1; }
 // Output of decoded bytes [16c, 16c + 16): a 16-byte store into a slot, or with job.vstride the two
 // 8-byte values to their payload records (only values inside the block's expect_len), or with
 // job.red_dst the two values folded into the thread's aggregate `acc` (nothing written)
+// whether value v of a fused block folds: every row, or (a filtered scan) the row's bit in red_bits
+__device__ __forceinline__ bool red_row(const Lz4Job& job, int v) {
+  if (!job.red_bits) return true;
+  const int64_t r = job.red_row0 + v;
+  return (job.red_bits[r >> 5] >> (r & 31)) & 1u;
+}
+
 __device__ __forceinline__ void out16(const Lz4Job& job, int c, const uint32_t w[4], uint64_t& acc) {
   if (job.red_dst) {
     const int v = 2 * c;
-    const bool has0 = (v + 1) * 8 <= job.expect_len, has1 = (v + 2) * 8 <= job.expect_len;
+    const bool has0 = (v + 1) * 8 <= job.expect_len && red_row(job, v),
+               has1 = (v + 2) * 8 <= job.expect_len && red_row(job, v + 1);
     const uint64_t x0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), x1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
     switch (job.red_code) {
       case kRedLongSum:
@@ -416,6 +424,8 @@ __device__ __forceinline__ Lz4Job fetch_job(const Lz4Launch& L, int b) {
   j.red_kind = T.red_kind;
   j.red_vkind = T.red_vkind;
   j.red_code = T.red_code;
+  j.red_bits = T.red_bits;
+  j.red_row0 = (int64_t)k * T.red_rpb;
   return j;
 }
 
@@ -1914,7 +1924,7 @@ __global__ __launch_bounds__(kRunThreads) void k_lz4_run(const Lz4Launch L, int3
       o += k;
       if ((o & 7) == 0) {
         if (fold) {
-          if (o <= job.expect_len) run_fold(job, win, acc);
+          if (o <= job.expect_len && red_row(job, (o >> 3) - 1)) run_fold(job, win, acc);
         } else {
           s_val[(o >> 3) - 1] = win;
         }

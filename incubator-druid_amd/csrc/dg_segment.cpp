@@ -520,6 +520,8 @@ Lz4Job lz4_job(const BlockColumn& b, int32_t k, uint8_t* dst, int32_t expect, in
   j.run_far = run ? b.run_far[k] : 0;
   j.red_dst = nullptr;
   j.red_op = j.red_kind = j.red_vkind = j.red_code = 0;
+  j.red_bits = nullptr;
+  j.red_row0 = 0;
   return j;
 }
 
