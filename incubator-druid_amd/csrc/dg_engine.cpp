@@ -2579,7 +2579,9 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
   DecodeBatch db;
   decode_events(ctx, &db, false);
   phase_event(ctx->ev[0], st);
+  ht.mark("setup");
   for (int i = 0; i < n; ++i) {
+    if (i == 1) ht.mark("segment0");
     Segment* seg = reinterpret_cast<Segment*>(segs[i]);
     cur[i] = plan_cursors(seg, i, q, gr);
     out_nb[i] = (int32_t)(cur[i].any ? cur[i].nbuckets : 0);
@@ -2605,8 +2607,10 @@ int dg_timeseries_run(dg_segment* const* segs, int32_t n, const dg_scan* q, int3
     std::vector<int64_t> tb;
     if (cur[i].need_time) {
       tb = time_block_buckets(seg, tcol, cur[i], q->period_ms, gr);
+      if (i == 0) ht.mark("seg0_buckets");
       rc = time_view(tcol, tb, cs, &db, &j.time, st);
       if (rc) return rc;
+      if (i == 0) ht.mark("seg0_time_view");
     }
     // the accumulators: a small table starts as identities in the call's upload (no fill kernel)
     const size_t outn = (size_t)cur[i].nbuckets * rec;
