@@ -4048,11 +4048,10 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
     uint64_t* k2 = static_cast<uint64_t*>(result_alloc(ctx, (size_t)c2 * 8));
     uint64_t* s2 = static_cast<uint64_t*>(result_alloc(ctx, (size_t)c2 * rec * 8));
     if (k2 && s2) {
-      if (ng > 0) {
-        DG_HIP(hipMemcpyAsync(k2, res->keys, (size_t)ng * 8, hipMemcpyDeviceToDevice, st));
-        DG_HIP(hipMemcpy2DAsync(s2, (size_t)c2 * 8, res->slots, (size_t)cap * 8, (size_t)ng * 8, (size_t)rec,
-                                hipMemcpyDeviceToDevice, st));
+      if (ng > 0) {  // (one copy kernel: the runtime's 2-D copy moved these at ≈ 0.8 TB/s)
+        launch_result_compact(res->keys, res->slots, cap, ng, rec, k2, s2, st);
         DG_HIP(hipStreamSynchronize(st));
+        DG_HIP(hipGetLastError());
       }
       result_free(ctx, res->keys);
       result_free(ctx, res->slots);

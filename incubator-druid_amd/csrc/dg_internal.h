@@ -677,6 +677,9 @@ void launch_fsum_runs(const GbJob* d_jobs, int njobs, int ntiles, SortBufs* sb, 
 void launch_slots_finalize(uint64_t* slots, const uint32_t* n_ptr, int64_t cap, AggPlan plan, hipStream_t s);
 // SoA slots [rec][cap] -> AoS records [n][rec]
 void launch_soa_to_aos(const uint64_t* soa, int64_t cap, int64_t n, int rec, uint64_t* aos, hipStream_t s);
+// a result laid out for `cap` records compacted to its n groups: keys [n], slots [rec][n] (16-byte copies)
+void launch_result_compact(const uint64_t* keys, const uint64_t* slots, int64_t cap, int64_t n, int rec, uint64_t* keys2,
+                           uint64_t* slots2, hipStream_t s);
 // groups [start, start + count): key fields -> bucket index and merged ids (int32 per dimension)
 struct KeyLayout {
   int32_t ndims;

@@ -504,6 +504,38 @@ __global__ __launch_bounds__(256) void k_scan_agg(const ScanJob* __restrict__ jo
   }
 
   // timeseries
+  // A tile of an unfiltered scan whose rows share one verdict and one bucket (no time needed, or a
+  // uniform __time block: time_view) and whose every aggregator is folded by the decoders for the
+  // tile's block (a tagged kViewFused block) or a plain count adds only its row count: no row is read.
+  if (!j.bitset) {
+    bool fast = j.time.kind == VIEW_ABSENT;
+    if (!fast) {
+      const int64_t tk = row0 >> j.time.log2_per;
+      fast = (reinterpret_cast<uintptr_t>(j.time.blocks[tk]) & 1u) && tk == ((row_end - 1) >> j.time.log2_per);
+    }
+    for (int a = 0; a < na && fast; ++a) {
+      if (plan.kind[a] == DG_AGG_COUNT && !j.agg_bits[a]) continue;
+      const ColView& v = j.vals[a];
+      const int64_t bk = row0 >> v.log2_per;
+      fast = (v.pad & kViewFused) && (reinterpret_cast<uintptr_t>(v.blocks[bk]) & 1u) && bk == ((row_end - 1) >> v.log2_per);
+    }
+    if (fast) {
+      if (threadIdx.x <= na) {
+        int64_t b = 0;
+        const bool sel = row_selected(j, row0, &b);  // (the whole tile's verdict and bucket)
+        const int s = threadIdx.x;
+        const uint64_t cnt = sel ? (uint64_t)(row_end - row0) : 0ull;
+        const bool counts = s == 0 || plan.kind[s - 1] == DG_AGG_COUNT;
+        if (j.part) {
+          j.part[(size_t)(tile - j.tile_begin) * (na + 1) + s] =
+              counts ? cnt : identity_of(plan.op[s - 1], plan.kind[s - 1]);
+        } else if (sel && counts && b >= 0 && b < j.nbuckets) {
+          atomicAdd(reinterpret_cast<unsigned long long*>(j.out + (size_t)b * (na + 1) + s), (unsigned long long)cnt);
+        }
+      }
+      return;
+    }
+  }
   if (threadIdx.x == 0) {
     int64_t b0 = 0;
     if (j.period && j.time.kind != VIEW_ABSENT) {

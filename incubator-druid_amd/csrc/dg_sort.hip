@@ -1289,6 +1289,33 @@ __global__ void k_soa_to_aos(const uint64_t* __restrict__ soa, int64_t cap, int6
     aos[i] = soa[(i % rec) * cap + i / rec];
 }
 
+// keys [n] and the rec slot rows [rec][cap] -> [rec][n]: row r (r = 0: the keys) is copied in 16-byte
+// pieces where both rows are 16-byte aligned, else word by word (an odd n shifts every later row by 8)
+__global__ __launch_bounds__(256) void k_result_compact(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ slots,
+                                                        int64_t cap, int64_t n, int rec, uint64_t* __restrict__ keys2,
+                                                        uint64_t* __restrict__ slots2) {
+  const int r = blockIdx.y;  // 0: keys, 1 + s: slot row s
+  const uint64_t* src = r == 0 ? keys : slots + (size_t)(r - 1) * cap;
+  uint64_t* dst = r == 0 ? keys2 : slots2 + (size_t)(r - 1) * n;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+    const int64_t n2 = n >> 1;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += stride)
+      reinterpret_cast<ulonglong2*>(dst)[i] = reinterpret_cast<const ulonglong2*>(src)[i];
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) dst[n - 1] = src[n - 1];
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+  }
+}
+
+void launch_result_compact(const uint64_t* keys, const uint64_t* slots, int64_t cap, int64_t n, int rec, uint64_t* keys2,
+                           uint64_t* slots2, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n / 2 + 255) / 256 + 1, 2048);
+  hipLaunchKernelGGL(k_result_compact, dim3((unsigned)blocks, (unsigned)(rec + 1)), dim3(256), 0, s, keys, slots, cap, n, rec,
+                     keys2, slots2);
+}
+
 void launch_soa_to_aos(const uint64_t* soa, int64_t cap, int64_t n, int rec, uint64_t* aos, hipStream_t s) {
   if (n <= 0) return;
   const int64_t blocks = std::min<int64_t>(16384, (n * rec + 255) / 256);
