@@ -367,6 +367,7 @@ struct BlockColumn {
   DevBuf job_desc;
   DevBuf kind_dev;
   std::vector<int32_t> kind_list[kKinds];
+  std::vector<int32_t> kind_pos[kKinds];    // [k] = blocks of the kind below block k (nblocks + 1): O(1) ranges
   std::vector<int64_t> kind_bytes[kKinds];  // [i] = stored bytes of list[0 .. i)
   int64_t kind_at[kKinds] = {0, 0, 0, 0, 0, 0};
 };

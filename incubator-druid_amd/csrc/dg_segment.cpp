@@ -547,6 +547,14 @@ static int decode_tables(BlockColumn* col) {
   }
   std::vector<int32_t> all;
   for (int kd = 0; kd < kKinds; ++kd) {
+    auto& pos = col->kind_pos[kd];
+    pos.assign((size_t)nb + 1, 0);
+    size_t at = 0;
+    for (int32_t k = 0; k < nb; ++k) {
+      pos[k] = (int32_t)at;
+      if (at < col->kind_list[kd].size() && col->kind_list[kd][at] == k) ++at;
+    }
+    pos[nb] = (int32_t)at;
     col->kind_at[kd] = (int64_t)all.size();
     all.insert(all.end(), col->kind_list[kd].begin(), col->kind_list[kd].end());
     auto& pb = col->kind_bytes[kd];

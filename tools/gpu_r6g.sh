@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r06}
-timeout -k 10 900 python -u -m pytest tests/test_cfg5_gpu.py tests/test_calendar_gpu.py tests/test_gpu_parity.py tests/test_filtered_gpu.py tests/test_incremental_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests/test_cfg5_gpu.py tests/test_calendar_gpu.py tests/test_gpu_parity.py tests/test_filtered_gpu.py tests/test_incremental_gpu.py tests/test_scale_gpu.py tests/test_limit_pushdown_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?
 tail -3 gpurun_out/${TAG}_pytest.log
