@@ -856,10 +856,12 @@ def main():
                 return R.run_topn(segs, query, stats)
             return D.gather_topn(dist, query, R.topn_raw(segs, query, stats), gdict, translations, segs)
         if isinstance(query, Q.TimeseriesQuery):
+            if dist is None:
+                # QueryRunnerFactory.mergeRunners: one engine call, the buckets folded natively
+                # (dg_timeseries_merge) — not the per-segment lists merged in Python
+                return R.run_query(query, segs, stats)
             per = R.timeseries_per_segment(segs, query, stats)
             res = R.merge_timeseries(query, per)
-            if dist is None:
-                return res
             return D.allreduce_timeseries(dist, query, res, ts_buckets)
         res = R.groupby_run(segs, query, stats)  # merged, ordered groups in HBM
         if dist is not None:
