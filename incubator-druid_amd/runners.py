@@ -486,12 +486,15 @@ def topn_merge_raw(query: Q.TopNQuery, cnt: np.ndarray, keys: np.ndarray, vals: 
 
 
 def _topn_entries(query: Q.TopNQuery, values: List[Optional[str]], slots) -> List[Dict]:
-    cols = _decode_slots(query.aggregations, slots) if len(values) and query.aggregations else []
+    # (tolist: Python ints / floats per column at once, as _py of each element would give)
+    cols = [c.tolist() for c in _decode_slots(query.aggregations, slots)] if len(values) and query.aggregations else []
+    names = [a.name for a in query.aggregations]
+    dim = query.dimension
     out = []
     for j, v in enumerate(values):
-        e = {query.dimension: v}
-        for a, col in zip(query.aggregations, cols):
-            e[a.name] = _py(col[j], a.output_type)
+        e = {dim: v}
+        for name, col in zip(names, cols):
+            e[name] = col[j]
         out.append(e)
     return out
 

@@ -1,6 +1,6 @@
 """Host-side split of one small bench step (diagnostic, GPU box): wall time per step with the phase
 timestamps off, the engine's own total_ms (query_wall), and a cProfile of the Python around it.
-usage: python tools/step_profile.py timeseries|topn [steps]"""
+usage: python tools/step_profile.py timeseries|filtered|topn|topn_numeric [steps]"""
 import cProfile
 import importlib
 import os
@@ -29,7 +29,7 @@ def main():
     def step(st):
         if isinstance(q, Q.TopNQuery):
             return R.run_topn(segs, q, st)
-        return R.merge_timeseries(q, R.timeseries_per_segment(segs, q, st))
+        return R.run_query(q, segs, st)  # (as bench.py's single-rank step)
 
     for _ in range(20):
         step(R.RunStats())
@@ -46,7 +46,8 @@ def main():
     for _ in range(steps):
         step(R.RunStats())
     prof.disable()
-    pstats.Stats(prof).sort_stats("tottime").print_stats(22)
+    pstats.Stats(prof).sort_stats("tottime").print_stats(25)
+    pstats.Stats(prof).sort_stats("cumulative").print_stats(25)
 
 
 if __name__ == "__main__":
