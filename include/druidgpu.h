@@ -549,13 +549,27 @@ int dg_debug_lz4_classify(const uint8_t* block, int32_t len, int32_t* kind);
  *   DG_PROBE_SORT      the groupBy sort alone: n packed [key | element index] words with the headline's key
  *                      shape (two uniform 17-bit dictionary ids below 100000), sorted by the engine's radix
  *                      passes (timed alone; the input is rewritten before each repetition) and checked
- *                      ascending afterwards (DG_ERR_DEVICE when not). */
+ *                      ascending afterwards (DG_ERR_DEVICE when not).
+ *   DG_PROBE_CHAIN     n dependent one-workgroup kernels in a row on one stream (each reads the word its
+ *                      predecessor wrote): the per-launch cost of a chain of small kernels
+ *   DG_PROBE_CHAIN_GRAPH  the same chain captured once into a hipGraph and replayed with hipGraphLaunch
+ *                      (capture and instantiation outside the timing)
+ *   DG_PROBE_HOST_LAUNCH  host time per kernel launch call (n launches of the chain's kernel, timed on the
+ *                      host without waiting for them)
+ *   DG_PROBE_HOST_H2D  host time per hipMemcpyAsync of n bytes pinned host -> device (the staged upload)
+ *   DG_PROBE_HOST_JOIN host time per cross-stream join (hipEventRecord on one stream + hipStreamWaitEvent
+ *                      on another) */
 #define DG_PROBE_COPY 0
 #define DG_PROBE_D2H 1
 #define DG_PROBE_H2D 2
 #define DG_PROBE_GATHER 3
 #define DG_PROBE_ZC_WRITE 4
 #define DG_PROBE_SORT 5
+#define DG_PROBE_CHAIN 6
+#define DG_PROBE_CHAIN_GRAPH 7
+#define DG_PROBE_HOST_LAUNCH 8
+#define DG_PROBE_HOST_H2D 9
+#define DG_PROBE_HOST_JOIN 10
 int dg_debug_probe(int32_t device, int32_t kind, int64_t n, int32_t iters, double* ms);
 
 #ifdef __cplusplus

@@ -2840,6 +2840,17 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   dg_metrics m;
   memset(&m, 0, sizeof m);
   const int na = plan.n, rec = na + 1;
+  // topN bin index (Column::tix_*): used when every segment's dimension is a present single-value
+  // column, over ALL granularity, with no floatSum pass and the bin's table within LDS; the first
+  // topN over a column builds it from the decoded ids, later ones skip the id decode and the per-call
+  // row partition (DG_NO_TOPN_INDEX=1: the per-call bins, k_topn_bin_*)
+  bool use_ix = q->period_ms == 0 && !has_float_sum(plan) && ((size_t)rec << kTopnIxShift) * 8 <= 48 * 1024 &&
+                !env_on("DG_NO_TOPN_INDEX");
+  for (int i = 0; i < n && use_ix; ++i) {
+    const Column* c = reinterpret_cast<Segment*>(segs[i])->find(t->dimension);
+    use_ix = c && c->type == DG_COL_STRING && !c->multi_value;
+  }
+  std::vector<char> ix_skip(n, 0);  // segment i's ids are not decoded (its index is built)
   std::vector<Cursors> cur(n);
   std::vector<ScanJob> jobs(n);
   std::vector<int64_t> card(n, 1), tiles_rows(n, 0);
@@ -2878,6 +2889,8 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       if (dc->multi_value) {  // every value of a row's list aggregates the row
         rc = multi_view(dc, cs, &db, &j.key, &j.key_off, st);
         any_multi = true;
+      } else if (use_ix && dc->tix_ready) {
+        ix_skip[i] = 1;
       } else {
         rc = column_view(dc, cs, &db, &j.key, st);
       }
@@ -2901,7 +2914,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   phase_event(ctx->ev[1], st);
   ht.mark("planned");
   // dictionary-id bins: every segment's table [card][rec] is written whole by the bin reduce
-  const int shift = topn_bin_shift(na);
+  const int shift = use_ix ? kTopnIxShift : topn_bin_shift(na);
   std::vector<int32_t> bin_first(n, 0), bin_seg;
   int64_t cap = 0;
   for (int i = 0; i < n; ++i) {
@@ -2928,9 +2941,9 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   const size_t nbw = (size_t)std::max(nbins, 1);
   int32_t* d_bin_first;
   int32_t* h_bins = up_take<int32_t>(cs, (size_t)n + 4 * nbw, &d_bin_first, st);
-  uint16_t* d_lid = dev_take<uint16_t>(cs, (size_t)std::max<int64_t>(cap, 1) + 8);
-  uint64_t* d_bvals = dev_take<uint64_t>(cs, (size_t)std::max<int64_t>(cap, 1) * std::max(na, 1));
-  if (!h_bins || !d_lid || !d_bvals) return set_error(DG_ERR_OOM, "topN bins");
+  uint16_t* d_lid = use_ix ? nullptr : dev_take<uint16_t>(cs, (size_t)std::max<int64_t>(cap, 1) + 8);
+  uint64_t* d_bvals = use_ix ? nullptr : dev_take<uint64_t>(cs, (size_t)std::max<int64_t>(cap, 1) * std::max(na, 1));
+  if (!h_bins || (!use_ix && (!d_lid || !d_bvals))) return set_error(DG_ERR_OOM, "topN bins");
   memcpy(h_bins, bin_first.data(), sizeof(int32_t) * n);
   if (nbins) memcpy(h_bins + n, bin_seg.data(), sizeof(int32_t) * nbins);
   memset(h_bins + n + nbw, 0, 4 * nbw);
@@ -2945,10 +2958,32 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   ScanJob* h_jobs = up_take<ScanJob>(cs, n, &d_jobs, st);
   if (!h_jobs) return set_error(DG_ERR_OOM, "scan jobs");
   memcpy(h_jobs, jobs.data(), sizeof(ScanJob) * n);
+  // the segments' bin indexes; those not built yet are built by this call from its decoded ids
+  TopnIx* d_ix = nullptr;
+  std::vector<int> ix_build;
+  if (use_ix) {
+    TopnIx* h_ix = up_take<TopnIx>(cs, n, &d_ix, st);
+    if (!h_ix) return set_error(DG_ERR_OOM, "topN index table");
+    for (int i = 0; i < n; ++i) {
+      memset(&h_ix[i], 0, sizeof(TopnIx));
+      if (!cur[i].any) continue;
+      Column* dc = reinterpret_cast<Segment*>(segs[i])->find(t->dimension);
+      bool queued = false;  // (a segment listed twice: one build)
+      for (int k : ix_build) queued |= reinterpret_cast<Segment*>(segs[k])->find(t->dimension) == dc;
+      if (!dc->tix_ready && !queued) {
+        const int64_t nb = (card[i] + (1ll << shift) - 1) >> shift;
+        const size_t rows = (size_t)std::max<int64_t>(jobs[i].nrows, 1);
+        if (!dc->tix_perm.alloc(4 * rows) || !dc->tix_lid.alloc(2 * rows) || !dc->tix_base.alloc(4 * (size_t)nb))
+          return set_error(DG_ERR_OOM, "topN index of %s", t->dimension);
+        ix_build.push_back(i);
+      }
+      h_ix[i] = TopnIx{dc->tix_perm.as<uint32_t>(), dc->tix_lid.as<uint16_t>(), dc->tix_base.as<uint32_t>()};
+    }
+  }
   // missing-dimension segments: the key view is absent; load_id would fault, so route them
   // through a 1-entry table with a zero id view
   for (int i = 0; i < n; ++i) {
-    if (cur[i].any && jobs[i].key.kind == VIEW_ABSENT) {
+    if (cur[i].any && !ix_skip[i] && jobs[i].key.kind == VIEW_ABSENT) {
       // a constant-zero id column: block pointer table pointing at a zeroed 64 KiB slot
       uint8_t* zero = dev_take<uint8_t>(cs, kBlockBytes);
       DG_HIP(hipMemsetAsync(zero, 0, kBlockBytes, st));
@@ -3089,8 +3124,21 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     launch_scan_agg(d_jobs, d_tile, ntiles, plan, 1, st);
   } else {
     DG_FLUSH(cs, st);
-    launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
-                     d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
+    if (use_ix) {
+      for (int i : ix_build) {
+        const int nb = (int)((card[i] + (1ll << shift) - 1) >> shift);
+        uint32_t* d_cnt = dev_take<uint32_t>(cs, 2 * (size_t)nb);  // counts | cursors
+        if (!d_cnt) return set_error(DG_ERR_OOM, "topN index build");
+        DG_HIP(hipMemsetAsync(d_cnt, 0, 4 * (size_t)nb, st));
+        Column* dc = reinterpret_cast<Segment*>(segs[i])->find(t->dimension);
+        launch_topn_ix_build(d_jobs, i, jobs[i].nrows, shift, nb, d_cnt, d_cnt + nb, dc->tix_base.as<uint32_t>(),
+                             dc->tix_perm.as<uint32_t>(), dc->tix_lid.as<uint16_t>(), st);
+      }
+      launch_topn_ix_reduce(d_jobs, d_ix, d_bin_first, d_bin_seg, nbins, shift, plan, st);
+    } else {
+      launch_topn_bins(d_jobs, d_tile, ntiles, d_bin_first, d_bin_seg, nbins, shift, d_bins, d_bins + nbins,
+                       d_bins + 2 * (size_t)nbins, plan, d_lid, d_bvals, std::max<int64_t>(cap, 1), st);
+    }
   }
   ht.mark("bins_launched");
   if (has_float_sum(plan)) {
@@ -3157,6 +3205,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   rc = finish_call(cs, st);
   ht.mark("synced");
   if (rc) return rc;
+  for (int i : ix_build) reinterpret_cast<Segment*>(segs[i])->find(t->dimension)->tix_ready = true;
   for (int k = 0; k < ns; ++k) h_ncand[k] = *reinterpret_cast<const int32_t*>(h_selmem + sel_words * k + 4);
   // k_topn_order left a list's records in output order (`sorted_at`); the replays that walk the
   // candidates in id order unpack them first (ids + rec-strided slots, back in id order)
@@ -4968,8 +5017,104 @@ extern "C" int dg_set_phase_timing(int32_t on) {
   return DG_OK;
 }
 
+// DG_PROBE_CHAIN / _GRAPH: n dependent tiny kernels per repetition, launched one by one or replayed
+// from one captured graph; checks that every step ran (the word counts the launches)
+static int probe_chain(int n, int iters, bool graph, double* ms, hipStream_t st) {
+  uint32_t* w = nullptr;
+  if (hipMalloc(&w, 4) != hipSuccess) return set_error(DG_ERR_OOM, "probe word");
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = DG_OK;
+  hipMemsetAsync(w, 0, 4, st);
+  if (graph) {
+    bool ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    if (ok) launch_probe_chain(w, n, st);
+    ok = hipStreamEndCapture(st, &g) == hipSuccess && ok;
+    ok = ok && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+    if (!ok) rc = set_error(DG_ERR_DEVICE, "probe: graph capture");
+  }
+  auto once = [&] {
+    if (graph) hipGraphLaunch(ge, st);
+    else launch_probe_chain(w, n, st);
+  };
+  if (rc == DG_OK) {
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    once();  // warm-up
+    hipEventRecord(e0, st);
+    for (int i = 0; i < iters; ++i) once();
+    hipEventRecord(e1, st);
+    uint32_t got = 0;
+    if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess ||
+        hipMemcpy(&got, w, 4, hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = set_error(DG_ERR_DEVICE, "probe failed");
+    } else if (got != (uint32_t)n * (uint32_t)(iters + 1)) {
+      rc = set_error(DG_ERR_DEVICE, "probe: chain counted %u of %lld steps", got, (long long)n * (iters + 1));
+    } else {
+      float f = 0;
+      hipEventElapsedTime(&f, e0, e1);
+      *ms = (double)f / iters;
+    }
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  if (ge) hipGraphExecDestroy(ge);
+  if (g) hipGraphDestroy(g);
+  hipFree(w);
+  return rc;
+}
+
+// DG_PROBE_HOST_*: host-side cost of the enqueue calls a small query makes (ms per call, host clock)
+static int probe_host(int kind, int64_t n, int iters, double* ms, hipStream_t st) {
+  uint32_t* w = nullptr;
+  void* h = nullptr;
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev = nullptr;
+  int rc = DG_OK;
+  const size_t bytes = kind == DG_PROBE_HOST_H2D ? (size_t)std::max<int64_t>(n, 4) : 4;
+  bool ok = hipMalloc(&w, bytes) == hipSuccess && hipHostMalloc(&h, bytes, hipHostMallocDefault) == hipSuccess &&
+            hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+  if (!ok) rc = set_error(DG_ERR_OOM, "probe buffers");
+  const int reps = kind == DG_PROBE_HOST_LAUNCH ? (int)std::min<int64_t>(n, 4096) : 1;
+  auto once = [&] {
+    if (kind == DG_PROBE_HOST_LAUNCH) {
+      launch_probe_chain(w, reps, st);
+    } else if (kind == DG_PROBE_HOST_H2D) {
+      hipMemcpyAsync(w, h, bytes, hipMemcpyHostToDevice, st);
+    } else {
+      hipEventRecord(ev, st);
+      hipStreamWaitEvent(s2, ev, 0);
+    }
+  };
+  if (rc == DG_OK) {
+    hipMemsetAsync(w, 0, bytes, st);
+    for (int i = 0; i < 8; ++i) once();  // warm-up
+    if (hipStreamSynchronize(st) != hipSuccess || hipStreamSynchronize(s2) != hipSuccess) rc = set_error(DG_ERR_DEVICE, "probe failed");
+  }
+  if (rc == DG_OK) {
+    double total = 0;
+    for (int i = 0; i < iters; ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      once();
+      total += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (hipStreamSynchronize(st) != hipSuccess || hipStreamSynchronize(s2) != hipSuccess) {
+        rc = set_error(DG_ERR_DEVICE, "probe failed");
+        break;
+      }
+    }
+    if (rc == DG_OK) *ms = total / iters / reps;
+  }
+  if (ev) hipEventDestroy(ev);
+  if (s2) hipStreamDestroy(s2);
+  if (h) hipHostFree(h);
+  if (w) hipFree(w);
+  return rc;
+}
+
 extern "C" int dg_debug_probe(int32_t device, int32_t kind, int64_t n, int32_t iters, double* ms) {
-  if (!ms || n <= 0 || iters <= 0 || kind < DG_PROBE_COPY || kind > DG_PROBE_SORT)
+  if (!ms || n <= 0 || iters <= 0 || kind < DG_PROBE_COPY || kind > DG_PROBE_HOST_JOIN)
     return set_error(DG_ERR_ARG, "bad probe arguments");
   DG_HIP(hipSetDevice(device));
   hipStream_t st;
@@ -4978,6 +5123,16 @@ extern "C" int dg_debug_probe(int32_t device, int32_t kind, int64_t n, int32_t i
     const int rcs = probe_sort(n, iters, ms, st);
     hipStreamDestroy(st);
     return rcs;
+  }
+  if (kind >= DG_PROBE_HOST_LAUNCH) {
+    const int rch = probe_host(kind, n, iters, ms, st);
+    hipStreamDestroy(st);
+    return rch;
+  }
+  if (kind == DG_PROBE_CHAIN || kind == DG_PROBE_CHAIN_GRAPH) {
+    const int rcc = probe_chain((int)std::min<int64_t>(n, 4096), iters, kind == DG_PROBE_CHAIN_GRAPH, ms, st);
+    hipStreamDestroy(st);
+    return rcc;
   }
   void *a = nullptr, *b = nullptr, *h = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;

@@ -411,6 +411,10 @@ struct Column {
   std::vector<int32_t> order_host[kOrderSlots];
   int32_t order_ties[kOrderSlots] = {};
   bool order_set[kOrderSlots] = {};
+  // topN bin index (built by the first topN over the column on the device, then reused): the rows
+  // grouped by dictionary-id bin (id >> kTopnIxShift), each with its id's low bits (TopnIx)
+  DevBuf tix_perm, tix_lid, tix_base;
+  bool tix_ready = false;
 };
 
 // Merged dictionary of one dimension over a set of segments (the union of their sorted
@@ -524,6 +528,7 @@ struct MvCheck {
 };
 // measurement probes (dg_debug_probe)
 void launch_probe_copy(const void* in, void* out, int64_t bytes, hipStream_t s);
+void launch_probe_chain(uint32_t* word, int n, hipStream_t s);
 void launch_probe_gather(const uint64_t* words, const void* rec, int64_t n, uint64_t* out, hipStream_t s);
 void launch_probe_fill(uint64_t* words, void* rec, int64_t n, hipStream_t s);
 // DG_PROBE_SORT: n words sorted iters times by launch_radix_sort (events around the sort only)
@@ -592,6 +597,18 @@ void launch_topn_part(const ScanJob* d_jobs, int njobs, int64_t max_card, AggPla
 // LDS table per bin); see dg_kernels.hip. bin_first[seg] = first global bin of segment seg,
 // bin_seg[b] = segment of global bin b; hist/base/cursor: nbins words (hist zeroed by the caller);
 // lid/vals: cap selected-row slots (vals is naggs x cap).
+// topN bin index of a dimension column (Column::tix_*): bin b's rows are perm[base[b] .. base[b + 1])
+// (the last bin ends at the segment's rows), lid = each row's dictionary id & (2^shift - 1)
+struct TopnIx {
+  const uint32_t* perm;
+  const uint16_t* lid;
+  const uint32_t* base;
+};
+constexpr int kTopnIxShift = 8;  // ids per index bin: 256
+void launch_topn_ix_build(const ScanJob* d_jobs, int seg, int64_t nrows, int shift, int nbins, uint32_t* d_cnt,
+                          uint32_t* d_cursor, uint32_t* base, uint32_t* perm, uint16_t* lid, hipStream_t s);
+void launch_topn_ix_reduce(const ScanJob* d_jobs, const TopnIx* d_ix, const int32_t* d_bin_first,
+                           const int32_t* d_bin_seg, int nbins, int shift, AggPlan plan, hipStream_t s);
 int topn_bin_shift(int naggs);
 void launch_topn_bins(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntiles, const int32_t* d_bin_first,
                       const int32_t* d_bin_seg, int nbins, int shift, uint32_t* d_hist, uint32_t* d_base,

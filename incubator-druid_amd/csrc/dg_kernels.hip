@@ -1080,6 +1080,83 @@ void launch_topn_bins(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntil
                      d_base, d_hist, plan, d_lid, d_vals, cap);
 }
 
+// topN by a cached bin index (the dimension column's rows grouped by dictionary-id bin, built by the
+// first topN over the column and kept with it): a query's bin reduce walks its bin's rows through the
+// index instead of counting, scanning and scattering the rows again, and the dictionary ids need no
+// decode. Same records as k_topn_bin_reduce (count + the aggregators' slots, identity-initialised,
+// every id of the bin written); the inputs are gathered per row from the decoded metric columns.
+//   k_tix_count / k_topn_bin_scan / k_tix_scatter   build: rows per bin, bin starts, rows by bin
+//   k_topn_ix_reduce                                per bin: LDS table of its 2^shift ids, its rows
+__global__ __launch_bounds__(256) void k_tix_count(const ScanJob* __restrict__ jobs, int seg, int shift,
+                                                   uint32_t* __restrict__ cnt) {
+  const ScanJob& j = jobs[seg];
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < j.nrows; r += (int64_t)gridDim.x * 256)
+    atomicAdd(&cnt[load_id(j.key, r) >> shift], 1u);
+}
+__global__ __launch_bounds__(256) void k_tix_scatter(const ScanJob* __restrict__ jobs, int seg, int shift,
+                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm,
+                                                     uint16_t* __restrict__ lid) {
+  const ScanJob& j = jobs[seg];
+  const uint32_t lmask = (1u << shift) - 1;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < j.nrows; r += (int64_t)gridDim.x * 256) {
+    const uint32_t id = load_id(j.key, r);
+    const uint32_t pos = atomicAdd(&cursor[id >> shift], 1u);
+    perm[pos] = (uint32_t)r;
+    lid[pos] = (uint16_t)(id & lmask);
+  }
+}
+
+void launch_topn_ix_build(const ScanJob* d_jobs, int seg, int64_t nrows, int shift, int nbins, uint32_t* d_cnt,
+                          uint32_t* d_cursor, uint32_t* base, uint32_t* perm, uint16_t* lid, hipStream_t s) {
+  if (nrows <= 0 || nbins <= 0) return;
+  const unsigned grid = (unsigned)std::min<int64_t>((nrows + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_tix_count, dim3(grid), dim3(256), 0, s, d_jobs, seg, shift, d_cnt);
+  hipLaunchKernelGGL(k_topn_bin_scan, dim3(1), dim3(1024), 0, s, d_cnt, base, d_cursor, nbins);
+  hipLaunchKernelGGL(k_tix_scatter, dim3(grid), dim3(256), 0, s, d_jobs, seg, shift, d_cursor, perm, lid);
+}
+
+__global__ __launch_bounds__(kBinThreads) void k_topn_ix_reduce(const ScanJob* __restrict__ jobs,
+                                                                const TopnIx* __restrict__ ixs,
+                                                                const int32_t* __restrict__ bin_seg,
+                                                                const int32_t* __restrict__ bin_first, int shift,
+                                                                AggPlan plan) {
+  extern __shared__ uint64_t s_tab[];
+  const int gb = blockIdx.x, seg = bin_seg[gb];
+  const ScanJob& j = jobs[seg];
+  const TopnIx ix = ixs[seg];
+  const int na = plan.n, rec = na + 1;
+  const int b = gb - bin_first[seg];
+  const int nb = (int)((j.nbuckets + (1ll << shift) - 1) >> shift);
+  const int64_t id0 = (int64_t)b << shift;
+  const int64_t nid = min((int64_t)j.nbuckets - id0, 1ll << shift);
+  const int nslots = (int)nid * rec;
+  for (int x = threadIdx.x; x < nslots; x += kBinThreads) {
+    const int sl = x % rec;
+    s_tab[x] = sl == 0 ? 0ull : identity_of(plan.op[sl - 1], plan.kind[sl - 1]);
+  }
+  __syncthreads();
+  const int64_t p0 = ix.base[b], p1 = b + 1 < nb ? (int64_t)ix.base[b + 1] : (int64_t)j.nrows;
+  for (int64_t p = p0 + threadIdx.x; p < p1; p += kBinThreads) {
+    const int64_t r = ix.perm[p];
+    int64_t bb;
+    if (!row_selected(j, r, &bb)) continue;
+    uint64_t* e = s_tab + (int)ix.lid[p] * rec;
+    atomicAdd(reinterpret_cast<unsigned long long*>(e), 1ull);
+    for (int a = 0; a < na; ++a) atomic_op(plan.op[a], e + 1 + a, agg_in(j, plan, a, r));
+  }
+  __syncthreads();
+  uint64_t* out = j.out + id0 * rec;
+  for (int x = threadIdx.x; x < nslots; x += kBinThreads) out[x] = s_tab[x];
+}
+
+void launch_topn_ix_reduce(const ScanJob* d_jobs, const TopnIx* d_ix, const int32_t* d_bin_first,
+                           const int32_t* d_bin_seg, int nbins, int shift, AggPlan plan, hipStream_t s) {
+  if (nbins <= 0) return;
+  const size_t lds = ((size_t)(plan.n + 1) << shift) * 8;
+  hipLaunchKernelGGL(k_topn_ix_reduce, dim3(nbins), dim3(kBinThreads), lds, s, d_jobs, d_ix, d_bin_seg, d_bin_first,
+                     shift, plan);
+}
+
 // ------------------------------------------------------------------------------------------------
 // topN selection for one segment: the K-th largest metric key among touched ids (8-bit radix
 // select over the ordered key), then the ids whose key >= that K-th key, compacted in id order.
@@ -1745,6 +1822,14 @@ __global__ void k_probe_fill(uint64_t* __restrict__ words, uint4* __restrict__ r
     words[i] = ((uint64_t)i << 32) | r;
     rec[i] = make_uint4((uint32_t)i, 1u, (uint32_t)(i * 3), 2u);
   }
+}
+
+// DG_PROBE_CHAIN: one 64-thread workgroup; lane 0 reads the word its predecessor wrote and writes it + 1
+__global__ __launch_bounds__(64) void k_probe_step(uint32_t* __restrict__ word) {
+  if (threadIdx.x == 0) word[0] = word[0] + 1u;
+}
+void launch_probe_chain(uint32_t* word, int n, hipStream_t s) {
+  for (int i = 0; i < n; ++i) hipLaunchKernelGGL(k_probe_step, dim3(1), dim3(64), 0, s, word);
 }
 
 void launch_probe_copy(const void* in, void* out, int64_t bytes, hipStream_t s) {

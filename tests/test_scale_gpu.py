@@ -66,6 +66,38 @@ def test_cfg2_topn_matches_oracle(R, Q, O, cfg2, name):
     assert_results(q, R.run_query(q, g), O.run(q, o))
 
 
+@pytest.mark.parametrize("no_index", ["0", "1"])
+def test_cfg2_topn_bin_index(R, Q, O, S, cfg2, no_index, monkeypatch):
+    """topN by the dimension's cached bin index (the first call over fresh segments builds it from the
+    decoded ids, the later ones reuse it without decoding the ids) and by the per-call bins
+    (DG_NO_TOPN_INDEX=1): numeric, inverted and dimension-ordered metrics, a filter, an interval that
+    cuts the segments, a segment listed twice, a topN over a second dimension — against the oracle."""
+    monkeypatch.setenv("DG_NO_TOPN_INDEX", no_index)
+    g0, o = cfg2
+    g = [S.GpuSegment(s.path) for s in g0]  # fresh segments: no index yet
+    aggs = [Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal"), Q.count("rows")]
+    qs = [Q.TopNQuery(intervals=IV, dimension="dimUniform", metric="sumFloatNormal", threshold=10, aggregations=aggs),
+          Q.TopNQuery(intervals=IV, dimension="dimUniform", metric="sumLongSequential", threshold=10, aggregations=aggs),
+          Q.TopNQuery(intervals=IV, dimension="dimUniform", threshold=7, aggregations=aggs,
+                      metric={"type": "inverted", "metric": {"type": "numeric", "metric": "rows"}}),
+          Q.TopNQuery(intervals=IV, dimension="dimUniform", threshold=10, aggregations=aggs[:1],
+                      metric={"type": "dimension", "ordering": "numeric", "previousStop": None}),
+          Q.TopNQuery(intervals=IV, dimension="dimUniform", metric="sumFloatNormal", threshold=10, aggregations=aggs,
+                      filter=Q.BoundDimFilter("dimSequential", "100", "500")),
+          Q.TopNQuery(intervals=["1970-01-01T00:02/1970-01-01T00:09"], dimension="dimUniform", metric="rows",
+                      threshold=10, aggregations=aggs),
+          Q.TopNQuery(intervals=IV, dimension="dimZipf", metric="sumFloatNormal", threshold=10, aggregations=aggs)]
+    try:
+        for rnd in range(2):  # build, then reuse
+            for q in qs:
+                assert_results(q, R.run_query(q, g), O.run(q, o))
+        q = qs[0]
+        assert_results(q, R.run_query(q, [g[0], g[1], g[0]]), O.run(q, [o[0], o[1], o[0]]))
+    finally:
+        for s in g:
+            s.close()
+
+
 def test_cfg2_floatsum_follows_the_reference_recurrence(R, Q, O, cfg2):
     """750k rows of N(5000, 1) per segment: the float32 row-order sum is off the exact sum by
     ~1e-2, far outside 1e-5 — the engine matches the reference's recurrence bit for bit."""

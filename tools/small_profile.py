@@ -25,7 +25,7 @@ def main():
         segs = [S.GpuSegment(p, device=0) for p in paths]
         q = bench.make_query(Q, cfg)
         run = (lambda st: R.run_topn(segs, q, st)) if cfg.startswith("topn") else \
-            (lambda st: R.merge_timeseries(q, R.timeseries_per_segment(segs, q, st)))
+            (lambda st: R.run_query(q, segs, st))
         for _ in range(10):
             run(R.RunStats())
         n = 50
