@@ -308,6 +308,18 @@ class JavaPriorityQueue:
         return top
 
 
+def _memo_key(key):
+    """key(v) computed once per value (a comparator calls it on both sides of every comparison)."""
+    memo: Dict = {}
+
+    def k(v):
+        r = memo.get(v, memo)
+        if r is memo:
+            r = memo[v] = key(v)
+        return r
+    return k
+
+
 def _key_cmp(key):
     def cmp(a, b):
         ka, kb = key(a), key(b)
@@ -325,7 +337,7 @@ class LexicographicResultBuilder:
     def __init__(self, query: Q.TopNQuery, threshold: int):
         spec = query.metric
         self.dim = query.dimension
-        self.key = O.sort_key(spec.ordering, spec.inverted)
+        self.key = _memo_key(O.sort_key(spec.ordering, spec.inverted))
         self.cmp = _key_cmp(self.key)
         self.threshold = threshold
         self.stop = spec.previous_stop
@@ -543,9 +555,14 @@ def _merge_topn_dimension(query: Q.TopNQuery, segments: Sequence[GpuSegment], ra
     lists = []
     for i in live:
         seg, base = segments[i], i * K
-        lists.append((int(raw.ts[i]), int(raw.cnt[i]),
-                      (lambda j, seg=seg, base=base: seg.dim_value(query.dimension, int(raw.ids[base + j]))),
-                      slots[base:base + int(raw.cnt[i])]))
+        memo: Dict[int, Optional[str]] = {}  # (each entry's value looked up once)
+
+        def value_of(j, seg=seg, base=base, memo=memo):
+            v = memo.get(j, memo)
+            if v is memo:
+                v = memo[j] = seg.dim_value(query.dimension, int(raw.ids[base + j]))
+            return v
+        lists.append((int(raw.ts[i]), int(raw.cnt[i]), value_of, slots[base:base + int(raw.cnt[i])]))
     return merge_dimension_lists(query, lists, tie_free)
 
 
