@@ -4063,7 +4063,12 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   if (!h_n) return set_error(DG_ERR_OOM, "groupBy counters");
   DG_FLUSH(cs, st);
   phase_event(ctx->ev[3], st);
-  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi);
+  // every row an element (no filter, no time view, no multi-value dimension, and no floatSum pass, which
+  // reads the per-tile counts): the keygen needs no count pass (DG_GB_COUNT=1: count anyway)
+  bool rows_elems = !any_multi && !has_float_sum(plan) && !env_on("DG_GB_COUNT");
+  for (int i = 0; i < n && rows_elems; ++i)
+    rows_elems = !cur[i].any || (!gj[i].bitset && gj[i].time.kind == VIEW_ABSENT && !gj[i].multi);
+  launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi, rows_elems ? total : -1);
   phase_event(ctx->ev[5], st);
   launch_radix_sort(&sb, key_bits, st);
   phase_event(ctx->ev[6], st);

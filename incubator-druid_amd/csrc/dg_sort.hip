@@ -282,12 +282,14 @@ template <bool MULTI>
 __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ jobs, const int32_t* __restrict__ tile_job,
                                                    const uint32_t* __restrict__ offs, uint64_t* __restrict__ keys,
                                                    uint32_t* __restrict__ refs, int kshift, AggPlan plan,
-                                                   uint64_t* __restrict__ payload, int pw, int rowref) {
+                                                   uint64_t* __restrict__ payload, int pw, int rowref, int rows_elems) {
   __shared__ uint32_t s_tmp[4];
   const GbJob& j = jobs[tile_job[blockIdx.x]];
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
   const int64_t r1 = min((int64_t)j.nrows, r0 + kTileRows);
-  uint32_t base = offs[blockIdx.x];
+  // rows_elems: every row of the call is an element, in row order (no filter, no time view, one
+  // element per row): the tile's first element is its first row's index over the call, no count pass
+  uint32_t base = rows_elems ? j.row_base + (uint32_t)r0 : offs[blockIdx.x];
   const uint32_t inplace = rowref ? j.inplace : 0u;
   const bool all_inplace = pw > 0 && inplace == (pw >= 32 ? 0xFFFFFFFFu : (1u << pw) - 1u);
   // the element's sort word(s) and payload record
@@ -437,18 +439,25 @@ void launch_gb_count(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles,
 }
 
 void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
-                      hipStream_t s, bool multi) {
+                      hipStream_t s, bool multi, int64_t all_rows) {
   if (ntiles <= 0) {
     zero_async(sb->n, 4, s);
     return;
   }
-  launch_gb_count(d_jobs, d_tile_job, ntiles, sb->tile_cnt, sb->n, multi, s);
+  const bool rows_elems = !multi && all_rows >= 0;
+  if (rows_elems) {  // the element count is the call's row count (no per-tile count + scan)
+    const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sb->n), (int)(uint32_t)all_rows, 1, s);
+    if (e != hipSuccess) note_launch_error(e);
+  } else {
+    launch_gb_count(d_jobs, d_tile_job, ntiles, sb->tile_cnt, sb->n, multi, s);
+  }
   if (multi)
     hipLaunchKernelGGL(k_gb_keygen<true>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, 0);
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, 0, 0);
   else
     hipLaunchKernelGGL(k_gb_keygen<false>, dim3(ntiles), dim3(256), 0, s, d_jobs, d_tile_job, sb->tile_cnt,
-                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->row_refs);
+                       sb->keys[sb->cur], sb->refs[sb->cur], sb->ref_bits, plan, sb->payload, sb->pw, sb->row_refs,
+                       rows_elems ? 1 : 0);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -205,7 +205,8 @@ def test_cfg4_compound_filters_on_large_segments(R, Q, O, S, DG, tmp_path_factor
 
 
 @pytest.mark.parametrize("mode", ["inplace", "agg_filter", "interval", "phase_off", "no_side", "fetch_pinned",
-                                  "fetch_staged", "flow_wgs_7", "per_block_run_first"])
+                                  "fetch_staged", "flow_wgs_7", "per_block_run_first", "rows_elems",
+                                  "rows_elems_counted"])
 def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
     """The headline's shape through the keygen paths: longSum / doubleSum of plain LZ4 columns decoded
     straight into the payload records (row-ref mode) next to a floatSum the keygen writes; a
@@ -216,7 +217,9 @@ def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
     payload decoded on the main stream (DG_NO_SIDE=1), the side stream's persistent flow decoder with
     7 workgroups (DG_FLOW_WGS=7: every workgroup decodes many blocks) or one workgroup per block after
     the run decoder (DG_FLOW_WGS=0, DG_GEN_FIRST=0: the round-5 placement), and the groups fetched into
-    pinned host memory by the pack kernel (zero-copy) or through the staged DMA copy (DG_FETCH_ZC=0)."""
+    pinned host memory by the pack kernel (zero-copy) or through the staged DMA copy (DG_FETCH_ZC=0);
+    without the floatSum every row is an element and the keygen runs without its count pass (and with
+    it, DG_GB_COUNT=1)."""
     N = importlib.import_module("incubator-druid_amd._native")
     if mode == "no_side":
         monkeypatch.setenv("DG_NO_SIDE", "1")
@@ -227,9 +230,13 @@ def test_cfg3_groupby_sort_paths(R, Q, O, cfg3, mode, monkeypatch):
     if mode == "per_block_run_first":
         monkeypatch.setenv("DG_FLOW_WGS", "0")
         monkeypatch.setenv("DG_GEN_FIRST", "0")
+    if mode == "rows_elems_counted":
+        monkeypatch.setenv("DG_GB_COUNT", "1")
     g, o = cfg3
     aggs = [Q.count("rows"), Q.long_sum("sumLongSequential"), Q.double_sum("sumFloatNormal"),
             Q.float_sum("fsum", "sumFloatNormal")]
+    if mode.startswith("rows_elems"):  # (no floatSum: every row an element, the keygen's count pass skipped)
+        aggs = aggs[:3]
     iv, flt = IV, None
     if mode == "agg_filter":
         aggs[1] = Q.filtered(Q.long_sum("sumLongSequential"), Q.BoundDimFilter("dimHyperUnique", "2", "7"))
