@@ -4063,11 +4063,22 @@ int dg_groupby_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const d
   if (!h_n) return set_error(DG_ERR_OOM, "groupBy counters");
   DG_FLUSH(cs, st);
   phase_event(ctx->ev[3], st);
-  // every row an element (no filter, no time view, no multi-value dimension, and no floatSum pass, which
-  // reads the per-tile counts): the keygen needs no count pass (DG_GB_COUNT=1: count anyway)
+  // every row an element (no filter, no multi-value dimension, every row's time inside the cursor's
+  // interval — no time view, or the attach-time block bounds of __time inside it — and no floatSum
+  // pass, which reads the per-tile counts): the keygen needs no count pass (DG_GB_COUNT=1: count anyway)
+  auto all_rows_in = [&](int i) {
+    if (gj[i].bitset || gj[i].multi) return false;
+    if (gj[i].time.kind == VIEW_ABSENT) return true;
+    const Column* tc = sv[i]->find("__time");
+    if (!tc || !tc->data.time_col || tc->data.nblocks <= 0 || tc->data.min8.size() != (size_t)tc->data.nblocks ||
+        tc->data.max8.size() != (size_t)tc->data.nblocks)
+      return false;
+    const int64_t lo = *std::min_element(tc->data.min8.begin(), tc->data.min8.end());
+    const int64_t hi = *std::max_element(tc->data.max8.begin(), tc->data.max8.end());
+    return lo >= gj[i].t_lo && hi < gj[i].t_hi;
+  };
   bool rows_elems = !any_multi && !has_float_sum(plan) && !env_on("DG_GB_COUNT");
-  for (int i = 0; i < n && rows_elems; ++i)
-    rows_elems = !cur[i].any || (!gj[i].bitset && gj[i].time.kind == VIEW_ABSENT && !gj[i].multi);
+  for (int i = 0; i < n && rows_elems; ++i) rows_elems = !cur[i].any || all_rows_in(i);
   launch_gb_keygen(d_jobs, d_tile, ntiles, &sb, plan, st, any_multi, rows_elems ? total : -1);
   phase_event(ctx->ev[5], st);
   launch_radix_sort(&sb, key_bits, st);

@@ -671,8 +671,9 @@ void launch_gb_count(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles,
 // multi-value element count: per-tile counts (0xFFFFFFFF = saturated) and their 64-bit total
 void launch_gb_count_total(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, uint32_t* tile_cnt,
                            unsigned long long* total, hipStream_t s);
-// all_rows >= 0: every row of the call's jobs is an element (no filter bitset, no time view, no
-// multi-value dimension) and all_rows is their count: no count pass before the keygen
+// all_rows >= 0: every row of the call's jobs is an element (no filter bitset, every row's time
+// inside the interval, no multi-value dimension) and all_rows is their count: no count pass before
+// the keygen
 void launch_gb_keygen(const GbJob* d_jobs, const int32_t* d_tile_job, int ntiles, SortBufs* sb, AggPlan plan,
                       hipStream_t s, bool multi = false, int64_t all_rows = -1);
 // stable LSD radix sort of sb->keys/refs[cur] on key bits [0, key_bits)

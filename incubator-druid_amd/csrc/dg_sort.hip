@@ -287,8 +287,9 @@ __global__ __launch_bounds__(256) void k_gb_keygen(const GbJob* __restrict__ job
   const GbJob& j = jobs[tile_job[blockIdx.x]];
   const int64_t r0 = (int64_t)(blockIdx.x - j.tile_begin) * kTileRows;
   const int64_t r1 = min((int64_t)j.nrows, r0 + kTileRows);
-  // rows_elems: every row of the call is an element, in row order (no filter, no time view, one
-  // element per row): the tile's first element is its first row's index over the call, no count pass
+  // rows_elems: every row of the call is an element, in row order (no filter, every row's time inside
+  // the interval, one element per row): the tile's first element is its first row's index over the
+  // call, no count pass
   uint32_t base = rows_elems ? j.row_base + (uint32_t)r0 : offs[blockIdx.x];
   const uint32_t inplace = rowref ? j.inplace : 0u;
   const bool all_inplace = pw > 0 && inplace == (pw >= 32 ? 0xFFFFFFFFu : (1u << pw) - 1u);

@@ -77,8 +77,13 @@ def test_hourly_timeseries(Q, O, R, cfg5, interval):
     assert_results(q, R.merge_timeseries(q, [[r] for rs in per for r in rs]), exp)
 
 
+@pytest.mark.parametrize("counted", ["0", "1"])
 @pytest.mark.parametrize("interval", [None, ["1970-01-01T05:30:00/1970-01-02T20:00:00"]])
-def test_hourly_groupby(Q, O, R, cfg5, interval):
+def test_hourly_groupby(Q, O, R, cfg5, interval, counted, monkeypatch):
+    """configs[4]b's hourly groupBy over the whole interval (every row an element: the keygen runs
+    without its count pass) and over an interval that cuts the segments (rows dropped by their time:
+    counted), and with the count pass forced (DG_GB_COUNT=1)."""
+    monkeypatch.setenv("DG_GB_COUNT", counted)
     B, g, o = cfg5
     q = B.make_query(Q, "groupby_hourly")
     if interval:
