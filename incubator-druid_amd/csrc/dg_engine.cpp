@@ -3205,7 +3205,12 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
   rc = finish_call(cs, st);
   ht.mark("synced");
   if (rc) return rc;
-  for (int i : ix_build) reinterpret_cast<Segment*>(segs[i])->find(t->dimension)->tix_ready = true;
+  for (int i : ix_build) {  // (the index's HBM counts toward the segment's footprint from now on)
+    Segment* seg = reinterpret_cast<Segment*>(segs[i]);
+    Column* dc = seg->find(t->dimension);
+    dc->tix_ready = true;
+    seg->device_bytes += (int64_t)(dc->tix_perm.n + dc->tix_lid.n + dc->tix_base.n);
+  }
   for (int k = 0; k < ns; ++k) h_ncand[k] = *reinterpret_cast<const int32_t*>(h_selmem + sel_words * k + 4);
   // k_topn_order left a list's records in output order (`sorted_at`); the replays that walk the
   // candidates in id order unpack them first (ids + rec-strided slots, back in id order)

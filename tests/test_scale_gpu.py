@@ -87,10 +87,15 @@ def test_cfg2_topn_bin_index(R, Q, O, S, cfg2, no_index, monkeypatch):
           Q.TopNQuery(intervals=["1970-01-01T00:02/1970-01-01T00:09"], dimension="dimUniform", metric="rows",
                       threshold=10, aggregations=aggs),
           Q.TopNQuery(intervals=IV, dimension="dimZipf", metric="sumFloatNormal", threshold=10, aggregations=aggs)]
+    before = [s.device_bytes() for s in g]
     try:
         for rnd in range(2):  # build, then reuse
             for q in qs:
                 assert_results(q, R.run_query(q, g), O.run(q, o))
+        # the indexes (dimUniform, dimZipf: 6 B per row + the bin starts each) count toward the footprint
+        for s, b in zip(g, before):
+            grown = s.device_bytes() - b
+            assert grown == 0 if no_index == "1" else 2 * 6 * s.num_rows <= grown <= 2 * 6 * s.num_rows + (1 << 20)
         q = qs[0]
         assert_results(q, R.run_query(q, [g[0], g[1], g[0]]), O.run(q, [o[0], o[1], o[0]]))
     finally:
