@@ -2973,7 +2973,7 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
       if (!dc->tix_ready && !queued) {
         const int64_t nb = (card[i] + (1ll << shift) - 1) >> shift;
         const size_t rows = (size_t)std::max<int64_t>(jobs[i].nrows, 1);
-        if (!dc->tix_perm.alloc(4 * rows) || !dc->tix_lid.alloc(2 * rows) || !dc->tix_base.alloc(4 * (size_t)nb))
+        if (!dc->tix_perm.alloc(4 * rows) || !dc->tix_lid.alloc(2 * rows) || !dc->tix_base.alloc(4 * (size_t)(nb + 1)))
           return set_error(DG_ERR_OOM, "topN index of %s", t->dimension);
         ix_build.push_back(i);
       }
@@ -3127,11 +3127,11 @@ int dg_topn_run(dg_segment* const* segs, int32_t n, const dg_scan* q, const dg_t
     if (use_ix) {
       for (int i : ix_build) {
         const int nb = (int)((card[i] + (1ll << shift) - 1) >> shift);
-        uint32_t* d_cnt = dev_take<uint32_t>(cs, 2 * (size_t)nb);  // counts | cursors
+        uint32_t* d_cnt = dev_take<uint32_t>(cs, 2 * (size_t)(nb + 1));  // counts (+ a zero) | cursors
         if (!d_cnt) return set_error(DG_ERR_OOM, "topN index build");
-        DG_HIP(hipMemsetAsync(d_cnt, 0, 4 * (size_t)nb, st));
+        DG_HIP(hipMemsetAsync(d_cnt, 0, 4 * (size_t)(nb + 1), st));
         Column* dc = reinterpret_cast<Segment*>(segs[i])->find(t->dimension);
-        launch_topn_ix_build(d_jobs, i, jobs[i].nrows, shift, nb, d_cnt, d_cnt + nb, dc->tix_base.as<uint32_t>(),
+        launch_topn_ix_build(d_jobs, i, jobs[i].nrows, shift, nb, d_cnt, d_cnt + nb + 1, dc->tix_base.as<uint32_t>(),
                              dc->tix_perm.as<uint32_t>(), dc->tix_lid.as<uint16_t>(), st);
       }
       launch_topn_ix_reduce(d_jobs, d_ix, d_bin_first, d_bin_seg, nbins, shift, plan, st);

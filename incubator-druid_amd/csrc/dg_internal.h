@@ -598,7 +598,7 @@ void launch_topn_part(const ScanJob* d_jobs, int njobs, int64_t max_card, AggPla
 // bin_seg[b] = segment of global bin b; hist/base/cursor: nbins words (hist zeroed by the caller);
 // lid/vals: cap selected-row slots (vals is naggs x cap).
 // topN bin index of a dimension column (Column::tix_*): bin b's rows are perm[base[b] .. base[b + 1])
-// (the last bin ends at the segment's rows), lid = each row's dictionary id & (2^shift - 1)
+// (base has bins + 1 entries), lid = each row's dictionary id & (2^shift - 1)
 struct TopnIx {
   const uint32_t* perm;
   const uint16_t* lid;

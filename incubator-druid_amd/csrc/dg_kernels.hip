@@ -1087,32 +1087,97 @@ void launch_topn_bins(const ScanJob* d_jobs, const int32_t* d_tile_job, int ntil
 // every id of the bin written); the inputs are gathered per row from the decoded metric columns.
 //   k_tix_count / k_topn_bin_scan / k_tix_scatter   build: rows per bin, bin starts, rows by bin
 //   k_topn_ix_reduce                                per bin: LDS table of its 2^shift ids, its rows
-__global__ __launch_bounds__(256) void k_tix_count(const ScanJob* __restrict__ jobs, int seg, int shift,
+__global__ __launch_bounds__(256) void k_tix_count(const ScanJob* __restrict__ jobs, int seg, int shift, int nbins,
                                                    uint32_t* __restrict__ cnt) {
   const ScanJob& j = jobs[seg];
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < j.nrows; r += (int64_t)gridDim.x * 256)
-    atomicAdd(&cnt[load_id(j.key, r) >> shift], 1u);
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < j.nrows; r += (int64_t)gridDim.x * 256) {
+    const uint32_t b = load_id(j.key, r) >> shift;
+    if (b < (uint32_t)nbins) atomicAdd(&cnt[b], 1u);  // (an id past the dictionary: not indexed)
+  }
 }
-__global__ __launch_bounds__(256) void k_tix_scatter(const ScanJob* __restrict__ jobs, int seg, int shift,
+__global__ __launch_bounds__(256) void k_tix_scatter(const ScanJob* __restrict__ jobs, int seg, int shift, int nbins,
                                                      uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm,
                                                      uint16_t* __restrict__ lid) {
   const ScanJob& j = jobs[seg];
   const uint32_t lmask = (1u << shift) - 1;
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < j.nrows; r += (int64_t)gridDim.x * 256) {
     const uint32_t id = load_id(j.key, r);
+    if ((id >> shift) >= (uint32_t)nbins) continue;
     const uint32_t pos = atomicAdd(&cursor[id >> shift], 1u);
     perm[pos] = (uint32_t)r;
     lid[pos] = (uint16_t)(id & lmask);
   }
 }
 
+// (dictionaries of at most kTixLdsBins bins: per workgroup of kTixRows rows, counts and ranks in LDS and
+// one global atomic per (workgroup, bin) — the per-row global atomics above contend on a few hundred
+// counters)
+constexpr int kTixLdsBins = 4096;
+constexpr int kTixPer = 16;                // rows per thread
+constexpr int kTixRows = 256 * kTixPer;   // rows per workgroup
+__global__ __launch_bounds__(256) void k_tix_count_lds(const ScanJob* __restrict__ jobs, int seg, int shift, int nbins,
+                                                       uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_cnt[kTixLdsBins];
+  const ScanJob& j = jobs[seg];
+  for (int b = threadIdx.x; b < nbins; b += 256) s_cnt[b] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kTixRows;
+  for (int u = 0; u < kTixPer; ++u) {
+    const int64_t r = r0 + u * 256 + threadIdx.x;
+    if (r >= j.nrows) continue;
+    const uint32_t b = load_id(j.key, r) >> shift;
+    if (b < (uint32_t)nbins) atomicAdd(&s_cnt[b], 1u);  // (an id past the dictionary: not indexed)
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += 256)
+    if (s_cnt[b]) atomicAdd(&cnt[b], s_cnt[b]);
+}
+__global__ __launch_bounds__(256) void k_tix_scatter_lds(const ScanJob* __restrict__ jobs, int seg, int shift, int nbins,
+                                                         uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm,
+                                                         uint16_t* __restrict__ lid) {
+  __shared__ uint32_t s_cnt[kTixLdsBins];  // counts, then this workgroup's first slot per bin
+  const ScanJob& j = jobs[seg];
+  const uint32_t lmask = (1u << shift) - 1;
+  for (int b = threadIdx.x; b < nbins; b += 256) s_cnt[b] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kTixRows;
+  uint32_t id[kTixPer], rk[kTixPer];
+#pragma unroll
+  for (int u = 0; u < kTixPer; ++u) {
+    const int64_t r = r0 + u * 256 + threadIdx.x;
+    id[u] = r < j.nrows ? load_id(j.key, r) : ~0u;
+    rk[u] = (id[u] >> shift) < (uint32_t)nbins ? atomicAdd(&s_cnt[id[u] >> shift], 1u) : 0u;
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += 256)
+    s_cnt[b] = s_cnt[b] ? atomicAdd(&cursor[b], s_cnt[b]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kTixPer; ++u) {
+    const int64_t r = r0 + u * 256 + threadIdx.x;
+    if (r >= j.nrows || (id[u] >> shift) >= (uint32_t)nbins) continue;
+    const uint32_t pos = s_cnt[id[u] >> shift] + rk[u];
+    perm[pos] = (uint32_t)r;
+    lid[pos] = (uint16_t)(id[u] & lmask);
+  }
+}
+
 void launch_topn_ix_build(const ScanJob* d_jobs, int seg, int64_t nrows, int shift, int nbins, uint32_t* d_cnt,
                           uint32_t* d_cursor, uint32_t* base, uint32_t* perm, uint16_t* lid, hipStream_t s) {
   if (nrows <= 0 || nbins <= 0) return;
+  // (the scan runs over nbins + 1 counts, the last one zero: base[nbins] = the indexed rows, the end
+  // of the last bin)
+  if (nbins <= kTixLdsBins) {
+    const unsigned grid = (unsigned)((nrows + kTixRows - 1) / kTixRows);
+    hipLaunchKernelGGL(k_tix_count_lds, dim3(grid), dim3(256), 0, s, d_jobs, seg, shift, nbins, d_cnt);
+    hipLaunchKernelGGL(k_topn_bin_scan, dim3(1), dim3(1024), 0, s, d_cnt, base, d_cursor, nbins + 1);
+    hipLaunchKernelGGL(k_tix_scatter_lds, dim3(grid), dim3(256), 0, s, d_jobs, seg, shift, nbins, d_cursor, perm, lid);
+    return;
+  }
   const unsigned grid = (unsigned)std::min<int64_t>((nrows + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_tix_count, dim3(grid), dim3(256), 0, s, d_jobs, seg, shift, d_cnt);
-  hipLaunchKernelGGL(k_topn_bin_scan, dim3(1), dim3(1024), 0, s, d_cnt, base, d_cursor, nbins);
-  hipLaunchKernelGGL(k_tix_scatter, dim3(grid), dim3(256), 0, s, d_jobs, seg, shift, d_cursor, perm, lid);
+  hipLaunchKernelGGL(k_tix_count, dim3(grid), dim3(256), 0, s, d_jobs, seg, shift, nbins, d_cnt);
+  hipLaunchKernelGGL(k_topn_bin_scan, dim3(1), dim3(1024), 0, s, d_cnt, base, d_cursor, nbins + 1);
+  hipLaunchKernelGGL(k_tix_scatter, dim3(grid), dim3(256), 0, s, d_jobs, seg, shift, nbins, d_cursor, perm, lid);
 }
 
 __global__ __launch_bounds__(kBinThreads) void k_topn_ix_reduce(const ScanJob* __restrict__ jobs,
@@ -1126,7 +1191,6 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_ix_reduce(const ScanJob* _
   const TopnIx ix = ixs[seg];
   const int na = plan.n, rec = na + 1;
   const int b = gb - bin_first[seg];
-  const int nb = (int)((j.nbuckets + (1ll << shift) - 1) >> shift);
   const int64_t id0 = (int64_t)b << shift;
   const int64_t nid = min((int64_t)j.nbuckets - id0, 1ll << shift);
   const int nslots = (int)nid * rec;
@@ -1135,7 +1199,7 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_ix_reduce(const ScanJob* _
     s_tab[x] = sl == 0 ? 0ull : identity_of(plan.op[sl - 1], plan.kind[sl - 1]);
   }
   __syncthreads();
-  const int64_t p0 = ix.base[b], p1 = b + 1 < nb ? (int64_t)ix.base[b + 1] : (int64_t)j.nrows;
+  const int64_t p0 = ix.base[b], p1 = ix.base[b + 1];
   for (int64_t p = p0 + threadIdx.x; p < p1; p += kBinThreads) {
     const int64_t r = ix.perm[p];
     int64_t bb;
