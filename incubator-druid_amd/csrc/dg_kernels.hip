@@ -1200,13 +1200,34 @@ __global__ __launch_bounds__(kBinThreads) void k_topn_ix_reduce(const ScanJob* _
   }
   __syncthreads();
   const int64_t p0 = ix.base[b], p1 = ix.base[b + 1];
-  for (int64_t p = p0 + threadIdx.x; p < p1; p += kBinThreads) {
-    const int64_t r = ix.perm[p];
-    int64_t bb;
-    if (!row_selected(j, r, &bb)) continue;
-    uint64_t* e = s_tab + (int)ix.lid[p] * rec;
-    atomicAdd(reinterpret_cast<unsigned long long*>(e), 1ull);
-    for (int a = 0; a < na; ++a) atomic_op(plan.op[a], e + 1 + a, agg_in(j, plan, a, r));
+  // kIxU rows per thread per round: their index entries, then their inputs, loaded together (each row's
+  // gather waits on its index load; one round trip of each per round instead of per row)
+  constexpr int kIxU = 4;
+  for (int64_t pb = p0 + threadIdx.x; pb < p1; pb += kBinThreads * kIxU) {
+    int64_t r[kIxU];
+    int e_at[kIxU];
+    bool ok[kIxU];
+#pragma unroll
+    for (int u = 0; u < kIxU; ++u) {
+      const int64_t p = pb + u * kBinThreads;
+      ok[u] = p < p1;
+      r[u] = ok[u] ? (int64_t)ix.perm[p] : 0;
+      e_at[u] = ok[u] ? (int)ix.lid[p] * rec : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kIxU; ++u) {
+      int64_t bb;
+      ok[u] = ok[u] && row_selected(j, r[u], &bb);
+      if (ok[u]) atomicAdd(reinterpret_cast<unsigned long long*>(s_tab + e_at[u]), 1ull);
+    }
+    for (int a = 0; a < na; ++a) {
+      uint64_t v[kIxU];
+#pragma unroll
+      for (int u = 0; u < kIxU; ++u) v[u] = ok[u] ? agg_in(j, plan, a, r[u]) : 0ull;
+#pragma unroll
+      for (int u = 0; u < kIxU; ++u)
+        if (ok[u]) atomic_op(plan.op[a], s_tab + e_at[u] + 1 + a, v[u]);
+    }
   }
   __syncthreads();
   uint64_t* out = j.out + id0 * rec;
