@@ -137,8 +137,16 @@ constexpr int kLtMaxDepth = 16;
 // 8 output bytes ride in a register, a near copy is a shift of it, and every aligned 8-byte value is
 // emitted as it completes. Index layout per block (16-byte aligned): u64 win[n], u32 tok[n] (token
 // offset | far-table offset << 17), u16 out[n], zero pad to 16, the far table, zero pad to 16.
-constexpr int kRunThreads = 256;   // one interval per thread (kBlockBytes / kRunTarget intervals at most)
-constexpr int kRunTarget = 256;    // output bytes per interval, at least (the last one excepted)
+// Interval length and threads of the run decoder: one thread's serial chain is its interval, so the
+// block's latency follows it; 96-byte intervals over 768 threads (round 6, same box: configs[4]a 8.03
+// -> 7.46 ms, topN and the headline within noise to -3 %; 128 / 64 bytes close behind,
+// profiles/r06_v51_ab_run.log) against 256 bytes over 256 threads before. (A/B builds override both.)
+#ifndef DG_RUN_TARGET
+#define DG_RUN_TARGET 96
+#define DG_RUN_THREADS 768
+#endif
+constexpr int kRunThreads = DG_RUN_THREADS;  // one interval per thread (kBlockBytes / kRunTarget intervals at most)
+constexpr int kRunTarget = DG_RUN_TARGET;    // output bytes per interval, at least (the last one excepted)
 constexpr int kRunFarMax = 4096;   // far-copy bytes a run block may list
 constexpr int kRunMaxRun = 1024;   // longest literal run / match of a run block (one thread's serial work)
 constexpr int kRunLdsMax = 40960;  // staged input + far table of one run block (four workgroups per CU)

@@ -1824,7 +1824,7 @@ __global__ __launch_bounds__(kLtThreads) void k_lz4_light(const Lz4Launch L, int
 // 128 KiB per-byte entry image, one block per CU. Here the attach-time index gives every interval of
 // >= kRunTarget output bytes the 8 bytes before it, so each thread decodes its interval alone: the
 // last 8 output bytes live in one 64-bit register (`win`, oldest byte lowest), a literal or far-copy
-// chunk is shifted in from the compressed block (L1/L2: a thread reads its own ~128 contiguous bytes),
+// chunk is shifted in from the compressed block (L1/L2: a thread reads its own interval's bytes),
 // a copy from d <= 8 bytes back is the window's last d bytes repeated, and every 8-byte-aligned value is
 // complete the moment it is emitted. Values go to the block's image in LDS (64 KiB: two blocks per CU)
 // and leave in coalesced stores after one barrier (a slot, or the payload records' 8-byte field: 64 lanes
