@@ -126,7 +126,10 @@ enum : int32_t { kRedGeneric = 0, kRedLongSum = 1, kRedDoubleSum = 2, kRedLongMa
 // intervals and copy chains of at most kLtMaxDepth hops. k_lz4_light decodes them with a small
 // sequence table in LDS (many blocks per CU), resolving every output byte back to its literal.
 constexpr int kLtMaxCps = 256;
-constexpr int kLtThreads = 512;  // light-decoder threads (at most one light checkpoint interval each)
+#ifndef DG_LT_THREADS  // (A/B builds)
+#define DG_LT_THREADS 512
+#endif
+constexpr int kLtThreads = DG_LT_THREADS;  // light-decoder threads (at most one light checkpoint interval each)
 constexpr int kLtMaxDepth = 16;
 
 // Run blocks: LZ4 blocks of 8-byte value runs (sequential longs, timestamps, constant columns) whose
